@@ -1,0 +1,240 @@
+"""oracle/oracle.py — TEST INFRASTRUCTURE ONLY.
+
+ctypes binding of oracle/liborc.so, the plain-C restatement of the MCL BLS12-381 path Lachain uses
+(see bls_oracle.h).  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liborc.so")
+        if not os.path.exists(path):
+            raise RuntimeError("oracle/liborc.so not built (run `make -C oracle`)")
+        _LIB = ctypes.CDLL(path)
+        _LIB.orc_init()
+        _LIB.orc_count_get.restype = ctypes.c_uint64
+    return _LIB
+
+
+def _buf(n):
+    return ctypes.create_string_buffer(n)
+
+
+def _ck(rc, what):
+    if rc != 0:
+        raise ValueError(f"oracle {what} failed ({rc})")
+
+
+# ---------------------------------------------------------------- Fr
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+
+
+def fr(v: int) -> bytes:
+    return (v % R).to_bytes(32, "little")
+
+
+def fr_mul(a, b):
+    o = _buf(32); _ck(lib().orc_fr_mul(o, a, b), "fr_mul"); return o.raw
+
+
+def fr_add(a, b):
+    o = _buf(32); _ck(lib().orc_fr_add(o, a, b), "fr_add"); return o.raw
+
+
+def fr_from_wide(b64: bytes) -> bytes:
+    o = _buf(32); lib().orc_fr_from_wide(o, b64); return o.raw
+
+
+# ---------------------------------------------------------------- groups
+def g1_gen():
+    o = _buf(48); lib().orc_g1_generator(o); return o.raw
+
+
+def g2_gen():
+    o = _buf(96); lib().orc_g2_generator(o); return o.raw
+
+
+def g1_mul(p, s):
+    o = _buf(48); _ck(lib().orc_g1_mul(o, p, s), "g1_mul"); return o.raw
+
+
+def g2_mul(p, s):
+    o = _buf(96); _ck(lib().orc_g2_mul(o, p, s), "g2_mul"); return o.raw
+
+
+def g1_add(a, b):
+    o = _buf(48); _ck(lib().orc_g1_add(o, a, b), "g1_add"); return o.raw
+
+
+def g2_add(a, b):
+    o = _buf(96); _ck(lib().orc_g2_add(o, a, b), "g2_add"); return o.raw
+
+
+def g1_neg(a):
+    o = _buf(48); _ck(lib().orc_g1_neg(o, a), "g1_neg"); return o.raw
+
+
+def g2_neg(a):
+    o = _buf(96); _ck(lib().orc_g2_neg(o, a), "g2_neg"); return o.raw
+
+
+def g1_valid(a):
+    return bool(lib().orc_g1_is_valid_encoding(a))
+
+
+def g2_valid(a):
+    return bool(lib().orc_g2_is_valid_encoding(a))
+
+
+def g1_in_subgroup(a):
+    return bool(lib().orc_g1_in_subgroup(a))
+
+
+def g2_in_subgroup(a):
+    return bool(lib().orc_g2_in_subgroup(a))
+
+
+def g2_hash(msg: bytes):
+    o = _buf(96); _ck(lib().orc_g2_hash(o, msg, ctypes.c_size_t(len(msg))), "g2_hash"); return o.raw
+
+
+def _lagr(fn, size, xs, ys):
+    o = _buf(size)
+    rc = fn(o, b"".join(xs), b"".join(ys), ctypes.c_size_t(len(xs)))
+    if rc != 0:
+        return None
+    return o.raw
+
+
+def g1_lagrange(xs, ys):
+    return _lagr(lib().orc_g1_lagrange, 48, xs, ys)
+
+
+def g2_lagrange(xs, ys):
+    return _lagr(lib().orc_g2_lagrange, 96, xs, ys)
+
+
+def fr_lagrange(xs, ys):
+    return _lagr(lib().orc_fr_lagrange, 32, xs, ys)
+
+
+def fr_eval_poly(coeffs, x):
+    o = _buf(32)
+    _ck(lib().orc_fr_eval_poly(o, b"".join(coeffs), ctypes.c_size_t(len(coeffs)), x), "eval_poly")
+    return o.raw
+
+
+def g1_msm(points, scalars):
+    o = _buf(48)
+    _ck(lib().orc_g1_msm(o, b"".join(points), b"".join(scalars), ctypes.c_size_t(len(points))), "msm")
+    return o.raw
+
+
+# ---------------------------------------------------------------- pairing
+def pairing(p, q):
+    o = _buf(576); _ck(lib().orc_pairing(o, p, q), "pairing"); return o.raw
+
+
+def pairing_slow(p, q):
+    o = _buf(576); _ck(lib().orc_pairing_slow(o, p, q), "pairing_slow"); return o.raw
+
+
+def miller_loop(p, q):
+    o = _buf(576); _ck(lib().orc_miller_loop(o, p, q), "miller"); return o.raw
+
+
+def final_exp(f):
+    o = _buf(576); _ck(lib().orc_final_exp(o, f), "fe"); return o.raw
+
+
+def final_exp_direct(f):
+    o = _buf(576); _ck(lib().orc_final_exp_direct(o, f), "fe_direct"); return o.raw
+
+
+def gt_pow(a, s):
+    o = _buf(576); _ck(lib().orc_gt_pow(o, a, s), "gt_pow"); return o.raw
+
+
+def gt_mul(a, b):
+    o = _buf(576); _ck(lib().orc_gt_mul(o, a, b), "gt_mul"); return o.raw
+
+
+# ---------------------------------------------------------------- hashing / KDF
+def sha3_256(m):
+    o = _buf(32); lib().orc_sha3_256(o, m, ctypes.c_size_t(len(m))); return o.raw
+
+
+def sha512(m):
+    o = _buf(64); lib().orc_sha512(o, m, ctypes.c_size_t(len(m))); return o.raw
+
+
+def sha256(m):
+    o = _buf(32); lib().orc_sha256(o, m, ctypes.c_size_t(len(m))); return o.raw
+
+
+def drg_bytes(seed: bytes, n: int) -> bytes:
+    o = _buf(n); lib().orc_drg_bytes(o, ctypes.c_size_t(n), seed, ctypes.c_size_t(len(seed))); return o.raw
+
+
+def xor_with_hash(g1b: bytes, data: bytes) -> bytes:
+    o = _buf(max(1, len(data))); lib().orc_xor_with_hash(o, g1b, data, ctypes.c_size_t(len(data)))
+    return o.raw[: len(data)]
+
+
+# ---------------------------------------------------------------- protocol
+def tpke_encrypt(y, data, r):
+    u, v, w = _buf(48), _buf(max(1, len(data))), _buf(96)
+    _ck(lib().orc_tpke_encrypt(u, v, w, y, data, ctypes.c_size_t(len(data)), r), "encrypt")
+    return u.raw, v.raw[: len(data)], w.raw
+
+
+def tpke_decrypt(u, v, w, x):
+    ui = _buf(48)
+    rc = lib().orc_tpke_decrypt(ui, u, v, ctypes.c_size_t(len(v)), w, x)
+    if rc == -1:
+        raise ValueError("Invalid share!")
+    _ck(rc, "decrypt")
+    return ui.raw
+
+
+def tpke_verify_share(y_i, u, v, w, ui):
+    return lib().orc_tpke_verify_share(y_i, u, v, ctypes.c_size_t(len(v)), w, ui)
+
+
+def tpke_full_decrypt(v, ids, uis):
+    o = _buf(max(1, len(v)))
+    ids_arr = (ctypes.c_int32 * max(1, len(ids)))(*ids)
+    _ck(lib().orc_tpke_full_decrypt(o, v, ctypes.c_size_t(len(v)), ids_arr, b"".join(uis),
+                                    ctypes.c_size_t(len(uis))), "full_decrypt")
+    return o.raw[: len(v)]
+
+
+def ts_sign(sk, msg):
+    o = _buf(96); _ck(lib().orc_ts_sign(o, sk, msg, ctypes.c_size_t(len(msg))), "sign"); return o.raw
+
+
+def ts_validate(pk, sig, msg):
+    return lib().orc_ts_validate(pk, sig, msg, ctypes.c_size_t(len(msg)))
+
+
+def set_g2_sign_from_b(v):
+    lib().orc_set_g2_sign_from_b(int(v))
+
+
+def set_g2_original_cofactor(v):
+    lib().orc_set_g2_original_cofactor(int(v))
+
+
+def count_reset():
+    lib().orc_count_reset()
+
+
+def count_get():
+    return lib().orc_count_get()
