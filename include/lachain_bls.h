@@ -1,0 +1,213 @@
+/*
+ * include/lachain_bls.h — C ABI of liblachain_bls.so, the MI355X (gfx950) replacement for the native
+ * BLS12-381 library behind Lachain's threshold-crypto hot path.
+ *
+ * Boundary being replaced: Lachain.Crypto (C#) P/Invokes herumi mcl through the NuGet packages
+ * MCL.BLS12_381.Net 0.0.4 / MCL.BLS12_381.Native 0.0.5
+ * (/root/reference/src/Lachain.Crypto/Lachain.Crypto.csproj:18-19).  That wrapper's sources are not in
+ * the reference tree; the export set below is mcl's public C API (mcl/bn.h, mclbn384_256 build) as
+ * inferred from the managed call sites (census in SURVEY.md §8b), so the managed wrapper can be
+ * re-pointed at this library by changing its DllImport name.  Every function cites the Lachain call
+ * site(s) it serves.  The lcb_* functions are the batch entry points the consensus layer (or a shim,
+ * INTEGRATION.md) calls with whole batches of shares.
+ *
+ * Data layouts: the in-memory structs are byte-compatible with mcl's: Montgomery form, 64-bit limbs
+ * little-endian (Fr: R = 2^256, Fp: R = 2^384), G1/G2 Jacobian (x, y, z), GT = Fp12 as 12 Fp.
+ * All-zero bytes = zero / point at infinity.  Serialized sizes: Fr 32 B, G1 48 B, G2 96 B, GT 576 B
+ * (mcl serialize format; pinned by test/Lachain.CryptoTest/SerializationTest.cs).
+ *
+ * Errors never cross the ABI as exceptions: int functions return 0 on success and -1 on failure,
+ * (de)serializers return the number of bytes written/read or 0.  Every entry point is re-entrant;
+ * GPU submission is serialized per device by an internal lock.  All arithmetic runs on the GPU; if no
+ * gfx950 device can be opened, mclBn_init returns -1 and every other call fails loudly (there is no
+ * CPU fallback).
+ */
+#ifndef LACHAIN_BLS_H
+#define LACHAIN_BLS_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MCL_BLS12_381 5
+#define MCLBN_COMPILED_TIME_VAR 46 /* mclbn384_256: (MCLBN_FP_UNIT_SIZE * 10 + MCLBN_FR_UNIT_SIZE) */
+
+typedef int64_t mclInt;
+typedef size_t mclSize;
+typedef struct { uint64_t d[4]; } mclBnFr;
+typedef struct { uint64_t d[6]; } mclBnFp;
+typedef struct { mclBnFp d[2]; } mclBnFp2;
+typedef struct { mclBnFp x, y, z; } mclBnG1;
+typedef struct { mclBnFp2 x, y, z; } mclBnG2;
+typedef struct { mclBnFp d[12]; } mclBnGT;
+
+/* ------------------------------------------------------------------ init / sizes
+   Mcl.Init / static constructor of the managed wrapper (dead test/ToolsTest.cs:18 shows `Mcl.Init()`) */
+int mclBn_init(int curve, int compiledTimeVar);
+int mclBn_getOpUnitSize(void);
+int mclBn_getG1ByteSize(void); /* G1.ByteSize = 48 (src/Lachain.Utility/Serialization/SerialiaztionUtils.cs:24-26) */
+int mclBn_getFrByteSize(void); /* Fr.ByteSize = 32 */
+int mclBn_getFpByteSize(void);
+
+/* ------------------------------------------------------------------ Fr
+   Fr.FromInt (23 call sites, e.g. TPKE/PublicKey.cs:79), Fr.GetRandom (TPKE/PublicKey.cs:29),
+   Fr.FromBytes / ToBytes (ThresholdSignature/PrivateKeyShare.cs:31), operators + * (MclTests.cs:57) */
+int mclBnFr_setInt(mclBnFr *y, mclInt x);
+int mclBnFr_setInt32(mclBnFr *y, int x);
+int mclBnFr_setByCSPRNG(mclBnFr *x);
+int mclBnFr_setLittleEndian(mclBnFr *x, const void *buf, mclSize bufSize);
+mclSize mclBnFr_serialize(void *buf, mclSize maxBufSize, const mclBnFr *x);
+mclSize mclBnFr_deserialize(mclBnFr *x, const void *buf, mclSize bufSize);
+void mclBnFr_clear(mclBnFr *x);
+int mclBnFr_isValid(const mclBnFr *x);
+int mclBnFr_isEqual(const mclBnFr *x, const mclBnFr *y);
+int mclBnFr_isZero(const mclBnFr *x);
+int mclBnFr_isOne(const mclBnFr *x);
+void mclBnFr_neg(mclBnFr *y, const mclBnFr *x);
+void mclBnFr_inv(mclBnFr *y, const mclBnFr *x);
+void mclBnFr_sqr(mclBnFr *y, const mclBnFr *x);
+void mclBnFr_add(mclBnFr *z, const mclBnFr *x, const mclBnFr *y);
+void mclBnFr_sub(mclBnFr *z, const mclBnFr *x, const mclBnFr *y);
+void mclBnFr_mul(mclBnFr *z, const mclBnFr *x, const mclBnFr *y);
+void mclBnFr_div(mclBnFr *z, const mclBnFr *x, const mclBnFr *y);
+
+/* ------------------------------------------------------------------ G1
+   G1.Generator (24 sites), G1.FromBytes (HoneyBadger decode, TPKE/PublicKey.cs:41), G1 * Fr
+   (TPKE/PublicKey.cs:30-32, TPKE/PrivateKey.cs:28), G1 + G1 (MclTests.cs:59), IsValid
+   (ThresholdKeygen/Data/Commitment.cs:78) */
+mclSize mclBnG1_serialize(void *buf, mclSize maxBufSize, const mclBnG1 *x);
+mclSize mclBnG1_deserialize(mclBnG1 *x, const void *buf, mclSize bufSize);
+int mclBnG1_isValid(const mclBnG1 *x);
+int mclBnG1_isEqual(const mclBnG1 *x, const mclBnG1 *y);
+int mclBnG1_isZero(const mclBnG1 *x);
+void mclBnG1_clear(mclBnG1 *x);
+void mclBnG1_neg(mclBnG1 *y, const mclBnG1 *x);
+void mclBnG1_dbl(mclBnG1 *y, const mclBnG1 *x);
+void mclBnG1_normalize(mclBnG1 *y, const mclBnG1 *x);
+void mclBnG1_add(mclBnG1 *z, const mclBnG1 *x, const mclBnG1 *y);
+void mclBnG1_sub(mclBnG1 *z, const mclBnG1 *x, const mclBnG1 *y);
+void mclBnG1_mul(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y);
+void mclBnG1_mulVec(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y, mclSize n);
+/* convenience (not in mcl): the Lachain G1 generator (SerializationTest.cs:36) */
+void lcb_g1_generator(mclBnG1 *g);
+
+/* ------------------------------------------------------------------ G2
+   G2.Generator, G2.FromBytes (ThresholdSignature/Signature.cs:38), G2.SetHashOf
+   (TPKE/Utils.cs:24-25, ThresholdSignature/PublicKey.cs:19, PrivateKeyShare.cs:24), G2 * Fr
+   (TPKE/PublicKey.cs:34, PrivateKeyShare.cs:25) */
+mclSize mclBnG2_serialize(void *buf, mclSize maxBufSize, const mclBnG2 *x);
+mclSize mclBnG2_deserialize(mclBnG2 *x, const void *buf, mclSize bufSize);
+int mclBnG2_isValid(const mclBnG2 *x);
+int mclBnG2_isEqual(const mclBnG2 *x, const mclBnG2 *y);
+int mclBnG2_isZero(const mclBnG2 *x);
+void mclBnG2_clear(mclBnG2 *x);
+int mclBnG2_hashAndMapTo(mclBnG2 *x, const void *buf, mclSize bufSize);
+void mclBnG2_neg(mclBnG2 *y, const mclBnG2 *x);
+void mclBnG2_dbl(mclBnG2 *y, const mclBnG2 *x);
+void mclBnG2_normalize(mclBnG2 *y, const mclBnG2 *x);
+void mclBnG2_add(mclBnG2 *z, const mclBnG2 *x, const mclBnG2 *y);
+void mclBnG2_sub(mclBnG2 *z, const mclBnG2 *x, const mclBnG2 *y);
+void mclBnG2_mul(mclBnG2 *z, const mclBnG2 *x, const mclBnFr *y);
+void lcb_g2_generator(mclBnG2 *g);
+
+/* ------------------------------------------------------------------ GT / pairing
+   GT.Pairing (8 sites: TPKE/PrivateKey.cs:26, TPKE/PublicKey.cs:91, ThresholdSignature/PublicKey.cs:20),
+   GT.Equals, GT.Pow (MclTests.cs:73) */
+void mclBn_pairing(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y);
+void mclBn_millerLoop(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y);
+void mclBn_millerLoopVec(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y, mclSize n);
+void mclBn_finalExp(mclBnGT *y, const mclBnGT *x);
+int mclBnGT_isEqual(const mclBnGT *x, const mclBnGT *y);
+int mclBnGT_isOne(const mclBnGT *x);
+int mclBnGT_isZero(const mclBnGT *x);
+void mclBnGT_clear(mclBnGT *x);
+void mclBnGT_mul(mclBnGT *z, const mclBnGT *x, const mclBnGT *y);
+void mclBnGT_pow(mclBnGT *z, const mclBnGT *x, const mclBnFr *y);
+mclSize mclBnGT_serialize(void *buf, mclSize maxBufSize, const mclBnGT *x);
+mclSize mclBnGT_deserialize(mclBnGT *x, const void *buf, mclSize bufSize);
+
+/* ------------------------------------------------------------------ polynomials / Lagrange
+   MclBls12381.LagrangeInterpolate (TPKE/PublicKey.cs:83, ThresholdSignature/PublicKeySet.cs:31,41,
+   ThresholdKeygen/Data/State.cs:43), MclBls12381.EvaluatePolynomial (TPKE/TrustedKeyGen.cs:23-33) */
+int mclBn_FrLagrangeInterpolation(mclBnFr *out, const mclBnFr *xVec, const mclBnFr *yVec, mclSize k);
+int mclBn_G1LagrangeInterpolation(mclBnG1 *out, const mclBnFr *xVec, const mclBnG1 *yVec, mclSize k);
+int mclBn_G2LagrangeInterpolation(mclBnG2 *out, const mclBnFr *xVec, const mclBnG2 *yVec, mclSize k);
+int mclBn_FrEvaluatePolynomial(mclBnFr *out, const mclBnFr *cVec, mclSize cSize, const mclBnFr *x);
+int mclBn_G1EvaluatePolynomial(mclBnG1 *out, const mclBnG1 *cVec, mclSize cSize, const mclBnFr *x);
+int mclBn_G2EvaluatePolynomial(mclBnG2 *out, const mclBnG2 *cVec, mclSize cSize, const mclBnFr *x);
+
+/* ================================================================== batch entry points (new)
+   Host-pointer forms copy to/from the GPU; *_dev forms take device pointers and a hipStream_t (as void*)
+   and enqueue without synchronizing.  All serialized inputs use the 48/96-byte wire formats. */
+
+/* library configuration */
+int lcb_set_device(int device_id);                 /* before mclBn_init; default: HIP device 0 */
+int lcb_get_device(void);
+void lcb_set_original_g2_cofactor(int enable);     /* unpinned mcl choice, DESIGN.md §Parity */
+const char *lcb_last_error(void);
+
+/* TPKE.PublicKey.VerifyShare for a batch (TPKE/PublicKey.cs:88-92, called per share from
+   HoneyBadger.cs:211-212).  Ciphertext c = (U_c, V_c, W_c) with V_c = v_data[v_off[c] .. v_off[c+1]);
+   share i pairs ciphertext ct_idx[i] with decryptor dec_idx[i] (verification key y_keys[dec_idx[i]]) and
+   partial decryption ui[i].  accept[i] = 1 iff e(Ui, H(U||V)) == e(Y_i, W) (malformed encodings -> 0). */
+int lcb_tpke_verify_shares(uint8_t *accept, size_t n_shares, const uint8_t *y_keys, size_t n_keys,
+                           const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
+                           const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
+                           const uint32_t *dec_idx, const uint8_t *ui);
+int lcb_tpke_verify_shares_dev(uint8_t *accept, size_t n_shares, const uint8_t *y_keys, size_t n_keys,
+                               const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
+                               const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
+                               const uint32_t *dec_idx, const uint8_t *ui, void *stream);
+
+/* TPKE.PrivateKey.Decrypt for a batch (TPKE/PrivateKey.cs:21-31): status[c] = 1 and ui[c] = x*U_c when
+   e(G, W_c) == e(U_c, H(U_c||V_c)), status[c] = 0 ("Invalid share!") otherwise. */
+int lcb_tpke_partial_decrypt(uint8_t *ui_out, uint8_t *status, const uint8_t x[32], const uint8_t *cts_u,
+                             const uint8_t *cts_w, const uint8_t *v_data, const uint32_t *v_off, size_t n_cts);
+
+/* TPKE.PublicKey.Encrypt for a batch with caller-supplied randomness r (TPKE/PublicKey.cs:25-37):
+   U = rG, T = rY (serialized, for the XorWithHash KDF done by the caller), W = r H(U||V). Two-phase
+   because V = data XOR KDF(T) is computed between the phases (TPKE/Utils.cs:12-19). */
+int lcb_tpke_encrypt_phase1(uint8_t *u_out, uint8_t *t_out, const uint8_t y[48], const uint8_t *r, size_t n);
+int lcb_tpke_encrypt_phase2(uint8_t *w_out, const uint8_t *u, const uint8_t *r, const uint8_t *v_data,
+                            const uint32_t *v_off, size_t n);
+
+/* ThresholdSignature.PublicKey.ValidateSignature for a batch (ThresholdSignature/PublicKey.cs:16-21,
+   ThresholdSigner.cs:62,89-92): share i is checked against message msg_idx[i] (messages concatenated in
+   msg_data with offsets msg_off) and public key pks[pk_idx[i]].  accept[i] = e(PK, H(m)) == e(G, sig). */
+int lcb_ts_verify_shares(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks, const uint8_t *sigs,
+                         const uint8_t *msg_data, const uint32_t *msg_off, size_t n_msgs,
+                         const uint32_t *msg_idx, const uint32_t *pk_idx);
+int lcb_ts_verify_shares_dev(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks, const uint8_t *sigs,
+                             const uint8_t *msg_data, const uint32_t *msg_off, size_t n_msgs,
+                             const uint32_t *msg_idx, const uint32_t *pk_idx, void *stream);
+
+/* PrivateKeyShare.HashAndSign for a batch of (key, message) pairs (ThresholdSignature/PrivateKeyShare.cs:21-27) */
+int lcb_ts_sign(uint8_t *sigs_out, const uint8_t *sks, const uint8_t *msg_data, const uint32_t *msg_off,
+                const uint32_t *msg_idx, size_t n);
+
+/* Batched Lagrange interpolation at 0 (MclBls12381.LagrangeInterpolate; PublicKeySet.AssembleSignature,
+   ThresholdSignature/PublicKeySet.cs:34-42, and TPKE FullDecrypt, TPKE/PublicKey.cs:74-84).
+   Problem j uses k = off[j+1]-off[j] entries starting at off[j]: x values as 32-byte Fr, y values serialized.
+   status[j] = 1 ok, 0 on k == 0, zero x or duplicate x (mcl returns -1). */
+int lcb_g1_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
+                          const uint32_t *off, size_t n_problems);
+int lcb_g2_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
+                          const uint32_t *off, size_t n_problems);
+
+/* G1 multi-scalar multiplication sum_i s_i P_i (serialized points, 32-byte LE scalars < r) */
+int lcb_g1_msm(uint8_t out[48], const uint8_t *points, const uint8_t *scalars, size_t n);
+
+/* batched scalar multiplication of the G1 / G2 generator or of given points (key generation, synthetic inputs) */
+int lcb_g1_mul_batch(uint8_t *out, const uint8_t *points, int points_is_generator, const uint8_t *scalars, size_t n);
+int lcb_g2_mul_batch(uint8_t *out, const uint8_t *points, int points_is_generator, const uint8_t *scalars, size_t n);
+int lcb_g2_hash_batch(uint8_t *out, const uint8_t *msg_data, const uint32_t *msg_off, size_t n);
+
+/* TPKE Utils.XorWithHash (BouncyCastle DigestRandomGenerator(Sha3Digest) keystream, TPKE/Utils.cs:12-19):
+   host-side byte work, provided so a non-.NET host can finish FullDecrypt/Encrypt. */
+void lcb_xor_with_hash(uint8_t *out, const uint8_t g1[48], const uint8_t *data, size_t len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,301 @@
+// lachain_amd/csrc/curve.hpp — G1 (E: y^2 = x^3 + 4 over Fp) and G2 (E': y^2 = x^3 + 4(1+i) over Fp2,
+// M-type twist) in Jacobian coordinates, MCL-format (de)serialization, the psi endomorphism and
+// scalar multiplication.  One point per lane.
+//
+// Wire formats (pinned by test/Lachain.CryptoTest/SerializationTest.cs:31-57):
+//   G1 48 B = x (LE) with bit 7 of byte 47 = parity(y); G2 96 B = x.a (LE) || x.b (LE), bit 7 of byte 95
+//   = parity(y.a) (mcl Fp2::isOdd looks at the `a` coordinate); all-zero = point at infinity.
+// Deserialization is mcl's default (lax): reject x >= p and points not on the curve, no subgroup check
+// (evidence: test/Lachain.ConsensusTest/HoneyBadgerSmartMalicious.cs:57-73).
+#pragma once
+#include "field.hpp"
+
+// ---------------------------------------------------------------- overload set used by the templates
+DI void f_add(fp &r, const fp &a, const fp &b) { fp_add(r, a, b); }
+DI void f_sub(fp &r, const fp &a, const fp &b) { fp_sub(r, a, b); }
+DI void f_mul(fp &r, const fp &a, const fp &b) { fp_mul(r, a, b); }
+DI void f_sqr(fp &r, const fp &a) { fp_sqr(r, a); }
+DI void f_neg(fp &r, const fp &a) { fp_neg(r, a); }
+DI void f_inv(fp &r, const fp &a) { fp_inv(r, a); }
+DI bool f_is_zero(const fp &a) { return fp_is_zero(a); }
+DI bool f_eq(const fp &a, const fp &b) { return fp_eq(a, b); }
+DI void f_one(fp &r) { r = fp_one(); }
+DI void f_zero(fp &r) { r = fp_zero(); }
+DI void f_add(fp2 &r, const fp2 &a, const fp2 &b) { fp2_add(r, a, b); }
+DI void f_sub(fp2 &r, const fp2 &a, const fp2 &b) { fp2_sub(r, a, b); }
+DI void f_mul(fp2 &r, const fp2 &a, const fp2 &b) { fp2_mul(r, a, b); }
+DI void f_sqr(fp2 &r, const fp2 &a) { fp2_sqr(r, a); }
+DI void f_neg(fp2 &r, const fp2 &a) { fp2_neg(r, a); }
+DI void f_inv(fp2 &r, const fp2 &a) { fp2_inv_n(r, a); }
+DI bool f_is_zero(const fp2 &a) { return fp2_is_zero(a); }
+DI bool f_eq(const fp2 &a, const fp2 &b) { return fp2_eq(a, b); }
+DI void f_one(fp2 &r) { r = fp2_one(); }
+DI void f_zero(fp2 &r) { r = fp2_zero(); }
+
+template <class F> struct jac { F x, y, z; };
+typedef jac<fp> g1;
+typedef jac<fp2> g2;
+template <class F> struct aff { F x, y; bool inf; };
+typedef aff<fp> g1a;
+typedef aff<fp2> g2a;
+
+template <class F> DI bool jac_is_inf(const jac<F> &p) { return f_is_zero(p.z); }
+template <class F> DI void jac_set_inf(jac<F> &p) { f_one(p.x); f_one(p.y); f_zero(p.z); }
+template <class F> DI void jac_from_aff(jac<F> &r, const aff<F> &a) {
+    if (a.inf) { jac_set_inf(r); return; }
+    r.x = a.x; r.y = a.y; f_one(r.z);
+}
+// dbl-2009-l (a = 0)
+template <class F> DI void jac_dbl(jac<F> &r, const jac<F> &p) {
+    F A, B, C, D, E, Fv, t, x3, y3, z3;
+    f_sqr(A, p.x);
+    f_sqr(B, p.y);
+    f_sqr(C, B);
+    f_add(D, p.x, B);
+    f_sqr(D, D);
+    f_sub(D, D, A);
+    f_sub(D, D, C);
+    f_add(D, D, D);
+    f_add(E, A, A);
+    f_add(E, E, A);
+    f_sqr(Fv, E);
+    f_add(t, D, D);
+    f_sub(x3, Fv, t);
+    f_sub(t, D, x3);
+    f_mul(y3, E, t);
+    f_add(t, C, C);
+    f_add(t, t, t);
+    f_add(t, t, t);
+    f_sub(y3, y3, t);
+    f_mul(z3, p.y, p.z);
+    f_add(z3, z3, z3);
+    r.x = x3; r.y = y3; r.z = z3;
+}
+// add-2007-bl, complete for the doubling / inverse / infinity special cases
+template <class F> DI void jac_add(jac<F> &r, const jac<F> &p, const jac<F> &q) {
+    if (jac_is_inf(p)) { r = q; return; }
+    if (jac_is_inf(q)) { r = p; return; }
+    F z1z1, z2z2, u1, u2, s1, s2, h, i, j, rr, v, t, x3, y3, z3;
+    f_sqr(z1z1, p.z);
+    f_sqr(z2z2, q.z);
+    f_mul(u1, p.x, z2z2);
+    f_mul(u2, q.x, z1z1);
+    f_mul(s1, p.y, q.z);
+    f_mul(s1, s1, z2z2);
+    f_mul(s2, q.y, p.z);
+    f_mul(s2, s2, z1z1);
+    if (f_eq(u1, u2)) {
+        if (f_eq(s1, s2)) { jac_dbl(r, p); return; }
+        jac_set_inf(r);
+        return;
+    }
+    f_sub(h, u2, u1);
+    f_add(i, h, h);
+    f_sqr(i, i);
+    f_mul(j, h, i);
+    f_sub(rr, s2, s1);
+    f_add(rr, rr, rr);
+    f_mul(v, u1, i);
+    f_sqr(x3, rr);
+    f_sub(x3, x3, j);
+    f_sub(x3, x3, v);
+    f_sub(x3, x3, v);
+    f_sub(t, v, x3);
+    f_mul(y3, rr, t);
+    f_mul(t, s1, j);
+    f_add(t, t, t);
+    f_sub(y3, y3, t);
+    f_add(z3, p.z, q.z);
+    f_sqr(z3, z3);
+    f_sub(z3, z3, z1z1);
+    f_sub(z3, z3, z2z2);
+    f_mul(z3, z3, h);
+    r.x = x3; r.y = y3; r.z = z3;
+}
+// madd-2007-bl: p + q with q affine (q finite)
+template <class F> DI void jac_add_aff(jac<F> &r, const jac<F> &p, const F &qx, const F &qy) {
+    if (jac_is_inf(p)) { r.x = qx; r.y = qy; f_one(r.z); return; }
+    F z1z1, u2, s2, h, hh, i, j, rr, v, t, x3, y3, z3;
+    f_sqr(z1z1, p.z);
+    f_mul(u2, qx, z1z1);
+    f_mul(s2, qy, p.z);
+    f_mul(s2, s2, z1z1);
+    if (f_eq(u2, p.x)) {
+        if (f_eq(s2, p.y)) { jac_dbl(r, p); return; }
+        jac_set_inf(r);
+        return;
+    }
+    f_sub(h, u2, p.x);
+    f_sqr(hh, h);
+    f_add(i, hh, hh);
+    f_add(i, i, i);
+    f_mul(j, h, i);
+    f_sub(rr, s2, p.y);
+    f_add(rr, rr, rr);
+    f_mul(v, p.x, i);
+    f_sqr(x3, rr);
+    f_sub(x3, x3, j);
+    f_sub(x3, x3, v);
+    f_sub(x3, x3, v);
+    f_sub(t, v, x3);
+    f_mul(y3, rr, t);
+    f_mul(t, p.y, j);
+    f_add(t, t, t);
+    f_sub(y3, y3, t);
+    f_add(z3, p.z, h);
+    f_sqr(z3, z3);
+    f_sub(z3, z3, z1z1);
+    f_sub(z3, z3, hh);
+    r.x = x3; r.y = y3; r.z = z3;
+}
+template <class F> DI void jac_neg(jac<F> &r, const jac<F> &p) { r.x = p.x; f_neg(r.y, p.y); r.z = p.z; }
+template <class F> DI void jac_to_aff(aff<F> &a, const jac<F> &p) {
+    if (jac_is_inf(p)) { a.inf = true; f_zero(a.x); f_zero(a.y); return; }
+    F zi, zi2;
+    f_inv(zi, p.z);
+    f_sqr(zi2, zi);
+    f_mul(a.x, p.x, zi2);
+    f_mul(zi2, zi2, zi);
+    f_mul(a.y, p.y, zi2);
+    a.inf = false;
+}
+DN void g1_dbl_n(g1 &r, const g1 &p) { g1 t; jac_dbl(t, p); r = t; }
+DN void g1_add_n(g1 &r, const g1 &p, const g1 &q) { g1 t; jac_add(t, p, q); r = t; }
+DN void g2_dbl_n(g2 &r, const g2 &p) { g2 t; jac_dbl(t, p); r = t; }
+DN void g2_add_n(g2 &r, const g2 &p, const g2 &q) { g2 t; jac_add(t, p, q); r = t; }
+DI void grp_dbl(g1 &r, const g1 &p) { g1_dbl_n(r, p); }
+DI void grp_add(g1 &r, const g1 &p, const g1 &q) { g1_add_n(r, p, q); }
+DI void grp_dbl(g2 &r, const g2 &p) { g2_dbl_n(r, p); }
+DI void grp_add(g2 &r, const g2 &p, const g2 &q) { g2_add_n(r, p, q); }
+// scalar multiplication by a canonical little-endian integer of nbits bits (left-to-right
+// double-and-add over the scalar's own bits; scalars differ per lane, so the add is predicated)
+template <class F> DI void jac_mul_bits(jac<F> &r, const jac<F> &p, const u32 *k, int nbits) {
+    jac<F> acc;
+    jac_set_inf(acc);
+    for (int i = nbits - 1; i >= 0; i--) {
+        grp_dbl(acc, acc);
+        if ((k[i >> 5] >> (i & 31)) & 1) grp_add(acc, acc, p);
+    }
+    r = acc;
+}
+template <class F> DI void jac_mul_u64(jac<F> &r, const jac<F> &p, u64 k) {
+    u32 kk[2] = {(u32)k, (u32)(k >> 32)};
+    jac_mul_bits(r, p, kk, 64);
+}
+
+// ---------------------------------------------------------------- G2 endomorphism psi (M-type twist)
+// psi(x, y) = (conj(x) xi^-(p-1)/3, conj(y) xi^-(p-1)/2); Jacobian-compatible since conj commutes
+DI void g2_psi(g2 &r, const g2 &p) {
+    fp2 cx, cy;
+    fp2_load_const(cx, LCB_PSI_X);
+    fp2_load_const(cy, LCB_PSI_Y);
+    fp2 x, y, z;
+    fp2_conj(x, p.x);
+    fp2_conj(y, p.y);
+    fp2_conj(z, p.z);
+    fp2_mul(r.x, x, cx);
+    fp2_mul(r.y, y, cy);
+    r.z = z;
+}
+DI void g2_psi2(g2 &r, const g2 &p) {
+    fp cx, cy;
+    fp_load_const(cx, LCB_PSI2_X);
+    fp_load_const(cy, LCB_PSI2_Y);
+    fp2_mul_fp(r.x, p.x, cx);
+    fp2_mul_fp(r.y, p.y, cy);
+    r.z = p.z;
+}
+
+// ---------------------------------------------------------------- serialization
+DI void bytes48_to_raw(fp &raw, const uint8_t *b) { // 4-byte aligned source
+    const u32 *w = (const u32 *)b;
+#pragma unroll
+    for (int j = 0; j < 12; j++) raw.v[j] = w[j];
+}
+DI void raw_to_bytes48(uint8_t *b, const fp &raw) {
+    u32 *w = (u32 *)b;
+#pragma unroll
+    for (int j = 0; j < 12; j++) w[j] = raw.v[j];
+}
+// G1.FromBytes: returns false on a malformed encoding
+DN bool g1_decompress(g1a &out, const uint8_t *b) {
+    fp raw;
+    bytes48_to_raw(raw, b);
+    u32 any = 0;
+#pragma unroll
+    for (int j = 0; j < 12; j++) any |= raw.v[j];
+    if (any == 0) { out.inf = true; out.x = fp_zero(); out.y = fp_zero(); return true; }
+    bool odd = raw.v[11] >> 31;
+    raw.v[11] &= 0x7fffffffu;
+    if (!fp_raw_lt_p(raw)) return false;
+    fp x, t, y, b1;
+    fp_from_raw(x, raw);
+    fp_sqr(t, x);
+    fp_mul(t, t, x);
+    fp_load_const(b1, LCB_B1);
+    fp_add(t, t, b1);
+    if (!fp_sqrt(y, t)) return false;
+    if (fp_is_odd(y) != odd) fp_neg(y, y);
+    out.x = x; out.y = y; out.inf = false;
+    return true;
+}
+DI void g1_compress(uint8_t *b, const g1a &a) {
+    if (a.inf) { fp z = fp_zero(); raw_to_bytes48(b, z); return; }
+    fp rx, ry;
+    fp_to_raw(rx, a.x);
+    fp_to_raw(ry, a.y);
+    if (ry.v[0] & 1) rx.v[11] |= 0x80000000u;
+    raw_to_bytes48(b, rx);
+}
+DN bool g2_decompress(g2a &out, const uint8_t *b) {
+    fp ra, rb;
+    bytes48_to_raw(ra, b);
+    bytes48_to_raw(rb, b + 48);
+    u32 any = 0;
+#pragma unroll
+    for (int j = 0; j < 12; j++) any |= ra.v[j] | rb.v[j];
+    if (any == 0) { out.inf = true; out.x = fp2_zero(); out.y = fp2_zero(); return true; }
+    bool odd = rb.v[11] >> 31;
+    rb.v[11] &= 0x7fffffffu;
+    if (!fp_raw_lt_p(ra) || !fp_raw_lt_p(rb)) return false;
+    fp2 x, t, y, b2;
+    fp_from_raw(x.a, ra);
+    fp_from_raw(x.b, rb);
+    fp2_sqr(t, x);
+    fp2_mul(t, t, x);
+    fp2_load_const(b2, LCB_B2);
+    fp2_add(t, t, b2);
+    if (!fp2_sqrt(y, t)) return false;
+    if (fp_is_odd(y.a) != odd) fp2_neg(y, y);
+    out.x = x; out.y = y; out.inf = false;
+    return true;
+}
+DI void g2_compress(uint8_t *b, const g2a &a) {
+    if (a.inf) {
+        fp z = fp_zero();
+        raw_to_bytes48(b, z);
+        raw_to_bytes48(b + 48, z);
+        return;
+    }
+    fp xa, xb, ya;
+    fp_to_raw(xa, a.x.a);
+    fp_to_raw(xb, a.x.b);
+    fp_to_raw(ya, a.y.a);
+    if (ya.v[0] & 1) xb.v[11] |= 0x80000000u;
+    raw_to_bytes48(b, xa);
+    raw_to_bytes48(b + 48, xb);
+}
+DN void g1_compress_jac(uint8_t *b, const g1 &p) { g1a a; jac_to_aff(a, p); g1_compress(b, a); }
+DN void g2_compress_jac(uint8_t *b, const g2 &p) { g2a a; jac_to_aff(a, p); g2_compress(b, a); }
+DI void g1_generator(g1a &g) {
+    fp_load_const(g.x, LCB_G1_GEN);
+    fp_load_const(g.y, LCB_G1_GEN + 12);
+    g.inf = false;
+}
+DI void g2_generator(g2a &g) {
+    fp_load_const(g.x.a, LCB_G2_GEN);
+    fp_load_const(g.x.b, LCB_G2_GEN + 12);
+    fp_load_const(g.y.a, LCB_G2_GEN + 24);
+    fp_load_const(g.y.b, LCB_G2_GEN + 36);
+    g.inf = false;
+}

@@ -1,0 +1,626 @@
+// lachain_amd/csrc/field.hpp — BLS12-381 field tower on gfx950 (device code).
+//
+// Fp : 12 x 32-bit limbs, Montgomery form (R = 2^384), always fully reduced to [0, p).
+// Fr : 8 x 32-bit limbs, Montgomery form (R = 2^256), fully reduced.
+// Fp2 = Fp[i]/(i^2 + 1), Fp6 = Fp2[v]/(v^3 - xi), Fp12 = Fp6[w]/(w^2 - v), xi = 1 + i: the herumi mcl
+// tower that Lachain reaches through MCL.BLS12_381.Native.
+//
+// Register / code-size strategy: one field element per lane, all state in VGPRs.
+// The Montgomery multiply is the only non-inlined leaf (`lcb_fp_mul_v`): it takes/returns vector
+// types so the AMDGPU calling convention keeps operands in v0..v23 (aggregates >16 registers would be
+// passed through scratch), and it needs < 40 VGPRs, so it clobbers no callee-saved registers.  Every
+// Fp2/Fp6/Fp12 routine is inlined around those calls, which keeps the hot loops' code in the I-cache.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bls_constants.hpp"
+#include "fp_mul_gen.hpp"
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+typedef u32 u32x12 __attribute__((ext_vector_type(12)));
+typedef u32 u32x8 __attribute__((ext_vector_type(8)));
+
+#define DI __device__ __forceinline__
+#define DN __device__ __noinline__
+
+struct fp { u32 v[12]; };
+struct fp2 { fp a, b; };
+struct fp6 { fp2 c0, c1, c2; };
+struct fp12 { fp6 c0, c1; };
+struct fr { u32 v[8]; };
+
+// ------------------------------------------------------------------------------------------------ Fp
+DI void fp_load_const(fp &r, const u32 *c) {
+#pragma unroll
+    for (int j = 0; j < 12; j++) r.v[j] = c[j];
+}
+DI fp fp_zero() { fp r; for (int j = 0; j < 12; j++) r.v[j] = 0; return r; }
+DI fp fp_one() { fp r; fp_load_const(r, LCB_ONE); return r; }
+DI bool fp_is_zero(const fp &a) {
+    u32 x = 0;
+#pragma unroll
+    for (int j = 0; j < 12; j++) x |= a.v[j];
+    return x == 0;
+}
+DI bool fp_eq(const fp &a, const fp &b) {
+    u32 x = 0;
+#pragma unroll
+    for (int j = 0; j < 12; j++) x |= a.v[j] ^ b.v[j];
+    return x == 0;
+}
+// r = (t >= p) ? t - p : t, for t < 2p
+DI void fp_reduce_once(fp &r, const fp &t) {
+    u32 d[12];
+    u32 br = 0;
+#pragma unroll
+    for (int j = 0; j < 12; j++) {
+        u64 x = (u64)t.v[j] - LCB_P[j] - br;
+        d[j] = (u32)x;
+        br = (u32)(x >> 32) & 1;
+    }
+#pragma unroll
+    for (int j = 0; j < 12; j++) r.v[j] = br ? t.v[j] : d[j];
+}
+DI void fp_add(fp &r, const fp &a, const fp &b) {
+    fp t;
+    u32 c = 0;
+#pragma unroll
+    for (int j = 0; j < 12; j++) {
+        u64 s = (u64)a.v[j] + b.v[j] + c;
+        t.v[j] = (u32)s;
+        c = (u32)(s >> 32);
+    }
+    fp_reduce_once(r, t); // a + b < 2p < 2^382: no carry out of limb 11
+}
+DI void fp_dbl(fp &r, const fp &a) { fp_add(r, a, a); }
+DI void fp_sub(fp &r, const fp &a, const fp &b) {
+    fp t;
+    u32 br = 0;
+#pragma unroll
+    for (int j = 0; j < 12; j++) {
+        u64 x = (u64)a.v[j] - b.v[j] - br;
+        t.v[j] = (u32)x;
+        br = (u32)(x >> 32) & 1;
+    }
+    fp d;
+    u32 c = 0;
+#pragma unroll
+    for (int j = 0; j < 12; j++) {
+        u64 s = (u64)t.v[j] + LCB_P[j] + c;
+        d.v[j] = (u32)s;
+        c = (u32)(s >> 32);
+    }
+#pragma unroll
+    for (int j = 0; j < 12; j++) r.v[j] = br ? d.v[j] : t.v[j];
+}
+DI void fp_neg(fp &r, const fp &a) {
+    fp z = fp_zero();
+    fp_sub(r, z, a);
+}
+
+DN u32x12 lcb_fp_mul_v(u32x12 a, u32x12 b) {
+    u32x12 r;
+    LCB_FP_MUL_BODY(a, b, r)
+    u32x12 d;
+    u32 br = 0;
+#pragma unroll
+    for (int j = 0; j < 12; j++) {
+        u64 x = (u64)r[j] - LCB_P[j] - br;
+        d[j] = (u32)x;
+        br = (u32)(x >> 32) & 1;
+    }
+    return br ? r : d;
+}
+DI u32x12 fp_to_v(const fp &a) {
+    u32x12 v;
+#pragma unroll
+    for (int j = 0; j < 12; j++) v[j] = a.v[j];
+    return v;
+}
+DI fp fp_from_v(const u32x12 &v) {
+    fp a;
+#pragma unroll
+    for (int j = 0; j < 12; j++) a.v[j] = v[j];
+    return a;
+}
+DI void fp_mul(fp &r, const fp &a, const fp &b) { r = fp_from_v(lcb_fp_mul_v(fp_to_v(a), fp_to_v(b))); }
+DI void fp_sqr(fp &r, const fp &a) { fp_mul(r, a, a); }
+
+// conversions between canonical integers (12 LE limbs) and Montgomery form
+DI void fp_from_raw(fp &r, const fp &raw) {
+    fp r2;
+    fp_load_const(r2, LCB_R2);
+    fp_mul(r, raw, r2);
+}
+DI void fp_to_raw(fp &r, const fp &a) {
+    fp one = fp_zero();
+    one.v[0] = 1;
+    fp_mul(r, a, one);
+}
+DI bool fp_raw_lt_p(const fp &raw) {
+    u32 br = 0;
+#pragma unroll
+    for (int j = 0; j < 12; j++) {
+        u64 x = (u64)raw.v[j] - LCB_P[j] - br;
+        br = (u32)(x >> 32) & 1;
+    }
+    return br != 0;
+}
+DI bool fp_is_odd(const fp &a) {
+    fp t;
+    fp_to_raw(t, a);
+    return t.v[0] & 1;
+}
+// a^e for an exponent given as 12 LE limbs in constant memory (left-to-right binary; the exponent bits
+// are wave-uniform, so the branch does not diverge).  Non-inlined, operands in VGPRs.
+DN u32x12 lcb_fp_pow_v(u32x12 av, const u32 *e) {
+    int top = 383;
+    while (top > 0 && !((e[top >> 5] >> (top & 31)) & 1)) top--;
+    u32x12 acc = av;
+    for (int i = top - 1; i >= 0; i--) {
+        acc = lcb_fp_mul_v(acc, acc);
+        if ((e[i >> 5] >> (i & 31)) & 1) acc = lcb_fp_mul_v(acc, av);
+    }
+    return acc;
+}
+DI void fp_pow_const(fp &r, const fp &a, const u32 *e) { r = fp_from_v(lcb_fp_pow_v(fp_to_v(a), e)); }
+DI void fp_inv(fp &r, const fp &a) { fp_pow_const(r, a, LCB_P_MINUS_2); }
+// mcl Fp::squareRoot for p = 3 mod 4: y = a^((p+1)/4), valid iff y^2 == a
+DI bool fp_sqrt(fp &r, const fp &a) {
+    fp y, t;
+    fp_pow_const(y, a, LCB_P_PLUS1_DIV4);
+    fp_sqr(t, y);
+    bool ok = fp_eq(t, a); // compare before writing r: callers pass r aliasing a
+    r = y;
+    return ok;
+}
+DI int fp_legendre(const fp &a) {
+    if (fp_is_zero(a)) return 0;
+    fp t;
+    fp_pow_const(t, a, LCB_P_MINUS1_DIV2);
+    return fp_eq(t, fp_one()) ? 1 : -1;
+}
+
+// ------------------------------------------------------------------------------------------------ Fp2
+DI void fp2_add(fp2 &r, const fp2 &x, const fp2 &y) { fp_add(r.a, x.a, y.a); fp_add(r.b, x.b, y.b); }
+DI void fp2_sub(fp2 &r, const fp2 &x, const fp2 &y) { fp_sub(r.a, x.a, y.a); fp_sub(r.b, x.b, y.b); }
+DI void fp2_dbl(fp2 &r, const fp2 &x) { fp_add(r.a, x.a, x.a); fp_add(r.b, x.b, x.b); }
+DI void fp2_neg(fp2 &r, const fp2 &x) { fp_neg(r.a, x.a); fp_neg(r.b, x.b); }
+DI void fp2_conj(fp2 &r, const fp2 &x) { r.a = x.a; fp_neg(r.b, x.b); }
+DI bool fp2_is_zero(const fp2 &x) { return fp_is_zero(x.a) && fp_is_zero(x.b); }
+DI bool fp2_eq(const fp2 &x, const fp2 &y) { return fp_eq(x.a, y.a) && fp_eq(x.b, y.b); }
+DI fp2 fp2_zero() { fp2 r; r.a = fp_zero(); r.b = fp_zero(); return r; }
+DI fp2 fp2_one() { fp2 r; r.a = fp_one(); r.b = fp_zero(); return r; }
+DI void fp2_load_const(fp2 &r, const u32 *c) { fp_load_const(r.a, c); fp_load_const(r.b, c + 12); }
+DI void fp2_mul(fp2 &r, const fp2 &x, const fp2 &y) {
+    fp t0, t1, t2, t3;
+    fp_mul(t0, x.a, y.a);
+    fp_mul(t1, x.b, y.b);
+    fp_add(t2, x.a, x.b);
+    fp_add(t3, y.a, y.b);
+    fp_mul(t2, t2, t3);
+    fp_sub(r.a, t0, t1);
+    fp_sub(t2, t2, t0);
+    fp_sub(r.b, t2, t1);
+}
+DI void fp2_sqr(fp2 &r, const fp2 &x) {
+    fp t0, t1, t2;
+    fp_add(t0, x.a, x.b);
+    fp_sub(t1, x.a, x.b);
+    fp_mul(t2, x.a, x.b);
+    fp_mul(r.a, t0, t1);
+    fp_add(r.b, t2, t2);
+}
+DI void fp2_mul_fp(fp2 &r, const fp2 &x, const fp &s) { fp_mul(r.a, x.a, s); fp_mul(r.b, x.b, s); }
+DI void fp2_mul_xi(fp2 &r, const fp2 &x) { // (a + b i)(1 + i) = (a - b) + (a + b) i
+    fp t;
+    fp_sub(t, x.a, x.b);
+    fp_add(r.b, x.a, x.b);
+    r.a = t;
+}
+DI void fp2_norm(fp &r, const fp2 &x) {
+    fp t;
+    fp_sqr(r, x.a);
+    fp_sqr(t, x.b);
+    fp_add(r, r, t);
+}
+DI void fp2_inv(fp2 &r, const fp2 &x) {
+    fp n;
+    fp2_norm(n, x);
+    fp_inv(n, n);
+    fp_mul(r.a, x.a, n);
+    fp_mul(r.b, x.b, n);
+    fp_neg(r.b, r.b);
+}
+// mcl Fp2T::squareRoot (norm method; root choice reproduced exactly)
+DI bool fp2_sqrt(fp2 &y, const fp2 &x) {
+    fp t1, t2, inv2;
+    fp_load_const(inv2, LCB_INV2);
+    if (fp_is_zero(x.b)) {
+        if (fp_sqrt(t1, x.a)) {
+            y.a = t1;
+            y.b = fp_zero();
+        } else {
+            fp na;
+            fp_neg(na, x.a);
+            if (!fp_sqrt(t1, na)) return false;
+            y.a = fp_zero();
+            y.b = t1;
+        }
+        return true;
+    }
+    fp_sqr(t1, x.a);
+    fp_sqr(t2, x.b);
+    fp_add(t1, t1, t2);
+    if (!fp_sqrt(t1, t1)) return false;
+    fp_add(t2, x.a, t1);
+    fp_mul(t2, t2, inv2);
+    if (!fp_sqrt(t2, t2)) {
+        fp_sub(t2, x.a, t1);
+        fp_mul(t2, t2, inv2);
+        if (!fp_sqrt(t2, t2)) return false;
+    }
+    y.a = t2;
+    fp_add(t2, t2, t2);
+    fp_inv(t2, t2);
+    fp_mul(y.b, x.b, t2);
+    return true;
+}
+
+// ------------------------------------------------------------------------------------------------ Fp6
+DI void fp6_add(fp6 &r, const fp6 &x, const fp6 &y) { fp2_add(r.c0, x.c0, y.c0); fp2_add(r.c1, x.c1, y.c1); fp2_add(r.c2, x.c2, y.c2); }
+DI void fp6_sub(fp6 &r, const fp6 &x, const fp6 &y) { fp2_sub(r.c0, x.c0, y.c0); fp2_sub(r.c1, x.c1, y.c1); fp2_sub(r.c2, x.c2, y.c2); }
+DI void fp6_neg(fp6 &r, const fp6 &x) { fp2_neg(r.c0, x.c0); fp2_neg(r.c1, x.c1); fp2_neg(r.c2, x.c2); }
+DI void fp6_mul(fp6 &r, const fp6 &a, const fp6 &b) {
+    fp2 t0, t1, t2, s0, s1, c0, c1, c2;
+    fp2_mul(t0, a.c0, b.c0);
+    fp2_mul(t1, a.c1, b.c1);
+    fp2_mul(t2, a.c2, b.c2);
+    fp2_add(s0, a.c1, a.c2);
+    fp2_add(s1, b.c1, b.c2);
+    fp2_mul(c0, s0, s1);
+    fp2_sub(c0, c0, t1);
+    fp2_sub(c0, c0, t2);
+    fp2_mul_xi(c0, c0);
+    fp2_add(c0, c0, t0);
+    fp2_add(s0, a.c0, a.c1);
+    fp2_add(s1, b.c0, b.c1);
+    fp2_mul(c1, s0, s1);
+    fp2_sub(c1, c1, t0);
+    fp2_sub(c1, c1, t1);
+    fp2_mul_xi(s0, t2);
+    fp2_add(c1, c1, s0);
+    fp2_add(s0, a.c0, a.c2);
+    fp2_add(s1, b.c0, b.c2);
+    fp2_mul(c2, s0, s1);
+    fp2_sub(c2, c2, t0);
+    fp2_sub(c2, c2, t2);
+    fp2_add(c2, c2, t1);
+    r.c0 = c0; r.c1 = c1; r.c2 = c2;
+}
+DI void fp6_mul_v(fp6 &r, const fp6 &a) { // a * v = (xi c2, c0, c1)
+    fp2 t;
+    fp2_mul_xi(t, a.c2);
+    r.c2 = a.c1;
+    r.c1 = a.c0;
+    r.c0 = t;
+}
+DI void fp6_mul_01(fp6 &r, const fp6 &a, const fp2 &b0, const fp2 &b1) { // a * (b0, b1, 0)
+    fp2 t0, t1, c0, c1, c2, s, u;
+    fp2_mul(t0, a.c0, b0);
+    fp2_mul(t1, a.c1, b1);
+    fp2_mul(c0, a.c2, b1);
+    fp2_mul_xi(c0, c0);
+    fp2_add(c0, c0, t0);
+    fp2_add(s, a.c0, a.c1);
+    fp2_add(u, b0, b1);
+    fp2_mul(c1, s, u);
+    fp2_sub(c1, c1, t0);
+    fp2_sub(c1, c1, t1);
+    fp2_mul(c2, a.c2, b0);
+    fp2_add(c2, c2, t1);
+    r.c0 = c0; r.c1 = c1; r.c2 = c2;
+}
+DI void fp6_mul_1(fp6 &r, const fp6 &a, const fp2 &b1) { // a * (0, b1, 0) = b1 (xi a2, a0, a1)
+    fp2 c0, c1, c2;
+    fp2_mul(c0, a.c2, b1);
+    fp2_mul_xi(c0, c0);
+    fp2_mul(c1, a.c0, b1);
+    fp2_mul(c2, a.c1, b1);
+    r.c0 = c0; r.c1 = c1; r.c2 = c2;
+}
+DI void fp6_inv(fp6 &r, const fp6 &a) {
+    fp2 c0, c1, c2, t, s;
+    fp2_sqr(c0, a.c0);
+    fp2_mul(t, a.c1, a.c2);
+    fp2_mul_xi(t, t);
+    fp2_sub(c0, c0, t);
+    fp2_sqr(c1, a.c2);
+    fp2_mul_xi(c1, c1);
+    fp2_mul(t, a.c0, a.c1);
+    fp2_sub(c1, c1, t);
+    fp2_sqr(c2, a.c1);
+    fp2_mul(t, a.c0, a.c2);
+    fp2_sub(c2, c2, t);
+    fp2_mul(t, a.c2, c1);
+    fp2_mul(s, a.c1, c2);
+    fp2_add(t, t, s);
+    fp2_mul_xi(t, t);
+    fp2_mul(s, a.c0, c0);
+    fp2_add(t, t, s);
+    fp2_inv(t, t);
+    fp2_mul(r.c0, c0, t);
+    fp2_mul(r.c1, c1, t);
+    fp2_mul(r.c2, c2, t);
+}
+
+// ------------------------------------------------------------------------------------------------ Fp12
+DI fp12 fp12_one() {
+    fp12 r;
+    r.c0.c0 = fp2_one(); r.c0.c1 = fp2_zero(); r.c0.c2 = fp2_zero();
+    r.c1.c0 = fp2_zero(); r.c1.c1 = fp2_zero(); r.c1.c2 = fp2_zero();
+    return r;
+}
+DI bool fp12_is_one(const fp12 &a) {
+    fp12 o = fp12_one();
+    const fp *x = &a.c0.c0.a, *y = &o.c0.c0.a;
+    bool eq = true;
+#pragma unroll
+    for (int i = 0; i < 12; i++) eq = eq && fp_eq(x[i], y[i]);
+    return eq;
+}
+DI void fp12_mul(fp12 &r, const fp12 &a, const fp12 &b) {
+    fp6 t0, t1, s0, s1;
+    fp6_mul(t0, a.c0, b.c0);
+    fp6_mul(t1, a.c1, b.c1);
+    fp6_add(s0, a.c0, a.c1);
+    fp6_add(s1, b.c0, b.c1);
+    fp6_mul(s0, s0, s1);
+    fp6_sub(s0, s0, t0);
+    fp6_sub(r.c1, s0, t1);
+    fp6_mul_v(t1, t1);
+    fp6_add(r.c0, t0, t1);
+}
+DI void fp12_sqr(fp12 &r, const fp12 &a) {
+    fp6 t, s0, s1, tv;
+    fp6_mul(t, a.c0, a.c1);
+    fp6_add(s0, a.c0, a.c1);
+    fp6_mul_v(s1, a.c1);
+    fp6_add(s1, s1, a.c0);
+    fp6_mul(s0, s0, s1);
+    fp6_sub(s0, s0, t);
+    fp6_mul_v(tv, t);
+    fp6_sub(r.c0, s0, tv);
+    fp6_add(r.c1, t, t);
+}
+DI void fp12_conj(fp12 &r, const fp12 &a) { r.c0 = a.c0; fp6_neg(r.c1, a.c1); }
+DI void fp12_inv(fp12 &r, const fp12 &a) {
+    fp6 t0, t1;
+    fp6_mul(t0, a.c0, a.c0);
+    fp6_mul(t1, a.c1, a.c1);
+    fp6_mul_v(t1, t1);
+    fp6_sub(t0, t0, t1);
+    fp6_inv(t0, t0);
+    fp6_mul(r.c0, a.c0, t0);
+    fp6_mul(r.c1, a.c1, t0);
+    fp6_neg(r.c1, r.c1);
+}
+// f *= (A + B v) + (C v) w  — the sparse shape of a Miller-loop line (13 Fp2 muls)
+DI void fp12_mul_line(fp12 &f, const fp2 &A, const fp2 &B, const fp2 &C) {
+    fp6 t0, t1, s;
+    fp2 bc;
+    fp6_mul_01(t0, f.c0, A, B);
+    fp6_mul_1(t1, f.c1, C);
+    fp6_add(s, f.c0, f.c1);
+    fp2_add(bc, B, C);
+    fp6_mul_01(s, s, A, bc);
+    fp6_sub(s, s, t0);
+    fp6_sub(f.c1, s, t1);
+    fp6_mul_v(t1, t1);
+    fp6_add(f.c0, t0, t1);
+}
+// Frobenius maps: element = sum g_k w^k, (g w^k)^p = conj(g) gamma1_k w^k; layout c0 = (g0, g2, g4),
+// c1 = (g1, g3, g5)
+DI void fp12_frob1(fp12 &r, const fp12 &a) {
+    const fp2 *in[6] = {&a.c0.c0, &a.c1.c0, &a.c0.c1, &a.c1.c1, &a.c0.c2, &a.c1.c2};
+    fp12 t;
+    fp2 *tt[6] = {&t.c0.c0, &t.c1.c0, &t.c0.c1, &t.c1.c1, &t.c0.c2, &t.c1.c2};
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        fp2 g, c;
+        fp2_conj(g, *in[k]);
+        if (k == 0) {
+            *tt[k] = g;
+        } else {
+            fp2_load_const(c, LCB_GAMMA1 + 24 * k);
+            fp2_mul(*tt[k], g, c);
+        }
+    }
+    r = t;
+}
+DI void fp12_frob2(fp12 &r, const fp12 &a) {
+    fp12 t;
+    const fp2 *in[6] = {&a.c0.c0, &a.c1.c0, &a.c0.c1, &a.c1.c1, &a.c0.c2, &a.c1.c2};
+    fp2 *tt[6] = {&t.c0.c0, &t.c1.c0, &t.c0.c1, &t.c1.c1, &t.c0.c2, &t.c1.c2};
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        if (k == 0) {
+            *tt[k] = *in[k];
+        } else {
+            fp c;
+            fp_load_const(c, LCB_GAMMA2 + 12 * k);
+            fp2_mul_fp(*tt[k], *in[k], c);
+        }
+    }
+    r = t;
+}
+DI void fp12_frob3(fp12 &r, const fp12 &a) {
+    fp12 t;
+    const fp2 *in[6] = {&a.c0.c0, &a.c1.c0, &a.c0.c1, &a.c1.c1, &a.c0.c2, &a.c1.c2};
+    fp2 *tt[6] = {&t.c0.c0, &t.c1.c0, &t.c0.c1, &t.c1.c1, &t.c0.c2, &t.c1.c2};
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        fp2 g, c;
+        fp2_conj(g, *in[k]);
+        if (k == 0) {
+            *tt[k] = g;
+        } else {
+            fp2_load_const(c, LCB_GAMMA3 + 24 * k);
+            fp2_mul(*tt[k], g, c);
+        }
+    }
+    r = t;
+}
+// Granger-Scott cyclotomic squaring (valid for elements of the cyclotomic subgroup)
+DI void fp4_sqr(fp2 &c0, fp2 &c1, const fp2 &a, const fp2 &b) {
+    fp2 t0, t1, t2;
+    fp2_sqr(t0, a);
+    fp2_sqr(t1, b);
+    fp2_mul_xi(t2, t1);
+    fp2_add(c0, t2, t0);
+    fp2_add(t2, a, b);
+    fp2_sqr(t2, t2);
+    fp2_sub(t2, t2, t0);
+    fp2_sub(c1, t2, t1);
+}
+DI void fp12_cyc_sqr(fp12 &r, const fp12 &f) {
+    fp2 z0 = f.c0.c0, z4 = f.c0.c1, z3 = f.c0.c2, z2 = f.c1.c0, z1 = f.c1.c1, z5 = f.c1.c2;
+    fp2 t0, t1, t2, t3;
+    fp4_sqr(t0, t1, z0, z1);
+    fp2_sub(z0, t0, z0); fp2_dbl(z0, z0); fp2_add(z0, z0, t0);
+    fp2_add(z1, t1, z1); fp2_dbl(z1, z1); fp2_add(z1, z1, t1);
+    fp4_sqr(t0, t1, z2, z3);
+    fp4_sqr(t2, t3, z4, z5);
+    fp2_sub(z4, t0, z4); fp2_dbl(z4, z4); fp2_add(z4, z4, t0);
+    fp2_add(z5, t1, z5); fp2_dbl(z5, z5); fp2_add(z5, z5, t1);
+    fp2_mul_xi(t0, t3);
+    fp2_add(z2, t0, z2); fp2_dbl(z2, z2); fp2_add(z2, z2, t0);
+    fp2_sub(z3, t2, z3); fp2_dbl(z3, z3); fp2_add(z3, z3, t2);
+    r.c0.c0 = z0; r.c0.c1 = z4; r.c0.c2 = z3;
+    r.c1.c0 = z2; r.c1.c1 = z1; r.c1.c2 = z5;
+}
+
+// ------------------------------------------------------------------------------------------------ Fr
+// Montgomery arithmetic mod r (8 x 32-bit limbs, R = 2^256), CIOS; used for Lagrange coefficients.
+DI void fr_reduce_once(fr &r, const u32 *t, u32 top) {
+    u32 d[8];
+    u32 br = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        u64 x = (u64)t[j] - LCB_R[j] - br;
+        d[j] = (u32)x;
+        br = (u32)(x >> 32) & 1;
+    }
+    bool ge = top || !br;
+#pragma unroll
+    for (int j = 0; j < 8; j++) r.v[j] = ge ? d[j] : t[j];
+}
+DI void fr_mul(fr &r, const fr &a, const fr &b) {
+    u32 t[10];
+#pragma unroll
+    for (int j = 0; j < 10; j++) t[j] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        u64 c = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            u64 s = (u64)a.v[j] * b.v[i] + t[j] + c;
+            t[j] = (u32)s;
+            c = s >> 32;
+        }
+        u64 s = (u64)t[8] + c;
+        t[8] = (u32)s;
+        t[9] = (u32)(s >> 32);
+        u32 m = t[0] * LCB_R_INV;
+        s = (u64)m * LCB_R[0] + t[0];
+        c = s >> 32;
+#pragma unroll
+        for (int j = 1; j < 8; j++) {
+            s = (u64)m * LCB_R[j] + t[j] + c;
+            t[j - 1] = (u32)s;
+            c = s >> 32;
+        }
+        s = (u64)t[8] + c;
+        t[7] = (u32)s;
+        t[8] = t[9] + (u32)(s >> 32);
+    }
+    fr_reduce_once(r, t, t[8]);
+}
+DI void fr_add(fr &r, const fr &a, const fr &b) {
+    u32 t[8];
+    u32 c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        u64 s = (u64)a.v[j] + b.v[j] + c;
+        t[j] = (u32)s;
+        c = (u32)(s >> 32);
+    }
+    fr_reduce_once(r, t, c);
+}
+DI void fr_sub(fr &r, const fr &a, const fr &b) {
+    u32 t[8];
+    u32 br = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        u64 x = (u64)a.v[j] - b.v[j] - br;
+        t[j] = (u32)x;
+        br = (u32)(x >> 32) & 1;
+    }
+    u32 c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        u64 s = (u64)t[j] + (br ? LCB_R[j] : 0u) + c;
+        r.v[j] = (u32)s;
+        c = (u32)(s >> 32);
+    }
+}
+DI bool fr_is_zero(const fr &a) {
+    u32 x = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) x |= a.v[j];
+    return x == 0;
+}
+DI fr fr_one() { fr r; for (int j = 0; j < 8; j++) r.v[j] = LCB_R_ONE[j]; return r; }
+DI void fr_from_raw(fr &r, const fr &raw) {
+    fr r2;
+    for (int j = 0; j < 8; j++) r2.v[j] = LCB_R_R2[j];
+    fr_mul(r, raw, r2);
+}
+DI void fr_to_raw(fr &r, const fr &a) {
+    fr one;
+    for (int j = 0; j < 8; j++) one.v[j] = j == 0;
+    fr_mul(r, a, one);
+}
+DI bool fr_raw_lt_r(const fr &raw) {
+    u32 br = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        u64 x = (u64)raw.v[j] - LCB_R[j] - br;
+        br = (u32)(x >> 32) & 1;
+    }
+    return br != 0;
+}
+DI void fr_inv(fr &r, const fr &a) {
+    fr acc = fr_one();
+    for (int i = 254; i >= 0; i--) {
+        fr_mul(acc, acc, acc);
+        if ((LCB_R_MINUS_2[i >> 5] >> (i & 31)) & 1) fr_mul(acc, acc, a);
+    }
+    r = acc;
+}
+
+// ------------------------------------------------------------------------------------------------ cold
+// Non-inlined Fp12 routines for the final exponentiation and other coarse uses: each call does >= 50
+// Fp multiplications, so passing operands through the private stack costs little, and it keeps one copy
+// of the code per translation unit (compile time and I-cache).
+DN void fp12_mul_n(fp12 &r, const fp12 &a, const fp12 &b) { fp12 t; fp12_mul(t, a, b); r = t; }
+DN void fp12_sqr_n(fp12 &r, const fp12 &a) { fp12 t; fp12_sqr(t, a); r = t; }
+DN void fp12_cyc_sqr_n(fp12 &r, const fp12 &a) { fp12 t; fp12_cyc_sqr(t, a); r = t; }
+DN void fp12_inv_n(fp12 &r, const fp12 &a) { fp12 t; fp12_inv(t, a); r = t; }
+DN void fp12_frob1_n(fp12 &r, const fp12 &a) { fp12 t; fp12_frob1(t, a); r = t; }
+DN void fp12_frob2_n(fp12 &r, const fp12 &a) { fp12 t; fp12_frob2(t, a); r = t; }
+DN void fp12_frob3_n(fp12 &r, const fp12 &a) { fp12 t; fp12_frob3(t, a); r = t; }
+DN void fp2_inv_n(fp2 &r, const fp2 &a) { fp2 t; fp2_inv(t, a); r = t; }
+DN bool fp2_sqrt_n(fp2 &r, const fp2 &a) { fp2 t; bool ok = fp2_sqrt(t, a); r = t; return ok; }

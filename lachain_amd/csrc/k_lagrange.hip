@@ -1,0 +1,177 @@
+// lachain_amd/csrc/k_lagrange.hip — gfx950 kernels: Lagrange interpolation at 0 and MSM.
+#include "kcommon.hpp"
+
+// ================================================================================= Lagrange at 0
+// lambda_i = prod_{j != i} x_j / (x_j - x_i) (mcl: a = prod x_j, b_i = x_i prod_{j!=i}(x_j - x_i),
+// lambda_i = a / b_i); one lane per problem; writes canonical raw lambdas and a status byte.
+extern "C" __global__ void LCB_BOUNDS k_lagrange_coeffs(const uint8_t *xs, const u32 *off, u32 n_problems,
+                                                       fr *lam_raw, uint8_t *status) {
+    u32 j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_problems) return;
+    u32 o0 = off[j], k = off[j + 1] - o0;
+    bool ok = k > 0;
+    // a = prod x
+    fr a = fr_one();
+    for (u32 i = 0; i < k && ok; i++) {
+        fr xr, x;
+        const u32 *w = (const u32 *)(xs + 32 * (size_t)(o0 + i));
+        for (int q = 0; q < 8; q++) xr.v[q] = w[q];
+        if (!fr_raw_lt_r(xr) || fr_is_zero(xr)) { ok = false; break; }
+        fr_from_raw(x, xr);
+        fr_mul(a, a, x);
+    }
+    // b_i and prefix products for one batch inversion (stored in lam_raw as scratch)
+    fr acc = fr_one();
+    for (u32 i = 0; i < k && ok; i++) {
+        fr xi_r, xi;
+        const u32 *w = (const u32 *)(xs + 32 * (size_t)(o0 + i));
+        for (int q = 0; q < 8; q++) xi_r.v[q] = w[q];
+        fr_from_raw(xi, xi_r);
+        fr b = xi;
+        for (u32 t = 0; t < k; t++) {
+            if (t == i) continue;
+            fr xt_r, xt, d;
+            const u32 *wt = (const u32 *)(xs + 32 * (size_t)(o0 + t));
+            for (int q = 0; q < 8; q++) xt_r.v[q] = wt[q];
+            fr_from_raw(xt, xt_r);
+            fr_sub(d, xt, xi);
+            if (fr_is_zero(d)) { ok = false; break; }
+            fr_mul(b, b, d);
+        }
+        if (!ok) break;
+        lam_raw[o0 + i] = b;      // b_i (Montgomery) for now
+    }
+    if (ok) {
+        // batch inversion of b_i: prefix products, one inversion, back-substitution
+        for (u32 i = 0; i < k; i++) {
+            fr b = lam_raw[o0 + i];
+            fr_mul(acc, acc, b);
+        }
+        fr inv;
+        fr_inv(inv, acc);
+        for (u32 i = k; i-- > 0;) {
+            // inv = 1/(b_0..b_i); prefix up to i-1 recomputed (k is small: O(k^2) Fr muls overall)
+            fr pre = fr_one();
+            for (u32 t = 0; t < i; t++) fr_mul(pre, pre, lam_raw[o0 + t]);
+            fr bi_inv, l, lr;
+            fr_mul(bi_inv, inv, pre);
+            fr_mul(inv, inv, lam_raw[o0 + i]);
+            fr_mul(l, a, bi_inv);
+            fr_to_raw(lr, l);
+            lam_raw[o0 + i] = lr;
+        }
+    }
+    status[j] = ok;
+}
+// partial products lambda_i * Y_i for every entry (one lane per entry)
+extern "C" __global__ void LCB_BOUNDS k_g1_mul_lanes(const uint8_t *ys, const fr *lam_raw, u32 n_entries, g1 *out,
+                                                    uint8_t *ok_out) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_entries) return;
+    g1a A;
+    bool ok = g1_decompress(A, ys + 48 * (size_t)i);
+    g1 P, R;
+    jac_from_aff(P, A);
+    fr k = lam_raw[i];
+    jac_mul_bits(R, P, k.v, 255);
+    out[i] = R;
+    ok_out[i] = ok;
+}
+extern "C" __global__ void LCB_BOUNDS k_g2_mul_lanes(const uint8_t *ys, const fr *lam_raw, u32 n_entries, g2 *out,
+                                                    uint8_t *ok_out) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_entries) return;
+    g2a A;
+    bool ok = g2_decompress(A, ys + 96 * (size_t)i);
+    g2 P, R;
+    jac_from_aff(P, A);
+    fr k = lam_raw[i];
+    jac_mul_bits(R, P, k.v, 255);
+    out[i] = R;
+    ok_out[i] = ok;
+}
+extern "C" __global__ void LCB_BOUNDS k_g1_sum(const g1 *parts, const uint8_t *ok_in, const u32 *off, u32 n_problems,
+                                              uint8_t *status, uint8_t *out) {
+    u32 j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_problems) return;
+    g1 acc;
+    jac_set_inf(acc);
+    bool ok = status[j];
+    for (u32 i = off[j]; i < off[j + 1]; i++) {
+        ok = ok && ok_in[i];
+        jac_add(acc, acc, parts[i]);
+    }
+    if (!ok) jac_set_inf(acc);
+    g1_compress_jac(out + 48 * (size_t)j, acc);
+    status[j] = ok;
+}
+extern "C" __global__ void LCB_BOUNDS k_g2_sum(const g2 *parts, const uint8_t *ok_in, const u32 *off, u32 n_problems,
+                                              uint8_t *status, uint8_t *out) {
+    u32 j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_problems) return;
+    g2 acc;
+    jac_set_inf(acc);
+    bool ok = status[j];
+    for (u32 i = off[j]; i < off[j + 1]; i++) {
+        ok = ok && ok_in[i];
+        jac_add(acc, acc, parts[i]);
+    }
+    if (!ok) jac_set_inf(acc);
+    g2_compress_jac(out + 96 * (size_t)j, acc);
+    status[j] = ok;
+}
+
+// ================================================================================= MSM (v0: per-point
+// products + pairwise tree reduction; the bucketed Pippenger is the next step)
+extern "C" __global__ void LCB_BOUNDS k_g1_msm_products(const uint8_t *pts, const uint8_t *scalars, u32 n, g1 *out,
+                                                       uint8_t *ok_out) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    g1a A;
+    bool ok = g1_decompress(A, pts + 48 * (size_t)i);
+    fr k;
+    const u32 *sw = (const u32 *)(scalars + 32 * (size_t)i);
+    for (int j = 0; j < 8; j++) k.v[j] = sw[j];
+    ok = ok && fr_raw_lt_r(k);
+    g1 P, R;
+    jac_from_aff(P, A);
+    jac_mul_bits(R, P, k.v, 255);
+    out[i] = R;
+    ok_out[i] = ok;
+}
+extern "C" __global__ void LCB_BOUNDS k_g1_reduce_pairs(g1 *v, u32 n_half, u32 n) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_half) return;
+    u32 j = i + n_half;
+    if (j < n) jac_add(v[i], v[i], v[j]);
+}
+extern "C" __global__ void k_g1_finish(const g1 *v, uint8_t *out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) g1_compress_jac(out, v[0]);
+}
+
+
+// ---------------------------------------------------------------- host launch wrappers
+extern "C" void lcbk_lagrange_coeffs(dim3 grid, hipStream_t s, const uint8_t *xs, const u32 *off, u32 n_problems, void *lam_raw, uint8_t *status) {
+    LCB_LAUNCH(k_lagrange_coeffs, xs, off, n_problems, (fr *)lam_raw, status);
+}
+extern "C" void lcbk_g1_mul_lanes(dim3 grid, hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out) {
+    LCB_LAUNCH(k_g1_mul_lanes, ys, (const fr *)lam_raw, n_entries, (g1 *)out, ok_out);
+}
+extern "C" void lcbk_g2_mul_lanes(dim3 grid, hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out) {
+    LCB_LAUNCH(k_g2_mul_lanes, ys, (const fr *)lam_raw, n_entries, (g2 *)out, ok_out);
+}
+extern "C" void lcbk_g1_sum(dim3 grid, hipStream_t s, const void *parts, const uint8_t *ok_in, const u32 *off, u32 n_problems, uint8_t *status, uint8_t *out) {
+    LCB_LAUNCH(k_g1_sum, (const g1 *)parts, ok_in, off, n_problems, status, out);
+}
+extern "C" void lcbk_g2_sum(dim3 grid, hipStream_t s, const void *parts, const uint8_t *ok_in, const u32 *off, u32 n_problems, uint8_t *status, uint8_t *out) {
+    LCB_LAUNCH(k_g2_sum, (const g2 *)parts, ok_in, off, n_problems, status, out);
+}
+extern "C" void lcbk_g1_msm_products(dim3 grid, hipStream_t s, const uint8_t *pts, const uint8_t *scalars, u32 n, void *out, uint8_t *ok_out) {
+    LCB_LAUNCH(k_g1_msm_products, pts, scalars, n, (g1 *)out, ok_out);
+}
+extern "C" void lcbk_g1_reduce_pairs(dim3 grid, hipStream_t s, void *v, u32 n_half, u32 n) {
+    LCB_LAUNCH(k_g1_reduce_pairs, (g1 *)v, n_half, n);
+}
+extern "C" void lcbk_g1_finish(dim3 grid, hipStream_t s, const void *v, uint8_t *out) {
+    LCB_LAUNCH(k_g1_finish, (const g1 *)v, out);
+}

@@ -1,0 +1,117 @@
+// lachain_amd/csrc/k_tpke.hip — gfx950 kernels: TPKE decryption-share pipeline (decompression, per-ciphertext preparation, per-share verification, partial decryption).
+#include "kcommon.hpp"
+
+// ================================================================================= decompression
+extern "C" __global__ void LCB_BOUNDS k_g1_decompress(const uint8_t *in, u32 n, g1a_st *out) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    g1a a;
+    bool ok = g1_decompress(a, in + 48 * (size_t)i);
+    g1a_st s;
+    s.x = a.x; s.y = a.y; s.inf = ok ? (u32)a.inf : 1u; s.ok = ok; s.pad[0] = s.pad[1] = 0;
+    out[i] = s;
+}
+extern "C" __global__ void LCB_BOUNDS k_g2_decompress(const uint8_t *in, u32 n, g2a_st *out) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    g2a a;
+    bool ok = g2_decompress(a, in + 96 * (size_t)i);
+    g2a_st s;
+    s.x = a.x; s.y = a.y; s.inf = ok ? (u32)a.inf : 1u; s.ok = ok; s.pad[0] = s.pad[1] = 0;
+    out[i] = s;
+}
+
+// ================================================================================= TPKE
+// lines layout: lines[(2*c + 0) * LINESET] = H lines, lines[(2*c + 1) * LINESET] = W lines
+extern "C" __global__ void LCB_BOUNDS k_tpke_ct_prepare(const uint8_t *cts_u, const uint8_t *cts_w,
+                                                       const uint8_t *v_data, const u32 *v_off, u32 n_cts,
+                                                       u32 *lines, uint8_t *ct_ok, int orig_cof) {
+    u32 c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_cts) return;
+    const uint8_t *ub = cts_u + 48 * (size_t)c;
+    g1a U;
+    g2a W, Ha;
+    bool ok = g1_decompress(U, ub);
+    ok = g2_decompress(W, cts_w + 96 * (size_t)c) && ok;
+    // H = G2.SetHashOf(U.ToBytes() || V): for a valid U the wire bytes are its canonical encoding
+    uint8_t d[64];
+    u32 v0 = v_off[c], v1 = v_off[c + 1];
+    sha512_2(d, ub, 48, v_data + v0, v1 - v0);
+    g2 H;
+    bool hok = g2_hash_digest(H, d, orig_cof != 0);
+    ok = ok && hok;
+    if (hok) jac_to_aff(Ha, H);
+    else { Ha.inf = true; Ha.x = fp2_zero(); Ha.y = fp2_zero(); }
+    if (!ok) { W.inf = true; Ha.inf = true; }
+    lineset_compute(lines + (size_t)(2 * c) * LCB_LINESET_WORDS, Ha);
+    lineset_compute(lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS, W);
+    ct_ok[c] = ok;
+}
+
+extern "C" __global__ void LCB_BOUNDS k_tpke_verify(const u32 *lines, const uint8_t *ct_ok, const g1a_st *keys,
+                                                   u32 n_keys, const u32 *ct_idx, const u32 *dec_idx,
+                                                   const uint8_t *ui, u32 n, uint8_t *accept) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    u32 c = ct_idx[i], d = dec_idx[i];
+    g1a Ui, Y;
+    bool ok = d < n_keys && ct_ok[c];
+    ok = g1_decompress(Ui, ui + 48 * (size_t)i) && ok;
+    g1a_st ks = keys[d < n_keys ? d : 0];
+    ok = ok && ks.ok;
+    st_to_g1a(Y, ks);
+    fp_neg(Y.y, Y.y); // -Y: e(Ui, H) == e(Y, W)  <=>  e(Ui, H) e(-Y, W) == 1
+    LinesFromMemory sH{lines + (size_t)(2 * c) * LCB_LINESET_WORDS};
+    LinesFromMemory sW{lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS};
+    fp12 f, e;
+    miller2(f, sH, Ui, sW, Y);
+    final_exp(e, f);
+    accept[i] = ok && fp12_is_one(e);
+}
+
+// TPKE.PrivateKey.Decrypt: validity e(G, W) == e(U, H) <=> e(-G, W) e(U, H) == 1; then Ui = x U
+extern "C" __global__ void LCB_BOUNDS k_tpke_partial_decrypt(const u32 *lines, const uint8_t *ct_ok,
+                                                            const uint8_t *cts_u, const fr *x_raw, u32 n_cts,
+                                                            uint8_t *ui_out, uint8_t *status) {
+    u32 c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_cts) return;
+    g1a U, G;
+    bool ok = g1_decompress(U, cts_u + 48 * (size_t)c) && ct_ok[c];
+    g1_generator(G);
+    fp_neg(G.y, G.y);
+    LinesFromMemory sH{lines + (size_t)(2 * c) * LCB_LINESET_WORDS};
+    LinesFromMemory sW{lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS};
+    fp12 f, e;
+    miller2(f, sH, U, sW, G);
+    final_exp(e, f);
+    ok = ok && fp12_is_one(e);
+    status[c] = ok;
+    g1 Uj, R;
+    jac_from_aff(Uj, U);
+    fr k = *x_raw;
+    jac_mul_bits(R, Uj, k.v, 256);
+    uint8_t *o = ui_out + 48 * (size_t)c;
+    if (ok) g1_compress_jac(o, R);
+    else {
+        fp z = fp_zero();
+        raw_to_bytes48(o, z);
+    }
+}
+
+
+// ---------------------------------------------------------------- host launch wrappers
+extern "C" void lcbk_g1_decompress(dim3 grid, hipStream_t s, const uint8_t *in, u32 n, void *out) {
+    LCB_LAUNCH(k_g1_decompress, in, n, (g1a_st *)out);
+}
+extern "C" void lcbk_g2_decompress(dim3 grid, hipStream_t s, const uint8_t *in, u32 n, void *out) {
+    LCB_LAUNCH(k_g2_decompress, in, n, (g2a_st *)out);
+}
+extern "C" void lcbk_tpke_ct_prepare(dim3 grid, hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data, const u32 *v_off, u32 n_cts, u32 *lines, uint8_t *ct_ok, int orig_cof) {
+    LCB_LAUNCH(k_tpke_ct_prepare, cts_u, cts_w, v_data, v_off, n_cts, lines, ct_ok, orig_cof);
+}
+extern "C" void lcbk_tpke_verify(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, uint8_t *accept) {
+    LCB_LAUNCH(k_tpke_verify, lines, ct_ok, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, accept);
+}
+extern "C" void lcbk_tpke_partial_decrypt(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, const uint8_t *cts_u, const void *x_raw, u32 n_cts, uint8_t *ui_out, uint8_t *status) {
+    LCB_LAUNCH(k_tpke_partial_decrypt, lines, ct_ok, cts_u, (const fr *)x_raw, n_cts, ui_out, status);
+}

@@ -1,0 +1,52 @@
+// lachain_amd/csrc/k_ts.hip — gfx950 kernels: threshold-signature share verification.
+#include "kcommon.hpp"
+
+// ================================================================================= threshold signatures
+extern "C" __global__ void LCB_BOUNDS k_ts_msg_prepare(const uint8_t *msg_data, const u32 *msg_off, u32 n_msgs,
+                                                      u32 *lines, uint8_t *msg_ok, int orig_cof) {
+    u32 m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= n_msgs) return;
+    uint8_t d[64];
+    u32 o0 = msg_off[m], o1 = msg_off[m + 1];
+    sha512_2(d, msg_data + o0, o1 - o0, msg_data, 0);
+    g2 H;
+    g2a Ha;
+    bool ok = g2_hash_digest(H, d, orig_cof != 0);
+    if (ok) jac_to_aff(Ha, H);
+    else { Ha.inf = true; Ha.x = fp2_zero(); Ha.y = fp2_zero(); }
+    lineset_compute(lines + (size_t)m * LCB_LINESET_WORDS, Ha);
+    msg_ok[m] = ok;
+}
+// ValidateSignature: e(PK, H) == e(G, sig) <=> e(PK, H) e(-G, sig) == 1
+extern "C" __global__ void LCB_BOUNDS k_ts_verify(const u32 *lines, const uint8_t *msg_ok, const g1a_st *pks,
+                                                 u32 n_pks, const uint8_t *sigs, const u32 *msg_idx,
+                                                 const u32 *pk_idx, u32 n, uint8_t *accept) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    u32 m = msg_idx[i], k = pk_idx[i];
+    g2a S;
+    g1a PK, G;
+    bool ok = k < n_pks && msg_ok[m];
+    ok = g2_decompress(S, sigs + 96 * (size_t)i) && ok;
+    g1a_st ps = pks[k < n_pks ? k : 0];
+    ok = ok && ps.ok;
+    st_to_g1a(PK, ps);
+    g1_generator(G);
+    fp_neg(G.y, G.y);
+    LinesFromMemory sH{lines + (size_t)m * LCB_LINESET_WORDS};
+    LinesOnTheFly sS;
+    sS.init(S);
+    fp12 f, e;
+    miller2(f, sH, PK, sS, G);
+    final_exp(e, f);
+    accept[i] = ok && fp12_is_one(e);
+}
+
+
+// ---------------------------------------------------------------- host launch wrappers
+extern "C" void lcbk_ts_msg_prepare(dim3 grid, hipStream_t s, const uint8_t *msg_data, const u32 *msg_off, u32 n_msgs, u32 *lines, uint8_t *msg_ok, int orig_cof) {
+    LCB_LAUNCH(k_ts_msg_prepare, msg_data, msg_off, n_msgs, lines, msg_ok, orig_cof);
+}
+extern "C" void lcbk_ts_verify(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *msg_ok, const void *pks, u32 n_pks, const uint8_t *sigs, const u32 *msg_idx, const u32 *pk_idx, u32 n, uint8_t *accept) {
+    LCB_LAUNCH(k_ts_verify, lines, msg_ok, (const g1a_st *)pks, n_pks, sigs, msg_idx, pk_idx, n, accept);
+}

@@ -1,0 +1,18 @@
+// lachain_amd/csrc/kcommon.hpp — shared definitions of the kernel translation units.
+#pragma once
+#include "h2g2.hpp"
+#include "pairing.hpp"
+#include "ops.h"
+
+#define LCB_BLOCK 256
+#define LCB_BOUNDS __launch_bounds__(LCB_BLOCK, 1)
+
+// affine point records in device memory
+struct g1a_st { fp x, y; u32 inf, ok, pad[2]; };   // 112 B
+struct g2a_st { fp2 x, y; u32 inf, ok, pad[2]; };  // 208 B
+DI void st_to_g1a(g1a &a, const g1a_st &s) { a.x = s.x; a.y = s.y; a.inf = s.inf != 0; }
+DI void st_to_g2a(g2a &a, const g2a_st &s) { a.x = s.x; a.y = s.y; a.inf = s.inf != 0; }
+
+#define LCB_LAUNCH(name, ...) hipLaunchKernelGGL(name, grid, dim3(LCB_BLOCK), 0, s, __VA_ARGS__)
+static_assert(sizeof(g1a_st) == 112 && sizeof(g2a_st) == 208, "record sizes");
+static_assert(sizeof(g1) == 144 && sizeof(g2) == 288 && sizeof(fr) == 32, "struct sizes");

@@ -1,0 +1,37 @@
+// lachain_amd/csrc/launch.h — host-side launch wrappers exported by the kernel translation units
+// (device-internal record types are passed as opaque pointers).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "ops.h"
+typedef uint32_t u32;
+extern "C" void lcbk_g1_decompress(dim3 grid, hipStream_t s, const uint8_t *in, u32 n, void *out);
+extern "C" void lcbk_g2_decompress(dim3 grid, hipStream_t s, const uint8_t *in, u32 n, void *out);
+extern "C" void lcbk_tpke_ct_prepare(dim3 grid, hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data, const u32 *v_off, u32 n_cts, u32 *lines, uint8_t *ct_ok, int orig_cof);
+extern "C" void lcbk_tpke_verify(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, uint8_t *accept);
+extern "C" void lcbk_tpke_partial_decrypt(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, const uint8_t *cts_u, const void *x_raw, u32 n_cts, uint8_t *ui_out, uint8_t *status);
+extern "C" void lcbk_ts_msg_prepare(dim3 grid, hipStream_t s, const uint8_t *msg_data, const u32 *msg_off, u32 n_msgs, u32 *lines, uint8_t *msg_ok, int orig_cof);
+extern "C" void lcbk_ts_verify(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *msg_ok, const void *pks, u32 n_pks, const uint8_t *sigs, const u32 *msg_idx, const u32 *pk_idx, u32 n, uint8_t *accept);
+extern "C" void lcbk_g1_mul(dim3 grid, hipStream_t s, const uint8_t *pts, int use_gen, const uint8_t *scalars, u32 n, uint8_t *out, uint8_t *ok_out);
+extern "C" void lcbk_g2_mul(dim3 grid, hipStream_t s, const uint8_t *pts, int use_gen, const uint8_t *scalars, u32 n, uint8_t *out, uint8_t *ok_out);
+extern "C" void lcbk_g2_hash(dim3 grid, hipStream_t s, const uint8_t *msg_data, const u32 *msg_off, u32 n, uint8_t *out, uint8_t *ok_out, int orig_cof);
+extern "C" void lcbk_tpke_encrypt1(dim3 grid, hipStream_t s, const uint8_t *ybytes, const uint8_t *rs, u32 n, uint8_t *u_out, uint8_t *t_out, uint8_t *ok_out);
+extern "C" void lcbk_tpke_encrypt2(dim3 grid, hipStream_t s, const uint8_t *u, const uint8_t *rs, const uint8_t *v_data, const u32 *v_off, u32 n, uint8_t *w_out, uint8_t *ok_out, int orig_cof);
+extern "C" void lcbk_ts_sign(dim3 grid, hipStream_t s, const uint8_t *sks, const uint8_t *msg_data, const u32 *msg_off, const u32 *msg_idx, u32 n, uint8_t *out, uint8_t *ok_out, int orig_cof);
+extern "C" void lcbk_lagrange_coeffs(dim3 grid, hipStream_t s, const uint8_t *xs, const u32 *off, u32 n_problems, void *lam_raw, uint8_t *status);
+extern "C" void lcbk_g1_mul_lanes(dim3 grid, hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out);
+extern "C" void lcbk_g2_mul_lanes(dim3 grid, hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out);
+extern "C" void lcbk_g1_sum(dim3 grid, hipStream_t s, const void *parts, const uint8_t *ok_in, const u32 *off, u32 n_problems, uint8_t *status, uint8_t *out);
+extern "C" void lcbk_g2_sum(dim3 grid, hipStream_t s, const void *parts, const uint8_t *ok_in, const u32 *off, u32 n_problems, uint8_t *status, uint8_t *out);
+extern "C" void lcbk_g1_msm_products(dim3 grid, hipStream_t s, const uint8_t *pts, const uint8_t *scalars, u32 n, void *out, uint8_t *ok_out);
+extern "C" void lcbk_g1_reduce_pairs(dim3 grid, hipStream_t s, void *v, u32 n_half, u32 n);
+extern "C" void lcbk_g1_finish(dim3 grid, hipStream_t s, const void *v, uint8_t *out);
+extern "C" void lcbk_op(dim3 grid, hipStream_t s, int op, u32 *io, int orig_cof);
+
+// sizes of the device records the host allocates
+#define LCB_G1A_ST_BYTES 112
+#define LCB_G2A_ST_BYTES 208
+#define LCB_FR_BYTES 32
+#define LCB_G1_JAC_BYTES 144
+#define LCB_G2_JAC_BYTES 288
+#define LCB_LINESET_BYTES 19584

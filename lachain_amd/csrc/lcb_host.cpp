@@ -1,0 +1,783 @@
+// lachain_amd/csrc/lcb_host.hip — host implementation of include/lachain_bls.h (liblachain_bls.so).
+//
+// Every arithmetic operation is executed by a gfx950 kernel (kernels.hip); the host only moves bytes,
+// validates arguments, and serializes GPU submission with a per-process lock (the reference calls mcl
+// concurrently from one thread per consensus protocol, /root/reference/src/Lachain.Consensus/AbstractProtocol.cs:46-47).
+// There is deliberately no CPU fallback: without a gfx950 device mclBn_init returns -1 and every entry
+// point fails (returns -1 / 0 bytes / leaves outputs zeroed) with lcb_last_error() describing why.
+#include <hip/hip_runtime.h>
+#include <string.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <mutex>
+#include <vector>
+#include <string>
+#include <sys/random.h>
+
+#include "launch.h"
+#include "bls_constants_host.h"
+#include "../../include/lachain_bls.h"
+#include "host_sha3.hpp"
+
+#define LCB_BLOCK 256
+
+namespace {
+
+std::mutex g_mu;
+int g_device = 0;
+bool g_ready = false;
+int g_orig_cofactor = 0;
+hipStream_t g_stream = nullptr;
+u32 *g_io = nullptr;          // device buffer for single operations
+u32 *g_io_host = nullptr;     // pinned staging
+const size_t IO_WORDS = 4096; // 16 KB
+thread_local std::string g_err;
+
+void set_err(const char *what, hipError_t e = hipSuccess) {
+    char buf[256];
+    if (e != hipSuccess) snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+    else snprintf(buf, sizeof buf, "%s", what);
+    g_err = buf;
+}
+
+bool init_locked() {
+    if (g_ready) return true;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= g_device) { set_err("no HIP device", e); return false; }
+    if ((e = hipSetDevice(g_device)) != hipSuccess) { set_err("hipSetDevice", e); return false; }
+    hipDeviceProp_t prop;
+    if ((e = hipGetDeviceProperties(&prop, g_device)) != hipSuccess) { set_err("hipGetDeviceProperties", e); return false; }
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) { set_err("device is not gfx950"); return false; }
+    if ((e = hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking)) != hipSuccess) { set_err("stream", e); return false; }
+    if ((e = hipMalloc(&g_io, IO_WORDS * 4)) != hipSuccess) { set_err("hipMalloc io", e); return false; }
+    if ((e = hipHostMalloc(&g_io_host, IO_WORDS * 4, hipHostMallocDefault)) != hipSuccess) { set_err("hipHostMalloc", e); return false; }
+    g_ready = true;
+    return true;
+}
+
+// run one k_op on the staging buffer: copy `in_words` words to the device, launch, copy `out_words` back
+bool run_op(int op, size_t in_words, size_t out_words) {
+    hipError_t e;
+    if ((e = hipMemcpyAsync(g_io, g_io_host, in_words * 4, hipMemcpyHostToDevice, g_stream)) != hipSuccess) { set_err("H2D", e); return false; }
+    lcbk_op(dim3(1), g_stream, op, g_io, g_orig_cofactor);
+    if ((e = hipGetLastError()) != hipSuccess) { set_err("k_op launch", e); return false; }
+    if ((e = hipMemcpyAsync(g_io_host, g_io, out_words * 4, hipMemcpyDeviceToHost, g_stream)) != hipSuccess) { set_err("D2H", e); return false; }
+    if ((e = hipStreamSynchronize(g_stream)) != hipSuccess) { set_err("k_op", e); return false; }
+    return true;
+}
+
+#define LOCKED_OR(ret)                        \
+    std::lock_guard<std::mutex> lk_(g_mu);    \
+    if (!init_locked()) return ret;
+
+// ------------------------------------------------------------------ device buffers for batch calls
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    void *get(size_t n) {
+        if (n == 0) n = 16;
+        if (n > cap) {
+            if (p) hipFree(p);
+            p = nullptr;
+            if (hipMalloc(&p, n) != hipSuccess) { cap = 0; return nullptr; }
+            cap = n;
+        }
+        return p;
+    }
+};
+DevBuf b_lines, b_ctok, b_keys, b_in[8], b_out[4];
+
+inline u32 nblk(size_t n) { return (u32)((n + LCB_BLOCK - 1) / LCB_BLOCK); }
+
+template <class T> T *up(DevBuf &b, const T *src, size_t count, hipStream_t s) {
+    T *d = (T *)b.get(count * sizeof(T));
+    if (d && count) hipMemcpyAsync(d, src, count * sizeof(T), hipMemcpyHostToDevice, s);
+    return d;
+}
+
+bool sync_check(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(g_stream);
+    if (e != hipSuccess) { set_err(what, e); return false; }
+    return true;
+}
+
+} // namespace
+
+// ================================================================== init / config
+extern "C" int lcb_set_device(int id) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_ready) return id == g_device ? 0 : -1;
+    g_device = id;
+    return 0;
+}
+extern "C" int lcb_get_device(void) { return g_device; }
+extern "C" void lcb_set_original_g2_cofactor(int enable) { g_orig_cofactor = enable != 0; }
+extern "C" const char *lcb_last_error(void) { return g_err.c_str(); }
+
+extern "C" int mclBn_init(int curve, int compiledTimeVar) {
+    if (curve != MCL_BLS12_381 || compiledTimeVar != MCLBN_COMPILED_TIME_VAR) {
+        set_err("unsupported curve / compiledTimeVar");
+        return -1;
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    return init_locked() ? 0 : -1;
+}
+extern "C" int mclBn_getOpUnitSize(void) { return 6; }
+extern "C" int mclBn_getG1ByteSize(void) { return 48; }
+extern "C" int mclBn_getFrByteSize(void) { return 32; }
+extern "C" int mclBn_getFpByteSize(void) { return 48; }
+
+// ================================================================== Fr
+static int fr_set_raw(mclBnFr *y, const u32 raw[8]) {
+    LOCKED_OR(-1)
+    memcpy(g_io_host + 8, raw, 32);
+    if (!run_op(OP_FR_FROM_RAW, 25, 25) || !g_io_host[24]) { memset(y, 0, 32); return -1; }
+    memcpy(y, g_io_host, 32);
+    return 0;
+}
+static int fr_get_raw(u32 raw[8], const mclBnFr *x) {
+    LOCKED_OR(-1)
+    memcpy(g_io_host + 8, x, 32);
+    if (!run_op(OP_FR_TO_RAW, 16, 8)) return -1;
+    memcpy(raw, g_io_host, 32);
+    return 0;
+}
+extern "C" int mclBnFr_setInt(mclBnFr *y, mclInt x) {
+    u32 raw[8] = {0};
+    uint64_t ax = x < 0 ? (uint64_t)(-(x + 1)) + 1 : (uint64_t)x;
+    raw[0] = (u32)ax; raw[1] = (u32)(ax >> 32);
+    if (fr_set_raw(y, raw)) return -1;
+    if (x < 0) mclBnFr_neg(y, y);
+    return 0;
+}
+extern "C" int mclBnFr_setInt32(mclBnFr *y, int x) { return mclBnFr_setInt(y, x); }
+extern "C" int mclBnFr_setByCSPRNG(mclBnFr *x) {
+    // rejection sampling of a uniform 255-bit value < r (host randomness, device conversion)
+    for (int tries = 0; tries < 64; tries++) {
+        u32 raw[8];
+        if (getrandom(raw, sizeof raw, 0) != (ssize_t)sizeof raw) return -1;
+        raw[7] &= 0x7fffffffu;
+        if (fr_set_raw(x, raw) == 0) return 0;
+    }
+    return -1;
+}
+extern "C" int mclBnFr_setLittleEndian(mclBnFr *x, const void *buf, mclSize n) {
+    // mcl setArrayMask: take at most 32 bytes, mask to 255 bits, and to 254 if still >= r
+    u32 raw[8] = {0};
+    memcpy(raw, buf, n < 32 ? n : 32);
+    raw[7] &= 0x7fffffffu;
+    static const u32 R_[8] = {0x00000001, 0xffffffff, 0xfffe5bfe, 0x53bda402, 0x09a1d805, 0x3339d808, 0x299d7d48, 0x73eda753};
+    bool ge = true;
+    for (int j = 7; j >= 0; j--) {
+        if (raw[j] != R_[j]) { ge = raw[j] > R_[j]; break; }
+    }
+    if (ge) raw[7] &= 0x3fffffffu;
+    return fr_set_raw(x, raw);
+}
+extern "C" mclSize mclBnFr_serialize(void *buf, mclSize max, const mclBnFr *x) {
+    if (max < 32) return 0;
+    u32 raw[8];
+    if (fr_get_raw(raw, x)) return 0;
+    memcpy(buf, raw, 32);
+    return 32;
+}
+extern "C" mclSize mclBnFr_deserialize(mclBnFr *x, const void *buf, mclSize n) {
+    if (n < 32) return 0;
+    u32 raw[8];
+    memcpy(raw, buf, 32);
+    return fr_set_raw(x, raw) == 0 ? 32 : 0;
+}
+extern "C" void mclBnFr_clear(mclBnFr *x) { memset(x, 0, sizeof *x); }
+extern "C" int mclBnFr_isValid(const mclBnFr *x) {
+    static const u32 R_[8] = {0x00000001, 0xffffffff, 0xfffe5bfe, 0x53bda402, 0x09a1d805, 0x3339d808, 0x299d7d48, 0x73eda753};
+    const u32 *w = (const u32 *)x;
+    for (int j = 7; j >= 0; j--)
+        if (w[j] != R_[j]) return w[j] < R_[j];
+    return 0;
+}
+extern "C" int mclBnFr_isEqual(const mclBnFr *x, const mclBnFr *y) { return memcmp(x, y, 32) == 0; }
+extern "C" int mclBnFr_isZero(const mclBnFr *x) {
+    static const mclBnFr z = {{0, 0, 0, 0}};
+    return memcmp(x, &z, 32) == 0;
+}
+extern "C" int mclBnFr_isOne(const mclBnFr *x) {
+    u32 raw[8];
+    if (fr_get_raw(raw, x)) return 0;
+    for (int j = 1; j < 8; j++) if (raw[j]) return 0;
+    return raw[0] == 1;
+}
+static void fr_binop(int op, mclBnFr *z, const mclBnFr *x, const mclBnFr *y) {
+    LOCKED_OR()
+    memcpy(g_io_host + 8, x, 32);
+    if (y) memcpy(g_io_host + 16, y, 32);
+    if (run_op(op, 24, 8)) memcpy(z, g_io_host, 32);
+}
+extern "C" void mclBnFr_neg(mclBnFr *y, const mclBnFr *x) { fr_binop(OP_FR_NEG, y, x, nullptr); }
+extern "C" void mclBnFr_inv(mclBnFr *y, const mclBnFr *x) { fr_binop(OP_FR_INV, y, x, nullptr); }
+extern "C" void mclBnFr_sqr(mclBnFr *y, const mclBnFr *x) { fr_binop(OP_FR_MUL, y, x, x); }
+extern "C" void mclBnFr_add(mclBnFr *z, const mclBnFr *x, const mclBnFr *y) { fr_binop(OP_FR_ADD, z, x, y); }
+extern "C" void mclBnFr_sub(mclBnFr *z, const mclBnFr *x, const mclBnFr *y) { fr_binop(OP_FR_SUB, z, x, y); }
+extern "C" void mclBnFr_mul(mclBnFr *z, const mclBnFr *x, const mclBnFr *y) { fr_binop(OP_FR_MUL, z, x, y); }
+extern "C" void mclBnFr_div(mclBnFr *z, const mclBnFr *x, const mclBnFr *y) {
+    mclBnFr t;
+    mclBnFr_inv(&t, y);
+    mclBnFr_mul(z, x, &t);
+}
+
+// ================================================================== G1
+extern "C" mclSize mclBnG1_serialize(void *buf, mclSize max, const mclBnG1 *x) {
+    if (max < 48) return 0;
+    LOCKED_OR(0)
+    memcpy(g_io_host + 36, x, 144);
+    if (!run_op(OP_G1_SER, 72, 128)) return 0;
+    memcpy(buf, g_io_host + 116, 48);
+    return 48;
+}
+extern "C" mclSize mclBnG1_deserialize(mclBnG1 *x, const void *buf, mclSize n) {
+    if (n < 48) return 0;
+    LOCKED_OR(0)
+    memcpy(g_io_host + 116, buf, 48);
+    if (!run_op(OP_G1_DESER, 128, 129) || !g_io_host[128]) return 0;
+    memcpy(x, g_io_host, 144);
+    return 48;
+}
+static int g1_flag_op(int op, const mclBnG1 *x, const mclBnG1 *y) {
+    LOCKED_OR(0)
+    memcpy(g_io_host + 36, x, 144);
+    if (y) memcpy(g_io_host + 72, y, 144);
+    if (!run_op(op, 108, 129)) return 0;
+    return (int)g_io_host[128];
+}
+extern "C" int mclBnG1_isValid(const mclBnG1 *x) { return g1_flag_op(OP_G1_VALID, x, nullptr); }
+extern "C" int mclBnG1_isEqual(const mclBnG1 *x, const mclBnG1 *y) { return g1_flag_op(OP_G1_EQ, x, y); }
+extern "C" int mclBnG1_isZero(const mclBnG1 *x) {
+    static const u32 z[12] = {0};
+    return memcmp(&x->z, z, 48) == 0;
+}
+extern "C" void mclBnG1_clear(mclBnG1 *x) { memset(x, 0, sizeof *x); }
+static void g1_op(int op, mclBnG1 *z, const mclBnG1 *x, const mclBnG1 *y, const mclBnFr *k) {
+    LOCKED_OR()
+    memcpy(g_io_host + 36, x, 144);
+    if (y) memcpy(g_io_host + 72, y, 144);
+    if (k) memcpy(g_io_host + 108, k, 32);
+    if (run_op(op, 116, 36)) memcpy(z, g_io_host, 144);
+}
+extern "C" void mclBnG1_neg(mclBnG1 *y, const mclBnG1 *x) { g1_op(OP_G1_NEG, y, x, nullptr, nullptr); }
+extern "C" void mclBnG1_dbl(mclBnG1 *y, const mclBnG1 *x) { g1_op(OP_G1_DBL, y, x, nullptr, nullptr); }
+extern "C" void mclBnG1_normalize(mclBnG1 *y, const mclBnG1 *x) { g1_op(OP_G1_NORM, y, x, nullptr, nullptr); }
+extern "C" void mclBnG1_add(mclBnG1 *z, const mclBnG1 *x, const mclBnG1 *y) { g1_op(OP_G1_ADD, z, x, y, nullptr); }
+extern "C" void mclBnG1_sub(mclBnG1 *z, const mclBnG1 *x, const mclBnG1 *y) {
+    mclBnG1 ny;
+    mclBnG1_neg(&ny, y);
+    mclBnG1_add(z, x, &ny);
+}
+extern "C" void mclBnG1_mul(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y) { g1_op(OP_G1_MUL, z, x, nullptr, y); }
+extern "C" void mclBnG1_mulVec(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y, mclSize n) {
+    mclBnG1 acc, t;
+    mclBnG1_clear(&acc);
+    for (mclSize i = 0; i < n; i++) {
+        mclBnG1_mul(&t, &x[i], &y[i]);
+        mclBnG1_add(&acc, &acc, &t);
+    }
+    *z = acc;
+}
+extern "C" void lcb_g1_generator(mclBnG1 *g) {
+    LOCKED_OR()
+    if (run_op(OP_G1_GEN, 0, 36)) memcpy(g, g_io_host, 144);
+}
+
+// ================================================================== G2
+extern "C" mclSize mclBnG2_serialize(void *buf, mclSize max, const mclBnG2 *x) {
+    if (max < 96) return 0;
+    LOCKED_OR(0)
+    memcpy(g_io_host + 72, x, 288);
+    if (!run_op(OP_G2_SER, 144, 248)) return 0;
+    memcpy(buf, g_io_host + 224, 96);
+    return 96;
+}
+extern "C" mclSize mclBnG2_deserialize(mclBnG2 *x, const void *buf, mclSize n) {
+    if (n < 96) return 0;
+    LOCKED_OR(0)
+    memcpy(g_io_host + 224, buf, 96);
+    if (!run_op(OP_G2_DESER, 248, 249) || !g_io_host[248]) return 0;
+    memcpy(x, g_io_host, 288);
+    return 96;
+}
+static int g2_flag_op(int op, const mclBnG2 *x, const mclBnG2 *y) {
+    LOCKED_OR(0)
+    memcpy(g_io_host + 72, x, 288);
+    if (y) memcpy(g_io_host + 144, y, 288);
+    if (!run_op(op, 216, 249)) return 0;
+    return (int)g_io_host[248];
+}
+extern "C" int mclBnG2_isValid(const mclBnG2 *x) { return g2_flag_op(OP_G2_VALID, x, nullptr); }
+extern "C" int mclBnG2_isEqual(const mclBnG2 *x, const mclBnG2 *y) { return g2_flag_op(OP_G2_EQ, x, y); }
+extern "C" int mclBnG2_isZero(const mclBnG2 *x) {
+    static const u32 z[24] = {0};
+    return memcmp(&x->z, z, 96) == 0;
+}
+extern "C" void mclBnG2_clear(mclBnG2 *x) { memset(x, 0, sizeof *x); }
+extern "C" int mclBnG2_hashAndMapTo(mclBnG2 *x, const void *buf, mclSize n) {
+    if (n > (IO_WORDS - 256) * 4) { set_err("message too long"); return -1; }
+    LOCKED_OR(-1)
+    g_io_host[250] = (u32)n;
+    memcpy(g_io_host + 256, buf, n);
+    if (!run_op(OP_G2_HASH, 256 + (n + 3) / 4, 249) || !g_io_host[248]) return -1;
+    memcpy(x, g_io_host, 288);
+    return 0;
+}
+static void g2_op(int op, mclBnG2 *z, const mclBnG2 *x, const mclBnG2 *y, const mclBnFr *k) {
+    LOCKED_OR()
+    memcpy(g_io_host + 72, x, 288);
+    if (y) memcpy(g_io_host + 144, y, 288);
+    if (k) memcpy(g_io_host + 216, k, 32);
+    if (run_op(op, 224, 72)) memcpy(z, g_io_host, 288);
+}
+extern "C" void mclBnG2_neg(mclBnG2 *y, const mclBnG2 *x) { g2_op(OP_G2_NEG, y, x, nullptr, nullptr); }
+extern "C" void mclBnG2_dbl(mclBnG2 *y, const mclBnG2 *x) { g2_op(OP_G2_DBL, y, x, nullptr, nullptr); }
+extern "C" void mclBnG2_normalize(mclBnG2 *y, const mclBnG2 *x) { g2_op(OP_G2_NORM, y, x, nullptr, nullptr); }
+extern "C" void mclBnG2_add(mclBnG2 *z, const mclBnG2 *x, const mclBnG2 *y) { g2_op(OP_G2_ADD, z, x, y, nullptr); }
+extern "C" void mclBnG2_sub(mclBnG2 *z, const mclBnG2 *x, const mclBnG2 *y) {
+    mclBnG2 ny;
+    mclBnG2_neg(&ny, y);
+    mclBnG2_add(z, x, &ny);
+}
+extern "C" void mclBnG2_mul(mclBnG2 *z, const mclBnG2 *x, const mclBnFr *y) { g2_op(OP_G2_MUL, z, x, nullptr, y); }
+extern "C" void lcb_g2_generator(mclBnG2 *g) {
+    LOCKED_OR()
+    if (run_op(OP_G2_GEN, 0, 72)) memcpy(g, g_io_host, 288);
+}
+
+// ================================================================== GT / pairing
+static void pair_op(int op, mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) {
+    LOCKED_OR()
+    memcpy(g_io_host + 144, x, 144);
+    memcpy(g_io_host + 180, y, 288);
+    if (run_op(op, 252, 144)) memcpy(z, g_io_host, 576);
+}
+extern "C" void mclBn_pairing(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) { pair_op(OP_PAIRING, z, x, y); }
+extern "C" void mclBn_millerLoop(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) { pair_op(OP_MILLER, z, x, y); }
+static void gt_op(int op, mclBnGT *z, const mclBnGT *a, const mclBnGT *b, const mclBnFr *k) {
+    LOCKED_OR()
+    memcpy(g_io_host + 252, a, 576);
+    if (b) memcpy(g_io_host + 396, b, 576);
+    if (k) memcpy(g_io_host + 540, k, 32);
+    if (run_op(op, 548, 144)) memcpy(z, g_io_host, 576);
+}
+extern "C" void mclBn_millerLoopVec(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y, mclSize n) {
+    mclBnGT acc, t;
+    memset(&acc, 0, sizeof acc);
+    for (mclSize i = 0; i < n; i++) {
+        mclBn_millerLoop(&t, &x[i], &y[i]);
+        if (i == 0) acc = t;
+        else gt_op(OP_GT_MUL, &acc, &acc, &t, nullptr);
+    }
+    *z = acc;
+}
+extern "C" void mclBn_finalExp(mclBnGT *y, const mclBnGT *x) { gt_op(OP_FINAL_EXP, y, x, nullptr, nullptr); }
+extern "C" void mclBnGT_mul(mclBnGT *z, const mclBnGT *x, const mclBnGT *y) { gt_op(OP_GT_MUL, z, x, y, nullptr); }
+extern "C" void mclBnGT_pow(mclBnGT *z, const mclBnGT *x, const mclBnFr *y) { gt_op(OP_GT_POW, z, x, nullptr, y); }
+extern "C" int mclBnGT_isEqual(const mclBnGT *x, const mclBnGT *y) { return memcmp(x, y, 576) == 0; }
+extern "C" int mclBnGT_isOne(const mclBnGT *x) {
+    // Montgomery one of Fp in the first coordinate, zero elsewhere
+    const u32 *w = (const u32 *)x;
+    if (memcmp(w, LCB_ONE_HOST, 48) != 0) return 0;
+    for (int i = 12; i < 144; i++) if (w[i]) return 0;
+    return 1;
+}
+extern "C" int mclBnGT_isZero(const mclBnGT *x) {
+    const u32 *w = (const u32 *)x;
+    for (int i = 0; i < 144; i++) if (w[i]) return 0;
+    return 1;
+}
+extern "C" void mclBnGT_clear(mclBnGT *x) { memset(x, 0, sizeof *x); }
+extern "C" mclSize mclBnGT_serialize(void *buf, mclSize max, const mclBnGT *x) {
+    if (max < 576) return 0;
+    LOCKED_OR(0)
+    memcpy(g_io_host + 252, x, 576);
+    if (!run_op(OP_GT_SER, 396, 144)) return 0;
+    memcpy(buf, g_io_host, 576);
+    return 576;
+}
+extern "C" mclSize mclBnGT_deserialize(mclBnGT *x, const void *buf, mclSize n) {
+    if (n < 576) return 0;
+    LOCKED_OR(0)
+    memcpy(g_io_host + 252, buf, 576);
+    if (!run_op(OP_GT_DESER, 396, 549) || !g_io_host[548]) return 0;
+    memcpy(x, g_io_host, 576);
+    return 576;
+}
+
+// ================================================================== Lagrange / polynomials (single)
+extern "C" int lcb_g1_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
+                                     const uint32_t *off, size_t n_problems);
+extern "C" int lcb_g2_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
+                                     const uint32_t *off, size_t n_problems);
+
+extern "C" int mclBn_FrLagrangeInterpolation(mclBnFr *out, const mclBnFr *xVec, const mclBnFr *yVec, mclSize k) {
+    if (k == 0) return -1;
+    // lambda_i via the G1 path's coefficient kernel would need raw x; do it with Fr single ops
+    for (mclSize i = 0; i < k; i++) {
+        if (mclBnFr_isZero(&xVec[i])) return -1;
+        for (mclSize j = 0; j < i; j++)
+            if (mclBnFr_isEqual(&xVec[i], &xVec[j])) return -1;
+    }
+    mclBnFr a, acc, t, d;
+    memcpy(&a, &xVec[0], 32);
+    for (mclSize i = 1; i < k; i++) mclBnFr_mul(&a, &a, &xVec[i]);
+    mclBnFr_clear(&acc);
+    for (mclSize i = 0; i < k; i++) {
+        mclBnFr b = xVec[i];
+        for (mclSize j = 0; j < k; j++) {
+            if (j == i) continue;
+            mclBnFr_sub(&d, &xVec[j], &xVec[i]);
+            mclBnFr_mul(&b, &b, &d);
+        }
+        mclBnFr_div(&t, &a, &b);
+        mclBnFr_mul(&t, &t, &yVec[i]);
+        mclBnFr_add(&acc, &acc, &t);
+    }
+    *out = acc;
+    return 0;
+}
+static int lagrange_points(int g, void *out, const mclBnFr *xVec, const void *yVec, mclSize k) {
+    if (k == 0) return -1;
+    size_t pb = g == 1 ? 48 : 96;
+    std::vector<uint8_t> xs(32 * k), ys(pb * k), o(pb);
+    for (mclSize i = 0; i < k; i++) {
+        if (mclBnFr_serialize(&xs[32 * i], 32, &xVec[i]) != 32) return -1;
+        if (g == 1) { if (mclBnG1_serialize(&ys[pb * i], pb, (const mclBnG1 *)yVec + i) != pb) return -1; }
+        else { if (mclBnG2_serialize(&ys[pb * i], pb, (const mclBnG2 *)yVec + i) != pb) return -1; }
+    }
+    uint32_t off[2] = {0, (uint32_t)k};
+    uint8_t st = 0;
+    int rc = g == 1 ? lcb_g1_lagrange_batch(o.data(), &st, xs.data(), ys.data(), off, 1)
+                    : lcb_g2_lagrange_batch(o.data(), &st, xs.data(), ys.data(), off, 1);
+    if (rc || !st) return -1;
+    if (g == 1) return mclBnG1_deserialize((mclBnG1 *)out, o.data(), pb) == pb ? 0 : -1;
+    return mclBnG2_deserialize((mclBnG2 *)out, o.data(), pb) == pb ? 0 : -1;
+}
+extern "C" int mclBn_G1LagrangeInterpolation(mclBnG1 *out, const mclBnFr *xVec, const mclBnG1 *yVec, mclSize k) {
+    if (k == 1) { *out = yVec[0]; return mclBnFr_isZero(&xVec[0]) ? -1 : 0; }
+    return lagrange_points(1, out, xVec, yVec, k);
+}
+extern "C" int mclBn_G2LagrangeInterpolation(mclBnG2 *out, const mclBnFr *xVec, const mclBnG2 *yVec, mclSize k) {
+    if (k == 1) { *out = yVec[0]; return mclBnFr_isZero(&xVec[0]) ? -1 : 0; }
+    return lagrange_points(2, out, xVec, yVec, k);
+}
+extern "C" int mclBn_FrEvaluatePolynomial(mclBnFr *out, const mclBnFr *c, mclSize n, const mclBnFr *x) {
+    if (n == 0) return -1;
+    mclBnFr acc = c[n - 1];
+    for (mclSize i = n - 1; i-- > 0;) {
+        mclBnFr_mul(&acc, &acc, x);
+        mclBnFr_add(&acc, &acc, &c[i]);
+    }
+    *out = acc;
+    return 0;
+}
+extern "C" int mclBn_G1EvaluatePolynomial(mclBnG1 *out, const mclBnG1 *c, mclSize n, const mclBnFr *x) {
+    if (n == 0) return -1;
+    mclBnG1 acc = c[n - 1];
+    for (mclSize i = n - 1; i-- > 0;) {
+        mclBnG1_mul(&acc, &acc, x);
+        mclBnG1_add(&acc, &acc, &c[i]);
+    }
+    *out = acc;
+    return 0;
+}
+extern "C" int mclBn_G2EvaluatePolynomial(mclBnG2 *out, const mclBnG2 *c, mclSize n, const mclBnFr *x) {
+    if (n == 0) return -1;
+    mclBnG2 acc = c[n - 1];
+    for (mclSize i = n - 1; i-- > 0;) {
+        mclBnG2_mul(&acc, &acc, x);
+        mclBnG2_add(&acc, &acc, &c[i]);
+    }
+    *out = acc;
+    return 0;
+}
+
+// ================================================================== batch: TPKE
+static int tpke_verify_enqueue(uint8_t *d_accept, size_t n, const uint8_t *d_y, size_t n_keys, const uint8_t *d_u,
+                               const uint8_t *d_w, const uint8_t *d_v, const uint32_t *d_voff, size_t n_cts,
+                               const uint32_t *d_ct, const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
+    u32 *lines = (u32 *)b_lines.get((size_t)n_cts * 2 * LCB_LINESET_BYTES);
+    uint8_t *ctok = (uint8_t *)b_ctok.get(n_cts);
+    void *keys = b_keys.get(n_keys * LCB_G1A_ST_BYTES);
+    if (!lines || !ctok || !keys) { set_err("device allocation failed"); return -1; }
+    if (n_keys) lcbk_g1_decompress(dim3(nblk(n_keys)), s, d_y, (u32)n_keys, keys);
+    if (n_cts)
+        lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), s, d_u, d_w, d_v, d_voff,
+                           (u32)n_cts, lines, ctok, g_orig_cofactor);
+    if (n)
+        lcbk_tpke_verify(dim3(nblk(n)), s, lines, ctok, keys, (u32)n_keys,
+                           d_ct, d_dec, d_ui, (u32)n, d_accept);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { set_err("tpke verify launch", e); return -1; }
+    return 0;
+}
+extern "C" int lcb_tpke_verify_shares_dev(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys,
+                                          const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
+                                          const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
+                                          const uint32_t *dec_idx, const uint8_t *ui, void *stream) {
+    LOCKED_OR(-1)
+    return tpke_verify_enqueue(accept, n, y_keys, n_keys, cts_u, cts_w, v_data, v_off, n_cts, ct_idx, dec_idx, ui,
+                               (hipStream_t)stream);
+}
+extern "C" int lcb_tpke_verify_shares(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys,
+                                      const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
+                                      const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
+                                      const uint32_t *dec_idx, const uint8_t *ui) {
+    LOCKED_OR(-1)
+    for (size_t i = 0; i < n; i++)
+        if (ct_idx[i] >= n_cts) { set_err("ct_idx out of range"); return -1; }
+    size_t vbytes = n_cts ? v_off[n_cts] : 0;
+    hipStream_t s = g_stream;
+    const uint8_t *dy = up(b_in[0], y_keys, 48 * n_keys, s);
+    const uint8_t *du = up(b_in[1], cts_u, 48 * n_cts, s);
+    const uint8_t *dw = up(b_in[2], cts_w, 96 * n_cts, s);
+    const uint8_t *dv = up(b_in[3], v_data, vbytes, s);
+    const uint32_t *dvo = up(b_in[4], v_off, n_cts + 1, s);
+    const uint32_t *dct = up(b_in[5], ct_idx, n, s);
+    const uint32_t *ddec = up(b_in[6], dec_idx, n, s);
+    const uint8_t *dui = up(b_in[7], ui, 48 * n, s);
+    uint8_t *dacc = (uint8_t *)b_out[0].get(n);
+    if (!dy || !du || !dw || !dv || !dvo || !dct || !ddec || !dui || !dacc) { set_err("device allocation failed"); return -1; }
+    if (tpke_verify_enqueue(dacc, n, dy, n_keys, du, dw, dv, dvo, n_cts, dct, ddec, dui, s)) return -1;
+    if (n) hipMemcpyAsync(accept, dacc, n, hipMemcpyDeviceToHost, s);
+    return sync_check("tpke verify") ? 0 : -1;
+}
+
+extern "C" int lcb_tpke_partial_decrypt(uint8_t *ui_out, uint8_t *status, const uint8_t x[32], const uint8_t *cts_u,
+                                        const uint8_t *cts_w, const uint8_t *v_data, const uint32_t *v_off,
+                                        size_t n_cts) {
+    LOCKED_OR(-1)
+    hipStream_t s = g_stream;
+    size_t vbytes = n_cts ? v_off[n_cts] : 0;
+    const uint8_t *du = up(b_in[1], cts_u, 48 * n_cts, s);
+    const uint8_t *dw = up(b_in[2], cts_w, 96 * n_cts, s);
+    const uint8_t *dv = up(b_in[3], v_data, vbytes, s);
+    const uint32_t *dvo = up(b_in[4], v_off, n_cts + 1, s);
+    const uint8_t *dx = up(b_in[0], x, 32, s);
+    u32 *lines = (u32 *)b_lines.get((size_t)n_cts * 2 * LCB_LINESET_BYTES);
+    uint8_t *ctok = (uint8_t *)b_ctok.get(n_cts);
+    uint8_t *dui = (uint8_t *)b_out[0].get(48 * n_cts);
+    uint8_t *dst = (uint8_t *)b_out[1].get(n_cts);
+    if (!du || !dw || !dv || !dvo || !dx || !lines || !ctok || !dui || !dst) { set_err("device allocation failed"); return -1; }
+    if (!n_cts) return 0;
+    lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), s, du, dw, dv, dvo, (u32)n_cts, lines,
+                       ctok, g_orig_cofactor);
+    lcbk_tpke_partial_decrypt(dim3(nblk(n_cts)), s, lines, ctok, du,
+                       dx, (u32)n_cts, dui, dst);
+    hipMemcpyAsync(ui_out, dui, 48 * n_cts, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(status, dst, n_cts, hipMemcpyDeviceToHost, s);
+    return sync_check("tpke partial decrypt") ? 0 : -1;
+}
+
+extern "C" int lcb_tpke_encrypt_phase1(uint8_t *u_out, uint8_t *t_out, const uint8_t y[48], const uint8_t *r, size_t n) {
+    LOCKED_OR(-1)
+    if (!n) return 0;
+    hipStream_t s = g_stream;
+    const uint8_t *dy = up(b_in[0], y, 48, s);
+    const uint8_t *dr = up(b_in[1], r, 32 * n, s);
+    uint8_t *du = (uint8_t *)b_out[0].get(48 * n), *dt = (uint8_t *)b_out[1].get(48 * n), *dok = (uint8_t *)b_out[2].get(n);
+    if (!dy || !dr || !du || !dt || !dok) { set_err("device allocation failed"); return -1; }
+    lcbk_tpke_encrypt1(dim3(nblk(n)), s, dy, dr, (u32)n, du, dt, dok);
+    std::vector<uint8_t> ok(n);
+    hipMemcpyAsync(u_out, du, 48 * n, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(t_out, dt, 48 * n, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, s);
+    if (!sync_check("tpke encrypt1")) return -1;
+    for (size_t i = 0; i < n; i++) if (!ok[i]) { set_err("invalid public key or scalar"); return -1; }
+    return 0;
+}
+extern "C" int lcb_tpke_encrypt_phase2(uint8_t *w_out, const uint8_t *u, const uint8_t *r, const uint8_t *v_data,
+                                       const uint32_t *v_off, size_t n) {
+    LOCKED_OR(-1)
+    if (!n) return 0;
+    hipStream_t s = g_stream;
+    const uint8_t *du = up(b_in[0], u, 48 * n, s);
+    const uint8_t *dr = up(b_in[1], r, 32 * n, s);
+    const uint8_t *dv = up(b_in[2], v_data, v_off[n], s);
+    const uint32_t *dvo = up(b_in[3], v_off, n + 1, s);
+    uint8_t *dw = (uint8_t *)b_out[0].get(96 * n), *dok = (uint8_t *)b_out[1].get(n);
+    if (!du || !dr || !dv || !dvo || !dw || !dok) { set_err("device allocation failed"); return -1; }
+    lcbk_tpke_encrypt2(dim3(nblk(n)), s, du, dr, dv, dvo, (u32)n, dw, dok,
+                       g_orig_cofactor);
+    std::vector<uint8_t> ok(n);
+    hipMemcpyAsync(w_out, dw, 96 * n, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, s);
+    if (!sync_check("tpke encrypt2")) return -1;
+    for (size_t i = 0; i < n; i++) if (!ok[i]) { set_err("hash-to-G2 failed"); return -1; }
+    return 0;
+}
+
+// ================================================================== batch: threshold signatures
+static int ts_verify_enqueue(uint8_t *d_accept, size_t n, const uint8_t *d_pks, size_t n_pks, const uint8_t *d_sigs,
+                             const uint8_t *d_msg, const uint32_t *d_moff, size_t n_msgs, const uint32_t *d_midx,
+                             const uint32_t *d_pidx, hipStream_t s) {
+    u32 *lines = (u32 *)b_lines.get((size_t)n_msgs * LCB_LINESET_BYTES);
+    uint8_t *mok = (uint8_t *)b_ctok.get(n_msgs);
+    void *keys = b_keys.get(n_pks * LCB_G1A_ST_BYTES);
+    if (!lines || !mok || !keys) { set_err("device allocation failed"); return -1; }
+    if (n_pks) lcbk_g1_decompress(dim3(nblk(n_pks)), s, d_pks, (u32)n_pks, keys);
+    if (n_msgs)
+        lcbk_ts_msg_prepare(dim3(nblk(n_msgs)), s, d_msg, d_moff, (u32)n_msgs,
+                           lines, mok, g_orig_cofactor);
+    if (n)
+        lcbk_ts_verify(dim3(nblk(n)), s, lines, mok, keys, (u32)n_pks, d_sigs,
+                           d_midx, d_pidx, (u32)n, d_accept);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { set_err("ts verify launch", e); return -1; }
+    return 0;
+}
+extern "C" int lcb_ts_verify_shares_dev(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks, const uint8_t *sigs,
+                                        const uint8_t *msg_data, const uint32_t *msg_off, size_t n_msgs,
+                                        const uint32_t *msg_idx, const uint32_t *pk_idx, void *stream) {
+    LOCKED_OR(-1)
+    return ts_verify_enqueue(accept, n, pks, n_pks, sigs, msg_data, msg_off, n_msgs, msg_idx, pk_idx, (hipStream_t)stream);
+}
+extern "C" int lcb_ts_verify_shares(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks, const uint8_t *sigs,
+                                    const uint8_t *msg_data, const uint32_t *msg_off, size_t n_msgs,
+                                    const uint32_t *msg_idx, const uint32_t *pk_idx) {
+    LOCKED_OR(-1)
+    for (size_t i = 0; i < n; i++)
+        if (msg_idx[i] >= n_msgs) { set_err("msg_idx out of range"); return -1; }
+    hipStream_t s = g_stream;
+    size_t mbytes = n_msgs ? msg_off[n_msgs] : 0;
+    const uint8_t *dpk = up(b_in[0], pks, 48 * n_pks, s);
+    const uint8_t *dsig = up(b_in[1], sigs, 96 * n, s);
+    const uint8_t *dm = up(b_in[2], msg_data, mbytes, s);
+    const uint32_t *dmo = up(b_in[3], msg_off, n_msgs + 1, s);
+    const uint32_t *dmi = up(b_in[4], msg_idx, n, s);
+    const uint32_t *dpi = up(b_in[5], pk_idx, n, s);
+    uint8_t *dacc = (uint8_t *)b_out[0].get(n);
+    if (!dpk || !dsig || !dm || !dmo || !dmi || !dpi || !dacc) { set_err("device allocation failed"); return -1; }
+    if (ts_verify_enqueue(dacc, n, dpk, n_pks, dsig, dm, dmo, n_msgs, dmi, dpi, s)) return -1;
+    if (n) hipMemcpyAsync(accept, dacc, n, hipMemcpyDeviceToHost, s);
+    return sync_check("ts verify") ? 0 : -1;
+}
+extern "C" int lcb_ts_sign(uint8_t *sigs_out, const uint8_t *sks, const uint8_t *msg_data, const uint32_t *msg_off,
+                           const uint32_t *msg_idx, size_t n) {
+    LOCKED_OR(-1)
+    if (!n) return 0;
+    u32 nm = 0;
+    for (size_t i = 0; i < n; i++) nm = msg_idx[i] + 1 > nm ? msg_idx[i] + 1 : nm;
+    hipStream_t s = g_stream;
+    const uint8_t *dsk = up(b_in[0], sks, 32 * n, s);
+    const uint8_t *dm = up(b_in[1], msg_data, msg_off[nm], s);
+    const uint32_t *dmo = up(b_in[2], msg_off, nm + 1, s);
+    const uint32_t *dmi = up(b_in[3], msg_idx, n, s);
+    uint8_t *dsig = (uint8_t *)b_out[0].get(96 * n), *dok = (uint8_t *)b_out[1].get(n);
+    if (!dsk || !dm || !dmo || !dmi || !dsig || !dok) { set_err("device allocation failed"); return -1; }
+    lcbk_ts_sign(dim3(nblk(n)), s, dsk, dm, dmo, dmi, (u32)n, dsig, dok,
+                       g_orig_cofactor);
+    std::vector<uint8_t> ok(n);
+    hipMemcpyAsync(sigs_out, dsig, 96 * n, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, s);
+    if (!sync_check("ts sign")) return -1;
+    for (size_t i = 0; i < n; i++) if (!ok[i]) { set_err("invalid key share"); return -1; }
+    return 0;
+}
+
+// ================================================================== batch: Lagrange, scalar mul, hash, MSM
+static int lagrange_batch(int g, uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys, const uint32_t *off,
+                          size_t np) {
+    LOCKED_OR(-1)
+    if (!np) return 0;
+    size_t ne = off[np];
+    size_t pb = g == 1 ? 48 : 96;
+    hipStream_t s = g_stream;
+    const uint8_t *dx = up(b_in[0], xs, 32 * ne, s);
+    const uint8_t *dy = up(b_in[1], ys, pb * ne, s);
+    const uint32_t *doff = up(b_in[2], off, np + 1, s);
+    void *lam = b_in[3].get(LCB_FR_BYTES * (ne ? ne : 1));
+    void *parts = b_in[4].get((g == 1 ? LCB_G1_JAC_BYTES : LCB_G2_JAC_BYTES) * (ne ? ne : 1));
+    uint8_t *pok = (uint8_t *)b_in[5].get(ne ? ne : 1);
+    uint8_t *dst = (uint8_t *)b_out[0].get(np), *dout = (uint8_t *)b_out[1].get(pb * np);
+    if (!dx || !dy || !doff || !lam || !parts || !pok || !dst || !dout) { set_err("device allocation failed"); return -1; }
+    lcbk_lagrange_coeffs(dim3(nblk(np)), s, dx, doff, (u32)np, lam, dst);
+    if (ne) {
+        if (g == 1) lcbk_g1_mul_lanes(dim3(nblk(ne)), s, dy, lam, (u32)ne, parts, pok);
+        else lcbk_g2_mul_lanes(dim3(nblk(ne)), s, dy, lam, (u32)ne, parts, pok);
+    }
+    if (g == 1) lcbk_g1_sum(dim3(nblk(np)), s, parts, pok, doff, (u32)np, dst, dout);
+    else lcbk_g2_sum(dim3(nblk(np)), s, parts, pok, doff, (u32)np, dst, dout);
+    hipMemcpyAsync(out, dout, pb * np, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(status, dst, np, hipMemcpyDeviceToHost, s);
+    return sync_check("lagrange") ? 0 : -1;
+}
+extern "C" int lcb_g1_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
+                                     const uint32_t *off, size_t n) { return lagrange_batch(1, out, status, xs, ys, off, n); }
+extern "C" int lcb_g2_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
+                                     const uint32_t *off, size_t n) { return lagrange_batch(2, out, status, xs, ys, off, n); }
+
+static int mul_batch(int g, uint8_t *out, const uint8_t *points, int use_gen, const uint8_t *scalars, size_t n) {
+    LOCKED_OR(-1)
+    if (!n) return 0;
+    size_t pb = g == 1 ? 48 : 96;
+    hipStream_t s = g_stream;
+    const uint8_t *dp = use_gen ? (const uint8_t *)b_in[0].get(16) : up(b_in[0], points, pb * n, s);
+    const uint8_t *dsc = up(b_in[1], scalars, 32 * n, s);
+    uint8_t *dout = (uint8_t *)b_out[0].get(pb * n), *dok = (uint8_t *)b_out[1].get(n);
+    if (!dp || !dsc || !dout || !dok) { set_err("device allocation failed"); return -1; }
+    if (g == 1) lcbk_g1_mul(dim3(nblk(n)), s, dp, use_gen, dsc, (u32)n, dout, dok);
+    else lcbk_g2_mul(dim3(nblk(n)), s, dp, use_gen, dsc, (u32)n, dout, dok);
+    std::vector<uint8_t> ok(n);
+    hipMemcpyAsync(out, dout, pb * n, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, s);
+    if (!sync_check("mul batch")) return -1;
+    for (size_t i = 0; i < n; i++) if (!ok[i]) { set_err("invalid point or scalar"); return -1; }
+    return 0;
+}
+extern "C" int lcb_g1_mul_batch(uint8_t *out, const uint8_t *points, int gen, const uint8_t *scalars, size_t n) {
+    return mul_batch(1, out, points, gen, scalars, n);
+}
+extern "C" int lcb_g2_mul_batch(uint8_t *out, const uint8_t *points, int gen, const uint8_t *scalars, size_t n) {
+    return mul_batch(2, out, points, gen, scalars, n);
+}
+extern "C" int lcb_g2_hash_batch(uint8_t *out, const uint8_t *msg_data, const uint32_t *msg_off, size_t n) {
+    LOCKED_OR(-1)
+    if (!n) return 0;
+    hipStream_t s = g_stream;
+    const uint8_t *dm = up(b_in[0], msg_data, msg_off[n], s);
+    const uint32_t *dmo = up(b_in[1], msg_off, n + 1, s);
+    uint8_t *dout = (uint8_t *)b_out[0].get(96 * n), *dok = (uint8_t *)b_out[1].get(n);
+    if (!dm || !dmo || !dout || !dok) { set_err("device allocation failed"); return -1; }
+    lcbk_g2_hash(dim3(nblk(n)), s, dm, dmo, (u32)n, dout, dok, g_orig_cofactor);
+    std::vector<uint8_t> ok(n);
+    hipMemcpyAsync(out, dout, 96 * n, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, s);
+    if (!sync_check("hash batch")) return -1;
+    for (size_t i = 0; i < n; i++) if (!ok[i]) { set_err("hash-to-G2 failed"); return -1; }
+    return 0;
+}
+extern "C" int lcb_g1_msm(uint8_t out[48], const uint8_t *points, const uint8_t *scalars, size_t n) {
+    LOCKED_OR(-1)
+    hipStream_t s = g_stream;
+    if (n == 0) { memset(out, 0, 48); return 0; }
+    const uint8_t *dp = up(b_in[0], points, 48 * n, s);
+    const uint8_t *dsc = up(b_in[1], scalars, 32 * n, s);
+    void *parts = b_in[2].get(LCB_G1_JAC_BYTES * n);
+    uint8_t *dok = (uint8_t *)b_out[0].get(n), *dout = (uint8_t *)b_out[1].get(48);
+    if (!dp || !dsc || !parts || !dok || !dout) { set_err("device allocation failed"); return -1; }
+    lcbk_g1_msm_products(dim3(nblk(n)), s, dp, dsc, (u32)n, parts, dok);
+    for (size_t m = n; m > 1;) {
+        size_t h = (m + 1) / 2;
+        lcbk_g1_reduce_pairs(dim3(nblk(h)), s, parts, (u32)h, (u32)m);
+        m = h;
+    }
+    lcbk_g1_finish(dim3(1), s, parts, dout);
+    std::vector<uint8_t> ok(n);
+    hipMemcpyAsync(out, dout, 48, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, s);
+    if (!sync_check("msm")) return -1;
+    for (size_t i = 0; i < n; i++) if (!ok[i]) { set_err("invalid point or scalar"); return -1; }
+    return 0;
+}
+
+// ================================================================== KDF (host byte work)
+extern "C" void lcb_xor_with_hash(uint8_t *out, const uint8_t g1b[48], const uint8_t *data, size_t len) {
+    lcb_host::xor_with_hash(out, g1b, data, len);
+}

@@ -1,0 +1,235 @@
+// lachain_amd/csrc/pairing.hpp — optimal-ate pairing on BLS12-381 for batched share verification.
+//
+// Miller loop over |z| = 0xd201000000010000 (63 doubling steps, 5 addition steps = 68 lines), z < 0
+// handled by a final conjugation.  Lines are computed in homogeneous projective coordinates on the
+// twist and written in the sparse shape  l = A + (Bc * xP) v + (Cc * yP) v w, so that everything that
+// depends only on the G2 point (A, Bc, Cc) can be PRECOMPUTED ONCE per G2 point and shared by all
+// G1 points paired with it (every decryption share of a ciphertext pairs with the same H and W:
+// /root/reference/src/Lachain.Crypto/TPKE/PublicKey.cs:88-92).  Line scalings by Fp2 constants are
+// killed by the final exponentiation, so the result equals the reference's e(P, Q) exactly.
+//   doubling : A = Y^2 - 3b'Z^2, Bc = -3X^2, Cc = 2YZ;  T <- 2T
+//   addition : theta = Y - yQ Z, lambda = X - xQ Z, A = theta xQ - lambda yQ, Bc = -theta, Cc = lambda
+// Final exponentiation: easy part f^((p^6-1)(p^2+1)), hard part via the decomposition
+// 3(p^4-p^2+1)/r = c0 + c1 p + c2 p^2 + c3 p^3 (mcl expHardPartBLS12 shape), cyclotomic squarings.
+// GT values therefore equal e(P, Q)^3 of the textbook reduced pairing — the normalisation mcl uses;
+// accept/reject decisions are unaffected by it (x -> x^3 is a bijection on mu_r).
+#pragma once
+#include "curve.hpp"
+
+#define LCB_NLINES 68
+#define LCB_LINE_WORDS (6 * 12)                      // A, Bc, Cc : three Fp2
+#define LCB_LINESET_WORDS (LCB_NLINES * LCB_LINE_WORDS) // 4896 u32 = 19584 B per G2 point
+
+struct line { fp2 A, Bc, Cc; };
+
+DI void line_dbl_step(g2 &T, line &l) {
+    fp2 XX, YY, ZZ, bZZ, t, YZ, b3;
+    fp2_load_const(b3, LCB_B2_3);
+    fp2_sqr(XX, T.x);
+    fp2_sqr(YY, T.y);
+    fp2_sqr(ZZ, T.z);
+    fp2_mul(bZZ, ZZ, b3);       // 3b'Z^2
+    fp2_mul(YZ, T.y, T.z);
+    fp2_sub(l.A, YY, bZZ);
+    fp2_add(t, XX, XX);
+    fp2_add(t, t, XX);
+    fp2_neg(l.Bc, t);
+    fp2_add(l.Cc, YZ, YZ);
+    // X3 = XY/2 (Y^2 - 9b'Z^2), Y3 = ((Y^2 + 9b'Z^2)/2)^2 - 27 b'^2 Z^4, Z3 = 2 Y^3 Z
+    fp2 b9, X3, Y3, Z3, s;
+    fp inv2;
+    fp_load_const(inv2, LCB_INV2);
+    fp2_add(b9, bZZ, bZZ);
+    fp2_add(b9, b9, bZZ);
+    fp2_mul(X3, T.x, T.y);
+    fp2_mul_fp(X3, X3, inv2);
+    fp2_sub(s, YY, b9);
+    fp2_mul(X3, X3, s);
+    fp2_add(s, YY, b9);
+    fp2_mul_fp(s, s, inv2);
+    fp2_sqr(Y3, s);
+    fp2_sqr(t, bZZ);
+    fp2_add(s, t, t);
+    fp2_add(s, s, t);
+    fp2_sub(Y3, Y3, s);
+    fp2_mul(Z3, YY, YZ);
+    fp2_add(Z3, Z3, Z3);
+    T.x = X3; T.y = Y3; T.z = Z3;
+}
+DI void line_add_step(g2 &T, const fp2 &xQ, const fp2 &yQ, line &l) {
+    fp2 th, la, t, s;
+    fp2_mul(t, yQ, T.z);
+    fp2_sub(th, T.y, t);
+    fp2_mul(t, xQ, T.z);
+    fp2_sub(la, T.x, t);
+    fp2_mul(l.A, th, xQ);
+    fp2_mul(t, la, yQ);
+    fp2_sub(l.A, l.A, t);
+    fp2_neg(l.Bc, th);
+    l.Cc = la;
+    fp2 C, D, E, F, G, H;
+    fp2_sqr(C, th);
+    fp2_sqr(D, la);
+    fp2_mul(E, la, D);
+    fp2_mul(F, T.z, C);
+    fp2_mul(G, T.x, D);
+    fp2_add(H, E, F);
+    fp2_sub(H, H, G);
+    fp2_sub(H, H, G);
+    fp2_mul(T.x, la, H);
+    fp2_sub(t, G, H);
+    fp2_mul(s, th, t);
+    fp2_mul(t, T.y, E);
+    fp2_sub(T.y, s, t);
+    fp2_mul(T.z, T.z, E);
+}
+// "one" line (for a point at infinity on either side): A = 1, Bc = Cc = 0
+DI void line_one(line &l) { l.A = fp2_one(); l.Bc = fp2_zero(); l.Cc = fp2_zero(); }
+
+DI void line_store(u32 *dst, const line &l) {
+    const u32 *s = (const u32 *)&l;
+#pragma unroll
+    for (int q = 0; q < LCB_LINE_WORDS / 4; q++)
+        ((uint4 *)dst)[q] = make_uint4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
+}
+DI void line_load(line &l, const u32 *src) {
+    u32 *d = (u32 *)&l;
+#pragma unroll
+    for (int q = 0; q < LCB_LINE_WORDS / 4; q++) {
+        uint4 v = ((const uint4 *)src)[q];
+        d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+    }
+}
+
+// all 68 lines of a G2 point (affine, possibly infinity) into dst[LCB_LINESET_WORDS]
+DN void lineset_compute(u32 *dst, const g2a &Q) {
+    line l;
+    if (Q.inf) {
+        line_one(l);
+        for (int k = 0; k < LCB_NLINES; k++) line_store(dst + k * LCB_LINE_WORDS, l);
+        return;
+    }
+    g2 T;
+    T.x = Q.x; T.y = Q.y; T.z = fp2_one();
+    int k = 0;
+    for (int i = 62; i >= 0; i--) {
+        line_dbl_step(T, l);
+        line_store(dst + (k++) * LCB_LINE_WORDS, l);
+        if ((LCB_Z_ABS >> i) & 1) {
+            line_add_step(T, Q.x, Q.y, l);
+            line_store(dst + (k++) * LCB_LINE_WORDS, l);
+        }
+    }
+}
+
+// f *= l evaluated at P = (xP, yP)
+DI void fp12_mul_line_at(fp12 &f, const line &l, const fp &xP, const fp &yP) {
+    fp2 B, C;
+    fp2_mul_fp(B, l.Bc, xP);
+    fp2_mul_fp(C, l.Cc, yP);
+    fp12_mul_line(f, l.A, B, C);
+}
+
+// Line sources for the two-pair Miller loop
+struct LinesFromMemory {
+    const u32 *p;
+    DI void next(line &l, bool) { line_load(l, p); p += LCB_LINE_WORDS; }
+};
+struct LinesOnTheFly {
+    g2 T; fp2 xQ, yQ; bool inf;
+    DI void init(const g2a &Q) { inf = Q.inf; xQ = Q.x; yQ = Q.y; T.x = Q.x; T.y = Q.y; T.z = fp2_one(); }
+    DI void next(line &l, bool is_add) {
+        if (inf) { line_one(l); return; }
+        if (is_add) line_add_step(T, xQ, yQ, l);
+        else line_dbl_step(T, l);
+    }
+};
+
+// f = prod_k f_{|z|, Q_k}(P_k), conjugated (z < 0).  A pair whose G1 point is infinity contributes 1.
+template <class S1, class S2>
+DI void miller2(fp12 &f, S1 &s1, const g1a &P1, S2 &s2, const g1a &P2) {
+    f = fp12_one();
+    line l;
+    bool first = true;
+    for (int i = 62; i >= 0; i--) {
+        if (!first) fp12_sqr(f, f);
+        first = false;
+        s1.next(l, false);
+        if (!P1.inf) fp12_mul_line_at(f, l, P1.x, P1.y);
+        s2.next(l, false);
+        if (!P2.inf) fp12_mul_line_at(f, l, P2.x, P2.y);
+        if ((LCB_Z_ABS >> i) & 1) {
+            s1.next(l, true);
+            if (!P1.inf) fp12_mul_line_at(f, l, P1.x, P1.y);
+            s2.next(l, true);
+            if (!P2.inf) fp12_mul_line_at(f, l, P2.x, P2.y);
+        }
+    }
+    fp12_conj(f, f);
+}
+template <class S1>
+DI void miller1(fp12 &f, S1 &s1, const g1a &P1) {
+    f = fp12_one();
+    line l;
+    bool first = true;
+    for (int i = 62; i >= 0; i--) {
+        if (!first) fp12_sqr(f, f);
+        first = false;
+        s1.next(l, false);
+        if (!P1.inf) fp12_mul_line_at(f, l, P1.x, P1.y);
+        if ((LCB_Z_ABS >> i) & 1) {
+            s1.next(l, true);
+            if (!P1.inf) fp12_mul_line_at(f, l, P1.x, P1.y);
+        }
+    }
+    fp12_conj(f, f);
+}
+
+// ---------------------------------------------------------------- final exponentiation
+DN void fe_easy(fp12 &r, const fp12 &f) {
+    fp12 t0, t1;
+    fp12_conj(t0, f);
+    fp12_inv_n(t1, f);
+    fp12_mul_n(t0, t0, t1);  // f^(p^6 - 1)
+    fp12_frob2_n(t1, t0);
+    fp12_mul_n(r, t1, t0);   // ^(p^2 + 1)
+}
+// x^z for unitary x (z = -|z|): cyclotomic square-and-multiply over |z|, then conjugate
+DN void cyc_pow_z(fp12 &r, const fp12 &x) {
+    fp12 acc = x;
+    for (int i = 62; i >= 0; i--) {
+        fp12_cyc_sqr(acc, acc);
+        if ((LCB_Z_ABS >> i) & 1) fp12_mul_n(acc, acc, x);
+    }
+    fp12_conj(r, acc);
+}
+DN void fe_hard(fp12 &y, const fp12 &x) {
+    fp12 a0, a1, a2, a3, a4, a5, a6, a7;
+    fp12_conj(a0, x);             // x^-1
+    fp12_cyc_sqr_n(a1, a0);       // x^-2
+    cyc_pow_z(a2, x);             // x^z
+    fp12_cyc_sqr_n(a3, a2);       // x^2z
+    fp12_mul_n(a1, a1, a2);       // x^(z-2)
+    cyc_pow_z(a7, a1);            // x^(z^2-2z)
+    cyc_pow_z(a4, a7);            // x^(z^3-2z^2)
+    cyc_pow_z(a5, a4);            // x^(z^4-2z^3)
+    fp12_mul_n(a3, a3, a5);       // x^(z^4-2z^3+2z)
+    cyc_pow_z(a6, a3);            // x^(z^5-2z^4+2z^2)
+    fp12_conj(a1, a1);            // x^(2-z)
+    fp12_mul_n(a1, a1, a6);
+    fp12_mul_n(a1, a1, x);        // x^c0
+    fp12_mul_n(a3, a3, a0);       // x^c1
+    fp12_frob1_n(a3, a3);
+    fp12_mul_n(a1, a1, a3);
+    fp12_mul_n(a4, a4, a2);       // x^c2
+    fp12_frob2_n(a4, a4);
+    fp12_mul_n(a1, a1, a4);
+    fp12_mul_n(a7, a7, x);        // x^c3
+    fp12_frob3_n(y, a7);
+    fp12_mul_n(y, y, a1);
+}
+DN void final_exp(fp12 &r, const fp12 &f) {
+    fp12 t;
+    fe_easy(t, f);
+    fe_hard(r, t);
+}

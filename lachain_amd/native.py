@@ -1,0 +1,302 @@
+"""lachain_amd/native.py — ctypes binding of liblachain_bls.so (include/lachain_bls.h).
+
+This is the product path: every call lands in gfx950 kernels.  There is no CPU fallback — if the
+library is missing or no gfx950 device can be opened, `lib()` raises.
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "liblachain_bls.so")
+MCL_BLS12_381 = 5
+MCLBN_COMPILED_TIME_VAR = 46
+
+_lib = None
+_lock = threading.Lock()
+
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+c_size = ctypes.c_size_t
+
+
+class mclBnFr(ctypes.Structure):
+    _fields_ = [("d", ctypes.c_uint64 * 4)]
+
+
+class mclBnFp(ctypes.Structure):
+    _fields_ = [("d", ctypes.c_uint64 * 6)]
+
+
+class mclBnFp2(ctypes.Structure):
+    _fields_ = [("d", mclBnFp * 2)]
+
+
+class mclBnG1(ctypes.Structure):
+    _fields_ = [("x", mclBnFp), ("y", mclBnFp), ("z", mclBnFp)]
+
+
+class mclBnG2(ctypes.Structure):
+    _fields_ = [("x", mclBnFp2), ("y", mclBnFp2), ("z", mclBnFp2)]
+
+
+class mclBnGT(ctypes.Structure):
+    _fields_ = [("d", mclBnFp * 12)]
+
+
+# exported symbols (also checked by tests/test_abi_exports.py against include/lachain_bls.h)
+_SIGS = {
+    "mclBn_init": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "lcb_set_device": (ctypes.c_int, [ctypes.c_int]),
+    "lcb_get_device": (ctypes.c_int, []),
+    "lcb_set_original_g2_cofactor": (None, [ctypes.c_int]),
+    "lcb_last_error": (ctypes.c_char_p, []),
+    "lcb_tpke_verify_shares": (ctypes.c_int, [c_u8p, c_size, c_u8p, c_size, c_u8p, c_u8p, c_u8p, c_u32p, c_size,
+                                              c_u32p, c_u32p, c_u8p]),
+    "lcb_tpke_verify_shares_dev": (ctypes.c_int, [ctypes.c_void_p, c_size, ctypes.c_void_p, c_size, ctypes.c_void_p,
+                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_size,
+                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "lcb_tpke_partial_decrypt": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_u8p, c_u8p, c_u32p, c_size]),
+    "lcb_tpke_encrypt_phase1": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_size]),
+    "lcb_tpke_encrypt_phase2": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_u32p, c_size]),
+    "lcb_ts_verify_shares": (ctypes.c_int, [c_u8p, c_size, c_u8p, c_size, c_u8p, c_u8p, c_u32p, c_size, c_u32p,
+                                            c_u32p]),
+    "lcb_ts_verify_shares_dev": (ctypes.c_int, [ctypes.c_void_p, c_size, ctypes.c_void_p, c_size, ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_void_p, c_size, ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_void_p]),
+    "lcb_ts_sign": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u32p, c_u32p, c_size]),
+    "lcb_g1_lagrange_batch": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_u32p, c_size]),
+    "lcb_g2_lagrange_batch": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_u32p, c_size]),
+    "lcb_g1_msm": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_size]),
+    "lcb_g1_mul_batch": (ctypes.c_int, [c_u8p, c_u8p, ctypes.c_int, c_u8p, c_size]),
+    "lcb_g2_mul_batch": (ctypes.c_int, [c_u8p, c_u8p, ctypes.c_int, c_u8p, c_size]),
+    "lcb_g2_hash_batch": (ctypes.c_int, [c_u8p, c_u8p, c_u32p, c_size]),
+    "lcb_xor_with_hash": (None, [c_u8p, c_u8p, c_u8p, c_size]),
+}
+
+
+def load(check_device=True):
+    """Load the shared library; with check_device, also initialise the GPU (mclBn_init)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(f"{LIB_PATH} is not built (run __graft_entry__.build() or make -C lachain_amd/csrc)")
+            lib_ = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in _SIGS.items():
+                fn = getattr(lib_, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib_
+        if check_device and not getattr(_lib, "_inited", False):
+            rc = _lib.mclBn_init(MCL_BLS12_381, MCLBN_COMPILED_TIME_VAR)
+            if rc != 0:
+                raise RuntimeError("liblachain_bls: mclBn_init failed: " + _lib.lcb_last_error().decode())
+            _lib._inited = True
+    return _lib
+
+
+def lib():
+    return load(True)
+
+
+def last_error():
+    return lib().lcb_last_error().decode()
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"liblachain_bls {what} failed: {last_error()}")
+
+
+def _bytes_ptr(b):
+    """ctypes uint8 pointer to an immutable bytes object (read-only use)."""
+    if not isinstance(b, (bytes, bytearray)):
+        b = bytes(b)
+    buf = (ctypes.c_uint8 * max(1, len(b))).from_buffer_copy(b if len(b) else b"\0")
+    return buf, ctypes.cast(buf, c_u8p)
+
+
+def _u32_ptr(vals):
+    arr = (ctypes.c_uint32 * max(1, len(vals)))(*vals)
+    return arr, ctypes.cast(arr, c_u32p)
+
+
+def _out(n):
+    buf = (ctypes.c_uint8 * max(1, n))()
+    return buf, ctypes.cast(buf, c_u8p)
+
+
+def _offsets(chunks):
+    off = [0]
+    for c in chunks:
+        off.append(off[-1] + len(c))
+    return off
+
+
+# ---------------------------------------------------------------- batch wrappers (bytes in / bytes out)
+def tpke_verify_shares(y_keys, cts, shares):
+    """y_keys: list of 48-byte verification keys; cts: list of (U48, V, W96);
+    shares: list of (ct_index, decryptor_index, Ui48).  Returns list of bools."""
+    n = len(shares)
+    keep = []
+    _, py = _bytes_ptr_keep(keep, b"".join(y_keys))
+    _, pu = _bytes_ptr_keep(keep, b"".join(c[0] for c in cts))
+    _, pw = _bytes_ptr_keep(keep, b"".join(c[2] for c in cts))
+    _, pv = _bytes_ptr_keep(keep, b"".join(c[1] for c in cts))
+    _, pvo = _u32_keep(keep, _offsets([c[1] for c in cts]))
+    _, pct = _u32_keep(keep, [s[0] for s in shares])
+    _, pdec = _u32_keep(keep, [s[1] for s in shares])
+    _, pui = _bytes_ptr_keep(keep, b"".join(s[2] for s in shares))
+    ob, po = _out(n)
+    _check(lib().lcb_tpke_verify_shares(po, n, py, len(y_keys), pu, pw, pv, pvo, len(cts), pct, pdec, pui),
+           "tpke_verify_shares")
+    return [bool(ob[i]) for i in range(n)]
+
+
+def _bytes_ptr_keep(keep, b):
+    buf, p = _bytes_ptr(b)
+    keep.append(buf)
+    return buf, p
+
+
+def _u32_keep(keep, vals):
+    arr, p = _u32_ptr(vals)
+    keep.append(arr)
+    return arr, p
+
+
+def tpke_partial_decrypt(x32, cts):
+    """cts: list of (U, V, W).  Returns list of (ok, Ui48)."""
+    keep = []
+    n = len(cts)
+    _, px = _bytes_ptr_keep(keep, x32)
+    _, pu = _bytes_ptr_keep(keep, b"".join(c[0] for c in cts))
+    _, pw = _bytes_ptr_keep(keep, b"".join(c[2] for c in cts))
+    _, pv = _bytes_ptr_keep(keep, b"".join(c[1] for c in cts))
+    _, pvo = _u32_keep(keep, _offsets([c[1] for c in cts]))
+    ob, po = _out(48 * n)
+    sb, ps = _out(n)
+    _check(lib().lcb_tpke_partial_decrypt(po, ps, px, pu, pw, pv, pvo, n), "tpke_partial_decrypt")
+    raw = bytes(ob)
+    return [(bool(sb[i]), raw[48 * i:48 * i + 48]) for i in range(n)]
+
+
+def tpke_encrypt_phase1(y48, rs):
+    keep = []
+    n = len(rs)
+    _, py = _bytes_ptr_keep(keep, y48)
+    _, pr = _bytes_ptr_keep(keep, b"".join(rs))
+    ub, pu = _out(48 * n)
+    tb, pt = _out(48 * n)
+    _check(lib().lcb_tpke_encrypt_phase1(pu, pt, py, pr, n), "tpke_encrypt_phase1")
+    u, t = bytes(ub), bytes(tb)
+    return [u[48 * i:48 * i + 48] for i in range(n)], [t[48 * i:48 * i + 48] for i in range(n)]
+
+
+def tpke_encrypt_phase2(us, rs, vs):
+    keep = []
+    n = len(us)
+    _, pu = _bytes_ptr_keep(keep, b"".join(us))
+    _, pr = _bytes_ptr_keep(keep, b"".join(rs))
+    _, pv = _bytes_ptr_keep(keep, b"".join(vs))
+    _, pvo = _u32_keep(keep, _offsets(vs))
+    wb, pw = _out(96 * n)
+    _check(lib().lcb_tpke_encrypt_phase2(pw, pu, pr, pv, pvo, n), "tpke_encrypt_phase2")
+    w = bytes(wb)
+    return [w[96 * i:96 * i + 96] for i in range(n)]
+
+
+def ts_verify_shares(pks, msgs, items):
+    """pks: list of 48-byte keys; msgs: list of bytes; items: list of (msg_index, pk_index, sig96)."""
+    keep = []
+    n = len(items)
+    _, ppk = _bytes_ptr_keep(keep, b"".join(pks))
+    _, psig = _bytes_ptr_keep(keep, b"".join(it[2] for it in items))
+    _, pm = _bytes_ptr_keep(keep, b"".join(msgs))
+    _, pmo = _u32_keep(keep, _offsets(msgs))
+    _, pmi = _u32_keep(keep, [it[0] for it in items])
+    _, ppi = _u32_keep(keep, [it[1] for it in items])
+    ob, po = _out(n)
+    _check(lib().lcb_ts_verify_shares(po, n, ppk, len(pks), psig, pm, pmo, len(msgs), pmi, ppi), "ts_verify_shares")
+    return [bool(ob[i]) for i in range(n)]
+
+
+def ts_sign(sks, msgs, msg_idx):
+    keep = []
+    n = len(sks)
+    _, psk = _bytes_ptr_keep(keep, b"".join(sks))
+    _, pm = _bytes_ptr_keep(keep, b"".join(msgs))
+    _, pmo = _u32_keep(keep, _offsets(msgs))
+    _, pmi = _u32_keep(keep, msg_idx)
+    ob, po = _out(96 * n)
+    _check(lib().lcb_ts_sign(po, psk, pm, pmo, pmi, n), "ts_sign")
+    o = bytes(ob)
+    return [o[96 * i:96 * i + 96] for i in range(n)]
+
+
+def lagrange_batch(group, problems):
+    """group 1 or 2; problems: list of (xs: list of Fr32, ys: list of points).  Returns list of point|None."""
+    keep = []
+    pb = 48 if group == 1 else 96
+    xs = [x for xs_, _ in problems for x in xs_]
+    ys = [y for _, ys_ in problems for y in ys_]
+    off = [0]
+    for xs_, _ in problems:
+        off.append(off[-1] + len(xs_))
+    _, px = _bytes_ptr_keep(keep, b"".join(xs))
+    _, py = _bytes_ptr_keep(keep, b"".join(ys))
+    _, poff = _u32_keep(keep, off)
+    np_ = len(problems)
+    ob, po = _out(pb * np_)
+    sb, ps = _out(np_)
+    fn = lib().lcb_g1_lagrange_batch if group == 1 else lib().lcb_g2_lagrange_batch
+    _check(fn(po, ps, px, py, poff, np_), "lagrange_batch")
+    o = bytes(ob)
+    return [o[pb * j:pb * j + pb] if sb[j] else None for j in range(np_)]
+
+
+def g1_msm(points, scalars):
+    keep = []
+    _, pp = _bytes_ptr_keep(keep, b"".join(points))
+    _, ps = _bytes_ptr_keep(keep, b"".join(scalars))
+    ob, po = _out(48)
+    _check(lib().lcb_g1_msm(po, pp, ps, len(points)), "g1_msm")
+    return bytes(ob)
+
+
+def mul_batch(group, points, scalars, generator=False):
+    keep = []
+    pb = 48 if group == 1 else 96
+    n = len(scalars)
+    _, pp = _bytes_ptr_keep(keep, b"".join(points) if not generator else b"\0")
+    _, ps = _bytes_ptr_keep(keep, b"".join(scalars))
+    ob, po = _out(pb * n)
+    fn = lib().lcb_g1_mul_batch if group == 1 else lib().lcb_g2_mul_batch
+    _check(fn(po, pp, 1 if generator else 0, ps, n), "mul_batch")
+    o = bytes(ob)
+    return [o[pb * i:pb * i + pb] for i in range(n)]
+
+
+def g2_hash_batch(msgs):
+    keep = []
+    n = len(msgs)
+    _, pm = _bytes_ptr_keep(keep, b"".join(msgs))
+    _, pmo = _u32_keep(keep, _offsets(msgs))
+    ob, po = _out(96 * n)
+    _check(lib().lcb_g2_hash_batch(po, pm, pmo, n), "g2_hash_batch")
+    o = bytes(ob)
+    return [o[96 * i:96 * i + 96] for i in range(n)]
+
+
+def xor_with_hash(g1_48, data):
+    keep = []
+    _, pg = _bytes_ptr_keep(keep, g1_48)
+    _, pd = _bytes_ptr_keep(keep, data)
+    ob, po = _out(len(data))
+    load(False).lcb_xor_with_hash(po, pg, pd, len(data))
+    return bytes(ob)[: len(data)]
+
+
+def set_original_g2_cofactor(enable):
+    lib().lcb_set_original_g2_cofactor(1 if enable else 0)

@@ -40,6 +40,10 @@ def fr(v: int) -> bytes:
     return (v % R).to_bytes(32, "little")
 
 
+def fr_from_int(v: int) -> bytes:
+    o = _buf(32); lib().orc_fr_from_int(o, ctypes.c_int64(v)); return o.raw
+
+
 def fr_mul(a, b):
     o = _buf(32); _ck(lib().orc_fr_mul(o, a, b), "fr_mul"); return o.raw
 

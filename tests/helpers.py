@@ -1,0 +1,33 @@
+"""Shared helpers for the tests: deterministic inputs and golden-fixture access."""
+import hashlib
+import json
+import os
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+
+
+def kats():
+    with open(os.path.join(GOLDEN, "reference_kats.json")) as f:
+        return json.load(f)
+
+
+class Drbg:
+    """Counter-mode SHA-256 DRBG -> Fr by 64-byte wide reduction."""
+
+    def __init__(self, seed: bytes):
+        self.seed = seed
+        self.ctr = 0
+
+    def bytes(self, n):
+        out = b""
+        while len(out) < n:
+            out += hashlib.sha256(self.seed + self.ctr.to_bytes(8, "little")).digest()
+            self.ctr += 1
+        return out[:n]
+
+    def fr_int(self):
+        return int.from_bytes(self.bytes(64), "little") % R
+
+    def fr(self):
+        return self.fr_int().to_bytes(32, "little")

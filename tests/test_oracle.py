@@ -1,0 +1,165 @@
+"""CPU tests: the oracle (oracle/liborc.so, a C restatement of the MCL path) against the reference's
+known-answer vectors, plus its internal self-consistency.  These pin the checker before it is trusted.
+"""
+import random
+
+import oracle as o
+import pytest
+
+from helpers import Drbg, kats
+
+
+def test_serialization_kats():
+    # test/Lachain.CryptoTest/SerializationTest.cs:20-57
+    k = kats()
+    assert o.fr_from_int(0).hex() == k["fr_0"]["hex"]
+    assert o.fr_from_int(1).hex() == k["fr_1"]["hex"]
+    g1, g2 = o.g1_gen(), o.g2_gen()
+    assert g1.hex() == k["g1_generator"]["hex"]
+    assert o.g1_mul(g1, o.fr(2)).hex() == k["g1_generator_x2"]["hex"]
+    assert o.g2_gen().hex() == k["g2_generator"]["hex"]
+    assert o.g2_mul(g2, o.fr(2)).hex() == k["g2_generator_x2"]["hex"]
+    assert o.g1_mul(g1, o.fr(0)).hex() == k["g1_zero"]["hex"]
+    assert o.g2_mul(g2, o.fr(0)).hex() == k["g2_zero"]["hex"]
+    # the doubling formulas agree with the addition formulas on the vectors
+    assert o.g1_add(g1, g1).hex() == k["g1_generator_x2"]["hex"]
+    assert o.g2_add(g2, g2).hex() == k["g2_generator_x2"]["hex"]
+
+
+def test_kdf_kat():
+    # test/Lachain.CryptoTest/CryptographyTest.cs:103-113 (BouncyCastle DigestRandomGenerator(Sha3Digest))
+    k = kats()["kdf_deadbeef_32"]
+    assert o.drg_bytes(bytes.fromhex(k["seed_hex"]), 32).hex() == k["hex"]
+
+
+def test_config_keys_decode():
+    # every G1 key in the reference's sample / network configs decodes, and re-serializes identically
+    for e in kats()["g1_config_keys"]:
+        b = bytes.fromhex(e["hex"])
+        assert o.g1_valid(b), e["source"]
+        assert o.g1_in_subgroup(b), e["source"]
+        assert o.g1_add(b, o.g1_mul(o.g1_gen(), o.fr(0))) == b
+
+
+def test_sha_vectors():
+    import hashlib
+    for m in [b"", b"abc", bytes(range(200))]:
+        assert o.sha256(m) == hashlib.sha256(m).digest()
+        assert o.sha512(m) == hashlib.sha512(m).digest()
+        assert o.sha3_256(m) == hashlib.sha3_256(m).digest()
+
+
+def test_pairing_bilinear_and_paths_agree():
+    d = Drbg(b"oracle-bilinear")
+    G1, G2 = o.g1_gen(), o.g2_gen()
+    e = o.pairing(G1, G2)
+    for _ in range(3):
+        a, b = d.fr_int(), d.fr_int()
+        A, B = o.g1_mul(G1, o.fr(a)), o.g2_mul(G2, o.fr(b))
+        eab = o.pairing(A, B)
+        assert eab == o.gt_pow(e, o.fr(a * b))            # MclTests.cs:64-75
+        assert eab == o.pairing_slow(A, B)                 # affine Miller loop + direct exponent
+        f = o.miller_loop(A, B)
+        assert o.final_exp(f) == o.final_exp_direct(f)     # addition chain == 3(p^4-p^2+1)/r power
+    assert e != o.pairing(G1, o.g2_mul(G2, o.fr(0)))
+
+
+def test_cyclotomic_and_sparse_helpers():
+    import ctypes
+    d = Drbg(b"oracle-helpers")
+    A = o.g1_mul(o.g1_gen(), d.fr())
+    B = o.g2_mul(o.g2_gen(), d.fr())
+    f = o.miller_loop(A, B)
+    out = ctypes.create_string_buffer(576)
+    assert o.lib().orc_test_cyc_sqr(out, f) == 0
+    rnd = random.Random(5)
+    abc = b"".join(rnd.randrange(o.P).to_bytes(48, "little") for _ in range(6))
+    assert o.lib().orc_test_sparse_line(f, abc) == 0
+
+
+def test_hash_to_g2_properties():
+    for m in [b"", b"\x00", b"lachain", bytes(range(100))]:
+        h = o.g2_hash(m)
+        assert o.g2_valid(h) and o.g2_in_subgroup(h)
+    o.set_g2_original_cofactor(1)
+    try:
+        h2 = o.g2_hash(b"lachain")
+        assert o.g2_in_subgroup(h2)
+    finally:
+        o.set_g2_original_cofactor(0)
+
+
+def test_lagrange_and_poly():
+    # MclTests.cs:90-118: evaluate a degree-9 polynomial at 100..110, interpolate the intercept
+    d = Drbg(b"oracle-poly")
+    poly = [d.fr() for _ in range(10)]
+    xs = [o.fr(100 + i) for i in range(11)]
+    ys = [o.fr_eval_poly(poly, x) for x in xs]
+    assert o.fr_lagrange(xs, ys) == poly[0]
+    # group versions: ys_i = poly(x_i) * G
+    G1, G2 = o.g1_gen(), o.g2_gen()
+    assert o.g1_lagrange(xs, [o.g1_mul(G1, y) for y in ys]) == o.g1_mul(G1, poly[0])
+    assert o.g2_lagrange(xs[:5], [o.g2_mul(G2, y) for y in ys[:5]]) != o.g2_mul(G2, poly[0])
+    # error cases: k == 0, zero x, duplicate x
+    assert o.g1_lagrange([], []) is None
+    assert o.g1_lagrange([o.fr(0), o.fr(1)], [G1, G1]) is None
+    assert o.g1_lagrange([o.fr(3), o.fr(3)], [G1, G1]) is None
+
+
+def test_tpke_roundtrip():
+    # test/Lachain.CryptoTest/TPKETest.cs:23-58 with N=7, F=2, Id=132
+    d = Drbg(b"oracle-tpke")
+    n, f = 7, 2
+    coeffs = [d.fr() for _ in range(f)]  # TPKE TrustedKeyGen: f coefficients
+    x = [o.fr_eval_poly(coeffs, o.fr(i + 1)) for i in range(n)]
+    y = o.g1_mul(o.g1_gen(), o.fr_eval_poly(coeffs, o.fr(0)))
+    yi = [o.g1_mul(o.g1_gen(), xi) for xi in x]
+    data = bytes(range(1, 10))
+    U, V, W = o.tpke_encrypt(y, data, d.fr())
+    parts = []
+    for i in (1, 4):
+        ui = o.tpke_decrypt(U, V, W, x[i])
+        assert o.tpke_verify_share(yi[i], U, V, W, ui) == 1
+        assert o.tpke_verify_share(yi[(i + 1) % n], U, V, W, ui) == 0
+        parts.append((i, ui))
+    assert o.tpke_full_decrypt(V, [i for i, _ in parts], [u for _, u in parts]) == data
+    with pytest.raises(ValueError):
+        o.tpke_decrypt(U, V, o.g2_mul(W, o.fr(2)), x[0])   # ciphertext validity check
+
+
+def test_threshold_signature_roundtrip():
+    # test/Lachain.CryptoTest/ThresholdSignatureTest.cs:11-43, n=7, f=2, msg = 0xdeadbeef LE
+    d = Drbg(b"oracle-ts")
+    n, f = 7, 2
+    coeffs = [d.fr() for _ in range(f + 1)]
+    sk = [o.fr_eval_poly(coeffs, o.fr(i + 1)) for i in range(n)]
+    pk = [o.g1_mul(o.g1_gen(), s) for s in sk]
+    msg = (0xdeadbeef).to_bytes(4, "little")
+    sigs = [o.ts_sign(s, msg) for s in sk]
+    for i in range(n):
+        assert o.ts_validate(pk[i], sigs[i], msg) == 1
+    assert o.ts_validate(pk[0], sigs[1], msg) == 0
+    xs = [o.fr(i + 1) for i in range(f + 1)]
+    combined = o.g2_lagrange(xs, sigs[: f + 1])
+    shared_pk = o.g1_lagrange([o.fr(i + 1) for i in range(n)], pk)
+    assert shared_pk == o.g1_mul(o.g1_gen(), coeffs[0])
+    assert o.ts_validate(shared_pk, combined, msg) == 1
+    assert combined == o.g2_lagrange([o.fr(i + 1) for i in range(2, 5)], sigs[2:5])
+
+
+def test_malformed_encodings_rejected():
+    g1 = bytearray(o.g1_gen())
+    bad = bytearray(g1)
+    bad[47] |= 0x60                      # x >= 2^381 > p
+    assert not o.g1_valid(bytes(bad))
+    # reversed bytes (HoneyBadgerMalicious.cs:23) are either rejected or a different point
+    rev = bytes(reversed(g1))
+    assert (not o.g1_valid(rev)) or rev != bytes(g1)
+    # an x with no square root of x^3 + 4 is rejected
+    x = 5
+    while True:
+        cand = x.to_bytes(48, "little")
+        if not o.g1_valid(cand):
+            break
+        x += 1
+    assert not o.g1_valid(cand)
