@@ -1,0 +1,260 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json metric on MI355X: batched TPKE decryption-share verifications per second.
+
+Workload (BASELINE.json configs[1]): 1,048,576 decryption shares of N=22, F=7
+validators = 47,663 ciphertexts x 22 decryptors (the last ciphertext carries 12 shares), V = 32 bytes,
+DKG-style keys of degree F, 1 % of shares corrupted (U_i + G) so the reject path is exercised.
+One "step" = one pass of the hot path over the whole batch, inputs resident in HBM:
+  lcb_tpke_prepare_dev          (k_g1_decompress: 22 keys; k_tpke_ct_prepare: per-ciphertext H(U||V) +
+                                 Miller lines of H and W)
+  lcb_tpke_verify_prepared_dev  (k_tpke_verify: per share, decompress U_i, 2-pair Miller loop, final exp)
+Launch: `python bench.py --gpus 1` or under torch.distributed.run with --gpus N (one rank per GPU, weak
+scaling: every rank verifies its own 1M-share batch; no data-path collective).
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
+SEED = 0x4C61636861696E
+
+# Canonical Fp-mul counts (oracle/bls.c:orc_count_units; frozen in BASELINE.md §3) and MACs per Fp-mul
+C = dict(C_ML1_EVAL=5192, C_ML2_EVAL=8116, C_LINES=2012, C_FE=8603, C_H2G2=7266, C_DEC1=611, C_DEC2=1837,
+         C_MUL1=2835, C_MUL2=6908, C_AFF2=625)
+MAC_PER_FPMUL = 300                      # 12x12 (a*b) + 12x12 (m*p) + 12 (m) 32-bit MACs, CIOS/FIPS Montgomery
+W_VERIFY = C["C_DEC1"] + C["C_ML2_EVAL"] + C["C_FE"]                                   # per share
+W_PREPARE = C["C_DEC1"] + C["C_DEC2"] + C["C_H2G2"] + C["C_AFF2"] + 2 * C["C_LINES"]  # per ciphertext
+# gfx950 v_mad_u64_u32 is half rate: 64 lane-MACs / clk / CU (profiles/r01_valu_rates.jsonl)
+PEAK_MAC32 = 256 * 64 * 2.4e9            # 3.93e13 MAC/s at the 2.4 GHz max clock
+
+
+class Drbg:
+    def __init__(self, seed: bytes):
+        self.seed, self.ctr = seed, 0
+
+    def block(self, n):
+        out = bytearray()
+        while len(out) < n:
+            out += hashlib.sha256(self.seed + self.ctr.to_bytes(8, "little")).digest()
+            self.ctr += 1
+        return bytes(out[:n])
+
+    def fr(self):
+        return int.from_bytes(self.block(64), "little") % R
+
+
+def make_inputs(nat, rank, n_shares, n_dec, f, vlen, corrupt_frac=0.01):
+    """Synthetic TPKE batch generated with the product's own batch kernels (untimed)."""
+    d = Drbg(SEED.to_bytes(8, "little") + rank.to_bytes(4, "little"))
+    coeffs = [d.fr() for _ in range(f + 1)]
+
+    def poly(x):
+        acc = 0
+        for c in reversed(coeffs):
+            acc = (acc * x + c) % R
+        return acc
+
+    xs = [poly(i + 1) for i in range(n_dec)]
+    y_secret = poly(0)
+    n_cts = (n_shares + n_dec - 1) // n_dec
+    rs = [d.fr() for _ in range(n_cts)]
+    fr = lambda v: v.to_bytes(32, "little")
+    y_keys = nat.mul_batch(1, None, [fr(x) for x in xs], generator=True)
+    (y_pub,) = nat.mul_batch(1, None, [fr(y_secret)], generator=True)
+    us, ts = nat.tpke_encrypt_phase1(y_pub, [fr(r) for r in rs])
+    plain = d.block(vlen * n_cts)
+    vs = [nat.xor_with_hash(ts[c], plain[c * vlen:(c + 1) * vlen]) for c in range(n_cts)]
+    ws = nat.tpke_encrypt_phase2(us, [fr(r) for r in rs], vs)
+    # shares: U_i = x_i U = (x_i r) G; corrupted: (x_i r + 1) G = U_i + G
+    ct_idx = np.empty(n_shares, dtype=np.uint32)
+    dec_idx = np.empty(n_shares, dtype=np.uint32)
+    scal = bytearray(32 * n_shares)
+    expect = np.ones(n_shares, dtype=np.uint8)
+    stride = int(round(1 / corrupt_frac)) if corrupt_frac > 0 else 0
+    for i in range(n_shares):
+        c, j = divmod(i, n_dec)
+        ct_idx[i], dec_idx[i] = c, j
+        s = xs[j] * rs[c] % R
+        if stride and i % stride == stride // 2:
+            s = (s + 1) % R
+            expect[i] = 0
+        scal[32 * i:32 * i + 32] = s.to_bytes(32, "little")
+    ui = nat.mul_batch_raw(1, b"", bytes(scal), n_shares, generator=True)
+    v_off = np.arange(0, vlen * (n_cts + 1), vlen, dtype=np.uint32)
+    return dict(y_keys=b"".join(y_keys), u=b"".join(us), w=b"".join(ws), v=b"".join(vs), v_off=v_off,
+                ct_idx=ct_idx, dec_idx=dec_idx, ui=ui, expect=expect, n_cts=n_cts, n_dec=n_dec,
+                keys_list=y_keys, cts_list=list(zip(us, vs, ws)))
+
+
+def to_dev(torch, dev, b):
+    if isinstance(b, np.ndarray):
+        return torch.from_numpy(b.view(np.uint8).copy()).to(dev)
+    return torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+
+
+def cpu_baseline(inp, target_s=15.0):
+    """Time the oracle's as-reference path (hash + two pairings per VerifyShare call) on host cores."""
+    import ctypes
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as o
+    lib = o.lib()
+    threads = max(1, min(16, os.cpu_count() or 1))
+    n_total = len(inp["expect"])
+    y = inp["y_keys"]
+    u, v, w, ui = inp["u"], inp["v"], inp["w"], inp["ui"]
+    vlen = int(inp["v_off"][1] - inp["v_off"][0])
+
+    def run(n):
+        acc = (ctypes.c_uint8 * n)()
+        ct = (ctypes.c_uint32 * n)(*[int(x) for x in inp["ct_idx"][:n]])
+        dc = (ctypes.c_uint32 * n)(*[int(x) for x in inp["dec_idx"][:n]])
+        t0 = time.perf_counter()
+        rc = lib.orc_tpke_verify_batch(acc, ctypes.c_size_t(n), y, u, v, ctypes.c_size_t(vlen), w, ct, dc,
+                                       ui[:48 * n], threads)
+        dt = time.perf_counter() - t0
+        assert rc == 0
+        mism = int(np.sum(np.frombuffer(bytes(acc), dtype=np.uint8) != inp["expect"][:n]))
+        return dt, mism
+
+    n = 4 * threads
+    dt, _ = run(n)
+    n = int(min(n_total, max(n, n * target_s / max(dt, 1e-3))))
+    dt, mism = run(n)
+    return dict(value=n / dt, unit="share verifications/s", cores=threads, kind="port",
+                sample=f"first {n} shares of the same batch, oracle/bls.c orc_tpke_verify_batch "
+                       f"(as-reference: G2.SetHashOf + two pairings per VerifyShare), {threads} OpenMP threads, "
+                       f"{dt:.1f} s, {mism} decision mismatches vs expected")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--shares", type=int, default=1048576)
+    ap.add_argument("--n", type=int, default=22)
+    ap.add_argument("--f", type=int, default=7)
+    ap.add_argument("--vlen", type=int, default=32)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    from lachain_amd import native as nat
+
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    nat.load(False).lcb_set_device(local_rank)
+    nat.lib()
+
+    t_gen = time.perf_counter()
+    inp = make_inputs(nat, rank, args.shares, args.n, args.f, args.vlen)
+    t_gen = time.perf_counter() - t_gen
+    n, n_cts, n_dec = args.shares, inp["n_cts"], inp["n_dec"]
+
+    d_y = to_dev(torch, dev, inp["y_keys"])
+    d_u = to_dev(torch, dev, inp["u"])
+    d_w = to_dev(torch, dev, inp["w"])
+    d_v = to_dev(torch, dev, inp["v"])
+    d_voff = to_dev(torch, dev, inp["v_off"])
+    d_ct = to_dev(torch, dev, inp["ct_idx"])
+    d_dec = to_dev(torch, dev, inp["dec_idx"])
+    d_ui = to_dev(torch, dev, inp["ui"])
+    d_acc = torch.zeros(n, dtype=torch.uint8, device=dev)
+    lib = nat.lib()
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        rc = lib.lcb_tpke_prepare_dev(d_y.data_ptr(), n_dec, d_u.data_ptr(), d_w.data_ptr(), d_v.data_ptr(),
+                                      d_voff.data_ptr(), n_cts, sh)
+        if ev is not None:
+            ev[1].record(stream)
+        rc |= lib.lcb_tpke_verify_prepared_dev(d_acc.data_ptr(), n, n_dec, n_cts, d_ct.data_ptr(), d_dec.data_ptr(),
+                                               d_ui.data_ptr(), sh)
+        if ev is not None:
+            ev[2].record(stream)
+        if rc != 0:
+            raise RuntimeError(nat.last_error())
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    got = d_acc.cpu().numpy()
+    mismatches = int(np.sum(got != inp["expect"]))
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prep_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+    ver_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    got = d_acc.cpu().numpy()
+    mismatches += int(np.sum(got != inp["expect"]))
+
+    t = torch.tensor([elapsed, float(mismatches), float(n)], dtype=torch.float64, device=dev)
+    if world > 1:
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        elapsed = float(tmax[0])
+    mismatches_all, shares_all = int(t[1]), int(t[2])
+    if rank == 0:
+        ms_per_step = 1e3 * elapsed / args.steps
+        value = shares_all * args.steps / elapsed
+        achieved = n * W_VERIFY * MAC_PER_FPMUL / (ver_ms * 1e-3)
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "r01_tpke_verify_pmc.json")
+        if os.path.exists(pmc):
+            with open(pmc) as fh:
+                traffic = json.load(fh).get("hbm_bytes_per_launch")
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(inp, args.cpu_seconds)
+        line = {
+            "metric": "BLS12-381 TPKE decryption-share verifications/sec (batched VerifyShare, N=22 F=7)",
+            "value": value, "unit": "share verifications/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32 (381-bit Montgomery, 12x32-bit limbs)", "data": "synthetic",
+            "config": {"workload": "configs[1]: 1M TPKE decryption shares, N=22 F=7 validators, one MI355X per rank",
+                       "shares_per_rank": n, "ciphertexts_per_rank": n_cts, "decryptors": n_dec, "degree": args.f,
+                       "v_bytes": args.vlen, "corrupted_fraction": 0.01, "parallelism": f"shard{world}",
+                       "decision_mismatches": mismatches_all},
+            "roofline": {"bound": "valu_int32", "kernel": "k_tpke_verify", "achieved": achieved / 1e12,
+                         "peak": PEAK_MAC32 / 1e12, "unit": "Tmac32/s", "frac": achieved / PEAK_MAC32,
+                         "traffic": traffic, "work_per_share_fpmul": W_VERIFY, "mac_per_fpmul": MAC_PER_FPMUL,
+                         "verify_ms": ver_ms, "prepare_ms": prep_ms},
+            "cpu_baseline": cpu,
+            "input_gen_s": t_gen,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -160,6 +160,15 @@ int lcb_tpke_verify_shares_dev(uint8_t *accept, size_t n_shares, const uint8_t *
                                const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
                                const uint32_t *dec_idx, const uint8_t *ui, void *stream);
 
+/* The two stages of lcb_tpke_verify_shares_dev, for callers that pipeline or time them separately:
+   prepare = verification-key decompression + per-ciphertext H(U||V) and Miller-line precomputation into
+   the library's device workspace; verify = the per-share pairing-product check against that workspace.
+   The workspace stays valid until the next TPKE call on this device. */
+int lcb_tpke_prepare_dev(const uint8_t *y_keys, size_t n_keys, const uint8_t *cts_u, const uint8_t *cts_w,
+                         const uint8_t *v_data, const uint32_t *v_off, size_t n_cts, void *stream);
+int lcb_tpke_verify_prepared_dev(uint8_t *accept, size_t n_shares, size_t n_keys, size_t n_cts,
+                                 const uint32_t *ct_idx, const uint32_t *dec_idx, const uint8_t *ui, void *stream);
+
 /* TPKE.PrivateKey.Decrypt for a batch (TPKE/PrivateKey.cs:21-31): status[c] = 1 and ui[c] = x*U_c when
    e(G, W_c) == e(U_c, H(U_c||V_c)), status[c] = 0 ("Invalid share!") otherwise. */
 int lcb_tpke_partial_decrypt(uint8_t *ui_out, uint8_t *status, const uint8_t x[32], const uint8_t *cts_u,

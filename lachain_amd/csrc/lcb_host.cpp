@@ -499,23 +499,45 @@ extern "C" int mclBn_G2EvaluatePolynomial(mclBnG2 *out, const mclBnG2 *c, mclSiz
 }
 
 // ================================================================== batch: TPKE
-static int tpke_verify_enqueue(uint8_t *d_accept, size_t n, const uint8_t *d_y, size_t n_keys, const uint8_t *d_u,
-                               const uint8_t *d_w, const uint8_t *d_v, const uint32_t *d_voff, size_t n_cts,
-                               const uint32_t *d_ct, const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
+static int tpke_prepare_enqueue(const uint8_t *d_y, size_t n_keys, const uint8_t *d_u, const uint8_t *d_w,
+                                const uint8_t *d_v, const uint32_t *d_voff, size_t n_cts, hipStream_t s) {
     u32 *lines = (u32 *)b_lines.get((size_t)n_cts * 2 * LCB_LINESET_BYTES);
     uint8_t *ctok = (uint8_t *)b_ctok.get(n_cts);
     void *keys = b_keys.get(n_keys * LCB_G1A_ST_BYTES);
     if (!lines || !ctok || !keys) { set_err("device allocation failed"); return -1; }
     if (n_keys) lcbk_g1_decompress(dim3(nblk(n_keys)), s, d_y, (u32)n_keys, keys);
-    if (n_cts)
-        lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), s, d_u, d_w, d_v, d_voff,
-                           (u32)n_cts, lines, ctok, g_orig_cofactor);
-    if (n)
-        lcbk_tpke_verify(dim3(nblk(n)), s, lines, ctok, keys, (u32)n_keys,
-                           d_ct, d_dec, d_ui, (u32)n, d_accept);
+    if (n_cts) lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), s, d_u, d_w, d_v, d_voff, (u32)n_cts, lines, ctok, g_orig_cofactor);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { set_err("tpke prepare launch", e); return -1; }
+    return 0;
+}
+static int tpke_verify_prepared_enqueue(uint8_t *d_accept, size_t n, size_t n_keys, size_t n_cts, const uint32_t *d_ct,
+                                        const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
+    if (b_lines.cap < (size_t)n_cts * 2 * LCB_LINESET_BYTES || b_ctok.cap < n_cts || b_keys.cap < n_keys * LCB_G1A_ST_BYTES) {
+        set_err("tpke verify: workspace not prepared for this batch");
+        return -1;
+    }
+    if (n) lcbk_tpke_verify(dim3(nblk(n)), s, (const u32 *)b_lines.p, (const uint8_t *)b_ctok.p, b_keys.p, (u32)n_keys,
+                            d_ct, d_dec, d_ui, (u32)n, d_accept);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) { set_err("tpke verify launch", e); return -1; }
     return 0;
+}
+static int tpke_verify_enqueue(uint8_t *d_accept, size_t n, const uint8_t *d_y, size_t n_keys, const uint8_t *d_u,
+                               const uint8_t *d_w, const uint8_t *d_v, const uint32_t *d_voff, size_t n_cts,
+                               const uint32_t *d_ct, const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
+    if (tpke_prepare_enqueue(d_y, n_keys, d_u, d_w, d_v, d_voff, n_cts, s)) return -1;
+    return tpke_verify_prepared_enqueue(d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, s);
+}
+extern "C" int lcb_tpke_prepare_dev(const uint8_t *y_keys, size_t n_keys, const uint8_t *cts_u, const uint8_t *cts_w,
+                                    const uint8_t *v_data, const uint32_t *v_off, size_t n_cts, void *stream) {
+    LOCKED_OR(-1)
+    return tpke_prepare_enqueue(y_keys, n_keys, cts_u, cts_w, v_data, v_off, n_cts, (hipStream_t)stream);
+}
+extern "C" int lcb_tpke_verify_prepared_dev(uint8_t *accept, size_t n, size_t n_keys, size_t n_cts, const uint32_t *ct_idx,
+                                            const uint32_t *dec_idx, const uint8_t *ui, void *stream) {
+    LOCKED_OR(-1)
+    return tpke_verify_prepared_enqueue(accept, n, n_keys, n_cts, ct_idx, dec_idx, ui, (hipStream_t)stream);
 }
 extern "C" int lcb_tpke_verify_shares_dev(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys,
                                           const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,

@@ -56,6 +56,10 @@ _SIGS = {
     "lcb_tpke_verify_shares_dev": (ctypes.c_int, [ctypes.c_void_p, c_size, ctypes.c_void_p, c_size, ctypes.c_void_p,
                                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_size,
                                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "lcb_tpke_prepare_dev": (ctypes.c_int, [ctypes.c_void_p, c_size, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, c_size, ctypes.c_void_p]),
+    "lcb_tpke_verify_prepared_dev": (ctypes.c_int, [ctypes.c_void_p, c_size, c_size, c_size, ctypes.c_void_p,
+                                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "lcb_tpke_partial_decrypt": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_u8p, c_u8p, c_u32p, c_size]),
     "lcb_tpke_encrypt_phase1": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_size]),
     "lcb_tpke_encrypt_phase2": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_u32p, c_size]),
@@ -276,6 +280,18 @@ def mul_batch(group, points, scalars, generator=False):
     _check(fn(po, pp, 1 if generator else 0, ps, n), "mul_batch")
     o = bytes(ob)
     return [o[pb * i:pb * i + pb] for i in range(n)]
+
+
+def mul_batch_raw(group, points: bytes, scalars: bytes, n: int, generator=False) -> bytes:
+    """Like mul_batch but with concatenated inputs/outputs (bulk synthetic-input generation)."""
+    keep = []
+    pb = 48 if group == 1 else 96
+    _, pp = _bytes_ptr_keep(keep, points if not generator else b"\0")
+    _, ps = _bytes_ptr_keep(keep, scalars)
+    ob, po = _out(pb * n)
+    fn = lib().lcb_g1_mul_batch if group == 1 else lib().lcb_g2_mul_batch
+    _check(fn(po, pp, 1 if generator else 0, ps, n), "mul_batch")
+    return bytes(ob)
 
 
 def g2_hash_batch(msgs):

@@ -576,6 +576,7 @@ void orc_set_g2_original_cofactor(int v) { g_orig_cofactor = v; }
     }                                                                                            \
     static void G##_neg(G *r, const G *p) { *r = *p; FNEG(&r->y, &p->y); }                       \
     static void G##_to_affine(F *x, F *y, const G *p) { /* p finite */                           \
+        if (FEQ(&p->z, &ONE)) { *x = p->x; *y = p->y; return; }                                  \
         F zi, zi2;                                                                               \
         FINV(&zi, &p->z);                                                                        \
         FSQR(&zi2, &zi);                                                                         \
@@ -985,6 +986,7 @@ static void add_step(fp2 *X, fp2 *Y, fp2 *Z, fp2 *A, fp2 *Bc, fp2 *C, const fp2 
     fp2_mul(Z, Z, &E);
 }
 /* multi-Miller loop over n pairs, shared squaring */
+static uint64_t g_line_count = 0; /* Fp-mul spent generating lines (dbl_step / add_step), instrumentation only */
 static void miller_multi(fp12 *f, const g1 *Ps, const g2 *Qs, int n) {
     fp xP[4], yP[4];
     fp2 xQ[4], yQ[4], X[4], Y[4], Z[4];
@@ -1003,14 +1005,18 @@ static void miller_multi(fp12 *f, const g1 *Ps, const g2 *Qs, int n) {
         for (int k = 0; k < n; k++) {
             if (!act[k]) continue;
             fp2 A, Bc, C;
+            uint64_t c0 = g_count;
             dbl_step(&X[k], &Y[k], &Z[k], &A, &Bc, &C, &xP[k], &yP[k]);
+            g_line_count += g_count - c0 - 4; /* the 4 evaluation muls (Bc xP, C yP) stay with the loop */
             fp12_mul_line(f, &A, &Bc, &C);
         }
         if ((Z_ABS >> i) & 1) {
             for (int k = 0; k < n; k++) {
                 if (!act[k]) continue;
                 fp2 A, Bc, C;
+                uint64_t c0 = g_count;
                 add_step(&X[k], &Y[k], &Z[k], &A, &Bc, &C, &xQ[k], &yQ[k], &xP[k], &yP[k]);
+                g_line_count += g_count - c0 - 4;
                 fp12_mul_line(f, &A, &Bc, &C);
             }
         }
@@ -1695,29 +1701,28 @@ int orc_test_sparse_line(const uint8_t fb[576], const uint8_t abc[288]) {
     fp12_mul_line_generic(&g, &A, &Bc, &C);
     return fp12_eq(&f, &g) ? 0 : 1;
 }
-/* Fp-mul counts of the canonical work units: out[0..] =
-   C_ML1, C_ML2, C_LINES, C_FE, C_H2G2, C_DEC1, C_DEC2, C_MUL1, C_MUL2 */
-int orc_count_units(uint64_t out[9]) {
+/* Fp-mul counts of the canonical work units, measured on this restatement:
+   out[0] C_ML1_EVAL  one-pair Miller loop, evaluation side only (lines precomputed)
+   out[1] C_ML2_EVAL  two-pair Miller loop with shared squarings, evaluation side only
+   out[2] C_LINES     line generation for one G2 point (63 doubling + 5 addition steps)
+   out[3] C_FE        final exponentiation (easy part incl. one Fp inversion + hard part)
+   out[4] C_H2G2      hash-and-map to G2 (SHA-512 not counted)
+   out[5] C_DEC1      G1 decompression from 48 bytes
+   out[6] C_DEC2      G2 decompression from 96 bytes
+   out[7] C_MUL1      255-bit G1 variable-base scalar multiplication (4-bit window, Jacobian)
+   out[8] C_MUL2      255-bit G2 variable-base scalar multiplication
+   out[9] C_AFF2      Jacobian -> affine conversion of a G2 point (one Fp2 inversion) */
+int orc_count_units(uint64_t out[10]) {
     orc_init();
     g1 P1 = G1_GEN, P2; g2 Q1 = G2_GEN, Q2;
     g1_dbl(&P2, &P1); g1_normalize(&P2);
     g2_dbl(&Q2, &Q1); g2_normalize(&Q2);
     g1 Ps[2] = {P1, P2}; g2 Qs[2] = {Q1, Q2};
     fp12 f, r;
-    orc_count_reset(); miller_multi(&f, Ps, Qs, 1); out[0] = orc_count_get();
-    orc_count_reset(); miller_multi(&f, Ps, Qs, 2); out[1] = orc_count_get();
-    {   /* line generation for one G2 point, without evaluation at P */
-        fp xP = FP_ONE_M, yP = FP_ONE_M;
-        fp2 X = Q1.x, Y = Q1.y, Z = FP2_ONE, A, Bc, C;
-        uint64_t c = 0;
-        for (int i = 62; i >= 0; i--) {
-            orc_count_reset(); dbl_step(&X, &Y, &Z, &A, &Bc, &C, &xP, &yP); c += orc_count_get() - 4;
-            if ((Z_ABS >> i) & 1) {
-                orc_count_reset(); add_step(&X, &Y, &Z, &A, &Bc, &C, &Q1.x, &Q1.y, &xP, &yP); c += orc_count_get() - 4;
-            }
-        }
-        out[2] = c;
-    }
+    orc_count_reset(); g_line_count = 0; miller_multi(&f, Ps, Qs, 1);
+    out[2] = g_line_count; out[0] = orc_count_get() - g_line_count;
+    orc_count_reset(); g_line_count = 0; miller_multi(&f, Ps, Qs, 2);
+    out[1] = orc_count_get() - g_line_count;
     orc_count_reset(); final_exp(&r, &f); out[3] = orc_count_get();
     g2 h; orc_count_reset(); g2_hash(&h, (const uint8_t *)"lachain", 7); out[4] = orc_count_get();
     uint8_t b1[48], b2[96]; g1_ser(b1, &P2); g2_ser(b2, &Q2);
@@ -1728,6 +1733,7 @@ int orc_count_units(uint64_t out[9]) {
     fr_from_int(&s, sv);
     orc_count_reset(); g1_mul_fr(&d1, &P2, &s); out[7] = orc_count_get();
     orc_count_reset(); g2_mul_fr(&d2, &Q2, &s); out[8] = orc_count_get();
+    fp2 ax, ay; orc_count_reset(); g2_to_affine(&ax, &ay, &d2); out[9] = orc_count_get();
     g_counting = 0;
     return 0;
 }
