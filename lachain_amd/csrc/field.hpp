@@ -15,7 +15,7 @@
 #include <stdint.h>
 
 #include "bls_constants.hpp"
-#include "fp_mul_gen.hpp"
+#include "asm_routines.hpp"
 
 typedef uint32_t u32;
 typedef uint64_t u64;
@@ -100,19 +100,6 @@ DI void fp_neg(fp &r, const fp &a) {
     fp_sub(r, z, a);
 }
 
-DN u32x12 lcb_fp_mul_v(u32x12 a, u32x12 b) {
-    u32x12 r;
-    LCB_FP_MUL_BODY(a, b, r)
-    u32x12 d;
-    u32 br = 0;
-#pragma unroll
-    for (int j = 0; j < 12; j++) {
-        u64 x = (u64)r[j] - LCB_P[j] - br;
-        d[j] = (u32)x;
-        br = (u32)(x >> 32) & 1;
-    }
-    return br ? r : d;
-}
 DI u32x12 fp_to_v(const fp &a) {
     u32x12 v;
 #pragma unroll
@@ -125,7 +112,7 @@ DI fp fp_from_v(const u32x12 &v) {
     for (int j = 0; j < 12; j++) a.v[j] = v[j];
     return a;
 }
-DI void fp_mul(fp &r, const fp &a, const fp &b) { r = fp_from_v(lcb_fp_mul_v(fp_to_v(a), fp_to_v(b))); }
+DI void fp_mul(fp &r, const fp &a, const fp &b) { r = fp_from_v(lcb_asm_fp_mul(fp_to_v(a), fp_to_v(b))); }
 DI void fp_sqr(fp &r, const fp &a) { fp_mul(r, a, a); }
 
 // conversions between canonical integers (12 LE limbs) and Montgomery form
@@ -160,8 +147,8 @@ DN u32x12 lcb_fp_pow_v(u32x12 av, const u32 *e) {
     while (top > 0 && !((e[top >> 5] >> (top & 31)) & 1)) top--;
     u32x12 acc = av;
     for (int i = top - 1; i >= 0; i--) {
-        acc = lcb_fp_mul_v(acc, acc);
-        if ((e[i >> 5] >> (i & 31)) & 1) acc = lcb_fp_mul_v(acc, av);
+        acc = lcb_asm_fp_mul(acc, acc);
+        if ((e[i >> 5] >> (i & 31)) & 1) acc = lcb_asm_fp_mul(acc, av);
     }
     return acc;
 }
@@ -194,26 +181,33 @@ DI bool fp2_eq(const fp2 &x, const fp2 &y) { return fp_eq(x.a, y.a) && fp_eq(x.b
 DI fp2 fp2_zero() { fp2 r; r.a = fp_zero(); r.b = fp_zero(); return r; }
 DI fp2 fp2_one() { fp2 r; r.a = fp_one(); r.b = fp_zero(); return r; }
 DI void fp2_load_const(fp2 &r, const u32 *c) { fp_load_const(r.a, c); fp_load_const(r.b, c + 12); }
+// Fp2 products go to the hand-scheduled assembly routines (tools/gen_asm.py): 3 (mul) or 2 (sqr, mul_fp)
+// independent Montgomery chains interleaved in one call.
 DI void fp2_mul(fp2 &r, const fp2 &x, const fp2 &y) {
-    fp t0, t1, t2, t3;
-    fp_mul(t0, x.a, y.a);
-    fp_mul(t1, x.b, y.b);
-    fp_add(t2, x.a, x.b);
-    fp_add(t3, y.a, y.b);
-    fp_mul(t2, t2, t3);
-    fp_sub(r.a, t0, t1);
-    fp_sub(t2, t2, t0);
-    fp_sub(r.b, t2, t1);
+    u32x12 xa = fp_to_v(x.a), xb = fp_to_v(x.b);
+    lcb_asm_fp2_mul(xa, xb, fp_to_v(y.a), fp_to_v(y.b));
+    r.a = fp_from_v(xa);
+    r.b = fp_from_v(xb);
 }
 DI void fp2_sqr(fp2 &r, const fp2 &x) {
-    fp t0, t1, t2;
-    fp_add(t0, x.a, x.b);
-    fp_sub(t1, x.a, x.b);
-    fp_mul(t2, x.a, x.b);
-    fp_mul(r.a, t0, t1);
-    fp_add(r.b, t2, t2);
+    u32x12 xa = fp_to_v(x.a), xb = fp_to_v(x.b);
+    lcb_asm_fp2_sqr(xa, xb);
+    r.a = fp_from_v(xa);
+    r.b = fp_from_v(xb);
 }
-DI void fp2_mul_fp(fp2 &r, const fp2 &x, const fp &s) { fp_mul(r.a, x.a, s); fp_mul(r.b, x.b, s); }
+DI void fp2_mul_fp(fp2 &r, const fp2 &x, const fp &s) {
+    u32x12 xa = fp_to_v(x.a), xb = fp_to_v(x.b);
+    lcb_asm_fp2_mul_fp(xa, xb, fp_to_v(s));
+    r.a = fp_from_v(xa);
+    r.b = fp_from_v(xb);
+}
+// two independent Fp products in one call
+DI void fp_mul2(fp &r0, const fp &a0, const fp &b0, fp &r1, const fp &a1, const fp &b1) {
+    u32x12 x0 = fp_to_v(a0), x1 = fp_to_v(a1);
+    lcb_asm_fp_mul2(x0, fp_to_v(b0), x1, fp_to_v(b1));
+    r0 = fp_from_v(x0);
+    r1 = fp_from_v(x1);
+}
 DI void fp2_mul_xi(fp2 &r, const fp2 &x) { // (a + b i)(1 + i) = (a - b) + (a + b) i
     fp t;
     fp_sub(t, x.a, x.b);
@@ -221,18 +215,18 @@ DI void fp2_mul_xi(fp2 &r, const fp2 &x) { // (a + b i)(1 + i) = (a - b) + (a + 
     r.a = t;
 }
 DI void fp2_norm(fp &r, const fp2 &x) {
-    fp t;
-    fp_sqr(r, x.a);
-    fp_sqr(t, x.b);
-    fp_add(r, r, t);
+    fp t, u;
+    fp_mul2(u, x.a, x.a, t, x.b, x.b);
+    fp_add(r, u, t);
 }
 DI void fp2_inv(fp2 &r, const fp2 &x) {
     fp n;
     fp2_norm(n, x);
     fp_inv(n, n);
-    fp_mul(r.a, x.a, n);
-    fp_mul(r.b, x.b, n);
-    fp_neg(r.b, r.b);
+    fp2 t;
+    fp2_mul_fp(t, x, n);
+    r.a = t.a;
+    fp_neg(r.b, t.b);
 }
 // mcl Fp2T::squareRoot (norm method; root choice reproduced exactly)
 DI bool fp2_sqrt(fp2 &y, const fp2 &x) {

@@ -1,6 +1,8 @@
 // lachain_amd/csrc/k_lagrange.hip — gfx950 kernels: Lagrange interpolation at 0 and MSM.
 #include "kcommon.hpp"
 
+LCB_ASM_LIBRARY(k_lagrange)
+
 // ================================================================================= Lagrange at 0
 // lambda_i = prod_{j != i} x_j / (x_j - x_i) (mcl: a = prod x_j, b_i = x_i prod_{j!=i}(x_j - x_i),
 // lambda_i = a / b_i); one lane per problem; writes canonical raw lambdas and a status byte.
@@ -145,7 +147,7 @@ extern "C" __global__ void LCB_BOUNDS k_g1_reduce_pairs(g1 *v, u32 n_half, u32 n
     u32 j = i + n_half;
     if (j < n) jac_add(v[i], v[i], v[j]);
 }
-extern "C" __global__ void k_g1_finish(const g1 *v, uint8_t *out) {
+extern "C" __global__ void LCB_BOUNDS k_g1_finish(const g1 *v, uint8_t *out) {
     if (threadIdx.x == 0 && blockIdx.x == 0) g1_compress_jac(out, v[0]);
 }
 

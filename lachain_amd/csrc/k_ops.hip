@@ -1,6 +1,8 @@
 // lachain_amd/csrc/k_ops.hip — gfx950 kernels: single mcl-shaped operations.
 #include "kcommon.hpp"
 
+LCB_ASM_LIBRARY(k_ops)
+
 // ================================================================================= single operations
 // One lane executes one mcl-shaped operation on mcl-layout structs held in `io` (u32 words).
 DI bool g1_on_curve(const g1 &p) { // Jacobian: Y^2 = X^3 + 4 Z^6
@@ -47,7 +49,7 @@ template <class G> DI bool jac_eq(const G &p, const G &q) {
     f_mul(s2, s2, z1z1);
     return f_eq(u1, u2) && f_eq(s1, s2);
 }
-extern "C" __global__ void k_op(int op, u32 *io, int orig_cof) {
+extern "C" __global__ void LCB_BOUNDS k_op(int op, u32 *io, int orig_cof) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     switch (op) {
     // ---- Fr: io[0..8) = out, io[8..16) = x, io[16..24) = y (mclBnFr layout = 8 u32 Montgomery)

@@ -1,6 +1,8 @@
 // lachain_amd/csrc/k_scalar.hip — gfx950 kernels: scalar multiplication, hash-to-G2, TPKE encrypt, HashAndSign.
 #include "kcommon.hpp"
 
+LCB_ASM_LIBRARY(k_scalar)
+
 // ================================================================================= scalar multiplication
 // out[i] = s_i * P_i (or s_i * generator), serialized; scalars are canonical 32-byte LE (< r checked)
 extern "C" __global__ void LCB_BOUNDS k_g1_mul(const uint8_t *pts, int use_gen, const uint8_t *scalars, u32 n,

@@ -1,6 +1,8 @@
 // lachain_amd/csrc/k_tpke.hip — gfx950 kernels: TPKE decryption-share pipeline (decompression, per-ciphertext preparation, per-share verification, partial decryption).
 #include "kcommon.hpp"
 
+LCB_ASM_LIBRARY(k_tpke)
+
 // ================================================================================= decompression
 extern "C" __global__ void LCB_BOUNDS k_g1_decompress(const uint8_t *in, u32 n, g1a_st *out) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;

@@ -1,6 +1,8 @@
 // lachain_amd/csrc/k_ts.hip — gfx950 kernels: threshold-signature share verification.
 #include "kcommon.hpp"
 
+LCB_ASM_LIBRARY(k_ts)
+
 // ================================================================================= threshold signatures
 extern "C" __global__ void LCB_BOUNDS k_ts_msg_prepare(const uint8_t *msg_data, const u32 *msg_off, u32 n_msgs,
                                                       u32 *lines, uint8_t *msg_ok, int orig_cof) {

@@ -197,9 +197,10 @@ DN void fe_easy(fp12 &r, const fp12 &f) {
 // x^z for unitary x (z = -|z|): cyclotomic square-and-multiply over |z|, then conjugate
 DN void cyc_pow_z(fp12 &r, const fp12 &x) {
     fp12 acc = x;
+    fp12 base = x; // kept in registers for the whole loop (the squaring chain never touches memory)
     for (int i = 62; i >= 0; i--) {
         fp12_cyc_sqr(acc, acc);
-        if ((LCB_Z_ABS >> i) & 1) fp12_mul_n(acc, acc, x);
+        if ((LCB_Z_ABS >> i) & 1) fp12_mul(acc, acc, base);
     }
     fp12_conj(r, acc);
 }

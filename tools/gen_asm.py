@@ -1,0 +1,334 @@
+#!/usr/bin/env python3
+"""tools/gen_asm.py — emits lachain_amd/csrc/asm_routines.hpp: hand-scheduled gfx950 assembly leaf
+routines for the hot field arithmetic, with a custom register calling convention, plus the HIP wrappers
+that call them.
+
+Why: the pairing runs one lane per share with ~400 live VGPRs (one wave per SIMD).  A compiler-built
+Montgomery multiply is a single dependent MAC chain (each v_mad_u64_u32 waits ~12 cycles for the previous
+one: profiles/r01_valu_rates.jsonl), and passing Fp2 operands to a non-inlined function goes through
+scratch (the AMDGPU ABI passes aggregates >16 registers in memory).  These routines instead take their
+operands in fixed VGPRs (v0..), interleave 2-3 independent Montgomery products column by column
+(product-scanning / FIPS Montgomery, 12x32-bit limbs, R = 2^384) so consecutive MACs are independent,
+and give each product chain its own SGPR carry pair.  Callers reach them with `s_swappc_b64` from inline
+asm whose register-tuple constraints and clobber list tell the compiler exactly which registers move.
+
+Per MAC: `v_mad_u64_u32 acc, s[c], x, y, acc` (half rate) + `v_addc_co_u32 hi, s[c], 0, hi, s[c]`.
+Modulus limbs live in VGPRs inside a routine (GFX9 VOP3 reads at most one SGPR per instruction).
+All routine outputs are fully reduced (< p); unreduced Karatsuba sums (< 2p) are valid multiplicands
+because R > 4p.
+
+Routines (label: inputs -> outputs, all 12-limb little-endian Montgomery):
+  lcb_r_fp_mul      v[0:11]=a, v[12:23]=b                 -> v[0:11]=a*b
+  lcb_r_fp_mul2     v[0:11]=a0, v[12:23]=b0, v[24:35]=a1, v[36:47]=b1 -> v[0:11]=a0*b0, v[24:35]=a1*b1
+  lcb_r_fp2_mul     v[0:23]=x, v[24:47]=y                 -> v[0:23]=x*y   (Karatsuba, 3 chains)
+  lcb_r_fp2_sqr     v[0:23]=x                             -> v[0:23]=x^2   ((a+b)(a-b), 2ab: 2 chains)
+  lcb_r_fp2_mul_fp  v[0:23]=x, v[24:35]=s                 -> v[0:23]=x*s   (2 chains)
+"""
+import os
+
+P = 0x1A0111EA397FE69A4B1BA7B6434BACD764774B84F38512BF6730D2A0F6B0F6241EABFFFEB153FFFFB9FEFFFFFFFFAAAB
+N = 12
+PINV = (-pow(P, -1, 1 << 32)) % (1 << 32)
+PL = [(P >> (32 * i)) & 0xFFFFFFFF for i in range(N)]
+
+S_PINV = 88
+CARRY = [90, 92, 94]          # per-chain carry SGPR pairs
+S_TMP = 96                    # scratch carry pair for add/sub chains (s[96:97])
+S_TMP2 = 98                   # second scratch pair (s[98:99])
+CLOBBER_SGPRS = [30, 31, S_PINV] + [c + d for c in CARRY for d in (0, 1)] + [S_TMP, S_TMP + 1, S_TMP2, S_TMP2 + 1]
+
+
+def v(i):
+    return f"v{i}"
+
+
+def vr(base):
+    return [base + j for j in range(N)]
+
+
+class Asm:
+    def __init__(self):
+        self.lines = []
+
+    def __call__(self, s):
+        self.lines.append("  " + s)
+
+    def label(self, name):
+        self.lines.append(f"{name}:")
+
+    def text(self):
+        return "\n".join(self.lines)
+
+
+def load_p(a, pbase):
+    for j in range(N):
+        a(f"v_mov_b32 v{pbase + j}, 0x{PL[j]:08x}")
+    a(f"s_mov_b32 s{S_PINV}, 0x{PINV:08x}")
+
+
+def products(a, chains, pbase):
+    """chains: list of dict(a=[12 regs], b=[12 regs], m=[12 regs], acc=even reg, out=[12 regs]).
+    out[j] may alias a[j] (written after a[j]'s last use).  Results are in [0, 2p) (not yet reduced)."""
+    q = len(chains)
+    for c in chains:
+        acc = c["acc"]
+        a(f"v_mov_b32 v{acc}, 0")
+        a(f"v_mov_b32 v{acc + 1}, 0")
+        a(f"v_mov_b32 v{acc + 2}, 0")
+    for k in range(2 * N - 1):
+        lo = 0 if k < N else k - (N - 1)
+        up = k if k < N else N - 1
+        terms = []
+        for i in range(lo, up + 1):
+            terms.append(("ab", i, k - i))
+            if i < k:
+                terms.append(("mp", i, k - i))
+        for (kind, i, j) in terms:
+            for t, c in enumerate(chains):
+                x = c["a"][i] if kind == "ab" else c["m"][i]
+                y = c["b"][j] if kind == "ab" else pbase + j
+                acc = c["acc"]
+                a(f"v_mad_u64_u32 v[{acc}:{acc + 1}], s[{CARRY[t]}:{CARRY[t] + 1}], v{x}, v{y}, v[{acc}:{acc + 1}]")
+            for t, c in enumerate(chains):
+                acc = c["acc"]
+                a(f"v_addc_co_u32_e64 v{acc + 2}, s[{CARRY[t]}:{CARRY[t] + 1}], 0, v{acc + 2}, s[{CARRY[t]}:{CARRY[t] + 1}]")
+        if k < N:
+            for t, c in enumerate(chains):
+                a(f"v_mul_lo_u32 v{c['m'][k]}, v{c['acc']}, s{S_PINV}")
+            for t, c in enumerate(chains):
+                acc = c["acc"]
+                a(f"v_mad_u64_u32 v[{acc}:{acc + 1}], s[{CARRY[t]}:{CARRY[t] + 1}], v{c['m'][k]}, v{pbase}, v[{acc}:{acc + 1}]")
+            for t, c in enumerate(chains):
+                acc = c["acc"]
+                a(f"v_addc_co_u32_e64 v{acc + 2}, s[{CARRY[t]}:{CARRY[t] + 1}], 0, v{acc + 2}, s[{CARRY[t]}:{CARRY[t] + 1}]")
+        else:
+            for c in chains:
+                a(f"v_mov_b32 v{c['out'][k - N]}, v{c['acc']}")
+        for c in chains:
+            acc = c["acc"]
+            a(f"v_mov_b32 v{acc}, v{acc + 1}")
+            a(f"v_mov_b32 v{acc + 1}, v{acc + 2}")
+            a(f"v_mov_b32 v{acc + 2}, 0")
+    for c in chains:
+        a(f"v_mov_b32 v{c['out'][N - 1]}, v{c['acc']}")
+
+
+def reduce_once(a, r, tmp, pbase, sc=S_TMP):
+    """r <- r - p if r >= p (r < 2p).  tmp: 12 scratch VGPRs."""
+    a(f"v_sub_co_u32_e64 v{tmp[0]}, s[{sc}:{sc + 1}], v{r[0]}, v{pbase}")
+    for j in range(1, N):
+        a(f"v_subb_co_u32_e64 v{tmp[j]}, s[{sc}:{sc + 1}], v{r[j]}, v{pbase + j}, s[{sc}:{sc + 1}]")
+    for j in range(N):
+        a(f"v_cndmask_b32_e64 v{r[j]}, v{tmp[j]}, v{r[j]}, s[{sc}:{sc + 1}]")
+
+
+def add_unreduced(a, r, x, y, sc=S_TMP):
+    """r <- x + y (no reduction; x, y < p so r < 2p < 2^382)."""
+    a(f"v_add_co_u32_e64 v{r[0]}, s[{sc}:{sc + 1}], v{x[0]}, v{y[0]}")
+    for j in range(1, N):
+        a(f"v_addc_co_u32_e64 v{r[j]}, s[{sc}:{sc + 1}], v{x[j]}, v{y[j]}, s[{sc}:{sc + 1}]")
+
+
+def sub_plus_p(a, r, x, y, pbase, sc=S_TMP):
+    """r <- x - y + p (no reduction; in (0, 2p) for x, y < p)."""
+    a(f"v_sub_co_u32_e64 v{r[0]}, s[{sc}:{sc + 1}], v{x[0]}, v{y[0]}")
+    for j in range(1, N):
+        a(f"v_subb_co_u32_e64 v{r[j]}, s[{sc}:{sc + 1}], v{x[j]}, v{y[j]}, s[{sc}:{sc + 1}]")
+    a(f"v_add_co_u32_e64 v{r[0]}, s[{sc}:{sc + 1}], v{r[0]}, v{pbase}")
+    for j in range(1, N):
+        a(f"v_addc_co_u32_e64 v{r[j]}, s[{sc}:{sc + 1}], v{r[j]}, v{pbase + j}, s[{sc}:{sc + 1}]")
+
+
+def sub_mod(a, r, x, y, tmp, pbase):
+    """r <- x - y mod p (x, y < p); r may alias x or y."""
+    sc, sc2 = S_TMP, S_TMP2
+    a(f"v_sub_co_u32_e64 v{tmp[0]}, s[{sc}:{sc + 1}], v{x[0]}, v{y[0]}")
+    for j in range(1, N):
+        a(f"v_subb_co_u32_e64 v{tmp[j]}, s[{sc}:{sc + 1}], v{x[j]}, v{y[j]}, s[{sc}:{sc + 1}]")
+    # r = borrow ? tmp + p : tmp
+    a(f"v_add_co_u32_e64 v{r[0]}, s[{sc2}:{sc2 + 1}], v{tmp[0]}, v{pbase}")
+    for j in range(1, N):
+        a(f"v_addc_co_u32_e64 v{r[j]}, s[{sc2}:{sc2 + 1}], v{tmp[j]}, v{pbase + j}, s[{sc2}:{sc2 + 1}]")
+    for j in range(N):
+        a(f"v_cndmask_b32_e64 v{r[j]}, v{tmp[j]}, v{r[j]}, s[{sc}:{sc + 1}]")
+
+
+def add_mod(a, r, x, y, tmp, pbase):
+    """r <- x + y mod p (x, y < p)."""
+    add_unreduced(a, r, x, y)
+    reduce_once(a, r, tmp, pbase)
+
+
+def mov(a, dst, src):
+    for j in range(N):
+        a(f"v_mov_b32 v{dst[j]}, v{src[j]}")
+
+
+# ------------------------------------------------------------------ routines
+def r_fp_mul():
+    a = Asm()
+    a.label("lcb_r_fp_mul")
+    P_ = 40
+    load_p(a, P_)
+    A, B, M = vr(0), vr(12), vr(24)
+    products(a, [dict(a=A, b=B, m=M, acc=36, out=A)], P_)
+    reduce_once(a, A, M, P_)
+    a("s_setpc_b64 s[30:31]")
+    return a.text(), 52
+
+
+def r_fp_mul2():
+    a = Asm()
+    a.label("lcb_r_fp_mul2")
+    P_ = 80
+    load_p(a, P_)
+    A0, B0, A1, B1, M0, M1 = vr(0), vr(12), vr(24), vr(36), vr(48), vr(60)
+    products(a, [dict(a=A0, b=B0, m=M0, acc=72, out=A0), dict(a=A1, b=B1, m=M1, acc=76, out=A1)], P_)
+    reduce_once(a, A0, M0, P_)
+    reduce_once(a, A1, M1, P_)
+    a("s_setpc_b64 s[30:31]")
+    return a.text(), 92
+
+
+def r_fp2_mul():
+    a = Asm()
+    a.label("lcb_r_fp2_mul")
+    P_ = 120
+    load_p(a, P_)
+    XA, XB, YA, YB, SA, SB = vr(0), vr(12), vr(24), vr(36), vr(48), vr(60)
+    M0, M1, M2 = vr(72), vr(84), vr(96)
+    add_unreduced(a, SA, XA, XB)
+    add_unreduced(a, SB, YA, YB)
+    products(a, [dict(a=XA, b=YA, m=M0, acc=108, out=XA),
+                 dict(a=XB, b=YB, m=M1, acc=112, out=XB),
+                 dict(a=SA, b=SB, m=M2, acc=116, out=SA)], P_)
+    reduce_once(a, XA, M0, P_)        # t0 = xa*ya
+    reduce_once(a, XB, M1, P_)        # t1 = xb*yb
+    reduce_once(a, SA, M2, P_)        # t2 = (xa+xb)(ya+yb)
+    sub_mod(a, YA, SA, XA, M0, P_)    # u = t2 - t0
+    sub_mod(a, YA, YA, XB, M1, P_)    # u = t2 - t0 - t1  (= r.b)
+    sub_mod(a, XA, XA, XB, M2, P_)    # r.a = t0 - t1
+    mov(a, XB, YA)
+    a("s_setpc_b64 s[30:31]")
+    return a.text(), 132
+
+
+def r_fp2_sqr():
+    a = Asm()
+    a.label("lcb_r_fp2_sqr")
+    P_ = 80
+    load_p(a, P_)
+    XA, XB, S, D, M0, M1 = vr(0), vr(12), vr(24), vr(36), vr(48), vr(60)
+    add_unreduced(a, S, XA, XB)       # a + b   (< 2p)
+    sub_plus_p(a, D, XA, XB, P_)      # a - b + p (< 2p)
+    products(a, [dict(a=S, b=D, m=M0, acc=72, out=S),
+                 dict(a=XA, b=XB, m=M1, acc=76, out=XA)], P_)
+    reduce_once(a, S, M0, P_)         # r.a = a^2 - b^2
+    reduce_once(a, XA, M1, P_)        # ab
+    add_mod(a, XB, XA, XA, M1, P_)    # r.b = 2ab
+    mov(a, XA, S)
+    a("s_setpc_b64 s[30:31]")
+    return a.text(), 92
+
+
+def r_fp2_mul_fp():
+    a = Asm()
+    a.label("lcb_r_fp2_mul_fp")
+    P_ = 80
+    load_p(a, P_)
+    XA, XB, S, M0, M1 = vr(0), vr(12), vr(24), vr(36), vr(48)
+    products(a, [dict(a=XA, b=S, m=M0, acc=72, out=XA), dict(a=XB, b=S, m=M1, acc=76, out=XB)], P_)
+    reduce_once(a, XA, M0, P_)
+    reduce_once(a, XB, M1, P_)
+    a("s_setpc_b64 s[30:31]")
+    return a.text(), 92
+
+
+ROUTINES = [r_fp_mul, r_fp_mul2, r_fp2_mul, r_fp2_sqr, r_fp2_mul_fp]
+
+
+def clobber_list(nvgpr, keep):
+    regs = [f'"v{i}"' for i in range(nvgpr) if i not in keep]
+    regs += [f'"s{s}"' for s in CLOBBER_SGPRS]
+    return ", ".join(regs)
+
+
+def call_seq(label):
+    return (f'"s_getpc_b64 s[{S_TMP}:{S_TMP + 1}]\\n\\t"\n'
+            f'        "s_add_u32 s{S_TMP}, s{S_TMP}, {label}@rel32@lo+4\\n\\t"\n'
+            f'        "s_addc_u32 s{S_TMP + 1}, s{S_TMP + 1}, {label}@rel32@hi+12\\n\\t"\n'
+            f'        "s_swappc_b64 s[30:31], s[{S_TMP}:{S_TMP + 1}]"')
+
+
+def emit():
+    bodies = []
+    nv = {}
+    for fn in ROUTINES:
+        txt, n = fn()
+        bodies.append(txt)
+        nv[fn.__name__] = n
+    lib = "\n".join(["  .p2align 8\n" + b for b in bodies])
+    out = []
+    out.append("// GENERATED by tools/gen_asm.py — do not edit.\n")
+    out.append("// gfx950 assembly leaf routines with a register calling convention (see the generator's docstring).\n")
+    out.append("#pragma once\n#include <hip/hip_runtime.h>\n#include <stdint.h>\n\n")
+    out.append("typedef uint32_t u32;\ntypedef u32 u32x12 __attribute__((ext_vector_type(12)));\n\n")
+    # library kernel (one per translation unit; never launched, it only hosts the routines' code)
+    out.append("#define LCB_ASM_LIBRARY(tag) \\\n")
+    out.append("extern \"C\" __global__ void __launch_bounds__(64) lcb_asm_library_##tag() { \\\n")
+    out.append("    asm volatile(LCB_ASM_LIBRARY_TEXT); \\\n}\n\n")
+    esc = lib.replace("\\", "\\\\").replace('"', '\\"')
+    out.append("#define LCB_ASM_LIBRARY_TEXT \\\n    \"  s_endpgm\\n\" \\\n")
+    for line in esc.split("\n"):
+        out.append(f'    "{line}\\n" \\\n')
+    out.append('    ""\n\n')
+    # wrappers
+    out.append(f"""// r = a*b
+__device__ __forceinline__ u32x12 lcb_asm_fp_mul(u32x12 a, u32x12 b) {{
+    asm({call_seq("lcb_r_fp_mul")}
+        : "+{{v[0:11]}}"(a), "+{{v[12:23]}}"(b)
+        :
+        : {clobber_list(nv['r_fp_mul'], set(range(24)))});
+    return a;
+}}
+// (a0*b0, a1*b1)
+__device__ __forceinline__ void lcb_asm_fp_mul2(u32x12 &a0, u32x12 b0, u32x12 &a1, u32x12 b1) {{
+    asm({call_seq("lcb_r_fp_mul2")}
+        : "+{{v[0:11]}}"(a0), "+{{v[12:23]}}"(b0), "+{{v[24:35]}}"(a1), "+{{v[36:47]}}"(b1)
+        :
+        : {clobber_list(nv['r_fp_mul2'], set(range(48)))});
+}}
+// x*y in Fp2: (xa, xb) <- (xa, xb) * (ya, yb)
+__device__ __forceinline__ void lcb_asm_fp2_mul(u32x12 &xa, u32x12 &xb, u32x12 ya, u32x12 yb) {{
+    asm({call_seq("lcb_r_fp2_mul")}
+        : "+{{v[0:11]}}"(xa), "+{{v[12:23]}}"(xb), "+{{v[24:35]}}"(ya), "+{{v[36:47]}}"(yb)
+        :
+        : {clobber_list(nv['r_fp2_mul'], set(range(48)))});
+}}
+// x^2 in Fp2
+__device__ __forceinline__ void lcb_asm_fp2_sqr(u32x12 &xa, u32x12 &xb) {{
+    asm({call_seq("lcb_r_fp2_sqr")}
+        : "+{{v[0:11]}}"(xa), "+{{v[12:23]}}"(xb)
+        :
+        : {clobber_list(nv['r_fp2_sqr'], set(range(24)))});
+}}
+// x*s for x in Fp2, s in Fp
+__device__ __forceinline__ void lcb_asm_fp2_mul_fp(u32x12 &xa, u32x12 &xb, u32x12 s) {{
+    asm({call_seq("lcb_r_fp2_mul_fp")}
+        : "+{{v[0:11]}}"(xa), "+{{v[12:23]}}"(xb), "+{{v[24:35]}}"(s)
+        :
+        : {clobber_list(nv['r_fp2_mul_fp'], set(range(36)))});
+}}
+""")
+    return "".join(out)
+
+
+def main():
+    dst = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "lachain_amd", "csrc", "asm_routines.hpp")
+    with open(dst, "w") as f:
+        f.write(emit())
+    print("wrote", os.path.normpath(dst))
+
+
+if __name__ == "__main__":
+    main()
