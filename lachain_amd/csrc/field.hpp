@@ -63,7 +63,7 @@ DI void fp_reduce_once(fp &r, const fp &t) {
 #pragma unroll
     for (int j = 0; j < 12; j++) r.v[j] = br ? t.v[j] : d[j];
 }
-DI void fp_add(fp &r, const fp &a, const fp &b) {
+DI void fp_add_c(fp &r, const fp &a, const fp &b) {
     fp t;
     u32 c = 0;
 #pragma unroll
@@ -74,8 +74,7 @@ DI void fp_add(fp &r, const fp &a, const fp &b) {
     }
     fp_reduce_once(r, t); // a + b < 2p < 2^382: no carry out of limb 11
 }
-DI void fp_dbl(fp &r, const fp &a) { fp_add(r, a, a); }
-DI void fp_sub(fp &r, const fp &a, const fp &b) {
+DI void fp_sub_c(fp &r, const fp &a, const fp &b) {
     fp t;
     u32 br = 0;
 #pragma unroll
@@ -95,10 +94,28 @@ DI void fp_sub(fp &r, const fp &a, const fp &b) {
 #pragma unroll
     for (int j = 0; j < 12; j++) r.v[j] = br ? d.v[j] : t.v[j];
 }
-DI void fp_neg(fp &r, const fp &a) {
+DI void fp_neg_c(fp &r, const fp &a) {
     fp z = fp_zero();
-    fp_sub(r, z, a);
+    fp_sub_c(r, z, a);
 }
+#ifndef LCB_C_ADD
+DI void fp_add(fp &r, const fp &a, const fp &b) { lcb_fp_add_asm(r.v, a.v, b.v); }  // 36-instruction VCC chain
+#else
+DI void fp_add(fp &r, const fp &a, const fp &b) { fp_add_c(r, a, b); }
+#endif
+// r = a + b without reduction (< 2p): only as a Montgomery multiplicand (R > 4p)
+DI void fp_add_nr(fp &r, const fp &a, const fp &b) { lcb_fp_add_nr_asm(r.v, a.v, b.v); }
+DI void fp_dbl(fp &r, const fp &a) { fp_add(r, a, a); }
+#ifndef LCB_C_SUB
+DI void fp_sub(fp &r, const fp &a, const fp &b) { lcb_fp_sub_asm(r.v, a.v, b.v); }
+#else
+DI void fp_sub(fp &r, const fp &a, const fp &b) { fp_sub_c(r, a, b); }
+#endif
+#ifndef LCB_C_NEG
+DI void fp_neg(fp &r, const fp &a) { lcb_fp_neg_asm(r.v, a.v); }
+#else
+DI void fp_neg(fp &r, const fp &a) { fp_neg_c(r, a); }
+#endif
 
 DI u32x12 fp_to_v(const fp &a) {
     u32x12 v;

@@ -153,6 +153,26 @@ extern "C" __global__ void LCB_BOUNDS k_op(int op, u32 *io, int orig_cof) {
     }
     case OP_G1_GEN: { g1a a; g1_generator(a); jac_from_aff(*(g1 *)io, a); break; }
     case OP_G2_GEN: { g2a a; g2_generator(a); jac_from_aff(*(g2 *)io, a); break; }
+    case OP_DEBUG_FP12: {
+        fp12 a = *(fp12 *)(io + 252), r = a;
+        switch (io[548]) {
+        case 0: fp12_inv_n(r, a); break;
+        case 1: fp12_cyc_sqr_n(r, a); break;
+        case 2: fp12_frob1_n(r, a); break;
+        case 3: fp12_frob2_n(r, a); break;
+        case 4: fp12_frob3_n(r, a); break;
+        case 5: fe_easy(r, a); break;
+        case 6: cyc_pow_z(r, a); break;
+        case 7: fp12_sqr_n(r, a); break;
+        case 8: fp6_inv(r.c0, a.c0); break;
+        case 9: fp2_inv_n(r.c0.c0, a.c0.c0); break;
+        case 10: fp12_conj(r, a); break;
+        case 11: fe_hard(r, a); break;
+        default: break;
+        }
+        *(fp12 *)io = r;
+        break;
+    }
     default: break;
     }
 }

@@ -376,6 +376,15 @@ extern "C" void mclBn_millerLoopVec(mclBnGT *z, const mclBnG1 *x, const mclBnG2 
     }
     *z = acc;
 }
+// debug-only (not in include/lachain_bls.h): apply tower routine `which` (k_ops.hip OP_DEBUG_FP12) to raw GT words
+extern "C" int lcb_debug_fp12(int which, const uint32_t in[144], uint32_t out[144]) {
+    LOCKED_OR(-1)
+    memcpy(g_io_host + 252, in, 576);
+    g_io_host[548] = (u32)which;
+    if (!run_op(OP_DEBUG_FP12, 549, 144)) return -1;
+    memcpy(out, g_io_host, 576);
+    return 0;
+}
 extern "C" void mclBn_finalExp(mclBnGT *y, const mclBnGT *x) { gt_op(OP_FINAL_EXP, y, x, nullptr, nullptr); }
 extern "C" void mclBnGT_mul(mclBnGT *z, const mclBnGT *x, const mclBnGT *y) { gt_op(OP_GT_MUL, z, x, y, nullptr); }
 extern "C" void mclBnGT_pow(mclBnGT *z, const mclBnGT *x, const mclBnFr *y) { gt_op(OP_GT_POW, z, x, nullptr, y); }

@@ -250,7 +250,8 @@ ROUTINES = [r_fp_mul, r_fp_mul2, r_fp2_mul, r_fp2_sqr, r_fp2_mul_fp]
 def clobber_list(nvgpr, keep):
     regs = [f'"v{i}"' for i in range(nvgpr) if i not in keep]
     regs += [f'"s{s}"' for s in CLOBBER_SGPRS]
-    return ", ".join(regs)
+    regs += ['"scc"']  # the call sequence's s_add_u32/s_addc_u32 write SCC; a compare the compiler hoisted
+    return ", ".join(regs)  # above the call would otherwise feed a stale SCC to the branch after it
 
 
 def call_seq(label):
@@ -323,10 +324,99 @@ __device__ __forceinline__ void lcb_asm_fp2_mul_fp(u32x12 &xa, u32x12 &xb, u32x1
     return "".join(out)
 
 
+# ------------------------------------------------------------------ inline add / sub (no call)
+# Compiler-built 12-limb add/sub with C carries costs ~160 VALU instructions (64-bit adds + shifts); these
+# are the 36-37 instruction carry chains.  Carries ride in VCC through VOP2 (e32) forms only: gfx940+ has a
+# 2-wait-state hazard for an explicit SGPR read right after a VALU SGPR write, the implicit VCC read of
+# VOP2 does not.  Operands are 12 separate u32 (r, temps, a, b) so the register allocator places them.
+def inline_fn(name, comment, body, n_tmp, n_in, reduced_doc, r_early=False, with_p=False):
+    outs = [f'"=&v"(t[{j}])' for j in range(n_tmp)]
+    r_ops = [f'"=&v"(r[{j}])' if r_early else f'"=v"(r[{j}])' for j in range(N)]
+    ins = []
+    for k in range(n_in):
+        ins += [f'"v"({"ab"[k]}[{j}])' for j in range(N)]
+    if with_p:
+        ins += [f'"v"(0x{PL[j]:08x}u)' for j in range(N)]
+    # gfx940+ hazard: a VALU write of VCC needs 2 wait states before a VALU reads it as carry-in
+    # (LLVM emits `s_nop 1` between the links of its own carry chains on gfx942/gfx950).
+    hz = []
+    for line in body:
+        if line.rstrip().endswith(", vcc") and hz and "vcc," in hz[-1]:
+            hz.append("s_nop 1")
+        hz.append(line)
+    txt = "\\n\\t".join(hz)
+    args = ", ".join(["u32 *r"] + [f"const u32 *{'ab'[k]}" for k in range(n_in)])
+    tmp_decl = f"    u32 t[{n_tmp}];\n" if n_tmp else ""
+    return (f"// {comment} ({reduced_doc})\n"
+            f"__device__ __forceinline__ void {name}({args}) {{\n{tmp_decl}"
+            f"    asm volatile(\"{txt}\"\n        : {', '.join(r_ops + outs)}\n        : {', '.join(ins)}\n        : \"vcc\");\n}}\n")
+
+
+def op_index(n_tmp):
+    """operand numbering: r = 0..11, t = 12..12+n_tmp-1, a = next 12, b = next 12"""
+    r = list(range(N))
+    t = list(range(N, N + n_tmp))
+    a = list(range(N + n_tmp, 2 * N + n_tmp))
+    b = list(range(2 * N + n_tmp, 3 * N + n_tmp))
+    return r, t, a, b
+
+
+def gen_add_mod():
+    # the compare-subtract chain needs p in VGPRs: a VOP2 with carry-in already uses the constant bus (VCC)
+    r, t, a, b = op_index(N)
+    pv = list(range(3 * N + N, 4 * N + N))
+    s = [f"v_add_co_u32_e32 %{t[0]}, vcc, %{a[0]}, %{b[0]}"]
+    s += [f"v_addc_co_u32_e32 %{t[j]}, vcc, %{a[j]}, %{b[j]}, vcc" for j in range(1, N)]
+    s += [f"v_sub_co_u32_e32 %{r[0]}, vcc, %{t[0]}, %{pv[0]}"]
+    s += [f"v_subb_co_u32_e32 %{r[j]}, vcc, %{t[j]}, %{pv[j]}, vcc" for j in range(1, N)]
+    s += [f"v_cndmask_b32_e32 %{r[j]}, %{r[j]}, %{t[j]}, vcc" for j in range(N)]  # borrow -> keep t
+    return inline_fn("lcb_fp_add_asm", "r = a + b mod p", s, N, 2, "a, b < p -> r < p", r_early=True, with_p=True)
+
+
+def gen_sub_mod():
+    r, t, a, b = op_index(N + 1)
+    mw = t[N]
+    s = [f"v_sub_co_u32_e32 %{t[0]}, vcc, %{a[0]}, %{b[0]}"]
+    s += [f"v_subb_co_u32_e32 %{t[j]}, vcc, %{a[j]}, %{b[j]}, vcc" for j in range(1, N)]
+    # mw = t0 - t0 - borrow = all-ones iff a < b
+    s += [f"v_subb_co_u32_e32 %{mw}, vcc, %{t[0]}, %{t[0]}, vcc"]
+    s += [f"v_and_b32_e32 %{r[j]}, 0x{PL[j]:08x}, %{mw}" for j in range(N)]
+    s += [f"v_add_co_u32_e32 %{r[0]}, vcc, %{t[0]}, %{r[0]}"]
+    s += [f"v_addc_co_u32_e32 %{r[j]}, vcc, %{t[j]}, %{r[j]}, vcc" for j in range(1, N)]
+    return inline_fn("lcb_fp_sub_asm", "r = a - b mod p", s, N + 1, 2, "a, b < p -> r < p")
+
+
+def gen_add_nr():
+    r, t, a, b = op_index(0)
+    s = [f"v_add_co_u32_e32 %{r[0]}, vcc, %{a[0]}, %{b[0]}"]
+    s += [f"v_addc_co_u32_e32 %{r[j]}, vcc, %{a[j]}, %{b[j]}, vcc" for j in range(1, N)]
+    return inline_fn("lcb_fp_add_nr_asm", "r = a + b, not reduced", s, 0, 2, "a, b < p -> r < 2p: multiplicand only",
+                     r_early=True)
+
+
+def gen_neg():
+    r, t, a, b = op_index(N + 1)
+    mw = t[N]
+    # t = 0 - a; borrow iff a != 0; r = t + (p & -borrow)
+    s = [f"v_sub_co_u32_e32 %{t[0]}, vcc, 0, %{a[0]}"]
+    s += [f"v_subb_co_u32_e32 %{t[j]}, vcc, 0, %{a[j]}, vcc" for j in range(1, N)]
+    s += [f"v_subb_co_u32_e32 %{mw}, vcc, %{t[0]}, %{t[0]}, vcc"]
+    s += [f"v_and_b32_e32 %{r[j]}, 0x{PL[j]:08x}, %{mw}" for j in range(N)]
+    s += [f"v_add_co_u32_e32 %{r[0]}, vcc, %{t[0]}, %{r[0]}"]
+    s += [f"v_addc_co_u32_e32 %{r[j]}, vcc, %{t[j]}, %{r[j]}, vcc" for j in range(1, N)]
+    return inline_fn("lcb_fp_neg_asm", "r = -a mod p", s, N + 1, 1, "a < p -> r < p")
+
+
+INLINE = [gen_add_mod, gen_sub_mod, gen_add_nr, gen_neg]
+
+
 def main():
     dst = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "lachain_amd", "csrc", "asm_routines.hpp")
     with open(dst, "w") as f:
         f.write(emit())
+        f.write("\n// ------------------------------------------------------------------ inline carry chains\n")
+        for g in INLINE:
+            f.write(g())
     print("wrote", os.path.normpath(dst))
 
 
