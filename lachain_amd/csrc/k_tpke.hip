@@ -71,6 +71,39 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_verify(const u32 *lines, const uint
     accept[i] = ok && fp12_is_one(e);
 }
 
+// Two-kernel form of k_tpke_verify: the Miller loop parks f in HBM (SoA, 576 B/share) and
+// k_final_exp_check finishes; each kernel gets its own register budget.  accept[i] carries the
+// decompression / key / ciphertext validity from the first kernel to the second.
+extern "C" __global__ void LCB_BOUNDS k_tpke_miller(const u32 *lines, const uint8_t *ct_ok, const g1a_st *keys,
+                                                   u32 n_keys, const u32 *ct_idx, const u32 *dec_idx,
+                                                   const uint8_t *ui, u32 n, u32 *f_soa, uint8_t *accept) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    u32 c = ct_idx[i], d = dec_idx[i];
+    g1a Ui, Y;
+    bool ok = d < n_keys && ct_ok[c];
+    ok = g1_decompress(Ui, ui + 48 * (size_t)i) && ok;
+    g1a_st ks = keys[d < n_keys ? d : 0];
+    ok = ok && ks.ok;
+    st_to_g1a(Y, ks);
+    fp_neg(Y.y, Y.y);
+    LinesFromMemory sH{lines + (size_t)(2 * c) * LCB_LINESET_WORDS};
+    LinesFromMemory sW{lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS};
+    fp12 f;
+    miller2(f, sH, Ui, sW, Y);
+    fp12_store_soa(f_soa, n, i, f);
+    accept[i] = ok;
+}
+// accept[i] &= (final_exp(f_i) == 1)
+extern "C" __global__ void LCB_BOUNDS k_final_exp_check(const u32 *f_soa, u32 n, uint8_t *accept) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fp12 f, e;
+    fp12_load_soa(f, f_soa, n, i);
+    final_exp(e, f);
+    accept[i] = accept[i] && fp12_is_one(e);
+}
+
 // TPKE.PrivateKey.Decrypt: validity e(G, W) == e(U, H) <=> e(-G, W) e(U, H) == 1; then Ui = x U
 extern "C" __global__ void LCB_BOUNDS k_tpke_partial_decrypt(const u32 *lines, const uint8_t *ct_ok,
                                                             const uint8_t *cts_u, const fr *x_raw, u32 n_cts,
@@ -113,6 +146,12 @@ extern "C" void lcbk_tpke_ct_prepare(dim3 grid, hipStream_t s, const uint8_t *ct
 }
 extern "C" void lcbk_tpke_verify(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, uint8_t *accept) {
     LCB_LAUNCH(k_tpke_verify, lines, ct_ok, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, accept);
+}
+extern "C" void lcbk_tpke_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, u32 *f_soa, uint8_t *accept) {
+    LCB_LAUNCH(k_tpke_miller, lines, ct_ok, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, f_soa, accept);
+}
+extern "C" void lcbk_final_exp_check(dim3 grid, hipStream_t s, const u32 *f_soa, u32 n, uint8_t *accept) {
+    LCB_LAUNCH(k_final_exp_check, f_soa, n, accept);
 }
 extern "C" void lcbk_tpke_partial_decrypt(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, const uint8_t *cts_u, const void *x_raw, u32 n_cts, uint8_t *ui_out, uint8_t *status) {
     LCB_LAUNCH(k_tpke_partial_decrypt, lines, ct_ok, cts_u, (const fr *)x_raw, n_cts, ui_out, status);

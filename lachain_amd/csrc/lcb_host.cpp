@@ -86,7 +86,13 @@ struct DevBuf {
         return p;
     }
 };
-DevBuf b_lines, b_ctok, b_keys, b_in[8], b_out[4];
+DevBuf b_lines, b_ctok, b_keys, b_fsoa, b_in[8], b_out[4];
+// LCB_FUSED_VERIFY=1 selects the single-kernel verify (Miller loop + final exponentiation in one launch)
+static bool fused_verify() {
+    static int v = -1;
+    if (v < 0) { const char *e = getenv("LCB_FUSED_VERIFY"); v = (e && *e == '1') ? 1 : 0; }
+    return v == 1;
+}
 
 inline u32 nblk(size_t n) { return (u32)((n + LCB_BLOCK - 1) / LCB_BLOCK); }
 
@@ -526,8 +532,16 @@ static int tpke_verify_prepared_enqueue(uint8_t *d_accept, size_t n, size_t n_ke
         set_err("tpke verify: workspace not prepared for this batch");
         return -1;
     }
-    if (n) lcbk_tpke_verify(dim3(nblk(n)), s, (const u32 *)b_lines.p, (const uint8_t *)b_ctok.p, b_keys.p, (u32)n_keys,
-                            d_ct, d_dec, d_ui, (u32)n, d_accept);
+    if (n && fused_verify()) {
+        lcbk_tpke_verify(dim3(nblk(n)), s, (const u32 *)b_lines.p, (const uint8_t *)b_ctok.p, b_keys.p, (u32)n_keys,
+                         d_ct, d_dec, d_ui, (u32)n, d_accept);
+    } else if (n) {
+        u32 *f = (u32 *)b_fsoa.get(n * 576);
+        if (!f) { set_err("device allocation failed"); return -1; }
+        lcbk_tpke_miller(dim3(nblk(n)), s, (const u32 *)b_lines.p, (const uint8_t *)b_ctok.p, b_keys.p, (u32)n_keys,
+                         d_ct, d_dec, d_ui, (u32)n, f, d_accept);
+        lcbk_final_exp_check(dim3(nblk(n)), s, f, (u32)n, d_accept);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) { set_err("tpke verify launch", e); return -1; }
     return 0;

@@ -1,0 +1,117 @@
+#!/usr/bin/env python3
+"""tools/asm_sim.py — single-lane interpreter for the gfx950 leaf routines in lachain_amd/csrc/asm_routines.hpp.
+
+Executes the generated routine text (the subset of VOP2/VOP3/SOP1 instructions tools/gen_asm.py emits) for
+one lane with Python integers, so the generator's arithmetic and its register contract (which VGPRs/SGPRs a
+routine may write) can be checked on the CPU, without a GPU.  Used by tests/test_asm_routines.py.
+"""
+import os
+import re
+
+M32 = (1 << 32) - 1
+HERE = os.path.dirname(os.path.abspath(__file__))
+HPP = os.path.join(HERE, "..", "lachain_amd", "csrc", "asm_routines.hpp")
+
+
+def load_library(path=HPP):
+    """-> {label: [(mnemonic, [operands])]} parsed from the LCB_ASM_LIBRARY_TEXT macro."""
+    src = open(path).read()
+    body = src[src.index("#define LCB_ASM_LIBRARY_TEXT"):]
+    body = body[:body.index('    ""\n')]
+    routines, cur = {}, None
+    for raw in re.findall(r'"(.*?)\\n"', body):
+        line = raw.strip()
+        if not line or line.startswith("."):
+            continue
+        if line.endswith(":"):
+            cur = line[:-1]
+            routines[cur] = []
+            continue
+        if cur is None:
+            continue
+        mn, _, rest = line.partition(" ")
+        ops = [o.strip() for o in rest.split(",")] if rest else []
+        routines[cur].append((mn, ops))
+    return routines
+
+
+def _regs(op):
+    """'v12' -> ('v', [12]); 'v[36:37]' -> ('v', [36, 37]); 's[90:91]' -> ('s', [90, 91])"""
+    m = re.fullmatch(r"([vs])(\d+)", op)
+    if m:
+        return m.group(1), [int(m.group(2))]
+    m = re.fullmatch(r"([vs])\[(\d+):(\d+)\]", op)
+    if m:
+        lo, hi = int(m.group(2)), int(m.group(3))
+        return m.group(1), list(range(lo, hi + 1))
+    return None, None
+
+
+class Lane:
+    def __init__(self):
+        self.v, self.s = {}, {}
+        self.written_v, self.written_s = set(), set()
+
+    def get(self, op):
+        kind, rr = _regs(op)
+        if kind is None:
+            return int(op, 0) & M32
+        f = self.v if kind == "v" else self.s
+        val = 0
+        for k, r in enumerate(rr):
+            if r not in f:
+                raise KeyError(f"read of undefined {kind}{r}")
+            val |= f[r] << (32 * k)
+        return val
+
+    def getmask(self, op):  # a lane-mask SGPR pair: this lane's bit
+        return self.get(op) & 1
+
+    def put(self, op, val):
+        kind, rr = _regs(op)
+        f, w = (self.v, self.written_v) if kind == "v" else (self.s, self.written_s)
+        if kind == "v" and len(rr) == 2 and rr[0] % 2:
+            raise ValueError(f"misaligned 64-bit VGPR pair {op}")
+        for k, r in enumerate(rr):
+            f[r] = (val >> (32 * k)) & M32
+            w.add(r)
+
+
+def run(routine, lane):
+    for mn, ops in routine:
+        g = lane.get
+        if mn == "v_mad_u64_u32":
+            r = g(ops[2]) * g(ops[3]) + g(ops[4])
+            lane.put(ops[0], r & ((1 << 64) - 1)); lane.put(ops[1], r >> 64)
+        elif mn in ("v_add_co_u32_e64", "v_addc_co_u32_e64"):
+            r = g(ops[2]) + g(ops[3]) + (lane.getmask(ops[4]) if mn == "v_addc_co_u32_e64" else 0)
+            lane.put(ops[0], r & M32); lane.put(ops[1], r >> 32)
+        elif mn in ("v_sub_co_u32_e64", "v_subb_co_u32_e64"):
+            r = g(ops[2]) - g(ops[3]) - (lane.getmask(ops[4]) if mn == "v_subb_co_u32_e64" else 0)
+            lane.put(ops[0], r & M32); lane.put(ops[1], 1 if r < 0 else 0)
+        elif mn == "v_cndmask_b32_e64":
+            lane.put(ops[0], g(ops[2]) if lane.getmask(ops[3]) else g(ops[1]))
+        elif mn == "v_mul_lo_u32":
+            lane.put(ops[0], (g(ops[1]) * g(ops[2])) & M32)
+        elif mn in ("v_mov_b32", "s_mov_b32"):
+            lane.put(ops[0], g(ops[1]))
+        elif mn == "s_setpc_b64":
+            return
+        elif mn == "s_endpgm":
+            return
+        else:
+            raise NotImplementedError(mn)
+    raise RuntimeError("routine fell off its end without s_setpc_b64")
+
+
+def call(routines, label, inputs):
+    """inputs: {first VGPR: 12-limb integer}.  Returns (lane, reader(first VGPR) -> integer)."""
+    lane = Lane()
+    for base, val in inputs.items():
+        for j in range(12):
+            lane.v[base + j] = (val >> (32 * j)) & M32
+    run(routines[label], lane)
+
+    def read(base):
+        return sum(lane.v[base + j] << (32 * j) for j in range(12))
+    return lane, read

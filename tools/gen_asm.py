@@ -67,14 +67,21 @@ def load_p(a, pbase):
 
 
 def products(a, chains, pbase):
-    """chains: list of dict(a=[12 regs], b=[12 regs], m=[12 regs], acc=even reg, out=[12 regs]).
-    out[j] may alias a[j] (written after a[j]'s last use).  Results are in [0, 2p) (not yet reduced)."""
-    q = len(chains)
+    """chains: list of dict(a=[12 regs], b=[12 regs], m=[12 regs], acc=reg base (4 regs, even), out=[12 regs]).
+    out[j] may alias a[j] (written after a[j]'s last use).  Results are in [0, 2p) (not yet reduced).
+
+    Column accumulator = an even-aligned 64-bit pair (v_mad_u64_u32 needs aligned pairs on gfx950) plus a
+    carry word, rotated through a 4-register ring so the 32-bit shift between columns is one v_mov:
+    even columns use pair (R0,R1) + carry R3, odd columns pair (R2,R3) + carry R1.  The first carry add of
+    a column writes the fresh carry word (0 + 0 + carry), so it needs no zeroing."""
+    def ring(c, k):
+        r = c["acc"]
+        return (r, r + 1, r + 3) if k % 2 == 0 else (r + 2, r + 3, r + 1)
+
     for c in chains:
         acc = c["acc"]
         a(f"v_mov_b32 v{acc}, 0")
         a(f"v_mov_b32 v{acc + 1}, 0")
-        a(f"v_mov_b32 v{acc + 2}, 0")
     for k in range(2 * N - 1):
         lo = 0 if k < N else k - (N - 1)
         up = k if k < N else N - 1
@@ -83,34 +90,38 @@ def products(a, chains, pbase):
             terms.append(("ab", i, k - i))
             if i < k:
                 terms.append(("mp", i, k - i))
-        for (kind, i, j) in terms:
-            for t, c in enumerate(chains):
-                x = c["a"][i] if kind == "ab" else c["m"][i]
-                y = c["b"][j] if kind == "ab" else pbase + j
-                acc = c["acc"]
-                a(f"v_mad_u64_u32 v[{acc}:{acc + 1}], s[{CARRY[t]}:{CARRY[t] + 1}], v{x}, v{y}, v[{acc}:{acc + 1}]")
-            for t, c in enumerate(chains):
-                acc = c["acc"]
-                a(f"v_addc_co_u32_e64 v{acc + 2}, s[{CARRY[t]}:{CARRY[t] + 1}], 0, v{acc + 2}, s[{CARRY[t]}:{CARRY[t] + 1}]")
         if k < N:
+            terms.append(("m", k, 0))
+        for n_t, (kind, i, j) in enumerate(terms):
+            if kind == "m":
+                for t, c in enumerate(chains):
+                    a(f"v_mul_lo_u32 v{c['m'][k]}, v{ring(c, k)[0]}, s{S_PINV}")
             for t, c in enumerate(chains):
-                a(f"v_mul_lo_u32 v{c['m'][k]}, v{c['acc']}, s{S_PINV}")
+                L, H, C = ring(c, k)
+                if kind == "ab":
+                    x, y = c["a"][i], c["b"][j]
+                elif kind == "mp":
+                    x, y = c["m"][i], pbase + j
+                else:
+                    x, y = c["m"][k], pbase
+                a(f"v_mad_u64_u32 v[{L}:{H}], s[{CARRY[t]}:{CARRY[t] + 1}], v{x}, v{y}, v[{L}:{H}]")
             for t, c in enumerate(chains):
-                acc = c["acc"]
-                a(f"v_mad_u64_u32 v[{acc}:{acc + 1}], s[{CARRY[t]}:{CARRY[t] + 1}], v{c['m'][k]}, v{pbase}, v[{acc}:{acc + 1}]")
-            for t, c in enumerate(chains):
-                acc = c["acc"]
-                a(f"v_addc_co_u32_e64 v{acc + 2}, s[{CARRY[t]}:{CARRY[t] + 1}], 0, v{acc + 2}, s[{CARRY[t]}:{CARRY[t] + 1}]")
-        else:
-            for c in chains:
-                a(f"v_mov_b32 v{c['out'][k - N]}, v{c['acc']}")
+                L, H, C = ring(c, k)
+                sc = f"s[{CARRY[t]}:{CARRY[t] + 1}]"
+                if n_t == 0:
+                    a(f"v_addc_co_u32_e64 v{C}, {sc}, 0, 0, {sc}")
+                else:
+                    a(f"v_addc_co_u32_e64 v{C}, {sc}, 0, v{C}, {sc}")
         for c in chains:
-            acc = c["acc"]
-            a(f"v_mov_b32 v{acc}, v{acc + 1}")
-            a(f"v_mov_b32 v{acc + 1}, v{acc + 2}")
-            a(f"v_mov_b32 v{acc + 2}, 0")
-    for c in chains:
-        a(f"v_mov_b32 v{c['out'][N - 1]}, v{c['acc']}")
+            L, H, C = ring(c, k)
+            if k >= N:
+                a(f"v_mov_b32 v{c['out'][k - N]}, v{L}")
+            if k == 2 * N - 2:
+                a(f"v_mov_b32 v{c['out'][N - 1]}, v{H}")   # top carry word is 0: result < 2p < 2^384
+            else:
+                L2, H2, C2 = ring(c, k + 1)
+                assert H2 == C
+                a(f"v_mov_b32 v{L2}, v{H}")
 
 
 def reduce_once(a, r, tmp, pbase, sc=S_TMP):
