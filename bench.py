@@ -8,6 +8,9 @@ One "step" = one pass of the hot path over the whole batch, inputs resident in H
   lcb_tpke_prepare_dev          (k_g1_decompress: 22 keys; k_tpke_ct_prepare: per-ciphertext H(U||V) +
                                  Miller lines of H and W)
   lcb_tpke_verify_prepared_dev  (k_tpke_verify: per share, decompress U_i, 2-pair Miller loop, final exp)
+Second line of the metric (BASELINE configs[3]): G1 Pippenger MSM of --msm-points points per rank (default
+2^21; 8 ranks = 2^24), reported under "msm" in the same JSON line with its own roofline and CPU baseline; at
+N > 1 the per-GPU Jacobian partials are all-gathered over RCCL and summed on the GPU.
 Launch: `python bench.py --gpus 1` or under torch.distributed.run with --gpus N (one rank per GPU, weak
 scaling: every rank verifies its own 1M-share batch; no data-path collective).
 Prints ONE JSON line on rank 0.
@@ -135,6 +138,138 @@ def cpu_baseline(inp, target_s=15.0):
                        f"{dt:.1f} s, {mism} decision mismatches vs expected")
 
 
+# ------------------------------------------------------------------ G1 MSM (BASELINE configs[3])
+R_TOP = R >> 192
+
+
+def msm_inputs(nat, rank, n):
+    """Points P_i = a_i G (a_i < 2^63, generated by the product's batch kernel), scalars uniform below r (top
+    64-bit limb drawn below r's, so every value is < r).  Known answer: MSM = (sum a_i s_i mod r) G."""
+    rng = np.random.default_rng([SEED, 0x4D534D, rank])
+    a = rng.integers(1, 1 << 63, size=n, dtype=np.uint64)
+    s = rng.integers(0, np.iinfo(np.uint64).max, size=(n, 4), dtype=np.uint64, endpoint=True)
+    s[:, 3] = rng.integers(0, R_TOP, size=n, dtype=np.uint64)
+    a_bytes = np.zeros((n, 4), dtype=np.uint64)
+    a_bytes[:, 0] = a
+    pts = nat.mul_batch_raw(1, b"", a_bytes.tobytes(), n, generator=True)
+    # sum_i a_i s_i exactly: 16-bit limbs, every partial dot product stays below 2^58
+    a16 = a.view(np.uint16).reshape(n, 4).astype(np.int64)
+    s16 = s.view(np.uint16).reshape(n, 16).astype(np.int64)
+    total = 0
+    for k in range(4):
+        for j in range(16):
+            total += int(np.dot(a16[:, k], s16[:, j])) << (16 * (k + j))
+    return pts, s.tobytes(), total % R
+
+
+def msm_cpu_baseline(pts, scal, n_total, target_s=10.0):
+    import ctypes
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as o
+    lib = o.lib()
+    threads = max(1, min(16, os.cpu_count() or 1))
+
+    def run(n):
+        out = ctypes.create_string_buffer(48)
+        t0 = time.perf_counter()
+        rc = lib.orc_g1_msm_mt(out, pts[:48 * n], scal[:32 * n], ctypes.c_size_t(n), threads)
+        assert rc == 0
+        return time.perf_counter() - t0
+
+    n = 64 * threads
+    dt = run(n)
+    n = int(min(n_total, max(n, n * target_s / max(dt, 1e-3))))
+    dt = run(n)
+    return dict(value=n / dt, unit="points/s", cores=threads, kind="port",
+                sample=f"first {n} points of the same MSM, oracle/bls.c orc_g1_msm_mt (one 255-bit var-base "
+                       f"multiplication per point as MCL LagrangeInterpolation does, {threads} OpenMP threads), "
+                       f"{dt:.1f} s")
+
+
+def run_msm(args, nat, torch, dev, rank, world, cpu):
+    import torch.distributed as dist
+    lib = nat.lib()
+    n = args.msm_points
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    pts, scal, expect_local = msm_inputs(nat, rank, n)
+    d_pts48 = to_dev(torch, dev, pts)
+    d_aff = torch.empty(96 * n, dtype=torch.uint8, device=dev)
+    d_ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+    d_sc = to_dev(torch, dev, scal)
+    d_jac = torch.zeros(144, dtype=torch.uint8, device=dev)
+    d_all = torch.zeros(144 * world, dtype=torch.uint8, device=dev)
+    d_out = torch.zeros(48, dtype=torch.uint8, device=dev)
+    if lib.lcb_g1_to_affine_dev(d_aff.data_ptr(), d_ok.data_ptr(), d_pts48.data_ptr(), n, sh) != 0:
+        raise RuntimeError(nat.last_error())
+    del d_pts48
+    c = lib.lcb_g1_msm_window(n)
+
+    def step():
+        if lib.lcb_g1_msm_dev(d_jac.data_ptr(), d_aff.data_ptr(), d_sc.data_ptr(), n, 0, sh) != 0:
+            raise RuntimeError(nat.last_error())
+        if world > 1:
+            dist.all_gather_into_tensor(d_all, d_jac)   # RCCL over xGMI: 144 B Jacobian partial per GPU
+        else:
+            d_all.copy_(d_jac)
+        if lib.lcb_g1_jac_sum_dev(d_out.data_ptr(), None, d_all.data_ptr(), world, sh) != 0:
+            raise RuntimeError(nat.last_error())
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.msm_steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    phases = nat.msm_phase_ms()
+    # known answer over all ranks: (sum of the per-rank sums) G
+    e = torch.tensor(list(expect_local.to_bytes(32, "little")), dtype=torch.uint8, device=dev)
+    ok_pts = bool(d_ok.all().item())
+    if world > 1:
+        ge = torch.zeros(32 * world, dtype=torch.uint8, device=dev)
+        dist.all_gather_into_tensor(ge, e)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt[0])
+        exp_total = sum(int.from_bytes(bytes(ge[32 * k:32 * k + 32].cpu().numpy().tobytes()), "little")
+                        for k in range(world)) % R
+    else:
+        exp_total = expect_local
+    if rank != 0:
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as o
+    got = bytes(d_out.cpu().numpy().tobytes())
+    correct = ok_pts and got == o.g1_mul(o.g1_gen(), o.fr(exp_total))
+    nwin = 255 // c + 1
+    t_acc = phases["bucket_acc"] * 1e-3
+    fpmul_acc = n * nwin * 11          # mixed adds, one per nonzero digit (zero digits: 2^-c of them)
+    fpmul_total = nwin * (n * 11 + (1 << (c - 1)) * 2 * 16)
+    bytes_acc = n * nwin * (96 + 4) + nwin * (1 << (c - 1)) * (8 + 144)
+    res = dict(
+        metric="BLS12-381 G1 MSM points/sec (Pippenger, sum_i s_i P_i)", value=n * world * args.msm_steps / elapsed,
+        unit="points/s", points_per_rank=n, window_bits=c, windows=nwin, steps=args.msm_steps,
+        ms_per_step=1e3 * elapsed / args.msm_steps, known_answer_ok=correct,
+        phase_ms={k: round(v, 3) for k, v in phases.items()},
+        roofline={"bound": "valu_int32", "kernel": "k_msm_bucket_acc",
+                  "achieved": fpmul_acc * MAC_PER_FPMUL / t_acc / 1e12, "peak": PEAK_MAC32 / 1e12,
+                  "unit": "Tmac32/s", "frac": fpmul_acc * MAC_PER_FPMUL / t_acc / PEAK_MAC32,
+                  "hbm_gbs_bucket_phase": bytes_acc / t_acc / 1e9, "hbm_peak_gbs": 8000.0,
+                  "algorithmic_fpmul_per_msm": fpmul_total},
+        config="configs[3]: G1 Pippenger MSM, points sharded across ranks, RCCL all-gather of 144 B Jacobian partials",
+    )
+    if cpu:
+        res["cpu_baseline"] = msm_cpu_baseline(pts, scal, n)
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -146,6 +281,8 @@ def main():
     ap.add_argument("--vlen", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--msm-points", type=int, default=1 << 21, help="G1 MSM points per rank (0 = skip)")
+    ap.add_argument("--msm-steps", type=int, default=3)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -225,6 +362,9 @@ def main():
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         elapsed = float(tmax[0])
     mismatches_all, shares_all = int(t[1]), int(t[2])
+    msm = None
+    if args.msm_points > 0:
+        msm = run_msm(args, nat, torch, dev, rank, world, cpu=(world == 1 and not args.no_cpu_baseline))
     if rank == 0:
         ms_per_step = 1e3 * elapsed / args.steps
         value = shares_all * args.steps / elapsed
@@ -252,6 +392,7 @@ def main():
                          "verify_ms": ver_ms, "prepare_ms": prep_ms},
             "cpu_baseline": cpu,
             "input_gen_s": t_gen,
+            "msm": msm,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

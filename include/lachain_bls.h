@@ -204,8 +204,27 @@ int lcb_g1_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_t *xs, cons
 int lcb_g2_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
                           const uint32_t *off, size_t n_problems);
 
-/* G1 multi-scalar multiplication sum_i s_i P_i (serialized points, 32-byte LE scalars < r) */
+/* G1 multi-scalar multiplication sum_i s_i P_i (serialized points, 32-byte LE scalars < r): the large-k form of
+   MclBls12381.LagrangeInterpolate / mclBnG1_mulVec (TPKE/PublicKey.cs:83, ThresholdSignature/PublicKeySet.cs:31).
+   Pippenger bucket method on the GPU (k_msm.hip).  Returns -1 on a malformed point or a scalar >= r. */
 int lcb_g1_msm(uint8_t out[48], const uint8_t *points, const uint8_t *scalars, size_t n);
+
+/* Device-resident MSM (BASELINE configs[3]).  points_aff: n x 96 B affine points in mcl's in-memory Fp layout
+   (x then y, Montgomery form, 6 x u64 LE each = the x,y words of a normalized mclBnG1; (0,0) = infinity);
+   scalars: n x 32 B LE, reduced mod r on the device.  out_jac: 144 B Jacobian result (mclBnG1 layout) in device
+   memory.  window_bits = 0 picks the Pippenger window width from n (lcb_g1_msm_window).  Enqueued on `stream`
+   (a hipStream_t); nothing is synchronised. */
+int lcb_g1_msm_dev(void *out_jac, const void *points_aff, const uint8_t *scalars, size_t n, int window_bits,
+                   void *stream);
+int lcb_g1_msm_window(size_t n);
+/* per-phase device time (ms) of the last MSM: digits, sort, bucket bounds, bucket accumulation, bucket
+   reduction, window combination (waits for the last MSM to finish) */
+int lcb_g1_msm_phase_ms(float *ms, int n_phases);
+/* 48-byte serialized G1 -> 96-byte affine device layout above; ok[i] = 0 for a malformed encoding (nullable) */
+int lcb_g1_to_affine_dev(void *out_aff, uint8_t *ok, const uint8_t *points, size_t n, void *stream);
+/* sum of k Jacobian G1 points (device, 144 B each, e.g. the per-GPU MSM partials after an RCCL all-gather);
+   writes the serialized sum to out48 and/or the Jacobian sum to out_jac (device pointers, either nullable) */
+int lcb_g1_jac_sum_dev(uint8_t *out48, void *out_jac, const void *parts, size_t k, void *stream);
 
 /* batched scalar multiplication of the G1 / G2 generator or of given points (key generation, synthetic inputs) */
 int lcb_g1_mul_batch(uint8_t *out, const uint8_t *points, int points_is_generator, const uint8_t *scalars, size_t n);

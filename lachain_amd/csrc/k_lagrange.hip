@@ -123,35 +123,6 @@ extern "C" __global__ void LCB_BOUNDS k_g2_sum(const g2 *parts, const uint8_t *o
     status[j] = ok;
 }
 
-// ================================================================================= MSM (v0: per-point
-// products + pairwise tree reduction; the bucketed Pippenger is the next step)
-extern "C" __global__ void LCB_BOUNDS k_g1_msm_products(const uint8_t *pts, const uint8_t *scalars, u32 n, g1 *out,
-                                                       uint8_t *ok_out) {
-    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    g1a A;
-    bool ok = g1_decompress(A, pts + 48 * (size_t)i);
-    fr k;
-    const u32 *sw = (const u32 *)(scalars + 32 * (size_t)i);
-    for (int j = 0; j < 8; j++) k.v[j] = sw[j];
-    ok = ok && fr_raw_lt_r(k);
-    g1 P, R;
-    jac_from_aff(P, A);
-    jac_mul_bits(R, P, k.v, 255);
-    out[i] = R;
-    ok_out[i] = ok;
-}
-extern "C" __global__ void LCB_BOUNDS k_g1_reduce_pairs(g1 *v, u32 n_half, u32 n) {
-    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_half) return;
-    u32 j = i + n_half;
-    if (j < n) jac_add(v[i], v[i], v[j]);
-}
-extern "C" __global__ void LCB_BOUNDS k_g1_finish(const g1 *v, uint8_t *out) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) g1_compress_jac(out, v[0]);
-}
-
-
 // ---------------------------------------------------------------- host launch wrappers
 extern "C" void lcbk_lagrange_coeffs(dim3 grid, hipStream_t s, const uint8_t *xs, const u32 *off, u32 n_problems, void *lam_raw, uint8_t *status) {
     LCB_LAUNCH(k_lagrange_coeffs, xs, off, n_problems, (fr *)lam_raw, status);
@@ -167,13 +138,4 @@ extern "C" void lcbk_g1_sum(dim3 grid, hipStream_t s, const void *parts, const u
 }
 extern "C" void lcbk_g2_sum(dim3 grid, hipStream_t s, const void *parts, const uint8_t *ok_in, const u32 *off, u32 n_problems, uint8_t *status, uint8_t *out) {
     LCB_LAUNCH(k_g2_sum, (const g2 *)parts, ok_in, off, n_problems, status, out);
-}
-extern "C" void lcbk_g1_msm_products(dim3 grid, hipStream_t s, const uint8_t *pts, const uint8_t *scalars, u32 n, void *out, uint8_t *ok_out) {
-    LCB_LAUNCH(k_g1_msm_products, pts, scalars, n, (g1 *)out, ok_out);
-}
-extern "C" void lcbk_g1_reduce_pairs(dim3 grid, hipStream_t s, void *v, u32 n_half, u32 n) {
-    LCB_LAUNCH(k_g1_reduce_pairs, (g1 *)v, n_half, n);
-}
-extern "C" void lcbk_g1_finish(dim3 grid, hipStream_t s, const void *v, uint8_t *out) {
-    LCB_LAUNCH(k_g1_finish, (const g1 *)v, out);
 }

@@ -1,0 +1,225 @@
+// lachain_amd/csrc/k_msm.hip — gfx950 Pippenger multi-scalar multiplication over G1 (SURVEY.md §8a row a4 at
+// scale, BASELINE configs[3]).  Lagrange-in-the-exponent for large k reduces to sum_i s_i P_i
+// (MclBls12381.LagrangeInterpolate, called from TPKE/PublicKey.cs:83 and ThresholdSignature/PublicKeySet.cs:31).
+//
+// Pipeline (one stream, no host round trip):
+//   1. k_msm_digits      one lane per point: signed c-bit digits of s_i (s_i mod r), one (key, value) record per
+//                        window; key = window * 2^(c-1) + |digit| - 1 (or a sentinel for digit 0), value = point
+//                        index | sign << 31.  Window-major so a wave writes 256 contiguous bytes per window.
+//   2. radix sort        hipCUB DeviceRadixSort on the (key, value) pairs, only the key bits that are used.
+//   3. k_msm_bounds      start/end of every bucket in the sorted order.
+//   4. k_msm_bucket_acc  one lane per bucket: Jacobian += affine (mixed add, 11 Fp-mul) over its points.  This is
+//                        the HBM phase: each record gathers a 96-byte affine point.
+//   5. k_msm_bucket_reduce  one lane per segment of L buckets: running-sum trick sum_j (j+1) B_j, plus a*T to
+//                        place the segment at its offset a inside the window.
+//   6. k_g1_jac_reduce_block (LDS tree, until one sum per window) + k_msm_horner: sum_w 2^(c w) W_w by doubling.
+// Points are affine, Montgomery form, 12 x u32 limbs per coordinate (= the x,y words of mcl's mclBnG1 with
+// z = 1); (0, 0) encodes the point at infinity.
+#include "kcommon.hpp"
+#include <hipcub/hipcub.hpp>
+
+LCB_ASM_LIBRARY(k_msm)
+
+// s mod r for any 256-bit s (2^256 < 3r: at most two subtractions)
+DI void fr_raw_reduce(fr &s) {
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        if (fr_raw_lt_r(s)) return;
+        u32 br = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            u64 x = (u64)s.v[j] - LCB_R[j] - br;
+            s.v[j] = (u32)x;
+            br = (u32)(x >> 32) & 1;
+        }
+    }
+}
+DI u32 word_sel(const fr &s, u32 k) {  // s.v[k] without dynamic register indexing (0 past the top)
+    u32 r = 0;
+#pragma unroll
+    for (u32 j = 0; j < 8; j++) r = (j == k) ? s.v[j] : r;
+    return r;
+}
+
+extern "C" __global__ void LCB_BOUNDS k_msm_digits(const uint8_t *scalars, u32 n, u32 c, u32 nwin, u32 *keys,
+                                                  u32 *vals) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fr s;
+    const uint4 *sw = (const uint4 *)(scalars + 32 * (size_t)i);
+    uint4 a = sw[0], b = sw[1];
+    s.v[0] = a.x; s.v[1] = a.y; s.v[2] = a.z; s.v[3] = a.w;
+    s.v[4] = b.x; s.v[5] = b.y; s.v[6] = b.z; s.v[7] = b.w;
+    fr_raw_reduce(s);
+    const u32 half = 1u << (c - 1), mask = (1u << c) - 1, sentinel = nwin << (c - 1);
+    u32 carry = 0;
+    for (u32 w = 0; w < nwin; w++) {
+        u32 bit = w * c, lo = bit >> 5, sh = bit & 31;
+        u64 word = (u64)word_sel(s, lo) | ((u64)word_sel(s, lo + 1) << 32);
+        u32 d = ((u32)(word >> sh) & mask) + carry;
+        u32 v = i;
+        if (d > half) { d = (1u << c) - d; carry = 1; v |= 0x80000000u; }
+        else carry = 0;
+        keys[(size_t)w * n + i] = d ? (w << (c - 1)) | (d - 1) : sentinel;
+        vals[(size_t)w * n + i] = v;
+    }
+}
+
+extern "C" __global__ void LCB_BOUNDS k_msm_bounds(const u32 *keys, u32 m, u32 sentinel, u32 *start, u32 *end) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    u32 k = keys[i];
+    if (k >= sentinel) return;
+    if (i == 0 || keys[i - 1] != k) start[k] = i;
+    if (i == m - 1 || keys[i + 1] != k) end[k] = i + 1;
+}
+
+DI void load_aff(fp &x, fp &y, const fp *pts, u32 idx) {
+    const uint4 *p = (const uint4 *)(pts + 2 * (size_t)idx);
+    uint4 q[6];
+#pragma unroll
+    for (int j = 0; j < 6; j++) q[j] = p[j];
+    const u32 *w = (const u32 *)q;
+#pragma unroll
+    for (int j = 0; j < 12; j++) { x.v[j] = w[j]; y.v[j] = w[12 + j]; }
+}
+
+extern "C" __global__ void LCB_BOUNDS k_msm_bucket_acc(const fp *pts, const u32 *vals, const u32 *start,
+                                                      const u32 *end, u32 nb, g1 *buckets) {
+    u32 b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    g1 acc;
+    jac_set_inf(acc);
+    u32 e1 = end[b];
+    for (u32 e = start[b]; e < e1; e++) {
+        u32 v = vals[e];
+        fp x, y;
+        load_aff(x, y, pts, v & 0x7fffffffu);
+        if (fp_is_zero(x) && fp_is_zero(y)) continue;  // point at infinity
+        if (v >> 31) fp_neg(y, y);
+        jac_add_aff(acc, acc, x, y);
+    }
+    buckets[b] = acc;
+}
+
+// segment q of window w covers buckets a = q*L .. a+L-1 (digit values a+1 .. a+L)
+extern "C" __global__ void LCB_BOUNDS k_msm_bucket_reduce(const g1 *buckets, u32 half, u32 L, u32 n_seg, g1 *seg_out) {
+    u32 s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n_seg) return;
+    u32 per_win = half / L, w = s / per_win, a = (s % per_win) * L;
+    const g1 *B = buckets + (size_t)w * half + a;
+    g1 run, acc;
+    jac_set_inf(run);
+    jac_set_inf(acc);
+    for (u32 j = L; j-- > 0;) {
+        grp_add(run, run, B[j]);
+        grp_add(acc, acc, run);
+    }
+    if (a) {
+        g1 t;
+        jac_mul_u64(t, run, a);
+        grp_add(acc, acc, t);
+    }
+    seg_out[s] = acc;
+}
+
+extern "C" __global__ void LCB_BOUNDS k_g1_jac_reduce_groups(const g1 *in, u32 n_in, u32 group, g1 *out) {
+    u32 j = blockIdx.x * blockDim.x + threadIdx.x;
+    u32 n_out = (n_in + group - 1) / group;
+    if (j >= n_out) return;
+    g1 acc;
+    jac_set_inf(acc);
+    u32 e = min(n_in, (j + 1) * group);
+    for (u32 i = j * group; i < e; i++) grp_add(acc, acc, in[i]);
+    out[j] = acc;
+}
+
+// out[b] = sum of in[b*group .. (b+1)*group) (clipped to n_in): lanes add strided inputs, then a log2(256)-deep
+// tree in LDS, so the dependent chain is group/256 + 8 additions instead of group
+extern "C" __global__ void LCB_BOUNDS k_g1_jac_reduce_block(const g1 *in, u32 n_in, u32 group, g1 *out) {
+    __shared__ g1 sh[LCB_BLOCK];
+    u32 t = threadIdx.x, b = blockIdx.x;
+    size_t lo = (size_t)b * group, hi = min((size_t)n_in, lo + group);
+    g1 acc;
+    jac_set_inf(acc);
+    for (size_t i = lo + t; i < hi; i += LCB_BLOCK) grp_add(acc, acc, in[i]);
+    sh[t] = acc;
+    __syncthreads();
+    for (u32 s = LCB_BLOCK / 2; s > 0; s >>= 1) {
+        if (t < s) {
+            g1 x = sh[t], y = sh[t + s];
+            grp_add(x, x, y);
+            sh[t] = x;
+        }
+        __syncthreads();
+    }
+    if (t == 0) out[b] = sh[0];
+}
+
+extern "C" __global__ void LCB_BOUNDS k_msm_horner(const g1 *win, u32 nwin, u32 c, g1 *out) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    g1 acc = win[nwin - 1];
+    for (u32 w = nwin - 1; w-- > 0;) {
+        for (u32 t = 0; t < c; t++) grp_dbl(acc, acc);
+        grp_add(acc, acc, win[w]);
+    }
+    out[0] = acc;
+}
+
+extern "C" __global__ void LCB_BOUNDS k_g1_jac_compress(const g1 *in, u32 n, uint8_t *out) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    g1_compress_jac(out + 48 * (size_t)i, in[i]);
+}
+
+// 48-byte serialized G1 -> 96-byte affine Montgomery (MSM input layout); ok[i] = 0 on a malformed encoding
+extern "C" __global__ void LCB_BOUNDS k_g1_to_affine(const uint8_t *in, u32 n, fp *out, uint8_t *ok) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    g1a A;
+    bool good = g1_decompress(A, in + 48 * (size_t)i);
+    if (!good || A.inf) { A.x = fp_zero(); A.y = fp_zero(); }
+    out[2 * (size_t)i] = A.x;
+    out[2 * (size_t)i + 1] = A.y;
+    if (ok) ok[i] = good;
+}
+
+// ---------------------------------------------------------------- host launch wrappers
+extern "C" void lcbk_msm_digits(dim3 grid, hipStream_t s, const uint8_t *scalars, u32 n, u32 c, u32 nwin, u32 *keys, u32 *vals) {
+    LCB_LAUNCH(k_msm_digits, scalars, n, c, nwin, keys, vals);
+}
+extern "C" void lcbk_msm_bounds(dim3 grid, hipStream_t s, const u32 *keys, u32 m, u32 sentinel, u32 *start, u32 *end) {
+    LCB_LAUNCH(k_msm_bounds, keys, m, sentinel, start, end);
+}
+extern "C" void lcbk_msm_bucket_acc(dim3 grid, hipStream_t s, const void *pts, const u32 *vals, const u32 *start, const u32 *end, u32 nb, void *buckets) {
+    LCB_LAUNCH(k_msm_bucket_acc, (const fp *)pts, vals, start, end, nb, (g1 *)buckets);
+}
+extern "C" void lcbk_msm_bucket_reduce(dim3 grid, hipStream_t s, const void *buckets, u32 half, u32 L, u32 n_seg, void *seg_out) {
+    LCB_LAUNCH(k_msm_bucket_reduce, (const g1 *)buckets, half, L, n_seg, (g1 *)seg_out);
+}
+extern "C" void lcbk_g1_jac_reduce_groups(dim3 grid, hipStream_t s, const void *in, u32 n_in, u32 group, void *out) {
+    LCB_LAUNCH(k_g1_jac_reduce_groups, (const g1 *)in, n_in, group, (g1 *)out);
+}
+extern "C" void lcbk_g1_jac_reduce_block(hipStream_t s, const void *in, u32 n_in, u32 group, void *out) {
+    dim3 grid((n_in + group - 1) / group);
+    LCB_LAUNCH(k_g1_jac_reduce_block, (const g1 *)in, n_in, group, (g1 *)out);
+}
+extern "C" void lcbk_msm_horner(hipStream_t s, const void *win, u32 nwin, u32 c, void *out) {
+    dim3 grid(1);
+    LCB_LAUNCH(k_msm_horner, (const g1 *)win, nwin, c, (g1 *)out);
+}
+extern "C" void lcbk_g1_jac_compress(dim3 grid, hipStream_t s, const void *in, u32 n, uint8_t *out) {
+    LCB_LAUNCH(k_g1_jac_compress, (const g1 *)in, n, out);
+}
+extern "C" void lcbk_g1_to_affine(dim3 grid, hipStream_t s, const uint8_t *in, u32 n, void *out, uint8_t *ok) {
+    LCB_LAUNCH(k_g1_to_affine, in, n, (fp *)out, ok);
+}
+// stable radix sort of (key, value) pairs on key bits [0, end_bit); temp == nullptr queries *temp_bytes.
+// Returns 1 when the sorted data ended in the alternate buffers (keys_alt / vals_alt).
+extern "C" int lcbk_sort_pairs(void *temp, size_t *temp_bytes, u32 *keys, u32 *keys_alt, u32 *vals, u32 *vals_alt,
+                               u32 m, int end_bit, hipStream_t s) {
+    hipcub::DoubleBuffer<u32> dk(keys, keys_alt), dv(vals, vals_alt);
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(temp, *temp_bytes, dk, dv, (int)m, 0, end_bit, s);
+    if (e != hipSuccess) return -1;
+    return dk.Current() == keys_alt ? 1 : 0;
+}

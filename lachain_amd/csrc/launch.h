@@ -25,9 +25,16 @@ extern "C" void lcbk_g1_mul_lanes(dim3 grid, hipStream_t s, const uint8_t *ys, c
 extern "C" void lcbk_g2_mul_lanes(dim3 grid, hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out);
 extern "C" void lcbk_g1_sum(dim3 grid, hipStream_t s, const void *parts, const uint8_t *ok_in, const u32 *off, u32 n_problems, uint8_t *status, uint8_t *out);
 extern "C" void lcbk_g2_sum(dim3 grid, hipStream_t s, const void *parts, const uint8_t *ok_in, const u32 *off, u32 n_problems, uint8_t *status, uint8_t *out);
-extern "C" void lcbk_g1_msm_products(dim3 grid, hipStream_t s, const uint8_t *pts, const uint8_t *scalars, u32 n, void *out, uint8_t *ok_out);
-extern "C" void lcbk_g1_reduce_pairs(dim3 grid, hipStream_t s, void *v, u32 n_half, u32 n);
-extern "C" void lcbk_g1_finish(dim3 grid, hipStream_t s, const void *v, uint8_t *out);
+extern "C" void lcbk_msm_digits(dim3 grid, hipStream_t s, const uint8_t *scalars, u32 n, u32 c, u32 nwin, u32 *keys, u32 *vals);
+extern "C" void lcbk_msm_bounds(dim3 grid, hipStream_t s, const u32 *keys, u32 m, u32 sentinel, u32 *start, u32 *end);
+extern "C" void lcbk_msm_bucket_acc(dim3 grid, hipStream_t s, const void *pts, const u32 *vals, const u32 *start, const u32 *end, u32 nb, void *buckets);
+extern "C" void lcbk_msm_bucket_reduce(dim3 grid, hipStream_t s, const void *buckets, u32 half, u32 L, u32 n_seg, void *seg_out);
+extern "C" void lcbk_g1_jac_reduce_groups(dim3 grid, hipStream_t s, const void *in, u32 n_in, u32 group, void *out);
+extern "C" void lcbk_g1_jac_reduce_block(hipStream_t s, const void *in, u32 n_in, u32 group, void *out);
+extern "C" void lcbk_msm_horner(hipStream_t s, const void *win, u32 nwin, u32 c, void *out);
+extern "C" void lcbk_g1_jac_compress(dim3 grid, hipStream_t s, const void *in, u32 n, uint8_t *out);
+extern "C" void lcbk_g1_to_affine(dim3 grid, hipStream_t s, const uint8_t *in, u32 n, void *out, uint8_t *ok);
+extern "C" int lcbk_sort_pairs(void *temp, size_t *temp_bytes, u32 *keys, u32 *keys_alt, u32 *vals, u32 *vals_alt, u32 m, int end_bit, hipStream_t s);
 extern "C" void lcbk_op(dim3 grid, hipStream_t s, int op, u32 *io, int orig_cof);
 
 // sizes of the device records the host allocates

@@ -109,6 +109,15 @@ bool sync_check(const char *what) {
     return true;
 }
 
+// canonical Fr bytes (32-byte LE < r)
+bool fr_bytes_lt_r(const uint8_t *b) {
+    for (int j = 7; j >= 0; j--) {
+        uint32_t w = (uint32_t)b[4 * j] | (uint32_t)b[4 * j + 1] << 8 | (uint32_t)b[4 * j + 2] << 16 | (uint32_t)b[4 * j + 3] << 24;
+        if (w != LCB_R_HOST[j]) return w < LCB_R_HOST[j];
+    }
+    return false;
+}
+
 } // namespace
 
 // ================================================================== init / config
@@ -798,22 +807,135 @@ extern "C" int lcb_g2_hash_batch(uint8_t *out, const uint8_t *msg_data, const ui
     for (size_t i = 0; i < n; i++) if (!ok[i]) { set_err("hash-to-G2 failed"); return -1; }
     return 0;
 }
+// ---------------------------------------------------------------- Pippenger MSM (k_msm.hip)
+DevBuf b_msm[12];
+hipEvent_t g_msm_ev[7];
+bool g_msm_ev_ready = false;
+
+// window width minimising ceil-windows * (n mixed adds * 11 + 2^(c-1) buckets * 2 Jacobian adds * 16) Fp-mul
+static u32 msm_window(size_t n) {
+    u32 best = 4;
+    double best_cost = 1e300;
+    for (u32 c = 4; c <= 20; c++) {
+        double w = 255 / c + 1;
+        double cost = w * ((double)n * 11.0 + (double)(1u << (c - 1)) * 32.0);
+        if (cost < best_cost) { best_cost = cost; best = c; }
+    }
+    return best;
+}
+extern "C" int lcb_g1_msm_window(size_t n) { return (int)msm_window(n); }
+
+static int msm_enqueue(void *out_jac, const void *pts, const uint8_t *scalars, size_t n, int window_bits, hipStream_t s) {
+    if (n > 0x7fffffffu) { set_err("msm: too many points"); return -1; }
+    u32 c = window_bits > 0 ? (u32)window_bits : msm_window(n);
+    if (c < 2 || c > 24) { set_err("msm: window bits out of range"); return -1; }
+    u32 nwin = 255 / c + 1, half = 1u << (c - 1), nb = nwin * half, sentinel = nb;
+    size_t m = (size_t)n * nwin;
+    if (m > 0xffffffffu) { set_err("msm: n * windows exceeds 2^32"); return -1; }
+    int end_bit = 1;
+    while ((1ull << end_bit) <= sentinel) end_bit++;
+    u32 L = 1;
+    while ((size_t)nb / (L * 2) >= 65536 && L * 2 <= half) L *= 2;
+    u32 n_seg = nb / L, per_win = half / L, n_l1 = n_seg / (per_win < 256 ? per_win : 256);
+    if (!g_msm_ev_ready) {
+        for (auto &e : g_msm_ev) hipEventCreate(&e);
+        g_msm_ev_ready = true;
+    }
+    u32 *keys = (u32 *)b_msm[0].get(m * 4), *keys2 = (u32 *)b_msm[1].get(m * 4);
+    u32 *vals = (u32 *)b_msm[2].get(m * 4), *vals2 = (u32 *)b_msm[3].get(m * 4);
+    u32 *st = (u32 *)b_msm[4].get((size_t)nb * 4), *en = (u32 *)b_msm[5].get((size_t)nb * 4);
+    void *buckets = b_msm[6].get((size_t)nb * LCB_G1_JAC_BYTES);
+    void *segs = b_msm[7].get((size_t)n_seg * LCB_G1_JAC_BYTES);
+    void *l1 = b_msm[8].get((size_t)n_l1 * LCB_G1_JAC_BYTES);
+    void *wins = b_msm[9].get((size_t)nwin * LCB_G1_JAC_BYTES);
+    size_t tb = 0;
+    if (n && lcbk_sort_pairs(nullptr, &tb, keys, keys2, vals, vals2, (u32)m, end_bit, s) < 0) { set_err("msm: sort query"); return -1; }
+    void *temp = b_msm[10].get(tb);
+    if (!keys || !keys2 || !vals || !vals2 || !st || !en || !buckets || !segs || !l1 || !wins || !temp) {
+        set_err("msm: device allocation failed");
+        return -1;
+    }
+    hipEventRecord(g_msm_ev[0], s);
+    if (n) lcbk_msm_digits(dim3(nblk(n)), s, scalars, (u32)n, c, nwin, keys, vals);
+    hipEventRecord(g_msm_ev[1], s);
+    int alt = n ? lcbk_sort_pairs(temp, &tb, keys, keys2, vals, vals2, (u32)m, end_bit, s) : 0;
+    if (alt < 0) { set_err("msm: radix sort"); return -1; }
+    if (alt) { keys = keys2; vals = vals2; }
+    hipEventRecord(g_msm_ev[2], s);
+    hipMemsetAsync(st, 0, (size_t)nb * 4, s);
+    hipMemsetAsync(en, 0, (size_t)nb * 4, s);
+    if (m) lcbk_msm_bounds(dim3(nblk(m)), s, keys, (u32)m, sentinel, st, en);
+    hipEventRecord(g_msm_ev[3], s);
+    lcbk_msm_bucket_acc(dim3(nblk(nb)), s, pts, vals, st, en, nb, buckets);
+    hipEventRecord(g_msm_ev[4], s);
+    lcbk_msm_bucket_reduce(dim3(nblk(n_seg)), s, buckets, half, L, n_seg, segs);
+    hipEventRecord(g_msm_ev[5], s);
+    // per-window sums: LDS tree reductions of up to 256 segment sums per block, ping-ponging segs <-> l1
+    void *cur = segs, *nxt = l1;
+    for (u32 cnt = per_win, total = n_seg; cnt > 1;) {
+        u32 g = cnt < 256 ? cnt : 256;
+        void *dst = (cnt == g) ? wins : nxt;
+        lcbk_g1_jac_reduce_block(s, cur, total, g, dst);
+        cnt /= g;
+        total /= g;
+        cur = dst;
+        nxt = (dst == l1) ? segs : l1;
+    }
+    if (per_win == 1) hipMemcpyAsync(wins, segs, (size_t)nwin * LCB_G1_JAC_BYTES, hipMemcpyDeviceToDevice, s);
+    lcbk_msm_horner(s, wins, nwin, c, out_jac);
+    hipEventRecord(g_msm_ev[6], s);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { set_err("msm launch", e); return -1; }
+    return 0;
+}
+extern "C" int lcb_g1_msm_dev(void *out_jac, const void *points_aff, const uint8_t *scalars, size_t n, int window_bits,
+                              void *stream) {
+    LOCKED_OR(-1)
+    return msm_enqueue(out_jac, points_aff, scalars, n, window_bits, (hipStream_t)stream);
+}
+extern "C" int lcb_g1_msm_phase_ms(float *ms, int n_phases) {
+    LOCKED_OR(-1)
+    if (!g_msm_ev_ready) { set_err("msm: no MSM has run"); return -1; }
+    if (hipEventSynchronize(g_msm_ev[6]) != hipSuccess) { set_err("msm: event sync"); return -1; }
+    for (int i = 0; i < n_phases && i < 6; i++)
+        if (hipEventElapsedTime(&ms[i], g_msm_ev[i], g_msm_ev[i + 1]) != hipSuccess) ms[i] = -1.0f;
+    return 0;
+}
+extern "C" int lcb_g1_to_affine_dev(void *out_aff, uint8_t *ok, const uint8_t *points, size_t n, void *stream) {
+    LOCKED_OR(-1)
+    if (n) lcbk_g1_to_affine(dim3(nblk(n)), (hipStream_t)stream, points, (u32)n, out_aff, ok);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { set_err("to_affine launch", e); return -1; }
+    return 0;
+}
+extern "C" int lcb_g1_jac_sum_dev(uint8_t *out48, void *out_jac, const void *parts, size_t k, void *stream) {
+    LOCKED_OR(-1)
+    hipStream_t s = (hipStream_t)stream;
+    void *acc = out_jac ? out_jac : b_msm[11].get(LCB_G1_JAC_BYTES);
+    if (!acc) { set_err("device allocation failed"); return -1; }
+    lcbk_g1_jac_reduce_groups(dim3(1), s, parts, (u32)k, k ? (u32)k : 1u, acc);
+    if (out48) lcbk_g1_jac_compress(dim3(1), s, acc, 1, out48);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { set_err("jac sum launch", e); return -1; }
+    return 0;
+}
 extern "C" int lcb_g1_msm(uint8_t out[48], const uint8_t *points, const uint8_t *scalars, size_t n) {
     LOCKED_OR(-1)
     hipStream_t s = g_stream;
     if (n == 0) { memset(out, 0, 48); return 0; }
+    for (size_t i = 0; i < n; i++) {   // mclBnFr values are canonical (< r); reject what mcl would not hold
+        const uint8_t *sc = scalars + 32 * i;
+        if (!fr_bytes_lt_r(sc)) { set_err("invalid point or scalar"); return -1; }
+    }
     const uint8_t *dp = up(b_in[0], points, 48 * n, s);
     const uint8_t *dsc = up(b_in[1], scalars, 32 * n, s);
-    void *parts = b_in[2].get(LCB_G1_JAC_BYTES * n);
+    void *aff = b_in[2].get(96 * n);
     uint8_t *dok = (uint8_t *)b_out[0].get(n), *dout = (uint8_t *)b_out[1].get(48);
-    if (!dp || !dsc || !parts || !dok || !dout) { set_err("device allocation failed"); return -1; }
-    lcbk_g1_msm_products(dim3(nblk(n)), s, dp, dsc, (u32)n, parts, dok);
-    for (size_t m = n; m > 1;) {
-        size_t h = (m + 1) / 2;
-        lcbk_g1_reduce_pairs(dim3(nblk(h)), s, parts, (u32)h, (u32)m);
-        m = h;
-    }
-    lcbk_g1_finish(dim3(1), s, parts, dout);
+    void *jac = b_out[2].get(LCB_G1_JAC_BYTES);
+    if (!dp || !dsc || !aff || !dok || !dout || !jac) { set_err("device allocation failed"); return -1; }
+    lcbk_g1_to_affine(dim3(nblk(n)), s, dp, (u32)n, aff, dok);
+    if (msm_enqueue(jac, aff, dsc, n, 0, s)) return -1;
+    lcbk_g1_jac_compress(dim3(1), s, jac, 1, dout);
     std::vector<uint8_t> ok(n);
     hipMemcpyAsync(out, dout, 48, hipMemcpyDeviceToHost, s);
     hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, s);

@@ -72,6 +72,14 @@ _SIGS = {
     "lcb_g1_lagrange_batch": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_u32p, c_size]),
     "lcb_g2_lagrange_batch": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_u32p, c_size]),
     "lcb_g1_msm": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_size]),
+    "lcb_g1_msm_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_size, ctypes.c_int,
+                                      ctypes.c_void_p]),
+    "lcb_g1_msm_window": (ctypes.c_int, [c_size]),
+    "lcb_g1_msm_phase_ms": (ctypes.c_int, [ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
+    "lcb_g1_to_affine_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_size,
+                                            ctypes.c_void_p]),
+    "lcb_g1_jac_sum_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_size,
+                                          ctypes.c_void_p]),
     "lcb_g1_mul_batch": (ctypes.c_int, [c_u8p, c_u8p, ctypes.c_int, c_u8p, c_size]),
     "lcb_g2_mul_batch": (ctypes.c_int, [c_u8p, c_u8p, ctypes.c_int, c_u8p, c_size]),
     "lcb_g2_hash_batch": (ctypes.c_int, [c_u8p, c_u8p, c_u32p, c_size]),
@@ -267,6 +275,16 @@ def g1_msm(points, scalars):
     ob, po = _out(48)
     _check(lib().lcb_g1_msm(po, pp, ps, len(points)), "g1_msm")
     return bytes(ob)
+
+
+MSM_PHASES = ("digits", "sort", "bounds", "bucket_acc", "bucket_reduce", "combine")
+
+
+def msm_phase_ms():
+    """Device time (ms) of each phase of the last MSM (lcb_g1_msm_phase_ms)."""
+    arr = (ctypes.c_float * len(MSM_PHASES))()
+    _check(lib().lcb_g1_msm_phase_ms(arr, len(MSM_PHASES)), "msm_phase_ms")
+    return dict(zip(MSM_PHASES, list(arr)))
 
 
 def mul_batch(group, points, scalars, generator=False):

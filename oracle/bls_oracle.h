@@ -68,6 +68,7 @@ int orc_g1_lagrange(uint8_t out[48], const uint8_t *xs, const uint8_t *ys, size_
 int orc_g2_lagrange(uint8_t out[96], const uint8_t *xs, const uint8_t *ys, size_t k);
 int orc_fr_lagrange(uint8_t out[32], const uint8_t *xs, const uint8_t *ys, size_t k);
 int orc_fr_eval_poly(uint8_t out[32], const uint8_t *coeffs, size_t n, const uint8_t x[32]);
+int orc_g1_msm_mt(uint8_t out[48], const uint8_t *pts, const uint8_t *scalars, size_t n, int nthreads);
 int orc_g1_msm(uint8_t out[48], const uint8_t *pts, const uint8_t *scalars, size_t n);
 
 /* ---- GT / pairing (GT = 12 Fp, canonical big-endian-free LE layout) ---- */

@@ -31,3 +31,18 @@ class Drbg:
 
     def fr(self):
         return self.fr_int().to_bytes(32, "little")
+
+
+def gpu_native():
+    """The product library, initialised for GPU tests.  torch's HIP runtime is brought up first: the tests that
+    hand torch-allocated device buffers to the *_dev entry points need torch and liblachain_bls to share the
+    device, and torch's bundled runtime refuses to initialise after another runtime has opened it."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except ImportError:
+        pass
+    from lachain_amd import native
+    native.lib()  # fails loudly without the library or a gfx950 device
+    return native

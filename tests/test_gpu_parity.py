@@ -5,16 +5,14 @@ comparison is bit-exact (serialized G1/G2/GT bytes, accept/reject bitmaps).
 import pytest
 
 import oracle as o
-from helpers import Drbg, kats
+from helpers import Drbg, gpu_native, kats
 
 pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(scope="module")
 def nat():
-    from lachain_amd import native
-    native.lib()  # fails loudly without the library or a gfx950 device
-    return native
+    return gpu_native()
 
 
 @pytest.fixture(scope="module")
