@@ -270,6 +270,139 @@ def run_msm(args, nat, torch, dev, rank, world, cpu):
     return res
 
 
+# ------------------------------------------------------------------ threshold signatures (BASELINE configs[2])
+W_TS = C["C_DEC2"] + C["C_ML2_EVAL"] + C["C_LINES"] + C["C_FE"]   # per share: sig decompress, Miller (one side's
+                                                                 # lines on the fly), final exponentiation
+
+
+def coin_id(era, agreement, epoch):
+    """CommonCoin message: CoinId.ToBytes() = Era || Agreement || Epoch, int64 LE (CoinId.cs:21-24)"""
+    return era.to_bytes(8, "little") + agreement.to_bytes(8, "little") + epoch.to_bytes(8, "little")
+
+
+def ts_inputs(nat, rank, rounds, n, f):
+    d = Drbg(SEED.to_bytes(8, "little") + b"TS" + rank.to_bytes(4, "little"))
+    coeffs = [d.fr() for _ in range(f + 1)]
+
+    def poly(x):
+        acc = 0
+        for c in reversed(coeffs):
+            acc = (acc * x + c) % R
+        return acc
+
+    sks = [poly(i + 1) for i in range(n)]
+    shared_sk = poly(0)
+    fr = lambda v: v.to_bytes(32, "little")
+    pks = nat.mul_batch(1, None, [fr(x) for x in sks] + [fr(shared_sk)], generator=True)   # 100 shares + shared
+    msgs = [coin_id(0, rank * rounds + r, 5) for r in range(rounds)]
+    hs = np.frombuffer(b"".join(nat.g2_hash_batch(msgs)), dtype=np.uint8).reshape(rounds, 96)
+    pts = np.repeat(hs, n, axis=0).tobytes()
+    sk_arr = np.frombuffer(b"".join(fr(x) for x in sks), dtype=np.uint8).reshape(n, 32)
+    sigs = bytearray(nat.mul_batch_raw(2, pts, np.tile(sk_arr, (rounds, 1)).tobytes(), rounds * n))
+    # corrupt one share per round (1 %): share j of round r carries the signature of share j+1 (valid point,
+    # wrong key); j = 7r mod n, so a third of the rounds lose one of their first F+1 shares
+    expect = np.ones(rounds * n, dtype=np.uint8)
+    for r in range(rounds):
+        j = (7 * r) % n
+        a, b = r * n + j, r * n + (j + 1) % n
+        sigs[96 * a:96 * a + 96] = sigs[96 * b:96 * b + 96]
+        expect[a] = 0
+    midx = np.repeat(np.arange(rounds, dtype=np.uint32), n)
+    pidx = np.tile(np.arange(n, dtype=np.uint32), rounds)
+    moff = np.arange(0, 24 * (rounds + 1), 24, dtype=np.uint32)
+    return dict(pks=b"".join(pks), msgs=b"".join(msgs), moff=moff, sigs=bytes(sigs), midx=midx, pidx=pidx,
+                expect=expect, shared_sk=shared_sk, msg_list=msgs)
+
+
+def run_ts(args, nat, torch, dev, rank, world):
+    import torch.distributed as dist
+    lib = nat.lib()
+    rounds, n, f = args.ts_rounds, args.ts_n, (args.ts_n - 1) // 3
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    t_gen = time.perf_counter()
+    inp = ts_inputs(nat, rank, rounds, n, f)
+    t_gen = time.perf_counter() - t_gen
+    d_pks, d_msg, d_moff = to_dev(torch, dev, inp["pks"]), to_dev(torch, dev, inp["msgs"]), to_dev(torch, dev, inp["moff"])
+    d_sigs, d_midx, d_pidx = to_dev(torch, dev, inp["sigs"]), to_dev(torch, dev, inp["midx"]), to_dev(torch, dev, inp["pidx"])
+    d_acc = torch.zeros(rounds * n, dtype=torch.uint8, device=dev)
+    d_comb = torch.zeros(96 * rounds, dtype=torch.uint8, device=dev)
+    d_cst = torch.zeros(rounds, dtype=torch.uint8, device=dev)
+    d_cacc = torch.zeros(rounds, dtype=torch.uint8, device=dev)
+    d_ridx = torch.arange(rounds, dtype=torch.int32, device=dev)
+    d_shared = torch.full((rounds,), n, dtype=torch.int32, device=dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+
+    def step(timed=False):
+        if timed:
+            ev[0].record(stream)
+        rc = lib.lcb_ts_prepare_dev(d_pks.data_ptr(), n + 1, d_msg.data_ptr(), d_moff.data_ptr(), rounds, sh)
+        if timed:
+            ev[1].record(stream)
+        rc |= lib.lcb_ts_verify_prepared_dev(d_acc.data_ptr(), rounds * n, n + 1, rounds, d_sigs.data_ptr(),
+                                             d_midx.data_ptr(), d_pidx.data_ptr(), sh)
+        if timed:
+            ev[2].record(stream)
+        rc |= lib.lcb_ts_assemble_dev(d_comb.data_ptr(), d_cst.data_ptr(), d_acc.data_ptr(), d_sigs.data_ptr(), n,
+                                      f + 1, rounds, sh)
+        rc |= lib.lcb_ts_verify_prepared_dev(d_cacc.data_ptr(), rounds, n + 1, rounds, d_comb.data_ptr(),
+                                             d_ridx.data_ptr(), d_shared.data_ptr(), sh)
+        if timed:
+            ev[3].record(stream)
+        if rc != 0:
+            raise RuntimeError(nat.last_error())
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    t_prep = t_ver = t_asm = 0.0
+    for _ in range(args.ts_steps):
+        step(True)
+        torch.cuda.synchronize(dev)
+        t_prep += ev[0].elapsed_time(ev[1])
+        t_ver += ev[1].elapsed_time(ev[2])
+        t_asm += ev[2].elapsed_time(ev[3])
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    mism = int(np.sum(d_acc.cpu().numpy() != inp["expect"]))
+    comb_ok = int(d_cst.cpu().numpy().sum()) == rounds and int(d_cacc.cpu().numpy().sum()) == rounds
+    # spot-check combined signatures against the oracle: sigma_r = shared_sk * H(msg_r) (ThresholdSignatureTest.cs)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as o
+    comb = d_comb.cpu().numpy().tobytes()
+    for r in (0, 1, rounds - 1):
+        comb_ok = comb_ok and comb[96 * r:96 * r + 96] == o.ts_sign(o.fr(inp["shared_sk"]), inp["msg_list"][r])
+    t = torch.tensor([elapsed, float(mism), float(0 if comb_ok else 1)], dtype=torch.float64, device=dev)
+    if world > 1:
+        tm = t[:1].clone()
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        t[0] = tm[0]
+    if rank != 0:
+        return None
+    elapsed = float(t[0])
+    per = args.ts_steps
+    ver_s = t_ver / per * 1e-3
+    return dict(
+        metric="BLS12-381 threshold-signature share verifications/sec (ValidateSignature + AddShare assembly)",
+        value=rounds * n * world * per / elapsed, unit="share verifications/s",
+        rounds_per_s=rounds * world * per / elapsed, rounds_per_rank=rounds, shares_per_round=n, threshold_k=f + 1,
+        steps=per, ms_per_step=1e3 * elapsed / per, decision_mismatches=int(t[1]), combined_ok=int(t[2]) == 0,
+        phase_ms={"prepare": t_prep / per, "verify_shares": t_ver / per, "assemble_and_verify_combined": t_asm / per},
+        roofline={"bound": "valu_int32", "kernel": "k_ts_miller + k_final_exp_check",
+                  "achieved": rounds * n * W_TS * MAC_PER_FPMUL / ver_s / 1e12, "peak": PEAK_MAC32 / 1e12,
+                  "unit": "Tmac32/s", "frac": rounds * n * W_TS * MAC_PER_FPMUL / ver_s / PEAK_MAC32,
+                  "work_per_share_fpmul": W_TS},
+        config=f"configs[2]: {rounds} rounds x N={n} F={f} CommonCoin shares per rank; per round: {n} share "
+               f"verifications, G2 Lagrange over the first {f + 1} valid shares, combined-signature verification",
+        input_gen_s=t_gen,
+    )
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -283,6 +416,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--msm-points", type=int, default=1 << 21, help="G1 MSM points per rank (0 = skip)")
     ap.add_argument("--msm-steps", type=int, default=3)
+    ap.add_argument("--ts-rounds", type=int, default=65536, help="CommonCoin rounds per rank (0 = skip)")
+    ap.add_argument("--ts-n", type=int, default=100)
+    ap.add_argument("--ts-steps", type=int, default=1)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -362,7 +498,9 @@ def main():
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         elapsed = float(tmax[0])
     mismatches_all, shares_all = int(t[1]), int(t[2])
-    msm = None
+    msm = ts = None
+    if args.ts_rounds > 0:
+        ts = run_ts(args, nat, torch, dev, rank, world)
     if args.msm_points > 0:
         msm = run_msm(args, nat, torch, dev, rank, world, cpu=(world == 1 and not args.no_cpu_baseline))
     if rank == 0:
@@ -393,6 +531,7 @@ def main():
             "cpu_baseline": cpu,
             "input_gen_s": t_gen,
             "msm": msm,
+            "threshold_signature": ts,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

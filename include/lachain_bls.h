@@ -191,6 +191,20 @@ int lcb_ts_verify_shares_dev(uint8_t *accept, size_t n, const uint8_t *pks, size
                              const uint8_t *msg_data, const uint32_t *msg_off, size_t n_msgs,
                              const uint32_t *msg_idx, const uint32_t *pk_idx, void *stream);
 
+/* Split form of lcb_ts_verify_shares_dev for callers that verify several batches against the same messages and
+   keys (e.g. the shares of a coin, then the combined signature): prepare decompresses the keys and hashes every
+   message to G2 with its Miller lines; verify_prepared checks items against that workspace. */
+int lcb_ts_prepare_dev(const uint8_t *pks, size_t n_pks, const uint8_t *msg_data, const uint32_t *msg_off,
+                       size_t n_msgs, void *stream);
+int lcb_ts_verify_prepared_dev(uint8_t *accept, size_t n, size_t n_pks, size_t n_msgs, const uint8_t *sigs,
+                               const uint32_t *msg_idx, const uint32_t *pk_idx, void *stream);
+/* ThresholdSigner.AddShare assembly for whole batches of rounds (ThresholdSigner.cs:62-75, PublicKeySet.cs:34-42):
+   round r owns shares [r*per_round, (r+1)*per_round) with verification bits in accept (device); the first k
+   accepted shares in index order (x = index + 1) are Lagrange-combined in G2.  sig_out: n_rounds x 96 B,
+   status[r] = 0 when round r has fewer than k valid shares.  All pointers are device pointers. */
+int lcb_ts_assemble_dev(uint8_t *sig_out, uint8_t *status, const uint8_t *accept, const uint8_t *sigs,
+                        size_t per_round, size_t k, size_t n_rounds, void *stream);
+
 /* PrivateKeyShare.HashAndSign for a batch of (key, message) pairs (ThresholdSignature/PrivateKeyShare.cs:21-27) */
 int lcb_ts_sign(uint8_t *sigs_out, const uint8_t *sks, const uint8_t *msg_data, const uint32_t *msg_off,
                 const uint32_t *msg_idx, size_t n);
@@ -203,6 +217,12 @@ int lcb_g1_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_t *xs, cons
                           const uint32_t *off, size_t n_problems);
 int lcb_g2_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
                           const uint32_t *off, size_t n_problems);
+
+/* Device-pointer forms of the batched Lagrange interpolation above (n_entries = off[n_problems]). */
+int lcb_g1_lagrange_dev(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys, const uint32_t *off,
+                        size_t n_problems, size_t n_entries, void *stream);
+int lcb_g2_lagrange_dev(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys, const uint32_t *off,
+                        size_t n_problems, size_t n_entries, void *stream);
 
 /* G1 multi-scalar multiplication sum_i s_i P_i (serialized points, 32-byte LE scalars < r): the large-k form of
    MclBls12381.LagrangeInterpolate / mclBnG1_mulVec (TPKE/PublicKey.cs:83, ThresholdSignature/PublicKeySet.cs:31).

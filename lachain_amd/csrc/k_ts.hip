@@ -43,7 +43,63 @@ extern "C" __global__ void LCB_BOUNDS k_ts_verify(const u32 *lines, const uint8_
     final_exp(e, f);
     accept[i] = ok && fp12_is_one(e);
 }
+// Split form (default): the 2-pair Miller loop parks f in HBM (word-major SoA) and k_final_exp_check
+// (k_tpke.hip) finishes, so each half gets its own register budget.
+extern "C" __global__ void LCB_BOUNDS k_ts_miller(const u32 *lines, const uint8_t *msg_ok, const g1a_st *pks,
+                                                 u32 n_pks, const uint8_t *sigs, const u32 *msg_idx,
+                                                 const u32 *pk_idx, u32 n, u32 *f_soa, uint8_t *accept) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    u32 m = msg_idx[i], k = pk_idx[i];
+    g2a S;
+    g1a PK, G;
+    bool ok = k < n_pks && msg_ok[m];
+    ok = g2_decompress(S, sigs + 96 * (size_t)i) && ok;
+    g1a_st ps = pks[k < n_pks ? k : 0];
+    ok = ok && ps.ok;
+    st_to_g1a(PK, ps);
+    g1_generator(G);
+    fp_neg(G.y, G.y);
+    LinesFromMemory sH{lines + (size_t)m * LCB_LINESET_WORDS};
+    LinesOnTheFly sS;
+    sS.init(S);
+    fp12 f;
+    miller2(f, sH, PK, sS, G);
+    fp12_store_soa(f_soa, n, i, f);
+    accept[i] = ok;
+}
 
+// ThresholdSigner.AddShare / PublicKeySet.AssembleSignature selection (ThresholdSigner.cs:62-75,
+// PublicKeySet.cs:34-42): per round, the first k shares (in index order) that passed verification; x = index + 1.
+// A round with fewer than k valid shares gets x = 0 entries, which the Lagrange stage reports as status 0
+// (the reference keeps waiting: AddShare returns without a signature).
+extern "C" __global__ void LCB_BOUNDS k_ts_select(const uint8_t *accept, const uint8_t *sigs, u32 per_round, u32 k,
+                                                 u32 n_rounds, uint8_t *xs, uint8_t *ys, u32 *off) {
+    u32 r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rounds) return;
+    off[r] = r * k;
+    if (r == n_rounds - 1) off[n_rounds] = n_rounds * k;
+    u32 cnt = 0;
+    for (u32 i = 0; i < per_round && cnt < k; i++) {
+        size_t src = (size_t)r * per_round + i;
+        if (!accept[src]) continue;
+        size_t dst = (size_t)r * k + cnt;
+        u32 *xw = (u32 *)(xs + 32 * dst);
+        xw[0] = i + 1;
+        for (int q = 1; q < 8; q++) xw[q] = 0;
+        const u32 *sw = (const u32 *)(sigs + 96 * src);
+        u32 *yw = (u32 *)(ys + 96 * dst);
+        for (int q = 0; q < 24; q++) yw[q] = sw[q];
+        cnt++;
+    }
+    for (; cnt < k; cnt++) {
+        size_t dst = (size_t)r * k + cnt;
+        u32 *xw = (u32 *)(xs + 32 * dst);
+        u32 *yw = (u32 *)(ys + 96 * dst);
+        for (int q = 0; q < 8; q++) xw[q] = 0;
+        for (int q = 0; q < 24; q++) yw[q] = 0;
+    }
+}
 
 // ---------------------------------------------------------------- host launch wrappers
 extern "C" void lcbk_ts_msg_prepare(dim3 grid, hipStream_t s, const uint8_t *msg_data, const u32 *msg_off, u32 n_msgs, u32 *lines, uint8_t *msg_ok, int orig_cof) {
@@ -51,4 +107,10 @@ extern "C" void lcbk_ts_msg_prepare(dim3 grid, hipStream_t s, const uint8_t *msg
 }
 extern "C" void lcbk_ts_verify(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *msg_ok, const void *pks, u32 n_pks, const uint8_t *sigs, const u32 *msg_idx, const u32 *pk_idx, u32 n, uint8_t *accept) {
     LCB_LAUNCH(k_ts_verify, lines, msg_ok, (const g1a_st *)pks, n_pks, sigs, msg_idx, pk_idx, n, accept);
+}
+extern "C" void lcbk_ts_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *msg_ok, const void *pks, u32 n_pks, const uint8_t *sigs, const u32 *msg_idx, const u32 *pk_idx, u32 n, u32 *f_soa, uint8_t *accept) {
+    LCB_LAUNCH(k_ts_miller, lines, msg_ok, (const g1a_st *)pks, n_pks, sigs, msg_idx, pk_idx, n, f_soa, accept);
+}
+extern "C" void lcbk_ts_select(dim3 grid, hipStream_t s, const uint8_t *accept, const uint8_t *sigs, u32 per_round, u32 k, u32 n_rounds, uint8_t *xs, uint8_t *ys, u32 *off) {
+    LCB_LAUNCH(k_ts_select, accept, sigs, per_round, k, n_rounds, xs, ys, off);
 }

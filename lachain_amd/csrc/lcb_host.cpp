@@ -668,23 +668,53 @@ extern "C" int lcb_tpke_encrypt_phase2(uint8_t *w_out, const uint8_t *u, const u
 }
 
 // ================================================================== batch: threshold signatures
-static int ts_verify_enqueue(uint8_t *d_accept, size_t n, const uint8_t *d_pks, size_t n_pks, const uint8_t *d_sigs,
-                             const uint8_t *d_msg, const uint32_t *d_moff, size_t n_msgs, const uint32_t *d_midx,
-                             const uint32_t *d_pidx, hipStream_t s) {
+static int ts_prepare_enqueue(const uint8_t *d_pks, size_t n_pks, const uint8_t *d_msg, const uint32_t *d_moff,
+                              size_t n_msgs, hipStream_t s) {
     u32 *lines = (u32 *)b_lines.get((size_t)n_msgs * LCB_LINESET_BYTES);
     uint8_t *mok = (uint8_t *)b_ctok.get(n_msgs);
     void *keys = b_keys.get(n_pks * LCB_G1A_ST_BYTES);
     if (!lines || !mok || !keys) { set_err("device allocation failed"); return -1; }
     if (n_pks) lcbk_g1_decompress(dim3(nblk(n_pks)), s, d_pks, (u32)n_pks, keys);
-    if (n_msgs)
-        lcbk_ts_msg_prepare(dim3(nblk(n_msgs)), s, d_msg, d_moff, (u32)n_msgs,
-                           lines, mok, g_orig_cofactor);
-    if (n)
-        lcbk_ts_verify(dim3(nblk(n)), s, lines, mok, keys, (u32)n_pks, d_sigs,
-                           d_midx, d_pidx, (u32)n, d_accept);
+    if (n_msgs) lcbk_ts_msg_prepare(dim3(nblk(n_msgs)), s, d_msg, d_moff, (u32)n_msgs, lines, mok, g_orig_cofactor);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { set_err("ts prepare launch", e); return -1; }
+    return 0;
+}
+static int ts_verify_prepared_enqueue(uint8_t *d_accept, size_t n, size_t n_pks, size_t n_msgs, const uint8_t *d_sigs,
+                                      const uint32_t *d_midx, const uint32_t *d_pidx, hipStream_t s) {
+    if (b_lines.cap < (size_t)n_msgs * LCB_LINESET_BYTES || b_ctok.cap < n_msgs || b_keys.cap < n_pks * LCB_G1A_ST_BYTES) {
+        set_err("ts verify: workspace not prepared for this batch");
+        return -1;
+    }
+    if (n && fused_verify()) {
+        lcbk_ts_verify(dim3(nblk(n)), s, (const u32 *)b_lines.p, (const uint8_t *)b_ctok.p, b_keys.p, (u32)n_pks,
+                       d_sigs, d_midx, d_pidx, (u32)n, d_accept);
+    } else if (n) {
+        u32 *f = (u32 *)b_fsoa.get(n * 576);
+        if (!f) { set_err("device allocation failed"); return -1; }
+        lcbk_ts_miller(dim3(nblk(n)), s, (const u32 *)b_lines.p, (const uint8_t *)b_ctok.p, b_keys.p, (u32)n_pks,
+                       d_sigs, d_midx, d_pidx, (u32)n, f, d_accept);
+        lcbk_final_exp_check(dim3(nblk(n)), s, f, (u32)n, d_accept);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) { set_err("ts verify launch", e); return -1; }
     return 0;
+}
+static int ts_verify_enqueue(uint8_t *d_accept, size_t n, const uint8_t *d_pks, size_t n_pks, const uint8_t *d_sigs,
+                             const uint8_t *d_msg, const uint32_t *d_moff, size_t n_msgs, const uint32_t *d_midx,
+                             const uint32_t *d_pidx, hipStream_t s) {
+    if (ts_prepare_enqueue(d_pks, n_pks, d_msg, d_moff, n_msgs, s)) return -1;
+    return ts_verify_prepared_enqueue(d_accept, n, n_pks, n_msgs, d_sigs, d_midx, d_pidx, s);
+}
+extern "C" int lcb_ts_prepare_dev(const uint8_t *pks, size_t n_pks, const uint8_t *msg_data, const uint32_t *msg_off,
+                                  size_t n_msgs, void *stream) {
+    LOCKED_OR(-1)
+    return ts_prepare_enqueue(pks, n_pks, msg_data, msg_off, n_msgs, (hipStream_t)stream);
+}
+extern "C" int lcb_ts_verify_prepared_dev(uint8_t *accept, size_t n, size_t n_pks, size_t n_msgs, const uint8_t *sigs,
+                                          const uint32_t *msg_idx, const uint32_t *pk_idx, void *stream) {
+    LOCKED_OR(-1)
+    return ts_verify_prepared_enqueue(accept, n, n_pks, n_msgs, sigs, msg_idx, pk_idx, (hipStream_t)stream);
 }
 extern "C" int lcb_ts_verify_shares_dev(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks, const uint8_t *sigs,
                                         const uint8_t *msg_data, const uint32_t *msg_off, size_t n_msgs,
@@ -736,6 +766,25 @@ extern "C" int lcb_ts_sign(uint8_t *sigs_out, const uint8_t *sks, const uint8_t 
 }
 
 // ================================================================== batch: Lagrange, scalar mul, hash, MSM
+DevBuf b_lag[3];
+// device-side Lagrange at 0 for np problems (entries off[j]..off[j+1]); dout = serialized results, dst = status
+static int lagrange_enqueue(int g, uint8_t *dout, uint8_t *dst, const uint8_t *dx, const uint8_t *dy, const uint32_t *doff,
+                            size_t np, size_t ne, hipStream_t s) {
+    void *lam = b_lag[0].get(LCB_FR_BYTES * (ne ? ne : 1));
+    void *parts = b_lag[1].get((g == 1 ? LCB_G1_JAC_BYTES : LCB_G2_JAC_BYTES) * (ne ? ne : 1));
+    uint8_t *pok = (uint8_t *)b_lag[2].get(ne ? ne : 1);
+    if (!lam || !parts || !pok) { set_err("device allocation failed"); return -1; }
+    lcbk_lagrange_coeffs(dim3(nblk(np)), s, dx, doff, (u32)np, lam, dst);
+    if (ne) {
+        if (g == 1) lcbk_g1_mul_lanes(dim3(nblk(ne)), s, dy, lam, (u32)ne, parts, pok);
+        else lcbk_g2_mul_lanes(dim3(nblk(ne)), s, dy, lam, (u32)ne, parts, pok);
+    }
+    if (g == 1) lcbk_g1_sum(dim3(nblk(np)), s, parts, pok, doff, (u32)np, dst, dout);
+    else lcbk_g2_sum(dim3(nblk(np)), s, parts, pok, doff, (u32)np, dst, dout);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { set_err("lagrange launch", e); return -1; }
+    return 0;
+}
 static int lagrange_batch(int g, uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys, const uint32_t *off,
                           size_t np) {
     LOCKED_OR(-1)
@@ -746,21 +795,36 @@ static int lagrange_batch(int g, uint8_t *out, uint8_t *status, const uint8_t *x
     const uint8_t *dx = up(b_in[0], xs, 32 * ne, s);
     const uint8_t *dy = up(b_in[1], ys, pb * ne, s);
     const uint32_t *doff = up(b_in[2], off, np + 1, s);
-    void *lam = b_in[3].get(LCB_FR_BYTES * (ne ? ne : 1));
-    void *parts = b_in[4].get((g == 1 ? LCB_G1_JAC_BYTES : LCB_G2_JAC_BYTES) * (ne ? ne : 1));
-    uint8_t *pok = (uint8_t *)b_in[5].get(ne ? ne : 1);
     uint8_t *dst = (uint8_t *)b_out[0].get(np), *dout = (uint8_t *)b_out[1].get(pb * np);
-    if (!dx || !dy || !doff || !lam || !parts || !pok || !dst || !dout) { set_err("device allocation failed"); return -1; }
-    lcbk_lagrange_coeffs(dim3(nblk(np)), s, dx, doff, (u32)np, lam, dst);
-    if (ne) {
-        if (g == 1) lcbk_g1_mul_lanes(dim3(nblk(ne)), s, dy, lam, (u32)ne, parts, pok);
-        else lcbk_g2_mul_lanes(dim3(nblk(ne)), s, dy, lam, (u32)ne, parts, pok);
-    }
-    if (g == 1) lcbk_g1_sum(dim3(nblk(np)), s, parts, pok, doff, (u32)np, dst, dout);
-    else lcbk_g2_sum(dim3(nblk(np)), s, parts, pok, doff, (u32)np, dst, dout);
+    if (!dx || !dy || !doff || !dst || !dout) { set_err("device allocation failed"); return -1; }
+    if (lagrange_enqueue(g, dout, dst, dx, dy, doff, np, ne, s)) return -1;
     hipMemcpyAsync(out, dout, pb * np, hipMemcpyDeviceToHost, s);
     hipMemcpyAsync(status, dst, np, hipMemcpyDeviceToHost, s);
     return sync_check("lagrange") ? 0 : -1;
+}
+extern "C" int lcb_g1_lagrange_dev(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
+                                   const uint32_t *off, size_t n_problems, size_t n_entries, void *stream) {
+    LOCKED_OR(-1)
+    return n_problems ? lagrange_enqueue(1, out, status, xs, ys, off, n_problems, n_entries, (hipStream_t)stream) : 0;
+}
+extern "C" int lcb_g2_lagrange_dev(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
+                                   const uint32_t *off, size_t n_problems, size_t n_entries, void *stream) {
+    LOCKED_OR(-1)
+    return n_problems ? lagrange_enqueue(2, out, status, xs, ys, off, n_problems, n_entries, (hipStream_t)stream) : 0;
+}
+DevBuf b_sel[3];
+extern "C" int lcb_ts_assemble_dev(uint8_t *sig_out, uint8_t *status, const uint8_t *accept, const uint8_t *sigs,
+                                   size_t per_round, size_t k, size_t n_rounds, void *stream) {
+    LOCKED_OR(-1)
+    if (!n_rounds) return 0;
+    if (k == 0 || k > per_round) { set_err("ts assemble: need 0 < k <= shares per round"); return -1; }
+    hipStream_t s = (hipStream_t)stream;
+    size_t ne = n_rounds * k;
+    uint8_t *xs = (uint8_t *)b_sel[0].get(32 * ne), *ys = (uint8_t *)b_sel[1].get(96 * ne);
+    u32 *off = (u32 *)b_sel[2].get(4 * (n_rounds + 1));
+    if (!xs || !ys || !off) { set_err("device allocation failed"); return -1; }
+    lcbk_ts_select(dim3(nblk(n_rounds)), s, accept, sigs, (u32)per_round, (u32)k, (u32)n_rounds, xs, ys, off);
+    return lagrange_enqueue(2, sig_out, status, xs, ys, off, n_rounds, ne, s);
 }
 extern "C" int lcb_g1_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
                                      const uint32_t *off, size_t n) { return lagrange_batch(1, out, status, xs, ys, off, n); }
