@@ -394,16 +394,19 @@ DI void fp12_mul(fp12 &r, const fp12 &a, const fp12 &b) {
     fp6_mul_v(t1, t1);
     fp6_add(r.c0, t0, t1);
 }
+// (c0 + c1 w)^2 = (c0^2 + v c1^2) + 2 c0 c1 w, computed as c0' = (c0 + c1)(c0 + v c1) - t - v t, c1' = 2t
+// (t = c0 c1), updating r in place so only t and s1 are live beside it (register pressure: one Fp12 per lane)
 DI void fp12_sqr(fp12 &r, const fp12 &a) {
-    fp6 t, s0, s1, tv;
-    fp6_mul(t, a.c0, a.c1);
-    fp6_add(s0, a.c0, a.c1);
-    fp6_mul_v(s1, a.c1);
-    fp6_add(s1, s1, a.c0);
-    fp6_mul(s0, s0, s1);
-    fp6_sub(s0, s0, t);
-    fp6_mul_v(tv, t);
-    fp6_sub(r.c0, s0, tv);
+    fp6 t, s1;
+    if (&r != &a) r = a;
+    fp6_mul(t, r.c0, r.c1);
+    fp6_mul_v(s1, r.c1);
+    fp6_add(s1, s1, r.c0);
+    fp6_add(r.c0, r.c0, r.c1);
+    fp6_mul(r.c0, r.c0, s1);
+    fp6_sub(r.c0, r.c0, t);
+    fp6_mul_v(s1, t);
+    fp6_sub(r.c0, r.c0, s1);
     fp6_add(r.c1, t, t);
 }
 DI void fp12_conj(fp12 &r, const fp12 &a) { r.c0 = a.c0; fp6_neg(r.c1, a.c1); }
@@ -420,17 +423,19 @@ DI void fp12_inv(fp12 &r, const fp12 &a) {
 }
 // f *= (A + B v) + (C v) w  — the sparse shape of a Miller-loop line (13 Fp2 muls)
 DI void fp12_mul_line(fp12 &f, const fp2 &A, const fp2 &B, const fp2 &C) {
-    fp6 t0, t1, s;
+    // f0' = f0 l0 + v f1 l1, f1' = (f0 + f1)(l0 + l1) - f0 l0 - f1 l1 with l0 = A + B v, l1 = C v;
+    // f is overwritten in place so only t1 = f1 l1 is live beside it
+    fp6 t1;
     fp2 bc;
-    fp6_mul_01(t0, f.c0, A, B);
     fp6_mul_1(t1, f.c1, C);
-    fp6_add(s, f.c0, f.c1);
+    fp6_add(f.c1, f.c0, f.c1);
+    fp6_mul_01(f.c0, f.c0, A, B);
     fp2_add(bc, B, C);
-    fp6_mul_01(s, s, A, bc);
-    fp6_sub(s, s, t0);
-    fp6_sub(f.c1, s, t1);
+    fp6_mul_01(f.c1, f.c1, A, bc);
+    fp6_sub(f.c1, f.c1, f.c0);
+    fp6_sub(f.c1, f.c1, t1);
     fp6_mul_v(t1, t1);
-    fp6_add(f.c0, t0, t1);
+    fp6_add(f.c0, f.c0, t1);
 }
 // Frobenius maps: element = sum g_k w^k, (g w^k)^p = conj(g) gamma1_k w^k; layout c0 = (g0, g2, g4),
 // c1 = (g1, g3, g5)

@@ -98,10 +98,10 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_miller(const u32 *lines, const uint
 extern "C" __global__ void LCB_BOUNDS k_final_exp_check(const u32 *f_soa, u32 n, uint8_t *accept) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    fp12 f, e;
+    fp12 f;
     fp12_load_soa(f, f_soa, n, i);
-    final_exp(e, f);
-    accept[i] = accept[i] && fp12_is_one(e);
+    final_exp_inplace(f);
+    accept[i] = accept[i] && fp12_is_one(f);
 }
 
 // TPKE.PrivateKey.Decrypt: validity e(G, W) == e(U, H) <=> e(-G, W) e(U, H) == 1; then Ui = x U

@@ -204,33 +204,42 @@ DN void cyc_pow_z(fp12 &r, const fp12 &x) {
     }
     fp12_conj(r, acc);
 }
+// Same exponent and product as mcl's expHardPartBLS12 (y = x^c0 (x^c1)^p (x^c2)^p^2 (x^c3)^p^3), evaluated
+// in an order that folds each Frobenius term into the accumulator as soon as its power is available, so at
+// most five Fp12 values (x, t, u, v, acc) are live at once instead of nine: every live Fp12 beyond the
+// register file is 576 B of per-lane scratch, and scratch traffic is what bounds this kernel.
 DN void fe_hard(fp12 &y, const fp12 &x) {
-    fp12 a0, a1, a2, a3, a4, a5, a6, a7;
-    fp12_conj(a0, x);             // x^-1
-    fp12_cyc_sqr_n(a1, a0);       // x^-2
-    cyc_pow_z(a2, x);             // x^z
-    fp12_cyc_sqr_n(a3, a2);       // x^2z
-    fp12_mul_n(a1, a1, a2);       // x^(z-2)
-    cyc_pow_z(a7, a1);            // x^(z^2-2z)
-    cyc_pow_z(a4, a7);            // x^(z^3-2z^2)
-    cyc_pow_z(a5, a4);            // x^(z^4-2z^3)
-    fp12_mul_n(a3, a3, a5);       // x^(z^4-2z^3+2z)
-    cyc_pow_z(a6, a3);            // x^(z^5-2z^4+2z^2)
-    fp12_conj(a1, a1);            // x^(2-z)
-    fp12_mul_n(a1, a1, a6);
-    fp12_mul_n(a1, a1, x);        // x^c0
-    fp12_mul_n(a3, a3, a0);       // x^c1
-    fp12_frob1_n(a3, a3);
-    fp12_mul_n(a1, a1, a3);
-    fp12_mul_n(a4, a4, a2);       // x^c2
-    fp12_frob2_n(a4, a4);
-    fp12_mul_n(a1, a1, a4);
-    fp12_mul_n(a7, a7, x);        // x^c3
-    fp12_frob3_n(y, a7);
-    fp12_mul_n(y, y, a1);
+    fp12 t, u, v, acc, w;
+    cyc_pow_z(t, x);              // t = x^z
+    fp12_conj(u, x);
+    fp12_cyc_sqr_n(u, u);         // x^-2
+    fp12_mul_n(u, u, t);          // u = x^(z-2)
+    cyc_pow_z(v, u);              // v = x^(z^2-2z)
+    fp12_mul_n(acc, v, x);        // x^c3
+    fp12_frob3_n(acc, acc);
+    cyc_pow_z(v, v);              // v = x^(z^3-2z^2)
+    fp12_mul_n(w, v, t);          // x^c2
+    fp12_frob2_n(w, w);
+    fp12_mul_n(acc, acc, w);
+    cyc_pow_z(v, v);              // v = x^(z^4-2z^3)
+    fp12_cyc_sqr_n(t, t);         // t = x^2z
+    fp12_mul_n(v, v, t);          // v = x^(z^4-2z^3+2z)
+    fp12_conj(w, x);
+    fp12_mul_n(w, w, v);          // x^c1
+    fp12_frob1_n(w, w);
+    fp12_mul_n(acc, acc, w);
+    cyc_pow_z(v, v);              // v = x^(z^5-2z^4+2z^2)
+    fp12_conj(u, u);              // x^(2-z)
+    fp12_mul_n(u, u, v);
+    fp12_mul_n(u, u, x);          // x^c0
+    fp12_mul_n(y, acc, u);
+}
+// in place: fe_easy and fe_hard read their input before writing their output, so no third Fp12 frame
+DN void final_exp_inplace(fp12 &f) {
+    fe_easy(f, f);
+    fe_hard(f, f);
 }
 DN void final_exp(fp12 &r, const fp12 &f) {
-    fp12 t;
-    fe_easy(t, f);
-    fe_hard(r, t);
+    r = f;
+    final_exp_inplace(r);
 }
