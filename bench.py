@@ -188,6 +188,7 @@ def msm_cpu_baseline(pts, scal, n_total, target_s=10.0):
 
 def run_msm(args, nat, torch, dev, rank, world, cpu):
     import torch.distributed as dist
+    from lachain_amd import shard
     lib = nat.lib()
     n = args.msm_points
     stream = torch.cuda.current_stream(dev)
@@ -198,22 +199,21 @@ def run_msm(args, nat, torch, dev, rank, world, cpu):
     d_ok = torch.zeros(n, dtype=torch.uint8, device=dev)
     d_sc = to_dev(torch, dev, scal)
     d_jac = torch.zeros(144, dtype=torch.uint8, device=dev)
-    d_all = torch.zeros(144 * world, dtype=torch.uint8, device=dev)
     d_out = torch.zeros(48, dtype=torch.uint8, device=dev)
     if lib.lcb_g1_to_affine_dev(d_aff.data_ptr(), d_ok.data_ptr(), d_pts48.data_ptr(), n, sh) != 0:
         raise RuntimeError(nat.last_error())
     del d_pts48
     c = lib.lcb_g1_msm_window(n)
 
+    def sum_partials(allp, w):
+        if lib.lcb_g1_jac_sum_dev(d_out.data_ptr(), None, allp.data_ptr(), w, sh) != 0:
+            raise RuntimeError(nat.last_error())
+
     def step():
         if lib.lcb_g1_msm_dev(d_jac.data_ptr(), d_aff.data_ptr(), d_sc.data_ptr(), n, 0, sh) != 0:
             raise RuntimeError(nat.last_error())
-        if world > 1:
-            dist.all_gather_into_tensor(d_all, d_jac)   # RCCL over xGMI: 144 B Jacobian partial per GPU
-        else:
-            d_all.copy_(d_jac)
-        if lib.lcb_g1_jac_sum_dev(d_out.data_ptr(), None, d_all.data_ptr(), world, sh) != 0:
-            raise RuntimeError(nat.last_error())
+        # RCCL over xGMI: all-gather of the 144 B Jacobian partials, summed on the GPU (lachain_amd/shard.py)
+        shard.msm_combine(dist, d_jac, world, sum_partials)
 
     for _ in range(args.warmup):
         step()
