@@ -277,7 +277,8 @@ W_TS = C["C_DEC2"] + C["C_ML2_EVAL"] + C["C_LINES"] + C["C_FE"]   # per share: s
 
 def coin_id(era, agreement, epoch):
     """CommonCoin message: CoinId.ToBytes() = Era || Agreement || Epoch, int64 LE (CoinId.cs:21-24)"""
-    return era.to_bytes(8, "little") + agreement.to_bytes(8, "little") + epoch.to_bytes(8, "little")
+    m64 = (1 << 64) - 1   # C# long.ToBytes(): two's complement, little-endian
+    return b"".join((v & m64).to_bytes(8, "little") for v in (era, agreement, epoch))
 
 
 def ts_inputs(nat, rank, rounds, n, f):
@@ -403,6 +404,167 @@ def run_ts(args, nat, torch, dev, rank, world):
     )
 
 
+# ------------------------------------------------------------------ HoneyBadger epoch replay (BASELINE configs[4])
+def replay_inputs(nat, n, f, n_coins, vlen=32):
+    """One era of an N-node network: N ciphertexts (one proposal per node), every node's decryption share of
+    every ciphertext, n_coins CommonCoin instances with every node's signature share.  One share per
+    ciphertext and one per coin is corrupted (share j carries share j+1's value) so the reject and the
+    first-F+1-valid selection paths run."""
+    d = Drbg(SEED.to_bytes(8, "little") + b"REPLAY")
+    fr = lambda v: v.to_bytes(32, "little")
+
+    def keys():
+        coeffs = [d.fr() for _ in range(f + 1)]
+        poly = lambda x: sum(c * pow(x, i, R) for i, c in enumerate(coeffs)) % R
+        return [poly(i + 1) for i in range(n)], poly(0)
+
+    xs, y_secret = keys()
+    y_keys = nat.mul_batch(1, None, [fr(x) for x in xs], generator=True)
+    (y_pub,) = nat.mul_batch(1, None, [fr(y_secret)], generator=True)
+    rs = [d.fr() for _ in range(n)]
+    us, ts = nat.tpke_encrypt_phase1(y_pub, [fr(r) for r in rs])
+    plain = d.block(vlen * n)
+    vs = [nat.xor_with_hash(ts[c], plain[c * vlen:(c + 1) * vlen]) for c in range(n)]
+    ws = nat.tpke_encrypt_phase2(us, [fr(r) for r in rs], vs)
+    scal = bytearray(32 * n * n)
+    expect_t = np.ones(n * n, dtype=np.uint8)
+    for c in range(n):
+        for j in range(n):
+            sc = xs[j] * rs[c] % R
+            if j == (7 * c) % n:
+                sc = xs[(j + 1) % n] * rs[c] % R
+                expect_t[c * n + j] = 0
+            scal[32 * (c * n + j):32 * (c * n + j) + 32] = fr(sc)
+    shares = nat.mul_batch_raw(1, b"", bytes(scal), n * n, generator=True)
+    sks, shared_sk = keys()
+    pks = nat.mul_batch(1, None, [fr(x) for x in sks] + [fr(shared_sk)], generator=True)
+    msgs = [coin_id(0, m - 1, 0) for m in range(n_coins)]   # root coin (agreement -1) + one per agreement
+    hs = np.frombuffer(b"".join(nat.g2_hash_batch(msgs)), dtype=np.uint8).reshape(n_coins, 96)
+    sk_arr = np.frombuffer(b"".join(fr(x) for x in sks), dtype=np.uint8).reshape(n, 32)
+    sigs = bytearray(nat.mul_batch_raw(2, np.repeat(hs, n, axis=0).tobytes(), np.tile(sk_arr, (n_coins, 1)).tobytes(),
+                                       n_coins * n))
+    expect_s = np.ones(n_coins * n, dtype=np.uint8)
+    for m in range(n_coins):
+        j = (3 * m) % n
+        a, b = m * n + j, m * n + (j + 1) % n
+        sigs[96 * a:96 * a + 96] = sigs[96 * b:96 * b + 96]
+        expect_s[a] = 0
+    return dict(xs=xs, y_keys=b"".join(y_keys), u=b"".join(us), w=b"".join(ws), v=b"".join(vs), plain=plain,
+                shares=shares, expect_t=expect_t, pks=b"".join(pks), msgs=b"".join(msgs), msg_list=msgs,
+                sigs=bytes(sigs), expect_s=expect_s, shared_sk=shared_sk)
+
+
+def run_replay(args, nat, torch, dev, rank, world):
+    """All N nodes' views of one era, views block-partitioned over the ranks (strong
+    scaling: N views in total).  Per view: N ciphertext checks + the node's own partial decryptions, N*N
+    decryption-share verifications, N FullDecrypt combinations (G1 Lagrange, k = F+1), and n_coins coins of
+    N signature-share verifications + G2 Lagrange (k = F+1) + combined-signature check."""
+    import torch.distributed as dist
+    from lachain_amd import shard
+    lib = nat.lib()
+    n = args.replay_n
+    f = (n - 1) // 3
+    n_coins = n + 1
+    v_lo, v_hi = shard.block_range(n, rank, world)
+    V = v_hi - v_lo
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    t_gen = time.perf_counter()
+    inp = replay_inputs(nat, n, f, n_coins)
+    t_gen = time.perf_counter() - t_gen
+    tile = lambda b, reps: to_dev(torch, dev, b).repeat(reps)
+    vlen = len(inp["v"]) // n
+    d_y = to_dev(torch, dev, inp["y_keys"])
+    d_u, d_w, d_v = tile(inp["u"], V), tile(inp["w"], V), tile(inp["v"], V)
+    d_voff = to_dev(torch, dev, np.arange(0, vlen * (V * n + 1), vlen, dtype=np.uint32))
+    x_views = np.frombuffer(b"".join(x.to_bytes(32, "little") for x in inp["xs"][v_lo:v_hi]), dtype=np.uint8)
+    d_x = to_dev(torch, dev, np.repeat(x_views.reshape(V, 32), n, axis=0))   # view v decrypts with its own x
+    d_own = torch.zeros(48 * V * n, dtype=torch.uint8, device=dev)
+    d_own_st = torch.zeros(V * n, dtype=torch.uint8, device=dev)
+    d_ct = to_dev(torch, dev, np.repeat(np.arange(V * n, dtype=np.uint32), n))
+    d_dec = to_dev(torch, dev, np.tile(np.arange(n, dtype=np.uint32), V * n))
+    d_sh = tile(inp["shares"], V)
+    d_acc_t = torch.zeros(V * n * n, dtype=torch.uint8, device=dev)
+    d_uc = torch.zeros(48 * V * n, dtype=torch.uint8, device=dev)
+    d_ucst = torch.zeros(V * n, dtype=torch.uint8, device=dev)
+    nm = V * n_coins
+    d_pks = to_dev(torch, dev, inp["pks"])
+    d_msg = tile(inp["msgs"], V)
+    d_moff = to_dev(torch, dev, np.arange(0, 24 * (nm + 1), 24, dtype=np.uint32))
+    d_sigs = tile(inp["sigs"], V)
+    d_midx = to_dev(torch, dev, np.repeat(np.arange(nm, dtype=np.uint32), n))
+    d_pidx = to_dev(torch, dev, np.tile(np.arange(n, dtype=np.uint32), nm))
+    d_acc_s = torch.zeros(nm * n, dtype=torch.uint8, device=dev)
+    d_comb = torch.zeros(96 * nm, dtype=torch.uint8, device=dev)
+    d_cst = torch.zeros(nm, dtype=torch.uint8, device=dev)
+    d_cacc = torch.zeros(nm, dtype=torch.uint8, device=dev)
+    d_ridx = to_dev(torch, dev, np.arange(nm, dtype=np.uint32))
+    d_shared = to_dev(torch, dev, np.full(nm, n, dtype=np.uint32))
+
+    def step():
+        rc = lib.lcb_tpke_prepare_dev(d_y.data_ptr(), n, d_u.data_ptr(), d_w.data_ptr(), d_v.data_ptr(),
+                                      d_voff.data_ptr(), V * n, sh)
+        rc |= lib.lcb_tpke_partial_decrypt_prepared_dev(d_own.data_ptr(), d_own_st.data_ptr(), d_x.data_ptr(), 1,
+                                                        d_u.data_ptr(), V * n, sh)
+        rc |= lib.lcb_tpke_verify_prepared_dev(d_acc_t.data_ptr(), V * n * n, n, V * n, d_ct.data_ptr(),
+                                               d_dec.data_ptr(), d_sh.data_ptr(), sh)
+        rc |= lib.lcb_tpke_combine_dev(d_uc.data_ptr(), d_ucst.data_ptr(), d_acc_t.data_ptr(), d_sh.data_ptr(), n,
+                                       f + 1, V * n, sh)
+        rc |= lib.lcb_ts_prepare_dev(d_pks.data_ptr(), n + 1, d_msg.data_ptr(), d_moff.data_ptr(), nm, sh)
+        rc |= lib.lcb_ts_verify_prepared_dev(d_acc_s.data_ptr(), nm * n, n + 1, nm, d_sigs.data_ptr(),
+                                             d_midx.data_ptr(), d_pidx.data_ptr(), sh)
+        rc |= lib.lcb_ts_assemble_dev(d_comb.data_ptr(), d_cst.data_ptr(), d_acc_s.data_ptr(), d_sigs.data_ptr(), n,
+                                      f + 1, nm, sh)
+        rc |= lib.lcb_ts_verify_prepared_dev(d_cacc.data_ptr(), nm, n + 1, nm, d_comb.data_ptr(), d_ridx.data_ptr(),
+                                             d_shared.data_ptr(), sh)
+        if rc != 0:
+            raise RuntimeError(nat.last_error())
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.replay_steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    # checks: bitmaps, every view decrypts every ciphertext and assembles every coin, spot values vs oracle
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as o
+    bad = int(np.sum(d_acc_t.cpu().numpy() != np.tile(inp["expect_t"], V)))
+    bad += int(np.sum(d_acc_s.cpu().numpy() != np.tile(inp["expect_s"], V)))
+    bad += int(V * n - d_own_st.cpu().numpy().sum()) + int(V * n - d_ucst.cpu().numpy().sum())
+    bad += int(nm - d_cst.cpu().numpy().sum()) + int(nm - d_cacc.cpu().numpy().sum())
+    uc, own = d_uc.cpu().numpy().tobytes(), d_own.cpu().numpy().tobytes()
+    for c in (0, n - 1):
+        bad += o.xor_with_hash(uc[48 * c:48 * c + 48], inp["v"][vlen * c:vlen * c + vlen]) != \
+            inp["plain"][vlen * c:vlen * c + vlen]
+        exp_own = o.tpke_decrypt(inp["u"][48 * c:48 * c + 48], inp["v"][vlen * c:vlen * c + vlen],
+                                 inp["w"][96 * c:96 * c + 96], o.fr(inp["xs"][v_lo]))
+        bad += own[48 * c:48 * c + 48] != exp_own
+    comb = d_comb.cpu().numpy().tobytes()
+    bad += comb[:96] != o.ts_sign(o.fr(inp["shared_sk"]), inp["msg_list"][0])
+    t = torch.tensor([elapsed, float(bad)], dtype=torch.float64, device=dev)
+    if world > 1:
+        tm = t[:1].clone()
+        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        t[0] = tm[0]
+    if rank != 0:
+        return None
+    elapsed = float(t[0]) / args.replay_steps
+    checks_per_view = n + n * n + n_coins * n + n_coins
+    return dict(metric="HoneyBadgerBFT epoch crypto replay: node views/sec (TPKE + CommonCoin)",
+                value=n / elapsed, unit="views/s", scaling="strong", views_total=n, n=n, f=f, coins=n_coins,
+                pairing_checks_per_s=n * checks_per_view / elapsed, ms_per_era=1e3 * elapsed,
+                steps=args.replay_steps, mismatches=int(t[1]), input_gen_s=t_gen,
+                config=f"configs[4]: all {n} nodes' views of one era (N={n}, F={f}), views block-partitioned over "
+                       f"ranks; per view {checks_per_view} pairing checks, {n} G1 and {n_coins} G2 Lagrange (k={f + 1})")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -419,6 +581,8 @@ def main():
     ap.add_argument("--ts-rounds", type=int, default=65536, help="CommonCoin rounds per rank (0 = skip)")
     ap.add_argument("--ts-n", type=int, default=100)
     ap.add_argument("--ts-steps", type=int, default=1)
+    ap.add_argument("--replay-n", type=int, default=256, help="epoch-replay network size N (0 = skip)")
+    ap.add_argument("--replay-steps", type=int, default=1)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -498,7 +662,9 @@ def main():
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         elapsed = float(tmax[0])
     mismatches_all, shares_all = int(t[1]), int(t[2])
-    msm = ts = None
+    msm = ts = replay = None
+    if args.replay_n > 0:
+        replay = run_replay(args, nat, torch, dev, rank, world)
     if args.ts_rounds > 0:
         ts = run_ts(args, nat, torch, dev, rank, world)
     if args.msm_points > 0:
@@ -532,6 +698,7 @@ def main():
             "input_gen_s": t_gen,
             "msm": msm,
             "threshold_signature": ts,
+            "epoch_replay": replay,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

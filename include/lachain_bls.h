@@ -205,6 +205,20 @@ int lcb_ts_verify_prepared_dev(uint8_t *accept, size_t n, size_t n_pks, size_t n
 int lcb_ts_assemble_dev(uint8_t *sig_out, uint8_t *status, const uint8_t *accept, const uint8_t *sigs,
                         size_t per_round, size_t k, size_t n_rounds, void *stream);
 
+/* TPKE.PrivateKey.Decrypt (TPKE/PrivateKey.cs:21-31) against the workspace of lcb_tpke_prepare_dev (same
+   ciphertexts): ciphertext validity e(G, W) == e(U, H), then U_i = x U.  x_raw: 32-byte LE secrets (device),
+   x_stride = 0 uses one secret for every ciphertext, 1 gives ciphertext c its own secret x_raw[c] (one
+   decrypting node per ciphertext, as in an epoch replay).  ui_out: 48 B per ciphertext (zero when invalid),
+   status[c] = validity.  Device pointers. */
+int lcb_tpke_partial_decrypt_prepared_dev(uint8_t *ui_out, uint8_t *status, const uint8_t *x_raw, size_t x_stride,
+                                          const uint8_t *cts_u, size_t n_cts, void *stream);
+/* TPKE.PublicKey.FullDecrypt's combination step (TPKE/PublicKey.cs:74-84) for whole batches: ciphertext c owns
+   shares [c*per_ct, (c+1)*per_ct) ordered by DecryptorId, with verification bits in accept; the first k
+   accepted shares (x = DecryptorId + 1) are Lagrange-combined in G1: u_out[c] = sum lambda_i U_i (48 B),
+   status[c] = 0 with fewer than k valid shares.  The plaintext is then lcb_xor_with_hash(u, V) on the host. */
+int lcb_tpke_combine_dev(uint8_t *u_out, uint8_t *status, const uint8_t *accept, const uint8_t *shares,
+                         size_t per_ct, size_t k, size_t n_cts, void *stream);
+
 /* PrivateKeyShare.HashAndSign for a batch of (key, message) pairs (ThresholdSignature/PrivateKeyShare.cs:21-27) */
 int lcb_ts_sign(uint8_t *sigs_out, const uint8_t *sks, const uint8_t *msg_data, const uint32_t *msg_off,
                 const uint32_t *msg_idx, size_t n);

@@ -106,8 +106,8 @@ extern "C" __global__ void LCB_BOUNDS k_final_exp_check(const u32 *f_soa, u32 n,
 
 // TPKE.PrivateKey.Decrypt: validity e(G, W) == e(U, H) <=> e(-G, W) e(U, H) == 1; then Ui = x U
 extern "C" __global__ void LCB_BOUNDS k_tpke_partial_decrypt(const u32 *lines, const uint8_t *ct_ok,
-                                                            const uint8_t *cts_u, const fr *x_raw, u32 n_cts,
-                                                            uint8_t *ui_out, uint8_t *status) {
+                                                            const uint8_t *cts_u, const fr *x_raw, u32 x_stride,
+                                                            u32 n_cts, uint8_t *ui_out, uint8_t *status) {
     u32 c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_cts) return;
     g1a U, G;
@@ -123,7 +123,7 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_partial_decrypt(const u32 *lines, c
     status[c] = ok;
     g1 Uj, R;
     jac_from_aff(Uj, U);
-    fr k = *x_raw;
+    fr k = x_raw[(size_t)c * x_stride];
     jac_mul_bits(R, Uj, k.v, 256);
     uint8_t *o = ui_out + 48 * (size_t)c;
     if (ok) g1_compress_jac(o, R);
@@ -153,6 +153,6 @@ extern "C" void lcbk_tpke_miller(dim3 grid, hipStream_t s, const u32 *lines, con
 extern "C" void lcbk_final_exp_check(dim3 grid, hipStream_t s, const u32 *f_soa, u32 n, uint8_t *accept) {
     LCB_LAUNCH(k_final_exp_check, f_soa, n, accept);
 }
-extern "C" void lcbk_tpke_partial_decrypt(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, const uint8_t *cts_u, const void *x_raw, u32 n_cts, uint8_t *ui_out, uint8_t *status) {
-    LCB_LAUNCH(k_tpke_partial_decrypt, lines, ct_ok, cts_u, (const fr *)x_raw, n_cts, ui_out, status);
+extern "C" void lcbk_tpke_partial_decrypt(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, const uint8_t *cts_u, const void *x_raw, u32 x_stride, u32 n_cts, uint8_t *ui_out, uint8_t *status) {
+    LCB_LAUNCH(k_tpke_partial_decrypt, lines, ct_ok, cts_u, (const fr *)x_raw, x_stride, n_cts, ui_out, status);
 }

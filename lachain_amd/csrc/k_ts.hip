@@ -69,35 +69,39 @@ extern "C" __global__ void LCB_BOUNDS k_ts_miller(const u32 *lines, const uint8_
     accept[i] = ok;
 }
 
-// ThresholdSigner.AddShare / PublicKeySet.AssembleSignature selection (ThresholdSigner.cs:62-75,
-// PublicKeySet.cs:34-42): per round, the first k shares (in index order) that passed verification; x = index + 1.
-// A round with fewer than k valid shares gets x = 0 entries, which the Lagrange stage reports as status 0
-// (the reference keeps waiting: AddShare returns without a signature).
-extern "C" __global__ void LCB_BOUNDS k_ts_select(const uint8_t *accept, const uint8_t *sigs, u32 per_round, u32 k,
-                                                 u32 n_rounds, uint8_t *xs, uint8_t *ys, u32 *off) {
+// Share selection for Lagrange assembly, one lane per group (a CommonCoin round, or a TPKE ciphertext):
+//   ThresholdSigner.AddShare -> PublicKeySet.AssembleSignature (ThresholdSigner.cs:62-75, PublicKeySet.cs:34-42)
+//   TPKE.PublicKey.FullDecrypt (TPKE/PublicKey.cs:55-86; shares ordered by DecryptorId)
+// takes the first k shares (in index order) that passed verification, x = index + 1.  A group with fewer than k
+// valid shares gets x = 0 entries, which the Lagrange stage reports as status 0 (the reference keeps waiting
+// for shares / FullDecrypt throws).  pbytes = 48 (G1) or 96 (G2).
+extern "C" __global__ void LCB_BOUNDS k_select_first_valid(const uint8_t *accept, const uint8_t *pts, u32 pbytes,
+                                                          u32 per_group, u32 k, u32 n_groups, uint8_t *xs,
+                                                          uint8_t *ys, u32 *off) {
     u32 r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= n_rounds) return;
+    if (r >= n_groups) return;
     off[r] = r * k;
-    if (r == n_rounds - 1) off[n_rounds] = n_rounds * k;
+    if (r == n_groups - 1) off[n_groups] = n_groups * k;
+    const u32 pw = pbytes / 4;
     u32 cnt = 0;
-    for (u32 i = 0; i < per_round && cnt < k; i++) {
-        size_t src = (size_t)r * per_round + i;
+    for (u32 i = 0; i < per_group && cnt < k; i++) {
+        size_t src = (size_t)r * per_group + i;
         if (!accept[src]) continue;
         size_t dst = (size_t)r * k + cnt;
         u32 *xw = (u32 *)(xs + 32 * dst);
         xw[0] = i + 1;
         for (int q = 1; q < 8; q++) xw[q] = 0;
-        const u32 *sw = (const u32 *)(sigs + 96 * src);
-        u32 *yw = (u32 *)(ys + 96 * dst);
-        for (int q = 0; q < 24; q++) yw[q] = sw[q];
+        const u32 *sw = (const u32 *)(pts + (size_t)pbytes * src);
+        u32 *yw = (u32 *)(ys + (size_t)pbytes * dst);
+        for (u32 q = 0; q < pw; q++) yw[q] = sw[q];
         cnt++;
     }
     for (; cnt < k; cnt++) {
         size_t dst = (size_t)r * k + cnt;
         u32 *xw = (u32 *)(xs + 32 * dst);
-        u32 *yw = (u32 *)(ys + 96 * dst);
+        u32 *yw = (u32 *)(ys + (size_t)pbytes * dst);
         for (int q = 0; q < 8; q++) xw[q] = 0;
-        for (int q = 0; q < 24; q++) yw[q] = 0;
+        for (u32 q = 0; q < pw; q++) yw[q] = 0;
     }
 }
 
@@ -111,6 +115,6 @@ extern "C" void lcbk_ts_verify(dim3 grid, hipStream_t s, const u32 *lines, const
 extern "C" void lcbk_ts_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *msg_ok, const void *pks, u32 n_pks, const uint8_t *sigs, const u32 *msg_idx, const u32 *pk_idx, u32 n, u32 *f_soa, uint8_t *accept) {
     LCB_LAUNCH(k_ts_miller, lines, msg_ok, (const g1a_st *)pks, n_pks, sigs, msg_idx, pk_idx, n, f_soa, accept);
 }
-extern "C" void lcbk_ts_select(dim3 grid, hipStream_t s, const uint8_t *accept, const uint8_t *sigs, u32 per_round, u32 k, u32 n_rounds, uint8_t *xs, uint8_t *ys, u32 *off) {
-    LCB_LAUNCH(k_ts_select, accept, sigs, per_round, k, n_rounds, xs, ys, off);
+extern "C" void lcbk_select_first_valid(dim3 grid, hipStream_t s, const uint8_t *accept, const uint8_t *pts, u32 pbytes, u32 per_group, u32 k, u32 n_groups, uint8_t *xs, uint8_t *ys, u32 *off) {
+    LCB_LAUNCH(k_select_first_valid, accept, pts, pbytes, per_group, k, n_groups, xs, ys, off);
 }

@@ -622,13 +622,26 @@ extern "C" int lcb_tpke_partial_decrypt(uint8_t *ui_out, uint8_t *status, const 
     if (!n_cts) return 0;
     lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), s, du, dw, dv, dvo, (u32)n_cts, lines,
                        ctok, g_orig_cofactor);
-    lcbk_tpke_partial_decrypt(dim3(nblk(n_cts)), s, lines, ctok, du,
-                       dx, (u32)n_cts, dui, dst);
+    lcbk_tpke_partial_decrypt(dim3(nblk(n_cts)), s, lines, ctok, du, dx, 0, (u32)n_cts, dui, dst);
     hipMemcpyAsync(ui_out, dui, 48 * n_cts, hipMemcpyDeviceToHost, s);
     hipMemcpyAsync(status, dst, n_cts, hipMemcpyDeviceToHost, s);
     return sync_check("tpke partial decrypt") ? 0 : -1;
 }
 
+extern "C" int lcb_tpke_partial_decrypt_prepared_dev(uint8_t *ui_out, uint8_t *status, const uint8_t *x_raw,
+                                                     size_t x_stride, const uint8_t *cts_u, size_t n_cts, void *stream) {
+    LOCKED_OR(-1)
+    if (b_lines.cap < (size_t)n_cts * 2 * LCB_LINESET_BYTES || b_ctok.cap < n_cts) {
+        set_err("tpke partial decrypt: workspace not prepared for this batch");
+        return -1;
+    }
+    if (n_cts)
+        lcbk_tpke_partial_decrypt(dim3(nblk(n_cts)), (hipStream_t)stream, (const u32 *)b_lines.p,
+                                  (const uint8_t *)b_ctok.p, cts_u, x_raw, (u32)x_stride, (u32)n_cts, ui_out, status);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { set_err("tpke partial decrypt launch", e); return -1; }
+    return 0;
+}
 extern "C" int lcb_tpke_encrypt_phase1(uint8_t *u_out, uint8_t *t_out, const uint8_t y[48], const uint8_t *r, size_t n) {
     LOCKED_OR(-1)
     if (!n) return 0;
@@ -813,18 +826,27 @@ extern "C" int lcb_g2_lagrange_dev(uint8_t *out, uint8_t *status, const uint8_t 
     return n_problems ? lagrange_enqueue(2, out, status, xs, ys, off, n_problems, n_entries, (hipStream_t)stream) : 0;
 }
 DevBuf b_sel[3];
+static int assemble_enqueue(int g, uint8_t *out, uint8_t *status, const uint8_t *accept, const uint8_t *pts,
+                            size_t per_group, size_t k, size_t n_groups, hipStream_t s) {
+    if (!n_groups) return 0;
+    if (k == 0 || k > per_group) { set_err("assemble: need 0 < k <= shares per group"); return -1; }
+    size_t pb = g == 1 ? 48 : 96, ne = n_groups * k;
+    uint8_t *xs = (uint8_t *)b_sel[0].get(32 * ne), *ys = (uint8_t *)b_sel[1].get(pb * ne);
+    u32 *off = (u32 *)b_sel[2].get(4 * (n_groups + 1));
+    if (!xs || !ys || !off) { set_err("device allocation failed"); return -1; }
+    lcbk_select_first_valid(dim3(nblk(n_groups)), s, accept, pts, (u32)pb, (u32)per_group, (u32)k, (u32)n_groups, xs,
+                            ys, off);
+    return lagrange_enqueue(g, out, status, xs, ys, off, n_groups, ne, s);
+}
 extern "C" int lcb_ts_assemble_dev(uint8_t *sig_out, uint8_t *status, const uint8_t *accept, const uint8_t *sigs,
                                    size_t per_round, size_t k, size_t n_rounds, void *stream) {
     LOCKED_OR(-1)
-    if (!n_rounds) return 0;
-    if (k == 0 || k > per_round) { set_err("ts assemble: need 0 < k <= shares per round"); return -1; }
-    hipStream_t s = (hipStream_t)stream;
-    size_t ne = n_rounds * k;
-    uint8_t *xs = (uint8_t *)b_sel[0].get(32 * ne), *ys = (uint8_t *)b_sel[1].get(96 * ne);
-    u32 *off = (u32 *)b_sel[2].get(4 * (n_rounds + 1));
-    if (!xs || !ys || !off) { set_err("device allocation failed"); return -1; }
-    lcbk_ts_select(dim3(nblk(n_rounds)), s, accept, sigs, (u32)per_round, (u32)k, (u32)n_rounds, xs, ys, off);
-    return lagrange_enqueue(2, sig_out, status, xs, ys, off, n_rounds, ne, s);
+    return assemble_enqueue(2, sig_out, status, accept, sigs, per_round, k, n_rounds, (hipStream_t)stream);
+}
+extern "C" int lcb_tpke_combine_dev(uint8_t *u_out, uint8_t *status, const uint8_t *accept, const uint8_t *shares,
+                                    size_t per_ct, size_t k, size_t n_cts, void *stream) {
+    LOCKED_OR(-1)
+    return assemble_enqueue(1, u_out, status, accept, shares, per_ct, k, n_cts, (hipStream_t)stream);
 }
 extern "C" int lcb_g1_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
                                      const uint32_t *off, size_t n) { return lagrange_batch(1, out, status, xs, ys, off, n); }

@@ -77,3 +77,61 @@ def test_ts_rounds_verify_assemble_combined(nat):
         assert comb[96 * r:96 * r + 96] == o.g2_lagrange(xs, ys)
         assert comb[96 * r:96 * r + 96] == o.ts_sign(o.fr(poly(0)), msgs[r])
     assert d_cacc.cpu().numpy().tolist() == [1, 1, 0, 1]
+
+
+def test_tpke_partial_decrypt_and_combine_dev(nat):
+    """TPKE Decrypt with one secret per ciphertext (lcb_tpke_partial_decrypt_prepared_dev) and FullDecrypt's
+    combination over the first F+1 valid shares (lcb_tpke_combine_dev), checked against the oracle's
+    tpke_decrypt / tpke_full_decrypt (TPKE/PrivateKey.cs:21-31, TPKE/PublicKey.cs:55-86)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    n, f = 4, 1
+    d = Drbg(b"gpu-tpke-combine")
+    coeffs = [d.fr_int() for _ in range(f + 1)]
+    poly = lambda x: sum(c * pow(x, i, R) for i, c in enumerate(coeffs)) % R
+    xs = [poly(i + 1) for i in range(n)]
+    y = o.g1_mul(o.g1_gen(), o.fr(poly(0)))
+    yi = [o.g1_mul(o.g1_gen(), o.fr(x)) for x in xs]
+    plains = [b"epoch replay payload %02d........" % c for c in range(3)]
+    cts = [o.tpke_encrypt(y, p, o.fr(d.fr_int())) for p in plains]
+    # shares[c][j] by DecryptorId; ciphertext 1 loses decryptor 0 (corrupted), ciphertext 2 keeps one valid share
+    shares = [[o.tpke_decrypt(U, V, W, o.fr(xs[j])) for j in range(n)] for (U, V, W) in cts]
+    shares[1][0] = o.g1_add(shares[1][0], o.g1_gen())
+    for j in (0, 1, 2):
+        shares[2][j] = o.g1_add(shares[2][j], o.g1_gen())
+    flat = [s for row in shares for s in row]
+    accept = [o.tpke_verify_share(yi[i % n], *cts[i // n], flat[i]) == 1 for i in range(len(flat))]
+    t = lambda b: torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
+    lib = nat.lib()
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    d_y = t(b"".join(yi))
+    d_u = t(b"".join(c[0] for c in cts))
+    d_w = t(b"".join(c[2] for c in cts))
+    d_v = t(b"".join(c[1] for c in cts))
+    d_voff = t(np.cumsum([0] + [len(c[1]) for c in cts]).astype(np.uint32).tobytes())
+    assert lib.lcb_tpke_prepare_dev(d_y.data_ptr(), n, d_u.data_ptr(), d_w.data_ptr(), d_v.data_ptr(),
+                                    d_voff.data_ptr(), len(cts), sh) == 0
+    # decryptor 2 decrypts ciphertexts 0 and 2, decryptor 3 ciphertext 1
+    who = [2, 3, 2]
+    d_x = t(b"".join(o.fr(xs[j]) for j in who))
+    d_ui = torch.zeros(48 * len(cts), dtype=torch.uint8, device=dev)
+    d_st = torch.zeros(len(cts), dtype=torch.uint8, device=dev)
+    assert lib.lcb_tpke_partial_decrypt_prepared_dev(d_ui.data_ptr(), d_st.data_ptr(), d_x.data_ptr(), 1,
+                                                     d_u.data_ptr(), len(cts), sh) == 0
+    d_acc = t(bytes(int(a) for a in accept))
+    d_sh = t(b"".join(flat))
+    d_out = torch.zeros(48 * len(cts), dtype=torch.uint8, device=dev)
+    d_cst = torch.zeros(len(cts), dtype=torch.uint8, device=dev)
+    assert lib.lcb_tpke_combine_dev(d_out.data_ptr(), d_cst.data_ptr(), d_acc.data_ptr(), d_sh.data_ptr(), n,
+                                    f + 1, len(cts), sh) == 0
+    torch.cuda.synchronize(dev)
+    ui = d_ui.cpu().numpy().tobytes()
+    assert d_st.cpu().numpy().tolist() == [1, 1, 1]
+    for c, j in enumerate(who):
+        assert ui[48 * c:48 * c + 48] == o.tpke_decrypt(*cts[c], o.fr(xs[j]))
+    assert d_cst.cpu().numpy().tolist() == [1, 1, 0]
+    u = d_out.cpu().numpy().tobytes()
+    for c in (0, 1):
+        valid = [j for j in range(n) if accept[c * n + j]][:f + 1]
+        assert o.xor_with_hash(u[48 * c:48 * c + 48], cts[c][1]) == plains[c]
+        assert o.tpke_full_decrypt(cts[c][1], valid, [shares[c][j] for j in valid]) == plains[c]
