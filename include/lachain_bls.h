@@ -219,6 +219,9 @@ int lcb_tpke_partial_decrypt_prepared_dev(uint8_t *ui_out, uint8_t *status, cons
 int lcb_tpke_combine_dev(uint8_t *u_out, uint8_t *status, const uint8_t *accept, const uint8_t *shares,
                          size_t per_ct, size_t k, size_t n_cts, void *stream);
 
+/* device time (ms) of k_tpke_miller and k_final_exp_check in the last split TPKE verify (waits for it) */
+int lcb_tpke_verify_phase_ms(float ms[2]);
+
 /* PrivateKeyShare.HashAndSign for a batch of (key, message) pairs (ThresholdSignature/PrivateKeyShare.cs:21-27) */
 int lcb_ts_sign(uint8_t *sigs_out, const uint8_t *sks, const uint8_t *msg_data, const uint32_t *msg_off,
                 const uint32_t *msg_idx, size_t n);

@@ -188,10 +188,18 @@ DI int fp_legendre(const fp &a) {
 }
 
 // ------------------------------------------------------------------------------------------------ Fp2
+#ifndef LCB_FP2_SPLIT_CHAINS
+// both components in one interleaved pair of carry chains (asm_routines.hpp, tools/gen_asm.py)
+DI void fp2_add(fp2 &r, const fp2 &x, const fp2 &y) { lcb_fp2_add_asm(r.a.v, r.b.v, x.a.v, x.b.v, y.a.v, y.b.v); }
+DI void fp2_sub(fp2 &r, const fp2 &x, const fp2 &y) { lcb_fp2_sub_asm(r.a.v, r.b.v, x.a.v, x.b.v, y.a.v, y.b.v); }
+DI void fp2_dbl(fp2 &r, const fp2 &x) { lcb_fp2_add_asm(r.a.v, r.b.v, x.a.v, x.b.v, x.a.v, x.b.v); }
+DI void fp2_neg(fp2 &r, const fp2 &x) { lcb_fp2_neg_asm(r.a.v, r.b.v, x.a.v, x.b.v); }
+#else
 DI void fp2_add(fp2 &r, const fp2 &x, const fp2 &y) { fp_add(r.a, x.a, y.a); fp_add(r.b, x.b, y.b); }
 DI void fp2_sub(fp2 &r, const fp2 &x, const fp2 &y) { fp_sub(r.a, x.a, y.a); fp_sub(r.b, x.b, y.b); }
 DI void fp2_dbl(fp2 &r, const fp2 &x) { fp_add(r.a, x.a, x.a); fp_add(r.b, x.b, x.b); }
 DI void fp2_neg(fp2 &r, const fp2 &x) { fp_neg(r.a, x.a); fp_neg(r.b, x.b); }
+#endif
 DI void fp2_conj(fp2 &r, const fp2 &x) { r.a = x.a; fp_neg(r.b, x.b); }
 DI bool fp2_is_zero(const fp2 &x) { return fp_is_zero(x.a) && fp_is_zero(x.b); }
 DI bool fp2_eq(const fp2 &x, const fp2 &y) { return fp_eq(x.a, y.a) && fp_eq(x.b, y.b); }
@@ -226,10 +234,14 @@ DI void fp_mul2(fp &r0, const fp &a0, const fp &b0, fp &r1, const fp &a1, const 
     r1 = fp_from_v(x1);
 }
 DI void fp2_mul_xi(fp2 &r, const fp2 &x) { // (a + b i)(1 + i) = (a - b) + (a + b) i
+#ifndef LCB_FP2_SPLIT_CHAINS
+    lcb_fp2_mul_xi_asm(r.a.v, r.b.v, x.a.v, x.b.v);
+#else
     fp t;
     fp_sub(t, x.a, x.b);
     fp_add(r.b, x.a, x.b);
     r.a = t;
+#endif
 }
 DI void fp2_norm(fp &r, const fp2 &x) {
     fp t, u;

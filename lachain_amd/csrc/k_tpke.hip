@@ -74,7 +74,7 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_verify(const u32 *lines, const uint
 // Two-kernel form of k_tpke_verify: the Miller loop parks f in HBM (SoA, 576 B/share) and
 // k_final_exp_check finishes; each kernel gets its own register budget.  accept[i] carries the
 // decompression / key / ciphertext validity from the first kernel to the second.
-extern "C" __global__ void LCB_BOUNDS k_tpke_miller(const u32 *lines, const uint8_t *ct_ok, const g1a_st *keys,
+extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_miller(const u32 *lines, const uint8_t *ct_ok, const g1a_st *keys,
                                                    u32 n_keys, const u32 *ct_idx, const u32 *dec_idx,
                                                    const uint8_t *ui, u32 n, u32 *f_soa, uint8_t *accept) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -95,7 +95,7 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_miller(const u32 *lines, const uint
     accept[i] = ok;
 }
 // accept[i] &= (final_exp(f_i) == 1)
-extern "C" __global__ void LCB_BOUNDS k_final_exp_check(const u32 *f_soa, u32 n, uint8_t *accept) {
+extern "C" __global__ void LCB_PAIR_BOUNDS k_final_exp_check(const u32 *f_soa, u32 n, uint8_t *accept) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     fp12 f;

@@ -45,7 +45,7 @@ extern "C" __global__ void LCB_BOUNDS k_ts_verify(const u32 *lines, const uint8_
 }
 // Split form (default): the 2-pair Miller loop parks f in HBM (word-major SoA) and k_final_exp_check
 // (k_tpke.hip) finishes, so each half gets its own register budget.
-extern "C" __global__ void LCB_BOUNDS k_ts_miller(const u32 *lines, const uint8_t *msg_ok, const g1a_st *pks,
+extern "C" __global__ void LCB_PAIR_BOUNDS k_ts_miller(const u32 *lines, const uint8_t *msg_ok, const g1a_st *pks,
                                                  u32 n_pks, const uint8_t *sigs, const u32 *msg_idx,
                                                  const u32 *pk_idx, u32 n, u32 *f_soa, uint8_t *accept) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;

@@ -6,6 +6,12 @@
 
 #define LCB_BLOCK 256
 #define LCB_BOUNDS __launch_bounds__(LCB_BLOCK, 1)
+// the pairing kernels are issue-latency bound at one wave per SIMD; LCB_PAIR_WAVES=2 trades spills for a second
+// wave per SIMD (256 registers per lane)
+#ifndef LCB_PAIR_WAVES
+#define LCB_PAIR_WAVES 1
+#endif
+#define LCB_PAIR_BOUNDS __launch_bounds__(LCB_BLOCK, LCB_PAIR_WAVES)
 
 // affine point records in device memory
 struct g1a_st { fp x, y; u32 inf, ok, pad[2]; };   // 112 B

@@ -535,6 +535,17 @@ static int tpke_prepare_enqueue(const uint8_t *d_y, size_t n_keys, const uint8_t
     if (e != hipSuccess) { set_err("tpke prepare launch", e); return -1; }
     return 0;
 }
+// HIP events around the two kernels of the last split TPKE verify (lcb_tpke_verify_phase_ms)
+hipEvent_t g_ver_ev[3];
+bool g_ver_ev_ready = false;
+extern "C" int lcb_tpke_verify_phase_ms(float ms[2]) {
+    LOCKED_OR(-1)
+    if (!g_ver_ev_ready) { set_err("tpke verify: no split verify has run"); return -1; }
+    if (hipEventSynchronize(g_ver_ev[2]) != hipSuccess) { set_err("tpke verify: event sync"); return -1; }
+    for (int i = 0; i < 2; i++)
+        if (hipEventElapsedTime(&ms[i], g_ver_ev[i], g_ver_ev[i + 1]) != hipSuccess) ms[i] = -1.0f;
+    return 0;
+}
 static int tpke_verify_prepared_enqueue(uint8_t *d_accept, size_t n, size_t n_keys, size_t n_cts, const uint32_t *d_ct,
                                         const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
     if (b_lines.cap < (size_t)n_cts * 2 * LCB_LINESET_BYTES || b_ctok.cap < n_cts || b_keys.cap < n_keys * LCB_G1A_ST_BYTES) {
@@ -547,9 +558,16 @@ static int tpke_verify_prepared_enqueue(uint8_t *d_accept, size_t n, size_t n_ke
     } else if (n) {
         u32 *f = (u32 *)b_fsoa.get(n * 576);
         if (!f) { set_err("device allocation failed"); return -1; }
+        if (!g_ver_ev_ready) {
+            for (auto &e : g_ver_ev) hipEventCreate(&e);
+            g_ver_ev_ready = true;
+        }
+        hipEventRecord(g_ver_ev[0], s);
         lcbk_tpke_miller(dim3(nblk(n)), s, (const u32 *)b_lines.p, (const uint8_t *)b_ctok.p, b_keys.p, (u32)n_keys,
                          d_ct, d_dec, d_ui, (u32)n, f, d_accept);
+        hipEventRecord(g_ver_ev[1], s);
         lcbk_final_exp_check(dim3(nblk(n)), s, f, (u32)n, d_accept);
+        hipEventRecord(g_ver_ev[2], s);
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) { set_err("tpke verify launch", e); return -1; }

@@ -79,6 +79,7 @@ _SIGS = {
     "lcb_tpke_partial_decrypt_prepared_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_size,
                                                              ctypes.c_void_p, c_size, ctypes.c_void_p]),
     "lcb_tpke_combine_dev": (ctypes.c_int, [ctypes.c_void_p] * 4 + [c_size, c_size, c_size, ctypes.c_void_p]),
+    "lcb_tpke_verify_phase_ms": (ctypes.c_int, [ctypes.POINTER(ctypes.c_float)]),
     "lcb_ts_sign": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u32p, c_u32p, c_size]),
     "lcb_g1_lagrange_batch": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_u32p, c_size]),
     "lcb_g2_lagrange_batch": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_u32p, c_size]),

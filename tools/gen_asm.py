@@ -418,7 +418,127 @@ def gen_neg():
     return inline_fn("lcb_fp_neg_asm", "r = -a mod p", s, N + 1, 1, "a < p -> r < p")
 
 
-INLINE = [gen_add_mod, gen_sub_mod, gen_add_nr, gen_neg]
+# ------------------------------------------------------------------ two-chain (Fp2) add / sub / neg
+# The single-chain forms above pay `s_nop 1` on every carry link: one wave per SIMD has nothing else to issue in
+# the hazard slots.  An Fp2 operation has two independent 12-limb chains; interleaving them (chain A carries in
+# VCC through VOP2, chain B in a compiler-chosen SGPR pair through VOP3) puts the other chain's instruction in
+# the slot and needs only `s_nop 0` per link pair.
+def _chain_add(r, t, a, b, pv, c):
+    e = "e32" if c == "vcc" else "e64"
+    s = [f"v_add_co_u32_{e} %{t[0]}, {c}, %{a[0]}, %{b[0]}"]
+    s += [f"v_addc_co_u32_{e} %{t[j]}, {c}, %{a[j]}, %{b[j]}, {c}" for j in range(1, N)]
+    s += [f"v_sub_co_u32_{e} %{r[0]}, {c}, %{t[0]}, %{pv[0]}"]
+    s += [f"v_subb_co_u32_{e} %{r[j]}, {c}, %{t[j]}, %{pv[j]}, {c}" for j in range(1, N)]
+    if c == "vcc":
+        s += [f"v_cndmask_b32_e32 %{r[j]}, %{r[j]}, %{t[j]}, vcc" for j in range(N)]
+    else:
+        s += [f"v_cndmask_b32_e64 %{r[j]}, %{r[j]}, %{t[j]}, {c}" for j in range(N)]
+    return s
+
+
+def _chain_sub(r, t, a, b, c, neg=False):
+    e = "e32" if c == "vcc" else "e64"
+    mw = t[N]
+    if neg:
+        s = [f"v_sub_co_u32_{e} %{t[0]}, {c}, 0, %{a[0]}"]
+        s += [f"v_subb_co_u32_{e} %{t[j]}, {c}, 0, %{a[j]}, {c}" for j in range(1, N)]
+    else:
+        s = [f"v_sub_co_u32_{e} %{t[0]}, {c}, %{a[0]}, %{b[0]}"]
+        s += [f"v_subb_co_u32_{e} %{t[j]}, {c}, %{a[j]}, %{b[j]}, {c}" for j in range(1, N)]
+    s += [f"v_subb_co_u32_{e} %{mw}, {c}, %{t[0]}, %{t[0]}, {c}"]
+    s += [f"v_and_b32_e32 %{r[j]}, 0x{PL[j]:08x}, %{mw}" for j in range(N)]
+    s += [f"v_add_co_u32_{e} %{r[0]}, {c}, %{t[0]}, %{r[0]}"]
+    s += [f"v_addc_co_u32_{e} %{r[j]}, {c}, %{t[j]}, %{r[j]}, {c}" for j in range(1, N)]
+    return s
+
+
+def _reads_carry(line):
+    return line.rstrip().endswith(", vcc") or line.rstrip().endswith(", %S")
+
+
+_CARRY_OPS = ("v_add_co_u32", "v_addc_co_u32", "v_sub_co_u32", "v_subb_co_u32")
+
+
+def _interleave(la, lb, sop):
+    """Alternate the two chains' instructions; before an instruction that reads its chain's carry, pad with
+    s_nop so that at least 2 wait states separate it from that chain's last carry write (chains of unequal
+    length finish alone with `s_nop 1` links)."""
+    out, last_w = [], {0: None, 1: None}
+    seqs = [list(la), list(lb)]
+    idx = [0, 0]
+    turn = 0
+    while idx[0] < len(seqs[0]) or idx[1] < len(seqs[1]):
+        if idx[turn] >= len(seqs[turn]):
+            turn ^= 1
+        line = seqs[turn][idx[turn]]
+        idx[turn] += 1
+        if _reads_carry(line) and last_w[turn] is not None:
+            gap = len(out) - last_w[turn] - 1          # instructions issued since the carry write
+            if gap < 2:
+                out.append(f"s_nop {1 - gap}")
+        if line.split()[0].startswith(_CARRY_OPS):
+            last_w[turn] = len(out)
+        out.append(line)
+        turn ^= 1
+    return [l.replace("%S", f"%{sop}") for l in out]
+
+
+def inline_fn2(name, comment, n_tmp, n_in, with_p, build, second_operands_swap=False):
+    # operands: rA 0..11, rB 12..23, tA, tB, S; inputs aA, aB, [bA, bB], [p]
+    rA, rB = list(range(N)), list(range(N, 2 * N))
+    tA = list(range(2 * N, 2 * N + n_tmp))
+    tB = list(range(2 * N + n_tmp, 2 * N + 2 * n_tmp))
+    sop = 2 * N + 2 * n_tmp
+    k = sop + 1
+    aA, aB = list(range(k, k + N)), list(range(k + N, k + 2 * N))
+    k += 2 * N
+    bA, bB = (list(range(k, k + N)), list(range(k + N, k + 2 * N))) if n_in == 2 else (None, None)
+    k += 2 * N if n_in == 2 else 0
+    pv = list(range(k, k + N)) if with_p else None
+    if second_operands_swap:   # both chains combine the two inputs: chain A (aA, aB), chain B (aA, aB)
+        body = _interleave(build(rA, tA, aA, aB, pv, "vcc"), build(rB, tB, aA, aB, pv, "%S"), sop)
+    else:
+        body = _interleave(build(rA, tA, aA, bA, pv, "vcc"), build(rB, tB, aB, bB, pv, "%S"), sop)
+    outs = [f'"=&v"(ra[{j}])' for j in range(N)] + [f'"=&v"(rb[{j}])' for j in range(N)]
+    outs += [f'"=&v"(ta[{j}])' for j in range(n_tmp)] + [f'"=&v"(tb[{j}])' for j in range(n_tmp)]
+    outs += ['"=&s"(sc)']
+    ins = [f'"v"(xa[{j}])' for j in range(N)] + [f'"v"(xb[{j}])' for j in range(N)]
+    if n_in == 2:
+        ins += [f'"v"(ya[{j}])' for j in range(N)] + [f'"v"(yb[{j}])' for j in range(N)]
+    if with_p:
+        ins += [f'"v"(0x{PL[j]:08x}u)' for j in range(N)]
+    args = "u32 *ra, u32 *rb, const u32 *xa, const u32 *xb" + (", const u32 *ya, const u32 *yb" if n_in == 2 else "")
+    txt = "\\n\\t".join(body)
+    return (f"// {comment}: both Fp components in one interleaved pair of carry chains\n"
+            f"__device__ __forceinline__ void {name}({args}) {{\n"
+            f"    u32 ta[{n_tmp}], tb[{n_tmp}];\n    unsigned long long sc;\n"
+            f"    asm volatile(\"{txt}\"\n        : {', '.join(outs)}\n        : {', '.join(ins)}\n        : \"vcc\");\n}}\n")
+
+
+def gen_fp2_mul_xi():
+    # (a + b i)(1 + i) = (a - b) + (a + b) i: a subtraction chain and an addition chain side by side
+    def build(r, t, a, b, pv, c):
+        return _chain_sub(r, t, a, b, c) if c == "vcc" else _chain_add(r, t, a, b, pv, c)
+    return inline_fn2("lcb_fp2_mul_xi_asm", "(ra, rb) = (xa - xb, xa + xb) mod p", N + 1, 1, True, build,
+                      second_operands_swap=True)
+
+
+def gen_fp2_add():
+    return inline_fn2("lcb_fp2_add_asm", "(ra, rb) = (xa + ya, xb + yb) mod p", N, 2, True,
+                      lambda r, t, a, b, pv, c: _chain_add(r, t, a, b, pv, c))
+
+
+def gen_fp2_sub():
+    return inline_fn2("lcb_fp2_sub_asm", "(ra, rb) = (xa - ya, xb - yb) mod p", N + 1, 2, False,
+                      lambda r, t, a, b, pv, c: _chain_sub(r, t, a, b, c))
+
+
+def gen_fp2_neg():
+    return inline_fn2("lcb_fp2_neg_asm", "(ra, rb) = (-xa, -xb) mod p", N + 1, 1, False,
+                      lambda r, t, a, b, pv, c: _chain_sub(r, t, a, None, c, neg=True))
+
+
+INLINE = [gen_add_mod, gen_sub_mod, gen_add_nr, gen_neg, gen_fp2_add, gen_fp2_sub, gen_fp2_neg, gen_fp2_mul_xi]
 
 
 def main():
