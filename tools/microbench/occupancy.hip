@@ -29,6 +29,27 @@ extern "C" __global__ void __launch_bounds__(256) k_fp2mul_loop2(u32 *out, int i
     out[i] = acc;
 }
 
+// the Miller-loop arithmetic without memory: 63 x (fp12 square + two sparse line products) per lane, lines held
+// in registers — compared with k_tpke_miller's per-iteration time it separates arithmetic from line loads / spills
+extern "C" __global__ void LCB_BOUNDS k_miller_arith(u32 *out, int iters) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    fp12 f;
+    u32 *fw = (u32 *)&f;
+    for (int j = 0; j < 144; j++) fw[j] = (i * 2654435761u + j * 40503u) & (j % 12 == 11 ? 0x0fffffffu : 0xffffffffu);
+    line l;
+    u32 *lw = (u32 *)&l;
+    for (int j = 0; j < 72; j++) lw[j] = (i + j * 977u) & (j % 12 == 11 ? 0x0fffffffu : 0xffffffffu);
+    fp x1 = f.c0.c0.a, y1 = f.c0.c1.b, x2 = f.c1.c2.a, y2 = f.c1.c0.b;
+    for (int k = 0; k < iters; k++) {
+        fp12_sqr(f, f);
+        fp12_mul_line_at(f, l, x1, y1);
+        fp12_mul_line_at(f, l, x2, y2);
+    }
+    u32 acc = 0;
+    for (int j = 0; j < 144; j++) acc ^= fw[j];
+    out[i] = acc;
+}
+
 int main() {
     hipDeviceProp_t prop;
     hipGetDeviceProperties(&prop, 0);
@@ -57,6 +78,19 @@ int main() {
                    chains, wps, ms, fp2 / (ms * 1e-3), 3 * fp2 / (ms * 1e-3),
                    ms * 1e-3 * 2.4e9 / (iters * chains));
         }
+    }
+    {
+        int blocks = cus;   // one 256-thread block per CU = one wave per SIMD, as k_tpke_miller runs
+        hipLaunchKernelGGL(k_miller_arith, dim3(blocks), dim3(256), 0, 0, d, 2);
+        hipDeviceSynchronize();
+        hipEventRecord(e0);
+        hipLaunchKernelGGL(k_miller_arith, dim3(blocks), dim3(256), 0, 0, d, 63);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        printf("{\"test\": \"miller arithmetic, lines in registers\", \"waves_per_simd\": 1, \"iters\": 63, \"ms\": %.3f, "
+               "\"cycles_per_iter_per_wave\": %.0f}\n", ms, ms * 1e-3 * 2.4e9 / 63);
     }
     return 0;
 }
