@@ -178,6 +178,23 @@ template <class F> DI void jac_mul_bits(jac<F> &r, const jac<F> &p, const u32 *k
     }
     r = acc;
 }
+DN void g1_madd_n(g1 &r, const g1 &p, const fp &qx, const fp &qy) { g1 t; jac_add_aff(t, p, qx, qy); r = t; }
+DN void g2_madd_n(g2 &r, const g2 &p, const fp2 &qx, const fp2 &qy) { g2 t; jac_add_aff(t, p, qx, qy); r = t; }
+DI void grp_madd(g1 &r, const g1 &p, const fp &qx, const fp &qy) { g1_madd_n(r, p, qx, qy); }
+DI void grp_madd(g2 &r, const g2 &p, const fp2 &qx, const fp2 &qy) { g2_madd_n(r, p, qx, qy); }
+// same for an affine base point: mixed additions (G1 7M+4S, G2 the same in Fp2) instead of full Jacobian ones
+// (11M+5S) — the base of every var-base multiplication on the path arrives affine (decompressed)
+template <class F> DI void jac_mul_aff(jac<F> &r, const aff<F> &p, const u32 *k, int nbits) {
+    jac<F> acc;
+    jac_set_inf(acc);
+    if (!p.inf) {
+        for (int i = nbits - 1; i >= 0; i--) {
+            grp_dbl(acc, acc);
+            if ((k[i >> 5] >> (i & 31)) & 1) grp_madd(acc, acc, p.x, p.y);
+        }
+    }
+    r = acc;
+}
 template <class F> DI void jac_mul_u64(jac<F> &r, const jac<F> &p, u64 k) {
     u32 kk[2] = {(u32)k, (u32)(k >> 32)};
     jac_mul_bits(r, p, kk, 64);

@@ -72,10 +72,9 @@ extern "C" __global__ void LCB_BOUNDS k_g1_mul_lanes(const uint8_t *ys, const fr
     if (i >= n_entries) return;
     g1a A;
     bool ok = g1_decompress(A, ys + 48 * (size_t)i);
-    g1 P, R;
-    jac_from_aff(P, A);
+    g1 R;
     fr k = lam_raw[i];
-    jac_mul_bits(R, P, k.v, 255);
+    jac_mul_aff(R, A, k.v, 255);
     out[i] = R;
     ok_out[i] = ok;
 }
@@ -85,10 +84,9 @@ extern "C" __global__ void LCB_BOUNDS k_g2_mul_lanes(const uint8_t *ys, const fr
     if (i >= n_entries) return;
     g2a A;
     bool ok = g2_decompress(A, ys + 96 * (size_t)i);
-    g2 P, R;
-    jac_from_aff(P, A);
+    g2 R;
     fr k = lam_raw[i];
-    jac_mul_bits(R, P, k.v, 255);
+    jac_mul_aff(R, A, k.v, 255);
     out[i] = R;
     ok_out[i] = ok;
 }

@@ -17,9 +17,8 @@ extern "C" __global__ void LCB_BOUNDS k_g1_mul(const uint8_t *pts, int use_gen, 
     const u32 *sw = (const u32 *)(scalars + 32 * (size_t)i);
     for (int j = 0; j < 8; j++) k.v[j] = sw[j];
     ok = ok && fr_raw_lt_r(k);
-    g1 P, R;
-    jac_from_aff(P, A);
-    jac_mul_bits(R, P, k.v, 255);
+    g1 R;
+    jac_mul_aff(R, A, k.v, 255);
     g1_compress_jac(out + 48 * (size_t)i, R);
     if (ok_out) ok_out[i] = ok;
 }
@@ -35,9 +34,8 @@ extern "C" __global__ void LCB_BOUNDS k_g2_mul(const uint8_t *pts, int use_gen, 
     const u32 *sw = (const u32 *)(scalars + 32 * (size_t)i);
     for (int j = 0; j < 8; j++) k.v[j] = sw[j];
     ok = ok && fr_raw_lt_r(k);
-    g2 P, R;
-    jac_from_aff(P, A);
-    jac_mul_bits(R, P, k.v, 255);
+    g2 R;
+    jac_mul_aff(R, A, k.v, 255);
     g2_compress_jac(out + 96 * (size_t)i, R);
     if (ok_out) ok_out[i] = ok;
 }
@@ -66,12 +64,10 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_encrypt1(const uint8_t *ybytes, con
     const u32 *sw = (const u32 *)(rs + 32 * (size_t)i);
     for (int j = 0; j < 8; j++) k.v[j] = sw[j];
     ok = ok && fr_raw_lt_r(k);
-    g1 P, R;
-    jac_from_aff(P, G);
-    jac_mul_bits(R, P, k.v, 255);
+    g1 R;
+    jac_mul_aff(R, G, k.v, 255);
     g1_compress_jac(u_out + 48 * (size_t)i, R);
-    jac_from_aff(P, Y);
-    jac_mul_bits(R, P, k.v, 255);
+    jac_mul_aff(R, Y, k.v, 255);
     g1_compress_jac(t_out + 48 * (size_t)i, R);
     ok_out[i] = ok;
 }

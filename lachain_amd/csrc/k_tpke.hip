@@ -121,10 +121,9 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_partial_decrypt(const u32 *lines, c
     final_exp(e, f);
     ok = ok && fp12_is_one(e);
     status[c] = ok;
-    g1 Uj, R;
-    jac_from_aff(Uj, U);
+    g1 R;
     fr k = x_raw[(size_t)c * x_stride];
-    jac_mul_bits(R, Uj, k.v, 256);
+    jac_mul_aff(R, U, k.v, 256);
     uint8_t *o = ui_out + 48 * (size_t)c;
     if (ok) g1_compress_jac(o, R);
     else {
