@@ -223,6 +223,60 @@ DI void g2_psi2(g2 &r, const g2 &p) {
     r.z = p.z;
 }
 
+// ---------------------------------------------------------------- GLS scalar multiplication in G2
+// psi acts on G2 as multiplication by p = z (mod r), and r = z^4 - z^2 + 1 < u^4 with u = |z|, so a canonical
+// scalar k < r splits into four base-u digits k = d0 + d1 u + d2 u^2 + d3 u^3 (d_i < u < 2^64) and
+// k Q = d0 Q + d1 (-psi Q) + d2 psi^2 Q + d3 (-psi^3 Q): 64 shared doublings instead of 255, same additions.
+DI void u256_divmod_u(u32 q[8], u64 &rem) {   // q <- q / u, rem <- q mod u (binary long division)
+    const u64 u = LCB_Z_ABS;
+    u32 out[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    u64 r = 0;
+    for (int w = 7; w >= 0; w--) {
+        u32 word = q[w], qw = 0;
+        for (int b = 31; b >= 0; b--) {
+            u64 hi = r >> 63;
+            r = (r << 1) | ((word >> b) & 1);
+            u32 take = (hi || r >= u) ? 1u : 0u;
+            if (take) r -= u;
+            qw = (qw << 1) | take;
+        }
+        out[w] = qw;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) q[j] = out[j];
+    rem = r;
+}
+DN void g2_mul_gls(g2 &r, const g2a &A, const u32 k[8]) {
+    g2 acc;
+    jac_set_inf(acc);
+    if (A.inf) { r = acc; return; }
+    u32 q[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) q[j] = k[j];
+    u64 d[4];
+    u256_divmod_u(q, d[0]);
+    u256_divmod_u(q, d[1]);
+    u256_divmod_u(q, d[2]);
+    d[3] = (u64)q[0] | ((u64)q[1] << 32);   // k < u^4: the last quotient fits in 64 bits
+    g2 P, T;
+    jac_from_aff(P, A);
+    g2a Q[4];
+    Q[0] = A;
+    g2_psi(T, P);                                   // psi Q   (z = 1 stays 1: conj(1) = 1)
+    Q[1].x = T.x; fp2_neg(Q[1].y, T.y); Q[1].inf = false;
+    g2_psi2(T, P);                                  // psi^2 Q
+    Q[2].x = T.x; Q[2].y = T.y; Q[2].inf = false;
+    g2_psi(T, T);                                   // psi^3 Q
+    Q[3].x = T.x; fp2_neg(Q[3].y, T.y); Q[3].inf = false;
+    for (int b = 63; b >= 0; b--) {
+        grp_dbl(acc, acc);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            if ((d[i] >> b) & 1) grp_madd(acc, acc, Q[i].x, Q[i].y);
+    }
+    r = acc;
+}
+
 // ---------------------------------------------------------------- serialization
 DI void bytes48_to_raw(fp &raw, const uint8_t *b) { // 4-byte aligned source
     const u32 *w = (const u32 *)b;

@@ -86,7 +86,7 @@ extern "C" __global__ void LCB_BOUNDS k_g2_mul_lanes(const uint8_t *ys, const fr
     bool ok = g2_decompress(A, ys + 96 * (size_t)i);
     g2 R;
     fr k = lam_raw[i];
-    jac_mul_aff(R, A, k.v, 255);
+    g2_mul_gls(R, A, k.v);
     out[i] = R;
     ok_out[i] = ok;
 }
