@@ -177,7 +177,7 @@ def msm_cpu_baseline(pts, scal, n_total, target_s=10.0):
         assert rc == 0
         return time.perf_counter() - t0
 
-    n = 64 * threads
+    n = min(n_total, 64 * threads)
     dt = run(n)
     n = int(min(n_total, max(n, n * target_s / max(dt, 1e-3))))
     dt = run(n)
@@ -316,6 +316,34 @@ def ts_inputs(nat, rank, rounds, n, f):
                 expect=expect, shared_sk=shared_sk, msg_list=msgs)
 
 
+def ts_cpu_baseline(inp, n_total, target_s=10.0):
+    """The oracle's as-reference ValidateSignature (hash + two pairings per share) on host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as o
+    lib = o.lib()
+    threads = max(1, min(16, os.cpu_count() or 1))
+
+    def run(k):
+        acc = ctypes.create_string_buffer(k)
+        mi = np.ascontiguousarray(inp["midx"][:k])
+        pi = np.ascontiguousarray(inp["pidx"][:k])
+        t0 = time.perf_counter()
+        lib.orc_ts_validate_batch(acc, ctypes.c_size_t(k), inp["pks"], inp["sigs"][:96 * k], inp["msgs"],
+                                  inp["moff"].ctypes.data_as(ctypes.c_void_p), mi.ctypes.data_as(ctypes.c_void_p),
+                                  pi.ctypes.data_as(ctypes.c_void_p), threads)
+        dt = time.perf_counter() - t0
+        return dt, int(np.sum(np.frombuffer(acc.raw, dtype=np.uint8) != inp["expect"][:k]))
+
+    k = min(n_total, 4 * threads)
+    dt, _ = run(k)
+    k = int(min(n_total, max(k, k * target_s / max(dt, 1e-3))))
+    dt, mism = run(k)
+    return dict(value=k / dt, unit="share verifications/s", cores=threads, kind="port",
+                sample=f"first {k} shares of the same rounds, oracle/bls.c orc_ts_validate_batch (as-reference: "
+                       f"G2.SetHashOf + two pairings per ValidateSignature), {threads} OpenMP threads, {dt:.1f} s, "
+                       f"{mism} decision mismatches vs expected")
+
+
 def run_ts(args, nat, torch, dev, rank, world):
     import torch.distributed as dist
     lib = nat.lib()
@@ -402,6 +430,7 @@ def run_ts(args, nat, torch, dev, rank, world):
         config=f"configs[2]: {rounds} rounds x N={n} F={f} CommonCoin shares per rank; per round: {n} share "
                f"verifications, G2 Lagrange over the first {f + 1} valid shares, combined-signature verification",
         input_gen_s=t_gen,
+        cpu_baseline=ts_cpu_baseline(inp, rounds * n) if (world == 1 and not args.no_cpu_baseline) else None,
     )
 
 

@@ -1686,6 +1686,22 @@ int orc_ts_sign(uint8_t sigb[96], const uint8_t skb[32], const uint8_t *msg, siz
 }
 
 /* ================================================================== CPU baseline batch */
+/* ThresholdSignature.PublicKey.ValidateSignature for a batch (ThresholdSignature/PublicKey.cs:16-21), as the
+   reference calls it: hash-to-G2 of the message and two pairings per share, OpenMP over shares.  The CPU
+   baseline of the CommonCoin bench line (test infrastructure). */
+int orc_ts_validate_batch(uint8_t *accept, size_t n, const uint8_t *pks, const uint8_t *sigs, const uint8_t *msgs,
+                          const uint32_t *msg_off, const uint32_t *msg_idx, const uint32_t *pk_idx, int nthreads) {
+    orc_init();
+#pragma omp parallel for schedule(dynamic, 4) num_threads(nthreads)
+    for (size_t i = 0; i < n; i++) {
+        uint32_t m = msg_idx[i];
+        int rc = orc_ts_validate(pks + 48 * (size_t)pk_idx[i], sigs + 96 * i, msgs + msg_off[m],
+                                 msg_off[m + 1] - msg_off[m]);
+        accept[i] = (uint8_t)(rc == 1);
+    }
+    return 0;
+}
+
 int orc_tpke_verify_batch(uint8_t *accept, size_t n, const uint8_t *y_keys, const uint8_t *cts_u,
                           const uint8_t *cts_v, size_t vlen, const uint8_t *cts_w, const uint32_t *ct_idx,
                           const uint32_t *dec_idx, const uint8_t *uis, int nthreads) {

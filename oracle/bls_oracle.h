@@ -68,6 +68,8 @@ int orc_g1_lagrange(uint8_t out[48], const uint8_t *xs, const uint8_t *ys, size_
 int orc_g2_lagrange(uint8_t out[96], const uint8_t *xs, const uint8_t *ys, size_t k);
 int orc_fr_lagrange(uint8_t out[32], const uint8_t *xs, const uint8_t *ys, size_t k);
 int orc_fr_eval_poly(uint8_t out[32], const uint8_t *coeffs, size_t n, const uint8_t x[32]);
+int orc_ts_validate_batch(uint8_t *accept, size_t n, const uint8_t *pks, const uint8_t *sigs, const uint8_t *msgs,
+                          const uint32_t *msg_off, const uint32_t *msg_idx, const uint32_t *pk_idx, int nthreads);
 int orc_g1_msm_mt(uint8_t out[48], const uint8_t *pts, const uint8_t *scalars, size_t n, int nthreads);
 int orc_g1_msm(uint8_t out[48], const uint8_t *pts, const uint8_t *scalars, size_t n);
 

@@ -163,3 +163,23 @@ def test_malformed_encodings_rejected():
             break
         x += 1
     assert not o.g1_valid(cand)
+
+
+def test_ts_validate_batch_matches_single():
+    """orc_ts_validate_batch (the CommonCoin CPU baseline) decides like orc_ts_validate share by share."""
+    import ctypes
+    import numpy as np
+    msgs = [b"coin-%d" % r for r in range(2)]
+    sks = [o.fr(7), o.fr(9), o.fr(13)]
+    pks = b"".join(o.g1_mul(o.g1_gen(), s) for s in sks)
+    sigs = [o.ts_sign(sks[i], msgs[r]) for r in range(2) for i in range(3)]
+    sigs[4] = sigs[3]                                   # round 1, share 1 carries share 0's signature
+    moff = np.array([0, len(msgs[0]), len(msgs[0]) + len(msgs[1])], dtype=np.uint32)
+    midx = np.array([0, 0, 0, 1, 1, 1], dtype=np.uint32)
+    pidx = np.array([0, 1, 2, 0, 1, 2], dtype=np.uint32)
+    acc = ctypes.create_string_buffer(6)
+    assert o.lib().orc_ts_validate_batch(acc, ctypes.c_size_t(6), pks, b"".join(sigs), b"".join(msgs),
+                                         moff.ctypes.data_as(ctypes.c_void_p), midx.ctypes.data_as(ctypes.c_void_p),
+                                         pidx.ctypes.data_as(ctypes.c_void_p), 2) == 0
+    single = [o.ts_validate(pks[48 * pidx[i]:48 * pidx[i] + 48], sigs[i], msgs[midx[i]]) == 1 for i in range(6)]
+    assert [b == 1 for b in acc.raw] == single == [True, True, True, True, False, True]
