@@ -11,7 +11,7 @@ CARRY_WRITERS = ("v_add_co_u32", "v_addc_co_u32", "v_sub_co_u32", "v_subb_co_u32
 
 def inline_bodies():
     text = open(HDR).read()
-    for m in re.finditer(r"__device__ __forceinline__ void (lcb_fp2?_\w+_asm)\(.*?asm volatile\(\"(.*?)\"\n", text, re.S):
+    for m in re.finditer(r"__device__ __forceinline__ void (lcb_fp\d?_\w+_asm)\(.*?asm volatile\(\"(.*?)\"\n", text, re.S):
         yield m.group(1), m.group(2).split("\\n\\t")
 
 

@@ -483,6 +483,70 @@ def _interleave(la, lb, sop):
     return [l.replace("%S", f"%{sop}") for l in out]
 
 
+def _interleave_k(seqs, sops):
+    """Round-robin over K chains (chain 0 carries in VCC, chain c > 0 in the SGPR pair operand sops[c-1]),
+    padding with s_nop where a chain's carry read would come < 2 wait states after its carry write."""
+    out, last_w = [], [None] * len(seqs)
+    idx = [0] * len(seqs)
+    c = 0
+    while any(idx[k] < len(seqs[k]) for k in range(len(seqs))):
+        while idx[c] >= len(seqs[c]):
+            c = (c + 1) % len(seqs)
+        line = seqs[c][idx[c]]
+        idx[c] += 1
+        if _reads_carry(line) and last_w[c] is not None:
+            gap = len(out) - last_w[c] - 1
+            if gap < 2:
+                out.append(f"s_nop {1 - gap}")
+        if line.split()[0].startswith(_CARRY_OPS):
+            last_w[c] = len(out)
+        out.append(line if c == 0 else line.replace("%S", f"%{sops[c - 1]}"))
+        c = (c + 1) % len(seqs)
+    return out
+
+
+def inline_fnk(name, comment, K, n_tmp, n_in, with_p, build):
+    """K independent 12-limb chains in one asm block: r_k = op(x_k[, y_k])."""
+    r = [list(range(k * N, (k + 1) * N)) for k in range(K)]
+    base = K * N
+    t = [list(range(base + k * n_tmp, base + (k + 1) * n_tmp)) for k in range(K)]
+    base += K * n_tmp
+    sops = list(range(base, base + K - 1))
+    base += K - 1
+    x = [list(range(base + k * N, base + (k + 1) * N)) for k in range(K)]
+    base += K * N
+    y = [list(range(base + k * N, base + (k + 1) * N)) for k in range(K)] if n_in == 2 else [None] * K
+    base += K * N if n_in == 2 else 0
+    pv = list(range(base, base + N)) if with_p else None
+    body = _interleave_k([build(r[k], t[k], x[k], y[k], pv, "vcc" if k == 0 else "%S") for k in range(K)], sops)
+    outs = [f'"=&v"(r{k}[{j}])' for k in range(K) for j in range(N)]
+    outs += [f'"=&v"(t{k}[{j}])' for k in range(K) for j in range(n_tmp)]
+    outs += [f'"=&s"(sc{k})' for k in range(1, K)]
+    ins = [f'"v"(x{k}[{j}])' for k in range(K) for j in range(N)]
+    if n_in == 2:
+        ins += [f'"v"(y{k}[{j}])' for k in range(K) for j in range(N)]
+    if with_p:
+        ins += [f'"v"(0x{PL[j]:08x}u)' for j in range(N)]
+    args = ", ".join([f"u32 *r{k}" for k in range(K)] + [f"const u32 *x{k}" for k in range(K)] +
+                     ([f"const u32 *y{k}" for k in range(K)] if n_in == 2 else []))
+    decl = "".join(f"    u32 t{k}[{n_tmp}];\n" for k in range(K))
+    decl += "    unsigned long long " + ", ".join(f"sc{k}" for k in range(1, K)) + ";\n"
+    txt = "\\n\\t".join(body)
+    return (f"// {comment}: {K} independent carry chains interleaved in one block\n"
+            f"__device__ __forceinline__ void {name}({args}) {{\n{decl}"
+            f"    asm volatile(\"{txt}\"\n        : {', '.join(outs)}\n        : {', '.join(ins)}\n        : \"vcc\");\n}}\n")
+
+
+def gen_fp3_add():
+    return inline_fnk("lcb_fp3_add_asm", "r_k = x_k + y_k mod p, k = 0..2", 3, N, 2, True,
+                      lambda r, t, a, b, pv, c: _chain_add(r, t, a, b, pv, c))
+
+
+def gen_fp3_sub():
+    return inline_fnk("lcb_fp3_sub_asm", "r_k = x_k - y_k mod p, k = 0..2", 3, N + 1, 2, False,
+                      lambda r, t, a, b, pv, c: _chain_sub(r, t, a, b, c))
+
+
 def inline_fn2(name, comment, n_tmp, n_in, with_p, build, second_operands_swap=False):
     # operands: rA 0..11, rB 12..23, tA, tB, S; inputs aA, aB, [bA, bB], [p]
     rA, rB = list(range(N)), list(range(N, 2 * N))
@@ -538,7 +602,7 @@ def gen_fp2_neg():
                       lambda r, t, a, b, pv, c: _chain_sub(r, t, a, None, c, neg=True))
 
 
-INLINE = [gen_add_mod, gen_sub_mod, gen_add_nr, gen_neg, gen_fp2_add, gen_fp2_sub, gen_fp2_neg, gen_fp2_mul_xi]
+INLINE = [gen_add_mod, gen_sub_mod, gen_add_nr, gen_neg, gen_fp2_add, gen_fp2_sub, gen_fp2_neg, gen_fp2_mul_xi, gen_fp3_add, gen_fp3_sub]
 
 
 def main():
