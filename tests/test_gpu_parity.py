@@ -261,3 +261,32 @@ def test_msm_known_answer(nat):
     got = nat.g1_msm(pts, [o.fr(v) for v in s])
     expect = o.g1_mul(o.g1_gen(), o.fr(sum(x * y for x, y in zip(a, s))))
     assert got == expect
+
+
+def test_decompression_validity_matches_oracle(mcl):
+    """G1/G2.FromBytes accept exactly the encodings the oracle accepts: random x under a valid point's flag
+    bits exercises the square-root (Fp exponentiation) path on residues and non-residues alike, plus x >= p."""
+    d = Drbg(b"gpu-decompress")
+    for P, size, gen, valid in ((mcl.G1, 48, o.g1_gen(), o.g1_valid), (mcl.G2, 96, o.g2_gen(), o.g2_valid)):
+        encs = [gen, o.g1_mul(gen, d.fr()) if size == 48 else o.g2_mul(gen, d.fr())]
+        for i in range(24):
+            b = bytearray(d.bytes(size))
+            b[47] = (b[47] & 0x1f) | (gen[47] & 0xe0)   # keep the flag bits of a valid encoding
+            if size == 96:
+                b[95] = (b[95] & 0x1f) | (gen[95] & 0xe0)
+            if i == 0:
+                b[47] |= 0x1f                             # x >= p
+            encs.append(bytes(b))
+        n_ok = 0
+        for b in encs:
+            want = valid(b)
+            try:
+                got = P.FromBytes(b)
+                ok = True
+            except ValueError:
+                ok = False
+            assert ok == want, (P.__name__, b.hex())
+            if ok:
+                n_ok += 1
+                assert got.ToBytes() == b
+        assert n_ok >= 2
