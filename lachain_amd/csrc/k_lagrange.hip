@@ -74,7 +74,7 @@ extern "C" __global__ void LCB_BOUNDS k_g1_mul_lanes(const uint8_t *ys, const fr
     bool ok = g1_decompress(A, ys + 48 * (size_t)i);
     g1 R;
     fr k = lam_raw[i];
-    jac_mul_aff(R, A, k.v, 255);
+    g1_mul_glv(R, A, k.v);
     out[i] = R;
     ok_out[i] = ok;
 }
