@@ -17,10 +17,18 @@
  * (mcl serialize format; pinned by test/Lachain.CryptoTest/SerializationTest.cs).
  *
  * Errors never cross the ABI as exceptions: int functions return 0 on success and -1 on failure,
- * (de)serializers return the number of bytes written/read or 0.  Every entry point is re-entrant;
- * GPU submission is serialized per device by an internal lock.  All arithmetic runs on the GPU; if no
+ * (de)serializers return the number of bytes written/read or 0.  All arithmetic runs on the GPU; if no
  * gfx950 device can be opened, mclBn_init returns -1 and every other call fails loudly (there is no
  * CPU fallback).
+ *
+ * Threading (callers: one thread per consensus protocol, src/Lachain.Consensus/AbstractProtocol.cs:46-47):
+ * every entry point may be called concurrently from any number of threads.  Single-element mcl operations are
+ * synchronous and serialized by an internal lock.  Batch calls run in an execution context (lcb_ctx) that owns
+ * their device workspaces: the lcb_ctx_* forms take one explicitly, the other forms use the calling thread's
+ * own implicit context (one for the *_dev entry points, another for the synchronous host-pointer ones).  Work
+ * of one context runs in the order it was enqueued whatever stream it is enqueued on, TPKE and threshold-
+ * signature workspaces are separate, and a *_prepared call fails unless its batch shape is the one prepared
+ * in the same context.  lcb_set_device applies to every calling thread.
  */
 #ifndef LACHAIN_BLS_H
 #define LACHAIN_BLS_H
@@ -162,8 +170,9 @@ int lcb_tpke_verify_shares_dev(uint8_t *accept, size_t n_shares, const uint8_t *
 
 /* The two stages of lcb_tpke_verify_shares_dev, for callers that pipeline or time them separately:
    prepare = verification-key decompression + per-ciphertext H(U||V) and Miller-line precomputation into
-   the library's device workspace; verify = the per-share pairing-product check against that workspace.
-   The workspace stays valid until the next TPKE call on this device. */
+   the calling thread's TPKE workspace; verify = the per-share pairing-product check against that workspace
+   (n_keys and n_cts must be the prepared ones).  The workspace stays valid until the next TPKE prepare in the
+   same context (lcb_ctx_* forms below for explicit contexts). */
 int lcb_tpke_prepare_dev(const uint8_t *y_keys, size_t n_keys, const uint8_t *cts_u, const uint8_t *cts_w,
                          const uint8_t *v_data, const uint32_t *v_off, size_t n_cts, void *stream);
 int lcb_tpke_verify_prepared_dev(uint8_t *accept, size_t n_shares, size_t n_keys, size_t n_cts,
@@ -221,6 +230,49 @@ int lcb_tpke_combine_dev(uint8_t *u_out, uint8_t *status, const uint8_t *accept,
 
 /* device time (ms) of k_tpke_miller and k_final_exp_check in the last split TPKE verify (waits for it) */
 int lcb_tpke_verify_phase_ms(float ms[2]);
+
+/* ------------------------------------------------------------------ explicit execution contexts
+   A context owns the device workspaces of the prepare/verify, assembly, Lagrange and MSM calls below
+   (the context-less forms above use the calling thread's implicit context).  ctx == NULL selects that implicit
+   context.  A context may be shared by threads (calls on it are serialized) and its work executes in enqueue
+   order across streams; lcb_ctx_synchronize waits for all of it. */
+typedef struct lcb_ctx lcb_ctx;
+lcb_ctx *lcb_ctx_create(void);
+void lcb_ctx_destroy(lcb_ctx *ctx);
+int lcb_ctx_synchronize(lcb_ctx *ctx);
+int lcb_ctx_tpke_prepare_dev(lcb_ctx *ctx, const uint8_t *y_keys, size_t n_keys, const uint8_t *cts_u,
+                             const uint8_t *cts_w, const uint8_t *v_data, const uint32_t *v_off, size_t n_cts,
+                             void *stream);
+int lcb_ctx_tpke_verify_prepared_dev(lcb_ctx *ctx, uint8_t *accept, size_t n_shares, size_t n_keys, size_t n_cts,
+                                     const uint32_t *ct_idx, const uint32_t *dec_idx, const uint8_t *ui, void *stream);
+int lcb_ctx_tpke_partial_decrypt_prepared_dev(lcb_ctx *ctx, uint8_t *ui_out, uint8_t *status, const uint8_t *x_raw,
+                                              size_t x_stride, const uint8_t *cts_u, size_t n_cts, void *stream);
+int lcb_ctx_tpke_combine_dev(lcb_ctx *ctx, uint8_t *u_out, uint8_t *status, const uint8_t *accept,
+                             const uint8_t *shares, size_t per_ct, size_t k, size_t n_cts, void *stream);
+int lcb_ctx_tpke_verify_phase_ms(lcb_ctx *ctx, float ms[2]);
+int lcb_ctx_ts_prepare_dev(lcb_ctx *ctx, const uint8_t *pks, size_t n_pks, const uint8_t *msg_data,
+                           const uint32_t *msg_off, size_t n_msgs, void *stream);
+int lcb_ctx_ts_verify_prepared_dev(lcb_ctx *ctx, uint8_t *accept, size_t n, size_t n_pks, size_t n_msgs,
+                                   const uint8_t *sigs, const uint32_t *msg_idx, const uint32_t *pk_idx, void *stream);
+int lcb_ctx_ts_assemble_dev(lcb_ctx *ctx, uint8_t *sig_out, uint8_t *status, const uint8_t *accept,
+                            const uint8_t *sigs, size_t per_round, size_t k, size_t n_rounds, void *stream);
+int lcb_ctx_g1_lagrange_dev(lcb_ctx *ctx, uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
+                            const uint32_t *off, size_t n_problems, size_t n_entries, void *stream);
+int lcb_ctx_g2_lagrange_dev(lcb_ctx *ctx, uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
+                            const uint32_t *off, size_t n_problems, size_t n_entries, void *stream);
+int lcb_ctx_g1_msm_dev(lcb_ctx *ctx, void *out_jac, const void *points_aff, const uint8_t *scalars, size_t n,
+                       int window_bits, void *stream);
+int lcb_ctx_g1_msm_phase_ms(lcb_ctx *ctx, float *ms, int n_phases);
+
+/* ------------------------------------------------------------------ CommonCoin consumers (row a13)
+   The combined signature's serialized bytes feed two consensus decisions:
+   CoinResult.Parity = popcount(XOR of all bytes) is odd   (src/Lachain.Consensus/CommonCoin/CoinResult.cs:16-20)
+   block nonce = little-endian u64 of the 8-byte XOR fold   (src/Lachain.Consensus/RootProtocol/RootProtocol.cs:316-322)
+   Host forms take any byte length; the device form folds n 96-byte signatures (8-byte aligned) in one launch,
+   either output nullable. */
+int lcb_coin_parity(const uint8_t *sig_bytes, size_t len);
+uint64_t lcb_coin_nonce(const uint8_t *sig_bytes, size_t len);
+int lcb_coin_fold_dev(uint8_t *parity, uint64_t *nonce, const uint8_t *sigs96, size_t n, void *stream);
 
 /* PrivateKeyShare.HashAndSign for a batch of (key, message) pairs (ThresholdSignature/PrivateKeyShare.cs:21-27) */
 int lcb_ts_sign(uint8_t *sigs_out, const uint8_t *sks, const uint8_t *msg_data, const uint32_t *msg_off,

@@ -277,6 +277,27 @@ DN void g2_mul_gls(g2 &r, const g2a &A, const u32 k[8]) {
     r = acc;
 }
 
+// G2 membership (Scott, "A note on group membership tests for G1, G2 and GT on BLS pairing-friendly curves"):
+// an on-curve point P of E' lies in G2 iff psi(P) == [z]P = -[|z|]P.  One 64-bit ladder (63 doublings, 5 mixed
+// additions) decides whether the GLS decomposition (valid only on G2) may be used.
+DN bool g2_in_subgroup(const g2a &A) {
+    if (A.inf) return true;
+    g2 P, T, S;
+    jac_from_aff(P, A);
+    const u32 u[2] = {(u32)LCB_Z_ABS, (u32)(LCB_Z_ABS >> 32)};
+    jac_mul_aff(T, A, u, 64);     // [|z|] P
+    if (jac_is_inf(T)) return false;
+    g2_psi(S, P);                 // psi(P), affine (Z stays 1)
+    fp2 z2, z3, t, ny;
+    fp2_sqr(z2, T.z);
+    fp2_mul(z3, z2, T.z);
+    fp2_mul(t, S.x, z2);
+    bool okx = fp2_eq(t, T.x);
+    fp2_mul(t, S.y, z3);
+    fp2_neg(ny, T.y);
+    return okx && fp2_eq(t, ny);
+}
+
 // ---------------------------------------------------------------- GLV scalar multiplication in G1
 // phi(x, y) = (beta x, y) acts on the r-torsion as lambda = z^2 - 1 = u^2 - 1.  Two base-u digits and the
 // quotient give k = d0 + d1 u + a1 u^2 = (a0 + a1) + a1 lambda with a0 = d0 + d1 u, so

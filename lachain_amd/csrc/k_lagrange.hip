@@ -72,9 +72,11 @@ extern "C" __global__ void LCB_BOUNDS k_g1_mul_lanes(const uint8_t *ys, const fr
     if (i >= n_entries) return;
     g1a A;
     bool ok = g1_decompress(A, ys + 48 * (size_t)i);
+    // plain double-and-add on the canonical integer lambda: exact for every on-curve input, including points
+    // outside the r-torsion that G1.FromBytes accepts (GLV would be wrong for their cofactor component)
     g1 R;
     fr k = lam_raw[i];
-    g1_mul_glv(R, A, k.v);
+    jac_mul_aff(R, A, k.v, 256);
     out[i] = R;
     ok_out[i] = ok;
 }
@@ -84,9 +86,12 @@ extern "C" __global__ void LCB_BOUNDS k_g2_mul_lanes(const uint8_t *ys, const fr
     if (i >= n_entries) return;
     g2a A;
     bool ok = g2_decompress(A, ys + 96 * (size_t)i);
+    // GLS (64 shared doublings) only for points proven to lie in G2 (psi(P) == [z]P, 64 doublings); any other
+    // on-curve input takes the plain ladder, so the result equals the oracle's for every input
     g2 R;
     fr k = lam_raw[i];
-    g2_mul_gls(R, A, k.v);
+    if (g2_in_subgroup(A)) g2_mul_gls(R, A, k.v);
+    else jac_mul_aff(R, A, k.v, 256);
     out[i] = R;
     ok_out[i] = ok;
 }

@@ -50,14 +50,16 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_ct_prepare(const uint8_t *cts_u, co
     ct_ok[c] = ok;
 }
 
-extern "C" __global__ void LCB_BOUNDS k_tpke_verify(const u32 *lines, const uint8_t *ct_ok, const g1a_st *keys,
-                                                   u32 n_keys, const u32 *ct_idx, const u32 *dec_idx,
-                                                   const uint8_t *ui, u32 n, uint8_t *accept) {
+extern "C" __global__ void LCB_BOUNDS k_tpke_verify(const u32 *lines, const uint8_t *ct_ok, u32 n_cts,
+                                                   const g1a_st *keys, u32 n_keys, const u32 *ct_idx,
+                                                   const u32 *dec_idx, const uint8_t *ui, u32 n, uint8_t *accept) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u32 c = ct_idx[i], d = dec_idx[i];
     g1a Ui, Y;
-    bool ok = d < n_keys && ct_ok[c];
+    bool ok = d < n_keys && c < n_cts;   // an out-of-range index rejects the share (and is clamped)
+    c = c < n_cts ? c : 0;
+    ok = ok && ct_ok[c];
     ok = g1_decompress(Ui, ui + 48 * (size_t)i) && ok;
     g1a_st ks = keys[d < n_keys ? d : 0];
     ok = ok && ks.ok;
@@ -74,14 +76,17 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_verify(const u32 *lines, const uint
 // Two-kernel form of k_tpke_verify: the Miller loop parks f in HBM (SoA, 576 B/share) and
 // k_final_exp_check finishes; each kernel gets its own register budget.  accept[i] carries the
 // decompression / key / ciphertext validity from the first kernel to the second.
-extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_miller(const u32 *lines, const uint8_t *ct_ok, const g1a_st *keys,
-                                                   u32 n_keys, const u32 *ct_idx, const u32 *dec_idx,
-                                                   const uint8_t *ui, u32 n, u32 *f_soa, uint8_t *accept) {
+extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_miller(const u32 *lines, const uint8_t *ct_ok, u32 n_cts,
+                                                         const g1a_st *keys, u32 n_keys, const u32 *ct_idx,
+                                                         const u32 *dec_idx, const uint8_t *ui, u32 n, u32 *f_soa,
+                                                         uint8_t *accept) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u32 c = ct_idx[i], d = dec_idx[i];
     g1a Ui, Y;
-    bool ok = d < n_keys && ct_ok[c];
+    bool ok = d < n_keys && c < n_cts;   // an out-of-range index rejects the share (and is clamped)
+    c = c < n_cts ? c : 0;
+    ok = ok && ct_ok[c];
     ok = g1_decompress(Ui, ui + 48 * (size_t)i) && ok;
     g1a_st ks = keys[d < n_keys ? d : 0];
     ok = ok && ks.ok;
@@ -143,11 +148,11 @@ extern "C" void lcbk_g2_decompress(dim3 grid, hipStream_t s, const uint8_t *in, 
 extern "C" void lcbk_tpke_ct_prepare(dim3 grid, hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data, const u32 *v_off, u32 n_cts, u32 *lines, uint8_t *ct_ok, int orig_cof) {
     LCB_LAUNCH(k_tpke_ct_prepare, cts_u, cts_w, v_data, v_off, n_cts, lines, ct_ok, orig_cof);
 }
-extern "C" void lcbk_tpke_verify(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, uint8_t *accept) {
-    LCB_LAUNCH(k_tpke_verify, lines, ct_ok, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, accept);
+extern "C" void lcbk_tpke_verify(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, uint8_t *accept) {
+    LCB_LAUNCH(k_tpke_verify, lines, ct_ok, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, accept);
 }
-extern "C" void lcbk_tpke_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, u32 *f_soa, uint8_t *accept) {
-    LCB_LAUNCH(k_tpke_miller, lines, ct_ok, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, f_soa, accept);
+extern "C" void lcbk_tpke_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, u32 *f_soa, uint8_t *accept) {
+    LCB_LAUNCH(k_tpke_miller, lines, ct_ok, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, f_soa, accept);
 }
 extern "C" void lcbk_final_exp_check(dim3 grid, hipStream_t s, const u32 *f_soa, u32 n, uint8_t *accept) {
     LCB_LAUNCH(k_final_exp_check, f_soa, n, accept);

@@ -20,7 +20,7 @@ extern "C" __global__ void LCB_BOUNDS k_ts_msg_prepare(const uint8_t *msg_data, 
     msg_ok[m] = ok;
 }
 // ValidateSignature: e(PK, H) == e(G, sig) <=> e(PK, H) e(-G, sig) == 1
-extern "C" __global__ void LCB_BOUNDS k_ts_verify(const u32 *lines, const uint8_t *msg_ok, const g1a_st *pks,
+extern "C" __global__ void LCB_BOUNDS k_ts_verify(const u32 *lines, const uint8_t *msg_ok, u32 n_msgs, const g1a_st *pks,
                                                  u32 n_pks, const uint8_t *sigs, const u32 *msg_idx,
                                                  const u32 *pk_idx, u32 n, uint8_t *accept) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -28,7 +28,9 @@ extern "C" __global__ void LCB_BOUNDS k_ts_verify(const u32 *lines, const uint8_
     u32 m = msg_idx[i], k = pk_idx[i];
     g2a S;
     g1a PK, G;
-    bool ok = k < n_pks && msg_ok[m];
+    bool ok = k < n_pks && m < n_msgs;   // an out-of-range index rejects the share (and is clamped)
+    m = m < n_msgs ? m : 0;
+    ok = ok && msg_ok[m];
     ok = g2_decompress(S, sigs + 96 * (size_t)i) && ok;
     g1a_st ps = pks[k < n_pks ? k : 0];
     ok = ok && ps.ok;
@@ -45,7 +47,7 @@ extern "C" __global__ void LCB_BOUNDS k_ts_verify(const u32 *lines, const uint8_
 }
 // Split form (default): the 2-pair Miller loop parks f in HBM (word-major SoA) and k_final_exp_check
 // (k_tpke.hip) finishes, so each half gets its own register budget.
-extern "C" __global__ void LCB_PAIR_BOUNDS k_ts_miller(const u32 *lines, const uint8_t *msg_ok, const g1a_st *pks,
+extern "C" __global__ void LCB_PAIR_BOUNDS k_ts_miller(const u32 *lines, const uint8_t *msg_ok, u32 n_msgs, const g1a_st *pks,
                                                  u32 n_pks, const uint8_t *sigs, const u32 *msg_idx,
                                                  const u32 *pk_idx, u32 n, u32 *f_soa, uint8_t *accept) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -53,7 +55,9 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_ts_miller(const u32 *lines, const u
     u32 m = msg_idx[i], k = pk_idx[i];
     g2a S;
     g1a PK, G;
-    bool ok = k < n_pks && msg_ok[m];
+    bool ok = k < n_pks && m < n_msgs;   // an out-of-range index rejects the share (and is clamped)
+    m = m < n_msgs ? m : 0;
+    ok = ok && msg_ok[m];
     ok = g2_decompress(S, sigs + 96 * (size_t)i) && ok;
     g1a_st ps = pks[k < n_pks ? k : 0];
     ok = ok && ps.ok;
@@ -105,16 +109,36 @@ extern "C" __global__ void LCB_BOUNDS k_select_first_valid(const uint8_t *accept
     }
 }
 
+// CommonCoin consumers of the combined signature bytes (one lane per coin):
+//   CoinResult.Parity  = popcount(XOR of all 96 bytes) odd        (src/Lachain.Consensus/CommonCoin/CoinResult.cs:16-20)
+//   GetNonceFromCoin   = 8-byte XOR fold of the 96 bytes, LE u64  (src/Lachain.Consensus/RootProtocol/RootProtocol.cs:316-322)
+extern "C" __global__ void LCB_BOUNDS k_coin_fold(const uint8_t *sigs, u32 n, uint8_t *parity, uint64_t *nonce) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint2 *w = (const uint2 *)(sigs + 96 * (size_t)i);
+    uint2 acc = make_uint2(0, 0);
+#pragma unroll
+    for (int q = 0; q < 12; q++) { uint2 v = w[q]; acc.x ^= v.x; acc.y ^= v.y; }
+    u32 b = acc.x ^ acc.y;
+    b ^= b >> 16;
+    b ^= b >> 8;                     // XOR of all 96 bytes in the low byte
+    if (parity) parity[i] = __popc(b & 0xffu) & 1;
+    if (nonce) nonce[i] = (uint64_t)acc.x | ((uint64_t)acc.y << 32);
+}
+
 // ---------------------------------------------------------------- host launch wrappers
 extern "C" void lcbk_ts_msg_prepare(dim3 grid, hipStream_t s, const uint8_t *msg_data, const u32 *msg_off, u32 n_msgs, u32 *lines, uint8_t *msg_ok, int orig_cof) {
     LCB_LAUNCH(k_ts_msg_prepare, msg_data, msg_off, n_msgs, lines, msg_ok, orig_cof);
 }
-extern "C" void lcbk_ts_verify(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *msg_ok, const void *pks, u32 n_pks, const uint8_t *sigs, const u32 *msg_idx, const u32 *pk_idx, u32 n, uint8_t *accept) {
-    LCB_LAUNCH(k_ts_verify, lines, msg_ok, (const g1a_st *)pks, n_pks, sigs, msg_idx, pk_idx, n, accept);
+extern "C" void lcbk_ts_verify(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *msg_ok, u32 n_msgs, const void *pks, u32 n_pks, const uint8_t *sigs, const u32 *msg_idx, const u32 *pk_idx, u32 n, uint8_t *accept) {
+    LCB_LAUNCH(k_ts_verify, lines, msg_ok, n_msgs, (const g1a_st *)pks, n_pks, sigs, msg_idx, pk_idx, n, accept);
 }
-extern "C" void lcbk_ts_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *msg_ok, const void *pks, u32 n_pks, const uint8_t *sigs, const u32 *msg_idx, const u32 *pk_idx, u32 n, u32 *f_soa, uint8_t *accept) {
-    LCB_LAUNCH(k_ts_miller, lines, msg_ok, (const g1a_st *)pks, n_pks, sigs, msg_idx, pk_idx, n, f_soa, accept);
+extern "C" void lcbk_ts_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *msg_ok, u32 n_msgs, const void *pks, u32 n_pks, const uint8_t *sigs, const u32 *msg_idx, const u32 *pk_idx, u32 n, u32 *f_soa, uint8_t *accept) {
+    LCB_LAUNCH(k_ts_miller, lines, msg_ok, n_msgs, (const g1a_st *)pks, n_pks, sigs, msg_idx, pk_idx, n, f_soa, accept);
 }
 extern "C" void lcbk_select_first_valid(dim3 grid, hipStream_t s, const uint8_t *accept, const uint8_t *pts, u32 pbytes, u32 per_group, u32 k, u32 n_groups, uint8_t *xs, uint8_t *ys, u32 *off) {
     LCB_LAUNCH(k_select_first_valid, accept, pts, pbytes, per_group, k, n_groups, xs, ys, off);
+}
+extern "C" void lcbk_coin_fold(dim3 grid, hipStream_t s, const uint8_t *sigs, u32 n, uint8_t *parity, uint64_t *nonce) {
+    LCB_LAUNCH(k_coin_fold, sigs, n, parity, nonce);
 }

@@ -1,10 +1,19 @@
-// lachain_amd/csrc/lcb_host.hip — host implementation of include/lachain_bls.h (liblachain_bls.so).
+// lachain_amd/csrc/lcb_host.cpp — host implementation of include/lachain_bls.h (liblachain_bls.so).
 //
-// Every arithmetic operation is executed by a gfx950 kernel (kernels.hip); the host only moves bytes,
-// validates arguments, and serializes GPU submission with a per-process lock (the reference calls mcl
-// concurrently from one thread per consensus protocol, /root/reference/src/Lachain.Consensus/AbstractProtocol.cs:46-47).
-// There is deliberately no CPU fallback: without a gfx950 device mclBn_init returns -1 and every entry
-// point fails (returns -1 / 0 bytes / leaves outputs zeroed) with lcb_last_error() describing why.
+// Every arithmetic operation is executed by a gfx950 kernel (k_*.hip); the host only moves bytes, validates
+// arguments and orders GPU work.  There is deliberately no CPU fallback: without a gfx950 device mclBn_init
+// returns -1 and every entry point fails (returns -1 / 0 bytes / leaves outputs zeroed) with lcb_last_error()
+// describing why.
+//
+// Concurrency model (the reference calls mcl from one thread per consensus protocol,
+// /root/reference/src/Lachain.Consensus/AbstractProtocol.cs:46-47):
+//   * single-element mcl operations share one staging buffer under a process-wide lock (synchronous);
+//   * every batch entry point runs in an lcb_ctx — explicit (lcb_ctx_*) or the calling thread's own default
+//     context — which owns all device workspaces the call needs (TPKE and TS line sets separately, Lagrange,
+//     MSM, staging).  A context's work executes in the order it was enqueued whatever stream it is enqueued on
+//     (each call waits on the context's last event and records a new one), and a *_prepared call checks the
+//     exact batch shape its prepare recorded, so no two callers can read or overwrite each other's workspace.
+//   * the HIP device is bound per calling thread (lcb_set_device applies to every thread that enters).
 #include <hip/hip_runtime.h>
 #include <string.h>
 #include <stdio.h>
@@ -18,12 +27,13 @@
 #include "bls_constants_host.h"
 #include "../../include/lachain_bls.h"
 #include "host_sha3.hpp"
+#include "lcb_ctx.hpp"
 
 #define LCB_BLOCK 256
 
 namespace {
 
-std::mutex g_mu;
+std::mutex g_mu;               // single-element operations + device initialisation
 int g_device = 0;
 bool g_ready = false;
 int g_orig_cofactor = 0;
@@ -32,6 +42,7 @@ u32 *g_io = nullptr;          // device buffer for single operations
 u32 *g_io_host = nullptr;     // pinned staging
 const size_t IO_WORDS = 4096; // 16 KB
 thread_local std::string g_err;
+thread_local int t_bound_device = -1;
 
 void set_err(const char *what, hipError_t e = hipSuccess) {
     char buf[256];
@@ -40,12 +51,21 @@ void set_err(const char *what, hipError_t e = hipSuccess) {
     g_err = buf;
 }
 
+// HIP's current device is per thread: bind every thread that enters the library to the configured device
+bool bind_thread() {
+    if (t_bound_device == g_device) return true;
+    hipError_t e = hipSetDevice(g_device);
+    if (e != hipSuccess) { set_err("hipSetDevice", e); return false; }
+    t_bound_device = g_device;
+    return true;
+}
+
 bool init_locked() {
-    if (g_ready) return true;
+    if (g_ready) return bind_thread();
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess || n <= g_device) { set_err("no HIP device", e); return false; }
-    if ((e = hipSetDevice(g_device)) != hipSuccess) { set_err("hipSetDevice", e); return false; }
+    if (!bind_thread()) return false;
     hipDeviceProp_t prop;
     if ((e = hipGetDeviceProperties(&prop, g_device)) != hipSuccess) { set_err("hipGetDeviceProperties", e); return false; }
     if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) { set_err("device is not gfx950"); return false; }
@@ -54,6 +74,13 @@ bool init_locked() {
     if ((e = hipHostMalloc(&g_io_host, IO_WORDS * 4, hipHostMallocDefault)) != hipSuccess) { set_err("hipHostMalloc", e); return false; }
     g_ready = true;
     return true;
+}
+
+// the library is usable from this thread (device opened once per process, bound once per thread)
+bool ready() {
+    if (g_ready && t_bound_device == g_device) return true;
+    std::lock_guard<std::mutex> lk(g_mu);
+    return init_locked();
 }
 
 // run one k_op on the staging buffer: copy `in_words` words to the device, launch, copy `out_words` back
@@ -71,43 +98,7 @@ bool run_op(int op, size_t in_words, size_t out_words) {
     std::lock_guard<std::mutex> lk_(g_mu);    \
     if (!init_locked()) return ret;
 
-// ------------------------------------------------------------------ device buffers for batch calls
-struct DevBuf {
-    void *p = nullptr;
-    size_t cap = 0;
-    void *get(size_t n) {
-        if (n == 0) n = 16;
-        if (n > cap) {
-            if (p) hipFree(p);
-            p = nullptr;
-            if (hipMalloc(&p, n) != hipSuccess) { cap = 0; return nullptr; }
-            cap = n;
-        }
-        return p;
-    }
-};
-DevBuf b_lines, b_ctok, b_keys, b_fsoa, b_in[8], b_out[4];
-// LCB_FUSED_VERIFY=1 selects the single-kernel verify (Miller loop + final exponentiation in one launch)
-static bool fused_verify() {
-    static int v = -1;
-    if (v < 0) { const char *e = getenv("LCB_FUSED_VERIFY"); v = (e && *e == '1') ? 1 : 0; }
-    return v == 1;
-}
-
 inline u32 nblk(size_t n) { return (u32)((n + LCB_BLOCK - 1) / LCB_BLOCK); }
-
-template <class T> T *up(DevBuf &b, const T *src, size_t count, hipStream_t s) {
-    T *d = (T *)b.get(count * sizeof(T));
-    if (d && count) hipMemcpyAsync(d, src, count * sizeof(T), hipMemcpyHostToDevice, s);
-    return d;
-}
-
-bool sync_check(const char *what) {
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = hipStreamSynchronize(g_stream);
-    if (e != hipSuccess) { set_err(what, e); return false; }
-    return true;
-}
 
 // canonical Fr bytes (32-byte LE < r)
 bool fr_bytes_lt_r(const uint8_t *b) {
@@ -522,288 +513,213 @@ extern "C" int mclBn_G2EvaluatePolynomial(mclBnG2 *out, const mclBnG2 *c, mclSiz
     return 0;
 }
 
-// ================================================================== batch: TPKE
-static int tpke_prepare_enqueue(const uint8_t *d_y, size_t n_keys, const uint8_t *d_u, const uint8_t *d_w,
-                                const uint8_t *d_v, const uint32_t *d_voff, size_t n_cts, hipStream_t s) {
-    u32 *lines = (u32 *)b_lines.get((size_t)n_cts * 2 * LCB_LINESET_BYTES);
-    uint8_t *ctok = (uint8_t *)b_ctok.get(n_cts);
-    void *keys = b_keys.get(n_keys * LCB_G1A_ST_BYTES);
+
+// ================================================================== execution contexts
+namespace {
+
+void ctx_free(lcb_ctx *c) {
+    if (!c) return;
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->order_valid) (void)hipEventSynchronize(c->order);
+    for (DevBuf *b : {&c->t_lines, &c->t_ctok, &c->t_keys, &c->t_f, &c->s_lines, &c->s_mok, &c->s_keys, &c->s_f})
+        b->release();
+    for (auto &b : c->lag) b.release();
+    for (auto &b : c->sel) b.release();
+    for (auto &b : c->msm) b.release();
+    for (auto &b : c->in) b.release();
+    for (auto &b : c->out) b.release();
+    if (c->ver_ev_ready) for (auto &e : c->ver_ev) (void)hipEventDestroy(e);
+    if (c->msm_ev_ready) for (auto &e : c->msm_ev) (void)hipEventDestroy(e);
+    if (c->order) (void)hipEventDestroy(c->order);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+lcb_ctx *ctx_new() {
+    if (!ready()) return nullptr;
+    lcb_ctx *c = new lcb_ctx;
+    c->device = g_device;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->order, hipEventDisableTiming);
+    if (e != hipSuccess) { set_err("context creation", e); ctx_free(c); return nullptr; }
+    return c;
+}
+// each thread owns two implicit contexts: one for the *_dev entry points without a context argument, one for the
+// synchronous host-pointer entry points (so a host-pointer call never touches a workspace a *_dev caller prepared)
+struct ThreadCtx {
+    lcb_ctx *c = nullptr;
+    ~ThreadCtx() { ctx_free(c); }
+};
+thread_local ThreadCtx t_dev_ctx, t_sync_ctx;
+lcb_ctx *resolve(lcb_ctx *c) {
+    if (!ready()) return nullptr;
+    if (c) {
+        if (c->device != g_device) { set_err("context belongs to another device"); return nullptr; }
+        return c;
+    }
+    if (!t_dev_ctx.c) t_dev_ctx.c = ctx_new();
+    return t_dev_ctx.c;
+}
+lcb_ctx *sync_ctx() {
+    if (!ready()) return nullptr;
+    if (!t_sync_ctx.c) t_sync_ctx.c = ctx_new();
+    return t_sync_ctx.c;
+}
+
+// Enqueue scope: exclusive use of the context, stream ordered after the context's previous work, and the
+// context's order event recorded after this call's work.
+struct Enq {
+    lcb_ctx *c;
+    hipStream_t s;
+    std::unique_lock<std::recursive_mutex> lk;
+    Enq(lcb_ctx *c_, hipStream_t s_) : c(c_), s(s_), lk(c_->mu) {
+        if (c->order_valid) (void)hipStreamWaitEvent(s, c->order, 0);
+    }
+    ~Enq() {
+        if (hipEventRecord(c->order, s) == hipSuccess) c->order_valid = true;
+    }
+};
+
+#define CTX_OR(var, ctxarg, ret)                 \
+    lcb_ctx *var = resolve(ctxarg);              \
+    if (!var) return ret;
+#define SYNC_CTX_OR(var, ret)                    \
+    lcb_ctx *var = sync_ctx();                   \
+    if (!var) return ret;
+
+template <class T> T *up(DevBuf &b, const T *src, size_t count, hipStream_t s) {
+    T *d = (T *)b.get(count * sizeof(T));
+    if (d && count) hipMemcpyAsync(d, src, count * sizeof(T), hipMemcpyHostToDevice, s);
+    return d;
+}
+bool launched(const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { set_err(what, e); return false; }
+    return true;
+}
+bool sync_check(lcb_ctx *c, const char *what) {
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) { set_err(what, e); return false; }
+    return true;
+}
+
+// LCB_FUSED_VERIFY=1 selects the single-kernel verify (Miller loop + final exponentiation in one launch)
+bool fused_verify() {
+    static int v = -1;
+    if (v < 0) { const char *e = getenv("LCB_FUSED_VERIFY"); v = (e && *e == '1') ? 1 : 0; }
+    return v == 1;
+}
+
+// ------------------------------------------------------------------ TPKE
+int tpke_prepare(lcb_ctx *c, const uint8_t *d_y, size_t n_keys, const uint8_t *d_u, const uint8_t *d_w,
+                 const uint8_t *d_v, const uint32_t *d_voff, size_t n_cts, hipStream_t s) {
+    if (n_cts > 0xffffffffu || n_keys > 0xffffffffu) { set_err("tpke prepare: batch too large"); return -1; }
+    c->t_ready = false;
+    u32 *lines = (u32 *)c->t_lines.get((size_t)n_cts * 2 * LCB_LINESET_BYTES);
+    uint8_t *ctok = (uint8_t *)c->t_ctok.get(n_cts);
+    void *keys = c->t_keys.get(n_keys * LCB_G1A_ST_BYTES);
     if (!lines || !ctok || !keys) { set_err("device allocation failed"); return -1; }
     if (n_keys) lcbk_g1_decompress(dim3(nblk(n_keys)), s, d_y, (u32)n_keys, keys);
     if (n_cts) lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), s, d_u, d_w, d_v, d_voff, (u32)n_cts, lines, ctok, g_orig_cofactor);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) { set_err("tpke prepare launch", e); return -1; }
+    if (!launched("tpke prepare launch")) return -1;
+    c->t_n_cts = n_cts;
+    c->t_n_keys = n_keys;
+    c->t_gen++;
+    c->t_ready = true;
     return 0;
 }
-// HIP events around the two kernels of the last split TPKE verify (lcb_tpke_verify_phase_ms)
-hipEvent_t g_ver_ev[3];
-bool g_ver_ev_ready = false;
-extern "C" int lcb_tpke_verify_phase_ms(float ms[2]) {
-    LOCKED_OR(-1)
-    if (!g_ver_ev_ready) { set_err("tpke verify: no split verify has run"); return -1; }
-    if (hipEventSynchronize(g_ver_ev[2]) != hipSuccess) { set_err("tpke verify: event sync"); return -1; }
-    for (int i = 0; i < 2; i++)
-        if (hipEventElapsedTime(&ms[i], g_ver_ev[i], g_ver_ev[i + 1]) != hipSuccess) ms[i] = -1.0f;
-    return 0;
-}
-static int tpke_verify_prepared_enqueue(uint8_t *d_accept, size_t n, size_t n_keys, size_t n_cts, const uint32_t *d_ct,
-                                        const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
-    if (b_lines.cap < (size_t)n_cts * 2 * LCB_LINESET_BYTES || b_ctok.cap < n_cts || b_keys.cap < n_keys * LCB_G1A_ST_BYTES) {
-        set_err("tpke verify: workspace not prepared for this batch");
-        return -1;
+bool tpke_shape_ok(lcb_ctx *c, size_t n_keys, size_t n_cts, const char *what) {
+    if (!c->t_ready) { set_err((std::string(what) + ": no TPKE batch prepared in this context").c_str()); return false; }
+    if (c->t_n_cts != n_cts || c->t_n_keys != n_keys) {
+        set_err((std::string(what) + ": batch shape differs from the one prepared in this context").c_str());
+        return false;
     }
+    return true;
+}
+int tpke_verify_prepared(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_keys, size_t n_cts, const uint32_t *d_ct,
+                         const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
+    if (!tpke_shape_ok(c, n_keys, n_cts, "tpke verify")) return -1;
+    if (n > 0xffffffffu) { set_err("tpke verify: batch too large"); return -1; }
+    const u32 *lines = (const u32 *)c->t_lines.p;
+    const uint8_t *ctok = (const uint8_t *)c->t_ctok.p;
     if (n && fused_verify()) {
-        lcbk_tpke_verify(dim3(nblk(n)), s, (const u32 *)b_lines.p, (const uint8_t *)b_ctok.p, b_keys.p, (u32)n_keys,
-                         d_ct, d_dec, d_ui, (u32)n, d_accept);
+        lcbk_tpke_verify(dim3(nblk(n)), s, lines, ctok, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct, d_dec, d_ui, (u32)n,
+                         d_accept);
     } else if (n) {
-        u32 *f = (u32 *)b_fsoa.get(n * 576);
+        u32 *f = (u32 *)c->t_f.get(n * 576);
         if (!f) { set_err("device allocation failed"); return -1; }
-        if (!g_ver_ev_ready) {
-            for (auto &e : g_ver_ev) hipEventCreate(&e);
-            g_ver_ev_ready = true;
+        if (!c->ver_ev_ready) {
+            for (auto &e : c->ver_ev) hipEventCreate(&e);
+            c->ver_ev_ready = true;
         }
-        hipEventRecord(g_ver_ev[0], s);
-        lcbk_tpke_miller(dim3(nblk(n)), s, (const u32 *)b_lines.p, (const uint8_t *)b_ctok.p, b_keys.p, (u32)n_keys,
-                         d_ct, d_dec, d_ui, (u32)n, f, d_accept);
-        hipEventRecord(g_ver_ev[1], s);
+        hipEventRecord(c->ver_ev[0], s);
+        lcbk_tpke_miller(dim3(nblk(n)), s, lines, ctok, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct, d_dec, d_ui, (u32)n,
+                         f, d_accept);
+        hipEventRecord(c->ver_ev[1], s);
         lcbk_final_exp_check(dim3(nblk(n)), s, f, (u32)n, d_accept);
-        hipEventRecord(g_ver_ev[2], s);
+        hipEventRecord(c->ver_ev[2], s);
+        c->ver_ran = true;
     }
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) { set_err("tpke verify launch", e); return -1; }
-    return 0;
+    return launched("tpke verify launch") ? 0 : -1;
 }
-static int tpke_verify_enqueue(uint8_t *d_accept, size_t n, const uint8_t *d_y, size_t n_keys, const uint8_t *d_u,
-                               const uint8_t *d_w, const uint8_t *d_v, const uint32_t *d_voff, size_t n_cts,
-                               const uint32_t *d_ct, const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
-    if (tpke_prepare_enqueue(d_y, n_keys, d_u, d_w, d_v, d_voff, n_cts, s)) return -1;
-    return tpke_verify_prepared_enqueue(d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, s);
-}
-extern "C" int lcb_tpke_prepare_dev(const uint8_t *y_keys, size_t n_keys, const uint8_t *cts_u, const uint8_t *cts_w,
-                                    const uint8_t *v_data, const uint32_t *v_off, size_t n_cts, void *stream) {
-    LOCKED_OR(-1)
-    return tpke_prepare_enqueue(y_keys, n_keys, cts_u, cts_w, v_data, v_off, n_cts, (hipStream_t)stream);
-}
-extern "C" int lcb_tpke_verify_prepared_dev(uint8_t *accept, size_t n, size_t n_keys, size_t n_cts, const uint32_t *ct_idx,
-                                            const uint32_t *dec_idx, const uint8_t *ui, void *stream) {
-    LOCKED_OR(-1)
-    return tpke_verify_prepared_enqueue(accept, n, n_keys, n_cts, ct_idx, dec_idx, ui, (hipStream_t)stream);
-}
-extern "C" int lcb_tpke_verify_shares_dev(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys,
-                                          const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
-                                          const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
-                                          const uint32_t *dec_idx, const uint8_t *ui, void *stream) {
-    LOCKED_OR(-1)
-    return tpke_verify_enqueue(accept, n, y_keys, n_keys, cts_u, cts_w, v_data, v_off, n_cts, ct_idx, dec_idx, ui,
-                               (hipStream_t)stream);
-}
-extern "C" int lcb_tpke_verify_shares(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys,
-                                      const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
-                                      const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
-                                      const uint32_t *dec_idx, const uint8_t *ui) {
-    LOCKED_OR(-1)
-    for (size_t i = 0; i < n; i++)
-        if (ct_idx[i] >= n_cts) { set_err("ct_idx out of range"); return -1; }
-    size_t vbytes = n_cts ? v_off[n_cts] : 0;
-    hipStream_t s = g_stream;
-    const uint8_t *dy = up(b_in[0], y_keys, 48 * n_keys, s);
-    const uint8_t *du = up(b_in[1], cts_u, 48 * n_cts, s);
-    const uint8_t *dw = up(b_in[2], cts_w, 96 * n_cts, s);
-    const uint8_t *dv = up(b_in[3], v_data, vbytes, s);
-    const uint32_t *dvo = up(b_in[4], v_off, n_cts + 1, s);
-    const uint32_t *dct = up(b_in[5], ct_idx, n, s);
-    const uint32_t *ddec = up(b_in[6], dec_idx, n, s);
-    const uint8_t *dui = up(b_in[7], ui, 48 * n, s);
-    uint8_t *dacc = (uint8_t *)b_out[0].get(n);
-    if (!dy || !du || !dw || !dv || !dvo || !dct || !ddec || !dui || !dacc) { set_err("device allocation failed"); return -1; }
-    if (tpke_verify_enqueue(dacc, n, dy, n_keys, du, dw, dv, dvo, n_cts, dct, ddec, dui, s)) return -1;
-    if (n) hipMemcpyAsync(accept, dacc, n, hipMemcpyDeviceToHost, s);
-    return sync_check("tpke verify") ? 0 : -1;
-}
-
-extern "C" int lcb_tpke_partial_decrypt(uint8_t *ui_out, uint8_t *status, const uint8_t x[32], const uint8_t *cts_u,
-                                        const uint8_t *cts_w, const uint8_t *v_data, const uint32_t *v_off,
-                                        size_t n_cts) {
-    LOCKED_OR(-1)
-    hipStream_t s = g_stream;
-    size_t vbytes = n_cts ? v_off[n_cts] : 0;
-    const uint8_t *du = up(b_in[1], cts_u, 48 * n_cts, s);
-    const uint8_t *dw = up(b_in[2], cts_w, 96 * n_cts, s);
-    const uint8_t *dv = up(b_in[3], v_data, vbytes, s);
-    const uint32_t *dvo = up(b_in[4], v_off, n_cts + 1, s);
-    const uint8_t *dx = up(b_in[0], x, 32, s);
-    u32 *lines = (u32 *)b_lines.get((size_t)n_cts * 2 * LCB_LINESET_BYTES);
-    uint8_t *ctok = (uint8_t *)b_ctok.get(n_cts);
-    uint8_t *dui = (uint8_t *)b_out[0].get(48 * n_cts);
-    uint8_t *dst = (uint8_t *)b_out[1].get(n_cts);
-    if (!du || !dw || !dv || !dvo || !dx || !lines || !ctok || !dui || !dst) { set_err("device allocation failed"); return -1; }
-    if (!n_cts) return 0;
-    lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), s, du, dw, dv, dvo, (u32)n_cts, lines,
-                       ctok, g_orig_cofactor);
-    lcbk_tpke_partial_decrypt(dim3(nblk(n_cts)), s, lines, ctok, du, dx, 0, (u32)n_cts, dui, dst);
-    hipMemcpyAsync(ui_out, dui, 48 * n_cts, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(status, dst, n_cts, hipMemcpyDeviceToHost, s);
-    return sync_check("tpke partial decrypt") ? 0 : -1;
-}
-
-extern "C" int lcb_tpke_partial_decrypt_prepared_dev(uint8_t *ui_out, uint8_t *status, const uint8_t *x_raw,
-                                                     size_t x_stride, const uint8_t *cts_u, size_t n_cts, void *stream) {
-    LOCKED_OR(-1)
-    if (b_lines.cap < (size_t)n_cts * 2 * LCB_LINESET_BYTES || b_ctok.cap < n_cts) {
-        set_err("tpke partial decrypt: workspace not prepared for this batch");
-        return -1;
-    }
+int tpke_partial_decrypt_prepared(lcb_ctx *c, uint8_t *ui_out, uint8_t *status, const uint8_t *x_raw, size_t x_stride,
+                                  const uint8_t *cts_u, size_t n_cts, hipStream_t s) {
+    if (!tpke_shape_ok(c, c->t_n_keys, n_cts, "tpke partial decrypt")) return -1;
     if (n_cts)
-        lcbk_tpke_partial_decrypt(dim3(nblk(n_cts)), (hipStream_t)stream, (const u32 *)b_lines.p,
-                                  (const uint8_t *)b_ctok.p, cts_u, x_raw, (u32)x_stride, (u32)n_cts, ui_out, status);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) { set_err("tpke partial decrypt launch", e); return -1; }
-    return 0;
-}
-extern "C" int lcb_tpke_encrypt_phase1(uint8_t *u_out, uint8_t *t_out, const uint8_t y[48], const uint8_t *r, size_t n) {
-    LOCKED_OR(-1)
-    if (!n) return 0;
-    hipStream_t s = g_stream;
-    const uint8_t *dy = up(b_in[0], y, 48, s);
-    const uint8_t *dr = up(b_in[1], r, 32 * n, s);
-    uint8_t *du = (uint8_t *)b_out[0].get(48 * n), *dt = (uint8_t *)b_out[1].get(48 * n), *dok = (uint8_t *)b_out[2].get(n);
-    if (!dy || !dr || !du || !dt || !dok) { set_err("device allocation failed"); return -1; }
-    lcbk_tpke_encrypt1(dim3(nblk(n)), s, dy, dr, (u32)n, du, dt, dok);
-    std::vector<uint8_t> ok(n);
-    hipMemcpyAsync(u_out, du, 48 * n, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(t_out, dt, 48 * n, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, s);
-    if (!sync_check("tpke encrypt1")) return -1;
-    for (size_t i = 0; i < n; i++) if (!ok[i]) { set_err("invalid public key or scalar"); return -1; }
-    return 0;
-}
-extern "C" int lcb_tpke_encrypt_phase2(uint8_t *w_out, const uint8_t *u, const uint8_t *r, const uint8_t *v_data,
-                                       const uint32_t *v_off, size_t n) {
-    LOCKED_OR(-1)
-    if (!n) return 0;
-    hipStream_t s = g_stream;
-    const uint8_t *du = up(b_in[0], u, 48 * n, s);
-    const uint8_t *dr = up(b_in[1], r, 32 * n, s);
-    const uint8_t *dv = up(b_in[2], v_data, v_off[n], s);
-    const uint32_t *dvo = up(b_in[3], v_off, n + 1, s);
-    uint8_t *dw = (uint8_t *)b_out[0].get(96 * n), *dok = (uint8_t *)b_out[1].get(n);
-    if (!du || !dr || !dv || !dvo || !dw || !dok) { set_err("device allocation failed"); return -1; }
-    lcbk_tpke_encrypt2(dim3(nblk(n)), s, du, dr, dv, dvo, (u32)n, dw, dok,
-                       g_orig_cofactor);
-    std::vector<uint8_t> ok(n);
-    hipMemcpyAsync(w_out, dw, 96 * n, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, s);
-    if (!sync_check("tpke encrypt2")) return -1;
-    for (size_t i = 0; i < n; i++) if (!ok[i]) { set_err("hash-to-G2 failed"); return -1; }
-    return 0;
+        lcbk_tpke_partial_decrypt(dim3(nblk(n_cts)), s, (const u32 *)c->t_lines.p, (const uint8_t *)c->t_ctok.p, cts_u,
+                                  x_raw, (u32)x_stride, (u32)n_cts, ui_out, status);
+    return launched("tpke partial decrypt launch") ? 0 : -1;
 }
 
-// ================================================================== batch: threshold signatures
-static int ts_prepare_enqueue(const uint8_t *d_pks, size_t n_pks, const uint8_t *d_msg, const uint32_t *d_moff,
-                              size_t n_msgs, hipStream_t s) {
-    u32 *lines = (u32 *)b_lines.get((size_t)n_msgs * LCB_LINESET_BYTES);
-    uint8_t *mok = (uint8_t *)b_ctok.get(n_msgs);
-    void *keys = b_keys.get(n_pks * LCB_G1A_ST_BYTES);
+// ------------------------------------------------------------------ threshold signatures
+int ts_prepare(lcb_ctx *c, const uint8_t *d_pks, size_t n_pks, const uint8_t *d_msg, const uint32_t *d_moff,
+               size_t n_msgs, hipStream_t s) {
+    if (n_msgs > 0xffffffffu || n_pks > 0xffffffffu) { set_err("ts prepare: batch too large"); return -1; }
+    c->s_ready = false;
+    u32 *lines = (u32 *)c->s_lines.get((size_t)n_msgs * LCB_LINESET_BYTES);
+    uint8_t *mok = (uint8_t *)c->s_mok.get(n_msgs);
+    void *keys = c->s_keys.get(n_pks * LCB_G1A_ST_BYTES);
     if (!lines || !mok || !keys) { set_err("device allocation failed"); return -1; }
     if (n_pks) lcbk_g1_decompress(dim3(nblk(n_pks)), s, d_pks, (u32)n_pks, keys);
     if (n_msgs) lcbk_ts_msg_prepare(dim3(nblk(n_msgs)), s, d_msg, d_moff, (u32)n_msgs, lines, mok, g_orig_cofactor);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) { set_err("ts prepare launch", e); return -1; }
+    if (!launched("ts prepare launch")) return -1;
+    c->s_n_msgs = n_msgs;
+    c->s_n_pks = n_pks;
+    c->s_gen++;
+    c->s_ready = true;
     return 0;
 }
-static int ts_verify_prepared_enqueue(uint8_t *d_accept, size_t n, size_t n_pks, size_t n_msgs, const uint8_t *d_sigs,
-                                      const uint32_t *d_midx, const uint32_t *d_pidx, hipStream_t s) {
-    if (b_lines.cap < (size_t)n_msgs * LCB_LINESET_BYTES || b_ctok.cap < n_msgs || b_keys.cap < n_pks * LCB_G1A_ST_BYTES) {
-        set_err("ts verify: workspace not prepared for this batch");
+int ts_verify_prepared(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_pks, size_t n_msgs, const uint8_t *d_sigs,
+                       const uint32_t *d_midx, const uint32_t *d_pidx, hipStream_t s) {
+    if (!c->s_ready) { set_err("ts verify: no threshold-signature batch prepared in this context"); return -1; }
+    if (c->s_n_msgs != n_msgs || c->s_n_pks != n_pks) {
+        set_err("ts verify: batch shape differs from the one prepared in this context");
         return -1;
     }
+    if (n > 0xffffffffu) { set_err("ts verify: batch too large"); return -1; }
+    const u32 *lines = (const u32 *)c->s_lines.p;
+    const uint8_t *mok = (const uint8_t *)c->s_mok.p;
     if (n && fused_verify()) {
-        lcbk_ts_verify(dim3(nblk(n)), s, (const u32 *)b_lines.p, (const uint8_t *)b_ctok.p, b_keys.p, (u32)n_pks,
-                       d_sigs, d_midx, d_pidx, (u32)n, d_accept);
+        lcbk_ts_verify(dim3(nblk(n)), s, lines, mok, (u32)n_msgs, c->s_keys.p, (u32)n_pks, d_sigs, d_midx, d_pidx, (u32)n,
+                       d_accept);
     } else if (n) {
-        u32 *f = (u32 *)b_fsoa.get(n * 576);
+        u32 *f = (u32 *)c->s_f.get(n * 576);
         if (!f) { set_err("device allocation failed"); return -1; }
-        lcbk_ts_miller(dim3(nblk(n)), s, (const u32 *)b_lines.p, (const uint8_t *)b_ctok.p, b_keys.p, (u32)n_pks,
-                       d_sigs, d_midx, d_pidx, (u32)n, f, d_accept);
+        lcbk_ts_miller(dim3(nblk(n)), s, lines, mok, (u32)n_msgs, c->s_keys.p, (u32)n_pks, d_sigs, d_midx, d_pidx, (u32)n,
+                       f, d_accept);
         lcbk_final_exp_check(dim3(nblk(n)), s, f, (u32)n, d_accept);
     }
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) { set_err("ts verify launch", e); return -1; }
-    return 0;
-}
-static int ts_verify_enqueue(uint8_t *d_accept, size_t n, const uint8_t *d_pks, size_t n_pks, const uint8_t *d_sigs,
-                             const uint8_t *d_msg, const uint32_t *d_moff, size_t n_msgs, const uint32_t *d_midx,
-                             const uint32_t *d_pidx, hipStream_t s) {
-    if (ts_prepare_enqueue(d_pks, n_pks, d_msg, d_moff, n_msgs, s)) return -1;
-    return ts_verify_prepared_enqueue(d_accept, n, n_pks, n_msgs, d_sigs, d_midx, d_pidx, s);
-}
-extern "C" int lcb_ts_prepare_dev(const uint8_t *pks, size_t n_pks, const uint8_t *msg_data, const uint32_t *msg_off,
-                                  size_t n_msgs, void *stream) {
-    LOCKED_OR(-1)
-    return ts_prepare_enqueue(pks, n_pks, msg_data, msg_off, n_msgs, (hipStream_t)stream);
-}
-extern "C" int lcb_ts_verify_prepared_dev(uint8_t *accept, size_t n, size_t n_pks, size_t n_msgs, const uint8_t *sigs,
-                                          const uint32_t *msg_idx, const uint32_t *pk_idx, void *stream) {
-    LOCKED_OR(-1)
-    return ts_verify_prepared_enqueue(accept, n, n_pks, n_msgs, sigs, msg_idx, pk_idx, (hipStream_t)stream);
-}
-extern "C" int lcb_ts_verify_shares_dev(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks, const uint8_t *sigs,
-                                        const uint8_t *msg_data, const uint32_t *msg_off, size_t n_msgs,
-                                        const uint32_t *msg_idx, const uint32_t *pk_idx, void *stream) {
-    LOCKED_OR(-1)
-    return ts_verify_enqueue(accept, n, pks, n_pks, sigs, msg_data, msg_off, n_msgs, msg_idx, pk_idx, (hipStream_t)stream);
-}
-extern "C" int lcb_ts_verify_shares(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks, const uint8_t *sigs,
-                                    const uint8_t *msg_data, const uint32_t *msg_off, size_t n_msgs,
-                                    const uint32_t *msg_idx, const uint32_t *pk_idx) {
-    LOCKED_OR(-1)
-    for (size_t i = 0; i < n; i++)
-        if (msg_idx[i] >= n_msgs) { set_err("msg_idx out of range"); return -1; }
-    hipStream_t s = g_stream;
-    size_t mbytes = n_msgs ? msg_off[n_msgs] : 0;
-    const uint8_t *dpk = up(b_in[0], pks, 48 * n_pks, s);
-    const uint8_t *dsig = up(b_in[1], sigs, 96 * n, s);
-    const uint8_t *dm = up(b_in[2], msg_data, mbytes, s);
-    const uint32_t *dmo = up(b_in[3], msg_off, n_msgs + 1, s);
-    const uint32_t *dmi = up(b_in[4], msg_idx, n, s);
-    const uint32_t *dpi = up(b_in[5], pk_idx, n, s);
-    uint8_t *dacc = (uint8_t *)b_out[0].get(n);
-    if (!dpk || !dsig || !dm || !dmo || !dmi || !dpi || !dacc) { set_err("device allocation failed"); return -1; }
-    if (ts_verify_enqueue(dacc, n, dpk, n_pks, dsig, dm, dmo, n_msgs, dmi, dpi, s)) return -1;
-    if (n) hipMemcpyAsync(accept, dacc, n, hipMemcpyDeviceToHost, s);
-    return sync_check("ts verify") ? 0 : -1;
-}
-extern "C" int lcb_ts_sign(uint8_t *sigs_out, const uint8_t *sks, const uint8_t *msg_data, const uint32_t *msg_off,
-                           const uint32_t *msg_idx, size_t n) {
-    LOCKED_OR(-1)
-    if (!n) return 0;
-    u32 nm = 0;
-    for (size_t i = 0; i < n; i++) nm = msg_idx[i] + 1 > nm ? msg_idx[i] + 1 : nm;
-    hipStream_t s = g_stream;
-    const uint8_t *dsk = up(b_in[0], sks, 32 * n, s);
-    const uint8_t *dm = up(b_in[1], msg_data, msg_off[nm], s);
-    const uint32_t *dmo = up(b_in[2], msg_off, nm + 1, s);
-    const uint32_t *dmi = up(b_in[3], msg_idx, n, s);
-    uint8_t *dsig = (uint8_t *)b_out[0].get(96 * n), *dok = (uint8_t *)b_out[1].get(n);
-    if (!dsk || !dm || !dmo || !dmi || !dsig || !dok) { set_err("device allocation failed"); return -1; }
-    lcbk_ts_sign(dim3(nblk(n)), s, dsk, dm, dmo, dmi, (u32)n, dsig, dok,
-                       g_orig_cofactor);
-    std::vector<uint8_t> ok(n);
-    hipMemcpyAsync(sigs_out, dsig, 96 * n, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, s);
-    if (!sync_check("ts sign")) return -1;
-    for (size_t i = 0; i < n; i++) if (!ok[i]) { set_err("invalid key share"); return -1; }
-    return 0;
+    return launched("ts verify launch") ? 0 : -1;
 }
 
-// ================================================================== batch: Lagrange, scalar mul, hash, MSM
-DevBuf b_lag[3];
+// ------------------------------------------------------------------ Lagrange / assembly
 // device-side Lagrange at 0 for np problems (entries off[j]..off[j+1]); dout = serialized results, dst = status
-static int lagrange_enqueue(int g, uint8_t *dout, uint8_t *dst, const uint8_t *dx, const uint8_t *dy, const uint32_t *doff,
-                            size_t np, size_t ne, hipStream_t s) {
-    void *lam = b_lag[0].get(LCB_FR_BYTES * (ne ? ne : 1));
-    void *parts = b_lag[1].get((g == 1 ? LCB_G1_JAC_BYTES : LCB_G2_JAC_BYTES) * (ne ? ne : 1));
-    uint8_t *pok = (uint8_t *)b_lag[2].get(ne ? ne : 1);
+int lagrange_enqueue(lcb_ctx *c, int g, uint8_t *dout, uint8_t *dst, const uint8_t *dx, const uint8_t *dy,
+                     const uint32_t *doff, size_t np, size_t ne, hipStream_t s) {
+    if (np > 0xffffffffu || ne > 0xffffffffu) { set_err("lagrange: batch too large"); return -1; }
+    void *lam = c->lag[0].get(LCB_FR_BYTES * (ne ? ne : 1));
+    void *parts = c->lag[1].get((g == 1 ? LCB_G1_JAC_BYTES : LCB_G2_JAC_BYTES) * (ne ? ne : 1));
+    uint8_t *pok = (uint8_t *)c->lag[2].get(ne ? ne : 1);
     if (!lam || !parts || !pok) { set_err("device allocation failed"); return -1; }
     lcbk_lagrange_coeffs(dim3(nblk(np)), s, dx, doff, (u32)np, lam, dst);
     if (ne) {
@@ -812,112 +728,25 @@ static int lagrange_enqueue(int g, uint8_t *dout, uint8_t *dst, const uint8_t *d
     }
     if (g == 1) lcbk_g1_sum(dim3(nblk(np)), s, parts, pok, doff, (u32)np, dst, dout);
     else lcbk_g2_sum(dim3(nblk(np)), s, parts, pok, doff, (u32)np, dst, dout);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) { set_err("lagrange launch", e); return -1; }
-    return 0;
+    return launched("lagrange launch") ? 0 : -1;
 }
-static int lagrange_batch(int g, uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys, const uint32_t *off,
-                          size_t np) {
-    LOCKED_OR(-1)
-    if (!np) return 0;
-    size_t ne = off[np];
-    size_t pb = g == 1 ? 48 : 96;
-    hipStream_t s = g_stream;
-    const uint8_t *dx = up(b_in[0], xs, 32 * ne, s);
-    const uint8_t *dy = up(b_in[1], ys, pb * ne, s);
-    const uint32_t *doff = up(b_in[2], off, np + 1, s);
-    uint8_t *dst = (uint8_t *)b_out[0].get(np), *dout = (uint8_t *)b_out[1].get(pb * np);
-    if (!dx || !dy || !doff || !dst || !dout) { set_err("device allocation failed"); return -1; }
-    if (lagrange_enqueue(g, dout, dst, dx, dy, doff, np, ne, s)) return -1;
-    hipMemcpyAsync(out, dout, pb * np, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(status, dst, np, hipMemcpyDeviceToHost, s);
-    return sync_check("lagrange") ? 0 : -1;
-}
-extern "C" int lcb_g1_lagrange_dev(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
-                                   const uint32_t *off, size_t n_problems, size_t n_entries, void *stream) {
-    LOCKED_OR(-1)
-    return n_problems ? lagrange_enqueue(1, out, status, xs, ys, off, n_problems, n_entries, (hipStream_t)stream) : 0;
-}
-extern "C" int lcb_g2_lagrange_dev(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
-                                   const uint32_t *off, size_t n_problems, size_t n_entries, void *stream) {
-    LOCKED_OR(-1)
-    return n_problems ? lagrange_enqueue(2, out, status, xs, ys, off, n_problems, n_entries, (hipStream_t)stream) : 0;
-}
-DevBuf b_sel[3];
-static int assemble_enqueue(int g, uint8_t *out, uint8_t *status, const uint8_t *accept, const uint8_t *pts,
-                            size_t per_group, size_t k, size_t n_groups, hipStream_t s) {
+int assemble_enqueue(lcb_ctx *c, int g, uint8_t *out, uint8_t *status, const uint8_t *accept, const uint8_t *pts,
+                     size_t per_group, size_t k, size_t n_groups, hipStream_t s) {
     if (!n_groups) return 0;
     if (k == 0 || k > per_group) { set_err("assemble: need 0 < k <= shares per group"); return -1; }
     size_t pb = g == 1 ? 48 : 96, ne = n_groups * k;
-    uint8_t *xs = (uint8_t *)b_sel[0].get(32 * ne), *ys = (uint8_t *)b_sel[1].get(pb * ne);
-    u32 *off = (u32 *)b_sel[2].get(4 * (n_groups + 1));
+    if (ne > 0xffffffffu || (size_t)n_groups * per_group > 0xffffffffu) { set_err("assemble: batch too large"); return -1; }
+    uint8_t *xs = (uint8_t *)c->sel[0].get(32 * ne), *ys = (uint8_t *)c->sel[1].get(pb * ne);
+    u32 *off = (u32 *)c->sel[2].get(4 * (n_groups + 1));
     if (!xs || !ys || !off) { set_err("device allocation failed"); return -1; }
     lcbk_select_first_valid(dim3(nblk(n_groups)), s, accept, pts, (u32)pb, (u32)per_group, (u32)k, (u32)n_groups, xs,
                             ys, off);
-    return lagrange_enqueue(g, out, status, xs, ys, off, n_groups, ne, s);
+    return lagrange_enqueue(c, g, out, status, xs, ys, off, n_groups, ne, s);
 }
-extern "C" int lcb_ts_assemble_dev(uint8_t *sig_out, uint8_t *status, const uint8_t *accept, const uint8_t *sigs,
-                                   size_t per_round, size_t k, size_t n_rounds, void *stream) {
-    LOCKED_OR(-1)
-    return assemble_enqueue(2, sig_out, status, accept, sigs, per_round, k, n_rounds, (hipStream_t)stream);
-}
-extern "C" int lcb_tpke_combine_dev(uint8_t *u_out, uint8_t *status, const uint8_t *accept, const uint8_t *shares,
-                                    size_t per_ct, size_t k, size_t n_cts, void *stream) {
-    LOCKED_OR(-1)
-    return assemble_enqueue(1, u_out, status, accept, shares, per_ct, k, n_cts, (hipStream_t)stream);
-}
-extern "C" int lcb_g1_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
-                                     const uint32_t *off, size_t n) { return lagrange_batch(1, out, status, xs, ys, off, n); }
-extern "C" int lcb_g2_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
-                                     const uint32_t *off, size_t n) { return lagrange_batch(2, out, status, xs, ys, off, n); }
 
-static int mul_batch(int g, uint8_t *out, const uint8_t *points, int use_gen, const uint8_t *scalars, size_t n) {
-    LOCKED_OR(-1)
-    if (!n) return 0;
-    size_t pb = g == 1 ? 48 : 96;
-    hipStream_t s = g_stream;
-    const uint8_t *dp = use_gen ? (const uint8_t *)b_in[0].get(16) : up(b_in[0], points, pb * n, s);
-    const uint8_t *dsc = up(b_in[1], scalars, 32 * n, s);
-    uint8_t *dout = (uint8_t *)b_out[0].get(pb * n), *dok = (uint8_t *)b_out[1].get(n);
-    if (!dp || !dsc || !dout || !dok) { set_err("device allocation failed"); return -1; }
-    if (g == 1) lcbk_g1_mul(dim3(nblk(n)), s, dp, use_gen, dsc, (u32)n, dout, dok);
-    else lcbk_g2_mul(dim3(nblk(n)), s, dp, use_gen, dsc, (u32)n, dout, dok);
-    std::vector<uint8_t> ok(n);
-    hipMemcpyAsync(out, dout, pb * n, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, s);
-    if (!sync_check("mul batch")) return -1;
-    for (size_t i = 0; i < n; i++) if (!ok[i]) { set_err("invalid point or scalar"); return -1; }
-    return 0;
-}
-extern "C" int lcb_g1_mul_batch(uint8_t *out, const uint8_t *points, int gen, const uint8_t *scalars, size_t n) {
-    return mul_batch(1, out, points, gen, scalars, n);
-}
-extern "C" int lcb_g2_mul_batch(uint8_t *out, const uint8_t *points, int gen, const uint8_t *scalars, size_t n) {
-    return mul_batch(2, out, points, gen, scalars, n);
-}
-extern "C" int lcb_g2_hash_batch(uint8_t *out, const uint8_t *msg_data, const uint32_t *msg_off, size_t n) {
-    LOCKED_OR(-1)
-    if (!n) return 0;
-    hipStream_t s = g_stream;
-    const uint8_t *dm = up(b_in[0], msg_data, msg_off[n], s);
-    const uint32_t *dmo = up(b_in[1], msg_off, n + 1, s);
-    uint8_t *dout = (uint8_t *)b_out[0].get(96 * n), *dok = (uint8_t *)b_out[1].get(n);
-    if (!dm || !dmo || !dout || !dok) { set_err("device allocation failed"); return -1; }
-    lcbk_g2_hash(dim3(nblk(n)), s, dm, dmo, (u32)n, dout, dok, g_orig_cofactor);
-    std::vector<uint8_t> ok(n);
-    hipMemcpyAsync(out, dout, 96 * n, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, s);
-    if (!sync_check("hash batch")) return -1;
-    for (size_t i = 0; i < n; i++) if (!ok[i]) { set_err("hash-to-G2 failed"); return -1; }
-    return 0;
-}
-// ---------------------------------------------------------------- Pippenger MSM (k_msm.hip)
-DevBuf b_msm[12];
-hipEvent_t g_msm_ev[7];
-bool g_msm_ev_ready = false;
-
+// ------------------------------------------------------------------ Pippenger MSM (k_msm.hip)
 // window width minimising ceil-windows * (n mixed adds * 11 + 2^(c-1) buckets * 2 Jacobian adds * 16) Fp-mul
-static u32 msm_window(size_t n) {
+u32 msm_window(size_t n) {
     u32 best = 4;
     double best_cost = 1e300;
     for (u32 c = 4; c <= 20; c++) {
@@ -927,9 +756,8 @@ static u32 msm_window(size_t n) {
     }
     return best;
 }
-extern "C" int lcb_g1_msm_window(size_t n) { return (int)msm_window(n); }
-
-static int msm_enqueue(void *out_jac, const void *pts, const uint8_t *scalars, size_t n, int window_bits, hipStream_t s) {
+int msm_enqueue(lcb_ctx *cx, void *out_jac, const void *pts, const uint8_t *scalars, size_t n, int window_bits,
+                hipStream_t s) {
     if (n > 0x7fffffffu) { set_err("msm: too many points"); return -1; }
     u32 c = window_bits > 0 ? (u32)window_bits : msm_window(n);
     if (c < 2 || c > 24) { set_err("msm: window bits out of range"); return -1; }
@@ -941,39 +769,40 @@ static int msm_enqueue(void *out_jac, const void *pts, const uint8_t *scalars, s
     u32 L = 1;
     while ((size_t)nb / (L * 2) >= 65536 && L * 2 <= half) L *= 2;
     u32 n_seg = nb / L, per_win = half / L, n_l1 = n_seg / (per_win < 256 ? per_win : 256);
-    if (!g_msm_ev_ready) {
-        for (auto &e : g_msm_ev) hipEventCreate(&e);
-        g_msm_ev_ready = true;
+    if (!cx->msm_ev_ready) {
+        for (auto &e : cx->msm_ev) hipEventCreate(&e);
+        cx->msm_ev_ready = true;
     }
-    u32 *keys = (u32 *)b_msm[0].get(m * 4), *keys2 = (u32 *)b_msm[1].get(m * 4);
-    u32 *vals = (u32 *)b_msm[2].get(m * 4), *vals2 = (u32 *)b_msm[3].get(m * 4);
-    u32 *st = (u32 *)b_msm[4].get((size_t)nb * 4), *en = (u32 *)b_msm[5].get((size_t)nb * 4);
-    void *buckets = b_msm[6].get((size_t)nb * LCB_G1_JAC_BYTES);
-    void *segs = b_msm[7].get((size_t)n_seg * LCB_G1_JAC_BYTES);
-    void *l1 = b_msm[8].get((size_t)n_l1 * LCB_G1_JAC_BYTES);
-    void *wins = b_msm[9].get((size_t)nwin * LCB_G1_JAC_BYTES);
+    DevBuf *b = cx->msm;
+    u32 *keys = (u32 *)b[0].get(m * 4), *keys2 = (u32 *)b[1].get(m * 4);
+    u32 *vals = (u32 *)b[2].get(m * 4), *vals2 = (u32 *)b[3].get(m * 4);
+    u32 *st = (u32 *)b[4].get((size_t)nb * 4), *en = (u32 *)b[5].get((size_t)nb * 4);
+    void *buckets = b[6].get((size_t)nb * LCB_G1_JAC_BYTES);
+    void *segs = b[7].get((size_t)n_seg * LCB_G1_JAC_BYTES);
+    void *l1 = b[8].get((size_t)n_l1 * LCB_G1_JAC_BYTES);
+    void *wins = b[9].get((size_t)nwin * LCB_G1_JAC_BYTES);
     size_t tb = 0;
     if (n && lcbk_sort_pairs(nullptr, &tb, keys, keys2, vals, vals2, (u32)m, end_bit, s) < 0) { set_err("msm: sort query"); return -1; }
-    void *temp = b_msm[10].get(tb);
+    void *temp = b[10].get(tb);
     if (!keys || !keys2 || !vals || !vals2 || !st || !en || !buckets || !segs || !l1 || !wins || !temp) {
         set_err("msm: device allocation failed");
         return -1;
     }
-    hipEventRecord(g_msm_ev[0], s);
+    hipEventRecord(cx->msm_ev[0], s);
     if (n) lcbk_msm_digits(dim3(nblk(n)), s, scalars, (u32)n, c, nwin, keys, vals);
-    hipEventRecord(g_msm_ev[1], s);
+    hipEventRecord(cx->msm_ev[1], s);
     int alt = n ? lcbk_sort_pairs(temp, &tb, keys, keys2, vals, vals2, (u32)m, end_bit, s) : 0;
     if (alt < 0) { set_err("msm: radix sort"); return -1; }
     if (alt) { keys = keys2; vals = vals2; }
-    hipEventRecord(g_msm_ev[2], s);
+    hipEventRecord(cx->msm_ev[2], s);
     hipMemsetAsync(st, 0, (size_t)nb * 4, s);
     hipMemsetAsync(en, 0, (size_t)nb * 4, s);
     if (m) lcbk_msm_bounds(dim3(nblk(m)), s, keys, (u32)m, sentinel, st, en);
-    hipEventRecord(g_msm_ev[3], s);
+    hipEventRecord(cx->msm_ev[3], s);
     lcbk_msm_bucket_acc(dim3(nblk(nb)), s, pts, vals, st, en, nb, buckets);
-    hipEventRecord(g_msm_ev[4], s);
+    hipEventRecord(cx->msm_ev[4], s);
     lcbk_msm_bucket_reduce(dim3(nblk(n_seg)), s, buckets, half, L, n_seg, segs);
-    hipEventRecord(g_msm_ev[5], s);
+    hipEventRecord(cx->msm_ev[5], s);
     // per-window sums: LDS tree reductions of up to 256 segment sums per block, ping-ponging segs <-> l1
     void *cur = segs, *nxt = l1;
     for (u32 cnt = per_win, total = n_seg; cnt > 1;) {
@@ -987,63 +816,435 @@ static int msm_enqueue(void *out_jac, const void *pts, const uint8_t *scalars, s
     }
     if (per_win == 1) hipMemcpyAsync(wins, segs, (size_t)nwin * LCB_G1_JAC_BYTES, hipMemcpyDeviceToDevice, s);
     lcbk_msm_horner(s, wins, nwin, c, out_jac);
-    hipEventRecord(g_msm_ev[6], s);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) { set_err("msm launch", e); return -1; }
+    hipEventRecord(cx->msm_ev[6], s);
+    cx->msm_ran = true;
+    return launched("msm launch") ? 0 : -1;
+}
+
+} // namespace
+
+extern "C" lcb_ctx *lcb_ctx_create(void) { return ctx_new(); }
+extern "C" void lcb_ctx_destroy(lcb_ctx *ctx) {
+    if (!ctx) return;
+    { std::lock_guard<std::recursive_mutex> lk(ctx->mu); }
+    ctx_free(ctx);
+}
+extern "C" int lcb_ctx_synchronize(lcb_ctx *ctx) {
+    CTX_OR(c, ctx, -1)
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    if (!c->order_valid) return 0;
+    hipError_t e = hipEventSynchronize(c->order);
+    if (e != hipSuccess) { set_err("context synchronize", e); return -1; }
     return 0;
+}
+
+// ================================================================== batch: TPKE
+extern "C" int lcb_ctx_tpke_prepare_dev(lcb_ctx *ctx, const uint8_t *y_keys, size_t n_keys, const uint8_t *cts_u,
+                                        const uint8_t *cts_w, const uint8_t *v_data, const uint32_t *v_off,
+                                        size_t n_cts, void *stream) {
+    CTX_OR(c, ctx, -1)
+    Enq q(c, (hipStream_t)stream);
+    return tpke_prepare(c, y_keys, n_keys, cts_u, cts_w, v_data, v_off, n_cts, q.s);
+}
+extern "C" int lcb_ctx_tpke_verify_prepared_dev(lcb_ctx *ctx, uint8_t *accept, size_t n, size_t n_keys, size_t n_cts,
+                                                const uint32_t *ct_idx, const uint32_t *dec_idx, const uint8_t *ui,
+                                                void *stream) {
+    CTX_OR(c, ctx, -1)
+    Enq q(c, (hipStream_t)stream);
+    return tpke_verify_prepared(c, accept, n, n_keys, n_cts, ct_idx, dec_idx, ui, q.s);
+}
+extern "C" int lcb_ctx_tpke_partial_decrypt_prepared_dev(lcb_ctx *ctx, uint8_t *ui_out, uint8_t *status,
+                                                         const uint8_t *x_raw, size_t x_stride, const uint8_t *cts_u,
+                                                         size_t n_cts, void *stream) {
+    CTX_OR(c, ctx, -1)
+    Enq q(c, (hipStream_t)stream);
+    return tpke_partial_decrypt_prepared(c, ui_out, status, x_raw, x_stride, cts_u, n_cts, q.s);
+}
+extern "C" int lcb_ctx_tpke_combine_dev(lcb_ctx *ctx, uint8_t *u_out, uint8_t *status, const uint8_t *accept,
+                                        const uint8_t *shares, size_t per_ct, size_t k, size_t n_cts, void *stream) {
+    CTX_OR(c, ctx, -1)
+    Enq q(c, (hipStream_t)stream);
+    return assemble_enqueue(c, 1, u_out, status, accept, shares, per_ct, k, n_cts, q.s);
+}
+extern "C" int lcb_ctx_tpke_verify_phase_ms(lcb_ctx *ctx, float ms[2]) {
+    CTX_OR(c, ctx, -1)
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    if (!c->ver_ran) { set_err("tpke verify: no split verify has run in this context"); return -1; }
+    if (hipEventSynchronize(c->ver_ev[2]) != hipSuccess) { set_err("tpke verify: event sync"); return -1; }
+    for (int i = 0; i < 2; i++)
+        if (hipEventElapsedTime(&ms[i], c->ver_ev[i], c->ver_ev[i + 1]) != hipSuccess) ms[i] = -1.0f;
+    return 0;
+}
+
+extern "C" int lcb_tpke_prepare_dev(const uint8_t *y_keys, size_t n_keys, const uint8_t *cts_u, const uint8_t *cts_w,
+                                    const uint8_t *v_data, const uint32_t *v_off, size_t n_cts, void *stream) {
+    return lcb_ctx_tpke_prepare_dev(nullptr, y_keys, n_keys, cts_u, cts_w, v_data, v_off, n_cts, stream);
+}
+extern "C" int lcb_tpke_verify_prepared_dev(uint8_t *accept, size_t n, size_t n_keys, size_t n_cts, const uint32_t *ct_idx,
+                                            const uint32_t *dec_idx, const uint8_t *ui, void *stream) {
+    return lcb_ctx_tpke_verify_prepared_dev(nullptr, accept, n, n_keys, n_cts, ct_idx, dec_idx, ui, stream);
+}
+extern "C" int lcb_tpke_partial_decrypt_prepared_dev(uint8_t *ui_out, uint8_t *status, const uint8_t *x_raw,
+                                                     size_t x_stride, const uint8_t *cts_u, size_t n_cts, void *stream) {
+    return lcb_ctx_tpke_partial_decrypt_prepared_dev(nullptr, ui_out, status, x_raw, x_stride, cts_u, n_cts, stream);
+}
+extern "C" int lcb_tpke_combine_dev(uint8_t *u_out, uint8_t *status, const uint8_t *accept, const uint8_t *shares,
+                                    size_t per_ct, size_t k, size_t n_cts, void *stream) {
+    return lcb_ctx_tpke_combine_dev(nullptr, u_out, status, accept, shares, per_ct, k, n_cts, stream);
+}
+extern "C" int lcb_tpke_verify_phase_ms(float ms[2]) { return lcb_ctx_tpke_verify_phase_ms(nullptr, ms); }
+extern "C" int lcb_tpke_verify_shares_dev(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys,
+                                          const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
+                                          const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
+                                          const uint32_t *dec_idx, const uint8_t *ui, void *stream) {
+    CTX_OR(c, nullptr, -1)
+    Enq q(c, (hipStream_t)stream);
+    if (tpke_prepare(c, y_keys, n_keys, cts_u, cts_w, v_data, v_off, n_cts, q.s)) return -1;
+    return tpke_verify_prepared(c, accept, n, n_keys, n_cts, ct_idx, dec_idx, ui, q.s);
+}
+extern "C" int lcb_tpke_verify_shares(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys,
+                                      const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
+                                      const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
+                                      const uint32_t *dec_idx, const uint8_t *ui) {
+    SYNC_CTX_OR(c, -1)
+    for (size_t i = 0; i < n; i++) {
+        if (ct_idx[i] >= n_cts) { set_err("ct_idx out of range"); return -1; }
+        if (dec_idx[i] >= n_keys) { set_err("dec_idx out of range"); return -1; }
+    }
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    size_t vbytes = n_cts ? v_off[n_cts] : 0;
+    const uint8_t *dy = up(c->in[0], y_keys, 48 * n_keys, s);
+    const uint8_t *du = up(c->in[1], cts_u, 48 * n_cts, s);
+    const uint8_t *dw = up(c->in[2], cts_w, 96 * n_cts, s);
+    const uint8_t *dv = up(c->in[3], v_data, vbytes, s);
+    const uint32_t *dvo = up(c->in[4], v_off, n_cts + 1, s);
+    const uint32_t *dct = up(c->in[5], ct_idx, n, s);
+    const uint32_t *ddec = up(c->in[6], dec_idx, n, s);
+    const uint8_t *dui = up(c->in[7], ui, 48 * n, s);
+    uint8_t *dacc = (uint8_t *)c->out[0].get(n);
+    if (!dy || !du || !dw || !dv || !dvo || !dct || !ddec || !dui || !dacc) { set_err("device allocation failed"); return -1; }
+    if (tpke_prepare(c, dy, n_keys, du, dw, dv, dvo, n_cts, s)) return -1;
+    if (tpke_verify_prepared(c, dacc, n, n_keys, n_cts, dct, ddec, dui, s)) return -1;
+    if (n) hipMemcpyAsync(accept, dacc, n, hipMemcpyDeviceToHost, s);
+    return sync_check(c, "tpke verify") ? 0 : -1;
+}
+
+extern "C" int lcb_tpke_partial_decrypt(uint8_t *ui_out, uint8_t *status, const uint8_t x[32], const uint8_t *cts_u,
+                                        const uint8_t *cts_w, const uint8_t *v_data, const uint32_t *v_off,
+                                        size_t n_cts) {
+    SYNC_CTX_OR(c, -1)
+    if (!n_cts) return 0;
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    size_t vbytes = v_off[n_cts];
+    const uint8_t *du = up(c->in[1], cts_u, 48 * n_cts, s);
+    const uint8_t *dw = up(c->in[2], cts_w, 96 * n_cts, s);
+    const uint8_t *dv = up(c->in[3], v_data, vbytes, s);
+    const uint32_t *dvo = up(c->in[4], v_off, n_cts + 1, s);
+    const uint8_t *dx = up(c->in[0], x, 32, s);
+    uint8_t *dui = (uint8_t *)c->out[0].get(48 * n_cts);
+    uint8_t *dst = (uint8_t *)c->out[1].get(n_cts);
+    if (!du || !dw || !dv || !dvo || !dx || !dui || !dst) { set_err("device allocation failed"); return -1; }
+    if (tpke_prepare(c, nullptr, 0, du, dw, dv, dvo, n_cts, s)) return -1;
+    if (tpke_partial_decrypt_prepared(c, dui, dst, dx, 0, du, n_cts, s)) return -1;
+    hipMemcpyAsync(ui_out, dui, 48 * n_cts, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(status, dst, n_cts, hipMemcpyDeviceToHost, s);
+    return sync_check(c, "tpke partial decrypt") ? 0 : -1;
+}
+
+extern "C" int lcb_tpke_encrypt_phase1(uint8_t *u_out, uint8_t *t_out, const uint8_t y[48], const uint8_t *r, size_t n) {
+    SYNC_CTX_OR(c, -1)
+    if (!n) return 0;
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    const uint8_t *dy = up(c->in[0], y, 48, s);
+    const uint8_t *dr = up(c->in[1], r, 32 * n, s);
+    uint8_t *du = (uint8_t *)c->out[0].get(48 * n), *dt = (uint8_t *)c->out[1].get(48 * n), *dok = (uint8_t *)c->out[2].get(n);
+    if (!dy || !dr || !du || !dt || !dok) { set_err("device allocation failed"); return -1; }
+    lcbk_tpke_encrypt1(dim3(nblk(n)), s, dy, dr, (u32)n, du, dt, dok);
+    std::vector<uint8_t> ok(n);
+    hipMemcpyAsync(u_out, du, 48 * n, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(t_out, dt, 48 * n, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, s);
+    if (!sync_check(c, "tpke encrypt1")) return -1;
+    for (size_t i = 0; i < n; i++) if (!ok[i]) { set_err("invalid public key or scalar"); return -1; }
+    return 0;
+}
+extern "C" int lcb_tpke_encrypt_phase2(uint8_t *w_out, const uint8_t *u, const uint8_t *r, const uint8_t *v_data,
+                                       const uint32_t *v_off, size_t n) {
+    SYNC_CTX_OR(c, -1)
+    if (!n) return 0;
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    const uint8_t *du = up(c->in[0], u, 48 * n, s);
+    const uint8_t *dr = up(c->in[1], r, 32 * n, s);
+    const uint8_t *dv = up(c->in[2], v_data, v_off[n], s);
+    const uint32_t *dvo = up(c->in[3], v_off, n + 1, s);
+    uint8_t *dw = (uint8_t *)c->out[0].get(96 * n), *dok = (uint8_t *)c->out[1].get(n);
+    if (!du || !dr || !dv || !dvo || !dw || !dok) { set_err("device allocation failed"); return -1; }
+    lcbk_tpke_encrypt2(dim3(nblk(n)), s, du, dr, dv, dvo, (u32)n, dw, dok, g_orig_cofactor);
+    std::vector<uint8_t> ok(n);
+    hipMemcpyAsync(w_out, dw, 96 * n, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, s);
+    if (!sync_check(c, "tpke encrypt2")) return -1;
+    for (size_t i = 0; i < n; i++) if (!ok[i]) { set_err("hash-to-G2 failed"); return -1; }
+    return 0;
+}
+
+// ================================================================== batch: threshold signatures
+extern "C" int lcb_ctx_ts_prepare_dev(lcb_ctx *ctx, const uint8_t *pks, size_t n_pks, const uint8_t *msg_data,
+                                      const uint32_t *msg_off, size_t n_msgs, void *stream) {
+    CTX_OR(c, ctx, -1)
+    Enq q(c, (hipStream_t)stream);
+    return ts_prepare(c, pks, n_pks, msg_data, msg_off, n_msgs, q.s);
+}
+extern "C" int lcb_ctx_ts_verify_prepared_dev(lcb_ctx *ctx, uint8_t *accept, size_t n, size_t n_pks, size_t n_msgs,
+                                              const uint8_t *sigs, const uint32_t *msg_idx, const uint32_t *pk_idx,
+                                              void *stream) {
+    CTX_OR(c, ctx, -1)
+    Enq q(c, (hipStream_t)stream);
+    return ts_verify_prepared(c, accept, n, n_pks, n_msgs, sigs, msg_idx, pk_idx, q.s);
+}
+extern "C" int lcb_ctx_ts_assemble_dev(lcb_ctx *ctx, uint8_t *sig_out, uint8_t *status, const uint8_t *accept,
+                                       const uint8_t *sigs, size_t per_round, size_t k, size_t n_rounds, void *stream) {
+    CTX_OR(c, ctx, -1)
+    Enq q(c, (hipStream_t)stream);
+    return assemble_enqueue(c, 2, sig_out, status, accept, sigs, per_round, k, n_rounds, q.s);
+}
+extern "C" int lcb_ts_prepare_dev(const uint8_t *pks, size_t n_pks, const uint8_t *msg_data, const uint32_t *msg_off,
+                                  size_t n_msgs, void *stream) {
+    return lcb_ctx_ts_prepare_dev(nullptr, pks, n_pks, msg_data, msg_off, n_msgs, stream);
+}
+extern "C" int lcb_ts_verify_prepared_dev(uint8_t *accept, size_t n, size_t n_pks, size_t n_msgs, const uint8_t *sigs,
+                                          const uint32_t *msg_idx, const uint32_t *pk_idx, void *stream) {
+    return lcb_ctx_ts_verify_prepared_dev(nullptr, accept, n, n_pks, n_msgs, sigs, msg_idx, pk_idx, stream);
+}
+extern "C" int lcb_ts_assemble_dev(uint8_t *sig_out, uint8_t *status, const uint8_t *accept, const uint8_t *sigs,
+                                   size_t per_round, size_t k, size_t n_rounds, void *stream) {
+    return lcb_ctx_ts_assemble_dev(nullptr, sig_out, status, accept, sigs, per_round, k, n_rounds, stream);
+}
+extern "C" int lcb_ts_verify_shares_dev(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks, const uint8_t *sigs,
+                                        const uint8_t *msg_data, const uint32_t *msg_off, size_t n_msgs,
+                                        const uint32_t *msg_idx, const uint32_t *pk_idx, void *stream) {
+    CTX_OR(c, nullptr, -1)
+    Enq q(c, (hipStream_t)stream);
+    if (ts_prepare(c, pks, n_pks, msg_data, msg_off, n_msgs, q.s)) return -1;
+    return ts_verify_prepared(c, accept, n, n_pks, n_msgs, sigs, msg_idx, pk_idx, q.s);
+}
+extern "C" int lcb_ts_verify_shares(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks, const uint8_t *sigs,
+                                    const uint8_t *msg_data, const uint32_t *msg_off, size_t n_msgs,
+                                    const uint32_t *msg_idx, const uint32_t *pk_idx) {
+    SYNC_CTX_OR(c, -1)
+    for (size_t i = 0; i < n; i++) {
+        if (msg_idx[i] >= n_msgs) { set_err("msg_idx out of range"); return -1; }
+        if (pk_idx[i] >= n_pks) { set_err("pk_idx out of range"); return -1; }
+    }
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    size_t mbytes = n_msgs ? msg_off[n_msgs] : 0;
+    const uint8_t *dpk = up(c->in[0], pks, 48 * n_pks, s);
+    const uint8_t *dsig = up(c->in[1], sigs, 96 * n, s);
+    const uint8_t *dm = up(c->in[2], msg_data, mbytes, s);
+    const uint32_t *dmo = up(c->in[3], msg_off, n_msgs + 1, s);
+    const uint32_t *dmi = up(c->in[4], msg_idx, n, s);
+    const uint32_t *dpi = up(c->in[5], pk_idx, n, s);
+    uint8_t *dacc = (uint8_t *)c->out[0].get(n);
+    if (!dpk || !dsig || !dm || !dmo || !dmi || !dpi || !dacc) { set_err("device allocation failed"); return -1; }
+    if (ts_prepare(c, dpk, n_pks, dm, dmo, n_msgs, s)) return -1;
+    if (ts_verify_prepared(c, dacc, n, n_pks, n_msgs, dsig, dmi, dpi, s)) return -1;
+    if (n) hipMemcpyAsync(accept, dacc, n, hipMemcpyDeviceToHost, s);
+    return sync_check(c, "ts verify") ? 0 : -1;
+}
+extern "C" int lcb_ts_sign(uint8_t *sigs_out, const uint8_t *sks, const uint8_t *msg_data, const uint32_t *msg_off,
+                           const uint32_t *msg_idx, size_t n) {
+    SYNC_CTX_OR(c, -1)
+    if (!n) return 0;
+    u32 nm = 0;
+    for (size_t i = 0; i < n; i++) nm = msg_idx[i] + 1 > nm ? msg_idx[i] + 1 : nm;
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    const uint8_t *dsk = up(c->in[0], sks, 32 * n, s);
+    const uint8_t *dm = up(c->in[1], msg_data, msg_off[nm], s);
+    const uint32_t *dmo = up(c->in[2], msg_off, nm + 1, s);
+    const uint32_t *dmi = up(c->in[3], msg_idx, n, s);
+    uint8_t *dsig = (uint8_t *)c->out[0].get(96 * n), *dok = (uint8_t *)c->out[1].get(n);
+    if (!dsk || !dm || !dmo || !dmi || !dsig || !dok) { set_err("device allocation failed"); return -1; }
+    lcbk_ts_sign(dim3(nblk(n)), s, dsk, dm, dmo, dmi, (u32)n, dsig, dok, g_orig_cofactor);
+    std::vector<uint8_t> ok(n);
+    hipMemcpyAsync(sigs_out, dsig, 96 * n, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, s);
+    if (!sync_check(c, "ts sign")) return -1;
+    for (size_t i = 0; i < n; i++) if (!ok[i]) { set_err("invalid key share"); return -1; }
+    return 0;
+}
+
+// ================================================================== coin consumers (CoinResult.Parity, block nonce)
+extern "C" int lcb_coin_parity(const uint8_t *sig_bytes, size_t len) {
+    uint32_t acc = 0;
+    for (size_t i = 0; i < len; i++) acc ^= sig_bytes[i];
+    return __builtin_popcount(acc) & 1;
+}
+extern "C" uint64_t lcb_coin_nonce(const uint8_t *sig_bytes, size_t len) {
+    uint8_t r[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (size_t i = 0; i < len; i++) r[i % 8] ^= sig_bytes[i];
+    uint64_t v = 0;
+    for (int j = 7; j >= 0; j--) v = (v << 8) | r[j];
+    return v;
+}
+extern "C" int lcb_coin_fold_dev(uint8_t *parity, uint64_t *nonce, const uint8_t *sigs, size_t n, void *stream) {
+    if (!ready()) return -1;
+    if (n > 0xffffffffu) { set_err("coin fold: batch too large"); return -1; }
+    if (n) lcbk_coin_fold(dim3(nblk(n)), (hipStream_t)stream, sigs, (u32)n, parity, nonce);
+    return launched("coin fold launch") ? 0 : -1;
+}
+
+// ================================================================== batch: Lagrange, scalar mul, hash, MSM
+static int lagrange_batch(int g, uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys, const uint32_t *off,
+                          size_t np) {
+    SYNC_CTX_OR(c, -1)
+    if (!np) return 0;
+    Enq q(c, c->stream);
+    size_t ne = off[np];
+    size_t pb = g == 1 ? 48 : 96;
+    hipStream_t s = c->stream;
+    const uint8_t *dx = up(c->in[0], xs, 32 * ne, s);
+    const uint8_t *dy = up(c->in[1], ys, pb * ne, s);
+    const uint32_t *doff = up(c->in[2], off, np + 1, s);
+    uint8_t *dst = (uint8_t *)c->out[0].get(np), *dout = (uint8_t *)c->out[1].get(pb * np);
+    if (!dx || !dy || !doff || !dst || !dout) { set_err("device allocation failed"); return -1; }
+    if (lagrange_enqueue(c, g, dout, dst, dx, dy, doff, np, ne, s)) return -1;
+    hipMemcpyAsync(out, dout, pb * np, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(status, dst, np, hipMemcpyDeviceToHost, s);
+    return sync_check(c, "lagrange") ? 0 : -1;
+}
+extern "C" int lcb_ctx_g1_lagrange_dev(lcb_ctx *ctx, uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
+                                       const uint32_t *off, size_t n_problems, size_t n_entries, void *stream) {
+    CTX_OR(c, ctx, -1)
+    Enq q(c, (hipStream_t)stream);
+    return n_problems ? lagrange_enqueue(c, 1, out, status, xs, ys, off, n_problems, n_entries, q.s) : 0;
+}
+extern "C" int lcb_ctx_g2_lagrange_dev(lcb_ctx *ctx, uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
+                                       const uint32_t *off, size_t n_problems, size_t n_entries, void *stream) {
+    CTX_OR(c, ctx, -1)
+    Enq q(c, (hipStream_t)stream);
+    return n_problems ? lagrange_enqueue(c, 2, out, status, xs, ys, off, n_problems, n_entries, q.s) : 0;
+}
+extern "C" int lcb_g1_lagrange_dev(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
+                                   const uint32_t *off, size_t n_problems, size_t n_entries, void *stream) {
+    return lcb_ctx_g1_lagrange_dev(nullptr, out, status, xs, ys, off, n_problems, n_entries, stream);
+}
+extern "C" int lcb_g2_lagrange_dev(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
+                                   const uint32_t *off, size_t n_problems, size_t n_entries, void *stream) {
+    return lcb_ctx_g2_lagrange_dev(nullptr, out, status, xs, ys, off, n_problems, n_entries, stream);
+}
+extern "C" int lcb_g1_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
+                                     const uint32_t *off, size_t n) { return lagrange_batch(1, out, status, xs, ys, off, n); }
+extern "C" int lcb_g2_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
+                                     const uint32_t *off, size_t n) { return lagrange_batch(2, out, status, xs, ys, off, n); }
+
+static int mul_batch(int g, uint8_t *out, const uint8_t *points, int use_gen, const uint8_t *scalars, size_t n) {
+    SYNC_CTX_OR(c, -1)
+    if (!n) return 0;
+    if (n > 0xffffffffu) { set_err("mul batch: too large"); return -1; }
+    Enq q(c, c->stream);
+    size_t pb = g == 1 ? 48 : 96;
+    hipStream_t s = c->stream;
+    const uint8_t *dp = use_gen ? (const uint8_t *)c->in[0].get(16) : up(c->in[0], points, pb * n, s);
+    const uint8_t *dsc = up(c->in[1], scalars, 32 * n, s);
+    uint8_t *dout = (uint8_t *)c->out[0].get(pb * n), *dok = (uint8_t *)c->out[1].get(n);
+    if (!dp || !dsc || !dout || !dok) { set_err("device allocation failed"); return -1; }
+    if (g == 1) lcbk_g1_mul(dim3(nblk(n)), s, dp, use_gen, dsc, (u32)n, dout, dok);
+    else lcbk_g2_mul(dim3(nblk(n)), s, dp, use_gen, dsc, (u32)n, dout, dok);
+    std::vector<uint8_t> ok(n);
+    hipMemcpyAsync(out, dout, pb * n, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, s);
+    if (!sync_check(c, "mul batch")) return -1;
+    for (size_t i = 0; i < n; i++) if (!ok[i]) { set_err("invalid point or scalar"); return -1; }
+    return 0;
+}
+extern "C" int lcb_g1_mul_batch(uint8_t *out, const uint8_t *points, int gen, const uint8_t *scalars, size_t n) {
+    return mul_batch(1, out, points, gen, scalars, n);
+}
+extern "C" int lcb_g2_mul_batch(uint8_t *out, const uint8_t *points, int gen, const uint8_t *scalars, size_t n) {
+    return mul_batch(2, out, points, gen, scalars, n);
+}
+extern "C" int lcb_g2_hash_batch(uint8_t *out, const uint8_t *msg_data, const uint32_t *msg_off, size_t n) {
+    SYNC_CTX_OR(c, -1)
+    if (!n) return 0;
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    const uint8_t *dm = up(c->in[0], msg_data, msg_off[n], s);
+    const uint32_t *dmo = up(c->in[1], msg_off, n + 1, s);
+    uint8_t *dout = (uint8_t *)c->out[0].get(96 * n), *dok = (uint8_t *)c->out[1].get(n);
+    if (!dm || !dmo || !dout || !dok) { set_err("device allocation failed"); return -1; }
+    lcbk_g2_hash(dim3(nblk(n)), s, dm, dmo, (u32)n, dout, dok, g_orig_cofactor);
+    std::vector<uint8_t> ok(n);
+    hipMemcpyAsync(out, dout, 96 * n, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, s);
+    if (!sync_check(c, "hash batch")) return -1;
+    for (size_t i = 0; i < n; i++) if (!ok[i]) { set_err("hash-to-G2 failed"); return -1; }
+    return 0;
+}
+
+extern "C" int lcb_g1_msm_window(size_t n) { return (int)msm_window(n); }
+extern "C" int lcb_ctx_g1_msm_dev(lcb_ctx *ctx, void *out_jac, const void *points_aff, const uint8_t *scalars, size_t n,
+                                  int window_bits, void *stream) {
+    CTX_OR(c, ctx, -1)
+    Enq q(c, (hipStream_t)stream);
+    return msm_enqueue(c, out_jac, points_aff, scalars, n, window_bits, q.s);
 }
 extern "C" int lcb_g1_msm_dev(void *out_jac, const void *points_aff, const uint8_t *scalars, size_t n, int window_bits,
                               void *stream) {
-    LOCKED_OR(-1)
-    return msm_enqueue(out_jac, points_aff, scalars, n, window_bits, (hipStream_t)stream);
+    return lcb_ctx_g1_msm_dev(nullptr, out_jac, points_aff, scalars, n, window_bits, stream);
 }
-extern "C" int lcb_g1_msm_phase_ms(float *ms, int n_phases) {
-    LOCKED_OR(-1)
-    if (!g_msm_ev_ready) { set_err("msm: no MSM has run"); return -1; }
-    if (hipEventSynchronize(g_msm_ev[6]) != hipSuccess) { set_err("msm: event sync"); return -1; }
+extern "C" int lcb_ctx_g1_msm_phase_ms(lcb_ctx *ctx, float *ms, int n_phases) {
+    CTX_OR(c, ctx, -1)
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    if (!c->msm_ran) { set_err("msm: no MSM has run in this context"); return -1; }
+    if (hipEventSynchronize(c->msm_ev[6]) != hipSuccess) { set_err("msm: event sync"); return -1; }
     for (int i = 0; i < n_phases && i < 6; i++)
-        if (hipEventElapsedTime(&ms[i], g_msm_ev[i], g_msm_ev[i + 1]) != hipSuccess) ms[i] = -1.0f;
+        if (hipEventElapsedTime(&ms[i], c->msm_ev[i], c->msm_ev[i + 1]) != hipSuccess) ms[i] = -1.0f;
     return 0;
 }
+extern "C" int lcb_g1_msm_phase_ms(float *ms, int n_phases) { return lcb_ctx_g1_msm_phase_ms(nullptr, ms, n_phases); }
 extern "C" int lcb_g1_to_affine_dev(void *out_aff, uint8_t *ok, const uint8_t *points, size_t n, void *stream) {
-    LOCKED_OR(-1)
+    if (!ready()) return -1;
+    if (n > 0xffffffffu) { set_err("to_affine: batch too large"); return -1; }
     if (n) lcbk_g1_to_affine(dim3(nblk(n)), (hipStream_t)stream, points, (u32)n, out_aff, ok);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) { set_err("to_affine launch", e); return -1; }
-    return 0;
+    return launched("to_affine launch") ? 0 : -1;
 }
 extern "C" int lcb_g1_jac_sum_dev(uint8_t *out48, void *out_jac, const void *parts, size_t k, void *stream) {
-    LOCKED_OR(-1)
-    hipStream_t s = (hipStream_t)stream;
-    void *acc = out_jac ? out_jac : b_msm[11].get(LCB_G1_JAC_BYTES);
+    CTX_OR(c, nullptr, -1)
+    Enq q(c, (hipStream_t)stream);
+    void *acc = out_jac ? out_jac : c->msm[11].get(LCB_G1_JAC_BYTES);
     if (!acc) { set_err("device allocation failed"); return -1; }
-    lcbk_g1_jac_reduce_groups(dim3(1), s, parts, (u32)k, k ? (u32)k : 1u, acc);
-    if (out48) lcbk_g1_jac_compress(dim3(1), s, acc, 1, out48);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) { set_err("jac sum launch", e); return -1; }
-    return 0;
+    lcbk_g1_jac_reduce_groups(dim3(1), q.s, parts, (u32)k, k ? (u32)k : 1u, acc);
+    if (out48) lcbk_g1_jac_compress(dim3(1), q.s, acc, 1, out48);
+    return launched("jac sum launch") ? 0 : -1;
 }
 extern "C" int lcb_g1_msm(uint8_t out[48], const uint8_t *points, const uint8_t *scalars, size_t n) {
-    LOCKED_OR(-1)
-    hipStream_t s = g_stream;
+    SYNC_CTX_OR(c, -1)
     if (n == 0) { memset(out, 0, 48); return 0; }
     for (size_t i = 0; i < n; i++) {   // mclBnFr values are canonical (< r); reject what mcl would not hold
         const uint8_t *sc = scalars + 32 * i;
         if (!fr_bytes_lt_r(sc)) { set_err("invalid point or scalar"); return -1; }
     }
-    const uint8_t *dp = up(b_in[0], points, 48 * n, s);
-    const uint8_t *dsc = up(b_in[1], scalars, 32 * n, s);
-    void *aff = b_in[2].get(96 * n);
-    uint8_t *dok = (uint8_t *)b_out[0].get(n), *dout = (uint8_t *)b_out[1].get(48);
-    void *jac = b_out[2].get(LCB_G1_JAC_BYTES);
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    const uint8_t *dp = up(c->in[0], points, 48 * n, s);
+    const uint8_t *dsc = up(c->in[1], scalars, 32 * n, s);
+    void *aff = c->in[2].get(96 * n);
+    uint8_t *dok = (uint8_t *)c->out[0].get(n), *dout = (uint8_t *)c->out[1].get(48);
+    void *jac = c->out[2].get(LCB_G1_JAC_BYTES);
     if (!dp || !dsc || !aff || !dok || !dout || !jac) { set_err("device allocation failed"); return -1; }
     lcbk_g1_to_affine(dim3(nblk(n)), s, dp, (u32)n, aff, dok);
-    if (msm_enqueue(jac, aff, dsc, n, 0, s)) return -1;
+    if (msm_enqueue(c, jac, aff, dsc, n, 0, s)) return -1;
     lcbk_g1_jac_compress(dim3(1), s, jac, 1, dout);
     std::vector<uint8_t> ok(n);
     hipMemcpyAsync(out, dout, 48, hipMemcpyDeviceToHost, s);
     hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, s);
-    if (!sync_check("msm")) return -1;
+    if (!sync_check(c, "msm")) return -1;
     for (size_t i = 0; i < n; i++) if (!ok[i]) { set_err("invalid point or scalar"); return -1; }
     return 0;
 }

@@ -96,7 +96,19 @@ _SIGS = {
     "lcb_g2_mul_batch": (ctypes.c_int, [c_u8p, c_u8p, ctypes.c_int, c_u8p, c_size]),
     "lcb_g2_hash_batch": (ctypes.c_int, [c_u8p, c_u8p, c_u32p, c_size]),
     "lcb_xor_with_hash": (None, [c_u8p, c_u8p, c_u8p, c_size]),
+    "lcb_coin_parity": (ctypes.c_int, [c_u8p, c_size]),
+    "lcb_coin_nonce": (ctypes.c_uint64, [c_u8p, c_size]),
+    "lcb_coin_fold_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_size, ctypes.c_void_p]),
+    "lcb_ctx_create": (ctypes.c_void_p, []),
+    "lcb_ctx_destroy": (None, [ctypes.c_void_p]),
+    "lcb_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
 }
+# explicit-context forms: the context pointer first, then the same arguments as the context-less form
+for _name in ("tpke_prepare_dev", "tpke_verify_prepared_dev", "tpke_partial_decrypt_prepared_dev", "tpke_combine_dev",
+              "tpke_verify_phase_ms", "ts_prepare_dev", "ts_verify_prepared_dev", "ts_assemble_dev", "g1_lagrange_dev",
+              "g2_lagrange_dev", "g1_msm_dev", "g1_msm_phase_ms"):
+    _res, _args = _SIGS["lcb_" + _name]
+    _SIGS["lcb_ctx_" + _name] = (_res, [ctypes.c_void_p] + list(_args))
 
 
 def load(check_device=True):
@@ -342,6 +354,43 @@ def xor_with_hash(g1_48, data):
     ob, po = _out(len(data))
     load(False).lcb_xor_with_hash(po, pg, pd, len(data))
     return bytes(ob)[: len(data)]
+
+
+def coin_parity(sig: bytes) -> bool:
+    """CoinResult.Parity of the combined signature bytes (src/Lachain.Consensus/CommonCoin/CoinResult.cs:16-20)."""
+    keep = []
+    _, p = _bytes_ptr_keep(keep, sig)
+    return bool(load(False).lcb_coin_parity(p, len(sig)))
+
+
+def coin_nonce(sig: bytes) -> int:
+    """RootProtocol.GetNonceFromCoin (src/Lachain.Consensus/RootProtocol/RootProtocol.cs:316-322)."""
+    keep = []
+    _, p = _bytes_ptr_keep(keep, sig)
+    return int(load(False).lcb_coin_nonce(p, len(sig)))
+
+
+class Context:
+    """An explicit lcb_ctx (include/lachain_bls.h): private device workspaces, enqueue-ordered across streams."""
+
+    def __init__(self):
+        self.ptr = lib().lcb_ctx_create()
+        if not self.ptr:
+            raise RuntimeError("lcb_ctx_create failed: " + last_error())
+
+    def synchronize(self):
+        _check(lib().lcb_ctx_synchronize(self.ptr), "ctx_synchronize")
+
+    def close(self):
+        if self.ptr:
+            lib().lcb_ctx_destroy(self.ptr)
+            self.ptr = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def set_original_g2_cofactor(enable):

@@ -89,6 +89,9 @@ void orc_sha256(uint8_t out[32], const uint8_t *m, size_t n);
 void orc_sha3_256(uint8_t out[32], const uint8_t *m, size_t n);
 /* TPKE Utils.XorWithHash: BouncyCastle DigestRandomGenerator(Sha3Digest) keystream XOR */
 void orc_xor_with_hash(uint8_t *out, const uint8_t g1[48], const uint8_t *data, size_t len);
+/* CoinResult.Parity / RootProtocol.GetNonceFromCoin over serialized signature bytes */
+int orc_coin_parity(const uint8_t *bytes, size_t len);
+uint64_t orc_coin_nonce(const uint8_t *bytes, size_t len);
 
 /* ---- Lachain.Crypto protocol restatements ---- */
 /* TPKE.PublicKey.Encrypt with caller-supplied r (TPKE/PublicKey.cs:25-37) */

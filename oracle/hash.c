@@ -234,3 +234,27 @@ void orc_drg_bytes(uint8_t *out, size_t len, const uint8_t *seed, size_t seedlen
         out[i] = g.state[off++];
     }
 }
+
+/* ---- CommonCoin consumers of the combined signature bytes (row a13) ----
+   CoinResult.Parity (src/Lachain.Consensus/CommonCoin/CoinResult.cs:16-20):
+     p = RawBytes.Aggregate(0u, (i, b) => i ^ b); return Popcount(p) % 2 == 1   (BitsUtils.Popcount)
+   RootProtocol.GetNonceFromCoin (src/Lachain.Consensus/RootProtocol/RootProtocol.cs:316-322):
+     res[i % 8] ^= RawBytes[i]; return res.ToUInt64()  (little-endian, SerialiaztionUtils.cs:256-259) */
+int orc_coin_parity(const uint8_t *bytes, size_t len) {
+    uint32_t p = 0;
+    for (size_t i = 0; i < len; i++) p ^= bytes[i];
+    /* BitsUtils.Popcount, restated */
+    p -= p >> 1 & 0x55555555u;
+    p = (p & 0x33333333u) + (p >> 2 & 0x33333333u);
+    p = (p + (p >> 4)) & 0x0f0f0f0fu;
+    p += p >> 8;
+    p += p >> 16;
+    return (int)((p & 0x7f) % 2 == 1);
+}
+uint64_t orc_coin_nonce(const uint8_t *bytes, size_t len) {
+    uint8_t res[8] = {0};
+    for (size_t i = 0; i < len; i++) res[i % 8] ^= bytes[i];
+    uint64_t v = 0;
+    for (int j = 0; j < 8; j++) v |= (uint64_t)res[j] << (8 * j);
+    return v;
+}

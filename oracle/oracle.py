@@ -192,6 +192,16 @@ def xor_with_hash(g1b: bytes, data: bytes) -> bytes:
     return o.raw[: len(data)]
 
 
+def coin_parity(sig: bytes) -> bool:
+    return bool(lib().orc_coin_parity(sig, ctypes.c_size_t(len(sig))))
+
+
+def coin_nonce(sig: bytes) -> int:
+    f = lib().orc_coin_nonce
+    f.restype = ctypes.c_uint64
+    return int(f(sig, ctypes.c_size_t(len(sig))))
+
+
 # ---------------------------------------------------------------- protocol
 def tpke_encrypt(y, data, r):
     u, v, w = _buf(48), _buf(max(1, len(data))), _buf(96)
