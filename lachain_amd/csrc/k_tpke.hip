@@ -80,6 +80,9 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_miller(const u32 *lines, const
                                                          const g1a_st *keys, u32 n_keys, const u32 *ct_idx,
                                                          const u32 *dec_idx, const uint8_t *ui, u32 n, u32 *f_soa,
                                                          uint8_t *accept) {
+#ifdef LCB_LEAN_MILLER
+    __shared__ u32 lds_t[72 * LCB_BLOCK];   // one Fp6 temporary per lane (lean.hpp)
+#endif
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u32 c = ct_idx[i], d = dec_idx[i];
@@ -95,18 +98,37 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_miller(const u32 *lines, const
     LinesFromMemory sH{lines + (size_t)(2 * c) * LCB_LINESET_WORDS};
     LinesFromMemory sW{lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS};
     fp12 f;
+#ifdef LCB_LEAN_MILLER
+    miller2_lean(f, sH, Ui, sW, Y, LdsCol{lds_t + threadIdx.x});
+#else
     miller2(f, sH, Ui, sW, Y);
+#endif
     fp12_store_soa(f_soa, n, i, f);
     accept[i] = ok;
 }
-// accept[i] &= (final_exp(f_i) == 1)
-extern "C" __global__ void LCB_PAIR_BOUNDS k_final_exp_check(const u32 *f_soa, u32 n, uint8_t *accept) {
+// accept[i] &= (final_exp(f_i) == 1).  park: SoA Fp12 slots per item (lcbk_fe_slots()), slot 0 = f from the
+// Miller kernel.  LCB_LEAN_FE selects lean.hpp's slot form (pow-by-|z| base in LDS): measured 30 % slower
+// than the register form, so off by default.
+#ifdef LCB_LEAN_FE
+extern "C" int lcbk_fe_slots() { return 6; }
+#else
+extern "C" int lcbk_fe_slots() { return 1; }
+#endif
+extern "C" __global__ void LCB_PAIR_BOUNDS k_final_exp_check(u32 *park, u32 n, uint8_t *accept) {
+#ifdef LCB_LEAN_FE
+    __shared__ u32 lds_base[144 * LCB_BLOCK];
+#endif
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+#ifdef LCB_LEAN_FE
+    final_exp_slots(park, n, i, lds_base + threadIdx.x);
+    accept[i] = accept[i] && fe_slot_is_one(park, n, i, 4);
+#else
     fp12 f;
-    fp12_load_soa(f, f_soa, n, i);
+    fp12_load_soa(f, park, n, i);
     final_exp_inplace(f);
     accept[i] = accept[i] && fp12_is_one(f);
+#endif
 }
 
 // TPKE.PrivateKey.Decrypt: validity e(G, W) == e(U, H) <=> e(-G, W) e(U, H) == 1; then Ui = x U
@@ -154,8 +176,8 @@ extern "C" void lcbk_tpke_verify(dim3 grid, hipStream_t s, const u32 *lines, con
 extern "C" void lcbk_tpke_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, u32 *f_soa, uint8_t *accept) {
     LCB_LAUNCH(k_tpke_miller, lines, ct_ok, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, f_soa, accept);
 }
-extern "C" void lcbk_final_exp_check(dim3 grid, hipStream_t s, const u32 *f_soa, u32 n, uint8_t *accept) {
-    LCB_LAUNCH(k_final_exp_check, f_soa, n, accept);
+extern "C" void lcbk_final_exp_check(dim3 grid, hipStream_t s, u32 *park, u32 n, uint8_t *accept) {
+    LCB_LAUNCH(k_final_exp_check, park, n, accept);
 }
 extern "C" void lcbk_tpke_partial_decrypt(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, const uint8_t *cts_u, const void *x_raw, u32 x_stride, u32 n_cts, uint8_t *ui_out, uint8_t *status) {
     LCB_LAUNCH(k_tpke_partial_decrypt, lines, ct_ok, cts_u, (const fr *)x_raw, x_stride, n_cts, ui_out, status);

@@ -50,6 +50,9 @@ extern "C" __global__ void LCB_BOUNDS k_ts_verify(const u32 *lines, const uint8_
 extern "C" __global__ void LCB_PAIR_BOUNDS k_ts_miller(const u32 *lines, const uint8_t *msg_ok, u32 n_msgs, const g1a_st *pks,
                                                  u32 n_pks, const uint8_t *sigs, const u32 *msg_idx,
                                                  const u32 *pk_idx, u32 n, u32 *f_soa, uint8_t *accept) {
+#ifdef LCB_LEAN_MILLER
+    __shared__ u32 lds_t[72 * LCB_BLOCK];   // one Fp6 temporary per lane (lean.hpp)
+#endif
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u32 m = msg_idx[i], k = pk_idx[i];
@@ -68,7 +71,11 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_ts_miller(const u32 *lines, const u
     LinesOnTheFly sS;
     sS.init(S);
     fp12 f;
+#ifdef LCB_LEAN_MILLER
+    miller2_lean(f, sH, PK, sS, G, LdsCol{lds_t + threadIdx.x});
+#else
     miller2(f, sH, PK, sS, G);
+#endif
     fp12_store_soa(f_soa, n, i, f);
     accept[i] = ok;
 }

@@ -2,6 +2,7 @@
 #pragma once
 #include "h2g2.hpp"
 #include "pairing.hpp"
+#include "lean.hpp"
 #include "ops.h"
 
 #define LCB_BLOCK 256

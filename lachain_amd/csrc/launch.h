@@ -10,7 +10,8 @@ extern "C" void lcbk_g2_decompress(dim3 grid, hipStream_t s, const uint8_t *in, 
 extern "C" void lcbk_tpke_ct_prepare(dim3 grid, hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data, const u32 *v_off, u32 n_cts, u32 *lines, uint8_t *ct_ok, int orig_cof);
 extern "C" void lcbk_tpke_verify(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, uint8_t *accept);
 extern "C" void lcbk_tpke_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, u32 *f_soa, uint8_t *accept);
-extern "C" void lcbk_final_exp_check(dim3 grid, hipStream_t s, const u32 *f_soa, u32 n, uint8_t *accept);
+extern "C" int lcbk_fe_slots();
+extern "C" void lcbk_final_exp_check(dim3 grid, hipStream_t s, u32 *park, u32 n, uint8_t *accept);
 extern "C" void lcbk_tpke_partial_decrypt(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, const uint8_t *cts_u, const void *x_raw, u32 x_stride, u32 n_cts, uint8_t *ui_out, uint8_t *status);
 extern "C" void lcbk_ts_msg_prepare(dim3 grid, hipStream_t s, const uint8_t *msg_data, const u32 *msg_off, u32 n_msgs, u32 *lines, uint8_t *msg_ok, int orig_cof);
 extern "C" void lcbk_ts_verify(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *msg_ok, u32 n_msgs, const void *pks, u32 n_pks, const uint8_t *sigs, const u32 *msg_idx, const u32 *pk_idx, u32 n, uint8_t *accept);

@@ -646,7 +646,7 @@ int tpke_verify_prepared(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_keys,
         lcbk_tpke_verify(dim3(nblk(n)), s, lines, ctok, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct, d_dec, d_ui, (u32)n,
                          d_accept);
     } else if (n) {
-        u32 *f = (u32 *)c->t_f.get(n * 576);
+        u32 *f = (u32 *)c->t_f.get(n * 576 * (size_t)lcbk_fe_slots())   /* SoA Fp12 slots: Miller output (+ final-exp parking) */;
         if (!f) { set_err("device allocation failed"); return -1; }
         if (!c->ver_ev_ready) {
             for (auto &e : c->ver_ev) hipEventCreate(&e);
@@ -703,7 +703,7 @@ int ts_verify_prepared(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_pks, si
         lcbk_ts_verify(dim3(nblk(n)), s, lines, mok, (u32)n_msgs, c->s_keys.p, (u32)n_pks, d_sigs, d_midx, d_pidx, (u32)n,
                        d_accept);
     } else if (n) {
-        u32 *f = (u32 *)c->s_f.get(n * 576);
+        u32 *f = (u32 *)c->s_f.get(n * 576 * (size_t)lcbk_fe_slots())   /* SoA Fp12 slots: Miller output (+ final-exp parking) */;
         if (!f) { set_err("device allocation failed"); return -1; }
         lcbk_ts_miller(dim3(nblk(n)), s, lines, mok, (u32)n_msgs, c->s_keys.p, (u32)n_pks, d_sigs, d_midx, d_pidx, (u32)n,
                        f, d_accept);

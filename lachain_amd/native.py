@@ -8,7 +8,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblachain_bls.so")
+# LCB_LIB_PATH selects another build of the same library (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("LCB_LIB_PATH") or os.path.join(_HERE, "liblachain_bls.so")
 MCL_BLS12_381 = 5
 MCLBN_COMPILED_TIME_VAR = 46
 
