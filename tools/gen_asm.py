@@ -203,7 +203,7 @@ def r_fp_mul2():
 
 def r_fp2_mul():
     a = Asm()
-    a.label("lcb_r_fp2_mul")
+    a.label("lcb_r_fp2_mul_eager")
     P_ = 120
     load_p(a, P_)
     XA, XB, YA, YB, SA, SB = vr(0), vr(12), vr(24), vr(36), vr(48), vr(60)
@@ -255,7 +255,167 @@ def r_fp2_mul_fp():
     return a.text(), 92
 
 
-ROUTINES = [r_fp_mul, r_fp_mul2, r_fp2_mul, r_fp2_sqr, r_fp2_mul_fp]
+# ------------------------------------------------------------------ lazy (double-width) reduction
+P2X4 = 4 * P * P          # 4p^2 < 2^764: keeps T0 - T1 + 4p^2 positive for multiplicands < 2p
+P2X4L = [(P2X4 >> (32 * i)) & 0xFFFFFFFF for i in range(2 * N)]
+
+
+def products_plain(a, chains):
+    """Comba products T = a*b (24 words) for interleaved chains: dict(a=[12], b=[12], acc=base (4 regs, even),
+    out=[24 regs]).  out[k] is written at the end of column k and may alias a[k-11] (k >= 11: a[k-11]'s last
+    use is column k) — that is how the 24-word products fit in the registers the operands free."""
+    def ring(c, k):
+        r = c["acc"]
+        return (r, r + 1, r + 3) if k % 2 == 0 else (r + 2, r + 3, r + 1)
+
+    for c in chains:
+        a(f"v_mov_b32 v{c['acc']}, 0")
+        a(f"v_mov_b32 v{c['acc'] + 1}, 0")
+    for k in range(2 * N - 1):
+        terms = [(i, k - i) for i in range(max(0, k - (N - 1)), min(k, N - 1) + 1)]
+        for n_t, (i, j) in enumerate(terms):
+            for t, c in enumerate(chains):
+                L, H, C = ring(c, k)
+                a(f"v_mad_u64_u32 v[{L}:{H}], s[{CARRY[t]}:{CARRY[t] + 1}], v{c['a'][i]}, v{c['b'][j]}, v[{L}:{H}]")
+            for t, c in enumerate(chains):
+                L, H, C = ring(c, k)
+                sc = f"s[{CARRY[t]}:{CARRY[t] + 1}]"
+                a(f"v_addc_co_u32_e64 v{C}, {sc}, 0, {0 if n_t == 0 else 'v%d' % C}, {sc}")
+        for c in chains:
+            L, H, C = ring(c, k)
+            a(f"v_mov_b32 v{c['out'][k]}, v{L}")
+            if k == 2 * N - 2:
+                a(f"v_mov_b32 v{c['out'][2 * N - 1]}, v{H}")   # top word; the carry word is 0 (T < 2^768)
+            else:
+                L2, H2, C2 = ring(c, k + 1)
+                assert H2 == C
+                a(f"v_mov_b32 v{L2}, v{H}")
+
+
+def redc(a, chains, pbase):
+    """Montgomery reduction (U + m p) / 2^384 of 24-word U, product scanning, interleaved chains:
+    dict(u=[24 regs], m=[12 regs], acc=base, out=[12 regs]); out[j] may alias u[j + 12] (consumed at the start
+    of column j + 12).  For U < 8p^2 the result is < 2p (not yet reduced)."""
+    def ring(c, k):
+        r = c["acc"]
+        return (r, r + 1, r + 3) if k % 2 == 0 else (r + 2, r + 3, r + 1)
+
+    for c in chains:
+        a(f"v_mov_b32 v{c['acc']}, 0")
+        a(f"v_mov_b32 v{c['acc'] + 1}, 0")
+    for k in range(2 * N):
+        # acc += U_k (the column's carry word starts fresh here)
+        for t, c in enumerate(chains):
+            L, H, C = ring(c, k)
+            a(f"v_add_co_u32_e64 v{L}, s[{CARRY[t]}:{CARRY[t] + 1}], v{L}, v{c['u'][k]}")
+        for t, c in enumerate(chains):
+            L, H, C = ring(c, k)
+            sc = f"s[{CARRY[t]}:{CARRY[t] + 1}]"
+            a(f"v_addc_co_u32_e64 v{H}, {sc}, v{H}, 0, {sc}")
+        for t, c in enumerate(chains):
+            L, H, C = ring(c, k)
+            sc = f"s[{CARRY[t]}:{CARRY[t] + 1}]"
+            a(f"v_addc_co_u32_e64 v{C}, {sc}, 0, 0, {sc}")
+        terms = [(i, k - i) for i in range(max(0, k - (N - 1)), min(k - 1, N - 1) + 1)]
+        if k < N:
+            terms.append(("m", k))
+        for kind in terms:
+            if kind[0] == "m":
+                for c in chains:
+                    L, H, C = ring(c, k)
+                    a(f"v_mul_lo_u32 v{c['m'][k]}, v{L}, s{S_PINV}")
+                x = lambda c: c["m"][k]
+                y = pbase
+            else:
+                i, j = kind
+                x = lambda c, i=i: c["m"][i]
+                y = pbase + j
+            for t, c in enumerate(chains):
+                L, H, C = ring(c, k)
+                a(f"v_mad_u64_u32 v[{L}:{H}], s[{CARRY[t]}:{CARRY[t] + 1}], v{x(c)}, v{y}, v[{L}:{H}]")
+            for t, c in enumerate(chains):
+                L, H, C = ring(c, k)
+                sc = f"s[{CARRY[t]}:{CARRY[t] + 1}]"
+                a(f"v_addc_co_u32_e64 v{C}, {sc}, 0, v{C}, {sc}")
+        for c in chains:
+            L, H, C = ring(c, k)
+            if k >= N:
+                a(f"v_mov_b32 v{c['out'][k - N]}, v{L}")
+            if k < 2 * N - 1:
+                L2, H2, C2 = ring(c, k + 1)
+                assert H2 == C
+                a(f"v_mov_b32 v{L2}, v{H}")
+
+
+def wide_sub(a, r, x, y, sc):
+    """r <- x - y over len(r) words (borrow chain in SGPR pair sc)"""
+    a(f"v_sub_co_u32_e64 v{r[0]}, s[{sc}:{sc + 1}], v{x[0]}, v{y[0]}")
+    for j in range(1, len(r)):
+        a(f"v_subb_co_u32_e64 v{r[j]}, s[{sc}:{sc + 1}], v{x[j]}, v{y[j]}, s[{sc}:{sc + 1}]")
+
+
+def wide_add(a, r, x, y, sc):
+    a(f"v_add_co_u32_e64 v{r[0]}, s[{sc}:{sc + 1}], v{x[0]}, v{y[0]}")
+    for j in range(1, len(r)):
+        a(f"v_addc_co_u32_e64 v{r[j]}, s[{sc}:{sc + 1}], v{x[j]}, v{y[j]}, s[{sc}:{sc + 1}]")
+
+
+def interleave2(a, emit0, emit1):
+    """emit two independent chains alternately (each emit_k(asm) appends its instructions)"""
+    s0, s1 = Asm(), Asm()
+    emit0(s0)
+    emit1(s1)
+    l0, l1 = s0.lines, s1.lines
+    for k in range(max(len(l0), len(l1))):
+        if k < len(l0):
+            a.lines.append(l0[k])
+        if k < len(l1):
+            a.lines.append(l1[k])
+
+
+def reduce_to(a, dst, src, tmp, pbase, sc):
+    """dst <- src - p if src >= p else src (src < 2p); tmp: 12 scratch VGPRs"""
+    a(f"v_sub_co_u32_e64 v{tmp[0]}, s[{sc}:{sc + 1}], v{src[0]}, v{pbase}")
+    for j in range(1, N):
+        a(f"v_subb_co_u32_e64 v{tmp[j]}, s[{sc}:{sc + 1}], v{src[j]}, v{pbase + j}, s[{sc}:{sc + 1}]")
+    for j in range(N):
+        a(f"v_cndmask_b32_e64 v{dst[j]}, v{tmp[j]}, v{src[j]}, s[{sc}:{sc + 1}]")
+
+
+def r_fp2_mul_lazy():
+    """x*y in Fp2 with one Montgomery reduction per output coefficient (Karatsuba over double-width products):
+    T0 = xa ya, T1 = xb yb, T2 = (xa + xb)(ya + yb) as 768-bit comba products (3 interleaved chains),
+    U1 = T2 - T0 - T1, U0 = T0 - T1 + 4p^2, then REDC(U0), REDC(U1) (2 chains) and one conditional subtraction
+    each: 3 x 144 + 2 x 156 = 744 MADs instead of 3 x 300 = 900, and no modular add/sub chains.
+    Same contract as the eager routine: v[0:23] = x, v[24:47] = y in; v[0:23] = x*y out (fully reduced)."""
+    a = Asm()
+    a.label("lcb_r_fp2_mul")
+    P_ = 120
+    XA, XB, YA, YB, SA, SB = vr(0), vr(12), vr(24), vr(36), vr(48), vr(60)
+    F0, F1, F2 = vr(72), vr(84), vr(96)
+    T0 = F0[:11] + XA + [F0[11]]
+    T1 = F1[:11] + XB + [F1[11]]
+    T2 = F2[:11] + SA + [F2[11]]
+    D = YA + YB                                   # b operands are dead after the products
+    load_p(a, P_)
+    interleave2(a, lambda q: add_unreduced(q, SA, XA, XB, sc=S_TMP),
+                lambda q: add_unreduced(q, SB, YA, YB, sc=S_TMP2))
+    products_plain(a, [dict(a=XA, b=YA, acc=108, out=T0),
+                       dict(a=XB, b=YB, acc=112, out=T1),
+                       dict(a=SA, b=SB, acc=116, out=T2)])
+    interleave2(a, lambda q: wide_sub(q, T2, T2, T0, S_TMP), lambda q: wide_sub(q, D, T0, T1, S_TMP2))
+    wide_sub(a, T2, T2, T1, S_TMP)                # U1 = T2 - T0 - T1  (>= 0)
+    for j in range(2 * N):                        # 4p^2 into T1's registers
+        a(f"v_mov_b32 v{T1[j]}, 0x{P2X4L[j]:08x}")
+    wide_add(a, D, D, T1, S_TMP2)                 # U0 = T0 - T1 + 4p^2  (> 0, mod 2^768)
+    redc(a, [dict(u=D, m=F0, acc=108, out=D[N:]), dict(u=T2, m=F1, acc=112, out=T2[N:])], P_)
+    interleave2(a, lambda q: reduce_to(q, XA, D[N:], SB, P_, S_TMP),
+                lambda q: reduce_to(q, XB, T2[N:], F0, P_, S_TMP2))
+    a("s_setpc_b64 s[30:31]")
+    return a.text(), 132
+
+
+ROUTINES = [r_fp_mul, r_fp_mul2, r_fp2_mul, r_fp2_mul_lazy, r_fp2_sqr, r_fp2_mul_fp]
 
 
 def clobber_list(nvgpr, keep):
@@ -310,13 +470,22 @@ __device__ __forceinline__ void lcb_asm_fp_mul2(u32x12 &a0, u32x12 b0, u32x12 &a
         :
         : {clobber_list(nv['r_fp_mul2'], set(range(48)))});
 }}
-// x*y in Fp2: (xa, xb) <- (xa, xb) * (ya, yb)
+// x*y in Fp2: (xa, xb) <- (xa, xb) * (ya, yb); lazy reduction (one REDC per coefficient) unless LCB_FP2_MUL_EAGER
+#ifndef LCB_FP2_MUL_EAGER
 __device__ __forceinline__ void lcb_asm_fp2_mul(u32x12 &xa, u32x12 &xb, u32x12 ya, u32x12 yb) {{
     asm({call_seq("lcb_r_fp2_mul")}
         : "+{{v[0:11]}}"(xa), "+{{v[12:23]}}"(xb), "+{{v[24:35]}}"(ya), "+{{v[36:47]}}"(yb)
         :
+        : {clobber_list(nv['r_fp2_mul_lazy'], set(range(48)))});
+}}
+#else
+__device__ __forceinline__ void lcb_asm_fp2_mul(u32x12 &xa, u32x12 &xb, u32x12 ya, u32x12 yb) {{
+    asm({call_seq("lcb_r_fp2_mul_eager")}
+        : "+{{v[0:11]}}"(xa), "+{{v[12:23]}}"(xb), "+{{v[24:35]}}"(ya), "+{{v[36:47]}}"(yb)
+        :
         : {clobber_list(nv['r_fp2_mul'], set(range(48)))});
 }}
+#endif
 // x^2 in Fp2
 __device__ __forceinline__ void lcb_asm_fp2_sqr(u32x12 &xa, u32x12 &xb) {{
     asm({call_seq("lcb_r_fp2_sqr")}
