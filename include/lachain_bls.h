@@ -264,6 +264,26 @@ int lcb_ctx_g1_msm_dev(lcb_ctx *ctx, void *out_jac, const void *points_aff, cons
                        int window_bits, void *stream);
 int lcb_ctx_g1_msm_phase_ms(lcb_ctx *ctx, float *ms, int n_phases);
 
+/* ------------------------------------------------------------------ aggregation queue (one share per call)
+   The consensus code verifies one share per call from many protocol threads (HoneyBadger.cs:156-158,211-212,
+   ThresholdSigner.cs:62, AbstractProtocol.cs:46-47).  A queue aggregates such calls into GPU batches: submit
+   returns a ticket (> 0, or -1 on bad arguments), a worker thread runs the pending shares as one batch when
+   max_batch are pending or the oldest has waited max_delay_us, and lcb_queue_wait returns the share's decision
+   (1 accept, 0 reject, -1 batch error / unknown or already-waited ticket).  Decisions equal the batch entry
+   points' (PublicKey.VerifyShare, TPKE/PublicKey.cs:88-92; ValidateSignature, ThresholdSignature/PublicKey.cs:16-21).
+   destroy flushes and runs everything still pending; stats: {batches, shares, largest batch}. */
+typedef struct lcb_queue lcb_queue;
+lcb_queue *lcb_queue_create(size_t max_batch, uint32_t max_delay_us);
+void lcb_queue_destroy(lcb_queue *q);
+int64_t lcb_queue_tpke_verify(lcb_queue *q, const uint8_t y48[48], const uint8_t u48[48], const uint8_t *v,
+                              size_t v_len, const uint8_t w96[96], const uint8_t ui48[48]);
+int64_t lcb_queue_ts_verify(lcb_queue *q, const uint8_t pk48[48], const uint8_t *msg, size_t msg_len,
+                            const uint8_t sig96[96]);
+int lcb_queue_wait(lcb_queue *q, int64_t ticket);
+int lcb_queue_flush(lcb_queue *q);
+int lcb_queue_stats(lcb_queue *q, uint64_t out[3]);
+const char *lcb_queue_last_error(lcb_queue *q);
+
 /* ------------------------------------------------------------------ CommonCoin consumers (row a13)
    The combined signature's serialized bytes feed two consensus decisions:
    CoinResult.Parity = popcount(XOR of all bytes) is odd   (src/Lachain.Consensus/CommonCoin/CoinResult.cs:16-20)

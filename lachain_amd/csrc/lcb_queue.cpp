@@ -1,0 +1,239 @@
+// lachain_amd/csrc/lcb_queue.cpp — in-library aggregation queue for one-share-per-call callers.
+//
+// The reference verifies one share per call, from one thread per protocol instance:
+//   HoneyBadger.HandleDecryptedMessage -> PublicKey.VerifyShare   (src/Lachain.Consensus/HoneyBadger/HoneyBadger.cs:211-212)
+//   HoneyBadger.HandleCommonSubset filter                         (HoneyBadger.cs:156-158)
+//   ThresholdSigner.AddShare -> IsShareValid -> ValidateSignature  (src/Lachain.Crypto/ThresholdSignature/ThresholdSigner.cs:62)
+//   threads: AbstractProtocol.cs:46-47
+// A GPU launch per share would be latency-bound, so callers submit single shares and get a ticket; a worker thread
+// flushes the pending shares as ONE batch (lcb_tpke_verify_shares / lcb_ts_verify_shares on its own context) when
+// max_batch shares are pending or the oldest pending share is max_delay_us old, and lcb_queue_wait(ticket) returns
+// that share's decision.  Ciphertexts, verification keys and messages are de-duplicated per batch, so the batch
+// shares hash-to-G2 and Miller-line precomputation exactly as a caller-built batch would.  Decisions are the
+// same per-share results the batch entry points produce (bit-exact with VerifyShare / ValidateSignature).
+#include <stdint.h>
+#include <string.h>
+#include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/lachain_bls.h"
+
+namespace {
+using clk = std::chrono::steady_clock;
+
+struct TpkeItem {
+    int64_t ticket;
+    std::string key, ct;   // key = Y (48 B); ct = U (48) || W (96) || V
+    uint8_t ui[48];
+};
+struct TsItem {
+    int64_t ticket;
+    std::string pk, msg;   // pk 48 B
+    uint8_t sig[96];
+};
+}  // namespace
+
+struct lcb_queue {
+    std::mutex mu;
+    std::condition_variable cv_work, cv_done;
+    size_t max_batch;
+    std::chrono::microseconds max_delay;
+    std::vector<TpkeItem> tpke;
+    std::vector<TsItem> ts;
+    clk::time_point oldest;
+    bool stop = false, flush_now = false;
+    int64_t next_ticket = 1;
+    std::unordered_map<int64_t, int8_t> results;     // ticket -> 1 / 0 / -1 (batch failed), until waited for
+    int64_t done_upto = 0;                            // every ticket <= this has its result (batches are FIFO)
+    uint64_t batches = 0, items = 0, max_seen = 0;
+    std::string last_error;
+    std::thread worker;
+};
+
+namespace {
+
+void run_tpke(lcb_queue *q, std::vector<TpkeItem> &items) {
+    std::unordered_map<std::string, uint32_t> kidx, cidx;
+    std::vector<uint8_t> keys, us, ws, vs, uis(48 * items.size());
+    std::vector<uint32_t> voff(1, 0), ct(items.size()), dec(items.size());
+    for (size_t i = 0; i < items.size(); i++) {
+        TpkeItem &it = items[i];
+        auto k = kidx.emplace(it.key, (uint32_t)kidx.size());
+        if (k.second) keys.insert(keys.end(), it.key.begin(), it.key.end());
+        auto c = cidx.emplace(it.ct, (uint32_t)cidx.size());
+        if (c.second) {
+            const uint8_t *b = (const uint8_t *)it.ct.data();
+            us.insert(us.end(), b, b + 48);
+            ws.insert(ws.end(), b + 48, b + 144);
+            vs.insert(vs.end(), b + 144, b + it.ct.size());
+            voff.push_back((uint32_t)vs.size());
+        }
+        dec[i] = k.first->second;
+        ct[i] = c.first->second;
+        memcpy(&uis[48 * i], it.ui, 48);
+    }
+    std::vector<uint8_t> acc(items.size());
+    if (vs.empty()) vs.push_back(0);
+    int rc = lcb_tpke_verify_shares(acc.data(), items.size(), keys.data(), kidx.size(), us.data(), ws.data(), vs.data(),
+                                    voff.data(), cidx.size(), ct.data(), dec.data(), uis.data());
+    std::lock_guard<std::mutex> lk(q->mu);
+    if (rc) q->last_error = lcb_last_error();
+    for (size_t i = 0; i < items.size(); i++) q->results[items[i].ticket] = rc ? -1 : (int8_t)(acc[i] != 0);
+}
+
+void run_ts(lcb_queue *q, std::vector<TsItem> &items) {
+    std::unordered_map<std::string, uint32_t> pidx, midx;
+    std::vector<uint8_t> pks, msgs, sigs(96 * items.size());
+    std::vector<uint32_t> moff(1, 0), mi(items.size()), pi(items.size());
+    for (size_t i = 0; i < items.size(); i++) {
+        TsItem &it = items[i];
+        auto p = pidx.emplace(it.pk, (uint32_t)pidx.size());
+        if (p.second) pks.insert(pks.end(), it.pk.begin(), it.pk.end());
+        auto m = midx.emplace(it.msg, (uint32_t)midx.size());
+        if (m.second) {
+            msgs.insert(msgs.end(), it.msg.begin(), it.msg.end());
+            moff.push_back((uint32_t)msgs.size());
+        }
+        pi[i] = p.first->second;
+        mi[i] = m.first->second;
+        memcpy(&sigs[96 * i], it.sig, 96);
+    }
+    std::vector<uint8_t> acc(items.size());
+    if (msgs.empty()) msgs.push_back(0);
+    int rc = lcb_ts_verify_shares(acc.data(), items.size(), pks.data(), pidx.size(), sigs.data(), msgs.data(),
+                                  moff.data(), midx.size(), mi.data(), pi.data());
+    std::lock_guard<std::mutex> lk(q->mu);
+    if (rc) q->last_error = lcb_last_error();
+    for (size_t i = 0; i < items.size(); i++) q->results[items[i].ticket] = rc ? -1 : (int8_t)(acc[i] != 0);
+}
+
+void worker_loop(lcb_queue *q) {
+    std::unique_lock<std::mutex> lk(q->mu);
+    for (;;) {
+        size_t pending = q->tpke.size() + q->ts.size();
+        if (pending == 0) {
+            if (q->stop) return;
+            q->cv_work.wait(lk);
+            continue;
+        }
+        bool due = q->stop || q->flush_now || pending >= q->max_batch || clk::now() >= q->oldest + q->max_delay;
+        if (!due) {
+            q->cv_work.wait_until(lk, q->oldest + q->max_delay);
+            continue;
+        }
+        std::vector<TpkeItem> t;
+        std::vector<TsItem> s;
+        t.swap(q->tpke);
+        s.swap(q->ts);
+        q->flush_now = false;
+        q->batches++;
+        q->items += pending;
+        if (pending > q->max_seen) q->max_seen = pending;
+        lk.unlock();
+        int64_t top = 0;
+        for (auto &x : t) top = x.ticket > top ? x.ticket : top;
+        for (auto &x : s) top = x.ticket > top ? x.ticket : top;
+        if (!t.empty()) run_tpke(q, t);
+        if (!s.empty()) run_ts(q, s);
+        lk.lock();
+        q->done_upto = top > q->done_upto ? top : q->done_upto;
+        q->cv_done.notify_all();
+    }
+}
+
+int64_t enqueue_common(lcb_queue *q, std::unique_lock<std::mutex> &lk) {
+    (void)lk;
+    size_t pending = q->tpke.size() + q->ts.size();
+    if (pending == 1) q->oldest = clk::now();
+    if (pending == 1 || pending >= q->max_batch) q->cv_work.notify_one();
+    return q->next_ticket - 1;
+}
+
+}  // namespace
+
+extern "C" lcb_queue *lcb_queue_create(size_t max_batch, uint32_t max_delay_us) {
+    lcb_queue *q = new lcb_queue;
+    q->max_batch = max_batch ? max_batch : 1;
+    q->max_delay = std::chrono::microseconds(max_delay_us);
+    q->worker = std::thread(worker_loop, q);
+    return q;
+}
+extern "C" void lcb_queue_destroy(lcb_queue *q) {
+    if (!q) return;
+    {
+        std::lock_guard<std::mutex> lk(q->mu);
+        q->stop = true;
+    }
+    q->cv_work.notify_all();
+    q->worker.join();
+    q->cv_done.notify_all();
+    delete q;
+}
+extern "C" int64_t lcb_queue_tpke_verify(lcb_queue *q, const uint8_t y48[48], const uint8_t u48[48], const uint8_t *v,
+                                         size_t v_len, const uint8_t w96[96], const uint8_t ui48[48]) {
+    if (!q || !y48 || !u48 || !w96 || !ui48 || (v_len && !v)) return -1;
+    TpkeItem it;
+    it.key.assign((const char *)y48, 48);
+    it.ct.reserve(144 + v_len);
+    it.ct.append((const char *)u48, 48);
+    it.ct.append((const char *)w96, 96);
+    if (v_len) it.ct.append((const char *)v, v_len);
+    memcpy(it.ui, ui48, 48);
+    std::unique_lock<std::mutex> lk(q->mu);
+    if (q->stop) return -1;
+    it.ticket = q->next_ticket++;
+    q->tpke.push_back(std::move(it));
+    return enqueue_common(q, lk);
+}
+extern "C" int64_t lcb_queue_ts_verify(lcb_queue *q, const uint8_t pk48[48], const uint8_t *msg, size_t msg_len,
+                                       const uint8_t sig96[96]) {
+    if (!q || !pk48 || !sig96 || (msg_len && !msg)) return -1;
+    TsItem it;
+    it.pk.assign((const char *)pk48, 48);
+    if (msg_len) it.msg.assign((const char *)msg, msg_len);
+    memcpy(it.sig, sig96, 96);
+    std::unique_lock<std::mutex> lk(q->mu);
+    if (q->stop) return -1;
+    it.ticket = q->next_ticket++;
+    q->ts.push_back(std::move(it));
+    return enqueue_common(q, lk);
+}
+extern "C" int lcb_queue_flush(lcb_queue *q) {
+    if (!q) return -1;
+    {
+        std::lock_guard<std::mutex> lk(q->mu);
+        q->flush_now = true;
+    }
+    q->cv_work.notify_all();
+    return 0;
+}
+extern "C" int lcb_queue_wait(lcb_queue *q, int64_t ticket) {
+    if (!q || ticket <= 0) return -1;
+    std::unique_lock<std::mutex> lk(q->mu);
+    if (ticket >= q->next_ticket) return -1;
+    for (;;) {
+        auto it = q->results.find(ticket);
+        if (it != q->results.end()) {
+            int r = it->second;
+            q->results.erase(it);
+            return r;
+        }
+        if (ticket <= q->done_upto) return -1;   // already waited for
+        q->cv_done.wait(lk);
+    }
+}
+extern "C" const char *lcb_queue_last_error(lcb_queue *q) { return q ? q->last_error.c_str() : ""; }
+extern "C" int lcb_queue_stats(lcb_queue *q, uint64_t out[3]) {
+    if (!q || !out) return -1;
+    std::lock_guard<std::mutex> lk(q->mu);
+    out[0] = q->batches;
+    out[1] = q->items;
+    out[2] = q->max_seen;
+    return 0;
+}

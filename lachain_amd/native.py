@@ -100,6 +100,16 @@ _SIGS = {
     "lcb_coin_parity": (ctypes.c_int, [c_u8p, c_size]),
     "lcb_coin_nonce": (ctypes.c_uint64, [c_u8p, c_size]),
     "lcb_coin_fold_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_size, ctypes.c_void_p]),
+    "lcb_queue_create": (ctypes.c_void_p, [c_size, ctypes.c_uint32]),
+    "lcb_queue_destroy": (None, [ctypes.c_void_p]),
+    "lcb_queue_tpke_verify": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
+                                               c_size, ctypes.c_char_p, ctypes.c_char_p]),
+    "lcb_queue_ts_verify": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, c_size,
+                                             ctypes.c_char_p]),
+    "lcb_queue_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    "lcb_queue_flush": (ctypes.c_int, [ctypes.c_void_p]),
+    "lcb_queue_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
+    "lcb_queue_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
     "lcb_ctx_create": (ctypes.c_void_p, []),
     "lcb_ctx_destroy": (None, [ctypes.c_void_p]),
     "lcb_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
@@ -369,6 +379,62 @@ def coin_nonce(sig: bytes) -> int:
     keep = []
     _, p = _bytes_ptr_keep(keep, sig)
     return int(load(False).lcb_coin_nonce(p, len(sig)))
+
+
+class BatchQueue:
+    """lcb_queue (include/lachain_bls.h): single shares submitted from many threads run as aggregated GPU batches.
+
+    submit_* return a ticket; wait(ticket) -> True / False (the share's decision); verify_* = submit + wait, the
+    drop-in shape of PublicKey.VerifyShare (TPKE/PublicKey.cs:88-92) and ValidateSignature
+    (ThresholdSignature/PublicKey.cs:16-21) for one-share-per-call callers."""
+
+    def __init__(self, max_batch=4096, max_delay_ms=5.0):
+        self.ptr = lib().lcb_queue_create(max_batch, int(max_delay_ms * 1000))
+        if not self.ptr:
+            raise RuntimeError("lcb_queue_create failed")
+
+    def submit_tpke(self, y48, u48, v, w96, ui48):
+        t = lib().lcb_queue_tpke_verify(self.ptr, y48, u48, v, len(v), w96, ui48)
+        if t <= 0:
+            raise ValueError("lcb_queue_tpke_verify: bad arguments")
+        return t
+
+    def submit_ts(self, pk48, msg, sig96):
+        t = lib().lcb_queue_ts_verify(self.ptr, pk48, msg, len(msg), sig96)
+        if t <= 0:
+            raise ValueError("lcb_queue_ts_verify: bad arguments")
+        return t
+
+    def wait(self, ticket) -> bool:
+        r = lib().lcb_queue_wait(self.ptr, ticket)
+        if r < 0:
+            raise RuntimeError("lcb_queue batch failed: " + lib().lcb_queue_last_error(self.ptr).decode())
+        return bool(r)
+
+    def verify_tpke(self, y48, u48, v, w96, ui48) -> bool:
+        return self.wait(self.submit_tpke(y48, u48, v, w96, ui48))
+
+    def verify_ts(self, pk48, msg, sig96) -> bool:
+        return self.wait(self.submit_ts(pk48, msg, sig96))
+
+    def flush(self):
+        lib().lcb_queue_flush(self.ptr)
+
+    def stats(self):
+        arr = (ctypes.c_uint64 * 3)()
+        lib().lcb_queue_stats(self.ptr, arr)
+        return dict(batches=int(arr[0]), shares=int(arr[1]), largest_batch=int(arr[2]))
+
+    def close(self):
+        if self.ptr:
+            lib().lcb_queue_destroy(self.ptr)
+            self.ptr = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 class Context:

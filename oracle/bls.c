@@ -1725,6 +1725,126 @@ int orc_tpke_verify_batch(uint8_t *accept, size_t n, const uint8_t *y_keys, cons
     return bad ? -1 : 0;
 }
 
+/* ================================================================== CPU baseline, amortized
+   The same algorithm the GPU runs, on host cores, so the GPU/CPU ratio compares like with like:
+   H(U||V) and the Miller lines of H and W are computed once per ciphertext (once per message for threshold
+   signatures), and each share costs one two-pair Miller loop against those lines plus ONE final exponentiation
+   of e(Ui, H) e(-Yi, W) (decision identical to the reference's two separate pairings + Equals,
+   TPKE/PublicKey.cs:88-92).  TEST INFRASTRUCTURE (bench.py cpu_baseline leg) only. */
+typedef struct { fp2 A, Bc, C; } oline;   /* unevaluated line: A + (Bc xP) v + (C yP) v w */
+#define OLINES 68
+static void lines_precompute(oline *L, const g2 *Qp) {
+    if (g2_is_inf(Qp)) {
+        for (int k = 0; k < OLINES; k++) { L[k].A = FP2_ONE; memset(&L[k].Bc, 0, sizeof(fp2)); memset(&L[k].C, 0, sizeof(fp2)); }
+        return;
+    }
+    fp2 xQ, yQ, X, Y, Z;
+    g2_to_affine(&xQ, &yQ, Qp);
+    X = xQ; Y = yQ; Z = FP2_ONE;
+    int nb = 64 - __builtin_clzll(Z_ABS), k = 0;
+    for (int i = nb - 2; i >= 0; i--) {
+        dbl_step(&X, &Y, &Z, &L[k].A, &L[k].Bc, &L[k].C, &FP_ONE_M, &FP_ONE_M); k++;
+        if ((Z_ABS >> i) & 1) { add_step(&X, &Y, &Z, &L[k].A, &L[k].Bc, &L[k].C, &xQ, &yQ, &FP_ONE_M, &FP_ONE_M); k++; }
+    }
+}
+/* f = f_{|z|,Q1}(P1) f_{|z|,Q2}(P2), conjugated (z < 0); a pair whose G1 point is infinity contributes 1 */
+static void miller2_lines(fp12 *f, const oline *L1, const g1 *P1, const oline *L2, const g1 *P2) {
+    const oline *L[2] = {L1, L2};
+    const g1 *P[2] = {P1, P2};
+    fp xP[2], yP[2];
+    int act[2];
+    for (int j = 0; j < 2; j++) {
+        act[j] = !g1_is_inf(P[j]);
+        if (act[j]) g1_to_affine(&xP[j], &yP[j], P[j]);
+    }
+    *f = FP12_ONE;
+    int nb = 64 - __builtin_clzll(Z_ABS), k = 0;
+    for (int i = nb - 2; i >= 0; i--) {
+        fp12_sqr(f, f);
+        int steps = ((Z_ABS >> i) & 1) ? 2 : 1;
+        for (int s_ = 0; s_ < steps; s_++, k++)
+            for (int j = 0; j < 2; j++) {
+                if (!act[j]) continue;
+                fp2 B, C;
+                fp2_mul_fp(&B, &L[j][k].Bc, &xP[j]);
+                fp2_mul_fp(&C, &L[j][k].C, &yP[j]);
+                fp12_mul_line(f, &L[j][k].A, &B, &C);
+            }
+    }
+    fp12_conj(f, f);
+}
+static int check_pair_product(const oline *L1, const g1 *P1, const oline *L2, const g1 *P2) {
+    fp12 f, e;
+    miller2_lines(&f, L1, P1, L2, P2);
+    final_exp(&e, &f);
+    return fp12_eq(&e, &FP12_ONE);
+}
+int orc_tpke_verify_batch_amortized(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys,
+                                    const uint8_t *cts_u, const uint8_t *cts_v, size_t vlen, const uint8_t *cts_w,
+                                    size_t n_cts, const uint32_t *ct_idx, const uint32_t *dec_idx, const uint8_t *uis,
+                                    int nthreads) {
+    orc_init();
+    oline *LH = malloc(sizeof(oline) * OLINES * (n_cts ? n_cts : 1));
+    oline *LW = malloc(sizeof(oline) * OLINES * (n_cts ? n_cts : 1));
+    uint8_t *ctok = malloc(n_cts ? n_cts : 1);
+    g1 *Y = malloc(sizeof(g1) * (n_keys ? n_keys : 1));
+    uint8_t *kok = malloc(n_keys ? n_keys : 1);
+    if (!LH || !LW || !ctok || !Y || !kok) { free(LH); free(LW); free(ctok); free(Y); free(kok); return -1; }
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+    for (size_t c = 0; c < n_cts; c++) {
+        g1 u; g2 w, h;
+        int ok = g1_load(&u, cts_u + 48 * c) && g2_load(&w, cts_w + 96 * c);
+        ok = ok && hash_to_g2_tpke(&h, &u, cts_v + vlen * c, vlen);
+        ctok[c] = (uint8_t)ok;
+        if (!ok) { memset(&h, 0, sizeof h); memset(&w, 0, sizeof w); }
+        lines_precompute(LH + OLINES * c, &h);
+        lines_precompute(LW + OLINES * c, &w);
+    }
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+    for (size_t d = 0; d < n_keys; d++) {
+        kok[d] = (uint8_t)g1_load(&Y[d], y_keys + 48 * d);
+        if (kok[d]) g1_neg(&Y[d], &Y[d]);   /* -Y: e(Ui, H) e(-Yi, W) == 1 */
+    }
+#pragma omp parallel for schedule(dynamic, 4) num_threads(nthreads)
+    for (size_t i = 0; i < n; i++) {
+        uint32_t c = ct_idx[i], d = dec_idx[i];
+        g1 ui;
+        int ok = c < n_cts && d < n_keys && ctok[c] && kok[d] && g1_load(&ui, uis + 48 * i);
+        accept[i] = (uint8_t)(ok && check_pair_product(LH + OLINES * c, &ui, LW + OLINES * c, &Y[d]));
+    }
+    free(LH); free(LW); free(ctok); free(Y); free(kok);
+    return 0;
+}
+int orc_ts_validate_batch_amortized(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks, const uint8_t *sigs,
+                                    const uint8_t *msgs, const uint32_t *msg_off, size_t n_msgs,
+                                    const uint32_t *msg_idx, const uint32_t *pk_idx, int nthreads) {
+    orc_init();
+    oline *LH = malloc(sizeof(oline) * OLINES * (n_msgs ? n_msgs : 1));
+    uint8_t *mok = malloc(n_msgs ? n_msgs : 1);
+    if (!LH || !mok) { free(LH); free(mok); return -1; }
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+    for (size_t m = 0; m < n_msgs; m++) {
+        g2 h;
+        int ok = g2_hash(&h, msgs + msg_off[m], msg_off[m + 1] - msg_off[m]);
+        mok[m] = (uint8_t)ok;
+        if (!ok) memset(&h, 0, sizeof h);
+        lines_precompute(LH + OLINES * m, &h);
+    }
+    g1 ngen;
+    g1_neg(&ngen, &G1_GEN);
+#pragma omp parallel for schedule(dynamic, 4) num_threads(nthreads)
+    for (size_t i = 0; i < n; i++) {
+        uint32_t m = msg_idx[i], k = pk_idx[i];
+        g1 pk; g2 sig;
+        oline LS[OLINES];
+        int ok = m < n_msgs && k < n_pks && mok[m] && g1_load(&pk, pks + 48 * (size_t)k) && g2_load(&sig, sigs + 96 * i);
+        if (ok) lines_precompute(LS, &sig);   /* the signature side's lines, once per share (on the fly on the GPU) */
+        accept[i] = (uint8_t)(ok && check_pair_product(LH + OLINES * m, &pk, LS, &ngen));
+    }
+    free(LH); free(mok);
+    return 0;
+}
+
 /* ---- test hooks (oracle self-checks) ---- */
 int orc_test_cyc_sqr(uint8_t out[576], const uint8_t fb[576]) {
     orc_init();

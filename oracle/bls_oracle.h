@@ -114,6 +114,15 @@ int orc_ts_sign(uint8_t sig[96], const uint8_t sk[32], const uint8_t *msg, size_
 /* ---- batch (CPU-baseline) entry points, OpenMP over items ---- */
 /* per share i: ct index ct_idx[i], decryptor dec_idx[i]; as-reference semantics
    (hash recomputed per share, two separate pairings compared) */
+/* CPU baseline with the GPU's algorithm (per-ciphertext / per-message H and Miller lines, one final exp per
+   share): bench.py's "amortized" cpu_baseline legs */
+int orc_tpke_verify_batch_amortized(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys,
+                                    const uint8_t *cts_u, const uint8_t *cts_v, size_t vlen, const uint8_t *cts_w,
+                                    size_t n_cts, const uint32_t *ct_idx, const uint32_t *dec_idx, const uint8_t *uis,
+                                    int nthreads);
+int orc_ts_validate_batch_amortized(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks, const uint8_t *sigs,
+                                    const uint8_t *msgs, const uint32_t *msg_off, size_t n_msgs,
+                                    const uint32_t *msg_idx, const uint32_t *pk_idx, int nthreads);
 int orc_tpke_verify_batch(uint8_t *accept, size_t n_shares, const uint8_t *y_keys,
                           const uint8_t *cts_u, const uint8_t *cts_v, size_t vlen, const uint8_t *cts_w,
                           const uint32_t *ct_idx, const uint32_t *dec_idx, const uint8_t *uis,

@@ -183,3 +183,55 @@ def test_ts_validate_batch_matches_single():
                                          pidx.ctypes.data_as(ctypes.c_void_p), 2) == 0
     single = [o.ts_validate(pks[48 * pidx[i]:48 * pidx[i] + 48], sigs[i], msgs[midx[i]]) == 1 for i in range(6)]
     assert [b == 1 for b in acc.raw] == single == [True, True, True, True, False, True]
+
+
+def test_amortized_cpu_baselines_match_as_reference():
+    """bench.py's amortized CPU legs (per-ciphertext H and Miller lines, one final exponentiation per share) decide
+    exactly like the as-reference path (hash + two pairings + Equals per call, TPKE/PublicKey.cs:88-92,
+    ThresholdSignature/PublicKey.cs:16-21), including malformed, wrong-key and infinity shares."""
+    import ctypes
+    import numpy as np
+    from helpers import Drbg, R
+    lib = o.lib()
+    d = Drbg(b"oracle-amortized")
+    n, f = 4, 1
+    coeffs = [d.fr_int() for _ in range(f + 1)]
+    poly = lambda x: sum(c * pow(x, i, R) for i, c in enumerate(coeffs)) % R
+    xs = [poly(i + 1) for i in range(n)]
+    yi = [o.g1_mul(o.g1_gen(), o.fr(x)) for x in xs]
+    y = o.g1_mul(o.g1_gen(), o.fr(poly(0)))
+    cts = [o.tpke_encrypt(y, d.bytes(32), o.fr(d.fr_int())) for _ in range(3)]
+    shares = [o.g1_mul(cts[c][0], o.fr(xs[j])) for c in range(3) for j in range(n)]
+    shares[1] = o.g1_add(shares[1], o.g1_gen())
+    shares[5] = bytes(48)                   # infinity
+    shares[6] = shares[6][::-1]             # reversed bytes (HoneyBadgerMalicious.cs:23)
+    shares[9] = shares[10]                  # another decryptor's share
+    m = len(shares)
+    ct = np.repeat(np.arange(3, dtype=np.uint32), n)
+    dec = np.tile(np.arange(n, dtype=np.uint32), 3)
+    u = b"".join(c[0] for c in cts); v = b"".join(c[1] for c in cts); w = b"".join(c[2] for c in cts)
+    a1 = ctypes.create_string_buffer(m); a2 = ctypes.create_string_buffer(m)
+    p = lambda arr: arr.ctypes.data_as(ctypes.c_void_p)
+    assert lib.orc_tpke_verify_batch(a1, ctypes.c_size_t(m), b"".join(yi), u, v, ctypes.c_size_t(32), w, p(ct), p(dec),
+                                     b"".join(shares), 2) in (0, -1)
+    assert lib.orc_tpke_verify_batch_amortized(a2, ctypes.c_size_t(m), b"".join(yi), ctypes.c_size_t(n), u, v,
+                                               ctypes.c_size_t(32), w, ctypes.c_size_t(3), p(ct), p(dec),
+                                               b"".join(shares), 2) == 0
+    assert a1.raw == a2.raw and sum(a1.raw) == m - 4
+    # threshold signatures
+    sks = [d.fr_int() for _ in range(3)]
+    pks = [o.g1_mul(o.g1_gen(), o.fr(s)) for s in sks]
+    msgs = [b"coin a", b"coin bb"]
+    sigs = [o.ts_sign(o.fr(sks[k]), msgs[mi]) for mi in range(2) for k in range(3)]
+    sigs[1] = sigs[2]
+    sigs[4] = bytes(96)
+    mo = np.array([0, 6, 13], dtype=np.uint32)
+    mi = np.repeat(np.arange(2, dtype=np.uint32), 3)
+    pi = np.tile(np.arange(3, dtype=np.uint32), 2)
+    b1 = ctypes.create_string_buffer(6); b2 = ctypes.create_string_buffer(6)
+    lib.orc_ts_validate_batch(b1, ctypes.c_size_t(6), b"".join(pks), b"".join(sigs), b"".join(msgs), p(mo), p(mi),
+                              p(pi), 2)
+    assert lib.orc_ts_validate_batch_amortized(b2, ctypes.c_size_t(6), b"".join(pks), ctypes.c_size_t(3),
+                                               b"".join(sigs), b"".join(msgs), p(mo), ctypes.c_size_t(2), p(mi), p(pi),
+                                               2) == 0
+    assert b1.raw == b2.raw and sum(b1.raw) == 4

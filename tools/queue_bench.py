@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""tools/queue_bench.py — latency / throughput of the aggregation queue (lcb_queue).
+
+T caller threads each verify ONE TPKE decryption share per call (submit + wait), as HoneyBadger's protocol threads
+do (HoneyBadger.cs:211-212, AbstractProtocol.cs:46-47), for a fixed wall time per setting.  Reported per batch
+deadline (1, 5, 20 ms) and caller count: shares/s, mean batch size, and submit->decision latency percentiles.
+Inputs: N=22 F=7 shares of 1,024 ciphertexts generated with the product's batch kernels (1 % corrupted); every
+decision is checked against the construction.  Callers are Python threads (ctypes releases the GIL in the call),
+so at high rates the Python side, not the GPU, bounds throughput; the numbers are the floor a native host gets.
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shares", type=int, default=22 * 1024)
+    ap.add_argument("--seconds", type=float, default=3.0)
+    ap.add_argument("--deadlines", default="1,5,20")
+    ap.add_argument("--threads", default="16,64")
+    ap.add_argument("--max-batch", type=int, default=65536)
+    args = ap.parse_args()
+    from lachain_amd import native as nat
+    import bench
+    nat.lib()
+    inp = bench.make_inputs(nat, 0, args.shares, 22, 7, 32)
+    vlen = 32
+    recs = []
+    for i in range(args.shares):
+        c, j = int(inp["ct_idx"][i]), int(inp["dec_idx"][i])
+        u, v, w = inp["cts_list"][c]
+        recs.append((inp["keys_list"][j], u, v, w, inp["ui"][48 * i:48 * i + 48], bool(inp["expect"][i])))
+    rows = []
+    for dl in [float(x) for x in args.deadlines.split(",")]:
+        for nt in [int(x) for x in args.threads.split(",")]:
+            lat, bad, count = [], [0], [0]
+            stop = time.perf_counter() + args.seconds
+            with nat.BatchQueue(max_batch=args.max_batch, max_delay_ms=dl) as q:
+                def caller(k):
+                    idx, my = k, []
+                    while time.perf_counter() < stop:
+                        y, u, v, w, ui, e = recs[idx % len(recs)]
+                        t0 = time.perf_counter()
+                        got = q.verify_tpke(y, u, v, w, ui)
+                        my.append(time.perf_counter() - t0)
+                        if got != e:
+                            bad[0] += 1
+                        idx += nt
+                    lat.extend(my)
+                    count[0] += len(my)
+                t_start = time.perf_counter()
+                th = [threading.Thread(target=caller, args=(k,)) for k in range(nt)]
+                for t in th:
+                    t.start()
+                for t in th:
+                    t.join()
+                elapsed = time.perf_counter() - t_start
+                st = q.stats()
+            ms = np.array(lat) * 1e3
+            rows.append(dict(deadline_ms=dl, callers=nt, shares_per_s=count[0] / elapsed,
+                             mean_batch=st["shares"] / max(1, st["batches"]), batches=st["batches"],
+                             latency_ms={"p50": float(np.percentile(ms, 50)), "p90": float(np.percentile(ms, 90)),
+                                         "p99": float(np.percentile(ms, 99))},
+                             decision_mismatches=bad[0]))
+            print(json.dumps(rows[-1]), flush=True)
+
+
+if __name__ == "__main__":
+    main()
