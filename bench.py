@@ -8,9 +8,9 @@ One "step" = one pass of the hot path over the whole batch, inputs resident in H
   lcb_tpke_prepare_dev          (k_g1_decompress: 22 keys; k_tpke_ct_prepare: per-ciphertext H(U||V) +
                                  Miller lines of H and W)
   lcb_tpke_verify_prepared_dev  (k_tpke_verify: per share, decompress U_i, 2-pair Miller loop, final exp)
-Second line of the metric (BASELINE configs[3]): G1 Pippenger MSM of --msm-points points per rank (default
-2^21; 8 ranks = 2^24), reported under "msm" in the same JSON line with its own roofline and CPU baseline; at
-N > 1 the per-GPU Jacobian partials are all-gathered over RCCL and summed on the GPU.
+Second line of the metric (BASELINE configs[3]): G1 Pippenger MSMs of 2^20 and 2^24 points in total, each
+sharded over the ranks, reported under "msm" in the same JSON line with their own roofline and CPU baseline;
+at N > 1 the per-GPU Jacobian partials are all-gathered over RCCL and summed on the GPU.
 Launch: `python bench.py --gpus 1` or under torch.distributed.run with --gpus N (one rank per GPU, weak
 scaling: every rank verifies its own 1M-share batch; no data-path collective).
 Prints ONE JSON line on rank 0.
@@ -39,6 +39,45 @@ W_VERIFY = C["C_DEC1"] + C["C_ML2_EVAL"] + C["C_FE"]                            
 W_PREPARE = C["C_DEC1"] + C["C_DEC2"] + C["C_H2G2"] + C["C_AFF2"] + 2 * C["C_LINES"]  # per ciphertext
 # gfx950 v_mad_u64_u32 is half rate: 64 lane-MACs / clk / CU (profiles/r01_valu_rates.jsonl)
 PEAK_MAC32 = 256 * 64 * 2.4e9            # 3.93e13 MAC/s at the 2.4 GHz max clock
+
+
+def oracle_timing_lib():
+    """The oracle built for timing on THIS host (oracle/liborc_native.so: gcc -O3 -march=native, so BMI2/ADX/AVX-512
+    where the host has them), made on first use; the portable test build (-O2 -march=x86-64-v2) if no compiler."""
+    import ctypes as ct
+    import subprocess
+    path = os.path.join(ROOT, "oracle", "liborc_native.so")
+    if not os.path.exists(path):
+        try:
+            subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native"], check=True, timeout=180,
+                           capture_output=True)
+        except Exception:  # noqa: BLE001 — fall back to the portable build below
+            pass
+    if os.path.exists(path):
+        lib = ct.CDLL(path)
+        lib.orc_init()
+        return lib, "oracle/liborc_native.so (gcc -O3 -march=native, built on this host)"
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as o
+    return o.lib(), "oracle/liborc.so (gcc -O2 -march=x86-64-v2)"
+
+
+def source_hash():
+    """sha256 over the kernel / host sources (the GPU box has no .git): ties a committed PMC file to the build"""
+    import glob
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "lachain_amd", "csrc")
+    for f in sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.hpp")) +
+                    glob.glob(os.path.join(csrc, "*.cpp")) + glob.glob(os.path.join(csrc, "*.h")) +
+                    [os.path.join(csrc, "Makefile")]):
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def cpu_threads():
+    return max(1, min(16, os.cpu_count() or 1))   # the GPU box's CPU share is 16 threads
 
 
 class Drbg:
@@ -105,38 +144,52 @@ def to_dev(torch, dev, b):
     return torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
 
 
-def cpu_baseline(inp, target_s=15.0):
-    """Time the oracle's as-reference path (hash + two pairings per VerifyShare call) on host cores."""
-    import ctypes
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as o
-    lib = o.lib()
-    threads = max(1, min(16, os.cpu_count() or 1))
-    n_total = len(inp["expect"])
-    y = inp["y_keys"]
-    u, v, w, ui = inp["u"], inp["v"], inp["w"], inp["ui"]
+def cpu_baseline(inp, target_s=12.0):
+    """configs[1] on host cores, two legs over the same shares (bounded samples, ~target_s each):
+    amortized   — the GPU's algorithm: H(U||V) and the Miller lines of H and W once per ciphertext, one two-pair
+                  Miller loop + ONE final exponentiation per share (orc_tpke_verify_batch_amortized);
+    as_reference — what Lachain calls per share: G2.SetHashOf + two pairings + Equals (TPKE/PublicKey.cs:88-92,
+                  orc_tpke_verify_batch).
+    The amortized leg is the headline baseline (like-for-like algorithm); both run on the timing build."""
+    lib, build = oracle_timing_lib()
+    threads = cpu_threads()
+    n_total, n_dec = len(inp["expect"]), inp["n_dec"]
+    y, u, v, w, ui = inp["y_keys"], inp["u"], inp["v"], inp["w"], inp["ui"]
     vlen = int(inp["v_off"][1] - inp["v_off"][0])
+    ct_all = np.ascontiguousarray(inp["ct_idx"], dtype=np.uint32)
+    dec_all = np.ascontiguousarray(inp["dec_idx"], dtype=np.uint32)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
 
-    def run(n):
-        acc = (ctypes.c_uint8 * n)()
-        ct = (ctypes.c_uint32 * n)(*[int(x) for x in inp["ct_idx"][:n]])
-        dc = (ctypes.c_uint32 * n)(*[int(x) for x in inp["dec_idx"][:n]])
+    def run(n, amortized):
+        n = max(n_dec, (n // n_dec) * n_dec)      # whole ciphertexts
+        n_cts = n // n_dec
+        acc = ctypes.create_string_buffer(n)
+        ct, dc = ct_all[:n], dec_all[:n]
         t0 = time.perf_counter()
-        rc = lib.orc_tpke_verify_batch(acc, ctypes.c_size_t(n), y, u, v, ctypes.c_size_t(vlen), w, ct, dc,
-                                       ui[:48 * n], threads)
+        if amortized:
+            rc = lib.orc_tpke_verify_batch_amortized(acc, ctypes.c_size_t(n), y, ctypes.c_size_t(n_dec), u, v,
+                                                     ctypes.c_size_t(vlen), w, ctypes.c_size_t(n_cts), p(ct), p(dc),
+                                                     ui[:48 * n], threads)
+        else:
+            rc = lib.orc_tpke_verify_batch(acc, ctypes.c_size_t(n), y, u, v, ctypes.c_size_t(vlen), w, p(ct), p(dc),
+                                           ui[:48 * n], threads)
         dt = time.perf_counter() - t0
         assert rc == 0
-        mism = int(np.sum(np.frombuffer(bytes(acc), dtype=np.uint8) != inp["expect"][:n]))
-        return dt, mism
+        mism = int(np.sum(np.frombuffer(acc.raw, dtype=np.uint8) != inp["expect"][:n]))
+        return n, dt, mism
 
-    n = 4 * threads
-    dt, _ = run(n)
-    n = int(min(n_total, max(n, n * target_s / max(dt, 1e-3))))
-    dt, mism = run(n)
-    return dict(value=n / dt, unit="share verifications/s", cores=threads, kind="port",
-                sample=f"first {n} shares of the same batch, oracle/bls.c orc_tpke_verify_batch "
-                       f"(as-reference: G2.SetHashOf + two pairings per VerifyShare), {threads} OpenMP threads, "
-                       f"{dt:.1f} s, {mism} decision mismatches vs expected")
+    legs = {}
+    for name, am in (("amortized", True), ("as_reference", False)):
+        n, dt, _ = run(8 * threads * n_dec if am else 4 * threads, am)
+        n, dt, mism = run(int(min(n_total, max(n, n * target_s / max(dt, 1e-3)))), am)
+        legs[name] = dict(value=n / dt, unit="share verifications/s", cores=threads, kind="port",
+                          sample=f"first {n} shares ({n // n_dec} ciphertexts x {n_dec}) of the same batch, "
+                                 f"{'orc_tpke_verify_batch_amortized' if am else 'orc_tpke_verify_batch'}, {build}, "
+                                 f"{threads} OpenMP threads, {dt:.1f} s, {mism} decision mismatches vs expected")
+    out = dict(legs["amortized"])
+    out["algorithm"] = "amortized (the GPU's algorithm)"
+    out["as_reference"] = legs["as_reference"]
+    return out
 
 
 # ------------------------------------------------------------------ G1 MSM (BASELINE configs[3])
@@ -164,11 +217,8 @@ def msm_inputs(nat, rank, n):
 
 
 def msm_cpu_baseline(pts, scal, n_total, target_s=10.0):
-    import ctypes
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as o
-    lib = o.lib()
-    threads = max(1, min(16, os.cpu_count() or 1))
+    lib, build = oracle_timing_lib()
+    threads = cpu_threads()
 
     def run(n):
         out = ctypes.create_string_buffer(48)
@@ -182,16 +232,27 @@ def msm_cpu_baseline(pts, scal, n_total, target_s=10.0):
     n = int(min(n_total, max(n, n * target_s / max(dt, 1e-3))))
     dt = run(n)
     return dict(value=n / dt, unit="points/s", cores=threads, kind="port",
-                sample=f"first {n} points of the same MSM, oracle/bls.c orc_g1_msm_mt (one 255-bit var-base "
-                       f"multiplication per point as MCL LagrangeInterpolation does, {threads} OpenMP threads), "
-                       f"{dt:.1f} s")
+                sample=f"first {n} points of the same MSM, orc_g1_msm_mt (one 255-bit var-base multiplication per "
+                       f"point, as MCL's LagrangeInterpolation does), {build}, {threads} OpenMP threads, {dt:.1f} s")
 
 
-def run_msm(args, nat, torch, dev, rank, world, cpu):
+def run_msm_sizes(args, nat, torch, dev, rank, world, cpu):
+    """configs[3]: one entry per total size in --msm-sizes (default 2^20 and 2^24 points), the points of each
+    MSM sharded over the ranks (n / world per rank) with the RCCL all-gather of the 144-byte partials."""
+    out = []
+    for k, total in enumerate(int(x) for x in args.msm_sizes.split(",") if x):
+        r = run_msm(args, nat, torch, dev, rank, world, cpu and k == 0, max(1, total // world))
+        if r is not None:
+            r["total_points"] = total
+            out.append(r)
+        torch.cuda.empty_cache()
+    return out
+
+
+def run_msm(args, nat, torch, dev, rank, world, cpu, n):
     import torch.distributed as dist
     from lachain_amd import shard
     lib = nat.lib()
-    n = args.msm_points
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     pts, scal, expect_local = msm_inputs(nat, rank, n)
@@ -316,32 +377,45 @@ def ts_inputs(nat, rank, rounds, n, f):
                 expect=expect, shared_sk=shared_sk, msg_list=msgs)
 
 
-def ts_cpu_baseline(inp, n_total, target_s=10.0):
-    """The oracle's as-reference ValidateSignature (hash + two pairings per share) on host cores."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as o
-    lib = o.lib()
-    threads = max(1, min(16, os.cpu_count() or 1))
+def ts_cpu_baseline(inp, n_total, n_per_round, target_s=10.0):
+    """configs[2] share verification on host cores: amortized (H(m) lines once per message, one final exp per
+    share: orc_ts_validate_batch_amortized) and as-reference (hash + two pairings per ValidateSignature call,
+    ThresholdSignature/PublicKey.cs:16-21: orc_ts_validate_batch)."""
+    lib, build = oracle_timing_lib()
+    threads = cpu_threads()
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    n_pks = len(inp["pks"]) // 48
 
-    def run(k):
+    def run(k, am):
+        k = max(n_per_round, (k // n_per_round) * n_per_round)
         acc = ctypes.create_string_buffer(k)
         mi = np.ascontiguousarray(inp["midx"][:k])
         pi = np.ascontiguousarray(inp["pidx"][:k])
+        n_msgs = int(mi[-1]) + 1
         t0 = time.perf_counter()
-        lib.orc_ts_validate_batch(acc, ctypes.c_size_t(k), inp["pks"], inp["sigs"][:96 * k], inp["msgs"],
-                                  inp["moff"].ctypes.data_as(ctypes.c_void_p), mi.ctypes.data_as(ctypes.c_void_p),
-                                  pi.ctypes.data_as(ctypes.c_void_p), threads)
+        if am:
+            rc = lib.orc_ts_validate_batch_amortized(acc, ctypes.c_size_t(k), inp["pks"], ctypes.c_size_t(n_pks),
+                                                     inp["sigs"][:96 * k], inp["msgs"], p(inp["moff"]),
+                                                     ctypes.c_size_t(n_msgs), p(mi), p(pi), threads)
+        else:
+            rc = lib.orc_ts_validate_batch(acc, ctypes.c_size_t(k), inp["pks"], inp["sigs"][:96 * k], inp["msgs"],
+                                           p(inp["moff"]), p(mi), p(pi), threads)
         dt = time.perf_counter() - t0
-        return dt, int(np.sum(np.frombuffer(acc.raw, dtype=np.uint8) != inp["expect"][:k]))
+        assert rc == 0
+        return k, dt, int(np.sum(np.frombuffer(acc.raw, dtype=np.uint8) != inp["expect"][:k]))
 
-    k = min(n_total, 4 * threads)
-    dt, _ = run(k)
-    k = int(min(n_total, max(k, k * target_s / max(dt, 1e-3))))
-    dt, mism = run(k)
-    return dict(value=k / dt, unit="share verifications/s", cores=threads, kind="port",
-                sample=f"first {k} shares of the same rounds, oracle/bls.c orc_ts_validate_batch (as-reference: "
-                       f"G2.SetHashOf + two pairings per ValidateSignature), {threads} OpenMP threads, {dt:.1f} s, "
-                       f"{mism} decision mismatches vs expected")
+    legs = {}
+    for name, am in (("amortized", True), ("as_reference", False)):
+        k, dt, _ = run(n_per_round * 2, am)
+        k, dt, mism = run(int(min(n_total, max(k, k * target_s / max(dt, 1e-3)))), am)
+        legs[name] = dict(value=k / dt, unit="share verifications/s", cores=threads, kind="port",
+                          sample=f"first {k} shares ({k // n_per_round} rounds) of the same rounds, "
+                                 f"{'orc_ts_validate_batch_amortized' if am else 'orc_ts_validate_batch'}, {build}, "
+                                 f"{threads} OpenMP threads, {dt:.1f} s, {mism} decision mismatches vs expected")
+    out = dict(legs["amortized"])
+    out["algorithm"] = "amortized (the GPU's algorithm)"
+    out["as_reference"] = legs["as_reference"]
+    return out
 
 
 def run_ts(args, nat, torch, dev, rank, world):
@@ -430,7 +504,7 @@ def run_ts(args, nat, torch, dev, rank, world):
         config=f"configs[2]: {rounds} rounds x N={n} F={f} CommonCoin shares per rank; per round: {n} share "
                f"verifications, G2 Lagrange over the first {f + 1} valid shares, combined-signature verification",
         input_gen_s=t_gen,
-        cpu_baseline=ts_cpu_baseline(inp, rounds * n) if (world == 1 and not args.no_cpu_baseline) else None,
+        cpu_baseline=ts_cpu_baseline(inp, rounds * n, n) if (world == 1 and not args.no_cpu_baseline) else None,
     )
 
 
@@ -482,6 +556,80 @@ def replay_inputs(nat, n, f, n_coins, vlen=32):
     return dict(xs=xs, y_keys=b"".join(y_keys), u=b"".join(us), w=b"".join(ws), v=b"".join(vs), plain=plain,
                 shares=shares, expect_t=expect_t, pks=b"".join(pks), msgs=b"".join(msgs), msg_list=msgs,
                 sigs=bytes(sigs), expect_s=expect_s, shared_sk=shared_sk)
+
+
+def replay_cpu_baseline(inp, n, f, n_coins, target_s=3.0):
+    """configs[4] on host cores, composed from bounded samples of the same era's inputs (every term measured here,
+    all threads busy): per view = n^2 decryption-share verifications (amortized, all n shares of a ciphertext in
+    one batch) + n partial decryptions (validity check + x U, orc_tpke_decrypt) + n FullDecrypt combinations
+    (G1 Lagrange k = f+1) + n_coins x (n signature-share verifications + G2 Lagrange k = f+1 + 1 combined check)."""
+    from concurrent.futures import ThreadPoolExecutor
+    lib, build = oracle_timing_lib()
+    threads = cpu_threads()
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    vlen = len(inp["v"]) // n
+    timings = {}
+
+    def timed(fn, units):
+        t0 = time.perf_counter()
+        fn()
+        return (time.perf_counter() - t0) / units
+
+    # decryption shares: C ciphertexts x n shares
+    def tpke(c):
+        m = c * n
+        acc = ctypes.create_string_buffer(m)
+        ct = np.repeat(np.arange(c, dtype=np.uint32), n)
+        dec = np.tile(np.arange(n, dtype=np.uint32), c)
+        rc = lib.orc_tpke_verify_batch_amortized(acc, ctypes.c_size_t(m), inp["y_keys"], ctypes.c_size_t(n), inp["u"],
+                                                 inp["v"], ctypes.c_size_t(vlen), inp["w"], ctypes.c_size_t(c), p(ct),
+                                                 p(dec), inp["shares"][:48 * m], threads)
+        assert rc == 0 and acc.raw == bytes(inp["expect_t"][:m])
+    c = max(1, threads // 8)
+    t = timed(lambda: tpke(c), c * n)
+    c = int(min(n, max(c, c * target_s / max(t * c * n, 1e-3))))
+    timings["tpke_share"] = timed(lambda: tpke(c), c * n)
+
+    def ts(mc):
+        m = mc * n
+        acc = ctypes.create_string_buffer(m)
+        mi = np.repeat(np.arange(mc, dtype=np.uint32), n)
+        pi = np.tile(np.arange(n, dtype=np.uint32), mc)
+        moff = np.arange(0, 24 * (mc + 1), 24, dtype=np.uint32)
+        rc = lib.orc_ts_validate_batch_amortized(acc, ctypes.c_size_t(m), inp["pks"], ctypes.c_size_t(n + 1),
+                                                 inp["sigs"][:96 * m], inp["msgs"], p(moff), ctypes.c_size_t(mc),
+                                                 p(mi), p(pi), threads)
+        assert rc == 0 and acc.raw == bytes(inp["expect_s"][:m])
+    mc = max(1, threads // 8)
+    t = timed(lambda: ts(mc), mc * n)
+    mc = int(min(n_coins, max(mc, mc * target_s / max(t * mc * n, 1e-3))))
+    timings["ts_share"] = timed(lambda: ts(mc), mc * n)
+
+    fr = lambda v: v.to_bytes(32, "little")
+    k = f + 1
+    xs = b"".join(fr(i + 1) for i in range(k))
+    g1s, g2s = inp["shares"][:48 * k], inp["sigs"][:96 * k]
+    x0 = fr(inp["xs"][0])
+
+    def pool(fn, jobs):
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(fn, range(jobs)))
+    g1l = lambda _: lib.orc_g1_lagrange(ctypes.create_string_buffer(48), xs, g1s, ctypes.c_size_t(k))
+    g2l = lambda _: lib.orc_g2_lagrange(ctypes.create_string_buffer(96), xs, g2s, ctypes.c_size_t(k))
+    dec = lambda j: lib.orc_tpke_decrypt(ctypes.create_string_buffer(48), inp["u"][48 * j:48 * j + 48],
+                                         inp["v"][vlen * j:vlen * j + vlen], ctypes.c_size_t(vlen),
+                                         inp["w"][96 * j:96 * j + 96], x0)
+    jobs = 2 * threads
+    timings["g1_lagrange"] = timed(lambda: pool(g1l, jobs), jobs)
+    timings["g2_lagrange"] = timed(lambda: pool(g2l, jobs), jobs)
+    timings["partial_decrypt"] = timed(lambda: pool(dec, jobs), jobs)
+    per_view = (n * n * timings["tpke_share"] + n * timings["partial_decrypt"] + n * timings["g1_lagrange"] +
+                n_coins * ((n + 1) * timings["ts_share"] + timings["g2_lagrange"]))
+    return dict(value=1.0 / per_view, unit="views/s", cores=threads, kind="port",
+                per_item_ms={kk: round(v * 1e3, 4) for kk, v in timings.items()},
+                sample=f"composed from measured samples of the same era ({c} ciphertexts x {n} decryption shares, "
+                       f"{mc} coins x {n} signature shares (amortized: the GPU's algorithm), {jobs} G1 / G2 Lagrange "
+                       f"problems at k={k} and {jobs} partial decryptions), {build}, {threads} threads")
 
 
 def run_replay(args, nat, torch, dev, rank, world):
@@ -587,7 +735,8 @@ def run_replay(args, nat, torch, dev, rank, world):
         return None
     elapsed = float(t[0]) / args.replay_steps
     checks_per_view = n + n * n + n_coins * n + n_coins
-    return dict(metric="HoneyBadgerBFT epoch crypto replay: node views/sec (TPKE + CommonCoin)",
+    cpu = replay_cpu_baseline(inp, n, f, n_coins) if (world == 1 and not args.no_cpu_baseline) else None
+    return dict(metric="HoneyBadgerBFT epoch crypto replay: node views/sec (TPKE + CommonCoin)", cpu_baseline=cpu,
                 value=n / elapsed, unit="views/s", scaling="strong", views_total=n, n=n, f=f, coins=n_coins,
                 pairing_checks_per_s=n * checks_per_view / elapsed, ms_per_era=1e3 * elapsed,
                 steps=args.replay_steps, mismatches=int(t[1]), input_gen_s=t_gen,
@@ -606,7 +755,8 @@ def main():
     ap.add_argument("--vlen", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--msm-points", type=int, default=1 << 21, help="G1 MSM points per rank (0 = skip)")
+    ap.add_argument("--msm-sizes", default=f"{1 << 20},{1 << 24}",
+                    help="total G1 MSM points per measurement, sharded over ranks (empty = skip)")
     ap.add_argument("--msm-steps", type=int, default=3)
     ap.add_argument("--ts-rounds", type=int, default=65536, help="CommonCoin rounds per rank (0 = skip)")
     ap.add_argument("--ts-n", type=int, default=100)
@@ -701,17 +851,26 @@ def main():
         replay = run_replay(args, nat, torch, dev, rank, world)
     if args.ts_rounds > 0:
         ts = run_ts(args, nat, torch, dev, rank, world)
-    if args.msm_points > 0:
-        msm = run_msm(args, nat, torch, dev, rank, world, cpu=(world == 1 and not args.no_cpu_baseline))
+    if args.msm_sizes:
+        msm = run_msm_sizes(args, nat, torch, dev, rank, world, cpu=(world == 1 and not args.no_cpu_baseline))
     if rank == 0:
         ms_per_step = 1e3 * elapsed / args.steps
         value = shares_all * args.steps / elapsed
         achieved = n * W_VERIFY * MAC_PER_FPMUL / (ver_ms * 1e-3)
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "r01_tpke_verify_pmc.json")
+        # HBM bytes per launch of the verify pair from the committed PMC passes, only if they were taken on THIS
+        # build (the file carries the source hash of the kernels it profiled; tools/pmc_to_json.py)
+        traffic, traffic_note = None, "no PMC file for this build"
+        src_hash = source_hash()
+        pmc = os.path.join(ROOT, "profiles", "pmc_tpke_verify.json")
         if os.path.exists(pmc):
             with open(pmc) as fh:
-                traffic = json.load(fh).get("hbm_bytes_per_launch")
+                pj = json.load(fh)
+            if pj.get("source_hash") == src_hash:
+                traffic = pj.get("hbm_bytes_per_launch_at_bench_size")
+                traffic_note = (f"{pmc[len(ROOT) + 1:]}: FETCH_SIZE x2 + WRITE_SIZE (KB->B) of k_tpke_miller + "
+                                f"k_final_exp_check, source hash {src_hash}")
+            else:
+                traffic_note = f"stale PMC file (profiled {pj.get('source_hash')}, this build {src_hash}): not reported"
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(inp, args.cpu_seconds)
@@ -733,7 +892,8 @@ def main():
                              "k_tpke_miller": n * (C["C_DEC1"] + C["C_ML2_EVAL"]) * MAC_PER_FPMUL
                              / (miller_ms * 1e-3) / PEAK_MAC32,
                              "k_final_exp_check": n * C["C_FE"] * MAC_PER_FPMUL / (fexp_ms * 1e-3) / PEAK_MAC32},
-                         "traffic_source": "profiles/r01_tpke_verify_pmc.json (PMC FETCH_SIZE x2 + WRITE_SIZE)"},
+                         "traffic_source": traffic_note},
+            "source_hash": src_hash,
             "cpu_baseline": cpu,
             "input_gen_s": t_gen,
             "msm": msm,

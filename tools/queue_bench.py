@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--deadlines", default="1,5,20")
     ap.add_argument("--threads", default="16,64")
     ap.add_argument("--max-batch", type=int, default=65536)
+    ap.add_argument("--burst", type=int, default=1,
+                    help="shares a caller submits before waiting for them (1 = strict one-share-per-call)")
     args = ap.parse_args()
     from lachain_amd import native as nat
     import bench
@@ -48,13 +50,17 @@ def main():
                 def caller(k):
                     idx, my = k, []
                     while time.perf_counter() < stop:
-                        y, u, v, w, ui, e = recs[idx % len(recs)]
                         t0 = time.perf_counter()
-                        got = q.verify_tpke(y, u, v, w, ui)
-                        my.append(time.perf_counter() - t0)
-                        if got != e:
-                            bad[0] += 1
-                        idx += nt
+                        pend = []
+                        for _ in range(args.burst):
+                            y, u, v, w, ui, e = recs[idx % len(recs)]
+                            pend.append((q.submit_tpke(y, u, v, w, ui), e))
+                            idx += nt
+                        for tk, e in pend:
+                            if q.wait(tk) != e:
+                                bad[0] += 1
+                        dt = time.perf_counter() - t0
+                        my.extend([dt] * len(pend))
                     lat.extend(my)
                     count[0] += len(my)
                 t_start = time.perf_counter()
@@ -66,7 +72,7 @@ def main():
                 elapsed = time.perf_counter() - t_start
                 st = q.stats()
             ms = np.array(lat) * 1e3
-            rows.append(dict(deadline_ms=dl, callers=nt, shares_per_s=count[0] / elapsed,
+            rows.append(dict(deadline_ms=dl, callers=nt, burst=args.burst, shares_per_s=count[0] / elapsed,
                              mean_batch=st["shares"] / max(1, st["batches"]), batches=st["batches"],
                              latency_ms={"p50": float(np.percentile(ms, 50)), "p90": float(np.percentile(ms, 90)),
                                          "p99": float(np.percentile(ms, 99))},
