@@ -264,6 +264,23 @@ int lcb_ctx_g1_msm_dev(lcb_ctx *ctx, void *out_jac, const void *points_aff, cons
                        int window_bits, void *stream);
 int lcb_ctx_g1_msm_phase_ms(lcb_ctx *ctx, float *ms, int n_phases);
 
+/* ------------------------------------------------------------------ trustless DKG G1 work
+   coeffs: n_comm commitments x (degree+1)(degree+2)/2 serialized G1 coefficients each, in Commitment's symmetric
+   Index(i, j) order (src/Lachain.Consensus/ThresholdKeygen/Data/Commitment.cs:14-21,55-59).
+   lcb_dkg_commitment_eval: out[q] = Commitment.Evaluate(xs[q], ys[q]) of commitment comm_idx[q] (Commitment.cs:23-37,
+     the per-value check of TrustlessKeygen.HandleSendValue, TrustlessKeygen.cs:150-152).
+   lcb_dkg_commitment_rows: rows_out[q] = Commitment.Evaluate(xs[q]) = degree+1 points (Commitment.cs:39-53; the
+     commit check of HandleCommit, TrustlessKeygen.cs:90-94, and TryGetKeys' Evaluate(0), :166).
+   lcb_g1_eval_poly_batch: MclBls12381.EvaluatePolynomial over G1 at many small x (TryGetKeys, TrustlessKeygen.cs:172-174).
+   x, y are the reference's int arguments (player indices); status[q] = 0 for a malformed coefficient or a
+   comm_idx >= n_comm.  Results equal the reference's Fr-power sums for coefficients in G1. */
+int lcb_dkg_commitment_eval(uint8_t *out, uint8_t *status, const uint8_t *coeffs, size_t n_comm, int degree,
+                            const uint32_t *comm_idx, const int32_t *xs, const int32_t *ys, size_t n_queries);
+int lcb_dkg_commitment_rows(uint8_t *rows_out, uint8_t *status, const uint8_t *coeffs, size_t n_comm, int degree,
+                            const uint32_t *comm_idx, const int32_t *xs, size_t n_queries);
+int lcb_g1_eval_poly_batch(uint8_t *out, uint8_t *status, const uint8_t *coeffs, size_t n_coeffs, const int32_t *xs,
+                           size_t n_points);
+
 /* ------------------------------------------------------------------ aggregation queue (one share per call)
    The consensus code verifies one share per call from many protocol threads (HoneyBadger.cs:156-158,211-212,
    ThresholdSigner.cs:62, AbstractProtocol.cs:46-47).  A queue aggregates such calls into GPU batches: submit

@@ -39,6 +39,9 @@ extern "C" void lcbk_msm_horner(hipStream_t s, const void *win, u32 nwin, u32 c,
 extern "C" void lcbk_g1_jac_compress(dim3 grid, hipStream_t s, const void *in, u32 n, uint8_t *out);
 extern "C" void lcbk_g1_to_affine(dim3 grid, hipStream_t s, const uint8_t *in, u32 n, void *out, uint8_t *ok);
 extern "C" int lcbk_sort_pairs(void *temp, size_t *temp_bytes, u32 *keys, u32 *keys_alt, u32 *vals, u32 *vals_alt, u32 m, int end_bit, hipStream_t s);
+extern "C" void lcbk_dkg_rows(dim3 grid, hipStream_t s, const void *coef, u32 n_coef, u32 n_comm, u32 D, const u32 *comm, const int *xs, u32 n_q, void *rows, uint8_t *ok_out);
+extern "C" void lcbk_dkg_horner(dim3 grid, hipStream_t s, const void *rows, const uint8_t *row_ok, u32 D, const u32 *row, const int *ys, u32 n_q, uint8_t *out48, uint8_t *status);
+extern "C" void lcbk_g1a_to_jac(dim3 grid, hipStream_t s, const void *in, u32 n, void *out, uint8_t *ok);
 extern "C" void lcbk_op(dim3 grid, hipStream_t s, int op, u32 *io, int orig_cof);
 
 // sizes of the device records the host allocates

@@ -47,7 +47,7 @@ struct lcb_ctx {
     uint64_t s_gen = 0;
     bool s_ready = false;
     // Lagrange / assembly / MSM / staging
-    DevBuf lag[3], sel[3], msm[12], in[8], out[4];
+    DevBuf lag[3], sel[3], msm[12], in[8], out[4], dkg[6];
     hipEvent_t ver_ev[3] = {};
     bool ver_ev_ready = false, ver_ran = false;
     hipEvent_t msm_ev[7] = {};

@@ -21,6 +21,7 @@
 #include <mutex>
 #include <vector>
 #include <string>
+#include <algorithm>
 #include <sys/random.h>
 
 #include "launch.h"
@@ -528,6 +529,7 @@ void ctx_free(lcb_ctx *c) {
     for (auto &b : c->msm) b.release();
     for (auto &b : c->in) b.release();
     for (auto &b : c->out) b.release();
+    for (auto &b : c->dkg) b.release();
     if (c->ver_ev_ready) for (auto &e : c->ver_ev) (void)hipEventDestroy(e);
     if (c->msm_ev_ready) for (auto &e : c->msm_ev) (void)hipEventDestroy(e);
     if (c->order) (void)hipEventDestroy(c->order);
@@ -1097,6 +1099,126 @@ extern "C" int lcb_coin_fold_dev(uint8_t *parity, uint64_t *nonce, const uint8_t
     if (n > 0xffffffffu) { set_err("coin fold: batch too large"); return -1; }
     if (n) lcbk_coin_fold(dim3(nblk(n)), (hipStream_t)stream, sigs, (u32)n, parity, nonce);
     return launched("coin fold launch") ? 0 : -1;
+}
+
+// ================================================================== trustless DKG G1 work (k_dkg.hip)
+// Commitment.Evaluate(x, y) / Evaluate(x) (src/Lachain.Consensus/ThresholdKeygen/Data/Commitment.cs:23-53) for whole
+// batches: rows of every distinct (commitment, x) once, then Horner in y per query.
+namespace {
+int dkg_rows_enqueue(lcb_ctx *c, const uint8_t *d_coeffs, size_t n_comm, size_t n_coef, int degree,
+                     const uint32_t *d_comm, const int32_t *d_xs, size_t n_rows, hipStream_t s, void **rows_out,
+                     uint8_t **rows_ok) {
+    size_t total = n_comm * n_coef, lanes = n_rows * (size_t)(degree + 1);
+    if (total > 0xffffffffu || lanes > 0xffffffffu) { set_err("dkg: batch too large"); return -1; }
+    void *aff = c->dkg[0].get(total * LCB_G1A_ST_BYTES);
+    void *rows = c->dkg[1].get(lanes * LCB_G1_JAC_BYTES);
+    uint8_t *rok = (uint8_t *)c->dkg[2].get(lanes);
+    if (!aff || !rows || !rok) { set_err("device allocation failed"); return -1; }
+    if (total) lcbk_g1_decompress(dim3(nblk(total)), s, d_coeffs, (u32)total, aff);
+    if (lanes)
+        lcbk_dkg_rows(dim3(nblk(lanes)), s, aff, (u32)n_coef, (u32)n_comm, (u32)degree, d_comm, d_xs, (u32)n_rows, rows,
+                      rok);
+    *rows_out = rows;
+    *rows_ok = rok;
+    return launched("dkg rows launch") ? 0 : -1;
+}
+bool dkg_shape(size_t n_comm, int degree, size_t *n_coef) {
+    if (degree < 0 || degree > 4096) { set_err("dkg: degree out of range"); return false; }
+    *n_coef = (size_t)(degree + 1) * (size_t)(degree + 2) / 2;
+    (void)n_comm;
+    return true;
+}
+}  // namespace
+extern "C" int lcb_dkg_commitment_rows(uint8_t *rows_out, uint8_t *status, const uint8_t *coeffs, size_t n_comm,
+                                       int degree, const uint32_t *comm_idx, const int32_t *xs, size_t n_queries) {
+    SYNC_CTX_OR(c, -1)
+    size_t n_coef;
+    if (!dkg_shape(n_comm, degree, &n_coef)) return -1;
+    if (!n_queries) return 0;
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    size_t lanes = n_queries * (size_t)(degree + 1);
+    const uint8_t *dco = up(c->in[0], coeffs, 48 * n_comm * n_coef, s);
+    const uint32_t *dci = up(c->in[1], comm_idx, n_queries, s);
+    const int32_t *dx = up(c->in[2], xs, n_queries, s);
+    uint8_t *dout = (uint8_t *)c->out[0].get(48 * lanes);
+    if (!dco || !dci || !dx || !dout) { set_err("device allocation failed"); return -1; }
+    void *rows;
+    uint8_t *rok;
+    if (dkg_rows_enqueue(c, dco, n_comm, n_coef, degree, dci, dx, n_queries, s, &rows, &rok)) return -1;
+    lcbk_g1_jac_compress(dim3(nblk(lanes)), s, rows, (u32)lanes, dout);
+    std::vector<uint8_t> ok(lanes);
+    hipMemcpyAsync(rows_out, dout, 48 * lanes, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(ok.data(), rok, lanes, hipMemcpyDeviceToHost, s);
+    if (!sync_check(c, "dkg rows")) return -1;
+    for (size_t qi = 0; qi < n_queries; qi++) {
+        uint8_t st = 1;
+        for (int i = 0; i <= degree; i++) st &= ok[qi * (degree + 1) + i];
+        status[qi] = st;
+    }
+    return 0;
+}
+extern "C" int lcb_dkg_commitment_eval(uint8_t *out, uint8_t *status, const uint8_t *coeffs, size_t n_comm, int degree,
+                                       const uint32_t *comm_idx, const int32_t *xs, const int32_t *ys,
+                                       size_t n_queries) {
+    SYNC_CTX_OR(c, -1)
+    size_t n_coef;
+    if (!dkg_shape(n_comm, degree, &n_coef)) return -1;
+    if (!n_queries) return 0;
+    // distinct (commitment, x) pairs -> rows; every query evaluates its row at y
+    std::vector<uint32_t> row_comm, row_of(n_queries);
+    std::vector<int32_t> row_x;
+    {
+        std::vector<std::pair<uint64_t, uint32_t>> keys(n_queries);
+        for (size_t i = 0; i < n_queries; i++) keys[i] = {((uint64_t)comm_idx[i] << 32) | (uint32_t)xs[i], (uint32_t)i};
+        std::sort(keys.begin(), keys.end());
+        for (size_t i = 0; i < n_queries; i++) {
+            if (i == 0 || keys[i].first != keys[i - 1].first) {
+                row_comm.push_back((uint32_t)(keys[i].first >> 32));
+                row_x.push_back((int32_t)(uint32_t)keys[i].first);
+            }
+            row_of[keys[i].second] = (uint32_t)(row_comm.size() - 1);
+        }
+    }
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    const uint8_t *dco = up(c->in[0], coeffs, 48 * n_comm * n_coef, s);
+    const uint32_t *drc = up(c->in[1], row_comm.data(), row_comm.size(), s);
+    const int32_t *drx = up(c->in[2], row_x.data(), row_x.size(), s);
+    const uint32_t *drow = up(c->in[3], row_of.data(), n_queries, s);
+    const int32_t *dy = up(c->in[4], ys, n_queries, s);
+    uint8_t *dout = (uint8_t *)c->out[0].get(48 * n_queries), *dst = (uint8_t *)c->out[1].get(n_queries);
+    if (!dco || !drc || !drx || !drow || !dy || !dout || !dst) { set_err("device allocation failed"); return -1; }
+    void *rows;
+    uint8_t *rok;
+    if (dkg_rows_enqueue(c, dco, n_comm, n_coef, degree, drc, drx, row_comm.size(), s, &rows, &rok)) return -1;
+    lcbk_dkg_horner(dim3(nblk(n_queries)), s, rows, rok, (u32)degree, drow, dy, (u32)n_queries, dout, dst);
+    hipMemcpyAsync(out, dout, 48 * n_queries, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(status, dst, n_queries, hipMemcpyDeviceToHost, s);
+    return sync_check(c, "dkg eval") ? 0 : -1;
+}
+extern "C" int lcb_g1_eval_poly_batch(uint8_t *out, uint8_t *status, const uint8_t *coeffs, size_t n_coeffs,
+                                      const int32_t *xs, size_t n_points) {
+    SYNC_CTX_OR(c, -1)
+    if (!n_coeffs) { set_err("eval poly: no coefficients"); return -1; }
+    if (!n_points) return 0;
+    if (n_coeffs > 0xffffffffu || n_points > 0xffffffffu) { set_err("eval poly: batch too large"); return -1; }
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    const uint8_t *dco = up(c->in[0], coeffs, 48 * n_coeffs, s);
+    const int32_t *dx = up(c->in[1], xs, n_points, s);
+    void *aff = c->dkg[0].get(n_coeffs * LCB_G1A_ST_BYTES), *rows = c->dkg[1].get(n_coeffs * LCB_G1_JAC_BYTES);
+    uint8_t *rok = (uint8_t *)c->dkg[2].get(n_coeffs);
+    uint32_t *drow = (uint32_t *)c->dkg[3].get(4 * n_points);
+    uint8_t *dout = (uint8_t *)c->out[0].get(48 * n_points), *dst = (uint8_t *)c->out[1].get(n_points);
+    if (!dco || !dx || !aff || !rows || !rok || !drow || !dout || !dst) { set_err("device allocation failed"); return -1; }
+    hipMemsetAsync(drow, 0, 4 * n_points, s);    // every point evaluates row 0 (the coefficient vector)
+    lcbk_g1_decompress(dim3(nblk(n_coeffs)), s, dco, (u32)n_coeffs, aff);
+    lcbk_g1a_to_jac(dim3(nblk(n_coeffs)), s, aff, (u32)n_coeffs, rows, rok);
+    lcbk_dkg_horner(dim3(nblk(n_points)), s, rows, rok, (u32)(n_coeffs - 1), drow, dx, (u32)n_points, dout, dst);
+    hipMemcpyAsync(out, dout, 48 * n_points, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(status, dst, n_points, hipMemcpyDeviceToHost, s);
+    return sync_check(c, "eval poly") ? 0 : -1;
 }
 
 // ================================================================== batch: Lagrange, scalar mul, hash, MSM

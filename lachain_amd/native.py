@@ -100,6 +100,11 @@ _SIGS = {
     "lcb_coin_parity": (ctypes.c_int, [c_u8p, c_size]),
     "lcb_coin_nonce": (ctypes.c_uint64, [c_u8p, c_size]),
     "lcb_coin_fold_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_size, ctypes.c_void_p]),
+    "lcb_dkg_commitment_eval": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_size, ctypes.c_int, c_u32p,
+                                               ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), c_size]),
+    "lcb_dkg_commitment_rows": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_size, ctypes.c_int, c_u32p,
+                                               ctypes.POINTER(ctypes.c_int32), c_size]),
+    "lcb_g1_eval_poly_batch": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_size, ctypes.POINTER(ctypes.c_int32), c_size]),
     "lcb_queue_create": (ctypes.c_void_p, [c_size, ctypes.c_uint32]),
     "lcb_queue_destroy": (None, [ctypes.c_void_p]),
     "lcb_queue_tpke_verify": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
@@ -365,6 +370,52 @@ def xor_with_hash(g1_48, data):
     ob, po = _out(len(data))
     load(False).lcb_xor_with_hash(po, pg, pd, len(data))
     return bytes(ob)[: len(data)]
+
+
+def _i32_keep(keep, vals):
+    arr = (ctypes.c_int32 * max(1, len(vals)))(*vals)
+    keep.append(arr)
+    return ctypes.cast(arr, ctypes.POINTER(ctypes.c_int32))
+
+
+def dkg_commitment_eval(commitments, degree, queries):
+    """commitments: list of coefficient lists (serialized G1, Commitment's Index order); queries: (comm, x, y).
+    -> list of 48-byte Commitment.Evaluate(x, y) or None (malformed)."""
+    keep = []
+    _, pc = _bytes_ptr_keep(keep, b"".join(b"".join(c) for c in commitments))
+    _, pi = _u32_keep(keep, [q[0] for q in queries])
+    px, py = _i32_keep(keep, [q[1] for q in queries]), _i32_keep(keep, [q[2] for q in queries])
+    n = len(queries)
+    ob, po = _out(48 * n)
+    sb, ps = _out(n)
+    _check(lib().lcb_dkg_commitment_eval(po, ps, pc, len(commitments), degree, pi, px, py, n), "dkg_commitment_eval")
+    o = bytes(ob)
+    return [o[48 * q:48 * q + 48] if sb[q] else None for q in range(n)]
+
+
+def dkg_commitment_rows(commitments, degree, queries):
+    """queries: (comm, x) -> list of degree+1 points (Commitment.Evaluate(x)) or None"""
+    keep = []
+    _, pc = _bytes_ptr_keep(keep, b"".join(b"".join(c) for c in commitments))
+    _, pi = _u32_keep(keep, [q[0] for q in queries])
+    px = _i32_keep(keep, [q[1] for q in queries])
+    n, w = len(queries), degree + 1
+    ob, po = _out(48 * n * w)
+    sb, ps = _out(n)
+    _check(lib().lcb_dkg_commitment_rows(po, ps, pc, len(commitments), degree, pi, px, n), "dkg_commitment_rows")
+    o = bytes(ob)
+    return [[o[48 * (q * w + i):48 * (q * w + i) + 48] for i in range(w)] if sb[q] else None for q in range(n)]
+
+
+def g1_eval_poly_batch(coeffs, xs):
+    keep = []
+    _, pc = _bytes_ptr_keep(keep, b"".join(coeffs))
+    px = _i32_keep(keep, xs)
+    ob, po = _out(48 * len(xs))
+    sb, ps = _out(len(xs))
+    _check(lib().lcb_g1_eval_poly_batch(po, ps, pc, len(coeffs), px, len(xs)), "g1_eval_poly_batch")
+    o = bytes(ob)
+    return [o[48 * q:48 * q + 48] if sb[q] else None for q in range(len(xs))]
 
 
 def coin_parity(sig: bytes) -> bool:

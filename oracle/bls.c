@@ -1685,6 +1685,81 @@ int orc_ts_sign(uint8_t sigb[96], const uint8_t skb[32], const uint8_t *msg, siz
     return 0;
 }
 
+/* ================================================================== trustless DKG (Commitment) restatement */
+static void fr_from_i32(fr *r, int32_t v) { uint8_t b[32]; orc_fr_from_int(b, v); fr_from_bytes(r, b); }
+static int dkg_index(int i, int j) { if (i > j) { int t = i; i = j; j = t; } return i * (i + 1) / 2 + j; } /* Commitment.cs:55-59 */
+/* Commitment.Evaluate(x, y) exactly as written (src/Lachain.Consensus/ThresholdKeygen/Data/Commitment.cs:23-37):
+   powX = Powers(Fr(x), D+1), powY = Powers(Fr(y), D+1); result += C[Index(i,j)] * powX[i] * powY[j], i.e. two
+   successive G1 x Fr multiplications per term, (D+1)^2 terms. */
+int orc_dkg_commitment_eval(uint8_t out[48], const uint8_t *coeffs, int D, int32_t x, int32_t y) {
+    orc_init();
+    int n = (D + 1) * (D + 2) / 2;
+    g1 *C = malloc(sizeof(g1) * n);
+    fr *px = malloc(sizeof(fr) * (D + 1)), *py = malloc(sizeof(fr) * (D + 1));
+    int ok = C && px && py;
+    for (int k = 0; ok && k < n; k++) ok = g1_load(&C[k], coeffs + 48 * (size_t)k);
+    if (ok) {
+        fr fx, fy;
+        fr_from_i32(&fx, x);
+        fr_from_i32(&fy, y);
+        fr_from_i32(&px[0], 1);
+        fr_from_i32(&py[0], 1);
+        for (int k = 1; k <= D; k++) { fr_mul(&px[k], &px[k - 1], &fx); fr_mul(&py[k], &py[k - 1], &fy); }
+        g1 acc, t;
+        memset(&acc, 0, sizeof acc);
+        for (int i = 0; i <= D; i++)
+            for (int j = 0; j <= D; j++) {
+                g1_mul_fr(&t, &C[dkg_index(i, j)], &px[i]);
+                g1_mul_fr(&t, &t, &py[j]);
+                g1_add(&acc, &acc, &t);
+            }
+        g1_ser(out, &acc);
+    }
+    free(C); free(px); free(py);
+    return ok ? 0 : -1;
+}
+/* Commitment.Evaluate(x) (Commitment.cs:39-53): row[i] = sum_j C[Index(i,j)] * x^j, D+1 points */
+int orc_dkg_commitment_row(uint8_t *out, const uint8_t *coeffs, int D, int32_t x) {
+    orc_init();
+    int n = (D + 1) * (D + 2) / 2;
+    g1 *C = malloc(sizeof(g1) * n);
+    int ok = C != NULL;
+    for (int k = 0; ok && k < n; k++) ok = g1_load(&C[k], coeffs + 48 * (size_t)k);
+    if (ok) {
+        fr fx;
+        fr_from_i32(&fx, x);
+        for (int i = 0; i <= D; i++) {
+            g1 acc, t;
+            memset(&acc, 0, sizeof acc);
+            fr xp;
+            fr_from_i32(&xp, 1);
+            for (int j = 0; j <= D; j++) {
+                g1_mul_fr(&t, &C[dkg_index(i, j)], &xp);
+                g1_add(&acc, &acc, &t);
+                fr_mul(&xp, &xp, &fx);
+            }
+            g1_ser(out + 48 * (size_t)i, &acc);
+        }
+    }
+    free(C);
+    return ok ? 0 : -1;
+}
+/* MclBls12381.EvaluatePolynomial over G1 (TrustlessKeygen.cs:172-174): sum_k c_k x^k by Horner with Fr x */
+int orc_g1_eval_poly(uint8_t out[48], const uint8_t *coeffs, size_t n, const uint8_t xb[32]) {
+    orc_init();
+    fr x;
+    if (!n || !fr_from_bytes(&x, xb)) return -1;
+    g1 acc, c;
+    if (!g1_load(&acc, coeffs + 48 * (n - 1))) return -1;
+    for (size_t k = n - 1; k-- > 0;) {
+        if (!g1_load(&c, coeffs + 48 * k)) return -1;
+        g1_mul_fr(&acc, &acc, &x);
+        g1_add(&acc, &acc, &c);
+    }
+    g1_ser(out, &acc);
+    return 0;
+}
+
 /* ================================================================== CPU baseline batch */
 /* ThresholdSignature.PublicKey.ValidateSignature for a batch (ThresholdSignature/PublicKey.cs:16-21), as the
    reference calls it: hash-to-G2 of the message and two pairings per share, OpenMP over shares.  The CPU

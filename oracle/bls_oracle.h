@@ -114,6 +114,10 @@ int orc_ts_sign(uint8_t sig[96], const uint8_t sk[32], const uint8_t *msg, size_
 /* ---- batch (CPU-baseline) entry points, OpenMP over items ---- */
 /* per share i: ct index ct_idx[i], decryptor dec_idx[i]; as-reference semantics
    (hash recomputed per share, two separate pairings compared) */
+/* trustless DKG: Commitment.Evaluate(x, y) / Evaluate(x) as the reference writes them, G1 polynomial evaluation */
+int orc_dkg_commitment_eval(uint8_t out[48], const uint8_t *coeffs, int D, int32_t x, int32_t y);
+int orc_dkg_commitment_row(uint8_t *out, const uint8_t *coeffs, int D, int32_t x);
+int orc_g1_eval_poly(uint8_t out[48], const uint8_t *coeffs, size_t n, const uint8_t x[32]);
 /* CPU baseline with the GPU's algorithm (per-ciphertext / per-message H and Miller lines, one final exp per
    share): bench.py's "amortized" cpu_baseline legs */
 int orc_tpke_verify_batch_amortized(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys,

@@ -141,6 +141,24 @@ def g1_msm(points, scalars):
     return o.raw
 
 
+def dkg_commitment_eval(coeffs, degree, x, y):
+    o = _buf(48)
+    _ck(lib().orc_dkg_commitment_eval(o, b"".join(coeffs), degree, ctypes.c_int32(x), ctypes.c_int32(y)), "dkg eval")
+    return o.raw
+
+
+def dkg_commitment_row(coeffs, degree, x):
+    o = _buf(48 * (degree + 1))
+    _ck(lib().orc_dkg_commitment_row(o, b"".join(coeffs), degree, ctypes.c_int32(x)), "dkg row")
+    return [o.raw[48 * i:48 * i + 48] for i in range(degree + 1)]
+
+
+def g1_eval_poly(coeffs, x):
+    o = _buf(48)
+    _ck(lib().orc_g1_eval_poly(o, b"".join(coeffs), ctypes.c_size_t(len(coeffs)), x), "g1 eval poly")
+    return o.raw
+
+
 # ---------------------------------------------------------------- pairing
 def pairing(p, q):
     o = _buf(576); _ck(lib().orc_pairing(o, p, q), "pairing"); return o.raw
