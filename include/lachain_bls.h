@@ -281,6 +281,17 @@ int lcb_dkg_commitment_rows(uint8_t *rows_out, uint8_t *status, const uint8_t *c
 int lcb_g1_eval_poly_batch(uint8_t *out, uint8_t *status, const uint8_t *coeffs, size_t n_coeffs, const int32_t *xs,
                            size_t n_points);
 
+/* ------------------------------------------------------------------ reliable broadcast: Reed-Solomon
+   The EncryptedShare bytes travel as N shards of a GF(2^8) Reed-Solomon code (polynomial 0x11D, alpha = 2, generator
+   roots alpha^0..alpha^(erasures-1): ErasureCoding.cs:13), erasures = 2F.
+   lcb_rs_encode = ReliableBroadcast.ErasureCodingShards(input, n_shards, erasures) (ReliableBroadcast.cs:393-419):
+     input_len must be a multiple of n_shards - erasures (AugmentInput pads it); shards_out = n_shards x shard bytes.
+   lcb_rs_decode = DecodeFromEchos (ReliableBroadcast.cs:421-446): exactly n_shards - erasures echoes, echo e is shard
+     from[e]; out = all n_shards shards.  -1 on bad arguments or an unsolvable erasure set (only with > 255 shards). */
+int lcb_rs_encode(uint8_t *shards_out, const uint8_t *input, size_t input_len, int n_shards, int erasures);
+int lcb_rs_decode(uint8_t *out, const uint8_t *echo_data, const int32_t *from, int n_echos, size_t shard_size,
+                  int n_shards, int erasures);
+
 /* ------------------------------------------------------------------ aggregation queue (one share per call)
    The consensus code verifies one share per call from many protocol threads (HoneyBadger.cs:156-158,211-212,
    ThresholdSigner.cs:62, AbstractProtocol.cs:46-47).  A queue aggregates such calls into GPU batches: submit

@@ -1221,6 +1221,94 @@ extern "C" int lcb_g1_eval_poly_batch(uint8_t *out, uint8_t *status, const uint8
     return sync_check(c, "eval poly") ? 0 : -1;
 }
 
+// ================================================================== reliable-broadcast Reed-Solomon (k_rs.hip)
+// ReliableBroadcast.ErasureCodingShards / DecodeFromEchos (src/Lachain.Consensus/ReliableBroadcast/ReliableBroadcast.cs:
+// 393-446): the erased / parity shards are M times the known shards, M = H_E^-1 H_K built on the GPU.
+namespace {
+int rs_enqueue(lcb_ctx *c, uint8_t *d_out, const uint8_t *d_known, const std::vector<int> &pe,
+               const std::vector<int> &pk, int n, size_t S, hipStream_t s, uint8_t **d_ok) {
+    static bool attr = false;
+    if (!attr) {
+        hipFuncSetAttribute((const void *)lcbk_rs_matrix_kernel(), hipFuncAttributeMaxDynamicSharedMemorySize, 65536 * 2);
+        attr = true;
+    }
+    int m = (int)pe.size(), k = (int)pk.size();
+    int *dpe = (int *)c->dkg[4].get(4 * (pe.size() + pk.size()));
+    uint8_t *M = (uint8_t *)c->dkg[5].get((size_t)m * k + 16);
+    if (!dpe || !M) { set_err("device allocation failed"); return -1; }
+    std::vector<int> both(pe);
+    both.insert(both.end(), pk.begin(), pk.end());
+    hipMemcpyAsync(dpe, both.data(), 4 * both.size(), hipMemcpyHostToDevice, s);
+    uint8_t *ok = M + (size_t)m * k;
+    lcbk_rs_matrix(s, dpe, m, dpe + m, k, n, M, ok);
+    lcbk_rs_apply(s, M, ok, m, k, d_known, S, dpe, d_out);
+    *d_ok = ok;
+    return launched("rs launch") ? 0 : -1;
+}
+}  // namespace
+extern "C" int lcb_rs_encode(uint8_t *shards_out, const uint8_t *input, size_t input_len, int n_shards, int erasures) {
+    SYNC_CTX_OR(c, -1)
+    int k = n_shards - erasures;
+    if (n_shards <= 0 || erasures < 0 || k <= 0 || input_len % (size_t)k) {
+        set_err("rs encode: need 0 <= erasures < shards and input length divisible by the data shards");
+        return -1;
+    }
+    size_t S = input_len / (size_t)k;
+    if (erasures == 0 || S == 0) { memcpy(shards_out, input, input_len); return 0; }
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    uint8_t *dout = (uint8_t *)c->out[0].get(S * n_shards);
+    if (!dout) { set_err("device allocation failed"); return -1; }
+    hipMemcpyAsync(dout, input, input_len, hipMemcpyHostToDevice, s);   // data shards stay in place (systematic)
+    std::vector<int> pe, pk;
+    for (int j = k; j < n_shards; j++) pe.push_back(j);
+    for (int j = 0; j < k; j++) pk.push_back(j);
+    uint8_t *dok;
+    if (rs_enqueue(c, dout, dout, pe, pk, n_shards, S, s, &dok)) return -1;
+    uint8_t ok = 0;
+    hipMemcpyAsync(shards_out, dout, S * n_shards, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(&ok, dok, 1, hipMemcpyDeviceToHost, s);
+    if (!sync_check(c, "rs encode")) return -1;
+    if (!ok) { set_err("rs encode: parity positions are not independent (more than 255 shards)"); return -1; }
+    return 0;
+}
+extern "C" int lcb_rs_decode(uint8_t *out, const uint8_t *echo_data, const int32_t *from, int n_echos, size_t shard_size,
+                             int n_shards, int erasures) {
+    SYNC_CTX_OR(c, -1)
+    int k = n_shards - erasures;
+    if (n_shards <= 0 || erasures < 0 || k <= 0 || n_echos != k) {
+        set_err("rs decode: need exactly shards - erasures echoes (DecodeFromEchos asserts N - 2F)");
+        return -1;
+    }
+    std::vector<char> have(n_shards, 0);
+    std::vector<int> pe, pk;
+    for (int e = 0; e < n_echos; e++) {
+        if (from[e] < 0 || from[e] >= n_shards || have[from[e]]) { set_err("rs decode: bad or duplicate echo index"); return -1; }
+        have[from[e]] = 1;
+        pk.push_back(from[e]);
+    }
+    for (int j = 0; j < n_shards; j++) if (!have[j]) pe.push_back(j);
+    size_t S = shard_size;
+    if (S == 0) return 0;
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    uint8_t *dout = (uint8_t *)c->out[0].get(S * n_shards);
+    const uint8_t *decho = up(c->in[0], echo_data, S * (size_t)n_echos, s);
+    if (!dout || !decho) { set_err("device allocation failed"); return -1; }
+    for (int e = 0; e < n_echos; e++)
+        hipMemcpyAsync(dout + (size_t)from[e] * S, decho + (size_t)e * S, S, hipMemcpyDeviceToDevice, s);
+    uint8_t ok = 1;
+    if (!pe.empty()) {
+        uint8_t *dok;
+        if (rs_enqueue(c, dout, decho, pe, pk, n_shards, S, s, &dok)) return -1;
+        hipMemcpyAsync(&ok, dok, 1, hipMemcpyDeviceToHost, s);
+    }
+    hipMemcpyAsync(out, dout, S * n_shards, hipMemcpyDeviceToHost, s);
+    if (!sync_check(c, "rs decode")) return -1;
+    if (!ok) { set_err("rs decode: erased positions share an evaluation point (more than 255 shards)"); return -1; }
+    return 0;
+}
+
 // ================================================================== batch: Lagrange, scalar mul, hash, MSM
 static int lagrange_batch(int g, uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys, const uint32_t *off,
                           size_t np) {

@@ -105,6 +105,9 @@ _SIGS = {
     "lcb_dkg_commitment_rows": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_size, ctypes.c_int, c_u32p,
                                                ctypes.POINTER(ctypes.c_int32), c_size]),
     "lcb_g1_eval_poly_batch": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_size, ctypes.POINTER(ctypes.c_int32), c_size]),
+    "lcb_rs_encode": (ctypes.c_int, [c_u8p, c_u8p, c_size, ctypes.c_int, ctypes.c_int]),
+    "lcb_rs_decode": (ctypes.c_int, [c_u8p, c_u8p, ctypes.POINTER(ctypes.c_int32), ctypes.c_int, c_size, ctypes.c_int,
+                                     ctypes.c_int]),
     "lcb_queue_create": (ctypes.c_void_p, [c_size, ctypes.c_uint32]),
     "lcb_queue_destroy": (None, [ctypes.c_void_p]),
     "lcb_queue_tpke_verify": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
@@ -416,6 +419,26 @@ def g1_eval_poly_batch(coeffs, xs):
     _check(lib().lcb_g1_eval_poly_batch(po, ps, pc, len(coeffs), px, len(xs)), "g1_eval_poly_batch")
     o = bytes(ob)
     return [o[48 * q:48 * q + 48] if sb[q] else None for q in range(len(xs))]
+
+
+def rs_encode(data: bytes, n_shards: int, erasures: int) -> bytes:
+    """ReliableBroadcast.ErasureCodingShards: all shards concatenated (len(data) divisible by the data shards)"""
+    keep = []
+    _, pd = _bytes_ptr_keep(keep, data)
+    k = n_shards - erasures
+    ob, po = _out(len(data) // k * n_shards if k > 0 else 0)
+    _check(lib().lcb_rs_encode(po, pd, len(data), n_shards, erasures), "rs_encode")
+    return bytes(ob)[: len(data) // k * n_shards]
+
+
+def rs_decode(echos, shard_size: int, n_shards: int, erasures: int) -> bytes:
+    """ReliableBroadcast.DecodeFromEchos: echos = [(from, shard bytes)] -> all shards concatenated"""
+    keep = []
+    _, pd = _bytes_ptr_keep(keep, b"".join(e[1] for e in echos))
+    pf = _i32_keep(keep, [e[0] for e in echos])
+    ob, po = _out(shard_size * n_shards)
+    _check(lib().lcb_rs_decode(po, pd, pf, len(echos), shard_size, n_shards, erasures), "rs_decode")
+    return bytes(ob)[: shard_size * n_shards]
 
 
 def coin_parity(sig: bytes) -> bool:

@@ -114,6 +114,12 @@ int orc_ts_sign(uint8_t sig[96], const uint8_t sk[32], const uint8_t *msg, size_
 /* ---- batch (CPU-baseline) entry points, OpenMP over items ---- */
 /* per share i: ct index ct_idx[i], decryptor dec_idx[i]; as-reference semantics
    (hash recomputed per share, two separate pairings compared) */
+/* reliable-broadcast Reed-Solomon erasure coding (rs.c) */
+int orc_rs_encode_codeword(int *cw, int n, int ecc);
+int orc_rs_decode_erasures(int *cw, int n, int ecc, const int *pos, int m);
+int orc_rs_encode_shards(uint8_t *out, const uint8_t *input, size_t len, int shards, int erasures);
+int orc_rs_decode_shards(uint8_t *out, const uint8_t *echo_data, const int32_t *from, int n_echos, size_t S, int shards,
+                         int erasures);
 /* trustless DKG: Commitment.Evaluate(x, y) / Evaluate(x) as the reference writes them, G1 polynomial evaluation */
 int orc_dkg_commitment_eval(uint8_t out[48], const uint8_t *coeffs, int D, int32_t x, int32_t y);
 int orc_dkg_commitment_row(uint8_t *out, const uint8_t *coeffs, int D, int32_t x);

@@ -159,6 +159,28 @@ def g1_eval_poly(coeffs, x):
     return o.raw
 
 
+def rs_encode_codeword(data, ecc):
+    n = len(data) + ecc
+    arr = (ctypes.c_int * n)(*(list(data) + [0] * ecc))
+    _ck(lib().orc_rs_encode_codeword(arr, n, ecc), "rs encode")
+    return list(arr)
+
+
+def rs_encode_shards(data: bytes, shards, erasures):
+    out = _buf(len(data) // (shards - erasures) * shards)
+    _ck(lib().orc_rs_encode_shards(out, data, ctypes.c_size_t(len(data)), shards, erasures), "rs encode shards")
+    return out.raw
+
+
+def rs_decode_shards(echos, shard_size, shards, erasures):
+    """echos: list of (from, shard bytes) -> all shards concatenated, or None if unsolvable"""
+    out = _buf(shard_size * shards)
+    frm = (ctypes.c_int32 * max(1, len(echos)))(*[e[0] for e in echos])
+    rc = lib().orc_rs_decode_shards(out, b"".join(e[1] for e in echos), frm, len(echos), ctypes.c_size_t(shard_size),
+                                    shards, erasures)
+    return out.raw if rc == 0 else None
+
+
 # ---------------------------------------------------------------- pairing
 def pairing(p, q):
     o = _buf(576); _ck(lib().orc_pairing(o, p, q), "pairing"); return o.raw
