@@ -179,6 +179,36 @@ void orc_sha3_256(uint8_t out[32], const uint8_t *m, size_t n) {
     sha3_final(&c, out);
 }
 
+/* original Keccak-256 (domain byte 0x01, BouncyCastle KeccakDigest(256) behind HashUtils.KeccakBytes,
+   src/Lachain.Crypto/HashUtils.cs:30-38) */
+void orc_keccak256(uint8_t out[32], const uint8_t *m, size_t n) {
+    const size_t rate = 136;
+    sha3_ctx c;
+    sha3_init(&c);
+    sha3_update(&c, m, n);
+    c.s[c.pos / 8] ^= (u64)0x01 << (8 * (c.pos % 8));
+    c.s[(rate - 1) / 8] ^= (u64)0x80 << (8 * ((rate - 1) % 8));
+    keccakf(c.s);
+    for (int i = 0; i < 32; i++) out[i] = (uint8_t)(c.s[i / 8] >> (8 * (i % 8)));
+}
+
+/* HashUtils.Keccak(BlockHeader) (HashUtils.cs:40-53): Keccak-256 of the RLP list [PrevBlockHash, StateHash,
+   MerkleRoot, Index, Nonce] with the hashes as their 32 raw bytes and Index / Nonce as 8 little-endian bytes
+   (ulong.ToBytes, SerialiaztionUtils.cs:210-213); Nethereum RLP: 0xa0 || 32 B, 0x88 || 8 B, list 0xf8 0x75 || 117 B */
+void orc_header_keccak(uint8_t out[32], const uint8_t prev[32], const uint8_t state[32], const uint8_t merkle[32],
+                       uint64_t index, uint64_t nonce) {
+    uint8_t b[119], *q = b;
+    *q++ = 0xf8; *q++ = 0x75;
+    const uint8_t *h[3] = {prev, state, merkle};
+    for (int i = 0; i < 3; i++) { *q++ = 0xa0; memcpy(q, h[i], 32); q += 32; }
+    uint64_t v[2] = {index, nonce};
+    for (int i = 0; i < 2; i++) {
+        *q++ = 0x88;
+        for (int j = 0; j < 8; j++) *q++ = (uint8_t)(v[i] >> (8 * j));
+    }
+    orc_keccak256(out, b, sizeof b);
+}
+
 /* BouncyCastle DigestRandomGenerator (Org.BouncyCastle.Crypto.Prng), CYCLE_COUNT = 10 */
 typedef struct { uint8_t seed[32], state[32]; int64_t seed_ctr, state_ctr; } drg_t;
 static void drg_add_counter(sha3_ctx *c, int64_t v) {

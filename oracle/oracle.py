@@ -292,3 +292,66 @@ def count_reset():
 
 def count_get():
     return lib().orc_count_get()
+
+
+# ---------------------------------------------------------------- secp256k1 ECDSA / Keccak (oracle/secp.c, §8f row 4)
+SECP_N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+SECP_P = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEFFFFFC2F
+
+
+def keccak256(m: bytes) -> bytes:
+    o = _buf(32); lib().orc_keccak256(o, m, ctypes.c_size_t(len(m))); return o.raw
+
+
+def header_keccak(prev: bytes, state: bytes, merkle: bytes, index: int, nonce: int) -> bytes:
+    o = _buf(32)
+    lib().orc_header_keccak(o, prev, state, merkle, ctypes.c_uint64(index), ctypes.c_uint64(nonce))
+    return o.raw
+
+
+def ecdsa_pubkey(priv: bytes):
+    """(compressed 33 B, uncompressed 65 B) public key of a 32-byte big-endian private key"""
+    c33, c65 = _buf(33), _buf(65)
+    _ck(lib().orc_ecdsa_pubkey(c33, c65, priv), "ecdsa_pubkey")
+    return c33.raw, c65.raw
+
+
+def ecdsa_sign_compact(hash32: bytes, priv: bytes, k: bytes):
+    """(r || s low-s, recovery id) with nonce k"""
+    sig, rid = _buf(64), ctypes.c_int(0)
+    _ck(lib().orc_ecdsa_sign_k(sig, ctypes.byref(rid), hash32, priv, k), "ecdsa_sign")
+    return sig.raw, rid.value
+
+
+def ecdsa_encode(sig64: bytes, recid: int, chain_id: int, use_new_chain_id: bool) -> bytes:
+    """DefaultCrypto.SignHashed's trailer (DefaultCrypto.cs:114-136): v = chainId * 2 + 35 + recId, 1 byte (low
+    byte of the int) for the old chain id, 2 bytes big-endian for the new one"""
+    v = chain_id * 2 + 35 + recid
+    return sig64 + ((v & 0xffff).to_bytes(2, "big") if use_new_chain_id else bytes([v & 0xff]))
+
+
+def ecdsa_verify_hashed(hash32: bytes, sig: bytes, pk: bytes, use_new_chain_id: bool, chain_id: int) -> bool:
+    f = lib().orc_ecdsa_verify_hashed
+    f.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                  ctypes.c_int, ctypes.c_int32]
+    return bool(f(hash32, len(hash32), sig, len(sig), pk, len(pk), int(bool(use_new_chain_id)), chain_id))
+
+
+def ecdsa_verify_batch(hashes: bytes, sigs: bytes, sig_len: int, pks: bytes, pk_len: int, pk_idx, n: int,
+                       use_new_chain_id: bool, chain_id: int, lib_=None) -> bytes:
+    import numpy as np
+    L = lib_ or lib()
+    idx = np.ascontiguousarray(np.asarray(pk_idx, dtype=np.int32))
+    o = _buf(max(1, n))
+    f = L.orc_ecdsa_verify_batch
+    f.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                  ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int, ctypes.c_int32]
+    f(o, hashes, sigs, sig_len, pks, pk_len, idx.ctypes.data, len(pks) // max(1, pk_len), n, int(bool(use_new_chain_id)),
+      chain_id)
+    return o.raw[:n]
+
+
+def ecdsa_recover(hash32: bytes, sig64: bytes, recid: int):
+    """compressed public key recovered from (hash, r || s, recid), or None"""
+    o = _buf(33)
+    return o.raw if lib().orc_ecdsa_recover(o, hash32, sig64, int(recid)) == 0 else None
