@@ -744,6 +744,133 @@ def run_replay(args, nat, torch, dev, rank, world):
                        f"ranks; per view {checks_per_view} pairing checks, {n} G1 and {n_coins} G2 Lagrange (k={f + 1})")
 
 
+# ------------------------------------------------------------------ secp256k1 header signatures
+W_ECDSA = 66 * 11 + 3        # Fp-mul per verification: <= 66 mixed additions (7M + 4S) + the r Z^2 comparison
+MAC_PER_FPMUL_SECP = 72      # 8x8 32-bit product + 8 for the fold by 2^32 + 977 (p = 2^256 - 2^32 - 977)
+
+
+def ecdsa_inputs(nat, rank, n, n_val, era, chain):
+    """n SignedHeaderMessages of one era from n_val validators (RootProtocol.cs:91-105): random headers with Index =
+    era, hashed and signed on the GPU with the product's own kernels (lcb_header_keccak_batch,
+    lcb_ecdsa_sign_hashed_batch, new chain id); 1 % of the signatures get one bit of s flipped (must reject)."""
+    rng = np.random.default_rng(0x4C61636861696E + 0x5EC + rank)
+
+    def scalars(k):
+        b = rng.integers(0, 256, (k, 32), dtype=np.uint8)
+        b[:, 0] &= 0x7F                                 # < 2^255 < n
+        b[:, 31] |= 1                                   # nonzero
+        return b
+    privs = scalars(n_val)
+    keys, ok = nat.ecdsa_pubkey_batch(privs.tobytes())
+    assert all(ok)
+    hdr = rng.integers(0, 256, (n, 112), dtype=np.uint8)
+    hdr[:, 0:8] = np.frombuffer(int(era).to_bytes(8, "little"), dtype=np.uint8)
+    hashes = nat.header_keccak_batch(hdr.tobytes())
+    idx = rng.integers(0, n_val, n, dtype=np.int32)
+    sigs, sok = nat.ecdsa_sign_hashed_batch(hashes, privs[idx].tobytes(), scalars(n).tobytes(), True, chain)
+    assert all(sok)
+    sig = np.frombuffer(sigs, dtype=np.uint8).reshape(n, 66).copy()
+    bad = rng.choice(n, max(1, n // 100), replace=False)
+    sig[bad, 40] ^= 1
+    expect = np.ones(n, dtype=np.uint8)
+    expect[bad] = 0
+    return dict(keys=keys, hdr=hdr.tobytes(), hashes=hashes, sigs=sig.tobytes(), idx=idx, expect=expect)
+
+
+def ecdsa_cpu_baseline(inp, n_total, chain, target_s=8.0):
+    lib, build = oracle_timing_lib()
+    threads = cpu_threads()
+
+    def run(m):
+        out = ctypes.create_string_buffer(m)
+        idx = np.ascontiguousarray(inp["idx"][:m])
+        f = lib.orc_ecdsa_verify_batch_mt
+        t0 = time.perf_counter()
+        f(out, inp["hashes"][:32 * m], inp["sigs"][:66 * m], ctypes.c_size_t(66), inp["keys"], ctypes.c_size_t(33),
+          ctypes.c_void_p(idx.ctypes.data), ctypes.c_size_t(len(inp["keys"]) // 33), ctypes.c_size_t(m), 1,
+          ctypes.c_int32(chain), threads)
+        dt = time.perf_counter() - t0
+        assert out.raw[:m] == inp["expect"][:m].tobytes()
+        return dt
+
+    m = min(n_total, 32 * threads)
+    dt = run(m)
+    m = int(min(n_total, max(m, m * target_s / max(dt, 1e-3))))
+    dt = run(m)
+    return dict(value=m / dt, unit="header signatures/s", cores=threads, kind="port",
+                sample=f"first {m} signatures of the same batch, orc_ecdsa_verify_batch_mt (libsecp256k1 verify "
+                       f"semantics, Straus-Shamir 4-bit windows, 4x64-bit Montgomery; the header Keccak (~1 us) is not "
+                       f"included), {build}, {threads} OpenMP threads, {dt:.1f} s")
+
+
+def run_ecdsa(args, nat, torch, dev, rank, world, cpu):
+    """RootProtocol header-signature checks: lcb_root_header_verify_dev over n headers of one era per rank (Keccak of
+    the header, the Index == era check, VerifySignatureHashed) against a 256-validator key set resident on the GPU."""
+    import torch.distributed as dist
+    lib = nat.lib()
+    n, era, chain = args.ecdsa_sigs, 4242, 225
+    t_gen = time.perf_counter()
+    inp = ecdsa_inputs(nat, rank, n, args.ecdsa_validators, era, chain)
+    t_gen = time.perf_counter() - t_gen
+    t_ks = time.perf_counter()
+    ks = nat.EcdsaKeySet(inp["keys"], 33)
+    t_ks = time.perf_counter() - t_ks
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    d_hdr = to_dev(torch, dev, inp["hdr"])
+    d_sig = to_dev(torch, dev, inp["sigs"])
+    d_idx = torch.from_numpy(inp["idx"]).to(dev)
+    d_acc = torch.zeros(n, dtype=torch.uint8, device=dev)
+
+    def step():
+        if lib.lcb_root_header_verify_dev(d_acc.data_ptr(), d_hdr.data_ptr(), era, d_sig.data_ptr(), 66,
+                                          d_idx.data_ptr(), n, ks.h, 1, chain, sh) != 0:
+            raise RuntimeError(nat.last_error())
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.ecdsa_steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kms = (ctypes.c_float * 3)()
+    if lib.lcb_ecdsa_phase_ms(kms) != 0:
+        raise RuntimeError(nat.last_error())
+    mism = int(np.sum(d_acc.cpu().numpy() != inp["expect"]))
+    t = torch.tensor([elapsed, float(mism)], dtype=torch.float64, device=dev)
+    if world > 1:
+        tm = t.clone()
+        dist.all_reduce(tm[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        elapsed = float(tm[0])
+    ks.close()
+    if rank != 0:
+        return None
+    hash_ms, scal_ms, ver_ms = (float(x) for x in kms)
+    achieved = n * W_ECDSA * MAC_PER_FPMUL_SECP / (ver_ms * 1e-3)
+    res = dict(
+        metric="secp256k1 ECDSA header-signature verifications/sec (RootProtocol SignedHeaderMessage check)",
+        value=n * world * args.ecdsa_steps / elapsed, unit="header signatures/s", signatures_per_rank=n,
+        validators=args.ecdsa_validators, steps=args.ecdsa_steps, ms_per_step=1e3 * elapsed / args.ecdsa_steps,
+        decision_mismatches=int(t[1]), input_gen_s=t_gen, keyset_build_s=t_ks,
+        kernel_ms={"k_secp_header_hash": hash_ms, "k_secp_scalars": scal_ms, "k_secp_verify": ver_ms},
+        roofline={"bound": "valu_int32", "kernel": "k_secp_verify", "achieved": achieved / 1e12,
+                  "peak": PEAK_MAC32 / 1e12, "unit": "Tmac32/s", "frac": achieved / PEAK_MAC32,
+                  "work_per_signature_fpmul": W_ECDSA, "mac_per_fpmul": MAC_PER_FPMUL_SECP},
+        config=f"SURVEY §8f row 4: {n} headers of one era per rank, {args.ecdsa_validators} validators' keys resident "
+               f"with fixed-base comb tables, new chain id {chain}, 1% corrupted; shards by era (no collective)",
+    )
+    if cpu:
+        res["cpu_baseline"] = ecdsa_cpu_baseline(inp, n, chain)
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -763,6 +890,9 @@ def main():
     ap.add_argument("--ts-steps", type=int, default=1)
     ap.add_argument("--replay-n", type=int, default=256, help="epoch-replay network size N (0 = skip)")
     ap.add_argument("--replay-steps", type=int, default=1)
+    ap.add_argument("--ecdsa-sigs", type=int, default=1 << 20, help="header signatures per rank (0 = skip)")
+    ap.add_argument("--ecdsa-validators", type=int, default=256)
+    ap.add_argument("--ecdsa-steps", type=int, default=3)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -846,7 +976,9 @@ def main():
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         elapsed = float(tmax[0])
     mismatches_all, shares_all = int(t[1]), int(t[2])
-    msm = ts = replay = None
+    msm = ts = replay = ecdsa = None
+    if args.ecdsa_sigs > 0:
+        ecdsa = run_ecdsa(args, nat, torch, dev, rank, world, cpu=(world == 1 and not args.no_cpu_baseline))
     if args.replay_n > 0:
         replay = run_replay(args, nat, torch, dev, rank, world)
     if args.ts_rounds > 0:
@@ -899,6 +1031,7 @@ def main():
             "msm": msm,
             "threshold_signature": ts,
             "epoch_replay": replay,
+            "ecdsa_headers": ecdsa,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

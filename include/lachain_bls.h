@@ -292,6 +292,72 @@ int lcb_rs_encode(uint8_t *shards_out, const uint8_t *input, size_t input_len, i
 int lcb_rs_decode(uint8_t *out, const uint8_t *echo_data, const int32_t *from, int n_echos, size_t shard_size,
                   int n_shards, int erasures);
 
+/* ------------------------------------------------------------------ secp256k1 ECDSA header signatures
+   RootProtocol checks every SignedHeaderMessage with
+     DefaultCrypto.VerifySignatureHashed(header.Keccak(), signature, EcdsaPublicKeySet[idx].EncodeCompressed(),
+                                         useNewChainId)            (RootProtocol.cs:91-105, DefaultCrypto.cs:79-101)
+   accept[i] = 1 exactly when the reference returns true: signature i is sig_len bytes (must equal 65 for the old
+   chain id, 66 for the new one, DefaultCrypto.cs:26-29), its recovery id (sig[64], or sig[64] * 256 + sig[65]) gives
+   (enc - 36) / 2 / chain_id in [0, 3] (C# int arithmetic; chain_id 0 rejects everything), r || s (big-endian) parse
+   below n, s <= (n - 1) / 2, and x(u1 G + u2 Q) mod n == r with u1 = z / s, u2 = r / s, z = hash mod n (libsecp256k1
+   semantics; Secp256k1.Net 0.1.55 / Secp256k1.Native 0.1.20, Lachain.Crypto.csproj:21-22).  key_idx[i] selects the
+   key; an index out of range or a key that fails secp256k1_ec_pubkey_parse (33-byte 02/03 or 65-byte 04/06/07
+   encodings) rejects.  `chain_id` is TransactionUtils.ChainId(use_new_chain_id) (TransactionUtils.cs:25-28).
+   A key set keeps the validators' keys resident on the device with a 270 KB fixed-base table per key, built once;
+   the host-pointer calls cache the last key list they saw in the calling thread's context. */
+typedef struct lcb_ecdsa_keyset lcb_ecdsa_keyset;
+/* BlockHeader (block.proto:7-15) as raw bytes; hashed as HashUtils.Keccak(BlockHeader) (HashUtils.cs:40-53) */
+typedef struct {
+    uint64_t index;
+    uint8_t prev_block_hash[32];
+    uint8_t merkle_root[32];
+    uint8_t state_hash[32];
+    uint64_t nonce;
+} lcb_block_header;
+lcb_ecdsa_keyset *lcb_ecdsa_keyset_create(const uint8_t *pubkeys, size_t pk_len, size_t n_keys);
+void lcb_ecdsa_keyset_destroy(lcb_ecdsa_keyset *ks);
+size_t lcb_ecdsa_keyset_size(const lcb_ecdsa_keyset *ks);
+int lcb_ecdsa_keyset_valid(const lcb_ecdsa_keyset *ks, uint8_t *ok_out);   /* per key: parsed (1) or not (0) */
+/* host pointers; hashes: n x 32 bytes (the reference's messageHash) */
+int lcb_ecdsa_verify_hashed_batch(uint8_t *accept, const uint8_t *hashes, const uint8_t *sigs, size_t sig_len,
+                                  const uint8_t *pubkeys, size_t pk_len, size_t n_keys, const int32_t *key_idx,
+                                  size_t n, int use_new_chain_id, int32_t chain_id);
+/* RootProtocol's whole check: header.Index == era (RootProtocol.cs:94-96), Keccak of the header, then the above */
+int lcb_root_header_verify_batch(uint8_t *accept, const lcb_block_header *headers, uint64_t era, const uint8_t *sigs,
+                                 size_t sig_len, const uint8_t *pubkeys, size_t pk_len, size_t n_keys,
+                                 const int32_t *key_idx, size_t n, int use_new_chain_id, int32_t chain_id);
+int lcb_header_keccak_batch(uint8_t *hashes, const lcb_block_header *headers, size_t n);
+/* device pointers, enqueued on `stream` in a context (NULL = the calling thread's default context) */
+int lcb_ctx_ecdsa_verify_hashed_dev(lcb_ctx *ctx, uint8_t *accept, const uint8_t *hashes, const uint8_t *sigs,
+                                    size_t sig_len, const int32_t *key_idx, size_t n, const lcb_ecdsa_keyset *ks,
+                                    int use_new_chain_id, int32_t chain_id, void *stream);
+int lcb_ctx_root_header_verify_dev(lcb_ctx *ctx, uint8_t *accept, const uint8_t *headers, uint64_t era,
+                                   const uint8_t *sigs, size_t sig_len, const int32_t *key_idx, size_t n,
+                                   const lcb_ecdsa_keyset *ks, int use_new_chain_id, int32_t chain_id, void *stream);
+/* signing side (EcdsaKeyPair / DefaultCrypto.SignHashed, DefaultCrypto.cs:107-137) with caller-given nonces (not
+   RFC 6979, so signature bytes differ from libsecp256k1's for the same key and hash; every one verifies): key
+   derivation out33 = compressed d G, and r || s (low s) || v encoded as SignHashed encodes it.  ok[i] = 0 for a
+   private key or nonce outside [1, n) or a zero r / s.  Used for synthetic inputs and the node's own header. */
+int lcb_ecdsa_pubkey_batch(uint8_t *out33, uint8_t *ok, const uint8_t *privs, size_t n);
+int lcb_ecdsa_sign_hashed_batch(uint8_t *sigs_out, uint8_t *ok, const uint8_t *hashes, const uint8_t *privs,
+                                const uint8_t *nonces, size_t n, int use_new_chain_id, int32_t chain_id);
+int lcb_ctx_ecdsa_pubkey_dev(lcb_ctx *ctx, uint8_t *out33, uint8_t *ok, const uint8_t *privs, size_t n, void *stream);
+int lcb_ctx_ecdsa_sign_hashed_dev(lcb_ctx *ctx, uint8_t *sigs_out, uint8_t *ok, const uint8_t *hashes,
+                                  const uint8_t *privs, const uint8_t *nonces, size_t n, int use_new_chain_id,
+                                  int32_t chain_id, void *stream);
+int lcb_ecdsa_pubkey_dev(uint8_t *out33, uint8_t *ok, const uint8_t *privs, size_t n, void *stream);
+int lcb_ecdsa_sign_hashed_dev(uint8_t *sigs_out, uint8_t *ok, const uint8_t *hashes, const uint8_t *privs,
+                              const uint8_t *nonces, size_t n, int use_new_chain_id, int32_t chain_id, void *stream);
+/* kernel milliseconds of the last verification in the context: header hash (0 if hashes were given), scalars, verify */
+int lcb_ctx_ecdsa_phase_ms(lcb_ctx *ctx, float ms[3]);
+int lcb_ecdsa_phase_ms(float ms[3]);
+int lcb_ecdsa_verify_hashed_dev(uint8_t *accept, const uint8_t *hashes, const uint8_t *sigs, size_t sig_len,
+                                const int32_t *key_idx, size_t n, const lcb_ecdsa_keyset *ks, int use_new_chain_id,
+                                int32_t chain_id, void *stream);
+int lcb_root_header_verify_dev(uint8_t *accept, const uint8_t *headers, uint64_t era, const uint8_t *sigs,
+                               size_t sig_len, const int32_t *key_idx, size_t n, const lcb_ecdsa_keyset *ks,
+                               int use_new_chain_id, int32_t chain_id, void *stream);
+
 /* ------------------------------------------------------------------ aggregation queue (one share per call)
    The consensus code verifies one share per call from many protocol threads (HoneyBadger.cs:156-158,211-212,
    ThresholdSigner.cs:62, AbstractProtocol.cs:46-47).  A queue aggregates such calls into GPU batches: submit

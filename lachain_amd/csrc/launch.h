@@ -45,6 +45,17 @@ extern "C" void lcbk_g1a_to_jac(dim3 grid, hipStream_t s, const void *in, u32 n,
 extern "C" const void *lcbk_rs_matrix_kernel();
 extern "C" void lcbk_rs_matrix(hipStream_t s, const int *pe, int m, const int *pk, int k, int n, uint8_t *M, uint8_t *ok);
 extern "C" void lcbk_rs_apply(hipStream_t s, const uint8_t *M, const uint8_t *ok, int m, int k, const uint8_t *src, size_t S, const int *pe, uint8_t *dst);
+extern "C" size_t lcbk_secp_job_bytes(void);
+extern "C" size_t lcbk_secp_table_bytes(void);
+extern "C" size_t lcbk_secp_aff_bytes(void);
+extern "C" void lcbk_secp_key_parse(hipStream_t s, const uint8_t *pks, u32 pk_len, u32 n_keys, void *out, u32 *ok);
+extern "C" void lcbk_secp_comb_build(hipStream_t s, const void *base, const u32 *base_ok, u32 n_tables, void *tables, void *tmp);
+extern "C" void lcbk_secp_header_hash(hipStream_t s, const uint8_t *hdr, u32 n, uint64_t era, uint8_t *hash, uint8_t *pre_ok);
+extern "C" void lcbk_secp_scalars(hipStream_t s, const uint8_t *hashes, const uint8_t *sigs, u32 sig_len, u32 want_len, int chain_id, const int32_t *key_idx, u32 n_keys, const u32 *key_ok, const uint8_t *pre_ok, u32 n, void *jobs);
+extern "C" void lcbk_secp_verify(hipStream_t s, const void *jobs, u32 n, const void *g_table, const void *key_tables, uint8_t *out);
+extern "C" void lcbk_secp_gen(hipStream_t s, void *out, u32 *ok);
+extern "C" void lcbk_secp_pubkey(hipStream_t s, const uint8_t *privs, u32 n, const void *g_table, uint8_t *out33, uint8_t *ok);
+extern "C" void lcbk_secp_sign(hipStream_t s, const uint8_t *hashes, const uint8_t *privs, const uint8_t *nonces, u32 n, const void *g_table, int chain_id, int use_new, uint8_t *out, uint8_t *ok);
 extern "C" void lcbk_op(dim3 grid, hipStream_t s, int op, u32 *io, int orig_cof);
 
 // sizes of the device records the host allocates

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <mutex>
+#include <vector>
 
 struct DevBuf {
     void *p = nullptr;
@@ -52,4 +53,25 @@ struct lcb_ctx {
     bool ver_ev_ready = false, ver_ran = false;
     hipEvent_t msm_ev[7] = {};
     bool msm_ev_ready = false, msm_ran = false;
+    // secp256k1 ECDSA (lcb_ecdsa.cpp): job records / header hashes / staging, and the host API's cached key set
+    DevBuf ec[6];
+    hipEvent_t ec_ev[4] = {};         // around header hash / scalars / verify of the last verification
+    bool ec_ev_ready = false, ec_ran = false, ec_hashed = false;
+    struct lcb_ecdsa_keyset *ec_cache = nullptr;
+    std::vector<uint8_t> ec_cache_keys;
+    size_t ec_cache_pk_len = 0;
+};
+
+// Enqueue scope: exclusive use of the context, stream ordered after the context's previous work, and the
+// context's order event recorded after this call's work.
+struct Enq {
+    lcb_ctx *c;
+    hipStream_t s;
+    std::unique_lock<std::recursive_mutex> lk;
+    Enq(lcb_ctx *c_, hipStream_t s_) : c(c_), s(s_), lk(c_->mu) {
+        if (c->order_valid) (void)hipStreamWaitEvent(s, c->order, 0);
+    }
+    ~Enq() {
+        if (hipEventRecord(c->order, s) == hipSuccess) c->order_valid = true;
+    }
 };

@@ -29,6 +29,7 @@
 #include "../../include/lachain_bls.h"
 #include "host_sha3.hpp"
 #include "lcb_ctx.hpp"
+#include "lcb_internal.hpp"
 
 #define LCB_BLOCK 256
 
@@ -530,6 +531,7 @@ void ctx_free(lcb_ctx *c) {
     for (auto &b : c->in) b.release();
     for (auto &b : c->out) b.release();
     for (auto &b : c->dkg) b.release();
+    lcb_int::ecdsa_ctx_release(c);
     if (c->ver_ev_ready) for (auto &e : c->ver_ev) (void)hipEventDestroy(e);
     if (c->msm_ev_ready) for (auto &e : c->msm_ev) (void)hipEventDestroy(e);
     if (c->order) (void)hipEventDestroy(c->order);
@@ -566,20 +568,6 @@ lcb_ctx *sync_ctx() {
     if (!t_sync_ctx.c) t_sync_ctx.c = ctx_new();
     return t_sync_ctx.c;
 }
-
-// Enqueue scope: exclusive use of the context, stream ordered after the context's previous work, and the
-// context's order event recorded after this call's work.
-struct Enq {
-    lcb_ctx *c;
-    hipStream_t s;
-    std::unique_lock<std::recursive_mutex> lk;
-    Enq(lcb_ctx *c_, hipStream_t s_) : c(c_), s(s_), lk(c_->mu) {
-        if (c->order_valid) (void)hipStreamWaitEvent(s, c->order, 0);
-    }
-    ~Enq() {
-        if (hipEventRecord(c->order, s) == hipSuccess) c->order_valid = true;
-    }
-};
 
 #define CTX_OR(var, ctxarg, ret)                 \
     lcb_ctx *var = resolve(ctxarg);              \
@@ -1463,3 +1451,13 @@ extern "C" int lcb_g1_msm(uint8_t out[48], const uint8_t *points, const uint8_t 
 extern "C" void lcb_xor_with_hash(uint8_t *out, const uint8_t g1b[48], const uint8_t *data, size_t len) {
     lcb_host::xor_with_hash(out, g1b, data, len);
 }
+
+// ================================================================== internal interface for the other host files
+namespace lcb_int {
+void set_error(const char *what, hipError_t e) { set_err(what, e); }
+lcb_ctx *ctx_resolve(lcb_ctx *c) { return resolve(c); }
+lcb_ctx *ctx_sync() { return sync_ctx(); }
+bool launch_ok(const char *what) { return launched(what); }
+bool sync_ok(lcb_ctx *c, const char *what) { return sync_check(c, what); }
+int device() { return g_device; }
+}  // namespace lcb_int

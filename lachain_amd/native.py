@@ -118,6 +118,31 @@ _SIGS = {
     "lcb_queue_flush": (ctypes.c_int, [ctypes.c_void_p]),
     "lcb_queue_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "lcb_queue_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
+    "lcb_ecdsa_keyset_create": (ctypes.c_void_p, [c_u8p, c_size, c_size]),
+    "lcb_ecdsa_keyset_destroy": (None, [ctypes.c_void_p]),
+    "lcb_ecdsa_keyset_size": (c_size, [ctypes.c_void_p]),
+    "lcb_ecdsa_keyset_valid": (ctypes.c_int, [ctypes.c_void_p, c_u8p]),
+    "lcb_ecdsa_verify_hashed_batch": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_size, c_u8p, c_size, c_size,
+                                                     ctypes.POINTER(ctypes.c_int32), c_size, ctypes.c_int,
+                                                     ctypes.c_int32]),
+    "lcb_root_header_verify_batch": (ctypes.c_int, [c_u8p, c_u8p, ctypes.c_uint64, c_u8p, c_size, c_u8p, c_size,
+                                                    c_size, ctypes.POINTER(ctypes.c_int32), c_size, ctypes.c_int,
+                                                    ctypes.c_int32]),
+    "lcb_header_keccak_batch": (ctypes.c_int, [c_u8p, c_u8p, c_size]),
+    "lcb_ecdsa_verify_hashed_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_size,
+                                                   ctypes.c_void_p, c_size, ctypes.c_void_p, ctypes.c_int,
+                                                   ctypes.c_int32, ctypes.c_void_p]),
+    "lcb_root_header_verify_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                  c_size, ctypes.c_void_p, c_size, ctypes.c_void_p, ctypes.c_int,
+                                                  ctypes.c_int32, ctypes.c_void_p]),
+    "lcb_ecdsa_phase_ms": (ctypes.c_int, [ctypes.POINTER(ctypes.c_float)]),
+    "lcb_ecdsa_pubkey_batch": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_size]),
+    "lcb_ecdsa_sign_hashed_batch": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_u8p, c_size, ctypes.c_int,
+                                                   ctypes.c_int32]),
+    "lcb_ecdsa_pubkey_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_size, ctypes.c_void_p]),
+    "lcb_ecdsa_sign_hashed_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_void_p, c_size, ctypes.c_int, ctypes.c_int32,
+                                                 ctypes.c_void_p]),
     "lcb_ctx_create": (ctypes.c_void_p, []),
     "lcb_ctx_destroy": (None, [ctypes.c_void_p]),
     "lcb_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
@@ -125,7 +150,8 @@ _SIGS = {
 # explicit-context forms: the context pointer first, then the same arguments as the context-less form
 for _name in ("tpke_prepare_dev", "tpke_verify_prepared_dev", "tpke_partial_decrypt_prepared_dev", "tpke_combine_dev",
               "tpke_verify_phase_ms", "ts_prepare_dev", "ts_verify_prepared_dev", "ts_assemble_dev", "g1_lagrange_dev",
-              "g2_lagrange_dev", "g1_msm_dev", "g1_msm_phase_ms"):
+              "g2_lagrange_dev", "g1_msm_dev", "g1_msm_phase_ms", "ecdsa_verify_hashed_dev",
+              "root_header_verify_dev", "ecdsa_pubkey_dev", "ecdsa_sign_hashed_dev", "ecdsa_phase_ms"):
     _res, _args = _SIGS["lcb_" + _name]
     _SIGS["lcb_ctx_" + _name] = (_res, [ctypes.c_void_p] + list(_args))
 
@@ -439,6 +465,107 @@ def rs_decode(echos, shard_size: int, n_shards: int, erasures: int) -> bytes:
     ob, po = _out(shard_size * n_shards)
     _check(lib().lcb_rs_decode(po, pd, pf, len(echos), shard_size, n_shards, erasures), "rs_decode")
     return bytes(ob)[: shard_size * n_shards]
+
+
+# ---------------------------------------------------------------- secp256k1 ECDSA header signatures (§8f row 4)
+def header_bytes(index: int, prev: bytes, merkle: bytes, state: bytes, nonce: int) -> bytes:
+    """lcb_block_header record (112 B): u64 index | prev_block_hash | merkle_root | state_hash | u64 nonce"""
+    assert len(prev) == len(merkle) == len(state) == 32
+    return index.to_bytes(8, "little") + prev + merkle + state + nonce.to_bytes(8, "little")
+
+
+def header_keccak_batch(headers: bytes) -> bytes:
+    """HashUtils.Keccak(BlockHeader) of each 112-byte record"""
+    n = len(headers) // 112
+    keep = []
+    _, ph = _bytes_ptr_keep(keep, headers)
+    ob, po = _out(32 * n)
+    _check(lib().lcb_header_keccak_batch(po, ph, n), "header_keccak_batch")
+    return bytes(ob)[: 32 * n]
+
+
+def ecdsa_verify_hashed_batch(hashes: bytes, sigs: bytes, sig_len: int, pubkeys: bytes, pk_len: int, key_idx,
+                              use_new_chain_id: bool, chain_id: int) -> bytes:
+    """DefaultCrypto.VerifySignatureHashed over a batch: one accept byte per signature"""
+    n = len(hashes) // 32
+    keep = []
+    _, ph = _bytes_ptr_keep(keep, hashes)
+    _, ps = _bytes_ptr_keep(keep, sigs)
+    _, pk = _bytes_ptr_keep(keep, pubkeys)
+    pi = _i32_keep(keep, key_idx)
+    ob, po = _out(n)
+    _check(lib().lcb_ecdsa_verify_hashed_batch(po, ph, ps, sig_len, pk, pk_len, len(pubkeys) // pk_len, pi, n,
+                                               int(bool(use_new_chain_id)), chain_id), "ecdsa_verify_hashed_batch")
+    return bytes(ob)[:n]
+
+
+def root_header_verify_batch(headers: bytes, era: int, sigs: bytes, sig_len: int, pubkeys: bytes, pk_len: int, key_idx,
+                             use_new_chain_id: bool, chain_id: int) -> bytes:
+    """RootProtocol's SignedHeaderMessage check (index == era, header Keccak, VerifySignatureHashed)"""
+    n = len(headers) // 112
+    keep = []
+    _, ph = _bytes_ptr_keep(keep, headers)
+    _, ps = _bytes_ptr_keep(keep, sigs)
+    _, pk = _bytes_ptr_keep(keep, pubkeys)
+    pi = _i32_keep(keep, key_idx)
+    ob, po = _out(n)
+    _check(lib().lcb_root_header_verify_batch(po, ph, era, ps, sig_len, pk, pk_len, len(pubkeys) // pk_len, pi, n,
+                                              int(bool(use_new_chain_id)), chain_id), "root_header_verify_batch")
+    return bytes(ob)[:n]
+
+
+def ecdsa_pubkey_batch(privs: bytes):
+    """(compressed keys, ok) for 32-byte big-endian private keys"""
+    n = len(privs) // 32
+    keep = []
+    _, pp = _bytes_ptr_keep(keep, privs)
+    ob, po = _out(33 * n)
+    okb, pok = _out(n)
+    _check(lib().lcb_ecdsa_pubkey_batch(po, pok, pp, n), "ecdsa_pubkey_batch")
+    return bytes(ob)[: 33 * n], bytes(okb)[:n]
+
+
+def ecdsa_sign_hashed_batch(hashes: bytes, privs: bytes, nonces: bytes, use_new_chain_id: bool, chain_id: int):
+    """(signatures, ok): r || s || v per DefaultCrypto.SignHashed's encoding, with the given nonces"""
+    n = len(hashes) // 32
+    L = 66 if use_new_chain_id else 65
+    keep = []
+    _, ph = _bytes_ptr_keep(keep, hashes)
+    _, pp = _bytes_ptr_keep(keep, privs)
+    _, pn = _bytes_ptr_keep(keep, nonces)
+    ob, po = _out(L * n)
+    okb, pok = _out(n)
+    _check(lib().lcb_ecdsa_sign_hashed_batch(po, pok, ph, pp, pn, n, int(bool(use_new_chain_id)), chain_id),
+           "ecdsa_sign_hashed_batch")
+    return bytes(ob)[: L * n], bytes(okb)[:n]
+
+
+class EcdsaKeySet:
+    """lcb_ecdsa_keyset: validator keys resident on the device with their comb tables"""
+
+    def __init__(self, pubkeys: bytes, pk_len: int):
+        keep = []
+        _, pk = _bytes_ptr_keep(keep, pubkeys)
+        self.n = len(pubkeys) // pk_len
+        self.h = lib().lcb_ecdsa_keyset_create(pk, pk_len, self.n)
+        if not self.h:
+            raise RuntimeError("lcb_ecdsa_keyset_create: " + lib().lcb_last_error().decode())
+
+    def valid(self) -> bytes:
+        ob, po = _out(self.n)
+        _check(lib().lcb_ecdsa_keyset_valid(self.h, po), "keyset_valid")
+        return bytes(ob)[: self.n]
+
+    def close(self):
+        if self.h:
+            lib().lcb_ecdsa_keyset_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def coin_parity(sig: bytes) -> bool:

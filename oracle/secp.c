@@ -323,11 +323,12 @@ int orc_ecdsa_verify_hashed(const uint8_t *hash32, size_t hash_len, const uint8_
 }
 
 /* batch of the above over a key table (the C leg of the CPU baseline); out[i] in {0, 1} */
-void orc_ecdsa_verify_batch(uint8_t *out, const uint8_t *hashes, const uint8_t *sigs, size_t sig_len,
-                            const uint8_t *pks, size_t pk_len, const int32_t *pk_idx, size_t n_pks, size_t n,
-                            int use_new_chain_id, int32_t chain_id) {
+void orc_ecdsa_verify_batch_mt(uint8_t *out, const uint8_t *hashes, const uint8_t *sigs, size_t sig_len,
+                               const uint8_t *pks, size_t pk_len, const int32_t *pk_idx, size_t n_pks, size_t n,
+                               int use_new_chain_id, int32_t chain_id, int threads) {
     init();
-#pragma omp parallel for schedule(dynamic, 16)
+    if (threads <= 0) threads = 1;
+#pragma omp parallel for schedule(dynamic, 16) num_threads(threads)
     for (long i = 0; i < (long)n; i++) {
         int32_t k = pk_idx[i];
         out[i] = (k >= 0 && (size_t)k < n_pks)
@@ -335,6 +336,12 @@ void orc_ecdsa_verify_batch(uint8_t *out, const uint8_t *hashes, const uint8_t *
                                                          pks + pk_len * (size_t)k, pk_len, use_new_chain_id, chain_id)
                      : 0;
     }
+}
+
+void orc_ecdsa_verify_batch(uint8_t *out, const uint8_t *hashes, const uint8_t *sigs, size_t sig_len,
+                            const uint8_t *pks, size_t pk_len, const int32_t *pk_idx, size_t n_pks, size_t n,
+                            int use_new_chain_id, int32_t chain_id) {
+    orc_ecdsa_verify_batch_mt(out, hashes, sigs, sig_len, pks, pk_len, pk_idx, n_pks, n, use_new_chain_id, chain_id, 8);
 }
 
 /* ---------------------------------------------------------------- test-vector helpers (signing side) */

@@ -13,3 +13,18 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
+
+
+import pytest  # noqa: E402
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _torch_hip_first(request):
+    """GPU sessions: initialise torch's HIP runtime before liblachain_bls.so initialises its own.  torch's wheel
+    bundles a HIP runtime; when the library's (system ROCm) runtime comes up first, torch's later lazy init can report
+    no devices.  bench.py orders it the same way."""
+    if any(item.get_closest_marker("gpu") for item in request.session.items):
+        import torch
+        if torch.cuda.is_available():
+            torch.zeros(1, device="cuda:0")
+    yield
