@@ -265,14 +265,19 @@ def run_msm(args, nat, torch, dev, rank, world, cpu, n):
     if lib.lcb_g1_to_affine_dev(d_aff.data_ptr(), d_ok.data_ptr(), d_pts48.data_ptr(), n, sh) != 0:
         raise RuntimeError(nat.last_error())
     del d_pts48
-    c = lib.lcb_g1_msm_window(n)
+    # configs[3]'s points are a_i G (order r), so the GLV entry point applies; it keeps the plain form where that is
+    # faster (large n) and reports that as a negative width
+    msm_fn = lib.lcb_g1_msm_dev if args.msm_no_glv else lib.lcb_g1_msm_glv_dev
+    c = lib.lcb_g1_msm_window(n) if args.msm_no_glv else lib.lcb_g1_msm_glv_window(n)
+    glv = c > 0 and not args.msm_no_glv
+    c = abs(c)
 
     def sum_partials(allp, w):
         if lib.lcb_g1_jac_sum_dev(d_out.data_ptr(), None, allp.data_ptr(), w, sh) != 0:
             raise RuntimeError(nat.last_error())
 
     def step():
-        if lib.lcb_g1_msm_dev(d_jac.data_ptr(), d_aff.data_ptr(), d_sc.data_ptr(), n, 0, sh) != 0:
+        if msm_fn(d_jac.data_ptr(), d_aff.data_ptr(), d_sc.data_ptr(), n, 0, sh) != 0:
             raise RuntimeError(nat.last_error())
         # RCCL over xGMI: all-gather of the 144 B Jacobian partials, summed on the GPU (lachain_amd/shard.py)
         shard.msm_combine(dist, d_jac, world, sum_partials)
@@ -310,14 +315,16 @@ def run_msm(args, nat, torch, dev, rank, world, cpu, n):
     import oracle as o
     got = bytes(d_out.cpu().numpy().tobytes())
     correct = ok_pts and got == o.g1_mul(o.g1_gen(), o.fr(exp_total))
-    nwin = 255 // c + 1
+    bits, npts = (128, 2 * n) if glv else (255, n)
+    nwin = (128 + c - 1) // c if glv else 255 // c + 1
     t_acc = phases["bucket_acc"] * 1e-3
-    fpmul_acc = n * nwin * 11          # mixed adds, one per nonzero digit (zero digits: 2^-c of them)
-    fpmul_total = nwin * (n * 11 + (1 << (c - 1)) * 2 * 16)
-    bytes_acc = n * nwin * (96 + 4) + nwin * (1 << (c - 1)) * (8 + 144)
+    fpmul_acc = npts * (bits / c) * 11     # mixed adds, one per nonzero digit (zero digits: 2^-c of them)
+    fpmul_total = nwin * (npts * 11 + (1 << (c - 1)) * 2 * 16)
+    bytes_acc = npts * (bits / c) * (96 + 4) + nwin * (1 << (c - 1)) * (8 + 144)
     res = dict(
         metric="BLS12-381 G1 MSM points/sec (Pippenger, sum_i s_i P_i)", value=n * world * args.msm_steps / elapsed,
         unit="points/s", points_per_rank=n, window_bits=c, windows=nwin, steps=args.msm_steps,
+        form="GLV: s = s1 + s2 lambda over P and phi(P) (points of order r)" if glv else "plain 255-bit digits",
         ms_per_step=1e3 * elapsed / args.msm_steps, known_answer_ok=correct,
         phase_ms={k: round(v, 3) for k, v in phases.items()},
         roofline={"bound": "valu_int32", "kernel": "k_msm_bucket_acc",
@@ -885,6 +892,7 @@ def main():
     ap.add_argument("--msm-sizes", default=f"{1 << 20},{1 << 24}",
                     help="total G1 MSM points per measurement, sharded over ranks (empty = skip)")
     ap.add_argument("--msm-steps", type=int, default=3)
+    ap.add_argument("--msm-no-glv", action="store_true", help="plain 255-bit Pippenger instead of the GLV form")
     ap.add_argument("--ts-rounds", type=int, default=65536, help="CommonCoin rounds per rank (0 = skip)")
     ap.add_argument("--ts-n", type=int, default=100)
     ap.add_argument("--ts-steps", type=int, default=1)

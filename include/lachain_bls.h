@@ -420,6 +420,16 @@ int lcb_g1_msm(uint8_t out[48], const uint8_t *points, const uint8_t *scalars, s
 int lcb_g1_msm_dev(void *out_jac, const void *points_aff, const uint8_t *scalars, size_t n, int window_bits,
                    void *stream);
 int lcb_g1_msm_window(size_t n);
+/* GLV form of the same MSM for points of order r (e.g. generated as a_i G, or checked with a subgroup test):
+   s_i = s1 + s2 lambda (lambda = z^2 - 1, s1 < 2^129, s2 < 2^128) over the 2n points P_i, phi(P_i) = (beta x, y):
+   half the windows, so half the serial window combination and bucket reduction.  For a point with a component
+   outside the r-subgroup phi(P) != lambda P and the result differs from lcb_g1_msm_dev's (which is exact for any
+   point), so wire-supplied points (e.g. LagrangeInterpolate over shares) must use lcb_g1_msm_dev. */
+int lcb_g1_msm_glv_dev(void *out_jac, const void *points_aff, const uint8_t *scalars, size_t n, int window_bits,
+                       void *stream);
+int lcb_ctx_g1_msm_glv_dev(lcb_ctx *ctx, void *out_jac, const void *points_aff, const uint8_t *scalars, size_t n,
+                           int window_bits, void *stream);
+int lcb_g1_msm_glv_window(size_t n);
 /* per-phase device time (ms) of the last MSM: digits, sort, bucket bounds, bucket accumulation, bucket
    reduction, window combination (waits for the last MSM to finish) */
 int lcb_g1_msm_phase_ms(float *ms, int n_phases);

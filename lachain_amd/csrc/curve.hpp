@@ -195,9 +195,16 @@ template <class F> DI void jac_mul_aff(jac<F> &r, const aff<F> &p, const u32 *k,
     }
     r = acc;
 }
+// k p for a small public k: doublings only from k's top bit (the bucket-reduce offsets are < 2^c)
 template <class F> DI void jac_mul_u64(jac<F> &r, const jac<F> &p, u64 k) {
-    u32 kk[2] = {(u32)k, (u32)(k >> 32)};
-    jac_mul_bits(r, p, kk, 64);
+    if (k == 0) { jac_set_inf(r); return; }
+    int top = 63 - __clzll(k);
+    jac<F> acc = p;
+    for (int i = top - 1; i >= 0; i--) {
+        grp_dbl(acc, acc);
+        if ((k >> i) & 1) grp_add(acc, acc, p);
+    }
+    r = acc;
 }
 
 // ---------------------------------------------------------------- G2 endomorphism psi (M-type twist)

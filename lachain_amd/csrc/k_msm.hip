@@ -65,6 +65,87 @@ extern "C" __global__ void LCB_BOUNDS k_msm_digits(const uint8_t *scalars, u32 n
     }
 }
 
+// GLV form (points of order r only): s = s1 + s2 lambda with lambda = u^2 - 1 = z^2 - 1 (u = |z|).  From two base-u
+// digits and the quotient, s = a1 u^2 + a0 = a1 lambda + (a0 + a1); s1 = (a0 + a1) mod lambda (at most two
+// subtractions), s2 = a1 + (number subtracted): both < lambda + 2 < 2^128.  Point i carries s1 and point n + i
+// (= phi(P_i) = (beta x, y) = lambda P_i) carries s2; records are window-major over the 2n points.  The scalars
+// are 128-bit, so windows 0 .. nwin-2 use signed digits and the top window takes its value plus the incoming carry
+// unsigned (no carry out of bit 128): its digits reach 2^tw (tw <= c), i.e. up to 2 half buckets, keyed as key
+// windows nwin - 1 and nwin (the reduction adds half to the latter's offsets and the combination folds them).
+DI void push_digits_glv(const u32 *sv, u32 idx, u32 c, u32 nwin, size_t stride, u32 *keys, u32 *vals) {
+    const u32 half = 1u << (c - 1), mask = (1u << c) - 1, sentinel = (nwin + 1) << (c - 1);
+    u32 carry = 0;
+    for (u32 w = 0; w < nwin; w++) {
+        u32 bit = w * c, lo = bit >> 5, sh = bit & 31;
+        u32 w0 = 0, w1 = 0;
+#pragma unroll
+        for (u32 j = 0; j < 4; j++) {
+            w0 = (j == lo) ? sv[j] : w0;
+            w1 = (j == lo + 1) ? sv[j] : w1;
+        }
+        u64 word = (u64)w0 | ((u64)w1 << 32);
+        u32 d = ((u32)(word >> sh) & mask) + carry;
+        u32 v = idx;
+        if (w + 1 < nwin && d > half) { d = (1u << c) - d; carry = 1; v |= 0x80000000u; }
+        else carry = 0;
+        keys[(size_t)w * stride + idx] = d ? (w << (c - 1)) + (d - 1) : sentinel;
+        vals[(size_t)w * stride + idx] = v;
+    }
+}
+extern "C" __global__ void LCB_BOUNDS k_msm_digits_glv(const uint8_t *scalars, u32 n, u32 c, u32 nwin, u32 *keys,
+                                                      u32 *vals) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fr s;
+    const uint4 *sw = (const uint4 *)(scalars + 32 * (size_t)i);
+    uint4 a = sw[0], b = sw[1];
+    s.v[0] = a.x; s.v[1] = a.y; s.v[2] = a.z; s.v[3] = a.w;
+    s.v[4] = b.x; s.v[5] = b.y; s.v[6] = b.z; s.v[7] = b.w;
+    fr_raw_reduce(s);
+    u32 q[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) q[j] = s.v[j];
+    u64 d0, d1;
+    u256_divmod_u(q, d0);
+    u256_divmod_u(q, d1);                                  // q = a1 < r / u^2 < 2^128
+    const u64 u = LCB_Z_ABS;
+    u64 m_lo = u * d1, m_hi = __umul64hi(u, d1);
+    u64 a0_lo = m_lo + d0, a0_hi = m_hi + (a0_lo < d0 ? 1 : 0);
+    u64 a1_lo = (u64)q[0] | ((u64)q[1] << 32), a1_hi = (u64)q[2] | ((u64)q[3] << 32);
+    u64 t_lo = a0_lo + a1_lo;
+    u64 cy = t_lo < a0_lo ? 1 : 0;
+    u64 t_hi = a0_hi + a1_hi + cy;
+    u64 t_top = (t_hi < a0_hi || (cy && t_hi == a0_hi)) ? 1 : 0;
+    // lambda = u^2 - 1 as a 128-bit value
+    const u64 l_lo = u * u - 1, l_hi = __umul64hi(u, u) - ((u * u) == 0 ? 1 : 0);
+#pragma unroll
+    for (int k = 0; k < 2; k++) {                          // t >= lambda: t -= lambda, a1 += 1
+        bool ge = t_top || t_hi > l_hi || (t_hi == l_hi && t_lo >= l_lo);
+        u64 nlo = t_lo - l_lo, b0 = t_lo < l_lo ? 1 : 0;
+        u64 nhi = t_hi - l_hi - b0;
+        u64 ntop = t_top - ((t_hi < l_hi || (t_hi == l_hi && b0)) ? 1 : 0);
+        if (ge) {
+            t_lo = nlo; t_hi = nhi; t_top = ntop;
+            a1_lo += 1;
+            if (a1_lo == 0) a1_hi += 1;
+        }
+    }
+    u32 s1[4] = {(u32)t_lo, (u32)(t_lo >> 32), (u32)t_hi, (u32)(t_hi >> 32)};
+    u32 s2[4] = {(u32)a1_lo, (u32)(a1_lo >> 32), (u32)a1_hi, (u32)(a1_hi >> 32)};
+    push_digits_glv(s1, i, c, nwin, 2 * (size_t)n, keys, vals);
+    push_digits_glv(s2, n + i, c, nwin, 2 * (size_t)n, keys, vals);
+}
+// phi(P) = (beta x, y) for the GLV form ((0, 0), the point at infinity, maps to itself)
+extern "C" __global__ void LCB_BOUNDS k_msm_phi(const fp *pts, u32 n, fp *out) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fp beta, x = pts[2 * (size_t)i], y = pts[2 * (size_t)i + 1];
+    fp_load_const(beta, LCB_G1_BETA);
+    fp_mul(x, x, beta);
+    out[2 * (size_t)i] = x;
+    out[2 * (size_t)i + 1] = y;
+}
+
 extern "C" __global__ void LCB_BOUNDS k_msm_bounds(const u32 *keys, u32 m, u32 sentinel, u32 *start, u32 *end) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
@@ -84,17 +165,30 @@ DI void load_aff(fp &x, fp &y, const fp *pts, u32 idx) {
     for (int j = 0; j < 12; j++) { x.v[j] = w[j]; y.v[j] = w[12 + j]; }
 }
 
-extern "C" __global__ void LCB_BOUNDS k_msm_bucket_acc(const fp *pts, const u32 *vals, const u32 *start,
-                                                      const u32 *end, u32 nb, g1 *buckets) {
+// point index v < n_pts reads pts, v >= n_pts reads pts2 (the phi(P) half of the GLV form).  The next record's
+// point is loaded while the current addition runs (one gather in flight per lane).
+extern "C" __global__ void LCB_BOUNDS k_msm_bucket_acc(const fp *pts, const fp *pts2, u32 n_pts, const u32 *vals,
+                                                      const u32 *start, const u32 *end, u32 nb, g1 *buckets) {
     u32 b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
     g1 acc;
     jac_set_inf(acc);
-    u32 e1 = end[b];
-    for (u32 e = start[b]; e < e1; e++) {
-        u32 v = vals[e];
-        fp x, y;
-        load_aff(x, y, pts, v & 0x7fffffffu);
+    u32 e = start[b], e1 = end[b];
+    fp nx, ny;
+    u32 nv = 0;
+    if (e < e1) {
+        nv = vals[e];
+        u32 idx = nv & 0x7fffffffu;
+        load_aff(nx, ny, idx < n_pts ? pts : pts2, idx < n_pts ? idx : idx - n_pts);
+    }
+    for (; e < e1; e++) {
+        fp x = nx, y = ny;
+        u32 v = nv;
+        if (e + 1 < e1) {
+            nv = vals[e + 1];
+            u32 idx = nv & 0x7fffffffu;
+            load_aff(nx, ny, idx < n_pts ? pts : pts2, idx < n_pts ? idx : idx - n_pts);
+        }
         if (fp_is_zero(x) && fp_is_zero(y)) continue;  // point at infinity
         if (v >> 31) fp_neg(y, y);
         jac_add_aff(acc, acc, x, y);
@@ -103,11 +197,15 @@ extern "C" __global__ void LCB_BOUNDS k_msm_bucket_acc(const fp *pts, const u32 
 }
 
 // segment q of window w covers buckets a = q*L .. a+L-1 (digit values a+1 .. a+L)
-extern "C" __global__ void LCB_BOUNDS k_msm_bucket_reduce(const g1 *buckets, u32 half, u32 L, u32 n_seg, g1 *seg_out) {
+// hi_win: the key window that holds the upper half of the GLV top window's digits (digit = half + a + j + 1), or
+// ~0u when there is none
+extern "C" __global__ void LCB_BOUNDS k_msm_bucket_reduce(const g1 *buckets, u32 half, u32 L, u32 n_seg, u32 hi_win,
+                                                         g1 *seg_out) {
     u32 s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n_seg) return;
     u32 per_win = half / L, w = s / per_win, a = (s % per_win) * L;
     const g1 *B = buckets + (size_t)w * half + a;
+    if (w == hi_win) a += half;
     g1 run, acc;
     jac_set_inf(run);
     jac_set_inf(acc);
@@ -156,9 +254,11 @@ extern "C" __global__ void LCB_BOUNDS k_g1_jac_reduce_block(const g1 *in, u32 n_
     if (t == 0) out[b] = sh[0];
 }
 
-extern "C" __global__ void LCB_BOUNDS k_msm_horner(const g1 *win, u32 nwin, u32 c, g1 *out) {
+// fold_top: win[nwin] has the same weight as win[nwin - 1] (the GLV top window's upper digit half)
+extern "C" __global__ void LCB_BOUNDS k_msm_horner(const g1 *win, u32 nwin, u32 c, u32 fold_top, g1 *out) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     g1 acc = win[nwin - 1];
+    if (fold_top) grp_add(acc, acc, win[nwin]);
     for (u32 w = nwin - 1; w-- > 0;) {
         for (u32 t = 0; t < c; t++) grp_dbl(acc, acc);
         grp_add(acc, acc, win[w]);
@@ -191,11 +291,17 @@ extern "C" void lcbk_msm_digits(dim3 grid, hipStream_t s, const uint8_t *scalars
 extern "C" void lcbk_msm_bounds(dim3 grid, hipStream_t s, const u32 *keys, u32 m, u32 sentinel, u32 *start, u32 *end) {
     LCB_LAUNCH(k_msm_bounds, keys, m, sentinel, start, end);
 }
-extern "C" void lcbk_msm_bucket_acc(dim3 grid, hipStream_t s, const void *pts, const u32 *vals, const u32 *start, const u32 *end, u32 nb, void *buckets) {
-    LCB_LAUNCH(k_msm_bucket_acc, (const fp *)pts, vals, start, end, nb, (g1 *)buckets);
+extern "C" void lcbk_msm_bucket_acc(dim3 grid, hipStream_t s, const void *pts, const void *pts2, u32 n_pts, const u32 *vals, const u32 *start, const u32 *end, u32 nb, void *buckets) {
+    LCB_LAUNCH(k_msm_bucket_acc, (const fp *)pts, (const fp *)pts2, n_pts, vals, start, end, nb, (g1 *)buckets);
 }
-extern "C" void lcbk_msm_bucket_reduce(dim3 grid, hipStream_t s, const void *buckets, u32 half, u32 L, u32 n_seg, void *seg_out) {
-    LCB_LAUNCH(k_msm_bucket_reduce, (const g1 *)buckets, half, L, n_seg, (g1 *)seg_out);
+extern "C" void lcbk_msm_digits_glv(dim3 grid, hipStream_t s, const uint8_t *scalars, u32 n, u32 c, u32 nwin, u32 *keys, u32 *vals) {
+    LCB_LAUNCH(k_msm_digits_glv, scalars, n, c, nwin, keys, vals);
+}
+extern "C" void lcbk_msm_phi(dim3 grid, hipStream_t s, const void *pts, u32 n, void *out) {
+    LCB_LAUNCH(k_msm_phi, (const fp *)pts, n, (fp *)out);
+}
+extern "C" void lcbk_msm_bucket_reduce(dim3 grid, hipStream_t s, const void *buckets, u32 half, u32 L, u32 n_seg, u32 hi_win, void *seg_out) {
+    LCB_LAUNCH(k_msm_bucket_reduce, (const g1 *)buckets, half, L, n_seg, hi_win, (g1 *)seg_out);
 }
 extern "C" void lcbk_g1_jac_reduce_groups(dim3 grid, hipStream_t s, const void *in, u32 n_in, u32 group, void *out) {
     LCB_LAUNCH(k_g1_jac_reduce_groups, (const g1 *)in, n_in, group, (g1 *)out);
@@ -204,9 +310,9 @@ extern "C" void lcbk_g1_jac_reduce_block(hipStream_t s, const void *in, u32 n_in
     dim3 grid((n_in + group - 1) / group);
     LCB_LAUNCH(k_g1_jac_reduce_block, (const g1 *)in, n_in, group, (g1 *)out);
 }
-extern "C" void lcbk_msm_horner(hipStream_t s, const void *win, u32 nwin, u32 c, void *out) {
+extern "C" void lcbk_msm_horner(hipStream_t s, const void *win, u32 nwin, u32 c, u32 fold_top, void *out) {
     dim3 grid(1);
-    LCB_LAUNCH(k_msm_horner, (const g1 *)win, nwin, c, (g1 *)out);
+    LCB_LAUNCH(k_msm_horner, (const g1 *)win, nwin, c, fold_top, (g1 *)out);
 }
 extern "C" void lcbk_g1_jac_compress(dim3 grid, hipStream_t s, const void *in, u32 n, uint8_t *out) {
     LCB_LAUNCH(k_g1_jac_compress, (const g1 *)in, n, out);

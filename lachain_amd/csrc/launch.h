@@ -31,11 +31,13 @@ extern "C" void lcbk_g1_sum(dim3 grid, hipStream_t s, const void *parts, const u
 extern "C" void lcbk_g2_sum(dim3 grid, hipStream_t s, const void *parts, const uint8_t *ok_in, const u32 *off, u32 n_problems, uint8_t *status, uint8_t *out);
 extern "C" void lcbk_msm_digits(dim3 grid, hipStream_t s, const uint8_t *scalars, u32 n, u32 c, u32 nwin, u32 *keys, u32 *vals);
 extern "C" void lcbk_msm_bounds(dim3 grid, hipStream_t s, const u32 *keys, u32 m, u32 sentinel, u32 *start, u32 *end);
-extern "C" void lcbk_msm_bucket_acc(dim3 grid, hipStream_t s, const void *pts, const u32 *vals, const u32 *start, const u32 *end, u32 nb, void *buckets);
-extern "C" void lcbk_msm_bucket_reduce(dim3 grid, hipStream_t s, const void *buckets, u32 half, u32 L, u32 n_seg, void *seg_out);
+extern "C" void lcbk_msm_bucket_acc(dim3 grid, hipStream_t s, const void *pts, const void *pts2, u32 n_pts, const u32 *vals, const u32 *start, const u32 *end, u32 nb, void *buckets);
+extern "C" void lcbk_msm_digits_glv(dim3 grid, hipStream_t s, const uint8_t *scalars, u32 n, u32 c, u32 nwin, u32 *keys, u32 *vals);
+extern "C" void lcbk_msm_phi(dim3 grid, hipStream_t s, const void *pts, u32 n, void *out);
+extern "C" void lcbk_msm_bucket_reduce(dim3 grid, hipStream_t s, const void *buckets, u32 half, u32 L, u32 n_seg, u32 hi_win, void *seg_out);
 extern "C" void lcbk_g1_jac_reduce_groups(dim3 grid, hipStream_t s, const void *in, u32 n_in, u32 group, void *out);
 extern "C" void lcbk_g1_jac_reduce_block(hipStream_t s, const void *in, u32 n_in, u32 group, void *out);
-extern "C" void lcbk_msm_horner(hipStream_t s, const void *win, u32 nwin, u32 c, void *out);
+extern "C" void lcbk_msm_horner(hipStream_t s, const void *win, u32 nwin, u32 c, u32 fold_top, void *out);
 extern "C" void lcbk_g1_jac_compress(dim3 grid, hipStream_t s, const void *in, u32 n, uint8_t *out);
 extern "C" void lcbk_g1_to_affine(dim3 grid, hipStream_t s, const uint8_t *in, u32 n, void *out, uint8_t *ok);
 extern "C" int lcbk_sort_pairs(void *temp, size_t *temp_bytes, u32 *keys, u32 *keys_alt, u32 *vals, u32 *vals_alt, u32 m, int end_bit, hipStream_t s);

@@ -736,9 +736,19 @@ int assemble_enqueue(lcb_ctx *c, int g, uint8_t *out, uint8_t *status, const uin
 
 // ------------------------------------------------------------------ Pippenger MSM (k_msm.hip)
 // window width minimising ceil-windows * (n mixed adds * 11 + 2^(c-1) buckets * 2 Jacobian adds * 16) Fp-mul
-u32 msm_window(size_t n) {
+// GLV form: 2n points with 128-bit scalars, windows ceil(128 / c); only widths whose top window is nearly full
+// (a short top window concentrates 2n records in few buckets, one lane each)
+u32 msm_window(size_t n, bool glv = false) {
     u32 best = 4;
     double best_cost = 1e300;
+    if (glv) {
+        for (u32 c : {8u, 10u, 13u, 16u}) {
+            double w = (128 + c - 1) / c;
+            double cost = w * (2.0 * (double)n * 11.0) + (w + 1) * (double)(1u << (c - 1)) * 32.0;
+            if (cost < best_cost) { best_cost = cost; best = c; }
+        }
+        return best;
+    }
     for (u32 c = 4; c <= 20; c++) {
         double w = 255 / c + 1;
         double cost = w * ((double)n * 11.0 + (double)(1u << (c - 1)) * 32.0);
@@ -746,19 +756,26 @@ u32 msm_window(size_t n) {
     }
     return best;
 }
+// the GLV form halves the serial window combination and the bucket reduction, but at the window widths it can use
+// (<= 16) it needs more additions than the plain form's wider windows once n is large
+bool msm_use_glv(size_t n) { return n <= ((size_t)1 << 22); }
 int msm_enqueue(lcb_ctx *cx, void *out_jac, const void *pts, const uint8_t *scalars, size_t n, int window_bits,
-                hipStream_t s) {
-    if (n > 0x7fffffffu) { set_err("msm: too many points"); return -1; }
-    u32 c = window_bits > 0 ? (u32)window_bits : msm_window(n);
+                hipStream_t s, bool glv = false) {
+    if (n > (glv ? 0x3fffffffu : 0x7fffffffu)) { set_err("msm: too many points"); return -1; }
+    u32 c = window_bits > 0 ? (u32)window_bits : msm_window(n, glv);
     if (c < 2 || c > 24) { set_err("msm: window bits out of range"); return -1; }
-    u32 nwin = 255 / c + 1, half = 1u << (c - 1), nb = nwin * half, sentinel = nb;
-    size_t m = (size_t)n * nwin;
+    // GLV: nwin windows of the 128-bit halves, plus one key window for the top window's upper digit half
+    u32 nwin = glv ? (128 + c - 1) / c : 255 / c + 1, half = 1u << (c - 1);
+    u32 nb = (glv ? nwin + 1 : nwin) * half, sentinel = nb;
+    size_t np = glv ? 2 * n : n;                 // points the digit records refer to
+    size_t m = np * nwin;
     if (m > 0xffffffffu) { set_err("msm: n * windows exceeds 2^32"); return -1; }
     int end_bit = 1;
     while ((1ull << end_bit) <= sentinel) end_bit++;
     u32 L = 1;
     while ((size_t)nb / (L * 2) >= 65536 && L * 2 <= half) L *= 2;
     u32 n_seg = nb / L, per_win = half / L, n_l1 = n_seg / (per_win < 256 ? per_win : 256);
+    u32 kwin = nb / half;                        // key windows (nwin, or nwin + 1 in the GLV form)
     if (!cx->msm_ev_ready) {
         for (auto &e : cx->msm_ev) hipEventCreate(&e);
         cx->msm_ev_ready = true;
@@ -770,7 +787,7 @@ int msm_enqueue(lcb_ctx *cx, void *out_jac, const void *pts, const uint8_t *scal
     void *buckets = b[6].get((size_t)nb * LCB_G1_JAC_BYTES);
     void *segs = b[7].get((size_t)n_seg * LCB_G1_JAC_BYTES);
     void *l1 = b[8].get((size_t)n_l1 * LCB_G1_JAC_BYTES);
-    void *wins = b[9].get((size_t)nwin * LCB_G1_JAC_BYTES);
+    void *wins = b[9].get((size_t)kwin * LCB_G1_JAC_BYTES);
     size_t tb = 0;
     if (n && lcbk_sort_pairs(nullptr, &tb, keys, keys2, vals, vals2, (u32)m, end_bit, s) < 0) { set_err("msm: sort query"); return -1; }
     void *temp = b[10].get(tb);
@@ -778,8 +795,15 @@ int msm_enqueue(lcb_ctx *cx, void *out_jac, const void *pts, const uint8_t *scal
         set_err("msm: device allocation failed");
         return -1;
     }
+    void *phi = glv ? b[11].get(n * 96) : nullptr;
+    if (glv && !phi) { set_err("msm: device allocation failed"); return -1; }
     hipEventRecord(cx->msm_ev[0], s);
-    if (n) lcbk_msm_digits(dim3(nblk(n)), s, scalars, (u32)n, c, nwin, keys, vals);
+    if (n && glv) {
+        lcbk_msm_phi(dim3(nblk(n)), s, pts, (u32)n, phi);
+        lcbk_msm_digits_glv(dim3(nblk(n)), s, scalars, (u32)n, c, nwin, keys, vals);
+    } else if (n) {
+        lcbk_msm_digits(dim3(nblk(n)), s, scalars, (u32)n, c, nwin, keys, vals);
+    }
     hipEventRecord(cx->msm_ev[1], s);
     int alt = n ? lcbk_sort_pairs(temp, &tb, keys, keys2, vals, vals2, (u32)m, end_bit, s) : 0;
     if (alt < 0) { set_err("msm: radix sort"); return -1; }
@@ -789,9 +813,9 @@ int msm_enqueue(lcb_ctx *cx, void *out_jac, const void *pts, const uint8_t *scal
     hipMemsetAsync(en, 0, (size_t)nb * 4, s);
     if (m) lcbk_msm_bounds(dim3(nblk(m)), s, keys, (u32)m, sentinel, st, en);
     hipEventRecord(cx->msm_ev[3], s);
-    lcbk_msm_bucket_acc(dim3(nblk(nb)), s, pts, vals, st, en, nb, buckets);
+    lcbk_msm_bucket_acc(dim3(nblk(nb)), s, pts, phi, (u32)n, vals, st, en, nb, buckets);
     hipEventRecord(cx->msm_ev[4], s);
-    lcbk_msm_bucket_reduce(dim3(nblk(n_seg)), s, buckets, half, L, n_seg, segs);
+    lcbk_msm_bucket_reduce(dim3(nblk(n_seg)), s, buckets, half, L, n_seg, glv ? nwin : 0xffffffffu, segs);
     hipEventRecord(cx->msm_ev[5], s);
     // per-window sums: LDS tree reductions of up to 256 segment sums per block, ping-ponging segs <-> l1
     void *cur = segs, *nxt = l1;
@@ -804,8 +828,8 @@ int msm_enqueue(lcb_ctx *cx, void *out_jac, const void *pts, const uint8_t *scal
         cur = dst;
         nxt = (dst == l1) ? segs : l1;
     }
-    if (per_win == 1) hipMemcpyAsync(wins, segs, (size_t)nwin * LCB_G1_JAC_BYTES, hipMemcpyDeviceToDevice, s);
-    lcbk_msm_horner(s, wins, nwin, c, out_jac);
+    if (per_win == 1) hipMemcpyAsync(wins, segs, (size_t)kwin * LCB_G1_JAC_BYTES, hipMemcpyDeviceToDevice, s);
+    lcbk_msm_horner(s, wins, nwin, c, glv ? 1u : 0u, out_jac);
     hipEventRecord(cx->msm_ev[6], s);
     cx->msm_ran = true;
     return launched("msm launch") ? 0 : -1;
@@ -1386,6 +1410,19 @@ extern "C" int lcb_g2_hash_batch(uint8_t *out, const uint8_t *msg_data, const ui
 }
 
 extern "C" int lcb_g1_msm_window(size_t n) { return (int)msm_window(n); }
+extern "C" int lcb_g1_msm_glv_window(size_t n) { return msm_use_glv(n) ? (int)msm_window(n, true) : -(int)msm_window(n); }
+// GLV form: every point must have order r (generated as a G or checked); see include/lachain_bls.h
+extern "C" int lcb_ctx_g1_msm_glv_dev(lcb_ctx *ctx, void *out_jac, const void *points_aff, const uint8_t *scalars,
+                                      size_t n, int window_bits, void *stream) {
+    CTX_OR(c, ctx, -1)
+    Enq q(c, (hipStream_t)stream);
+    bool glv = window_bits > 0 || msm_use_glv(n);   // an explicit width selects the GLV form
+    return msm_enqueue(c, out_jac, points_aff, scalars, n, window_bits, q.s, glv);
+}
+extern "C" int lcb_g1_msm_glv_dev(void *out_jac, const void *points_aff, const uint8_t *scalars, size_t n,
+                                  int window_bits, void *stream) {
+    return lcb_ctx_g1_msm_glv_dev(nullptr, out_jac, points_aff, scalars, n, window_bits, stream);
+}
 extern "C" int lcb_ctx_g1_msm_dev(lcb_ctx *ctx, void *out_jac, const void *points_aff, const uint8_t *scalars, size_t n,
                                   int window_bits, void *stream) {
     CTX_OR(c, ctx, -1)

@@ -88,6 +88,9 @@ _SIGS = {
     "lcb_g1_msm_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_size, ctypes.c_int,
                                       ctypes.c_void_p]),
     "lcb_g1_msm_window": (ctypes.c_int, [c_size]),
+    "lcb_g1_msm_glv_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_size, ctypes.c_int,
+                                          ctypes.c_void_p]),
+    "lcb_g1_msm_glv_window": (ctypes.c_int, [c_size]),
     "lcb_g1_msm_phase_ms": (ctypes.c_int, [ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
     "lcb_g1_to_affine_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_size,
                                             ctypes.c_void_p]),
@@ -150,7 +153,7 @@ _SIGS = {
 # explicit-context forms: the context pointer first, then the same arguments as the context-less form
 for _name in ("tpke_prepare_dev", "tpke_verify_prepared_dev", "tpke_partial_decrypt_prepared_dev", "tpke_combine_dev",
               "tpke_verify_phase_ms", "ts_prepare_dev", "ts_verify_prepared_dev", "ts_assemble_dev", "g1_lagrange_dev",
-              "g2_lagrange_dev", "g1_msm_dev", "g1_msm_phase_ms", "ecdsa_verify_hashed_dev",
+              "g2_lagrange_dev", "g1_msm_dev", "g1_msm_glv_dev", "g1_msm_phase_ms", "ecdsa_verify_hashed_dev",
               "root_header_verify_dev", "ecdsa_pubkey_dev", "ecdsa_sign_hashed_dev", "ecdsa_phase_ms"):
     _res, _args = _SIGS["lcb_" + _name]
     _SIGS["lcb_ctx_" + _name] = (_res, [ctypes.c_void_p] + list(_args))

@@ -33,7 +33,7 @@ def _expected(points, scalars):
     return acc
 
 
-def _dev_msm(nat, torch, dev, points48, scalars_raw, window_bits=0):
+def _dev_msm(nat, torch, dev, points48, scalars_raw, window_bits=0, glv=False):
     """points48: serialized G1; scalars_raw: 32-byte LE (any 256-bit value) -> serialized MSM via the _dev ABI"""
     n = len(points48)
     lib = nat.lib()
@@ -45,7 +45,8 @@ def _dev_msm(nat, torch, dev, points48, scalars_raw, window_bits=0):
     d_jac = torch.zeros(144, dtype=torch.uint8, device=dev)
     d_out = torch.zeros(48, dtype=torch.uint8, device=dev)
     assert lib.lcb_g1_to_affine_dev(d_aff.data_ptr(), d_ok.data_ptr(), d_in.data_ptr(), n, s) == 0
-    assert lib.lcb_g1_msm_dev(d_jac.data_ptr(), d_aff.data_ptr(), d_sc.data_ptr(), n, window_bits, s) == 0, nat.last_error()
+    fn = lib.lcb_g1_msm_glv_dev if glv else lib.lcb_g1_msm_dev
+    assert fn(d_jac.data_ptr(), d_aff.data_ptr(), d_sc.data_ptr(), n, window_bits, s) == 0, nat.last_error()
     assert lib.lcb_g1_jac_sum_dev(d_out.data_ptr(), None, d_jac.data_ptr(), 1, s) == 0
     torch.cuda.synchronize(dev)
     if n:
@@ -141,3 +142,40 @@ def test_msm_partials_sum(nat, torch_dev):
     assert nat.lib().lcb_g1_jac_sum_dev(out.data_ptr(), None, cat.data_ptr(), 4, st) == 0
     torch.cuda.synchronize(dev)
     assert bytes(out.cpu().numpy().tobytes()) == o.g1_mul(o.g1_gen(), o.fr(total % R))
+
+
+def test_glv_msm_vs_oracle(nat, torch_dev):
+    """lcb_g1_msm_glv_dev (points of order r): s = s1 + s2 lambda over P and phi(P); edge scalars 0, 1, r - 1,
+    lambda, lambda + 1, u^2 multiples, raw values >= r, duplicated / opposite points, infinity; every window width
+    with a special case in the 129-bit digit split"""
+    torch, dev = torch_dev
+    d = Drbg(b"gpu-msm-glv")
+    G = o.g1_gen()
+    lam = 0xD201000000010000 ** 2 - 1
+    u2 = 0xD201000000010000 ** 2
+    edge = [0, 1, R - 1, lam, lam + 1, u2, u2 - 1, 2 * u2 + 5, (R - 1) // u2 * u2, 2 ** 256 - 1, R, R + 7]
+    for n in (1, 2, 13, 300):
+        pts = [o.g1_mul(G, d.fr()) for _ in range(n)]
+        if n >= 13:
+            pts[3] = pts[2]
+            pts[4] = o.g1_neg(pts[2])
+            pts[5] = bytes(48)
+        raw = [d.fr_int() for _ in range(n)]
+        for k, e in enumerate(edge[: n]):
+            raw[k] = e
+        sc = [(v % 2 ** 256).to_bytes(32, "little") for v in raw]
+        want = o.g1_msm(pts, [o.fr(v % R) for v in raw])
+        for c in (0, 4, 5, 7, 8, 13, 16, 17):
+            got, _ = _dev_msm(nat, torch, dev, pts, sc, c, glv=True)
+            assert got == want, (n, c)
+
+
+def test_glv_msm_known_answer_1m(nat, torch_dev):
+    torch, dev = torch_dev
+    d = Drbg(b"gpu-msm-glv-1m")
+    n = 1 << 20
+    a = [d.fr_int() for _ in range(n)]
+    s = [d.fr_int() for _ in range(n)]
+    pts = nat.mul_batch_raw(1, None, b"".join(o.fr(v) for v in a), n, generator=True)
+    got, _ = _dev_msm(nat, torch, dev, [pts[48 * i:48 * i + 48] for i in range(n)], [o.fr(v) for v in s], 0, glv=True)
+    assert got == o.g1_mul(o.g1_gen(), o.fr(sum(x * y for x, y in zip(a, s)) % R))
