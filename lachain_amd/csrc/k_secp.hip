@@ -265,6 +265,12 @@ extern "C" __global__ void __launch_bounds__(SECP_BLOCK) k_secp_scalars(const ui
 }
 
 // ------------------------------------------------------------------------------------------------ verify
+__device__ __forceinline__ void comb_add_entry(secp_jac &acc, const secp_aff &e, int d) {
+    if (d == 0) return;
+    fe y = e.y;
+    if (d < 0) fe_neg(y, y);
+    jac_add_aff(acc, acc, e.x, y);
+}
 __device__ __forceinline__ void comb_add(secp_jac &acc, const secp_aff *tab, int w, int d) {
     if (d == 0) return;
     const secp_aff e = tab[w * SECP_TAB + (d < 0 ? -d : d) - 1];
@@ -284,9 +290,21 @@ extern "C" __global__ void __launch_bounds__(SECP_BLOCK) k_secp_verify(const sec
     secp_jac acc;
     acc.inf = true;
     acc.x = acc.y = acc.z = fe_zero();
-    for (int w = 0; w < SECP_WIN; w++) {              // digits re-read from the (cached) record: no indexed registers
-        comb_add(acc, g_table, w, jp->d1[w]);
-        comb_add(acc, KT, w, jp->d2[w]);
+    // digits re-read from the (cached) record (no indexed registers); the next window's two table entries are
+    // loaded while the current window's additions run
+    int dg = jp->d1[0], dk = jp->d2[0];
+    secp_aff eg = g_table[dg ? (dg < 0 ? -dg : dg) - 1 : 0], ek = KT[dk ? (dk < 0 ? -dk : dk) - 1 : 0];
+    for (int w = 0; w < SECP_WIN; w++) {
+        const int cg = dg, ck = dk;
+        const secp_aff xg = eg, xk = ek;
+        if (w + 1 < SECP_WIN) {
+            dg = jp->d1[w + 1];
+            dk = jp->d2[w + 1];
+            eg = g_table[(w + 1) * SECP_TAB + (dg ? (dg < 0 ? -dg : dg) - 1 : 0)];
+            ek = KT[(w + 1) * SECP_TAB + (dk ? (dk < 0 ? -dk : dk) - 1 : 0)];
+        }
+        comb_add_entry(acc, xg, cg);
+        comb_add_entry(acc, xk, ck);
     }
     bool good = false;
     if (!acc.inf) {

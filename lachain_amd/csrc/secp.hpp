@@ -102,6 +102,14 @@ SDI void fe_reduce_wide(fe &r, const u32 *t) {
     c += t[15];                     // (hi << 32) contributes hi[7] at limb 8
     fe_fold(r, w, c);
 }
+#if !defined(SECP_HOST_EMULATION) && !defined(SECP_C_FIELD)
+#include "secp_asm.hpp"
+// gfx950: generated inline-assembly product / square (tools/gen_secp_asm.py); SECP_C_FIELD selects the C++ below
+SDI u32x8 fe_to_v(const fe &a) { u32x8 v; for (int i = 0; i < 8; i++) v[i] = a.v[i]; return v; }
+SDI fe fe_from_v(const u32x8 &v) { fe a; for (int i = 0; i < 8; i++) a.v[i] = v[i]; return a; }
+SDI void fe_mul(fe &r, const fe &a, const fe &b) { r = fe_from_v(secp_asm_mul(fe_to_v(a), fe_to_v(b))); }
+SDI void fe_sqr(fe &r, const fe &a) { r = fe_from_v(secp_asm_sqr(fe_to_v(a))); }
+#else
 SDI void fe_mul(fe &r, const fe &a, const fe &b) {
     u32 t[16];
 #pragma unroll
@@ -153,6 +161,11 @@ SDI void fe_sqr(fe &r, const fe &a) {
     }
     fe_reduce_wide(r, t);
 }
+#endif
+#if !defined(SECP_HOST_EMULATION) && !defined(SECP_C_FIELD)
+SDI void fe_add(fe &r, const fe &a, const fe &b) { secp_asm_add(r, a, b); }
+SDI void fe_sub(fe &r, const fe &a, const fe &b) { secp_asm_sub(r, a, b); }
+#else
 SDI void fe_add(fe &r, const fe &a, const fe &b) {
     u32 t[8];
     u64 c = 0;
@@ -188,6 +201,7 @@ SDI void fe_sub(fe &r, const fe &a, const fe &b) {
 #pragma unroll
     for (int i = 0; i < 8; i++) r.v[i] = t[i];
 }
+#endif
 SDI void fe_neg(fe &r, const fe &a) { fe_sub(r, fe_zero(), a); }
 SDI void fe_dbl(fe &r, const fe &a) { fe_add(r, a, a); }
 // canonical representative in [0, p)
