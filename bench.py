@@ -878,6 +878,86 @@ def run_ecdsa(args, nat, torch, dev, rank, world, cpu):
     return res
 
 
+# ------------------------------------------------------------------ DKG G1 work and RBC erasure coding
+def run_dkg(args, nat, rank):
+    """Trustless-DKG value checks of one node (TrustlessKeygen.cs:150-152): Commitment.Evaluate(x, y) of all N dealers'
+    commitments (degree F, (F+1)(F+2)/2 G1 coefficients each, generated as c_k G on the GPU) at x = the node's index,
+    y = the dealer's.  Host-pointer API (lcb_dkg_commitment_eval): the rate includes the coefficient upload."""
+    if rank != 0:
+        return None
+    n_val, deg = args.dkg_n, args.dkg_f
+    ncoef = (deg + 1) * (deg + 2) // 2
+    rng = np.random.default_rng(0x4C61636861696E + 0xD6)
+    sc = rng.integers(0, 256, (n_val * ncoef, 32), dtype=np.uint8)
+    sc[:, 31] &= 0x3F                                   # < 2^254 < r
+    pts = nat.mul_batch_raw(1, None, sc.tobytes(), n_val * ncoef, generator=True)
+    comms = [[pts[48 * (c * ncoef + k):48 * (c * ncoef + k) + 48] for k in range(ncoef)] for c in range(n_val)]
+    queries = [(j, 1, j + 1) for j in range(n_val)]    # node 0's checks of every dealer's value
+    nat.dkg_commitment_eval(comms, deg, queries[:2])   # warm-up (allocation)
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        got = nat.dkg_commitment_eval(comms, deg, queries)
+    dt = (time.perf_counter() - t0) / reps
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as o
+    t1 = time.perf_counter()
+    m = 0
+    while m < 4 and (m == 0 or time.perf_counter() - t1 < args.cpu_seconds / 3):
+        assert o.dkg_commitment_eval(comms[m], deg, 1, m + 1) == got[m]
+        m += 1
+    cdt = (time.perf_counter() - t1) / m
+    return dict(metric="Commitment.Evaluate(x, y) checks/sec (trustless DKG, one node's view of every dealer)",
+                value=n_val / dt, unit="evaluations/s", dealers=n_val, degree=deg, ms_per_batch=1e3 * dt,
+                api="lcb_dkg_commitment_eval (host pointers: includes the upload of the coefficients)",
+                parity=f"first {m} results equal the oracle's literal (F+1)^2-product Commitment.Evaluate",
+                cpu_baseline=dict(value=1.0 / cdt, unit="evaluations/s", cores=1, kind="port",
+                                  sample=f"{m} evaluations, oracle orc_dkg_commitment_eval as the reference computes it "
+                                         f"((F+1)^2 G1 x Fr products, Commitment.cs:23-37), one thread"))
+
+
+def run_rs(args, nat, rank):
+    """Reliable-broadcast erasure coding at N = 256 (F = 85: 86 data + 170 parity shards, ErasureCoding.cs:13):
+    ErasureCodingShards of a payload and DecodeFromEchos from 86 random echoes (ReliableBroadcast.cs:393-446).
+    Host-pointer API: the rate includes the payload / shard transfers."""
+    if rank != 0:
+        return None
+    n_sh, era = args.rs_n, 2 * ((args.rs_n - 1) // 3)
+    k = n_sh - era
+    size = (args.rs_bytes // k) * k
+    rng = np.random.default_rng(0x4C61636861696E + 0x125)
+    data = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+    S = size // k
+    nat.rs_encode(data[:k], n_sh, era)
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        enc = nat.rs_encode(data, n_sh, era)
+    t_enc = (time.perf_counter() - t0) / reps
+    keep = sorted(rng.choice(n_sh, k, replace=False).tolist())
+    echos = [(j, enc[j * S:(j + 1) * S]) for j in keep]
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dec = nat.rs_decode(echos, S, n_sh, era)
+    t_dec = (time.perf_counter() - t0) / reps
+    ok = dec == enc and enc[:size] == data
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as o
+    sample = max(k, (min(size, 1 << 16) // k) * k)
+    t1 = time.perf_counter()
+    ref = o.rs_encode_shards(data[:sample], n_sh, era)
+    c_enc = time.perf_counter() - t1
+    s2 = sample // k
+    assert ref == nat.rs_encode(data[:sample], n_sh, era)
+    return dict(metric="Reed-Solomon erasure coding of reliable-broadcast payloads (N = %d shards, %d erasures)" % (n_sh, era),
+                value=size / t_enc / 1e6, unit="payload MB/s (encode)", decode_mb_s=size / t_dec / 1e6,
+                payload_bytes=size, shard_bytes=S, round_trip_exact=bool(ok),
+                api="lcb_rs_encode / lcb_rs_decode (host pointers: includes the transfers)",
+                cpu_baseline=dict(value=sample / c_enc / 1e6, unit="payload MB/s (encode)", cores=1, kind="port",
+                                  sample=f"{sample} bytes ({s2} B shards), oracle orc_rs_encode_shards (ZXing-style "
+                                         f"polynomial division per byte column), one thread; equal to the GPU shards"))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -901,6 +981,10 @@ def main():
     ap.add_argument("--ecdsa-sigs", type=int, default=1 << 20, help="header signatures per rank (0 = skip)")
     ap.add_argument("--ecdsa-validators", type=int, default=256)
     ap.add_argument("--ecdsa-steps", type=int, default=3)
+    ap.add_argument("--dkg-n", type=int, default=256, help="DKG dealers (0 = skip)")
+    ap.add_argument("--dkg-f", type=int, default=85)
+    ap.add_argument("--rs-n", type=int, default=256, help="RBC shards (0 = skip)")
+    ap.add_argument("--rs-bytes", type=int, default=1 << 24)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -984,7 +1068,11 @@ def main():
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         elapsed = float(tmax[0])
     mismatches_all, shares_all = int(t[1]), int(t[2])
-    msm = ts = replay = ecdsa = None
+    msm = ts = replay = ecdsa = dkg = rs = None
+    if args.dkg_n > 0 and world == 1:
+        dkg = run_dkg(args, nat, rank)
+    if args.rs_n > 0 and world == 1:
+        rs = run_rs(args, nat, rank)
     if args.ecdsa_sigs > 0:
         ecdsa = run_ecdsa(args, nat, torch, dev, rank, world, cpu=(world == 1 and not args.no_cpu_baseline))
     if args.replay_n > 0:
@@ -1040,6 +1128,8 @@ def main():
             "threshold_signature": ts,
             "epoch_replay": replay,
             "ecdsa_headers": ecdsa,
+            "dkg": dkg,
+            "rbc_erasure_coding": rs,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -5,7 +5,7 @@ TAG=${1:-pmc}
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
-CMD=${PMC_CMD:-"python3 $R/bench.py --shares 262144 --steps 1 --warmup 0 --no-cpu-baseline --ts-rounds 4096 --msm-steps 1 --msm-sizes 1048576 --replay-n 0 --ecdsa-sigs 262144 --ecdsa-steps 1"}
+CMD=${PMC_CMD:-"python3 $R/bench.py --shares 262144 --steps 1 --warmup 0 --no-cpu-baseline --ts-rounds 4096 --msm-steps 1 --msm-sizes 1048576 --replay-n 0 --ecdsa-sigs 262144 --ecdsa-steps 1 --dkg-n 0 --rs-n 0"}
 i=0
 PMC_GROUPS=${PMC_GROUPS:-"SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU;FETCH_SIZE;WRITE_SIZE"}
 IFS=';' read -ra GRPS <<< "$PMC_GROUPS"
