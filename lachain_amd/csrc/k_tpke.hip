@@ -1,7 +1,9 @@
 // lachain_amd/csrc/k_tpke.hip — gfx950 kernels: TPKE decryption-share pipeline (decompression, per-ciphertext preparation, per-share verification, partial decryption).
 #include "kcommon.hpp"
+#include "fe_asm.hpp"
 
 LCB_ASM_LIBRARY(k_tpke)
+LCB_ASM_TOWER_LIBRARY(k_tpke)
 
 // ================================================================================= decompression
 extern "C" __global__ void LCB_BOUNDS k_g1_decompress(const uint8_t *in, u32 n, g1a_st *out) {
@@ -107,12 +109,19 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_miller(const u32 *lines, const
     accept[i] = ok;
 }
 // accept[i] &= (final_exp(f_i) == 1).  park: SoA Fp12 slots per item (lcbk_fe_slots()), slot 0 = f from the
-// Miller kernel.  LCB_LEAN_FE selects lean.hpp's slot form (pow-by-|z| base in LDS): measured 30 % slower
-// than the register form, so off by default.
-#ifdef LCB_LEAN_FE
+// Miller kernel.  Default: fe_asm.hpp (exponentiations by z over the AGPR-resident Fp12 assembly squaring, the
+// hard part's other values in slots 0..4).  LCB_FE_FUNCS: the round-2 compiler-built form (pairing.hpp's
+// __noinline__ Fp12 functions).  LCB_LEAN_FE selects lean.hpp's slot form (pow-by-|z| base in LDS): measured 30 %
+// slower than LCB_FE_FUNCS.  LCB_FE_STAGED (kcommon.hpp: the exp-by-z loop inlined in the kernel, base parked in
+// slot 1) measured 10 % slower than LCB_FE_FUNCS (69.1 vs 62.5 ms per 262,144 shares).
+#if defined(LCB_LEAN_FE)
 extern "C" int lcbk_fe_slots() { return 6; }
-#else
+#elif defined(LCB_FE_STAGED)
+extern "C" int lcbk_fe_slots() { return 2; }      // slot 0: f from the Miller kernel; slot 1: final_exp_staged's base
+#elif defined(LCB_FE_FUNCS)
 extern "C" int lcbk_fe_slots() { return 1; }
+#else
+extern "C" int lcbk_fe_slots() { return LCB_FE_ASM_SLOTS; }
 #endif
 extern "C" __global__ void LCB_PAIR_BOUNDS k_final_exp_check(u32 *park, u32 n, uint8_t *accept) {
 #ifdef LCB_LEAN_FE
@@ -123,10 +132,20 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_final_exp_check(u32 *park, u32 n, u
 #ifdef LCB_LEAN_FE
     final_exp_slots(park, n, i, lds_base + threadIdx.x);
     accept[i] = accept[i] && fe_slot_is_one(park, n, i, 4);
-#else
+#elif defined(LCB_FE_STAGED)
+    fp12 f;
+    fp12_load_soa(f, park, n, i);
+    final_exp_staged(f, park, n, i);
+    accept[i] = accept[i] && fp12_is_one(f);
+#elif defined(LCB_FE_FUNCS)
     fp12 f;
     fp12_load_soa(f, park, n, i);
     final_exp_inplace(f);
+    accept[i] = accept[i] && fp12_is_one(f);
+#else
+    final_exp_asm(park, n, i);
+    fp12 f;
+    fp12_load_soa(f, park, n, i);
     accept[i] = accept[i] && fp12_is_one(f);
 #endif
 }

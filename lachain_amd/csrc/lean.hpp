@@ -232,7 +232,7 @@ DI void fp12_cyc_sqr_inplace(fp12 &f) {
 struct FeSlots {
     u32 *base;
     size_t n, i;
-    DI u32 *at(int s, int w) const { return base + ((size_t)s * 144 + w) * n + i; }
+    DI u32 *at(int s, int w) const { return base + (size_t)s * 144 * n + soa_at(n, i, w); }
     DI void store(int s, const fp12 &f) const {
         const u32 *w = (const u32 *)&f;
 #pragma unroll

@@ -16,6 +16,9 @@
 #pragma once
 #include "curve.hpp"
 
+// word w of parked Fp12 item i (of n) in the quad-major SoA layout (kcommon.hpp)
+DI size_t soa_at(size_t n, size_t i, int w) { return ((size_t)(w >> 2) * n + i) * 4 + (w & 3); }
+
 #define LCB_NLINES 68
 #define LCB_LINE_WORDS (6 * 12)                      // A, Bc, Cc : three Fp2
 #define LCB_LINESET_WORDS (LCB_NLINES * LCB_LINE_WORDS) // 4896 u32 = 19584 B per G2 point
@@ -290,6 +293,9 @@ DN void fe_easy(fp12 &r, const fp12 &f) {
 }
 // x^z for unitary x (z = -|z|): cyclotomic square-and-multiply over |z|, then conjugate
 DN void cyc_pow_z(fp12 &r, const fp12 &x) {
+#ifdef LCB_FN_AGPR
+    asm volatile("; AGPRs usable as spill space in this function" ::: "a255");
+#endif
     fp12 acc = x;
     fp12 base = x; // kept in registers for the whole loop (the squaring chain never touches memory)
     for (int i = 62; i >= 0; i--) {

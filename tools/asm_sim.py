@@ -13,10 +13,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 HPP = os.path.join(HERE, "..", "lachain_amd", "csrc", "asm_routines.hpp")
 
 
-def load_library(path=HPP):
-    """-> {label: [(mnemonic, [operands])]} parsed from the LCB_ASM_LIBRARY_TEXT macro."""
+TOWER_HPP = os.path.join(HERE, "..", "lachain_amd", "csrc", "asm_tower.hpp")
+
+
+def load_library(path=HPP, macro="LCB_ASM_LIBRARY_TEXT"):
+    """-> {label: [(mnemonic, [operands])]} parsed from the library text macro."""
     src = open(path).read()
-    body = src[src.index("#define LCB_ASM_LIBRARY_TEXT"):]
+    body = src[src.index("#define " + macro):]
     body = body[:body.index('    ""\n')]
     routines, cur = {}, None
     for raw in re.findall(r'"(.*?)\\n"', body):
@@ -37,10 +40,10 @@ def load_library(path=HPP):
 
 def _regs(op):
     """'v12' -> ('v', [12]); 'v[36:37]' -> ('v', [36, 37]); 's[90:91]' -> ('s', [90, 91])"""
-    m = re.fullmatch(r"([vs])(\d+)", op)
+    m = re.fullmatch(r"([vsa])(\d+)", op)
     if m:
         return m.group(1), [int(m.group(2))]
-    m = re.fullmatch(r"([vs])\[(\d+):(\d+)\]", op)
+    m = re.fullmatch(r"([vsa])\[(\d+):(\d+)\]", op)
     if m:
         lo, hi = int(m.group(2)), int(m.group(3))
         return m.group(1), list(range(lo, hi + 1))
@@ -49,14 +52,15 @@ def _regs(op):
 
 class Lane:
     def __init__(self):
-        self.v, self.s = {}, {}
-        self.written_v, self.written_s = set(), set()
+        self.v, self.s, self.a = {}, {}, {}
+        self.written_v, self.written_s, self.written_a = set(), set(), set()
+        self.counts = {}
 
     def get(self, op):
         kind, rr = _regs(op)
         if kind is None:
             return int(op, 0) & M32
-        f = self.v if kind == "v" else self.s
+        f = {"v": self.v, "s": self.s, "a": self.a}[kind]
         val = 0
         for k, r in enumerate(rr):
             if r not in f:
@@ -69,7 +73,7 @@ class Lane:
 
     def put(self, op, val):
         kind, rr = _regs(op)
-        f, w = (self.v, self.written_v) if kind == "v" else (self.s, self.written_s)
+        f, w = {"v": (self.v, self.written_v), "s": (self.s, self.written_s), "a": (self.a, self.written_a)}[kind]
         if kind == "v" and len(rr) == 2 and rr[0] % 2:
             raise ValueError(f"misaligned 64-bit VGPR pair {op}")
         for k, r in enumerate(rr):
@@ -77,9 +81,11 @@ class Lane:
             w.add(r)
 
 
-def run(routine, lane):
+def run(routine, lane, routines=None):
+    target = None
     for mn, ops in routine:
         g = lane.get
+        lane.counts[mn] = lane.counts.get(mn, 0) + 1
         if mn == "v_mad_u64_u32":
             r = g(ops[2]) * g(ops[3]) + g(ops[4])
             lane.put(ops[0], r & ((1 << 64) - 1)); lane.put(ops[1], r >> 64)
@@ -93,8 +99,14 @@ def run(routine, lane):
             lane.put(ops[0], g(ops[2]) if lane.getmask(ops[3]) else g(ops[1]))
         elif mn == "v_mul_lo_u32":
             lane.put(ops[0], (g(ops[1]) * g(ops[2])) & M32)
-        elif mn in ("v_mov_b32", "s_mov_b32"):
+        elif mn in ("v_mov_b32", "s_mov_b32", "v_accvgpr_read_b32", "v_accvgpr_write_b32"):
             lane.put(ops[0], g(ops[1]))
+        elif mn in ("s_nop", "s_getpc_b64", "s_addc_u32"):
+            pass
+        elif mn == "s_add_u32":             # call sequence: remember the target label
+            target = ops[2].split("@")[0]
+        elif mn == "s_swappc_b64":
+            run(routines[target], lane, routines)
         elif mn == "s_setpc_b64":
             return
         elif mn == "s_endpgm":
@@ -104,13 +116,17 @@ def run(routine, lane):
     raise RuntimeError("routine fell off its end without s_setpc_b64")
 
 
-def call(routines, label, inputs):
-    """inputs: {first VGPR: 12-limb integer}.  Returns (lane, reader(first VGPR) -> integer)."""
+def call(routines, label, inputs, agprs=None):
+    """inputs: {first VGPR: 12-limb integer}; agprs: {first AGPR: 12-limb integer}.
+    Returns (lane, reader(first VGPR) -> integer)."""
     lane = Lane()
     for base, val in inputs.items():
         for j in range(12):
             lane.v[base + j] = (val >> (32 * j)) & M32
-    run(routines[label], lane)
+    for base, val in (agprs or {}).items():
+        for j in range(12):
+            lane.a[base + j] = (val >> (32 * j)) & M32
+    run(routines[label], lane, routines)
 
     def read(base):
         return sum(lane.v[base + j] << (32 * j) for j in range(12))
