@@ -35,8 +35,16 @@ SEED = 0x4C61636861696E
 C = dict(C_ML1_EVAL=5192, C_ML2_EVAL=8116, C_LINES=2012, C_FE=8603, C_H2G2=7266, C_DEC1=611, C_DEC2=1837,
          C_MUL1=2835, C_MUL2=6908, C_AFF2=625)
 MAC_PER_FPMUL = 300                      # 12x12 (a*b) + 12x12 (m*p) + 12 (m) 32-bit MACs, CIOS/FIPS Montgomery
-W_VERIFY = C["C_DEC1"] + C["C_ML2_EVAL"] + C["C_FE"]                                   # per share
-W_PREPARE = C["C_DEC1"] + C["C_DEC2"] + C["C_H2G2"] + C["C_AFF2"] + 2 * C["C_LINES"]  # per ciphertext
+# Round 2: precomputed line sets are normalised to A = 1 (pairing.hpp lineset_compute), so a line product costs
+# 9 instead of 13 Fp2 products (-12 Fp-mul per line, 68 lines per set); normalising a set costs one Fp2
+# inversion (C_FP2_INV) + 68 x (1 prefix product + 4 backward products) Fp2 products (3 Fp-mul each).
+C["C_FP2_INV"] = 2 + 463 + 2 + 2                                      # norm, Fp inversion, 2 x (Fp2 x Fp)
+C["C_NORM"] = C["C_FP2_INV"] + 68 * 5 * 3                            # per line set
+C["C_ML2_NORM2"] = C["C_ML2_EVAL"] - 2 * 68 * 12                     # TPKE: both sets normalised
+C["C_ML2_NORM1"] = C["C_ML2_EVAL"] - 68 * 12                         # TS: message set normalised, share lines on the fly
+W_VERIFY = C["C_DEC1"] + C["C_ML2_NORM2"] + C["C_FE"]                                  # per share
+W_PREPARE = (C["C_DEC1"] + C["C_DEC2"] + C["C_H2G2"] + C["C_AFF2"] + 2 * C["C_LINES"]
+             + 2 * C["C_NORM"])                                                        # per ciphertext
 # gfx950 v_mad_u64_u32 is half rate: 64 lane-MACs / clk / CU (profiles/r01_valu_rates.jsonl)
 PEAK_MAC32 = 256 * 64 * 2.4e9            # 3.93e13 MAC/s at the 2.4 GHz max clock
 
@@ -340,7 +348,7 @@ def run_msm(args, nat, torch, dev, rank, world, cpu, n):
 
 
 # ------------------------------------------------------------------ threshold signatures (BASELINE configs[2])
-W_TS = C["C_DEC2"] + C["C_ML2_EVAL"] + C["C_LINES"] + C["C_FE"]   # per share: sig decompress, Miller (one side's
+W_TS = C["C_DEC2"] + C["C_ML2_NORM1"] + C["C_LINES"] + C["C_FE"]  # per share: sig decompress, Miller (one side's
                                                                  # lines on the fly), final exponentiation
 
 
@@ -1117,7 +1125,7 @@ def main():
                          "mac_per_fpmul": MAC_PER_FPMUL, "verify_ms": ver_ms, "prepare_ms": prep_ms,
                          "kernel_ms": {"k_tpke_miller": miller_ms, "k_final_exp_check": fexp_ms},
                          "kernel_frac": {
-                             "k_tpke_miller": n * (C["C_DEC1"] + C["C_ML2_EVAL"]) * MAC_PER_FPMUL
+                             "k_tpke_miller": n * (C["C_DEC1"] + C["C_ML2_NORM2"]) * MAC_PER_FPMUL
                              / (miller_ms * 1e-3) / PEAK_MAC32,
                              "k_final_exp_check": n * C["C_FE"] * MAC_PER_FPMUL / (fexp_ms * 1e-3) / PEAK_MAC32},
                          "traffic_source": traffic_note},

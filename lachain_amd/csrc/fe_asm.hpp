@@ -22,14 +22,88 @@ DN void fx_easy(u32 *x, size_t n, size_t i) {
     fe_easy(f, f);
     fp12_store_soa(x, n, i, f);
 }
-// dst = (conj_a ? conj(a) : a) * b  (dst may alias a or b)
-DN void fx_mul(u32 *dst, const u32 *a, const u32 *b, int conj_a, size_t n, size_t i) {
-    fp12 x, y, r;
-    fp12_load_soa(x, a, n, i);
-    if (conj_a) fp12_conj(x, x);
-    fp12_load_soa(y, b, n, i);
-    fp12_mul(r, x, y);
-    fp12_store_soa(dst, n, i, r);
+// one lane's column of the block's LDS scratch: 36 quads (t0 = quads 0..17, t1 = quads 18..35), quad g at
+// p[g * LCB_BLOCK] (a wave's 64 lanes touch 1 KB contiguous per quad access)
+struct FxLds { uint4 *p; };
+DI void fp6_load_half(fp6 &x, const u32 *slot, int half, size_t n, size_t i) {
+    u32 *d = (u32 *)&x;
+    u32 n16 = (u32)(n * 16), off = (u32)(i * 16);
+    asm volatile("" : "+v"(off));
+    const char *b = (const char *)slot;
+#pragma unroll
+    for (int g = 0; g < 18; g++) {
+        uint4 v = *(const uint4 *)(b + (u32)((18 * half + g) * n16 + off));
+        d[4 * g] = v.x; d[4 * g + 1] = v.y; d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
+    }
+}
+DI void fp6_store_half(u32 *slot, int half, size_t n, size_t i, const fp6 &x) {
+    const u32 *s = (const u32 *)&x;
+    u32 n16 = (u32)(n * 16), off = (u32)(i * 16);
+    asm volatile("" : "+v"(off));
+    char *b = (char *)slot;
+#pragma unroll
+    for (int g = 0; g < 18; g++)
+        *(uint4 *)(b + (u32)((18 * half + g) * n16 + off)) = make_uint4(s[4 * g], s[4 * g + 1], s[4 * g + 2], s[4 * g + 3]);
+}
+DI void fp6_lds_store(FxLds t, int which, const fp6 &x) {
+    const u32 *s = (const u32 *)&x;
+#pragma unroll
+    for (int g = 0; g < 18; g++)
+        t.p[(18 * which + g) * LCB_BLOCK] = make_uint4(s[4 * g], s[4 * g + 1], s[4 * g + 2], s[4 * g + 3]);
+}
+DI void fp6_lds_load(fp6 &x, FxLds t, int which) {
+    u32 *d = (u32 *)&x;
+#pragma unroll
+    for (int g = 0; g < 18; g++) {
+        uint4 v = t.p[(18 * which + g) * LCB_BLOCK];
+        d[4 * g] = v.x; d[4 * g + 1] = v.y; d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
+    }
+}
+// dst = (conj_a ? conj(a) : a) * b  (dst may alias a or b).  Karatsuba over Fp6 in phases that each hold at
+// most two Fp6 operands + one product: t1 = a1 b1 and t0 = a0 b0 are parked in LDS, the operands re-read from
+// their slots, so the compiler-built Fp6 products run without scratch spills.
+DN void fx_mul(u32 *dst, const u32 *a, const u32 *b, int conj_a, size_t n, size_t i, FxLds t) {
+    {
+        fp6 x, y, r;
+        fp6_load_half(x, a, 1, n, i);
+        if (conj_a) fp6_neg(x, x);
+        fp6_load_half(y, b, 1, n, i);
+        fp6_mul(r, x, y);
+        fp6_lds_store(t, 1, r);                            // t1 = a1 b1
+    }
+    asm volatile("" ::: "memory");
+    {
+        fp6 x, y, r;
+        fp6_load_half(x, a, 0, n, i);
+        fp6_load_half(y, b, 0, n, i);
+        fp6_mul(r, x, y);
+        fp6_lds_store(t, 0, r);                            // t0 = a0 b0
+    }
+    asm volatile("" ::: "memory");
+    fp6 s;
+    {
+        fp6 x, y, u;
+        fp6_load_half(x, a, 0, n, i);
+        fp6_load_half(u, a, 1, n, i);
+        if (conj_a) fp6_sub(x, x, u);
+        else fp6_add(x, x, u);
+        fp6_load_half(y, b, 0, n, i);
+        fp6_load_half(u, b, 1, n, i);
+        fp6_add(y, y, u);
+        fp6_mul(s, x, y);                                  // (a0 + a1)(b0 + b1)
+    }
+    asm volatile("" ::: "memory");
+    {
+        fp6 t0, t1;
+        fp6_lds_load(t0, t, 0);
+        fp6_lds_load(t1, t, 1);
+        fp6_sub(s, s, t0);
+        fp6_sub(s, s, t1);
+        fp6_store_half(dst, 1, n, i, s);                   // r1 = s - t0 - t1
+        fp6_mul_v(t1, t1);
+        fp6_add(t0, t0, t1);
+        fp6_store_half(dst, 0, n, i, t0);                  // r0 = t0 + v t1
+    }
 }
 // dst = frob_k(a), k = 1, 2, 3
 DN void fx_frob(u32 *dst, const u32 *a, int k, size_t n, size_t i) {
@@ -50,7 +124,7 @@ DN void fx_conj(u32 *dst, const u32 *a, size_t n, size_t i) {
 // dst = x^z (z = -|z| < 0, x unitary in slot `base`), slot `acc` as the accumulator: each run of squarings
 // between the set bits of |z| (1, 2, 3, 9, 32, 16) is ONE call of the assembly routine, the five products by x
 // are slot products; dst may alias base
-DI void fx_pow_z(u32 *dst, const u32 *base, u32 *acc, size_t n, size_t i) {
+DI void fx_pow_z(u32 *dst, const u32 *base, u32 *acc, size_t n, size_t i, FxLds t) {
     const u32 n16 = (u32)(n * 16), off = (u32)(i * 16);
     bool first = true;
     int b = 62;
@@ -64,7 +138,7 @@ DI void fx_pow_z(u32 *dst, const u32 *base, u32 *acc, size_t n, size_t i) {
         }
         lcb_asm_cyc_sqr_n(first ? base : acc, acc, n16, off, cnt);
         first = false;
-        if (bb >= 0) fx_mul(acc, acc, base, 0, n, i);   // bit bb of |z| is set
+        if (bb >= 0) fx_mul(acc, acc, base, 0, n, i, t);   // bit bb of |z| is set
         b = bb - 1;
     }
     fx_conj(dst, acc, n, i);
@@ -72,28 +146,28 @@ DI void fx_pow_z(u32 *dst, const u32 *base, u32 *acc, size_t n, size_t i) {
 
 // f^((p^12 - 1)/r) (x3, mcl's normalisation) of the Fp12 in slot 0 -> slot 0; slots 1..5 as working space.
 // Stage structure and products: fe_hard (pairing.hpp).
-DI void final_exp_asm(u32 *park, size_t n, size_t i) {
+DI void final_exp_asm(u32 *park, size_t n, size_t i, FxLds t) {
     u32 *X = park, *T = park + (size_t)144 * n, *U = park + (size_t)288 * n, *V = park + (size_t)432 * n,
         *A = park + (size_t)576 * n, *W = park + (size_t)720 * n;
     fx_easy(X, n, i);
-    fx_pow_z(T, X, W, n, i);                          // t = x^z
+    fx_pow_z(T, X, W, n, i, t);                          // t = x^z
     lcb_asm_cyc_sqr_n(X, U, (u32)(n * 16), (u32)(i * 16), 1);
-    fx_mul(U, U, T, 1, n, i);                         // u = conj(x^2) t = x^(z-2)
-    fx_pow_z(V, U, W, n, i);                          // v = x^(z^2-2z)
-    fx_mul(A, V, X, 0, n, i);
+    fx_mul(U, U, T, 1, n, i, t);                         // u = conj(x^2) t = x^(z-2)
+    fx_pow_z(V, U, W, n, i, t);                          // v = x^(z^2-2z)
+    fx_mul(A, V, X, 0, n, i, t);
     fx_frob(A, A, 3, n, i);                           // acc = (v x)^(p^3)
-    fx_pow_z(V, V, W, n, i);                          // v = x^(z^3-2z^2)
-    fx_mul(W, V, T, 0, n, i);
+    fx_pow_z(V, V, W, n, i, t);                          // v = x^(z^3-2z^2)
+    fx_mul(W, V, T, 0, n, i, t);
     fx_frob(W, W, 2, n, i);
-    fx_mul(A, A, W, 0, n, i);                         // acc *= (v t)^(p^2)
-    fx_pow_z(V, V, W, n, i);                          // v = x^(z^4-2z^3)
+    fx_mul(A, A, W, 0, n, i, t);                         // acc *= (v t)^(p^2)
+    fx_pow_z(V, V, W, n, i, t);                          // v = x^(z^4-2z^3)
     lcb_asm_cyc_sqr_n(T, T, (u32)(n * 16), (u32)(i * 16), 1);
-    fx_mul(V, V, T, 0, n, i);                         // v = x^(z^4-2z^3+2z)
-    fx_mul(W, X, V, 1, n, i);
+    fx_mul(V, V, T, 0, n, i, t);                         // v = x^(z^4-2z^3+2z)
+    fx_mul(W, X, V, 1, n, i, t);
     fx_frob(W, W, 1, n, i);
-    fx_mul(A, A, W, 0, n, i);                         // acc *= (x^-1 v)^p
-    fx_pow_z(V, V, W, n, i);                          // v = x^(z^5-2z^4+2z^2)
-    fx_mul(U, U, V, 1, n, i);                         // x^(2-z) v
-    fx_mul(U, U, X, 0, n, i);                         //   ... x
-    fx_mul(X, A, U, 0, n, i);
+    fx_mul(A, A, W, 0, n, i, t);                         // acc *= (x^-1 v)^p
+    fx_pow_z(V, V, W, n, i, t);                          // v = x^(z^5-2z^4+2z^2)
+    fx_mul(U, U, V, 1, n, i, t);                         // x^(2-z) v
+    fx_mul(U, U, X, 0, n, i, t);                         //   ... x
+    fx_mul(X, A, U, 0, n, i, t);
 }

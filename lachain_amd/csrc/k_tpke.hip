@@ -67,10 +67,8 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_verify(const u32 *lines, const uint
     ok = ok && ks.ok;
     st_to_g1a(Y, ks);
     fp_neg(Y.y, Y.y); // -Y: e(Ui, H) == e(Y, W)  <=>  e(Ui, H) e(-Y, W) == 1
-    LinesFromMemory sH{lines + (size_t)(2 * c) * LCB_LINESET_WORDS};
-    LinesFromMemory sW{lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS};
     fp12 f, e;
-    miller2(f, sH, Ui, sW, Y);
+    miller2_sets(f, lines + (size_t)(2 * c) * LCB_LINESET_WORDS, Ui, lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS, Y);
     final_exp(e, f);
     accept[i] = ok && fp12_is_one(e);
 }
@@ -97,13 +95,11 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_miller(const u32 *lines, const
     ok = ok && ks.ok;
     st_to_g1a(Y, ks);
     fp_neg(Y.y, Y.y);
-    LinesFromMemory sH{lines + (size_t)(2 * c) * LCB_LINESET_WORDS};
-    LinesFromMemory sW{lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS};
     fp12 f;
 #ifdef LCB_LEAN_MILLER
-    miller2_lean(f, sH, Ui, sW, Y, LdsCol{lds_t + threadIdx.x});
+#error "LCB_LEAN_MILLER reads round-2 general line sets; the line sets are normalised since round 2 (pairing.hpp)"
 #else
-    miller2(f, sH, Ui, sW, Y);
+    miller2_sets(f, lines + (size_t)(2 * c) * LCB_LINESET_WORDS, Ui, lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS, Y);
 #endif
     fp12_store_soa(f_soa, n, i, f);
     accept[i] = ok;
@@ -126,6 +122,8 @@ extern "C" int lcbk_fe_slots() { return LCB_FE_ASM_SLOTS; }
 extern "C" __global__ void LCB_PAIR_BOUNDS k_final_exp_check(u32 *park, u32 n, uint8_t *accept) {
 #ifdef LCB_LEAN_FE
     __shared__ u32 lds_base[144 * LCB_BLOCK];
+#elif !defined(LCB_FE_STAGED) && !defined(LCB_FE_FUNCS)
+    __shared__ uint4 fx_lds[36 * LCB_BLOCK];      // per lane: the two Fp6 products of a slot multiplication
 #endif
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -143,7 +141,7 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_final_exp_check(u32 *park, u32 n, u
     final_exp_inplace(f);
     accept[i] = accept[i] && fp12_is_one(f);
 #else
-    final_exp_asm(park, n, i);
+    final_exp_asm(park, n, i, FxLds{fx_lds + threadIdx.x});
     fp12 f;
     fp12_load_soa(f, park, n, i);
     accept[i] = accept[i] && fp12_is_one(f);
@@ -160,10 +158,8 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_partial_decrypt(const u32 *lines, c
     bool ok = g1_decompress(U, cts_u + 48 * (size_t)c) && ct_ok[c];
     g1_generator(G);
     fp_neg(G.y, G.y);
-    LinesFromMemory sH{lines + (size_t)(2 * c) * LCB_LINESET_WORDS};
-    LinesFromMemory sW{lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS};
     fp12 f, e;
-    miller2(f, sH, U, sW, G);
+    miller2_sets(f, lines + (size_t)(2 * c) * LCB_LINESET_WORDS, U, lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS, G);
     final_exp(e, f);
     ok = ok && fp12_is_one(e);
     status[c] = ok;

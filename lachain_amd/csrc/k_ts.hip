@@ -19,6 +19,27 @@ extern "C" __global__ void LCB_BOUNDS k_ts_msg_prepare(const uint8_t *msg_data, 
     lineset_compute(lines + (size_t)m * LCB_LINESET_WORDS, Ha);
     msg_ok[m] = ok;
 }
+// two-pair Miller loop of a signature check: the message's line set (normalised, or its point's lines on the fly
+// when it could not be normalised) and the share's lines on the fly
+DN void miller2_ts_fallback(fp12 &f, const u32 *lsH, const g1a &PK, const g2a &S, const g1a &G) {
+    g2a Q;
+    lineset_point(Q, lsH);
+    LinesOnTheFly sH, sS;
+    sH.init(Q);
+    sS.init(S);
+    miller2(f, sH, PK, sS, G);
+}
+DI void miller2_ts(fp12 &f, const u32 *lsH, const g1a &PK, const g2a &S, const g1a &G) {
+    if (lineset_normalised(lsH)) {
+        LinesNorm sH{lsH};
+        LinesOnTheFly sS;
+        sS.init(S);
+        miller2(f, sH, PK, sS, G);
+    } else {
+        miller2_ts_fallback(f, lsH, PK, S, G);
+    }
+}
+
 // ValidateSignature: e(PK, H) == e(G, sig) <=> e(PK, H) e(-G, sig) == 1
 extern "C" __global__ void LCB_BOUNDS k_ts_verify(const u32 *lines, const uint8_t *msg_ok, u32 n_msgs, const g1a_st *pks,
                                                  u32 n_pks, const uint8_t *sigs, const u32 *msg_idx,
@@ -37,11 +58,8 @@ extern "C" __global__ void LCB_BOUNDS k_ts_verify(const u32 *lines, const uint8_
     st_to_g1a(PK, ps);
     g1_generator(G);
     fp_neg(G.y, G.y);
-    LinesFromMemory sH{lines + (size_t)m * LCB_LINESET_WORDS};
-    LinesOnTheFly sS;
-    sS.init(S);
     fp12 f, e;
-    miller2(f, sH, PK, sS, G);
+    miller2_ts(f, lines + (size_t)m * LCB_LINESET_WORDS, PK, S, G);
     final_exp(e, f);
     accept[i] = ok && fp12_is_one(e);
 }
@@ -67,14 +85,11 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_ts_miller(const u32 *lines, const u
     st_to_g1a(PK, ps);
     g1_generator(G);
     fp_neg(G.y, G.y);
-    LinesFromMemory sH{lines + (size_t)m * LCB_LINESET_WORDS};
-    LinesOnTheFly sS;
-    sS.init(S);
     fp12 f;
 #ifdef LCB_LEAN_MILLER
-    miller2_lean(f, sH, PK, sS, G, LdsCol{lds_t + threadIdx.x});
+#error "LCB_LEAN_MILLER reads round-2 general line sets; the line sets are normalised since round 2 (pairing.hpp)"
 #else
-    miller2(f, sH, PK, sS, G);
+    miller2_ts(f, lines + (size_t)m * LCB_LINESET_WORDS, PK, S, G);
 #endif
     fp12_store_soa(f_soa, n, i, f);
     accept[i] = ok;

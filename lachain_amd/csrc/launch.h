@@ -66,4 +66,4 @@ extern "C" void lcbk_op(dim3 grid, hipStream_t s, int op, u32 *io, int orig_cof)
 #define LCB_FR_BYTES 32
 #define LCB_G1_JAC_BYTES 144
 #define LCB_G2_JAC_BYTES 288
-#define LCB_LINESET_BYTES 19584
+#define LCB_LINESET_BYTES 26368   /* pairing.hpp LCB_LINESET_WORDS * 4 */

@@ -33,7 +33,8 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_sqr_c(u32 *park, u32 n) {
 extern "C" __global__ void LCB_PAIR_BOUNDS k_mul_slot(u32 *park, u32 n) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    for (int k = 0; k < 5; k++) fx_mul(park, park, park + (size_t)144 * n, 0, n, i);
+    __shared__ uint4 lds[36 * LCB_BLOCK];
+    for (int k = 0; k < 5; k++) fx_mul(park, park, park + (size_t)144 * n, 0, n, i, FxLds{lds + threadIdx.x});
 }
 extern "C" __global__ void LCB_PAIR_BOUNDS k_easy(u32 *park, u32 n) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -43,7 +44,8 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_easy(u32 *park, u32 n) {
 extern "C" __global__ void LCB_PAIR_BOUNDS k_fe_asm(u32 *park, u32 n) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    final_exp_asm(park, n, i);
+    __shared__ uint4 lds[36 * LCB_BLOCK];
+    final_exp_asm(park, n, i, FxLds{lds + threadIdx.x});
 }
 extern "C" __global__ void LCB_PAIR_BOUNDS k_fe_funcs(u32 *park, u32 n) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
