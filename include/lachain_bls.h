@@ -153,6 +153,10 @@ int mclBn_G2EvaluatePolynomial(mclBnG2 *out, const mclBnG2 *cVec, mclSize cSize,
 int lcb_set_device(int device_id);                 /* before mclBn_init; default: HIP device 0 */
 int lcb_get_device(void);
 void lcb_set_original_g2_cofactor(int enable);     /* unpinned mcl choice, DESIGN.md §Parity */
+/* Line sets prepared for TPKE ciphertexts / signed messages are normalised (A = 1) unless a line has A == 0, in
+   which case the Miller loop computes that point's lines on the fly.  general = 1 makes every later prepare take
+   the on-the-fly path (test hook: the fallback must give the same decisions); 0 restores the default. */
+void lcb_set_line_mode(int general);
 const char *lcb_last_error(void);
 
 /* TPKE.PublicKey.VerifyShare for a batch (TPKE/PublicKey.cs:88-92, called per share from

@@ -29,7 +29,8 @@ extern "C" __global__ void LCB_BOUNDS k_g2_decompress(const uint8_t *in, u32 n, 
 // lines layout: lines[(2*c + 0) * LINESET] = H lines, lines[(2*c + 1) * LINESET] = W lines
 extern "C" __global__ void LCB_BOUNDS k_tpke_ct_prepare(const uint8_t *cts_u, const uint8_t *cts_w,
                                                        const uint8_t *v_data, const u32 *v_off, u32 n_cts,
-                                                       u32 *lines, uint8_t *ct_ok, int orig_cof) {
+                                                       u32 *lines, uint8_t *ct_ok, int flags) {
+    // flags: bit 0 = mcl's original G2 cofactor clearing in hash-to-G2, bit 1 = mark the line sets un-normalised
     u32 c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_cts) return;
     const uint8_t *ub = cts_u + 48 * (size_t)c;
@@ -42,14 +43,30 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_ct_prepare(const uint8_t *cts_u, co
     u32 v0 = v_off[c], v1 = v_off[c + 1];
     sha512_2(d, ub, 48, v_data + v0, v1 - v0);
     g2 H;
-    bool hok = g2_hash_digest(H, d, orig_cof != 0);
+    bool hok = g2_hash_digest(H, d, (flags & 1) != 0);
     ok = ok && hok;
     if (hok) jac_to_aff(Ha, H);
     else { Ha.inf = true; Ha.x = fp2_zero(); Ha.y = fp2_zero(); }
     if (!ok) { W.inf = true; Ha.inf = true; }
-    lineset_compute(lines + (size_t)(2 * c) * LCB_LINESET_WORDS, Ha);
-    lineset_compute(lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS, W);
+    // the two points go to their line sets' point slots; k_lineset_fill computes the 2 * n_cts line sets one lane
+    // each (the per-ciphertext serial path is hash + one line set instead of hash + two)
+    u32 *lsH = lines + (size_t)(2 * c) * LCB_LINESET_WORDS, *lsW = lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS;
+    lineset_put_point(lsH, Ha);
+    lineset_put_point(lsW, W);
+    lsH[LCB_LS_FLAG + 2] = lsW[LCB_LS_FLAG + 2] = (flags & 2) ? 1 : 0;
     ct_ok[c] = ok;
+}
+
+// line sets of points stored by a prepare kernel (lineset_put_point): one lane per set
+extern "C" __global__ void LCB_BOUNDS k_lineset_fill(u32 *lines, u32 n_sets) {
+    u32 k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_sets) return;
+    u32 *ls = lines + (size_t)k * LCB_LINESET_WORDS;
+    g2a Q;
+    lineset_get_point(Q, ls);
+    u32 force_general = ls[LCB_LS_FLAG + 2];
+    lineset_compute(ls, Q);
+    if (force_general) ls[LCB_LS_FLAG] = 0;
 }
 
 extern "C" __global__ void LCB_BOUNDS k_tpke_verify(const u32 *lines, const uint8_t *ct_ok, u32 n_cts,
@@ -184,6 +201,9 @@ extern "C" void lcbk_g2_decompress(dim3 grid, hipStream_t s, const uint8_t *in, 
 }
 extern "C" void lcbk_tpke_ct_prepare(dim3 grid, hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data, const u32 *v_off, u32 n_cts, u32 *lines, uint8_t *ct_ok, int orig_cof) {
     LCB_LAUNCH(k_tpke_ct_prepare, cts_u, cts_w, v_data, v_off, n_cts, lines, ct_ok, orig_cof);
+}
+extern "C" void lcbk_lineset_fill(dim3 grid, hipStream_t s, u32 *lines, u32 n_sets) {
+    LCB_LAUNCH(k_lineset_fill, lines, n_sets);
 }
 extern "C" void lcbk_tpke_verify(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, uint8_t *accept) {
     LCB_LAUNCH(k_tpke_verify, lines, ct_ok, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, accept);

@@ -5,7 +5,7 @@ LCB_ASM_LIBRARY(k_ts)
 
 // ================================================================================= threshold signatures
 extern "C" __global__ void LCB_BOUNDS k_ts_msg_prepare(const uint8_t *msg_data, const u32 *msg_off, u32 n_msgs,
-                                                      u32 *lines, uint8_t *msg_ok, int orig_cof) {
+                                                      u32 *lines, uint8_t *msg_ok, int flags) {
     u32 m = blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= n_msgs) return;
     uint8_t d[64];
@@ -13,10 +13,11 @@ extern "C" __global__ void LCB_BOUNDS k_ts_msg_prepare(const uint8_t *msg_data, 
     sha512_2(d, msg_data + o0, o1 - o0, msg_data, 0);
     g2 H;
     g2a Ha;
-    bool ok = g2_hash_digest(H, d, orig_cof != 0);
+    bool ok = g2_hash_digest(H, d, (flags & 1) != 0);
     if (ok) jac_to_aff(Ha, H);
     else { Ha.inf = true; Ha.x = fp2_zero(); Ha.y = fp2_zero(); }
     lineset_compute(lines + (size_t)m * LCB_LINESET_WORDS, Ha);
+    if (flags & 2) lines[(size_t)m * LCB_LINESET_WORDS + LCB_LS_FLAG] = 0;
     msg_ok[m] = ok;
 }
 // two-pair Miller loop of a signature check: the message's line set (normalised, or its point's lines on the fly

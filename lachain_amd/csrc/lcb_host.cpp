@@ -122,6 +122,8 @@ extern "C" int lcb_set_device(int id) {
 }
 extern "C" int lcb_get_device(void) { return g_device; }
 extern "C" void lcb_set_original_g2_cofactor(int enable) { g_orig_cofactor = enable != 0; }
+int g_line_mode = 0;   // 1: prepare marks every line set un-normalised (test hook for the on-the-fly fallback)
+extern "C" void lcb_set_line_mode(int general) { g_line_mode = general != 0; }
 extern "C" const char *lcb_last_error(void) { return g_err.c_str(); }
 
 extern "C" int mclBn_init(int curve, int compiledTimeVar) {
@@ -610,7 +612,11 @@ int tpke_prepare(lcb_ctx *c, const uint8_t *d_y, size_t n_keys, const uint8_t *d
     void *keys = c->t_keys.get(n_keys * LCB_G1A_ST_BYTES);
     if (!lines || !ctok || !keys) { set_err("device allocation failed"); return -1; }
     if (n_keys) lcbk_g1_decompress(dim3(nblk(n_keys)), s, d_y, (u32)n_keys, keys);
-    if (n_cts) lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), s, d_u, d_w, d_v, d_voff, (u32)n_cts, lines, ctok, g_orig_cofactor);
+    if (n_cts) {
+        lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), s, d_u, d_w, d_v, d_voff, (u32)n_cts, lines, ctok,
+                             g_orig_cofactor | (g_line_mode << 1));
+        lcbk_lineset_fill(dim3(nblk(2 * n_cts)), s, lines, (u32)(2 * n_cts));
+    }
     if (!launched("tpke prepare launch")) return -1;
     c->t_n_cts = n_cts;
     c->t_n_keys = n_keys;
@@ -671,7 +677,8 @@ int ts_prepare(lcb_ctx *c, const uint8_t *d_pks, size_t n_pks, const uint8_t *d_
     void *keys = c->s_keys.get(n_pks * LCB_G1A_ST_BYTES);
     if (!lines || !mok || !keys) { set_err("device allocation failed"); return -1; }
     if (n_pks) lcbk_g1_decompress(dim3(nblk(n_pks)), s, d_pks, (u32)n_pks, keys);
-    if (n_msgs) lcbk_ts_msg_prepare(dim3(nblk(n_msgs)), s, d_msg, d_moff, (u32)n_msgs, lines, mok, g_orig_cofactor);
+    if (n_msgs) lcbk_ts_msg_prepare(dim3(nblk(n_msgs)), s, d_msg, d_moff, (u32)n_msgs, lines, mok,
+                                      g_orig_cofactor | (g_line_mode << 1));
     if (!launched("ts prepare launch")) return -1;
     c->s_n_msgs = n_msgs;
     c->s_n_pks = n_pks;

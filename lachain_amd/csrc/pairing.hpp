@@ -137,6 +137,7 @@ DI void fp2_load_w(fp2 &x, const u32 *src) {
 DN bool lineset_compute(u32 *dst, const g2a &Q) {
     fp2_store_w(dst + LCB_LS_POINT, Q.x);
     fp2_store_w(dst + LCB_LS_POINT + 24, Q.y);
+    dst[LCB_LS_FLAG + 1] = Q.inf ? 1 : 0;
     if (Q.inf) {                                      // every line is the constant 1: B' = C' = 0
         fp2 z = fp2_zero();
         for (int k = 0; k < LCB_NLINES; k++) {
@@ -337,8 +338,15 @@ DI bool lineset_normalised(const u32 *ls) { return ls[LCB_LS_FLAG] != 0; }
 DI void lineset_point(g2a &Q, const u32 *ls) {
     fp2_load_w(Q.x, ls + LCB_LS_POINT);
     fp2_load_w(Q.y, ls + LCB_LS_POINT + 24);
-    Q.inf = false;                                     // an infinity point always normalises
+    Q.inf = ls[LCB_LS_FLAG + 1] != 0;
 }
+// a prepare kernel stores the point; k_lineset_fill computes its lines
+DI void lineset_put_point(u32 *ls, const g2a &Q) {
+    fp2_store_w(ls + LCB_LS_POINT, Q.x);
+    fp2_store_w(ls + LCB_LS_POINT + 24, Q.y);
+    ls[LCB_LS_FLAG + 1] = Q.inf ? 1 : 0;
+}
+DI void lineset_get_point(g2a &Q, const u32 *ls) { lineset_point(Q, ls); }
 
 // f = prod_k f_{|z|, Q_k}(P_k), conjugated (z < 0).  A pair whose G1 point is infinity contributes 1.
 // LCB_MILLER_LINE_PAIR: multiply the two lines of a step together first (23 instead of 26 Fp2 products).

@@ -51,6 +51,7 @@ _SIGS = {
     "lcb_set_device": (ctypes.c_int, [ctypes.c_int]),
     "lcb_get_device": (ctypes.c_int, []),
     "lcb_set_original_g2_cofactor": (None, [ctypes.c_int]),
+    "lcb_set_line_mode": (None, [ctypes.c_int]),
     "lcb_last_error": (ctypes.c_char_p, []),
     "lcb_tpke_verify_shares": (ctypes.c_int, [c_u8p, c_size, c_u8p, c_size, c_u8p, c_u8p, c_u8p, c_u32p, c_size,
                                               c_u32p, c_u32p, c_u8p]),
@@ -666,3 +667,9 @@ class Context:
 
 def set_original_g2_cofactor(enable):
     lib().lcb_set_original_g2_cofactor(1 if enable else 0)
+
+
+def set_line_mode(general):
+    """general=True: later prepares mark every line set un-normalised, so the Miller loops take the on-the-fly
+    fallback (pairing.hpp miller2_sets_fallback); False restores the normalised default"""
+    lib().lcb_set_line_mode(1 if general else 0)

@@ -24,8 +24,17 @@ def nat():
     return native
 
 
+@pytest.fixture(params=["normalised", "on_the_fly"])
+def line_mode(nat, request):
+    """every transcript runs through the normalised line sets (default) and through the on-the-fly fallback that
+    a set with a zero line coefficient takes (forced by lcb_set_line_mode): both must reproduce the fixture"""
+    nat.set_line_mode(request.param == "on_the_fly")
+    yield request.param
+    nat.set_line_mode(False)
+
+
 @pytest.mark.parametrize("key", ["tpke_n4", "tpke_n22"])
-def test_tpke_transcript(nat, key):
+def test_tpke_transcript(nat, key, line_mode):
     t = T[key]
     cts = [(H(c["u"]), H(c["v"]), H(c["w"])) for c in t["ciphertexts"]]
     shares = [(ci, i, H(s)) for ci, c in enumerate(t["ciphertexts"]) for i, s in enumerate(c["shares"])]
@@ -39,7 +48,7 @@ def test_tpke_transcript(nat, key):
 
 
 @pytest.mark.parametrize("key", ["ts_n7", "ts_n100"])
-def test_ts_transcript(nat, key):
+def test_ts_transcript(nat, key, line_mode):
     t = T[key]
     msgs = [H(r["msg"]) for r in t["rounds"]]
     items = [(ri, i, H(s)) for ri, r in enumerate(t["rounds"]) for i, s in enumerate(r["sigs"])]
