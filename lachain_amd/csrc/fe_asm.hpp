@@ -27,23 +27,23 @@ DN void fx_easy(u32 *x, size_t n, size_t i) {
 struct FxLds { uint4 *p; };
 DI void fp6_load_half(fp6 &x, const u32 *slot, int half, size_t n, size_t i) {
     u32 *d = (u32 *)&x;
-    u32 n16 = (u32)(n * 16), off = (u32)(i * 16);
+    u32 off = (u32)(i * 16);
     asm volatile("" : "+v"(off));
     const char *b = (const char *)slot;
 #pragma unroll
     for (int g = 0; g < 18; g++) {
-        uint4 v = *(const uint4 *)(b + (u32)((18 * half + g) * n16 + off));
+        uint4 v = *(const uint4 *)(b + (size_t)(18 * half + g) * n * 16 + off);
         d[4 * g] = v.x; d[4 * g + 1] = v.y; d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
     }
 }
 DI void fp6_store_half(u32 *slot, int half, size_t n, size_t i, const fp6 &x) {
     const u32 *s = (const u32 *)&x;
-    u32 n16 = (u32)(n * 16), off = (u32)(i * 16);
+    u32 off = (u32)(i * 16);
     asm volatile("" : "+v"(off));
     char *b = (char *)slot;
 #pragma unroll
     for (int g = 0; g < 18; g++)
-        *(uint4 *)(b + (u32)((18 * half + g) * n16 + off)) = make_uint4(s[4 * g], s[4 * g + 1], s[4 * g + 2], s[4 * g + 3]);
+        *(uint4 *)(b + (size_t)(18 * half + g) * n * 16 + off) = make_uint4(s[4 * g], s[4 * g + 1], s[4 * g + 2], s[4 * g + 3]);
 }
 DI void fp6_lds_store(FxLds t, int which, const fp6 &x) {
     const u32 *s = (const u32 *)&x;

@@ -23,25 +23,26 @@ DI void st_to_g2a(g2a &a, const g2a_st &s) { a.x = s.x; a.y = s.y; a.inf = s.inf
 // Fp12 values parked in HBM between the Miller-loop and final-exponentiation kernels: quad-major SoA (words
 // 4g..4g+3 of item i at u32 index (g * n + i) * 4), so a wave's 64 lanes read / write 1 KB contiguous per
 // 16-byte access and the assembly routines (asm_tower.hpp) move an Fp12 with 36 global_load/store_dwordx4.
-// Addresses are formed from a 32-bit per-lane byte offset (i * 16) that is made opaque first, so the compiler
-// cannot hoist 36 per-lane 64-bit addresses per slot out of the callers' loops (it did, and spilled them).
+// Addresses: a wave-uniform 64-bit base per quad (SGPRs, advanced by n * 16 bytes per quad) plus a 32-bit per-lane
+// byte offset (i * 16) that is made opaque first, so the compiler cannot hoist 36 per-lane 64-bit addresses per slot
+// out of the callers' loops (it did, and spilled them).  Valid for any n < 2^28 (the lane offset stays 32-bit).
 DI void fp12_store_soa(u32 *base, size_t n, size_t i, const fp12 &f) {
     const u32 *s = (const u32 *)&f;
-    u32 n16 = (u32)(n * 16), off = (u32)(i * 16);
+    u32 off = (u32)(i * 16);
     asm volatile("" : "+v"(off));
     char *b = (char *)base;
 #pragma unroll
     for (int g = 0; g < 36; g++)
-        *(uint4 *)(b + (u32)(g * n16 + off)) = make_uint4(s[4 * g], s[4 * g + 1], s[4 * g + 2], s[4 * g + 3]);
+        *(uint4 *)(b + (size_t)g * n * 16 + off) = make_uint4(s[4 * g], s[4 * g + 1], s[4 * g + 2], s[4 * g + 3]);
 }
 DI void fp12_load_soa(fp12 &f, const u32 *base, size_t n, size_t i) {
     u32 *d = (u32 *)&f;
-    u32 n16 = (u32)(n * 16), off = (u32)(i * 16);
+    u32 off = (u32)(i * 16);
     asm volatile("" : "+v"(off));
     const char *b = (const char *)base;
 #pragma unroll
     for (int g = 0; g < 36; g++) {
-        uint4 v = *(const uint4 *)(b + (u32)(g * n16 + off));
+        uint4 v = *(const uint4 *)(b + (size_t)g * n * 16 + off);
         d[4 * g] = v.x; d[4 * g + 1] = v.y; d[4 * g + 2] = v.z; d[4 * g + 3] = v.w;
     }
 }

@@ -603,6 +603,8 @@ bool fused_verify() {
 }
 
 // ------------------------------------------------------------------ TPKE
+#define LCB_VERIFY_CHUNK ((size_t)1 << 21)   // shares per Miller + final-exponentiation launch pair
+
 int tpke_prepare(lcb_ctx *c, const uint8_t *d_y, size_t n_keys, const uint8_t *d_u, const uint8_t *d_w,
                  const uint8_t *d_v, const uint32_t *d_voff, size_t n_cts, hipStream_t s) {
     if (n_cts > 0xffffffffu || n_keys > 0xffffffffu) { set_err("tpke prepare: batch too large"); return -1; }
@@ -642,18 +644,24 @@ int tpke_verify_prepared(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_keys,
         lcbk_tpke_verify(dim3(nblk(n)), s, lines, ctok, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct, d_dec, d_ui, (u32)n,
                          d_accept);
     } else if (n) {
-        u32 *f = (u32 *)c->t_f.get(n * 576 * (size_t)lcbk_fe_slots())   /* SoA Fp12 slots: Miller output (+ final-exp parking) */;
+        // chunks of at most LCB_VERIFY_CHUNK shares: bounded park buffer (slots x 576 B per share) whatever n is;
+        // the phase events time the first chunk
+        const size_t nf = n < LCB_VERIFY_CHUNK ? n : LCB_VERIFY_CHUNK;
+        u32 *f = (u32 *)c->t_f.get(nf * 576 * (size_t)lcbk_fe_slots())   /* SoA Fp12 slots: Miller output (+ final-exp parking) */;
         if (!f) { set_err("device allocation failed"); return -1; }
         if (!c->ver_ev_ready) {
             for (auto &e : c->ver_ev) hipEventCreate(&e);
             c->ver_ev_ready = true;
         }
-        hipEventRecord(c->ver_ev[0], s);
-        lcbk_tpke_miller(dim3(nblk(n)), s, lines, ctok, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct, d_dec, d_ui, (u32)n,
-                         f, d_accept);
-        hipEventRecord(c->ver_ev[1], s);
-        lcbk_final_exp_check(dim3(nblk(n)), s, f, (u32)n, d_accept);
-        hipEventRecord(c->ver_ev[2], s);
+        for (size_t o = 0; o < n; o += LCB_VERIFY_CHUNK) {
+            const size_t m = n - o < LCB_VERIFY_CHUNK ? n - o : LCB_VERIFY_CHUNK;
+            if (o == 0) hipEventRecord(c->ver_ev[0], s);
+            lcbk_tpke_miller(dim3(nblk(m)), s, lines, ctok, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct + o, d_dec + o,
+                             d_ui + 48 * o, (u32)m, f, d_accept + o);
+            if (o == 0) hipEventRecord(c->ver_ev[1], s);
+            lcbk_final_exp_check(dim3(nblk(m)), s, f, (u32)m, d_accept + o);
+            if (o == 0) hipEventRecord(c->ver_ev[2], s);
+        }
         c->ver_ran = true;
     }
     return launched("tpke verify launch") ? 0 : -1;
@@ -700,11 +708,15 @@ int ts_verify_prepared(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_pks, si
         lcbk_ts_verify(dim3(nblk(n)), s, lines, mok, (u32)n_msgs, c->s_keys.p, (u32)n_pks, d_sigs, d_midx, d_pidx, (u32)n,
                        d_accept);
     } else if (n) {
-        u32 *f = (u32 *)c->s_f.get(n * 576 * (size_t)lcbk_fe_slots())   /* SoA Fp12 slots: Miller output (+ final-exp parking) */;
+        const size_t nf = n < LCB_VERIFY_CHUNK ? n : LCB_VERIFY_CHUNK;
+        u32 *f = (u32 *)c->s_f.get(nf * 576 * (size_t)lcbk_fe_slots())   /* SoA Fp12 slots: Miller output (+ final-exp parking) */;
         if (!f) { set_err("device allocation failed"); return -1; }
-        lcbk_ts_miller(dim3(nblk(n)), s, lines, mok, (u32)n_msgs, c->s_keys.p, (u32)n_pks, d_sigs, d_midx, d_pidx, (u32)n,
-                       f, d_accept);
-        lcbk_final_exp_check(dim3(nblk(n)), s, f, (u32)n, d_accept);
+        for (size_t o = 0; o < n; o += LCB_VERIFY_CHUNK) {
+            const size_t m = n - o < LCB_VERIFY_CHUNK ? n - o : LCB_VERIFY_CHUNK;
+            lcbk_ts_miller(dim3(nblk(m)), s, lines, mok, (u32)n_msgs, c->s_keys.p, (u32)n_pks, d_sigs + 96 * o,
+                           d_midx + o, d_pidx + o, (u32)m, f, d_accept + o);
+            lcbk_final_exp_check(dim3(nblk(m)), s, f, (u32)m, d_accept + o);
+        }
     }
     return launched("ts verify launch") ? 0 : -1;
 }

@@ -318,3 +318,47 @@ def test_msm_known_answer_2p24_c20(nat, tdev):
     got, exp = _msm_known_answer(nat, torch, dev, 1 << 24, 20, 24)
     assert got == o.g1_mul(o.g1_gen(), o.fr(exp))
     torch.cuda.empty_cache()
+
+
+def test_tpke_verify_beyond_one_chunk(nat, tdev):
+    """More shares than one Miller / final-exponentiation launch pair takes (LCB_VERIFY_CHUNK = 2^21): 2,097,280
+    shares tiled from 32 known decisions (4 ciphertexts x 8 decryptors with wrong, reversed and off-subgroup
+    shares), so chunk boundaries and the park-slot addressing beyond 2^21 items are checked bit-exactly."""
+    torch, dev = tdev
+    n, f, c = 8, 2, 4
+    d = Drbg(b"gpu-verify-chunks")
+    xs, y_secret = keyset(d, n, f)
+    y = o.g1_mul(o.g1_gen(), o.fr(y_secret))
+    yi = [o.g1_mul(o.g1_gen(), o.fr(x)) for x in xs]
+    plains = [d.bytes(32) for _ in range(c)]
+    cts = [o.tpke_encrypt(y, p, o.fr(d.fr_int())) for p in plains]
+    shares = [[o.g1_mul(U, o.fr(x)) for x in xs] for (U, _, _) in cts]
+    shares[0][1] = shares[0][2]
+    shares[1][3] = shares[1][3][::-1]
+    shares[2][5] = off_subgroup_g1(d)
+    shares[3][0] = o.g1_add(shares[3][0], shares[3][0])
+    base = [s for row in shares for s in row]
+    ok = lambda i: o.g1_valid(base[i]) and o.tpke_verify_share(yi[i % n], *cts[i // n], base[i]) == 1
+    expect = np.array([ok(i) for i in range(c * n)], dtype=np.uint8)
+    assert expect.sum() in (c * n - 4, c * n - 3)
+    reps = 65540
+    total = reps * c * n
+    assert total > (1 << 21)
+    lib = nat.lib()
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    d_y = up(torch, dev, b"".join(yi))
+    d_u = up(torch, dev, b"".join(ct[0] for ct in cts))
+    d_w = up(torch, dev, b"".join(ct[2] for ct in cts))
+    d_v = up(torch, dev, b"".join(ct[1] for ct in cts))
+    d_voff = up(torch, dev, np.arange(0, 32 * (c + 1), 32, dtype=np.uint32))
+    d_ct = up(torch, dev, np.tile(np.repeat(np.arange(c, dtype=np.uint32), n), reps))
+    d_dec = up(torch, dev, np.tile(np.arange(n, dtype=np.uint32), c * reps))
+    d_sh = up(torch, dev, b"".join(base)).repeat(reps)
+    d_acc = torch.full((total,), 7, dtype=torch.uint8, device=dev)
+    assert lib.lcb_tpke_prepare_dev(d_y.data_ptr(), n, d_u.data_ptr(), d_w.data_ptr(), d_v.data_ptr(),
+                                    d_voff.data_ptr(), c, sh) == 0
+    assert lib.lcb_tpke_verify_prepared_dev(d_acc.data_ptr(), total, n, c, d_ct.data_ptr(), d_dec.data_ptr(),
+                                            d_sh.data_ptr(), sh) == 0
+    torch.cuda.synchronize(dev)
+    got = d_acc.cpu().numpy()
+    assert np.array_equal(got, np.tile(expect, reps))

@@ -421,14 +421,15 @@ def gen_cyc_sqr(fp4_outs, fp4_used):
 
 # ------------------------------------------------------------------ lcb_r_cyc_sqr_n
 # in:  s[20:21] = input slot, s[22:23] = output slot (byte addresses of quad-major SoA Fp12 slots), s19 = n * 16
-#      (bytes between word quads), v248 = this lane's byte offset i * 16, s18 = number of squarings (>= 1)
+#      (bytes between word quads, < 2^32), v248 = this lane's byte offset i * 16, s18 = number of squarings (>= 1);
+#      s[16:17] walks the quads (64-bit scalar base + 32-bit lane offset: any n < 2^28)
 # out: output slot = input^(2^s18); s18 = 0.  Return address saved in s[24:25] across the nested calls.
 def gen_cyc_sqr_n():
-    b = ["s_mov_b64 s[24:25], s[30:31]", "v_mov_b32 v0, v248"]
-    for g in range(36):
-        b.append(f"global_load_dwordx4 a[{4 * g}:{4 * g + 3}], v0, s[20:21]")
+    b = ["s_mov_b64 s[24:25], s[30:31]", "s_mov_b64 s[16:17], s[20:21]"]
+    for g in range(36):     # quad g of this lane at s[16:17] + g * n16 + v248 (64-bit scalar base, 32-bit lane offset)
+        b.append(f"global_load_dwordx4 a[{4 * g}:{4 * g + 3}], v248, s[16:17]")
         if g < 35:
-            b.append("v_add_u32_e32 v0, s19, v0")
+            b += ["s_add_u32 s16, s16, s19", "s_addc_u32 s17, s17, 0"]
     b.append("s_waitcnt vmcnt(0)")
     b.append("lcb_cyc_sqr_n_loop:")
     b += ["s_getpc_b64 s[26:27]",
@@ -439,11 +440,11 @@ def gen_cyc_sqr_n():
           "s_cmp_lg_u32 s18, 0",
           "s_cbranch_scc1 lcb_cyc_sqr_n_loop",
           "s_nop 4",                       # AGPR writes by the squaring -> stores of them
-          "v_mov_b32 v0, v248"]
+          "s_mov_b64 s[16:17], s[22:23]"]
     for g in range(36):
-        b.append(f"global_store_dwordx4 v0, a[{4 * g}:{4 * g + 3}], s[22:23]")
+        b.append(f"global_store_dwordx4 v248, a[{4 * g}:{4 * g + 3}], s[16:17]")
         if g < 35:
-            b.append("v_add_u32_e32 v0, s19, v0")
+            b += ["s_add_u32 s16, s16, s19", "s_addc_u32 s17, s17, 0"]
     b.append("s_setpc_b64 s[24:25]")
     return ["lcb_r_cyc_sqr_n:"] + b
 
@@ -451,7 +452,7 @@ def gen_cyc_sqr_n():
 # ------------------------------------------------------------------ emit
 def clobbers_n():
     regs = [f'"v{i}"' for i in range(VMAX)] + [f'"a{i}"' for i in range(A_PARK + 2 * N)]
-    regs += [f'"s{s}"' for s in CLOBBER_SGPRS + [24, 25]] + ['"scc"', '"vcc"']
+    regs += [f'"s{s}"' for s in CLOBBER_SGPRS + [16, 17, 24, 25]] + ['"scc"', '"vcc"']
     return ", ".join(regs)
 
 
