@@ -100,6 +100,7 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_miller(const u32 *lines, const
 #ifdef LCB_LEAN_MILLER
     __shared__ u32 lds_t[72 * LCB_BLOCK];   // one Fp6 temporary per lane (lean.hpp)
 #endif
+    __shared__ uint4 lds_pts[12 * LCB_BLOCK];   // the lane's two G1 points (LinesNormLds)
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u32 c = ct_idx[i], d = dec_idx[i];
@@ -116,7 +117,15 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_miller(const u32 *lines, const
 #ifdef LCB_LEAN_MILLER
 #error "LCB_LEAN_MILLER reads round-2 general line sets; the line sets are normalised since round 2 (pairing.hpp)"
 #else
-    miller2_sets(f, lines + (size_t)(2 * c) * LCB_LINESET_WORDS, Ui, lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS, Y);
+    const u32 *lsH = lines + (size_t)(2 * c) * LCB_LINESET_WORDS, *lsW = lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS;
+    if (lineset_normalised(lsH) && lineset_normalised(lsW)) {
+        uint4 *pt = lds_pts + threadIdx.x;               // Ui at quads 0..5, -Y at quads 6..11
+        g1_park_lds(pt, Ui);
+        g1_park_lds(pt + 6 * LCB_BLOCK_PTS, Y);
+        miller2_norm_lds(f, lsH, pt, Ui.inf, lsW, pt + 6 * LCB_BLOCK_PTS, Y.inf);
+    } else {
+        miller2_sets_fallback(f, lsH, Ui, lsW, Y);
+    }
 #endif
     fp12_store_soa(f_soa, n, i, f);
     accept[i] = ok;

@@ -268,32 +268,33 @@ DI void fp12_mul_line_pair(fp12 &f, const fp2 &A1, const fp2 &B1, const fp2 &C1,
 // The three coefficient positions are processed in the order 2, 1, 0 so f is updated in place: position k reads
 // X_k = f0_{k-1}, Y_k = f1_{k-1} (X_0 = xi f0_2, Y_0 = xi f1_2, taken first).
 DI void fp12_mul_line_n(fp12 &f, const fp2 &b, const fp2 &c) {
-    fp2 bc, X0, Y0, t1[3];
+    fp2 bc, X0, Y0, t12;
     fp2_add(bc, b, c);
     fp2_mul_xi(X0, f.c0.c2);
     fp2_mul_xi(Y0, f.c1.c2);
     fp2 *f0[3] = {&f.c0.c0, &f.c0.c1, &f.c0.c2};
     fp2 *f1[3] = {&f.c1.c0, &f.c1.c1, &f.c1.c2};
+    // v (c Y) = (xi t1_2, t1_0, t1_1) is folded in as soon as each t1_k exists: t1_1 into f0_2 (no longer read),
+    // t1_0 into f0_1 (read as X_2 before), only t1_2 waits for the end (f0_0 is X_1)
 #pragma unroll
     for (int k = 2; k >= 0; k--) {
         const fp2 &X = k == 0 ? X0 : *f0[k - 1];
         const fp2 &Y = k == 0 ? Y0 : *f1[k - 1];
-        fp2 t0, s, u;
+        fp2 t0, t1, s, u;
         fp2_mul(t0, b, X);
-        fp2_mul(t1[k], c, Y);
+        fp2_mul(t1, c, Y);
         fp2_add(u, X, Y);
         fp2_mul(s, bc, u);
         fp2_sub(s, s, t0);
-        fp2_sub(s, s, t1[k]);
+        fp2_sub(s, s, t1);
         fp2_add(*f1[k], *f1[k], s);                    // f1_k is not read after position k
-        if (k != 0) fp2_add(*f0[k], *f0[k], t0);       // f0_k was last read as X_{k+1}
-        else fp2_add(*f0[0], *f0[0], t0);
+        fp2_add(*f0[k], *f0[k], t0);                   // f0_k was last read as X_{k+1}
+        if (k == 2) t12 = t1;
+        else fp2_add(*f0[k + 1], *f0[k + 1], t1);      // f0_2 += t1_1, f0_1 += t1_0
     }
     fp2 w;
-    fp2_mul_xi(w, t1[2]);
-    fp2_add(f.c0.c0, f.c0.c0, w);                      // + v (c Y): (xi t1_2, t1_0, t1_1)
-    fp2_add(f.c0.c1, f.c0.c1, t1[0]);
-    fp2_add(f.c0.c2, f.c0.c2, t1[1]);
+    fp2_mul_xi(w, t12);
+    fp2_add(f.c0.c0, f.c0.c0, w);
 }
 
 // Line sources for the two-pair Miller loop: apply(f, P, is_add) multiplies f by the source's next line
@@ -334,6 +335,87 @@ struct LinesNorm {          // normalised lines of a line set (lineset_compute)
         fp12_mul_line_n(f, b, c);
     }
 };
+// the same, with its G1 point parked in LDS (6 quads per lane, quad q at pt[q * LCB_BLOCK_PTS]) and re-read at
+// every line: keeps the point's 24 words out of the Miller loop's live registers (the loop otherwise spills)
+#ifndef LCB_BLOCK_PTS
+#define LCB_BLOCK_PTS 256
+#endif
+struct LinesNormLds {
+    const u32 *p;
+    const uint4 *pt;
+    bool inf;
+    DI void apply(fp12 &f, const g1a &, bool) {
+        fp2 b, c;
+        fp2_load_w(b, p);
+        fp2_load_w(c, p + 24);
+        p += LCB_NLINE_WORDS;
+        if (inf) return;
+        asm volatile("" ::: "memory");                // re-read the point: not kept live across the loop
+        fp x, y;
+        u32 *xw = x.v, *yw = y.v;
+#pragma unroll
+        for (int q = 0; q < 3; q++) {
+            uint4 vx = pt[q * LCB_BLOCK_PTS], vy = pt[(3 + q) * LCB_BLOCK_PTS];
+            xw[4 * q] = vx.x; xw[4 * q + 1] = vx.y; xw[4 * q + 2] = vx.z; xw[4 * q + 3] = vx.w;
+            yw[4 * q] = vy.x; yw[4 * q + 1] = vy.y; yw[4 * q + 2] = vy.z; yw[4 * q + 3] = vy.w;
+        }
+        fp2_mul_fp(b, b, x);
+        fp2_mul_fp(c, c, y);
+        fp12_mul_line_n(f, b, c);
+    }
+};
+// f *= the normalised line at lp evaluated at the point parked at pt (nothing for a point at infinity)
+DI void apply_norm_lds(fp12 &f, const u32 *lp, const uint4 *pt, bool inf) {
+    fp2 b, c;
+    fp2_load_w(b, lp);
+    fp2_load_w(c, lp + 24);
+    if (inf) return;
+    asm volatile("" ::: "memory");
+    fp x, y;
+    u32 *xw = x.v, *yw = y.v;
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        uint4 vx = pt[q * LCB_BLOCK_PTS], vy = pt[(3 + q) * LCB_BLOCK_PTS];
+        xw[4 * q] = vx.x; xw[4 * q + 1] = vx.y; xw[4 * q + 2] = vx.z; xw[4 * q + 3] = vx.w;
+        yw[4 * q] = vy.x; yw[4 * q + 1] = vy.y; yw[4 * q + 2] = vy.z; yw[4 * q + 3] = vy.w;
+    }
+    fp2_mul_fp(b, b, x);
+    fp2_mul_fp(c, c, y);
+    fp12_mul_line_n(f, b, c);
+}
+// miller2 over two normalised line sets with LDS-parked points, written as a loop over the 68 lines so the
+// squaring and the line product each appear ONCE in the code (the bit-driven form inlines the line product
+// four times: ~150 KB of loop body, beyond the instruction cache)
+DI void miller2_norm_lds(fp12 &f, const u32 *ls1, const uint4 *pt1, bool inf1, const u32 *ls2, const uint4 *pt2,
+                         bool inf2) {
+    f = fp12_one();
+    int i = 62;
+    bool add_next = false;
+#pragma unroll 1
+    for (int k = 0; k < LCB_NLINES; k++) {
+        if (add_next) {
+            add_next = false;
+        } else {
+            if (k > 0) fp12_sqr(f, f);
+            add_next = (LCB_Z_ABS >> i) & 1;
+            i--;
+        }
+#pragma unroll 1
+        for (int s = 0; s < 2; s++) {
+            const u32 *lp = (s == 0 ? ls1 : ls2) + (size_t)k * LCB_NLINE_WORDS;
+            apply_norm_lds(f, lp, s == 0 ? pt1 : pt2, s == 0 ? inf1 : inf2);
+        }
+    }
+    fp12_conj(f, f);
+}
+DI void g1_park_lds(uint4 *pt, const g1a &P) {
+    const u32 *x = P.x.v, *y = P.y.v;
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        pt[q * LCB_BLOCK_PTS] = make_uint4(x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]);
+        pt[(3 + q) * LCB_BLOCK_PTS] = make_uint4(y[4 * q], y[4 * q + 1], y[4 * q + 2], y[4 * q + 3]);
+    }
+}
 DI bool lineset_normalised(const u32 *ls) { return ls[LCB_LS_FLAG] != 0; }
 DI void lineset_point(g2a &Q, const u32 *ls) {
     fp2_load_w(Q.x, ls + LCB_LS_POINT);
