@@ -1822,6 +1822,46 @@ static void lines_precompute(oline *L, const g2 *Qp) {
         if ((Z_ABS >> i) & 1) { add_step(&X, &Y, &Z, &L[k].A, &L[k].Bc, &L[k].C, &xQ, &yQ, &FP_ONE_M, &FP_ONE_M); k++; }
     }
 }
+/* Round 2 (as the GPU, lachain_amd/csrc/pairing.hpp lineset_compute): normalise a line set to A = 1 with one
+   Fp2 inversion (Montgomery's batch trick); the Fp2 factors A^-1 change the Miller value by an Fp6 element, which
+   the final exponentiation maps to 1.  Returns 0 (set left as is) when some A == 0. */
+static int lines_normalise(oline *L) {
+    fp2 pre[OLINES], acc = FP2_ONE, inv;
+    for (int k = 0; k < OLINES; k++) {
+        fp2_mul(&acc, &acc, &L[k].A);
+        pre[k] = acc;
+    }
+    if (fp2_is_zero(&acc)) return 0;
+    fp2_inv(&inv, &acc);
+    for (int k = OLINES - 1; k >= 0; k--) {
+        fp2 ai;
+        if (k > 0) fp2_mul(&ai, &inv, &pre[k - 1]);
+        else ai = inv;
+        fp2_mul(&inv, &inv, &L[k].A);
+        fp2_mul(&L[k].Bc, &L[k].Bc, &ai);
+        fp2_mul(&L[k].C, &L[k].C, &ai);
+        L[k].A = FP2_ONE;
+    }
+    return 1;
+}
+/* f *= 1 + b v + c v w: Karatsuba over Fp6 with X = v f0, Y = v f1 — 9 Fp2 muls (pairing.hpp fp12_mul_line_n) */
+static void fp12_mul_line_n(fp12 *f, const fp2 *b, const fp2 *c) {
+    fp6 X, Y, t0, t1, s, u;
+    fp2 bc;
+    fp6_mul_v(&X, &f->c0);
+    fp6_mul_v(&Y, &f->c1);
+    fp2_mul(&t0.c0, b, &X.c0); fp2_mul(&t0.c1, b, &X.c1); fp2_mul(&t0.c2, b, &X.c2);
+    fp2_mul(&t1.c0, c, &Y.c0); fp2_mul(&t1.c1, c, &Y.c1); fp2_mul(&t1.c2, c, &Y.c2);
+    fp2_add(&bc, b, c);
+    fp6_add(&u, &X, &Y);
+    fp2_mul(&s.c0, &bc, &u.c0); fp2_mul(&s.c1, &bc, &u.c1); fp2_mul(&s.c2, &bc, &u.c2);
+    fp6_sub(&s, &s, &t0);
+    fp6_sub(&s, &s, &t1);
+    fp6_add(&f->c1, &f->c1, &s);                  /* f1 + b Y + c X */
+    fp6_mul_v(&t1, &t1);
+    fp6_add(&f->c0, &f->c0, &t0);
+    fp6_add(&f->c0, &f->c0, &t1);                 /* f0 + b X + v c Y */
+}
 /* f = f_{|z|,Q1}(P1) f_{|z|,Q2}(P2), conjugated (z < 0); a pair whose G1 point is infinity contributes 1 */
 static void miller2_lines(fp12 *f, const oline *L1, const g1 *P1, const oline *L2, const g1 *P2) {
     const oline *L[2] = {L1, L2};
@@ -1843,7 +1883,8 @@ static void miller2_lines(fp12 *f, const oline *L1, const g1 *P1, const oline *L
                 fp2 B, C;
                 fp2_mul_fp(&B, &L[j][k].Bc, &xP[j]);
                 fp2_mul_fp(&C, &L[j][k].C, &yP[j]);
-                fp12_mul_line(f, &L[j][k].A, &B, &C);
+                if (fp2_eq(&L[j][k].A, &FP2_ONE)) fp12_mul_line_n(f, &B, &C);   /* normalised set */
+                else fp12_mul_line(f, &L[j][k].A, &B, &C);
             }
     }
     fp12_conj(f, f);
@@ -1874,6 +1915,8 @@ int orc_tpke_verify_batch_amortized(uint8_t *accept, size_t n, const uint8_t *y_
         if (!ok) { memset(&h, 0, sizeof h); memset(&w, 0, sizeof w); }
         lines_precompute(LH + OLINES * c, &h);
         lines_precompute(LW + OLINES * c, &w);
+        lines_normalise(LH + OLINES * c);
+        lines_normalise(LW + OLINES * c);
     }
 #pragma omp parallel for schedule(static) num_threads(nthreads)
     for (size_t d = 0; d < n_keys; d++) {
@@ -1904,6 +1947,7 @@ int orc_ts_validate_batch_amortized(uint8_t *accept, size_t n, const uint8_t *pk
         mok[m] = (uint8_t)ok;
         if (!ok) memset(&h, 0, sizeof h);
         lines_precompute(LH + OLINES * m, &h);
+        lines_normalise(LH + OLINES * m);
     }
     g1 ngen;
     g1_neg(&ngen, &G1_GEN);
