@@ -965,6 +965,69 @@ def run_rs(args, nat, rank):
                                   sample=f"{sample} bytes ({s2} B shards), oracle orc_rs_encode_shards (ZXing-style "
                                          f"polynomial division per byte column), one thread; equal to the GPU shards"))
 
+C["C_MUL1_64"] = round(C["C_MUL1"] * 64 / 255)          # 64-bit var-base G1 multiplication (double-and-add)
+W_RLC_POINTS = C["C_DEC1"] + 2 * C["C_MUL1_64"]           # per share: decompress U_i, r_i U_i, r_i Y_i
+
+
+def run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, dd, n, n_cts, n_dec, sh):
+    """Randomized batch verify (lcb_tpke_verify_prepared_batched_dev, k_batch.hip) on the same prepared batch:
+    same timing discipline as the exact path (prepare + verify per step, warmup, barrier + synchronize)."""
+    import torch.distributed as dist
+    lib = nat.lib()
+    d_ct, d_dec, d_ui = dd
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        rc = lib.lcb_tpke_prepare_dev(*PREP_ARGS[0], sh)
+        rc |= lib.lcb_tpke_verify_prepared_batched_dev(d_acc.data_ptr(), n, n_dec, n_cts, d_ct.data_ptr(),
+                                                       d_dec.data_ptr(), d_ui.data_ptr(), sh)
+        if rc != 0:
+            raise RuntimeError(nat.last_error())
+
+    d_acc.fill_(7)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    mism = int(np.sum(d_acc.cpu().numpy() != inp["expect"])) if args.warmup > 0 else 0
+    d_acc.fill_(7)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    mism += int(np.sum(d_acc.cpu().numpy() != inp["expect"]))
+    levels, (ms_points, ms_groups) = nat.tpke_batched_stats()
+    t = torch.tensor([elapsed, float(mism), float(n)], dtype=torch.float64, device=dev)
+    if world > 1:
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        elapsed = float(tmax[0])
+    group_fpmul = C["C_ML2_NORM2"] + C["C_FE"]
+    ach = n * W_RLC_POINTS * MAC_PER_FPMUL / (ms_points * 1e-3)
+    return dict(
+        metric="BLS12-381 TPKE decryption-share verifications/sec, randomized batch check (small-exponent test)",
+        value=float(t[2]) * args.steps / elapsed, unit="share verifications/s", steps=args.steps,
+        ms_per_step=1e3 * elapsed / args.steps, decision_mismatches=int(t[1]),
+        algorithm=("per ciphertext group: e(sum r_i U_i, H) == e(sum r_i Y_i, W), secret 64-bit r_i (ChaCha20 key "
+                   "from getrandom per call); failed groups split ~sqrt(len) ways down to single shares; every "
+                   "rejection exact, false accept <= 2^-64 per group"),
+        levels=levels, device_ms={"randomise_and_group": ms_points, "group_checks": ms_groups},
+        group_checks_per_share=sum(levels) / n,
+        roofline={"bound": "valu_int32", "kernel": "k_tpke_rlc_points (+ k_rlc_groups)",
+                  "achieved": ach / 1e12, "peak": PEAK_MAC32 / 1e12, "unit": "Tmac32/s", "frac": ach / PEAK_MAC32,
+                  "work_per_share_fpmul": W_RLC_POINTS, "work_per_group_check_fpmul": group_fpmul,
+                  "group_checks_frac": sum(levels) * group_fpmul * MAC_PER_FPMUL / (ms_groups * 1e-3) / PEAK_MAC32},
+    )
+
+
+PREP_ARGS = []
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -976,6 +1039,7 @@ def main():
     ap.add_argument("--f", type=int, default=7)
     ap.add_argument("--vlen", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--tpke-batched", type=int, default=1, help="also time the randomized batch verify (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--msm-sizes", default=f"{1 << 20},{1 << 24}",
                     help="total G1 MSM points per measurement, sharded over ranks (empty = skip)")
@@ -1027,6 +1091,8 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
 
+    PREP_ARGS.append((d_y.data_ptr(), n_dec, d_u.data_ptr(), d_w.data_ptr(), d_v.data_ptr(), d_voff.data_ptr(), n_cts))
+
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
@@ -1069,6 +1135,9 @@ def main():
     got = d_acc.cpu().numpy()
     mismatches += int(np.sum(got != inp["expect"]))
 
+    batched = None
+    if args.tpke_batched:
+        batched = run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, (d_ct, d_dec, d_ui), n, n_cts, n_dec, sh)
     t = torch.tensor([elapsed, float(mismatches), float(n)], dtype=torch.float64, device=dev)
     if world > 1:
         tmax = t.clone()
@@ -1131,6 +1200,7 @@ def main():
                          "traffic_source": traffic_note},
             "source_hash": src_hash,
             "cpu_baseline": cpu,
+            "batched": batched,
             "input_gen_s": t_gen,
             "msm": msm,
             "threshold_signature": ts,

@@ -235,6 +235,26 @@ int lcb_tpke_combine_dev(uint8_t *u_out, uint8_t *status, const uint8_t *accept,
 /* device time (ms) of k_tpke_miller and k_final_exp_check in the last split TPKE verify (waits for it) */
 int lcb_tpke_verify_phase_ms(float ms[2]);
 
+/* Randomized batch form of lcb_tpke_verify_prepared_dev (same arguments, same workspace, same validity rules;
+   replaces the per-share loop over TPKE/PublicKey.cs:88-92 driven from HoneyBadger.cs:211-212).  Shares are grouped
+   into runs of one ciphertext (pass ciphertext-major batches); a group is accepted when
+   e(sum r_i U_i, H) == e(sum r_i Y_i, W) for secret 64-bit r_i (getrandom per call), a failed group is split and
+   re-checked down to single shares.  Every rejection is exact; a false acceptance has probability <= 2^-64 per group.
+   Returns when the decisions are final (one small device-to-host read per splitting level). */
+int lcb_tpke_verify_prepared_batched_dev(uint8_t *accept, size_t n_shares, size_t n_keys, size_t n_cts,
+                                         const uint32_t *ct_idx, const uint32_t *dec_idx, const uint8_t *ui,
+                                         void *stream);
+/* host-pointer form of the batched verify (arguments of lcb_tpke_verify_shares) */
+int lcb_tpke_verify_shares_batched(uint8_t *accept, size_t n_shares, const uint8_t *y_keys, size_t n_keys,
+                                   const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
+                                   const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
+                                   const uint32_t *dec_idx, const uint8_t *ui);
+/* groups checked per level of the last batched verify (levels[0] = first level) and device ms of
+   [randomisation + grouping, group checks]; returns the number of levels (waits for the call) */
+int lcb_tpke_batched_stats(uint32_t levels[8], float ms[2]);
+/* test hook: fixed 32-byte ChaCha20 key for the batch exponents (NULL restores getrandom) */
+void lcb_set_batch_seed(const uint8_t *seed32);
+
 /* ------------------------------------------------------------------ explicit execution contexts
    A context owns the device workspaces of the prepare/verify, assembly, Lagrange and MSM calls below
    (the context-less forms above use the calling thread's implicit context).  ctx == NULL selects that implicit
@@ -254,6 +274,10 @@ int lcb_ctx_tpke_partial_decrypt_prepared_dev(lcb_ctx *ctx, uint8_t *ui_out, uin
 int lcb_ctx_tpke_combine_dev(lcb_ctx *ctx, uint8_t *u_out, uint8_t *status, const uint8_t *accept,
                              const uint8_t *shares, size_t per_ct, size_t k, size_t n_cts, void *stream);
 int lcb_ctx_tpke_verify_phase_ms(lcb_ctx *ctx, float ms[2]);
+int lcb_ctx_tpke_verify_prepared_batched_dev(lcb_ctx *ctx, uint8_t *accept, size_t n_shares, size_t n_keys,
+                                             size_t n_cts, const uint32_t *ct_idx, const uint32_t *dec_idx,
+                                             const uint8_t *ui, void *stream);
+int lcb_ctx_tpke_batched_stats(lcb_ctx *ctx, uint32_t levels[8], float ms[2]);
 int lcb_ctx_ts_prepare_dev(lcb_ctx *ctx, const uint8_t *pks, size_t n_pks, const uint8_t *msg_data,
                            const uint32_t *msg_off, size_t n_msgs, void *stream);
 int lcb_ctx_ts_verify_prepared_dev(lcb_ctx *ctx, uint8_t *accept, size_t n, size_t n_pks, size_t n_msgs,

@@ -1,0 +1,244 @@
+// lachain_amd/csrc/k_batch.hip — gfx950 kernels: randomized batch verification of TPKE decryption shares
+// (small-exponent test, Bellare–Garay–Rabin 1998) over the per-share check of TPKE/PublicKey.cs:88-92.
+//
+// The reference decides every share on its own: e(U_i, H) == e(Y_i, W) (two pairings per share).  Every value
+// e(., .) is a reduced pairing, so the ratio g_i = e(U_i, H) / e(Y_i, W) lies in mu_r (order r, prime) whatever
+// U_i is (an off-subgroup U_i included: the reduced pairing is linear in its G1 argument on all of E(Fp)).  For
+// secret random 64-bit r_i != 0:  prod_i g_i^(r_i) == 1  <=>  e(sum r_i U_i, H) e(-sum r_i Y_i, W) == 1, and if some
+// g_i != 1 the product is 1 with probability <= 2^-64.  So one Miller pair + final exponentiation decides a whole
+// group of shares of one ciphertext; a group that fails is split (about sqrt(len) sub-groups) and re-checked, down to
+// single shares, where g_i^(r_i) == 1 <=> g_i == 1 (gcd(r_i, r) = 1): every rejected share is rejected by an exact
+// check of its own, every accepted share is accepted by a group check (false accept <= 2^-64 per group).
+//
+// Pipeline (host loop in lcb_host.cpp: tpke_verify_prepared_rlc):
+//   k_tpke_rlc_points   one lane per share: validity as k_tpke_miller, r_i = ChaCha20(key, i), r_i U_i and r_i Y_i
+//                       (64-bit double-and-add) -> quad-major SoA Jacobian records (invalid share: infinity)
+//   k_rlc_groups        one lane per 256 consecutive shares: runs of equal ciphertext index (<= 32) -> level-1 groups
+//   k_tpke_rlc_sum      one lane per group: the two sums, to affine with one shared inversion, -sum r_i Y_i
+//   k_tpke_rlc_miller   one lane per group: the two-pair Miller loop over the ciphertext's line sets
+//   k_final_exp_check   (k_tpke.hip) group decision
+//   k_rlc_resolve       one lane per group: failed single share -> reject; failed group -> sub-groups of the next level
+#include "kcommon.hpp"
+
+LCB_ASM_LIBRARY(k_batch)
+
+struct rlc_key { u32 k[8]; u32 nonce[2]; };   // ChaCha20 key (256 bit, from getrandom) and a per-call nonce
+
+#define LCB_RLC_RUN 32          // longest level-1 group
+#define LCB_RLC_SPAN 256        // shares scanned by one k_rlc_groups lane
+
+// ---------------------------------------------------------------- ChaCha20 (RFC 8439 block function)
+DI u32 rotl32(u32 x, int r) { return (x << r) | (x >> (32 - r)); }
+#define CHACHA_QR(a, b, c, d)                  \
+    a += b; d ^= a; d = rotl32(d, 16);         \
+    c += d; b ^= c; b = rotl32(b, 12);         \
+    a += b; d ^= a; d = rotl32(d, 8);          \
+    c += d; b ^= c; b = rotl32(b, 7);
+// 64-bit share exponent r_i: words 0, 1 of block i (counter = i); 0 -> 1 (r_i must be invertible mod r)
+DI u64 rlc_scalar(const rlc_key &key, u32 i) {
+    u32 x[16], s[16];
+    s[0] = 0x61707865u; s[1] = 0x3320646eu; s[2] = 0x79622d32u; s[3] = 0x6b206574u;
+#pragma unroll
+    for (int j = 0; j < 8; j++) s[4 + j] = key.k[j];
+    s[12] = i; s[13] = 0; s[14] = key.nonce[0]; s[15] = key.nonce[1];
+#pragma unroll
+    for (int j = 0; j < 16; j++) x[j] = s[j];
+#pragma unroll 1
+    for (int r = 0; r < 10; r++) {
+        CHACHA_QR(x[0], x[4], x[8], x[12]);
+        CHACHA_QR(x[1], x[5], x[9], x[13]);
+        CHACHA_QR(x[2], x[6], x[10], x[14]);
+        CHACHA_QR(x[3], x[7], x[11], x[15]);
+        CHACHA_QR(x[0], x[5], x[10], x[15]);
+        CHACHA_QR(x[1], x[6], x[11], x[12]);
+        CHACHA_QR(x[2], x[7], x[8], x[13]);
+        CHACHA_QR(x[3], x[4], x[9], x[14]);
+    }
+    u64 v = (u64)(x[0] + s[0]) | ((u64)(x[1] + s[1]) << 32);
+    return v ? v : 1;
+}
+
+// ---------------------------------------------------------------- quad-major SoA Jacobian G1 records (36 words)
+DI void g1_store_soa(u32 *base, size_t n, size_t i, const g1 &p) {
+    const u32 *s = (const u32 *)&p;
+#pragma unroll
+    for (int q = 0; q < 9; q++)
+        *(uint4 *)(base + ((size_t)q * n + i) * 4) = make_uint4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
+}
+DI void g1_load_soa(g1 &p, const u32 *base, size_t n, size_t i) {
+    u32 *d = (u32 *)&p;
+#pragma unroll
+    for (int q = 0; q < 9; q++) {
+        uint4 v = *(const uint4 *)(base + ((size_t)q * n + i) * 4);
+        d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+    }
+}
+DN void g1_mul64_n(g1 &r, const g1a &P, u64 k) {
+    const u32 kw[2] = {(u32)k, (u32)(k >> 32)};
+    jac_mul_aff(r, P, kw, 64);
+}
+
+// ---------------------------------------------------------------- per-share randomisation
+extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_points(const uint8_t *ct_ok, u32 n_cts, const g1a_st *keys,
+                                                       u32 n_keys, const u32 *ct_idx, const u32 *dec_idx,
+                                                       const uint8_t *ui, u32 n, rlc_key key, u32 *rU, u32 *rY,
+                                                       uint8_t *accept) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    u32 c = ct_idx[i], d = dec_idx[i];
+    bool ok = d < n_keys && c < n_cts;   // same validity rules as k_tpke_miller
+    c = c < n_cts ? c : 0;
+    ok = ok && ct_ok[c];
+    g1a Ui, Y;
+    ok = g1_decompress(Ui, ui + 48 * (size_t)i) && ok;
+    g1a_st ks = keys[d < n_keys ? d : 0];
+    ok = ok && ks.ok;
+    st_to_g1a(Y, ks);
+    g1 a, b;
+    if (ok) {
+        u64 r = rlc_scalar(key, i);
+        g1_mul64_n(a, Ui, r);
+        g1_mul64_n(b, Y, r);
+    } else {                             // an invalid share is rejected and contributes nothing to its group
+        jac_set_inf(a);
+        jac_set_inf(b);
+    }
+    g1_store_soa(rU, n, i, a);
+    g1_store_soa(rY, n, i, b);
+    accept[i] = ok;
+}
+
+// ---------------------------------------------------------------- level-1 groups: runs of one ciphertext
+// desc = {first share, length, ciphertext, 0}; order of the records is irrelevant
+extern "C" __global__ void LCB_BOUNDS k_rlc_groups(const u32 *ct_idx, u32 n, u32 n_cts, uint4 *desc, u32 *count) {
+    u32 b = blockIdx.x * blockDim.x + threadIdx.x;
+    size_t lo = (size_t)b * LCB_RLC_SPAN;
+    if (lo >= n) return;
+    u32 hi = (u32)min((size_t)n, lo + LCB_RLC_SPAN);
+    u32 start = (u32)lo, cur = ct_idx[lo];
+    cur = cur < n_cts ? cur : 0;
+    for (u32 j = (u32)lo + 1; j <= hi; j++) {
+        u32 c = 0;
+        if (j < hi) { c = ct_idx[j]; c = c < n_cts ? c : 0; }
+        if (j == hi || c != cur || j - start == LCB_RLC_RUN) {
+            u32 slot = atomicAdd(count, 1u);
+            desc[slot] = make_uint4(start, j - start, cur, 0);
+            start = j;
+            cur = c;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- group sums -> two affine points per group
+// gpts[2g] = sum r_i U_i, gpts[2g + 1] = -sum r_i Y_i (g1a_st records; inf = 1 for the point at infinity)
+extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_groups, const u32 *rU, const u32 *rY,
+                                                    u32 n, g1a_st *gpts) {
+    u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_groups) return;
+    uint4 dsc = desc[g];
+    g1 su, sy, t;
+    jac_set_inf(su);
+    jac_set_inf(sy);
+    for (u32 j = 0; j < dsc.y; j++) {
+        g1_load_soa(t, rU, n, dsc.x + j);
+        grp_add(su, su, t);
+        g1_load_soa(t, rY, n, dsc.x + j);
+        grp_add(sy, sy, t);
+    }
+    // one inversion for both: 1 / (z_u z_y), an infinite sum's z replaced by 1
+    bool iu = jac_is_inf(su), iy = jac_is_inf(sy);
+    fp zu = iu ? fp_one() : su.z, zy = iy ? fp_one() : sy.z, zz, inv, zi, zi2;
+    fp_mul(zz, zu, zy);
+    fp_inv(inv, zz);
+    g1a_st o;
+    o.ok = 1; o.pad[0] = o.pad[1] = 0;
+    fp_mul(zi, inv, zy);                 // 1 / z_u
+    fp_sqr(zi2, zi);
+    fp_mul(o.x, su.x, zi2);
+    fp_mul(zi2, zi2, zi);
+    fp_mul(o.y, su.y, zi2);
+    o.inf = iu;
+    if (iu) { o.x = fp_zero(); o.y = fp_zero(); }
+    gpts[2 * (size_t)g] = o;
+    fp_mul(zi, inv, zu);                 // 1 / z_y
+    fp_sqr(zi2, zi);
+    fp_mul(o.x, sy.x, zi2);
+    fp_mul(zi2, zi2, zi);
+    fp_mul(o.y, sy.y, zi2);
+    fp_neg(o.y, o.y);
+    o.inf = iy;
+    if (iy) { o.x = fp_zero(); o.y = fp_zero(); }
+    gpts[2 * (size_t)g + 1] = o;
+}
+
+// ---------------------------------------------------------------- group Miller loops (k_tpke_miller's loop)
+extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_rlc_miller(const u32 *lines, const uint4 *desc, const g1a_st *gpts,
+                                                            u32 n_groups, u32 *f_soa, uint8_t *gacc) {
+    __shared__ uint4 lds_pts[12 * LCB_BLOCK];
+    u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_groups) return;
+    u32 c = desc[g].z;
+    g1a P, Q;
+    st_to_g1a(P, gpts[2 * (size_t)g]);
+    st_to_g1a(Q, gpts[2 * (size_t)g + 1]);
+    fp12 f;
+    const u32 *lsH = lines + (size_t)(2 * c) * LCB_LINESET_WORDS, *lsW = lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS;
+    if (lineset_normalised(lsH) && lineset_normalised(lsW)) {
+        uint4 *pt = lds_pts + threadIdx.x;
+        g1_park_lds(pt, P);
+        g1_park_lds(pt + 6 * LCB_BLOCK_PTS, Q);
+        miller2_norm_lds(f, lsH, pt, P.inf, lsW, pt + 6 * LCB_BLOCK_PTS, Q.inf);
+    } else {
+        miller2_sets_fallback(f, lsH, P, lsW, Q);
+    }
+    fp12_store_soa(f_soa, n_groups, g, f);
+    gacc[g] = 1;
+}
+
+// ---------------------------------------------------------------- resolve a level
+// a failed group of one share rejects it; a failed group of len > 1 becomes ceil(len / s) sub-groups of s =
+// ceil(len / ceil(sqrt(len))) shares (one bad share among len then costs about 2 sqrt(len) group checks)
+extern "C" __global__ void LCB_BOUNDS k_rlc_resolve(const uint4 *desc, u32 n_groups, const uint8_t *gacc,
+                                                   uint8_t *accept, uint4 *next, u32 *next_count) {
+    u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_groups) return;
+    if (gacc[g]) return;
+    uint4 d = desc[g];
+    if (d.y == 1) { accept[d.x] = 0; return; }
+    u32 parts = 1;
+    while (parts * parts < d.y) parts++;
+    u32 s = (d.y + parts - 1) / parts;
+    u32 m = (d.y + s - 1) / s;
+    u32 slot = atomicAdd(next_count, m);
+    for (u32 k = 0; k < m; k++) {
+        u32 st = d.x + k * s, len = min(s, d.y - k * s);
+        next[slot + k] = make_uint4(st, len, d.z, 0);
+    }
+}
+
+// ---------------------------------------------------------------- host launch wrappers
+extern "C" void lcbk_tpke_rlc_points(dim3 grid, hipStream_t s, const uint8_t *ct_ok, u32 n_cts, const void *keys,
+                                     u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n,
+                                     const u32 key[10], u32 *rU, u32 *rY, uint8_t *accept) {
+    rlc_key k;
+    for (int j = 0; j < 8; j++) k.k[j] = key[j];
+    k.nonce[0] = key[8];
+    k.nonce[1] = key[9];
+    LCB_LAUNCH(k_tpke_rlc_points, ct_ok, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, k, rU, rY, accept);
+}
+extern "C" u32 lcbk_rlc_span() { return LCB_RLC_SPAN; }
+extern "C" void lcbk_rlc_groups(dim3 grid, hipStream_t s, const u32 *ct_idx, u32 n, u32 n_cts, void *desc, u32 *count) {
+    LCB_LAUNCH(k_rlc_groups, ct_idx, n, n_cts, (uint4 *)desc, count);
+}
+extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, const u32 *rU,
+                                  const u32 *rY, u32 n, void *gpts) {
+    LCB_LAUNCH(k_tpke_rlc_sum, (const uint4 *)desc, n_groups, rU, rY, n, (g1a_st *)gpts);
+}
+extern "C" void lcbk_tpke_rlc_miller(dim3 grid, hipStream_t s, const u32 *lines, const void *desc, const void *gpts,
+                                     u32 n_groups, u32 *f_soa, uint8_t *gacc) {
+    LCB_LAUNCH(k_tpke_rlc_miller, lines, (const uint4 *)desc, (const g1a_st *)gpts, n_groups, f_soa, gacc);
+}
+extern "C" void lcbk_rlc_resolve(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, const uint8_t *gacc,
+                                 uint8_t *accept, void *next, u32 *next_count) {
+    LCB_LAUNCH(k_rlc_resolve, (const uint4 *)desc, n_groups, gacc, accept, (uint4 *)next, next_count);
+}

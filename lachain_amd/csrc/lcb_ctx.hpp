@@ -51,6 +51,13 @@ struct lcb_ctx {
     DevBuf lag[3], sel[3], msm[12], in[8], out[4], dkg[6];
     hipEvent_t ver_ev[3] = {};
     bool ver_ev_ready = false, ver_ran = false;
+    // randomized batch verification (k_batch.hip): r_i U_i / r_i Y_i records, group lists, group points, counts
+    DevBuf rlc[7];
+    hipEvent_t rlc_ev[3] = {};
+    bool rlc_ev_ready = false, rlc_ran = false;
+    uint32_t rlc_levels[8] = {};
+    int rlc_nlev = 0;
+    uint64_t rlc_calls = 0;
     hipEvent_t msm_ev[7] = {};
     bool msm_ev_ready = false, msm_ran = false;
     // secp256k1 ECDSA (lcb_ecdsa.cpp): job records / header hashes / staging, and the host API's cached key set

@@ -533,6 +533,8 @@ void ctx_free(lcb_ctx *c) {
     for (auto &b : c->in) b.release();
     for (auto &b : c->out) b.release();
     for (auto &b : c->dkg) b.release();
+    for (auto &b : c->rlc) b.release();
+    if (c->rlc_ev_ready) for (auto &e : c->rlc_ev) (void)hipEventDestroy(e);
     lcb_int::ecdsa_ctx_release(c);
     if (c->ver_ev_ready) for (auto &e : c->ver_ev) (void)hipEventDestroy(e);
     if (c->msm_ev_ready) for (auto &e : c->msm_ev) (void)hipEventDestroy(e);
@@ -673,6 +675,76 @@ int tpke_partial_decrypt_prepared(lcb_ctx *c, uint8_t *ui_out, uint8_t *status, 
         lcbk_tpke_partial_decrypt(dim3(nblk(n_cts)), s, (const u32 *)c->t_lines.p, (const uint8_t *)c->t_ctok.p, cts_u,
                                   x_raw, (u32)x_stride, (u32)n_cts, ui_out, status);
     return launched("tpke partial decrypt launch") ? 0 : -1;
+}
+
+// Randomized batch verification (k_batch.hip header): the same accept / reject decisions as tpke_verify_prepared,
+// except with probability <= 2^-64 per accepted group (a false accept needs the secret 64-bit exponents).  Groups are
+// runs of shares of one ciphertext in the caller's order (ciphertext-major batches give one group per ciphertext);
+// a level's group count comes back to the host (one 4-byte read per level) to size the next launches.
+uint8_t g_rlc_seed[32];
+bool g_rlc_seed_set = false;
+int tpke_verify_prepared_rlc(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_keys, size_t n_cts, const uint32_t *d_ct,
+                             const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
+    if (!tpke_shape_ok(c, n_keys, n_cts, "tpke batched verify")) return -1;
+    if (n > 0xffffffffu) { set_err("tpke batched verify: batch too large"); return -1; }
+    c->rlc_nlev = 0;
+    if (!n) return 0;
+    u32 key[10];
+    if (g_rlc_seed_set) memcpy(key, g_rlc_seed, 32);
+    else if (getrandom(key, 32, 0) != 32) { set_err("tpke batched verify: getrandom failed"); return -1; }
+    c->rlc_calls++;
+    key[8] = (u32)c->rlc_calls;
+    key[9] = (u32)(c->rlc_calls >> 32);
+    u32 *rU = (u32 *)c->rlc[0].get(n * LCB_G1_JAC_BYTES), *rY = (u32 *)c->rlc[1].get(n * LCB_G1_JAC_BYTES);
+    uint8_t *dA = (uint8_t *)c->rlc[2].get(n * 16), *dB = (uint8_t *)c->rlc[3].get(n * 16);
+    u32 *cnt = (u32 *)c->rlc[4].get(16);
+    if (!rU || !rY || !dA || !dB || !cnt) { set_err("device allocation failed"); return -1; }
+    if (!c->rlc_ev_ready) {
+        for (auto &e : c->rlc_ev) hipEventCreate(&e);
+        c->rlc_ev_ready = true;
+    }
+    const u32 *lines = (const u32 *)c->t_lines.p;
+    hipEventRecord(c->rlc_ev[0], s);
+    hipMemsetAsync(cnt, 0, 8, s);
+    lcbk_tpke_rlc_points(dim3(nblk(n)), s, (const uint8_t *)c->t_ctok.p, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct,
+                         d_dec, d_ui, (u32)n, key, rU, rY, d_accept);
+    const size_t span = lcbk_rlc_span();
+    lcbk_rlc_groups(dim3(nblk((n + span - 1) / span)), s, d_ct, (u32)n, (u32)n_cts, dA, cnt);
+    hipEventRecord(c->rlc_ev[1], s);
+    u32 groups = 0;
+    if (hipMemcpyAsync(&groups, cnt, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+        set_err("tpke batched verify: group count");
+        return -1;
+    }
+    for (int lev = 0; groups; lev++) {
+        if (lev < 8) c->rlc_levels[lev] = groups;
+        c->rlc_nlev = lev + 1;
+        void *gpts = c->rlc[5].get((size_t)groups * 2 * LCB_G1A_ST_BYTES);
+        uint8_t *gacc = (uint8_t *)c->rlc[6].get(groups);
+        const size_t nf = groups < LCB_VERIFY_CHUNK ? groups : LCB_VERIFY_CHUNK;
+        u32 *f = (u32 *)c->t_f.get(nf * 576 * (size_t)lcbk_fe_slots());
+        if (!gpts || !gacc || !f) { set_err("device allocation failed"); return -1; }
+        hipMemsetAsync(cnt + 1, 0, 4, s);
+        lcbk_tpke_rlc_sum(dim3(nblk(groups)), s, dA, groups, rU, rY, (u32)n, gpts);
+        for (size_t o = 0; o < groups; o += LCB_VERIFY_CHUNK) {
+            const size_t m = groups - o < LCB_VERIFY_CHUNK ? groups - o : LCB_VERIFY_CHUNK;
+            lcbk_tpke_rlc_miller(dim3(nblk(m)), s, lines, dA + 16 * o, (const uint8_t *)gpts + 2 * LCB_G1A_ST_BYTES * o,
+                                 (u32)m, f, gacc + o);
+            lcbk_final_exp_check(dim3(nblk(m)), s, f, (u32)m, gacc + o);
+        }
+        lcbk_rlc_resolve(dim3(nblk(groups)), s, dA, groups, gacc, d_accept, dB, cnt + 1);
+        if (!launched("tpke batched verify launch")) return -1;
+        if (hipMemcpyAsync(&groups, cnt + 1, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            set_err("tpke batched verify: group count");
+            return -1;
+        }
+        std::swap(dA, dB);
+        if (lev > 40) { set_err("tpke batched verify: group splitting did not terminate"); return -1; }
+    }
+    hipEventRecord(c->rlc_ev[2], s);
+    c->rlc_ran = true;
+    return launched("tpke batched verify launch") ? 0 : -1;
 }
 
 // ------------------------------------------------------------------ threshold signatures
@@ -909,6 +981,34 @@ extern "C" int lcb_ctx_tpke_verify_phase_ms(lcb_ctx *ctx, float ms[2]) {
     return 0;
 }
 
+extern "C" int lcb_ctx_tpke_verify_prepared_batched_dev(lcb_ctx *ctx, uint8_t *accept, size_t n, size_t n_keys,
+                                                        size_t n_cts, const uint32_t *ct_idx, const uint32_t *dec_idx,
+                                                        const uint8_t *ui, void *stream) {
+    CTX_OR(c, ctx, -1)
+    Enq q(c, (hipStream_t)stream);
+    return tpke_verify_prepared_rlc(c, accept, n, n_keys, n_cts, ct_idx, dec_idx, ui, q.s);
+}
+extern "C" int lcb_tpke_verify_prepared_batched_dev(uint8_t *accept, size_t n, size_t n_keys, size_t n_cts,
+                                                    const uint32_t *ct_idx, const uint32_t *dec_idx, const uint8_t *ui,
+                                                    void *stream) {
+    return lcb_ctx_tpke_verify_prepared_batched_dev(nullptr, accept, n, n_keys, n_cts, ct_idx, dec_idx, ui, stream);
+}
+extern "C" int lcb_ctx_tpke_batched_stats(lcb_ctx *ctx, uint32_t levels[8], float ms[2]) {
+    CTX_OR(c, ctx, -1)
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    if (!c->rlc_ran) { set_err("tpke batched verify: none has run in this context"); return -1; }
+    if (hipEventSynchronize(c->rlc_ev[2]) != hipSuccess) { set_err("tpke batched verify: event sync"); return -1; }
+    for (int i = 0; i < 8; i++) levels[i] = i < c->rlc_nlev ? c->rlc_levels[i] : 0;
+    for (int i = 0; i < 2; i++)
+        if (hipEventElapsedTime(&ms[i], c->rlc_ev[i], c->rlc_ev[i + 1]) != hipSuccess) ms[i] = -1.0f;
+    return c->rlc_nlev;
+}
+extern "C" int lcb_tpke_batched_stats(uint32_t levels[8], float ms[2]) { return lcb_ctx_tpke_batched_stats(nullptr, levels, ms); }
+extern "C" void lcb_set_batch_seed(const uint8_t *seed32) {
+    if (seed32) { memcpy(g_rlc_seed, seed32, 32); g_rlc_seed_set = true; }
+    else g_rlc_seed_set = false;
+}
+
 extern "C" int lcb_tpke_prepare_dev(const uint8_t *y_keys, size_t n_keys, const uint8_t *cts_u, const uint8_t *cts_w,
                                     const uint8_t *v_data, const uint32_t *v_off, size_t n_cts, void *stream) {
     return lcb_ctx_tpke_prepare_dev(nullptr, y_keys, n_keys, cts_u, cts_w, v_data, v_off, n_cts, stream);
@@ -935,10 +1035,10 @@ extern "C" int lcb_tpke_verify_shares_dev(uint8_t *accept, size_t n, const uint8
     if (tpke_prepare(c, y_keys, n_keys, cts_u, cts_w, v_data, v_off, n_cts, q.s)) return -1;
     return tpke_verify_prepared(c, accept, n, n_keys, n_cts, ct_idx, dec_idx, ui, q.s);
 }
-extern "C" int lcb_tpke_verify_shares(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys,
-                                      const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
-                                      const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
-                                      const uint32_t *dec_idx, const uint8_t *ui) {
+static int tpke_verify_shares_host(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys,
+                                   const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
+                                   const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
+                                   const uint32_t *dec_idx, const uint8_t *ui, bool batched) {
     SYNC_CTX_OR(c, -1)
     for (size_t i = 0; i < n; i++) {
         if (ct_idx[i] >= n_cts) { set_err("ct_idx out of range"); return -1; }
@@ -958,9 +1058,25 @@ extern "C" int lcb_tpke_verify_shares(uint8_t *accept, size_t n, const uint8_t *
     uint8_t *dacc = (uint8_t *)c->out[0].get(n);
     if (!dy || !du || !dw || !dv || !dvo || !dct || !ddec || !dui || !dacc) { set_err("device allocation failed"); return -1; }
     if (tpke_prepare(c, dy, n_keys, du, dw, dv, dvo, n_cts, s)) return -1;
-    if (tpke_verify_prepared(c, dacc, n, n_keys, n_cts, dct, ddec, dui, s)) return -1;
+    if (batched ? tpke_verify_prepared_rlc(c, dacc, n, n_keys, n_cts, dct, ddec, dui, s)
+                : tpke_verify_prepared(c, dacc, n, n_keys, n_cts, dct, ddec, dui, s))
+        return -1;
     if (n) hipMemcpyAsync(accept, dacc, n, hipMemcpyDeviceToHost, s);
     return sync_check(c, "tpke verify") ? 0 : -1;
+}
+extern "C" int lcb_tpke_verify_shares(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys,
+                                      const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
+                                      const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
+                                      const uint32_t *dec_idx, const uint8_t *ui) {
+    return tpke_verify_shares_host(accept, n, y_keys, n_keys, cts_u, cts_w, v_data, v_off, n_cts, ct_idx, dec_idx, ui,
+                                   false);
+}
+extern "C" int lcb_tpke_verify_shares_batched(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys,
+                                              const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
+                                              const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
+                                              const uint32_t *dec_idx, const uint8_t *ui) {
+    return tpke_verify_shares_host(accept, n, y_keys, n_keys, cts_u, cts_w, v_data, v_off, n_cts, ct_idx, dec_idx, ui,
+                                   true);
 }
 
 extern "C" int lcb_tpke_partial_decrypt(uint8_t *ui_out, uint8_t *status, const uint8_t x[32], const uint8_t *cts_u,

@@ -62,6 +62,12 @@ _SIGS = {
                                             ctypes.c_void_p, c_size, ctypes.c_void_p]),
     "lcb_tpke_verify_prepared_dev": (ctypes.c_int, [ctypes.c_void_p, c_size, c_size, c_size, ctypes.c_void_p,
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "lcb_tpke_verify_shares_batched": (ctypes.c_int, [c_u8p, c_size, c_u8p, c_size, c_u8p, c_u8p, c_u8p, c_u32p,
+                                                      c_size, c_u32p, c_u32p, c_u8p]),
+    "lcb_tpke_verify_prepared_batched_dev": (ctypes.c_int, [ctypes.c_void_p, c_size, c_size, c_size, ctypes.c_void_p,
+                                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "lcb_tpke_batched_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_float)]),
+    "lcb_set_batch_seed": (None, [ctypes.c_char_p]),
     "lcb_tpke_partial_decrypt": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_u8p, c_u8p, c_u32p, c_size]),
     "lcb_tpke_encrypt_phase1": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_size]),
     "lcb_tpke_encrypt_phase2": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_u32p, c_size]),
@@ -152,7 +158,7 @@ _SIGS = {
     "lcb_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
 }
 # explicit-context forms: the context pointer first, then the same arguments as the context-less form
-for _name in ("tpke_prepare_dev", "tpke_verify_prepared_dev", "tpke_partial_decrypt_prepared_dev", "tpke_combine_dev",
+for _name in ("tpke_prepare_dev", "tpke_verify_prepared_dev", "tpke_verify_prepared_batched_dev", "tpke_batched_stats", "tpke_partial_decrypt_prepared_dev", "tpke_combine_dev",
               "tpke_verify_phase_ms", "ts_prepare_dev", "ts_verify_prepared_dev", "ts_assemble_dev", "g1_lagrange_dev",
               "g2_lagrange_dev", "g1_msm_dev", "g1_msm_glv_dev", "g1_msm_phase_ms", "ecdsa_verify_hashed_dev",
               "root_header_verify_dev", "ecdsa_pubkey_dev", "ecdsa_sign_hashed_dev", "ecdsa_phase_ms"):
@@ -220,9 +226,10 @@ def _offsets(chunks):
 
 
 # ---------------------------------------------------------------- batch wrappers (bytes in / bytes out)
-def tpke_verify_shares(y_keys, cts, shares):
+def tpke_verify_shares(y_keys, cts, shares, batched=False):
     """y_keys: list of 48-byte verification keys; cts: list of (U48, V, W96);
-    shares: list of (ct_index, decryptor_index, Ui48).  Returns list of bools."""
+    shares: list of (ct_index, decryptor_index, Ui48).  Returns list of bools.  batched=True runs the randomized
+    group check (lcb_tpke_verify_shares_batched: same decisions, false accept <= 2^-64 per group)."""
     n = len(shares)
     keep = []
     _, py = _bytes_ptr_keep(keep, b"".join(y_keys))
@@ -234,8 +241,8 @@ def tpke_verify_shares(y_keys, cts, shares):
     _, pdec = _u32_keep(keep, [s[1] for s in shares])
     _, pui = _bytes_ptr_keep(keep, b"".join(s[2] for s in shares))
     ob, po = _out(n)
-    _check(lib().lcb_tpke_verify_shares(po, n, py, len(y_keys), pu, pw, pv, pvo, len(cts), pct, pdec, pui),
-           "tpke_verify_shares")
+    fn = lib().lcb_tpke_verify_shares_batched if batched else lib().lcb_tpke_verify_shares
+    _check(fn(po, n, py, len(y_keys), pu, pw, pv, pvo, len(cts), pct, pdec, pui), "tpke_verify_shares")
     return [bool(ob[i]) for i in range(n)]
 
 
@@ -667,6 +674,19 @@ class Context:
 
 def set_original_g2_cofactor(enable):
     lib().lcb_set_original_g2_cofactor(1 if enable else 0)
+
+
+def set_batch_seed(seed32=None):
+    """fixed ChaCha20 key for the batched verify's exponents (None: getrandom per call)"""
+    lib().lcb_set_batch_seed(seed32)
+
+
+def tpke_batched_stats():
+    lv = (ctypes.c_uint32 * 8)()
+    ms = (ctypes.c_float * 2)()
+    k = lib().lcb_tpke_batched_stats(lv, ms)
+    _check(0 if k >= 0 else k, "tpke_batched_stats")
+    return list(lv[:k]), (ms[0], ms[1])
 
 
 def set_line_mode(general):

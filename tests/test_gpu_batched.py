@@ -1,0 +1,215 @@
+"""GPU parity of the randomized batch verification of TPKE decryption shares (lcb_tpke_verify_prepared_batched_dev,
+lcb_tpke_verify_shares_batched; k_batch.hip) against the oracle's per-share check (TPKE/PublicKey.cs:88-92).
+
+The batched form must give the reference's decision for every share: groups of one ciphertext's shares are accepted
+by one check of e(sum r_i U_i, H) == e(sum r_i Y_i, W), failed groups are split down to single shares.  Covered:
+the committed transcripts (wrong-player, reversed, off-subgroup, infinity shares; both line-set modes), shares with a
+cofactor-torsion component (accepted by the reference's check, so by every group containing them), corruption
+densities 0 %, 1 %, 30 % and 100 % (every share split out), shares in scattered (non-ciphertext-major) order, groups
+longer than one level-1 run, out-of-range indices through the device API, and fixed vs fresh exponent keys."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle as o
+from helpers import Drbg, R, gpu_native
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+T = json.load(open(os.path.join(HERE, "golden", "transcripts.json")))
+H = bytes.fromhex
+
+
+@pytest.fixture(scope="module")
+def nat():
+    return gpu_native()
+
+
+@pytest.fixture(scope="module")
+def tdev():
+    import torch
+    return torch, torch.device("cuda", 0)
+
+
+@pytest.fixture(params=["normalised", "on_the_fly"])
+def line_mode(nat, request):
+    nat.set_line_mode(request.param == "on_the_fly")
+    yield request.param
+    nat.set_line_mode(False)
+
+
+def up(torch, dev, b):
+    if isinstance(b, np.ndarray):
+        b = b.tobytes()
+    return torch.frombuffer(bytearray(b if len(b) else b"\0"), dtype=torch.uint8).to(dev)
+
+
+def keyset(d, n, f):
+    coeffs = [d.fr_int() for _ in range(f + 1)]
+    poly = lambda x: sum(c * pow(x, i, R) for i, c in enumerate(coeffs)) % R
+    return [poly(i + 1) for i in range(n)], poly(0)
+
+
+def off_subgroup_g1(d):
+    while True:
+        x = int.from_bytes(d.bytes(48), "little") % o.P
+        enc = bytearray(x.to_bytes(48, "little"))
+        enc[47] |= 0x80 * (d.bytes(1)[0] & 1)
+        enc = bytes(enc)
+        if o.g1_valid(enc) and enc != bytes(48) and not o.g1_in_subgroup(enc):
+            return enc
+
+
+def torsion_g1(d):
+    q = off_subgroup_g1(d)
+    return o.g1_add(o.g1_mul(q, o.fr(R - 1)), q)
+
+
+class Batch:
+    """n decryptors, c ciphertexts; good[c][j] = valid share, bad[c][j] = the share plus G (a wrong valid point)"""
+
+    def __init__(self, seed, n, f, c):
+        d = Drbg(seed)
+        self.d = d
+        xs, y_secret = keyset(d, n, f)
+        y = o.g1_mul(o.g1_gen(), o.fr(y_secret))
+        self.n, self.c = n, c
+        self.yi = [o.g1_mul(o.g1_gen(), o.fr(x)) for x in xs]
+        self.cts = [o.tpke_encrypt(y, d.bytes(32), o.fr(d.fr_int())) for _ in range(c)]
+        self.good = [[o.g1_mul(U, o.fr(x)) for x in xs] for (U, _, _) in self.cts]
+        self.bad = [[o.g1_add(s, o.g1_gen()) for s in row] for row in self.good]
+
+    def expect(self, ct, dec, share):
+        return o.g1_valid(share) and o.tpke_verify_share(self.yi[dec], *self.cts[ct], share) == 1
+
+
+def run_dev(nat, tdev, b, ct_idx, dec_idx, shares, n_keys=None, n_cts=None):
+    torch, dev = tdev
+    lib = nat.lib()
+    sh = torch.cuda.current_stream(dev).cuda_stream
+    n = len(shares) if isinstance(shares, list) else len(shares) // 48
+    d_y = up(torch, dev, b"".join(b.yi))
+    d_u = up(torch, dev, b"".join(ct[0] for ct in b.cts))
+    d_w = up(torch, dev, b"".join(ct[2] for ct in b.cts))
+    d_v = up(torch, dev, b"".join(ct[1] for ct in b.cts))
+    d_voff = up(torch, dev, np.arange(0, 32 * (b.c + 1), 32, dtype=np.uint32))
+    d_ct = up(torch, dev, np.asarray(ct_idx, dtype=np.uint32))
+    d_dec = up(torch, dev, np.asarray(dec_idx, dtype=np.uint32))
+    d_sh = up(torch, dev, b"".join(shares) if isinstance(shares, list) else shares)
+    d_acc = torch.full((n,), 7, dtype=torch.uint8, device=dev)
+    nk = b.n if n_keys is None else n_keys
+    nc = b.c if n_cts is None else n_cts
+    assert lib.lcb_tpke_prepare_dev(d_y.data_ptr(), b.n, d_u.data_ptr(), d_w.data_ptr(), d_v.data_ptr(),
+                                    d_voff.data_ptr(), b.c, sh) == 0
+    assert nk == b.n and nc == b.c
+    rc = lib.lcb_tpke_verify_prepared_batched_dev(d_acc.data_ptr(), n, nk, nc, d_ct.data_ptr(), d_dec.data_ptr(),
+                                                  d_sh.data_ptr(), sh)
+    assert rc == 0, nat.last_error()
+    torch.cuda.synchronize(dev)
+    return d_acc.cpu().numpy()
+
+
+@pytest.mark.parametrize("key", ["tpke_n4", "tpke_n22"])
+def test_batched_transcript(nat, key, line_mode):
+    t = T[key]
+    cts = [(H(c["u"]), H(c["v"]), H(c["w"])) for c in t["ciphertexts"]]
+    shares = [(ci, i, H(s)) for ci, c in enumerate(t["ciphertexts"]) for i, s in enumerate(c["shares"])]
+    got = nat.tpke_verify_shares([H(y) for y in t["y_i"]], cts, shares, batched=True)
+    assert got == [a for c in t["ciphertexts"] for a in c["accept"]]
+
+
+def test_batched_malicious_kinds_tiled(nat, tdev):
+    """4 ciphertexts x 8 decryptors with other-player, reversed, off-subgroup, doubled and cofactor-torsion shares,
+    tiled 2048 times (65,536 shares): every decision equals the oracle's, and the level-1 groups are the runs of one
+    ciphertext (one group per ciphertext row of 8)"""
+    b = Batch(b"gpu-batched-kinds", 8, 2, 4)
+    rows = [list(r) for r in b.good]
+    rows[0][1] = rows[0][2]
+    rows[1][3] = rows[1][3][::-1]
+    rows[2][5] = off_subgroup_g1(b.d)
+    rows[3][0] = o.g1_add(rows[3][0], rows[3][0])
+    rows[3][6] = o.g1_add(rows[3][6], torsion_g1(b.d))          # passes the reference's check
+    rows[2][0] = bytes(48)                                      # infinity: fails e(O, H) == e(Y, W)
+    base = [s for r in rows for s in r]
+    expect = np.array([b.expect(i // 8, i % 8, base[i]) for i in range(32)], dtype=np.uint8)
+    assert expect[3 * 8 + 6] == 1 and expect.sum() == 32 - 5
+    reps = 2048
+    ct = np.tile(np.repeat(np.arange(4, dtype=np.uint32), 8), reps)
+    dec = np.tile(np.arange(8, dtype=np.uint32), 4 * reps)
+    got = run_dev(nat, tdev, b, ct, dec, b"".join(base) * reps)
+    assert np.array_equal(got, np.tile(expect, reps))
+    levels, ms = nat.tpke_batched_stats()
+    assert levels[0] == 4 * reps and len(levels) >= 2
+
+
+@pytest.mark.parametrize("density", [0.0, 0.01, 0.3, 1.0])
+def test_batched_corruption_density(nat, tdev, density):
+    """22 decryptors (configs[1]'s N), 6 ciphertexts tiled to 8,448 shares; each share independently replaced by a
+    wrong one with the given probability"""
+    b = Batch(b"gpu-batched-density", 22, 7, 6)
+    rng = np.random.default_rng(int(density * 1000) + 5)
+    reps = 64
+    n = 6 * 22 * reps
+    bad = rng.random(n) < density
+    ct = np.tile(np.repeat(np.arange(6, dtype=np.uint32), 22), reps)
+    dec = np.tile(np.arange(22, dtype=np.uint32), 6 * reps)
+    shares = [(b.bad if bad[i] else b.good)[ct[i]][dec[i]] for i in range(n)]
+    got = run_dev(nat, tdev, b, ct, dec, shares)
+    assert np.array_equal(got, (~bad).astype(np.uint8))
+    levels, _ = nat.tpke_batched_stats()
+    assert 6 * reps <= levels[0] <= 6 * reps + n // 256 + 1   # runs of one ciphertext, cut at 256-share spans
+    if density == 0.0:
+        assert len(levels) == 1
+    if density == 1.0:
+        assert len(levels) >= 3           # every group fails and is split down to single shares
+
+
+def test_batched_scattered_order_and_long_runs(nat, tdev):
+    """shares in ciphertext-major order with 192-share runs of one ciphertext (longer than one level-1 group of
+    32), then in random order (level-1 groups of one or two shares): the same decisions either way"""
+    b = Batch(b"gpu-batched-order", 16, 5, 3)
+    rng = np.random.default_rng(11)
+    reps = 12
+    n = 3 * 16 * reps
+    bad = rng.random(n) < 0.05
+    ct = np.repeat(np.arange(3, dtype=np.uint32), 16 * reps)
+    dec = np.tile(np.arange(16, dtype=np.uint32), 3 * reps)
+    expect = (~bad).astype(np.uint8)
+    shares = [(b.bad if bad[i] else b.good)[ct[i]][dec[i]] for i in range(n)]
+    got = run_dev(nat, tdev, b, ct, dec, shares)
+    assert np.array_equal(got, expect)
+    perm = rng.permutation(n)
+    got = run_dev(nat, tdev, b, ct[perm], dec[perm], [shares[i] for i in perm])
+    assert np.array_equal(got, expect[perm])
+
+
+def test_batched_out_of_range_indices(nat, tdev):
+    """a device caller's out-of-range ciphertext or decryptor index rejects that share only"""
+    b = Batch(b"gpu-batched-range", 4, 1, 2)
+    ct = np.array([0, 0, 0, 0, 1, 1, 7, 1], dtype=np.uint32)
+    dec = np.array([0, 1, 2, 9, 0, 1, 2, 3], dtype=np.uint32)
+    shares = [b.good[min(c, 1)][min(j, 3)] for c, j in zip(ct, dec)]
+    got = run_dev(nat, tdev, b, ct, dec, shares)
+    assert got.tolist() == [1, 1, 1, 0, 1, 1, 0, 1]
+
+
+def test_batched_fixed_and_fresh_keys(nat):
+    """decisions do not depend on the exponent key: a fixed key, a second fixed key and getrandom agree with the
+    exact per-share path"""
+    b = Batch(b"gpu-batched-keys", 7, 2, 3)
+    shares = []
+    for c in range(3):
+        for j in range(7):
+            s = b.good[c][j] if (c * 7 + j) % 5 else b.bad[c][j]
+            shares.append((c, j, s))
+    exact = nat.tpke_verify_shares(b.yi, b.cts, shares)
+    try:
+        for seed in (bytes(32), bytes(range(32))):
+            nat.set_batch_seed(seed)
+            assert nat.tpke_verify_shares(b.yi, b.cts, shares, batched=True) == exact
+    finally:
+        nat.set_batch_seed(None)
+    assert nat.tpke_verify_shares(b.yi, b.cts, shares, batched=True) == exact
+    assert exact.count(False) == 5
