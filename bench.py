@@ -152,7 +152,7 @@ def to_dev(torch, dev, b):
     return torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev)
 
 
-def cpu_baseline(inp, target_s=12.0):
+def cpu_baseline(inp, target_s=12.0, batched=False):
     """configs[1] on host cores, two legs over the same shares (bounded samples, ~target_s each):
     amortized   — the GPU's algorithm: H(U||V) and the Miller lines of H and W once per ciphertext, one two-pair
                   Miller loop + ONE final exponentiation per share (orc_tpke_verify_batch_amortized);
@@ -174,7 +174,12 @@ def cpu_baseline(inp, target_s=12.0):
         acc = ctypes.create_string_buffer(n)
         ct, dc = ct_all[:n], dec_all[:n]
         t0 = time.perf_counter()
-        if amortized:
+        if amortized == "rlc":
+            rc = lib.orc_tpke_verify_batch_rlc(acc, ctypes.c_size_t(n), y, ctypes.c_size_t(n_dec), u, v,
+                                               ctypes.c_size_t(vlen), w, ctypes.c_size_t(n_cts), p(ct), p(dc),
+                                               ui[:48 * n], ctypes.c_uint64(int.from_bytes(os.urandom(8), "little")),
+                                               threads)
+        elif amortized:
             rc = lib.orc_tpke_verify_batch_amortized(acc, ctypes.c_size_t(n), y, ctypes.c_size_t(n_dec), u, v,
                                                      ctypes.c_size_t(vlen), w, ctypes.c_size_t(n_cts), p(ct), p(dc),
                                                      ui[:48 * n], threads)
@@ -187,15 +192,22 @@ def cpu_baseline(inp, target_s=12.0):
         return n, dt, mism
 
     legs = {}
-    for name, am in (("amortized", True), ("as_reference", False)):
+    fn = {"rlc": "orc_tpke_verify_batch_rlc", True: "orc_tpke_verify_batch_amortized", False: "orc_tpke_verify_batch"}
+    kinds = (("batched", "rlc"),) if batched else ()
+    for name, am in kinds + (("amortized", True), ("as_reference", False)):
         n, dt, _ = run(8 * threads * n_dec if am else 4 * threads, am)
         n, dt, mism = run(int(min(n_total, max(n, n * target_s / max(dt, 1e-3)))), am)
         legs[name] = dict(value=n / dt, unit="share verifications/s", cores=threads, kind="port",
                           sample=f"first {n} shares ({n // n_dec} ciphertexts x {n_dec}) of the same batch, "
-                                 f"{'orc_tpke_verify_batch_amortized' if am else 'orc_tpke_verify_batch'}, {build}, "
+                                 f"{fn[am]}, {build}, "
                                  f"{threads} OpenMP threads, {dt:.1f} s, {mism} decision mismatches vs expected")
-    out = dict(legs["amortized"])
-    out["algorithm"] = "amortized (the GPU's algorithm)"
+    if batched:       # like-for-like with the GPU headline: the same randomized batch algorithm on the host cores
+        out = dict(legs["batched"])
+        out["algorithm"] = "randomized batch check (the GPU's algorithm, k_batch.hip restated)"
+        out["amortized_exact"] = dict(legs["amortized"], algorithm="exact per-share check, per-ciphertext lines")
+    else:
+        out = dict(legs["amortized"])
+        out["algorithm"] = "amortized (the GPU's algorithm)"
     out["as_reference"] = legs["as_reference"]
     return out
 
@@ -966,7 +978,8 @@ def run_rs(args, nat, rank):
                                          f"polynomial division per byte column), one thread; equal to the GPU shards"))
 
 C["C_MUL1_64"] = round(C["C_MUL1"] * 64 / 255)          # 64-bit var-base G1 multiplication (double-and-add)
-W_RLC_POINTS = C["C_DEC1"] + 2 * C["C_MUL1_64"]           # per share: decompress U_i, r_i U_i, r_i Y_i
+C["C_MUL_AB32"] = round(C["C_MUL1"] * 32 / 255) + 1     # a P + b phi(P), 32-bit a, b: 32 doublings, ~32 mixed adds
+W_RLC_POINTS = C["C_DEC1"] + 2 * C["C_MUL_AB32"]          # per share: decompress U_i, s_i U_i, s_i Y_i
 
 
 def run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, dd, n, n_cts, n_dec, sh):
@@ -977,10 +990,11 @@ def run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, dd, n, n_cts, n_d
     d_ct, d_dec, d_ui = dd
     stream = torch.cuda.current_stream(dev)
 
-    def step():
-        rc = lib.lcb_tpke_prepare_dev(*PREP_ARGS[0], sh)
-        rc |= lib.lcb_tpke_verify_prepared_batched_dev(d_acc.data_ptr(), n, n_dec, n_cts, d_ct.data_ptr(),
-                                                       d_dec.data_ptr(), d_ui.data_ptr(), sh)
+    py, nk, pu, pw, pv, pvo, nc = PREP_ARGS[0]
+
+    def step():     # one call: key decompression, randomisation beside the ciphertext preparation, group checks
+        rc = lib.lcb_tpke_verify_shares_batched_dev(d_acc.data_ptr(), n, py, nk, pu, pw, pv, pvo, nc, d_ct.data_ptr(),
+                                                    d_dec.data_ptr(), d_ui.data_ptr(), sh)
         if rc != 0:
             raise RuntimeError(nat.last_error())
 
@@ -1001,28 +1015,41 @@ def run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, dd, n, n_cts, n_d
         dist.barrier()
     elapsed = time.perf_counter() - t0
     mism += int(np.sum(d_acc.cpu().numpy() != inp["expect"]))
-    levels, (ms_points, ms_groups) = nat.tpke_batched_stats()
+    levels, ms = nat.tpke_batched_stats()
+    ms_points, ms_groups, ms_sum, ms_miller, ms_fe, ms_resolve = ms
     t = torch.tensor([elapsed, float(mism), float(n)], dtype=torch.float64, device=dev)
     if world > 1:
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         elapsed = float(tmax[0])
-    group_fpmul = C["C_ML2_NORM2"] + C["C_FE"]
-    ach = n * W_RLC_POINTS * MAC_PER_FPMUL / (ms_points * 1e-3)
+    checks = sum(levels)
+    ach_pair = checks * (C["C_ML2_NORM2"] + C["C_FE"]) * MAC_PER_FPMUL / ((ms_miller + ms_fe) * 1e-3)
+    ach_pts = n * W_RLC_POINTS * MAC_PER_FPMUL / (ms_points * 1e-3)
+    step_fpmul = n * W_RLC_POINTS + checks * (C["C_ML2_NORM2"] + C["C_FE"]) + n_cts * W_PREPARE
     return dict(
         metric="BLS12-381 TPKE decryption-share verifications/sec, randomized batch check (small-exponent test)",
         value=float(t[2]) * args.steps / elapsed, unit="share verifications/s", steps=args.steps,
         ms_per_step=1e3 * elapsed / args.steps, decision_mismatches=int(t[1]),
-        algorithm=("per ciphertext group: e(sum r_i U_i, H) == e(sum r_i Y_i, W), secret 64-bit r_i (ChaCha20 key "
-                   "from getrandom per call); failed groups split ~sqrt(len) ways down to single shares; every "
-                   "rejection exact, false accept <= 2^-64 per group"),
-        levels=levels, device_ms={"randomise_and_group": ms_points, "group_checks": ms_groups},
-        group_checks_per_share=sum(levels) / n,
-        roofline={"bound": "valu_int32", "kernel": "k_tpke_rlc_points (+ k_rlc_groups)",
-                  "achieved": ach / 1e12, "peak": PEAK_MAC32 / 1e12, "unit": "Tmac32/s", "frac": ach / PEAK_MAC32,
-                  "work_per_share_fpmul": W_RLC_POINTS, "work_per_group_check_fpmul": group_fpmul,
-                  "group_checks_frac": sum(levels) * group_fpmul * MAC_PER_FPMUL / (ms_groups * 1e-3) / PEAK_MAC32},
+        algorithm=("per ciphertext group: e(sum s_i U_i, H) == e(sum s_i Y_i, W), secret s_i = a_i + b_i lambda "
+                   "(32-bit a_i, b_i from ChaCha20 keyed by getrandom per call: 2^64 exponents); failed groups split "
+                   "~sqrt(len) ways, groups <= 8 into single shares; every rejection exact, false accept <= 2^-64 "
+                   "per group"),
+        api="lcb_tpke_verify_shares_batched_dev (prepare + verify, randomisation on a second stream)",
+        levels=levels, group_checks_per_share=checks / n,
+        device_ms={"randomise_and_group (beside prepare)": ms_points, "all_levels": ms_groups, "group_sums": ms_sum,
+                   "k_tpke_rlc_miller": ms_miller, "k_final_exp_check": ms_fe, "resolve_and_count_reads": ms_resolve},
+        roofline={"bound": "valu_int32", "kernel": "k_tpke_rlc_miller + k_final_exp_check (group checks, all levels)",
+                  "achieved": ach_pair / 1e12, "peak": PEAK_MAC32 / 1e12, "unit": "Tmac32/s",
+                  "frac": ach_pair / PEAK_MAC32, "traffic": None,
+                  "work_per_group_check_fpmul": C["C_ML2_NORM2"] + C["C_FE"], "group_checks": checks,
+                  "mac_per_fpmul": MAC_PER_FPMUL, "kernel_ms": {"pair (summed over levels)": ms_miller + ms_fe},
+                  "note": ("each level is one launch of <= 1 wave per SIMD (latency-bound: one lane's serial "
+                           "pairing check), so the pair runs below its full-occupancy rate (tpke_exact.roofline)"),
+                  "kernel_frac": {"k_tpke_rlc_points (+ k_rlc_groups), beside k_tpke_ct_prepare":
+                                  ach_pts / PEAK_MAC32},
+                  "work_per_share_fpmul_randomise": W_RLC_POINTS,
+                  "step_frac": step_fpmul * MAC_PER_FPMUL / (1e-3 * 1e3 * elapsed / args.steps) / PEAK_MAC32},
     )
 
 
@@ -1039,7 +1066,10 @@ def main():
     ap.add_argument("--f", type=int, default=7)
     ap.add_argument("--vlen", type=int, default=32)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--tpke-batched", type=int, default=1, help="also time the randomized batch verify (0 = skip)")
+    ap.add_argument("--tpke-batched", type=int, default=1, help="time the randomized batch verify (0 = skip)")
+    ap.add_argument("--tpke-exact", type=int, default=1, help="time the exact per-share verify (0 = skip)")
+    ap.add_argument("--headline", choices=("batched", "exact"), default="batched",
+                    help="which TPKE path the line's value / roofline / cpu_baseline describe")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--msm-sizes", default=f"{1 << 20},{1 << 24}",
                     help="total G1 MSM points per measurement, sharded over ranks (empty = skip)")
@@ -1107,44 +1137,62 @@ def main():
         if rc != 0:
             raise RuntimeError(nat.last_error())
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    mismatches = 0
-    if args.warmup > 0:
+    exact = None
+    if args.tpke_exact:
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        mismatches = 0
+        if args.warmup > 0:
+            got = d_acc.cpu().numpy()
+            mismatches = int(np.sum(got != inp["expect"]))
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            step(evs[k])
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        prep_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+        ver_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+        kms = (ctypes.c_float * 2)()
+        if lib.lcb_tpke_verify_phase_ms(kms) != 0:      # the two kernels of the last timed step (library events)
+            raise RuntimeError(nat.last_error())
+        miller_ms, fexp_ms = float(kms[0]), float(kms[1])
         got = d_acc.cpu().numpy()
-        mismatches = int(np.sum(got != inp["expect"]))
-
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(evs[k])
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    prep_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
-    ver_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
-    kms = (ctypes.c_float * 2)()
-    if lib.lcb_tpke_verify_phase_ms(kms) != 0:      # the two kernels of the last timed step (library events)
-        raise RuntimeError(nat.last_error())
-    miller_ms, fexp_ms = float(kms[0]), float(kms[1])
-    got = d_acc.cpu().numpy()
-    mismatches += int(np.sum(got != inp["expect"]))
-
+        mismatches += int(np.sum(got != inp["expect"]))
+        t = torch.tensor([elapsed, float(mismatches), float(n)], dtype=torch.float64, device=dev)
+        if world > 1:
+            tmax = t.clone()
+            dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+            dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+            elapsed = float(tmax[0])
+        achieved = n * W_VERIFY * MAC_PER_FPMUL / (ver_ms * 1e-3)
+        exact = dict(
+            metric="BLS12-381 TPKE decryption-share verifications/sec, exact per-share check (the reference's "
+                   "algorithm: one pairing-product check per share)",
+            value=float(t[2]) * args.steps / float(t[0]), unit="share verifications/s", steps=args.steps,
+            ms_per_step=1e3 * float(t[0]) / args.steps, decision_mismatches=int(t[1]),
+            api="lcb_tpke_prepare_dev + lcb_tpke_verify_prepared_dev",
+            roofline={"bound": "valu_int32", "kernel": "k_tpke_miller + k_final_exp_check",
+                      "achieved": achieved / 1e12, "peak": PEAK_MAC32 / 1e12, "unit": "Tmac32/s",
+                      "frac": achieved / PEAK_MAC32, "work_per_share_fpmul": W_VERIFY,
+                      "mac_per_fpmul": MAC_PER_FPMUL, "verify_ms": ver_ms, "prepare_ms": prep_ms,
+                      "kernel_ms": {"k_tpke_miller": miller_ms, "k_final_exp_check": fexp_ms},
+                      "kernel_frac": {
+                          "k_tpke_miller": n * (C["C_DEC1"] + C["C_ML2_NORM2"]) * MAC_PER_FPMUL
+                          / (miller_ms * 1e-3) / PEAK_MAC32,
+                          "k_final_exp_check": n * C["C_FE"] * MAC_PER_FPMUL / (fexp_ms * 1e-3) / PEAK_MAC32}})
     batched = None
     if args.tpke_batched:
         batched = run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, (d_ct, d_dec, d_ui), n, n_cts, n_dec, sh)
-    t = torch.tensor([elapsed, float(mismatches), float(n)], dtype=torch.float64, device=dev)
-    if world > 1:
-        tmax = t.clone()
-        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        elapsed = float(tmax[0])
-    mismatches_all, shares_all = int(t[1]), int(t[2])
+    head = batched if (args.headline == "batched" and batched) else exact
+    if head is None:
+        raise SystemExit("nothing to report: --tpke-exact 0 and --tpke-batched 0")
     msm = ts = replay = ecdsa = dkg = rs = None
     if args.dkg_n > 0 and world == 1:
         dkg = run_dkg(args, nat, rank)
@@ -1159,11 +1207,8 @@ def main():
     if args.msm_sizes:
         msm = run_msm_sizes(args, nat, torch, dev, rank, world, cpu=(world == 1 and not args.no_cpu_baseline))
     if rank == 0:
-        ms_per_step = 1e3 * elapsed / args.steps
-        value = shares_all * args.steps / elapsed
-        achieved = n * W_VERIFY * MAC_PER_FPMUL / (ver_ms * 1e-3)
-        # HBM bytes per launch of the verify pair from the committed PMC passes, only if they were taken on THIS
-        # build (the file carries the source hash of the kernels it profiled; tools/pmc_to_json.py)
+        # HBM bytes per launch of the group-check / verify pair from the committed PMC passes, only if they were taken
+        # on THIS build (the file carries the source hash of the kernels it profiled; tools/pmc_to_json.py)
         traffic, traffic_note = None, "no PMC file for this build"
         src_hash = source_hash()
         pmc = os.path.join(ROOT, "profiles", "pmc_tpke_verify.json")
@@ -1173,34 +1218,37 @@ def main():
             if pj.get("source_hash") == src_hash:
                 traffic = pj.get("hbm_bytes_per_launch_at_bench_size")
                 traffic_note = (f"{pmc[len(ROOT) + 1:]}: FETCH_SIZE x2 + WRITE_SIZE (KB->B) of k_tpke_miller + "
-                                f"k_final_exp_check, source hash {src_hash}")
+                                f"k_final_exp_check at the bench launch size, source hash {src_hash}")
             else:
                 traffic_note = f"stale PMC file (profiled {pj.get('source_hash')}, this build {src_hash}): not reported"
+        if exact is not None:
+            exact["roofline"]["traffic"] = traffic
+            exact["roofline"]["traffic_source"] = traffic_note
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(inp, args.cpu_seconds)
+            cpu = cpu_baseline(inp, args.cpu_seconds, batched=batched is not None)
+        if head is batched:
+            roofline = dict(batched.pop("roofline"))
+            cpu_line = cpu
+            algo = batched["algorithm"]
+        else:
+            roofline = dict(exact.pop("roofline"))
+            cpu_line = cpu
+            algo = "exact per-share check"
         line = {
             "metric": "BLS12-381 TPKE decryption-share verifications/sec (batched VerifyShare, N=22 F=7)",
-            "value": value, "unit": "share verifications/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+            "value": head["value"], "unit": "share verifications/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": head["ms_per_step"], "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u32 (381-bit Montgomery, 12x32-bit limbs)", "data": "synthetic",
             "config": {"workload": "configs[1]: 1M TPKE decryption shares, N=22 F=7 validators, one MI355X per rank",
                        "shares_per_rank": n, "ciphertexts_per_rank": n_cts, "decryptors": n_dec, "degree": args.f,
                        "v_bytes": args.vlen, "corrupted_fraction": 0.01, "parallelism": f"shard{world}",
-                       "decision_mismatches": mismatches_all},
-            "roofline": {"bound": "valu_int32", "kernel": "k_tpke_miller + k_final_exp_check",
-                         "achieved": achieved / 1e12, "peak": PEAK_MAC32 / 1e12, "unit": "Tmac32/s",
-                         "frac": achieved / PEAK_MAC32, "traffic": traffic, "work_per_share_fpmul": W_VERIFY,
-                         "mac_per_fpmul": MAC_PER_FPMUL, "verify_ms": ver_ms, "prepare_ms": prep_ms,
-                         "kernel_ms": {"k_tpke_miller": miller_ms, "k_final_exp_check": fexp_ms},
-                         "kernel_frac": {
-                             "k_tpke_miller": n * (C["C_DEC1"] + C["C_ML2_NORM2"]) * MAC_PER_FPMUL
-                             / (miller_ms * 1e-3) / PEAK_MAC32,
-                             "k_final_exp_check": n * C["C_FE"] * MAC_PER_FPMUL / (fexp_ms * 1e-3) / PEAK_MAC32},
-                         "traffic_source": traffic_note},
+                       "decision_mismatches": head["decision_mismatches"], "algorithm": algo, "api": head["api"]},
+            "roofline": roofline,
             "source_hash": src_hash,
-            "cpu_baseline": cpu,
-            "batched": batched,
+            "cpu_baseline": cpu_line,
+            "tpke_batched": batched if head is batched else None,
+            "tpke_exact": exact,
             "input_gen_s": t_gen,
             "msm": msm,
             "threshold_signature": ts,

@@ -244,14 +244,22 @@ int lcb_tpke_verify_phase_ms(float ms[2]);
 int lcb_tpke_verify_prepared_batched_dev(uint8_t *accept, size_t n_shares, size_t n_keys, size_t n_cts,
                                          const uint32_t *ct_idx, const uint32_t *dec_idx, const uint8_t *ui,
                                          void *stream);
+/* prepare + batched verify in one call (arguments of lcb_tpke_verify_shares_dev): the per-share randomisation runs on
+   a second stream of the context beside the per-ciphertext hashing and line sets; the prepared workspace is left as
+   lcb_tpke_prepare_dev leaves it */
+int lcb_tpke_verify_shares_batched_dev(uint8_t *accept, size_t n_shares, const uint8_t *y_keys, size_t n_keys,
+                                       const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
+                                       const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
+                                       const uint32_t *dec_idx, const uint8_t *ui, void *stream);
 /* host-pointer form of the batched verify (arguments of lcb_tpke_verify_shares) */
 int lcb_tpke_verify_shares_batched(uint8_t *accept, size_t n_shares, const uint8_t *y_keys, size_t n_keys,
                                    const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
                                    const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
                                    const uint32_t *dec_idx, const uint8_t *ui);
 /* groups checked per level of the last batched verify (levels[0] = first level) and device ms of
-   [randomisation + grouping, group checks]; returns the number of levels (waits for the call) */
-int lcb_tpke_batched_stats(uint32_t levels[8], float ms[2]);
+   [randomisation + grouping, all levels, then summed over the levels: group sums, k_tpke_rlc_miller,
+   k_final_exp_check, resolve]; returns the number of levels (waits for the call) */
+int lcb_tpke_batched_stats(uint32_t levels[8], float ms[6]);
 /* test hook: fixed 32-byte ChaCha20 key for the batch exponents (NULL restores getrandom) */
 void lcb_set_batch_seed(const uint8_t *seed32);
 
@@ -277,7 +285,12 @@ int lcb_ctx_tpke_verify_phase_ms(lcb_ctx *ctx, float ms[2]);
 int lcb_ctx_tpke_verify_prepared_batched_dev(lcb_ctx *ctx, uint8_t *accept, size_t n_shares, size_t n_keys,
                                              size_t n_cts, const uint32_t *ct_idx, const uint32_t *dec_idx,
                                              const uint8_t *ui, void *stream);
-int lcb_ctx_tpke_batched_stats(lcb_ctx *ctx, uint32_t levels[8], float ms[2]);
+int lcb_ctx_tpke_verify_shares_batched_dev(lcb_ctx *ctx, uint8_t *accept, size_t n_shares, const uint8_t *y_keys,
+                                           size_t n_keys, const uint8_t *cts_u, const uint8_t *cts_w,
+                                           const uint8_t *v_data, const uint32_t *v_off, size_t n_cts,
+                                           const uint32_t *ct_idx, const uint32_t *dec_idx, const uint8_t *ui,
+                                           void *stream);
+int lcb_ctx_tpke_batched_stats(lcb_ctx *ctx, uint32_t levels[8], float ms[6]);
 int lcb_ctx_ts_prepare_dev(lcb_ctx *ctx, const uint8_t *pks, size_t n_pks, const uint8_t *msg_data,
                            const uint32_t *msg_off, size_t n_msgs, void *stream);
 int lcb_ctx_ts_verify_prepared_dev(lcb_ctx *ctx, uint8_t *accept, size_t n, size_t n_pks, size_t n_msgs,

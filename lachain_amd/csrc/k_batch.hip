@@ -3,18 +3,21 @@
 //
 // The reference decides every share on its own: e(U_i, H) == e(Y_i, W) (two pairings per share).  Every value
 // e(., .) is a reduced pairing, so the ratio g_i = e(U_i, H) / e(Y_i, W) lies in mu_r (order r, prime) whatever
-// U_i is (an off-subgroup U_i included: the reduced pairing is linear in its G1 argument on all of E(Fp)).  For
-// secret random 64-bit r_i != 0:  prod_i g_i^(r_i) == 1  <=>  e(sum r_i U_i, H) e(-sum r_i Y_i, W) == 1, and if some
-// g_i != 1 the product is 1 with probability <= 2^-64.  So one Miller pair + final exponentiation decides a whole
-// group of shares of one ciphertext; a group that fails is split (about sqrt(len) sub-groups) and re-checked, down to
-// single shares, where g_i^(r_i) == 1 <=> g_i == 1 (gcd(r_i, r) = 1): every rejected share is rejected by an exact
-// check of its own, every accepted share is accepted by a group check (false accept <= 2^-64 per group).
+// U_i is (an off-subgroup U_i included: the reduced pairing is linear in its G1 argument on all of E(Fp) and kills
+// the cofactor-torsion part).  For secret random exponents s_i (2^64 values, none 0 mod r; rlc_scalar):
+// prod_i g_i^(s_i) == 1  <=>  e(sum s_i U_i, H) e(-sum s_i Y_i, W) == 1, and if some g_i != 1 the product is 1 with
+// probability <= 2^-64.  So one Miller pair + final exponentiation decides a whole group of shares of one ciphertext;
+// a group that fails is split and re-checked, down to single shares, where g_i^(s_i) == 1 <=> g_i == 1 (gcd(s_i, r)
+// = 1): every rejected share is rejected by an exact check of its own, every accepted share by a group check (false
+// accept <= 2^-64 per group, over the secret exponents).
 //
-// Pipeline (host loop in lcb_host.cpp: tpke_verify_prepared_rlc):
-//   k_tpke_rlc_points   one lane per share: validity as k_tpke_miller, r_i = ChaCha20(key, i), r_i U_i and r_i Y_i
-//                       (64-bit double-and-add) -> quad-major SoA Jacobian records (invalid share: infinity)
+// Pipeline (host side in lcb_host.cpp: rlc_points_enqueue + rlc_levels):
+//   k_tpke_rlc_points   one lane per share: validity as k_tpke_miller, (a_i, b_i) = ChaCha20(key, i), s_i U_i and
+//                       s_i Y_i with s_i = a_i + b_i lambda (32-bit GLV form, rlc_scalar) -> quad-major SoA Jacobian
+//                       records (invalid share: infinity)
 //   k_rlc_groups        one lane per 256 consecutive shares: runs of equal ciphertext index (<= 32) -> level-1 groups
-//   k_tpke_rlc_sum      one lane per group: the two sums, to affine with one shared inversion, -sum r_i Y_i
+//   k_tpke_rlc_sum      one lane per group: ciphertext validity, the two sums, to affine with one shared inversion,
+//                       -sum r_i Y_i
 //   k_tpke_rlc_miller   one lane per group: the two-pair Miller loop over the ciphertext's line sets
 //   k_final_exp_check   (k_tpke.hip) group decision
 //   k_rlc_resolve       one lane per group: failed single share -> reject; failed group -> sub-groups of the next level
@@ -26,6 +29,7 @@ struct rlc_key { u32 k[8]; u32 nonce[2]; };   // ChaCha20 key (256 bit, from get
 
 #define LCB_RLC_RUN 32          // longest level-1 group
 #define LCB_RLC_SPAN 256        // shares scanned by one k_rlc_groups lane
+#define LCB_RLC_SINGLES 8       // a failed group this short splits into single shares
 
 // ---------------------------------------------------------------- ChaCha20 (RFC 8439 block function)
 DI u32 rotl32(u32 x, int r) { return (x << r) | (x >> (32 - r)); }
@@ -34,8 +38,12 @@ DI u32 rotl32(u32 x, int r) { return (x << r) | (x >> (32 - r)); }
     c += d; b ^= c; b = rotl32(b, 12);         \
     a += b; d ^= a; d = rotl32(d, 8);          \
     c += d; b ^= c; b = rotl32(b, 7);
-// 64-bit share exponent r_i: words 0, 1 of block i (counter = i); 0 -> 1 (r_i must be invertible mod r)
-DI u64 rlc_scalar(const rlc_key &key, u32 i) {
+// share exponent s_i = a_i + b_i lambda (lambda = z^2 - 1, phi(x, y) = (beta x, y)) from the 32-bit words a_i, b_i of
+// ChaCha20 block i: a_i P + b_i phi(P) takes 32 shared doublings.  phi acts as lambda on the r-torsion and the reduced
+// pairing kills every other component of an E(Fp) point, so e(a P + b phi(P), Q) = e(P, Q)^(a + b lambda) for ANY
+// P on the curve; the 2^64 pairs (a, b) give 2^64 distinct exponents mod r (a + b lambda < 2^160 < r), none zero
+// ((0, 0) -> (1, 0)): the soundness of a uniform 64-bit exponent.
+DI void rlc_scalar(const rlc_key &key, u32 i, u32 &a, u32 &b) {
     u32 x[16], s[16];
     s[0] = 0x61707865u; s[1] = 0x3320646eu; s[2] = 0x79622d32u; s[3] = 0x6b206574u;
 #pragma unroll
@@ -54,8 +62,9 @@ DI u64 rlc_scalar(const rlc_key &key, u32 i) {
         CHACHA_QR(x[2], x[7], x[8], x[13]);
         CHACHA_QR(x[3], x[4], x[9], x[14]);
     }
-    u64 v = (u64)(x[0] + s[0]) | ((u64)(x[1] + s[1]) << 32);
-    return v ? v : 1;
+    a = x[0] + s[0];
+    b = x[1] + s[1];
+    if ((a | b) == 0) a = 1;
 }
 
 // ---------------------------------------------------------------- quad-major SoA Jacobian G1 records (36 words)
@@ -73,38 +82,81 @@ DI void g1_load_soa(g1 &p, const u32 *base, size_t n, size_t i) {
         d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
     }
 }
-DN void g1_mul64_n(g1 &r, const g1a &P, u64 k) {
-    const u32 kw[2] = {(u32)k, (u32)(k >> 32)};
-    jac_mul_aff(r, P, kw, 64);
+// a P + b phi(P) for an affine P: 32 doublings, mixed additions of P and phi(P)
+DN void g1_mul_ab_n(g1 &r, const g1a &P, u32 a, u32 b) {
+    g1 acc;
+    jac_set_inf(acc);
+    if (!P.inf) {
+        fp beta, phx;
+        fp_load_const(beta, LCB_G1_BETA);
+        fp_mul(phx, P.x, beta);
+        for (int k = 31; k >= 0; k--) {
+            grp_dbl(acc, acc);
+            if ((a >> k) & 1) grp_madd(acc, acc, P.x, P.y);
+            if ((b >> k) & 1) grp_madd(acc, acc, phx, P.y);
+        }
+    }
+    r = acc;
+}
+
+// both multiplications in one loop with the point arithmetic inlined (two independent dependency chains per lane, no
+// call frames): a U + b phi(U) and a Y + b phi(Y).  Opt-in (LCB_RLC_JOINT): measured slower than the two calls to
+// g1_mul_ab_n (randomisation 77.7 vs 63.5 ms per 1M shares): 290 VGPRs allow one wave per SIMD instead of two.
+DI void g1_mul_ab2(g1 &ru, g1 &ry, const g1a &U, const g1a &Y, u32 a, u32 b) {
+    fp beta, pux, pyx;
+    fp_load_const(beta, LCB_G1_BETA);
+    fp_mul(pux, U.x, beta);
+    fp_mul(pyx, Y.x, beta);
+    jac_set_inf(ru);
+    jac_set_inf(ry);
+#pragma unroll 1
+    for (int k = 31; k >= 0; k--) {
+        jac_dbl(ru, ru);
+        jac_dbl(ry, ry);
+        if ((a >> k) & 1) {
+            jac_add_aff(ru, ru, U.x, U.y);
+            jac_add_aff(ry, ry, Y.x, Y.y);
+        }
+        if ((b >> k) & 1) {
+            jac_add_aff(ru, ru, pux, U.y);
+            jac_add_aff(ry, ry, pyx, Y.y);
+        }
+    }
+    if (U.inf) jac_set_inf(ru);
+    if (Y.inf) jac_set_inf(ry);
 }
 
 // ---------------------------------------------------------------- per-share randomisation
-extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_points(const uint8_t *ct_ok, u32 n_cts, const g1a_st *keys,
-                                                       u32 n_keys, const u32 *ct_idx, const u32 *dec_idx,
-                                                       const uint8_t *ui, u32 n, rlc_key key, u32 *rU, u32 *rY,
-                                                       uint8_t *accept) {
+// validity as k_tpke_miller except the ciphertext's (applied per group by k_tpke_rlc_sum, so this kernel needs only
+// the decompressed keys and may run beside the ciphertext preparation)
+extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_points(u32 n_cts, const g1a_st *keys, u32 n_keys, const u32 *ct_idx,
+                                                       const u32 *dec_idx, const uint8_t *ui, u32 n, rlc_key key,
+                                                       u32 *rU, u32 *rY, uint8_t *accept) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u32 c = ct_idx[i], d = dec_idx[i];
-    bool ok = d < n_keys && c < n_cts;   // same validity rules as k_tpke_miller
-    c = c < n_cts ? c : 0;
-    ok = ok && ct_ok[c];
+    bool ok = d < n_keys && c < n_cts;
     g1a Ui, Y;
     ok = g1_decompress(Ui, ui + 48 * (size_t)i) && ok;
     g1a_st ks = keys[d < n_keys ? d : 0];
     ok = ok && ks.ok;
     st_to_g1a(Y, ks);
-    g1 a, b;
+    g1 p, q;
     if (ok) {
-        u64 r = rlc_scalar(key, i);
-        g1_mul64_n(a, Ui, r);
-        g1_mul64_n(b, Y, r);
+        u32 a, b;
+        rlc_scalar(key, i, a, b);
+#ifdef LCB_RLC_JOINT
+        g1_mul_ab2(p, q, Ui, Y, a, b);
+#else
+        g1_mul_ab_n(p, Ui, a, b);
+        g1_mul_ab_n(q, Y, a, b);
+#endif
     } else {                             // an invalid share is rejected and contributes nothing to its group
-        jac_set_inf(a);
-        jac_set_inf(b);
+        jac_set_inf(p);
+        jac_set_inf(q);
     }
-    g1_store_soa(rU, n, i, a);
-    g1_store_soa(rY, n, i, b);
+    g1_store_soa(rU, n, i, p);
+    g1_store_soa(rY, n, i, q);
     accept[i] = ok;
 }
 
@@ -131,15 +183,20 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_groups(const u32 *ct_idx, u32 n, u32
 
 // ---------------------------------------------------------------- group sums -> two affine points per group
 // gpts[2g] = sum r_i U_i, gpts[2g + 1] = -sum r_i Y_i (g1a_st records; inf = 1 for the point at infinity)
-extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_groups, const u32 *rU, const u32 *rY,
-                                                    u32 n, g1a_st *gpts) {
+// a group of an invalid ciphertext rejects its shares and checks two points at infinity (it passes)
+extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_groups, const uint8_t *ct_ok,
+                                                    const u32 *rU, const u32 *rY, u32 n, g1a_st *gpts,
+                                                    uint8_t *accept) {
     u32 g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n_groups) return;
     uint4 dsc = desc[g];
     g1 su, sy, t;
     jac_set_inf(su);
     jac_set_inf(sy);
-    for (u32 j = 0; j < dsc.y; j++) {
+    const bool cok = ct_ok[dsc.z];
+    if (!cok)
+        for (u32 j = 0; j < dsc.y; j++) accept[dsc.x + j] = 0;
+    for (u32 j = 0; cok && j < dsc.y; j++) {
         g1_load_soa(t, rU, n, dsc.x + j);
         grp_add(su, su, t);
         g1_load_soa(t, rY, n, dsc.x + j);
@@ -197,7 +254,9 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_rlc_miller(const u32 *lines, c
 
 // ---------------------------------------------------------------- resolve a level
 // a failed group of one share rejects it; a failed group of len > 1 becomes ceil(len / s) sub-groups of s =
-// ceil(len / ceil(sqrt(len))) shares (one bad share among len then costs about 2 sqrt(len) group checks)
+// ceil(len / ceil(sqrt(len))) shares (one bad share among len then costs about 2 sqrt(len) group checks), or single
+// shares when len <= LCB_RLC_SINGLES: every level is one latency-bound launch (~one serial pairing check per lane), so
+// fewer levels beat fewer checks there
 extern "C" __global__ void LCB_BOUNDS k_rlc_resolve(const uint4 *desc, u32 n_groups, const uint8_t *gacc,
                                                    uint8_t *accept, uint4 *next, u32 *next_count) {
     u32 g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -207,7 +266,7 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_resolve(const uint4 *desc, u32 n_gro
     if (d.y == 1) { accept[d.x] = 0; return; }
     u32 parts = 1;
     while (parts * parts < d.y) parts++;
-    u32 s = (d.y + parts - 1) / parts;
+    u32 s = d.y <= LCB_RLC_SINGLES ? 1u : (d.y + parts - 1) / parts;
     u32 m = (d.y + s - 1) / s;
     u32 slot = atomicAdd(next_count, m);
     for (u32 k = 0; k < m; k++) {
@@ -217,22 +276,22 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_resolve(const uint4 *desc, u32 n_gro
 }
 
 // ---------------------------------------------------------------- host launch wrappers
-extern "C" void lcbk_tpke_rlc_points(dim3 grid, hipStream_t s, const uint8_t *ct_ok, u32 n_cts, const void *keys,
-                                     u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n,
+extern "C" void lcbk_tpke_rlc_points(dim3 grid, hipStream_t s, u32 n_cts, const void *keys, u32 n_keys,
+                                     const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n,
                                      const u32 key[10], u32 *rU, u32 *rY, uint8_t *accept) {
     rlc_key k;
     for (int j = 0; j < 8; j++) k.k[j] = key[j];
     k.nonce[0] = key[8];
     k.nonce[1] = key[9];
-    LCB_LAUNCH(k_tpke_rlc_points, ct_ok, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, k, rU, rY, accept);
+    LCB_LAUNCH(k_tpke_rlc_points, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, k, rU, rY, accept);
 }
 extern "C" u32 lcbk_rlc_span() { return LCB_RLC_SPAN; }
 extern "C" void lcbk_rlc_groups(dim3 grid, hipStream_t s, const u32 *ct_idx, u32 n, u32 n_cts, void *desc, u32 *count) {
     LCB_LAUNCH(k_rlc_groups, ct_idx, n, n_cts, (uint4 *)desc, count);
 }
-extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, const u32 *rU,
-                                  const u32 *rY, u32 n, void *gpts) {
-    LCB_LAUNCH(k_tpke_rlc_sum, (const uint4 *)desc, n_groups, rU, rY, n, (g1a_st *)gpts);
+extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, const uint8_t *ct_ok,
+                                  const u32 *rU, const u32 *rY, u32 n, void *gpts, uint8_t *accept) {
+    LCB_LAUNCH(k_tpke_rlc_sum, (const uint4 *)desc, n_groups, ct_ok, rU, rY, n, (g1a_st *)gpts, accept);
 }
 extern "C" void lcbk_tpke_rlc_miller(dim3 grid, hipStream_t s, const u32 *lines, const void *desc, const void *gpts,
                                      u32 n_groups, u32 *f_soa, uint8_t *gacc) {

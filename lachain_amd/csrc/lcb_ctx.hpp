@@ -54,10 +54,15 @@ struct lcb_ctx {
     // randomized batch verification (k_batch.hip): r_i U_i / r_i Y_i records, group lists, group points, counts
     DevBuf rlc[7];
     hipEvent_t rlc_ev[3] = {};
+    hipEvent_t rlc_lev_ev[4] = {};    // per level: before sum / Miller / final exp / resolve
+    float rlc_ms[4] = {};             // accumulated over the levels of the last call: sum, Miller, final exp, resolve
     bool rlc_ev_ready = false, rlc_ran = false;
     uint32_t rlc_levels[8] = {};
     int rlc_nlev = 0;
     uint64_t rlc_calls = 0;
+    hipStream_t aux = nullptr;        // second stream of the fused batched verify (randomisation beside preparation)
+    hipEvent_t fork_ev[2] = {};
+    bool fork_ready = false;
     hipEvent_t msm_ev[7] = {};
     bool msm_ev_ready = false, msm_ran = false;
     // secp256k1 ECDSA (lcb_ecdsa.cpp): job records / header hashes / staging, and the host API's cached key set

@@ -534,7 +534,15 @@ void ctx_free(lcb_ctx *c) {
     for (auto &b : c->out) b.release();
     for (auto &b : c->dkg) b.release();
     for (auto &b : c->rlc) b.release();
-    if (c->rlc_ev_ready) for (auto &e : c->rlc_ev) (void)hipEventDestroy(e);
+    if (c->rlc_ev_ready) {
+        for (auto &e : c->rlc_ev) (void)hipEventDestroy(e);
+        for (auto &e : c->rlc_lev_ev) (void)hipEventDestroy(e);
+    }
+    if (c->fork_ready) {
+        (void)hipStreamSynchronize(c->aux);
+        for (auto &e : c->fork_ev) (void)hipEventDestroy(e);
+        (void)hipStreamDestroy(c->aux);
+    }
     lcb_int::ecdsa_ctx_release(c);
     if (c->ver_ev_ready) for (auto &e : c->ver_ev) (void)hipEventDestroy(e);
     if (c->msm_ev_ready) for (auto &e : c->msm_ev) (void)hipEventDestroy(e);
@@ -678,45 +686,57 @@ int tpke_partial_decrypt_prepared(lcb_ctx *c, uint8_t *ui_out, uint8_t *status, 
 }
 
 // Randomized batch verification (k_batch.hip header): the same accept / reject decisions as tpke_verify_prepared,
-// except with probability <= 2^-64 per accepted group (a false accept needs the secret 64-bit exponents).  Groups are
-// runs of shares of one ciphertext in the caller's order (ciphertext-major batches give one group per ciphertext);
-// a level's group count comes back to the host (one 4-byte read per level) to size the next launches.
+// except with probability <= 2^-64 per accepted group (a false accept needs the secret exponents).  Groups are runs of
+// shares of one ciphertext in the caller's order (ciphertext-major batches give one group per ciphertext); a level's
+// group count comes back to the host (one 4-byte read per level) to size the next launches.
 uint8_t g_rlc_seed[32];
 bool g_rlc_seed_set = false;
-int tpke_verify_prepared_rlc(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_keys, size_t n_cts, const uint32_t *d_ct,
-                             const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
-    if (!tpke_shape_ok(c, n_keys, n_cts, "tpke batched verify")) return -1;
-    if (n > 0xffffffffu) { set_err("tpke batched verify: batch too large"); return -1; }
-    c->rlc_nlev = 0;
-    if (!n) return 0;
+struct RlcWs { u32 *rU, *rY; uint8_t *dA, *dB; u32 *cnt; };
+// phase 1 (needs the decompressed keys only): per-share exponent multiples + level-1 groups (count left on device)
+int rlc_points_enqueue(lcb_ctx *c, RlcWs &w, uint8_t *d_accept, size_t n, size_t n_keys, size_t n_cts,
+                       const uint32_t *d_ct, const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
     u32 key[10];
     if (g_rlc_seed_set) memcpy(key, g_rlc_seed, 32);
     else if (getrandom(key, 32, 0) != 32) { set_err("tpke batched verify: getrandom failed"); return -1; }
     c->rlc_calls++;
     key[8] = (u32)c->rlc_calls;
     key[9] = (u32)(c->rlc_calls >> 32);
-    u32 *rU = (u32 *)c->rlc[0].get(n * LCB_G1_JAC_BYTES), *rY = (u32 *)c->rlc[1].get(n * LCB_G1_JAC_BYTES);
-    uint8_t *dA = (uint8_t *)c->rlc[2].get(n * 16), *dB = (uint8_t *)c->rlc[3].get(n * 16);
-    u32 *cnt = (u32 *)c->rlc[4].get(16);
-    if (!rU || !rY || !dA || !dB || !cnt) { set_err("device allocation failed"); return -1; }
+    w.rU = (u32 *)c->rlc[0].get(n * LCB_G1_JAC_BYTES);
+    w.rY = (u32 *)c->rlc[1].get(n * LCB_G1_JAC_BYTES);
+    w.dA = (uint8_t *)c->rlc[2].get(n * 16);
+    w.dB = (uint8_t *)c->rlc[3].get(n * 16);
+    w.cnt = (u32 *)c->rlc[4].get(16);
+    if (!w.rU || !w.rY || !w.dA || !w.dB || !w.cnt) { set_err("device allocation failed"); return -1; }
     if (!c->rlc_ev_ready) {
         for (auto &e : c->rlc_ev) hipEventCreate(&e);
+        for (auto &e : c->rlc_lev_ev) hipEventCreate(&e);
         c->rlc_ev_ready = true;
     }
-    const u32 *lines = (const u32 *)c->t_lines.p;
     hipEventRecord(c->rlc_ev[0], s);
-    hipMemsetAsync(cnt, 0, 8, s);
-    lcbk_tpke_rlc_points(dim3(nblk(n)), s, (const uint8_t *)c->t_ctok.p, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct,
-                         d_dec, d_ui, (u32)n, key, rU, rY, d_accept);
+    hipMemsetAsync(w.cnt, 0, 8, s);
+    lcbk_tpke_rlc_points(dim3(nblk(n)), s, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct, d_dec, d_ui, (u32)n, key, w.rU,
+                         w.rY, d_accept);
     const size_t span = lcbk_rlc_span();
-    lcbk_rlc_groups(dim3(nblk((n + span - 1) / span)), s, d_ct, (u32)n, (u32)n_cts, dA, cnt);
+    lcbk_rlc_groups(dim3(nblk((n + span - 1) / span)), s, d_ct, (u32)n, (u32)n_cts, w.dA, w.cnt);
     hipEventRecord(c->rlc_ev[1], s);
-    u32 groups = 0;
-    if (hipMemcpyAsync(&groups, cnt, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+    return launched("tpke batched verify launch") ? 0 : -1;
+}
+bool read_count(u32 &v, const u32 *d, hipStream_t s) {
+    if (hipMemcpyAsync(&v, d, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
         set_err("tpke batched verify: group count");
-        return -1;
+        return false;
     }
+    return true;
+}
+// phase 2 (after the ciphertext preparation): group checks, level by level
+int rlc_levels(lcb_ctx *c, RlcWs &w, uint8_t *d_accept, size_t n, hipStream_t s) {
+    const u32 *lines = (const u32 *)c->t_lines.p;
+    const uint8_t *ctok = (const uint8_t *)c->t_ctok.p;
+    u32 groups = 0;
+    for (auto &m : c->rlc_ms) m = 0.0f;
+    if (!read_count(groups, w.cnt, s)) return -1;
     for (int lev = 0; groups; lev++) {
+        if (lev > 40) { set_err("tpke batched verify: group splitting did not terminate"); return -1; }
         if (lev < 8) c->rlc_levels[lev] = groups;
         c->rlc_nlev = lev + 1;
         void *gpts = c->rlc[5].get((size_t)groups * 2 * LCB_G1A_ST_BYTES);
@@ -724,27 +744,89 @@ int tpke_verify_prepared_rlc(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_k
         const size_t nf = groups < LCB_VERIFY_CHUNK ? groups : LCB_VERIFY_CHUNK;
         u32 *f = (u32 *)c->t_f.get(nf * 576 * (size_t)lcbk_fe_slots());
         if (!gpts || !gacc || !f) { set_err("device allocation failed"); return -1; }
-        hipMemsetAsync(cnt + 1, 0, 4, s);
-        lcbk_tpke_rlc_sum(dim3(nblk(groups)), s, dA, groups, rU, rY, (u32)n, gpts);
+        hipMemsetAsync(w.cnt + 1, 0, 4, s);
+        hipEvent_t *ev = c->rlc_lev_ev;
+        hipEventRecord(ev[0], s);
+        lcbk_tpke_rlc_sum(dim3(nblk(groups)), s, w.dA, groups, ctok, w.rU, w.rY, (u32)n, gpts, d_accept);
+        float ms[3] = {0, 0, 0}, t;
         for (size_t o = 0; o < groups; o += LCB_VERIFY_CHUNK) {
             const size_t m = groups - o < LCB_VERIFY_CHUNK ? groups - o : LCB_VERIFY_CHUNK;
-            lcbk_tpke_rlc_miller(dim3(nblk(m)), s, lines, dA + 16 * o, (const uint8_t *)gpts + 2 * LCB_G1A_ST_BYTES * o,
-                                 (u32)m, f, gacc + o);
+            hipEventRecord(ev[1], s);
+            lcbk_tpke_rlc_miller(dim3(nblk(m)), s, lines, w.dA + 16 * o,
+                                 (const uint8_t *)gpts + 2 * LCB_G1A_ST_BYTES * o, (u32)m, f, gacc + o);
+            hipEventRecord(ev[2], s);
             lcbk_final_exp_check(dim3(nblk(m)), s, f, (u32)m, gacc + o);
+            hipEventRecord(ev[3], s);
+            if (o == 0 && hipEventSynchronize(ev[1]) == hipSuccess && hipEventElapsedTime(&t, ev[0], ev[1]) == hipSuccess) ms[0] += t;
+            if (hipEventSynchronize(ev[3]) == hipSuccess) {
+                if (hipEventElapsedTime(&t, ev[1], ev[2]) == hipSuccess) ms[1] += t;
+                if (hipEventElapsedTime(&t, ev[2], ev[3]) == hipSuccess) ms[2] += t;
+            }
         }
-        lcbk_rlc_resolve(dim3(nblk(groups)), s, dA, groups, gacc, d_accept, dB, cnt + 1);
+        lcbk_rlc_resolve(dim3(nblk(groups)), s, w.dA, groups, gacc, d_accept, w.dB, w.cnt + 1);
+        hipEventRecord(ev[0], s);
         if (!launched("tpke batched verify launch")) return -1;
-        if (hipMemcpyAsync(&groups, cnt + 1, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess) {
-            set_err("tpke batched verify: group count");
-            return -1;
-        }
-        std::swap(dA, dB);
-        if (lev > 40) { set_err("tpke batched verify: group splitting did not terminate"); return -1; }
+        if (!read_count(groups, w.cnt + 1, s)) return -1;
+        if (hipEventElapsedTime(&t, ev[3], ev[0]) == hipSuccess) c->rlc_ms[3] += t;
+        for (int k = 0; k < 3; k++) c->rlc_ms[k] += ms[k];
+        std::swap(w.dA, w.dB);            // the next level's groups; its count was read from cnt[1]
     }
     hipEventRecord(c->rlc_ev[2], s);
     c->rlc_ran = true;
     return launched("tpke batched verify launch") ? 0 : -1;
+}
+int tpke_verify_prepared_rlc(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_keys, size_t n_cts, const uint32_t *d_ct,
+                             const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
+    if (!tpke_shape_ok(c, n_keys, n_cts, "tpke batched verify")) return -1;
+    if (n > 0xffffffffu) { set_err("tpke batched verify: batch too large"); return -1; }
+    c->rlc_nlev = 0;
+    if (!n) return 0;
+    RlcWs w;
+    if (rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, s)) return -1;
+    return rlc_levels(c, w, d_accept, n, s);
+}
+
+// prepare + batched verify in one call: the randomisation (needs only the keys) runs on the context's second
+// stream beside the per-ciphertext hashing / line sets (latency-bound: < 1 wave per SIMD for 50 K ciphertexts)
+int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const uint8_t *d_y, size_t n_keys,
+                                 const uint8_t *d_u, const uint8_t *d_w, const uint8_t *d_v, const uint32_t *d_voff,
+                                 size_t n_cts, const uint32_t *d_ct, const uint32_t *d_dec, const uint8_t *d_ui,
+                                 hipStream_t s) {
+    if (n_cts > 0xffffffffu || n_keys > 0xffffffffu || n > 0xffffffffu) { set_err("tpke batched verify: batch too large"); return -1; }
+    c->t_ready = false;
+    c->rlc_nlev = 0;
+    u32 *lines = (u32 *)c->t_lines.get((size_t)n_cts * 2 * LCB_LINESET_BYTES);
+    uint8_t *ctok = (uint8_t *)c->t_ctok.get(n_cts);
+    void *keys = c->t_keys.get(n_keys * LCB_G1A_ST_BYTES);
+    if (!lines || !ctok || !keys) { set_err("device allocation failed"); return -1; }
+    if (!c->fork_ready) {
+        hipError_t e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
+        for (auto &ev : c->fork_ev)
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e != hipSuccess) { set_err("tpke batched verify: stream creation", e); return -1; }
+        c->fork_ready = true;
+    }
+    if (n_keys) lcbk_g1_decompress(dim3(nblk(n_keys)), s, d_y, (u32)n_keys, keys);
+    RlcWs w;
+    if (n) {
+        hipEventRecord(c->fork_ev[0], s);
+        hipStreamWaitEvent(c->aux, c->fork_ev[0], 0);
+        if (rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, c->aux)) return -1;
+        hipEventRecord(c->fork_ev[1], c->aux);
+    }
+    if (n_cts) {
+        lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), s, d_u, d_w, d_v, d_voff, (u32)n_cts, lines, ctok,
+                             g_orig_cofactor | (g_line_mode << 1));
+        lcbk_lineset_fill(dim3(nblk(2 * n_cts)), s, lines, (u32)(2 * n_cts));
+    }
+    if (!launched("tpke prepare launch")) return -1;
+    c->t_n_cts = n_cts;
+    c->t_n_keys = n_keys;
+    c->t_gen++;
+    c->t_ready = true;
+    if (!n) return 0;
+    hipStreamWaitEvent(s, c->fork_ev[1], 0);
+    return rlc_levels(c, w, d_accept, n, s);
 }
 
 // ------------------------------------------------------------------ threshold signatures
@@ -988,12 +1070,29 @@ extern "C" int lcb_ctx_tpke_verify_prepared_batched_dev(lcb_ctx *ctx, uint8_t *a
     Enq q(c, (hipStream_t)stream);
     return tpke_verify_prepared_rlc(c, accept, n, n_keys, n_cts, ct_idx, dec_idx, ui, q.s);
 }
+extern "C" int lcb_ctx_tpke_verify_shares_batched_dev(lcb_ctx *ctx, uint8_t *accept, size_t n, const uint8_t *y_keys,
+                                                      size_t n_keys, const uint8_t *cts_u, const uint8_t *cts_w,
+                                                      const uint8_t *v_data, const uint32_t *v_off, size_t n_cts,
+                                                      const uint32_t *ct_idx, const uint32_t *dec_idx,
+                                                      const uint8_t *ui, void *stream) {
+    CTX_OR(c, ctx, -1)
+    Enq q(c, (hipStream_t)stream);
+    return tpke_verify_shares_rlc_fused(c, accept, n, y_keys, n_keys, cts_u, cts_w, v_data, v_off, n_cts, ct_idx,
+                                        dec_idx, ui, q.s);
+}
+extern "C" int lcb_tpke_verify_shares_batched_dev(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys,
+                                                  const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
+                                                  const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
+                                                  const uint32_t *dec_idx, const uint8_t *ui, void *stream) {
+    return lcb_ctx_tpke_verify_shares_batched_dev(nullptr, accept, n, y_keys, n_keys, cts_u, cts_w, v_data, v_off,
+                                                  n_cts, ct_idx, dec_idx, ui, stream);
+}
 extern "C" int lcb_tpke_verify_prepared_batched_dev(uint8_t *accept, size_t n, size_t n_keys, size_t n_cts,
                                                     const uint32_t *ct_idx, const uint32_t *dec_idx, const uint8_t *ui,
                                                     void *stream) {
     return lcb_ctx_tpke_verify_prepared_batched_dev(nullptr, accept, n, n_keys, n_cts, ct_idx, dec_idx, ui, stream);
 }
-extern "C" int lcb_ctx_tpke_batched_stats(lcb_ctx *ctx, uint32_t levels[8], float ms[2]) {
+extern "C" int lcb_ctx_tpke_batched_stats(lcb_ctx *ctx, uint32_t levels[8], float ms[6]) {
     CTX_OR(c, ctx, -1)
     std::lock_guard<std::recursive_mutex> lk(c->mu);
     if (!c->rlc_ran) { set_err("tpke batched verify: none has run in this context"); return -1; }
@@ -1001,9 +1100,10 @@ extern "C" int lcb_ctx_tpke_batched_stats(lcb_ctx *ctx, uint32_t levels[8], floa
     for (int i = 0; i < 8; i++) levels[i] = i < c->rlc_nlev ? c->rlc_levels[i] : 0;
     for (int i = 0; i < 2; i++)
         if (hipEventElapsedTime(&ms[i], c->rlc_ev[i], c->rlc_ev[i + 1]) != hipSuccess) ms[i] = -1.0f;
+    for (int i = 0; i < 4; i++) ms[2 + i] = c->rlc_ms[i];
     return c->rlc_nlev;
 }
-extern "C" int lcb_tpke_batched_stats(uint32_t levels[8], float ms[2]) { return lcb_ctx_tpke_batched_stats(nullptr, levels, ms); }
+extern "C" int lcb_tpke_batched_stats(uint32_t levels[8], float ms[6]) { return lcb_ctx_tpke_batched_stats(nullptr, levels, ms); }
 extern "C" void lcb_set_batch_seed(const uint8_t *seed32) {
     if (seed32) { memcpy(g_rlc_seed, seed32, 32); g_rlc_seed_set = true; }
     else g_rlc_seed_set = false;
@@ -1057,10 +1157,12 @@ static int tpke_verify_shares_host(uint8_t *accept, size_t n, const uint8_t *y_k
     const uint8_t *dui = up(c->in[7], ui, 48 * n, s);
     uint8_t *dacc = (uint8_t *)c->out[0].get(n);
     if (!dy || !du || !dw || !dv || !dvo || !dct || !ddec || !dui || !dacc) { set_err("device allocation failed"); return -1; }
-    if (tpke_prepare(c, dy, n_keys, du, dw, dv, dvo, n_cts, s)) return -1;
-    if (batched ? tpke_verify_prepared_rlc(c, dacc, n, n_keys, n_cts, dct, ddec, dui, s)
-                : tpke_verify_prepared(c, dacc, n, n_keys, n_cts, dct, ddec, dui, s))
-        return -1;
+    if (batched) {
+        if (tpke_verify_shares_rlc_fused(c, dacc, n, dy, n_keys, du, dw, dv, dvo, n_cts, dct, ddec, dui, s)) return -1;
+    } else {
+        if (tpke_prepare(c, dy, n_keys, du, dw, dv, dvo, n_cts, s)) return -1;
+        if (tpke_verify_prepared(c, dacc, n, n_keys, n_cts, dct, ddec, dui, s)) return -1;
+    }
     if (n) hipMemcpyAsync(accept, dacc, n, hipMemcpyDeviceToHost, s);
     return sync_check(c, "tpke verify") ? 0 : -1;
 }

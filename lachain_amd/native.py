@@ -64,6 +64,10 @@ _SIGS = {
                                                     ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "lcb_tpke_verify_shares_batched": (ctypes.c_int, [c_u8p, c_size, c_u8p, c_size, c_u8p, c_u8p, c_u8p, c_u32p,
                                                       c_size, c_u32p, c_u32p, c_u8p]),
+    "lcb_tpke_verify_shares_batched_dev": (ctypes.c_int, [ctypes.c_void_p, c_size, ctypes.c_void_p, c_size,
+                                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                          ctypes.c_void_p, c_size, ctypes.c_void_p, ctypes.c_void_p,
+                                                          ctypes.c_void_p, ctypes.c_void_p]),
     "lcb_tpke_verify_prepared_batched_dev": (ctypes.c_int, [ctypes.c_void_p, c_size, c_size, c_size, ctypes.c_void_p,
                                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "lcb_tpke_batched_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_float)]),
@@ -158,7 +162,8 @@ _SIGS = {
     "lcb_ctx_synchronize": (ctypes.c_int, [ctypes.c_void_p]),
 }
 # explicit-context forms: the context pointer first, then the same arguments as the context-less form
-for _name in ("tpke_prepare_dev", "tpke_verify_prepared_dev", "tpke_verify_prepared_batched_dev", "tpke_batched_stats", "tpke_partial_decrypt_prepared_dev", "tpke_combine_dev",
+for _name in ("tpke_prepare_dev", "tpke_verify_prepared_dev", "tpke_verify_prepared_batched_dev", "tpke_batched_stats",
+              "tpke_verify_shares_batched_dev", "tpke_partial_decrypt_prepared_dev", "tpke_combine_dev",
               "tpke_verify_phase_ms", "ts_prepare_dev", "ts_verify_prepared_dev", "ts_assemble_dev", "g1_lagrange_dev",
               "g2_lagrange_dev", "g1_msm_dev", "g1_msm_glv_dev", "g1_msm_phase_ms", "ecdsa_verify_hashed_dev",
               "root_header_verify_dev", "ecdsa_pubkey_dev", "ecdsa_sign_hashed_dev", "ecdsa_phase_ms"):
@@ -683,10 +688,10 @@ def set_batch_seed(seed32=None):
 
 def tpke_batched_stats():
     lv = (ctypes.c_uint32 * 8)()
-    ms = (ctypes.c_float * 2)()
+    ms = (ctypes.c_float * 6)()
     k = lib().lcb_tpke_batched_stats(lv, ms)
     _check(0 if k >= 0 else k, "tpke_batched_stats")
-    return list(lv[:k]), (ms[0], ms[1])
+    return list(lv[:k]), tuple(ms)
 
 
 def set_line_mode(general):

@@ -1964,6 +1964,177 @@ int orc_ts_validate_batch_amortized(uint8_t *accept, size_t n, const uint8_t *pk
     return 0;
 }
 
+/* ================================================================== CPU baseline, randomized batch (k_batch.hip)
+   The GPU's batched algorithm restated for the host cores: groups = runs of one ciphertext (<= 32 shares), exponents
+   s_i = a_i + b_i lambda from 32-bit a_i, b_i (splitmix64 from `seed`: the cost of the GPU's ChaCha20 is negligible
+   beside the curve arithmetic; this leg is timing and parity, not a randomness source), one two-pair Miller loop +
+   final exponentiation per group, failed groups split ceil(sqrt(len)) ways (<= 8 shares: single shares), a single
+   share decided by its own check.  Decisions equal orc_tpke_verify_batch's (tests/test_oracle.py). */
+static fp G1_BETA_O;
+static int g1_beta_ready = 0;
+static void g1_beta_init(void) {
+    if (g1_beta_ready) return;
+    /* the cube root of unity beta with (beta x, y) = lambda (x, y) on the r-torsion, lambda = z^2 - 1 */
+    u64 e[NP];
+    u128 rem = 0;
+    for (int j = NP - 1; j >= 0; j--) {   /* (p - 1) / 3 */
+        u128 cur = (rem << 64) | (j == 0 ? P[0] - 1 : P[j]);
+        e[j] = (u64)(cur / 3);
+        rem = cur % 3;
+    }
+    fp two, c, c2;
+    fp_set_u64(&two, 2);
+    fp_pow(&c, &two, e, NP);
+    fp_mul(&c2, &c, &c);
+    u64 lam[2];
+    u128 z2 = (u128)Z_ABS * Z_ABS - 1;
+    lam[0] = (u64)z2;
+    lam[1] = (u64)(z2 >> 64);
+    g1 t;
+    g1_mul_int(&t, &G1_GEN, lam, 2);
+    fp tx, ty, gx, gy, bx;
+    g1_to_affine(&tx, &ty, &t);
+    g1_to_affine(&gx, &gy, &G1_GEN);
+    fp_mul(&bx, &gx, &c);
+    G1_BETA_O = fp_eq(&bx, &tx) ? c : c2;
+    g1_beta_ready = 1;
+}
+/* p + (qx, qy), q affine and finite (madd-2007-bl; the doubling / inverse cases through the full addition) */
+static void g1_madd(g1 *r, const g1 *p, const fp *qx, const fp *qy) {
+    g1 q;
+    q.x = *qx; q.y = *qy; q.z = FP_ONE_M;
+    if (g1_is_inf(p)) { *r = q; return; }
+    fp z1z1, u2, s2, h, hh, i4, j, rr, v, t;
+    fp_sqr(&z1z1, &p->z);
+    fp_mul(&u2, qx, &z1z1);
+    fp_mul(&s2, qy, &p->z);
+    fp_mul(&s2, &s2, &z1z1);
+    if (fp_eq(&u2, &p->x)) { g1_add(r, p, &q); return; }
+    fp_sub(&h, &u2, &p->x);
+    fp_sqr(&hh, &h);
+    fp_add(&i4, &hh, &hh);
+    fp_add(&i4, &i4, &i4);
+    fp_mul(&j, &h, &i4);
+    fp_sub(&rr, &s2, &p->y);
+    fp_add(&rr, &rr, &rr);
+    fp_mul(&v, &p->x, &i4);
+    g1 o;
+    fp_sqr(&o.x, &rr);
+    fp_sub(&o.x, &o.x, &j);
+    fp_sub(&o.x, &o.x, &v);
+    fp_sub(&o.x, &o.x, &v);
+    fp_sub(&t, &v, &o.x);
+    fp_mul(&o.y, &rr, &t);
+    fp_mul(&t, &p->y, &j);
+    fp_add(&t, &t, &t);
+    fp_sub(&o.y, &o.y, &t);
+    fp_add(&o.z, &p->z, &h);
+    fp_sqr(&o.z, &o.z);
+    fp_sub(&o.z, &o.z, &z1z1);
+    fp_sub(&o.z, &o.z, &hh);
+    *r = o;
+}
+/* a P + b phi(P): 32 shared doublings */
+static void g1_mul_ab(g1 *r, const g1 *P_, uint32_t a, uint32_t b) {
+    g1_set_inf(r);
+    if (g1_is_inf(P_)) return;
+    fp x, y, px;
+    g1_to_affine(&x, &y, P_);
+    fp_mul(&px, &x, &G1_BETA_O);
+    for (int k = 31; k >= 0; k--) {
+        g1_dbl(r, r);
+        if ((a >> k) & 1) g1_madd(r, r, &x, &y);
+        if ((b >> k) & 1) g1_madd(r, r, &px, &y);
+    }
+}
+static u64 splitmix64(u64 *st) {
+    u64 z = (*st += 0x9E3779B97F4A7C15ULL);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+static void rlc_check_group(uint8_t *accept, const g1 *sU, const g1 *sY, size_t st, size_t len, const oline *LH,
+                            const oline *LW) {
+    g1 a, b;
+    g1_set_inf(&a);
+    g1_set_inf(&b);
+    for (size_t j = st; j < st + len; j++) {
+        g1_add(&a, &a, &sU[j]);
+        g1_add(&b, &b, &sY[j]);
+    }
+    if (check_pair_product(LH, &a, LW, &b)) return;      /* every (valid) share of the group accepted */
+    if (len == 1) { accept[st] = 0; return; }
+    size_t parts = 1;
+    while (parts * parts < len) parts++;
+    size_t sz = len <= 8 ? 1 : (len + parts - 1) / parts;
+    for (size_t k = st; k < st + len; k += sz) rlc_check_group(accept, sU, sY, k, (st + len - k) < sz ? st + len - k : sz, LH, LW);
+}
+int orc_tpke_verify_batch_rlc(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys, const uint8_t *cts_u,
+                              const uint8_t *cts_v, size_t vlen, const uint8_t *cts_w, size_t n_cts,
+                              const uint32_t *ct_idx, const uint32_t *dec_idx, const uint8_t *uis, uint64_t seed,
+                              int nthreads) {
+    orc_init();
+    g1_beta_init();
+    oline *LH = malloc(sizeof(oline) * OLINES * (n_cts ? n_cts : 1));
+    oline *LW = malloc(sizeof(oline) * OLINES * (n_cts ? n_cts : 1));
+    uint8_t *ctok = malloc(n_cts ? n_cts : 1);
+    g1 *Y = malloc(sizeof(g1) * (n_keys ? n_keys : 1));
+    uint8_t *kok = malloc(n_keys ? n_keys : 1);
+    g1 *sU = malloc(sizeof(g1) * (n ? n : 1)), *sY = malloc(sizeof(g1) * (n ? n : 1));
+    size_t *gst = malloc(sizeof(size_t) * (n + 1));
+    if (!LH || !LW || !ctok || !Y || !kok || !sU || !sY || !gst) {
+        free(LH); free(LW); free(ctok); free(Y); free(kok); free(sU); free(sY); free(gst);
+        return -1;
+    }
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+    for (size_t c = 0; c < n_cts; c++) {
+        g1 u; g2 w, h;
+        int ok = g1_load(&u, cts_u + 48 * c) && g2_load(&w, cts_w + 96 * c);
+        ok = ok && hash_to_g2_tpke(&h, &u, cts_v + vlen * c, vlen);
+        ctok[c] = (uint8_t)ok;
+        if (!ok) { memset(&h, 0, sizeof h); memset(&w, 0, sizeof w); }
+        lines_precompute(LH + OLINES * c, &h);
+        lines_precompute(LW + OLINES * c, &w);
+        lines_normalise(LH + OLINES * c);
+        lines_normalise(LW + OLINES * c);
+    }
+#pragma omp parallel for schedule(static) num_threads(nthreads)
+    for (size_t d = 0; d < n_keys; d++) {
+        kok[d] = (uint8_t)g1_load(&Y[d], y_keys + 48 * d);
+        if (kok[d]) g1_neg(&Y[d], &Y[d]);   /* -Y: e(sum s U, H) e(-sum s Y, W) == 1 */
+    }
+#pragma omp parallel for schedule(dynamic, 64) num_threads(nthreads)
+    for (size_t i = 0; i < n; i++) {
+        uint32_t c = ct_idx[i], d = dec_idx[i];
+        g1 ui;
+        int ok = c < n_cts && d < n_keys && ctok[c] && kok[d] && g1_load(&ui, uis + 48 * i);
+        accept[i] = (uint8_t)ok;
+        if (!ok) { g1_set_inf(&sU[i]); g1_set_inf(&sY[i]); continue; }
+        u64 st = seed ^ (0x9E3779B97F4A7C15ULL * (i + 1));
+        u64 r = splitmix64(&st);
+        uint32_t a = (uint32_t)r, b = (uint32_t)(r >> 32);
+        if ((a | b) == 0) a = 1;
+        g1_mul_ab(&sU[i], &ui, a, b);
+        g1_mul_ab(&sY[i], &Y[d], a, b);
+    }
+    size_t ng = 0;                                    /* runs of one ciphertext, at most 32 shares */
+    for (size_t i = 0; i < n;) {
+        size_t j = i + 1;
+        while (j < n && j - i < 32 && ct_idx[j] == ct_idx[i]) j++;
+        gst[ng++] = i;
+        i = j;
+    }
+    gst[ng] = n;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+    for (size_t g = 0; g < ng; g++) {
+        size_t c = ct_idx[gst[g]];
+        if (c >= n_cts) continue;                     /* its shares are already rejected */
+        rlc_check_group(accept, sU, sY, gst[g], gst[g + 1] - gst[g], LH + OLINES * c, LW + OLINES * c);
+    }
+    free(LH); free(LW); free(ctok); free(Y); free(kok); free(sU); free(sY); free(gst);
+    return 0;
+}
+
 /* ---- test hooks (oracle self-checks) ---- */
 int orc_test_cyc_sqr(uint8_t out[576], const uint8_t fb[576]) {
     orc_init();

@@ -85,7 +85,7 @@ class Batch:
         return o.g1_valid(share) and o.tpke_verify_share(self.yi[dec], *self.cts[ct], share) == 1
 
 
-def run_dev(nat, tdev, b, ct_idx, dec_idx, shares, n_keys=None, n_cts=None):
+def run_dev(nat, tdev, b, ct_idx, dec_idx, shares, n_keys=None, n_cts=None, fused=False):
     torch, dev = tdev
     lib = nat.lib()
     sh = torch.cuda.current_stream(dev).cuda_stream
@@ -101,9 +101,16 @@ def run_dev(nat, tdev, b, ct_idx, dec_idx, shares, n_keys=None, n_cts=None):
     d_acc = torch.full((n,), 7, dtype=torch.uint8, device=dev)
     nk = b.n if n_keys is None else n_keys
     nc = b.c if n_cts is None else n_cts
+    assert nk == b.n and nc == b.c
+    if fused:        # prepare + verify in one call, randomisation on the context's second stream
+        rc = lib.lcb_tpke_verify_shares_batched_dev(d_acc.data_ptr(), n, d_y.data_ptr(), nk, d_u.data_ptr(),
+                                                    d_w.data_ptr(), d_v.data_ptr(), d_voff.data_ptr(), nc,
+                                                    d_ct.data_ptr(), d_dec.data_ptr(), d_sh.data_ptr(), sh)
+        assert rc == 0, nat.last_error()
+        torch.cuda.synchronize(dev)
+        return d_acc.cpu().numpy()
     assert lib.lcb_tpke_prepare_dev(d_y.data_ptr(), b.n, d_u.data_ptr(), d_w.data_ptr(), d_v.data_ptr(),
                                     d_voff.data_ptr(), b.c, sh) == 0
-    assert nk == b.n and nc == b.c
     rc = lib.lcb_tpke_verify_prepared_batched_dev(d_acc.data_ptr(), n, nk, nc, d_ct.data_ptr(), d_dec.data_ptr(),
                                                   d_sh.data_ptr(), sh)
     assert rc == 0, nat.last_error()
@@ -142,10 +149,15 @@ def test_batched_malicious_kinds_tiled(nat, tdev):
     assert np.array_equal(got, np.tile(expect, reps))
     levels, ms = nat.tpke_batched_stats()
     assert levels[0] == 4 * reps and len(levels) >= 2
+    got = run_dev(nat, tdev, b, ct, dec, b"".join(base) * reps, fused=True)
+    assert np.array_equal(got, np.tile(expect, reps))
+    levels, ms = nat.tpke_batched_stats()
+    assert levels[0] == 4 * reps and len(levels) >= 2
 
 
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("density", [0.0, 0.01, 0.3, 1.0])
-def test_batched_corruption_density(nat, tdev, density):
+def test_batched_corruption_density(nat, tdev, density, fused):
     """22 decryptors (configs[1]'s N), 6 ciphertexts tiled to 8,448 shares; each share independently replaced by a
     wrong one with the given probability"""
     b = Batch(b"gpu-batched-density", 22, 7, 6)
@@ -156,7 +168,7 @@ def test_batched_corruption_density(nat, tdev, density):
     ct = np.tile(np.repeat(np.arange(6, dtype=np.uint32), 22), reps)
     dec = np.tile(np.arange(22, dtype=np.uint32), 6 * reps)
     shares = [(b.bad if bad[i] else b.good)[ct[i]][dec[i]] for i in range(n)]
-    got = run_dev(nat, tdev, b, ct, dec, shares)
+    got = run_dev(nat, tdev, b, ct, dec, shares, fused=fused)
     assert np.array_equal(got, (~bad).astype(np.uint8))
     levels, _ = nat.tpke_batched_stats()
     assert 6 * reps <= levels[0] <= 6 * reps + n // 256 + 1   # runs of one ciphertext, cut at 256-share spans
@@ -213,3 +225,20 @@ def test_batched_fixed_and_fresh_keys(nat):
         nat.set_batch_seed(None)
     assert nat.tpke_verify_shares(b.yi, b.cts, shares, batched=True) == exact
     assert exact.count(False) == 5
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_batched_invalid_ciphertext(nat, tdev, fused):
+    """a ciphertext whose W does not decode (TPKE.PublicKey.VerifyShare then cannot pass): all of its shares are
+    rejected, the other ciphertexts' groups are unaffected"""
+    b = Batch(b"gpu-batched-badct", 6, 1, 3)
+    u, v, w = b.cts[1]
+    b.cts[1] = (u, v, w[::-1])
+    ct = np.repeat(np.arange(3, dtype=np.uint32), 6)
+    dec = np.tile(np.arange(6, dtype=np.uint32), 3)
+    shares = [b.good[c][j] for c, j in zip(ct, dec)]
+    shares[2] = b.bad[0][2]
+    expect = [int(b.expect(c, j, s)) for c, j, s in zip(ct, dec, shares)]
+    assert expect[6:12] == [0] * 6 and sum(expect) == 11
+    got = run_dev(nat, tdev, b, ct, dec, shares, fused=fused)
+    assert got.tolist() == expect

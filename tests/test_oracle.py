@@ -235,3 +235,38 @@ def test_amortized_cpu_baselines_match_as_reference():
                                                b"".join(sigs), b"".join(msgs), p(mo), ctypes.c_size_t(2), p(mi), p(pi),
                                                2) == 0
     assert b1.raw == b2.raw and sum(b1.raw) == 4
+
+
+def test_rlc_cpu_baseline_matches_transcripts():
+    """bench.py's randomized-batch CPU leg (orc_tpke_verify_batch_rlc: the GPU's k_batch.hip algorithm on the host)
+    reproduces every decision of the committed TPKE transcripts (wrong-player, reversed, off-subgroup and infinity
+    shares), tiled 1x and 3x, under two exponent seeds"""
+    import ctypes
+    import json
+    import os
+    import numpy as np
+    from helpers import GOLDEN
+    lib = o.lib()
+    T = json.load(open(os.path.join(GOLDEN, "transcripts.json")))
+    p = lambda arr: arr.ctypes.data_as(ctypes.c_void_p)
+    H = bytes.fromhex
+    for key in ("tpke_n4", "tpke_n22"):
+        t = T[key]
+        cs = t["ciphertexts"]
+        n = len(t["y_i"])
+        assert all(len(H(c["v"])) == len(H(cs[0]["v"])) for c in cs)
+        shares = [H(s) for c in cs for s in c["shares"]]
+        for rep in (1, 3):                      # a 3-fold tiling puts several runs of one ciphertext in a row
+            sh = shares * rep
+            m = len(sh)
+            ct = np.tile(np.repeat(np.arange(len(cs), dtype=np.uint32), n), rep)
+            dec = np.tile(np.arange(n, dtype=np.uint32), len(cs) * rep)
+            expect = bytes([a for c in cs for a in c["accept"]] * rep)
+            for seed in (1, 0xDEADBEEF):
+                acc = ctypes.create_string_buffer(m)
+                assert lib.orc_tpke_verify_batch_rlc(
+                    acc, ctypes.c_size_t(m), b"".join(H(y) for y in t["y_i"]), ctypes.c_size_t(n),
+                    b"".join(H(c["u"]) for c in cs), b"".join(H(c["v"]) for c in cs), ctypes.c_size_t(len(H(cs[0]["v"]))),
+                    b"".join(H(c["w"]) for c in cs), ctypes.c_size_t(len(cs)), p(ct), p(dec), b"".join(sh),
+                    ctypes.c_uint64(seed), 2) == 0
+                assert acc.raw == expect, (key, rep, seed)
