@@ -3,8 +3,10 @@
 //
 // The reference decides every share on its own: e(U_i, H) == e(Y_i, W) (two pairings per share).  Every value
 // e(., .) is a reduced pairing, so the ratio g_i = e(U_i, H) / e(Y_i, W) lies in mu_r (order r, prime) whatever
-// U_i is (an off-subgroup U_i included: the reduced pairing is linear in its G1 argument on all of E(Fp) and kills
-// the cofactor-torsion part).  For secret random exponents s_i (2^64 values, none 0 mod r; rlc_scalar):
+// U_i is: for a G2 point Q the (ate) pairing is linear in its G1 argument on all of E(Fp) (Weil reciprocity; the
+// error term is an r-th power, killed by the final exponentiation) and kills the cofactor-torsion part, so off-
+// subgroup U_i / Y_i are covered.  H is in G2 by construction; W is checked (k_tpke_ct_g2check) and a ciphertext with
+// W outside G2 gets exact per-share checks.  For secret random exponents s_i (2^64 values, none 0 mod r; rlc_scalar):
 // prod_i g_i^(s_i) == 1  <=>  e(sum s_i U_i, H) e(-sum s_i Y_i, W) == 1, and if some g_i != 1 the product is 1 with
 // probability <= 2^-64.  So one Miller pair + final exponentiation decides a whole group of shares of one ciphertext;
 // a group that fails is split and re-checked, down to single shares, where g_i^(s_i) == 1 <=> g_i == 1 (gcd(s_i, r)
@@ -16,8 +18,9 @@
 //                       s_i Y_i with s_i = a_i + b_i lambda (32-bit GLV form, rlc_scalar) -> quad-major SoA Jacobian
 //                       records (invalid share: infinity)
 //   k_rlc_groups        one lane per 256 consecutive shares: runs of equal ciphertext index (<= 32) -> level-1 groups
+//   k_tpke_ct_g2check   one lane per ciphertext: W in G2 (else its shares get exact per-share checks)
 //   k_tpke_rlc_sum      one lane per group: ciphertext validity, the two sums, to affine with one shared inversion,
-//                       -sum r_i Y_i
+//                       -sum s_i Y_i (or an exact single share's own U_i, -Y_i)
 //   k_tpke_rlc_miller   one lane per group: the two-pair Miller loop over the ciphertext's line sets
 //   k_final_exp_check   (k_tpke.hip) group decision
 //   k_rlc_resolve       one lane per group: failed single share -> reject; failed group -> sub-groups of the next level
@@ -182,21 +185,53 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_groups(const u32 *ct_idx, u32 n, u32
 }
 
 // ---------------------------------------------------------------- group sums -> two affine points per group
-// gpts[2g] = sum r_i U_i, gpts[2g + 1] = -sum r_i Y_i (g1a_st records; inf = 1 for the point at infinity)
-// a group of an invalid ciphertext rejects its shares and checks two points at infinity (it passes)
+// gpts[2g] = sum s_i U_i, gpts[2g + 1] = -sum s_i Y_i (g1a_st records; inf = 1 for the point at infinity).
+// desc.w = 0: a randomized group.  A group of an invalid ciphertext rejects its shares; a group whose ciphertext's W
+// is outside G2 (the pairing is linear in its G1 argument only for a G2 point: W comes from the wire unchecked) is
+// handed to exact checks (gexact = 1: resolve re-emits its shares as desc.w = 1 singles).  Both check two points at
+// infinity (they pass).  desc.w = 1: the exact single check of share desc.x, e(U_i, H) e(-Y_i, W) == 1 as
+// k_tpke_miller does it (a share already rejected checks infinity).
 extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_groups, const uint8_t *ct_ok,
-                                                    const u32 *rU, const u32 *rY, u32 n, g1a_st *gpts,
-                                                    uint8_t *accept) {
+                                                    const uint8_t *ct_g2, const g1a_st *keys, u32 n_keys,
+                                                    const u32 *dec_idx, const uint8_t *ui, const u32 *rU,
+                                                    const u32 *rY, u32 n, g1a_st *gpts, uint8_t *accept,
+                                                    uint8_t *gexact) {
     u32 g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n_groups) return;
     uint4 dsc = desc[g];
+    g1a_st o;
+    o.ok = 1; o.pad[0] = o.pad[1] = 0;
+    o.inf = 1; o.x = fp_zero(); o.y = fp_zero();
+    gexact[g] = 0;
+    if (dsc.w == 1) {                    // exact single
+        g1a U, Y;
+        bool live = accept[dsc.x] != 0;
+        if (live) {
+            u32 d = dec_idx[dsc.x];
+            live = g1_decompress(U, ui + 48 * (size_t)dsc.x) && d < n_keys;
+            st_to_g1a(Y, keys[d < n_keys ? d : 0]);
+        }
+        if (live && !U.inf) { o.x = U.x; o.y = U.y; o.inf = 0; }
+        gpts[2 * (size_t)g] = o;
+        o.inf = 1; o.x = fp_zero(); o.y = fp_zero();
+        if (live && !Y.inf) { o.x = Y.x; fp_neg(o.y, Y.y); o.inf = 0; }
+        gpts[2 * (size_t)g + 1] = o;
+        return;
+    }
+    const bool cok = ct_ok[dsc.z];
+    if (!cok || !ct_g2[dsc.z]) {
+        if (!cok)
+            for (u32 j = 0; j < dsc.y; j++) accept[dsc.x + j] = 0;
+        else
+            gexact[g] = 1;
+        gpts[2 * (size_t)g] = o;
+        gpts[2 * (size_t)g + 1] = o;
+        return;
+    }
     g1 su, sy, t;
     jac_set_inf(su);
     jac_set_inf(sy);
-    const bool cok = ct_ok[dsc.z];
-    if (!cok)
-        for (u32 j = 0; j < dsc.y; j++) accept[dsc.x + j] = 0;
-    for (u32 j = 0; cok && j < dsc.y; j++) {
+    for (u32 j = 0; j < dsc.y; j++) {
         g1_load_soa(t, rU, n, dsc.x + j);
         grp_add(su, su, t);
         g1_load_soa(t, rY, n, dsc.x + j);
@@ -207,8 +242,6 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_gr
     fp zu = iu ? fp_one() : su.z, zy = iy ? fp_one() : sy.z, zz, inv, zi, zi2;
     fp_mul(zz, zu, zy);
     fp_inv(inv, zz);
-    g1a_st o;
-    o.ok = 1; o.pad[0] = o.pad[1] = 0;
     fp_mul(zi, inv, zy);                 // 1 / z_u
     fp_sqr(zi2, zi);
     fp_mul(o.x, su.x, zi2);
@@ -226,6 +259,17 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_gr
     o.inf = iy;
     if (iy) { o.x = fp_zero(); o.y = fp_zero(); }
     gpts[2 * (size_t)g + 1] = o;
+}
+
+// W of every ciphertext in G2 (Scott's psi test, curve.hpp g2_in_subgroup); H = hash-to-G2 output is in G2 by
+// construction
+extern "C" __global__ void LCB_BOUNDS k_tpke_ct_g2check(const u32 *lines, const uint8_t *ct_ok, u32 n_cts,
+                                                       uint8_t *ct_g2) {
+    u32 c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_cts) return;
+    g2a W;
+    lineset_point(W, lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS);
+    ct_g2[c] = ct_ok[c] ? g2_in_subgroup(W) : 0;
 }
 
 // ---------------------------------------------------------------- group Miller loops (k_tpke_miller's loop)
@@ -258,11 +302,17 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_rlc_miller(const u32 *lines, c
 // shares when len <= LCB_RLC_SINGLES: every level is one latency-bound launch (~one serial pairing check per lane), so
 // fewer levels beat fewer checks there
 extern "C" __global__ void LCB_BOUNDS k_rlc_resolve(const uint4 *desc, u32 n_groups, const uint8_t *gacc,
-                                                   uint8_t *accept, uint4 *next, u32 *next_count) {
+                                                   const uint8_t *gexact, uint8_t *accept, uint4 *next,
+                                                   u32 *next_count) {
     u32 g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n_groups) return;
-    if (gacc[g]) return;
     uint4 d = desc[g];
+    if (gexact[g]) {                     // W outside G2: every share of the group gets its exact check
+        u32 slot = atomicAdd(next_count, d.y);
+        for (u32 k = 0; k < d.y; k++) next[slot + k] = make_uint4(d.x + k, 1, d.z, 1);
+        return;
+    }
+    if (gacc[g]) return;
     if (d.y == 1) { accept[d.x] = 0; return; }
     u32 parts = 1;
     while (parts * parts < d.y) parts++;
@@ -271,7 +321,7 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_resolve(const uint4 *desc, u32 n_gro
     u32 slot = atomicAdd(next_count, m);
     for (u32 k = 0; k < m; k++) {
         u32 st = d.x + k * s, len = min(s, d.y - k * s);
-        next[slot + k] = make_uint4(st, len, d.z, 0);
+        next[slot + k] = make_uint4(st, len, d.z, 0);     // (a failed exact single has d.y == 1: rejected above)
     }
 }
 
@@ -290,14 +340,21 @@ extern "C" void lcbk_rlc_groups(dim3 grid, hipStream_t s, const u32 *ct_idx, u32
     LCB_LAUNCH(k_rlc_groups, ct_idx, n, n_cts, (uint4 *)desc, count);
 }
 extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, const uint8_t *ct_ok,
-                                  const u32 *rU, const u32 *rY, u32 n, void *gpts, uint8_t *accept) {
-    LCB_LAUNCH(k_tpke_rlc_sum, (const uint4 *)desc, n_groups, ct_ok, rU, rY, n, (g1a_st *)gpts, accept);
+                                  const uint8_t *ct_g2, const void *keys, u32 n_keys, const u32 *dec_idx,
+                                  const uint8_t *ui, const u32 *rU, const u32 *rY, u32 n, void *gpts,
+                                  uint8_t *accept, uint8_t *gexact) {
+    LCB_LAUNCH(k_tpke_rlc_sum, (const uint4 *)desc, n_groups, ct_ok, ct_g2, (const g1a_st *)keys, n_keys, dec_idx, ui,
+               rU, rY, n, (g1a_st *)gpts, accept, gexact);
+}
+extern "C" void lcbk_tpke_ct_g2check(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts,
+                                     uint8_t *ct_g2) {
+    LCB_LAUNCH(k_tpke_ct_g2check, lines, ct_ok, n_cts, ct_g2);
 }
 extern "C" void lcbk_tpke_rlc_miller(dim3 grid, hipStream_t s, const u32 *lines, const void *desc, const void *gpts,
                                      u32 n_groups, u32 *f_soa, uint8_t *gacc) {
     LCB_LAUNCH(k_tpke_rlc_miller, lines, (const uint4 *)desc, (const g1a_st *)gpts, n_groups, f_soa, gacc);
 }
 extern "C" void lcbk_rlc_resolve(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, const uint8_t *gacc,
-                                 uint8_t *accept, void *next, u32 *next_count) {
-    LCB_LAUNCH(k_rlc_resolve, (const uint4 *)desc, n_groups, gacc, accept, (uint4 *)next, next_count);
+                                 const uint8_t *gexact, uint8_t *accept, void *next, u32 *next_count) {
+    LCB_LAUNCH(k_rlc_resolve, (const uint4 *)desc, n_groups, gacc, gexact, accept, (uint4 *)next, next_count);
 }

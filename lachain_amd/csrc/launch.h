@@ -62,9 +62,10 @@ extern "C" void lcbk_secp_sign(hipStream_t s, const uint8_t *hashes, const uint8
 extern "C" void lcbk_tpke_rlc_points(dim3 grid, hipStream_t s, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, const u32 key[10], u32 *rU, u32 *rY, uint8_t *accept);
 extern "C" u32 lcbk_rlc_span();
 extern "C" void lcbk_rlc_groups(dim3 grid, hipStream_t s, const u32 *ct_idx, u32 n, u32 n_cts, void *desc, u32 *count);
-extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, const uint8_t *ct_ok, const u32 *rU, const u32 *rY, u32 n, void *gpts, uint8_t *accept);
+extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, const uint8_t *ct_ok, const uint8_t *ct_g2, const void *keys, u32 n_keys, const u32 *dec_idx, const uint8_t *ui, const u32 *rU, const u32 *rY, u32 n, void *gpts, uint8_t *accept, uint8_t *gexact);
+extern "C" void lcbk_tpke_ct_g2check(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, uint8_t *ct_g2);
 extern "C" void lcbk_tpke_rlc_miller(dim3 grid, hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups, u32 *f_soa, uint8_t *gacc);
-extern "C" void lcbk_rlc_resolve(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, const uint8_t *gacc, uint8_t *accept, void *next, u32 *next_count);
+extern "C" void lcbk_rlc_resolve(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, const uint8_t *gacc, const uint8_t *gexact, uint8_t *accept, void *next, u32 *next_count);
 extern "C" void lcbk_op(dim3 grid, hipStream_t s, int op, u32 *io, int orig_cof);
 
 // sizes of the device records the host allocates

@@ -729,9 +729,20 @@ bool read_count(u32 &v, const u32 *d, hipStream_t s) {
     return true;
 }
 // phase 2 (after the ciphertext preparation): group checks, level by level
-int rlc_levels(lcb_ctx *c, RlcWs &w, uint8_t *d_accept, size_t n, hipStream_t s) {
+// W of every prepared ciphertext in G2 -> rlc[8]
+int rlc_g2check(lcb_ctx *c, hipStream_t s) {
+    uint8_t *ctg2 = (uint8_t *)c->rlc[8].get(c->t_n_cts);
+    if (!ctg2) { set_err("device allocation failed"); return -1; }
+    if (c->t_n_cts)
+        lcbk_tpke_ct_g2check(dim3(nblk(c->t_n_cts)), s, (const u32 *)c->t_lines.p, (const uint8_t *)c->t_ctok.p,
+                             (u32)c->t_n_cts, ctg2);
+    return 0;
+}
+int rlc_levels(lcb_ctx *c, RlcWs &w, uint8_t *d_accept, size_t n, const uint32_t *d_dec, const uint8_t *d_ui,
+               hipStream_t s) {
     const u32 *lines = (const u32 *)c->t_lines.p;
     const uint8_t *ctok = (const uint8_t *)c->t_ctok.p;
+    const uint8_t *ctg2 = (const uint8_t *)c->rlc[8].p;
     u32 groups = 0;
     for (auto &m : c->rlc_ms) m = 0.0f;
     if (!read_count(groups, w.cnt, s)) return -1;
@@ -740,14 +751,15 @@ int rlc_levels(lcb_ctx *c, RlcWs &w, uint8_t *d_accept, size_t n, hipStream_t s)
         if (lev < 8) c->rlc_levels[lev] = groups;
         c->rlc_nlev = lev + 1;
         void *gpts = c->rlc[5].get((size_t)groups * 2 * LCB_G1A_ST_BYTES);
-        uint8_t *gacc = (uint8_t *)c->rlc[6].get(groups);
+        uint8_t *gacc = (uint8_t *)c->rlc[6].get(groups), *gex = (uint8_t *)c->rlc[7].get(groups);
         const size_t nf = groups < LCB_VERIFY_CHUNK ? groups : LCB_VERIFY_CHUNK;
         u32 *f = (u32 *)c->t_f.get(nf * 576 * (size_t)lcbk_fe_slots());
-        if (!gpts || !gacc || !f) { set_err("device allocation failed"); return -1; }
+        if (!gpts || !gacc || !gex || !f) { set_err("device allocation failed"); return -1; }
         hipMemsetAsync(w.cnt + 1, 0, 4, s);
         hipEvent_t *ev = c->rlc_lev_ev;
         hipEventRecord(ev[0], s);
-        lcbk_tpke_rlc_sum(dim3(nblk(groups)), s, w.dA, groups, ctok, w.rU, w.rY, (u32)n, gpts, d_accept);
+        lcbk_tpke_rlc_sum(dim3(nblk(groups)), s, w.dA, groups, ctok, ctg2, c->t_keys.p, (u32)c->t_n_keys, d_dec, d_ui,
+                          w.rU, w.rY, (u32)n, gpts, d_accept, gex);
         float ms[3] = {0, 0, 0}, t;
         for (size_t o = 0; o < groups; o += LCB_VERIFY_CHUNK) {
             const size_t m = groups - o < LCB_VERIFY_CHUNK ? groups - o : LCB_VERIFY_CHUNK;
@@ -763,7 +775,7 @@ int rlc_levels(lcb_ctx *c, RlcWs &w, uint8_t *d_accept, size_t n, hipStream_t s)
                 if (hipEventElapsedTime(&t, ev[2], ev[3]) == hipSuccess) ms[2] += t;
             }
         }
-        lcbk_rlc_resolve(dim3(nblk(groups)), s, w.dA, groups, gacc, d_accept, w.dB, w.cnt + 1);
+        lcbk_rlc_resolve(dim3(nblk(groups)), s, w.dA, groups, gacc, gex, d_accept, w.dB, w.cnt + 1);
         hipEventRecord(ev[0], s);
         if (!launched("tpke batched verify launch")) return -1;
         if (!read_count(groups, w.cnt + 1, s)) return -1;
@@ -783,7 +795,8 @@ int tpke_verify_prepared_rlc(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_k
     if (!n) return 0;
     RlcWs w;
     if (rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, s)) return -1;
-    return rlc_levels(c, w, d_accept, n, s);
+    if (rlc_g2check(c, s)) return -1;
+    return rlc_levels(c, w, d_accept, n, d_dec, d_ui, s);
 }
 
 // prepare + batched verify in one call: the randomisation (needs only the keys) runs on the context's second
@@ -825,8 +838,9 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
     c->t_gen++;
     c->t_ready = true;
     if (!n) return 0;
+    if (rlc_g2check(c, s)) return -1;      // still beside the randomisation on the second stream
     hipStreamWaitEvent(s, c->fork_ev[1], 0);
-    return rlc_levels(c, w, d_accept, n, s);
+    return rlc_levels(c, w, d_accept, n, d_dec, d_ui, s);
 }
 
 // ------------------------------------------------------------------ threshold signatures

@@ -242,3 +242,41 @@ def test_batched_invalid_ciphertext(nat, tdev, fused):
     assert expect[6:12] == [0] * 6 and sum(expect) == 11
     got = run_dev(nat, tdev, b, ct, dec, shares, fused=fused)
     assert got.tolist() == expect
+
+
+def off_subgroup_g2(d):
+    while True:
+        xa = int.from_bytes(d.bytes(48), "little") % o.P
+        xb = int.from_bytes(d.bytes(48), "little") % o.P
+        enc = bytearray(xa.to_bytes(48, "little") + xb.to_bytes(48, "little"))
+        enc[95] |= 0x80 * (d.bytes(1)[0] & 1)
+        enc = bytes(enc)
+        if o.g2_valid(enc) and not o.g2_in_subgroup(enc):
+            return enc
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_batched_w_outside_g2(nat, tdev, fused):
+    """a ciphertext whose W carries a G2 cofactor-torsion component (on the curve, so G2.FromBytes accepts it; the
+    pairing is not linear in the G1 argument against such a W): its shares must get their exact per-share decisions
+    (k_tpke_ct_g2check -> exact singles), equal to the oracle's and to the exact GPU path; the other ciphertexts'
+    groups are unaffected"""
+    b = Batch(b"gpu-batched-w-torsion", 8, 2, 3)
+    q = off_subgroup_g2(b.d)
+    t2 = o.g2_add(o.g2_mul(q, o.fr(R - 1)), q)          # [r] Q: a nonzero point of the G2 cofactor torsion
+    assert not o.g2_in_subgroup(t2)
+    u, v, w = b.cts[1]
+    w2 = o.g2_add(w, t2)
+    assert o.g2_valid(w2) and not o.g2_in_subgroup(w2)
+    b.cts[1] = (u, v, w2)
+    ct = np.repeat(np.arange(3, dtype=np.uint32), 8)
+    dec = np.tile(np.arange(8, dtype=np.uint32), 3)
+    shares = [b.good[c][j] for c, j in zip(ct, dec)]
+    shares[8 + 3] = b.bad[1][3]
+    shares[8 + 5] = o.g1_add(b.good[1][5], torsion_g1(b.d))
+    shares[2] = b.bad[0][2]
+    expect = [int(b.expect(c, j, s)) for c, j, s in zip(ct, dec, shares)]
+    got = run_dev(nat, tdev, b, ct, dec, shares, fused=fused)
+    assert got.tolist() == expect
+    exact = nat.tpke_verify_shares(b.yi, b.cts, [(int(c), int(j), s) for c, j, s in zip(ct, dec, shares)])
+    assert [int(x) for x in exact] == expect
