@@ -130,14 +130,16 @@ def make_inputs(nat, rank, n_shares, n_dec, f, vlen, corrupt_frac=0.01):
     dec_idx = np.empty(n_shares, dtype=np.uint32)
     scal = bytearray(32 * n_shares)
     expect = np.ones(n_shares, dtype=np.uint8)
-    stride = int(round(1 / corrupt_frac)) if corrupt_frac > 0 else 0
+    # round(1 %) of the shares at seeded uniformly random positions (so some ciphertexts carry two or more bad shares,
+    # the case the batched check's level-2 search cannot resolve alone)
+    rng = np.random.default_rng(SEED + rank)
+    expect[rng.choice(n_shares, size=int(round(corrupt_frac * n_shares)), replace=False)] = 0
     for i in range(n_shares):
         c, j = divmod(i, n_dec)
         ct_idx[i], dec_idx[i] = c, j
         s = xs[j] * rs[c] % R
-        if stride and i % stride == stride // 2:
+        if not expect[i]:
             s = (s + 1) % R
-            expect[i] = 0
         scal[32 * i:32 * i + 32] = s.to_bytes(32, "little")
     ui = nat.mul_batch_raw(1, b"", bytes(scal), n_shares, generator=True)
     v_off = np.arange(0, vlen * (n_cts + 1), vlen, dtype=np.uint32)
@@ -446,6 +448,10 @@ def ts_cpu_baseline(inp, n_total, n_per_round, target_s=10.0):
 
 
 def run_ts(args, nat, torch, dev, rank, world):
+    """configs[2]: per step, prepare (keys, H(m) + lines) + verify every share, assemble the first F+1 valid shares
+    per round (G2 Lagrange) and verify the combined signatures.  Timed twice on the same rounds: the randomized batch
+    share check (lcb_ts_verify_shares_batched_dev: prepare + group checks in one call, the line's value) and the exact
+    per-share check (lcb_ts_prepare_dev + lcb_ts_verify_prepared_dev, under "exact")."""
     import torch.distributed as dist
     lib = nat.lib()
     rounds, n, f = args.ts_rounds, args.ts_n, (args.ts_n - 1) // 3
@@ -463,76 +469,109 @@ def run_ts(args, nat, torch, dev, rank, world):
     d_ridx = torch.arange(rounds, dtype=torch.int32, device=dev)
     d_shared = torch.full((rounds,), n, dtype=torch.int32, device=dev)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-
-    def step(timed=False):
-        if timed:
-            ev[0].record(stream)
-        rc = lib.lcb_ts_prepare_dev(d_pks.data_ptr(), n + 1, d_msg.data_ptr(), d_moff.data_ptr(), rounds, sh)
-        if timed:
-            ev[1].record(stream)
-        rc |= lib.lcb_ts_verify_prepared_dev(d_acc.data_ptr(), rounds * n, n + 1, rounds, d_sigs.data_ptr(),
-                                             d_midx.data_ptr(), d_pidx.data_ptr(), sh)
-        if timed:
-            ev[2].record(stream)
-        rc |= lib.lcb_ts_assemble_dev(d_comb.data_ptr(), d_cst.data_ptr(), d_acc.data_ptr(), d_sigs.data_ptr(), n,
-                                      f + 1, rounds, sh)
-        rc |= lib.lcb_ts_verify_prepared_dev(d_cacc.data_ptr(), rounds, n + 1, rounds, d_comb.data_ptr(),
-                                             d_ridx.data_ptr(), d_shared.data_ptr(), sh)
-        if timed:
-            ev[3].record(stream)
-        if rc != 0:
-            raise RuntimeError(nat.last_error())
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    t_prep = t_ver = t_asm = 0.0
-    for _ in range(args.ts_steps):
-        step(True)
-        torch.cuda.synchronize(dev)
-        t_prep += ev[0].elapsed_time(ev[1])
-        t_ver += ev[1].elapsed_time(ev[2])
-        t_asm += ev[2].elapsed_time(ev[3])
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    mism = int(np.sum(d_acc.cpu().numpy() != inp["expect"]))
-    comb_ok = int(d_cst.cpu().numpy().sum()) == rounds and int(d_cacc.cpu().numpy().sum()) == rounds
-    # spot-check combined signatures against the oracle: sigma_r = shared_sk * H(msg_r) (ThresholdSignatureTest.cs)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as o
-    comb = d_comb.cpu().numpy().tobytes()
-    for r in (0, 1, rounds - 1):
-        comb_ok = comb_ok and comb[96 * r:96 * r + 96] == o.ts_sign(o.fr(inp["shared_sk"]), inp["msg_list"][r])
-    t = torch.tensor([elapsed, float(mism), float(0 if comb_ok else 1)], dtype=torch.float64, device=dev)
-    if world > 1:
-        tm = t[:1].clone()
-        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        t[0] = tm[0]
+
+    def run(batched):
+        def step(timed=False):
+            if timed:
+                ev[0].record(stream)
+            if batched:
+                rc = lib.lcb_ts_verify_shares_batched_dev(d_acc.data_ptr(), rounds * n, d_pks.data_ptr(), n + 1,
+                                                          d_sigs.data_ptr(), d_msg.data_ptr(), d_moff.data_ptr(),
+                                                          rounds, d_midx.data_ptr(), d_pidx.data_ptr(), sh)
+                if timed:
+                    ev[1].record(stream)
+            else:
+                rc = lib.lcb_ts_prepare_dev(d_pks.data_ptr(), n + 1, d_msg.data_ptr(), d_moff.data_ptr(), rounds, sh)
+                if timed:
+                    ev[1].record(stream)
+                rc |= lib.lcb_ts_verify_prepared_dev(d_acc.data_ptr(), rounds * n, n + 1, rounds, d_sigs.data_ptr(),
+                                                     d_midx.data_ptr(), d_pidx.data_ptr(), sh)
+            if timed:
+                ev[2].record(stream)
+            rc |= lib.lcb_ts_assemble_dev(d_comb.data_ptr(), d_cst.data_ptr(), d_acc.data_ptr(), d_sigs.data_ptr(), n,
+                                          f + 1, rounds, sh)
+            rc |= lib.lcb_ts_verify_prepared_dev(d_cacc.data_ptr(), rounds, n + 1, rounds, d_comb.data_ptr(),
+                                                 d_ridx.data_ptr(), d_shared.data_ptr(), sh)
+            if timed:
+                ev[3].record(stream)
+            if rc != 0:
+                raise RuntimeError(nat.last_error())
+
+        d_acc.fill_(7)
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        t_prep = t_ver = t_asm = 0.0
+        for _ in range(args.ts_steps):
+            step(True)
+            torch.cuda.synchronize(dev)
+            t_prep += ev[0].elapsed_time(ev[1])
+            t_ver += ev[1].elapsed_time(ev[2])
+            t_asm += ev[2].elapsed_time(ev[3])
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        levels = nat.tpke_batched_stats()[0] if batched else None
+        mism = int(np.sum(d_acc.cpu().numpy() != inp["expect"]))
+        comb_ok = int(d_cst.cpu().numpy().sum()) == rounds and int(d_cacc.cpu().numpy().sum()) == rounds
+        # spot-check combined signatures against the oracle: sigma_r = shared_sk * H(msg_r) (ThresholdSignatureTest.cs)
+        comb = d_comb.cpu().numpy().tobytes()
+        for r in (0, 1, rounds - 1):
+            comb_ok = comb_ok and comb[96 * r:96 * r + 96] == o.ts_sign(o.fr(inp["shared_sk"]), inp["msg_list"][r])
+        t = torch.tensor([elapsed, float(mism), float(0 if comb_ok else 1)], dtype=torch.float64, device=dev)
+        if world > 1:
+            tm = t[:1].clone()
+            dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+            dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+            t[0] = tm[0]
+        per = args.ts_steps
+        elapsed = float(t[0])
+        out = dict(value=rounds * n * world * per / elapsed, unit="share verifications/s",
+                   rounds_per_s=rounds * world * per / elapsed, ms_per_step=1e3 * elapsed / per,
+                   decision_mismatches=int(t[1]), combined_ok=int(t[2]) == 0)
+        if batched:
+            out["phase_ms"] = {"prepare_and_verify_shares (one call)": (t_prep + t_ver) / per,
+                               "assemble_and_verify_combined": t_asm / per}
+            out["levels"] = levels
+            out["api"] = "lcb_ts_verify_shares_batched_dev (prepare + randomized group checks)"
+        else:
+            ver_s = t_ver / per * 1e-3
+            out["phase_ms"] = {"prepare": t_prep / per, "verify_shares": t_ver / per,
+                               "assemble_and_verify_combined": t_asm / per}
+            out["api"] = "lcb_ts_prepare_dev + lcb_ts_verify_prepared_dev"
+            out["roofline"] = {"bound": "valu_int32", "kernel": "k_ts_miller + k_final_exp_check",
+                               "achieved": rounds * n * W_TS * MAC_PER_FPMUL / ver_s / 1e12,
+                               "peak": PEAK_MAC32 / 1e12, "unit": "Tmac32/s",
+                               "frac": rounds * n * W_TS * MAC_PER_FPMUL / ver_s / PEAK_MAC32,
+                               "work_per_share_fpmul": W_TS}
+        return out
+
+    bat = run(True) if args.ts_batched else None
+    exact = run(False) if args.ts_exact else None
     if rank != 0:
         return None
-    elapsed = float(t[0])
-    per = args.ts_steps
-    ver_s = t_ver / per * 1e-3
-    return dict(
+    head = bat or exact
+    res = dict(
         metric="BLS12-381 threshold-signature share verifications/sec (ValidateSignature + AddShare assembly)",
-        value=rounds * n * world * per / elapsed, unit="share verifications/s",
-        rounds_per_s=rounds * world * per / elapsed, rounds_per_rank=rounds, shares_per_round=n, threshold_k=f + 1,
-        steps=per, ms_per_step=1e3 * elapsed / per, decision_mismatches=int(t[1]), combined_ok=int(t[2]) == 0,
-        phase_ms={"prepare": t_prep / per, "verify_shares": t_ver / per, "assemble_and_verify_combined": t_asm / per},
-        roofline={"bound": "valu_int32", "kernel": "k_ts_miller + k_final_exp_check",
-                  "achieved": rounds * n * W_TS * MAC_PER_FPMUL / ver_s / 1e12, "peak": PEAK_MAC32 / 1e12,
-                  "unit": "Tmac32/s", "frac": rounds * n * W_TS * MAC_PER_FPMUL / ver_s / PEAK_MAC32,
-                  "work_per_share_fpmul": W_TS},
-        config=f"configs[2]: {rounds} rounds x N={n} F={f} CommonCoin shares per rank; per round: {n} share "
-               f"verifications, G2 Lagrange over the first {f + 1} valid shares, combined-signature verification",
+        rounds_per_rank=rounds, shares_per_round=n, threshold_k=f + 1, steps=args.ts_steps,
+        config=f"configs[2]: {rounds} rounds x N={n} F={f} CommonCoin shares per rank (one wrong share per round); "
+               f"per round: {n} share verifications, G2 Lagrange over the first {f + 1} valid shares, "
+               f"combined-signature verification",
         input_gen_s=t_gen,
-        cpu_baseline=ts_cpu_baseline(inp, rounds * n, n) if (world == 1 and not args.no_cpu_baseline) else None,
-    )
+        algorithm=("randomized batch check per round (e(sum s_i PK_i, H) == e(G, sum s_i sig_i), secret 64-bit "
+                   "exponents; level 2 names a round's single bad share from gamma' = gamma^c)" if bat else
+                   "exact per-share check"))
+    res.update(head)
+    if bat and exact:
+        res["exact"] = exact
+    if world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = ts_cpu_baseline(inp, rounds * n, n)
+    return res
 
 
 # ------------------------------------------------------------------ HoneyBadger epoch replay (BASELINE configs[4])
@@ -1078,6 +1117,8 @@ def main():
     ap.add_argument("--ts-rounds", type=int, default=65536, help="CommonCoin rounds per rank (0 = skip)")
     ap.add_argument("--ts-n", type=int, default=100)
     ap.add_argument("--ts-steps", type=int, default=1)
+    ap.add_argument("--ts-batched", type=int, default=1, help="time the randomized batch share check (0 = skip)")
+    ap.add_argument("--ts-exact", type=int, default=1, help="time the exact per-share check (0 = skip)")
     ap.add_argument("--replay-n", type=int, default=256, help="epoch-replay network size N (0 = skip)")
     ap.add_argument("--replay-steps", type=int, default=1)
     ap.add_argument("--ecdsa-sigs", type=int, default=1 << 20, help="header signatures per rank (0 = skip)")

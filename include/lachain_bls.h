@@ -256,9 +256,23 @@ int lcb_tpke_verify_shares_batched(uint8_t *accept, size_t n_shares, const uint8
                                    const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
                                    const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
                                    const uint32_t *dec_idx, const uint8_t *ui);
-/* groups checked per level of the last batched verify (levels[0] = first level) and device ms of
-   [randomisation + grouping, all levels, then summed over the levels: group sums, k_tpke_rlc_miller,
-   k_final_exp_check, resolve]; returns the number of levels (waits for the call) */
+/* Randomized batch forms of the threshold-signature share check (ThresholdSignature/PublicKey.cs:16-21, called per
+   share from ThresholdSigner.cs:62): groups = runs of shares of one message (pass message-major batches), checked as
+   e(sum s_i PK_i, H(m)) == e(G, sum s_i sig_i); a share whose signature is outside G2 gets its exact check.  Same
+   arguments as lcb_ts_verify_prepared_dev / lcb_ts_verify_shares_dev / lcb_ts_verify_shares. */
+int lcb_ts_verify_prepared_batched_dev(uint8_t *accept, size_t n, size_t n_pks, size_t n_msgs, const uint8_t *sigs,
+                                       const uint32_t *msg_idx, const uint32_t *pk_idx, void *stream);
+int lcb_ts_verify_shares_batched_dev(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks, const uint8_t *sigs,
+                                     const uint8_t *msg_data, const uint32_t *msg_off, size_t n_msgs,
+                                     const uint32_t *msg_idx, const uint32_t *pk_idx, void *stream);
+int lcb_ts_verify_shares_batched(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks, const uint8_t *sigs,
+                                 const uint8_t *msg_data, const uint32_t *msg_off, size_t n_msgs,
+                                 const uint32_t *msg_idx, const uint32_t *pk_idx);
+/* the last batched verify (TPKE or threshold signatures) completed by the calling thread (any context; the
+   lcb_ctx_ form: the last one of that context): groups checked per level
+   (levels[0] = level 1, levels[1] = the level-2 weighted re-checks of failed groups, then single checks) and device
+   ms of [randomisation + grouping, all levels, then summed over the levels: group sums, group Miller loops, final
+   exponentiations (+ resolve / search), 0]; returns the number of levels (waits for the call) */
 int lcb_tpke_batched_stats(uint32_t levels[8], float ms[6]);
 /* test hook: fixed 32-byte ChaCha20 key for the batch exponents (NULL restores getrandom) */
 void lcb_set_batch_seed(const uint8_t *seed32);
@@ -291,6 +305,13 @@ int lcb_ctx_tpke_verify_shares_batched_dev(lcb_ctx *ctx, uint8_t *accept, size_t
                                            const uint32_t *ct_idx, const uint32_t *dec_idx, const uint8_t *ui,
                                            void *stream);
 int lcb_ctx_tpke_batched_stats(lcb_ctx *ctx, uint32_t levels[8], float ms[6]);
+int lcb_ctx_ts_verify_prepared_batched_dev(lcb_ctx *ctx, uint8_t *accept, size_t n, size_t n_pks, size_t n_msgs,
+                                           const uint8_t *sigs, const uint32_t *msg_idx, const uint32_t *pk_idx,
+                                           void *stream);
+int lcb_ctx_ts_verify_shares_batched_dev(lcb_ctx *ctx, uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks,
+                                         const uint8_t *sigs, const uint8_t *msg_data, const uint32_t *msg_off,
+                                         size_t n_msgs, const uint32_t *msg_idx, const uint32_t *pk_idx,
+                                         void *stream);
 int lcb_ctx_ts_prepare_dev(lcb_ctx *ctx, const uint8_t *pks, size_t n_pks, const uint8_t *msg_data,
                            const uint32_t *msg_off, size_t n_msgs, void *stream);
 int lcb_ctx_ts_verify_prepared_dev(lcb_ctx *ctx, uint8_t *accept, size_t n, size_t n_pks, size_t n_msgs,

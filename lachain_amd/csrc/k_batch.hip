@@ -13,6 +13,13 @@
 // = 1): every rejected share is rejected by an exact check of its own, every accepted share by a group check (false
 // accept <= 2^-64 per group, over the secret exponents).
 //
+// Level 2 (one bad share per group, the usual failure): the first level also forms W = sum (j+1) s_j U_j etc. (j = the
+// share's position in its group, so the weights c_j = j+1 are distinct and public).  A failed group's gamma =
+// prod g_i^(s_i) (its final-exponentiation output) and gamma' = prod g_i^(c_i s_i) (one more group check) satisfy
+// gamma' = gamma^(c_j) exactly when j is the only bad share: k_rlc_search tries c = 1..len (len Fp12 products) and
+// rejects share j; with two or more bad shares no c matches except with probability <= len 2^-64 (the exponents
+// s_i are secret), and the group's shares get single checks at the next level.  So at most three levels.
+//
 // Pipeline (host side in lcb_host.cpp: rlc_points_enqueue + rlc_levels):
 //   k_tpke_rlc_points   one lane per share: validity as k_tpke_miller, (a_i, b_i) = ChaCha20(key, i), s_i U_i and
 //                       s_i Y_i with s_i = a_i + b_i lambda (32-bit GLV form, rlc_scalar) -> quad-major SoA Jacobian
@@ -30,9 +37,7 @@ LCB_ASM_LIBRARY(k_batch)
 
 struct rlc_key { u32 k[8]; u32 nonce[2]; };   // ChaCha20 key (256 bit, from getrandom) and a per-call nonce
 
-#define LCB_RLC_RUN 32          // longest level-1 group
-#define LCB_RLC_SPAN 256        // shares scanned by one k_rlc_groups lane
-#define LCB_RLC_SINGLES 8       // a failed group this short splits into single shares
+#define LCB_RLC_SINGLES 8       // a failed group this short (below level 1) splits into single shares
 
 // ---------------------------------------------------------------- ChaCha20 (RFC 8439 block function)
 DI u32 rotl32(u32 x, int r) { return (x << r) | (x >> (32 - r)); }
@@ -70,21 +75,26 @@ DI void rlc_scalar(const rlc_key &key, u32 i, u32 &a, u32 &b) {
     if ((a | b) == 0) a = 1;
 }
 
-// ---------------------------------------------------------------- quad-major SoA Jacobian G1 records (36 words)
-DI void g1_store_soa(u32 *base, size_t n, size_t i, const g1 &p) {
-    const u32 *s = (const u32 *)&p;
+// ---------------------------------------------------------------- quad-major SoA records (NW words, NW % 4 == 0)
+template <int NW> DI void soa_store(u32 *base, size_t n, size_t i, const void *v) {
+    const u32 *s = (const u32 *)v;
 #pragma unroll
-    for (int q = 0; q < 9; q++)
+    for (int q = 0; q < NW / 4; q++)
         *(uint4 *)(base + ((size_t)q * n + i) * 4) = make_uint4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
 }
-DI void g1_load_soa(g1 &p, const u32 *base, size_t n, size_t i) {
-    u32 *d = (u32 *)&p;
+template <int NW> DI void soa_load(void *v, const u32 *base, size_t n, size_t i) {
+    u32 *d = (u32 *)v;
 #pragma unroll
-    for (int q = 0; q < 9; q++) {
-        uint4 v = *(const uint4 *)(base + ((size_t)q * n + i) * 4);
-        d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+    for (int q = 0; q < NW / 4; q++) {
+        uint4 x = *(const uint4 *)(base + ((size_t)q * n + i) * 4);
+        d[4 * q] = x.x; d[4 * q + 1] = x.y; d[4 * q + 2] = x.z; d[4 * q + 3] = x.w;
     }
 }
+DI void g1_store_soa(u32 *base, size_t n, size_t i, const g1 &p) { soa_store<36>(base, n, i, &p); }
+DI void g1_load_soa(g1 &p, const u32 *base, size_t n, size_t i) { soa_load<36>(&p, base, n, i); }
+DI void g2_store_soa(u32 *base, size_t n, size_t i, const g2 &p) { soa_store<72>(base, n, i, &p); }
+DI void g2_load_soa(g2 &p, const u32 *base, size_t n, size_t i) { soa_load<72>(&p, base, n, i); }
+
 // a P + b phi(P) for an affine P: 32 doublings, mixed additions of P and phi(P)
 DN void g1_mul_ab_n(g1 &r, const g1a &P, u32 a, u32 b) {
     g1 acc;
@@ -101,7 +111,26 @@ DN void g1_mul_ab_n(g1 &r, const g1a &P, u32 a, u32 b) {
     }
     r = acc;
 }
-
+// (a + b lambda) S for S in G2: psi^2 acts on G2 as p^2 = z^2 (mod r), so lambda S = psi^2(S) - S and
+// (a + b lambda) S = (a - b) S + b psi^2(S): 32 doublings, mixed additions of +-S and psi^2(S)
+DN void g2_mul_ab_n(g2 &r, const g2a &S, u32 a, u32 b) {
+    g2 acc;
+    jac_set_inf(acc);
+    if (!S.inf) {
+        g2 J, T;
+        jac_from_aff(J, S);
+        g2_psi2(T, J);                   // z = 1 stays 1: affine
+        fp2 sy = S.y;
+        u32 d = a - b;
+        if (a < b) { d = b - a; fp2_neg(sy, sy); }
+        for (int k = 31; k >= 0; k--) {
+            grp_dbl(acc, acc);
+            if ((d >> k) & 1) grp_madd(acc, acc, S.x, sy);
+            if ((b >> k) & 1) grp_madd(acc, acc, T.x, T.y);
+        }
+    }
+    r = acc;
+}
 // both multiplications in one loop with the point arithmetic inlined (two independent dependency chains per lane, no
 // call frames): a U + b phi(U) and a Y + b phi(Y).  Opt-in (LCB_RLC_JOINT): measured slower than the two calls to
 // g1_mul_ab_n (randomisation 77.7 vs 63.5 ms per 1M shares): 290 VGPRs allow one wave per SIMD instead of two.
@@ -128,8 +157,28 @@ DI void g1_mul_ab2(g1 &ru, g1 &ry, const g1a &U, const g1a &Y, u32 a, u32 b) {
     if (U.inf) jac_set_inf(ru);
     if (Y.inf) jac_set_inf(ry);
 }
+// affine records of Jacobian points (inf = 1 for the point at infinity), optionally negated
+DI void g1_to_st(g1a_st &o, const g1 &p, bool neg) {
+    g1a a;
+    jac_to_aff(a, p);
+    o.ok = 1; o.pad[0] = o.pad[1] = 0;
+    o.inf = a.inf;
+    o.x = a.x;
+    if (neg && !a.inf) fp_neg(o.y, a.y);
+    else o.y = a.y;
+}
+DI void g2_to_st(g2a_st &o, const g2 &p) {
+    g2a a;
+    jac_to_aff(a, p);
+    o.ok = 1; o.pad[0] = o.pad[1] = 0;
+    o.inf = a.inf;
+    o.x = a.x;
+    o.y = a.y;
+}
+DI void g1_inf_st(g1a_st &o) { o.ok = 1; o.pad[0] = o.pad[1] = 0; o.inf = 1; o.x = fp_zero(); o.y = fp_zero(); }
+DI void g2_inf_st(g2a_st &o) { o.ok = 1; o.pad[0] = o.pad[1] = 0; o.inf = 1; o.x = fp2_zero(); o.y = fp2_zero(); }
 
-// ---------------------------------------------------------------- per-share randomisation
+// ---------------------------------------------------------------- TPKE: per-share randomisation
 // validity as k_tpke_miller except the ciphertext's (applied per group by k_tpke_rlc_sum, so this kernel needs only
 // the decompressed keys and may run beside the ciphertext preparation)
 extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_points(u32 n_cts, const g1a_st *keys, u32 n_keys, const u32 *ct_idx,
@@ -163,45 +212,53 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_points(u32 n_cts, const g1a_st 
     accept[i] = ok;
 }
 
-// ---------------------------------------------------------------- level-1 groups: runs of one ciphertext
-// desc = {first share, length, ciphertext, 0}; order of the records is irrelevant
-extern "C" __global__ void LCB_BOUNDS k_rlc_groups(const u32 *ct_idx, u32 n, u32 n_cts, uint4 *desc, u32 *count) {
-    u32 b = blockIdx.x * blockDim.x + threadIdx.x;
-    size_t lo = (size_t)b * LCB_RLC_SPAN;
-    if (lo >= n) return;
-    u32 hi = (u32)min((size_t)n, lo + LCB_RLC_SPAN);
-    u32 start = (u32)lo, cur = ct_idx[lo];
-    cur = cur < n_cts ? cur : 0;
-    for (u32 j = (u32)lo + 1; j <= hi; j++) {
-        u32 c = 0;
-        if (j < hi) { c = ct_idx[j]; c = c < n_cts ? c : 0; }
-        if (j == hi || c != cur || j - start == LCB_RLC_RUN) {
-            u32 slot = atomicAdd(count, 1u);
-            desc[slot] = make_uint4(start, j - start, cur, 0);
-            start = j;
-            cur = c;
-        }
+// ---------------------------------------------------------------- level-1 groups: runs of one ciphertext / message
+// one lane per share; the first share of a run emits the run as groups of at most `cap` shares.
+// desc = {first share, length, ciphertext / message, 0}; order of the records is irrelevant
+extern "C" __global__ void LCB_BOUNDS k_rlc_groups(const u32 *key_idx, u32 n, u32 n_keys, u32 cap, uint4 *desc,
+                                                  u32 *count) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    u32 c = key_idx[i];
+    c = c < n_keys ? c : 0;
+    if (i > 0) {
+        u32 p = key_idx[i - 1];
+        p = p < n_keys ? p : 0;
+        if (p == c) return;
+    }
+    u32 j = i + 1;
+    while (j < n) {
+        u32 q = key_idx[j];
+        q = q < n_keys ? q : 0;
+        if (q != c) break;
+        j++;
+    }
+    for (u32 st = i; st < j; st += cap) {
+        u32 len = min(cap, j - st);
+        u32 slot = atomicAdd(count, 1u);
+        desc[slot] = make_uint4(st, len, c, 0);
     }
 }
 
-// ---------------------------------------------------------------- group sums -> two affine points per group
+// ---------------------------------------------------------------- TPKE group sums -> two affine points per group
 // gpts[2g] = sum s_i U_i, gpts[2g + 1] = -sum s_i Y_i (g1a_st records; inf = 1 for the point at infinity).
 // desc.w = 0: a randomized group.  A group of an invalid ciphertext rejects its shares; a group whose ciphertext's W
 // is outside G2 (the pairing is linear in its G1 argument only for a G2 point: W comes from the wire unchecked) is
 // handed to exact checks (gexact = 1: resolve re-emits its shares as desc.w = 1 singles).  Both check two points at
 // infinity (they pass).  desc.w = 1: the exact single check of share desc.x, e(U_i, H) e(-Y_i, W) == 1 as
 // k_tpke_miller does it (a share already rejected checks infinity).
-extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_groups, const uint8_t *ct_ok,
+// first != 0 (level 1): also the weighted sums sum (j+1) s_j U_j, sum (j+1) s_j Y_j (j = position in the group) into
+// wsum (Jacobian SoA, stride n_groups) for the level-2 search.
+extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_groups, u32 first, const uint8_t *ct_ok,
                                                     const uint8_t *ct_g2, const g1a_st *keys, u32 n_keys,
                                                     const u32 *dec_idx, const uint8_t *ui, const u32 *rU,
                                                     const u32 *rY, u32 n, g1a_st *gpts, uint8_t *accept,
-                                                    uint8_t *gexact) {
+                                                    uint8_t *gexact, u32 *wsum) {
     u32 g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n_groups) return;
     uint4 dsc = desc[g];
     g1a_st o;
-    o.ok = 1; o.pad[0] = o.pad[1] = 0;
-    o.inf = 1; o.x = fp_zero(); o.y = fp_zero();
+    g1_inf_st(o);
     gexact[g] = 0;
     if (dsc.w == 1) {                    // exact single
         g1a U, Y;
@@ -213,7 +270,7 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_gr
         }
         if (live && !U.inf) { o.x = U.x; o.y = U.y; o.inf = 0; }
         gpts[2 * (size_t)g] = o;
-        o.inf = 1; o.x = fp_zero(); o.y = fp_zero();
+        g1_inf_st(o);
         if (live && !Y.inf) { o.x = Y.x; fp_neg(o.y, Y.y); o.inf = 0; }
         gpts[2 * (size_t)g + 1] = o;
         return;
@@ -228,36 +285,44 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_gr
         gpts[2 * (size_t)g + 1] = o;
         return;
     }
-    g1 su, sy, t;
+    g1 su, sy, t, wu, wy, cu, cy;
     jac_set_inf(su);
     jac_set_inf(sy);
-    for (u32 j = 0; j < dsc.y; j++) {
+    jac_set_inf(wu);
+    jac_set_inf(wy);
+    for (u32 j = dsc.y; j-- > 0;) {      // last to first: su = suffix sums, wu = sum of the suffix sums
         g1_load_soa(t, rU, n, dsc.x + j);
         grp_add(su, su, t);
         g1_load_soa(t, rY, n, dsc.x + j);
         grp_add(sy, sy, t);
+        if (first) {
+            grp_add(wu, wu, su);
+            grp_add(wy, wy, sy);
+        }
     }
-    // one inversion for both: 1 / (z_u z_y), an infinite sum's z replaced by 1
-    bool iu = jac_is_inf(su), iy = jac_is_inf(sy);
-    fp zu = iu ? fp_one() : su.z, zy = iy ? fp_one() : sy.z, zz, inv, zi, zi2;
-    fp_mul(zz, zu, zy);
-    fp_inv(inv, zz);
-    fp_mul(zi, inv, zy);                 // 1 / z_u
-    fp_sqr(zi2, zi);
-    fp_mul(o.x, su.x, zi2);
-    fp_mul(zi2, zi2, zi);
-    fp_mul(o.y, su.y, zi2);
-    o.inf = iu;
-    if (iu) { o.x = fp_zero(); o.y = fp_zero(); }
+    if (first) {
+        g1_store_soa(wsum, 2 * (size_t)n_groups, 2 * (size_t)g, wu);
+        g1_store_soa(wsum, 2 * (size_t)n_groups, 2 * (size_t)g + 1, wy);
+    }
+    g1_to_st(o, su, false);
     gpts[2 * (size_t)g] = o;
-    fp_mul(zi, inv, zu);                 // 1 / z_y
-    fp_sqr(zi2, zi);
-    fp_mul(o.x, sy.x, zi2);
-    fp_mul(zi2, zi2, zi);
-    fp_mul(o.y, sy.y, zi2);
-    fp_neg(o.y, o.y);
-    o.inf = iy;
-    if (iy) { o.x = fp_zero(); o.y = fp_zero(); }
+    g1_to_st(o, sy, true);
+    gpts[2 * (size_t)g + 1] = o;
+}
+
+// the weighted sums of the level-1 groups listed in sdesc (.w = level-1 group index) as affine records
+extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum(const uint4 *sdesc, u32 n_s, const u32 *wsum, u32 n_l1,
+                                                     g1a_st *gpts) {
+    u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_s) return;
+    u32 l = sdesc[g].w;
+    g1 p;
+    g1a_st o;
+    g1_load_soa(p, wsum, 2 * (size_t)n_l1, 2 * (size_t)l);
+    g1_to_st(o, p, false);
+    gpts[2 * (size_t)g] = o;
+    g1_load_soa(p, wsum, 2 * (size_t)n_l1, 2 * (size_t)l + 1);
+    g1_to_st(o, p, true);
     gpts[2 * (size_t)g + 1] = o;
 }
 
@@ -272,7 +337,7 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_ct_g2check(const u32 *lines, const 
     ct_g2[c] = ct_ok[c] ? g2_in_subgroup(W) : 0;
 }
 
-// ---------------------------------------------------------------- group Miller loops (k_tpke_miller's loop)
+// ---------------------------------------------------------------- TPKE group Miller loops (k_tpke_miller's loop)
 extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_rlc_miller(const u32 *lines, const uint4 *desc, const g1a_st *gpts,
                                                             u32 n_groups, u32 *f_soa, uint8_t *gacc) {
     __shared__ uint4 lds_pts[12 * LCB_BLOCK];
@@ -296,33 +361,219 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_rlc_miller(const u32 *lines, c
     gacc[g] = 1;
 }
 
-// ---------------------------------------------------------------- resolve a level
-// a failed group of one share rejects it; a failed group of len > 1 becomes ceil(len / s) sub-groups of s =
-// ceil(len / ceil(sqrt(len))) shares (one bad share among len then costs about 2 sqrt(len) group checks), or single
-// shares when len <= LCB_RLC_SINGLES: every level is one latency-bound launch (~one serial pairing check per lane), so
-// fewer levels beat fewer checks there
-extern "C" __global__ void LCB_BOUNDS k_rlc_resolve(const uint4 *desc, u32 n_groups, const uint8_t *gacc,
-                                                   const uint8_t *gexact, uint8_t *accept, uint4 *next,
-                                                   u32 *next_count) {
+// ---------------------------------------------------------------- threshold signatures (ValidateSignature)
+// e(PK_i, H(m)) == e(G, sig_i) <=> e(PK_i, H) e(-G, sig_i) == 1.  The randomisation of sig_i uses linearity of the
+// pairing in its G2 argument, which holds on G2: a share whose sig_i is outside G2 (G2.FromBytes does not check) is
+// emitted straight away as an exact single (desc.w = 1) and contributes nothing to its group.
+// TS group record: g1a_st P (sum s_i PK_i) then g2a_st S (sum s_i sig_i), 320 B
+struct ts_grp { g1a_st p; g2a_st s; };
+extern "C" __global__ void LCB_BOUNDS k_ts_rlc_points(u32 n_msgs, const g1a_st *pks, u32 n_pks, const u32 *msg_idx,
+                                                     const u32 *pk_idx, const uint8_t *sigs, u32 n, rlc_key key,
+                                                     u32 *rP, u32 *rS, uint8_t *accept, uint4 *desc, u32 *count) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    u32 m = msg_idx[i], k = pk_idx[i];
+    bool ok = k < n_pks && m < n_msgs;
+    g2a S;
+    g1a PK;
+    ok = g2_decompress(S, sigs + 96 * (size_t)i) && ok;
+    g1a_st ps = pks[k < n_pks ? k : 0];
+    ok = ok && ps.ok;
+    st_to_g1a(PK, ps);
+    g1 p;
+    g2 q;
+    jac_set_inf(p);
+    jac_set_inf(q);
+    if (ok) {
+        if (g2_in_subgroup(S)) {
+            u32 a, b;
+            rlc_scalar(key, i, a, b);
+            g1_mul_ab_n(p, PK, a, b);
+            g2_mul_ab_n(q, S, a, b);
+        } else {
+            u32 slot = atomicAdd(count, 1u);
+            desc[slot] = make_uint4(i, 1, m < n_msgs ? m : 0, 1);
+        }
+    }
+    g1_store_soa(rP, n, i, p);
+    g2_store_soa(rS, n, i, q);
+    accept[i] = ok;
+}
+extern "C" __global__ void LCB_BOUNDS k_ts_rlc_sum(const uint4 *desc, u32 n_groups, u32 first, const uint8_t *msg_ok,
+                                                  const g1a_st *pks, u32 n_pks, const u32 *pk_idx, const uint8_t *sigs,
+                                                  const u32 *rP, const u32 *rS, u32 n, ts_grp *gpts, uint8_t *accept,
+                                                  uint8_t *gexact, u32 *wsum) {
     u32 g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n_groups) return;
+    uint4 dsc = desc[g];
+    ts_grp o;
+    g1_inf_st(o.p);
+    g2_inf_st(o.s);
+    gexact[g] = 0;
+    if (dsc.w == 1) {                    // exact single: the share's own PK and sig
+        if (accept[dsc.x] && msg_ok[dsc.z]) {
+            g2a S;
+            u32 k = pk_idx[dsc.x];
+            if (g2_decompress(S, sigs + 96 * (size_t)dsc.x) && k < n_pks) {
+                o.p = pks[k];
+                o.s.x = S.x; o.s.y = S.y; o.s.inf = S.inf;
+            }
+        } else {
+            accept[dsc.x] = 0;
+        }
+        gpts[g] = o;
+        return;
+    }
+    if (!msg_ok[dsc.z]) {
+        for (u32 j = 0; j < dsc.y; j++) accept[dsc.x + j] = 0;
+        gpts[g] = o;
+        return;
+    }
+    g1 sp, t, wp;
+    g2 ss, u, ws;
+    jac_set_inf(sp);
+    jac_set_inf(wp);
+    jac_set_inf(ss);
+    jac_set_inf(ws);
+    for (u32 j = dsc.y; j-- > 0;) {
+        g1_load_soa(t, rP, n, dsc.x + j);
+        grp_add(sp, sp, t);
+        g2_load_soa(u, rS, n, dsc.x + j);
+        grp_add(ss, ss, u);
+        if (first) {
+            grp_add(wp, wp, sp);
+            grp_add(ws, ws, ss);
+        }
+    }
+    if (first) {
+        g1_store_soa(wsum, n_groups, g, wp);
+        g2_store_soa(wsum + (size_t)36 * n_groups, n_groups, g, ws);
+    }
+    g1_to_st(o.p, sp, false);
+    g2_to_st(o.s, ss);
+    gpts[g] = o;
+}
+extern "C" __global__ void LCB_BOUNDS k_ts_rlc_wsum(const uint4 *sdesc, u32 n_s, const u32 *wsum, u32 n_l1,
+                                                   ts_grp *gpts) {
+    u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_s) return;
+    u32 l = sdesc[g].w;
+    g1 p;
+    g2 q;
+    ts_grp o;
+    g1_load_soa(p, wsum, n_l1, l);
+    g2_load_soa(q, wsum + (size_t)36 * n_l1, n_l1, l);
+    g1_to_st(o.p, p, false);
+    g2_to_st(o.s, q);
+    gpts[g] = o;
+}
+// miller2_ts (k_ts.hip): the message's line set with sum s_i PK_i, the group signature's lines on the fly with -G
+DN void miller2_ts_grp(fp12 &f, const u32 *lsH, const g1a &PK, const g2a &S, const g1a &G) {
+    g2a Q;
+    LinesOnTheFly sS;
+    sS.init(S);
+    if (lineset_normalised(lsH)) {
+        LinesNorm sH{lsH};
+        miller2(f, sH, PK, sS, G);
+    } else {
+        lineset_point(Q, lsH);
+        LinesOnTheFly sH;
+        sH.init(Q);
+        miller2(f, sH, PK, sS, G);
+    }
+}
+extern "C" __global__ void LCB_PAIR_BOUNDS k_ts_rlc_miller(const u32 *lines, const uint4 *desc, const ts_grp *gpts,
+                                                          u32 n_groups, u32 *f_soa, uint8_t *gacc) {
+    u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_groups) return;
+    u32 m = desc[g].z;
+    g1a P, G;
+    g2a S;
+    st_to_g1a(P, gpts[g].p);
+    st_to_g2a(S, gpts[g].s);
+    g1_generator(G);
+    fp_neg(G.y, G.y);
+    fp12 f;
+    miller2_ts_grp(f, lines + (size_t)m * LCB_LINESET_WORDS, P, S, G);
+    fp12_store_soa(f_soa, n_groups, g, f);
+    gacc[g] = 1;
+}
+
+// ---------------------------------------------------------------- resolve a level (TPKE and TS)
+// Groups [o, o + m) of this level, decided by the final-exponentiation chunk park (stride m).  A failed group of one
+// share rejects it.  At level 1 (first) a failed group of len > 1 goes to the search list (its gamma copied out of the
+// park); below level 1 it becomes ceil(len / s) sub-groups of s = ceil(len / ceil(sqrt(len))) shares, or single
+// shares when len <= LCB_RLC_SINGLES.  gexact (TPKE: W outside G2): every share of the group gets an exact single.
+extern "C" __global__ void LCB_BOUNDS k_rlc_resolve(const uint4 *desc, u32 o, u32 m, const uint8_t *gacc,
+                                                   const uint8_t *gexact, const u32 *park, u32 first, uint8_t *accept,
+                                                   uint4 *next, u32 *next_count, uint4 *search, u32 *search_count,
+                                                   u32 *gamma) {
+    u32 gl = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gl >= m) return;
+    u32 g = o + gl;
     uint4 d = desc[g];
-    if (gexact[g]) {                     // W outside G2: every share of the group gets its exact check
+    if (gexact && gexact[g]) {           // W outside G2: every share of the group gets its exact check
         u32 slot = atomicAdd(next_count, d.y);
         for (u32 k = 0; k < d.y; k++) next[slot + k] = make_uint4(d.x + k, 1, d.z, 1);
         return;
     }
     if (gacc[g]) return;
-    if (d.y == 1) { accept[d.x] = 0; return; }
+    if (d.y == 1) { accept[d.x] = 0; return; }        // (exact singles always have d.y == 1)
+    if (first) {
+        u32 slot = atomicAdd(search_count, 1u);
+        search[slot] = make_uint4(d.x, d.y, d.z, g);
+        fp12 f;
+        fp12_load_soa(f, park, m, gl);
+        const u32 *w = (const u32 *)&f;
+        uint4 *dst = (uint4 *)(gamma + (size_t)slot * 144);
+#pragma unroll
+        for (int q = 0; q < 36; q++) dst[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+        return;
+    }
     u32 parts = 1;
     while (parts * parts < d.y) parts++;
     u32 s = d.y <= LCB_RLC_SINGLES ? 1u : (d.y + parts - 1) / parts;
-    u32 m = (d.y + s - 1) / s;
-    u32 slot = atomicAdd(next_count, m);
-    for (u32 k = 0; k < m; k++) {
+    u32 cnt = (d.y + s - 1) / s;
+    u32 slot = atomicAdd(next_count, cnt);
+    for (u32 k = 0; k < cnt; k++) {
         u32 st = d.x + k * s, len = min(s, d.y - k * s);
-        next[slot + k] = make_uint4(st, len, d.z, 0);     // (a failed exact single has d.y == 1: rejected above)
+        next[slot + k] = make_uint4(st, len, d.z, 0);
     }
+}
+// Level 2: search entries [o, o + m): gamma' (the weighted group check's final-exponentiation output, park stride m)
+// against gamma^c, c = 1..len.  A match rejects share c - 1 of the group (the only bad one, see the header); no match
+// sends every share of the group to a single check at the next level.
+extern "C" __global__ void LCB_BOUNDS k_rlc_search(const uint4 *search, u32 o, u32 m, const u32 *gamma, const u32 *park,
+                                                  uint8_t *accept, uint4 *next, u32 *next_count) {
+    u32 gl = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gl >= m) return;
+    u32 g = o + gl;
+    uint4 d = search[g];
+    fp12 gm, gp, acc;
+    u32 *w = (u32 *)&gm;
+    const uint4 *src = (const uint4 *)(gamma + (size_t)g * 144);
+#pragma unroll
+    for (int q = 0; q < 36; q++) {
+        uint4 v = src[q];
+        w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+    fp12_load_soa(gp, park, m, gl);
+    acc = gm;
+    u32 found = 0;
+    for (u32 c = 1; c <= d.y; c++) {
+        const u32 *a = (const u32 *)&acc, *b = (const u32 *)&gp;
+        u32 x = 0;
+#pragma unroll
+        for (int q = 0; q < 144; q++) x |= a[q] ^ b[q];
+        if (x == 0) { found = c; break; }
+        fp12_mul_n(acc, acc, gm);
+    }
+    if (found) {
+        accept[d.x + found - 1] = 0;
+        return;
+    }
+    u32 slot = atomicAdd(next_count, d.y);
+    for (u32 k = 0; k < d.y; k++) next[slot + k] = make_uint4(d.x + k, 1, d.z, 0);
 }
 
 // ---------------------------------------------------------------- host launch wrappers
@@ -335,16 +586,30 @@ extern "C" void lcbk_tpke_rlc_points(dim3 grid, hipStream_t s, u32 n_cts, const 
     k.nonce[1] = key[9];
     LCB_LAUNCH(k_tpke_rlc_points, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, k, rU, rY, accept);
 }
-extern "C" u32 lcbk_rlc_span() { return LCB_RLC_SPAN; }
-extern "C" void lcbk_rlc_groups(dim3 grid, hipStream_t s, const u32 *ct_idx, u32 n, u32 n_cts, void *desc, u32 *count) {
-    LCB_LAUNCH(k_rlc_groups, ct_idx, n, n_cts, (uint4 *)desc, count);
+extern "C" void lcbk_ts_rlc_points(dim3 grid, hipStream_t s, u32 n_msgs, const void *pks, u32 n_pks,
+                                   const u32 *msg_idx, const u32 *pk_idx, const uint8_t *sigs, u32 n,
+                                   const u32 key[10], u32 *rP, u32 *rS, uint8_t *accept, void *desc, u32 *count) {
+    rlc_key k;
+    for (int j = 0; j < 8; j++) k.k[j] = key[j];
+    k.nonce[0] = key[8];
+    k.nonce[1] = key[9];
+    LCB_LAUNCH(k_ts_rlc_points, n_msgs, (const g1a_st *)pks, n_pks, msg_idx, pk_idx, sigs, n, k, rP, rS, accept,
+               (uint4 *)desc, count);
 }
-extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, const uint8_t *ct_ok,
-                                  const uint8_t *ct_g2, const void *keys, u32 n_keys, const u32 *dec_idx,
-                                  const uint8_t *ui, const u32 *rU, const u32 *rY, u32 n, void *gpts,
-                                  uint8_t *accept, uint8_t *gexact) {
-    LCB_LAUNCH(k_tpke_rlc_sum, (const uint4 *)desc, n_groups, ct_ok, ct_g2, (const g1a_st *)keys, n_keys, dec_idx, ui,
-               rU, rY, n, (g1a_st *)gpts, accept, gexact);
+extern "C" void lcbk_rlc_groups(dim3 grid, hipStream_t s, const u32 *key_idx, u32 n, u32 n_keys, u32 cap, void *desc,
+                                u32 *count) {
+    LCB_LAUNCH(k_rlc_groups, key_idx, n, n_keys, cap, (uint4 *)desc, count);
+}
+extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 first,
+                                  const uint8_t *ct_ok, const uint8_t *ct_g2, const void *keys, u32 n_keys,
+                                  const u32 *dec_idx, const uint8_t *ui, const u32 *rU, const u32 *rY, u32 n,
+                                  void *gpts, uint8_t *accept, uint8_t *gexact, u32 *wsum) {
+    LCB_LAUNCH(k_tpke_rlc_sum, (const uint4 *)desc, n_groups, first, ct_ok, ct_g2, (const g1a_st *)keys, n_keys,
+               dec_idx, ui, rU, rY, n, (g1a_st *)gpts, accept, gexact, wsum);
+}
+extern "C" void lcbk_tpke_rlc_wsum(dim3 grid, hipStream_t s, const void *sdesc, u32 n_s, const u32 *wsum, u32 n_l1,
+                                   void *gpts) {
+    LCB_LAUNCH(k_tpke_rlc_wsum, (const uint4 *)sdesc, n_s, wsum, n_l1, (g1a_st *)gpts);
 }
 extern "C" void lcbk_tpke_ct_g2check(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts,
                                      uint8_t *ct_g2) {
@@ -354,7 +619,29 @@ extern "C" void lcbk_tpke_rlc_miller(dim3 grid, hipStream_t s, const u32 *lines,
                                      u32 n_groups, u32 *f_soa, uint8_t *gacc) {
     LCB_LAUNCH(k_tpke_rlc_miller, lines, (const uint4 *)desc, (const g1a_st *)gpts, n_groups, f_soa, gacc);
 }
-extern "C" void lcbk_rlc_resolve(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, const uint8_t *gacc,
-                                 const uint8_t *gexact, uint8_t *accept, void *next, u32 *next_count) {
-    LCB_LAUNCH(k_rlc_resolve, (const uint4 *)desc, n_groups, gacc, gexact, accept, (uint4 *)next, next_count);
+extern "C" void lcbk_ts_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 first,
+                                const uint8_t *msg_ok, const void *pks, u32 n_pks, const u32 *pk_idx,
+                                const uint8_t *sigs, const u32 *rP, const u32 *rS, u32 n, void *gpts, uint8_t *accept,
+                                uint8_t *gexact, u32 *wsum) {
+    LCB_LAUNCH(k_ts_rlc_sum, (const uint4 *)desc, n_groups, first, msg_ok, (const g1a_st *)pks, n_pks, pk_idx, sigs,
+               rP, rS, n, (ts_grp *)gpts, accept, gexact, wsum);
 }
+extern "C" void lcbk_ts_rlc_wsum(dim3 grid, hipStream_t s, const void *sdesc, u32 n_s, const u32 *wsum, u32 n_l1,
+                                 void *gpts) {
+    LCB_LAUNCH(k_ts_rlc_wsum, (const uint4 *)sdesc, n_s, wsum, n_l1, (ts_grp *)gpts);
+}
+extern "C" void lcbk_ts_rlc_miller(dim3 grid, hipStream_t s, const u32 *lines, const void *desc, const void *gpts,
+                                   u32 n_groups, u32 *f_soa, uint8_t *gacc) {
+    LCB_LAUNCH(k_ts_rlc_miller, lines, (const uint4 *)desc, (const ts_grp *)gpts, n_groups, f_soa, gacc);
+}
+extern "C" void lcbk_rlc_resolve(dim3 grid, hipStream_t s, const void *desc, u32 o, u32 m, const uint8_t *gacc,
+                                 const uint8_t *gexact, const u32 *park, u32 first, uint8_t *accept, void *next,
+                                 u32 *next_count, void *search, u32 *search_count, u32 *gamma) {
+    LCB_LAUNCH(k_rlc_resolve, (const uint4 *)desc, o, m, gacc, gexact, park, first, accept, (uint4 *)next, next_count,
+               (uint4 *)search, search_count, gamma);
+}
+extern "C" void lcbk_rlc_search(dim3 grid, hipStream_t s, const void *search, u32 o, u32 m, const u32 *gamma,
+                                const u32 *park, uint8_t *accept, void *next, u32 *next_count) {
+    LCB_LAUNCH(k_rlc_search, (const uint4 *)search, o, m, gamma, park, accept, (uint4 *)next, next_count);
+}
+extern "C" size_t lcbk_ts_grp_bytes() { return sizeof(ts_grp); }

@@ -52,10 +52,11 @@ struct lcb_ctx {
     hipEvent_t ver_ev[3] = {};
     bool ver_ev_ready = false, ver_ran = false;
     // randomized batch verification (k_batch.hip): r_i U_i / r_i Y_i records, group lists, group points, counts
-    DevBuf rlc[9];
+    DevBuf rlc[12];
     hipEvent_t rlc_ev[3] = {};
     hipEvent_t rlc_lev_ev[4] = {};    // per level: before sum / Miller / final exp / resolve
-    float rlc_ms[4] = {};             // accumulated over the levels of the last call: sum, Miller, final exp, resolve
+    float rlc_ms[4] = {};             // accumulated over the levels of the last call: sums, Miller, final exp (+ resolve
+                                      // / search), unused
     bool rlc_ev_ready = false, rlc_ran = false;
     uint32_t rlc_levels[8] = {};
     int rlc_nlev = 0;

@@ -685,50 +685,70 @@ int tpke_partial_decrypt_prepared(lcb_ctx *c, uint8_t *ui_out, uint8_t *status, 
     return launched("tpke partial decrypt launch") ? 0 : -1;
 }
 
-// Randomized batch verification (k_batch.hip header): the same accept / reject decisions as tpke_verify_prepared,
-// except with probability <= 2^-64 per accepted group (a false accept needs the secret exponents).  Groups are runs of
-// shares of one ciphertext in the caller's order (ciphertext-major batches give one group per ciphertext); a level's
-// group count comes back to the host (one 4-byte read per level) to size the next launches.
+// Randomized batch verification (k_batch.hip header): the same accept / reject decisions as the exact per-share
+// checks, except with probability <= 2^-64 per group decision (the exponents are secret).  Groups are runs of shares
+// of one ciphertext (TPKE) / message (threshold signatures) in the caller's order: ciphertext- / message-major batches
+// give one group per ciphertext / message.  A level's group count comes back to the host (one 8-byte read per level).
 uint8_t g_rlc_seed[32];
 bool g_rlc_seed_set = false;
-struct RlcWs { u32 *rU, *rY; uint8_t *dA, *dB; u32 *cnt; };
-// phase 1 (needs the decompressed keys only): per-share exponent multiples + level-1 groups (count left on device)
-int rlc_points_enqueue(lcb_ctx *c, RlcWs &w, uint8_t *d_accept, size_t n, size_t n_keys, size_t n_cts,
-                       const uint32_t *d_ct, const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
-    u32 key[10];
+enum RlcKind { RLC_TPKE = 0, RLC_TS = 1 };
+struct RlcStats { bool valid = false; int nlev = 0; uint32_t levels[8] = {}; float ms[6] = {}; };
+thread_local RlcStats t_rlc_stats;
+struct RlcWs { u32 *rA, *rB; uint8_t *dA, *dB; u32 *cnt; };    // cnt: [current, next, search]
+bool rlc_key_fill(lcb_ctx *c, u32 key[10]) {
     if (g_rlc_seed_set) memcpy(key, g_rlc_seed, 32);
-    else if (getrandom(key, 32, 0) != 32) { set_err("tpke batched verify: getrandom failed"); return -1; }
+    else if (getrandom(key, 32, 0) != 32) { set_err("batched verify: getrandom failed"); return false; }
     c->rlc_calls++;
     key[8] = (u32)c->rlc_calls;
     key[9] = (u32)(c->rlc_calls >> 32);
-    w.rU = (u32 *)c->rlc[0].get(n * LCB_G1_JAC_BYTES);
-    w.rY = (u32 *)c->rlc[1].get(n * LCB_G1_JAC_BYTES);
+    return true;
+}
+bool rlc_ws(lcb_ctx *c, RlcWs &w, size_t n, size_t rec_a, size_t rec_b) {
+    w.rA = (u32 *)c->rlc[0].get(n * rec_a);
+    w.rB = (u32 *)c->rlc[1].get(n * rec_b);
     w.dA = (uint8_t *)c->rlc[2].get(n * 16);
     w.dB = (uint8_t *)c->rlc[3].get(n * 16);
     w.cnt = (u32 *)c->rlc[4].get(16);
-    if (!w.rU || !w.rY || !w.dA || !w.dB || !w.cnt) { set_err("device allocation failed"); return -1; }
+    if (!w.rA || !w.rB || !w.dA || !w.dB || !w.cnt) { set_err("device allocation failed"); return false; }
     if (!c->rlc_ev_ready) {
         for (auto &e : c->rlc_ev) hipEventCreate(&e);
         for (auto &e : c->rlc_lev_ev) hipEventCreate(&e);
         c->rlc_ev_ready = true;
     }
+    return true;
+}
+// phase 1 (needs the decompressed keys only): per-share exponent multiples + level-1 groups (count left on device)
+int rlc_points_enqueue(lcb_ctx *c, RlcWs &w, uint8_t *d_accept, size_t n, size_t n_keys, size_t n_cts,
+                       const uint32_t *d_ct, const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
+    u32 key[10];
+    if (!rlc_key_fill(c, key) || !rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G1_JAC_BYTES)) return -1;
     hipEventRecord(c->rlc_ev[0], s);
-    hipMemsetAsync(w.cnt, 0, 8, s);
-    lcbk_tpke_rlc_points(dim3(nblk(n)), s, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct, d_dec, d_ui, (u32)n, key, w.rU,
-                         w.rY, d_accept);
-    const size_t span = lcbk_rlc_span();
-    lcbk_rlc_groups(dim3(nblk((n + span - 1) / span)), s, d_ct, (u32)n, (u32)n_cts, w.dA, w.cnt);
+    hipMemsetAsync(w.cnt, 0, 16, s);
+    lcbk_tpke_rlc_points(dim3(nblk(n)), s, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct, d_dec, d_ui, (u32)n, key, w.rA,
+                         w.rB, d_accept);
+    lcbk_rlc_groups(dim3(nblk(n)), s, d_ct, (u32)n, (u32)n_cts, 32, w.dA, w.cnt);
     hipEventRecord(c->rlc_ev[1], s);
     return launched("tpke batched verify launch") ? 0 : -1;
 }
-bool read_count(u32 &v, const u32 *d, hipStream_t s) {
-    if (hipMemcpyAsync(&v, d, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
-        set_err("tpke batched verify: group count");
+int ts_rlc_points_enqueue(lcb_ctx *c, RlcWs &w, uint8_t *d_accept, size_t n, size_t n_pks, size_t n_msgs,
+                          const uint8_t *d_sigs, const uint32_t *d_midx, const uint32_t *d_pidx, hipStream_t s) {
+    u32 key[10];
+    if (!rlc_key_fill(c, key) || !rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G2_JAC_BYTES)) return -1;
+    hipEventRecord(c->rlc_ev[0], s);
+    hipMemsetAsync(w.cnt, 0, 16, s);
+    lcbk_ts_rlc_points(dim3(nblk(n)), s, (u32)n_msgs, c->s_keys.p, (u32)n_pks, d_midx, d_pidx, d_sigs, (u32)n, key,
+                       w.rA, w.rB, d_accept, w.dA, w.cnt);
+    lcbk_rlc_groups(dim3(nblk(n)), s, d_midx, (u32)n, (u32)n_msgs, 128, w.dA, w.cnt);
+    hipEventRecord(c->rlc_ev[1], s);
+    return launched("ts batched verify launch") ? 0 : -1;
+}
+bool read_counts(u32 *v, const u32 *d, int k, hipStream_t s) {
+    if (hipMemcpyAsync(v, d, 4 * k, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+        set_err("batched verify: group count");
         return false;
     }
     return true;
 }
-// phase 2 (after the ciphertext preparation): group checks, level by level
 // W of every prepared ciphertext in G2 -> rlc[8]
 int rlc_g2check(lcb_ctx *c, hipStream_t s) {
     uint8_t *ctg2 = (uint8_t *)c->rlc[8].get(c->t_n_cts);
@@ -738,54 +758,114 @@ int rlc_g2check(lcb_ctx *c, hipStream_t s) {
                              (u32)c->t_n_cts, ctg2);
     return 0;
 }
-int rlc_levels(lcb_ctx *c, RlcWs &w, uint8_t *d_accept, size_t n, const uint32_t *d_dec, const uint8_t *d_ui,
-               hipStream_t s) {
-    const u32 *lines = (const u32 *)c->t_lines.p;
-    const uint8_t *ctok = (const uint8_t *)c->t_ctok.p;
+struct RlcIo {                     // the per-share inputs the exact singles re-read
+    const uint32_t *d_key;         // dec_idx (TPKE) / pk_idx (TS)
+    const uint8_t *d_pts;          // ui (TPKE) / sigs (TS)
+};
+// phase 2 (after the preparation): level 1 group checks; level 2: weighted re-check + search of the failed groups;
+// then single checks
+int rlc_levels(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, size_t n, RlcIo io, hipStream_t s) {
+    const bool ts = kind == RLC_TS;
+    const u32 *lines = (const u32 *)(ts ? c->s_lines.p : c->t_lines.p);
+    const uint8_t *okv = (const uint8_t *)(ts ? c->s_mok.p : c->t_ctok.p);
     const uint8_t *ctg2 = (const uint8_t *)c->rlc[8].p;
-    u32 groups = 0;
+    const size_t rec = ts ? lcbk_ts_grp_bytes() : 2 * LCB_G1A_ST_BYTES;
+    const size_t wrec = ts ? LCB_G1_JAC_BYTES + LCB_G2_JAC_BYTES : 2 * LCB_G1_JAC_BYTES;
+    u32 cnt[3] = {0, 0, 0};
     for (auto &m : c->rlc_ms) m = 0.0f;
-    if (!read_count(groups, w.cnt, s)) return -1;
-    for (int lev = 0; groups; lev++) {
-        if (lev > 40) { set_err("tpke batched verify: group splitting did not terminate"); return -1; }
-        if (lev < 8) c->rlc_levels[lev] = groups;
-        c->rlc_nlev = lev + 1;
-        void *gpts = c->rlc[5].get((size_t)groups * 2 * LCB_G1A_ST_BYTES);
-        uint8_t *gacc = (uint8_t *)c->rlc[6].get(groups), *gex = (uint8_t *)c->rlc[7].get(groups);
-        const size_t nf = groups < LCB_VERIFY_CHUNK ? groups : LCB_VERIFY_CHUNK;
-        u32 *f = (u32 *)c->t_f.get(nf * 576 * (size_t)lcbk_fe_slots());
-        if (!gpts || !gacc || !gex || !f) { set_err("device allocation failed"); return -1; }
-        hipMemsetAsync(w.cnt + 1, 0, 4, s);
-        hipEvent_t *ev = c->rlc_lev_ev;
-        hipEventRecord(ev[0], s);
-        lcbk_tpke_rlc_sum(dim3(nblk(groups)), s, w.dA, groups, ctok, ctg2, c->t_keys.p, (u32)c->t_n_keys, d_dec, d_ui,
-                          w.rU, w.rY, (u32)n, gpts, d_accept, gex);
-        float ms[3] = {0, 0, 0}, t;
-        for (size_t o = 0; o < groups; o += LCB_VERIFY_CHUNK) {
-            const size_t m = groups - o < LCB_VERIFY_CHUNK ? groups - o : LCB_VERIFY_CHUNK;
+    if (!read_counts(cnt, w.cnt, 1, s)) return -1;
+    u32 groups = cnt[0];
+    hipEvent_t *ev = c->rlc_lev_ev;
+    float t;
+    // Miller + final exponentiation (+ resolve / search) over the groups of desc in chunks; gpts holds the points
+    auto checks = [&](const uint8_t *desc, u32 count, void *gpts, uint8_t *gacc, u32 *f, bool search_stage,
+                      bool first, uint8_t *gex, uint4 *sdesc, u32 *gamma) {
+        for (size_t o = 0; o < count; o += LCB_VERIFY_CHUNK) {
+            const size_t m = count - o < LCB_VERIFY_CHUNK ? count - o : LCB_VERIFY_CHUNK;
             hipEventRecord(ev[1], s);
-            lcbk_tpke_rlc_miller(dim3(nblk(m)), s, lines, w.dA + 16 * o,
-                                 (const uint8_t *)gpts + 2 * LCB_G1A_ST_BYTES * o, (u32)m, f, gacc + o);
+            if (ts)
+                lcbk_ts_rlc_miller(dim3(nblk(m)), s, lines, desc + 16 * o, (const uint8_t *)gpts + rec * o, (u32)m, f,
+                                   gacc + o);
+            else
+                lcbk_tpke_rlc_miller(dim3(nblk(m)), s, lines, desc + 16 * o, (const uint8_t *)gpts + rec * o, (u32)m, f,
+                                     gacc + o);
             hipEventRecord(ev[2], s);
             lcbk_final_exp_check(dim3(nblk(m)), s, f, (u32)m, gacc + o);
             hipEventRecord(ev[3], s);
-            if (o == 0 && hipEventSynchronize(ev[1]) == hipSuccess && hipEventElapsedTime(&t, ev[0], ev[1]) == hipSuccess) ms[0] += t;
+            if (search_stage)
+                lcbk_rlc_search(dim3(nblk(m)), s, sdesc, (u32)o, (u32)m, gamma, f, d_accept, w.dB, w.cnt + 1);
+            else
+                lcbk_rlc_resolve(dim3(nblk(m)), s, desc, (u32)o, (u32)m, gacc, gex, f, first ? 1u : 0u, d_accept, w.dB,
+                                 w.cnt + 1, sdesc, w.cnt + 2, gamma);
             if (hipEventSynchronize(ev[3]) == hipSuccess) {
-                if (hipEventElapsedTime(&t, ev[1], ev[2]) == hipSuccess) ms[1] += t;
-                if (hipEventElapsedTime(&t, ev[2], ev[3]) == hipSuccess) ms[2] += t;
+                if (hipEventElapsedTime(&t, ev[1], ev[2]) == hipSuccess) c->rlc_ms[1] += t;
+                if (hipEventElapsedTime(&t, ev[2], ev[3]) == hipSuccess) c->rlc_ms[2] += t;
             }
         }
-        lcbk_rlc_resolve(dim3(nblk(groups)), s, w.dA, groups, gacc, gex, d_accept, w.dB, w.cnt + 1);
+    };
+    for (int lev = 0; groups; lev++) {
+        if (lev > 40) { set_err("batched verify: group splitting did not terminate"); return -1; }
+        if (lev < 8) c->rlc_levels[lev] = groups;
+        c->rlc_nlev = lev + 1;
+        const bool first = lev == 0;
+        void *gpts = c->rlc[5].get((size_t)groups * rec);
+        uint8_t *gacc = (uint8_t *)c->rlc[6].get(groups), *gex = (uint8_t *)c->rlc[7].get(groups);
+        const size_t nf = groups < LCB_VERIFY_CHUNK ? groups : LCB_VERIFY_CHUNK;
+        u32 *f = (u32 *)c->t_f.get(nf * 576 * (size_t)lcbk_fe_slots());
+        uint4 *sdesc = nullptr;
+        u32 *gamma = nullptr, *wsum = nullptr;
+        if (first) {
+            sdesc = (uint4 *)c->rlc[9].get((size_t)groups * 16);
+            gamma = (u32 *)c->rlc[10].get((size_t)groups * 576);
+            wsum = (u32 *)c->rlc[11].get((size_t)groups * wrec);
+        }
+        if (!gpts || !gacc || !gex || !f || (first && (!sdesc || !gamma || !wsum))) {
+            set_err("device allocation failed");
+            return -1;
+        }
+        hipMemsetAsync(w.cnt + 1, 0, 8, s);
         hipEventRecord(ev[0], s);
-        if (!launched("tpke batched verify launch")) return -1;
-        if (!read_count(groups, w.cnt + 1, s)) return -1;
-        if (hipEventElapsedTime(&t, ev[3], ev[0]) == hipSuccess) c->rlc_ms[3] += t;
-        for (int k = 0; k < 3; k++) c->rlc_ms[k] += ms[k];
-        std::swap(w.dA, w.dB);            // the next level's groups; its count was read from cnt[1]
+        if (ts)
+            lcbk_ts_rlc_sum(dim3(nblk(groups)), s, w.dA, groups, first, okv, c->s_keys.p, (u32)c->s_n_pks, io.d_key,
+                            io.d_pts, w.rA, w.rB, (u32)n, gpts, d_accept, gex, wsum);
+        else
+            lcbk_tpke_rlc_sum(dim3(nblk(groups)), s, w.dA, groups, first, okv, ctg2, c->t_keys.p, (u32)c->t_n_keys,
+                              io.d_key, io.d_pts, w.rA, w.rB, (u32)n, gpts, d_accept, gex, wsum);
+        hipEventRecord(ev[1], s);
+        if (hipEventSynchronize(ev[1]) == hipSuccess && hipEventElapsedTime(&t, ev[0], ev[1]) == hipSuccess)
+            c->rlc_ms[0] += t;
+        checks(w.dA, groups, gpts, gacc, f, false, first, gex, sdesc, gamma);
+        if (!launched("batched verify launch")) return -1;
+        if (!read_counts(cnt, w.cnt, 3, s)) return -1;
+        if (first && cnt[2]) {           // level 2: weighted re-check of the failed groups, then the search
+            const u32 ns = cnt[2];
+            if (lev + 1 < 8) c->rlc_levels[lev + 1] = ns;
+            c->rlc_nlev = ++lev + 1;
+            void *gp2 = c->rlc[5].get((size_t)ns * rec);   // (ns <= groups: the level-1 buffers are large enough)
+            hipEventRecord(ev[0], s);
+            if (ts) lcbk_ts_rlc_wsum(dim3(nblk(ns)), s, sdesc, ns, wsum, groups, gp2);
+            else lcbk_tpke_rlc_wsum(dim3(nblk(ns)), s, sdesc, ns, wsum, groups, gp2);
+            hipEventRecord(ev[1], s);
+            if (hipEventSynchronize(ev[1]) == hipSuccess && hipEventElapsedTime(&t, ev[0], ev[1]) == hipSuccess)
+                c->rlc_ms[0] += t;
+            checks((const uint8_t *)sdesc, ns, gp2, gacc, f, true, false, nullptr, sdesc, gamma);
+            if (!launched("batched verify launch")) return -1;
+            if (!read_counts(cnt + 1, w.cnt + 1, 1, s)) return -1;
+        }
+        groups = cnt[1];
+        std::swap(w.dA, w.dB);            // the next level's groups
     }
     hipEventRecord(c->rlc_ev[2], s);
     c->rlc_ran = true;
-    return launched("tpke batched verify launch") ? 0 : -1;
+    // the calling thread's copy of the statistics (lcb_tpke_batched_stats without a context)
+    RlcStats &st = t_rlc_stats;
+    st.valid = hipEventSynchronize(c->rlc_ev[2]) == hipSuccess;
+    st.nlev = c->rlc_nlev;
+    for (int i = 0; i < 8; i++) st.levels[i] = i < c->rlc_nlev ? c->rlc_levels[i] : 0;
+    for (int i = 0; i < 2; i++)
+        if (!st.valid || hipEventElapsedTime(&st.ms[i], c->rlc_ev[i], c->rlc_ev[i + 1]) != hipSuccess) st.ms[i] = -1.0f;
+    for (int i = 0; i < 4; i++) st.ms[2 + i] = c->rlc_ms[i];
+    return launched("batched verify launch") ? 0 : -1;
 }
 int tpke_verify_prepared_rlc(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_keys, size_t n_cts, const uint32_t *d_ct,
                              const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
@@ -796,9 +876,17 @@ int tpke_verify_prepared_rlc(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_k
     RlcWs w;
     if (rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, s)) return -1;
     if (rlc_g2check(c, s)) return -1;
-    return rlc_levels(c, w, d_accept, n, d_dec, d_ui, s);
+    return rlc_levels(c, RLC_TPKE, w, d_accept, n, RlcIo{d_dec, d_ui}, s);
 }
-
+bool fork_ready(lcb_ctx *c) {
+    if (c->fork_ready) return true;
+    hipError_t e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
+    for (auto &ev : c->fork_ev)
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    if (e != hipSuccess) { set_err("batched verify: stream creation", e); return false; }
+    c->fork_ready = true;
+    return true;
+}
 // prepare + batched verify in one call: the randomisation (needs only the keys) runs on the context's second
 // stream beside the per-ciphertext hashing / line sets (latency-bound: < 1 wave per SIMD for 50 K ciphertexts)
 int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const uint8_t *d_y, size_t n_keys,
@@ -812,13 +900,7 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
     uint8_t *ctok = (uint8_t *)c->t_ctok.get(n_cts);
     void *keys = c->t_keys.get(n_keys * LCB_G1A_ST_BYTES);
     if (!lines || !ctok || !keys) { set_err("device allocation failed"); return -1; }
-    if (!c->fork_ready) {
-        hipError_t e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
-        for (auto &ev : c->fork_ev)
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-        if (e != hipSuccess) { set_err("tpke batched verify: stream creation", e); return -1; }
-        c->fork_ready = true;
-    }
+    if (!fork_ready(c)) return -1;
     if (n_keys) lcbk_g1_decompress(dim3(nblk(n_keys)), s, d_y, (u32)n_keys, keys);
     RlcWs w;
     if (n) {
@@ -840,7 +922,7 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
     if (!n) return 0;
     if (rlc_g2check(c, s)) return -1;      // still beside the randomisation on the second stream
     hipStreamWaitEvent(s, c->fork_ev[1], 0);
-    return rlc_levels(c, w, d_accept, n, d_dec, d_ui, s);
+    return rlc_levels(c, RLC_TPKE, w, d_accept, n, RlcIo{d_dec, d_ui}, s);
 }
 
 // ------------------------------------------------------------------ threshold signatures
@@ -887,6 +969,57 @@ int ts_verify_prepared(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_pks, si
         }
     }
     return launched("ts verify launch") ? 0 : -1;
+}
+
+bool ts_shape_ok(lcb_ctx *c, size_t n_pks, size_t n_msgs, const char *what) {
+    if (!c->s_ready) { set_err((std::string(what) + ": no threshold-signature batch prepared in this context").c_str()); return false; }
+    if (c->s_n_msgs != n_msgs || c->s_n_pks != n_pks) {
+        set_err((std::string(what) + ": batch shape differs from the one prepared in this context").c_str());
+        return false;
+    }
+    return true;
+}
+// randomized batch form of ts_verify_prepared (k_batch.hip): groups = runs of one message (<= 128 shares)
+int ts_verify_prepared_rlc(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_pks, size_t n_msgs, const uint8_t *d_sigs,
+                           const uint32_t *d_midx, const uint32_t *d_pidx, hipStream_t s) {
+    if (!ts_shape_ok(c, n_pks, n_msgs, "ts batched verify")) return -1;
+    if (n > 0xffffffffu) { set_err("ts batched verify: batch too large"); return -1; }
+    c->rlc_nlev = 0;
+    if (!n) return 0;
+    RlcWs w;
+    if (ts_rlc_points_enqueue(c, w, d_accept, n, n_pks, n_msgs, d_sigs, d_midx, d_pidx, s)) return -1;
+    return rlc_levels(c, RLC_TS, w, d_accept, n, RlcIo{d_pidx, d_sigs}, s);
+}
+// prepare + batched verify: the randomisation (keys only) beside the message hashing on the second stream
+int ts_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const uint8_t *d_pks, size_t n_pks,
+                               const uint8_t *d_sigs, const uint8_t *d_msg, const uint32_t *d_moff, size_t n_msgs,
+                               const uint32_t *d_midx, const uint32_t *d_pidx, hipStream_t s) {
+    if (n_msgs > 0xffffffffu || n_pks > 0xffffffffu || n > 0xffffffffu) { set_err("ts batched verify: batch too large"); return -1; }
+    c->s_ready = false;
+    c->rlc_nlev = 0;
+    u32 *lines = (u32 *)c->s_lines.get((size_t)n_msgs * LCB_LINESET_BYTES);
+    uint8_t *mok = (uint8_t *)c->s_mok.get(n_msgs);
+    void *keys = c->s_keys.get(n_pks * LCB_G1A_ST_BYTES);
+    if (!lines || !mok || !keys) { set_err("device allocation failed"); return -1; }
+    if (!fork_ready(c)) return -1;
+    if (n_pks) lcbk_g1_decompress(dim3(nblk(n_pks)), s, d_pks, (u32)n_pks, keys);
+    RlcWs w;
+    if (n) {
+        hipEventRecord(c->fork_ev[0], s);
+        hipStreamWaitEvent(c->aux, c->fork_ev[0], 0);
+        if (ts_rlc_points_enqueue(c, w, d_accept, n, n_pks, n_msgs, d_sigs, d_midx, d_pidx, c->aux)) return -1;
+        hipEventRecord(c->fork_ev[1], c->aux);
+    }
+    if (n_msgs) lcbk_ts_msg_prepare(dim3(nblk(n_msgs)), s, d_msg, d_moff, (u32)n_msgs, lines, mok,
+                                    g_orig_cofactor | (g_line_mode << 1));
+    if (!launched("ts prepare launch")) return -1;
+    c->s_n_msgs = n_msgs;
+    c->s_n_pks = n_pks;
+    c->s_gen++;
+    c->s_ready = true;
+    if (!n) return 0;
+    hipStreamWaitEvent(s, c->fork_ev[1], 0);
+    return rlc_levels(c, RLC_TS, w, d_accept, n, RlcIo{d_pidx, d_sigs}, s);
 }
 
 // ------------------------------------------------------------------ Lagrange / assembly
@@ -1117,7 +1250,13 @@ extern "C" int lcb_ctx_tpke_batched_stats(lcb_ctx *ctx, uint32_t levels[8], floa
     for (int i = 0; i < 4; i++) ms[2 + i] = c->rlc_ms[i];
     return c->rlc_nlev;
 }
-extern "C" int lcb_tpke_batched_stats(uint32_t levels[8], float ms[6]) { return lcb_ctx_tpke_batched_stats(nullptr, levels, ms); }
+extern "C" int lcb_tpke_batched_stats(uint32_t levels[8], float ms[6]) {
+    const RlcStats &st = t_rlc_stats;
+    if (!st.valid) { set_err("batched verify: none has completed on this thread"); return -1; }
+    for (int i = 0; i < 8; i++) levels[i] = st.levels[i];
+    for (int i = 0; i < 6; i++) ms[i] = st.ms[i];
+    return st.nlev;
+}
 extern "C" void lcb_set_batch_seed(const uint8_t *seed32) {
     if (seed32) { memcpy(g_rlc_seed, seed32, 32); g_rlc_seed_set = true; }
     else g_rlc_seed_set = false;
@@ -1297,9 +1436,36 @@ extern "C" int lcb_ts_verify_shares_dev(uint8_t *accept, size_t n, const uint8_t
     if (ts_prepare(c, pks, n_pks, msg_data, msg_off, n_msgs, q.s)) return -1;
     return ts_verify_prepared(c, accept, n, n_pks, n_msgs, sigs, msg_idx, pk_idx, q.s);
 }
-extern "C" int lcb_ts_verify_shares(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks, const uint8_t *sigs,
-                                    const uint8_t *msg_data, const uint32_t *msg_off, size_t n_msgs,
-                                    const uint32_t *msg_idx, const uint32_t *pk_idx) {
+extern "C" int lcb_ctx_ts_verify_prepared_batched_dev(lcb_ctx *ctx, uint8_t *accept, size_t n, size_t n_pks,
+                                                      size_t n_msgs, const uint8_t *sigs, const uint32_t *msg_idx,
+                                                      const uint32_t *pk_idx, void *stream) {
+    CTX_OR(c, ctx, -1)
+    Enq q(c, (hipStream_t)stream);
+    return ts_verify_prepared_rlc(c, accept, n, n_pks, n_msgs, sigs, msg_idx, pk_idx, q.s);
+}
+extern "C" int lcb_ts_verify_prepared_batched_dev(uint8_t *accept, size_t n, size_t n_pks, size_t n_msgs,
+                                                  const uint8_t *sigs, const uint32_t *msg_idx, const uint32_t *pk_idx,
+                                                  void *stream) {
+    return lcb_ctx_ts_verify_prepared_batched_dev(nullptr, accept, n, n_pks, n_msgs, sigs, msg_idx, pk_idx, stream);
+}
+extern "C" int lcb_ctx_ts_verify_shares_batched_dev(lcb_ctx *ctx, uint8_t *accept, size_t n, const uint8_t *pks,
+                                                    size_t n_pks, const uint8_t *sigs, const uint8_t *msg_data,
+                                                    const uint32_t *msg_off, size_t n_msgs, const uint32_t *msg_idx,
+                                                    const uint32_t *pk_idx, void *stream) {
+    CTX_OR(c, ctx, -1)
+    Enq q(c, (hipStream_t)stream);
+    return ts_verify_shares_rlc_fused(c, accept, n, pks, n_pks, sigs, msg_data, msg_off, n_msgs, msg_idx, pk_idx, q.s);
+}
+extern "C" int lcb_ts_verify_shares_batched_dev(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks,
+                                                const uint8_t *sigs, const uint8_t *msg_data, const uint32_t *msg_off,
+                                                size_t n_msgs, const uint32_t *msg_idx, const uint32_t *pk_idx,
+                                                void *stream) {
+    return lcb_ctx_ts_verify_shares_batched_dev(nullptr, accept, n, pks, n_pks, sigs, msg_data, msg_off, n_msgs,
+                                                msg_idx, pk_idx, stream);
+}
+static int ts_verify_shares_host(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks, const uint8_t *sigs,
+                                 const uint8_t *msg_data, const uint32_t *msg_off, size_t n_msgs,
+                                 const uint32_t *msg_idx, const uint32_t *pk_idx, bool batched) {
     SYNC_CTX_OR(c, -1)
     for (size_t i = 0; i < n; i++) {
         if (msg_idx[i] >= n_msgs) { set_err("msg_idx out of range"); return -1; }
@@ -1316,10 +1482,24 @@ extern "C" int lcb_ts_verify_shares(uint8_t *accept, size_t n, const uint8_t *pk
     const uint32_t *dpi = up(c->in[5], pk_idx, n, s);
     uint8_t *dacc = (uint8_t *)c->out[0].get(n);
     if (!dpk || !dsig || !dm || !dmo || !dmi || !dpi || !dacc) { set_err("device allocation failed"); return -1; }
-    if (ts_prepare(c, dpk, n_pks, dm, dmo, n_msgs, s)) return -1;
-    if (ts_verify_prepared(c, dacc, n, n_pks, n_msgs, dsig, dmi, dpi, s)) return -1;
+    if (batched) {
+        if (ts_verify_shares_rlc_fused(c, dacc, n, dpk, n_pks, dsig, dm, dmo, n_msgs, dmi, dpi, s)) return -1;
+    } else {
+        if (ts_prepare(c, dpk, n_pks, dm, dmo, n_msgs, s)) return -1;
+        if (ts_verify_prepared(c, dacc, n, n_pks, n_msgs, dsig, dmi, dpi, s)) return -1;
+    }
     if (n) hipMemcpyAsync(accept, dacc, n, hipMemcpyDeviceToHost, s);
     return sync_check(c, "ts verify") ? 0 : -1;
+}
+extern "C" int lcb_ts_verify_shares(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks, const uint8_t *sigs,
+                                    const uint8_t *msg_data, const uint32_t *msg_off, size_t n_msgs,
+                                    const uint32_t *msg_idx, const uint32_t *pk_idx) {
+    return ts_verify_shares_host(accept, n, pks, n_pks, sigs, msg_data, msg_off, n_msgs, msg_idx, pk_idx, false);
+}
+extern "C" int lcb_ts_verify_shares_batched(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks,
+                                            const uint8_t *sigs, const uint8_t *msg_data, const uint32_t *msg_off,
+                                            size_t n_msgs, const uint32_t *msg_idx, const uint32_t *pk_idx) {
+    return ts_verify_shares_host(accept, n, pks, n_pks, sigs, msg_data, msg_off, n_msgs, msg_idx, pk_idx, true);
 }
 extern "C" int lcb_ts_sign(uint8_t *sigs_out, const uint8_t *sks, const uint8_t *msg_data, const uint32_t *msg_off,
                            const uint32_t *msg_idx, size_t n) {

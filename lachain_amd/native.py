@@ -70,6 +70,13 @@ _SIGS = {
                                                           ctypes.c_void_p, ctypes.c_void_p]),
     "lcb_tpke_verify_prepared_batched_dev": (ctypes.c_int, [ctypes.c_void_p, c_size, c_size, c_size, ctypes.c_void_p,
                                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "lcb_ts_verify_shares_batched": (ctypes.c_int, [c_u8p, c_size, c_u8p, c_size, c_u8p, c_u8p, c_u32p, c_size,
+                                                    c_u32p, c_u32p]),
+    "lcb_ts_verify_prepared_batched_dev": (ctypes.c_int, [ctypes.c_void_p, c_size, c_size, c_size, ctypes.c_void_p,
+                                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "lcb_ts_verify_shares_batched_dev": (ctypes.c_int, [ctypes.c_void_p, c_size, ctypes.c_void_p, c_size,
+                                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_size,
+                                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "lcb_tpke_batched_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_float)]),
     "lcb_set_batch_seed": (None, [ctypes.c_char_p]),
     "lcb_tpke_partial_decrypt": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_u8p, c_u8p, c_u32p, c_size]),
@@ -163,7 +170,7 @@ _SIGS = {
 }
 # explicit-context forms: the context pointer first, then the same arguments as the context-less form
 for _name in ("tpke_prepare_dev", "tpke_verify_prepared_dev", "tpke_verify_prepared_batched_dev", "tpke_batched_stats",
-              "tpke_verify_shares_batched_dev", "tpke_partial_decrypt_prepared_dev", "tpke_combine_dev",
+              "tpke_verify_shares_batched_dev", "ts_verify_prepared_batched_dev", "ts_verify_shares_batched_dev", "tpke_partial_decrypt_prepared_dev", "tpke_combine_dev",
               "tpke_verify_phase_ms", "ts_prepare_dev", "ts_verify_prepared_dev", "ts_assemble_dev", "g1_lagrange_dev",
               "g2_lagrange_dev", "g1_msm_dev", "g1_msm_glv_dev", "g1_msm_phase_ms", "ecdsa_verify_hashed_dev",
               "root_header_verify_dev", "ecdsa_pubkey_dev", "ecdsa_sign_hashed_dev", "ecdsa_phase_ms"):
@@ -304,8 +311,9 @@ def tpke_encrypt_phase2(us, rs, vs):
     return [w[96 * i:96 * i + 96] for i in range(n)]
 
 
-def ts_verify_shares(pks, msgs, items):
-    """pks: list of 48-byte keys; msgs: list of bytes; items: list of (msg_index, pk_index, sig96)."""
+def ts_verify_shares(pks, msgs, items, batched=False):
+    """pks: list of 48-byte keys; msgs: list of bytes; items: list of (msg_index, pk_index, sig96).  batched=True runs
+    the randomized group check (lcb_ts_verify_shares_batched)."""
     keep = []
     n = len(items)
     _, ppk = _bytes_ptr_keep(keep, b"".join(pks))
@@ -315,7 +323,8 @@ def ts_verify_shares(pks, msgs, items):
     _, pmi = _u32_keep(keep, [it[0] for it in items])
     _, ppi = _u32_keep(keep, [it[1] for it in items])
     ob, po = _out(n)
-    _check(lib().lcb_ts_verify_shares(po, n, ppk, len(pks), psig, pm, pmo, len(msgs), pmi, ppi), "ts_verify_shares")
+    fn = lib().lcb_ts_verify_shares_batched if batched else lib().lcb_ts_verify_shares
+    _check(fn(po, n, ppk, len(pks), psig, pm, pmo, len(msgs), pmi, ppi), "ts_verify_shares")
     return [bool(ob[i]) for i in range(n)]
 
 
