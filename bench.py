@@ -406,7 +406,7 @@ def ts_inputs(nat, rank, rounds, n, f):
                 expect=expect, shared_sk=shared_sk, msg_list=msgs)
 
 
-def ts_cpu_baseline(inp, n_total, n_per_round, target_s=10.0):
+def ts_cpu_baseline(inp, n_total, n_per_round, target_s=10.0, batched=False):
     """configs[2] share verification on host cores: amortized (H(m) lines once per message, one final exp per
     share: orc_ts_validate_batch_amortized) and as-reference (hash + two pairings per ValidateSignature call,
     ThresholdSignature/PublicKey.cs:16-21: orc_ts_validate_batch)."""
@@ -422,7 +422,12 @@ def ts_cpu_baseline(inp, n_total, n_per_round, target_s=10.0):
         pi = np.ascontiguousarray(inp["pidx"][:k])
         n_msgs = int(mi[-1]) + 1
         t0 = time.perf_counter()
-        if am:
+        if am == "rlc":
+            rc = lib.orc_ts_validate_batch_rlc(acc, ctypes.c_size_t(k), inp["pks"], ctypes.c_size_t(n_pks),
+                                               inp["sigs"][:96 * k], inp["msgs"], p(inp["moff"]),
+                                               ctypes.c_size_t(n_msgs), p(mi), p(pi),
+                                               ctypes.c_uint64(int.from_bytes(os.urandom(8), "little")), threads)
+        elif am:
             rc = lib.orc_ts_validate_batch_amortized(acc, ctypes.c_size_t(k), inp["pks"], ctypes.c_size_t(n_pks),
                                                      inp["sigs"][:96 * k], inp["msgs"], p(inp["moff"]),
                                                      ctypes.c_size_t(n_msgs), p(mi), p(pi), threads)
@@ -434,15 +439,21 @@ def ts_cpu_baseline(inp, n_total, n_per_round, target_s=10.0):
         return k, dt, int(np.sum(np.frombuffer(acc.raw, dtype=np.uint8) != inp["expect"][:k]))
 
     legs = {}
-    for name, am in (("amortized", True), ("as_reference", False)):
+    fn = {"rlc": "orc_ts_validate_batch_rlc", True: "orc_ts_validate_batch_amortized", False: "orc_ts_validate_batch"}
+    kinds = (("batched", "rlc"),) if batched else ()
+    for name, am in kinds + (("amortized", True), ("as_reference", False)):
         k, dt, _ = run(n_per_round * 2, am)
         k, dt, mism = run(int(min(n_total, max(k, k * target_s / max(dt, 1e-3)))), am)
         legs[name] = dict(value=k / dt, unit="share verifications/s", cores=threads, kind="port",
-                          sample=f"first {k} shares ({k // n_per_round} rounds) of the same rounds, "
-                                 f"{'orc_ts_validate_batch_amortized' if am else 'orc_ts_validate_batch'}, {build}, "
+                          sample=f"first {k} shares ({k // n_per_round} rounds) of the same rounds, {fn[am]}, {build}, "
                                  f"{threads} OpenMP threads, {dt:.1f} s, {mism} decision mismatches vs expected")
-    out = dict(legs["amortized"])
-    out["algorithm"] = "amortized (the GPU's algorithm)"
+    if batched:
+        out = dict(legs["batched"])
+        out["algorithm"] = "randomized batch check (the GPU's algorithm, k_batch.hip restated)"
+        out["amortized_exact"] = dict(legs["amortized"], algorithm="exact per-share check, per-message lines")
+    else:
+        out = dict(legs["amortized"])
+        out["algorithm"] = "amortized (the GPU's algorithm)"
     out["as_reference"] = legs["as_reference"]
     return out
 
@@ -570,7 +581,7 @@ def run_ts(args, nat, torch, dev, rank, world):
     if bat and exact:
         res["exact"] = exact
     if world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = ts_cpu_baseline(inp, rounds * n, n)
+        res["cpu_baseline"] = ts_cpu_baseline(inp, rounds * n, n, batched=bat is not None)
     return res
 
 
@@ -744,18 +755,32 @@ def run_replay(args, nat, torch, dev, rank, world):
     d_ridx = to_dev(torch, dev, np.arange(nm, dtype=np.uint32))
     d_shared = to_dev(torch, dev, np.full(nm, n, dtype=np.uint32))
 
+    batched = not args.replay_exact
+
     def step():
-        rc = lib.lcb_tpke_prepare_dev(d_y.data_ptr(), n, d_u.data_ptr(), d_w.data_ptr(), d_v.data_ptr(),
-                                      d_voff.data_ptr(), V * n, sh)
+        if batched:      # prepare + randomized group checks in one call each (k_batch.hip)
+            rc = lib.lcb_tpke_verify_shares_batched_dev(d_acc_t.data_ptr(), V * n * n, d_y.data_ptr(), n,
+                                                        d_u.data_ptr(), d_w.data_ptr(), d_v.data_ptr(),
+                                                        d_voff.data_ptr(), V * n, d_ct.data_ptr(), d_dec.data_ptr(),
+                                                        d_sh.data_ptr(), sh)
+        else:
+            rc = lib.lcb_tpke_prepare_dev(d_y.data_ptr(), n, d_u.data_ptr(), d_w.data_ptr(), d_v.data_ptr(),
+                                          d_voff.data_ptr(), V * n, sh)
         rc |= lib.lcb_tpke_partial_decrypt_prepared_dev(d_own.data_ptr(), d_own_st.data_ptr(), d_x.data_ptr(), 1,
                                                         d_u.data_ptr(), V * n, sh)
-        rc |= lib.lcb_tpke_verify_prepared_dev(d_acc_t.data_ptr(), V * n * n, n, V * n, d_ct.data_ptr(),
-                                               d_dec.data_ptr(), d_sh.data_ptr(), sh)
+        if not batched:
+            rc |= lib.lcb_tpke_verify_prepared_dev(d_acc_t.data_ptr(), V * n * n, n, V * n, d_ct.data_ptr(),
+                                                   d_dec.data_ptr(), d_sh.data_ptr(), sh)
         rc |= lib.lcb_tpke_combine_dev(d_uc.data_ptr(), d_ucst.data_ptr(), d_acc_t.data_ptr(), d_sh.data_ptr(), n,
                                        f + 1, V * n, sh)
-        rc |= lib.lcb_ts_prepare_dev(d_pks.data_ptr(), n + 1, d_msg.data_ptr(), d_moff.data_ptr(), nm, sh)
-        rc |= lib.lcb_ts_verify_prepared_dev(d_acc_s.data_ptr(), nm * n, n + 1, nm, d_sigs.data_ptr(),
-                                             d_midx.data_ptr(), d_pidx.data_ptr(), sh)
+        if batched:
+            rc |= lib.lcb_ts_verify_shares_batched_dev(d_acc_s.data_ptr(), nm * n, d_pks.data_ptr(), n + 1,
+                                                       d_sigs.data_ptr(), d_msg.data_ptr(), d_moff.data_ptr(), nm,
+                                                       d_midx.data_ptr(), d_pidx.data_ptr(), sh)
+        else:
+            rc |= lib.lcb_ts_prepare_dev(d_pks.data_ptr(), n + 1, d_msg.data_ptr(), d_moff.data_ptr(), nm, sh)
+            rc |= lib.lcb_ts_verify_prepared_dev(d_acc_s.data_ptr(), nm * n, n + 1, nm, d_sigs.data_ptr(),
+                                                 d_midx.data_ptr(), d_pidx.data_ptr(), sh)
         rc |= lib.lcb_ts_assemble_dev(d_comb.data_ptr(), d_cst.data_ptr(), d_acc_s.data_ptr(), d_sigs.data_ptr(), n,
                                       f + 1, nm, sh)
         rc |= lib.lcb_ts_verify_prepared_dev(d_cacc.data_ptr(), nm, n + 1, nm, d_comb.data_ptr(), d_ridx.data_ptr(),
@@ -806,6 +831,8 @@ def run_replay(args, nat, torch, dev, rank, world):
                 value=n / elapsed, unit="views/s", scaling="strong", views_total=n, n=n, f=f, coins=n_coins,
                 pairing_checks_per_s=n * checks_per_view / elapsed, ms_per_era=1e3 * elapsed,
                 steps=args.replay_steps, mismatches=int(t[1]), input_gen_s=t_gen,
+                share_checks=("randomized batch checks (lcb_tpke_verify_shares_batched_dev, "
+                              "lcb_ts_verify_shares_batched_dev)" if batched else "exact per-share checks"),
                 config=f"configs[4]: all {n} nodes' views of one era (N={n}, F={f}), views block-partitioned over "
                        f"ranks; per view {checks_per_view} pairing checks, {n} G1 and {n_coins} G2 Lagrange (k={f + 1})")
 
@@ -1121,6 +1148,7 @@ def main():
     ap.add_argument("--ts-exact", type=int, default=1, help="time the exact per-share check (0 = skip)")
     ap.add_argument("--replay-n", type=int, default=256, help="epoch-replay network size N (0 = skip)")
     ap.add_argument("--replay-steps", type=int, default=1)
+    ap.add_argument("--replay-exact", type=int, default=0, help="epoch replay with the exact per-share checks")
     ap.add_argument("--ecdsa-sigs", type=int, default=1 << 20, help="header signatures per rank (0 = skip)")
     ap.add_argument("--ecdsa-validators", type=int, default=256)
     ap.add_argument("--ecdsa-steps", type=int, default=3)

@@ -1968,8 +1968,8 @@ int orc_ts_validate_batch_amortized(uint8_t *accept, size_t n, const uint8_t *pk
    The GPU's batched algorithm restated for the host cores: groups = runs of one ciphertext (<= 32 shares), exponents
    s_i = a_i + b_i lambda from 32-bit a_i, b_i (splitmix64 from `seed`: the cost of the GPU's ChaCha20 is negligible
    beside the curve arithmetic; this leg is timing and parity, not a randomness source), one two-pair Miller loop +
-   final exponentiation per group, failed groups split ceil(sqrt(len)) ways (<= 8 shares: single shares), a single
-   share decided by its own check.  Decisions equal orc_tpke_verify_batch's (tests/test_oracle.py). */
+   final exponentiation per group, for a failed group the weighted re-check and the level-2 search, single checks when
+   the search names no share.  Decisions equal orc_tpke_verify_batch's (tests/test_oracle.py). */
 static fp G1_BETA_O;
 static int g1_beta_ready = 0;
 static void g1_beta_init(void) {
@@ -2053,21 +2053,42 @@ static u64 splitmix64(u64 *st) {
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
     return z ^ (z >> 31);
 }
+/* e = final_exp(Miller(P1 on L1) Miller(P2 on L2)) */
+static void pair_product_gt(fp12 *e, const oline *L1, const g1 *P1, const oline *L2, const g1 *P2) {
+    fp12 f;
+    miller2_lines(&f, L1, P1, L2, P2);
+    final_exp(e, &f);
+}
+/* Level 2 search (k_rlc_search): gamma' == gamma^c for c = 1..len names the group's only bad share (index c - 1) */
+static int rlc_search(const fp12 *gm, const fp12 *gp, size_t len) {
+    fp12 acc = *gm;
+    for (size_t c = 1; c <= len; c++) {
+        if (fp12_eq(&acc, gp)) return (int)c;
+        fp12_mul(&acc, &acc, gm);
+    }
+    return 0;
+}
+/* the GPU's level structure on one group (k_batch.hip): the group check; if it fails, the weighted re-check with
+   weights j+1 and the search; if that names no share, single checks of every share */
 static void rlc_check_group(uint8_t *accept, const g1 *sU, const g1 *sY, size_t st, size_t len, const oline *LH,
                             const oline *LW) {
-    g1 a, b;
-    g1_set_inf(&a);
-    g1_set_inf(&b);
-    for (size_t j = st; j < st + len; j++) {
+    g1 a, b, wa, wb;
+    g1_set_inf(&a); g1_set_inf(&b); g1_set_inf(&wa); g1_set_inf(&wb);
+    for (size_t j = st + len; j-- > st;) {       /* suffix sums: wa = sum (j - st + 1) sU_j */
         g1_add(&a, &a, &sU[j]);
         g1_add(&b, &b, &sY[j]);
+        g1_add(&wa, &wa, &a);
+        g1_add(&wb, &wb, &b);
     }
-    if (check_pair_product(LH, &a, LW, &b)) return;      /* every (valid) share of the group accepted */
+    fp12 gm, gp;
+    pair_product_gt(&gm, LH, &a, LW, &b);
+    if (fp12_eq(&gm, &FP12_ONE)) return;                 /* every (valid) share of the group accepted */
     if (len == 1) { accept[st] = 0; return; }
-    size_t parts = 1;
-    while (parts * parts < len) parts++;
-    size_t sz = len <= 8 ? 1 : (len + parts - 1) / parts;
-    for (size_t k = st; k < st + len; k += sz) rlc_check_group(accept, sU, sY, k, (st + len - k) < sz ? st + len - k : sz, LH, LW);
+    pair_product_gt(&gp, LH, &wa, LW, &wb);
+    int c = rlc_search(&gm, &gp, len);
+    if (c) { accept[st + c - 1] = 0; return; }
+    for (size_t j = st; j < st + len; j++)
+        if (!check_pair_product(LH, &sU[j], LW, &sY[j])) accept[j] = 0;
 }
 int orc_tpke_verify_batch_rlc(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys, const uint8_t *cts_u,
                               const uint8_t *cts_v, size_t vlen, const uint8_t *cts_w, size_t n_cts,
@@ -2132,6 +2153,138 @@ int orc_tpke_verify_batch_rlc(uint8_t *accept, size_t n, const uint8_t *y_keys, 
         rlc_check_group(accept, sU, sY, gst[g], gst[g + 1] - gst[g], LH + OLINES * c, LW + OLINES * c);
     }
     free(LH); free(LW); free(ctok); free(Y); free(kok); free(sU); free(sY); free(gst);
+    return 0;
+}
+
+/* G2 membership as the GPU tests it (Scott: psi(P) == [z] P = -[|z|] P on G2), for the batched CPU legs */
+static int g2_in_subgroup_psi(const g2 *P_) {
+    if (g2_is_inf(P_)) return 1;
+    g2 t, ps;
+    g2_mul_u64(&t, P_, Z_ABS);
+    g2_neg(&t, &t);
+    g2_psi(&ps, P_);
+    return g2_eq(&ps, &t);
+}
+int orc_g2_in_subgroup_psi(const uint8_t a[96]) {
+    orc_init();
+    g2 p;
+    if (!g2_load(&p, a)) return 0;
+    return g2_in_subgroup_psi(&p);
+}
+/* (a + b lambda) S = (a - b) S + b psi^2(S) on G2 */
+static void g2_mul_ab(g2 *r, const g2 *S, uint32_t a, uint32_t b) {
+    g2_set_inf(r);
+    if (g2_is_inf(S)) return;
+    g2 s2, p1;
+    g2_psi(&s2, S);
+    g2_psi(&s2, &s2);
+    p1 = *S;
+    uint32_t d = a - b;
+    if (a < b) { d = b - a; g2_neg(&p1, &p1); }
+    for (int k = 31; k >= 0; k--) {
+        g2_dbl(r, r);
+        if ((d >> k) & 1) g2_add(r, r, &p1);
+        if ((b >> k) & 1) g2_add(r, r, &s2);
+    }
+}
+static void ts_rlc_check_group(uint8_t *accept, const g1 *sP, const g2 *sS, const uint8_t *exact, size_t st,
+                               size_t len, const oline *LH, const g1 *ngen, const g1 *pkv, const g2 *sigv) {
+    g1 a, wa;
+    g2 b, wb;
+    g1_set_inf(&a); g1_set_inf(&wa); g2_set_inf(&b); g2_set_inf(&wb);
+    for (size_t j = st + len; j-- > st;) {
+        if (!exact[j]) {
+            g1_add(&a, &a, &sP[j]);
+            g2_add(&b, &b, &sS[j]);
+        }
+        g1_add(&wa, &wa, &a);
+        g2_add(&wb, &wb, &b);
+    }
+    oline LS[OLINES];
+    fp12 gm, gp;
+    lines_precompute(LS, &b);
+    pair_product_gt(&gm, LH, &a, LS, ngen);
+    if (fp12_eq(&gm, &FP12_ONE)) return;
+    int c = 0;
+    if (len > 1) {
+        lines_precompute(LS, &wb);
+        pair_product_gt(&gp, LH, &wa, LS, ngen);
+        c = rlc_search(&gm, &gp, len);
+    }
+    if (c) { accept[st + c - 1] = 0; return; }
+    for (size_t j = st; j < st + len; j++) {
+        if (!accept[j] || exact[j]) continue;
+        lines_precompute(LS, &sigv[j]);
+        if (!check_pair_product(LH, &pkv[j], LS, ngen)) accept[j] = 0;
+    }
+}
+/* CPU baseline with the GPU's batched threshold-signature algorithm (k_batch.hip): groups = runs of one message
+   (<= 128 shares), s_i = a_i + b_i lambda (splitmix64, see orc_tpke_verify_batch_rlc), signatures outside G2 checked
+   exactly, the level-2 search, single checks when it names no share */
+int orc_ts_validate_batch_rlc(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks, const uint8_t *sigs,
+                              const uint8_t *msgs, const uint32_t *msg_off, size_t n_msgs, const uint32_t *msg_idx,
+                              const uint32_t *pk_idx, uint64_t seed, int nthreads) {
+    orc_init();
+    g1_beta_init();
+    oline *LH = malloc(sizeof(oline) * OLINES * (n_msgs ? n_msgs : 1));
+    uint8_t *mok = malloc(n_msgs ? n_msgs : 1), *exact = malloc(n ? n : 1);
+    g1 *sP = malloc(sizeof(g1) * (n ? n : 1)), *pkv = malloc(sizeof(g1) * (n ? n : 1));
+    g2 *sS = malloc(sizeof(g2) * (n ? n : 1)), *sigv = malloc(sizeof(g2) * (n ? n : 1));
+    size_t *gst = malloc(sizeof(size_t) * (n + 1));
+    if (!LH || !mok || !exact || !sP || !pkv || !sS || !sigv || !gst) {
+        free(LH); free(mok); free(exact); free(sP); free(pkv); free(sS); free(sigv); free(gst);
+        return -1;
+    }
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+    for (size_t m = 0; m < n_msgs; m++) {
+        g2 h;
+        int ok = g2_hash(&h, msgs + msg_off[m], msg_off[m + 1] - msg_off[m]);
+        mok[m] = (uint8_t)ok;
+        if (!ok) memset(&h, 0, sizeof h);
+        lines_precompute(LH + OLINES * m, &h);
+        lines_normalise(LH + OLINES * m);
+    }
+    g1 ngen;
+    g1_neg(&ngen, &G1_GEN);
+#pragma omp parallel for schedule(dynamic, 64) num_threads(nthreads)
+    for (size_t i = 0; i < n; i++) {
+        uint32_t m = msg_idx[i], k = pk_idx[i];
+        int ok = m < n_msgs && k < n_pks && mok[m] && g1_load(&pkv[i], pks + 48 * (size_t)k) &&
+                 g2_load(&sigv[i], sigs + 96 * i);
+        accept[i] = (uint8_t)ok;
+        exact[i] = 0;
+        g1_set_inf(&sP[i]);
+        g2_set_inf(&sS[i]);
+        if (!ok) continue;
+        if (!g2_in_subgroup_psi(&sigv[i])) {      /* exact check, as the GPU's desc.w = 1 singles */
+            oline LS[OLINES];
+            exact[i] = 1;
+            lines_precompute(LS, &sigv[i]);
+            accept[i] = (uint8_t)check_pair_product(LH + OLINES * m, &pkv[i], LS, &ngen);
+            continue;
+        }
+        u64 st = seed ^ (0x9E3779B97F4A7C15ULL * (i + 1));
+        u64 r = splitmix64(&st);
+        uint32_t a = (uint32_t)r, b = (uint32_t)(r >> 32);
+        if ((a | b) == 0) a = 1;
+        g1_mul_ab(&sP[i], &pkv[i], a, b);
+        g2_mul_ab(&sS[i], &sigv[i], a, b);
+    }
+    size_t ng = 0;
+    for (size_t i = 0; i < n;) {
+        size_t j = i + 1;
+        while (j < n && j - i < 128 && msg_idx[j] == msg_idx[i]) j++;
+        gst[ng++] = i;
+        i = j;
+    }
+    gst[ng] = n;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+    for (size_t g = 0; g < ng; g++) {
+        size_t m = msg_idx[gst[g]];
+        if (m >= n_msgs || !mok[m]) continue;          /* its shares are already rejected */
+        ts_rlc_check_group(accept, sP, sS, exact, gst[g], gst[g + 1] - gst[g], LH + OLINES * m, &ngen, pkv, sigv);
+    }
+    free(LH); free(mok); free(exact); free(sP); free(pkv); free(sS); free(sigv); free(gst);
     return 0;
 }
 

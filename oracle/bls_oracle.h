@@ -138,6 +138,10 @@ int orc_tpke_verify_batch_rlc(uint8_t *accept, size_t n, const uint8_t *y_keys, 
                               const uint8_t *cts_v, size_t vlen, const uint8_t *cts_w, size_t n_cts,
                               const uint32_t *ct_idx, const uint32_t *dec_idx, const uint8_t *uis, uint64_t seed,
                               int nthreads);
+int orc_ts_validate_batch_rlc(uint8_t *accept, size_t n, const uint8_t *pks, size_t n_pks, const uint8_t *sigs,
+                              const uint8_t *msgs, const uint32_t *msg_off, size_t n_msgs, const uint32_t *msg_idx,
+                              const uint32_t *pk_idx, uint64_t seed, int nthreads);
+int orc_g2_in_subgroup_psi(const uint8_t a[96]);
 int orc_tpke_verify_batch(uint8_t *accept, size_t n_shares, const uint8_t *y_keys,
                           const uint8_t *cts_u, const uint8_t *cts_v, size_t vlen, const uint8_t *cts_w,
                           const uint32_t *ct_idx, const uint32_t *dec_idx, const uint8_t *uis,

@@ -270,3 +270,47 @@ def test_rlc_cpu_baseline_matches_transcripts():
                     b"".join(H(c["w"]) for c in cs), ctypes.c_size_t(len(cs)), p(ct), p(dec), b"".join(sh),
                     ctypes.c_uint64(seed), 2) == 0
                 assert acc.raw == expect, (key, rep, seed)
+
+
+def test_rlc_cpu_ts_baseline_and_psi_membership():
+    """the batched threshold-signature CPU leg (orc_ts_validate_batch_rlc) reproduces the N=7 / N=100 transcripts
+    (wrong-signer, reversed, off-subgroup, infinity shares), and the psi membership test it shares with the GPU
+    (psi(P) == [z] P) agrees with the definition ([r] P == O) on in- and off-subgroup points"""
+    import ctypes
+    import json
+    import os
+    import numpy as np
+    from helpers import GOLDEN, Drbg
+    lib = o.lib()
+    d = Drbg(b"oracle-psi-membership")
+    for k in range(6):
+        if k % 2:
+            p = o.g2_mul(o.g2_gen(), o.fr(d.fr_int()))
+        else:
+            while True:
+                xa = int.from_bytes(d.bytes(48), "little") % o.P
+                xb = int.from_bytes(d.bytes(48), "little") % o.P
+                enc = bytearray(xa.to_bytes(48, "little") + xb.to_bytes(48, "little"))
+                enc[95] |= 0x80 * (d.bytes(1)[0] & 1)
+                p = bytes(enc)
+                if o.g2_valid(p):
+                    break
+        assert lib.orc_g2_in_subgroup_psi(p) == o.g2_in_subgroup(p) == (k % 2 == 1)
+    T = json.load(open(os.path.join(GOLDEN, "transcripts.json")))
+    pp = lambda arr: arr.ctypes.data_as(ctypes.c_void_p)
+    H = bytes.fromhex
+    for key in ("ts_n7", "ts_n100"):
+        t = T[key]
+        rs = t["rounds"]
+        n = len(t["pk_i"])
+        msgs = [H(r["msg"]) for r in rs]
+        mo = np.cumsum([0] + [len(m) for m in msgs]).astype(np.uint32)
+        sigs = b"".join(H(s) for r in rs for s in r["sigs"])
+        m = len(rs) * n
+        mi = np.repeat(np.arange(len(rs), dtype=np.uint32), n)
+        pi = np.tile(np.arange(n, dtype=np.uint32), len(rs))
+        acc = ctypes.create_string_buffer(m)
+        assert lib.orc_ts_validate_batch_rlc(acc, ctypes.c_size_t(m), b"".join(H(x) for x in t["pk_i"]),
+                                             ctypes.c_size_t(n), sigs, b"".join(msgs), pp(mo),
+                                             ctypes.c_size_t(len(rs)), pp(mi), pp(pi), ctypes.c_uint64(7), 2) == 0
+        assert acc.raw == bytes(a for r in rs for a in r["accept"]), key
