@@ -1044,27 +1044,55 @@ def run_rs(args, nat, rank):
                                          f"polynomial division per byte column), one thread; equal to the GPU shards"))
 
 C["C_MUL1_64"] = round(C["C_MUL1"] * 64 / 255)          # 64-bit var-base G1 multiplication (double-and-add)
-C["C_MUL_AB32"] = round(C["C_MUL1"] * 32 / 255) + 1     # a P + b phi(P), 32-bit a, b: 32 doublings, ~32 mixed adds
-W_RLC_POINTS = C["C_DEC1"] + 2 * C["C_MUL_AB32"]          # per share: decompress U_i, s_i U_i, s_i Y_i
+C["C_MADD1"] = 11                                          # G1 mixed addition (7M + 4S)
+C["C_JADD1"] = 16                                          # G1 Jacobian addition (11M + 5S)
+C["C_DBL1"] = (C["C_MUL1"] - 127.5 * C["C_MADD1"]) / 255   # G1 doubling, from the 255-bit ladder's count
+C["C_MUL_AB32"] = round(32 * C["C_DBL1"] + 32 * C["C_MADD1"]) + 1   # a P + b phi(P): 32 dbl, ~2 x 16 madds, beta x
+C["C_KTAB"] = 7 * C["C_JADD1"] + 1                         # a Y + b phi(Y) from the key's byte tables
+W_RLC_POINTS = C["C_DEC1"] + C["C_MUL_AB32"] + C["C_KTAB"]  # per share: decompress U_i, s_i U_i, s_i Y_i
 
 
 def run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, dd, n, n_cts, n_dec, sh):
-    """Randomized batch verify (lcb_tpke_verify_prepared_batched_dev, k_batch.hip) on the same prepared batch:
-    same timing discipline as the exact path (prepare + verify per step, warmup, barrier + synchronize)."""
+    """Randomized batch verify (lcb_ctx_tpke_verify_shares_batched_dev, k_batch.hip) of the same 1M-share batch: same
+    timing discipline as the exact path (prepare + verify per step, warmup, barrier + synchronize).  With
+    --tpke-streams K the batch is split by ciphertext into K contiguous parts verified concurrently, each by its own
+    host thread, library context and HIP stream (the library is re-entrant per context): a part's splitting levels
+    are latency-bound launches of < 1 wave per SIMD, and the other parts' randomisation fills the idle SIMDs."""
+    import concurrent.futures
     import torch.distributed as dist
     lib = nat.lib()
     d_ct, d_dec, d_ui = dd
-    stream = torch.cuda.current_stream(dev)
-
     py, nk, pu, pw, pv, pvo, nc = PREP_ARGS[0]
+    K = max(1, args.tpke_streams)
+    vlen = int(inp["v_off"][1] - inp["v_off"][0])
+    bounds = [round(n_cts * k / K) for k in range(K + 1)]
+    parts = []
+    for k in range(K):
+        c0, c1 = bounds[k], bounds[k + 1]
+        s0, s1 = c0 * n_dec, min(n, c1 * n_dec)
+        if s1 <= s0:
+            continue
+        ct_local = to_dev(torch, dev, np.ascontiguousarray(inp["ct_idx"][s0:s1] - c0, dtype=np.uint32))
+        voff = to_dev(torch, dev, np.arange(0, vlen * (c1 - c0 + 1), vlen, dtype=np.uint32))
+        ctx = nat.Context()
+        st = torch.cuda.Stream(dev)
+        parts.append(dict(c0=c0, nc=c1 - c0, s0=s0, ns=s1 - s0, ct=ct_local, voff=voff, ctx=ctx, stream=st))
+    pool = concurrent.futures.ThreadPoolExecutor(max_workers=len(parts))
 
-    def step():     # one call: key decompression, randomisation beside the ciphertext preparation, group checks
-        rc = lib.lcb_tpke_verify_shares_batched_dev(d_acc.data_ptr(), n, py, nk, pu, pw, pv, pvo, nc, d_ct.data_ptr(),
-                                                    d_dec.data_ptr(), d_ui.data_ptr(), sh)
+    def one(p):
+        rc = lib.lcb_ctx_tpke_verify_shares_batched_dev(
+            p["ctx"].ptr, d_acc.data_ptr() + p["s0"], p["ns"], py, nk, pu + 48 * p["c0"], pw + 96 * p["c0"],
+            pv + vlen * p["c0"], p["voff"].data_ptr(), p["nc"], p["ct"].data_ptr(), d_dec.data_ptr() + 4 * p["s0"],
+            d_ui.data_ptr() + 48 * p["s0"], p["stream"].cuda_stream)
         if rc != 0:
             raise RuntimeError(nat.last_error())
 
+    def step():
+        for f in [pool.submit(one, p) for p in parts]:
+            f.result()
+
     d_acc.fill_(7)
+    torch.cuda.synchronize(dev)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -1081,7 +1109,20 @@ def run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, dd, n, n_cts, n_d
         dist.barrier()
     elapsed = time.perf_counter() - t0
     mism += int(np.sum(d_acc.cpu().numpy() != inp["expect"]))
-    levels, ms = nat.tpke_batched_stats()
+    pool.shutdown()
+    levels, ms = [], [0.0] * 6
+    for p in parts:
+        lv = (ctypes.c_uint32 * 8)()
+        m6 = (ctypes.c_float * 6)()
+        k = lib.lcb_ctx_tpke_batched_stats(p["ctx"].ptr, lv, m6)
+        if k < 0:
+            raise RuntimeError(nat.last_error())
+        levels.append(list(lv[:k]))
+        ms = [max(a, b) for a, b in zip(ms, m6)] if K > 1 else list(m6)
+    for p in parts:
+        p["ctx"].close()
+    if K == 1:
+        levels = levels[0]
     ms_points, ms_groups, ms_sum, ms_miller, ms_fe, ms_resolve = ms
     t = torch.tensor([elapsed, float(mism), float(n)], dtype=torch.float64, device=dev)
     if world > 1:
@@ -1089,10 +1130,11 @@ def run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, dd, n, n_cts, n_d
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         elapsed = float(tmax[0])
-    checks = sum(levels)
+    checks = sum(sum(lv) for lv in levels) if K > 1 else sum(levels)
     ach_pair = checks * (C["C_ML2_NORM2"] + C["C_FE"]) * MAC_PER_FPMUL / ((ms_miller + ms_fe) * 1e-3)
     ach_pts = n * W_RLC_POINTS * MAC_PER_FPMUL / (ms_points * 1e-3)
     step_fpmul = n * W_RLC_POINTS + checks * (C["C_ML2_NORM2"] + C["C_FE"]) + n_cts * W_PREPARE
+    step_ach = step_fpmul * MAC_PER_FPMUL / (elapsed / args.steps)
     return dict(
         metric="BLS12-381 TPKE decryption-share verifications/sec, randomized batch check (small-exponent test)",
         value=float(t[2]) * args.steps / elapsed, unit="share verifications/s", steps=args.steps,
@@ -1101,21 +1143,27 @@ def run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, dd, n, n_cts, n_d
                    "(32-bit a_i, b_i from ChaCha20 keyed by getrandom per call: 2^64 exponents); failed groups split "
                    "~sqrt(len) ways, groups <= 8 into single shares; every rejection exact, false accept <= 2^-64 "
                    "per group"),
-        api="lcb_tpke_verify_shares_batched_dev (prepare + verify, randomisation on a second stream)",
+        api="lcb_ctx_tpke_verify_shares_batched_dev (prepare + verify, randomisation on a second stream)",
+        concurrent_parts=K,
         levels=levels, group_checks_per_share=checks / n,
         device_ms={"randomise_and_group (beside prepare)": ms_points, "all_levels": ms_groups, "group_sums": ms_sum,
                    "k_tpke_rlc_miller": ms_miller, "k_final_exp_check": ms_fe, "resolve_and_count_reads": ms_resolve},
-        roofline={"bound": "valu_int32", "kernel": "k_tpke_rlc_miller + k_final_exp_check (group checks, all levels)",
-                  "achieved": ach_pair / 1e12, "peak": PEAK_MAC32 / 1e12, "unit": "Tmac32/s",
-                  "frac": ach_pair / PEAK_MAC32, "traffic": None,
-                  "work_per_group_check_fpmul": C["C_ML2_NORM2"] + C["C_FE"], "group_checks": checks,
-                  "mac_per_fpmul": MAC_PER_FPMUL, "kernel_ms": {"pair (summed over levels)": ms_miller + ms_fe},
-                  "note": ("each level is one launch of <= 1 wave per SIMD (latency-bound: one lane's serial "
-                           "pairing check), so the pair runs below its full-occupancy rate (tpke_exact.roofline)"),
-                  "kernel_frac": {"k_tpke_rlc_points (+ k_rlc_groups), beside k_tpke_ct_prepare":
-                                  ach_pts / PEAK_MAC32},
-                  "work_per_share_fpmul_randomise": W_RLC_POINTS,
-                  "step_frac": step_fpmul * MAC_PER_FPMUL / (1e-3 * 1e3 * elapsed / args.steps) / PEAK_MAC32},
+        roofline={"bound": "valu_int32",
+                  "kernel": ("whole batched step: k_tpke_rlc_points + k_tpke_ct_prepare / k_lineset_fill + "
+                             "k_tpke_rlc_miller / k_final_exp_check over all levels"),
+                  "achieved": step_ach / 1e12, "peak": PEAK_MAC32 / 1e12, "unit": "Tmac32/s",
+                  "frac": step_ach / PEAK_MAC32, "traffic": None, "mac_per_fpmul": MAC_PER_FPMUL,
+                  "work_per_step_fpmul": step_fpmul,
+                  "work_breakdown_fpmul": {"randomise (per share)": W_RLC_POINTS, "prepare (per ciphertext)": W_PREPARE,
+                                           "group check (per group)": C["C_ML2_NORM2"] + C["C_FE"],
+                                           "group_checks": checks},
+                  "note": ("algorithmic Fp-mul of the step / step time; the splitting levels are launches of < 1 wave "
+                           "per SIMD (latency-bound), which the concurrent parts overlap with the other parts' "
+                           "randomisation; the full-occupancy rate of the same Miller / final-exponentiation code is "
+                           "tpke_exact.roofline"),
+                  "kernel_frac": ({"k_tpke_rlc_miller + k_final_exp_check (all levels, one part)": ach_pair / PEAK_MAC32,
+                                   "k_tpke_rlc_points (+ k_rlc_groups), beside k_tpke_ct_prepare": ach_pts / PEAK_MAC32}
+                                  if K == 1 else None)},
     )
 
 
@@ -1134,6 +1182,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--tpke-batched", type=int, default=1, help="time the randomized batch verify (0 = skip)")
     ap.add_argument("--tpke-exact", type=int, default=1, help="time the exact per-share verify (0 = skip)")
+    ap.add_argument("--tpke-streams", type=int, default=1,
+                    help="batched verify: concurrent parts (contexts / streams / host threads) per step; measured "
+                         "slower with 2 / 4 parts (177 / 261 vs 156 ms per 1M shares: the parts' kernels serialize)")
     ap.add_argument("--headline", choices=("batched", "exact"), default="batched",
                     help="which TPKE path the line's value / roofline / cpu_baseline describe")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -1293,6 +1344,20 @@ def main():
         if exact is not None:
             exact["roofline"]["traffic"] = traffic
             exact["roofline"]["traffic_source"] = traffic_note
+        if batched is not None:          # the whole batched step's HBM bytes (tools/pmc_batched_to_json.py)
+            pmcb = os.path.join(ROOT, "profiles", "pmc_tpke_batched.json")
+            bt, bnote = None, "no batched PMC file for this build"
+            if os.path.exists(pmcb):
+                with open(pmcb) as fh:
+                    pb = json.load(fh)
+                if pb.get("source_hash") == src_hash:
+                    bt = pb.get("hbm_bytes_per_step")
+                    bnote = (f"{pmcb[len(ROOT) + 1:]}: FETCH_SIZE x2 + WRITE_SIZE (KB->B) summed over the step's "
+                             f"dispatches, source hash {src_hash}")
+                else:
+                    bnote = f"stale PMC file (profiled {pb.get('source_hash')}, this build {src_hash}): not reported"
+            batched["roofline"]["traffic"] = bt
+            batched["roofline"]["traffic_source"] = bnote
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(inp, args.cpu_seconds, batched=batched is not None)

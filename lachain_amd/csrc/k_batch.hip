@@ -178,12 +178,54 @@ DI void g2_to_st(g2a_st &o, const g2 &p) {
 DI void g1_inf_st(g1a_st &o) { o.ok = 1; o.pad[0] = o.pad[1] = 0; o.inf = 1; o.x = fp_zero(); o.y = fp_zero(); }
 DI void g2_inf_st(g2a_st &o) { o.ok = 1; o.pad[0] = o.pad[1] = 0; o.inf = 1; o.x = fp2_zero(); o.y = fp2_zero(); }
 
+// ---------------------------------------------------------------- fixed-base tables of the validators' keys
+// The keys (TPKE verification keys Y_d, threshold-signature public keys PK_k) are the same for every ciphertext /
+// coin of a batch: per key, table[w][d - 1] = d 2^(8w) K (Jacobian, d = 1..255, w = 0..3) turns a K + b phi(K) for
+// 32-bit a, b into at most 7 Jacobian additions (4 byte digits of a, 4 of b, phi applied once to the b sum) instead of
+// 32 doublings + ~32 mixed additions.  One lane per (key, window): 8w doublings, then 254 additions.
+#define LCB_KTAB_ENTRIES (4 * 255)
+extern "C" __global__ void LCB_BOUNDS k_rlc_key_tables(const g1a_st *keys, u32 n_keys, u32 *tab) {
+    u32 t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 4 * n_keys) return;
+    u32 k = t >> 2, w = t & 3;
+    g1a K;
+    g1a_st ks = keys[k];
+    st_to_g1a(K, ks);
+    const size_t stride = (size_t)n_keys * LCB_KTAB_ENTRIES;      // SoA over every (key, entry)
+    size_t e0 = (size_t)k * LCB_KTAB_ENTRIES + (size_t)w * 255;
+    g1 B, acc;
+    jac_from_aff(B, K);
+    if (!ks.ok) jac_set_inf(B);
+    for (u32 j = 0; j < 8 * w; j++) grp_dbl(B, B);
+    acc = B;
+    for (u32 d = 1; d <= 255; d++) {
+        g1_store_soa(tab, stride, e0 + d - 1, acc);
+        grp_add(acc, acc, B);
+    }
+}
+// a K + b phi(K) from key k's table
+DN void g1_mul_ab_tab(g1 &r, const u32 *tab, u32 n_keys, u32 k, u32 a, u32 b) {
+    const size_t stride = (size_t)n_keys * LCB_KTAB_ENTRIES, e0 = (size_t)k * LCB_KTAB_ENTRIES;
+    g1 sa, sb, t;
+    jac_set_inf(sa);
+    jac_set_inf(sb);
+    for (u32 w = 0; w < 4; w++) {
+        u32 da = (a >> (8 * w)) & 255, db = (b >> (8 * w)) & 255;
+        if (da) { g1_load_soa(t, tab, stride, e0 + w * 255 + da - 1); grp_add(sa, sa, t); }
+        if (db) { g1_load_soa(t, tab, stride, e0 + w * 255 + db - 1); grp_add(sb, sb, t); }
+    }
+    fp beta;
+    fp_load_const(beta, LCB_G1_BETA);
+    fp_mul(sb.x, sb.x, beta);            // phi on Jacobian coordinates: (beta X, Y, Z)
+    grp_add(r, sa, sb);
+}
+
 // ---------------------------------------------------------------- TPKE: per-share randomisation
 // validity as k_tpke_miller except the ciphertext's (applied per group by k_tpke_rlc_sum, so this kernel needs only
 // the decompressed keys and may run beside the ciphertext preparation)
 extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_points(u32 n_cts, const g1a_st *keys, u32 n_keys, const u32 *ct_idx,
                                                        const u32 *dec_idx, const uint8_t *ui, u32 n, rlc_key key,
-                                                       u32 *rU, u32 *rY, uint8_t *accept) {
+                                                       u32 *rU, u32 *rY, uint8_t *accept, const u32 *ktab) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u32 c = ct_idx[i], d = dec_idx[i];
@@ -201,7 +243,8 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_points(u32 n_cts, const g1a_st 
         g1_mul_ab2(p, q, Ui, Y, a, b);
 #else
         g1_mul_ab_n(p, Ui, a, b);
-        g1_mul_ab_n(q, Y, a, b);
+        if (ktab) g1_mul_ab_tab(q, ktab, n_keys, d, a, b);
+        else g1_mul_ab_n(q, Y, a, b);
 #endif
     } else {                             // an invalid share is rejected and contributes nothing to its group
         jac_set_inf(p);
@@ -369,7 +412,8 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_rlc_miller(const u32 *lines, c
 struct ts_grp { g1a_st p; g2a_st s; };
 extern "C" __global__ void LCB_BOUNDS k_ts_rlc_points(u32 n_msgs, const g1a_st *pks, u32 n_pks, const u32 *msg_idx,
                                                      const u32 *pk_idx, const uint8_t *sigs, u32 n, rlc_key key,
-                                                     u32 *rP, u32 *rS, uint8_t *accept, uint4 *desc, u32 *count) {
+                                                     u32 *rP, u32 *rS, uint8_t *accept, uint4 *desc, u32 *count,
+                                                     const u32 *ktab) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u32 m = msg_idx[i], k = pk_idx[i];
@@ -388,7 +432,8 @@ extern "C" __global__ void LCB_BOUNDS k_ts_rlc_points(u32 n_msgs, const g1a_st *
         if (g2_in_subgroup(S)) {
             u32 a, b;
             rlc_scalar(key, i, a, b);
-            g1_mul_ab_n(p, PK, a, b);
+            if (ktab) g1_mul_ab_tab(p, ktab, n_pks, k, a, b);
+            else g1_mul_ab_n(p, PK, a, b);
             g2_mul_ab_n(q, S, a, b);
         } else {
             u32 slot = atomicAdd(count, 1u);
@@ -577,24 +622,29 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_search(const uint4 *search, u32 o, u
 }
 
 // ---------------------------------------------------------------- host launch wrappers
+extern "C" size_t lcbk_key_table_bytes(u32 n_keys) { return (size_t)n_keys * LCB_KTAB_ENTRIES * 144; }
+extern "C" void lcbk_rlc_key_tables(dim3 grid, hipStream_t s, const void *keys, u32 n_keys, u32 *tab) {
+    LCB_LAUNCH(k_rlc_key_tables, (const g1a_st *)keys, n_keys, tab);
+}
 extern "C" void lcbk_tpke_rlc_points(dim3 grid, hipStream_t s, u32 n_cts, const void *keys, u32 n_keys,
                                      const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n,
-                                     const u32 key[10], u32 *rU, u32 *rY, uint8_t *accept) {
+                                     const u32 key[10], u32 *rU, u32 *rY, uint8_t *accept, const u32 *ktab) {
     rlc_key k;
     for (int j = 0; j < 8; j++) k.k[j] = key[j];
     k.nonce[0] = key[8];
     k.nonce[1] = key[9];
-    LCB_LAUNCH(k_tpke_rlc_points, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, k, rU, rY, accept);
+    LCB_LAUNCH(k_tpke_rlc_points, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, k, rU, rY, accept, ktab);
 }
 extern "C" void lcbk_ts_rlc_points(dim3 grid, hipStream_t s, u32 n_msgs, const void *pks, u32 n_pks,
                                    const u32 *msg_idx, const u32 *pk_idx, const uint8_t *sigs, u32 n,
-                                   const u32 key[10], u32 *rP, u32 *rS, uint8_t *accept, void *desc, u32 *count) {
+                                   const u32 key[10], u32 *rP, u32 *rS, uint8_t *accept, void *desc, u32 *count,
+                                   const u32 *ktab) {
     rlc_key k;
     for (int j = 0; j < 8; j++) k.k[j] = key[j];
     k.nonce[0] = key[8];
     k.nonce[1] = key[9];
     LCB_LAUNCH(k_ts_rlc_points, n_msgs, (const g1a_st *)pks, n_pks, msg_idx, pk_idx, sigs, n, k, rP, rS, accept,
-               (uint4 *)desc, count);
+               (uint4 *)desc, count, ktab);
 }
 extern "C" void lcbk_rlc_groups(dim3 grid, hipStream_t s, const u32 *key_idx, u32 n, u32 n_keys, u32 cap, void *desc,
                                 u32 *count) {

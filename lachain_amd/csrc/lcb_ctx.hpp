@@ -52,7 +52,7 @@ struct lcb_ctx {
     hipEvent_t ver_ev[3] = {};
     bool ver_ev_ready = false, ver_ran = false;
     // randomized batch verification (k_batch.hip): r_i U_i / r_i Y_i records, group lists, group points, counts
-    DevBuf rlc[12];
+    DevBuf rlc[13];                   // [12]: the keys' fixed-base tables
     hipEvent_t rlc_ev[3] = {};
     hipEvent_t rlc_lev_ev[4] = {};    // per level: before sum / Miller / final exp / resolve
     float rlc_ms[4] = {};             // accumulated over the levels of the last call: sums, Miller, final exp (+ resolve
