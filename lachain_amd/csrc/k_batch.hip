@@ -131,6 +131,24 @@ DN void g2_mul_ab_n(g2 &r, const g2a &S, u32 a, u32 b) {
     }
     r = acc;
 }
+// the same with the point arithmetic inlined (no call frames: the DN form passes the accumulator through scratch at
+// every doubling / addition)
+DI void g1_mul_ab_inl(g1 &r, const g1a &P, u32 a, u32 b) {
+    jac_set_inf(r);
+    if (P.inf) return;
+    fp beta, phx;
+    fp_load_const(beta, LCB_G1_BETA);
+    fp_mul(phx, P.x, beta);
+#pragma unroll 1
+    for (int k = 31; k >= 0; k--) {
+        jac_dbl(r, r);
+        if ((a >> k) & 1) jac_add_aff(r, r, P.x, P.y);
+        if ((b >> k) & 1) jac_add_aff(r, r, phx, P.y);
+    }
+}
+#ifndef LCB_RLC_POINTS_WAVES
+#define LCB_RLC_POINTS_WAVES 1
+#endif
 // both multiplications in one loop with the point arithmetic inlined (two independent dependency chains per lane, no
 // call frames): a U + b phi(U) and a Y + b phi(Y).  Opt-in (LCB_RLC_JOINT): measured slower than the two calls to
 // g1_mul_ab_n (randomisation 77.7 vs 63.5 ms per 1M shares): 290 VGPRs allow one wave per SIMD instead of two.
@@ -180,11 +198,14 @@ DI void g2_inf_st(g2a_st &o) { o.ok = 1; o.pad[0] = o.pad[1] = 0; o.inf = 1; o.x
 
 // ---------------------------------------------------------------- fixed-base tables of the validators' keys
 // The keys (TPKE verification keys Y_d, threshold-signature public keys PK_k) are the same for every ciphertext /
-// coin of a batch: per key, table[w][d - 1] = d 2^(8w) K (Jacobian, d = 1..255, w = 0..3) turns a K + b phi(K) for
-// 32-bit a, b into at most 7 Jacobian additions (4 byte digits of a, 4 of b, phi applied once to the b sum) instead of
-// 32 doublings + ~32 mixed additions.  One lane per (key, window): 8w doublings, then 254 additions.
+// coin of a batch: per key, table[w][d - 1] = d 2^(8w) K (affine x, y and beta x, d = 1..255, w = 0..3) turns
+// a K + b phi(K) for 32-bit a, b into at most 8 mixed additions (4 byte digits of a, 4 of b on the phi entries) instead
+// of 32 doublings + ~32 mixed additions.  One lane per (key, window): 8w doublings, 254 additions into a
+// Jacobian scratch, then one batched inversion (Montgomery's trick) to affine.  A key whose chain meets the point at
+// infinity (a key with no r-torsion part) or that did not decompress gets ktab_ok = 0: its shares use the ladder.
 #define LCB_KTAB_ENTRIES (4 * 255)
-extern "C" __global__ void LCB_BOUNDS k_rlc_key_tables(const g1a_st *keys, u32 n_keys, u32 *tab) {
+extern "C" __global__ void LCB_BOUNDS k_rlc_key_tables(const g1a_st *keys, u32 n_keys, u32 *jtab, u32 *pre, u32 *tab,
+                                                      uint8_t *ktab_ok) {
     u32 t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= 4 * n_keys) return;
     u32 k = t >> 2, w = t & 3;
@@ -192,40 +213,75 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_key_tables(const g1a_st *keys, u32 n
     g1a_st ks = keys[k];
     st_to_g1a(K, ks);
     const size_t stride = (size_t)n_keys * LCB_KTAB_ENTRIES;      // SoA over every (key, entry)
-    size_t e0 = (size_t)k * LCB_KTAB_ENTRIES + (size_t)w * 255;
+    const size_t e0 = (size_t)k * LCB_KTAB_ENTRIES + (size_t)w * 255;
+    bool ok = ks.ok && !K.inf;
     g1 B, acc;
     jac_from_aff(B, K);
-    if (!ks.ok) jac_set_inf(B);
-    for (u32 j = 0; j < 8 * w; j++) grp_dbl(B, B);
+    for (u32 j = 0; ok && j < 8 * w; j++) grp_dbl(B, B);
     acc = B;
-    for (u32 d = 1; d <= 255; d++) {
-        g1_store_soa(tab, stride, e0 + d - 1, acc);
+    fp run = fp_one();
+    for (u32 d = 1; ok && d <= 255; d++) {            // Jacobian entries and the running product of their z
+        if (jac_is_inf(acc)) { ok = false; break; }
+        g1_store_soa(jtab, stride, e0 + d - 1, acc);
+        fp_mul(run, run, acc.z);
+        soa_store<12>(pre, stride, e0 + d - 1, &run);
         grp_add(acc, acc, B);
     }
+    ktab_ok[t] = ok;
+    if (!ok) return;
+    fp inv, beta;
+    fp_inv(inv, run);                                  // 1 / (z_1 ... z_255)
+    fp_load_const(beta, LCB_G1_BETA);
+    for (u32 d = 255; d >= 1; d--) {
+        g1 p;
+        g1_load_soa(p, jtab, stride, e0 + d - 1);
+        fp zi, zi2, pd;
+        if (d > 1) {
+            soa_load<12>(&pd, pre, stride, e0 + d - 2);
+            fp_mul(zi, inv, pd);                       // 1 / z_d
+            fp_mul(inv, inv, p.z);
+        } else {
+            zi = inv;
+        }
+        fp_sqr(zi2, zi);
+        fp xyb[3];                                     // x, y, beta x (phi(x, y) = (beta x, y))
+        fp_mul(xyb[0], p.x, zi2);
+        fp_mul(zi2, zi2, zi);
+        fp_mul(xyb[1], p.y, zi2);
+        fp_mul(xyb[2], xyb[0], beta);
+        soa_store<36>(tab, stride, e0 + d - 1, xyb);
+    }
 }
-// a K + b phi(K) from key k's table
+// a K + b phi(K) from key k's affine table (phi(x, y) = (beta x, y) also acts on Jacobian coordinates)
 DN void g1_mul_ab_tab(g1 &r, const u32 *tab, u32 n_keys, u32 k, u32 a, u32 b) {
     const size_t stride = (size_t)n_keys * LCB_KTAB_ENTRIES, e0 = (size_t)k * LCB_KTAB_ENTRIES;
-    g1 sa, sb, t;
-    jac_set_inf(sa);
-    jac_set_inf(sb);
-    for (u32 w = 0; w < 4; w++) {
-        u32 da = (a >> (8 * w)) & 255, db = (b >> (8 * w)) & 255;
-        if (da) { g1_load_soa(t, tab, stride, e0 + w * 255 + da - 1); grp_add(sa, sa, t); }
-        if (db) { g1_load_soa(t, tab, stride, e0 + w * 255 + db - 1); grp_add(sb, sb, t); }
+    g1 acc;
+    jac_set_inf(acc);
+    fp xyb[3];
+    // one digit at a time (the loads are not hoisted: eight live table points would cost 192 registers); the b digits
+    // add phi(entry) = (beta x, y), stored beside the entry
+#pragma unroll 1
+    for (u32 j = 0; j < 8; j++) {
+        u32 w = j & 3, dg = ((j < 4 ? b : a) >> (8 * w)) & 255;
+        if (!dg) continue;
+        asm volatile("" ::: "memory");
+        soa_load<36>(xyb, tab, stride, e0 + w * 255 + dg - 1);
+        grp_madd(acc, acc, j < 4 ? xyb[2] : xyb[0], xyb[1]);
     }
-    fp beta;
-    fp_load_const(beta, LCB_G1_BETA);
-    fp_mul(sb.x, sb.x, beta);            // phi on Jacobian coordinates: (beta X, Y, Z)
-    grp_add(r, sa, sb);
+    r = acc;
+}
+DI bool ktab_usable(const uint8_t *ktab_ok, u32 k) {
+    return ktab_ok && (ktab_ok[4 * k] & ktab_ok[4 * k + 1] & ktab_ok[4 * k + 2] & ktab_ok[4 * k + 3]);
 }
 
 // ---------------------------------------------------------------- TPKE: per-share randomisation
 // validity as k_tpke_miller except the ciphertext's (applied per group by k_tpke_rlc_sum, so this kernel needs only
 // the decompressed keys and may run beside the ciphertext preparation)
-extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_points(u32 n_cts, const g1a_st *keys, u32 n_keys, const u32 *ct_idx,
+extern "C" __global__ void __launch_bounds__(LCB_BLOCK) __attribute__((amdgpu_waves_per_eu(LCB_RLC_POINTS_WAVES)))
+k_tpke_rlc_points(u32 n_cts, const g1a_st *keys, u32 n_keys, const u32 *ct_idx,
                                                        const u32 *dec_idx, const uint8_t *ui, u32 n, rlc_key key,
-                                                       u32 *rU, u32 *rY, uint8_t *accept, const u32 *ktab) {
+                                                       u32 *rU, u32 *rY, uint8_t *accept, const u32 *ktab,
+                                                       const uint8_t *ktab_ok) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u32 c = ct_idx[i], d = dec_idx[i];
@@ -242,9 +298,17 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_points(u32 n_cts, const g1a_st 
 #ifdef LCB_RLC_JOINT
         g1_mul_ab2(p, q, Ui, Y, a, b);
 #else
-        g1_mul_ab_n(p, Ui, a, b);
-        if (ktab) g1_mul_ab_tab(q, ktab, n_keys, d, a, b);
+#ifdef LCB_RLC_CALLS
+        g1_mul_ab_n(p, Ui, a, b);        // measured 148.8 vs 144.7 ms per 1M-share batched step (inline, default)
+#else
+        g1_mul_ab_inl(p, Ui, a, b);
+#endif
+#ifdef LCB_RLC_NO_TABLE_CODE              // measured 159.8 vs 148.8 ms per step (tables, default)
+        g1_mul_ab_n(q, Y, a, b);
+#else
+        if (ktab_usable(ktab_ok, d)) g1_mul_ab_tab(q, ktab, n_keys, d, a, b);
         else g1_mul_ab_n(q, Y, a, b);
+#endif
 #endif
     } else {                             // an invalid share is rejected and contributes nothing to its group
         jac_set_inf(p);
@@ -413,7 +477,7 @@ struct ts_grp { g1a_st p; g2a_st s; };
 extern "C" __global__ void LCB_BOUNDS k_ts_rlc_points(u32 n_msgs, const g1a_st *pks, u32 n_pks, const u32 *msg_idx,
                                                      const u32 *pk_idx, const uint8_t *sigs, u32 n, rlc_key key,
                                                      u32 *rP, u32 *rS, uint8_t *accept, uint4 *desc, u32 *count,
-                                                     const u32 *ktab) {
+                                                     const u32 *ktab, const uint8_t *ktab_ok) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u32 m = msg_idx[i], k = pk_idx[i];
@@ -432,7 +496,7 @@ extern "C" __global__ void LCB_BOUNDS k_ts_rlc_points(u32 n_msgs, const g1a_st *
         if (g2_in_subgroup(S)) {
             u32 a, b;
             rlc_scalar(key, i, a, b);
-            if (ktab) g1_mul_ab_tab(p, ktab, n_pks, k, a, b);
+            if (ktab_usable(ktab_ok, k)) g1_mul_ab_tab(p, ktab, n_pks, k, a, b);
             else g1_mul_ab_n(p, PK, a, b);
             g2_mul_ab_n(q, S, a, b);
         } else {
@@ -622,29 +686,38 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_search(const uint4 *search, u32 o, u
 }
 
 // ---------------------------------------------------------------- host launch wrappers
-extern "C" size_t lcbk_key_table_bytes(u32 n_keys) { return (size_t)n_keys * LCB_KTAB_ENTRIES * 144; }
-extern "C" void lcbk_rlc_key_tables(dim3 grid, hipStream_t s, const void *keys, u32 n_keys, u32 *tab) {
-    LCB_LAUNCH(k_rlc_key_tables, (const g1a_st *)keys, n_keys, tab);
+// table workspace per key: Jacobian scratch 144 B + prefix products 48 B + table 144 B per entry + 4 flags
+extern "C" size_t lcbk_key_table_bytes(u32 n_keys) { return (size_t)n_keys * (LCB_KTAB_ENTRIES * 336 + 4); }
+extern "C" void lcbk_rlc_key_tables(dim3 grid, hipStream_t s, const void *keys, u32 n_keys, u32 *ws, u32 **tab,
+                                    uint8_t **ktab_ok) {
+    const size_t ne = (size_t)n_keys * LCB_KTAB_ENTRIES;
+    u32 *jtab = ws, *pre = ws + 36 * ne, *t = ws + 48 * ne;
+    uint8_t *okv = (uint8_t *)(ws + 84 * ne);
+    *tab = t;
+    *ktab_ok = okv;
+    LCB_LAUNCH(k_rlc_key_tables, (const g1a_st *)keys, n_keys, jtab, pre, t, okv);
 }
 extern "C" void lcbk_tpke_rlc_points(dim3 grid, hipStream_t s, u32 n_cts, const void *keys, u32 n_keys,
                                      const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n,
-                                     const u32 key[10], u32 *rU, u32 *rY, uint8_t *accept, const u32 *ktab) {
+                                     const u32 key[10], u32 *rU, u32 *rY, uint8_t *accept, const u32 *ktab,
+                                     const uint8_t *ktab_ok) {
     rlc_key k;
     for (int j = 0; j < 8; j++) k.k[j] = key[j];
     k.nonce[0] = key[8];
     k.nonce[1] = key[9];
-    LCB_LAUNCH(k_tpke_rlc_points, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, k, rU, rY, accept, ktab);
+    LCB_LAUNCH(k_tpke_rlc_points, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, k, rU, rY, accept, ktab,
+               ktab_ok);
 }
 extern "C" void lcbk_ts_rlc_points(dim3 grid, hipStream_t s, u32 n_msgs, const void *pks, u32 n_pks,
                                    const u32 *msg_idx, const u32 *pk_idx, const uint8_t *sigs, u32 n,
                                    const u32 key[10], u32 *rP, u32 *rS, uint8_t *accept, void *desc, u32 *count,
-                                   const u32 *ktab) {
+                                   const u32 *ktab, const uint8_t *ktab_ok) {
     rlc_key k;
     for (int j = 0; j < 8; j++) k.k[j] = key[j];
     k.nonce[0] = key[8];
     k.nonce[1] = key[9];
     LCB_LAUNCH(k_ts_rlc_points, n_msgs, (const g1a_st *)pks, n_pks, msg_idx, pk_idx, sigs, n, k, rP, rS, accept,
-               (uint4 *)desc, count, ktab);
+               (uint4 *)desc, count, ktab, ktab_ok);
 }
 extern "C" void lcbk_rlc_groups(dim3 grid, hipStream_t s, const u32 *key_idx, u32 n, u32 n_keys, u32 cap, void *desc,
                                 u32 *count) {

@@ -60,9 +60,9 @@ extern "C" void lcbk_secp_gen(hipStream_t s, void *out, u32 *ok);
 extern "C" void lcbk_secp_pubkey(hipStream_t s, const uint8_t *privs, u32 n, const void *g_table, uint8_t *out33, uint8_t *ok);
 extern "C" void lcbk_secp_sign(hipStream_t s, const uint8_t *hashes, const uint8_t *privs, const uint8_t *nonces, u32 n, const void *g_table, int chain_id, int use_new, uint8_t *out, uint8_t *ok);
 extern "C" size_t lcbk_key_table_bytes(u32 n_keys);
-extern "C" void lcbk_rlc_key_tables(dim3 grid, hipStream_t s, const void *keys, u32 n_keys, u32 *tab);
-extern "C" void lcbk_tpke_rlc_points(dim3 grid, hipStream_t s, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, const u32 key[10], u32 *rU, u32 *rY, uint8_t *accept, const u32 *ktab);
-extern "C" void lcbk_ts_rlc_points(dim3 grid, hipStream_t s, u32 n_msgs, const void *pks, u32 n_pks, const u32 *msg_idx, const u32 *pk_idx, const uint8_t *sigs, u32 n, const u32 key[10], u32 *rP, u32 *rS, uint8_t *accept, void *desc, u32 *count, const u32 *ktab);
+extern "C" void lcbk_rlc_key_tables(dim3 grid, hipStream_t s, const void *keys, u32 n_keys, u32 *ws, u32 **tab, uint8_t **ktab_ok);
+extern "C" void lcbk_tpke_rlc_points(dim3 grid, hipStream_t s, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, const u32 key[10], u32 *rU, u32 *rY, uint8_t *accept, const u32 *ktab, const uint8_t *ktab_ok);
+extern "C" void lcbk_ts_rlc_points(dim3 grid, hipStream_t s, u32 n_msgs, const void *pks, u32 n_pks, const u32 *msg_idx, const u32 *pk_idx, const uint8_t *sigs, u32 n, const u32 key[10], u32 *rP, u32 *rS, uint8_t *accept, void *desc, u32 *count, const u32 *ktab, const uint8_t *ktab_ok);
 extern "C" void lcbk_rlc_groups(dim3 grid, hipStream_t s, const u32 *key_idx, u32 n, u32 n_keys, u32 cap, void *desc, u32 *count);
 extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 first, const uint8_t *ct_ok, const uint8_t *ct_g2, const void *keys, u32 n_keys, const u32 *dec_idx, const uint8_t *ui, const u32 *rU, const u32 *rY, u32 n, void *gpts, uint8_t *accept, uint8_t *gexact, u32 *wsum);
 extern "C" void lcbk_tpke_rlc_wsum(dim3 grid, hipStream_t s, const void *sdesc, u32 n_s, const u32 *wsum, u32 n_l1, void *gpts);

@@ -719,11 +719,13 @@ bool rlc_ws(lcb_ctx *c, RlcWs &w, size_t n, size_t rec_a, size_t rec_b) {
 }
 // fixed-base tables of the batch's keys (k_rlc_key_tables), when the batch is large enough to repay them
 // (4 x 255 points per key, ~250 additions of latency); nullptr: the points kernel multiplies the keys directly
-u32 *rlc_key_tables(lcb_ctx *c, const void *keys, size_t n_keys, hipStream_t s) {
+u32 *rlc_key_tables(lcb_ctx *c, const void *keys, size_t n_keys, hipStream_t s, uint8_t **ktab_ok) {
+    *ktab_ok = nullptr;
     if (!n_keys || n_keys > 4096 || getenv("LCB_RLC_NO_KEY_TABLES")) return nullptr;
-    u32 *tab = (u32 *)c->rlc[12].get(lcbk_key_table_bytes((u32)n_keys));
-    if (!tab) return nullptr;
-    lcbk_rlc_key_tables(dim3(nblk(4 * n_keys)), s, keys, (u32)n_keys, tab);
+    u32 *ws = (u32 *)c->rlc[12].get(lcbk_key_table_bytes((u32)n_keys));
+    if (!ws) return nullptr;
+    u32 *tab = nullptr;
+    lcbk_rlc_key_tables(dim3(nblk(4 * n_keys)), s, keys, (u32)n_keys, ws, &tab, ktab_ok);
     return tab;
 }
 // phase 1 (needs the decompressed keys only): per-share exponent multiples + level-1 groups (count left on device)
@@ -733,9 +735,10 @@ int rlc_points_enqueue(lcb_ctx *c, RlcWs &w, uint8_t *d_accept, size_t n, size_t
     if (!rlc_key_fill(c, key) || !rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G1_JAC_BYTES)) return -1;
     hipEventRecord(c->rlc_ev[0], s);
     hipMemsetAsync(w.cnt, 0, 16, s);
-    u32 *ktab = rlc_key_tables(c, c->t_keys.p, n_keys, s);
+    uint8_t *kok = nullptr;
+    u32 *ktab = rlc_key_tables(c, c->t_keys.p, n_keys, s, &kok);
     lcbk_tpke_rlc_points(dim3(nblk(n)), s, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct, d_dec, d_ui, (u32)n, key, w.rA,
-                         w.rB, d_accept, ktab);
+                         w.rB, d_accept, ktab, kok);
     lcbk_rlc_groups(dim3(nblk(n)), s, d_ct, (u32)n, (u32)n_cts, 32, w.dA, w.cnt);
     hipEventRecord(c->rlc_ev[1], s);
     return launched("tpke batched verify launch") ? 0 : -1;
@@ -746,9 +749,10 @@ int ts_rlc_points_enqueue(lcb_ctx *c, RlcWs &w, uint8_t *d_accept, size_t n, siz
     if (!rlc_key_fill(c, key) || !rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G2_JAC_BYTES)) return -1;
     hipEventRecord(c->rlc_ev[0], s);
     hipMemsetAsync(w.cnt, 0, 16, s);
-    u32 *ktab = rlc_key_tables(c, c->s_keys.p, n_pks, s);
+    uint8_t *kok = nullptr;
+    u32 *ktab = rlc_key_tables(c, c->s_keys.p, n_pks, s, &kok);
     lcbk_ts_rlc_points(dim3(nblk(n)), s, (u32)n_msgs, c->s_keys.p, (u32)n_pks, d_midx, d_pidx, d_sigs, (u32)n, key,
-                       w.rA, w.rB, d_accept, w.dA, w.cnt, ktab);
+                       w.rA, w.rB, d_accept, w.dA, w.cnt, ktab, kok);
     lcbk_rlc_groups(dim3(nblk(n)), s, d_midx, (u32)n, (u32)n_msgs, 128, w.dA, w.cnt);
     hipEventRecord(c->rlc_ev[1], s);
     return launched("ts batched verify launch") ? 0 : -1;
