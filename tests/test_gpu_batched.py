@@ -280,3 +280,26 @@ def test_batched_w_outside_g2(nat, tdev, fused):
     assert got.tolist() == expect
     exact = nat.tpke_verify_shares(b.yi, b.cts, [(int(c), int(j), s) for c, j, s in zip(ct, dec, shares)])
     assert [int(x) for x in exact] == expect
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_batched_small_order_key(nat, tdev, fused):
+    """a verification key of order 3 ((0, -2) is on y^2 = x^3 + 4): its fixed-base table meets the point at infinity
+    (3 K = O), so its shares take the ladder (ktab_ok = 0); the pairing kills K, so the reference accepts exactly the
+    shares U with e(U, H) = 1 (U = O or a torsion point) — decisions must equal the oracle's"""
+    b = Batch(b"gpu-batched-order3", 6, 1, 2)
+    k3 = bytearray(48)
+    k3[47] |= 0x80                        # x = 0, y odd: y = p - 2
+    k3 = bytes(k3)
+    assert o.g1_valid(k3) and not o.g1_in_subgroup(k3) and o.g1_mul(k3, o.fr(3)) == bytes(48)
+    b.yi[2] = k3
+    ct = np.repeat(np.arange(2, dtype=np.uint32), 6)
+    dec = np.tile(np.arange(6, dtype=np.uint32), 2)
+    shares = [b.good[c][j] for c, j in zip(ct, dec)]
+    shares[2] = k3                        # accepted: e(K, H) = 1 = e(K, W)
+    shares[6 + 2] = bytes(48)             # infinity: accepted for the same reason
+    shares[5] = b.bad[0][5]
+    expect = [int(b.expect(int(c), int(j), s)) for c, j, s in zip(ct, dec, shares)]
+    assert expect[2] == 1 and expect[8] == 1 and expect[5] == 0
+    got = run_dev(nat, tdev, b, ct, dec, shares, fused=fused)
+    assert got.tolist() == expect
