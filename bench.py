@@ -1079,11 +1079,21 @@ def run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, dd, n, n_cts, n_d
         parts.append(dict(c0=c0, nc=c1 - c0, s0=s0, ns=s1 - s0, ct=ct_local, voff=voff, ctx=ctx, stream=st))
     pool = concurrent.futures.ThreadPoolExecutor(max_workers=len(parts))
 
+    single_stream = K > 1 and args.tpke_parts_single_stream
+
     def one(p):
-        rc = lib.lcb_ctx_tpke_verify_shares_batched_dev(
-            p["ctx"].ptr, d_acc.data_ptr() + p["s0"], p["ns"], py, nk, pu + 48 * p["c0"], pw + 96 * p["c0"],
-            pv + vlen * p["c0"], p["voff"].data_ptr(), p["nc"], p["ct"].data_ptr(), d_dec.data_ptr() + 4 * p["s0"],
-            d_ui.data_ptr() + 48 * p["s0"], p["stream"].cuda_stream)
+        if single_stream:       # prepare + verify_prepared on the part's one stream (no second stream per context)
+            rc = lib.lcb_ctx_tpke_prepare_dev(p["ctx"].ptr, py, nk, pu + 48 * p["c0"], pw + 96 * p["c0"],
+                                              pv + vlen * p["c0"], p["voff"].data_ptr(), p["nc"],
+                                              p["stream"].cuda_stream)
+            rc |= lib.lcb_ctx_tpke_verify_prepared_batched_dev(
+                p["ctx"].ptr, d_acc.data_ptr() + p["s0"], p["ns"], nk, p["nc"], p["ct"].data_ptr(),
+                d_dec.data_ptr() + 4 * p["s0"], d_ui.data_ptr() + 48 * p["s0"], p["stream"].cuda_stream)
+        else:
+            rc = lib.lcb_ctx_tpke_verify_shares_batched_dev(
+                p["ctx"].ptr, d_acc.data_ptr() + p["s0"], p["ns"], py, nk, pu + 48 * p["c0"], pw + 96 * p["c0"],
+                pv + vlen * p["c0"], p["voff"].data_ptr(), p["nc"], p["ct"].data_ptr(), d_dec.data_ptr() + 4 * p["s0"],
+                d_ui.data_ptr() + 48 * p["s0"], p["stream"].cuda_stream)
         if rc != 0:
             raise RuntimeError(nat.last_error())
 
@@ -1182,9 +1192,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--tpke-batched", type=int, default=1, help="time the randomized batch verify (0 = skip)")
     ap.add_argument("--tpke-exact", type=int, default=1, help="time the exact per-share verify (0 = skip)")
+    ap.add_argument("--tpke-parts-single-stream", type=int, default=0,
+                    help="with --tpke-streams K > 1: each part prepares and verifies on one stream")
     ap.add_argument("--tpke-streams", type=int, default=1,
                     help="batched verify: concurrent parts (contexts / streams / host threads) per step; measured "
-                         "slower with 2 / 4 parts (177 / 261 vs 156 ms per 1M shares: the parts' kernels serialize)")
+                         "no faster with 2 or 3 parts (147 - 159 vs 145 ms per 1M shares)")
     ap.add_argument("--headline", choices=("batched", "exact"), default="batched",
                     help="which TPKE path the line's value / roofline / cpu_baseline describe")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
