@@ -439,6 +439,10 @@ int lcb_queue_wait(lcb_queue *q, int64_t ticket);
 int lcb_queue_flush(lcb_queue *q);
 int lcb_queue_stats(lcb_queue *q, uint64_t out[3]);
 const char *lcb_queue_last_error(lcb_queue *q);
+/* flushes of at least min_shares shares use the randomized batch checks (lcb_tpke_verify_shares_batched /
+   lcb_ts_verify_shares_batched, shares reordered by ciphertext / message inside the flush); 0 = exact checks only
+   (the default) */
+int lcb_queue_set_batched(lcb_queue *q, size_t min_shares);
 
 /* ------------------------------------------------------------------ CommonCoin consumers (row a13)
    The combined signature's serialized bytes feed two consensus decisions:

@@ -11,8 +11,11 @@
 // that share's decision.  Ciphertexts, verification keys and messages are de-duplicated per batch, so the batch
 // shares hash-to-G2 and Miller-line precomputation exactly as a caller-built batch would.  Decisions are the
 // same per-share results the batch entry points produce (bit-exact with VerifyShare / ValidateSignature).
+// lcb_queue_set_batched(q, m) sends flushes of at least m shares through the randomized batch checks instead
+// (k_batch.hip): more shares per GPU-second, a few more latency-bound launches per flush.
 #include <stdint.h>
 #include <string.h>
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -52,6 +55,9 @@ struct lcb_queue {
     std::unordered_map<int64_t, int8_t> results;     // ticket -> 1 / 0 / -1 (batch failed), until waited for
     int64_t done_upto = 0;                            // every ticket <= this has its result (batches are FIFO)
     uint64_t batches = 0, items = 0, max_seen = 0;
+    // randomized batch checks (lcb_queue_set_batched): flushes of at least batched_min shares go through the
+    // *_batched entry points, shares ordered by ciphertext / message so each one's shares form a group
+    size_t batched_min = 0;
     std::string last_error;
     std::thread worker;
 };
@@ -80,8 +86,26 @@ void run_tpke(lcb_queue *q, std::vector<TpkeItem> &items) {
     }
     std::vector<uint8_t> acc(items.size());
     if (vs.empty()) vs.push_back(0);
-    int rc = lcb_tpke_verify_shares(acc.data(), items.size(), keys.data(), kidx.size(), us.data(), ws.data(), vs.data(),
+    int rc;
+    if (q->batched_min && items.size() >= q->batched_min) {
+        // ciphertext-major order for the group checks (stable: a ciphertext's shares keep their submission order)
+        std::vector<uint32_t> ord(items.size());
+        for (size_t i = 0; i < ord.size(); i++) ord[i] = (uint32_t)i;
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return ct[a] < ct[b]; });
+        std::vector<uint32_t> ct2(ord.size()), dec2(ord.size());
+        std::vector<uint8_t> uis2(uis.size()), acc2(ord.size());
+        for (size_t j = 0; j < ord.size(); j++) {
+            ct2[j] = ct[ord[j]];
+            dec2[j] = dec[ord[j]];
+            memcpy(&uis2[48 * j], &uis[48 * (size_t)ord[j]], 48);
+        }
+        rc = lcb_tpke_verify_shares_batched(acc2.data(), items.size(), keys.data(), kidx.size(), us.data(), ws.data(),
+                                            vs.data(), voff.data(), cidx.size(), ct2.data(), dec2.data(), uis2.data());
+        for (size_t j = 0; j < ord.size(); j++) acc[ord[j]] = acc2[j];
+    } else {
+        rc = lcb_tpke_verify_shares(acc.data(), items.size(), keys.data(), kidx.size(), us.data(), ws.data(), vs.data(),
                                     voff.data(), cidx.size(), ct.data(), dec.data(), uis.data());
+    }
     std::lock_guard<std::mutex> lk(q->mu);
     if (rc) q->last_error = lcb_last_error();
     for (size_t i = 0; i < items.size(); i++) q->results[items[i].ticket] = rc ? -1 : (int8_t)(acc[i] != 0);
@@ -106,8 +130,25 @@ void run_ts(lcb_queue *q, std::vector<TsItem> &items) {
     }
     std::vector<uint8_t> acc(items.size());
     if (msgs.empty()) msgs.push_back(0);
-    int rc = lcb_ts_verify_shares(acc.data(), items.size(), pks.data(), pidx.size(), sigs.data(), msgs.data(),
+    int rc;
+    if (q->batched_min && items.size() >= q->batched_min) {
+        std::vector<uint32_t> ord(items.size());
+        for (size_t i = 0; i < ord.size(); i++) ord[i] = (uint32_t)i;
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return mi[a] < mi[b]; });
+        std::vector<uint32_t> mi2(ord.size()), pi2(ord.size());
+        std::vector<uint8_t> sigs2(sigs.size()), acc2(ord.size());
+        for (size_t j = 0; j < ord.size(); j++) {
+            mi2[j] = mi[ord[j]];
+            pi2[j] = pi[ord[j]];
+            memcpy(&sigs2[96 * j], &sigs[96 * (size_t)ord[j]], 96);
+        }
+        rc = lcb_ts_verify_shares_batched(acc2.data(), items.size(), pks.data(), pidx.size(), sigs2.data(), msgs.data(),
+                                          moff.data(), midx.size(), mi2.data(), pi2.data());
+        for (size_t j = 0; j < ord.size(); j++) acc[ord[j]] = acc2[j];
+    } else {
+        rc = lcb_ts_verify_shares(acc.data(), items.size(), pks.data(), pidx.size(), sigs.data(), msgs.data(),
                                   moff.data(), midx.size(), mi.data(), pi.data());
+    }
     std::lock_guard<std::mutex> lk(q->mu);
     if (rc) q->last_error = lcb_last_error();
     for (size_t i = 0; i < items.size(); i++) q->results[items[i].ticket] = rc ? -1 : (int8_t)(acc[i] != 0);
@@ -229,6 +270,12 @@ extern "C" int lcb_queue_wait(lcb_queue *q, int64_t ticket) {
     }
 }
 extern "C" const char *lcb_queue_last_error(lcb_queue *q) { return q ? q->last_error.c_str() : ""; }
+extern "C" int lcb_queue_set_batched(lcb_queue *q, size_t min_shares) {
+    if (!q) return -1;
+    std::lock_guard<std::mutex> lk(q->mu);
+    q->batched_min = min_shares;
+    return 0;
+}
 extern "C" int lcb_queue_stats(lcb_queue *q, uint64_t out[3]) {
     if (!q || !out) return -1;
     std::lock_guard<std::mutex> lk(q->mu);

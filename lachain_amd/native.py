@@ -139,6 +139,7 @@ _SIGS = {
     "lcb_queue_flush": (ctypes.c_int, [ctypes.c_void_p]),
     "lcb_queue_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
     "lcb_queue_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
+    "lcb_queue_set_batched": (ctypes.c_int, [ctypes.c_void_p, c_size]),
     "lcb_ecdsa_keyset_create": (ctypes.c_void_p, [c_u8p, c_size, c_size]),
     "lcb_ecdsa_keyset_destroy": (None, [ctypes.c_void_p]),
     "lcb_ecdsa_keyset_size": (c_size, [ctypes.c_void_p]),
@@ -614,10 +615,12 @@ class BatchQueue:
     drop-in shape of PublicKey.VerifyShare (TPKE/PublicKey.cs:88-92) and ValidateSignature
     (ThresholdSignature/PublicKey.cs:16-21) for one-share-per-call callers."""
 
-    def __init__(self, max_batch=4096, max_delay_ms=5.0):
+    def __init__(self, max_batch=4096, max_delay_ms=5.0, batched_min=0):
         self.ptr = lib().lcb_queue_create(max_batch, int(max_delay_ms * 1000))
         if not self.ptr:
             raise RuntimeError("lcb_queue_create failed")
+        if batched_min:
+            _check(lib().lcb_queue_set_batched(self.ptr, batched_min), "queue_set_batched")
 
     def submit_tpke(self, y48, u48, v, w96, ui48):
         t = lib().lcb_queue_tpke_verify(self.ptr, y48, u48, v, len(v), w96, ui48)

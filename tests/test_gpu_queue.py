@@ -53,9 +53,12 @@ def items():
     return out
 
 
-def test_queue_sixteen_threads_single_shares(nat, items):
+@pytest.mark.parametrize("batched_min", [0, 8])
+def test_queue_sixteen_threads_single_shares(nat, items, batched_min):
+    """batched_min = 8: flushes of >= 8 shares go through the randomized batch checks (lcb_queue_set_batched), the
+    shares of a flush reordered by ciphertext / message inside the library; decisions still equal the oracle's"""
     errors = []
-    with nat.BatchQueue(max_batch=64, max_delay_ms=3.0) as q:
+    with nat.BatchQueue(max_batch=64, max_delay_ms=3.0, batched_min=batched_min) as q:
         def worker(k):
             try:
                 for rep in range(3):
