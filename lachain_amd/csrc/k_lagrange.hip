@@ -65,6 +65,47 @@ extern "C" __global__ void LCB_BOUNDS k_lagrange_coeffs(const uint8_t *xs, const
     }
     status[j] = ok;
 }
+// Inlined ladders for the lanes below (no call frames: the DN group operations pass the accumulator through scratch
+// at every step).  LCB_LAG_CALLS restores the call form.
+template <class F> DI void jac_mul_aff_inl(jac<F> &r, const aff<F> &p, const u32 *k, int nbits) {
+    jac_set_inf(r);
+    if (p.inf) return;
+#pragma unroll 1
+    for (int i = nbits - 1; i >= 0; i--) {
+        jac_dbl(r, r);
+        if ((k[i >> 5] >> (i & 31)) & 1) jac_add_aff(r, r, p.x, p.y);
+    }
+}
+// g2_mul_gls (curve.hpp) with the loop inlined
+DI void g2_mul_gls_inl(g2 &r, const g2a &A, const u32 k[8]) {
+    jac_set_inf(r);
+    if (A.inf) return;
+    u32 q[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) q[j] = k[j];
+    u64 d[4];
+    u256_divmod_u(q, d[0]);
+    u256_divmod_u(q, d[1]);
+    u256_divmod_u(q, d[2]);
+    d[3] = (u64)q[0] | ((u64)q[1] << 32);
+    g2 P, T;
+    jac_from_aff(P, A);
+    g2a Q[4];
+    Q[0] = A;
+    g2_psi(T, P);
+    Q[1].x = T.x; fp2_neg(Q[1].y, T.y); Q[1].inf = false;
+    g2_psi2(T, P);
+    Q[2].x = T.x; Q[2].y = T.y; Q[2].inf = false;
+    g2_psi(T, T);
+    Q[3].x = T.x; fp2_neg(Q[3].y, T.y); Q[3].inf = false;
+#pragma unroll 1
+    for (int b = 63; b >= 0; b--) {
+        jac_dbl(r, r);
+#pragma unroll 1
+        for (int i = 0; i < 4; i++)
+            if ((d[i] >> b) & 1) jac_add_aff(r, r, Q[i].x, Q[i].y);
+    }
+}
 // partial products lambda_i * Y_i for every entry (one lane per entry)
 extern "C" __global__ void LCB_BOUNDS k_g1_mul_lanes(const uint8_t *ys, const fr *lam_raw, u32 n_entries, g1 *out,
                                                     uint8_t *ok_out) {
@@ -76,7 +117,11 @@ extern "C" __global__ void LCB_BOUNDS k_g1_mul_lanes(const uint8_t *ys, const fr
     // outside the r-torsion that G1.FromBytes accepts (GLV would be wrong for their cofactor component)
     g1 R;
     fr k = lam_raw[i];
+#ifdef LCB_LAG_CALLS
     jac_mul_aff(R, A, k.v, 256);
+#else
+    jac_mul_aff_inl(R, A, k.v, 256);
+#endif
     out[i] = R;
     ok_out[i] = ok;
 }
@@ -90,8 +135,13 @@ extern "C" __global__ void LCB_BOUNDS k_g2_mul_lanes(const uint8_t *ys, const fr
     // on-curve input takes the plain ladder, so the result equals the oracle's for every input
     g2 R;
     fr k = lam_raw[i];
+#ifdef LCB_LAG_CALLS
     if (g2_in_subgroup(A)) g2_mul_gls(R, A, k.v);
     else jac_mul_aff(R, A, k.v, 256);
+#else
+    if (g2_in_subgroup(A)) g2_mul_gls_inl(R, A, k.v);
+    else jac_mul_aff_inl(R, A, k.v, 256);
+#endif
     out[i] = R;
     ok_out[i] = ok;
 }
