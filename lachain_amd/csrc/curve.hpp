@@ -305,6 +305,28 @@ DN bool g2_in_subgroup(const g2a &A) {
     return okx && fp2_eq(t, ny);
 }
 
+// g2_in_subgroup with the 64-bit ladder inlined (no call frames: for kernels where the test is a hot step)
+DI bool g2_in_subgroup_inl(const g2a &A) {
+    if (A.inf) return true;
+    g2 T, S, P;
+    jac_set_inf(T);
+#pragma unroll 1
+    for (int i = 63; i >= 0; i--) {
+        jac_dbl(T, T);
+        if ((LCB_Z_ABS >> i) & 1) jac_add_aff(T, T, A.x, A.y);
+    }
+    if (jac_is_inf(T)) return false;
+    jac_from_aff(P, A);
+    g2_psi(S, P);
+    fp2 z2, z3, t, ny;
+    fp2_sqr(z2, T.z);
+    fp2_mul(z3, z2, T.z);
+    fp2_mul(t, S.x, z2);
+    bool okx = fp2_eq(t, T.x);
+    fp2_mul(t, S.y, z3);
+    fp2_neg(ny, T.y);
+    return okx && fp2_eq(t, ny);
+}
 // ---------------------------------------------------------------- GLV scalar multiplication in G1
 // phi(x, y) = (beta x, y) acts on the r-torsion as lambda = z^2 - 1 = u^2 - 1.  Two base-u digits and the
 // quotient give k = d0 + d1 u + a1 u^2 = (a0 + a1) + a1 lambda with a0 = d0 + d1 u, so

@@ -166,28 +166,6 @@ DI void g2_mul_ab_inl(g2 &r, const g2a &S, u32 a, u32 b) {
         if ((b >> k) & 1) jac_add_aff(r, r, T.x, T.y);
     }
 }
-// g2_in_subgroup (curve.hpp: psi(P) == [z] P) with the 64-bit ladder inlined
-DI bool g2_in_subgroup_inl(const g2a &A) {
-    if (A.inf) return true;
-    g2 T, S, P;
-    jac_set_inf(T);
-#pragma unroll 1
-    for (int i = 63; i >= 0; i--) {
-        jac_dbl(T, T);
-        if ((LCB_Z_ABS >> i) & 1) jac_add_aff(T, T, A.x, A.y);
-    }
-    if (jac_is_inf(T)) return false;
-    jac_from_aff(P, A);
-    g2_psi(S, P);
-    fp2 z2, z3, t, ny;
-    fp2_sqr(z2, T.z);
-    fp2_mul(z3, z2, T.z);
-    fp2_mul(t, S.x, z2);
-    bool okx = fp2_eq(t, T.x);
-    fp2_mul(t, S.y, z3);
-    fp2_neg(ny, T.y);
-    return okx && fp2_eq(t, ny);
-}
 // both multiplications in one loop with the point arithmetic inlined (two independent dependency chains per lane, no
 // call frames): a U + b phi(U) and a Y + b phi(Y).  Opt-in (LCB_RLC_JOINT): measured slower than the two calls to
 // g1_mul_ab_n (randomisation 77.7 vs 63.5 ms per 1M shares): 290 VGPRs allow one wave per SIMD instead of two.

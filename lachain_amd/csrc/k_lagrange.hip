@@ -139,7 +139,7 @@ extern "C" __global__ void LCB_BOUNDS k_g2_mul_lanes(const uint8_t *ys, const fr
     if (g2_in_subgroup(A)) g2_mul_gls(R, A, k.v);
     else jac_mul_aff(R, A, k.v, 256);
 #else
-    if (g2_in_subgroup(A)) g2_mul_gls_inl(R, A, k.v);
+    if (g2_in_subgroup_inl(A)) g2_mul_gls_inl(R, A, k.v);
     else jac_mul_aff_inl(R, A, k.v, 256);
 #endif
     out[i] = R;
