@@ -207,6 +207,19 @@ template <class F> DI void jac_mul_u64(jac<F> &r, const jac<F> &p, u64 k) {
     r = acc;
 }
 
+// jac_mul_u64 with the group operations inlined (the latency chains of hash-to-G2's cofactor clearing)
+template <class F> DI void jac_mul_u64_inl(jac<F> &r, const jac<F> &p, u64 k) {
+    if (k == 0) { jac_set_inf(r); return; }
+    int top = 63 - __clzll(k);
+    jac<F> acc = p;
+#pragma unroll 1
+    for (int i = top - 1; i >= 0; i--) {
+        jac_dbl(acc, acc);
+        if ((k >> i) & 1) jac_add(acc, acc, p);
+    }
+    r = acc;
+}
+
 // ---------------------------------------------------------------- G2 endomorphism psi (M-type twist)
 // psi(x, y) = (conj(x) xi^-(p-1)/3, conj(y) xi^-(p-1)/2); Jacobian-compatible since conj commutes
 DI void g2_psi(g2 &r, const g2 &p) {
