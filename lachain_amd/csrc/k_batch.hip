@@ -221,11 +221,14 @@ DI void g2_inf_st(g2a_st &o) { o.ok = 1; o.pad[0] = o.pad[1] = 0; o.inf = 1; o.x
 // Jacobian scratch, then one batched inversion (Montgomery's trick) to affine.  A key whose chain meets the point at
 // infinity (a key with no r-torsion part) or that did not decompress gets ktab_ok = 0: its shares use the ladder.
 #define LCB_KTAB_ENTRIES (4 * 255)
+#define LCB_KTAB_CHUNK 32                              // entries per lane: 8 lanes per (key, window)
+#define LCB_KTAB_LANES 32                              // lanes (and flags) per key
 extern "C" __global__ void LCB_BOUNDS k_rlc_key_tables(const g1a_st *keys, u32 n_keys, u32 *jtab, u32 *pre, u32 *tab,
                                                       uint8_t *ktab_ok) {
     u32 t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= 4 * n_keys) return;
-    u32 k = t >> 2, w = t & 3;
+    if (t >= LCB_KTAB_LANES * n_keys) return;
+    u32 k = t / LCB_KTAB_LANES, w = (t / 8) & 3, ch = t & 7;
+    u32 d0 = ch * LCB_KTAB_CHUNK + 1, d1 = min(255u, d0 + LCB_KTAB_CHUNK - 1);   // entries d0 .. d1
     g1a K;
     g1a_st ks = keys[k];
     st_to_g1a(K, ks);
@@ -234,26 +237,29 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_key_tables(const g1a_st *keys, u32 n
     bool ok = ks.ok && !K.inf;
     g1 B, acc;
     jac_from_aff(B, K);
-    for (u32 j = 0; ok && j < 8 * w; j++) grp_dbl(B, B);
-    acc = B;
+#pragma unroll 1
+    for (u32 j = 0; ok && j < 8 * w; j++) jac_dbl(B, B);            // B = 2^(8w) K
+    jac_mul_u64_inl(acc, B, d0);                                   // d0 B
     fp run = fp_one();
-    for (u32 d = 1; ok && d <= 255; d++) {            // Jacobian entries and the running product of their z
+#pragma unroll 1
+    for (u32 d = d0; ok && d <= d1; d++) {            // Jacobian entries and the running product of their z
         if (jac_is_inf(acc)) { ok = false; break; }
         g1_store_soa(jtab, stride, e0 + d - 1, acc);
         fp_mul(run, run, acc.z);
         soa_store<12>(pre, stride, e0 + d - 1, &run);
-        grp_add(acc, acc, B);
+        jac_add(acc, acc, B);
     }
     ktab_ok[t] = ok;
     if (!ok) return;
     fp inv, beta;
-    fp_inv(inv, run);                                  // 1 / (z_1 ... z_255)
+    fp_inv(inv, run);                                  // 1 / (z_d0 ... z_d1)
     fp_load_const(beta, LCB_G1_BETA);
-    for (u32 d = 255; d >= 1; d--) {
+#pragma unroll 1
+    for (u32 d = d1; d >= d0; d--) {
         g1 p;
         g1_load_soa(p, jtab, stride, e0 + d - 1);
         fp zi, zi2, pd;
-        if (d > 1) {
+        if (d > d0) {
             soa_load<12>(&pd, pre, stride, e0 + d - 2);
             fp_mul(zi, inv, pd);                       // 1 / z_d
             fp_mul(inv, inv, p.z);
@@ -287,8 +293,11 @@ DN void g1_mul_ab_tab(g1 &r, const u32 *tab, u32 n_keys, u32 k, u32 a, u32 b) {
     }
     r = acc;
 }
-DI bool ktab_usable(const uint8_t *ktab_ok, u32 k) {
-    return ktab_ok && (ktab_ok[4 * k] & ktab_ok[4 * k + 1] & ktab_ok[4 * k + 2] & ktab_ok[4 * k + 3]);
+DI bool ktab_usable(const uint8_t *ktab_ok, u32 k) {      // all 32 lanes of the key's table succeeded
+    if (!ktab_ok) return false;
+    const uint4 *f = (const uint4 *)(ktab_ok + (size_t)LCB_KTAB_LANES * k);
+    uint4 x = f[0], y = f[1];
+    return (x.x & x.y & x.z & x.w & y.x & y.y & y.z & y.w) == 0x01010101u;
 }
 
 // ---------------------------------------------------------------- TPKE: per-share randomisation
@@ -712,8 +721,10 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_search(const uint4 *search, u32 o, u
 }
 
 // ---------------------------------------------------------------- host launch wrappers
-// table workspace per key: Jacobian scratch 144 B + prefix products 48 B + table 144 B per entry + 4 flags
-extern "C" size_t lcbk_key_table_bytes(u32 n_keys) { return (size_t)n_keys * (LCB_KTAB_ENTRIES * 336 + 4); }
+// table workspace per key: Jacobian scratch 144 B + prefix products 48 B + table 144 B per entry + 32 flags
+extern "C" size_t lcbk_key_table_bytes(u32 n_keys) {
+    return (size_t)n_keys * (LCB_KTAB_ENTRIES * 336 + LCB_KTAB_LANES) + 16;
+}
 extern "C" void lcbk_rlc_key_tables(dim3 grid, hipStream_t s, const void *keys, u32 n_keys, u32 *ws, u32 **tab,
                                     uint8_t **ktab_ok) {
     const size_t ne = (size_t)n_keys * LCB_KTAB_ENTRIES;
@@ -721,6 +732,7 @@ extern "C" void lcbk_rlc_key_tables(dim3 grid, hipStream_t s, const void *keys, 
     uint8_t *okv = (uint8_t *)(ws + 84 * ne);
     *tab = t;
     *ktab_ok = okv;
+    grid = dim3((LCB_KTAB_LANES * n_keys + LCB_BLOCK - 1) / LCB_BLOCK);
     LCB_LAUNCH(k_rlc_key_tables, (const g1a_st *)keys, n_keys, jtab, pre, t, okv);
 }
 extern "C" void lcbk_tpke_rlc_points(dim3 grid, hipStream_t s, u32 n_cts, const void *keys, u32 n_keys,

@@ -718,14 +718,14 @@ bool rlc_ws(lcb_ctx *c, RlcWs &w, size_t n, size_t rec_a, size_t rec_b) {
     return true;
 }
 // fixed-base tables of the batch's keys (k_rlc_key_tables), when the batch is large enough to repay them
-// (4 x 255 points per key, ~250 additions of latency); nullptr: the points kernel multiplies the keys directly
+// (4 x 255 points per key, 32 lanes per key, ~40 additions of latency); nullptr: the points kernel multiplies the keys directly
 u32 *rlc_key_tables(lcb_ctx *c, const void *keys, size_t n_keys, hipStream_t s, uint8_t **ktab_ok) {
     *ktab_ok = nullptr;
     if (!n_keys || n_keys > 4096 || getenv("LCB_RLC_NO_KEY_TABLES")) return nullptr;
     u32 *ws = (u32 *)c->rlc[12].get(lcbk_key_table_bytes((u32)n_keys));
     if (!ws) return nullptr;
     u32 *tab = nullptr;
-    lcbk_rlc_key_tables(dim3(nblk(4 * n_keys)), s, keys, (u32)n_keys, ws, &tab, ktab_ok);
+    lcbk_rlc_key_tables(dim3(nblk(32 * n_keys)), s, keys, (u32)n_keys, ws, &tab, ktab_ok);
     return tab;
 }
 // phase 1 (needs the decompressed keys only): per-share exponent multiples + level-1 groups (count left on device)
