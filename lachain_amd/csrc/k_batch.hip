@@ -95,38 +95,51 @@ DI void g1_load_soa(g1 &p, const u32 *base, size_t n, size_t i) { soa_load<36>(&
 DI void g2_store_soa(u32 *base, size_t n, size_t i, const g2 &p) { soa_store<72>(base, n, i, &p); }
 DI void g2_load_soa(g2 &p, const u32 *base, size_t n, size_t i) { soa_load<72>(&p, base, n, i); }
 
-// a P + b phi(P) for an affine P: 32 doublings, mixed additions of P and phi(P)
+// a P + b phi(P) for an affine P, phi(x, y) = (beta x, y).  Joint bits: the addend is P (1, 0), phi(P) (0, 1) or
+// P + phi(P) = (beta^2 x, -y) (1, 1; the chord through two points of equal y has slope 0 and 1 + beta + beta^2 = 0),
+// so each bit costs one mixed addition, and a wave (whose lanes' bits differ) executes 32 of them instead of 64.
+DI void g1_ab_addends(fp &bx, fp &b2x, fp &ny, const g1a &P) {
+    fp beta;
+    fp_load_const(beta, LCB_G1_BETA);
+    fp_mul(bx, P.x, beta);
+    fp_mul(b2x, bx, beta);
+    fp_neg(ny, P.y);
+}
 DN void g1_mul_ab_n(g1 &r, const g1a &P, u32 a, u32 b) {
     g1 acc;
     jac_set_inf(acc);
     if (!P.inf) {
-        fp beta, phx;
-        fp_load_const(beta, LCB_G1_BETA);
-        fp_mul(phx, P.x, beta);
+        fp bx, b2x, ny;
+        g1_ab_addends(bx, b2x, ny, P);
         for (int k = 31; k >= 0; k--) {
             grp_dbl(acc, acc);
-            if ((a >> k) & 1) grp_madd(acc, acc, P.x, P.y);
-            if ((b >> k) & 1) grp_madd(acc, acc, phx, P.y);
+            u32 da = (a >> k) & 1, db = (b >> k) & 1;
+            if (da | db) grp_madd(acc, acc, da ? (db ? b2x : P.x) : bx, (da & db) ? ny : P.y);
         }
     }
     r = acc;
 }
-// (a + b lambda) S for S in G2: psi^2 acts on G2 as p^2 = z^2 (mod r), so lambda S = psi^2(S) - S and
-// (a + b lambda) S = (a - b) S + b psi^2(S): 32 doublings, mixed additions of +-S and psi^2(S)
+// (a + b lambda) S for S in G2: psi^2(x, y) = (beta x, -y) acts on G2 as z^2 (mod r) and psi^4(x, y) = (beta^2 x, y)
+// as z^4 = z^2 - 1 = lambda, so (a + b lambda) S = a S + b psi^4(S); the joint addend S + psi^4(S) = psi^2(S) (equal
+// y again): one mixed addition per bit as in G1
+DI void g2_ab_addends(fp2 &x4, fp2 &x2, fp2 &ny, const g2a &S) {
+    fp beta, b2;
+    fp_load_const(beta, LCB_G1_BETA);
+    fp_sqr(b2, beta);
+    fp2_mul_fp(x4, S.x, b2);
+    fp2_mul_fp(x2, S.x, beta);
+    fp2_neg(ny, S.y);
+}
 DN void g2_mul_ab_n(g2 &r, const g2a &S, u32 a, u32 b) {
     g2 acc;
     jac_set_inf(acc);
     if (!S.inf) {
-        g2 J, T;
-        jac_from_aff(J, S);
-        g2_psi2(T, J);                   // z = 1 stays 1: affine
-        fp2 sy = S.y;
-        u32 d = a - b;
-        if (a < b) { d = b - a; fp2_neg(sy, sy); }
+        fp2 x4, x2, ny;
+        g2_ab_addends(x4, x2, ny, S);
         for (int k = 31; k >= 0; k--) {
             grp_dbl(acc, acc);
-            if ((d >> k) & 1) grp_madd(acc, acc, S.x, sy);
-            if ((b >> k) & 1) grp_madd(acc, acc, T.x, T.y);
+            u32 da = (a >> k) & 1, db = (b >> k) & 1;
+            if (da | db) grp_madd(acc, acc, da ? (db ? x2 : S.x) : x4, (da & db) ? ny : S.y);
         }
     }
     r = acc;
@@ -136,34 +149,29 @@ DN void g2_mul_ab_n(g2 &r, const g2a &S, u32 a, u32 b) {
 DI void g1_mul_ab_inl(g1 &r, const g1a &P, u32 a, u32 b) {
     jac_set_inf(r);
     if (P.inf) return;
-    fp beta, phx;
-    fp_load_const(beta, LCB_G1_BETA);
-    fp_mul(phx, P.x, beta);
+    fp bx, b2x, ny;
+    g1_ab_addends(bx, b2x, ny, P);
 #pragma unroll 1
     for (int k = 31; k >= 0; k--) {
         jac_dbl(r, r);
-        if ((a >> k) & 1) jac_add_aff(r, r, P.x, P.y);
-        if ((b >> k) & 1) jac_add_aff(r, r, phx, P.y);
+        u32 da = (a >> k) & 1, db = (b >> k) & 1;
+        if (da | db) jac_add_aff(r, r, da ? (db ? b2x : P.x) : bx, (da & db) ? ny : P.y);
     }
 }
 #ifndef LCB_RLC_POINTS_WAVES
 #define LCB_RLC_POINTS_WAVES 1
 #endif
-// G2 form of g1_mul_ab_inl: (a - b) S + b psi^2(S) with the point arithmetic inlined
+// G2 form of g1_mul_ab_inl: a S + b psi^4(S) with the point arithmetic inlined
 DI void g2_mul_ab_inl(g2 &r, const g2a &S, u32 a, u32 b) {
     jac_set_inf(r);
     if (S.inf) return;
-    g2 J, T;
-    jac_from_aff(J, S);
-    g2_psi2(T, J);
-    fp2 sy = S.y;
-    u32 d = a - b;
-    if (a < b) { d = b - a; fp2_neg(sy, sy); }
+    fp2 x4, x2, ny;
+    g2_ab_addends(x4, x2, ny, S);
 #pragma unroll 1
     for (int k = 31; k >= 0; k--) {
         jac_dbl(r, r);
-        if ((d >> k) & 1) jac_add_aff(r, r, S.x, sy);
-        if ((b >> k) & 1) jac_add_aff(r, r, T.x, T.y);
+        u32 da = (a >> k) & 1, db = (b >> k) & 1;
+        if (da | db) jac_add_aff(r, r, da ? (db ? x2 : S.x) : x4, (da & db) ? ny : S.y);
     }
 }
 // both multiplications in one loop with the point arithmetic inlined (two independent dependency chains per lane, no
