@@ -106,6 +106,85 @@ DI void g2_mul_gls_inl(g2 &r, const g2a &A, const u32 k[8]) {
             if ((d[i] >> b) & 1) jac_add_aff(r, r, Q[i].x, Q[i].y);
     }
 }
+// Affine tables for the lanes below: Jacobian entries t[1..n-1] turned affine with one batched inversion (Montgomery's
+// trick); false when an entry is the point at infinity (small-order inputs), and the caller takes its plain ladder.
+template <class F, int N> DI bool jac_table_to_aff(aff<F> (&ta)[N], jac<F> (&t)[N]) {
+    F pre[N];
+    f_one(pre[0]);
+#pragma unroll 1
+    for (int i = 1; i < N; i++) f_mul(pre[i], pre[i - 1], t[i].z);
+    if (f_is_zero(pre[N - 1])) return false;
+    F inv;
+    f_inv(inv, pre[N - 1]);
+#pragma unroll 1
+    for (int i = N - 1; i >= 1; i--) {
+        F zi, zi2;
+        f_mul(zi, inv, pre[i - 1]);        // 1 / z_i
+        f_mul(inv, inv, t[i].z);
+        f_sqr(zi2, zi);
+        f_mul(ta[i].x, t[i].x, zi2);
+        f_mul(zi2, zi2, zi);
+        f_mul(ta[i].y, t[i].y, zi2);
+        ta[i].inf = false;
+    }
+    return true;
+}
+// k P for any on-curve P with a fixed 4-bit window: 256 doublings and 64 mixed additions of table entries (1..15) P,
+// instead of 256 doublings and 256 additions per wave (some lane of a wave has every bit set).  Integer scalar
+// multiplication throughout, so exact outside the r-torsion too (G1.FromBytes accepts such points).
+DI void g1_mul_win4(g1 &r, const g1a &P, const u32 k[8]) {
+    jac_set_inf(r);
+    if (P.inf) return;
+    g1 t[16];
+    jac_from_aff(t[1], P);
+    jac_dbl(t[2], t[1]);
+#pragma unroll 1
+    for (int i = 3; i < 16; i++) jac_add_aff(t[i], t[i - 1], P.x, P.y);
+    g1a ta[16];
+    if (!jac_table_to_aff(ta, t)) { jac_mul_aff_inl(r, P, k, 256); return; }
+#pragma unroll 1
+    for (int w = 63; w >= 0; w--) {
+        jac_dbl(r, r); jac_dbl(r, r); jac_dbl(r, r); jac_dbl(r, r);
+        u32 nib = (k[w >> 3] >> (4 * (w & 7))) & 15;
+        if (nib) jac_add_aff(r, r, ta[nib].x, ta[nib].y);
+    }
+}
+// GLS in G2 with one addition per digit column: the 15 non-empty sums of Q = {A, -psi A, psi^2 A, -psi^3 A} (index
+// bit i <-> Q_i) in an affine table — Q_2, Q_3 = psi^2(Q_0, Q_1), so 1 + 9 additions and one batched inversion —
+// then 64 doublings and 64 mixed additions instead of 64 doublings and 256 additions per wave.  For A in G2 no entry
+// is infinity (|i0 - i1 z + i2 z^2 - i3 z^3| < r); the plain GLS loop stays as a guard.
+DI void g2_mul_gls_tab(g2 &r, const g2a &A, const u32 k[8]) {
+    jac_set_inf(r);
+    if (A.inf) return;
+    u32 q[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) q[j] = k[j];
+    u64 d[4];
+    u256_divmod_u(q, d[0]);
+    u256_divmod_u(q, d[1]);
+    u256_divmod_u(q, d[2]);
+    d[3] = (u64)q[0] | ((u64)q[1] << 32);
+    g2 t[16];
+    jac_from_aff(t[1], A);
+    g2_psi(t[2], t[1]);
+    fp2_neg(t[2].y, t[2].y);                         // -psi(A), z = 1
+    jac_add_aff(t[3], t[1], t[2].x, t[2].y);
+#pragma unroll 1
+    for (int j = 1; j < 4; j++) g2_psi2(t[4 * j], t[j]);
+#pragma unroll 1
+    for (int j = 4; j < 16; j += 4)
+#pragma unroll 1
+        for (int i = 1; i < 4; i++) jac_add(t[j + i], t[i], t[j]);
+    g2a ta[16];
+    if (!jac_table_to_aff(ta, t)) { g2_mul_gls_inl(r, A, k); return; }
+#pragma unroll 1
+    for (int b = 63; b >= 0; b--) {
+        jac_dbl(r, r);
+        u32 idx = (u32)((d[0] >> b) & 1) | (u32)((d[1] >> b) & 1) << 1 | (u32)((d[2] >> b) & 1) << 2 |
+                  (u32)((d[3] >> b) & 1) << 3;
+        if (idx) jac_add_aff(r, r, ta[idx].x, ta[idx].y);
+    }
+}
 // partial products lambda_i * Y_i for every entry (one lane per entry)
 extern "C" __global__ void LCB_BOUNDS k_g1_mul_lanes(const uint8_t *ys, const fr *lam_raw, u32 n_entries, g1 *out,
                                                     uint8_t *ok_out) {
@@ -119,8 +198,10 @@ extern "C" __global__ void LCB_BOUNDS k_g1_mul_lanes(const uint8_t *ys, const fr
     fr k = lam_raw[i];
 #ifdef LCB_LAG_CALLS
     jac_mul_aff(R, A, k.v, 256);
-#else
+#elif defined(LCB_LAG_NO_TABLES)
     jac_mul_aff_inl(R, A, k.v, 256);
+#else
+    g1_mul_win4(R, A, k.v);
 #endif
     out[i] = R;
     ok_out[i] = ok;
@@ -138,8 +219,11 @@ extern "C" __global__ void LCB_BOUNDS k_g2_mul_lanes(const uint8_t *ys, const fr
 #ifdef LCB_LAG_CALLS
     if (g2_in_subgroup(A)) g2_mul_gls(R, A, k.v);
     else jac_mul_aff(R, A, k.v, 256);
-#else
+#elif defined(LCB_LAG_NO_TABLES)
     if (g2_in_subgroup_inl(A)) g2_mul_gls_inl(R, A, k.v);
+    else jac_mul_aff_inl(R, A, k.v, 256);
+#else
+    if (g2_in_subgroup_inl(A)) g2_mul_gls_tab(R, A, k.v);
     else jac_mul_aff_inl(R, A, k.v, 256);
 #endif
     out[i] = R;
