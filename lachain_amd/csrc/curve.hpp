@@ -195,6 +195,50 @@ template <class F> DI void jac_mul_aff(jac<F> &r, const aff<F> &p, const u32 *k,
     }
     r = acc;
 }
+// Affine tables for the windowed ladders: Jacobian entries t[1..n-1] turned affine with one batched inversion (Montgomery's
+// trick); false when an entry is the point at infinity (small-order inputs), and the caller takes its plain ladder.
+template <class F, int N> DI bool jac_table_to_aff(aff<F> (&ta)[N], jac<F> (&t)[N]) {
+    F pre[N];
+    f_one(pre[0]);
+#pragma unroll 1
+    for (int i = 1; i < N; i++) f_mul(pre[i], pre[i - 1], t[i].z);
+    if (f_is_zero(pre[N - 1])) return false;
+    F inv;
+    f_inv(inv, pre[N - 1]);
+#pragma unroll 1
+    for (int i = N - 1; i >= 1; i--) {
+        F zi, zi2;
+        f_mul(zi, inv, pre[i - 1]);        // 1 / z_i
+        f_mul(inv, inv, t[i].z);
+        f_sqr(zi2, zi);
+        f_mul(ta[i].x, t[i].x, zi2);
+        f_mul(zi2, zi2, zi);
+        f_mul(ta[i].y, t[i].y, zi2);
+        ta[i].inf = false;
+    }
+    return true;
+}
+// k P (k: 8 LE words) for any on-curve P with a fixed 4-bit window: 256 doublings and 64 mixed additions of table
+// entries (1..15) P, instead of 256 doublings and 256 additions per wave (some lane of a wave has every bit set).
+// Integer scalar multiplication throughout, so exact outside the r-torsion too (G1.FromBytes accepts such points);
+// a table entry at infinity (a point of order <= 15) falls back to the binary ladder.
+template <class F> DI void jac_mul_win4(jac<F> &r, const aff<F> &P, const u32 k[8]) {
+    jac_set_inf(r);
+    if (P.inf) return;
+    jac<F> t[16];
+    jac_from_aff(t[1], P);
+    jac_dbl(t[2], t[1]);
+#pragma unroll 1
+    for (int i = 3; i < 16; i++) jac_add_aff(t[i], t[i - 1], P.x, P.y);
+    aff<F> ta[16];
+    if (!jac_table_to_aff(ta, t)) { jac_mul_aff(r, P, k, 256); return; }
+#pragma unroll 1
+    for (int w = 63; w >= 0; w--) {
+        jac_dbl(r, r); jac_dbl(r, r); jac_dbl(r, r); jac_dbl(r, r);
+        u32 nib = (k[w >> 3] >> (4 * (w & 7))) & 15;
+        if (nib) jac_add_aff(r, r, ta[nib].x, ta[nib].y);
+    }
+}
 // k p for a small public k: doublings only from k's top bit (the bucket-reduce offsets are < 2^c)
 template <class F> DI void jac_mul_u64(jac<F> &r, const jac<F> &p, u64 k) {
     if (k == 0) { jac_set_inf(r); return; }

@@ -106,49 +106,6 @@ DI void g2_mul_gls_inl(g2 &r, const g2a &A, const u32 k[8]) {
             if ((d[i] >> b) & 1) jac_add_aff(r, r, Q[i].x, Q[i].y);
     }
 }
-// Affine tables for the lanes below: Jacobian entries t[1..n-1] turned affine with one batched inversion (Montgomery's
-// trick); false when an entry is the point at infinity (small-order inputs), and the caller takes its plain ladder.
-template <class F, int N> DI bool jac_table_to_aff(aff<F> (&ta)[N], jac<F> (&t)[N]) {
-    F pre[N];
-    f_one(pre[0]);
-#pragma unroll 1
-    for (int i = 1; i < N; i++) f_mul(pre[i], pre[i - 1], t[i].z);
-    if (f_is_zero(pre[N - 1])) return false;
-    F inv;
-    f_inv(inv, pre[N - 1]);
-#pragma unroll 1
-    for (int i = N - 1; i >= 1; i--) {
-        F zi, zi2;
-        f_mul(zi, inv, pre[i - 1]);        // 1 / z_i
-        f_mul(inv, inv, t[i].z);
-        f_sqr(zi2, zi);
-        f_mul(ta[i].x, t[i].x, zi2);
-        f_mul(zi2, zi2, zi);
-        f_mul(ta[i].y, t[i].y, zi2);
-        ta[i].inf = false;
-    }
-    return true;
-}
-// k P for any on-curve P with a fixed 4-bit window: 256 doublings and 64 mixed additions of table entries (1..15) P,
-// instead of 256 doublings and 256 additions per wave (some lane of a wave has every bit set).  Integer scalar
-// multiplication throughout, so exact outside the r-torsion too (G1.FromBytes accepts such points).
-DI void g1_mul_win4(g1 &r, const g1a &P, const u32 k[8]) {
-    jac_set_inf(r);
-    if (P.inf) return;
-    g1 t[16];
-    jac_from_aff(t[1], P);
-    jac_dbl(t[2], t[1]);
-#pragma unroll 1
-    for (int i = 3; i < 16; i++) jac_add_aff(t[i], t[i - 1], P.x, P.y);
-    g1a ta[16];
-    if (!jac_table_to_aff(ta, t)) { jac_mul_aff_inl(r, P, k, 256); return; }
-#pragma unroll 1
-    for (int w = 63; w >= 0; w--) {
-        jac_dbl(r, r); jac_dbl(r, r); jac_dbl(r, r); jac_dbl(r, r);
-        u32 nib = (k[w >> 3] >> (4 * (w & 7))) & 15;
-        if (nib) jac_add_aff(r, r, ta[nib].x, ta[nib].y);
-    }
-}
 // GLS in G2 with one addition per digit column: the 15 non-empty sums of Q = {A, -psi A, psi^2 A, -psi^3 A} (index
 // bit i <-> Q_i) in an affine table — Q_2, Q_3 = psi^2(Q_0, Q_1), so 1 + 9 additions and one batched inversion —
 // then 64 doublings and 64 mixed additions instead of 64 doublings and 256 additions per wave.  For A in G2 no entry
@@ -201,7 +158,7 @@ extern "C" __global__ void LCB_BOUNDS k_g1_mul_lanes(const uint8_t *ys, const fr
 #elif defined(LCB_LAG_NO_TABLES)
     jac_mul_aff_inl(R, A, k.v, 256);
 #else
-    g1_mul_win4(R, A, k.v);
+    jac_mul_win4(R, A, k.v);
 #endif
     out[i] = R;
     ok_out[i] = ok;

@@ -18,7 +18,8 @@ extern "C" __global__ void LCB_BOUNDS k_g1_mul(const uint8_t *pts, int use_gen, 
     for (int j = 0; j < 8; j++) k.v[j] = sw[j];
     ok = ok && fr_raw_lt_r(k);
     g1 R;
-    jac_mul_aff(R, A, k.v, 255);
+    k.v[7] &= 0x7fffffffu;                  // 255-bit scalars (k < r is checked above)
+    jac_mul_win4(R, A, k.v);
     g1_compress_jac(out + 48 * (size_t)i, R);
     if (ok_out) ok_out[i] = ok;
 }
@@ -35,7 +36,8 @@ extern "C" __global__ void LCB_BOUNDS k_g2_mul(const uint8_t *pts, int use_gen, 
     for (int j = 0; j < 8; j++) k.v[j] = sw[j];
     ok = ok && fr_raw_lt_r(k);
     g2 R;
-    jac_mul_aff(R, A, k.v, 255);
+    k.v[7] &= 0x7fffffffu;                  // 255-bit scalars (k < r is checked above)
+    jac_mul_win4(R, A, k.v);
     g2_compress_jac(out + 96 * (size_t)i, R);
     if (ok_out) ok_out[i] = ok;
 }
