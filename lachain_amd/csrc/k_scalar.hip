@@ -67,9 +67,10 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_encrypt1(const uint8_t *ybytes, con
     for (int j = 0; j < 8; j++) k.v[j] = sw[j];
     ok = ok && fr_raw_lt_r(k);
     g1 R;
-    jac_mul_aff(R, G, k.v, 255);
+    k.v[7] &= 0x7fffffffu;                  // 255-bit scalars (k < r is checked above)
+    jac_mul_win4(R, G, k.v);
     g1_compress_jac(u_out + 48 * (size_t)i, R);
-    jac_mul_aff(R, Y, k.v, 255);
+    jac_mul_win4(R, Y, k.v);
     g1_compress_jac(t_out + 48 * (size_t)i, R);
     ok_out[i] = ok;
 }

@@ -63,6 +63,14 @@ def test_fp_mul(lib):
     check_contract("lcb_r_fp_mul", lane)
 
 
+def test_fp_sqr(lib):
+    rng = random.Random(11)
+    for a, _ in cases(rng, 40):
+        lane, rd = asm_sim.call(lib, "lcb_r_fp_sqr", {0: a})
+        assert rd(0) == mont(a, a)
+    check_contract("lcb_r_fp_sqr", lane)
+
+
 def test_fp_mul_unreduced_multiplicands(lib):
     # Karatsuba sums reach the multiplier unreduced (< 2p); outputs must still be fully reduced
     rng = random.Random(2)

@@ -97,6 +97,11 @@ def run(routine, lane, routines=None):
             lane.put(ops[0], r & M32); lane.put(ops[1], 1 if r < 0 else 0)
         elif mn == "v_cndmask_b32_e64":
             lane.put(ops[0], g(ops[2]) if lane.getmask(ops[3]) else g(ops[1]))
+        elif mn == "v_alignbit_b32":         # ({S0, S1} >> S2[4:0]) low word
+            r = ((g(ops[1]) << 32) | g(ops[2])) >> (g(ops[3]) & 31)
+            lane.put(ops[0], r & M32)
+        elif mn == "v_lshlrev_b32":
+            lane.put(ops[0], (g(ops[2]) << (g(ops[1]) & 31)) & M32)
         elif mn == "v_mul_lo_u32":
             lane.put(ops[0], (g(ops[1]) * g(ops[2])) & M32)
         elif mn in ("v_mov_b32", "s_mov_b32", "v_accvgpr_read_b32", "v_accvgpr_write_b32"):

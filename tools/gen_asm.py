@@ -19,6 +19,7 @@ because R > 4p.
 
 Routines (label: inputs -> outputs, all 12-limb little-endian Montgomery):
   lcb_r_fp_mul      v[0:11]=a, v[12:23]=b                 -> v[0:11]=a*b
+  lcb_r_fp_sqr      v[0:11]=a                             -> v[0:11]=a^2   (78 products for a*a)
   lcb_r_fp_mul2     v[0:11]=a0, v[12:23]=b0, v[24:35]=a1, v[36:47]=b1 -> v[0:11]=a0*b0, v[24:35]=a1*b1
   lcb_r_fp2_mul     v[0:23]=x, v[24:47]=y                 -> v[0:23]=x*y   (Karatsuba, 3 chains)
   lcb_r_fp2_sqr     v[0:23]=x                             -> v[0:23]=x^2   ((a+b)(a-b), 2ab: 2 chains)
@@ -224,6 +225,67 @@ def r_fp2_mul():
     return a.text(), 132
 
 
+def products_sqr(a, A, F, E, M, acc, pbase):
+    """Montgomery square of A (FIPS as products(), one chain): a^2 = sum_i a_i 2^(32i) W_i with
+    W_i = a_i 2^(32i) + 2 sum_{j>i} a_j 2^(32j), whose limbs are a_i (j = i), F[j] = a_j << 1 (j = i + 1) and
+    E[j] = limb j of 2a = (a_j << 1) | (a_{j-1} >> 31) (j > i + 1; a_11 < 2^29, so no limb 12): 78 products
+    instead of 144 for the a*a half.  F, E are indexed by limb (dicts); the result (< 2p) is written over A."""
+    def ring(k):
+        return (acc, acc + 1, acc + 3) if k % 2 == 0 else (acc + 2, acc + 3, acc + 1)
+
+    a(f"v_mov_b32 v{acc}, 0")
+    a(f"v_mov_b32 v{acc + 1}, 0")
+    sc = f"s[{CARRY[0]}:{CARRY[0] + 1}]"
+    for k in range(2 * N - 1):
+        terms = []
+        for i in range(max(0, k - (N - 1)), k // 2 + 1):
+            j = k - i
+            terms.append(("sq", A[i], A[i] if j == i else (F[j] if j == i + 1 else E[j])))
+        lo = 0 if k < N else k - (N - 1)
+        up = k if k < N else N - 1
+        for i in range(lo, up + 1):
+            if i < k:
+                terms.append(("mp", M[i], pbase + k - i))
+        if k < N:
+            terms.append(("m", M[k], pbase))
+        L, H, C = ring(k)
+        for n_t, (kind, x, y) in enumerate(terms):
+            if kind == "m":
+                a(f"v_mul_lo_u32 v{M[k]}, v{L}, s{S_PINV}")
+            a(f"v_mad_u64_u32 v[{L}:{H}], {sc}, v{x}, v{y}, v[{L}:{H}]")
+            if n_t == 0:
+                a(f"v_addc_co_u32_e64 v{C}, {sc}, 0, 0, {sc}")
+            else:
+                a(f"v_addc_co_u32_e64 v{C}, {sc}, 0, v{C}, {sc}")
+        if k >= N:
+            a(f"v_mov_b32 v{A[k - N]}, v{L}")      # A[k-N]'s last use (as a_i, i <= k - 12 ... ) was column k - 1
+        if k == 2 * N - 2:
+            a(f"v_mov_b32 v{A[N - 1]}, v{H}")
+        else:
+            L2, H2, C2 = ring(k + 1)
+            assert H2 == C
+            a(f"v_mov_b32 v{L2}, v{H}")
+
+
+def r_fp_sqr():
+    a = Asm()
+    a.label("lcb_r_fp_sqr")
+    P_ = 50
+    load_p(a, P_)
+    A = vr(0)
+    F = {j: 11 + j for j in range(1, N)}          # v12..v22
+    E = {j: 21 + j for j in range(2, N)}          # v23..v32
+    M = [33 + j for j in range(N)]                # v33..v44
+    for j in range(1, N):
+        a(f"v_lshlrev_b32 v{F[j]}, 1, v{A[j]}")
+    for j in range(2, N):
+        a(f"v_alignbit_b32 v{E[j]}, v{A[j]}, v{A[j - 1]}, 31")
+    products_sqr(a, A, F, E, M, 46, P_)
+    reduce_once(a, A, M, P_)
+    a("s_setpc_b64 s[30:31]")
+    return a.text(), 62
+
+
 def r_fp2_sqr():
     a = Asm()
     a.label("lcb_r_fp2_sqr")
@@ -415,7 +477,7 @@ def r_fp2_mul_lazy():
     return a.text(), 132
 
 
-ROUTINES = [r_fp_mul, r_fp_mul2, r_fp2_mul, r_fp2_mul_lazy, r_fp2_sqr, r_fp2_mul_fp]
+ROUTINES = [r_fp_mul, r_fp_sqr, r_fp_mul2, r_fp2_mul, r_fp2_mul_lazy, r_fp2_sqr, r_fp2_mul_fp]
 
 
 def clobber_list(nvgpr, keep):
@@ -461,6 +523,14 @@ __device__ __forceinline__ u32x12 lcb_asm_fp_mul(u32x12 a, u32x12 b) {{
         : "+{{v[0:11]}}"(a), "+{{v[12:23]}}"(b)
         :
         : {clobber_list(nv['r_fp_mul'], set(range(24)))});
+    return a;
+}}
+// r = a^2 (78 + 144 products instead of 288)
+__device__ __forceinline__ u32x12 lcb_asm_fp_sqr(u32x12 a) {{
+    asm({call_seq("lcb_r_fp_sqr")}
+        : "+{{v[0:11]}}"(a)
+        :
+        : {clobber_list(nv['r_fp_sqr'], set(range(12)))});
     return a;
 }}
 // (a0*b0, a1*b1)
