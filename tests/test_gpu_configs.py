@@ -270,6 +270,14 @@ def test_lagrange_off_subgroup_inputs(nat):
     ys = [o.g1_mul(G1, d.fr()) for _ in range(4)]
     ys[2] = o.g1_add(ys[2], torsion_g1(d))
     assert nat.lagrange_batch(1, [(xs, ys)])[0] == o.g1_lagrange(xs, ys)
+    # a point of order 3 ((0, -2)): the G1 lanes' 4-bit window table meets infinity (3 P = O), so the lane takes the
+    # binary ladder; alone and beside honest inputs, and plus a subgroup point
+    k3 = bytearray(48)
+    k3[47] |= 0x80
+    k3 = bytes(k3)
+    assert o.g1_valid(k3) and o.g1_mul(k3, o.fr(3)) == bytes(48)
+    for ys in ([k3, ys[0], ys[1], ys[3]], [ys[0], o.g1_add(ys[1], k3), k3, ys[3]]):
+        assert nat.lagrange_batch(1, [(xs, ys)])[0] == o.g1_lagrange(xs, ys)
 
 
 # ---------------------------------------------------------------- configs[3]: MSM at 2^20 and 2^24 points
