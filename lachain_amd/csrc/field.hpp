@@ -354,6 +354,42 @@ DI bool fp2_sqrt(fp2 &y, const fp2 &x) {
     fp_mul(y.b, x.b, t2);
     return true;
 }
+// A square root of x in Fp2 when the caller fixes the sign itself (G2 decompression): two exponentiations instead
+// of fp2_sqrt's four per wave (its second Fp root runs whenever one lane needs it, and it ends in an inversion).
+// With t = sqrt(a^2 + b^2), c = (a + t)/2 and s = c^((p-3)/4): if c is a square, y = (c s, b s / 2) (c s = c^((p+1)/4)
+// and 1/(c s) = s since c s^2 = 1); otherwise d = (a - t)/2 = -b^2/(4c) is one, s^2 = -1/c and y = (b s / 2, -c s).
+// The root may differ in sign from fp2_sqrt's; the result is checked (y^2 == x) before it is returned.
+DI bool fp2_sqrt_any(fp2 &y, const fp2 &x) {
+    if (fp_is_zero(x.b)) return fp2_sqrt(y, x);
+    fp t, c, s, u, inv2, bs;
+    fp_load_const(inv2, LCB_INV2);
+    fp_sqr(t, x.a);
+    fp_sqr(u, x.b);
+    fp_add(t, t, u);
+    if (!fp_sqrt(t, t)) return false;                  // N(x) is a square iff x is
+    fp_add(c, x.a, t);
+    fp_mul(c, c, inv2);
+    fp_pow_const(s, c, LCB_P_MINUS3_DIV4);
+    fp_sqr(u, s);
+    fp_mul(u, u, c);                                   // c^((p-1)/2) = +-1
+    fp_mul(bs, x.b, s);
+    fp_mul(bs, bs, inv2);                              // b s / 2
+    fp cs;
+    fp_mul(cs, c, s);
+    fp2 r;
+    if (fp_eq(u, fp_one())) {
+        r.a = cs;
+        r.b = bs;
+    } else {
+        r.a = bs;
+        fp_neg(r.b, cs);
+    }
+    fp2 chk;
+    fp2_sqr(chk, r);
+    if (!(fp_eq(chk.a, x.a) && fp_eq(chk.b, x.b))) return false;
+    y = r;
+    return true;
+}
 
 // ------------------------------------------------------------------------------------------------ Fp6
 // LCB_FP6_THREE_CHAINS: measured 2 % slower in k_tpke_miller (231 vs 227 ms per 1M shares): the wider operand
