@@ -40,6 +40,10 @@ MAC_PER_FPMUL = 300                      # 12x12 (a*b) + 12x12 (m*p) + 12 (m) 32
 # inversion (C_FP2_INV) + 68 x (1 prefix product + 4 backward products) Fp2 products (3 Fp-mul each).
 C["C_FP2_INV"] = 2 + 463 + 2 + 2                                      # norm, Fp inversion, 2 x (Fp2 x Fp)
 C["C_NORM"] = C["C_FP2_INV"] + 68 * 5 * 3                            # per line set
+# Round 2f: G2 decompression takes its square root with two exponentiations (field.hpp fp2_sqrt_any) instead of the
+# mcl-order root measured above (sqrt of the norm, one or two Fp roots, an inversion): x^3 + b 5, norm 2, two
+# exponentiations 2 x 463 + 1 check, c, u, b s / 2, c s 6, the y^2 == x check 2, parity 1
+C["C_DEC2"] = 5 + 2 + 2 * 463 + 1 + 6 + 2 + 1
 C["C_ML2_NORM2"] = C["C_ML2_EVAL"] - 2 * 68 * 12                     # TPKE: both sets normalised
 C["C_ML2_NORM1"] = C["C_ML2_EVAL"] - 68 * 12                         # TS: message set normalised, share lines on the fly
 W_VERIFY = C["C_DEC1"] + C["C_ML2_NORM2"] + C["C_FE"]                                  # per share
