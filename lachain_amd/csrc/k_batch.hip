@@ -502,6 +502,45 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_rlc_miller(const u32 *lines, c
     gacc[g] = 1;
 }
 
+// Small levels (re-checks, singles): two lanes per group, one Miller pair each.  Below one wave per SIMD a level costs
+// one lane's serial work, and one pair (63 squarings + 68 line products) is shorter than the shared-squaring pair
+// (63 squarings + 136 line products); k_rlc_fpair_mul then forms f_H f_W — the same Fp12 element as
+// k_tpke_rlc_miller's (the Miller function is multiplicative and both use the same lines).
+extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_rlc_miller_split(const u32 *lines, const uint4 *desc,
+                                                                  const g1a_st *gpts, u32 n_groups, u32 *f_soa) {
+    u32 t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 2 * n_groups) return;
+    u32 g = t >> 1, side = t & 1;
+    u32 c = desc[g].z;
+    g1a P;
+    st_to_g1a(P, gpts[2 * (size_t)g + side]);
+    const u32 *ls = lines + (size_t)(2 * c + side) * LCB_LINESET_WORDS;
+    fp12 f;
+    if (P.inf) {
+        f = fp12_one();
+    } else if (lineset_normalised(ls)) {
+        LinesNorm sn{ls};
+        miller1(f, sn, P);
+    } else {
+        g2a Q;
+        lineset_point(Q, ls);
+        LinesOnTheFly so;
+        so.init(Q);
+        miller1(f, so, P);
+    }
+    fp12_store_soa(f_soa + (size_t)side * n_groups * 144, n_groups, g, f);
+}
+extern "C" __global__ void LCB_BOUNDS k_rlc_fpair_mul(u32 *f_soa, u32 n_groups, uint8_t *gacc) {
+    u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_groups) return;
+    fp12 a, b;
+    fp12_load_soa(a, f_soa, n_groups, g);
+    fp12_load_soa(b, f_soa + (size_t)n_groups * 144, n_groups, g);
+    fp12_mul(a, a, b);
+    fp12_store_soa(f_soa, n_groups, g, a);
+    gacc[g] = 1;
+}
+
 // ---------------------------------------------------------------- threshold signatures (ValidateSignature)
 // e(PK_i, H(m)) == e(G, sig_i) <=> e(PK_i, H) e(-G, sig_i) == 1.  The randomisation of sig_i uses linearity of the
 // pairing in its G2 argument, which holds on G2: a share whose sig_i is outside G2 (G2.FromBytes does not check) is
@@ -787,6 +826,13 @@ extern "C" void lcbk_tpke_ct_g2check(dim3 grid, hipStream_t s, const u32 *lines,
 extern "C" void lcbk_tpke_rlc_miller(dim3 grid, hipStream_t s, const u32 *lines, const void *desc, const void *gpts,
                                      u32 n_groups, u32 *f_soa, uint8_t *gacc) {
     LCB_LAUNCH(k_tpke_rlc_miller, lines, (const uint4 *)desc, (const g1a_st *)gpts, n_groups, f_soa, gacc);
+}
+extern "C" void lcbk_tpke_rlc_miller_split(hipStream_t s, const u32 *lines, const void *desc, const void *gpts,
+                                           u32 n_groups, u32 *f_soa, uint8_t *gacc) {
+    dim3 grid((2 * n_groups + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_tpke_rlc_miller_split, lines, (const uint4 *)desc, (const g1a_st *)gpts, n_groups, f_soa);
+    grid = dim3((n_groups + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_rlc_fpair_mul, f_soa, n_groups, gacc);
 }
 extern "C" void lcbk_ts_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 first,
                                 const uint8_t *msg_ok, const void *pks, u32 n_pks, const u32 *pk_idx,

@@ -773,6 +773,13 @@ int rlc_g2check(lcb_ctx *c, hipStream_t s) {
                              (u32)c->t_n_cts, ctg2);
     return 0;
 }
+// levels of at most 32,768 groups (under one wave per SIMD as two lanes per group) run their TPKE Miller loops as two
+// single pairs per group (k_tpke_rlc_miller_split; measured 130.0 -> 123.3 ms per 1M-share batched step) unless
+// LCB_RLC_SPLIT=0
+static bool rlc_split_levels() {
+    static const bool on = [] { const char *e = getenv("LCB_RLC_SPLIT"); return !(e && e[0] == '0'); }();
+    return on;
+}
 struct RlcIo {                     // the per-share inputs the exact singles re-read
     const uint32_t *d_key;         // dec_idx (TPKE) / pk_idx (TS)
     const uint8_t *d_pts;          // ui (TPKE) / sigs (TS)
@@ -801,6 +808,9 @@ int rlc_levels(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, size_t n, 
             if (ts)
                 lcbk_ts_rlc_miller(dim3(nblk(m)), s, lines, desc + 16 * o, (const uint8_t *)gpts + rec * o, (u32)m, f,
                                    gacc + o);
+            else if (2 * m <= 65536 && rlc_split_levels())   // under one wave per SIMD: one Miller pair per lane
+                lcbk_tpke_rlc_miller_split(s, lines, desc + 16 * o, (const uint8_t *)gpts + rec * o, (u32)m, f,
+                                           gacc + o);
             else
                 lcbk_tpke_rlc_miller(dim3(nblk(m)), s, lines, desc + 16 * o, (const uint8_t *)gpts + rec * o, (u32)m, f,
                                      gacc + o);
