@@ -149,7 +149,136 @@ def make_inputs(nat, rank, n_shares, n_dec, f, vlen, corrupt_frac=0.01):
     v_off = np.arange(0, vlen * (n_cts + 1), vlen, dtype=np.uint32)
     return dict(y_keys=b"".join(y_keys), u=b"".join(us), w=b"".join(ws), v=b"".join(vs), v_off=v_off,
                 ct_idx=ct_idx, dec_idx=dec_idx, ui=ui, expect=expect, n_cts=n_cts, n_dec=n_dec,
-                keys_list=y_keys, cts_list=list(zip(us, vs, ws)))
+                keys_list=y_keys, cts_list=list(zip(us, vs, ws)), scal=bytes(scal))
+
+
+# Byzantine patterns of the reference's own tests: a faulty validator corrupts its share in EVERY ciphertext
+# (HoneyBadgerMalicious.cs:17-23 reverses the share bytes; validator 0 is the faulty one, HoneyBadgerTest.cs:75-94;
+# HoneyBadgerSmartMalicious.cs:28-48 sends valid points that are not the share -> "wrong": U_i + G).
+def byzantine_patterns(f):
+    return {
+        "random_1pct": None,                                   # the headline's pattern (make_inputs)
+        "one_validator_reversed": ([0], "reversed"),
+        "f_validators_reversed": (list(range(f)), "reversed"),
+        "one_validator_wrong": ([0], "wrong"),
+        "f_validators_wrong": (list(range(f)), "wrong"),
+        "all_wrong": (None, "wrong"),
+    }
+
+
+def pattern_inputs(nat, inp, spec):
+    """ui bytes and expected decisions of one pattern, from the batch's share scalars (wrong = scalar + 1)"""
+    n = len(inp["expect"])
+    if spec is None:
+        return inp["ui"], inp["expect"]
+    faulty, kind = spec
+    scal = np.frombuffer(inp["scal"], dtype=np.uint8).reshape(n, 32)
+    bad_scal = scal.copy()
+    # the batch's 1 % corrupted shares carry scalar + 1: restore every share's good scalar first
+    bad_idx = np.nonzero(inp["expect"] == 0)[0]
+    good_scal = scal.copy()
+    for i in bad_idx:
+        v = (int.from_bytes(scal[i].tobytes(), "little") - 1) % R
+        good_scal[i] = np.frombuffer(v.to_bytes(32, "little"), dtype=np.uint8)
+    if "good_ui" not in inp:
+        inp["good_ui"] = nat.mul_batch_raw(1, b"", good_scal.tobytes(), n, generator=True)
+    ui = np.frombuffer(inp["good_ui"], dtype=np.uint8).reshape(n, 48).copy()
+    sel = np.ones(n, dtype=bool) if faulty is None else np.isin(inp["dec_idx"], np.asarray(faulty, dtype=np.uint32))
+    idx = np.nonzero(sel)[0]
+    if kind == "reversed":
+        ui[idx] = ui[idx, ::-1]
+    else:
+        for i in idx:
+            v = (int.from_bytes(good_scal[i].tobytes(), "little") + 1) % R
+            bad_scal[i] = np.frombuffer(v.to_bytes(32, "little"), dtype=np.uint8)
+        ui[idx] = np.frombuffer(nat.mul_batch_raw(1, b"", bad_scal[idx].tobytes(), len(idx), generator=True),
+                                dtype=np.uint8).reshape(len(idx), 48)
+    expect = (~sel).astype(np.uint8)
+    return ui.tobytes(), expect
+
+
+def run_tpke_patterns(args, nat, torch, dev, world, inp, n, n_cts, n_dec):
+    """The batched path (headline API) and the exact path on every Byzantine pattern of the reference's tests, same
+    batch and timing discipline as the headline; decisions compared with the construction and with each other."""
+    import torch.distributed as dist
+    lib = nat.lib()
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    py, nk, pu, pw, pv, pvo, nc = PREP_ARGS[0]
+    d_ct = to_dev(torch, dev, inp["ct_idx"])
+    d_dec = to_dev(torch, dev, inp["dec_idx"])
+    d_acc = torch.zeros(n, dtype=torch.uint8, device=dev)
+    ctx = nat.Context()
+    out = {}
+    for name, spec in byzantine_patterns(args.f).items():
+        if args.patterns and name not in args.patterns.split(","):
+            continue
+        ui_b, expect = pattern_inputs(nat, inp, spec)
+        d_ui = to_dev(torch, dev, ui_b)
+
+        def batched():
+            rc = lib.lcb_ctx_tpke_verify_shares_batched_dev(ctx.ptr, d_acc.data_ptr(), n, py, nk, pu, pw, pv, pvo, nc,
+                                                            d_ct.data_ptr(), d_dec.data_ptr(), d_ui.data_ptr(), sh)
+            if rc != 0:
+                raise RuntimeError(nat.last_error())
+
+        def exact():
+            rc = lib.lcb_ctx_tpke_prepare_dev(ctx.ptr, py, nk, pu, pw, pv, pvo, nc, sh)
+            rc |= lib.lcb_ctx_tpke_verify_prepared_dev(ctx.ptr, d_acc.data_ptr(), n, nk, nc, d_ct.data_ptr(),
+                                                       d_dec.data_ptr(), d_ui.data_ptr(), sh)
+            if rc != 0:
+                raise RuntimeError(nat.last_error())
+
+        rec = {}
+        got = {}
+        for label, fn in (("batched", batched), ("exact", exact)):
+            for _ in range(max(1, args.warmup)):
+                fn()
+            torch.cuda.synchronize(dev)
+            got[label] = d_acc.cpu().numpy().copy()
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for _ in range(args.pattern_steps):
+                fn()
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            el = time.perf_counter() - t0
+            mism = int(np.sum(got[label] != expect)) + int(np.sum(d_acc.cpu().numpy() != expect))
+            t = torch.tensor([el, float(mism)], dtype=torch.float64, device=dev)
+            if world > 1:
+                tm = t.clone()
+                dist.all_reduce(tm[:1], op=dist.ReduceOp.MAX)
+                dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+                t[0] = tm[0]
+            rec[label] = {"value": world * n * args.pattern_steps / float(t[0]),
+                          "ms_per_step": 1e3 * float(t[0]) / args.pattern_steps, "decision_mismatches": int(t[1])}
+            if label == "batched":
+                lv = (ctypes.c_uint32 * 8)()
+                m6 = (ctypes.c_float * 6)()
+                k = lib.lcb_ctx_tpke_batched_stats(ctx.ptr, lv, m6)
+                cs = (ctypes.c_uint32 * 4)()
+                lib.lcb_ctx_batched_census(ctx.ptr, cs)
+                rec[label]["levels"] = list(lv[:k])
+                rec[label]["census"] = {"shares": cs[0], "suspect_keys": cs[1], "level1_groups": cs[2],
+                                        "level1_entries_after_split": cs[3]}
+        rec["rejected_shares"] = int(n - expect.sum())
+        rec["batched_over_exact"] = rec["batched"]["value"] / rec["exact"]["value"]
+        rec["batched_vs_exact_decisions_equal"] = bool(np.array_equal(got["batched"], got["exact"]))
+        out[name] = rec
+        del d_ui
+    ctx.close()
+    worst = min(out.values(), key=lambda r: r["batched_over_exact"]) if out else None
+    return {"patterns": out,
+            "worst_batched_over_exact": worst["batched_over_exact"] if worst else None,
+            "note": ("reversed = the share's 48 bytes reversed (HoneyBadgerMalicious.cs:23; most do not decode and are "
+                     "rejected without a pairing), wrong = a valid point that is not the share (U_i + G); faulty "
+                     "validators 0..k-1 corrupt their share in every ciphertext; batched = "
+                     "lcb_ctx_tpke_verify_shares_batched_dev (census of suspect keys + randomized group checks), "
+                     "exact = lcb_ctx_tpke_prepare_dev + lcb_ctx_tpke_verify_prepared_dev; "
+                     f"{args.pattern_steps} timed steps after {max(1, args.warmup)} warmup per path")}
 
 
 def to_dev(torch, dev, b):
@@ -395,6 +524,7 @@ def ts_inputs(nat, rank, rounds, n, f):
     pts = np.repeat(hs, n, axis=0).tobytes()
     sk_arr = np.frombuffer(b"".join(fr(x) for x in sks), dtype=np.uint8).reshape(n, 32)
     sigs = bytearray(nat.mul_batch_raw(2, pts, np.tile(sk_arr, (rounds, 1)).tobytes(), rounds * n))
+    good_sigs = bytes(sigs)
     # corrupt one share per round (1 %): share j of round r carries the signature of share j+1 (valid point,
     # wrong key); j = 7r mod n, so a third of the rounds lose one of their first F+1 shares
     expect = np.ones(rounds * n, dtype=np.uint8)
@@ -407,7 +537,7 @@ def ts_inputs(nat, rank, rounds, n, f):
     pidx = np.tile(np.arange(n, dtype=np.uint32), rounds)
     moff = np.arange(0, 24 * (rounds + 1), 24, dtype=np.uint32)
     return dict(pks=b"".join(pks), msgs=b"".join(msgs), moff=moff, sigs=bytes(sigs), midx=midx, pidx=pidx,
-                expect=expect, shared_sk=shared_sk, msg_list=msgs)
+                expect=expect, shared_sk=shared_sk, msg_list=msgs, good_sigs=good_sigs)
 
 
 def ts_cpu_baseline(inp, n_total, n_per_round, target_s=10.0, batched=False):
@@ -568,6 +698,66 @@ def run_ts(args, nat, torch, dev, rank, world):
 
     bat = run(True) if args.ts_batched else None
     exact = run(False) if args.ts_exact else None
+
+    def patterns():
+        """faulty signers send a wrong share (the next signer's signature: a valid point) in EVERY round; the share
+        checks alone (batched call vs exact prepare + verify), same rounds"""
+        res = {}
+        good = np.frombuffer(inp["good_sigs"], dtype=np.uint8).reshape(rounds, n, 96)
+        for name, faulty in (("one_signer_wrong", [0]), ("f_signers_wrong", list(range(f)))):
+            sg = good.copy()
+            for j in faulty:
+                sg[:, j] = good[:, (j + 1) % n] if (j + 1) % n not in faulty else good[:, (faulty[-1] + 1) % n]
+            exp = np.ones((rounds, n), dtype=np.uint8)
+            exp[:, faulty] = 0
+            exp = exp.reshape(-1)
+            d_sg = to_dev(torch, dev, sg.tobytes())
+            rec = {}
+            for label in ("batched", "exact"):
+                def call():
+                    if label == "batched":
+                        rc = lib.lcb_ts_verify_shares_batched_dev(d_acc.data_ptr(), rounds * n, d_pks.data_ptr(),
+                                                                  n + 1, d_sg.data_ptr(), d_msg.data_ptr(),
+                                                                  d_moff.data_ptr(), rounds, d_midx.data_ptr(),
+                                                                  d_pidx.data_ptr(), sh)
+                    else:
+                        rc = lib.lcb_ts_prepare_dev(d_pks.data_ptr(), n + 1, d_msg.data_ptr(), d_moff.data_ptr(),
+                                                    rounds, sh)
+                        rc |= lib.lcb_ts_verify_prepared_dev(d_acc.data_ptr(), rounds * n, n + 1, rounds,
+                                                             d_sg.data_ptr(), d_midx.data_ptr(), d_pidx.data_ptr(), sh)
+                    if rc != 0:
+                        raise RuntimeError(nat.last_error())
+                call()
+                torch.cuda.synchronize(dev)
+                mism = int(np.sum(d_acc.cpu().numpy() != exp))
+                if world > 1:
+                    dist.barrier()
+                t0 = time.perf_counter()
+                call()
+                torch.cuda.synchronize(dev)
+                if world > 1:
+                    dist.barrier()
+                el = time.perf_counter() - t0
+                mism += int(np.sum(d_acc.cpu().numpy() != exp))
+                t = torch.tensor([el, float(mism)], dtype=torch.float64, device=dev)
+                if world > 1:
+                    tm = t[:1].clone()
+                    dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+                    dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+                    t[0] = tm[0]
+                rec[label] = {"value": rounds * n * world / float(t[0]), "ms_per_step": 1e3 * float(t[0]),
+                              "decision_mismatches": int(t[1])}
+                if label == "batched":
+                    rec[label]["levels"] = nat.tpke_batched_stats()[0]
+                    cs = nat.batched_census()
+                    rec[label]["census"] = {"shares": cs[0], "suspect_keys": cs[1], "level1_groups": cs[2],
+                                            "level1_entries_after_split": cs[3]}
+            rec["batched_over_exact"] = rec["batched"]["value"] / rec["exact"]["value"]
+            res[name] = rec
+            del d_sg
+        return res
+
+    byz = patterns() if (args.pattern_steps > 0 and args.ts_batched and args.ts_exact) else None
     if rank != 0:
         return None
     head = bat or exact
@@ -584,6 +774,7 @@ def run_ts(args, nat, torch, dev, rank, world):
     res.update(head)
     if bat and exact:
         res["exact"] = exact
+    res["byzantine"] = byz
     if world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = ts_cpu_baseline(inp, rounds * n, n, batched=bat is not None)
     return res
@@ -1204,6 +1395,9 @@ def main():
     ap.add_argument("--headline", choices=("batched", "exact"), default="batched",
                     help="which TPKE path the line's value / roofline / cpu_baseline describe")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--pattern-steps", type=int, default=2,
+                    help="timed steps per Byzantine pattern and path (0 = skip the patterns)")
+    ap.add_argument("--patterns", default="", help="comma-separated subset of the Byzantine patterns (default all)")
     ap.add_argument("--msm-sizes", default=f"{1 << 20},{1 << 24}",
                     help="total G1 MSM points per measurement, sharded over ranks (empty = skip)")
     ap.add_argument("--msm-steps", type=int, default=3)
@@ -1326,6 +1520,9 @@ def main():
     batched = None
     if args.tpke_batched:
         batched = run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, (d_ct, d_dec, d_ui), n, n_cts, n_dec, sh)
+    byz = None
+    if args.pattern_steps > 0:
+        byz = run_tpke_patterns(args, nat, torch, dev, world, inp, n, n_cts, n_dec)
     head = batched if (args.headline == "batched" and batched) else exact
     if head is None:
         raise SystemExit("nothing to report: --tpke-exact 0 and --tpke-batched 0")
@@ -1399,6 +1596,7 @@ def main():
             "cpu_baseline": cpu_line,
             "tpke_batched": batched if head is batched else None,
             "tpke_exact": exact,
+            "tpke_byzantine": byz,
             "input_gen_s": t_gen,
             "msm": msm,
             "threshold_signature": ts,

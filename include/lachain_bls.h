@@ -274,8 +274,27 @@ int lcb_ts_verify_shares_batched(uint8_t *accept, size_t n, const uint8_t *pks, 
    ms of [randomisation + grouping, all levels, then summed over the levels: group sums, group Miller loops, final
    exponentiations (+ resolve / search), 0]; returns the number of levels (waits for the call) */
 int lcb_tpke_batched_stats(uint32_t levels[8], float ms[6]);
-/* test hook: fixed 32-byte ChaCha20 key for the batch exponents (NULL restores getrandom) */
+/* test hook: fixed 32-byte ChaCha20 key for the batch exponents (NULL restores getrandom).  Honoured only when the
+   environment has LCB_ALLOW_FIXED_BATCH_SEED=1 (a fixed key makes the exponents predictable); ignored otherwise. */
 void lcb_set_batch_seed(const uint8_t *seed32);
+/* Byzantine validators (HoneyBadgerMalicious.cs:17-23 corrupts the share a faulty validator sends in EVERY
+   ciphertext): batched calls of at least min_shares shares (default 16384; 0 = never) first check a prefix of the
+   batch (512..2048 shares, at most a quarter) share by share — the census — and mark a key suspect when at least half
+   of its sampled, decodable shares failed; every share of a suspect key is then checked on its own and the groups are
+   summed over the other keys.  Decisions are unchanged; only the cost changes. */
+void lcb_set_batch_census(size_t min_shares);
+/* census of the last batched verify: {census shares, suspect keys, level-1 groups, level-1 entries after moving the
+   suspect keys' shares to single checks} (lcb_ctx_ form: that context's last one) */
+int lcb_batched_census(uint32_t out[4]);
+/* TPKE levels of at most max_groups groups run their Miller loops as two single pairs per group (one pair per lane;
+   default 32768), larger ones as the shared-squaring pair (test hook to cover both kernels) */
+void lcb_set_rlc_split_max(uint32_t max_groups);
+/* levels of at most max_checks group checks run on the cooperative kernels (k_coop.hip: nine lanes per pairing check,
+   lower latency below one wave per SIMD); 0 = always one check per lane.  Default 32768. */
+void lcb_set_coop_max(uint32_t max_checks);
+/* test hook: final exponentiation of n Fp12 values (144 x u32 each, Montgomery form, field.hpp layout) by the one-lane
+   (coop = 0) or the cooperative (coop = 1) kernel */
+int lcb_debug_final_exp(const uint32_t *in, size_t n, uint32_t *out, int coop);
 
 /* ------------------------------------------------------------------ explicit execution contexts
    A context owns the device workspaces of the prepare/verify, assembly, Lagrange and MSM calls below
@@ -305,6 +324,7 @@ int lcb_ctx_tpke_verify_shares_batched_dev(lcb_ctx *ctx, uint8_t *accept, size_t
                                            const uint32_t *ct_idx, const uint32_t *dec_idx, const uint8_t *ui,
                                            void *stream);
 int lcb_ctx_tpke_batched_stats(lcb_ctx *ctx, uint32_t levels[8], float ms[6]);
+int lcb_ctx_batched_census(lcb_ctx *ctx, uint32_t out[4]);
 int lcb_ctx_ts_verify_prepared_batched_dev(lcb_ctx *ctx, uint8_t *accept, size_t n, size_t n_pks, size_t n_msgs,
                                            const uint8_t *sigs, const uint32_t *msg_idx, const uint32_t *pk_idx,
                                            void *stream);

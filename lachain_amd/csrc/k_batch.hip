@@ -39,6 +39,23 @@ struct rlc_key { u32 k[8]; u32 nonce[2]; };   // ChaCha20 key (256 bit, from get
 
 #define LCB_RLC_SINGLES 8       // a failed group this short (below level 1) splits into single shares
 
+// ---------------------------------------------------------------- suspect keys (Byzantine validators)
+// A faulty validator corrupts its share in EVERY ciphertext / coin (HoneyBadgerMalicious.cs:17-23 reverses each
+// share it sends; HoneyBadgerSmartMalicious.cs:28-48 sends valid off-subgroup points), so with F of them every group
+// carries F bad shares and every group check fails.  The census (exact single checks of a prefix of the batch, before
+// the groups are formed) marks a key suspect when at least half of its sampled shares that decoded failed their exact
+// check; every share of a suspect key is then checked on its own and the groups are summed over the other keys only.
+// The bitmap only changes the cost: every decision is still an exact single check or a group check.
+DI bool key_suspect(const u32 *susp, u32 k, u32 n_keys) {
+    return susp && k < n_keys && ((susp[k >> 5] >> (k & 31)) & 1u);
+}
+// the same read while the census may still be writing the bitmap (k_*_rlc_points runs beside it on the other
+// stream): a stale 0 only costs a randomisation that is not used
+DI bool key_suspect_live(const u32 *susp, u32 k, u32 n_keys) {
+    if (!susp || k >= n_keys) return false;
+    return (__atomic_load_n(susp + (k >> 5), __ATOMIC_RELAXED) >> (k & 31)) & 1u;
+}
+
 // ---------------------------------------------------------------- ChaCha20 (RFC 8439 block function)
 DI u32 rotl32(u32 x, int r) { return (x << r) | (x >> (32 - r)); }
 #define CHACHA_QR(a, b, c, d)                  \
@@ -130,20 +147,6 @@ DI void g2_ab_addends(fp2 &x4, fp2 &x2, fp2 &ny, const g2a &S) {
     fp2_mul_fp(x2, S.x, beta);
     fp2_neg(ny, S.y);
 }
-DN void g2_mul_ab_n(g2 &r, const g2a &S, u32 a, u32 b) {
-    g2 acc;
-    jac_set_inf(acc);
-    if (!S.inf) {
-        fp2 x4, x2, ny;
-        g2_ab_addends(x4, x2, ny, S);
-        for (int k = 31; k >= 0; k--) {
-            grp_dbl(acc, acc);
-            u32 da = (a >> k) & 1, db = (b >> k) & 1;
-            if (da | db) grp_madd(acc, acc, da ? (db ? x2 : S.x) : x4, (da & db) ? ny : S.y);
-        }
-    }
-    r = acc;
-}
 // the same with the point arithmetic inlined (no call frames: the DN form passes the accumulator through scratch at
 // every doubling / addition)
 DI void g1_mul_ab_inl(g1 &r, const g1a &P, u32 a, u32 b) {
@@ -173,32 +176,6 @@ DI void g2_mul_ab_inl(g2 &r, const g2a &S, u32 a, u32 b) {
         u32 da = (a >> k) & 1, db = (b >> k) & 1;
         if (da | db) jac_add_aff(r, r, da ? (db ? x2 : S.x) : x4, (da & db) ? ny : S.y);
     }
-}
-// both multiplications in one loop with the point arithmetic inlined (two independent dependency chains per lane, no
-// call frames): a U + b phi(U) and a Y + b phi(Y).  Opt-in (LCB_RLC_JOINT): measured slower than the two calls to
-// g1_mul_ab_n (randomisation 77.7 vs 63.5 ms per 1M shares): 290 VGPRs allow one wave per SIMD instead of two.
-DI void g1_mul_ab2(g1 &ru, g1 &ry, const g1a &U, const g1a &Y, u32 a, u32 b) {
-    fp beta, pux, pyx;
-    fp_load_const(beta, LCB_G1_BETA);
-    fp_mul(pux, U.x, beta);
-    fp_mul(pyx, Y.x, beta);
-    jac_set_inf(ru);
-    jac_set_inf(ry);
-#pragma unroll 1
-    for (int k = 31; k >= 0; k--) {
-        jac_dbl(ru, ru);
-        jac_dbl(ry, ry);
-        if ((a >> k) & 1) {
-            jac_add_aff(ru, ru, U.x, U.y);
-            jac_add_aff(ry, ry, Y.x, Y.y);
-        }
-        if ((b >> k) & 1) {
-            jac_add_aff(ru, ru, pux, U.y);
-            jac_add_aff(ry, ry, pyx, Y.y);
-        }
-    }
-    if (U.inf) jac_set_inf(ru);
-    if (Y.inf) jac_set_inf(ry);
 }
 // affine records of Jacobian points (inf = 1 for the point at infinity), optionally negated
 DI void g1_to_st(g1a_st &o, const g1 &p, bool neg) {
@@ -311,12 +288,14 @@ DI bool ktab_usable(const uint8_t *ktab_ok, u32 k) {      // all 32 lanes of the
 // ---------------------------------------------------------------- TPKE: per-share randomisation
 // validity as k_tpke_miller except the ciphertext's (applied per group by k_tpke_rlc_sum, so this kernel needs only
 // the decompressed keys and may run beside the ciphertext preparation)
+// Shares [i0, n) (the census decides [0, i0) exactly); a share of a key the census has already marked suspect only
+// gets its validity (it is checked on its own).
 extern "C" __global__ void __launch_bounds__(LCB_BLOCK) __attribute__((amdgpu_waves_per_eu(LCB_RLC_POINTS_WAVES)))
 k_tpke_rlc_points(u32 n_cts, const g1a_st *keys, u32 n_keys, const u32 *ct_idx,
-                                                       const u32 *dec_idx, const uint8_t *ui, u32 n, rlc_key key,
-                                                       u32 *rU, u32 *rY, uint8_t *accept, const u32 *ktab,
-                                                       const uint8_t *ktab_ok) {
-    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+                                                       const u32 *dec_idx, const uint8_t *ui, u32 i0, u32 n,
+                                                       rlc_key key, u32 *rU, u32 *rY, uint8_t *accept,
+                                                       const u32 *ktab, const uint8_t *ktab_ok, const u32 *susp) {
+    u32 i = i0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u32 c = ct_idx[i], d = dec_idx[i];
     bool ok = d < n_keys && c < n_cts;
@@ -326,25 +305,15 @@ k_tpke_rlc_points(u32 n_cts, const g1a_st *keys, u32 n_keys, const u32 *ct_idx,
     ok = ok && ks.ok;
     st_to_g1a(Y, ks);
     g1 p, q;
-    if (ok) {
+    if (ok && !key_suspect_live(susp, d, n_keys)) {
         u32 a, b;
         rlc_scalar(key, i, a, b);
-#ifdef LCB_RLC_JOINT
-        g1_mul_ab2(p, q, Ui, Y, a, b);
-#else
-#ifdef LCB_RLC_CALLS
-        g1_mul_ab_n(p, Ui, a, b);        // measured 148.8 vs 144.7 ms per 1M-share batched step (inline, default)
-#else
+        // share side inlined (measured 144.7 vs 148.8 ms per 1M-share step with the call), key side from the key's
+        // fixed-base table (148.8 vs 159.8 ms without)
         g1_mul_ab_inl(p, Ui, a, b);
-#endif
-#ifdef LCB_RLC_NO_TABLE_CODE              // measured 159.8 vs 148.8 ms per step (tables, default)
-        g1_mul_ab_n(q, Y, a, b);
-#else
         if (ktab_usable(ktab_ok, d)) g1_mul_ab_tab(q, ktab, n_keys, d, a, b);
         else g1_mul_ab_n(q, Y, a, b);
-#endif
-#endif
-    } else {                             // an invalid share is rejected and contributes nothing to its group
+    } else {                             // an invalid (or suspect) share contributes nothing to its group
         jac_set_inf(p);
         jac_set_inf(q);
     }
@@ -356,13 +325,13 @@ k_tpke_rlc_points(u32 n_cts, const g1a_st *keys, u32 n_keys, const u32 *ct_idx,
 // ---------------------------------------------------------------- level-1 groups: runs of one ciphertext / message
 // one lane per share; the first share of a run emits the run as groups of at most `cap` shares.
 // desc = {first share, length, ciphertext / message, 0}; order of the records is irrelevant
-extern "C" __global__ void LCB_BOUNDS k_rlc_groups(const u32 *key_idx, u32 n, u32 n_keys, u32 cap, uint4 *desc,
-                                                  u32 *count) {
-    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+extern "C" __global__ void LCB_BOUNDS k_rlc_groups(const u32 *key_idx, u32 i0, u32 n, u32 n_keys, u32 cap,
+                                                  uint4 *desc, u32 *count) {
+    u32 i = i0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u32 c = key_idx[i];
     c = c < n_keys ? c : 0;
-    if (i > 0) {
+    if (i > i0) {
         u32 p = key_idx[i - 1];
         p = p < n_keys ? p : 0;
         if (p == c) return;
@@ -389,26 +358,33 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_groups(const u32 *key_idx, u32 n, u3
 // infinity (they pass).  desc.w = 1: the exact single check of share desc.x, e(U_i, H) e(-Y_i, W) == 1 as
 // k_tpke_miller does it (a share already rejected checks infinity).
 // first != 0 (level 1): also the weighted sums sum (j+1) s_j U_j, sum (j+1) s_j Y_j (j = position in the group) into
-// wsum (Jacobian SoA, stride n_groups) for the level-2 search.
+// wsum (Jacobian SoA, stride n_groups) for the level-2 search.  Shares of suspect keys are skipped (they have singles of
+// their own); they keep their positions, so the weights stay c_j = j + 1.  A single re-derives the share's whole
+// validity (census singles have had none yet): a share that is not live is rejected, and cval (census only) records
+// which shares were live.
 extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_groups, u32 first, const uint8_t *ct_ok,
                                                     const uint8_t *ct_g2, const g1a_st *keys, u32 n_keys,
                                                     const u32 *dec_idx, const uint8_t *ui, const u32 *rU,
                                                     const u32 *rY, u32 n, g1a_st *gpts, uint8_t *accept,
-                                                    uint8_t *gexact, u32 *wsum) {
+                                                    uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval) {
     u32 g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n_groups) return;
     uint4 dsc = desc[g];
     g1a_st o;
     g1_inf_st(o);
     gexact[g] = 0;
-    if (dsc.w == 1) {                    // exact single
+    if (dsc.w == 1) {                    // exact single of share dsc.x of ciphertext dsc.z
         g1a U, Y;
-        bool live = accept[dsc.x] != 0;
+        U.inf = Y.inf = true;
+        u32 d = dec_idx[dsc.x];
+        bool live = accept[dsc.x] != 0 && d < n_keys && ct_ok[dsc.z];
         if (live) {
-            u32 d = dec_idx[dsc.x];
-            live = g1_decompress(U, ui + 48 * (size_t)dsc.x) && d < n_keys;
-            st_to_g1a(Y, keys[d < n_keys ? d : 0]);
+            g1a_st ks = keys[d];
+            live = ks.ok && g1_decompress(U, ui + 48 * (size_t)dsc.x);
+            st_to_g1a(Y, ks);
         }
+        if (!live) accept[dsc.x] = 0;
+        if (cval) cval[dsc.x] = live;
         if (live && !U.inf) { o.x = U.x; o.y = U.y; o.inf = 0; }
         gpts[2 * (size_t)g] = o;
         g1_inf_st(o);
@@ -432,10 +408,12 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_gr
     jac_set_inf(wu);
     jac_set_inf(wy);
     for (u32 j = dsc.y; j-- > 0;) {      // last to first: su = suffix sums, wu = sum of the suffix sums
-        g1_load_soa(t, rU, n, dsc.x + j);
-        grp_add(su, su, t);
-        g1_load_soa(t, rY, n, dsc.x + j);
-        grp_add(sy, sy, t);
+        if (!key_suspect(susp, dec_idx[dsc.x + j], n_keys)) {
+            g1_load_soa(t, rU, n, dsc.x + j);
+            grp_add(su, su, t);
+            g1_load_soa(t, rY, n, dsc.x + j);
+            grp_add(sy, sy, t);
+        }
         if (first) {
             grp_add(wu, wu, su);
             grp_add(wy, wy, sy);
@@ -548,10 +526,11 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_fpair_mul(u32 *f_soa, u32 n_groups, 
 // TS group record: g1a_st P (sum s_i PK_i) then g2a_st S (sum s_i sig_i), 320 B
 struct ts_grp { g1a_st p; g2a_st s; };
 extern "C" __global__ void LCB_BOUNDS k_ts_rlc_points(u32 n_msgs, const g1a_st *pks, u32 n_pks, const u32 *msg_idx,
-                                                     const u32 *pk_idx, const uint8_t *sigs, u32 n, rlc_key key,
-                                                     u32 *rP, u32 *rS, uint8_t *accept, uint4 *desc, u32 *count,
-                                                     const u32 *ktab, const uint8_t *ktab_ok) {
-    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+                                                     const u32 *pk_idx, const uint8_t *sigs, u32 i0, u32 n,
+                                                     rlc_key key, u32 *rP, u32 *rS, uint8_t *accept, uint4 *desc,
+                                                     u32 *count, const u32 *ktab, const uint8_t *ktab_ok,
+                                                     const u32 *susp) {
+    u32 i = i0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u32 m = msg_idx[i], k = pk_idx[i];
     bool ok = k < n_pks && m < n_msgs;
@@ -565,22 +544,13 @@ extern "C" __global__ void LCB_BOUNDS k_ts_rlc_points(u32 n_msgs, const g1a_st *
     g2 q;
     jac_set_inf(p);
     jac_set_inf(q);
-    if (ok) {
-#ifdef LCB_RLC_G2TEST_CALLS
-        const bool member = g2_in_subgroup(S);
-#else
-        const bool member = g2_in_subgroup_inl(S);
-#endif
-        if (member) {
+    if (ok && !key_suspect_live(susp, k, n_pks)) {      // (a suspect key's shares get their singles from the split)
+        if (g2_in_subgroup_inl(S)) {    // inline: measured faster than the call (CommonCoin batch)
             u32 a, b;
             rlc_scalar(key, i, a, b);
             if (ktab_usable(ktab_ok, k)) g1_mul_ab_tab(p, ktab, n_pks, k, a, b);
             else g1_mul_ab_n(p, PK, a, b);
-#ifdef LCB_RLC_G2_CALLS
-            g2_mul_ab_n(q, S, a, b);     // measured 1015 vs 937 ms per 6.55M-share CommonCoin batch (inline, default)
-#else
-            g2_mul_ab_inl(q, S, a, b);
-#endif
+            g2_mul_ab_inl(q, S, a, b);  // inline: 937 vs 1015 ms per 6.55M-share CommonCoin batch with the call
         } else {
             u32 slot = atomicAdd(count, 1u);
             desc[slot] = make_uint4(i, 1, m < n_msgs ? m : 0, 1);
@@ -593,7 +563,7 @@ extern "C" __global__ void LCB_BOUNDS k_ts_rlc_points(u32 n_msgs, const g1a_st *
 extern "C" __global__ void LCB_BOUNDS k_ts_rlc_sum(const uint4 *desc, u32 n_groups, u32 first, const uint8_t *msg_ok,
                                                   const g1a_st *pks, u32 n_pks, const u32 *pk_idx, const uint8_t *sigs,
                                                   const u32 *rP, const u32 *rS, u32 n, ts_grp *gpts, uint8_t *accept,
-                                                  uint8_t *gexact, u32 *wsum) {
+                                                  uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval) {
     u32 g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n_groups) return;
     uint4 dsc = desc[g];
@@ -601,17 +571,19 @@ extern "C" __global__ void LCB_BOUNDS k_ts_rlc_sum(const uint4 *desc, u32 n_grou
     g1_inf_st(o.p);
     g2_inf_st(o.s);
     gexact[g] = 0;
-    if (dsc.w == 1) {                    // exact single: the share's own PK and sig
-        if (accept[dsc.x] && msg_ok[dsc.z]) {
+    if (dsc.w == 1) {                    // exact single: the share's own PK and sig (whole validity re-derived)
+        u32 k = pk_idx[dsc.x];
+        bool live = accept[dsc.x] && msg_ok[dsc.z] && k < n_pks;
+        if (live) {
             g2a S;
-            u32 k = pk_idx[dsc.x];
-            if (g2_decompress(S, sigs + 96 * (size_t)dsc.x) && k < n_pks) {
+            live = pks[k].ok && g2_decompress(S, sigs + 96 * (size_t)dsc.x);
+            if (live) {
                 o.p = pks[k];
                 o.s.x = S.x; o.s.y = S.y; o.s.inf = S.inf;
             }
-        } else {
-            accept[dsc.x] = 0;
         }
+        if (!live) accept[dsc.x] = 0;
+        if (cval) cval[dsc.x] = live;
         gpts[g] = o;
         return;
     }
@@ -627,10 +599,12 @@ extern "C" __global__ void LCB_BOUNDS k_ts_rlc_sum(const uint4 *desc, u32 n_grou
     jac_set_inf(ss);
     jac_set_inf(ws);
     for (u32 j = dsc.y; j-- > 0;) {
-        g1_load_soa(t, rP, n, dsc.x + j);
-        grp_add(sp, sp, t);
-        g2_load_soa(u, rS, n, dsc.x + j);
-        grp_add(ss, ss, u);
+        if (!key_suspect(susp, pk_idx[dsc.x + j], n_pks)) {
+            g1_load_soa(t, rP, n, dsc.x + j);
+            grp_add(sp, sp, t);
+            g2_load_soa(u, rS, n, dsc.x + j);
+            grp_add(ss, ss, u);
+        }
         if (first) {
             grp_add(wp, wp, sp);
             grp_add(ws, ws, ss);
@@ -691,6 +665,20 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_ts_rlc_miller(const u32 *lines, con
 }
 
 // ---------------------------------------------------------------- resolve a level (TPKE and TS)
+// The shares of group d that still need a check of their own, as singles of kind w (0: a group of one randomized
+// share, 1: an exact single): not those already rejected, nor those of suspect keys (they have exact singles since
+// level 1).
+DI void emit_singles(const uint4 &d, u32 w, const uint8_t *accept, const u32 *key_idx, u32 n_keys, const u32 *susp,
+                     uint4 *next, u32 *next_count) {
+    u32 cnt = 0;
+    for (u32 k = 0; k < d.y; k++)
+        cnt += accept[d.x + k] && !key_suspect(susp, key_idx[d.x + k], n_keys);
+    if (!cnt) return;
+    u32 slot = atomicAdd(next_count, cnt);
+    for (u32 k = 0; k < d.y; k++)
+        if (accept[d.x + k] && !key_suspect(susp, key_idx[d.x + k], n_keys))
+            next[slot++] = make_uint4(d.x + k, 1, d.z, w);
+}
 // Groups [o, o + m) of this level, decided by the final-exponentiation chunk park (stride m).  A failed group of one
 // share rejects it.  At level 1 (first) a failed group of len > 1 goes to the search list (its gamma copied out of the
 // park); below level 1 it becomes ceil(len / s) sub-groups of s = ceil(len / ceil(sqrt(len))) shares, or single
@@ -698,14 +686,13 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_ts_rlc_miller(const u32 *lines, con
 extern "C" __global__ void LCB_BOUNDS k_rlc_resolve(const uint4 *desc, u32 o, u32 m, const uint8_t *gacc,
                                                    const uint8_t *gexact, const u32 *park, u32 first, uint8_t *accept,
                                                    uint4 *next, u32 *next_count, uint4 *search, u32 *search_count,
-                                                   u32 *gamma) {
+                                                   u32 *gamma, const u32 *key_idx, u32 n_keys, const u32 *susp) {
     u32 gl = blockIdx.x * blockDim.x + threadIdx.x;
     if (gl >= m) return;
     u32 g = o + gl;
     uint4 d = desc[g];
     if (gexact && gexact[g]) {           // W outside G2: every share of the group gets its exact check
-        u32 slot = atomicAdd(next_count, d.y);
-        for (u32 k = 0; k < d.y; k++) next[slot + k] = make_uint4(d.x + k, 1, d.z, 1);
+        emit_singles(d, 1, accept, key_idx, n_keys, susp, next, next_count);
         return;
     }
     if (gacc[g]) return;
@@ -721,9 +708,13 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_resolve(const uint4 *desc, u32 o, u3
         for (int q = 0; q < 36; q++) dst[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
         return;
     }
+    if (d.y <= LCB_RLC_SINGLES) {
+        emit_singles(d, 0, accept, key_idx, n_keys, susp, next, next_count);
+        return;
+    }
     u32 parts = 1;
     while (parts * parts < d.y) parts++;
-    u32 s = d.y <= LCB_RLC_SINGLES ? 1u : (d.y + parts - 1) / parts;
+    u32 s = (d.y + parts - 1) / parts;
     u32 cnt = (d.y + s - 1) / s;
     u32 slot = atomicAdd(next_count, cnt);
     for (u32 k = 0; k < cnt; k++) {
@@ -735,7 +726,8 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_resolve(const uint4 *desc, u32 o, u3
 // against gamma^c, c = 1..len.  A match rejects share c - 1 of the group (the only bad one, see the header); no match
 // sends every share of the group to a single check at the next level.
 extern "C" __global__ void LCB_BOUNDS k_rlc_search(const uint4 *search, u32 o, u32 m, const u32 *gamma, const u32 *park,
-                                                  uint8_t *accept, uint4 *next, u32 *next_count) {
+                                                  uint8_t *accept, uint4 *next, u32 *next_count, const u32 *key_idx,
+                                                  u32 n_keys, const u32 *susp) {
     u32 gl = blockIdx.x * blockDim.x + threadIdx.x;
     if (gl >= m) return;
     u32 g = o + gl;
@@ -763,8 +755,57 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_search(const uint4 *search, u32 o, u
         accept[d.x + found - 1] = 0;
         return;
     }
-    u32 slot = atomicAdd(next_count, d.y);
-    for (u32 k = 0; k < d.y; k++) next[slot + k] = make_uint4(d.x + k, 1, d.z, 0);
+    emit_singles(d, 0, accept, key_idx, n_keys, susp, next, next_count);
+}
+
+// ---------------------------------------------------------------- census (suspect keys) and the level-1 split
+// exact singles of shares [0, m): desc = {i, 1, group index (ciphertext / message), 1}; an out-of-range index rejects
+extern "C" __global__ void LCB_BOUNDS k_rlc_census_desc(const u32 *grp_idx, const u32 *key_idx, u32 m, u32 n_grp,
+                                                       u32 n_keys, uint4 *desc, uint8_t *accept) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    u32 c = grp_idx[i];
+    bool ok = c < n_grp && key_idx[i] < n_keys;
+    accept[i] = ok;
+    desc[i] = make_uint4(i, 1, ok ? c : 0, 1);
+}
+// one lane per key: over the census shares that were live (cval), the key is suspect when at least two were sampled
+// and at least half of them failed their exact check.  count[0] += suspect keys.
+extern "C" __global__ void LCB_BOUNDS k_rlc_census_stats(const u32 *key_idx, u32 m, u32 n_keys, const uint8_t *cval,
+                                                        const uint8_t *accept, u32 *susp, u32 *count) {
+    u32 k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_keys) return;
+    u32 live = 0, bad = 0;
+    for (u32 i = 0; i < m; i++) {
+        if (key_idx[i] != k || !cval[i]) continue;
+        live++;
+        bad += accept[i] == 0;
+    }
+    if (live >= 2 && 2 * bad >= live) {
+        atomicOr(susp + (k >> 5), 1u << (k & 31));
+        atomicAdd(count, 1u);
+    }
+}
+// level 1 with suspect keys: every group keeps its place (its sum skips the suspect keys' shares) unless it has no
+// live share of another key (then it is dropped), and each live share of a suspect key becomes an exact single.  count: [0] entries out
+extern "C" __global__ void LCB_BOUNDS k_rlc_suspect_split(const uint4 *desc, u32 n_groups, const u32 *key_idx,
+                                                         u32 n_keys, const u32 *susp, const uint8_t *accept,
+                                                         uint4 *out, u32 *count) {
+    u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_groups) return;
+    uint4 d = desc[g];
+    u32 ns = 0, nc = 0;
+    for (u32 k = 0; k < d.y; k++) {
+        if (!accept[d.x + k]) continue;
+        if (key_suspect(susp, key_idx[d.x + k], n_keys)) ns++;
+        else nc++;
+    }
+    if (!nc && !ns) return;              // nothing live: every share of the group is already rejected
+    u32 slot = atomicAdd(count, ns + (nc ? 1u : 0u));
+    if (nc) out[slot++] = d;
+    for (u32 k = 0; k < d.y; k++)
+        if (accept[d.x + k] && key_suspect(susp, key_idx[d.x + k], n_keys))
+            out[slot++] = make_uint4(d.x + k, 1, d.z, 1);
 }
 
 // ---------------------------------------------------------------- host launch wrappers
@@ -782,38 +823,42 @@ extern "C" void lcbk_rlc_key_tables(dim3 grid, hipStream_t s, const void *keys, 
     grid = dim3((LCB_KTAB_LANES * n_keys + LCB_BLOCK - 1) / LCB_BLOCK);
     LCB_LAUNCH(k_rlc_key_tables, (const g1a_st *)keys, n_keys, jtab, pre, t, okv);
 }
-extern "C" void lcbk_tpke_rlc_points(dim3 grid, hipStream_t s, u32 n_cts, const void *keys, u32 n_keys,
-                                     const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n,
-                                     const u32 key[10], u32 *rU, u32 *rY, uint8_t *accept, const u32 *ktab,
-                                     const uint8_t *ktab_ok) {
+extern "C" void lcbk_tpke_rlc_points(hipStream_t s, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx,
+                                     const u32 *dec_idx, const uint8_t *ui, u32 i0, u32 n, const u32 key[10], u32 *rU,
+                                     u32 *rY, uint8_t *accept, const u32 *ktab, const uint8_t *ktab_ok,
+                                     const u32 *susp) {
     rlc_key k;
     for (int j = 0; j < 8; j++) k.k[j] = key[j];
     k.nonce[0] = key[8];
     k.nonce[1] = key[9];
-    LCB_LAUNCH(k_tpke_rlc_points, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, k, rU, rY, accept, ktab,
-               ktab_ok);
+    dim3 grid((n - i0 + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_tpke_rlc_points, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, i0, n, k, rU, rY, accept,
+               ktab, ktab_ok, susp);
 }
-extern "C" void lcbk_ts_rlc_points(dim3 grid, hipStream_t s, u32 n_msgs, const void *pks, u32 n_pks,
-                                   const u32 *msg_idx, const u32 *pk_idx, const uint8_t *sigs, u32 n,
-                                   const u32 key[10], u32 *rP, u32 *rS, uint8_t *accept, void *desc, u32 *count,
-                                   const u32 *ktab, const uint8_t *ktab_ok) {
+extern "C" void lcbk_ts_rlc_points(hipStream_t s, u32 n_msgs, const void *pks, u32 n_pks, const u32 *msg_idx,
+                                   const u32 *pk_idx, const uint8_t *sigs, u32 i0, u32 n, const u32 key[10], u32 *rP,
+                                   u32 *rS, uint8_t *accept, void *desc, u32 *count, const u32 *ktab,
+                                   const uint8_t *ktab_ok, const u32 *susp) {
     rlc_key k;
     for (int j = 0; j < 8; j++) k.k[j] = key[j];
     k.nonce[0] = key[8];
     k.nonce[1] = key[9];
-    LCB_LAUNCH(k_ts_rlc_points, n_msgs, (const g1a_st *)pks, n_pks, msg_idx, pk_idx, sigs, n, k, rP, rS, accept,
-               (uint4 *)desc, count, ktab, ktab_ok);
+    dim3 grid((n - i0 + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_ts_rlc_points, n_msgs, (const g1a_st *)pks, n_pks, msg_idx, pk_idx, sigs, i0, n, k, rP, rS, accept,
+               (uint4 *)desc, count, ktab, ktab_ok, susp);
 }
-extern "C" void lcbk_rlc_groups(dim3 grid, hipStream_t s, const u32 *key_idx, u32 n, u32 n_keys, u32 cap, void *desc,
+extern "C" void lcbk_rlc_groups(hipStream_t s, const u32 *key_idx, u32 i0, u32 n, u32 n_keys, u32 cap, void *desc,
                                 u32 *count) {
-    LCB_LAUNCH(k_rlc_groups, key_idx, n, n_keys, cap, (uint4 *)desc, count);
+    dim3 grid((n - i0 + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_rlc_groups, key_idx, i0, n, n_keys, cap, (uint4 *)desc, count);
 }
 extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 first,
                                   const uint8_t *ct_ok, const uint8_t *ct_g2, const void *keys, u32 n_keys,
                                   const u32 *dec_idx, const uint8_t *ui, const u32 *rU, const u32 *rY, u32 n,
-                                  void *gpts, uint8_t *accept, uint8_t *gexact, u32 *wsum) {
+                                  void *gpts, uint8_t *accept, uint8_t *gexact, u32 *wsum, const u32 *susp,
+                                  uint8_t *cval) {
     LCB_LAUNCH(k_tpke_rlc_sum, (const uint4 *)desc, n_groups, first, ct_ok, ct_g2, (const g1a_st *)keys, n_keys,
-               dec_idx, ui, rU, rY, n, (g1a_st *)gpts, accept, gexact, wsum);
+               dec_idx, ui, rU, rY, n, (g1a_st *)gpts, accept, gexact, wsum, susp, cval);
 }
 extern "C" void lcbk_tpke_rlc_wsum(dim3 grid, hipStream_t s, const void *sdesc, u32 n_s, const u32 *wsum, u32 n_l1,
                                    void *gpts) {
@@ -837,9 +882,9 @@ extern "C" void lcbk_tpke_rlc_miller_split(hipStream_t s, const u32 *lines, cons
 extern "C" void lcbk_ts_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 first,
                                 const uint8_t *msg_ok, const void *pks, u32 n_pks, const u32 *pk_idx,
                                 const uint8_t *sigs, const u32 *rP, const u32 *rS, u32 n, void *gpts, uint8_t *accept,
-                                uint8_t *gexact, u32 *wsum) {
+                                uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval) {
     LCB_LAUNCH(k_ts_rlc_sum, (const uint4 *)desc, n_groups, first, msg_ok, (const g1a_st *)pks, n_pks, pk_idx, sigs,
-               rP, rS, n, (ts_grp *)gpts, accept, gexact, wsum);
+               rP, rS, n, (ts_grp *)gpts, accept, gexact, wsum, susp, cval);
 }
 extern "C" void lcbk_ts_rlc_wsum(dim3 grid, hipStream_t s, const void *sdesc, u32 n_s, const u32 *wsum, u32 n_l1,
                                  void *gpts) {
@@ -851,12 +896,30 @@ extern "C" void lcbk_ts_rlc_miller(dim3 grid, hipStream_t s, const u32 *lines, c
 }
 extern "C" void lcbk_rlc_resolve(dim3 grid, hipStream_t s, const void *desc, u32 o, u32 m, const uint8_t *gacc,
                                  const uint8_t *gexact, const u32 *park, u32 first, uint8_t *accept, void *next,
-                                 u32 *next_count, void *search, u32 *search_count, u32 *gamma) {
+                                 u32 *next_count, void *search, u32 *search_count, u32 *gamma, const u32 *key_idx,
+                                 u32 n_keys, const u32 *susp) {
     LCB_LAUNCH(k_rlc_resolve, (const uint4 *)desc, o, m, gacc, gexact, park, first, accept, (uint4 *)next, next_count,
-               (uint4 *)search, search_count, gamma);
+               (uint4 *)search, search_count, gamma, key_idx, n_keys, susp);
 }
 extern "C" void lcbk_rlc_search(dim3 grid, hipStream_t s, const void *search, u32 o, u32 m, const u32 *gamma,
-                                const u32 *park, uint8_t *accept, void *next, u32 *next_count) {
-    LCB_LAUNCH(k_rlc_search, (const uint4 *)search, o, m, gamma, park, accept, (uint4 *)next, next_count);
+                                const u32 *park, uint8_t *accept, void *next, u32 *next_count, const u32 *key_idx,
+                                u32 n_keys, const u32 *susp) {
+    LCB_LAUNCH(k_rlc_search, (const uint4 *)search, o, m, gamma, park, accept, (uint4 *)next, next_count, key_idx,
+               n_keys, susp);
+}
+extern "C" void lcbk_rlc_census_desc(hipStream_t s, const u32 *grp_idx, const u32 *key_idx, u32 m, u32 n_grp,
+                                     u32 n_keys, void *desc, uint8_t *accept) {
+    dim3 grid((m + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_rlc_census_desc, grp_idx, key_idx, m, n_grp, n_keys, (uint4 *)desc, accept);
+}
+extern "C" void lcbk_rlc_census_stats(hipStream_t s, const u32 *key_idx, u32 m, u32 n_keys, const uint8_t *cval,
+                                      const uint8_t *accept, u32 *susp, u32 *count) {
+    dim3 grid((n_keys + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_rlc_census_stats, key_idx, m, n_keys, cval, accept, susp, count);
+}
+extern "C" void lcbk_rlc_suspect_split(hipStream_t s, const void *desc, u32 n_groups, const u32 *key_idx, u32 n_keys,
+                                       const u32 *susp, const uint8_t *accept, void *out, u32 *count) {
+    dim3 grid((n_groups + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_rlc_suspect_split, (const uint4 *)desc, n_groups, key_idx, n_keys, susp, accept, (uint4 *)out, count);
 }
 extern "C" size_t lcbk_ts_grp_bytes() { return sizeof(ts_grp); }

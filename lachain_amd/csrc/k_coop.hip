@@ -1,0 +1,108 @@
+// lachain_amd/csrc/k_coop.hip — gfx950 kernels of the cooperative pairing check (coop.hpp: nine lanes per check,
+// seven checks per wave): the randomized batch check's group Miller loops and final exponentiations at the small
+// levels, and the single pairings of the mcl surface.  Same Fp12 values as the one-lane kernels (k_batch.hip,
+// k_tpke.hip), which they replace where a launch would be below one wave per SIMD.
+#include "coop.hpp"
+
+LCB_ASM_LIBRARY(k_coop)
+
+// TPKE group check Miller pair (k_tpke_rlc_miller's function): f = f_{|z|,H}(sum s_i U_i) f_{|z|,W}(-sum s_i Y_i)
+// conjugated, from the ciphertext's two normalised line sets.  Lanes 3..6 evaluate the line coefficients
+// (B'_1 x_1, C'_1 y_1, B'_2 x_2, C'_2 y_2).  A group whose line sets are not normalised (some A_k == 0, only for
+// adversarial W) is flagged in fb and left to k_rlc_miller_fallback.
+extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_tpke_miller(const u32 *lines, const uint4 *desc,
+                                                                         const g1a_st *gpts, u32 n_groups,
+                                                                         u32 *f_soa, uint8_t *gacc, uint8_t *fb) {
+    __shared__ uint4 lds[CP_LDS_QUADS];
+    const Cp c = cp_init(lds);
+    const u32 item = blockIdx.x * CP_G + c.g;
+    const bool live = c.g < CP_G && item < n_groups;
+    const u32 it = live ? item : 0;
+    if (c.j == 0) cp_put(c, S_Z, fp2_zero());
+    const u32 ct = desc[it].z;
+    const u32 *ls1 = lines + (size_t)(2 * ct) * LCB_LINESET_WORDS, *ls2 = ls1 + LCB_LINESET_WORDS;
+    const bool norm = lineset_normalised(ls1) && lineset_normalised(ls2);
+    const int e = c.j - 3;
+    const bool evl = e >= 0 && e < 4;
+    const int ee = evl ? e : 0, pr = ee >> 1, cf = ee & 1;
+    const u32 *lse = (pr ? ls2 : ls1) + 24 * cf;
+    CpEval ev;
+    ev.on = evl;
+    {
+        const g1a_st P = gpts[2 * (size_t)it + pr];
+        ev.y.a = P.inf ? fp_zero() : (cf ? P.y : P.x);      // a point at infinity: every line evaluates to 1
+        ev.y.b = fp_zero();
+    }
+    cp_sync();
+    fp2 R;
+    cp_one(R, c);
+    int k = 0;
+#pragma unroll 1
+    for (int i = 62; i >= 0; i--) {
+        fp2_load_w(ev.x, lse + (size_t)k * LCB_NLINE_WORDS);
+        if (i == 62) cp_eval_round(c, ev);
+        else cp_sqr12(R, c, ev);
+        cp_line(R, c, S_LE, S_LE + 1);
+        cp_line(R, c, S_LE + 2, S_LE + 3);
+        k++;
+        if ((LCB_Z_ABS >> i) & 1) {
+            fp2_load_w(ev.x, lse + (size_t)k * LCB_NLINE_WORDS);
+            cp_eval_round(c, ev);
+            cp_line(R, c, S_LE, S_LE + 1);
+            cp_line(R, c, S_LE + 2, S_LE + 3);
+            k++;
+        }
+    }
+    cp_conj(R, c);
+    park_put(f_soa, n_groups, it, c.j, live && norm, R);
+    if (live && c.j == 0) {
+        gacc[item] = 1;
+        fb[item] = !norm;
+    }
+}
+// the groups k_coop_tpke_miller flagged: one lane each, the one-lane fallback (lines of the un-normalised set computed
+// on the fly)
+extern "C" __global__ void LCB_PAIR_BOUNDS k_rlc_miller_fallback(const u32 *lines, const uint4 *desc, const g1a_st *gpts,
+                                                                u32 n_groups, u32 *f_soa, const uint8_t *fb) {
+    u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_groups || !fb[g]) return;
+    u32 c = desc[g].z;
+    g1a P, Q;
+    st_to_g1a(P, gpts[2 * (size_t)g]);
+    st_to_g1a(Q, gpts[2 * (size_t)g + 1]);
+    fp12 f;
+    miller2_sets_fallback(f, lines + (size_t)(2 * c) * LCB_LINESET_WORDS, P, lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS, Q);
+    fp12_store_soa(f_soa, n_groups, g, f);
+}
+
+// accept[i] &= (final_exp(f_i) == 1) for f_i in park slot 0 (slots 0..4 as working space); keep_result: slot 0 <- the
+// final exponentiation (the GT value) instead of only the decision
+extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_final_exp_check(u32 *park, u32 n, uint8_t *accept,
+                                                                             int keep_result) {
+    __shared__ uint4 lds[CP_LDS_QUADS];
+    const Cp c = cp_init(lds);
+    const u32 item = blockIdx.x * CP_G + c.g;
+    const bool live = c.g < CP_G && item < n;
+    const size_t it = live ? item : 0;
+    if (c.j == 0) cp_put(c, S_Z, fp2_zero());
+    cp_sync();
+    fp2 R;
+    cp_final_exp(R, c, park, n, it, live);
+    const bool one = cp_is_one(R, c);
+    if (keep_result) park_put(park, n, it, c.j, live, R);
+    if (live && c.j == 0 && accept) accept[item] = accept[item] && one;
+}
+
+// ---------------------------------------------------------------- host launch wrappers
+extern "C" void lcbk_coop_tpke_miller(hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups,
+                                      u32 *f_soa, uint8_t *gacc, uint8_t *fb) {
+    dim3 grid((n_groups + CP_G - 1) / CP_G);
+    hipLaunchKernelGGL(k_coop_tpke_miller, grid, dim3(CP_BLOCK), 0, s, lines, (const uint4 *)desc, (const g1a_st *)gpts,
+                       n_groups, f_soa, gacc, fb);
+    grid = dim3((n_groups + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_rlc_miller_fallback, lines, (const uint4 *)desc, (const g1a_st *)gpts, n_groups, f_soa, fb);
+}
+extern "C" void lcbk_coop_final_exp_check(hipStream_t s, u32 *park, u32 n, uint8_t *accept, int keep_result) {
+    dim3 grid((n + CP_G - 1) / CP_G);
+    hipLaunchKernelGGL(k_coop_final_exp_check, grid, dim3(CP_BLOCK), 0, s, park, n, accept, keep_result);
+}

@@ -61,21 +61,26 @@ extern "C" void lcbk_secp_pubkey(hipStream_t s, const uint8_t *privs, u32 n, con
 extern "C" void lcbk_secp_sign(hipStream_t s, const uint8_t *hashes, const uint8_t *privs, const uint8_t *nonces, u32 n, const void *g_table, int chain_id, int use_new, uint8_t *out, uint8_t *ok);
 extern "C" size_t lcbk_key_table_bytes(u32 n_keys);
 extern "C" void lcbk_rlc_key_tables(dim3 grid, hipStream_t s, const void *keys, u32 n_keys, u32 *ws, u32 **tab, uint8_t **ktab_ok);
-extern "C" void lcbk_tpke_rlc_points(dim3 grid, hipStream_t s, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, const u32 key[10], u32 *rU, u32 *rY, uint8_t *accept, const u32 *ktab, const uint8_t *ktab_ok);
-extern "C" void lcbk_ts_rlc_points(dim3 grid, hipStream_t s, u32 n_msgs, const void *pks, u32 n_pks, const u32 *msg_idx, const u32 *pk_idx, const uint8_t *sigs, u32 n, const u32 key[10], u32 *rP, u32 *rS, uint8_t *accept, void *desc, u32 *count, const u32 *ktab, const uint8_t *ktab_ok);
-extern "C" void lcbk_rlc_groups(dim3 grid, hipStream_t s, const u32 *key_idx, u32 n, u32 n_keys, u32 cap, void *desc, u32 *count);
-extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 first, const uint8_t *ct_ok, const uint8_t *ct_g2, const void *keys, u32 n_keys, const u32 *dec_idx, const uint8_t *ui, const u32 *rU, const u32 *rY, u32 n, void *gpts, uint8_t *accept, uint8_t *gexact, u32 *wsum);
+extern "C" void lcbk_tpke_rlc_points(hipStream_t s, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 i0, u32 n, const u32 key[10], u32 *rU, u32 *rY, uint8_t *accept, const u32 *ktab, const uint8_t *ktab_ok, const u32 *susp);
+extern "C" void lcbk_ts_rlc_points(hipStream_t s, u32 n_msgs, const void *pks, u32 n_pks, const u32 *msg_idx, const u32 *pk_idx, const uint8_t *sigs, u32 i0, u32 n, const u32 key[10], u32 *rP, u32 *rS, uint8_t *accept, void *desc, u32 *count, const u32 *ktab, const uint8_t *ktab_ok, const u32 *susp);
+extern "C" void lcbk_rlc_groups(hipStream_t s, const u32 *key_idx, u32 i0, u32 n, u32 n_keys, u32 cap, void *desc, u32 *count);
+extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 first, const uint8_t *ct_ok, const uint8_t *ct_g2, const void *keys, u32 n_keys, const u32 *dec_idx, const uint8_t *ui, const u32 *rU, const u32 *rY, u32 n, void *gpts, uint8_t *accept, uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval);
 extern "C" void lcbk_tpke_rlc_wsum(dim3 grid, hipStream_t s, const void *sdesc, u32 n_s, const u32 *wsum, u32 n_l1, void *gpts);
 extern "C" void lcbk_tpke_ct_g2check(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, uint8_t *ct_g2);
 extern "C" void lcbk_tpke_rlc_miller_split(hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups,
                                            u32 *f_soa, uint8_t *gacc);
 extern "C" void lcbk_tpke_rlc_miller(dim3 grid, hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups, u32 *f_soa, uint8_t *gacc);
-extern "C" void lcbk_ts_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 first, const uint8_t *msg_ok, const void *pks, u32 n_pks, const u32 *pk_idx, const uint8_t *sigs, const u32 *rP, const u32 *rS, u32 n, void *gpts, uint8_t *accept, uint8_t *gexact, u32 *wsum);
+extern "C" void lcbk_ts_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 first, const uint8_t *msg_ok, const void *pks, u32 n_pks, const u32 *pk_idx, const uint8_t *sigs, const u32 *rP, const u32 *rS, u32 n, void *gpts, uint8_t *accept, uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval);
 extern "C" void lcbk_ts_rlc_wsum(dim3 grid, hipStream_t s, const void *sdesc, u32 n_s, const u32 *wsum, u32 n_l1, void *gpts);
 extern "C" void lcbk_ts_rlc_miller(dim3 grid, hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups, u32 *f_soa, uint8_t *gacc);
-extern "C" void lcbk_rlc_resolve(dim3 grid, hipStream_t s, const void *desc, u32 o, u32 m, const uint8_t *gacc, const uint8_t *gexact, const u32 *park, u32 first, uint8_t *accept, void *next, u32 *next_count, void *search, u32 *search_count, u32 *gamma);
-extern "C" void lcbk_rlc_search(dim3 grid, hipStream_t s, const void *search, u32 o, u32 m, const u32 *gamma, const u32 *park, uint8_t *accept, void *next, u32 *next_count);
+extern "C" void lcbk_rlc_resolve(dim3 grid, hipStream_t s, const void *desc, u32 o, u32 m, const uint8_t *gacc, const uint8_t *gexact, const u32 *park, u32 first, uint8_t *accept, void *next, u32 *next_count, void *search, u32 *search_count, u32 *gamma, const u32 *key_idx, u32 n_keys, const u32 *susp);
+extern "C" void lcbk_rlc_search(dim3 grid, hipStream_t s, const void *search, u32 o, u32 m, const u32 *gamma, const u32 *park, uint8_t *accept, void *next, u32 *next_count, const u32 *key_idx, u32 n_keys, const u32 *susp);
+extern "C" void lcbk_rlc_census_desc(hipStream_t s, const u32 *grp_idx, const u32 *key_idx, u32 m, u32 n_grp, u32 n_keys, void *desc, uint8_t *accept);
+extern "C" void lcbk_rlc_census_stats(hipStream_t s, const u32 *key_idx, u32 m, u32 n_keys, const uint8_t *cval, const uint8_t *accept, u32 *susp, u32 *count);
+extern "C" void lcbk_rlc_suspect_split(hipStream_t s, const void *desc, u32 n_groups, const u32 *key_idx, u32 n_keys, const u32 *susp, const uint8_t *accept, void *out, u32 *count);
 extern "C" size_t lcbk_ts_grp_bytes();
+extern "C" void lcbk_coop_tpke_miller(hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups, u32 *f_soa, uint8_t *gacc, uint8_t *fb);
+extern "C" void lcbk_coop_final_exp_check(hipStream_t s, u32 *park, u32 n, uint8_t *accept, int keep_result);
 extern "C" void lcbk_op(dim3 grid, hipStream_t s, int op, u32 *io, int orig_cof);
 
 // sizes of the device records the host allocates

@@ -52,13 +52,14 @@ struct lcb_ctx {
     hipEvent_t ver_ev[3] = {};
     bool ver_ev_ready = false, ver_ran = false;
     // randomized batch verification (k_batch.hip): r_i U_i / r_i Y_i records, group lists, group points, counts
-    DevBuf rlc[13];                   // [12]: the keys' fixed-base tables
+    DevBuf rlc[16];                   // [12]: the keys' fixed-base tables, [13] suspect-key bitmap, [14] census validity
     hipEvent_t rlc_ev[3] = {};
     hipEvent_t rlc_lev_ev[4] = {};    // per level: before sum / Miller / final exp / resolve
     float rlc_ms[4] = {};             // accumulated over the levels of the last call: sums, Miller, final exp (+ resolve
                                       // / search), unused
     bool rlc_ev_ready = false, rlc_ran = false;
     uint32_t rlc_levels[8] = {};
+    uint32_t rlc_census[4] = {};      // census shares, suspect keys, level-1 groups before / entries after the split
     int rlc_nlev = 0;
     uint64_t rlc_calls = 0;
     hipStream_t aux = nullptr;        // second stream of the fused batched verify (randomisation beside preparation)

@@ -19,6 +19,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <mutex>
+#include <atomic>
 #include <vector>
 #include <string>
 #include <algorithm>
@@ -689,71 +690,109 @@ int tpke_partial_decrypt_prepared(lcb_ctx *c, uint8_t *ui_out, uint8_t *status, 
 // checks, except with probability <= 2^-64 per group decision (the exponents are secret).  Groups are runs of shares
 // of one ciphertext (TPKE) / message (threshold signatures) in the caller's order: ciphertext- / message-major batches
 // give one group per ciphertext / message.  A level's group count comes back to the host (one 8-byte read per level).
+std::mutex g_seed_mu;                       // lcb_set_batch_seed (test hook) vs. the callers' key fills
 uint8_t g_rlc_seed[32];
 bool g_rlc_seed_set = false;
+std::atomic<size_t> g_census_min{16384};    // lcb_set_batch_census: batches of at least this many shares get a census
+std::atomic<uint32_t> g_split_max{32768};   // lcb_set_rlc_split_max: TPKE levels of <= this many groups split pairs
+std::atomic<uint32_t> g_coop_max{32768};    // lcb_set_coop_max: levels of <= this many checks use the 9-lane kernels
 enum RlcKind { RLC_TPKE = 0, RLC_TS = 1 };
-struct RlcStats { bool valid = false; int nlev = 0; uint32_t levels[8] = {}; float ms[6] = {}; };
+struct RlcStats {
+    bool valid = false;
+    int nlev = 0;
+    uint32_t levels[8] = {};
+    float ms[6] = {};
+    uint32_t census[4] = {};
+};
 thread_local RlcStats t_rlc_stats;
-struct RlcWs { u32 *rA, *rB; uint8_t *dA, *dB; u32 *cnt; };    // cnt: [current, next, search]
+// cnt: [0] current level's groups, [1] next level's, [2] search entries, [3] suspect keys, [4] level-1 entries after
+// the suspect split; susp: the suspect-key bitmap; m: census shares [0, m)
+struct RlcWs { u32 *rA, *rB; uint8_t *dA, *dB; u32 *cnt; u32 *susp; u32 m; };
 bool rlc_key_fill(lcb_ctx *c, u32 key[10]) {
-    if (g_rlc_seed_set) memcpy(key, g_rlc_seed, 32);
-    else if (getrandom(key, 32, 0) != 32) { set_err("batched verify: getrandom failed"); return false; }
+    bool fixed;
+    {
+        std::lock_guard<std::mutex> lk(g_seed_mu);
+        fixed = g_rlc_seed_set;
+        if (fixed) memcpy(key, g_rlc_seed, 32);
+    }
+    if (!fixed && getrandom(key, 32, 0) != 32) { set_err("batched verify: getrandom failed"); return false; }
     c->rlc_calls++;
     key[8] = (u32)c->rlc_calls;
     key[9] = (u32)(c->rlc_calls >> 32);
     return true;
 }
-bool rlc_ws(lcb_ctx *c, RlcWs &w, size_t n, size_t rec_a, size_t rec_b) {
+// census size: a prefix of the batch large enough to sample every key a few times (>= 8 shares per key on average,
+// 512 .. 2048 shares), at most a quarter of the batch; 0 = no census (small batches, or disabled)
+u32 census_size(size_t n, size_t n_keys) {
+    const size_t min_n = g_census_min.load();
+    if (!min_n || n < min_n || n_keys < 2 || n_keys > 4096) return 0;
+    size_t m = std::min<size_t>(std::max<size_t>(512, 8 * n_keys), 2048);
+    m = std::min(m, n / 4);
+    return m < 16 ? 0 : (u32)m;
+}
+bool rlc_ws(lcb_ctx *c, RlcWs &w, size_t n, size_t rec_a, size_t rec_b, size_t n_keys, u32 m, hipStream_t s) {
     w.rA = (u32 *)c->rlc[0].get(n * rec_a);
     w.rB = (u32 *)c->rlc[1].get(n * rec_b);
     w.dA = (uint8_t *)c->rlc[2].get(n * 16);
     w.dB = (uint8_t *)c->rlc[3].get(n * 16);
-    w.cnt = (u32 *)c->rlc[4].get(16);
-    if (!w.rA || !w.rB || !w.dA || !w.dB || !w.cnt) { set_err("device allocation failed"); return false; }
+    w.cnt = (u32 *)c->rlc[4].get(32);
+    const size_t sw = (n_keys + 31) / 32;
+    w.susp = m ? (u32 *)c->rlc[13].get(4 * sw) : nullptr;
+    w.m = m;
+    if (!w.rA || !w.rB || !w.dA || !w.dB || !w.cnt || (m && !w.susp)) { set_err("device allocation failed"); return false; }
     if (!c->rlc_ev_ready) {
         for (auto &e : c->rlc_ev) hipEventCreate(&e);
         for (auto &e : c->rlc_lev_ev) hipEventCreate(&e);
         c->rlc_ev_ready = true;
     }
+    // zeroed on the calling stream before any kernel of the call (the randomisation on the second stream reads
+    // the bitmap while the census writes it)
+    hipMemsetAsync(w.cnt, 0, 32, s);
+    if (m) hipMemsetAsync(w.susp, 0, 4 * sw, s);
+    c->rlc_census[0] = m;
+    c->rlc_census[1] = c->rlc_census[2] = c->rlc_census[3] = 0;
     return true;
 }
 // fixed-base tables of the batch's keys (k_rlc_key_tables), when the batch is large enough to repay them
 // (4 x 255 points per key, 32 lanes per key, ~40 additions of latency); nullptr: the points kernel multiplies the keys directly
 u32 *rlc_key_tables(lcb_ctx *c, const void *keys, size_t n_keys, hipStream_t s, uint8_t **ktab_ok) {
     *ktab_ok = nullptr;
-    if (!n_keys || n_keys > 4096 || getenv("LCB_RLC_NO_KEY_TABLES")) return nullptr;
+    if (!n_keys || n_keys > 4096) return nullptr;
     u32 *ws = (u32 *)c->rlc[12].get(lcbk_key_table_bytes((u32)n_keys));
     if (!ws) return nullptr;
     u32 *tab = nullptr;
     lcbk_rlc_key_tables(dim3(nblk(32 * n_keys)), s, keys, (u32)n_keys, ws, &tab, ktab_ok);
     return tab;
 }
-// phase 1 (needs the decompressed keys only): per-share exponent multiples + level-1 groups (count left on device)
+// phase 1 (needs the decompressed keys only): per-share exponent multiples of shares [m, n) + level-1 groups (count
+// left on device in cnt[0])
 int rlc_points_enqueue(lcb_ctx *c, RlcWs &w, uint8_t *d_accept, size_t n, size_t n_keys, size_t n_cts,
                        const uint32_t *d_ct, const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
     u32 key[10];
-    if (!rlc_key_fill(c, key) || !rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G1_JAC_BYTES)) return -1;
+    if (!rlc_key_fill(c, key)) return -1;
     hipEventRecord(c->rlc_ev[0], s);
-    hipMemsetAsync(w.cnt, 0, 16, s);
-    uint8_t *kok = nullptr;
-    u32 *ktab = rlc_key_tables(c, c->t_keys.p, n_keys, s, &kok);
-    lcbk_tpke_rlc_points(dim3(nblk(n)), s, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct, d_dec, d_ui, (u32)n, key, w.rA,
-                         w.rB, d_accept, ktab, kok);
-    lcbk_rlc_groups(dim3(nblk(n)), s, d_ct, (u32)n, (u32)n_cts, 32, w.dA, w.cnt);
+    if (w.m < n) {
+        uint8_t *kok = nullptr;
+        u32 *ktab = rlc_key_tables(c, c->t_keys.p, n_keys, s, &kok);
+        lcbk_tpke_rlc_points(s, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct, d_dec, d_ui, w.m, (u32)n, key, w.rA, w.rB,
+                             d_accept, ktab, kok, w.susp);
+        lcbk_rlc_groups(s, d_ct, w.m, (u32)n, (u32)n_cts, 32, w.dA, w.cnt);
+    }
     hipEventRecord(c->rlc_ev[1], s);
     return launched("tpke batched verify launch") ? 0 : -1;
 }
 int ts_rlc_points_enqueue(lcb_ctx *c, RlcWs &w, uint8_t *d_accept, size_t n, size_t n_pks, size_t n_msgs,
                           const uint8_t *d_sigs, const uint32_t *d_midx, const uint32_t *d_pidx, hipStream_t s) {
     u32 key[10];
-    if (!rlc_key_fill(c, key) || !rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G2_JAC_BYTES)) return -1;
+    if (!rlc_key_fill(c, key)) return -1;
     hipEventRecord(c->rlc_ev[0], s);
-    hipMemsetAsync(w.cnt, 0, 16, s);
-    uint8_t *kok = nullptr;
-    u32 *ktab = rlc_key_tables(c, c->s_keys.p, n_pks, s, &kok);
-    lcbk_ts_rlc_points(dim3(nblk(n)), s, (u32)n_msgs, c->s_keys.p, (u32)n_pks, d_midx, d_pidx, d_sigs, (u32)n, key,
-                       w.rA, w.rB, d_accept, w.dA, w.cnt, ktab, kok);
-    lcbk_rlc_groups(dim3(nblk(n)), s, d_midx, (u32)n, (u32)n_msgs, 128, w.dA, w.cnt);
+    if (w.m < n) {
+        uint8_t *kok = nullptr;
+        u32 *ktab = rlc_key_tables(c, c->s_keys.p, n_pks, s, &kok);
+        lcbk_ts_rlc_points(s, (u32)n_msgs, c->s_keys.p, (u32)n_pks, d_midx, d_pidx, d_sigs, w.m, (u32)n, key, w.rA,
+                           w.rB, d_accept, w.dA, w.cnt, ktab, kok, w.susp);
+        lcbk_rlc_groups(s, d_midx, w.m, (u32)n, (u32)n_msgs, 128, w.dA, w.cnt);
+    }
     hipEventRecord(c->rlc_ev[1], s);
     return launched("ts batched verify launch") ? 0 : -1;
 }
@@ -773,67 +812,129 @@ int rlc_g2check(lcb_ctx *c, hipStream_t s) {
                              (u32)c->t_n_cts, ctg2);
     return 0;
 }
-// levels of at most 32,768 groups (under one wave per SIMD as two lanes per group) run their TPKE Miller loops as two
-// single pairs per group (k_tpke_rlc_miller_split; measured 130.0 -> 123.3 ms per 1M-share batched step) unless
-// LCB_RLC_SPLIT=0
-static bool rlc_split_levels() {
-    static const bool on = [] { const char *e = getenv("LCB_RLC_SPLIT"); return !(e && e[0] == '0'); }();
-    return on;
-}
 struct RlcIo {                     // the per-share inputs the exact singles re-read
     const uint32_t *d_key;         // dec_idx (TPKE) / pk_idx (TS)
     const uint8_t *d_pts;          // ui (TPKE) / sigs (TS)
+    const uint32_t *d_grp;         // ct_idx (TPKE) / msg_idx (TS): the census singles' groups
 };
-// phase 2 (after the preparation): level 1 group checks; level 2: weighted re-check + search of the failed groups;
-// then single checks
-int rlc_levels(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, size_t n, RlcIo io, hipStream_t s) {
-    const bool ts = kind == RLC_TS;
-    const u32 *lines = (const u32 *)(ts ? c->s_lines.p : c->t_lines.p);
-    const uint8_t *okv = (const uint8_t *)(ts ? c->s_mok.p : c->t_ctok.p);
-    const uint8_t *ctg2 = (const uint8_t *)c->rlc[8].p;
-    const size_t rec = ts ? lcbk_ts_grp_bytes() : 2 * LCB_G1A_ST_BYTES;
-    const size_t wrec = ts ? LCB_G1_JAC_BYTES + LCB_G2_JAC_BYTES : 2 * LCB_G1_JAC_BYTES;
-    u32 cnt[3] = {0, 0, 0};
-    for (auto &m : c->rlc_ms) m = 0.0f;
-    if (!read_counts(cnt, w.cnt, 1, s)) return -1;
-    u32 groups = cnt[0];
+struct RlcKindInfo {
+    bool ts;
+    const u32 *lines;
+    const uint8_t *okv, *ctg2;
+    const void *keys;
+    size_t n_keys, n_grp, rec, wrec;
+};
+RlcKindInfo rlc_kind(lcb_ctx *c, RlcKind kind) {
+    RlcKindInfo k;
+    k.ts = kind == RLC_TS;
+    k.lines = (const u32 *)(k.ts ? c->s_lines.p : c->t_lines.p);
+    k.okv = (const uint8_t *)(k.ts ? c->s_mok.p : c->t_ctok.p);
+    k.ctg2 = (const uint8_t *)c->rlc[8].p;
+    k.keys = k.ts ? c->s_keys.p : c->t_keys.p;
+    k.n_keys = k.ts ? c->s_n_pks : c->t_n_keys;
+    k.n_grp = k.ts ? c->s_n_msgs : c->t_n_cts;
+    k.rec = k.ts ? lcbk_ts_grp_bytes() : 2 * LCB_G1A_ST_BYTES;
+    k.wrec = k.ts ? LCB_G1_JAC_BYTES + LCB_G2_JAC_BYTES : 2 * LCB_G1_JAC_BYTES;
+    return k;
+}
+// the group sums / singles of a level's desc list -> gpts (k_*_rlc_sum)
+void rlc_sum_enqueue(const RlcKindInfo &K, RlcWs &w, const uint8_t *desc, u32 groups, bool first, uint8_t *d_accept,
+                     size_t n, RlcIo io, void *gpts, uint8_t *gex, u32 *wsum, uint8_t *cval, hipStream_t s) {
+    const u32 *susp = w.susp;
+    if (K.ts)
+        lcbk_ts_rlc_sum(dim3(nblk(groups)), s, desc, groups, first, K.okv, K.keys, (u32)K.n_keys, io.d_key, io.d_pts,
+                        w.rA, w.rB, (u32)n, gpts, d_accept, gex, wsum, susp, cval);
+    else
+        lcbk_tpke_rlc_sum(dim3(nblk(groups)), s, desc, groups, first, K.okv, K.ctg2, K.keys, (u32)K.n_keys, io.d_key,
+                          io.d_pts, w.rA, w.rB, (u32)n, gpts, d_accept, gex, wsum, susp, cval);
+}
+// Miller + final exponentiation (+ resolve / search) over the groups of desc in chunks; gpts holds the points
+void rlc_checks(lcb_ctx *c, const RlcKindInfo &K, RlcWs &w, const uint8_t *desc, u32 count, void *gpts, uint8_t *gacc,
+                u32 *f, bool search_stage, bool first, uint8_t *gex, uint4 *sdesc, u32 *gamma, uint8_t *d_accept,
+                RlcIo io, hipStream_t s) {
     hipEvent_t *ev = c->rlc_lev_ev;
     float t;
-    // Miller + final exponentiation (+ resolve / search) over the groups of desc in chunks; gpts holds the points
-    auto checks = [&](const uint8_t *desc, u32 count, void *gpts, uint8_t *gacc, u32 *f, bool search_stage,
-                      bool first, uint8_t *gex, uint4 *sdesc, u32 *gamma) {
-        for (size_t o = 0; o < count; o += LCB_VERIFY_CHUNK) {
-            const size_t m = count - o < LCB_VERIFY_CHUNK ? count - o : LCB_VERIFY_CHUNK;
-            hipEventRecord(ev[1], s);
-            if (ts)
-                lcbk_ts_rlc_miller(dim3(nblk(m)), s, lines, desc + 16 * o, (const uint8_t *)gpts + rec * o, (u32)m, f,
-                                   gacc + o);
-            else if (2 * m <= 65536 && rlc_split_levels())   // under one wave per SIMD: one Miller pair per lane
-                lcbk_tpke_rlc_miller_split(s, lines, desc + 16 * o, (const uint8_t *)gpts + rec * o, (u32)m, f,
-                                           gacc + o);
-            else
-                lcbk_tpke_rlc_miller(dim3(nblk(m)), s, lines, desc + 16 * o, (const uint8_t *)gpts + rec * o, (u32)m, f,
-                                     gacc + o);
-            hipEventRecord(ev[2], s);
-            lcbk_final_exp_check(dim3(nblk(m)), s, f, (u32)m, gacc + o);
-            hipEventRecord(ev[3], s);
-            if (search_stage)
-                lcbk_rlc_search(dim3(nblk(m)), s, sdesc, (u32)o, (u32)m, gamma, f, d_accept, w.dB, w.cnt + 1);
-            else
-                lcbk_rlc_resolve(dim3(nblk(m)), s, desc, (u32)o, (u32)m, gacc, gex, f, first ? 1u : 0u, d_accept, w.dB,
-                                 w.cnt + 1, sdesc, w.cnt + 2, gamma);
-            if (hipEventSynchronize(ev[3]) == hipSuccess) {
-                if (hipEventElapsedTime(&t, ev[1], ev[2]) == hipSuccess) c->rlc_ms[1] += t;
-                if (hipEventElapsedTime(&t, ev[2], ev[3]) == hipSuccess) c->rlc_ms[2] += t;
-            }
+    for (size_t o = 0; o < count; o += LCB_VERIFY_CHUNK) {
+        const size_t m = count - o < LCB_VERIFY_CHUNK ? count - o : LCB_VERIFY_CHUNK;
+        hipEventRecord(ev[1], s);
+        // small levels (below one wave per SIMD as one check per lane): nine lanes per check (k_coop.hip)
+        const bool coop = m <= g_coop_max.load();
+        if (K.ts)
+            lcbk_ts_rlc_miller(dim3(nblk(m)), s, K.lines, desc + 16 * o, (const uint8_t *)gpts + K.rec * o, (u32)m, f,
+                               gacc + o);
+        else if (coop)
+            lcbk_coop_tpke_miller(s, K.lines, desc + 16 * o, (const uint8_t *)gpts + K.rec * o, (u32)m, f, gacc + o,
+                                  (uint8_t *)c->rlc[15].get(m));
+        else if (m <= g_split_max.load())    // under one wave per SIMD: one Miller pair per lane
+            lcbk_tpke_rlc_miller_split(s, K.lines, desc + 16 * o, (const uint8_t *)gpts + K.rec * o, (u32)m, f,
+                                       gacc + o);
+        else
+            lcbk_tpke_rlc_miller(dim3(nblk(m)), s, K.lines, desc + 16 * o, (const uint8_t *)gpts + K.rec * o, (u32)m, f,
+                                 gacc + o);
+        hipEventRecord(ev[2], s);
+        if (coop) lcbk_coop_final_exp_check(s, f, (u32)m, gacc + o, 0);
+        else lcbk_final_exp_check(dim3(nblk(m)), s, f, (u32)m, gacc + o);
+        hipEventRecord(ev[3], s);
+        if (search_stage)
+            lcbk_rlc_search(dim3(nblk(m)), s, sdesc, (u32)o, (u32)m, gamma, f, d_accept, w.dB, w.cnt + 1, io.d_key,
+                            (u32)K.n_keys, w.susp);
+        else
+            lcbk_rlc_resolve(dim3(nblk(m)), s, desc, (u32)o, (u32)m, gacc, gex, f, first ? 1u : 0u, d_accept, w.dB,
+                             w.cnt + 1, sdesc, w.cnt + 2, gamma, io.d_key, (u32)K.n_keys, w.susp);
+        if (hipEventSynchronize(ev[3]) == hipSuccess) {
+            if (hipEventElapsedTime(&t, ev[1], ev[2]) == hipSuccess) c->rlc_ms[1] += t;
+            if (hipEventElapsedTime(&t, ev[2], ev[3]) == hipSuccess) c->rlc_ms[2] += t;
         }
-    };
+    }
+}
+// the census (SURVEY-style Byzantine validators, k_batch.hip "suspect keys"): exact single checks of shares [0, m),
+// then the suspect-key bitmap and its count (cnt[3]); everything stays on the device (no host read)
+int rlc_census(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, RlcIo io, hipStream_t s) {
+    if (!w.m) return 0;
+    const RlcKindInfo K = rlc_kind(c, kind);
+    const u32 m = w.m;
+    // the census uses dB as its desc list (dA is the level-1 list being built on the second stream)
+    void *gpts = c->rlc[5].get((size_t)m * K.rec);
+    uint8_t *gacc = (uint8_t *)c->rlc[6].get(m), *gex = (uint8_t *)c->rlc[7].get(m);
+    uint8_t *cval = (uint8_t *)c->rlc[14].get(m);
+    u32 *f = (u32 *)c->t_f.get((size_t)m * 576 * (size_t)lcbk_fe_slots());
+    if (!gpts || !gacc || !gex || !cval || !f) { set_err("device allocation failed"); return -1; }
+    lcbk_rlc_census_desc(s, io.d_grp, io.d_key, m, (u32)K.n_grp, (u32)K.n_keys, w.dB, d_accept);
+    RlcWs cw = w;
+    cw.susp = nullptr;                  // the census singles are exact checks whatever the bitmap says
+    rlc_sum_enqueue(K, cw, w.dB, m, false, d_accept, m, io, gpts, gex, nullptr, cval, s);
+    rlc_checks(c, K, cw, w.dB, m, gpts, gacc, f, false, false, gex, nullptr, nullptr, d_accept, io, s);
+    lcbk_rlc_census_stats(s, io.d_key, m, (u32)K.n_keys, cval, d_accept, w.susp, w.cnt + 3);
+    return launched("batched verify census launch") ? 0 : -1;
+}
+// phase 2 (after the preparation and the randomisation): level 1 group checks (with suspect keys: the groups summed
+// over the other keys, every share of a suspect key as an exact single); level 2: weighted re-check + search of the
+// failed groups; then single checks
+int rlc_levels(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, size_t n, RlcIo io, hipStream_t s) {
+    const RlcKindInfo K = rlc_kind(c, kind);
+    u32 cnt[5] = {0, 0, 0, 0, 0};
+    for (auto &m : c->rlc_ms) m = 0.0f;
+    if (!read_counts(cnt, w.cnt, 4, s)) return -1;
+    u32 groups = cnt[0];
+    c->rlc_census[1] = cnt[3];
+    c->rlc_census[2] = c->rlc_census[3] = groups;
+    hipEvent_t *ev = c->rlc_lev_ev;
+    float t;
+    if (cnt[3] && groups) {             // suspect keys: split their shares out of the level-1 groups
+        lcbk_rlc_suspect_split(s, w.dA, groups, io.d_key, (u32)K.n_keys, w.susp, d_accept, w.dB, w.cnt + 4);
+        if (!launched("batched verify launch") || !read_counts(cnt + 4, w.cnt + 4, 1, s)) return -1;
+        groups = cnt[4];
+        c->rlc_census[3] = groups;
+        std::swap(w.dA, w.dB);
+    } else {
+        w.susp = nullptr;               // no suspect key: the sums need not test the bitmap
+    }
     for (int lev = 0; groups; lev++) {
         if (lev > 40) { set_err("batched verify: group splitting did not terminate"); return -1; }
         if (lev < 8) c->rlc_levels[lev] = groups;
         c->rlc_nlev = lev + 1;
         const bool first = lev == 0;
-        void *gpts = c->rlc[5].get((size_t)groups * rec);
+        void *gpts = c->rlc[5].get((size_t)groups * K.rec);
         uint8_t *gacc = (uint8_t *)c->rlc[6].get(groups), *gex = (uint8_t *)c->rlc[7].get(groups);
         const size_t nf = groups < LCB_VERIFY_CHUNK ? groups : LCB_VERIFY_CHUNK;
         u32 *f = (u32 *)c->t_f.get(nf * 576 * (size_t)lcbk_fe_slots());
@@ -842,7 +943,7 @@ int rlc_levels(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, size_t n, 
         if (first) {
             sdesc = (uint4 *)c->rlc[9].get((size_t)groups * 16);
             gamma = (u32 *)c->rlc[10].get((size_t)groups * 576);
-            wsum = (u32 *)c->rlc[11].get((size_t)groups * wrec);
+            wsum = (u32 *)c->rlc[11].get((size_t)groups * K.wrec);
         }
         if (!gpts || !gacc || !gex || !f || (first && (!sdesc || !gamma || !wsum))) {
             set_err("device allocation failed");
@@ -850,30 +951,26 @@ int rlc_levels(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, size_t n, 
         }
         hipMemsetAsync(w.cnt + 1, 0, 8, s);
         hipEventRecord(ev[0], s);
-        if (ts)
-            lcbk_ts_rlc_sum(dim3(nblk(groups)), s, w.dA, groups, first, okv, c->s_keys.p, (u32)c->s_n_pks, io.d_key,
-                            io.d_pts, w.rA, w.rB, (u32)n, gpts, d_accept, gex, wsum);
-        else
-            lcbk_tpke_rlc_sum(dim3(nblk(groups)), s, w.dA, groups, first, okv, ctg2, c->t_keys.p, (u32)c->t_n_keys,
-                              io.d_key, io.d_pts, w.rA, w.rB, (u32)n, gpts, d_accept, gex, wsum);
+        rlc_sum_enqueue(K, w, w.dA, groups, first, d_accept, n, io, gpts, gex, wsum, nullptr, s);
         hipEventRecord(ev[1], s);
         if (hipEventSynchronize(ev[1]) == hipSuccess && hipEventElapsedTime(&t, ev[0], ev[1]) == hipSuccess)
             c->rlc_ms[0] += t;
-        checks(w.dA, groups, gpts, gacc, f, false, first, gex, sdesc, gamma);
+        rlc_checks(c, K, w, w.dA, groups, gpts, gacc, f, false, first, gex, sdesc, gamma, d_accept, io, s);
         if (!launched("batched verify launch")) return -1;
         if (!read_counts(cnt, w.cnt, 3, s)) return -1;
         if (first && cnt[2]) {           // level 2: weighted re-check of the failed groups, then the search
             const u32 ns = cnt[2];
             if (lev + 1 < 8) c->rlc_levels[lev + 1] = ns;
             c->rlc_nlev = ++lev + 1;
-            void *gp2 = c->rlc[5].get((size_t)ns * rec);   // (ns <= groups: the level-1 buffers are large enough)
+            void *gp2 = c->rlc[5].get((size_t)ns * K.rec);   // (ns <= groups: the level-1 buffers are large enough)
             hipEventRecord(ev[0], s);
-            if (ts) lcbk_ts_rlc_wsum(dim3(nblk(ns)), s, sdesc, ns, wsum, groups, gp2);
+            if (K.ts) lcbk_ts_rlc_wsum(dim3(nblk(ns)), s, sdesc, ns, wsum, groups, gp2);
             else lcbk_tpke_rlc_wsum(dim3(nblk(ns)), s, sdesc, ns, wsum, groups, gp2);
             hipEventRecord(ev[1], s);
             if (hipEventSynchronize(ev[1]) == hipSuccess && hipEventElapsedTime(&t, ev[0], ev[1]) == hipSuccess)
                 c->rlc_ms[0] += t;
-            checks((const uint8_t *)sdesc, ns, gp2, gacc, f, true, false, nullptr, sdesc, gamma);
+            rlc_checks(c, K, w, (const uint8_t *)sdesc, ns, gp2, gacc, f, true, false, nullptr, sdesc, gamma, d_accept,
+                       io, s);
             if (!launched("batched verify launch")) return -1;
             if (!read_counts(cnt + 1, w.cnt + 1, 1, s)) return -1;
         }
@@ -890,6 +987,7 @@ int rlc_levels(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, size_t n, 
     for (int i = 0; i < 2; i++)
         if (!st.valid || hipEventElapsedTime(&st.ms[i], c->rlc_ev[i], c->rlc_ev[i + 1]) != hipSuccess) st.ms[i] = -1.0f;
     for (int i = 0; i < 4; i++) st.ms[2 + i] = c->rlc_ms[i];
+    for (int i = 0; i < 4; i++) st.census[i] = c->rlc_census[i];
     return launched("batched verify launch") ? 0 : -1;
 }
 int tpke_verify_prepared_rlc(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_keys, size_t n_cts, const uint32_t *d_ct,
@@ -899,9 +997,12 @@ int tpke_verify_prepared_rlc(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_k
     c->rlc_nlev = 0;
     if (!n) return 0;
     RlcWs w;
-    if (rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, s)) return -1;
+    const RlcIo io{d_dec, d_ui, d_ct};
+    if (!rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G1_JAC_BYTES, n_keys, census_size(n, n_keys), s)) return -1;
     if (rlc_g2check(c, s)) return -1;
-    return rlc_levels(c, RLC_TPKE, w, d_accept, n, RlcIo{d_dec, d_ui}, s);
+    if (rlc_census(c, RLC_TPKE, w, d_accept, io, s)) return -1;   // before the randomisation: suspects skip it
+    if (rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, s)) return -1;
+    return rlc_levels(c, RLC_TPKE, w, d_accept, n, io, s);
 }
 bool fork_ready(lcb_ctx *c) {
     if (c->fork_ready) return true;
@@ -913,7 +1014,8 @@ bool fork_ready(lcb_ctx *c) {
     return true;
 }
 // prepare + batched verify in one call: the randomisation (needs only the keys) runs on the context's second
-// stream beside the per-ciphertext hashing / line sets (latency-bound: < 1 wave per SIMD for 50 K ciphertexts)
+// stream beside the per-ciphertext hashing / line sets and the census (latency-bound: < 1 wave per SIMD for 50 K
+// ciphertexts); a key the census marks suspect before the randomisation reaches its shares skips them
 int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const uint8_t *d_y, size_t n_keys,
                                  const uint8_t *d_u, const uint8_t *d_w, const uint8_t *d_v, const uint32_t *d_voff,
                                  size_t n_cts, const uint32_t *d_ct, const uint32_t *d_dec, const uint8_t *d_ui,
@@ -928,7 +1030,9 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
     if (!fork_ready(c)) return -1;
     if (n_keys) lcbk_g1_decompress(dim3(nblk(n_keys)), s, d_y, (u32)n_keys, keys);
     RlcWs w;
+    const RlcIo io{d_dec, d_ui, d_ct};
     if (n) {
+        if (!rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G1_JAC_BYTES, n_keys, census_size(n, n_keys), s)) return -1;
         hipEventRecord(c->fork_ev[0], s);
         hipStreamWaitEvent(c->aux, c->fork_ev[0], 0);
         if (rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, c->aux)) return -1;
@@ -946,8 +1050,9 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
     c->t_ready = true;
     if (!n) return 0;
     if (rlc_g2check(c, s)) return -1;      // still beside the randomisation on the second stream
+    if (rlc_census(c, RLC_TPKE, w, d_accept, io, s)) return -1;
     hipStreamWaitEvent(s, c->fork_ev[1], 0);
-    return rlc_levels(c, RLC_TPKE, w, d_accept, n, RlcIo{d_dec, d_ui}, s);
+    return rlc_levels(c, RLC_TPKE, w, d_accept, n, io, s);
 }
 
 // ------------------------------------------------------------------ threshold signatures
@@ -1012,10 +1117,14 @@ int ts_verify_prepared_rlc(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_pks
     c->rlc_nlev = 0;
     if (!n) return 0;
     RlcWs w;
+    const RlcIo io{d_pidx, d_sigs, d_midx};
+    if (!rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G2_JAC_BYTES, n_pks, census_size(n, n_pks), s)) return -1;
+    if (rlc_census(c, RLC_TS, w, d_accept, io, s)) return -1;
     if (ts_rlc_points_enqueue(c, w, d_accept, n, n_pks, n_msgs, d_sigs, d_midx, d_pidx, s)) return -1;
-    return rlc_levels(c, RLC_TS, w, d_accept, n, RlcIo{d_pidx, d_sigs}, s);
+    return rlc_levels(c, RLC_TS, w, d_accept, n, io, s);
 }
-// prepare + batched verify: the randomisation (keys only) beside the message hashing on the second stream
+// prepare + batched verify: the randomisation (keys only) beside the message hashing and the census on the second
+// stream
 int ts_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const uint8_t *d_pks, size_t n_pks,
                                const uint8_t *d_sigs, const uint8_t *d_msg, const uint32_t *d_moff, size_t n_msgs,
                                const uint32_t *d_midx, const uint32_t *d_pidx, hipStream_t s) {
@@ -1029,7 +1138,9 @@ int ts_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const ui
     if (!fork_ready(c)) return -1;
     if (n_pks) lcbk_g1_decompress(dim3(nblk(n_pks)), s, d_pks, (u32)n_pks, keys);
     RlcWs w;
+    const RlcIo io{d_pidx, d_sigs, d_midx};
     if (n) {
+        if (!rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G2_JAC_BYTES, n_pks, census_size(n, n_pks), s)) return -1;
         hipEventRecord(c->fork_ev[0], s);
         hipStreamWaitEvent(c->aux, c->fork_ev[0], 0);
         if (ts_rlc_points_enqueue(c, w, d_accept, n, n_pks, n_msgs, d_sigs, d_midx, d_pidx, c->aux)) return -1;
@@ -1043,8 +1154,9 @@ int ts_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const ui
     c->s_gen++;
     c->s_ready = true;
     if (!n) return 0;
+    if (rlc_census(c, RLC_TS, w, d_accept, io, s)) return -1;
     hipStreamWaitEvent(s, c->fork_ev[1], 0);
-    return rlc_levels(c, RLC_TS, w, d_accept, n, RlcIo{d_pidx, d_sigs}, s);
+    return rlc_levels(c, RLC_TS, w, d_accept, n, io, s);
 }
 
 // ------------------------------------------------------------------ Lagrange / assembly
@@ -1283,8 +1395,50 @@ extern "C" int lcb_tpke_batched_stats(uint32_t levels[8], float ms[6]) {
     return st.nlev;
 }
 extern "C" void lcb_set_batch_seed(const uint8_t *seed32) {
-    if (seed32) { memcpy(g_rlc_seed, seed32, 32); g_rlc_seed_set = true; }
+    // test hook: a fixed ChaCha key makes the batch exponents predictable, so it is honoured only when the process
+    // opted in (LCB_ALLOW_FIXED_BATCH_SEED=1); otherwise the call is ignored and the exponents stay secret
+    const char *e = getenv("LCB_ALLOW_FIXED_BATCH_SEED");
+    std::lock_guard<std::mutex> lk(g_seed_mu);
+    if (seed32 && e && e[0] == '1') { memcpy(g_rlc_seed, seed32, 32); g_rlc_seed_set = true; }
     else g_rlc_seed_set = false;
+}
+extern "C" void lcb_set_batch_census(size_t min_shares) { g_census_min.store(min_shares); }
+extern "C" void lcb_set_rlc_split_max(uint32_t max_groups) { g_split_max.store(max_groups); }
+extern "C" void lcb_set_coop_max(uint32_t max_checks) { g_coop_max.store(max_checks); }
+// the final exponentiation of n Fp12 values (144 words each, Montgomery form, AoS) by the one-lane kernel (coop = 0) or
+// the nine-lane kernel (coop = 1): tests compare the two bit for bit
+extern "C" int lcb_debug_final_exp(const uint32_t *in, size_t n, uint32_t *out, int coop) {
+    SYNC_CTX_OR(c, -1)
+    Enq q(c, c->stream);
+    if (!n || n > 65536) { set_err("debug final exp: 1..65536 values"); return -1; }
+    std::vector<u32> soa((size_t)144 * n * lcbk_fe_slots(), 0);
+    for (size_t i = 0; i < n; i++)
+        for (int w = 0; w < 144; w++) soa[((size_t)(w >> 2) * n + i) * 4 + (w & 3)] = in[144 * i + w];
+    u32 *d = (u32 *)c->out[0].get(soa.size() * 4);
+    uint8_t *acc = (uint8_t *)c->out[1].get(n);
+    if (!d || !acc) { set_err("device allocation failed"); return -1; }
+    hipMemcpyAsync(d, soa.data(), soa.size() * 4, hipMemcpyHostToDevice, q.s);
+    hipMemsetAsync(acc, 1, n, q.s);
+    if (coop) lcbk_coop_final_exp_check(q.s, d, (u32)n, acc, 1);
+    else lcbk_final_exp_check(dim3(nblk(n)), q.s, d, (u32)n, acc);
+    hipMemcpyAsync(soa.data(), d, (size_t)144 * n * 4, hipMemcpyDeviceToHost, q.s);
+    if (!sync_check(c, "debug final exp")) return -1;
+    for (size_t i = 0; i < n; i++)
+        for (int w = 0; w < 144; w++) out[144 * i + w] = soa[((size_t)(w >> 2) * n + i) * 4 + (w & 3)];
+    return 0;
+}
+extern "C" int lcb_ctx_batched_census(lcb_ctx *ctx, uint32_t out[4]) {
+    CTX_OR(c, ctx, -1)
+    std::lock_guard<std::recursive_mutex> lk(c->mu);
+    if (!c->rlc_ran) { set_err("batched verify: none has run in this context"); return -1; }
+    for (int i = 0; i < 4; i++) out[i] = c->rlc_census[i];
+    return 0;
+}
+extern "C" int lcb_batched_census(uint32_t out[4]) {
+    const RlcStats &st = t_rlc_stats;
+    if (!st.valid) { set_err("batched verify: none has completed on this thread"); return -1; }
+    for (int i = 0; i < 4; i++) out[i] = st.census[i];
+    return 0;
 }
 
 extern "C" int lcb_tpke_prepare_dev(const uint8_t *y_keys, size_t n_keys, const uint8_t *cts_u, const uint8_t *cts_w,

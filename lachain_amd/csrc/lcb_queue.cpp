@@ -64,7 +64,7 @@ struct lcb_queue {
 
 namespace {
 
-void run_tpke(lcb_queue *q, std::vector<TpkeItem> &items) {
+void run_tpke(lcb_queue *q, std::vector<TpkeItem> &items, size_t batched_min) {
     std::unordered_map<std::string, uint32_t> kidx, cidx;
     std::vector<uint8_t> keys, us, ws, vs, uis(48 * items.size());
     std::vector<uint32_t> voff(1, 0), ct(items.size()), dec(items.size());
@@ -87,7 +87,7 @@ void run_tpke(lcb_queue *q, std::vector<TpkeItem> &items) {
     std::vector<uint8_t> acc(items.size());
     if (vs.empty()) vs.push_back(0);
     int rc;
-    if (q->batched_min && items.size() >= q->batched_min) {
+    if (batched_min && items.size() >= batched_min) {
         // ciphertext-major order for the group checks (stable: a ciphertext's shares keep their submission order)
         std::vector<uint32_t> ord(items.size());
         for (size_t i = 0; i < ord.size(); i++) ord[i] = (uint32_t)i;
@@ -111,7 +111,7 @@ void run_tpke(lcb_queue *q, std::vector<TpkeItem> &items) {
     for (size_t i = 0; i < items.size(); i++) q->results[items[i].ticket] = rc ? -1 : (int8_t)(acc[i] != 0);
 }
 
-void run_ts(lcb_queue *q, std::vector<TsItem> &items) {
+void run_ts(lcb_queue *q, std::vector<TsItem> &items, size_t batched_min) {
     std::unordered_map<std::string, uint32_t> pidx, midx;
     std::vector<uint8_t> pks, msgs, sigs(96 * items.size());
     std::vector<uint32_t> moff(1, 0), mi(items.size()), pi(items.size());
@@ -131,7 +131,7 @@ void run_ts(lcb_queue *q, std::vector<TsItem> &items) {
     std::vector<uint8_t> acc(items.size());
     if (msgs.empty()) msgs.push_back(0);
     int rc;
-    if (q->batched_min && items.size() >= q->batched_min) {
+    if (batched_min && items.size() >= batched_min) {
         std::vector<uint32_t> ord(items.size());
         for (size_t i = 0; i < ord.size(); i++) ord[i] = (uint32_t)i;
         std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return mi[a] < mi[b]; });
@@ -173,6 +173,7 @@ void worker_loop(lcb_queue *q) {
         t.swap(q->tpke);
         s.swap(q->ts);
         q->flush_now = false;
+        const size_t batched_min = q->batched_min;     // read under the lock (lcb_queue_set_batched writes it)
         q->batches++;
         q->items += pending;
         if (pending > q->max_seen) q->max_seen = pending;
@@ -180,8 +181,8 @@ void worker_loop(lcb_queue *q) {
         int64_t top = 0;
         for (auto &x : t) top = x.ticket > top ? x.ticket : top;
         for (auto &x : s) top = x.ticket > top ? x.ticket : top;
-        if (!t.empty()) run_tpke(q, t);
-        if (!s.empty()) run_ts(q, s);
+        if (!t.empty()) run_tpke(q, t, batched_min);
+        if (!s.empty()) run_ts(q, s, batched_min);
         lk.lock();
         q->done_upto = top > q->done_upto ? top : q->done_upto;
         q->cv_done.notify_all();

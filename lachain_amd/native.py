@@ -79,6 +79,12 @@ _SIGS = {
                                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "lcb_tpke_batched_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_float)]),
     "lcb_set_batch_seed": (None, [ctypes.c_char_p]),
+    "lcb_set_batch_census": (None, [c_size]),
+    "lcb_set_coop_max": (None, [ctypes.c_uint32]),
+    "lcb_debug_final_exp": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), c_size, ctypes.POINTER(ctypes.c_uint32),
+                                           ctypes.c_int]),
+    "lcb_set_rlc_split_max": (None, [ctypes.c_uint32]),
+    "lcb_batched_census": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32)]),
     "lcb_tpke_partial_decrypt": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_u8p, c_u8p, c_u32p, c_size]),
     "lcb_tpke_encrypt_phase1": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_size]),
     "lcb_tpke_encrypt_phase2": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_u32p, c_size]),
@@ -694,8 +700,42 @@ def set_original_g2_cofactor(enable):
 
 
 def set_batch_seed(seed32=None):
-    """fixed ChaCha20 key for the batched verify's exponents (None: getrandom per call)"""
+    """fixed ChaCha20 key for the batched verify's exponents (None: getrandom per call); the library honours it only
+    when the process environment has LCB_ALLOW_FIXED_BATCH_SEED=1"""
     lib().lcb_set_batch_seed(seed32)
+
+
+def set_batch_census(min_shares):
+    """batched calls of >= min_shares shares start with the census of suspect keys (0 = never; default 16384)"""
+    lib().lcb_set_batch_census(min_shares)
+
+
+def set_rlc_split_max(max_groups):
+    """TPKE levels of <= max_groups groups use the split (one pair per lane) Miller kernel (default 32768)"""
+    lib().lcb_set_rlc_split_max(max_groups)
+
+
+def set_coop_max(max_checks):
+    """levels of <= max_checks group checks use the nine-lane cooperative kernels (0 = never; default 32768)"""
+    lib().lcb_set_coop_max(max_checks)
+
+
+def debug_final_exp(values, coop):
+    """final exponentiation of Fp12 values given as 144 u32 words each (Montgomery form) by the one-lane (coop=False)
+    or the nine-lane (coop=True) kernel; returns the 144-word results"""
+    n = len(values)
+    a = (ctypes.c_uint32 * (144 * n))(*[w for v in values for w in v])
+    out = (ctypes.c_uint32 * (144 * n))()
+    _check(lib().lcb_debug_final_exp(a, n, out, 1 if coop else 0), "debug_final_exp")
+    return [list(out[144 * i:144 * i + 144]) for i in range(n)]
+
+
+def batched_census():
+    """{census shares, suspect keys, level-1 groups, level-1 entries after the split} of this thread's last batched
+    verify"""
+    out = (ctypes.c_uint32 * 4)()
+    _check(lib().lcb_batched_census(out), "batched_census")
+    return list(out)
 
 
 def tpke_batched_stats():

@@ -145,14 +145,16 @@ def test_batched_malicious_kinds_tiled(nat, tdev):
     reps = 2048
     ct = np.tile(np.repeat(np.arange(4, dtype=np.uint32), 8), reps)
     dec = np.tile(np.arange(8, dtype=np.uint32), 4 * reps)
-    got = run_dev(nat, tdev, b, ct, dec, b"".join(base) * reps)
-    assert np.array_equal(got, np.tile(expect, reps))
-    levels, ms = nat.tpke_batched_stats()
-    assert levels[0] == 4 * reps and len(levels) >= 2
-    got = run_dev(nat, tdev, b, ct, dec, b"".join(base) * reps, fused=True)
-    assert np.array_equal(got, np.tile(expect, reps))
-    levels, ms = nat.tpke_batched_stats()
-    assert levels[0] == 4 * reps and len(levels) >= 2
+    for fused in (False, True):
+        got = run_dev(nat, tdev, b, ct, dec, b"".join(base) * reps, fused=fused)
+        assert np.array_equal(got, np.tile(expect, reps))
+        levels, ms = nat.tpke_batched_stats()
+        # 65,536 shares get a census (the first 512 shares checked one by one); decryptor 0's share is wrong in two of
+        # the four rows, so the census marks key 0 suspect and its shares become exact singles at level 1
+        m, n_susp, groups, entries = nat.batched_census()
+        assert m == 512 and n_susp == 1
+        assert groups == 4 * reps - m // 8 and entries == 2 * groups     # every row: its group + key 0's single
+        assert levels[0] == entries and len(levels) >= 2
 
 
 @pytest.mark.parametrize("fused", [False, True])
@@ -217,12 +219,14 @@ def test_batched_fixed_and_fresh_keys(nat):
             s = b.good[c][j] if (c * 7 + j) % 5 else b.bad[c][j]
             shares.append((c, j, s))
     exact = nat.tpke_verify_shares(b.yi, b.cts, shares)
+    os.environ["LCB_ALLOW_FIXED_BATCH_SEED"] = "1"      # the library ignores the hook without this opt-in
     try:
         for seed in (bytes(32), bytes(range(32))):
             nat.set_batch_seed(seed)
             assert nat.tpke_verify_shares(b.yi, b.cts, shares, batched=True) == exact
     finally:
         nat.set_batch_seed(None)
+        del os.environ["LCB_ALLOW_FIXED_BATCH_SEED"]
     assert nat.tpke_verify_shares(b.yi, b.cts, shares, batched=True) == exact
     assert exact.count(False) == 5
 
