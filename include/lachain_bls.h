@@ -295,6 +295,10 @@ void lcb_set_coop_max(uint32_t max_checks);
 /* test hook: final exponentiation of n Fp12 values (144 x u32 each, Montgomery form, field.hpp layout) by the one-lane
    (coop = 0) or the cooperative (coop = 1) kernel */
 int lcb_debug_final_exp(const uint32_t *in, size_t n, uint32_t *out, int coop);
+/* test hook: one cooperative Fp12 operation (op: 0 square, 1 cyclotomic square, 2 product, 3 product by the conjugate,
+   4..6 Frobenius 1..3, 7 inverse, 8 conjugate, 9 sparse line product, 10 final exponentiation) on n values a (and b),
+   with the one-lane field.hpp result beside it in ref */
+int lcb_debug_coop_op(int op, const uint32_t *a, const uint32_t *b, size_t n, uint32_t *out, uint32_t *ref);
 
 /* ------------------------------------------------------------------ explicit execution contexts
    A context owns the device workspaces of the prepare/verify, assembly, Lagrange and MSM calls below

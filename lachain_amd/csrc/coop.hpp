@@ -348,7 +348,7 @@ DI void cp_fp6_pair(const Cp &c, int xa, int ya, int xb, int yb) {
         const int pk = 9 * r + j;                      // product 0..11 (12..17: idle)
         const int m = pk < 6 ? pk : pk - 6;            // index within its fp6 product
         const int bx = pk < 6 ? xa : xb, by = pk < 6 ? ya : yb;
-        const int i0 = (int)((0x000120u >> (4 * m)) & 15), i1 = (int)((0x210000u >> (4 * m)) & 15);
+        const int i0 = (int)((0x001210u >> (4 * m)) & 15), i1 = (int)((0x212000u >> (4 * m)) & 15);
         const bool two = m >= 3;
         const bool on = pk < 12;
         cp_prod(c, bx + i0, two ? bx + i1 : S_Z, by + i0, two ? by + i1 : S_Z, false, on ? pk : -1);

@@ -93,6 +93,59 @@ extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_final_exp_check(u3
     if (live && c.j == 0 && accept) accept[item] = accept[item] && one;
 }
 
+// ---------------------------------------------------------------- test hook: one cooperative operation vs field.hpp
+// op: 0 sqr12, 1 cyc_sqr, 2 mul12, 3 mul12 (conj a), 4..6 frob1..3, 7 inverse, 8 conj, 9 line (b, c = coefficients 0, 1
+// of b), 10 final exponentiation.  a in park slot 0 of ws (6 slots), b in b_soa; out = cooperative result, ref = the
+// one-lane field.hpp / pairing.hpp result (computed by lane 0 of each group)
+extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_debug(int op, u32 *ws, const u32 *b_soa, u32 n, u32 *out,
+                                                                   u32 *ref) {
+    __shared__ uint4 lds[CP_LDS_QUADS];
+    const Cp c = cp_init(lds);
+    const u32 item = blockIdx.x * CP_G + c.g;
+    const bool live = c.g < CP_G && item < n;
+    const size_t it = live ? item : 0;
+    if (c.j == 0) cp_put(c, S_Z, fp2_zero());
+    cp_sync();
+    fp12 fa, fb, fr;
+    if (c.j == 0) {
+        fp12_load_soa(fa, ws, n, it);
+        fp12_load_soa(fb, b_soa, n, it);
+    }
+    fp2 R;
+    park_get(R, ws, n, it, c.j);
+    if (op == 0) { CpEval ev; ev.on = false; ev.x = fp2_zero(); ev.y = fp2_zero(); cp_sqr12(R, c, ev); }
+    else if (op == 1) cp_cyc_sqr(R, c);
+    else if (op == 2 || op == 3) cp_mul12(R, c, op == 3, b_soa, n, it);
+    else if (op >= 4 && op <= 6) cp_frob(R, c, op - 3);
+    else if (op == 7) cp_inv(R, c);
+    else if (op == 8) cp_conj(R, c);
+    else if (op == 9) {
+        fp2 b, cc;
+        park_get(b, b_soa, n, it, 0);
+        park_get(cc, b_soa, n, it, 1);
+        if (c.j == 0) { cp_put(c, S_LE, b); cp_put(c, S_LE + 1, cc); }
+        cp_sync();
+        cp_line(R, c, S_LE, S_LE + 1);
+    } else {
+        cp_final_exp(R, c, ws, n, it, live);
+    }
+    park_put(out, n, it, c.j, live, R);
+    if (live && c.j == 0) {
+        if (op == 0) fp12_sqr_n(fr, fa);
+        else if (op == 1) fp12_cyc_sqr_n(fr, fa);
+        else if (op == 2) fp12_mul_n(fr, fa, fb);
+        else if (op == 3) { fp12_conj(fa, fa); fp12_mul_n(fr, fa, fb); }
+        else if (op == 4) fp12_frob1_n(fr, fa);
+        else if (op == 5) fp12_frob2_n(fr, fa);
+        else if (op == 6) fp12_frob3_n(fr, fa);
+        else if (op == 7) fp12_inv_n(fr, fa);
+        else if (op == 8) fp12_conj(fr, fa);
+        else if (op == 9) { fr = fa; fp12_mul_line_n(fr, fb.c0.c0, fb.c0.c1); }
+        else final_exp(fr, fa);
+        fp12_store_soa(ref, n, it, fr);
+    }
+}
+
 // ---------------------------------------------------------------- host launch wrappers
 extern "C" void lcbk_coop_tpke_miller(hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups,
                                       u32 *f_soa, uint8_t *gacc, uint8_t *fb) {
@@ -105,4 +158,8 @@ extern "C" void lcbk_coop_tpke_miller(hipStream_t s, const u32 *lines, const voi
 extern "C" void lcbk_coop_final_exp_check(hipStream_t s, u32 *park, u32 n, uint8_t *accept, int keep_result) {
     dim3 grid((n + CP_G - 1) / CP_G);
     hipLaunchKernelGGL(k_coop_final_exp_check, grid, dim3(CP_BLOCK), 0, s, park, n, accept, keep_result);
+}
+extern "C" void lcbk_coop_debug(hipStream_t s, int op, u32 *ws, const u32 *b_soa, u32 n, u32 *out, u32 *ref) {
+    dim3 grid((n + CP_G - 1) / CP_G);
+    hipLaunchKernelGGL(k_coop_debug, grid, dim3(CP_BLOCK), 0, s, op, ws, b_soa, n, out, ref);
 }

@@ -80,6 +80,7 @@ extern "C" void lcbk_rlc_census_stats(hipStream_t s, const u32 *key_idx, u32 m, 
 extern "C" void lcbk_rlc_suspect_split(hipStream_t s, const void *desc, u32 n_groups, const u32 *key_idx, u32 n_keys, const u32 *susp, const uint8_t *accept, void *out, u32 *count);
 extern "C" size_t lcbk_ts_grp_bytes();
 extern "C" void lcbk_coop_tpke_miller(hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups, u32 *f_soa, uint8_t *gacc, uint8_t *fb);
+extern "C" void lcbk_coop_debug(hipStream_t s, int op, u32 *ws, const u32 *b_soa, u32 n, u32 *out, u32 *ref);
 extern "C" void lcbk_coop_final_exp_check(hipStream_t s, u32 *park, u32 n, uint8_t *accept, int keep_result);
 extern "C" void lcbk_op(dim3 grid, hipStream_t s, int op, u32 *io, int orig_cof);
 

@@ -1405,6 +1405,34 @@ extern "C" void lcb_set_batch_seed(const uint8_t *seed32) {
 extern "C" void lcb_set_batch_census(size_t min_shares) { g_census_min.store(min_shares); }
 extern "C" void lcb_set_rlc_split_max(uint32_t max_groups) { g_split_max.store(max_groups); }
 extern "C" void lcb_set_coop_max(uint32_t max_checks) { g_coop_max.store(max_checks); }
+// one cooperative Fp12 operation (k_coop_debug) on n values a (and b) vs the one-lane field.hpp routine: AoS in / out
+extern "C" int lcb_debug_coop_op(int op, const uint32_t *a, const uint32_t *b, size_t n, uint32_t *out, uint32_t *ref) {
+    SYNC_CTX_OR(c, -1)
+    Enq q(c, c->stream);
+    if (!n || n > 65536) { set_err("debug coop op: 1..65536 values"); return -1; }
+    const size_t W = (size_t)144 * n;
+    std::vector<u32> sa(W * 6, 0), sb(W), so(W), sr(W);
+    for (size_t i = 0; i < n; i++)
+        for (int w = 0; w < 144; w++) {
+            sa[((size_t)(w >> 2) * n + i) * 4 + (w & 3)] = a[144 * i + w];
+            sb[((size_t)(w >> 2) * n + i) * 4 + (w & 3)] = b[144 * i + w];
+        }
+    u32 *da = (u32 *)c->out[0].get(W * 24), *db = (u32 *)c->out[1].get(W * 4), *dout = (u32 *)c->out[2].get(W * 4),
+        *dref = (u32 *)c->out[3].get(W * 4);
+    if (!da || !db || !dout || !dref) { set_err("device allocation failed"); return -1; }
+    hipMemcpyAsync(da, sa.data(), W * 24, hipMemcpyHostToDevice, q.s);
+    hipMemcpyAsync(db, sb.data(), W * 4, hipMemcpyHostToDevice, q.s);
+    lcbk_coop_debug(q.s, op, da, db, (u32)n, dout, dref);
+    hipMemcpyAsync(so.data(), dout, W * 4, hipMemcpyDeviceToHost, q.s);
+    hipMemcpyAsync(sr.data(), dref, W * 4, hipMemcpyDeviceToHost, q.s);
+    if (!sync_check(c, "debug coop op")) return -1;
+    for (size_t i = 0; i < n; i++)
+        for (int w = 0; w < 144; w++) {
+            out[144 * i + w] = so[((size_t)(w >> 2) * n + i) * 4 + (w & 3)];
+            ref[144 * i + w] = sr[((size_t)(w >> 2) * n + i) * 4 + (w & 3)];
+        }
+    return 0;
+}
 // the final exponentiation of n Fp12 values (144 words each, Montgomery form, AoS) by the one-lane kernel (coop = 0) or
 // the nine-lane kernel (coop = 1): tests compare the two bit for bit
 extern "C" int lcb_debug_final_exp(const uint32_t *in, size_t n, uint32_t *out, int coop) {

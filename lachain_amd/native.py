@@ -81,6 +81,8 @@ _SIGS = {
     "lcb_set_batch_seed": (None, [ctypes.c_char_p]),
     "lcb_set_batch_census": (None, [c_size]),
     "lcb_set_coop_max": (None, [ctypes.c_uint32]),
+    "lcb_debug_coop_op": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                                         c_size, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
     "lcb_debug_final_exp": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), c_size, ctypes.POINTER(ctypes.c_uint32),
                                            ctypes.c_int]),
     "lcb_set_rlc_split_max": (None, [ctypes.c_uint32]),
@@ -728,6 +730,17 @@ def debug_final_exp(values, coop):
     out = (ctypes.c_uint32 * (144 * n))()
     _check(lib().lcb_debug_final_exp(a, n, out, 1 if coop else 0), "debug_final_exp")
     return [list(out[144 * i:144 * i + 144]) for i in range(n)]
+
+
+def debug_coop_op(op, a_values, b_values):
+    """one cooperative Fp12 operation (lcb_debug_coop_op) -> (cooperative results, one-lane results)"""
+    n = len(a_values)
+    a = (ctypes.c_uint32 * (144 * n))(*[w for v in a_values for w in v])
+    b = (ctypes.c_uint32 * (144 * n))(*[w for v in b_values for w in v])
+    out = (ctypes.c_uint32 * (144 * n))()
+    ref = (ctypes.c_uint32 * (144 * n))()
+    _check(lib().lcb_debug_coop_op(op, a, b, n, out, ref), "debug_coop_op")
+    return ([list(out[144 * i:144 * i + 144]) for i in range(n)], [list(ref[144 * i:144 * i + 144]) for i in range(n)])
 
 
 def batched_census():

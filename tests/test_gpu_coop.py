@@ -43,6 +43,29 @@ def words_to_raw(words):
     return b
 
 
+OPS = {0: "sqr12", 1: "cyc_sqr", 2: "mul12", 3: "mul12_conj", 4: "frob1", 5: "frob2", 6: "frob3", 7: "inv",
+       8: "conj", 9: "line", 10: "final_exp"}
+
+
+def test_coop_ops_match_one_lane(nat):
+    """every cooperative Fp12 operation on 16 random values (and one unitary value for the cyclotomic square) equals
+    the one-lane field.hpp / pairing.hpp routine, word for word"""
+    rng = random.Random(99)
+    rnd = lambda: raw_to_words(b"".join(rng.randrange(o.P).to_bytes(48, "little") for _ in range(12)))
+    a = [rnd() for _ in range(16)]
+    b = [rnd() for _ in range(16)]
+    # a unitary value (final exponentiation output) for the cyclotomic square
+    u = raw_to_words(o.pairing(o.g1_gen(), o.g2_gen()))
+    bad = []
+    for op, name in OPS.items():
+        aa = [u] * 16 if op == 1 else a
+        out, ref = nat.debug_coop_op(op, aa, b)
+        if out != ref:
+            bad.append((name, [i for i in range(16) if out[i] != ref[i]][:4],
+                        [w // 24 for w in range(144) if out[0][w] != ref[0][w]][:6]))
+    assert not bad, bad
+
+
 def test_coop_final_exp_bit_exact(nat):
     """39 random Fp12 values, 1 and a real Miller value: nine-lane == one-lane == oracle"""
     rng = random.Random(20261017)
