@@ -75,10 +75,9 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_rlc_miller_fallback(const u32 *line
     fp12_store_soa(f_soa, n_groups, g, f);
 }
 
-// accept[i] &= (final_exp(f_i) == 1) for f_i in park slot 0 (slots 0..4 as working space); keep_result: slot 0 <- the
-// final exponentiation (the GT value) instead of only the decision
-extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_final_exp_check(u32 *park, u32 n, uint8_t *accept,
-                                                                             int keep_result) {
+// accept[i] &= (final_exp(f_i) == 1) for f_i in park slot 0 (slots 0..4 as working space); slot 0 <- the final
+// exponentiation (the GT value: the level-2 search of k_batch.hip compares these), as k_final_exp_check leaves it
+extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_final_exp_check(u32 *park, u32 n, uint8_t *accept) {
     __shared__ uint4 lds[CP_LDS_QUADS];
     const Cp c = cp_init(lds);
     const u32 item = blockIdx.x * CP_G + c.g;
@@ -89,7 +88,7 @@ extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_final_exp_check(u3
     fp2 R;
     cp_final_exp(R, c, park, n, it, live);
     const bool one = cp_is_one(R, c);
-    if (keep_result) park_put(park, n, it, c.j, live, R);
+    park_put(park, n, it, c.j, live, R);
     if (live && c.j == 0 && accept) accept[item] = accept[item] && one;
 }
 
@@ -155,9 +154,9 @@ extern "C" void lcbk_coop_tpke_miller(hipStream_t s, const u32 *lines, const voi
     grid = dim3((n_groups + LCB_BLOCK - 1) / LCB_BLOCK);
     LCB_LAUNCH(k_rlc_miller_fallback, lines, (const uint4 *)desc, (const g1a_st *)gpts, n_groups, f_soa, fb);
 }
-extern "C" void lcbk_coop_final_exp_check(hipStream_t s, u32 *park, u32 n, uint8_t *accept, int keep_result) {
+extern "C" void lcbk_coop_final_exp_check(hipStream_t s, u32 *park, u32 n, uint8_t *accept) {
     dim3 grid((n + CP_G - 1) / CP_G);
-    hipLaunchKernelGGL(k_coop_final_exp_check, grid, dim3(CP_BLOCK), 0, s, park, n, accept, keep_result);
+    hipLaunchKernelGGL(k_coop_final_exp_check, grid, dim3(CP_BLOCK), 0, s, park, n, accept);
 }
 extern "C" void lcbk_coop_debug(hipStream_t s, int op, u32 *ws, const u32 *b_soa, u32 n, u32 *out, u32 *ref) {
     dim3 grid((n + CP_G - 1) / CP_G);

@@ -81,7 +81,7 @@ extern "C" void lcbk_rlc_suspect_split(hipStream_t s, const void *desc, u32 n_gr
 extern "C" size_t lcbk_ts_grp_bytes();
 extern "C" void lcbk_coop_tpke_miller(hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups, u32 *f_soa, uint8_t *gacc, uint8_t *fb);
 extern "C" void lcbk_coop_debug(hipStream_t s, int op, u32 *ws, const u32 *b_soa, u32 n, u32 *out, u32 *ref);
-extern "C" void lcbk_coop_final_exp_check(hipStream_t s, u32 *park, u32 n, uint8_t *accept, int keep_result);
+extern "C" void lcbk_coop_final_exp_check(hipStream_t s, u32 *park, u32 n, uint8_t *accept);
 extern "C" void lcbk_op(dim3 grid, hipStream_t s, int op, u32 *io, int orig_cof);
 
 // sizes of the device records the host allocates

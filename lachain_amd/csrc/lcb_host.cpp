@@ -872,7 +872,7 @@ void rlc_checks(lcb_ctx *c, const RlcKindInfo &K, RlcWs &w, const uint8_t *desc,
             lcbk_tpke_rlc_miller(dim3(nblk(m)), s, K.lines, desc + 16 * o, (const uint8_t *)gpts + K.rec * o, (u32)m, f,
                                  gacc + o);
         hipEventRecord(ev[2], s);
-        if (coop) lcbk_coop_final_exp_check(s, f, (u32)m, gacc + o, 0);
+        if (coop) lcbk_coop_final_exp_check(s, f, (u32)m, gacc + o);
         else lcbk_final_exp_check(dim3(nblk(m)), s, f, (u32)m, gacc + o);
         hipEventRecord(ev[3], s);
         if (search_stage)
@@ -1447,7 +1447,7 @@ extern "C" int lcb_debug_final_exp(const uint32_t *in, size_t n, uint32_t *out, 
     if (!d || !acc) { set_err("device allocation failed"); return -1; }
     hipMemcpyAsync(d, soa.data(), soa.size() * 4, hipMemcpyHostToDevice, q.s);
     hipMemsetAsync(acc, 1, n, q.s);
-    if (coop) lcbk_coop_final_exp_check(q.s, d, (u32)n, acc, 1);
+    if (coop) lcbk_coop_final_exp_check(q.s, d, (u32)n, acc);
     else lcbk_final_exp_check(dim3(nblk(n)), q.s, d, (u32)n, acc);
     hipMemcpyAsync(soa.data(), d, (size_t)144 * n * 4, hipMemcpyDeviceToHost, q.s);
     if (!sync_check(c, "debug final exp")) return -1;
