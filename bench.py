@@ -260,7 +260,8 @@ def run_tpke_patterns(args, nat, torch, dev, world, inp, n, n_cts, n_dec):
                 m6 = (ctypes.c_float * 6)()
                 k = lib.lcb_ctx_tpke_batched_stats(ctx.ptr, lv, m6)
                 cs = (ctypes.c_uint32 * 4)()
-                lib.lcb_ctx_batched_census(ctx.ptr, cs)
+                if lib.lcb_ctx_batched_census(ctx.ptr, cs) != 0:
+                    raise RuntimeError(nat.last_error())
                 rec[label]["levels"] = list(lv[:k])
                 rec[label]["census"] = {"shares": cs[0], "suspect_keys": cs[1], "level1_groups": cs[2],
                                         "level1_entries_after_split": cs[3]}
@@ -1398,6 +1399,8 @@ def main():
     ap.add_argument("--pattern-steps", type=int, default=2,
                     help="timed steps per Byzantine pattern and path (0 = skip the patterns)")
     ap.add_argument("--patterns", default="", help="comma-separated subset of the Byzantine patterns (default all)")
+    ap.add_argument("--coop-max", type=int, default=-1,
+                    help="levels of <= this many group checks on the nine-lane cooperative kernels (-1: library default)")
     ap.add_argument("--msm-sizes", default=f"{1 << 20},{1 << 24}",
                     help="total G1 MSM points per measurement, sharded over ranks (empty = skip)")
     ap.add_argument("--msm-steps", type=int, default=3)
@@ -1432,6 +1435,8 @@ def main():
     dev = torch.device("cuda", local_rank)
     nat.load(False).lcb_set_device(local_rank)
     nat.lib()
+    if args.coop_max >= 0:
+        nat.set_coop_max(args.coop_max)
 
     t_gen = time.perf_counter()
     inp = make_inputs(nat, rank, args.shares, args.n, args.f, args.vlen)
