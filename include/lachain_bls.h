@@ -286,9 +286,6 @@ void lcb_set_batch_census(size_t min_shares);
 /* census of the last batched verify: {census shares, suspect keys, level-1 groups, level-1 entries after moving the
    suspect keys' shares to single checks} (lcb_ctx_ form: that context's last one) */
 int lcb_batched_census(uint32_t out[4]);
-/* TPKE levels of at most max_groups groups run their Miller loops as two single pairs per group (one pair per lane;
-   default 32768), larger ones as the shared-squaring pair (test hook to cover both kernels) */
-void lcb_set_rlc_split_max(uint32_t max_groups);
 /* levels of at most max_checks group checks run on the cooperative kernels (k_coop.hip: nine lanes per pairing check,
    lower latency below one wave per SIMD); 0 = always one check per lane.  Default 32768. */
 void lcb_set_coop_max(uint32_t max_checks);

@@ -483,11 +483,7 @@ DN bool g2_decompress(g2a &out, const uint8_t *b) {
     fp2_mul(t, t, x);
     fp2_load_const(b2, LCB_B2);
     fp2_add(t, t, b2);
-#ifdef LCB_G2_DECOMP_SQRT_MCL
-    if (!fp2_sqrt(y, t)) return false;
-#else
     if (!fp2_sqrt_any(y, t)) return false;            // the sign is fixed below, so any root serves
-#endif
     if (fp_is_odd(y.a) != odd) fp2_neg(y, y);
     out.x = x; out.y = y; out.inf = false;
     return true;

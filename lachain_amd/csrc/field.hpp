@@ -98,24 +98,12 @@ DI void fp_neg_c(fp &r, const fp &a) {
     fp z = fp_zero();
     fp_sub_c(r, z, a);
 }
-#ifndef LCB_C_ADD
 DI void fp_add(fp &r, const fp &a, const fp &b) { lcb_fp_add_asm(r.v, a.v, b.v); }  // 36-instruction VCC chain
-#else
-DI void fp_add(fp &r, const fp &a, const fp &b) { fp_add_c(r, a, b); }
-#endif
 // r = a + b without reduction (< 2p): only as a Montgomery multiplicand (R > 4p)
 DI void fp_add_nr(fp &r, const fp &a, const fp &b) { lcb_fp_add_nr_asm(r.v, a.v, b.v); }
 DI void fp_dbl(fp &r, const fp &a) { fp_add(r, a, a); }
-#ifndef LCB_C_SUB
 DI void fp_sub(fp &r, const fp &a, const fp &b) { lcb_fp_sub_asm(r.v, a.v, b.v); }
-#else
-DI void fp_sub(fp &r, const fp &a, const fp &b) { fp_sub_c(r, a, b); }
-#endif
-#ifndef LCB_C_NEG
 DI void fp_neg(fp &r, const fp &a) { lcb_fp_neg_asm(r.v, a.v); }
-#else
-DI void fp_neg(fp &r, const fp &a) { fp_neg_c(r, a); }
-#endif
 
 DI u32x12 fp_to_v(const fp &a) {
     u32x12 v;
@@ -130,14 +118,9 @@ DI fp fp_from_v(const u32x12 &v) {
     return a;
 }
 DI void fp_mul(fp &r, const fp &a, const fp &b) { r = fp_from_v(lcb_asm_fp_mul(fp_to_v(a), fp_to_v(b))); }
-#ifndef LCB_FP_SQR_AS_MUL
 // dedicated Montgomery square (tools/gen_asm.py lcb_r_fp_sqr: 78 + 144 products, 551 instructions against 662)
 DI void fp_sqr(fp &r, const fp &a) { r = fp_from_v(lcb_asm_fp_sqr(fp_to_v(a))); }
 #define LCB_POW_SQR(x) lcb_asm_fp_sqr(x)
-#else
-DI void fp_sqr(fp &r, const fp &a) { fp_mul(r, a, a); }
-#define LCB_POW_SQR(x) lcb_asm_fp_mul(x, x)
-#endif
 
 // conversions between canonical integers (12 LE limbs) and Montgomery form
 DI void fp_from_raw(fp &r, const fp &raw) {
@@ -166,19 +149,6 @@ DI bool fp_is_odd(const fp &a) {
 }
 // a^e for an exponent given as 12 LE limbs in constant memory.  The exponent bits are wave-uniform, so no
 // branch diverges.  Non-inlined, operands in VGPRs.
-#ifdef LCB_FP_POW_BINARY
-// left-to-right binary: ~381 squarings + popcount(e) products (~190 for p - 2)
-DN u32x12 lcb_fp_pow_v(u32x12 av, const u32 *e) {
-    int top = 383;
-    while (top > 0 && !((e[top >> 5] >> (top & 31)) & 1)) top--;
-    u32x12 acc = av;
-    for (int i = top - 1; i >= 0; i--) {
-        acc = LCB_POW_SQR(acc);
-        if ((e[i >> 5] >> (i & 31)) & 1) acc = lcb_asm_fp_mul(acc, av);
-    }
-    return acc;
-}
-#else
 // left-to-right sliding window of width 4 over the odd powers a, a^3, ..., a^15 (8 precomputation products):
 // ~381 squarings + ~76 window products instead of ~190 for p - 2, (p + 1)/4 and (p - 1)/2.  The table is
 // selected by a uniform switch over named registers, never by a dynamic register index (that would go to scratch).
@@ -231,7 +201,6 @@ DN u32x12 lcb_fp_pow_v(u32x12 av, const u32 *e) {
     }
     return acc;
 }
-#endif
 DI void fp_pow_const(fp &r, const fp &a, const u32 *e) { r = fp_from_v(lcb_fp_pow_v(fp_to_v(a), e)); }
 DI void fp_inv(fp &r, const fp &a) { fp_pow_const(r, a, LCB_P_MINUS_2); }
 // mcl Fp::squareRoot for p = 3 mod 4: y = a^((p+1)/4), valid iff y^2 == a
@@ -251,18 +220,11 @@ DI int fp_legendre(const fp &a) {
 }
 
 // ------------------------------------------------------------------------------------------------ Fp2
-#ifndef LCB_FP2_SPLIT_CHAINS
 // both components in one interleaved pair of carry chains (asm_routines.hpp, tools/gen_asm.py)
 DI void fp2_add(fp2 &r, const fp2 &x, const fp2 &y) { lcb_fp2_add_asm(r.a.v, r.b.v, x.a.v, x.b.v, y.a.v, y.b.v); }
 DI void fp2_sub(fp2 &r, const fp2 &x, const fp2 &y) { lcb_fp2_sub_asm(r.a.v, r.b.v, x.a.v, x.b.v, y.a.v, y.b.v); }
 DI void fp2_dbl(fp2 &r, const fp2 &x) { lcb_fp2_add_asm(r.a.v, r.b.v, x.a.v, x.b.v, x.a.v, x.b.v); }
 DI void fp2_neg(fp2 &r, const fp2 &x) { lcb_fp2_neg_asm(r.a.v, r.b.v, x.a.v, x.b.v); }
-#else
-DI void fp2_add(fp2 &r, const fp2 &x, const fp2 &y) { fp_add(r.a, x.a, y.a); fp_add(r.b, x.b, y.b); }
-DI void fp2_sub(fp2 &r, const fp2 &x, const fp2 &y) { fp_sub(r.a, x.a, y.a); fp_sub(r.b, x.b, y.b); }
-DI void fp2_dbl(fp2 &r, const fp2 &x) { fp_add(r.a, x.a, x.a); fp_add(r.b, x.b, x.b); }
-DI void fp2_neg(fp2 &r, const fp2 &x) { fp_neg(r.a, x.a); fp_neg(r.b, x.b); }
-#endif
 DI void fp2_conj(fp2 &r, const fp2 &x) { r.a = x.a; fp_neg(r.b, x.b); }
 DI bool fp2_is_zero(const fp2 &x) { return fp_is_zero(x.a) && fp_is_zero(x.b); }
 DI bool fp2_eq(const fp2 &x, const fp2 &y) { return fp_eq(x.a, y.a) && fp_eq(x.b, y.b); }
@@ -297,14 +259,7 @@ DI void fp_mul2(fp &r0, const fp &a0, const fp &b0, fp &r1, const fp &a1, const 
     r1 = fp_from_v(x1);
 }
 DI void fp2_mul_xi(fp2 &r, const fp2 &x) { // (a + b i)(1 + i) = (a - b) + (a + b) i
-#ifndef LCB_FP2_SPLIT_CHAINS
     lcb_fp2_mul_xi_asm(r.a.v, r.b.v, x.a.v, x.b.v);
-#else
-    fp t;
-    fp_sub(t, x.a, x.b);
-    fp_add(r.b, x.a, x.b);
-    r.a = t;
-#endif
 }
 DI void fp2_norm(fp &r, const fp2 &x) {
     fp t, u;
@@ -392,22 +347,9 @@ DI bool fp2_sqrt_any(fp2 &y, const fp2 &x) {
 }
 
 // ------------------------------------------------------------------------------------------------ Fp6
-// LCB_FP6_THREE_CHAINS: measured 2 % slower in k_tpke_miller (231 vs 227 ms per 1M shares): the wider operand
-// set of the three-chain blocks adds spills that cost more than the removed s_nop slots.  Off by default.
-#ifdef LCB_FP6_THREE_CHAINS
-// the three a-components, then the three b-components, as three interleaved carry chains (no s_nop)
-DI void fp6_add(fp6 &r, const fp6 &x, const fp6 &y) {
-    lcb_fp3_add_asm(r.c0.a.v, r.c1.a.v, r.c2.a.v, x.c0.a.v, x.c1.a.v, x.c2.a.v, y.c0.a.v, y.c1.a.v, y.c2.a.v);
-    lcb_fp3_add_asm(r.c0.b.v, r.c1.b.v, r.c2.b.v, x.c0.b.v, x.c1.b.v, x.c2.b.v, y.c0.b.v, y.c1.b.v, y.c2.b.v);
-}
-DI void fp6_sub(fp6 &r, const fp6 &x, const fp6 &y) {
-    lcb_fp3_sub_asm(r.c0.a.v, r.c1.a.v, r.c2.a.v, x.c0.a.v, x.c1.a.v, x.c2.a.v, y.c0.a.v, y.c1.a.v, y.c2.a.v);
-    lcb_fp3_sub_asm(r.c0.b.v, r.c1.b.v, r.c2.b.v, x.c0.b.v, x.c1.b.v, x.c2.b.v, y.c0.b.v, y.c1.b.v, y.c2.b.v);
-}
-#else
+// (three interleaved carry chains per Fp6 addition measured 2 % slower in k_tpke_miller: more spills)
 DI void fp6_add(fp6 &r, const fp6 &x, const fp6 &y) { fp2_add(r.c0, x.c0, y.c0); fp2_add(r.c1, x.c1, y.c1); fp2_add(r.c2, x.c2, y.c2); }
 DI void fp6_sub(fp6 &r, const fp6 &x, const fp6 &y) { fp2_sub(r.c0, x.c0, y.c0); fp2_sub(r.c1, x.c1, y.c1); fp2_sub(r.c2, x.c2, y.c2); }
-#endif
 DI void fp6_neg(fp6 &r, const fp6 &x) { fp2_neg(r.c0, x.c0); fp2_neg(r.c1, x.c1); fp2_neg(r.c2, x.c2); }
 DI void fp6_mul(fp6 &r, const fp6 &a, const fp6 &b) {
     fp2 t0, t1, t2, s0, s1, c0, c1, c2;

@@ -161,9 +161,6 @@ DI void g1_mul_ab_inl(g1 &r, const g1a &P, u32 a, u32 b) {
         if (da | db) jac_add_aff(r, r, da ? (db ? b2x : P.x) : bx, (da & db) ? ny : P.y);
     }
 }
-#ifndef LCB_RLC_POINTS_WAVES
-#define LCB_RLC_POINTS_WAVES 1
-#endif
 // G2 form of g1_mul_ab_inl: a S + b psi^4(S) with the point arithmetic inlined
 DI void g2_mul_ab_inl(g2 &r, const g2a &S, u32 a, u32 b) {
     jac_set_inf(r);
@@ -290,7 +287,7 @@ DI bool ktab_usable(const uint8_t *ktab_ok, u32 k) {      // all 32 lanes of the
 // the decompressed keys and may run beside the ciphertext preparation)
 // Shares [i0, n) (the census decides [0, i0) exactly); a share of a key the census has already marked suspect only
 // gets its validity (it is checked on its own).
-extern "C" __global__ void __launch_bounds__(LCB_BLOCK) __attribute__((amdgpu_waves_per_eu(LCB_RLC_POINTS_WAVES)))
+extern "C" __global__ void __launch_bounds__(LCB_BLOCK) __attribute__((amdgpu_waves_per_eu(1)))
 k_tpke_rlc_points(u32 n_cts, const g1a_st *keys, u32 n_keys, const u32 *ct_idx,
                                                        const u32 *dec_idx, const uint8_t *ui, u32 i0, u32 n,
                                                        rlc_key key, u32 *rU, u32 *rY, uint8_t *accept,
@@ -477,45 +474,6 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_rlc_miller(const u32 *lines, c
         miller2_sets_fallback(f, lsH, P, lsW, Q);
     }
     fp12_store_soa(f_soa, n_groups, g, f);
-    gacc[g] = 1;
-}
-
-// Small levels (re-checks, singles): two lanes per group, one Miller pair each.  Below one wave per SIMD a level costs
-// one lane's serial work, and one pair (63 squarings + 68 line products) is shorter than the shared-squaring pair
-// (63 squarings + 136 line products); k_rlc_fpair_mul then forms f_H f_W — the same Fp12 element as
-// k_tpke_rlc_miller's (the Miller function is multiplicative and both use the same lines).
-extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_rlc_miller_split(const u32 *lines, const uint4 *desc,
-                                                                  const g1a_st *gpts, u32 n_groups, u32 *f_soa) {
-    u32 t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= 2 * n_groups) return;
-    u32 g = t >> 1, side = t & 1;
-    u32 c = desc[g].z;
-    g1a P;
-    st_to_g1a(P, gpts[2 * (size_t)g + side]);
-    const u32 *ls = lines + (size_t)(2 * c + side) * LCB_LINESET_WORDS;
-    fp12 f;
-    if (P.inf) {
-        f = fp12_one();
-    } else if (lineset_normalised(ls)) {
-        LinesNorm sn{ls};
-        miller1(f, sn, P);
-    } else {
-        g2a Q;
-        lineset_point(Q, ls);
-        LinesOnTheFly so;
-        so.init(Q);
-        miller1(f, so, P);
-    }
-    fp12_store_soa(f_soa + (size_t)side * n_groups * 144, n_groups, g, f);
-}
-extern "C" __global__ void LCB_BOUNDS k_rlc_fpair_mul(u32 *f_soa, u32 n_groups, uint8_t *gacc) {
-    u32 g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= n_groups) return;
-    fp12 a, b;
-    fp12_load_soa(a, f_soa, n_groups, g);
-    fp12_load_soa(b, f_soa + (size_t)n_groups * 144, n_groups, g);
-    fp12_mul(a, a, b);
-    fp12_store_soa(f_soa, n_groups, g, a);
     gacc[g] = 1;
 }
 
@@ -871,13 +829,6 @@ extern "C" void lcbk_tpke_ct_g2check(dim3 grid, hipStream_t s, const u32 *lines,
 extern "C" void lcbk_tpke_rlc_miller(dim3 grid, hipStream_t s, const u32 *lines, const void *desc, const void *gpts,
                                      u32 n_groups, u32 *f_soa, uint8_t *gacc) {
     LCB_LAUNCH(k_tpke_rlc_miller, lines, (const uint4 *)desc, (const g1a_st *)gpts, n_groups, f_soa, gacc);
-}
-extern "C" void lcbk_tpke_rlc_miller_split(hipStream_t s, const u32 *lines, const void *desc, const void *gpts,
-                                           u32 n_groups, u32 *f_soa, uint8_t *gacc) {
-    dim3 grid((2 * n_groups + LCB_BLOCK - 1) / LCB_BLOCK);
-    LCB_LAUNCH(k_tpke_rlc_miller_split, lines, (const uint4 *)desc, (const g1a_st *)gpts, n_groups, f_soa);
-    grid = dim3((n_groups + LCB_BLOCK - 1) / LCB_BLOCK);
-    LCB_LAUNCH(k_rlc_fpair_mul, f_soa, n_groups, gacc);
 }
 extern "C" void lcbk_ts_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 first,
                                 const uint8_t *msg_ok, const void *pks, u32 n_pks, const u32 *pk_idx,

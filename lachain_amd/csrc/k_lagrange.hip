@@ -153,13 +153,7 @@ extern "C" __global__ void LCB_BOUNDS k_g1_mul_lanes(const uint8_t *ys, const fr
     // outside the r-torsion that G1.FromBytes accepts (GLV would be wrong for their cofactor component)
     g1 R;
     fr k = lam_raw[i];
-#ifdef LCB_LAG_CALLS
-    jac_mul_aff(R, A, k.v, 256);
-#elif defined(LCB_LAG_NO_TABLES)
-    jac_mul_aff_inl(R, A, k.v, 256);
-#else
-    jac_mul_win4(R, A, k.v);
-#endif
+    jac_mul_win4(R, A, k.v);      // 4-bit window, affine table (measured faster than the plain ladder)
     out[i] = R;
     ok_out[i] = ok;
 }
@@ -173,16 +167,8 @@ extern "C" __global__ void LCB_BOUNDS k_g2_mul_lanes(const uint8_t *ys, const fr
     // on-curve input takes the plain ladder, so the result equals the oracle's for every input
     g2 R;
     fr k = lam_raw[i];
-#ifdef LCB_LAG_CALLS
-    if (g2_in_subgroup(A)) g2_mul_gls(R, A, k.v);
-    else jac_mul_aff(R, A, k.v, 256);
-#elif defined(LCB_LAG_NO_TABLES)
-    if (g2_in_subgroup_inl(A)) g2_mul_gls_inl(R, A, k.v);
-    else jac_mul_aff_inl(R, A, k.v, 256);
-#else
     if (g2_in_subgroup_inl(A)) g2_mul_gls_tab(R, A, k.v);
     else jac_mul_aff_inl(R, A, k.v, 256);
-#endif
     out[i] = R;
     ok_out[i] = ok;
 }

@@ -196,16 +196,11 @@ extern "C" __global__ void LCB_BOUNDS k_msm_bucket_acc(const fp *pts, const fp *
     buckets[b] = acc;
 }
 
-// The reduction / combination kernels are latency chains (one lane's serial additions and doublings).  Opt-in
-// LCB_MSM_INLINE inlines their group operations: measured mixed (2^20: bucket reduce 1.21 vs 1.06 ms, combine 2.17 vs
-// 1.98 ms; 2^24: combine 3.26 vs 3.59 ms), so the call forms stay the default.
-#ifdef LCB_MSM_INLINE
-#define MSM_ADD(r, p, q) jac_add(r, p, q)
-#define MSM_DBL(r, p) jac_dbl(r, p)
-#else
+// The reduction / combination kernels are latency chains (one lane's serial additions and doublings); their group
+// operations are the call forms (inlining them measured mixed: 2^20 bucket reduce 1.21 vs 1.06 ms, combine 2.17 vs
+// 1.98 ms; 2^24 combine 3.26 vs 3.59 ms).
 #define MSM_ADD(r, p, q) grp_add(r, p, q)
 #define MSM_DBL(r, p) grp_dbl(r, p)
-#endif
 // segment q of window w covers buckets a = q*L .. a+L-1 (digit values a+1 .. a+L)
 // hi_win: the key window that holds the upper half of the GLV top window's digits (digit = half + a + j + 1), or
 // ~0u when there is none

@@ -69,37 +69,13 @@ extern "C" __global__ void LCB_BOUNDS k_lineset_fill(u32 *lines, u32 n_sets) {
     if (force_general) ls[LCB_LS_FLAG] = 0;
 }
 
-extern "C" __global__ void LCB_BOUNDS k_tpke_verify(const u32 *lines, const uint8_t *ct_ok, u32 n_cts,
-                                                   const g1a_st *keys, u32 n_keys, const u32 *ct_idx,
-                                                   const u32 *dec_idx, const uint8_t *ui, u32 n, uint8_t *accept) {
-    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    u32 c = ct_idx[i], d = dec_idx[i];
-    g1a Ui, Y;
-    bool ok = d < n_keys && c < n_cts;   // an out-of-range index rejects the share (and is clamped)
-    c = c < n_cts ? c : 0;
-    ok = ok && ct_ok[c];
-    ok = g1_decompress(Ui, ui + 48 * (size_t)i) && ok;
-    g1a_st ks = keys[d < n_keys ? d : 0];
-    ok = ok && ks.ok;
-    st_to_g1a(Y, ks);
-    fp_neg(Y.y, Y.y); // -Y: e(Ui, H) == e(Y, W)  <=>  e(Ui, H) e(-Y, W) == 1
-    fp12 f, e;
-    miller2_sets(f, lines + (size_t)(2 * c) * LCB_LINESET_WORDS, Ui, lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS, Y);
-    final_exp(e, f);
-    accept[i] = ok && fp12_is_one(e);
-}
-
-// Two-kernel form of k_tpke_verify: the Miller loop parks f in HBM (SoA, 576 B/share) and
-// k_final_exp_check finishes; each kernel gets its own register budget.  accept[i] carries the
+// Exact per-share check, two kernels: the Miller loop parks f in HBM (SoA, 576 B/share) and k_final_exp_check finishes;
+// each kernel gets its own register budget (a single fused kernel spilled more and measured slower).  accept[i] carries the
 // decompression / key / ciphertext validity from the first kernel to the second.
 extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_miller(const u32 *lines, const uint8_t *ct_ok, u32 n_cts,
                                                          const g1a_st *keys, u32 n_keys, const u32 *ct_idx,
                                                          const u32 *dec_idx, const uint8_t *ui, u32 n, u32 *f_soa,
                                                          uint8_t *accept) {
-#ifdef LCB_LEAN_MILLER
-    __shared__ u32 lds_t[72 * LCB_BLOCK];   // one Fp6 temporary per lane (lean.hpp)
-#endif
     __shared__ uint4 lds_pts[12 * LCB_BLOCK];   // the lane's two G1 points (LinesNormLds)
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -114,9 +90,6 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_miller(const u32 *lines, const
     st_to_g1a(Y, ks);
     fp_neg(Y.y, Y.y);
     fp12 f;
-#ifdef LCB_LEAN_MILLER
-#error "LCB_LEAN_MILLER reads round-2 general line sets; the line sets are normalised since round 2 (pairing.hpp)"
-#else
     const u32 *lsH = lines + (size_t)(2 * c) * LCB_LINESET_WORDS, *lsW = lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS;
     if (lineset_normalised(lsH) && lineset_normalised(lsW)) {
         uint4 *pt = lds_pts + threadIdx.x;               // Ui at quads 0..5, -Y at quads 6..11
@@ -126,52 +99,23 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_miller(const u32 *lines, const
     } else {
         miller2_sets_fallback(f, lsH, Ui, lsW, Y);
     }
-#endif
     fp12_store_soa(f_soa, n, i, f);
     accept[i] = ok;
 }
-// accept[i] &= (final_exp(f_i) == 1).  park: SoA Fp12 slots per item (lcbk_fe_slots()), slot 0 = f from the
-// Miller kernel.  Default: fe_asm.hpp (exponentiations by z over the AGPR-resident Fp12 assembly squaring, the
-// hard part's other values in slots 0..4).  LCB_FE_FUNCS: the round-2 compiler-built form (pairing.hpp's
-// __noinline__ Fp12 functions).  LCB_LEAN_FE selects lean.hpp's slot form (pow-by-|z| base in LDS): measured 30 %
-// slower than LCB_FE_FUNCS.  LCB_FE_STAGED (kcommon.hpp: the exp-by-z loop inlined in the kernel, base parked in
-// slot 1) measured 10 % slower than LCB_FE_FUNCS (69.1 vs 62.5 ms per 262,144 shares).
-#if defined(LCB_LEAN_FE)
-extern "C" int lcbk_fe_slots() { return 6; }
-#elif defined(LCB_FE_STAGED)
-extern "C" int lcbk_fe_slots() { return 2; }      // slot 0: f from the Miller kernel; slot 1: final_exp_staged's base
-#elif defined(LCB_FE_FUNCS)
-extern "C" int lcbk_fe_slots() { return 1; }
-#else
+// accept[i] &= (final_exp(f_i) == 1).  park: SoA Fp12 slots per item (lcbk_fe_slots()), slot 0 = f from the Miller
+// kernel, left holding the final exponentiation (the level-2 search reads it): fe_asm.hpp (exponentiations by z over
+// the AGPR-resident Fp12 assembly squaring, the hard part's other values in slots 0..5).  Measured alternatives, removed:
+// the compiler-built __noinline__ Fp12 functions 62.5 ms, the exp-by-z loop inlined in the kernel 69.1 ms per 262,144
+// shares, Fp12 state parked in LDS 30 % slower than the former.
 extern "C" int lcbk_fe_slots() { return LCB_FE_ASM_SLOTS; }
-#endif
 extern "C" __global__ void LCB_PAIR_BOUNDS k_final_exp_check(u32 *park, u32 n, uint8_t *accept) {
-#ifdef LCB_LEAN_FE
-    __shared__ u32 lds_base[144 * LCB_BLOCK];
-#elif !defined(LCB_FE_STAGED) && !defined(LCB_FE_FUNCS)
     __shared__ uint4 fx_lds[36 * LCB_BLOCK];      // per lane: the two Fp6 products of a slot multiplication
-#endif
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-#ifdef LCB_LEAN_FE
-    final_exp_slots(park, n, i, lds_base + threadIdx.x);
-    accept[i] = accept[i] && fe_slot_is_one(park, n, i, 4);
-#elif defined(LCB_FE_STAGED)
-    fp12 f;
-    fp12_load_soa(f, park, n, i);
-    final_exp_staged(f, park, n, i);
-    accept[i] = accept[i] && fp12_is_one(f);
-#elif defined(LCB_FE_FUNCS)
-    fp12 f;
-    fp12_load_soa(f, park, n, i);
-    final_exp_inplace(f);
-    accept[i] = accept[i] && fp12_is_one(f);
-#else
     final_exp_asm(park, n, i, FxLds{fx_lds + threadIdx.x});
     fp12 f;
     fp12_load_soa(f, park, n, i);
     accept[i] = accept[i] && fp12_is_one(f);
-#endif
 }
 
 // TPKE.PrivateKey.Decrypt: validity e(G, W) == e(U, H) <=> e(-G, W) e(U, H) == 1; then Ui = x U
@@ -213,9 +157,6 @@ extern "C" void lcbk_tpke_ct_prepare(dim3 grid, hipStream_t s, const uint8_t *ct
 }
 extern "C" void lcbk_lineset_fill(dim3 grid, hipStream_t s, u32 *lines, u32 n_sets) {
     LCB_LAUNCH(k_lineset_fill, lines, n_sets);
-}
-extern "C" void lcbk_tpke_verify(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, uint8_t *accept) {
-    LCB_LAUNCH(k_tpke_verify, lines, ct_ok, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, accept);
 }
 extern "C" void lcbk_tpke_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, u32 *f_soa, uint8_t *accept) {
     LCB_LAUNCH(k_tpke_miller, lines, ct_ok, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, f_soa, accept);

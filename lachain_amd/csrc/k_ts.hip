@@ -42,36 +42,11 @@ DI void miller2_ts(fp12 &f, const u32 *lsH, const g1a &PK, const g2a &S, const g
 }
 
 // ValidateSignature: e(PK, H) == e(G, sig) <=> e(PK, H) e(-G, sig) == 1
-extern "C" __global__ void LCB_BOUNDS k_ts_verify(const u32 *lines, const uint8_t *msg_ok, u32 n_msgs, const g1a_st *pks,
-                                                 u32 n_pks, const uint8_t *sigs, const u32 *msg_idx,
-                                                 const u32 *pk_idx, u32 n, uint8_t *accept) {
-    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    u32 m = msg_idx[i], k = pk_idx[i];
-    g2a S;
-    g1a PK, G;
-    bool ok = k < n_pks && m < n_msgs;   // an out-of-range index rejects the share (and is clamped)
-    m = m < n_msgs ? m : 0;
-    ok = ok && msg_ok[m];
-    ok = g2_decompress(S, sigs + 96 * (size_t)i) && ok;
-    g1a_st ps = pks[k < n_pks ? k : 0];
-    ok = ok && ps.ok;
-    st_to_g1a(PK, ps);
-    g1_generator(G);
-    fp_neg(G.y, G.y);
-    fp12 f, e;
-    miller2_ts(f, lines + (size_t)m * LCB_LINESET_WORDS, PK, S, G);
-    final_exp(e, f);
-    accept[i] = ok && fp12_is_one(e);
-}
-// Split form (default): the 2-pair Miller loop parks f in HBM (word-major SoA) and k_final_exp_check
+// Exact per-share check, two kernels: the 2-pair Miller loop parks f in HBM (word-major SoA) and k_final_exp_check
 // (k_tpke.hip) finishes, so each half gets its own register budget.
 extern "C" __global__ void LCB_PAIR_BOUNDS k_ts_miller(const u32 *lines, const uint8_t *msg_ok, u32 n_msgs, const g1a_st *pks,
                                                  u32 n_pks, const uint8_t *sigs, const u32 *msg_idx,
                                                  const u32 *pk_idx, u32 n, u32 *f_soa, uint8_t *accept) {
-#ifdef LCB_LEAN_MILLER
-    __shared__ u32 lds_t[72 * LCB_BLOCK];   // one Fp6 temporary per lane (lean.hpp)
-#endif
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u32 m = msg_idx[i], k = pk_idx[i];
@@ -87,11 +62,7 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_ts_miller(const u32 *lines, const u
     g1_generator(G);
     fp_neg(G.y, G.y);
     fp12 f;
-#ifdef LCB_LEAN_MILLER
-#error "LCB_LEAN_MILLER reads round-2 general line sets; the line sets are normalised since round 2 (pairing.hpp)"
-#else
     miller2_ts(f, lines + (size_t)m * LCB_LINESET_WORDS, PK, S, G);
-#endif
     fp12_store_soa(f_soa, n, i, f);
     accept[i] = ok;
 }
@@ -152,9 +123,6 @@ extern "C" __global__ void LCB_BOUNDS k_coin_fold(const uint8_t *sigs, u32 n, ui
 // ---------------------------------------------------------------- host launch wrappers
 extern "C" void lcbk_ts_msg_prepare(dim3 grid, hipStream_t s, const uint8_t *msg_data, const u32 *msg_off, u32 n_msgs, u32 *lines, uint8_t *msg_ok, int orig_cof) {
     LCB_LAUNCH(k_ts_msg_prepare, msg_data, msg_off, n_msgs, lines, msg_ok, orig_cof);
-}
-extern "C" void lcbk_ts_verify(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *msg_ok, u32 n_msgs, const void *pks, u32 n_pks, const uint8_t *sigs, const u32 *msg_idx, const u32 *pk_idx, u32 n, uint8_t *accept) {
-    LCB_LAUNCH(k_ts_verify, lines, msg_ok, n_msgs, (const g1a_st *)pks, n_pks, sigs, msg_idx, pk_idx, n, accept);
 }
 extern "C" void lcbk_ts_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *msg_ok, u32 n_msgs, const void *pks, u32 n_pks, const uint8_t *sigs, const u32 *msg_idx, const u32 *pk_idx, u32 n, u32 *f_soa, uint8_t *accept) {
     LCB_LAUNCH(k_ts_miller, lines, msg_ok, n_msgs, (const g1a_st *)pks, n_pks, sigs, msg_idx, pk_idx, n, f_soa, accept);

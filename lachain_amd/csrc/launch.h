@@ -9,13 +9,11 @@ extern "C" void lcbk_g1_decompress(dim3 grid, hipStream_t s, const uint8_t *in, 
 extern "C" void lcbk_g2_decompress(dim3 grid, hipStream_t s, const uint8_t *in, u32 n, void *out);
 extern "C" void lcbk_tpke_ct_prepare(dim3 grid, hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data, const u32 *v_off, u32 n_cts, u32 *lines, uint8_t *ct_ok, int orig_cof);
 extern "C" void lcbk_lineset_fill(dim3 grid, hipStream_t s, u32 *lines, u32 n_sets);
-extern "C" void lcbk_tpke_verify(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, uint8_t *accept);
 extern "C" void lcbk_tpke_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, u32 *f_soa, uint8_t *accept);
 extern "C" int lcbk_fe_slots();
 extern "C" void lcbk_final_exp_check(dim3 grid, hipStream_t s, u32 *park, u32 n, uint8_t *accept);
 extern "C" void lcbk_tpke_partial_decrypt(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, const uint8_t *cts_u, const void *x_raw, u32 x_stride, u32 n_cts, uint8_t *ui_out, uint8_t *status);
 extern "C" void lcbk_ts_msg_prepare(dim3 grid, hipStream_t s, const uint8_t *msg_data, const u32 *msg_off, u32 n_msgs, u32 *lines, uint8_t *msg_ok, int orig_cof);
-extern "C" void lcbk_ts_verify(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *msg_ok, u32 n_msgs, const void *pks, u32 n_pks, const uint8_t *sigs, const u32 *msg_idx, const u32 *pk_idx, u32 n, uint8_t *accept);
 extern "C" void lcbk_ts_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *msg_ok, u32 n_msgs, const void *pks, u32 n_pks, const uint8_t *sigs, const u32 *msg_idx, const u32 *pk_idx, u32 n, u32 *f_soa, uint8_t *accept);
 extern "C" void lcbk_coin_fold(dim3 grid, hipStream_t s, const uint8_t *sigs, u32 n, uint8_t *parity, uint64_t *nonce);
 extern "C" void lcbk_select_first_valid(dim3 grid, hipStream_t s, const uint8_t *accept, const uint8_t *pts, u32 pbytes, u32 per_group, u32 k, u32 n_groups, uint8_t *xs, uint8_t *ys, u32 *off);
@@ -43,7 +41,11 @@ extern "C" void lcbk_g1_jac_compress(dim3 grid, hipStream_t s, const void *in, u
 extern "C" void lcbk_g1_to_affine(dim3 grid, hipStream_t s, const uint8_t *in, u32 n, void *out, uint8_t *ok);
 extern "C" int lcbk_sort_pairs(void *temp, size_t *temp_bytes, u32 *keys, u32 *keys_alt, u32 *vals, u32 *vals_alt, u32 m, int end_bit, hipStream_t s);
 extern "C" void lcbk_dkg_rows(dim3 grid, hipStream_t s, const void *coef, u32 n_coef, u32 n_comm, u32 D, const u32 *comm, const int *xs, u32 n_q, void *rows, uint8_t *ok_out);
-extern "C" void lcbk_dkg_horner(dim3 grid, hipStream_t s, const void *rows, const uint8_t *row_ok, u32 D, const u32 *row, const int *ys, u32 n_q, uint8_t *out48, uint8_t *status);
+extern "C" void lcbk_dkg_horner(dim3 grid, hipStream_t s, const void *rows, const uint8_t *row_ok, u32 D, const u32 *row, const int *ys, u32 n_q, uint8_t *out48, uint8_t *status, u32 neg_exact);
+extern "C" void lcbk_and_groups(hipStream_t s, const uint8_t *in, u32 n_out, u32 group, uint8_t *out);
+extern "C" void lcbk_g1_subgroup_any(hipStream_t s, const void *pts, u32 n, u32 *any);
+extern "C" void lcbk_dkg_exact_terms(hipStream_t s, const void *coef, u32 n_coef, u32 n_comm, u32 D, const u32 *comm, const int *xs, u32 n_q, void *terms, uint8_t *ok_out);
+extern "C" void lcbk_dkg_exact_combine(hipStream_t s, const void *rows, u32 D, const u32 *row, const int *ys, u32 n_q, void *terms);
 extern "C" void lcbk_g1a_to_jac(dim3 grid, hipStream_t s, const void *in, u32 n, void *out, uint8_t *ok);
 extern "C" const void *lcbk_rs_matrix_kernel();
 extern "C" void lcbk_rs_matrix(hipStream_t s, const int *pe, int m, const int *pk, int k, int n, uint8_t *M, uint8_t *ok);
@@ -67,8 +69,6 @@ extern "C" void lcbk_rlc_groups(hipStream_t s, const u32 *key_idx, u32 i0, u32 n
 extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 first, const uint8_t *ct_ok, const uint8_t *ct_g2, const void *keys, u32 n_keys, const u32 *dec_idx, const uint8_t *ui, const u32 *rU, const u32 *rY, u32 n, void *gpts, uint8_t *accept, uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval);
 extern "C" void lcbk_tpke_rlc_wsum(dim3 grid, hipStream_t s, const void *sdesc, u32 n_s, const u32 *wsum, u32 n_l1, void *gpts);
 extern "C" void lcbk_tpke_ct_g2check(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, uint8_t *ct_g2);
-extern "C" void lcbk_tpke_rlc_miller_split(hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups,
-                                           u32 *f_soa, uint8_t *gacc);
 extern "C" void lcbk_tpke_rlc_miller(dim3 grid, hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups, u32 *f_soa, uint8_t *gacc);
 extern "C" void lcbk_ts_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 first, const uint8_t *msg_ok, const void *pks, u32 n_pks, const u32 *pk_idx, const uint8_t *sigs, const u32 *rP, const u32 *rS, u32 n, void *gpts, uint8_t *accept, uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval);
 extern "C" void lcbk_ts_rlc_wsum(dim3 grid, hipStream_t s, const void *sdesc, u32 n_s, const u32 *wsum, u32 n_l1, void *gpts);

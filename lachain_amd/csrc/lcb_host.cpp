@@ -606,13 +606,6 @@ bool sync_check(lcb_ctx *c, const char *what) {
     return true;
 }
 
-// LCB_FUSED_VERIFY=1 selects the single-kernel verify (Miller loop + final exponentiation in one launch)
-bool fused_verify() {
-    static int v = -1;
-    if (v < 0) { const char *e = getenv("LCB_FUSED_VERIFY"); v = (e && *e == '1') ? 1 : 0; }
-    return v == 1;
-}
-
 // ------------------------------------------------------------------ TPKE
 #define LCB_VERIFY_CHUNK ((size_t)1 << 21)   // shares per Miller + final-exponentiation launch pair
 
@@ -651,10 +644,7 @@ int tpke_verify_prepared(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_keys,
     if (n > 0xffffffffu) { set_err("tpke verify: batch too large"); return -1; }
     const u32 *lines = (const u32 *)c->t_lines.p;
     const uint8_t *ctok = (const uint8_t *)c->t_ctok.p;
-    if (n && fused_verify()) {
-        lcbk_tpke_verify(dim3(nblk(n)), s, lines, ctok, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct, d_dec, d_ui, (u32)n,
-                         d_accept);
-    } else if (n) {
+    if (n) {
         // chunks of at most LCB_VERIFY_CHUNK shares: bounded park buffer (slots x 576 B per share) whatever n is;
         // the phase events time the first chunk
         const size_t nf = n < LCB_VERIFY_CHUNK ? n : LCB_VERIFY_CHUNK;
@@ -694,7 +684,6 @@ std::mutex g_seed_mu;                       // lcb_set_batch_seed (test hook) vs
 uint8_t g_rlc_seed[32];
 bool g_rlc_seed_set = false;
 std::atomic<size_t> g_census_min{16384};    // lcb_set_batch_census: batches of at least this many shares get a census
-std::atomic<uint32_t> g_split_max{32768};   // lcb_set_rlc_split_max: TPKE levels of <= this many groups split pairs
 std::atomic<uint32_t> g_coop_max{32768};    // lcb_set_coop_max: levels of <= this many checks use the 9-lane kernels
 enum RlcKind { RLC_TPKE = 0, RLC_TS = 1 };
 struct RlcStats {
@@ -865,9 +854,6 @@ void rlc_checks(lcb_ctx *c, const RlcKindInfo &K, RlcWs &w, const uint8_t *desc,
         else if (coop)
             lcbk_coop_tpke_miller(s, K.lines, desc + 16 * o, (const uint8_t *)gpts + K.rec * o, (u32)m, f, gacc + o,
                                   (uint8_t *)c->rlc[15].get(m));
-        else if (m <= g_split_max.load())    // under one wave per SIMD: one Miller pair per lane
-            lcbk_tpke_rlc_miller_split(s, K.lines, desc + 16 * o, (const uint8_t *)gpts + K.rec * o, (u32)m, f,
-                                       gacc + o);
         else
             lcbk_tpke_rlc_miller(dim3(nblk(m)), s, K.lines, desc + 16 * o, (const uint8_t *)gpts + K.rec * o, (u32)m, f,
                                  gacc + o);
@@ -1084,10 +1070,7 @@ int ts_verify_prepared(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_pks, si
     if (n > 0xffffffffu) { set_err("ts verify: batch too large"); return -1; }
     const u32 *lines = (const u32 *)c->s_lines.p;
     const uint8_t *mok = (const uint8_t *)c->s_mok.p;
-    if (n && fused_verify()) {
-        lcbk_ts_verify(dim3(nblk(n)), s, lines, mok, (u32)n_msgs, c->s_keys.p, (u32)n_pks, d_sigs, d_midx, d_pidx, (u32)n,
-                       d_accept);
-    } else if (n) {
+    if (n) {
         const size_t nf = n < LCB_VERIFY_CHUNK ? n : LCB_VERIFY_CHUNK;
         u32 *f = (u32 *)c->s_f.get(nf * 576 * (size_t)lcbk_fe_slots())   /* SoA Fp12 slots: Miller output (+ final-exp parking) */;
         if (!f) { set_err("device allocation failed"); return -1; }
@@ -1403,7 +1386,6 @@ extern "C" void lcb_set_batch_seed(const uint8_t *seed32) {
     else g_rlc_seed_set = false;
 }
 extern "C" void lcb_set_batch_census(size_t min_shares) { g_census_min.store(min_shares); }
-extern "C" void lcb_set_rlc_split_max(uint32_t max_groups) { g_split_max.store(max_groups); }
 extern "C" void lcb_set_coop_max(uint32_t max_checks) { g_coop_max.store(max_checks); }
 // one cooperative Fp12 operation (k_coop_debug) on n values a (and b) vs the one-lane field.hpp routine: AoS in / out
 extern "C" int lcb_debug_coop_op(int op, const uint32_t *a, const uint32_t *b, size_t n, uint32_t *out, uint32_t *ref) {
@@ -1755,9 +1737,22 @@ extern "C" int lcb_coin_fold_dev(uint8_t *parity, uint64_t *nonce, const uint8_t
 // Commitment.Evaluate(x, y) / Evaluate(x) (src/Lachain.Consensus/ThresholdKeygen/Data/Commitment.cs:23-53) for whole
 // batches: rows of every distinct (commitment, x) once, then Horner in y per query.
 namespace {
+// any decodable point of d_aff (n records) outside G1 (k_g1_subgroup_any; one 4-byte read)
+int g1_any_off_subgroup(lcb_ctx *c, const void *d_aff, size_t n, hipStream_t s, bool *any) {
+    u32 *d = (u32 *)c->dkg[8].get(4);
+    if (!d) { set_err("device allocation failed"); return -1; }
+    hipMemsetAsync(d, 0, 4, s);
+    if (n) lcbk_g1_subgroup_any(s, d_aff, (u32)n, d);
+    u32 h = 0;
+    if (!launched("subgroup test launch") || !read_counts(&h, d, 1, s)) return -1;
+    *any = h != 0;
+    return 0;
+}
+// Commitment.Evaluate(x) rows of n_rows (commitment, x) pairs.  Honest commitments (every coefficient in G1): Horner in
+// the small x (k_dkg_rows).  A batch with a coefficient outside G1: the reference's own terms [x^j mod r] C (exact).
 int dkg_rows_enqueue(lcb_ctx *c, const uint8_t *d_coeffs, size_t n_comm, size_t n_coef, int degree,
                      const uint32_t *d_comm, const int32_t *d_xs, size_t n_rows, hipStream_t s, void **rows_out,
-                     uint8_t **rows_ok) {
+                     uint8_t **rows_ok, bool *exact) {
     size_t total = n_comm * n_coef, lanes = n_rows * (size_t)(degree + 1);
     if (total > 0xffffffffu || lanes > 0xffffffffu) { set_err("dkg: batch too large"); return -1; }
     void *aff = c->dkg[0].get(total * LCB_G1A_ST_BYTES);
@@ -1765,9 +1760,20 @@ int dkg_rows_enqueue(lcb_ctx *c, const uint8_t *d_coeffs, size_t n_comm, size_t 
     uint8_t *rok = (uint8_t *)c->dkg[2].get(lanes);
     if (!aff || !rows || !rok) { set_err("device allocation failed"); return -1; }
     if (total) lcbk_g1_decompress(dim3(nblk(total)), s, d_coeffs, (u32)total, aff);
-    if (lanes)
+    if (g1_any_off_subgroup(c, aff, total, s, exact)) return -1;
+    if (lanes && !*exact) {
         lcbk_dkg_rows(dim3(nblk(lanes)), s, aff, (u32)n_coef, (u32)n_comm, (u32)degree, d_comm, d_xs, (u32)n_rows, rows,
                       rok);
+    } else if (lanes) {
+        const size_t nt = lanes * (size_t)(degree + 1);
+        if (nt > 0xffffffffu) { set_err("dkg: batch too large for the exact form"); return -1; }
+        void *terms = c->dkg[6].get(nt * LCB_G1_JAC_BYTES);
+        uint8_t *tok = (uint8_t *)c->dkg[7].get(nt);
+        if (!terms || !tok) { set_err("device allocation failed"); return -1; }
+        lcbk_dkg_exact_terms(s, aff, (u32)n_coef, (u32)n_comm, (u32)degree, d_comm, d_xs, (u32)n_rows, terms, tok);
+        lcbk_g1_jac_reduce_groups(dim3(nblk(lanes)), s, terms, (u32)nt, (u32)(degree + 1), rows);
+        lcbk_and_groups(s, tok, (u32)lanes, (u32)(degree + 1), rok);
+    }
     *rows_out = rows;
     *rows_ok = rok;
     return launched("dkg rows launch") ? 0 : -1;
@@ -1795,7 +1801,8 @@ extern "C" int lcb_dkg_commitment_rows(uint8_t *rows_out, uint8_t *status, const
     if (!dco || !dci || !dx || !dout) { set_err("device allocation failed"); return -1; }
     void *rows;
     uint8_t *rok;
-    if (dkg_rows_enqueue(c, dco, n_comm, n_coef, degree, dci, dx, n_queries, s, &rows, &rok)) return -1;
+    bool exact = false;
+    if (dkg_rows_enqueue(c, dco, n_comm, n_coef, degree, dci, dx, n_queries, s, &rows, &rok, &exact)) return -1;
     lcbk_g1_jac_compress(dim3(nblk(lanes)), s, rows, (u32)lanes, dout);
     std::vector<uint8_t> ok(lanes);
     hipMemcpyAsync(rows_out, dout, 48 * lanes, hipMemcpyDeviceToHost, s);
@@ -1841,11 +1848,32 @@ extern "C" int lcb_dkg_commitment_eval(uint8_t *out, uint8_t *status, const uint
     if (!dco || !drc || !drx || !drow || !dy || !dout || !dst) { set_err("device allocation failed"); return -1; }
     void *rows;
     uint8_t *rok;
-    if (dkg_rows_enqueue(c, dco, n_comm, n_coef, degree, drc, drx, row_comm.size(), s, &rows, &rok)) return -1;
-    lcbk_dkg_horner(dim3(nblk(n_queries)), s, rows, rok, (u32)degree, drow, dy, (u32)n_queries, dout, dst);
+    bool exact = false;
+    if (dkg_rows_enqueue(c, dco, n_comm, n_coef, degree, drc, drx, row_comm.size(), s, &rows, &rok, &exact)) return -1;
+    if (!exact) {
+        lcbk_dkg_horner(dim3(nblk(n_queries)), s, rows, rok, (u32)degree, drow, dy, (u32)n_queries, dout, dst, 0);
+        hipMemcpyAsync(out, dout, 48 * n_queries, hipMemcpyDeviceToHost, s);
+        hipMemcpyAsync(status, dst, n_queries, hipMemcpyDeviceToHost, s);
+        return sync_check(c, "dkg eval") ? 0 : -1;
+    }
+    // a coefficient outside G1: sum_j [y^j mod r] row_j(x) (Commitment.cs:23-37 as written)
+    const size_t D1 = (size_t)degree + 1, nt = n_queries * D1;
+    void *terms = c->dkg[6].get(nt * LCB_G1_JAC_BYTES), *sums = c->dkg[3].get(n_queries * LCB_G1_JAC_BYTES);
+    if (!terms || !sums) { set_err("device allocation failed"); return -1; }
+    lcbk_dkg_exact_combine(s, rows, (u32)degree, drow, dy, (u32)n_queries, terms);
+    lcbk_g1_jac_reduce_groups(dim3(nblk(n_queries)), s, terms, (u32)nt, (u32)D1, sums);
+    lcbk_g1_jac_compress(dim3(nblk(n_queries)), s, sums, (u32)n_queries, dout);
+    std::vector<uint8_t> rk(row_comm.size() * D1);
     hipMemcpyAsync(out, dout, 48 * n_queries, hipMemcpyDeviceToHost, s);
-    hipMemcpyAsync(status, dst, n_queries, hipMemcpyDeviceToHost, s);
-    return sync_check(c, "dkg eval") ? 0 : -1;
+    hipMemcpyAsync(rk.data(), rok, rk.size(), hipMemcpyDeviceToHost, s);
+    if (!sync_check(c, "dkg eval")) return -1;
+    for (size_t qi = 0; qi < n_queries; qi++) {
+        uint8_t st = 1;
+        for (size_t j = 0; j < D1; j++) st &= rk[row_of[qi] * D1 + j];
+        status[qi] = st;
+        if (!st) memset(out + 48 * qi, 0, 48);
+    }
+    return 0;
 }
 extern "C" int lcb_g1_eval_poly_batch(uint8_t *out, uint8_t *status, const uint8_t *coeffs, size_t n_coeffs,
                                       const int32_t *xs, size_t n_points) {
@@ -1864,8 +1892,13 @@ extern "C" int lcb_g1_eval_poly_batch(uint8_t *out, uint8_t *status, const uint8
     if (!dco || !dx || !aff || !rows || !rok || !drow || !dout || !dst) { set_err("device allocation failed"); return -1; }
     hipMemsetAsync(drow, 0, 4 * n_points, s);    // every point evaluates row 0 (the coefficient vector)
     lcbk_g1_decompress(dim3(nblk(n_coeffs)), s, dco, (u32)n_coeffs, aff);
+    bool off = false;                            // a coefficient outside G1: negative x multiply by Fr.FromInt(x)
+    bool neg = false;
+    for (size_t i = 0; i < n_points; i++) neg |= xs[i] < 0;
+    if (neg && g1_any_off_subgroup(c, aff, n_coeffs, s, &off)) return -1;
     lcbk_g1a_to_jac(dim3(nblk(n_coeffs)), s, aff, (u32)n_coeffs, rows, rok);
-    lcbk_dkg_horner(dim3(nblk(n_points)), s, rows, rok, (u32)(n_coeffs - 1), drow, dx, (u32)n_points, dout, dst);
+    lcbk_dkg_horner(dim3(nblk(n_points)), s, rows, rok, (u32)(n_coeffs - 1), drow, dx, (u32)n_points, dout, dst,
+                    off ? 1u : 0u);
     hipMemcpyAsync(out, dout, 48 * n_points, hipMemcpyDeviceToHost, s);
     hipMemcpyAsync(status, dst, n_points, hipMemcpyDeviceToHost, s);
     return sync_check(c, "eval poly") ? 0 : -1;

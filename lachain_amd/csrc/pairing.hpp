@@ -337,9 +337,7 @@ struct LinesNorm {          // normalised lines of a line set (lineset_compute)
 };
 // the same, with its G1 point parked in LDS (6 quads per lane, quad q at pt[q * LCB_BLOCK_PTS]) and re-read at
 // every line: keeps the point's 24 words out of the Miller loop's live registers (the loop otherwise spills)
-#ifndef LCB_BLOCK_PTS
 #define LCB_BLOCK_PTS 256
-#endif
 struct LinesNormLds {
     const u32 *p;
     const uint4 *pt;
@@ -430,36 +428,9 @@ DI void lineset_put_point(u32 *ls, const g2a &Q) {
 }
 DI void lineset_get_point(g2a &Q, const u32 *ls) { lineset_point(Q, ls); }
 
-// f = prod_k f_{|z|, Q_k}(P_k), conjugated (z < 0).  A pair whose G1 point is infinity contributes 1.
-// LCB_MILLER_LINE_PAIR: multiply the two lines of a step together first (23 instead of 26 Fp2 products).
-// Measured slower on gfx950 (k_tpke_miller 227 -> 232 ms per 1M shares): the six live evaluated Fp2 values
-// double the loop's spill traffic, which costs more than the three saved products.  Off by default.
-#ifdef LCB_MILLER_LINE_PAIR
-template <class S1, class S2>
-DI void miller2(fp12 &f, S1 &s1, const g1a &P1, S2 &s2, const g1a &P2) {
-    f = fp12_one();
-    line l;
-    fp2 A1, B1, C1, A2, B2, C2;
-    bool first = true;
-    for (int i = 62; i >= 0; i--) {
-        if (!first) fp12_sqr(f, f);
-        first = false;
-        s1.next(l, false);
-        line_eval(A1, B1, C1, l, P1);
-        s2.next(l, false);
-        line_eval(A2, B2, C2, l, P2);
-        fp12_mul_line_pair(f, A1, B1, C1, A2, B2, C2);
-        if ((LCB_Z_ABS >> i) & 1) {
-            s1.next(l, true);
-            line_eval(A1, B1, C1, l, P1);
-            s2.next(l, true);
-            line_eval(A2, B2, C2, l, P2);
-            fp12_mul_line_pair(f, A1, B1, C1, A2, B2, C2);
-        }
-    }
-    fp12_conj(f, f);
-}
-#else
+// f = prod_k f_{|z|, Q_k}(P_k), conjugated (z < 0).  A pair whose G1 point is infinity contributes 1.  (Multiplying the
+// two lines of a step together first, 23 instead of 26 Fp2 products, measured slower: k_tpke_miller 227 -> 232 ms per
+// 1M shares, the six live evaluated Fp2 values doubled the spill traffic.)
 template <class S1, class S2>
 DI void miller2(fp12 &f, S1 &s1, const g1a &P1, S2 &s2, const g1a &P2) {
     f = fp12_one();
@@ -476,7 +447,6 @@ DI void miller2(fp12 &f, S1 &s1, const g1a &P1, S2 &s2, const g1a &P2) {
     }
     fp12_conj(f, f);
 }
-#endif
 template <class S1>
 DI void miller1(fp12 &f, S1 &s1, const g1a &P1) {
     f = fp12_one();
@@ -535,9 +505,6 @@ DN void fe_easy(fp12 &r, const fp12 &f) {
 }
 // x^z for unitary x (z = -|z|): cyclotomic square-and-multiply over |z|, then conjugate
 DN void cyc_pow_z(fp12 &r, const fp12 &x) {
-#ifdef LCB_FN_AGPR
-    asm volatile("; AGPRs usable as spill space in this function" ::: "a255");
-#endif
     fp12 acc = x;
     fp12 base = x; // kept in registers for the whole loop (the squaring chain never touches memory)
     for (int i = 62; i >= 0; i--) {

@@ -85,7 +85,6 @@ _SIGS = {
                                          c_size, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
     "lcb_debug_final_exp": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), c_size, ctypes.POINTER(ctypes.c_uint32),
                                            ctypes.c_int]),
-    "lcb_set_rlc_split_max": (None, [ctypes.c_uint32]),
     "lcb_batched_census": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32)]),
     "lcb_tpke_partial_decrypt": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_u8p, c_u8p, c_u32p, c_size]),
     "lcb_tpke_encrypt_phase1": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_size]),
@@ -710,11 +709,6 @@ def set_batch_seed(seed32=None):
 def set_batch_census(min_shares):
     """batched calls of >= min_shares shares start with the census of suspect keys (0 = never; default 16384)"""
     lib().lcb_set_batch_census(min_shares)
-
-
-def set_rlc_split_max(max_groups):
-    """TPKE levels of <= max_groups groups use the split (one pair per lane) Miller kernel (default 32768)"""
-    lib().lcb_set_rlc_split_max(max_groups)
 
 
 def set_coop_max(max_checks):

@@ -89,3 +89,34 @@ def test_g1_eval_poly_batch(nat):
         assert g == o.g1_mul(G, o.fr(sum(c * pow(x, k, R) for k, c in enumerate(a)) % R)), x
     for x in (0, 1, 256, -5):
         assert got[xs.index(x)] == o.g1_eval_poly(coeffs, o.fr(x))
+
+
+def test_commitment_off_subgroup_coefficients(nat):
+    """A Byzantine dealer's commitment with coefficients outside G1 (G1.FromBytes accepts them, SURVEY A.8;
+    TrustlessKeygen never calls Commitment.IsValid): one coefficient carries the order-3 point (0, -2), one is a random
+    on-curve point.  With x^i y^j >= r the powers' reduction mod r changes the result, so the GPU must take the
+    reference's own form [y^j mod r]([x^i mod r] C) (Commitment.cs:23-37) — equal to the oracle's literal evaluation —
+    and the rows (Commitment.cs:39-53) likewise; an honest commitment in the same call is unaffected."""
+    from test_gpu_batched import off_subgroup_g1
+    d = Drbg(b"gpu-dkg-off-subgroup")
+    degree = 40
+    c, pts = commitment(nat, d, degree)
+    t3 = bytes(47) + b"\x80"                        # x = 0, odd y: (0, p - 2), order 3
+    assert o.g1_valid(t3) and not o.g1_in_subgroup(t3)
+    bad = list(pts)
+    bad[index(3, 5)] = o.g1_add(pts[index(3, 5)], t3)
+    bad[index(0, 7)] = off_subgroup_g1(d)
+    queries = [(1, 200, 150), (1, 7, 230), (0, 200, 150), (1, 255, 255)]
+    got = nat.dkg_commitment_eval([pts, bad], degree, queries)
+    for (k, x, y), g in zip(queries, got):
+        assert g == o.dkg_commitment_eval([pts, bad][k], degree, x, y), (k, x, y)
+    # the honest commitment's value is still G * f(x, y)
+    assert got[2] == o.g1_mul(o.g1_gen(), o.fr(f_xy(c, degree, 200, 150)))
+    rows = nat.dkg_commitment_rows([pts, bad], degree, [(1, 200), (0, 200)])
+    assert rows[0] == o.dkg_commitment_row(bad, degree, 200)
+    assert rows[1] == o.dkg_commitment_row(pts, degree, 200)
+    # MclBls12381.EvaluatePolynomial with a negative x: Fr.FromInt(x) = r - |x| multiplies the off-subgroup terms
+    coeffs = bad[:12]
+    for x in (-3, 5):
+        xb = o.fr(x % R)
+        assert nat.g1_eval_poly_batch(coeffs, [x]) == [o.g1_eval_poly(coeffs, xb)], x

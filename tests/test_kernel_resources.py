@@ -1,0 +1,99 @@
+"""Register-spill and scratch gate for the built library (CPU test; no GPU needed).
+
+Reads every kernel's code-object metadata (tools/kernel_resources.py: .vgpr_spill_count, .private_segment_fixed_size)
+and fails when a kernel spills more VGPRs, or uses more per-lane scratch, than its budget below.  Kernels not listed
+must not spill at all.  The budgets are the figures of the current build: a change that adds spills to a kernel has to
+lower another figure or justify the new budget here.  The cooperative pairing kernels (k_coop.hip), the batch-check
+bookkeeping kernels and the MSM / ECDSA hot loops are held at zero spills.
+"""
+import os
+import shutil
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SO = os.path.join(ROOT, "lachain_amd", "liblachain_bls.so")
+
+# kernel: (max VGPR spills, max scratch bytes per lane) — measured on this build
+BUDGET = {
+    "k_coop_debug": (96, 7620),               # test hook: the one-lane reference routines beside the coop ones
+    "k_coop_final_exp_check": (0, 576),
+    "k_coop_tpke_miller": (0, 0),
+    "k_dkg_exact_combine": (0, 312),
+    "k_dkg_exact_terms": (0, 408),
+    "k_dkg_horner": (0, 896),
+    "k_dkg_rows": (0, 312),
+    "k_final_exp_check": (0, 4288),
+    "k_g1_decompress": (0, 800),
+    "k_g1_jac_compress": (0, 704),
+    "k_g1_jac_reduce_block": (0, 456),
+    "k_g1_jac_reduce_groups": (0, 168),
+    "k_g1_mul": (0, 5568),
+    "k_g1_mul_lanes": (0, 5424),
+    "k_g1_subgroup_any": (12, 0),
+    "k_g1_sum": (0, 752),
+    "k_g1_to_affine": (0, 704),
+    "k_g2_decompress": (0, 992),
+    "k_g2_hash": (0, 3336),
+    "k_g2_mul": (206, 10624),
+    "k_g2_mul_lanes": (1276, 10288),
+    "k_g2_sum": (204, 1008),
+    "k_lineset_fill": (0, 1824),
+    "k_msm_bucket_reduce": (0, 600),
+    "k_msm_horner": (0, 168),
+    "k_op": (3038, 8484),                     # mcl single-element surface: every operation in one kernel
+    "k_rlc_key_tables": (12, 576),
+    "k_rlc_miller_fallback": (0, 2376),
+    "k_rlc_search": (93, 2264),
+    "k_secp_scalars": (0, 528),
+    "k_tpke_ct_g2check": (0, 1048),
+    "k_tpke_ct_prepare": (0, 3736),
+    "k_tpke_encrypt1": (0, 6432),
+    "k_tpke_encrypt2": (0, 3912),
+    "k_tpke_miller": (348, 2616),
+    "k_tpke_partial_decrypt": (972, 7652),
+    "k_tpke_rlc_miller": (360, 2616),
+    "k_tpke_rlc_points": (60, 944),
+    "k_tpke_rlc_sum": (0, 1328),
+    "k_tpke_rlc_wsum": (0, 576),
+    "k_ts_miller": (1248, 3292),
+    "k_ts_msg_prepare": (0, 3624),
+    "k_ts_rlc_miller": (0, 2524),
+    "k_ts_rlc_points": (554, 1376),
+    "k_ts_rlc_sum": (0, 2136),
+    "k_ts_rlc_wsum": (12, 992),
+    "k_ts_sign": (0, 3912),
+}
+ZERO_SPILL = ["k_coop_tpke_miller", "k_coop_final_exp_check", "k_msm_bucket_acc", "k_secp_verify",
+              "k_rlc_census_stats", "k_rlc_suspect_split", "k_rlc_resolve", "k_tpke_rlc_sum", "k_ts_rlc_miller"]
+
+
+@pytest.fixture(scope="module")
+def resources():
+    if not os.path.exists(SO):
+        pytest.skip("liblachain_bls.so not built")
+    if not shutil.which("llvm-objdump", path="/opt/rocm/lib/llvm/bin"):
+        pytest.skip("llvm-objdump not available")
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from kernel_resources import kernel_resources
+    return kernel_resources(SO)
+
+
+def test_every_kernel_within_its_spill_and_scratch_budget(resources):
+    over = []
+    for name, r in resources.items():
+        if name.startswith("lcb_asm_") or name.startswith("_Z"):      # asm-library stubs, hipCUB sort kernels
+            continue
+        spill, scratch = BUDGET.get(name, (0, None))
+        if r["vgpr_spill_count"] > spill:
+            over.append((name, "vgpr_spill", r["vgpr_spill_count"], spill))
+        if scratch is not None and r["private_segment_fixed_size"] > scratch:
+            over.append((name, "scratch", r["private_segment_fixed_size"], scratch))
+    assert not over, over
+
+
+def test_hot_kernels_do_not_spill(resources):
+    for name in ZERO_SPILL:
+        assert name in resources, name
+        assert resources[name]["vgpr_spill_count"] == 0, name
