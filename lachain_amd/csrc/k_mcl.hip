@@ -1,0 +1,126 @@
+// lachain_amd/csrc/k_mcl.hip — gfx950 kernels behind the mcl single-element surface (include/lachain_bls.h, SURVEY.md
+// §8b): the pairing on the cooperative kernels, G1 multi-scalar products, Horner evaluation with an Fr point and the
+// conversion of mcl's Jacobian records to wire bytes for the batched Lagrange path.  mcl's G1 / G2 records are the
+// device's own Jacobian layout (x, y, z in Montgomery form, 12 x u32 per Fp), scalars arrive as canonical integers.
+#include "coop.hpp"
+
+LCB_ASM_LIBRARY(k_mcl)
+
+// mclBn_pairing(P, Q) (GT.Pairing in the reference, e.g. TPKE/PublicKey.cs:91) as a one-group cooperative check:
+// P and the point at infinity as the group's two G1 points, Q's line set and the set of infinity (every line 1).
+// in: P Jacobian (36 words) then Q Jacobian (72 words)
+extern "C" __global__ void LCB_BOUNDS k_pairing_prep(const u32 *in, g1a_st *gpts, u32 *lines, uint4 *desc) {
+    if (blockIdx.x || threadIdx.x) return;
+    g1 p = *(const g1 *)in;
+    g2 q = *(const g2 *)(in + 36);
+    g1a pa;
+    g2a qa, inf;
+    jac_to_aff(pa, p);
+    jac_to_aff(qa, q);
+    g1a_st s;
+    s.x = pa.x; s.y = pa.y; s.inf = pa.inf; s.ok = 1; s.pad[0] = s.pad[1] = 0;
+    gpts[0] = s;
+    s.inf = 1; s.x = fp_zero(); s.y = fp_zero();
+    gpts[1] = s;
+    inf.inf = true;
+    inf.x = fp2_zero();
+    inf.y = fp2_zero();
+    lineset_put_point(lines, qa);
+    lineset_put_point(lines + LCB_LINESET_WORDS, inf);
+    lines[LCB_LS_FLAG + 2] = lines[LCB_LINESET_WORDS + LCB_LS_FLAG + 2] = 0;
+    desc[0] = make_uint4(0, 1, 0, 0);
+}
+
+// terms[i] = [k_i] P_i for n G1 points (Jacobian) and canonical 256-bit scalars: the 4-bit windowed ladder over the
+// point's affine table, exact for every on-curve input (k_lagrange.hip)
+extern "C" __global__ void LCB_BOUNDS k_mcl_g1_terms(const g1 *pts, const fr *scal, u32 n, g1 *terms) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    g1a a;
+    jac_to_aff(a, pts[i]);
+    fr k = scal[i];
+    g1 r;
+    jac_mul_win4(r, a, k.v);
+    terms[i] = r;
+}
+
+// Horner with an Fr point x (mcl evaluatePolynomial: y = c[n-1]; y = y x + c[i]), one lane; g = 1 (G1) or 2 (G2)
+extern "C" __global__ void LCB_BOUNDS k_mcl_horner(int g, const u32 *coef, u32 n, const fr *x_raw, u32 *out) {
+    if (blockIdx.x || threadIdx.x) return;
+    const fr x = *x_raw;
+    if (g == 1) {
+        const g1 *c = (const g1 *)coef;
+        g1 acc = c[n - 1];
+        for (u32 i = n - 1; i-- > 0;) {
+            jac_mul_bits(acc, acc, x.v, 255);
+            grp_add(acc, acc, c[i]);
+        }
+        *(g1 *)out = acc;
+    } else {
+        const g2 *c = (const g2 *)coef;
+        g2 acc = c[n - 1];
+        for (u32 i = n - 1; i-- > 0;) {
+            jac_mul_bits(acc, acc, x.v, 255);
+            grp_add(acc, acc, c[i]);
+        }
+        *(g2 *)out = acc;
+    }
+}
+
+// out = sum of n G1 Jacobian records, one lane (mulVec's final sum for n <= one block; larger n reduce by blocks first)
+extern "C" __global__ void LCB_BOUNDS k_mcl_g1_sum(const g1 *in, u32 n, g1 *out) {
+    if (blockIdx.x || threadIdx.x) return;
+    g1 acc;
+    jac_set_inf(acc);
+    for (u32 i = 0; i < n; i++) grp_add(acc, acc, in[i]);
+    *out = acc;
+}
+
+// wire encodings -> mcl Jacobian records (z = 1, or the point at infinity), ok[i] = the encoding decoded
+extern "C" __global__ void LCB_BOUNDS k_mcl_from_bytes(int g, const uint8_t *in, u32 n, u32 *out, uint8_t *ok) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (g == 1) {
+        g1a a;
+        ok[i] = g1_decompress(a, in + 48 * (size_t)i);
+        jac_from_aff(((g1 *)out)[i], a);
+    } else {
+        g2a a;
+        ok[i] = g2_decompress(a, in + 96 * (size_t)i);
+        jac_from_aff(((g2 *)out)[i], a);
+    }
+}
+
+// mcl Jacobian records -> 48 / 96-byte wire encodings (g = 1 / 2)
+extern "C" __global__ void LCB_BOUNDS k_mcl_to_bytes(int g, const u32 *in, u32 n, uint8_t *out) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (g == 1) g1_compress_jac(out + 48 * (size_t)i, ((const g1 *)in)[i]);
+    else g2_compress_jac(out + 96 * (size_t)i, ((const g2 *)in)[i]);
+}
+
+// ---------------------------------------------------------------- host launch wrappers
+extern "C" void lcbk_pairing_prep(hipStream_t s, const u32 *in, void *gpts, u32 *lines, void *desc) {
+    dim3 grid(1);
+    LCB_LAUNCH(k_pairing_prep, in, (g1a_st *)gpts, lines, (uint4 *)desc);
+}
+extern "C" void lcbk_mcl_g1_terms(hipStream_t s, const void *pts, const void *scal, u32 n, void *terms) {
+    dim3 grid((n + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_mcl_g1_terms, (const g1 *)pts, (const fr *)scal, n, (g1 *)terms);
+}
+extern "C" void lcbk_mcl_horner(hipStream_t s, int g, const u32 *coef, u32 n, const void *x_raw, u32 *out) {
+    dim3 grid(1);
+    LCB_LAUNCH(k_mcl_horner, g, coef, n, (const fr *)x_raw, out);
+}
+extern "C" void lcbk_mcl_g1_sum(hipStream_t s, const void *in, u32 n, void *out) {
+    dim3 grid(1);
+    LCB_LAUNCH(k_mcl_g1_sum, (const g1 *)in, n, (g1 *)out);
+}
+extern "C" void lcbk_mcl_from_bytes(hipStream_t s, int g, const uint8_t *in, u32 n, u32 *out, uint8_t *ok) {
+    dim3 grid((n + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_mcl_from_bytes, g, in, n, out, ok);
+}
+extern "C" void lcbk_mcl_to_bytes(hipStream_t s, int g, const u32 *in, u32 n, uint8_t *out) {
+    dim3 grid((n + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_mcl_to_bytes, g, in, n, out);
+}

@@ -49,6 +49,7 @@ struct lcb_ctx {
     bool s_ready = false;
     // Lagrange / assembly / MSM / staging
     DevBuf lag[3], sel[3], msm[12], in[8], out[4], dkg[9];
+    DevBuf mcl[8];                    // the mcl surface's pairing / multi-scalar / Horner / Lagrange staging
     hipEvent_t ver_ev[3] = {};
     bool ver_ev_ready = false, ver_ran = false;
     // randomized batch verification (k_batch.hip): r_i U_i / r_i Y_i records, group lists, group points, counts

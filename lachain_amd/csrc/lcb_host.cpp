@@ -7,7 +7,9 @@
 //
 // Concurrency model (the reference calls mcl from one thread per consensus protocol,
 // /root/reference/src/Lachain.Consensus/AbstractProtocol.cs:46-47):
-//   * single-element mcl operations share one staging buffer under a process-wide lock (synchronous);
+//   * scalar Fr arithmetic runs on the host (fr_host.hpp); every other single-element mcl operation is a GPU round trip
+//     on the calling thread's own staging buffers and stream (no process-wide lock), and the pairing, multi-scalar
+//     products, Lagrange interpolation and polynomial evaluation go to batch / cooperative kernels;
 //   * every batch entry point runs in an lcb_ctx — explicit (lcb_ctx_*) or the calling thread's own default
 //     context — which owns all device workspaces the call needs (TPKE and TS line sets separately, Lagrange,
 //     MSM, staging).  A context's work executes in the order it was enqueued whatever stream it is enqueued on
@@ -31,19 +33,17 @@
 #include "host_sha3.hpp"
 #include "lcb_ctx.hpp"
 #include "lcb_internal.hpp"
+#include "fr_host.hpp"
 
 #define LCB_BLOCK 256
 
 namespace {
 
-std::mutex g_mu;               // single-element operations + device initialisation
+std::mutex g_mu;               // device initialisation
 int g_device = 0;
 bool g_ready = false;
 int g_orig_cofactor = 0;
-hipStream_t g_stream = nullptr;
-u32 *g_io = nullptr;          // device buffer for single operations
-u32 *g_io_host = nullptr;     // pinned staging
-const size_t IO_WORDS = 4096; // 16 KB
+const size_t IO_WORDS = 4096; // 16 KB staging per thread
 thread_local std::string g_err;
 thread_local int t_bound_device = -1;
 
@@ -72,9 +72,6 @@ bool init_locked() {
     hipDeviceProp_t prop;
     if ((e = hipGetDeviceProperties(&prop, g_device)) != hipSuccess) { set_err("hipGetDeviceProperties", e); return false; }
     if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) { set_err("device is not gfx950"); return false; }
-    if ((e = hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking)) != hipSuccess) { set_err("stream", e); return false; }
-    if ((e = hipMalloc(&g_io, IO_WORDS * 4)) != hipSuccess) { set_err("hipMalloc io", e); return false; }
-    if ((e = hipHostMalloc(&g_io_host, IO_WORDS * 4, hipHostMallocDefault)) != hipSuccess) { set_err("hipHostMalloc", e); return false; }
     g_ready = true;
     return true;
 }
@@ -86,20 +83,42 @@ bool ready() {
     return init_locked();
 }
 
-// run one k_op on the staging buffer: copy `in_words` words to the device, launch, copy `out_words` back
+// single-element operations: every calling thread owns its staging (device and pinned host buffers, a stream), so the
+// protocol threads (AbstractProtocol.cs:46-47) never queue behind each other's round trips
+struct OpStage {
+    u32 *dev = nullptr, *host = nullptr;
+    hipStream_t s = nullptr;
+    ~OpStage() {
+        if (s) (void)hipStreamDestroy(s);
+        if (dev) (void)hipFree(dev);
+        if (host) (void)hipHostFree(host);
+    }
+};
+thread_local OpStage t_stage;
+bool stage_ready() {
+    if (!ready()) return false;
+    if (t_stage.s) return true;
+    hipError_t e = hipStreamCreateWithFlags(&t_stage.s, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&t_stage.dev, IO_WORDS * 4);
+    if (e == hipSuccess) e = hipHostMalloc(&t_stage.host, IO_WORDS * 4, hipHostMallocDefault);
+    if (e != hipSuccess) { set_err("single-operation staging", e); return false; }
+    return true;
+}
+#define IOH (t_stage.host)
+
+// run one k_op on the thread's staging buffer: copy `in_words` words to the device, launch, copy `out_words` back
 bool run_op(int op, size_t in_words, size_t out_words) {
     hipError_t e;
-    if ((e = hipMemcpyAsync(g_io, g_io_host, in_words * 4, hipMemcpyHostToDevice, g_stream)) != hipSuccess) { set_err("H2D", e); return false; }
-    lcbk_op(dim3(1), g_stream, op, g_io, g_orig_cofactor);
+    if ((e = hipMemcpyAsync(t_stage.dev, t_stage.host, in_words * 4, hipMemcpyHostToDevice, t_stage.s)) != hipSuccess) { set_err("H2D", e); return false; }
+    lcbk_op(dim3(1), t_stage.s, op, t_stage.dev, g_orig_cofactor);
     if ((e = hipGetLastError()) != hipSuccess) { set_err("k_op launch", e); return false; }
-    if ((e = hipMemcpyAsync(g_io_host, g_io, out_words * 4, hipMemcpyDeviceToHost, g_stream)) != hipSuccess) { set_err("D2H", e); return false; }
-    if ((e = hipStreamSynchronize(g_stream)) != hipSuccess) { set_err("k_op", e); return false; }
+    if ((e = hipMemcpyAsync(t_stage.host, t_stage.dev, out_words * 4, hipMemcpyDeviceToHost, t_stage.s)) != hipSuccess) { set_err("D2H", e); return false; }
+    if ((e = hipStreamSynchronize(t_stage.s)) != hipSuccess) { set_err("k_op", e); return false; }
     return true;
 }
 
 #define LOCKED_OR(ret)                        \
-    std::lock_guard<std::mutex> lk_(g_mu);    \
-    if (!init_locked()) return ret;
+    if (!stage_ready()) return ret;
 
 inline u32 nblk(size_t n) { return (u32)((n + LCB_BLOCK - 1) / LCB_BLOCK); }
 
@@ -140,19 +159,20 @@ extern "C" int mclBn_getG1ByteSize(void) { return 48; }
 extern "C" int mclBn_getFrByteSize(void) { return 32; }
 extern "C" int mclBn_getFpByteSize(void) { return 48; }
 
-// ================================================================== Fr
+// ================================================================== Fr (host arithmetic, fr_host.hpp)
+static inline const uint64_t *FRV(const mclBnFr *x) { return (const uint64_t *)x; }
+static inline uint64_t *FRW(mclBnFr *x) { return (uint64_t *)x; }
 static int fr_set_raw(mclBnFr *y, const u32 raw[8]) {
-    LOCKED_OR(-1)
-    memcpy(g_io_host + 8, raw, 32);
-    if (!run_op(OP_FR_FROM_RAW, 25, 25) || !g_io_host[24]) { memset(y, 0, 32); return -1; }
-    memcpy(y, g_io_host, 32);
+    uint64_t r[4];
+    memcpy(r, raw, 32);
+    if (!frh::lt_r(r)) { memset(y, 0, 32); return -1; }
+    frh::from_raw(FRW(y), r);
     return 0;
 }
 static int fr_get_raw(u32 raw[8], const mclBnFr *x) {
-    LOCKED_OR(-1)
-    memcpy(g_io_host + 8, x, 32);
-    if (!run_op(OP_FR_TO_RAW, 16, 8)) return -1;
-    memcpy(raw, g_io_host, 32);
+    uint64_t r[4];
+    frh::to_raw(r, FRV(x));
+    memcpy(raw, r, 32);
     return 0;
 }
 extern "C" int mclBnFr_setInt(mclBnFr *y, mclInt x) {
@@ -165,7 +185,7 @@ extern "C" int mclBnFr_setInt(mclBnFr *y, mclInt x) {
 }
 extern "C" int mclBnFr_setInt32(mclBnFr *y, int x) { return mclBnFr_setInt(y, x); }
 extern "C" int mclBnFr_setByCSPRNG(mclBnFr *x) {
-    // rejection sampling of a uniform 255-bit value < r (host randomness, device conversion)
+    // rejection sampling of a uniform 255-bit value < r
     for (int tries = 0; tries < 64; tries++) {
         u32 raw[8];
         if (getrandom(raw, sizeof raw, 0) != (ssize_t)sizeof raw) return -1;
@@ -179,18 +199,15 @@ extern "C" int mclBnFr_setLittleEndian(mclBnFr *x, const void *buf, mclSize n) {
     u32 raw[8] = {0};
     memcpy(raw, buf, n < 32 ? n : 32);
     raw[7] &= 0x7fffffffu;
-    static const u32 R_[8] = {0x00000001, 0xffffffff, 0xfffe5bfe, 0x53bda402, 0x09a1d805, 0x3339d808, 0x299d7d48, 0x73eda753};
-    bool ge = true;
-    for (int j = 7; j >= 0; j--) {
-        if (raw[j] != R_[j]) { ge = raw[j] > R_[j]; break; }
-    }
-    if (ge) raw[7] &= 0x3fffffffu;
+    uint64_t r[4];
+    memcpy(r, raw, 32);
+    if (!frh::lt_r(r)) raw[7] &= 0x3fffffffu;
     return fr_set_raw(x, raw);
 }
 extern "C" mclSize mclBnFr_serialize(void *buf, mclSize max, const mclBnFr *x) {
     if (max < 32) return 0;
     u32 raw[8];
-    if (fr_get_raw(raw, x)) return 0;
+    fr_get_raw(raw, x);
     memcpy(buf, raw, 32);
     return 32;
 }
@@ -201,36 +218,16 @@ extern "C" mclSize mclBnFr_deserialize(mclBnFr *x, const void *buf, mclSize n) {
     return fr_set_raw(x, raw) == 0 ? 32 : 0;
 }
 extern "C" void mclBnFr_clear(mclBnFr *x) { memset(x, 0, sizeof *x); }
-extern "C" int mclBnFr_isValid(const mclBnFr *x) {
-    static const u32 R_[8] = {0x00000001, 0xffffffff, 0xfffe5bfe, 0x53bda402, 0x09a1d805, 0x3339d808, 0x299d7d48, 0x73eda753};
-    const u32 *w = (const u32 *)x;
-    for (int j = 7; j >= 0; j--)
-        if (w[j] != R_[j]) return w[j] < R_[j];
-    return 0;
-}
+extern "C" int mclBnFr_isValid(const mclBnFr *x) { return frh::lt_r(FRV(x)); }
 extern "C" int mclBnFr_isEqual(const mclBnFr *x, const mclBnFr *y) { return memcmp(x, y, 32) == 0; }
-extern "C" int mclBnFr_isZero(const mclBnFr *x) {
-    static const mclBnFr z = {{0, 0, 0, 0}};
-    return memcmp(x, &z, 32) == 0;
-}
-extern "C" int mclBnFr_isOne(const mclBnFr *x) {
-    u32 raw[8];
-    if (fr_get_raw(raw, x)) return 0;
-    for (int j = 1; j < 8; j++) if (raw[j]) return 0;
-    return raw[0] == 1;
-}
-static void fr_binop(int op, mclBnFr *z, const mclBnFr *x, const mclBnFr *y) {
-    LOCKED_OR()
-    memcpy(g_io_host + 8, x, 32);
-    if (y) memcpy(g_io_host + 16, y, 32);
-    if (run_op(op, 24, 8)) memcpy(z, g_io_host, 32);
-}
-extern "C" void mclBnFr_neg(mclBnFr *y, const mclBnFr *x) { fr_binop(OP_FR_NEG, y, x, nullptr); }
-extern "C" void mclBnFr_inv(mclBnFr *y, const mclBnFr *x) { fr_binop(OP_FR_INV, y, x, nullptr); }
-extern "C" void mclBnFr_sqr(mclBnFr *y, const mclBnFr *x) { fr_binop(OP_FR_MUL, y, x, x); }
-extern "C" void mclBnFr_add(mclBnFr *z, const mclBnFr *x, const mclBnFr *y) { fr_binop(OP_FR_ADD, z, x, y); }
-extern "C" void mclBnFr_sub(mclBnFr *z, const mclBnFr *x, const mclBnFr *y) { fr_binop(OP_FR_SUB, z, x, y); }
-extern "C" void mclBnFr_mul(mclBnFr *z, const mclBnFr *x, const mclBnFr *y) { fr_binop(OP_FR_MUL, z, x, y); }
+extern "C" int mclBnFr_isZero(const mclBnFr *x) { return frh::is_zero(FRV(x)); }
+extern "C" int mclBnFr_isOne(const mclBnFr *x) { return memcmp(x, frh::ONE, 32) == 0; }
+extern "C" void mclBnFr_neg(mclBnFr *y, const mclBnFr *x) { frh::neg(FRW(y), FRV(x)); }
+extern "C" void mclBnFr_inv(mclBnFr *y, const mclBnFr *x) { frh::inv(FRW(y), FRV(x)); }
+extern "C" void mclBnFr_sqr(mclBnFr *y, const mclBnFr *x) { frh::mul(FRW(y), FRV(x), FRV(x)); }
+extern "C" void mclBnFr_add(mclBnFr *z, const mclBnFr *x, const mclBnFr *y) { frh::add(FRW(z), FRV(x), FRV(y)); }
+extern "C" void mclBnFr_sub(mclBnFr *z, const mclBnFr *x, const mclBnFr *y) { frh::sub(FRW(z), FRV(x), FRV(y)); }
+extern "C" void mclBnFr_mul(mclBnFr *z, const mclBnFr *x, const mclBnFr *y) { frh::mul(FRW(z), FRV(x), FRV(y)); }
 extern "C" void mclBnFr_div(mclBnFr *z, const mclBnFr *x, const mclBnFr *y) {
     mclBnFr t;
     mclBnFr_inv(&t, y);
@@ -241,25 +238,25 @@ extern "C" void mclBnFr_div(mclBnFr *z, const mclBnFr *x, const mclBnFr *y) {
 extern "C" mclSize mclBnG1_serialize(void *buf, mclSize max, const mclBnG1 *x) {
     if (max < 48) return 0;
     LOCKED_OR(0)
-    memcpy(g_io_host + 36, x, 144);
+    memcpy(IOH + 36, x, 144);
     if (!run_op(OP_G1_SER, 72, 128)) return 0;
-    memcpy(buf, g_io_host + 116, 48);
+    memcpy(buf, IOH + 116, 48);
     return 48;
 }
 extern "C" mclSize mclBnG1_deserialize(mclBnG1 *x, const void *buf, mclSize n) {
     if (n < 48) return 0;
     LOCKED_OR(0)
-    memcpy(g_io_host + 116, buf, 48);
-    if (!run_op(OP_G1_DESER, 128, 129) || !g_io_host[128]) return 0;
-    memcpy(x, g_io_host, 144);
+    memcpy(IOH + 116, buf, 48);
+    if (!run_op(OP_G1_DESER, 128, 129) || !IOH[128]) return 0;
+    memcpy(x, IOH, 144);
     return 48;
 }
 static int g1_flag_op(int op, const mclBnG1 *x, const mclBnG1 *y) {
     LOCKED_OR(0)
-    memcpy(g_io_host + 36, x, 144);
-    if (y) memcpy(g_io_host + 72, y, 144);
+    memcpy(IOH + 36, x, 144);
+    if (y) memcpy(IOH + 72, y, 144);
     if (!run_op(op, 108, 129)) return 0;
-    return (int)g_io_host[128];
+    return (int)IOH[128];
 }
 extern "C" int mclBnG1_isValid(const mclBnG1 *x) { return g1_flag_op(OP_G1_VALID, x, nullptr); }
 extern "C" int mclBnG1_isEqual(const mclBnG1 *x, const mclBnG1 *y) { return g1_flag_op(OP_G1_EQ, x, y); }
@@ -270,10 +267,10 @@ extern "C" int mclBnG1_isZero(const mclBnG1 *x) {
 extern "C" void mclBnG1_clear(mclBnG1 *x) { memset(x, 0, sizeof *x); }
 static void g1_op(int op, mclBnG1 *z, const mclBnG1 *x, const mclBnG1 *y, const mclBnFr *k) {
     LOCKED_OR()
-    memcpy(g_io_host + 36, x, 144);
-    if (y) memcpy(g_io_host + 72, y, 144);
-    if (k) memcpy(g_io_host + 108, k, 32);
-    if (run_op(op, 116, 36)) memcpy(z, g_io_host, 144);
+    memcpy(IOH + 36, x, 144);
+    if (y) memcpy(IOH + 72, y, 144);
+    if (k) memcpy(IOH + 108, k, 32);
+    if (run_op(op, 116, 36)) memcpy(z, IOH, 144);
 }
 extern "C" void mclBnG1_neg(mclBnG1 *y, const mclBnG1 *x) { g1_op(OP_G1_NEG, y, x, nullptr, nullptr); }
 extern "C" void mclBnG1_dbl(mclBnG1 *y, const mclBnG1 *x) { g1_op(OP_G1_DBL, y, x, nullptr, nullptr); }
@@ -285,43 +282,34 @@ extern "C" void mclBnG1_sub(mclBnG1 *z, const mclBnG1 *x, const mclBnG1 *y) {
     mclBnG1_add(z, x, &ny);
 }
 extern "C" void mclBnG1_mul(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y) { g1_op(OP_G1_MUL, z, x, nullptr, y); }
-extern "C" void mclBnG1_mulVec(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y, mclSize n) {
-    mclBnG1 acc, t;
-    mclBnG1_clear(&acc);
-    for (mclSize i = 0; i < n; i++) {
-        mclBnG1_mul(&t, &x[i], &y[i]);
-        mclBnG1_add(&acc, &acc, &t);
-    }
-    *z = acc;
-}
 extern "C" void lcb_g1_generator(mclBnG1 *g) {
     LOCKED_OR()
-    if (run_op(OP_G1_GEN, 0, 36)) memcpy(g, g_io_host, 144);
+    if (run_op(OP_G1_GEN, 0, 36)) memcpy(g, IOH, 144);
 }
 
 // ================================================================== G2
 extern "C" mclSize mclBnG2_serialize(void *buf, mclSize max, const mclBnG2 *x) {
     if (max < 96) return 0;
     LOCKED_OR(0)
-    memcpy(g_io_host + 72, x, 288);
+    memcpy(IOH + 72, x, 288);
     if (!run_op(OP_G2_SER, 144, 248)) return 0;
-    memcpy(buf, g_io_host + 224, 96);
+    memcpy(buf, IOH + 224, 96);
     return 96;
 }
 extern "C" mclSize mclBnG2_deserialize(mclBnG2 *x, const void *buf, mclSize n) {
     if (n < 96) return 0;
     LOCKED_OR(0)
-    memcpy(g_io_host + 224, buf, 96);
-    if (!run_op(OP_G2_DESER, 248, 249) || !g_io_host[248]) return 0;
-    memcpy(x, g_io_host, 288);
+    memcpy(IOH + 224, buf, 96);
+    if (!run_op(OP_G2_DESER, 248, 249) || !IOH[248]) return 0;
+    memcpy(x, IOH, 288);
     return 96;
 }
 static int g2_flag_op(int op, const mclBnG2 *x, const mclBnG2 *y) {
     LOCKED_OR(0)
-    memcpy(g_io_host + 72, x, 288);
-    if (y) memcpy(g_io_host + 144, y, 288);
+    memcpy(IOH + 72, x, 288);
+    if (y) memcpy(IOH + 144, y, 288);
     if (!run_op(op, 216, 249)) return 0;
-    return (int)g_io_host[248];
+    return (int)IOH[248];
 }
 extern "C" int mclBnG2_isValid(const mclBnG2 *x) { return g2_flag_op(OP_G2_VALID, x, nullptr); }
 extern "C" int mclBnG2_isEqual(const mclBnG2 *x, const mclBnG2 *y) { return g2_flag_op(OP_G2_EQ, x, y); }
@@ -333,18 +321,18 @@ extern "C" void mclBnG2_clear(mclBnG2 *x) { memset(x, 0, sizeof *x); }
 extern "C" int mclBnG2_hashAndMapTo(mclBnG2 *x, const void *buf, mclSize n) {
     if (n > (IO_WORDS - 256) * 4) { set_err("message too long"); return -1; }
     LOCKED_OR(-1)
-    g_io_host[250] = (u32)n;
-    memcpy(g_io_host + 256, buf, n);
-    if (!run_op(OP_G2_HASH, 256 + (n + 3) / 4, 249) || !g_io_host[248]) return -1;
-    memcpy(x, g_io_host, 288);
+    IOH[250] = (u32)n;
+    memcpy(IOH + 256, buf, n);
+    if (!run_op(OP_G2_HASH, 256 + (n + 3) / 4, 249) || !IOH[248]) return -1;
+    memcpy(x, IOH, 288);
     return 0;
 }
 static void g2_op(int op, mclBnG2 *z, const mclBnG2 *x, const mclBnG2 *y, const mclBnFr *k) {
     LOCKED_OR()
-    memcpy(g_io_host + 72, x, 288);
-    if (y) memcpy(g_io_host + 144, y, 288);
-    if (k) memcpy(g_io_host + 216, k, 32);
-    if (run_op(op, 224, 72)) memcpy(z, g_io_host, 288);
+    memcpy(IOH + 72, x, 288);
+    if (y) memcpy(IOH + 144, y, 288);
+    if (k) memcpy(IOH + 216, k, 32);
+    if (run_op(op, 224, 72)) memcpy(z, IOH, 288);
 }
 extern "C" void mclBnG2_neg(mclBnG2 *y, const mclBnG2 *x) { g2_op(OP_G2_NEG, y, x, nullptr, nullptr); }
 extern "C" void mclBnG2_dbl(mclBnG2 *y, const mclBnG2 *x) { g2_op(OP_G2_DBL, y, x, nullptr, nullptr); }
@@ -358,24 +346,23 @@ extern "C" void mclBnG2_sub(mclBnG2 *z, const mclBnG2 *x, const mclBnG2 *y) {
 extern "C" void mclBnG2_mul(mclBnG2 *z, const mclBnG2 *x, const mclBnFr *y) { g2_op(OP_G2_MUL, z, x, nullptr, y); }
 extern "C" void lcb_g2_generator(mclBnG2 *g) {
     LOCKED_OR()
-    if (run_op(OP_G2_GEN, 0, 72)) memcpy(g, g_io_host, 288);
+    if (run_op(OP_G2_GEN, 0, 72)) memcpy(g, IOH, 288);
 }
 
 // ================================================================== GT / pairing
 static void pair_op(int op, mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) {
     LOCKED_OR()
-    memcpy(g_io_host + 144, x, 144);
-    memcpy(g_io_host + 180, y, 288);
-    if (run_op(op, 252, 144)) memcpy(z, g_io_host, 576);
+    memcpy(IOH + 144, x, 144);
+    memcpy(IOH + 180, y, 288);
+    if (run_op(op, 252, 144)) memcpy(z, IOH, 576);
 }
-extern "C" void mclBn_pairing(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) { pair_op(OP_PAIRING, z, x, y); }
 extern "C" void mclBn_millerLoop(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) { pair_op(OP_MILLER, z, x, y); }
 static void gt_op(int op, mclBnGT *z, const mclBnGT *a, const mclBnGT *b, const mclBnFr *k) {
     LOCKED_OR()
-    memcpy(g_io_host + 252, a, 576);
-    if (b) memcpy(g_io_host + 396, b, 576);
-    if (k) memcpy(g_io_host + 540, k, 32);
-    if (run_op(op, 548, 144)) memcpy(z, g_io_host, 576);
+    memcpy(IOH + 252, a, 576);
+    if (b) memcpy(IOH + 396, b, 576);
+    if (k) memcpy(IOH + 540, k, 32);
+    if (run_op(op, 548, 144)) memcpy(z, IOH, 576);
 }
 extern "C" void mclBn_millerLoopVec(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y, mclSize n) {
     mclBnGT acc, t;
@@ -390,13 +377,12 @@ extern "C" void mclBn_millerLoopVec(mclBnGT *z, const mclBnG1 *x, const mclBnG2 
 // debug-only (not in include/lachain_bls.h): apply tower routine `which` (k_ops.hip OP_DEBUG_FP12) to raw GT words
 extern "C" int lcb_debug_fp12(int which, const uint32_t in[144], uint32_t out[144]) {
     LOCKED_OR(-1)
-    memcpy(g_io_host + 252, in, 576);
-    g_io_host[548] = (u32)which;
+    memcpy(IOH + 252, in, 576);
+    IOH[548] = (u32)which;
     if (!run_op(OP_DEBUG_FP12, 549, 144)) return -1;
-    memcpy(out, g_io_host, 576);
+    memcpy(out, IOH, 576);
     return 0;
 }
-extern "C" void mclBn_finalExp(mclBnGT *y, const mclBnGT *x) { gt_op(OP_FINAL_EXP, y, x, nullptr, nullptr); }
 extern "C" void mclBnGT_mul(mclBnGT *z, const mclBnGT *x, const mclBnGT *y) { gt_op(OP_GT_MUL, z, x, y, nullptr); }
 extern "C" void mclBnGT_pow(mclBnGT *z, const mclBnGT *x, const mclBnFr *y) { gt_op(OP_GT_POW, z, x, nullptr, y); }
 extern "C" int mclBnGT_isEqual(const mclBnGT *x, const mclBnGT *y) { return memcmp(x, y, 576) == 0; }
@@ -416,34 +402,30 @@ extern "C" void mclBnGT_clear(mclBnGT *x) { memset(x, 0, sizeof *x); }
 extern "C" mclSize mclBnGT_serialize(void *buf, mclSize max, const mclBnGT *x) {
     if (max < 576) return 0;
     LOCKED_OR(0)
-    memcpy(g_io_host + 252, x, 576);
+    memcpy(IOH + 252, x, 576);
     if (!run_op(OP_GT_SER, 396, 144)) return 0;
-    memcpy(buf, g_io_host, 576);
+    memcpy(buf, IOH, 576);
     return 576;
 }
 extern "C" mclSize mclBnGT_deserialize(mclBnGT *x, const void *buf, mclSize n) {
     if (n < 576) return 0;
     LOCKED_OR(0)
-    memcpy(g_io_host + 252, buf, 576);
-    if (!run_op(OP_GT_DESER, 396, 549) || !g_io_host[548]) return 0;
-    memcpy(x, g_io_host, 576);
+    memcpy(IOH + 252, buf, 576);
+    if (!run_op(OP_GT_DESER, 396, 549) || !IOH[548]) return 0;
+    memcpy(x, IOH, 576);
     return 576;
 }
 
-// ================================================================== Lagrange / polynomials (single)
-extern "C" int lcb_g1_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
-                                     const uint32_t *off, size_t n_problems);
-extern "C" int lcb_g2_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
-                                     const uint32_t *off, size_t n_problems);
-
+// ================================================================== Fr Lagrange / polynomials (host, fr_host.hpp)
 extern "C" int mclBn_FrLagrangeInterpolation(mclBnFr *out, const mclBnFr *xVec, const mclBnFr *yVec, mclSize k) {
+    // mcl LagrangeInterpolation: sum_i y_i prod_{j != i} x_j / (x_j - x_i); zero or repeated x is an error
     if (k == 0) return -1;
-    // lambda_i via the G1 path's coefficient kernel would need raw x; do it with Fr single ops
     for (mclSize i = 0; i < k; i++) {
         if (mclBnFr_isZero(&xVec[i])) return -1;
         for (mclSize j = 0; j < i; j++)
             if (mclBnFr_isEqual(&xVec[i], &xVec[j])) return -1;
     }
+    if (k == 1) { *out = yVec[0]; return 0; }
     mclBnFr a, acc, t, d;
     memcpy(&a, &xVec[0], 32);
     for (mclSize i = 1; i < k; i++) mclBnFr_mul(&a, &a, &xVec[i]);
@@ -462,31 +444,6 @@ extern "C" int mclBn_FrLagrangeInterpolation(mclBnFr *out, const mclBnFr *xVec, 
     *out = acc;
     return 0;
 }
-static int lagrange_points(int g, void *out, const mclBnFr *xVec, const void *yVec, mclSize k) {
-    if (k == 0) return -1;
-    size_t pb = g == 1 ? 48 : 96;
-    std::vector<uint8_t> xs(32 * k), ys(pb * k), o(pb);
-    for (mclSize i = 0; i < k; i++) {
-        if (mclBnFr_serialize(&xs[32 * i], 32, &xVec[i]) != 32) return -1;
-        if (g == 1) { if (mclBnG1_serialize(&ys[pb * i], pb, (const mclBnG1 *)yVec + i) != pb) return -1; }
-        else { if (mclBnG2_serialize(&ys[pb * i], pb, (const mclBnG2 *)yVec + i) != pb) return -1; }
-    }
-    uint32_t off[2] = {0, (uint32_t)k};
-    uint8_t st = 0;
-    int rc = g == 1 ? lcb_g1_lagrange_batch(o.data(), &st, xs.data(), ys.data(), off, 1)
-                    : lcb_g2_lagrange_batch(o.data(), &st, xs.data(), ys.data(), off, 1);
-    if (rc || !st) return -1;
-    if (g == 1) return mclBnG1_deserialize((mclBnG1 *)out, o.data(), pb) == pb ? 0 : -1;
-    return mclBnG2_deserialize((mclBnG2 *)out, o.data(), pb) == pb ? 0 : -1;
-}
-extern "C" int mclBn_G1LagrangeInterpolation(mclBnG1 *out, const mclBnFr *xVec, const mclBnG1 *yVec, mclSize k) {
-    if (k == 1) { *out = yVec[0]; return mclBnFr_isZero(&xVec[0]) ? -1 : 0; }
-    return lagrange_points(1, out, xVec, yVec, k);
-}
-extern "C" int mclBn_G2LagrangeInterpolation(mclBnG2 *out, const mclBnFr *xVec, const mclBnG2 *yVec, mclSize k) {
-    if (k == 1) { *out = yVec[0]; return mclBnFr_isZero(&xVec[0]) ? -1 : 0; }
-    return lagrange_points(2, out, xVec, yVec, k);
-}
 extern "C" int mclBn_FrEvaluatePolynomial(mclBnFr *out, const mclBnFr *c, mclSize n, const mclBnFr *x) {
     if (n == 0) return -1;
     mclBnFr acc = c[n - 1];
@@ -497,27 +454,6 @@ extern "C" int mclBn_FrEvaluatePolynomial(mclBnFr *out, const mclBnFr *c, mclSiz
     *out = acc;
     return 0;
 }
-extern "C" int mclBn_G1EvaluatePolynomial(mclBnG1 *out, const mclBnG1 *c, mclSize n, const mclBnFr *x) {
-    if (n == 0) return -1;
-    mclBnG1 acc = c[n - 1];
-    for (mclSize i = n - 1; i-- > 0;) {
-        mclBnG1_mul(&acc, &acc, x);
-        mclBnG1_add(&acc, &acc, &c[i]);
-    }
-    *out = acc;
-    return 0;
-}
-extern "C" int mclBn_G2EvaluatePolynomial(mclBnG2 *out, const mclBnG2 *c, mclSize n, const mclBnFr *x) {
-    if (n == 0) return -1;
-    mclBnG2 acc = c[n - 1];
-    for (mclSize i = n - 1; i-- > 0;) {
-        mclBnG2_mul(&acc, &acc, x);
-        mclBnG2_add(&acc, &acc, &c[i]);
-    }
-    *out = acc;
-    return 0;
-}
-
 
 // ================================================================== execution contexts
 namespace {
@@ -534,6 +470,7 @@ void ctx_free(lcb_ctx *c) {
     for (auto &b : c->in) b.release();
     for (auto &b : c->out) b.release();
     for (auto &b : c->dkg) b.release();
+    for (auto &b : c->mcl) b.release();
     for (auto &b : c->rlc) b.release();
     if (c->rlc_ev_ready) {
         for (auto &e : c->rlc_ev) (void)hipEventDestroy(e);
@@ -2035,6 +1972,148 @@ extern "C" int lcb_g1_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_
                                      const uint32_t *off, size_t n) { return lagrange_batch(1, out, status, xs, ys, off, n); }
 extern "C" int lcb_g2_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_t *xs, const uint8_t *ys,
                                      const uint32_t *off, size_t n) { return lagrange_batch(2, out, status, xs, ys, off, n); }
+
+// ================================================================== mcl surface on the batch / cooperative kernels
+// (k_mcl.hip, k_coop.hip) — each a single synchronous call on the calling thread's own context
+
+// mclBn_pairing (GT.Pairing: TPKE/PrivateKey.cs:26, TPKE/PublicKey.cs:91, ThresholdSignature/PublicKey.cs:20) as a
+// one-group cooperative check: P and the point at infinity, Q's normalised line set and the set of infinity, then
+// the nine-lane final exponentiation.  The lines are normalised (divided by their Fp2 leading coefficient), which
+// changes the Miller value by a factor the final exponentiation removes: the GT value is mcl's.
+extern "C" void mclBn_pairing(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) {
+    SYNC_CTX_OR(c, )
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    const size_t slots = lcbk_fe_slots() > 6 ? (size_t)lcbk_fe_slots() : 6;
+    u32 *in = (u32 *)c->mcl[0].get(108 * 4);
+    void *gpts = c->mcl[1].get(2 * LCB_G1A_ST_BYTES);
+    u32 *lines = (u32 *)c->mcl[2].get(2 * LCB_LINESET_BYTES);
+    void *desc = c->mcl[3].get(16);
+    u32 *park = (u32 *)c->mcl[4].get(576 * slots);
+    uint8_t *fl = (uint8_t *)c->mcl[5].get(64);
+    if (!in || !gpts || !lines || !desc || !park || !fl) { set_err("device allocation failed"); return; }
+    hipMemcpyAsync(in, x, 144, hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(in + 36, y, 288, hipMemcpyHostToDevice, s);
+    lcbk_pairing_prep(s, in, gpts, lines, desc);
+    lcbk_lineset_fill(dim3(1), s, lines, 2);
+    lcbk_coop_tpke_miller(s, lines, desc, gpts, 1, park, fl, fl + 32);
+    lcbk_coop_final_exp_check(s, park, 1, nullptr);
+    u32 r[144];
+    hipMemcpyAsync(r, park, 576, hipMemcpyDeviceToHost, s);
+    if (sync_check(c, "pairing")) memcpy(z, r, 576);
+}
+// mclBn_finalExp on the nine-lane kernel (park slot 0 of a one-value workspace)
+extern "C" void mclBn_finalExp(mclBnGT *y, const mclBnGT *x) {
+    SYNC_CTX_OR(c, )
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    const size_t slots = lcbk_fe_slots() > 6 ? (size_t)lcbk_fe_slots() : 6;
+    u32 *park = (u32 *)c->mcl[4].get(576 * slots);
+    if (!park) { set_err("device allocation failed"); return; }
+    hipMemcpyAsync(park, x, 576, hipMemcpyHostToDevice, s);
+    lcbk_coop_final_exp_check(s, park, 1, nullptr);
+    u32 r[144];
+    hipMemcpyAsync(r, park, 576, hipMemcpyDeviceToHost, s);
+    if (sync_check(c, "final exp")) memcpy(y, r, 576);
+}
+// mclBnG1_mulVec: sum_i [y_i] x_i with the canonical scalars (mcl's per-term product, exact for any on-curve x_i):
+// one lane per term (windowed ladder), then block reductions and a one-lane sum
+extern "C" void mclBnG1_mulVec(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y, mclSize n) {
+    if (n == 0) { mclBnG1_clear(z); return; }
+    SYNC_CTX_OR(c, )
+    if (n > 0xffffffffu) { set_err("mulVec: too large"); return; }
+    std::vector<uint64_t> raw(4 * n);
+    for (size_t i = 0; i < n; i++) frh::to_raw(&raw[4 * i], FRV(&y[i]));
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    const u32 *pts = up(c->mcl[0], (const u32 *)x, 36 * n, s);
+    const uint64_t *sc = up(c->mcl[1], raw.data(), 4 * n, s);
+    uint8_t *terms = (uint8_t *)c->mcl[2].get(LCB_G1_JAC_BYTES * n);
+    uint8_t *tmp = (uint8_t *)c->mcl[3].get(LCB_G1_JAC_BYTES * ((n + 255) / 256));
+    uint8_t *dz = (uint8_t *)c->mcl[5].get(LCB_G1_JAC_BYTES);
+    if (!pts || !sc || !terms || !tmp || !dz) { set_err("device allocation failed"); return; }
+    lcbk_mcl_g1_terms(s, pts, sc, (u32)n, terms);
+    uint8_t *cur = terms;
+    size_t cnt = n;
+    while (cnt > 256) {
+        uint8_t *dst = cur == terms ? tmp : terms;
+        lcbk_g1_jac_reduce_block(s, cur, (u32)cnt, 256, dst);
+        cnt = (cnt + 255) / 256;
+        cur = dst;
+    }
+    lcbk_mcl_g1_sum(s, cur, (u32)cnt, dz);
+    mclBnG1 r;
+    hipMemcpyAsync(&r, dz, 144, hipMemcpyDeviceToHost, s);
+    if (sync_check(c, "mulVec")) *z = r;
+}
+// G1 / G2 Lagrange interpolation of one problem on the batch kernels: mcl records -> wire bytes on the device, the
+// k_lagrange.hip coefficient + product kernels, the result decoded back into an mcl record (one round trip)
+static int lagrange_points(int g, void *out, const mclBnFr *xVec, const void *yVec, mclSize k) {
+    if (k == 0) return -1;
+    SYNC_CTX_OR(c, -1)
+    if (k > 0xffffffffu) { set_err("lagrange: too large"); return -1; }
+    const size_t pb = g == 1 ? 48 : 96, words = g == 1 ? 36 : 72;
+    std::vector<uint64_t> xs(4 * k);
+    for (size_t i = 0; i < k; i++) frh::to_raw(&xs[4 * i], FRV(&xVec[i]));
+    const uint32_t off[2] = {0, (uint32_t)k};
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    const uint8_t *dx = (const uint8_t *)up(c->mcl[0], xs.data(), 4 * k, s);
+    const u32 *dyr = up(c->mcl[1], (const u32 *)yVec, words * k, s);
+    const uint32_t *doff = up(c->mcl[2], off, 2, s);
+    uint8_t *dy = (uint8_t *)c->mcl[3].get(pb * k);
+    uint8_t *dst = (uint8_t *)c->mcl[4].get(16), *dout = (uint8_t *)c->mcl[5].get(pb);
+    u32 *rec = (u32 *)c->mcl[6].get(words * 4);
+    uint8_t *dok = (uint8_t *)c->mcl[7].get(16);
+    if (!dx || !dyr || !doff || !dy || !dst || !dout || !rec || !dok) { set_err("device allocation failed"); return -1; }
+    lcbk_mcl_to_bytes(s, g, dyr, (u32)k, dy);
+    if (lagrange_enqueue(c, g, dout, dst, dx, dy, doff, 1, k, s)) return -1;
+    lcbk_mcl_from_bytes(s, g, dout, 1, rec, dok);
+    u32 r[72];
+    uint8_t st = 0, ok = 0;
+    hipMemcpyAsync(r, rec, words * 4, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(&st, dst, 1, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(&ok, dok, 1, hipMemcpyDeviceToHost, s);
+    if (!sync_check(c, "lagrange") || !st || !ok) return -1;
+    memcpy(out, r, words * 4);
+    return 0;
+}
+extern "C" int mclBn_G1LagrangeInterpolation(mclBnG1 *out, const mclBnFr *xVec, const mclBnG1 *yVec, mclSize k) {
+    if (k == 1) { *out = yVec[0]; return mclBnFr_isZero(&xVec[0]) ? -1 : 0; }
+    return lagrange_points(1, out, xVec, yVec, k);
+}
+extern "C" int mclBn_G2LagrangeInterpolation(mclBnG2 *out, const mclBnFr *xVec, const mclBnG2 *yVec, mclSize k) {
+    if (k == 1) { *out = yVec[0]; return mclBnFr_isZero(&xVec[0]) ? -1 : 0; }
+    return lagrange_points(2, out, xVec, yVec, k);
+}
+// G1 / G2 EvaluatePolynomial: mcl's Horner rule (y = c[n-1]; y = y x + c[i]) in one kernel launch — the products are
+// by the integer x, as mcl's, so off-subgroup coefficients give mcl's value too
+static int eval_poly(int g, void *out, const void *coef, mclSize n, const mclBnFr *x) {
+    if (n == 0) return -1;
+    SYNC_CTX_OR(c, -1)
+    if (n > 0xffffffffu) { set_err("evaluate polynomial: too large"); return -1; }
+    const size_t words = g == 1 ? 36 : 72;
+    uint64_t xr[4];
+    frh::to_raw(xr, FRV(x));
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    const u32 *dc = up(c->mcl[0], (const u32 *)coef, words * n, s);
+    const uint64_t *dx = up(c->mcl[1], xr, 4, s);
+    u32 *dout = (u32 *)c->mcl[2].get(words * 4);
+    if (!dc || !dx || !dout) { set_err("device allocation failed"); return -1; }
+    lcbk_mcl_horner(s, g, dc, (u32)n, dx, dout);
+    u32 r[72];
+    hipMemcpyAsync(r, dout, words * 4, hipMemcpyDeviceToHost, s);
+    if (!sync_check(c, "evaluate polynomial")) return -1;
+    memcpy(out, r, words * 4);
+    return 0;
+}
+extern "C" int mclBn_G1EvaluatePolynomial(mclBnG1 *out, const mclBnG1 *c, mclSize n, const mclBnFr *x) {
+    return eval_poly(1, out, c, n, x);
+}
+extern "C" int mclBn_G2EvaluatePolynomial(mclBnG2 *out, const mclBnG2 *c, mclSize n, const mclBnFr *x) {
+    return eval_poly(2, out, c, n, x);
+}
 
 static int mul_batch(int g, uint8_t *out, const uint8_t *points, int use_gen, const uint8_t *scalars, size_t n) {
     SYNC_CTX_OR(c, -1)
