@@ -1239,6 +1239,96 @@ def run_rs(args, nat, rank):
                                   sample=f"{sample} bytes ({s2} B shards), oracle orc_rs_encode_shards (ZXing-style "
                                          f"polynomial division per byte column), one thread; equal to the GPU shards"))
 
+def run_mcl_latency(args, nat, rank):
+    """Per-call latency of the mcl single-element surface (include/lachain_bls.h, the calls Lachain's protocol code
+    makes one at a time): scalar Fr product (host), G1 / G2 products and addition (k_op), the pairing and the final
+    exponentiation (nine-lane cooperative kernels), mulVec / Lagrange / Horner at the consensus sizes (N = 22,
+    F = 7), and PublicKey.VerifyShare written as the reference writes it (HashToG2 + two GT.Pairing + Equals,
+    TPKE/PublicKey.cs:88-92) beside the library's one-share batch call.  Median wall time per call from Python
+    through ctypes (the ctypes overhead, ~1 us, is included); the oracle's single-threaded time for the same call
+    beside the GPU-backed ones."""
+    if rank != 0:
+        return None
+    from lachain_amd import mcl
+    from lachain_amd.tpke import PublicKey, EncryptedShare, PartiallyDecryptedShare
+    Fr, G1, G2, GT, M = mcl.Fr, mcl.G1, mcl.G2, mcl.GT, mcl.MclBls12381
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as o
+    reps = args.mcl_reps
+
+    def med(fn, r=reps):
+        fn()
+        ts = []
+        for _ in range(r):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        return 1e3 * ts[len(ts) // 2]
+
+    a, b = Fr.GetRandom(), Fr.GetRandom()
+    P, Q = G1.Generator() * a, G2.Generator() * b
+    ab, bb, Pb, Qb = a.ToBytes(), b.ToBytes(), P.ToBytes(), Q.ToBytes()
+    f = GT()
+    mcl._f("mclBn_millerLoop", None, [ctypes.POINTER(type(f.v)), ctypes.POINTER(type(P.v)),
+                                      ctypes.POINTER(type(Q.v))])(ctypes.byref(f.v), ctypes.byref(P.v), ctypes.byref(Q.v))
+    fe = mcl._f("mclBn_finalExp", None, [ctypes.POINTER(type(f.v))] * 2)
+    g = GT()
+    xs = [Fr.FromInt(i + 1) for i in range(args.f + 1)]
+    ys = [G1.Generator() * Fr.GetRandom() for _ in range(args.f + 1)]
+    cs = [G1.Generator() * Fr.GetRandom() for _ in range(args.f + 1)]
+    vs = [G1.Generator() * Fr.GetRandom() for _ in range(args.n)]
+    ks = [Fr.GetRandom() for _ in range(args.n)]
+    from lachain_amd.native import mclBnG1, mclBnFr
+    pa = (mclBnG1 * args.n)(*[p.v for p in vs])
+    sa = (mclBnFr * args.n)(*[k.v for k in ks])
+    mv = mcl._f("mclBnG1_mulVec", None, [ctypes.POINTER(mclBnG1), ctypes.POINTER(mclBnG1), ctypes.POINTER(mclBnFr),
+                                        ctypes.c_size_t])
+    out = G1()
+    # one TPKE share as the protocol sees it
+    x = Fr.GetRandom()
+    Y = (G1.Generator() * x).ToBytes()
+    pk = PublicKey(Y, args.f + 1)
+    r = Fr.GetRandom()
+    U = (G1.Generator() * r).ToBytes()
+    V = bytes(32)
+    Hb = nat.g2_hash_batch([U + V])[0]
+    W = (G2.FromBytes(Hb) * r).ToBytes()
+    Ui = (G1.FromBytes(U) * x).ToBytes()
+    share, ps = EncryptedShare(U, V, W, 0), PartiallyDecryptedShare(Ui, 0, 0)
+    Ug, Yg, Wg, Uig = G1.FromBytes(U), G1.FromBytes(Y), G2.FromBytes(W), G1.FromBytes(Ui)
+
+    def verify_mcl():
+        h = G2()
+        h.SetHashOf(U + V)
+        return GT.Pairing(Uig, h) == GT.Pairing(Yg, Wg)
+
+    assert verify_mcl() and pk.VerifyShare(share, ps)
+    res = {
+        "Fr_mul": 1e3 * med(lambda: a * b, 2000),
+        "G1_add": 1e3 * med(lambda: P + P),
+        "G1_mul": 1e3 * med(lambda: P * a),
+        "G2_mul": 1e3 * med(lambda: Q * a),
+        "pairing": 1e3 * med(lambda: GT.Pairing(P, Q)),
+        "finalExp": 1e3 * med(lambda: fe(ctypes.byref(g.v), ctypes.byref(f.v))),
+        "G1_mulVec_n%d" % args.n: 1e3 * med(lambda: mv(ctypes.byref(out.v), pa, sa, args.n)),
+        "G1_Lagrange_k%d" % (args.f + 1): 1e3 * med(lambda: M.LagrangeInterpolate(xs, ys)),
+        "G1_EvaluatePolynomial_n%d" % (args.f + 1): 1e3 * med(lambda: M.EvaluatePolynomial(cs, xs[3])),
+        "VerifyShare_via_mcl": 1e3 * med(verify_mcl),
+        "VerifyShare_batch_api_n1": 1e3 * med(lambda: pk.VerifyShare(share, ps)),
+    }
+    ref = {
+        "Fr_mul": 1e3 * med(lambda: o.fr_mul(ab, bb), 2000),
+        "G1_mul": 1e3 * med(lambda: o.g1_mul(Pb, ab)),
+        "G2_mul": 1e3 * med(lambda: o.g2_mul(Qb, ab)),
+        "pairing": 1e3 * med(lambda: o.pairing(Pb, Qb), max(3, reps // 3)),
+    }
+    return dict(metric="mcl single-call latency (median, one thread, through ctypes)", unit="us per call",
+                gpu=res, oracle_cpu=ref,
+                note="GPU-backed calls are a synchronous round trip each (launch + copies); Fr arithmetic is host "
+                     "code (fr_host.hpp).  oracle_cpu: the oracle's plain-C routines, one thread, same inputs")
+
+
 C["C_MUL1_64"] = round(C["C_MUL1"] * 64 / 255)          # 64-bit var-base G1 multiplication (double-and-add)
 C["C_MADD1"] = 11                                          # G1 mixed addition (7M + 4S)
 C["C_JADD1"] = 16                                          # G1 Jacobian addition (11M + 5S)
@@ -1420,6 +1510,7 @@ def main():
     ap.add_argument("--dkg-f", type=int, default=85)
     ap.add_argument("--rs-n", type=int, default=256, help="RBC shards (0 = skip)")
     ap.add_argument("--rs-bytes", type=int, default=1 << 24)
+    ap.add_argument("--mcl-reps", type=int, default=30, help="per-call latency samples of the mcl surface (0 = skip)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -1531,7 +1622,9 @@ def main():
     head = batched if (args.headline == "batched" and batched) else exact
     if head is None:
         raise SystemExit("nothing to report: --tpke-exact 0 and --tpke-batched 0")
-    msm = ts = replay = ecdsa = dkg = rs = None
+    msm = ts = replay = ecdsa = dkg = rs = mcl_lat = None
+    if args.mcl_reps > 0 and world == 1:
+        mcl_lat = run_mcl_latency(args, nat, rank)
     if args.dkg_n > 0 and world == 1:
         dkg = run_dkg(args, nat, rank)
     if args.rs_n > 0 and world == 1:
@@ -1609,6 +1702,7 @@ def main():
             "ecdsa_headers": ecdsa,
             "dkg": dkg,
             "rbc_erasure_coding": rs,
+            "mcl_latency": mcl_lat,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

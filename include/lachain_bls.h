@@ -231,6 +231,15 @@ int lcb_tpke_partial_decrypt_prepared_dev(uint8_t *ui_out, uint8_t *status, cons
    status[c] = 0 with fewer than k valid shares.  The plaintext is then lcb_xor_with_hash(u, V) on the host. */
 int lcb_tpke_combine_dev(uint8_t *u_out, uint8_t *status, const uint8_t *accept, const uint8_t *shares,
                          size_t per_ct, size_t k, size_t n_cts, void *stream);
+/* Arrival-order forms of the two combinations: HoneyBadger.cs:237-247 / ThresholdSigner.cs:62-75 combine the first
+   F+1 valid shares to ARRIVE.  order (device, per_group u32 per group): order[g * per_group + j] = the position
+   (DecryptorId / signer index) of the j-th share to arrive in group g; entries >= per_group mark arrivals that did
+   not happen.  A position listed twice makes the group fail (status 0: repeated abscissa).  The selection then
+   walks this order instead of index order; everything else is as lcb_tpke_combine_dev / lcb_ts_assemble_dev. */
+int lcb_tpke_combine_ordered_dev(uint8_t *u_out, uint8_t *status, const uint8_t *accept, const uint8_t *shares,
+                                 const uint32_t *order, size_t per_ct, size_t k, size_t n_cts, void *stream);
+int lcb_ts_assemble_ordered_dev(uint8_t *sig_out, uint8_t *status, const uint8_t *accept, const uint8_t *sigs,
+                                const uint32_t *order, size_t per_round, size_t k, size_t n_rounds, void *stream);
 
 /* device time (ms) of k_tpke_miller and k_final_exp_check in the last split TPKE verify (waits for it) */
 int lcb_tpke_verify_phase_ms(float ms[2]);
@@ -315,6 +324,12 @@ int lcb_ctx_tpke_partial_decrypt_prepared_dev(lcb_ctx *ctx, uint8_t *ui_out, uin
                                               size_t x_stride, const uint8_t *cts_u, size_t n_cts, void *stream);
 int lcb_ctx_tpke_combine_dev(lcb_ctx *ctx, uint8_t *u_out, uint8_t *status, const uint8_t *accept,
                              const uint8_t *shares, size_t per_ct, size_t k, size_t n_cts, void *stream);
+int lcb_ctx_tpke_combine_ordered_dev(lcb_ctx *ctx, uint8_t *u_out, uint8_t *status, const uint8_t *accept,
+                                     const uint8_t *shares, const uint32_t *order, size_t per_ct, size_t k,
+                                     size_t n_cts, void *stream);
+int lcb_ctx_ts_assemble_ordered_dev(lcb_ctx *ctx, uint8_t *sig_out, uint8_t *status, const uint8_t *accept,
+                                    const uint8_t *sigs, const uint32_t *order, size_t per_round, size_t k,
+                                    size_t n_rounds, void *stream);
 int lcb_ctx_tpke_verify_phase_ms(lcb_ctx *ctx, float ms[2]);
 int lcb_ctx_tpke_verify_prepared_batched_dev(lcb_ctx *ctx, uint8_t *accept, size_t n_shares, size_t n_keys,
                                              size_t n_cts, const uint32_t *ct_idx, const uint32_t *dec_idx,

@@ -73,16 +73,20 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_ts_miller(const u32 *lines, const u
 // takes the first k shares (in index order) that passed verification, x = index + 1.  A group with fewer than k
 // valid shares gets x = 0 entries, which the Lagrange stage reports as status 0 (the reference keeps waiting
 // for shares / FullDecrypt throws).  pbytes = 48 (G1) or 96 (G2).
+// order (nullable): the caller's arrival order per group — order[r * per_group + j] = the position (DecryptorId /
+// signer index) of the j-th share to arrive; entries >= per_group are absent arrivals.  Null: index order.
 extern "C" __global__ void LCB_BOUNDS k_select_first_valid(const uint8_t *accept, const uint8_t *pts, u32 pbytes,
                                                           u32 per_group, u32 k, u32 n_groups, uint8_t *xs,
-                                                          uint8_t *ys, u32 *off) {
+                                                          uint8_t *ys, u32 *off, const u32 *order) {
     u32 r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n_groups) return;
     off[r] = r * k;
     if (r == n_groups - 1) off[n_groups] = n_groups * k;
     const u32 pw = pbytes / 4;
     u32 cnt = 0;
-    for (u32 i = 0; i < per_group && cnt < k; i++) {
+    for (u32 j = 0; j < per_group && cnt < k; j++) {
+        const u32 i = order ? order[(size_t)r * per_group + j] : j;
+        if (i >= per_group) continue;
         size_t src = (size_t)r * per_group + i;
         if (!accept[src]) continue;
         size_t dst = (size_t)r * k + cnt;
@@ -127,8 +131,8 @@ extern "C" void lcbk_ts_msg_prepare(dim3 grid, hipStream_t s, const uint8_t *msg
 extern "C" void lcbk_ts_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *msg_ok, u32 n_msgs, const void *pks, u32 n_pks, const uint8_t *sigs, const u32 *msg_idx, const u32 *pk_idx, u32 n, u32 *f_soa, uint8_t *accept) {
     LCB_LAUNCH(k_ts_miller, lines, msg_ok, n_msgs, (const g1a_st *)pks, n_pks, sigs, msg_idx, pk_idx, n, f_soa, accept);
 }
-extern "C" void lcbk_select_first_valid(dim3 grid, hipStream_t s, const uint8_t *accept, const uint8_t *pts, u32 pbytes, u32 per_group, u32 k, u32 n_groups, uint8_t *xs, uint8_t *ys, u32 *off) {
-    LCB_LAUNCH(k_select_first_valid, accept, pts, pbytes, per_group, k, n_groups, xs, ys, off);
+extern "C" void lcbk_select_first_valid(dim3 grid, hipStream_t s, const uint8_t *accept, const uint8_t *pts, u32 pbytes, u32 per_group, u32 k, u32 n_groups, uint8_t *xs, uint8_t *ys, u32 *off, const u32 *order) {
+    LCB_LAUNCH(k_select_first_valid, accept, pts, pbytes, per_group, k, n_groups, xs, ys, off, order);
 }
 extern "C" void lcbk_coin_fold(dim3 grid, hipStream_t s, const uint8_t *sigs, u32 n, uint8_t *parity, uint64_t *nonce) {
     LCB_LAUNCH(k_coin_fold, sigs, n, parity, nonce);

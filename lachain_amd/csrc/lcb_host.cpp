@@ -1098,7 +1098,7 @@ int lagrange_enqueue(lcb_ctx *c, int g, uint8_t *dout, uint8_t *dst, const uint8
     return launched("lagrange launch") ? 0 : -1;
 }
 int assemble_enqueue(lcb_ctx *c, int g, uint8_t *out, uint8_t *status, const uint8_t *accept, const uint8_t *pts,
-                     size_t per_group, size_t k, size_t n_groups, hipStream_t s) {
+                     size_t per_group, size_t k, size_t n_groups, hipStream_t s, const uint32_t *order = nullptr) {
     if (!n_groups) return 0;
     if (k == 0 || k > per_group) { set_err("assemble: need 0 < k <= shares per group"); return -1; }
     size_t pb = g == 1 ? 48 : 96, ne = n_groups * k;
@@ -1107,7 +1107,7 @@ int assemble_enqueue(lcb_ctx *c, int g, uint8_t *out, uint8_t *status, const uin
     u32 *off = (u32 *)c->sel[2].get(4 * (n_groups + 1));
     if (!xs || !ys || !off) { set_err("device allocation failed"); return -1; }
     lcbk_select_first_valid(dim3(nblk(n_groups)), s, accept, pts, (u32)pb, (u32)per_group, (u32)k, (u32)n_groups, xs,
-                            ys, off);
+                            ys, off, order);
     return lagrange_enqueue(c, g, out, status, xs, ys, off, n_groups, ne, s);
 }
 
@@ -1256,6 +1256,18 @@ extern "C" int lcb_ctx_tpke_combine_dev(lcb_ctx *ctx, uint8_t *u_out, uint8_t *s
     CTX_OR(c, ctx, -1)
     Enq q(c, (hipStream_t)stream);
     return assemble_enqueue(c, 1, u_out, status, accept, shares, per_ct, k, n_cts, q.s);
+}
+extern "C" int lcb_ctx_tpke_combine_ordered_dev(lcb_ctx *ctx, uint8_t *u_out, uint8_t *status, const uint8_t *accept,
+                                                const uint8_t *shares, const uint32_t *order, size_t per_ct, size_t k,
+                                                size_t n_cts, void *stream) {
+    CTX_OR(c, ctx, -1)
+    Enq q(c, (hipStream_t)stream);
+    return assemble_enqueue(c, 1, u_out, status, accept, shares, per_ct, k, n_cts, q.s, order);
+}
+extern "C" int lcb_tpke_combine_ordered_dev(uint8_t *u_out, uint8_t *status, const uint8_t *accept,
+                                           const uint8_t *shares, const uint32_t *order, size_t per_ct, size_t k,
+                                           size_t n_cts, void *stream) {
+    return lcb_ctx_tpke_combine_ordered_dev(nullptr, u_out, status, accept, shares, order, per_ct, k, n_cts, stream);
 }
 extern "C" int lcb_ctx_tpke_verify_phase_ms(lcb_ctx *ctx, float ms[2]) {
     CTX_OR(c, ctx, -1)
@@ -1541,6 +1553,18 @@ extern "C" int lcb_ctx_ts_assemble_dev(lcb_ctx *ctx, uint8_t *sig_out, uint8_t *
     CTX_OR(c, ctx, -1)
     Enq q(c, (hipStream_t)stream);
     return assemble_enqueue(c, 2, sig_out, status, accept, sigs, per_round, k, n_rounds, q.s);
+}
+extern "C" int lcb_ctx_ts_assemble_ordered_dev(lcb_ctx *ctx, uint8_t *sig_out, uint8_t *status, const uint8_t *accept,
+                                               const uint8_t *sigs, const uint32_t *order, size_t per_round, size_t k,
+                                               size_t n_rounds, void *stream) {
+    CTX_OR(c, ctx, -1)
+    Enq q(c, (hipStream_t)stream);
+    return assemble_enqueue(c, 2, sig_out, status, accept, sigs, per_round, k, n_rounds, q.s, order);
+}
+extern "C" int lcb_ts_assemble_ordered_dev(uint8_t *sig_out, uint8_t *status, const uint8_t *accept, const uint8_t *sigs,
+                                          const uint32_t *order, size_t per_round, size_t k, size_t n_rounds,
+                                          void *stream) {
+    return lcb_ctx_ts_assemble_ordered_dev(nullptr, sig_out, status, accept, sigs, order, per_round, k, n_rounds, stream);
 }
 extern "C" int lcb_ts_prepare_dev(const uint8_t *pks, size_t n_pks, const uint8_t *msg_data, const uint32_t *msg_off,
                                   size_t n_msgs, void *stream) {

@@ -105,6 +105,8 @@ _SIGS = {
     "lcb_tpke_partial_decrypt_prepared_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_size,
                                                              ctypes.c_void_p, c_size, ctypes.c_void_p]),
     "lcb_tpke_combine_dev": (ctypes.c_int, [ctypes.c_void_p] * 4 + [c_size, c_size, c_size, ctypes.c_void_p]),
+    "lcb_tpke_combine_ordered_dev": (ctypes.c_int, [ctypes.c_void_p] * 5 + [c_size, c_size, c_size, ctypes.c_void_p]),
+    "lcb_ts_assemble_ordered_dev": (ctypes.c_int, [ctypes.c_void_p] * 5 + [c_size, c_size, c_size, ctypes.c_void_p]),
     "lcb_tpke_verify_phase_ms": (ctypes.c_int, [ctypes.POINTER(ctypes.c_float)]),
     "lcb_ts_sign": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u32p, c_u32p, c_size]),
     "lcb_g1_lagrange_batch": (ctypes.c_int, [c_u8p, c_u8p, c_u8p, c_u8p, c_u32p, c_size]),
@@ -181,7 +183,8 @@ for _name in ("tpke_prepare_dev", "tpke_verify_prepared_dev", "tpke_verify_prepa
               "tpke_verify_shares_batched_dev", "ts_verify_prepared_batched_dev", "ts_verify_shares_batched_dev", "tpke_partial_decrypt_prepared_dev", "tpke_combine_dev",
               "tpke_verify_phase_ms", "ts_prepare_dev", "ts_verify_prepared_dev", "ts_assemble_dev", "g1_lagrange_dev",
               "g2_lagrange_dev", "g1_msm_dev", "g1_msm_glv_dev", "g1_msm_phase_ms", "ecdsa_verify_hashed_dev",
-              "root_header_verify_dev", "ecdsa_pubkey_dev", "ecdsa_sign_hashed_dev", "ecdsa_phase_ms", "batched_census"):
+              "root_header_verify_dev", "ecdsa_pubkey_dev", "ecdsa_sign_hashed_dev", "ecdsa_phase_ms", "batched_census",
+              "tpke_combine_ordered_dev", "ts_assemble_ordered_dev"):
     _res, _args = _SIGS["lcb_" + _name]
     _SIGS["lcb_ctx_" + _name] = (_res, [ctypes.c_void_p] + list(_args))
 

@@ -209,6 +209,31 @@ def test_epoch_slice_n256_k86(nat, tdev):
     # (wrong) plaintext — bit-exact agreement is what matters for consensus
     assert o.xor_with_hash(uc[:48], cts[0][1]) == plains[0]
     assert o.xor_with_hash(uc[48:], cts[1][1]) != plains[1]
+    # arrival order (HoneyBadger.cs:237-247 combines the first F+1 valid shares to ARRIVE): ciphertext 0 in reverse
+    # order, ciphertext 1 in a shuffled order in which the torsion share 7 arrives last and 20 decryptors never send
+    rng = np.random.default_rng(7)
+    perm = [j for j in rng.permutation(n).tolist() if j != 7] + [7]
+    order1 = perm[:n - 21] + [7] + [0xFFFFFFFF] * 20
+    orders = [list(range(n - 1, -1, -1)), order1]
+    d_ord = up(torch, dev, np.array(orders, dtype=np.uint32))
+    assert lib.lcb_tpke_combine_ordered_dev(d_uc.data_ptr(), d_ust.data_ptr(), d_acc.data_ptr(), d_sh.data_ptr(),
+                                            d_ord.data_ptr(), n, k, 2, sh) == 0
+    torch.cuda.synchronize(dev)
+    assert d_ust.cpu().numpy().tolist() == [1, 1]
+    uc = d_uc.cpu().numpy().tobytes()
+    for c in (0, 1):
+        valid = [j for j in orders[c] if j < n and expect[c * n + j]][:k]
+        assert 7 not in valid or c == 0
+        u_exp = o.g1_lagrange([o.fr(j + 1) for j in valid], [shares[c][j] for j in valid])
+        assert uc[48 * c:48 * c + 48] == u_exp, c
+        assert o.xor_with_hash(uc[48 * c:48 * c + 48], cts[c][1]) == plains[c]     # no torsion share combined
+    # a decryptor listed twice is a repeated abscissa: the group fails
+    dup = [orders[0], [3, 3] + [j for j in range(n) if j != 3]][:2]
+    d_ord = up(torch, dev, np.array([dup[0], dup[1][:n]], dtype=np.uint32))
+    assert lib.lcb_tpke_combine_ordered_dev(d_uc.data_ptr(), d_ust.data_ptr(), d_acc.data_ptr(), d_sh.data_ptr(),
+                                            d_ord.data_ptr(), n, k, 2, sh) == 0
+    torch.cuda.synchronize(dev)
+    assert d_ust.cpu().numpy().tolist() == [1, 0]
 
     # two coins of the era (root coin agreement -1, one BA coin), 256 signature shares each, k = 86
     sks, shared = keyset(d, n, f)
