@@ -126,6 +126,14 @@ static u64 g_count = 0;
 static int g_counting = 0;
 void orc_count_reset(void) { g_count = 0; g_counting = 1; }
 uint64_t orc_count_get(void) { return g_count; }
+/* 1 when this build's Fp product is the MULX / ADX assembly (timing build), 0 for the portable C product */
+int orc_fp_impl(void) {
+#if defined(ORC_FAST) && defined(__x86_64__) && defined(__ADX__) && defined(__BMI2__)
+    return 1;
+#else
+    return 0;
+#endif
+}
 
 static u64 neg_inv64(u64 m0) { /* -m0^{-1} mod 2^64 */
     u64 x = 1;
@@ -169,10 +177,18 @@ DEF_MONT_MUL(mont_mul4, 4)
 typedef struct { u64 l[NP]; } fp;
 static fp FP_ZERO, FP_ONE_M;
 
+#if defined(ORC_FAST) && defined(__x86_64__) && defined(__ADX__) && defined(__BMI2__)
+/* timing build (bench CPU baseline, `make native`): MULX / ADCX / ADOX product, no operation counting */
+#include "mont_adx.h"
+static u64 PX[NP + 1];
+static inline void fp_mul(fp *r, const fp *a, const fp *b) { mont_mul6_adx(r->l, a->l, b->l, PX); }
+#define ORC_FP_ADX 1
+#else
 static inline void fp_mul(fp *r, const fp *a, const fp *b) {
     if (g_counting) g_count++;
     mont_mul6(r->l, a->l, b->l, P, P_INV);
 }
+#endif
 static inline void fp_sqr(fp *r, const fp *a) { fp_mul(r, a, a); }
 static inline void fp_add(fp *r, const fp *a, const fp *b) {
     u64 c = bn_add(r->l, a->l, b->l, NP);
@@ -1127,6 +1143,10 @@ void orc_init(void) {
     bn_from_hex(P, NP, P_HEX);
     bn_from_hex(R_, NR, R_HEX);
     P_INV = neg_inv64(P[0]);
+#ifdef ORC_FP_ADX
+    memcpy(PX, P, sizeof P);
+    PX[NP] = P_INV;
+#endif
     R_INV = neg_inv64(R_[0]);
     /* R2 = 2^(2*64*N) mod m by repeated doubling of 1 */
     {
