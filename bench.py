@@ -27,6 +27,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+from lachain_amd import shard  # noqa: E402  (host-side partition / cross-rank reduction helpers, no GPU work)
 
 R = 0x73EDA753299D7D483339D80809A1D80553BDA402FFFE5BFEFFFFFFFF00000001
 SEED = 0x4C61636861696E
@@ -247,12 +248,7 @@ def run_tpke_patterns(args, nat, torch, dev, world, inp, n, n_cts, n_dec):
                 dist.barrier()
             el = time.perf_counter() - t0
             mism = int(np.sum(got[label] != expect)) + int(np.sum(d_acc.cpu().numpy() != expect))
-            t = torch.tensor([el, float(mism)], dtype=torch.float64, device=dev)
-            if world > 1:
-                tm = t.clone()
-                dist.all_reduce(tm[:1], op=dist.ReduceOp.MAX)
-                dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-                t[0] = tm[0]
+            t = shard.max_time_sum(dist, torch, dev, el, mism)
             rec[label] = {"value": world * n * args.pattern_steps / float(t[0]),
                           "ms_per_step": 1e3 * float(t[0]) / args.pattern_steps, "decision_mismatches": int(t[1])}
             if label == "batched":
@@ -456,11 +452,8 @@ def run_msm(args, nat, torch, dev, rank, world, cpu, n):
     e = torch.tensor(list(expect_local.to_bytes(32, "little")), dtype=torch.uint8, device=dev)
     ok_pts = bool(d_ok.all().item())
     if world > 1:
-        ge = torch.zeros(32 * world, dtype=torch.uint8, device=dev)
-        dist.all_gather_into_tensor(ge, e)
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt[0])
+        ge = shard.all_gather_fixed(dist, e, world)
+        elapsed = shard.max_time_sum(dist, torch, dev, elapsed)[0]
         exp_total = sum(int.from_bytes(bytes(ge[32 * k:32 * k + 32].cpu().numpy().tobytes()), "little")
                         for k in range(world)) % R
     else:
@@ -669,12 +662,7 @@ def run_ts(args, nat, torch, dev, rank, world):
         comb = d_comb.cpu().numpy().tobytes()
         for r in (0, 1, rounds - 1):
             comb_ok = comb_ok and comb[96 * r:96 * r + 96] == o.ts_sign(o.fr(inp["shared_sk"]), inp["msg_list"][r])
-        t = torch.tensor([elapsed, float(mism), float(0 if comb_ok else 1)], dtype=torch.float64, device=dev)
-        if world > 1:
-            tm = t[:1].clone()
-            dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-            dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-            t[0] = tm[0]
+        t = shard.max_time_sum(dist, torch, dev, elapsed, mism, 0 if comb_ok else 1)
         per = args.ts_steps
         elapsed = float(t[0])
         out = dict(value=rounds * n * world * per / elapsed, unit="share verifications/s",
@@ -740,12 +728,7 @@ def run_ts(args, nat, torch, dev, rank, world):
                     dist.barrier()
                 el = time.perf_counter() - t0
                 mism += int(np.sum(d_acc.cpu().numpy() != exp))
-                t = torch.tensor([el, float(mism)], dtype=torch.float64, device=dev)
-                if world > 1:
-                    tm = t[:1].clone()
-                    dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-                    dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-                    t[0] = tm[0]
+                t = shard.max_time_sum(dist, torch, dev, el, mism)
                 rec[label] = {"value": rounds * n * world / float(t[0]), "ms_per_step": 1e3 * float(t[0]),
                               "decision_mismatches": int(t[1])}
                 if label == "batched":
@@ -1012,12 +995,7 @@ def run_replay(args, nat, torch, dev, rank, world):
         bad += own[48 * c:48 * c + 48] != exp_own
     comb = d_comb.cpu().numpy().tobytes()
     bad += comb[:96] != o.ts_sign(o.fr(inp["shared_sk"]), inp["msg_list"][0])
-    t = torch.tensor([elapsed, float(bad)], dtype=torch.float64, device=dev)
-    if world > 1:
-        tm = t[:1].clone()
-        dist.all_reduce(tm, op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        t[0] = tm[0]
+    t = shard.max_time_sum(dist, torch, dev, elapsed, bad)
     if rank != 0:
         return None
     elapsed = float(t[0]) / args.replay_steps
@@ -1132,12 +1110,8 @@ def run_ecdsa(args, nat, torch, dev, rank, world, cpu):
     if lib.lcb_ecdsa_phase_ms(kms) != 0:
         raise RuntimeError(nat.last_error())
     mism = int(np.sum(d_acc.cpu().numpy() != inp["expect"]))
-    t = torch.tensor([elapsed, float(mism)], dtype=torch.float64, device=dev)
-    if world > 1:
-        tm = t.clone()
-        dist.all_reduce(tm[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        elapsed = float(tm[0])
+    t = shard.max_time_sum(dist, torch, dev, elapsed, mism)
+    elapsed = t[0]
     ks.close()
     if rank != 0:
         return None
@@ -1420,12 +1394,8 @@ def run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, dd, n, n_cts, n_d
     if K == 1:
         levels = levels[0]
     ms_points, ms_groups, ms_sum, ms_miller, ms_fe, ms_resolve = ms
-    t = torch.tensor([elapsed, float(mism), float(n)], dtype=torch.float64, device=dev)
-    if world > 1:
-        tmax = t.clone()
-        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        elapsed = float(tmax[0])
+    t = shard.max_time_sum(dist, torch, dev, elapsed, mism, n)
+    elapsed = t[0]
     checks = sum(sum(lv) for lv in levels) if K > 1 else sum(levels)
     ach_pair = checks * (C["C_ML2_NORM2"] + C["C_FE"]) * MAC_PER_FPMUL / ((ms_miller + ms_fe) * 1e-3)
     ach_pts = n * W_RLC_POINTS * MAC_PER_FPMUL / (ms_points * 1e-3)
@@ -1521,10 +1491,13 @@ def main():
     from lachain_amd import native as nat
 
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    nat.load(False).lcb_set_device(local_rank)
+        # RCCL over xGMI on the 8-GPU node; LCB_BENCH_BACKEND=gloo runs the same code with host collectives (the
+        # world-size-2 test on a one-GPU box, where both ranks share the device)
+        dist.init_process_group(os.environ.get("LCB_BENCH_BACKEND", "nccl"), init_method="env://")
+    gpu = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    nat.load(False).lcb_set_device(gpu)
     nat.lib()
     if args.coop_max >= 0:
         nat.set_coop_max(args.coop_max)
@@ -1591,12 +1564,8 @@ def main():
         miller_ms, fexp_ms = float(kms[0]), float(kms[1])
         got = d_acc.cpu().numpy()
         mismatches += int(np.sum(got != inp["expect"]))
-        t = torch.tensor([elapsed, float(mismatches), float(n)], dtype=torch.float64, device=dev)
-        if world > 1:
-            tmax = t.clone()
-            dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
-            dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-            elapsed = float(tmax[0])
+        t = shard.max_time_sum(dist, torch, dev, elapsed, mismatches, n)
+        elapsed = t[0]
         achieved = n * W_VERIFY * MAC_PER_FPMUL / (ver_ms * 1e-3)
         exact = dict(
             metric="BLS12-381 TPKE decryption-share verifications/sec, exact per-share check (the reference's "

@@ -92,6 +92,33 @@ extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_final_exp_check(u3
     if (live && c.j == 0 && accept) accept[item] = accept[item] && one;
 }
 
+// The exact per-share check (k_tpke_miller's inputs) in the cooperative kernels' form, for small batches: share i
+// becomes check i with points (U_i, -Y_i) on ciphertext c's two line sets.  accept[i] = the share's validity
+// (index range, decompression, key, ciphertext), ANDed with the pairing result by k_coop_final_exp_check.
+extern "C" __global__ void LCB_BOUNDS k_tpke_exact_points(const uint8_t *ct_ok, u32 n_cts, const g1a_st *keys,
+                                                         u32 n_keys, const u32 *ct_idx, const u32 *dec_idx,
+                                                         const uint8_t *ui, u32 n, g1a_st *gpts, uint4 *desc,
+                                                         uint8_t *accept) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    u32 c = ct_idx[i], d = dec_idx[i];
+    bool ok = d < n_keys && c < n_cts;
+    c = c < n_cts ? c : 0;
+    ok = ok && ct_ok[c];
+    g1a U;
+    ok = g1_decompress(U, ui + 48 * (size_t)i) && ok;
+    g1a_st ks = keys[d < n_keys ? d : 0];
+    ok = ok && ks.ok;
+    g1a_st o;
+    o.ok = 1; o.pad[0] = o.pad[1] = 0;
+    o.inf = U.inf ? 1 : 0; o.x = U.x; o.y = U.y;
+    gpts[2 * (size_t)i] = o;
+    o.inf = ks.inf; o.x = ks.x; fp_neg(o.y, ks.y);
+    gpts[2 * (size_t)i + 1] = o;
+    desc[i] = make_uint4(i, 1, c, 0);
+    accept[i] = ok;
+}
+
 // ---------------------------------------------------------------- test hook: one cooperative operation vs field.hpp
 // op: 0 sqr12, 1 cyc_sqr, 2 mul12, 3 mul12 (conj a), 4..6 frob1..3, 7 inverse, 8 conj, 9 line (b, c = coefficients 0, 1
 // of b), 10 final exponentiation.  a in park slot 0 of ws (6 slots), b in b_soa; out = cooperative result, ref = the
@@ -157,6 +184,13 @@ extern "C" void lcbk_coop_tpke_miller(hipStream_t s, const u32 *lines, const voi
 extern "C" void lcbk_coop_final_exp_check(hipStream_t s, u32 *park, u32 n, uint8_t *accept) {
     dim3 grid((n + CP_G - 1) / CP_G);
     hipLaunchKernelGGL(k_coop_final_exp_check, grid, dim3(CP_BLOCK), 0, s, park, n, accept);
+}
+extern "C" void lcbk_tpke_exact_points(hipStream_t s, const uint8_t *ct_ok, u32 n_cts, const void *keys, u32 n_keys,
+                                       const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, void *gpts,
+                                       void *desc, uint8_t *accept) {
+    dim3 grid((n + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_tpke_exact_points, ct_ok, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, (g1a_st *)gpts,
+               (uint4 *)desc, accept);
 }
 extern "C" void lcbk_coop_debug(hipStream_t s, int op, u32 *ws, const u32 *b_soa, u32 n, u32 *out, u32 *ref) {
     dim3 grid((n + CP_G - 1) / CP_G);

@@ -86,6 +86,7 @@ extern "C" void lcbk_mcl_horner(hipStream_t s, int g, const u32 *coef, u32 n, co
 extern "C" void lcbk_mcl_g1_sum(hipStream_t s, const void *in, u32 n, void *out);
 extern "C" void lcbk_mcl_from_bytes(hipStream_t s, int g, const uint8_t *in, u32 n, u32 *out, uint8_t *ok);
 extern "C" void lcbk_mcl_to_bytes(hipStream_t s, int g, const u32 *in, u32 n, uint8_t *out);
+extern "C" void lcbk_tpke_exact_points(hipStream_t s, const uint8_t *ct_ok, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, void *gpts, void *desc, uint8_t *accept);
 extern "C" void lcbk_coop_debug(hipStream_t s, int op, u32 *ws, const u32 *b_soa, u32 n, u32 *out, u32 *ref);
 extern "C" void lcbk_coop_final_exp_check(hipStream_t s, u32 *park, u32 n, uint8_t *accept);
 extern "C" void lcbk_op(dim3 grid, hipStream_t s, int op, u32 *io, int orig_cof);

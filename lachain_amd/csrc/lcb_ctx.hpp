@@ -39,6 +39,7 @@ struct lcb_ctx {
     bool order_valid = false;
     // TPKE workspace (lcb_*tpke_prepare_dev): line sets of H and W per ciphertext, validity, decompressed keys
     DevBuf t_lines, t_ctok, t_keys, t_f;
+    DevBuf t_coop[3];                 // small exact batches on the cooperative kernels: point records, checks, flags
     size_t t_n_cts = 0, t_n_keys = 0;
     uint64_t t_gen = 0;
     bool t_ready = false;

@@ -471,6 +471,7 @@ void ctx_free(lcb_ctx *c) {
     for (auto &b : c->out) b.release();
     for (auto &b : c->dkg) b.release();
     for (auto &b : c->mcl) b.release();
+    for (auto &b : c->t_coop) b.release();
     for (auto &b : c->rlc) b.release();
     if (c->rlc_ev_ready) {
         for (auto &e : c->rlc_ev) (void)hipEventDestroy(e);
@@ -575,6 +576,7 @@ bool tpke_shape_ok(lcb_ctx *c, size_t n_keys, size_t n_cts, const char *what) {
     }
     return true;
 }
+std::atomic<uint32_t> g_coop_max{32768};    // lcb_set_coop_max: batches / levels of <= this many checks use the 9-lane kernels
 int tpke_verify_prepared(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_keys, size_t n_cts, const uint32_t *d_ct,
                          const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
     if (!tpke_shape_ok(c, n_keys, n_cts, "tpke verify")) return -1;
@@ -591,13 +593,27 @@ int tpke_verify_prepared(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_keys,
             for (auto &e : c->ver_ev) hipEventCreate(&e);
             c->ver_ev_ready = true;
         }
+        // small batches (the protocol's one-share-per-call shape, the queue's flushes): nine lanes per check
+        // (k_coop.hip) instead of one, below the size where the one-lane kernels fill the GPU
+        const bool coop = n <= g_coop_max.load();
+        void *gpts = coop ? c->t_coop[0].get(n * 2 * LCB_G1A_ST_BYTES) : nullptr;
+        void *desc = coop ? c->t_coop[1].get(n * 16) : nullptr;
+        uint8_t *fl = coop ? (uint8_t *)c->t_coop[2].get(2 * n) : nullptr;
+        if (coop && (!gpts || !desc || !fl)) { set_err("device allocation failed"); return -1; }
         for (size_t o = 0; o < n; o += LCB_VERIFY_CHUNK) {
             const size_t m = n - o < LCB_VERIFY_CHUNK ? n - o : LCB_VERIFY_CHUNK;
             if (o == 0) hipEventRecord(c->ver_ev[0], s);
-            lcbk_tpke_miller(dim3(nblk(m)), s, lines, ctok, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct + o, d_dec + o,
-                             d_ui + 48 * o, (u32)m, f, d_accept + o);
+            if (coop) {
+                lcbk_tpke_exact_points(s, ctok, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct, d_dec, d_ui, (u32)m, gpts,
+                                       desc, d_accept);
+                lcbk_coop_tpke_miller(s, lines, desc, gpts, (u32)m, f, fl, fl + n);
+            } else {
+                lcbk_tpke_miller(dim3(nblk(m)), s, lines, ctok, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct + o,
+                                 d_dec + o, d_ui + 48 * o, (u32)m, f, d_accept + o);
+            }
             if (o == 0) hipEventRecord(c->ver_ev[1], s);
-            lcbk_final_exp_check(dim3(nblk(m)), s, f, (u32)m, d_accept + o);
+            if (coop) lcbk_coop_final_exp_check(s, f, (u32)m, d_accept + o);
+            else lcbk_final_exp_check(dim3(nblk(m)), s, f, (u32)m, d_accept + o);
             if (o == 0) hipEventRecord(c->ver_ev[2], s);
         }
         c->ver_ran = true;
@@ -621,7 +637,6 @@ std::mutex g_seed_mu;                       // lcb_set_batch_seed (test hook) vs
 uint8_t g_rlc_seed[32];
 bool g_rlc_seed_set = false;
 std::atomic<size_t> g_census_min{16384};    // lcb_set_batch_census: batches of at least this many shares get a census
-std::atomic<uint32_t> g_coop_max{32768};    // lcb_set_coop_max: levels of <= this many checks use the 9-lane kernels
 enum RlcKind { RLC_TPKE = 0, RLC_TS = 1 };
 struct RlcStats {
     bool valid = false;

@@ -28,15 +28,38 @@ def tpke_shard(ct_idx, n_cts, rank, world):
     return lo, hi, sel
 
 
+def _host_comm(dist, t):
+    """gloo moves host tensors only: a device tensor is exchanged through host memory under a non-RCCL backend"""
+    return t.is_cuda and dist.get_backend() != "nccl"
+
+
 def all_gather_fixed(dist, local, world):
     """All-gather of equal-sized 1-D uint8 tensors -> one tensor of world * len(local) bytes (rank order)."""
     import torch
     out = torch.empty(world * local.numel(), dtype=local.dtype, device=local.device)
     if world == 1:
         out.copy_(local)
+    elif _host_comm(dist, local):
+        host = torch.empty(world * local.numel(), dtype=local.dtype)
+        dist.all_gather_into_tensor(host, local.cpu())
+        out.copy_(host)
     else:
         dist.all_gather_into_tensor(out, local)
     return out
+
+
+def max_time_sum(dist, torch, dev, elapsed, *counts):
+    """The bench's cross-rank reduction: [max over ranks of elapsed (a job takes as long as its slowest rank),
+    sum over ranks of each count].  Plain floats at world size 1 or without a process group."""
+    vals = [float(elapsed)] + [float(c) for c in counts]
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return vals
+    cd = dev if dist.get_backend() == "nccl" else "cpu"
+    tm = torch.tensor(vals[:1], dtype=torch.float64, device=cd)
+    ts = torch.tensor(vals[1:] + [0.0], dtype=torch.float64, device=cd)
+    dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+    dist.all_reduce(ts, op=dist.ReduceOp.SUM)
+    return [float(tm[0])] + [float(x) for x in ts.tolist()[:len(counts)]]
 
 
 def gather_bitmaps(dist, local_bits, world):

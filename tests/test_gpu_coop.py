@@ -129,3 +129,23 @@ def test_batched_density_coop(nat, coop_mode):
     shares = [(ct[i], dec[i], (b.bad if bad[i] else b.good)[ct[i]][dec[i]]) for i in range(n)]
     got = nat.tpke_verify_shares(b.yi, b.cts, shares, batched=True)
     assert got == [not x for x in bad]
+
+
+@pytest.mark.parametrize("general_lines", [False, True])
+@pytest.mark.parametrize("key", ["tpke_n4", "tpke_n22"])
+def test_exact_transcripts_coop(nat, coop_mode, key, general_lines):
+    """The exact per-share check (lcb_tpke_verify_shares) on the nine-lane kernels (small batches) and on the one-lane
+    kernels: the transcripts' decisions either way, with normalised line sets and with every set forced onto the
+    on-the-fly fallback (k_rlc_miller_fallback)"""
+    nat.set_line_mode(general_lines)
+    try:
+        t = T[key]
+        cts = [(H(c["u"]), H(c["v"]), H(c["w"])) for c in t["ciphertexts"]]
+        shares = [(ci, i, H(s)) for ci, c in enumerate(t["ciphertexts"]) for i, s in enumerate(c["shares"])]
+        want = [a for c in t["ciphertexts"] for a in c["accept"]]
+        assert nat.tpke_verify_shares([H(y) for y in t["y_i"]], cts, shares) == want
+        # out-of-range ciphertext / decryptor indices reject (and are clamped), on either kernel family
+        bad = [(len(cts), 0, shares[0][2]), (0, len(t["y_i"]), shares[0][2])] + shares[:3]
+        assert nat.tpke_verify_shares([H(y) for y in t["y_i"]], cts, bad) == [False, False] + want[:3]
+    finally:
+        nat.set_line_mode(False)
