@@ -144,8 +144,11 @@ def test_exact_transcripts_coop(nat, coop_mode, key, general_lines):
         shares = [(ci, i, H(s)) for ci, c in enumerate(t["ciphertexts"]) for i, s in enumerate(c["shares"])]
         want = [a for c in t["ciphertexts"] for a in c["accept"]]
         assert nat.tpke_verify_shares([H(y) for y in t["y_i"]], cts, shares) == want
-        # out-of-range ciphertext / decryptor indices reject (and are clamped), on either kernel family
-        bad = [(len(cts), 0, shares[0][2]), (0, len(t["y_i"]), shares[0][2])] + shares[:3]
-        assert nat.tpke_verify_shares([H(y) for y in t["y_i"]], cts, bad) == [False, False] + want[:3]
+        # a malformed share (bytes reversed, HoneyBadgerMalicious.cs:23) and a valid point that is not the share
+        ys = [H(y) for y in t["y_i"]]
+        bad = [(0, 0, shares[0][2][::-1]), (0, 1, shares[0][2])]
+        exp = [o.g1_valid(ui) and o.tpke_verify_share(ys[d], *cts[c], ui) == 1 for c, d, ui in bad]
+        assert exp[1] is False
+        assert nat.tpke_verify_shares(ys, cts, bad + shares[:3]) == exp + want[:3]
     finally:
         nat.set_line_mode(False)
