@@ -51,6 +51,11 @@ struct lcb_ctx {
     // Lagrange / assembly / MSM / staging
     DevBuf lag[3], sel[3], msm[12], in[8], out[4], dkg[9];
     DevBuf mcl[8];                    // the mcl surface's pairing / multi-scalar / Horner / Lagrange staging
+    // mclBn_pairing's cache of G2 line sets (mcl[2]: slot k = Q_k's set and the infinity set), least recently used
+    // slot replaced: the protocol pairs every share of a ciphertext / coin with the same H, W (TPKE/PublicKey.cs:91)
+    std::vector<uint32_t> pc_keys;    // 72 words (the mclBnG2 record) per slot
+    std::vector<uint64_t> pc_used;    // last use (0: empty)
+    uint64_t pc_tick = 0;
     hipEvent_t ver_ev[3] = {};
     bool ver_ev_ready = false, ver_ran = false;
     // randomized batch verification (k_batch.hip): r_i U_i / r_i Y_i records, group lists, group points, counts

@@ -2015,6 +2015,7 @@ extern "C" int lcb_g2_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_
 // ================================================================== mcl surface on the batch / cooperative kernels
 // (k_mcl.hip, k_coop.hip) — each a single synchronous call on the calling thread's own context
 
+#define LCB_PAIR_CACHE 32    // line-set slots per context (2 x 26 KB each)
 // mclBn_pairing (GT.Pairing: TPKE/PrivateKey.cs:26, TPKE/PublicKey.cs:91, ThresholdSignature/PublicKey.cs:20) as a
 // one-group cooperative check: P and the point at infinity, Q's normalised line set and the set of infinity, then
 // the nine-lane final exponentiation.  The lines are normalised (divided by their Fp2 leading coefficient), which
@@ -2026,20 +2027,33 @@ extern "C" void mclBn_pairing(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) {
     const size_t slots = lcbk_fe_slots() > 6 ? (size_t)lcbk_fe_slots() : 6;
     u32 *in = (u32 *)c->mcl[0].get(108 * 4);
     void *gpts = c->mcl[1].get(2 * LCB_G1A_ST_BYTES);
-    u32 *lines = (u32 *)c->mcl[2].get(2 * LCB_LINESET_BYTES);
+    u32 *lines = (u32 *)c->mcl[2].get((size_t)2 * LCB_PAIR_CACHE * LCB_LINESET_BYTES);
     void *desc = c->mcl[3].get(16);
     u32 *park = (u32 *)c->mcl[4].get(576 * slots);
     uint8_t *fl = (uint8_t *)c->mcl[5].get(64);
     if (!in || !gpts || !lines || !desc || !park || !fl) { set_err("device allocation failed"); return; }
+    if (c->pc_used.empty()) {
+        c->pc_keys.assign((size_t)72 * LCB_PAIR_CACHE, 0);
+        c->pc_used.assign(LCB_PAIR_CACHE, 0);
+    }
+    u32 slot = 0;
+    bool hit = false;
+    for (u32 k = 0; k < LCB_PAIR_CACHE; k++) {
+        if (c->pc_used[k] && memcmp(&c->pc_keys[72 * (size_t)k], y, 288) == 0) { slot = k; hit = true; break; }
+        if (c->pc_used[k] < c->pc_used[slot]) slot = k;
+    }
+    c->pc_used[slot] = ++c->pc_tick;
+    if (!hit) memcpy(&c->pc_keys[72 * (size_t)slot], y, 288);
     hipMemcpyAsync(in, x, 144, hipMemcpyHostToDevice, s);
-    hipMemcpyAsync(in + 36, y, 288, hipMemcpyHostToDevice, s);
-    lcbk_pairing_prep(s, in, gpts, lines, desc);
-    lcbk_lineset_fill(dim3(1), s, lines, 2);
+    if (!hit) hipMemcpyAsync(in + 36, y, 288, hipMemcpyHostToDevice, s);
+    lcbk_pairing_prep(s, in, gpts, lines, desc, slot, hit ? 0 : 1);
+    if (!hit) lcbk_lineset_fill(dim3(1), s, lines + (size_t)2 * slot * (LCB_LINESET_BYTES / 4), 2);
     lcbk_coop_tpke_miller(s, lines, desc, gpts, 1, park, fl, fl + 32);
     lcbk_coop_final_exp_check(s, park, 1, nullptr);
     u32 r[144];
     hipMemcpyAsync(r, park, 576, hipMemcpyDeviceToHost, s);
     if (sync_check(c, "pairing")) memcpy(z, r, 576);
+    else c->pc_used[slot] = 0;                    // the slot's lines may be incomplete
 }
 // mclBn_finalExp on the nine-lane kernel (park slot 0 of a one-value workspace)
 extern "C" void mclBn_finalExp(mclBnGT *y, const mclBnGT *x) {

@@ -154,3 +154,20 @@ def test_single_operations_from_many_threads(mcl):
         t.join()
     assert not errs, errs
     assert got == want
+
+
+def test_pairing_line_cache(mcl):
+    """mclBn_pairing keeps the line sets of the last 32 distinct G2 arguments per thread: hits, misses and evictions
+    (40 distinct Q, revisited out of order) all give the oracle's GT value"""
+    Fr, G1, G2, GT = mcl.Fr, mcl.G1, mcl.G2, mcl.GT
+    P = G1.Generator() * Fr.FromInt(7)
+    Qs = [G2.Generator() * Fr.FromInt(i + 2) for i in range(40)]
+    want = {}
+    order = list(range(40)) + [39, 0, 5, 38, 1, 1, 20, 33, 8, 39]
+    for i in order:
+        if i not in want:
+            want[i] = o.pairing(P.ToBytes(), Qs[i].ToBytes())
+        assert GT.Pairing(P, Qs[i]).ToBytes() == want[i], i
+    # the same Q with another P hits the cache
+    P2 = G1.Generator() * Fr.FromInt(11)
+    assert GT.Pairing(P2, Qs[39]).ToBytes() == o.pairing(P2.ToBytes(), Qs[39].ToBytes())
