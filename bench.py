@@ -1243,6 +1243,9 @@ def run_mcl_latency(args, nat, rank):
     a, b = Fr.GetRandom(), Fr.GetRandom()
     P, Q = G1.Generator() * a, G2.Generator() * b
     ab, bb, Pb, Qb = a.ToBytes(), b.ToBytes(), P.ToBytes(), Q.ToBytes()
+    import itertools
+    Qring = [G2.Generator() * Fr.GetRandom() for _ in range(40)]       # more than the 32-slot line-set cache
+    qi = itertools.count()
     f = GT()
     mcl._f("mclBn_millerLoop", None, [ctypes.POINTER(type(f.v)), ctypes.POINTER(type(P.v)),
                                       ctypes.POINTER(type(Q.v))])(ctypes.byref(f.v), ctypes.byref(P.v), ctypes.byref(Q.v))
@@ -1284,6 +1287,7 @@ def run_mcl_latency(args, nat, rank):
         "G1_mul": 1e3 * med(lambda: P * a),
         "G2_mul": 1e3 * med(lambda: Q * a),
         "pairing": 1e3 * med(lambda: GT.Pairing(P, Q)),
+        "pairing_new_Q": 1e3 * med(lambda: GT.Pairing(P, Qring[next(qi) % len(Qring)])),
         "finalExp": 1e3 * med(lambda: fe(ctypes.byref(g.v), ctypes.byref(f.v))),
         "G1_mulVec_n%d" % args.n: 1e3 * med(lambda: mv(ctypes.byref(out.v), pa, sa, args.n)),
         "G1_Lagrange_k%d" % (args.f + 1): 1e3 * med(lambda: M.LagrangeInterpolate(xs, ys)),
@@ -1300,7 +1304,10 @@ def run_mcl_latency(args, nat, rank):
     return dict(metric="mcl single-call latency (median, one thread, through ctypes)", unit="us per call",
                 gpu=res, oracle_cpu=ref,
                 note="GPU-backed calls are a synchronous round trip each (launch + copies); Fr arithmetic is host "
-                     "code (fr_host.hpp).  oracle_cpu: the oracle's plain-C routines, one thread, same inputs")
+                     "code (fr_host.hpp).  pairing: a repeated G2 argument (its line set cached per thread, as for "
+                     "the H and W every share of a ciphertext is paired with); pairing_new_Q: 40 rotating G2 "
+                     "arguments (every call computes its line set).  oracle_cpu: the oracle's plain-C routines "
+                     "(portable build), one thread, same inputs")
 
 
 C["C_MUL1_64"] = round(C["C_MUL1"] * 64 / 255)          # 64-bit var-base G1 multiplication (double-and-add)
