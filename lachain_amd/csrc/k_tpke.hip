@@ -27,12 +27,14 @@ extern "C" __global__ void LCB_BOUNDS k_g2_decompress(const uint8_t *in, u32 n, 
 
 // ================================================================================= TPKE
 // lines layout: lines[(2*c + 0) * LINESET] = H lines, lines[(2*c + 1) * LINESET] = W lines
+// slot (nullable): ciphertext c's line sets and validity go to slot[c] instead of c (the prepared-ciphertext cache)
 extern "C" __global__ void LCB_BOUNDS k_tpke_ct_prepare(const uint8_t *cts_u, const uint8_t *cts_w,
                                                        const uint8_t *v_data, const u32 *v_off, u32 n_cts,
-                                                       u32 *lines, uint8_t *ct_ok, int flags) {
+                                                       u32 *lines, uint8_t *ct_ok, int flags, const u32 *slot) {
     // flags: bit 0 = mcl's original G2 cofactor clearing in hash-to-G2, bit 1 = mark the line sets un-normalised
     u32 c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_cts) return;
+    const u32 o = slot ? slot[c] : c;
     const uint8_t *ub = cts_u + 48 * (size_t)c;
     g1a U;
     g2a W, Ha;
@@ -50,18 +52,19 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_ct_prepare(const uint8_t *cts_u, co
     if (!ok) { W.inf = true; Ha.inf = true; }
     // the two points go to their line sets' point slots; k_lineset_fill computes the 2 * n_cts line sets one lane
     // each (the per-ciphertext serial path is hash + one line set instead of hash + two)
-    u32 *lsH = lines + (size_t)(2 * c) * LCB_LINESET_WORDS, *lsW = lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS;
+    u32 *lsH = lines + (size_t)(2 * o) * LCB_LINESET_WORDS, *lsW = lines + (size_t)(2 * o + 1) * LCB_LINESET_WORDS;
     lineset_put_point(lsH, Ha);
     lineset_put_point(lsW, W);
     lsH[LCB_LS_FLAG + 2] = lsW[LCB_LS_FLAG + 2] = (flags & 2) ? 1 : 0;
-    ct_ok[c] = ok;
+    ct_ok[o] = ok;
 }
 
-// line sets of points stored by a prepare kernel (lineset_put_point): one lane per set
-extern "C" __global__ void LCB_BOUNDS k_lineset_fill(u32 *lines, u32 n_sets) {
+// line sets of points stored by a prepare kernel (lineset_put_point): one lane per set; sets (nullable) lists the
+// set indices to fill (the prepared-ciphertext cache fills scattered slots)
+extern "C" __global__ void LCB_BOUNDS k_lineset_fill(u32 *lines, u32 n_sets, const u32 *sets) {
     u32 k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_sets) return;
-    u32 *ls = lines + (size_t)k * LCB_LINESET_WORDS;
+    u32 *ls = lines + (size_t)(sets ? sets[k] : k) * LCB_LINESET_WORDS;
     g2a Q;
     lineset_get_point(Q, ls);
     u32 force_general = ls[LCB_LS_FLAG + 2];
@@ -152,11 +155,11 @@ extern "C" void lcbk_g1_decompress(dim3 grid, hipStream_t s, const uint8_t *in, 
 extern "C" void lcbk_g2_decompress(dim3 grid, hipStream_t s, const uint8_t *in, u32 n, void *out) {
     LCB_LAUNCH(k_g2_decompress, in, n, (g2a_st *)out);
 }
-extern "C" void lcbk_tpke_ct_prepare(dim3 grid, hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data, const u32 *v_off, u32 n_cts, u32 *lines, uint8_t *ct_ok, int orig_cof) {
-    LCB_LAUNCH(k_tpke_ct_prepare, cts_u, cts_w, v_data, v_off, n_cts, lines, ct_ok, orig_cof);
+extern "C" void lcbk_tpke_ct_prepare(dim3 grid, hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data, const u32 *v_off, u32 n_cts, u32 *lines, uint8_t *ct_ok, int orig_cof, const u32 *slot) {
+    LCB_LAUNCH(k_tpke_ct_prepare, cts_u, cts_w, v_data, v_off, n_cts, lines, ct_ok, orig_cof, slot);
 }
-extern "C" void lcbk_lineset_fill(dim3 grid, hipStream_t s, u32 *lines, u32 n_sets) {
-    LCB_LAUNCH(k_lineset_fill, lines, n_sets);
+extern "C" void lcbk_lineset_fill(dim3 grid, hipStream_t s, u32 *lines, u32 n_sets, const u32 *sets) {
+    LCB_LAUNCH(k_lineset_fill, lines, n_sets, sets);
 }
 extern "C" void lcbk_tpke_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, u32 *f_soa, uint8_t *accept) {
     LCB_LAUNCH(k_tpke_miller, lines, ct_ok, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, f_soa, accept);

@@ -10,6 +10,8 @@
 #include <stdint.h>
 #include <mutex>
 #include <vector>
+#include <string>
+#include <unordered_map>
 
 struct DevBuf {
     void *p = nullptr;
@@ -40,6 +42,13 @@ struct lcb_ctx {
     // TPKE workspace (lcb_*tpke_prepare_dev): line sets of H and W per ciphertext, validity, decompressed keys
     DevBuf t_lines, t_ctok, t_keys, t_f;
     DevBuf t_coop[3];                 // small exact batches on the cooperative kernels: point records, checks, flags
+    // prepared-ciphertext cache of lcb_tpke_verify_shares_cached (line sets + validity per slot, keyed by the bytes)
+    DevBuf cc_lines, cc_ok;
+    std::unordered_map<std::string, uint32_t> cc_map;
+    std::vector<std::string> cc_keys;
+    std::vector<uint64_t> cc_used;
+    uint64_t cc_tick = 0;
+    int cc_flags = -1;
     size_t t_n_cts = 0, t_n_keys = 0;
     uint64_t t_gen = 0;
     bool t_ready = false;

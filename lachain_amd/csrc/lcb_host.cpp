@@ -472,6 +472,8 @@ void ctx_free(lcb_ctx *c) {
     for (auto &b : c->dkg) b.release();
     for (auto &b : c->mcl) b.release();
     for (auto &b : c->t_coop) b.release();
+    c->cc_lines.release();
+    c->cc_ok.release();
     for (auto &b : c->rlc) b.release();
     if (c->rlc_ev_ready) {
         for (auto &e : c->rlc_ev) (void)hipEventDestroy(e);
@@ -546,6 +548,7 @@ bool sync_check(lcb_ctx *c, const char *what) {
 
 // ------------------------------------------------------------------ TPKE
 #define LCB_VERIFY_CHUNK ((size_t)1 << 21)   // shares per Miller + final-exponentiation launch pair
+#define LCB_CT_CACHE 1024                       // prepared-ciphertext cache slots per context (52.7 KB of lines each)
 
 int tpke_prepare(lcb_ctx *c, const uint8_t *d_y, size_t n_keys, const uint8_t *d_u, const uint8_t *d_w,
                  const uint8_t *d_v, const uint32_t *d_voff, size_t n_cts, hipStream_t s) {
@@ -558,8 +561,8 @@ int tpke_prepare(lcb_ctx *c, const uint8_t *d_y, size_t n_keys, const uint8_t *d
     if (n_keys) lcbk_g1_decompress(dim3(nblk(n_keys)), s, d_y, (u32)n_keys, keys);
     if (n_cts) {
         lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), s, d_u, d_w, d_v, d_voff, (u32)n_cts, lines, ctok,
-                             g_orig_cofactor | (g_line_mode << 1));
-        lcbk_lineset_fill(dim3(nblk(2 * n_cts)), s, lines, (u32)(2 * n_cts));
+                             g_orig_cofactor | (g_line_mode << 1), nullptr);
+        lcbk_lineset_fill(dim3(nblk(2 * n_cts)), s, lines, (u32)(2 * n_cts), nullptr);
     }
     if (!launched("tpke prepare launch")) return -1;
     c->t_n_cts = n_cts;
@@ -577,12 +580,10 @@ bool tpke_shape_ok(lcb_ctx *c, size_t n_keys, size_t n_cts, const char *what) {
     return true;
 }
 std::atomic<uint32_t> g_coop_max{32768};    // lcb_set_coop_max: batches / levels of <= this many checks use the 9-lane kernels
-int tpke_verify_prepared(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_keys, size_t n_cts, const uint32_t *d_ct,
-                         const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
-    if (!tpke_shape_ok(c, n_keys, n_cts, "tpke verify")) return -1;
+// the exact check of n shares against prepared line sets (lines, ctok: n_cts ciphertexts) and decompressed keys
+int tpke_verify_core(lcb_ctx *c, const u32 *lines, const uint8_t *ctok, size_t n_cts, size_t n_keys, uint8_t *d_accept,
+                     size_t n, const uint32_t *d_ct, const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
     if (n > 0xffffffffu) { set_err("tpke verify: batch too large"); return -1; }
-    const u32 *lines = (const u32 *)c->t_lines.p;
-    const uint8_t *ctok = (const uint8_t *)c->t_ctok.p;
     if (n) {
         // chunks of at most LCB_VERIFY_CHUNK shares: bounded park buffer (slots x 576 B per share) whatever n is;
         // the phase events time the first chunk
@@ -619,6 +620,12 @@ int tpke_verify_prepared(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_keys,
         c->ver_ran = true;
     }
     return launched("tpke verify launch") ? 0 : -1;
+}
+int tpke_verify_prepared(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_keys, size_t n_cts, const uint32_t *d_ct,
+                         const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
+    if (!tpke_shape_ok(c, n_keys, n_cts, "tpke verify")) return -1;
+    return tpke_verify_core(c, (const u32 *)c->t_lines.p, (const uint8_t *)c->t_ctok.p, n_cts, n_keys, d_accept, n, d_ct,
+                            d_dec, d_ui, s);
 }
 int tpke_partial_decrypt_prepared(lcb_ctx *c, uint8_t *ui_out, uint8_t *status, const uint8_t *x_raw, size_t x_stride,
                                   const uint8_t *cts_u, size_t n_cts, hipStream_t s) {
@@ -978,8 +985,8 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
     }
     if (n_cts) {
         lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), s, d_u, d_w, d_v, d_voff, (u32)n_cts, lines, ctok,
-                             g_orig_cofactor | (g_line_mode << 1));
-        lcbk_lineset_fill(dim3(nblk(2 * n_cts)), s, lines, (u32)(2 * n_cts));
+                             g_orig_cofactor | (g_line_mode << 1), nullptr);
+        lcbk_lineset_fill(dim3(nblk(2 * n_cts)), s, lines, (u32)(2 * n_cts), nullptr);
     }
     if (!launched("tpke prepare launch")) return -1;
     c->t_n_cts = n_cts;
@@ -1471,6 +1478,102 @@ static int tpke_verify_shares_host(uint8_t *accept, size_t n, const uint8_t *y_k
     }
     if (n) hipMemcpyAsync(accept, dacc, n, hipMemcpyDeviceToHost, s);
     return sync_check(c, "tpke verify") ? 0 : -1;
+}
+// lcb_tpke_verify_shares with a per-context cache of prepared ciphertexts (the line sets of H and W and the
+// validity, keyed by the ciphertext's bytes, least recently used slot replaced): the protocol verifies the N shares of
+// a ciphertext in separate calls (HoneyBadger.cs:211-212), so each ciphertext is hashed to G2 and its lines computed
+// once, not once per call.  Same decisions as lcb_tpke_verify_shares (a cache entry is the prepare output for the
+// same bytes under the same prepare flags).
+extern "C" int lcb_tpke_verify_shares_cached(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys,
+                                             const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
+                                             const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
+                                             const uint32_t *dec_idx, const uint8_t *ui) {
+    SYNC_CTX_OR(c, -1)
+    if (n_cts > LCB_CT_CACHE / 2)        // a batch this wide gains nothing from the cache
+        return tpke_verify_shares_host(accept, n, y_keys, n_keys, cts_u, cts_w, v_data, v_off, n_cts, ct_idx, dec_idx,
+                                       ui, false);
+    for (size_t i = 0; i < n; i++) {
+        if (ct_idx[i] >= n_cts) { set_err("ct_idx out of range"); return -1; }
+        if (dec_idx[i] >= n_keys) { set_err("dec_idx out of range"); return -1; }
+    }
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    const int flags = g_orig_cofactor | (g_line_mode << 1);
+    if (c->cc_used.empty() || c->cc_flags != flags) {           // first use, or prepare flags changed: empty cache
+        c->cc_map.clear();
+        c->cc_keys.assign(LCB_CT_CACHE, std::string());
+        c->cc_used.assign(LCB_CT_CACHE, 0);
+        c->cc_flags = flags;
+    }
+    u32 *lines = (u32 *)c->cc_lines.get((size_t)LCB_CT_CACHE * 2 * LCB_LINESET_BYTES);
+    uint8_t *ctok = (uint8_t *)c->cc_ok.get(LCB_CT_CACHE);
+    void *keys = c->t_keys.get((n_keys ? n_keys : 1) * LCB_G1A_ST_BYTES);
+    if (!lines || !ctok || !keys) { set_err("device allocation failed"); return -1; }
+    const uint64_t tick = ++c->cc_tick;
+    std::vector<u32> slot_of(n_cts), miss;
+    for (size_t k = 0; k < n_cts; k++) {
+        const u32 v0 = v_off[k], v1 = v_off[k + 1];
+        std::string key((const char *)cts_u + 48 * k, 48);
+        key.append((const char *)cts_w + 96 * k, 96);
+        key.append((const char *)v_data + v0, v1 - v0);
+        auto it = c->cc_map.find(key);
+        if (it != c->cc_map.end()) {
+            slot_of[k] = it->second;
+            c->cc_used[it->second] = tick;
+            continue;
+        }
+        u32 victim = 0;                  // least recently used slot not taken by this batch
+        for (u32 j = 1; j < LCB_CT_CACHE; j++)
+            if (c->cc_used[j] < c->cc_used[victim]) victim = j;
+        if (!c->cc_keys[victim].empty()) c->cc_map.erase(c->cc_keys[victim]);
+        c->cc_keys[victim] = key;
+        c->cc_map.emplace(std::move(key), victim);
+        c->cc_used[victim] = tick;
+        slot_of[k] = victim;
+        miss.push_back((u32)k);
+    }
+    // prepare the misses straight into their slots
+    const uint8_t *dy = up(c->in[0], y_keys, 48 * n_keys, s);
+    if (n_keys) lcbk_g1_decompress(dim3(nblk(n_keys)), s, dy, (u32)n_keys, keys);
+    if (!miss.empty()) {
+        const size_t m = miss.size();
+        std::vector<uint8_t> mu(48 * m), mw(96 * m), mv;
+        std::vector<u32> mvo(1, 0), mslot(m), msets(2 * m);
+        for (size_t j = 0; j < m; j++) {
+            const u32 k = miss[j];
+            memcpy(&mu[48 * j], cts_u + 48 * (size_t)k, 48);
+            memcpy(&mw[96 * j], cts_w + 96 * (size_t)k, 96);
+            mv.insert(mv.end(), v_data + v_off[k], v_data + v_off[k + 1]);
+            mvo.push_back((u32)mv.size());
+            mslot[j] = slot_of[k];
+            msets[2 * j] = 2 * slot_of[k];
+            msets[2 * j + 1] = 2 * slot_of[k] + 1;
+        }
+        if (mv.empty()) mv.push_back(0);
+        const uint8_t *du = up(c->in[1], mu.data(), mu.size(), s);
+        const uint8_t *dw = up(c->in[2], mw.data(), mw.size(), s);
+        const uint8_t *dv = up(c->in[3], mv.data(), mv.size(), s);
+        const uint32_t *dvo = up(c->in[4], mvo.data(), mvo.size(), s);
+        const uint32_t *dsl = up(c->sel[0], mslot.data(), m, s);
+        const uint32_t *dse = up(c->sel[1], msets.data(), 2 * m, s);
+        if (!du || !dw || !dv || !dvo || !dsl || !dse) { set_err("device allocation failed"); return -1; }
+        lcbk_tpke_ct_prepare(dim3(nblk(m)), s, du, dw, dv, dvo, (u32)m, lines, ctok, flags, dsl);
+        lcbk_lineset_fill(dim3(nblk(2 * m)), s, lines, (u32)(2 * m), dse);
+    }
+    std::vector<u32> cslot(n);
+    for (size_t i = 0; i < n; i++) cslot[i] = slot_of[ct_idx[i]];
+    const uint32_t *dct = up(c->in[5], cslot.data(), n, s);
+    const uint32_t *ddec = up(c->in[6], dec_idx, n, s);
+    const uint8_t *dui = up(c->in[7], ui, 48 * n, s);
+    uint8_t *dacc = (uint8_t *)c->out[0].get(n);
+    if (!dy || !dct || !ddec || !dui || !dacc) { set_err("device allocation failed"); return -1; }
+    if (tpke_verify_core(c, lines, ctok, LCB_CT_CACHE, n_keys, dacc, n, dct, ddec, dui, s)) return -1;
+    if (n) hipMemcpyAsync(accept, dacc, n, hipMemcpyDeviceToHost, s);
+    if (!sync_check(c, "tpke verify (cached)")) {
+        c->cc_used.clear();              // slots written by a failed call may be incomplete
+        return -1;
+    }
+    return 0;
 }
 extern "C" int lcb_tpke_verify_shares(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys,
                                       const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
@@ -2047,7 +2150,7 @@ extern "C" void mclBn_pairing(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) {
     hipMemcpyAsync(in, x, 144, hipMemcpyHostToDevice, s);
     if (!hit) hipMemcpyAsync(in + 36, y, 288, hipMemcpyHostToDevice, s);
     lcbk_pairing_prep(s, in, gpts, lines, desc, slot, hit ? 0 : 1);
-    if (!hit) lcbk_lineset_fill(dim3(1), s, lines + (size_t)2 * slot * (LCB_LINESET_BYTES / 4), 2);
+    if (!hit) lcbk_lineset_fill(dim3(1), s, lines + (size_t)2 * slot * (LCB_LINESET_BYTES / 4), 2, nullptr);
     lcbk_coop_tpke_miller(s, lines, desc, gpts, 1, park, fl, fl + 32);
     lcbk_coop_final_exp_check(s, park, 1, nullptr);
     u32 r[144];

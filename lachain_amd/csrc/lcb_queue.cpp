@@ -103,8 +103,10 @@ void run_tpke(lcb_queue *q, std::vector<TpkeItem> &items, size_t batched_min) {
                                             vs.data(), voff.data(), cidx.size(), ct2.data(), dec2.data(), uis2.data());
         for (size_t j = 0; j < ord.size(); j++) acc[ord[j]] = acc2[j];
     } else {
-        rc = lcb_tpke_verify_shares(acc.data(), items.size(), keys.data(), kidx.size(), us.data(), ws.data(), vs.data(),
-                                    voff.data(), cidx.size(), ct.data(), dec.data(), uis.data());
+        // the worker thread's context keeps a ciphertext's prepared line sets across flushes (its N shares arrive over
+        // several of them)
+        rc = lcb_tpke_verify_shares_cached(acc.data(), items.size(), keys.data(), kidx.size(), us.data(), ws.data(),
+                                           vs.data(), voff.data(), cidx.size(), ct.data(), dec.data(), uis.data());
     }
     std::lock_guard<std::mutex> lk(q->mu);
     if (rc) q->last_error = lcb_last_error();

@@ -55,6 +55,8 @@ _SIGS = {
     "lcb_last_error": (ctypes.c_char_p, []),
     "lcb_tpke_verify_shares": (ctypes.c_int, [c_u8p, c_size, c_u8p, c_size, c_u8p, c_u8p, c_u8p, c_u32p, c_size,
                                               c_u32p, c_u32p, c_u8p]),
+    "lcb_tpke_verify_shares_cached": (ctypes.c_int, [c_u8p, c_size, c_u8p, c_size, c_u8p, c_u8p, c_u8p, c_u32p, c_size,
+                                                     c_u32p, c_u32p, c_u8p]),
     "lcb_tpke_verify_shares_dev": (ctypes.c_int, [ctypes.c_void_p, c_size, ctypes.c_void_p, c_size, ctypes.c_void_p,
                                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_size,
                                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
@@ -249,7 +251,7 @@ def _offsets(chunks):
 
 
 # ---------------------------------------------------------------- batch wrappers (bytes in / bytes out)
-def tpke_verify_shares(y_keys, cts, shares, batched=False):
+def tpke_verify_shares(y_keys, cts, shares, batched=False, cached=False):
     """y_keys: list of 48-byte verification keys; cts: list of (U48, V, W96);
     shares: list of (ct_index, decryptor_index, Ui48).  Returns list of bools.  batched=True runs the randomized
     group check (lcb_tpke_verify_shares_batched: same decisions, false accept <= 2^-64 per group)."""
@@ -264,7 +266,8 @@ def tpke_verify_shares(y_keys, cts, shares, batched=False):
     _, pdec = _u32_keep(keep, [s[1] for s in shares])
     _, pui = _bytes_ptr_keep(keep, b"".join(s[2] for s in shares))
     ob, po = _out(n)
-    fn = lib().lcb_tpke_verify_shares_batched if batched else lib().lcb_tpke_verify_shares
+    fn = (lib().lcb_tpke_verify_shares_batched if batched else
+          lib().lcb_tpke_verify_shares_cached if cached else lib().lcb_tpke_verify_shares)
     _check(fn(po, n, py, len(y_keys), pu, pw, pv, pvo, len(cts), pct, pdec, pui), "tpke_verify_shares")
     return [bool(ob[i]) for i in range(n)]
 
