@@ -5,8 +5,8 @@
 //   HoneyBadger.HandleCommonSubset filter                         (HoneyBadger.cs:156-158)
 //   ThresholdSigner.AddShare -> IsShareValid -> ValidateSignature  (src/Lachain.Crypto/ThresholdSignature/ThresholdSigner.cs:62)
 //   threads: AbstractProtocol.cs:46-47
-// A GPU launch per share would be latency-bound, so callers submit single shares and get a ticket; a worker thread
-// flushes the pending shares as ONE batch (lcb_tpke_verify_shares / lcb_ts_verify_shares on its own context) when
+// A GPU launch per share would be latency-bound, so callers submit single shares and get a ticket; a worker thread (two
+// of them, so one flush runs while the next collects) flushes the pending shares as ONE batch (lcb_tpke_verify_shares / lcb_ts_verify_shares on its own context) when
 // max_batch shares are pending or the oldest pending share is max_delay_us old, and lcb_queue_wait(ticket) returns
 // that share's decision.  Ciphertexts, verification keys and messages are de-duplicated per batch, so the batch
 // shares hash-to-G2 and Miller-line precomputation exactly as a caller-built batch would.  Decisions are the
@@ -20,6 +20,7 @@
 #include <condition_variable>
 #include <deque>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -53,14 +54,17 @@ struct lcb_queue {
     bool stop = false, flush_now = false;
     int64_t next_ticket = 1;
     std::unordered_map<int64_t, int8_t> results;     // ticket -> 1 / 0 / -1 (batch failed), until waited for
-    int64_t done_upto = 0;                            // every ticket <= this has its result (batches are FIFO)
+    std::set<int64_t> open;                           // tickets submitted whose result is not yet produced
     uint64_t batches = 0, items = 0, max_seen = 0;
     // randomized batch checks (lcb_queue_set_batched): flushes of at least batched_min shares go through the
     // *_batched entry points, shares ordered by ciphertext / message so each one's shares form a group
     size_t batched_min = 0;
     std::string last_error;
-    std::thread worker;
+    // two workers, each with its own thread context (and prepared-ciphertext cache): a flush does not wait for the
+    // previous one's GPU round trip, so a share's latency is its own batch's, not two
+    std::vector<std::thread> workers;
 };
+#define LCB_QUEUE_WORKERS 2
 
 namespace {
 
@@ -110,7 +114,10 @@ void run_tpke(lcb_queue *q, std::vector<TpkeItem> &items, size_t batched_min) {
     }
     std::lock_guard<std::mutex> lk(q->mu);
     if (rc) q->last_error = lcb_last_error();
-    for (size_t i = 0; i < items.size(); i++) q->results[items[i].ticket] = rc ? -1 : (int8_t)(acc[i] != 0);
+    for (size_t i = 0; i < items.size(); i++) {
+        q->results[items[i].ticket] = rc ? -1 : (int8_t)(acc[i] != 0);
+        q->open.erase(items[i].ticket);
+    }
 }
 
 void run_ts(lcb_queue *q, std::vector<TsItem> &items, size_t batched_min) {
@@ -153,7 +160,10 @@ void run_ts(lcb_queue *q, std::vector<TsItem> &items, size_t batched_min) {
     }
     std::lock_guard<std::mutex> lk(q->mu);
     if (rc) q->last_error = lcb_last_error();
-    for (size_t i = 0; i < items.size(); i++) q->results[items[i].ticket] = rc ? -1 : (int8_t)(acc[i] != 0);
+    for (size_t i = 0; i < items.size(); i++) {
+        q->results[items[i].ticket] = rc ? -1 : (int8_t)(acc[i] != 0);
+        q->open.erase(items[i].ticket);
+    }
 }
 
 void worker_loop(lcb_queue *q) {
@@ -180,13 +190,9 @@ void worker_loop(lcb_queue *q) {
         q->items += pending;
         if (pending > q->max_seen) q->max_seen = pending;
         lk.unlock();
-        int64_t top = 0;
-        for (auto &x : t) top = x.ticket > top ? x.ticket : top;
-        for (auto &x : s) top = x.ticket > top ? x.ticket : top;
         if (!t.empty()) run_tpke(q, t, batched_min);
         if (!s.empty()) run_ts(q, s, batched_min);
         lk.lock();
-        q->done_upto = top > q->done_upto ? top : q->done_upto;
         q->cv_done.notify_all();
     }
 }
@@ -205,7 +211,7 @@ extern "C" lcb_queue *lcb_queue_create(size_t max_batch, uint32_t max_delay_us) 
     lcb_queue *q = new lcb_queue;
     q->max_batch = max_batch ? max_batch : 1;
     q->max_delay = std::chrono::microseconds(max_delay_us);
-    q->worker = std::thread(worker_loop, q);
+    for (int k = 0; k < LCB_QUEUE_WORKERS; k++) q->workers.emplace_back(worker_loop, q);
     return q;
 }
 extern "C" void lcb_queue_destroy(lcb_queue *q) {
@@ -215,7 +221,7 @@ extern "C" void lcb_queue_destroy(lcb_queue *q) {
         q->stop = true;
     }
     q->cv_work.notify_all();
-    q->worker.join();
+    for (auto &w : q->workers) w.join();
     q->cv_done.notify_all();
     delete q;
 }
@@ -232,6 +238,7 @@ extern "C" int64_t lcb_queue_tpke_verify(lcb_queue *q, const uint8_t y48[48], co
     std::unique_lock<std::mutex> lk(q->mu);
     if (q->stop) return -1;
     it.ticket = q->next_ticket++;
+    q->open.insert(it.ticket);
     q->tpke.push_back(std::move(it));
     return enqueue_common(q, lk);
 }
@@ -245,6 +252,7 @@ extern "C" int64_t lcb_queue_ts_verify(lcb_queue *q, const uint8_t pk48[48], con
     std::unique_lock<std::mutex> lk(q->mu);
     if (q->stop) return -1;
     it.ticket = q->next_ticket++;
+    q->open.insert(it.ticket);
     q->ts.push_back(std::move(it));
     return enqueue_common(q, lk);
 }
@@ -268,7 +276,7 @@ extern "C" int lcb_queue_wait(lcb_queue *q, int64_t ticket) {
             q->results.erase(it);
             return r;
         }
-        if (ticket <= q->done_upto) return -1;   // already waited for
+        if (!q->open.count(ticket)) return -1;   // already waited for
         q->cv_done.wait(lk);
     }
 }
