@@ -25,7 +25,7 @@
 
 #define CP_L 9                 // lanes per pairing check
 #define CP_G 7                 // checks per wave (lanes 0..62; lane 63 is a dummy group of its own)
-#define CP_AREAS 8
+#define CP_AREAS 7             // one LDS area per live group (the dummy lane 63 reads area 0 and never writes)
 #define CP_BLOCK 64            // one wave per workgroup (__syncthreads is the wave's LDS ordering point)
 // Fp2 slots of a group's LDS area (96 B each)
 #define S_F 0                  // 6: the published accumulator
@@ -33,9 +33,9 @@
 #define S_P 7                  // 18: products
 #define S_XP 25                // 18: xi * products
 #define S_AUX 43               // 9: pre-sums / recombination outputs
-#define S_JUNK 52              // sink for lanes with nothing to publish
+#define S_JUNK (-1)            // "nothing to publish": the store is skipped (exec-masked)
 #define S_LE (S_P + 14)        // 4 evaluated line coefficients (Miller loop only; overlays P[14..17])
-#define CP_NS 53               // 8 areas x 53 x 96 B = 40,704 B per wave: four waves per CU
+#define CP_NS 52               // 7 areas x 52 x 96 B = 34,944 B per wave: four waves per CU
 #define CP_LDS_QUADS (CP_AREAS * CP_NS * 6)
 
 typedef unsigned long long u64c;
@@ -59,11 +59,12 @@ DI Cp cp_init(uint4 *lds) {
     const int l = threadIdx.x & 63;
     c.g = l / CP_L;
     c.j = l - CP_L * c.g;
-    c.s = lds + c.g * (CP_NS * 6);
+    c.s = lds + (c.g < CP_G ? c.g : 0) * (CP_NS * 6);
     return c;
 }
 DI void cp_sync() { __syncthreads(); }
 DI void cp_put(const Cp &c, int slot, const fp2 &x) {
+    if (slot < 0 || c.g >= CP_G) return;
     uint4 *p = c.s + slot * 6;
     const u32 *w = (const u32 *)&x;
 #pragma unroll
