@@ -364,13 +364,16 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_gr
                                                     const u32 *dec_idx, const uint8_t *ui, const u32 *rU,
                                                     const u32 *rY, u32 n, g1a_st *gpts, uint8_t *accept,
                                                     uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval) {
-    u32 g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= n_groups) return;
+    // two lanes per group: side 0 sums the U records (and handles singles / invalid ciphertexts), side 1 the Y records
+    u32 t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 2 * n_groups) return;
+    const u32 g = t >> 1, side = t & 1;
     uint4 dsc = desc[g];
     g1a_st o;
     g1_inf_st(o);
-    gexact[g] = 0;
     if (dsc.w == 1) {                    // exact single of share dsc.x of ciphertext dsc.z
+        if (side) return;
+        gexact[g] = 0;
         g1a U, Y;
         U.inf = Y.inf = true;
         u32 d = dec_idx[dsc.x];
@@ -391,39 +394,28 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_gr
     }
     const bool cok = ct_ok[dsc.z];
     if (!cok || !ct_g2[dsc.z]) {
+        gpts[2 * (size_t)g + side] = o;
+        if (side) return;
+        gexact[g] = cok ? 1 : 0;
         if (!cok)
             for (u32 j = 0; j < dsc.y; j++) accept[dsc.x + j] = 0;
-        else
-            gexact[g] = 1;
-        gpts[2 * (size_t)g] = o;
-        gpts[2 * (size_t)g + 1] = o;
         return;
     }
-    g1 su, sy, t, wu, wy, cu, cy;
+    if (!side) gexact[g] = 0;
+    const u32 *rec = side ? rY : rU;
+    g1 su, tp, wu;
     jac_set_inf(su);
-    jac_set_inf(sy);
     jac_set_inf(wu);
-    jac_set_inf(wy);
-    for (u32 j = dsc.y; j-- > 0;) {      // last to first: su = suffix sums, wu = sum of the suffix sums
-        if (!key_suspect(susp, dec_idx[dsc.x + j], n_keys)) {
-            g1_load_soa(t, rU, n, dsc.x + j);
-            grp_add(su, su, t);
-            g1_load_soa(t, rY, n, dsc.x + j);
-            grp_add(sy, sy, t);
+    for (u32 j = dsc.y; j-- > 0;) {      // last to first: su = suffix sums, wu = sum of the suffix sums (TS-style
+        if (!key_suspect(susp, dec_idx[dsc.x + j], n_keys)) {      // weighted sum, only when wsum is given)
+            g1_load_soa(tp, rec, n, dsc.x + j);
+            grp_add(su, su, tp);
         }
-        if (first) {
-            grp_add(wu, wu, su);
-            grp_add(wy, wy, sy);
-        }
+        if (first && wsum) grp_add(wu, wu, su);
     }
-    if (first) {
-        g1_store_soa(wsum, 2 * (size_t)n_groups, 2 * (size_t)g, wu);
-        g1_store_soa(wsum, 2 * (size_t)n_groups, 2 * (size_t)g + 1, wy);
-    }
-    g1_to_st(o, su, false);
-    gpts[2 * (size_t)g] = o;
-    g1_to_st(o, sy, true);
-    gpts[2 * (size_t)g + 1] = o;
+    if (first && wsum) g1_store_soa(wsum, 2 * (size_t)n_groups, 2 * (size_t)g + side, wu);
+    g1_to_st(o, su, side != 0);
+    gpts[2 * (size_t)g + side] = o;
 }
 
 // the weighted sums of the level-1 groups listed in sdesc (.w = level-1 group index) as affine records
@@ -440,6 +432,37 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum(const uint4 *sdesc, u32 n_
     g1_load_soa(p, wsum, 2 * (size_t)n_l1, 2 * (size_t)l + 1);
     g1_to_st(o, p, true);
     gpts[2 * (size_t)g + 1] = o;
+}
+
+// Level 2 of TPKE (two-error location, see k_tpke_rlc_search2): the weighted sums of the failed level-1 groups listed
+// in sdesc, formed from the shares' randomised records: two lanes per group (U side, Y side), last share to first,
+// s = suffix sum, w = sum of the s (weights c_j = j + 1), v = sum of the w (weights t_j = c_j (c_j + 1) / 2).  Shares of
+// suspect keys keep their positions and add nothing.  gpts[2g + side] = w, gpts[2 (ns + g) + side] = v (Y side
+// negated), so checks g and ns + g give gamma_c = prod g_i^(c_i s_i) and gamma_t = prod g_i^(t_i s_i).
+extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum2(const uint4 *sdesc, u32 ns, const u32 *rU, const u32 *rY, u32 n,
+                                                      const u32 *dec_idx, u32 n_keys, const u32 *susp, g1a_st *gpts) {
+    u32 t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 2 * ns) return;
+    const u32 g = t >> 1, side = t & 1;
+    const uint4 d = sdesc[g];
+    const u32 *rec = side ? rY : rU;
+    g1 sa, wa, va, p;
+    jac_set_inf(sa);
+    jac_set_inf(wa);
+    jac_set_inf(va);
+    for (u32 j = d.y; j-- > 0;) {
+        if (!key_suspect(susp, dec_idx[d.x + j], n_keys)) {
+            g1_load_soa(p, rec, n, d.x + j);
+            grp_add(sa, sa, p);
+        }
+        grp_add(wa, wa, sa);
+        grp_add(va, va, wa);
+    }
+    g1a_st o;
+    g1_to_st(o, wa, side != 0);
+    gpts[2 * (size_t)g + side] = o;
+    g1_to_st(o, va, side != 0);
+    gpts[2 * ((size_t)ns + g) + side] = o;
 }
 
 // W of every ciphertext in G2 (Scott's psi test, curve.hpp g2_in_subgroup); H = hash-to-G2 output is in G2 by
@@ -716,6 +739,114 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_search(const uint4 *search, u32 o, u
     emit_singles(d, 0, accept, key_idx, n_keys, susp, next, next_count);
 }
 
+// the final-exponentiation outputs of checks [o, o + m) (park stride m) -> rows o.. of dst (576 B each)
+extern "C" __global__ void LCB_BOUNDS k_rlc_park_copy(const u32 *park, u32 o, u32 m, u32 *dst) {
+    u32 gl = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gl >= m) return;
+    fp12 f;
+    fp12_load_soa(f, park, m, gl);
+    const u32 *w = (const u32 *)&f;
+    uint4 *d = (uint4 *)(dst + (size_t)(o + gl) * 144);
+#pragma unroll
+    for (int q = 0; q < 36; q++) d[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+DI void fp12_load_row(fp12 &f, const u32 *row) {
+    u32 *w = (u32 *)&f;
+    const uint4 *src = (const uint4 *)row;
+#pragma unroll
+    for (int q = 0; q < 36; q++) {
+        uint4 v = src[q];
+        w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+}
+DI bool fp12_words_eq(const fp12 &a, const fp12 &b) {
+    const u32 *x = (const u32 *)&a, *y = (const u32 *)&b;
+    u32 d = 0;
+#pragma unroll
+    for (int q = 0; q < 144; q++) d |= x[q] ^ y[q];
+    return d == 0;
+}
+// r = a^e for a in the cyclotomic subgroup (GT), 1 <= e < 2^8
+DN void gt_pow_small(fp12 &r, const fp12 &a, u32 e) {
+    fp12 t = a;
+    int top = 7;
+    while (top > 0 && !((e >> top) & 1)) top--;
+    for (int b = top - 1; b >= 0; b--) {
+        fp12_cyc_sqr_n(t, t);
+        if ((e >> b) & 1) fp12_mul_n(t, t, a);
+    }
+    r = t;
+}
+DI u32 half_ballot(bool p) {
+    const unsigned long long m = __ballot(p);
+    return (u32)(m >> (32 * ((threadIdx.x >> 5) & 1)));
+}
+// Level 2 of TPKE: locate up to TWO bad shares per failed group.  With e_i = s_i log g_i (nonzero exactly for the bad
+// shares) the three group values are gamma_0 (level 1) ~ sum e_i, gamma_c ~ sum e_i c_i and gamma_t ~ sum e_i t_i, so
+// gamma_2 = gamma_t^2 / gamma_c ~ sum e_i c_i^2 (c^2 = 2t - c).
+//   one error at j:      gamma_c = gamma_0^(c_j)  (k_tpke_rlc_search2a: one lane per group, c = 1..len as k_rlc_search);
+//   two errors at j, k:  for lane j of the group's half-wave (k_tpke_rlc_search2b, only the groups 2a left open),
+//                        D_j = gamma_c / gamma_0^(c_j) ~ e_k (c_k - c_j) and E_j = gamma_2 / gamma_c^(c_j) ~
+//                        e_k c_k (c_k - c_j), so E_j = D_j^(c_k): exactly two lanes whose searches name each other
+//                        reject both shares.
+// Any other outcome (three or more bad shares) sends the group's shares to single checks.  A false location needs a
+// relation among the e_i, whose factors s_i are secret: probability <= len^2 2^-64 per group.
+extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_search2a(const uint4 *search, u32 ns, const u32 *gamma0,
+                                                         const u32 *gamma12, uint8_t *accept, u32 *open,
+                                                         u32 *open_count) {
+    u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= ns) return;
+    const uint4 d = search[g];
+    fp12 gm, gc, acc;
+    fp12_load_row(gm, gamma0 + (size_t)g * 144);
+    fp12_load_row(gc, gamma12 + (size_t)g * 144);
+    acc = gm;
+    u32 found = 0;
+    for (u32 c = 1; c <= d.y; c++) {
+        if (fp12_words_eq(acc, gc)) { found = c; break; }
+        if (c < d.y) fp12_mul_n(acc, acc, gm);
+    }
+    if (found) accept[d.x + found - 1] = 0;
+    else open[atomicAdd(open_count, 1u)] = g;
+}
+extern "C" __global__ void __launch_bounds__(64) k_tpke_rlc_search2b(const uint4 *search, u32 ns, const u32 *gamma0,
+                                                                    const u32 *gamma12, const u32 *open,
+                                                                    const u32 *open_count, uint8_t *accept, uint4 *next,
+                                                                    u32 *next_count, const u32 *key_idx, u32 n_keys,
+                                                                    const u32 *susp) {
+    const u32 j = threadIdx.x & 31, k = blockIdx.x * 2 + (threadIdx.x >> 5);
+    if (blockIdx.x * 2 >= *open_count) return;          // (uniform per block)
+    const bool live = k < *open_count;
+    const u32 g = live ? open[k] : 0;
+    const uint4 d = live ? search[g] : make_uint4(0, 0, 0, 0);
+    const bool cand = live && j < d.y && accept[d.x + j] && !key_suspect(susp, key_idx[d.x + j], n_keys);
+    const u32 cj = j + 1;
+    fp12 a, b, D, E;
+    fp12_load_row(a, gamma0 + (size_t)g * 144);
+    gt_pow_small(b, a, cj);
+    fp12_conj(b, b);
+    fp12_load_row(a, gamma12 + (size_t)g * 144);           // gamma_c
+    fp12_mul_n(D, a, b);                                   // D_j = gamma_c / gamma_0^(c_j)
+    gt_pow_small(b, a, cj + 1);                            // gamma_c^(c_j + 1)
+    fp12_conj(b, b);
+    fp12_load_row(a, gamma12 + ((size_t)ns + g) * 144);    // gamma_t
+    fp12_cyc_sqr_n(a, a);
+    fp12_mul_n(E, a, b);                                   // E_j = gamma_t^2 / gamma_c^(c_j + 1) = gamma_2 / gamma_c^(c_j)
+    u32 found = 0;
+    a = D;
+    for (u32 c = 1; cand && c <= d.y; c++) {
+        if (c != cj && fp12_words_eq(a, E)) { found = c; break; }
+        if (c < d.y) fp12_mul_n(a, a, D);
+    }
+    const u32 m2 = half_ballot(found != 0);
+    const u32 m3 = half_ballot(found != 0 && !((m2 >> (found - 1)) & 1u));
+    if (__popc(m2) == 2 && !m3) {
+        if (found) accept[d.x + j] = 0;
+    } else if (live && j == 0) {
+        emit_singles(d, 0, accept, key_idx, n_keys, susp, next, next_count);
+    }
+}
+
 // ---------------------------------------------------------------- census (suspect keys) and the level-1 split
 // exact singles of shares [0, m): desc = {i, 1, group index (ciphertext / message), 1}; an out-of-range index rejects
 extern "C" __global__ void LCB_BOUNDS k_rlc_census_desc(const u32 *grp_idx, const u32 *key_idx, u32 m, u32 n_grp,
@@ -857,6 +988,24 @@ extern "C" void lcbk_rlc_search(dim3 grid, hipStream_t s, const void *search, u3
                                 u32 n_keys, const u32 *susp) {
     LCB_LAUNCH(k_rlc_search, (const uint4 *)search, o, m, gamma, park, accept, (uint4 *)next, next_count, key_idx,
                n_keys, susp);
+}
+extern "C" void lcbk_tpke_rlc_wsum2(hipStream_t s, const void *sdesc, u32 ns, const u32 *rU, const u32 *rY, u32 n,
+                                    const u32 *dec_idx, u32 n_keys, const u32 *susp, void *gpts) {
+    dim3 grid((2 * ns + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_tpke_rlc_wsum2, (const uint4 *)sdesc, ns, rU, rY, n, dec_idx, n_keys, susp, (g1a_st *)gpts);
+}
+extern "C" void lcbk_rlc_park_copy(hipStream_t s, const u32 *park, u32 o, u32 m, u32 *dst) {
+    dim3 grid((m + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_rlc_park_copy, park, o, m, dst);
+}
+extern "C" void lcbk_tpke_rlc_search2(hipStream_t s, const void *search, u32 ns, const u32 *gamma0, const u32 *gamma12,
+                                      uint8_t *accept, void *next, u32 *next_count, const u32 *key_idx, u32 n_keys,
+                                      const u32 *susp, u32 *open, u32 *open_count) {
+    (void)hipMemsetAsync(open_count, 0, 4, s);
+    dim3 grid((ns + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_tpke_rlc_search2a, (const uint4 *)search, ns, gamma0, gamma12, accept, open, open_count);
+    hipLaunchKernelGGL(k_tpke_rlc_search2b, dim3((ns + 1) / 2), dim3(64), 0, s, (const uint4 *)search, ns, gamma0,
+                       gamma12, open, open_count, accept, (uint4 *)next, next_count, key_idx, n_keys, susp);
 }
 extern "C" void lcbk_rlc_census_desc(hipStream_t s, const u32 *grp_idx, const u32 *key_idx, u32 m, u32 n_grp,
                                      u32 n_keys, void *desc, uint8_t *accept) {

@@ -793,12 +793,13 @@ void rlc_sum_enqueue(const RlcKindInfo &K, RlcWs &w, const uint8_t *desc, u32 gr
         lcbk_ts_rlc_sum(dim3(nblk(groups)), s, desc, groups, first, K.okv, K.keys, (u32)K.n_keys, io.d_key, io.d_pts,
                         w.rA, w.rB, (u32)n, gpts, d_accept, gex, wsum, susp, cval);
     else
-        lcbk_tpke_rlc_sum(dim3(nblk(groups)), s, desc, groups, first, K.okv, K.ctg2, K.keys, (u32)K.n_keys, io.d_key,
+        lcbk_tpke_rlc_sum(dim3(nblk(2 * (size_t)groups)), s, desc, groups, first, K.okv, K.ctg2, K.keys, (u32)K.n_keys, io.d_key,
                           io.d_pts, w.rA, w.rB, (u32)n, gpts, d_accept, gex, wsum, susp, cval);
 }
 // Miller + final exponentiation (+ resolve / search) over the groups of desc in chunks; gpts holds the points
+enum RlcStage { RLC_RESOLVE = 0, RLC_SEARCH = 1, RLC_COPY = 2 };   // after a chunk's checks: resolve / search / copy out
 void rlc_checks(lcb_ctx *c, const RlcKindInfo &K, RlcWs &w, const uint8_t *desc, u32 count, void *gpts, uint8_t *gacc,
-                u32 *f, bool search_stage, bool first, uint8_t *gex, uint4 *sdesc, u32 *gamma, uint8_t *d_accept,
+                u32 *f, RlcStage stage, bool first, uint8_t *gex, uint4 *sdesc, u32 *gamma, uint8_t *d_accept,
                 RlcIo io, hipStream_t s) {
     hipEvent_t *ev = c->rlc_lev_ev;
     float t;
@@ -820,7 +821,9 @@ void rlc_checks(lcb_ctx *c, const RlcKindInfo &K, RlcWs &w, const uint8_t *desc,
         if (coop) lcbk_coop_final_exp_check(s, f, (u32)m, gacc + o);
         else lcbk_final_exp_check(dim3(nblk(m)), s, f, (u32)m, gacc + o);
         hipEventRecord(ev[3], s);
-        if (search_stage)
+        if (stage == RLC_COPY)
+            lcbk_rlc_park_copy(s, f, (u32)o, (u32)m, gamma);
+        else if (stage == RLC_SEARCH)
             lcbk_rlc_search(dim3(nblk(m)), s, sdesc, (u32)o, (u32)m, gamma, f, d_accept, w.dB, w.cnt + 1, io.d_key,
                             (u32)K.n_keys, w.susp);
         else
@@ -848,7 +851,7 @@ int rlc_census(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, RlcIo io, 
     RlcWs cw = w;
     cw.susp = nullptr;                  // the census singles are exact checks whatever the bitmap says
     rlc_sum_enqueue(K, cw, w.dB, m, false, d_accept, m, io, gpts, gex, nullptr, cval, s);
-    rlc_checks(c, K, cw, w.dB, m, gpts, gacc, f, false, false, gex, nullptr, nullptr, d_accept, io, s);
+    rlc_checks(c, K, cw, w.dB, m, gpts, gacc, f, RLC_RESOLVE, false, gex, nullptr, nullptr, d_accept, io, s);
     lcbk_rlc_census_stats(s, io.d_key, m, (u32)K.n_keys, cval, d_accept, w.susp, w.cnt + 3);
     return launched("batched verify census launch") ? 0 : -1;
 }
@@ -886,11 +889,11 @@ int rlc_levels(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, size_t n, 
         uint4 *sdesc = nullptr;
         u32 *gamma = nullptr, *wsum = nullptr;
         if (first) {
-            sdesc = (uint4 *)c->rlc[9].get((size_t)groups * 16);
+            sdesc = (uint4 *)c->rlc[9].get((size_t)groups * 16 * (K.ts ? 1 : 2));
             gamma = (u32 *)c->rlc[10].get((size_t)groups * 576);
-            wsum = (u32 *)c->rlc[11].get((size_t)groups * K.wrec);
+            if (K.ts) wsum = (u32 *)c->rlc[11].get((size_t)groups * K.wrec);   // (TPKE: formed at level 2)
         }
-        if (!gpts || !gacc || !gex || !f || (first && (!sdesc || !gamma || !wsum))) {
+        if (!gpts || !gacc || !gex || !f || (first && (!sdesc || !gamma || (K.ts && !wsum)))) {
             set_err("device allocation failed");
             return -1;
         }
@@ -900,10 +903,34 @@ int rlc_levels(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, size_t n, 
         hipEventRecord(ev[1], s);
         if (hipEventSynchronize(ev[1]) == hipSuccess && hipEventElapsedTime(&t, ev[0], ev[1]) == hipSuccess)
             c->rlc_ms[0] += t;
-        rlc_checks(c, K, w, w.dA, groups, gpts, gacc, f, false, first, gex, sdesc, gamma, d_accept, io, s);
+        rlc_checks(c, K, w, w.dA, groups, gpts, gacc, f, RLC_RESOLVE, first, gex, sdesc, gamma, d_accept, io, s);
         if (!launched("batched verify launch")) return -1;
         if (!read_counts(cnt, w.cnt, 3, s)) return -1;
-        if (first && cnt[2]) {           // level 2: weighted re-check of the failed groups, then the search
+        if (first && cnt[2] && !K.ts) {  // TPKE level 2: two weighted re-checks per failed group, two-error location
+            const u32 ns = cnt[2];
+            if (lev + 1 < 8) c->rlc_levels[lev + 1] = 2 * ns;
+            c->rlc_nlev = ++lev + 1;
+            const size_t nc = 2 * (size_t)ns, nf2 = nc < LCB_VERIFY_CHUNK ? nc : LCB_VERIFY_CHUNK;
+            hipMemcpyAsync(sdesc + ns, sdesc, (size_t)ns * 16, hipMemcpyDeviceToDevice, s);
+            void *gp2 = c->rlc[5].get(nc * K.rec);
+            uint8_t *gacc2 = (uint8_t *)c->rlc[6].get(nc);
+            u32 *g12 = (u32 *)c->rlc[16].get(nc * 576);
+            u32 *f2 = (u32 *)c->t_f.get(nf2 * 576 * (size_t)lcbk_fe_slots());
+            if (!gp2 || !gacc2 || !g12 || !f2) { set_err("device allocation failed"); return -1; }
+            hipEventRecord(ev[0], s);
+            lcbk_tpke_rlc_wsum2(s, sdesc, ns, w.rA, w.rB, (u32)n, io.d_key, (u32)K.n_keys, w.susp, gp2);
+            hipEventRecord(ev[1], s);
+            if (hipEventSynchronize(ev[1]) == hipSuccess && hipEventElapsedTime(&t, ev[0], ev[1]) == hipSuccess)
+                c->rlc_ms[0] += t;
+            rlc_checks(c, K, w, (const uint8_t *)sdesc, (u32)nc, gp2, gacc2, f2, RLC_COPY, false, nullptr, sdesc, g12,
+                       d_accept, io, s);
+            u32 *open = (u32 *)c->rlc[17].get((size_t)ns * 4 + 16);    // unresolved groups + their count
+            if (!open) { set_err("device allocation failed"); return -1; }
+            lcbk_tpke_rlc_search2(s, sdesc, ns, gamma, g12, d_accept, w.dB, w.cnt + 1, io.d_key, (u32)K.n_keys, w.susp,
+                                  open + 4, open);
+            if (!launched("batched verify launch")) return -1;
+            if (!read_counts(cnt + 1, w.cnt + 1, 1, s)) return -1;
+        } else if (first && cnt[2]) {    // level 2: weighted re-check of the failed groups, then the search
             const u32 ns = cnt[2];
             if (lev + 1 < 8) c->rlc_levels[lev + 1] = ns;
             c->rlc_nlev = ++lev + 1;
@@ -914,8 +941,8 @@ int rlc_levels(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, size_t n, 
             hipEventRecord(ev[1], s);
             if (hipEventSynchronize(ev[1]) == hipSuccess && hipEventElapsedTime(&t, ev[0], ev[1]) == hipSuccess)
                 c->rlc_ms[0] += t;
-            rlc_checks(c, K, w, (const uint8_t *)sdesc, ns, gp2, gacc, f, true, false, nullptr, sdesc, gamma, d_accept,
-                       io, s);
+            rlc_checks(c, K, w, (const uint8_t *)sdesc, ns, gp2, gacc, f, RLC_SEARCH, false, nullptr, sdesc, gamma,
+                       d_accept, io, s);
             if (!launched("batched verify launch")) return -1;
             if (!read_counts(cnt + 1, w.cnt + 1, 1, s)) return -1;
         }

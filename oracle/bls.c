@@ -2088,25 +2088,68 @@ static int rlc_search(const fp12 *gm, const fp12 *gp, size_t len) {
     }
     return 0;
 }
-/* the GPU's level structure on one group (k_batch.hip): the group check; if it fails, the weighted re-check with
-   weights j+1 and the search; if that names no share, single checks of every share */
+/* a^e for a small exponent e >= 1 */
+static void fp12_pow_small(fp12 *r, const fp12 *a, unsigned e) {
+    fp12 t = *a;
+    int top = 31;
+    while (top > 0 && !((e >> top) & 1)) top--;
+    for (int b = top - 1; b >= 0; b--) {
+        fp12_sqr(&t, &t);
+        if ((e >> b) & 1) fp12_mul(&t, &t, a);
+    }
+    *r = t;
+}
+/* Level 2, two-error location (k_tpke_rlc_search2b): with gamma_0 = gm, gamma_c = gp (weights c_j = j + 1) and
+   gamma_t = gt (weights t_j = c_j (c_j + 1) / 2), D_j = gamma_c / gamma_0^(c_j) and E_j = gamma_t^2 / gamma_c^(c_j + 1);
+   E_j = D_j^(c_k) (c_k != c_j) names the partner k of bad share j.  Returns 1 and the two shares when exactly two
+   shares name each other. */
+static int rlc_search2(const fp12 *gm, const fp12 *gp, const fp12 *gt, size_t len, size_t *j0, size_t *j1) {
+    unsigned found[32] = {0};
+    fp12 t2;
+    fp12_sqr(&t2, gt);
+    size_t nf = 0;
+    for (size_t j = 0; j < len && j < 32; j++) {
+        fp12 b, D, E, acc;
+        fp12_pow_small(&b, gm, (unsigned)j + 1);
+        fp12_conj(&b, &b);
+        fp12_mul(&D, gp, &b);
+        fp12_pow_small(&b, gp, (unsigned)j + 2);
+        fp12_conj(&b, &b);
+        fp12_mul(&E, &t2, &b);
+        acc = D;
+        for (size_t c = 1; c <= len; c++) {
+            if (c != j + 1 && fp12_eq(&acc, &E)) { found[j] = (unsigned)c; break; }
+            fp12_mul(&acc, &acc, &D);
+        }
+        if (found[j]) { if (nf == 0) *j0 = j; else *j1 = j; nf++; }
+    }
+    return nf == 2 && found[*j0] == *j1 + 1 && found[*j1] == *j0 + 1;
+}
+/* the GPU's level structure on one group (k_batch.hip): the group check; if it fails, the weighted re-checks with
+   weights c_j = j+1 and t_j = c_j (c_j + 1) / 2, the one-error search, then the two-error location; if that names no
+   pair, single checks of every share */
 static void rlc_check_group(uint8_t *accept, const g1 *sU, const g1 *sY, size_t st, size_t len, const oline *LH,
                             const oline *LW) {
-    g1 a, b, wa, wb;
-    g1_set_inf(&a); g1_set_inf(&b); g1_set_inf(&wa); g1_set_inf(&wb);
-    for (size_t j = st + len; j-- > st;) {       /* suffix sums: wa = sum (j - st + 1) sU_j */
+    g1 a, b, wa, wb, va, vb;
+    g1_set_inf(&a); g1_set_inf(&b); g1_set_inf(&wa); g1_set_inf(&wb); g1_set_inf(&va); g1_set_inf(&vb);
+    for (size_t j = st + len; j-- > st;) {       /* suffix sums: wa = sum c_j sU_j, va = sum t_j sU_j */
         g1_add(&a, &a, &sU[j]);
         g1_add(&b, &b, &sY[j]);
         g1_add(&wa, &wa, &a);
         g1_add(&wb, &wb, &b);
+        g1_add(&va, &va, &wa);
+        g1_add(&vb, &vb, &wb);
     }
-    fp12 gm, gp;
+    fp12 gm, gp, gt;
     pair_product_gt(&gm, LH, &a, LW, &b);
     if (fp12_eq(&gm, &FP12_ONE)) return;                 /* every (valid) share of the group accepted */
     if (len == 1) { accept[st] = 0; return; }
     pair_product_gt(&gp, LH, &wa, LW, &wb);
+    pair_product_gt(&gt, LH, &va, LW, &vb);
     int c = rlc_search(&gm, &gp, len);
     if (c) { accept[st + c - 1] = 0; return; }
+    size_t j0 = 0, j1 = 0;
+    if (rlc_search2(&gm, &gp, &gt, len, &j0, &j1)) { accept[st + j0] = 0; accept[st + j1] = 0; return; }
     for (size_t j = st; j < st + len; j++)
         if (!check_pair_product(LH, &sU[j], LW, &sY[j])) accept[j] = 0;
 }
@@ -2367,5 +2410,104 @@ int orc_count_units(uint64_t out[10]) {
     orc_count_reset(); g2_mul_fr(&d2, &Q2, &s); out[8] = orc_count_get();
     fp2 ax, ay; orc_count_reset(); g2_to_affine(&ax, &ay, &d2); out[9] = orc_count_get();
     g_counting = 0;
+    return 0;
+}
+
+/* ================================================================== CPU Pippenger MSM (bench CPU leg)
+   The bucket method the GPU runs (k_msm.hip), on the host cores: signed c-bit digits of the 255-bit scalars, per
+   (window, slice of the points) task 2^(c-1) Jacobian buckets filled with mixed additions, a running-sum bucket
+   reduction per task, the task sums added per window and the windows combined by Horner (c doublings each).  The
+   points are decompressed beforehand (orc_g1_affine_batch; the GPU's points are resident affine records too), so the
+   timed part is the same algorithm as the GPU's plain form.  Result equals orc_g1_msm (tests/test_oracle.py). */
+typedef struct { fp x, y; } g1aff_o;
+int orc_g1_affine_batch(uint8_t *aff, const uint8_t *pts, size_t n, int nthreads) {
+    orc_init();
+    if (nthreads < 1) nthreads = 1;
+    g1aff_o *a = (g1aff_o *)aff;
+    int bad = 0;
+#pragma omp parallel for num_threads(nthreads) schedule(static) reduction(| : bad)
+    for (size_t i = 0; i < n; i++) {
+        g1 p;
+        if (!g1_load(&p, pts + 48 * i)) { bad = 1; continue; }
+        if (g1_is_inf(&p)) { memset(&a[i], 0, sizeof a[i]); continue; }   /* (0, 0) is not on the curve: infinity */
+        g1_to_affine(&a[i].x, &a[i].y, &p);
+    }
+    return bad ? -1 : 0;
+}
+size_t orc_g1_affine_bytes(void) { return sizeof(g1aff_o); }
+static int aff_is_inf(const g1aff_o *p) { return fp_is_zero(&p->x) && fp_is_zero(&p->y); }
+int orc_g1_msm_pippenger(uint8_t out[48], const uint8_t *aff, const uint8_t *scalars, size_t n, int c, int nthreads) {
+    orc_init();
+    if (nthreads < 1) nthreads = 1;
+    if (c < 2 || c > 20) return -1;
+    const g1aff_o *a = (const g1aff_o *)aff;
+    const int nwin = (256 + c - 1) / c + 1;                 /* one more window for the last signed carry */
+    const size_t nb = (size_t)1 << (c - 1);
+    /* signed digits, window-major: d[w * n + i] in [-2^(c-1), 2^(c-1)] */
+    int32_t *dg = malloc(sizeof(int32_t) * (size_t)nwin * (n ? n : 1));
+    if (!dg) return -1;
+    int bad = 0;
+#pragma omp parallel for num_threads(nthreads) schedule(static) reduction(| : bad)
+    for (size_t i = 0; i < n; i++) {
+        u64 s[4];
+        memcpy(s, scalars + 32 * i, 32);
+        if (bn_cmp(s, R_, NR) >= 0) { bad = 1; continue; }
+        int carry = 0;
+        for (int w = 0; w < nwin; w++) {
+            int v = carry;
+            for (int k = 0; k < c; k++) {
+                int bit = w * c + k;
+                if (bit < 256) v += (int)((s[bit >> 6] >> (bit & 63)) & 1) << k;
+            }
+            carry = v > (1 << (c - 1));
+            if (carry) v -= 1 << c;
+            dg[(size_t)w * n + i] = v;
+        }
+    }
+    if (bad) { free(dg); return -1; }
+    int splits = (2 * nthreads + nwin - 1) / nwin;
+    if ((size_t)splits > n / 1024 + 1) splits = (int)(n / 1024 + 1);
+    const int ntask = nwin * splits;
+    g1 *tsum = malloc(sizeof(g1) * ntask);
+    if (!tsum) { free(dg); return -1; }
+#pragma omp parallel num_threads(nthreads)
+    {
+        g1 *bk = malloc(sizeof(g1) * nb);
+#pragma omp for schedule(dynamic, 1)
+        for (int t = 0; t < ntask; t++) {
+            const int w = t / splits, sp = t % splits;
+            const size_t lo = n * (size_t)sp / splits, hi = n * (size_t)(sp + 1) / splits;
+            for (size_t b = 0; b < nb; b++) g1_set_inf(&bk[b]);
+            const int32_t *d = dg + (size_t)w * n;
+            for (size_t i = lo; i < hi; i++) {
+                int v = d[i];
+                if (!v || aff_is_inf(&a[i])) continue;
+                if (v > 0) g1_madd(&bk[v - 1], &bk[v - 1], &a[i].x, &a[i].y);
+                else {
+                    fp ny;
+                    fp_neg(&ny, &a[i].y);
+                    g1_madd(&bk[-v - 1], &bk[-v - 1], &a[i].x, &ny);
+                }
+            }
+            g1 run, acc;                                    /* sum_b (b + 1) bk[b] by running sums */
+            g1_set_inf(&run);
+            g1_set_inf(&acc);
+            for (size_t b = nb; b-- > 0;) {
+                g1_add(&run, &run, &bk[b]);
+                g1_add(&acc, &acc, &run);
+            }
+            tsum[t] = acc;
+        }
+        free(bk);
+    }
+    g1 res;
+    g1_set_inf(&res);
+    for (int w = nwin - 1; w >= 0; w--) {
+        for (int k = 0; k < c; k++) g1_dbl(&res, &res);
+        for (int sp = 0; sp < splits; sp++) g1_add(&res, &res, &tsum[w * splits + sp]);
+    }
+    free(tsum);
+    free(dg);
+    g1_ser(out, &res);
     return 0;
 }

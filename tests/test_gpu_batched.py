@@ -158,6 +158,32 @@ def test_batched_malicious_kinds_tiled(nat, tdev):
 
 
 @pytest.mark.parametrize("fused", [False, True])
+def test_batched_two_error_location(nat, tdev, fused):
+    """level 2 locates up to two bad shares per group (k_tpke_rlc_search2): 22 decryptors, 8 ciphertexts with 0, 1, 2
+    (first and last position), 2 (adjacent), 3, 1 + an undecodable (reversed) share, 2 (a wrong point and another
+    player's share) and 2 again (a wrong point and an off-subgroup point) bad shares; only the three-error group reaches
+    single checks, so the levels are [8 groups, 2 x 7 weighted checks, 22 singles]"""
+    b = Batch(b"gpu-batched-two-errors", 22, 7, 8)
+    rows = [list(r) for r in b.good]
+    bad = {1: [5], 2: [0, 21], 3: [3, 4], 4: [1, 7, 12], 5: [9], 6: [10], 7: [6]}
+    for r, pos in bad.items():
+        for j in pos:
+            rows[r][j] = b.bad[r][j]
+    rows[5][2] = rows[5][2][::-1]
+    rows[6][11] = rows[6][12]
+    rows[7][17] = off_subgroup_g1(b.d)
+    shares = [s for r in rows for s in r]
+    expect = np.array([b.expect(i // 22, i % 22, shares[i]) for i in range(len(shares))], dtype=np.uint8)
+    assert expect.sum() == len(shares) - 14
+    ct = np.repeat(np.arange(8, dtype=np.uint32), 22)
+    dec = np.tile(np.arange(22, dtype=np.uint32), 8)
+    got = run_dev(nat, tdev, b, ct, dec, shares, fused=fused)
+    assert np.array_equal(got, expect)
+    levels, _ = nat.tpke_batched_stats()
+    assert levels == [8, 14, 22], levels
+
+
+@pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("density", [0.0, 0.01, 0.3, 1.0])
 def test_batched_corruption_density(nat, tdev, density, fused):
     """22 decryptors (configs[1]'s N), 6 ciphertexts tiled to 8,448 shares; each share independently replaced by a

@@ -6,7 +6,7 @@ import random
 import oracle as o
 import pytest
 
-from helpers import Drbg, kats
+from helpers import Drbg, R, kats
 
 
 def test_serialization_kats():
@@ -314,3 +314,29 @@ def test_rlc_cpu_ts_baseline_and_psi_membership():
                                              ctypes.c_size_t(n), sigs, b"".join(msgs), pp(mo),
                                              ctypes.c_size_t(len(rs)), pp(mi), pp(pi), ctypes.c_uint64(7), 2) == 0
         assert acc.raw == bytes(a for r in rs for a in r["accept"]), key
+
+
+def test_cpu_pippenger_msm_matches_plain_msm():
+    """bench.py's MSM CPU leg (orc_g1_msm_pippenger: signed-digit bucket method over pre-decompressed points) equals the
+    plain sum of scalar multiplications (orc_g1_msm), with infinity, repeated and negated points, scalars 0, 1, r - 1
+    and every window width the bench may pick"""
+    import ctypes
+    lib = o.lib()
+    d = Drbg(b"cpu-pippenger")
+    g = o.g1_gen()
+    base = [o.g1_mul(g, o.fr(d.fr_int())) for _ in range(40)]
+    pts = base + [base[0], o.g1_neg(base[1]), o.g1_mul(g, o.fr(0)), base[2]]
+    scal = [d.fr_int() for _ in range(40)] + [0, 1, R - 1, 12345]
+    pts, scal = pts * 3, scal * 3
+    n = len(pts)
+    pb = b"".join(pts)
+    sb = b"".join(s.to_bytes(32, "little") for s in scal)
+    want = ctypes.create_string_buffer(48)
+    assert lib.orc_g1_msm(want, pb, sb, ctypes.c_size_t(n)) == 0
+    lib.orc_g1_affine_bytes.restype = ctypes.c_size_t
+    aff = ctypes.create_string_buffer(lib.orc_g1_affine_bytes() * n)
+    assert lib.orc_g1_affine_batch(aff, pb, ctypes.c_size_t(n), 4) == 0
+    for c in (2, 5, 8, 13, 16):
+        got = ctypes.create_string_buffer(48)
+        assert lib.orc_g1_msm_pippenger(got, aff, sb, ctypes.c_size_t(n), c, 4) == 0
+        assert got.raw == want.raw, c
