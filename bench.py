@@ -1486,6 +1486,8 @@ def main():
     ap.add_argument("--pattern-steps", type=int, default=2,
                     help="timed steps per Byzantine pattern and path (0 = skip the patterns)")
     ap.add_argument("--patterns", default="", help="comma-separated subset of the Byzantine patterns (default all)")
+    ap.add_argument("--fork-mode", type=int, default=-1,
+                    help="fused batched verify stream layout (lcb_set_fork_mode; -1: library default)")
     ap.add_argument("--coop-max", type=int, default=-1,
                     help="levels of <= this many group checks on the nine-lane cooperative kernels (-1: library default)")
     ap.add_argument("--msm-sizes", default=f"{1 << 20},{1 << 24}",
@@ -1528,6 +1530,8 @@ def main():
     nat.lib()
     if args.coop_max >= 0:
         nat.set_coop_max(args.coop_max)
+    if args.fork_mode >= 0:
+        nat.set_fork_mode(args.fork_mode)
 
     t_gen = time.perf_counter()
     inp = make_inputs(nat, rank, args.shares, args.n, args.f, args.vlen)

@@ -30,23 +30,28 @@
 // Fp2 slots of a group's LDS area (96 B each)
 #define S_F 0                  // 6: the published accumulator
 #define S_Z 6                  // the constant 0
-#define S_P 7                  // 18: products
-#define S_XP 25                // 18: xi * products
-#define S_AUX 43               // 9: pre-sums / recombination outputs
+#define S_P 7                  // 18: products (a reader applies xi itself: cp_lin4's flags)
+#define S_AUX 25               // 9: pre-sums / recombination outputs
 #define S_JUNK (-1)            // "nothing to publish": the store is skipped (exec-masked)
 #define S_LE (S_P + 14)        // 4 evaluated line coefficients (Miller loop only; overlays P[14..17])
-#define CP_NS 52               // 7 areas x 52 x 96 B = 34,944 B per wave: four waves per CU
+#define CP_NS 34               // 7 areas x 34 x 96 B = 22,848 B per wave: seven waves per CU
 #define CP_LDS_QUADS (CP_AREAS * CP_NS * 6)
 
 typedef unsigned long long u64c;
 #define PK9(a0, a1, a2, a3, a4, a5, a6, a7, a8)                                                                        \
     ((u64c)(a0) | (u64c)(a1) << 6 | (u64c)(a2) << 12 | (u64c)(a3) << 18 | (u64c)(a4) << 24 | (u64c)(a5) << 30 |       \
      (u64c)(a6) << 36 | (u64c)(a7) << 42 | (u64c)(a8) << 48)
-DI int sel9(u64c t, int j) { return (int)((t >> (6 * j)) & 63); }
+DI int sel9(u64c t, int j) {
+    asm volatile("" : "+v"(j));       // per use: the per-lane slot indices are not hoisted into long-lived registers
+    return (int)((t >> (6 * j)) & 63);
+}
+DI bool bit9(unsigned m, int j) {      // this lane's flag of a 9-bit per-role mask
+    asm volatile("" : "+v"(j));
+    return (m >> j) & 1u;
+}
 // aliases for the tables
 #define Z_ S_Z
 #define P_(k) (S_P + (k))
-#define X_(k) (S_XP + (k))
 #define A_(k) (S_AUX + (k))
 
 struct Cp {
@@ -54,6 +59,14 @@ struct Cp {
     int j;             // role 0..8
     int g;             // group in the wave (7 = the dummy lane)
 };
+// the lane's role, re-read at every use: the per-lane slot indices, LDS and park addresses derived from it are then
+// recomputed where they are used (a few instructions each) instead of being hoisted out of the program loops into
+// ~100 long-lived registers (the final exponentiation kernel held 391 registers with them, 230 without)
+DI int cpj(const Cp &c) {
+    int j = c.j;
+    asm volatile("" : "+v"(j));
+    return j;
+}
 DI Cp cp_init(uint4 *lds) {
     Cp c;
     const int l = threadIdx.x & 63;
@@ -88,20 +101,22 @@ DI void fp2_sel(fp2 &r, bool c, const fp2 &a, const fp2 &b) {       // r = c ? a
 DI void fp2_cxi(fp2 &r, const fp2 &x, bool c) { fp2 t; fp2_mul_xi(t, x); fp2_sel(r, c, t, x); }
 DI void fp2_cneg(fp2 &r, const fp2 &x, bool c) { fp2 t; fp2_neg(t, x); fp2_sel(r, c, t, x); }
 // the publish of R (lanes 0..5) and the zero slot
-DI void cp_publish(const Cp &c, const fp2 &R) { cp_put(c, c.j < 6 ? S_F + c.j : S_JUNK, R); }
-// out = L[a] - L[b] - L[cc] + xi^dx L[d]
-DI void cp_lin4(fp2 &o, const Cp &c, int a, int b, int cc, int d, bool dx) {
+DI void cp_publish(const Cp &c, const fp2 &R) { cp_put(c, cpj(c) < 6 ? S_F + cpj(c) : S_JUNK, R); }
+// out = xi^fa (L[a] - L[b] - L[cc]) + xi^fd L[d]: the recombinations of the Karatsuba / Granger-Scott products
+// (every lane's formula is a difference of three values and a fourth, each group with one power of xi)
+DI void cp_lin4(fp2 &o, const Cp &c, int a, int b, int cc, int d, bool fa, bool fd) {
     fp2 x;
     cp_get(o, c, a);
     cp_get(x, c, b);
     fp2_sub(o, o, x);
     cp_get(x, c, cc);
     fp2_sub(o, o, x);
+    fp2_cxi(o, o, fa);
     cp_get(x, c, d);
-    fp2_cxi(x, x, dx);
+    fp2_cxi(x, x, fd);
     fp2_add(o, o, x);
 }
-// one product per lane: (L[xa] + L[xb]) * xi^yx (L[ya] + L[yb]) -> P[pk], XP[pk] (pk = -1: JUNK)
+// one product per lane: (L[xa] + L[xb]) * xi^yx (L[ya] + L[yb]) -> P[pk] (pk = -1: nothing published)
 DI void cp_prod(const Cp &c, int xa, int xb, int ya, int yb, bool yx, int pk) {
     fp2 x, y, t;
     cp_get(x, c, xa);
@@ -112,9 +127,7 @@ DI void cp_prod(const Cp &c, int xa, int xb, int ya, int yb, bool yx, int pk) {
     fp2_add(y, y, t);
     fp2_cxi(y, y, yx);
     fp2_mul(x, x, y);
-    fp2_mul_xi(t, x);
     cp_put(c, pk >= 0 ? S_P + pk : S_JUNK, x);
-    cp_put(c, pk >= 0 ? S_XP + pk : S_JUNK, t);
 }
 
 // ---------------------------------------------------------------- park (HBM) access: lane j < 6 owns coefficient j
@@ -148,12 +161,25 @@ DI void park_coef(fp2 &x, const u32 *slot, size_t n, size_t i, int k) {
 // R <- R^2 (any Fp12): T = c0 c1 and Q = (c0 + c1)(c0 + v c1) as two Karatsuba Fp6 products (12 products), then
 // c0' = Q - T - v T, c1' = 2 T (field.hpp fp12_sqr).  Round B's idle lanes 3..6 evaluate the next line's coefficients
 // (ev: a product whose operands come from HBM: a line coefficient and a point coordinate).
-struct CpEval {                // a product lane's HBM operands: line coefficient x point coordinate (as (c, 0))
-    bool on;
-    fp2 x, y;
+struct CpEval {                // a product lane's HBM operands: line coefficient x point coordinate (as (c, 0)),
+    bool on;                   // read where they are used (not held across the loop)
+    bool yinf;                 // the point is at infinity: coordinate 0, so every line evaluates to 1
+    const u32 *xp, *yp;
 };
+DI void cp_ev_get(fp2 &x, fp2 &y, const CpEval &ev) {
+    fp2_load_w(x, ev.xp);
+    const uint4 *q = (const uint4 *)ev.yp;
+    u32 *w = (u32 *)&y.a;
+#pragma unroll
+    for (int g = 0; g < 3; g++) {
+        uint4 v = q[g];
+        w[4 * g] = v.x; w[4 * g + 1] = v.y; w[4 * g + 2] = v.z; w[4 * g + 3] = v.w;
+    }
+    if (ev.yinf) y.a = fp_zero();
+    y.b = fp_zero();
+}
 DI void cp_sqr12(fp2 &R, const Cp &c, const CpEval &ev) {
-    const int j = c.j;
+    const int j = cpj(c);
     cp_publish(c, R);
     cp_sync();
     {   // S_k = a_k + b_k (lanes 0..2), U = (a0 + xi b2, a1 + b0, a2 + b1) (lanes 3..5) -> AUX0..5
@@ -176,21 +202,23 @@ DI void cp_sqr12(fp2 &R, const Cp &c, const CpEval &ev) {
         cp_get(y, c, sel9(PK9(A_(4), A_(3), A_(3), Z_, Z_, Z_, Z_, Z_, Z_), j));
         cp_get(t, c, sel9(PK9(A_(5), A_(4), A_(5), Z_, Z_, Z_, Z_, Z_, Z_), j));
         fp2_add(y, y, t);
-        fp2_sel(x, ev.on, ev.x, x);
-        fp2_sel(y, ev.on, ev.y, y);
+        {
+            fp2 ex, ey;
+            cp_ev_get(ex, ey, ev);
+            fp2_sel(x, ev.on, ex, x);
+            fp2_sel(y, ev.on, ey, y);
+        }
         fp2_mul(x, x, y);
-        fp2_mul_xi(t, x);
         const int slot = j < 3 ? S_P + 9 + j : (ev.on ? S_LE + j - 3 : S_JUNK);
         cp_put(c, slot, x);
-        cp_put(c, j < 3 ? S_XP + 9 + j : S_JUNK, t);
     }
     cp_sync();
     {   // T_k = fp6 recombination of P0..5 (lanes 0..2), Q_k of P6..11 (lanes 3..5) -> AUX0..5
         fp2 o;
-        cp_lin4(o, c, sel9(PK9(X_(3), P_(4), P_(5), X_(9), P_(10), P_(11), Z_, Z_, Z_), j),
-                sel9(PK9(X_(1), P_(0), P_(0), X_(7), P_(6), P_(6), Z_, Z_, Z_), j),
-                sel9(PK9(X_(2), P_(1), P_(2), X_(8), P_(7), P_(8), Z_, Z_, Z_), j),
-                sel9(PK9(P_(0), X_(2), P_(1), P_(6), X_(8), P_(7), Z_, Z_, Z_), j), false);
+        cp_lin4(o, c, sel9(PK9(P_(3), P_(4), P_(1), P_(9), P_(10), P_(7), Z_, Z_, Z_), j),
+                sel9(PK9(P_(1), P_(0), P_(0), P_(7), P_(6), P_(6), Z_, Z_, Z_), j),
+                sel9(PK9(P_(2), P_(1), P_(2), P_(8), P_(7), P_(8), Z_, Z_, Z_), j),
+                sel9(PK9(P_(0), P_(2), P_(5), P_(6), P_(8), P_(11), Z_, Z_, Z_), j), bit9(0x009u, j), bit9(0x012u, j));
         cp_put(c, j < 6 ? S_AUX + j : S_JUNK, o);
     }
     cp_sync();
@@ -211,7 +239,7 @@ DI void cp_sqr12(fp2 &R, const Cp &c, const CpEval &ev) {
 // X = v f0, Y = v f1; t0_k = b X_k, t1_k = c Y_k, s_k = (b + c)(X_k + Y_k);
 // f0_k += t0_k + (v t1)_k, f1_k += s_k - t0_k - t1_k
 DI void cp_line(fp2 &R, const Cp &c, int sb, int sc) {
-    const int j = c.j;
+    const int j = cpj(c);
     cp_publish(c, R);
     cp_sync();
     const int xa = j < 3 ? sb : (j < 6 ? sc : sb), xb = j < 6 ? S_Z : sc;
@@ -219,25 +247,26 @@ DI void cp_line(fp2 &R, const Cp &c, int sb, int sc) {
             j == 0 || j == 3 || j == 6, j);
     cp_sync();
     fp2 o;
-    cp_lin4(o, c, sel9(PK9(P_(0), P_(1), P_(2), P_(6), P_(7), P_(8), Z_, Z_, Z_), j),
+    cp_lin4(o, c, sel9(PK9(P_(5), P_(3), P_(4), P_(6), P_(7), P_(8), Z_, Z_, Z_), j),
             sel9(PK9(Z_, Z_, Z_, P_(0), P_(1), P_(2), Z_, Z_, Z_), j),
             sel9(PK9(Z_, Z_, Z_, P_(3), P_(4), P_(5), Z_, Z_, Z_), j),
-            sel9(PK9(X_(5), P_(3), P_(4), Z_, Z_, Z_, Z_, Z_, Z_), j), false);
+            sel9(PK9(P_(0), P_(1), P_(2), Z_, Z_, Z_, Z_, Z_, Z_), j), bit9(0x001u, j), false);
     fp2_add(o, o, R);
     if (j < 6) R = o;
 }
 // a round of products whose operands come from HBM only (the line evaluations of a step without squaring)
 // (the evaluating lanes are 3..6, as in cp_sqr12's round B)
 DI void cp_eval_round(const Cp &c, const CpEval &ev) {
-    fp2 x = ev.x, y = ev.y;
+    fp2 x, y;
+    cp_ev_get(x, y, ev);
     fp2_mul(x, x, y);
-    cp_put(c, ev.on ? S_LE + c.j - 3 : S_JUNK, x);
+    cp_put(c, ev.on ? S_LE + cpj(c) - 3 : S_JUNK, x);
 }
 // R <- R^2 for R in the cyclotomic subgroup (Granger-Scott, field.hpp fp12_cyc_sqr): per pair (a, b) of
 // (z0, z1) = (F0, F4), (z2, z3) = (F3, F2), (z4, z5) = (F1, F5): a^2, b^2, (a + b)^2; c0 = a^2 + xi b^2,
 // c1 = (a + b)^2 - a^2 - b^2; z' = 3 c -/+ 2 z
 DI void cp_cyc_sqr(fp2 &R, const Cp &c) {
-    const int j = c.j;
+    const int j = cpj(c);
     cp_publish(c, R);
     cp_sync();
     {
@@ -246,17 +275,15 @@ DI void cp_cyc_sqr(fp2 &R, const Cp &c) {
         cp_get(t, c, sel9(PK9(Z_, Z_, 4, Z_, Z_, 2, Z_, Z_, 5), j));
         fp2_add(x, x, t);
         fp2_sqr(x, x);
-        fp2_mul_xi(t, x);
         cp_put(c, S_P + j, x);
-        cp_put(c, S_XP + j, t);
     }
     cp_sync();
     fp2 y, u;
     // F0: c0(0) = P0 + xi P1, F1: c0(1) = P3 + xi P4, F2: c0(2) = P6 + xi P7, F3: xi c1(2), F4: c1(0), F5: c1(1)
-    cp_lin4(y, c, sel9(PK9(P_(0), P_(3), P_(6), X_(8), P_(2), P_(5), Z_, Z_, Z_), j),
-            sel9(PK9(Z_, Z_, Z_, X_(6), P_(0), P_(3), Z_, Z_, Z_), j),
-            sel9(PK9(Z_, Z_, Z_, X_(7), P_(1), P_(4), Z_, Z_, Z_), j),
-            sel9(PK9(X_(1), X_(4), X_(7), Z_, Z_, Z_, Z_, Z_, Z_), j), false);
+    cp_lin4(y, c, sel9(PK9(P_(1), P_(4), P_(7), P_(8), P_(2), P_(5), Z_, Z_, Z_), j),
+            sel9(PK9(Z_, Z_, Z_, P_(6), P_(0), P_(3), Z_, Z_, Z_), j),
+            sel9(PK9(Z_, Z_, Z_, P_(7), P_(1), P_(4), Z_, Z_, Z_), j),
+            sel9(PK9(P_(0), P_(3), P_(6), Z_, Z_, Z_, Z_, Z_, Z_), j), bit9(0x00fu, j), false);
     fp2_cneg(u, R, j < 3);          // 3y - 2z (c0 outputs) or 3y + 2z (c1 outputs) = y + 2 (y -/+ z)
     fp2_add(u, u, y);
     fp2_add(u, u, u);
@@ -266,7 +293,7 @@ DI void cp_cyc_sqr(fp2 &R, const Cp &c) {
 // R <- (conj_a ? conj(R) : R) * B with B parked at bslot (Karatsuba over Fp6: T = a0 b0, U = a1 b1,
 // M = (a0 + a1)(b0 + b1): 18 products in two rounds; c0 = T + v U, c1 = M - T - U)
 DI void cp_mul12(fp2 &R, const Cp &c, bool conj_a, const u32 *bslot, size_t n, size_t i) {
-    const int j = c.j;
+    const int j = cpj(c);
     fp2 a;
     fp2_cneg(a, R, conj_a && j >= 3);
     cp_publish(c, a);
@@ -300,33 +327,32 @@ DI void cp_mul12(fp2 &R, const Cp &c, bool conj_a, const u32 *bslot, size_t n, s
         park_coef(t, bslot, n, i, sel9(Y3, j));
         fp2_add(y, y, t);
         fp2_mul(x, x, y);
-        fp2_mul_xi(t, x);
         cp_put(c, S_P + 9 * r + j, x);
-        cp_put(c, S_XP + 9 * r + j, t);
     }
     cp_sync();
     {   // T_k (lanes 0..2), U_k (3..5), M_k (6..8): fp6 recombination of P0..5, P6..11, P12..17 -> AUX0..8
         fp2 o;
-        cp_lin4(o, c, sel9(PK9(X_(3), P_(4), P_(5), X_(9), P_(10), P_(11), X_(15), P_(16), P_(17)), j),
-                sel9(PK9(X_(1), P_(0), P_(0), X_(7), P_(6), P_(6), X_(13), P_(12), P_(12)), j),
-                sel9(PK9(X_(2), P_(1), P_(2), X_(8), P_(7), P_(8), X_(14), P_(13), P_(14)), j),
-                sel9(PK9(P_(0), X_(2), P_(1), P_(6), X_(8), P_(7), P_(12), X_(14), P_(13)), j), false);
+        cp_lin4(o, c, sel9(PK9(P_(3), P_(4), P_(1), P_(9), P_(10), P_(7), P_(15), P_(16), P_(13)), j),
+                sel9(PK9(P_(1), P_(0), P_(0), P_(7), P_(6), P_(6), P_(13), P_(12), P_(12)), j),
+                sel9(PK9(P_(2), P_(1), P_(2), P_(8), P_(7), P_(8), P_(14), P_(13), P_(14)), j),
+                sel9(PK9(P_(0), P_(2), P_(5), P_(6), P_(8), P_(11), P_(12), P_(14), P_(17)), j), bit9(0x049u, j),
+                bit9(0x092u, j));
         cp_put(c, S_AUX + j, o);
     }
     cp_sync();
     {   // c0 = (T0 + xi U2, T1 + U0, T2 + U1) (lanes 0..2), c1_k = M_k - T_k - U_k (lanes 3..5)
         fp2 o;
-        cp_lin4(o, c, sel9(PK9(A_(0), A_(1), A_(2), A_(6), A_(7), A_(8), Z_, Z_, Z_), j),
+        cp_lin4(o, c, sel9(PK9(A_(5), A_(3), A_(4), A_(6), A_(7), A_(8), Z_, Z_, Z_), j),
                 sel9(PK9(Z_, Z_, Z_, A_(0), A_(1), A_(2), Z_, Z_, Z_), j),
                 sel9(PK9(Z_, Z_, Z_, A_(3), A_(4), A_(5), Z_, Z_, Z_), j),
-                sel9(PK9(A_(5), A_(3), A_(4), Z_, Z_, Z_, Z_, Z_, Z_), j), j == 0);
+                sel9(PK9(A_(0), A_(1), A_(2), Z_, Z_, Z_, Z_, Z_, Z_), j), bit9(0x001u, j), false);
         if (j < 6) R = o;
     }
 }
 // Frobenius maps (field.hpp fp12_frob1/2/3): coefficient g_m (m = (0, 2, 4, 1, 3, 5)[j]) times gamma_k[m], conjugated
 // for k = 1, 3
 DI void cp_frob(fp2 &R, const Cp &c, int k) {
-    const int j = c.j < 6 ? c.j : 0;
+    const int j = cpj(c) < 6 ? cpj(c) : 0;
     const int m = (int)((0x531420u >> (4 * j)) & 15);
     fp2 g, cst;
     if (k != 2) fp2_conj(g, R);
@@ -335,15 +361,15 @@ DI void cp_frob(fp2 &R, const Cp &c, int k) {
     else if (k == 3) fp2_load_const(cst, LCB_GAMMA3 + 24 * m);
     else { fp_load_const(cst.a, LCB_GAMMA2 + 12 * m); cst.b = fp_zero(); }
     fp2_mul(g, g, cst);
-    if (c.j < 6) R = g;
+    if (cpj(c) < 6) R = g;
 }
-DI void cp_conj(fp2 &R, const Cp &c) { fp2_cneg(R, R, c.j >= 3 && c.j < 6); }
-DI void cp_one(fp2 &R, const Cp &c) { R = c.j == 0 ? fp2_one() : fp2_zero(); }
+DI void cp_conj(fp2 &R, const Cp &c) { fp2_cneg(R, R, cpj(c) >= 3 && cpj(c) < 6); }
+DI void cp_one(fp2 &R, const Cp &c) { R = cpj(c) == 0 ? fp2_one() : fp2_zero(); }
 // fp6 products of two Fp6 operands held in slots, two per call: (a0 (slots xa..xa+2) x b0 (ya..)) -> P0..5 and
 // (a1 (xb..) x b1 (yb..)) -> P6..11, Karatsuba (t_k = a_k b_k, (a1+a2)(b1+b2), (a0+a1)(b0+b1), (a0+a2)(b0+b2)) in two
 // rounds of nine lanes
 DI void cp_fp6_pair(const Cp &c, int xa, int ya, int xb, int yb) {
-    const int j = c.j;
+    const int j = cpj(c);
 #pragma unroll
     for (int r = 0; r < 2; r++) {
         const int pk = 9 * r + j;                      // product 0..11 (12..17: idle)
@@ -358,17 +384,17 @@ DI void cp_fp6_pair(const Cp &c, int xa, int ya, int xb, int yb) {
 // R <- R^-1 (field.hpp fp12_inv / fp6_inv / fp2_inv): c0^2 and c1^2, d = c0^2 - v c1^2, d^-1 by the fp6 adjugate and
 // one Fp inversion (role-0 lanes only), then (c0 d^-1, -c1 d^-1)
 DI void cp_inv(fp2 &R, const Cp &c) {
-    const int j = c.j;
+    const int j = cpj(c);
     cp_publish(c, R);
     cp_sync();
     cp_fp6_pair(c, 0, 0, 3, 3);                        // c0^2 -> P0..5, c1^2 -> P6..11
     cp_sync();
     {   // T = c0^2 (lanes 0..2), U = c1^2 (lanes 3..5) -> AUX0..5 (fp6 recombination, as cp_sqr12 stage 1)
         fp2 o;
-        cp_lin4(o, c, sel9(PK9(X_(3), P_(4), P_(5), X_(9), P_(10), P_(11), Z_, Z_, Z_), j),
-                sel9(PK9(X_(1), P_(0), P_(0), X_(7), P_(6), P_(6), Z_, Z_, Z_), j),
-                sel9(PK9(X_(2), P_(1), P_(2), X_(8), P_(7), P_(8), Z_, Z_, Z_), j),
-                sel9(PK9(P_(0), X_(2), P_(1), P_(6), X_(8), P_(7), Z_, Z_, Z_), j), false);
+        cp_lin4(o, c, sel9(PK9(P_(3), P_(4), P_(1), P_(9), P_(10), P_(7), Z_, Z_, Z_), j),
+                sel9(PK9(P_(1), P_(0), P_(0), P_(7), P_(6), P_(6), Z_, Z_, Z_), j),
+                sel9(PK9(P_(2), P_(1), P_(2), P_(8), P_(7), P_(8), Z_, Z_, Z_), j),
+                sel9(PK9(P_(0), P_(2), P_(5), P_(6), P_(8), P_(11), Z_, Z_, Z_), j), bit9(0x009u, j), bit9(0x012u, j));
         cp_put(c, j < 6 ? S_AUX + j : S_JUNK, o);
     }
     cp_sync();
@@ -387,8 +413,9 @@ DI void cp_inv(fp2 &R, const Cp &c) {
     cp_sync();
     {   // A = d0^2 - xi d1 d2, B = xi d2^2 - d0 d1, C = d1^2 - d0 d2 (lanes 0..2) -> AUX0..2
         fp2 o;
-        cp_lin4(o, c, sel9(PK9(P_(0), X_(2), P_(4), Z_, Z_, Z_, Z_, Z_, Z_), j),
-                sel9(PK9(X_(1), P_(3), P_(5), Z_, Z_, Z_, Z_, Z_, Z_), j), S_Z, S_Z, false);
+        cp_lin4(o, c, sel9(PK9(Z_, Z_, P_(4), Z_, Z_, Z_, Z_, Z_, Z_), j),
+                sel9(PK9(P_(1), P_(3), P_(5), Z_, Z_, Z_, Z_, Z_, Z_), j), S_Z,
+                sel9(PK9(P_(0), P_(2), Z_, Z_, Z_, Z_, Z_, Z_, Z_), j), bit9(0x001u, j), bit9(0x002u, j));
         cp_put(c, j < 3 ? S_AUX + j : S_JUNK, o);
     }
     cp_sync();
@@ -425,17 +452,17 @@ DI void cp_inv(fp2 &R, const Cp &c) {
     cp_fp6_pair(c, S_F + 0, S_AUX + 6, S_F + 3, S_AUX + 6);   // c0 d^-1 -> P0..5, c1 d^-1 -> P6..11
     cp_sync();
     fp2 o;
-    cp_lin4(o, c, sel9(PK9(X_(3), P_(4), P_(5), X_(9), P_(10), P_(11), Z_, Z_, Z_), j),
-            sel9(PK9(X_(1), P_(0), P_(0), X_(7), P_(6), P_(6), Z_, Z_, Z_), j),
-            sel9(PK9(X_(2), P_(1), P_(2), X_(8), P_(7), P_(8), Z_, Z_, Z_), j),
-            sel9(PK9(P_(0), X_(2), P_(1), P_(6), X_(8), P_(7), Z_, Z_, Z_), j), false);
+    cp_lin4(o, c, sel9(PK9(P_(3), P_(4), P_(1), P_(9), P_(10), P_(7), Z_, Z_, Z_), j),
+            sel9(PK9(P_(1), P_(0), P_(0), P_(7), P_(6), P_(6), Z_, Z_, Z_), j),
+            sel9(PK9(P_(2), P_(1), P_(2), P_(8), P_(7), P_(8), Z_, Z_, Z_), j),
+            sel9(PK9(P_(0), P_(2), P_(5), P_(6), P_(8), P_(11), Z_, Z_, Z_), j), bit9(0x009u, j), bit9(0x012u, j));
     fp2_cneg(o, o, j >= 3);                            // r1 = -(c1 d^-1)
     if (j < 6) R = o;
 }
 // all six coefficients equal those of 1 (wave ballot over the group's lanes 0..5)
 DI bool cp_is_one(const fp2 &R, const Cp &c) {
-    fp2 e = c.j == 0 ? fp2_one() : fp2_zero();
-    const bool bad = c.j < 6 && !fp2_eq(R, e);
+    fp2 e = cpj(c) == 0 ? fp2_one() : fp2_zero();
+    const bool bad = cpj(c) < 6 && !fp2_eq(R, e);
     const u64c m = __ballot(bad);
     return ((m >> (CP_L * c.g)) & 0x3f) == 0;
 }
@@ -489,8 +516,8 @@ DI void cp_final_exp(fp2 &R, const Cp &c, u32 *park, size_t n, size_t i, bool li
     for (int pc = 0; pc < np; pc++) {
         const int op = LCB_FE_PROG.op[pc], kind = op & 15, s = op >> 4;
         u32 *slot = fe_slot(park, n, s);
-        if (kind == FE_LD) park_get(R, slot, n, i, c.j);
-        else if (kind == FE_ST) park_put(slot, n, i, c.j, live, R);
+        if (kind == FE_LD) park_get(R, slot, n, i, cpj(c));
+        else if (kind == FE_ST) park_put(slot, n, i, cpj(c), live, R);
         else if (kind == FE_CJ) cp_conj(R, c);
         else if (kind == FE_CS) cp_cyc_sqr(R, c);
         else if (kind == FE_MU || kind == FE_MC) cp_mul12(R, c, kind == FE_MC, slot, n, i);

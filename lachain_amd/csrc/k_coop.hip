@@ -10,28 +10,31 @@ LCB_ASM_LIBRARY(k_coop)
 // conjugated, from the ciphertext's two normalised line sets.  Lanes 3..6 evaluate the line coefficients
 // (B'_1 x_1, C'_1 y_1, B'_2 x_2, C'_2 y_2).  A group whose line sets are not normalised (some A_k == 0, only for
 // adversarial W) is flagged in fb and left to k_rlc_miller_fallback.
+// npairs = 1: only the first pair (mclBn_pairing: the second set is the point at infinity's, whose lines are 1 — the
+// skipped products are exact multiplications by 1, so the value is the same)
 extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_tpke_miller(const u32 *lines, const uint4 *desc,
                                                                          const g1a_st *gpts, u32 n_groups,
-                                                                         u32 *f_soa, uint8_t *gacc, uint8_t *fb) {
+                                                                         u32 *f_soa, uint8_t *gacc, uint8_t *fb,
+                                                                         u32 npairs) {
     __shared__ uint4 lds[CP_LDS_QUADS];
     const Cp c = cp_init(lds);
     const u32 item = blockIdx.x * CP_G + c.g;
     const bool live = c.g < CP_G && item < n_groups;
     const u32 it = live ? item : 0;
-    if (c.j == 0) cp_put(c, S_Z, fp2_zero());
+    if (cpj(c) == 0) cp_put(c, S_Z, fp2_zero());
     const u32 ct = desc[it].z;
     const u32 *ls1 = lines + (size_t)(2 * ct) * LCB_LINESET_WORDS, *ls2 = ls1 + LCB_LINESET_WORDS;
     const bool norm = lineset_normalised(ls1) && lineset_normalised(ls2);
-    const int e = c.j - 3;
+    const int e = cpj(c) - 3;
     const bool evl = e >= 0 && e < 4;
     const int ee = evl ? e : 0, pr = ee >> 1, cf = ee & 1;
     const u32 *lse = (pr ? ls2 : ls1) + 24 * cf;
     CpEval ev;
     ev.on = evl;
     {
-        const g1a_st P = gpts[2 * (size_t)it + pr];
-        ev.y.a = P.inf ? fp_zero() : (cf ? P.y : P.x);      // a point at infinity: every line evaluates to 1
-        ev.y.b = fp_zero();
+        const g1a_st *P = gpts + 2 * (size_t)it + pr;
+        ev.yinf = P->inf != 0;                               // a point at infinity: every line evaluates to 1
+        ev.yp = (const u32 *)(cf ? &P->y : &P->x);
     }
     cp_sync();
     fp2 R;
@@ -39,23 +42,23 @@ extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_tpke_miller(const 
     int k = 0;
 #pragma unroll 1
     for (int i = 62; i >= 0; i--) {
-        fp2_load_w(ev.x, lse + (size_t)k * LCB_NLINE_WORDS);
+        ev.xp = lse + (size_t)k * LCB_NLINE_WORDS;
         if (i == 62) cp_eval_round(c, ev);
         else cp_sqr12(R, c, ev);
         cp_line(R, c, S_LE, S_LE + 1);
-        cp_line(R, c, S_LE + 2, S_LE + 3);
+        if (npairs > 1) cp_line(R, c, S_LE + 2, S_LE + 3);
         k++;
         if ((LCB_Z_ABS >> i) & 1) {
-            fp2_load_w(ev.x, lse + (size_t)k * LCB_NLINE_WORDS);
+            ev.xp = lse + (size_t)k * LCB_NLINE_WORDS;
             cp_eval_round(c, ev);
             cp_line(R, c, S_LE, S_LE + 1);
-            cp_line(R, c, S_LE + 2, S_LE + 3);
+            if (npairs > 1) cp_line(R, c, S_LE + 2, S_LE + 3);
             k++;
         }
     }
     cp_conj(R, c);
-    park_put(f_soa, n_groups, it, c.j, live && norm, R);
-    if (live && c.j == 0) {
+    park_put(f_soa, n_groups, it, cpj(c), live && norm, R);
+    if (live && cpj(c) == 0) {
         gacc[item] = 1;
         fb[item] = !norm;
     }
@@ -83,13 +86,13 @@ extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_final_exp_check(u3
     const u32 item = blockIdx.x * CP_G + c.g;
     const bool live = c.g < CP_G && item < n;
     const size_t it = live ? item : 0;
-    if (c.j == 0) cp_put(c, S_Z, fp2_zero());
+    if (cpj(c) == 0) cp_put(c, S_Z, fp2_zero());
     cp_sync();
     fp2 R;
     cp_final_exp(R, c, park, n, it, live);
     const bool one = cp_is_one(R, c);
-    park_put(park, n, it, c.j, live, R);
-    if (live && c.j == 0 && accept) accept[item] = accept[item] && one;
+    park_put(park, n, it, cpj(c), live, R);
+    if (live && cpj(c) == 0 && accept) accept[item] = accept[item] && one;
 }
 
 // The exact per-share check (k_tpke_miller's inputs) in the cooperative kernels' form, for small batches: share i
@@ -130,16 +133,16 @@ extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_debug(int op, u32 
     const u32 item = blockIdx.x * CP_G + c.g;
     const bool live = c.g < CP_G && item < n;
     const size_t it = live ? item : 0;
-    if (c.j == 0) cp_put(c, S_Z, fp2_zero());
+    if (cpj(c) == 0) cp_put(c, S_Z, fp2_zero());
     cp_sync();
     fp12 fa, fb, fr;
-    if (c.j == 0) {
+    if (cpj(c) == 0) {
         fp12_load_soa(fa, ws, n, it);
         fp12_load_soa(fb, b_soa, n, it);
     }
     fp2 R;
-    park_get(R, ws, n, it, c.j);
-    if (op == 0) { CpEval ev; ev.on = false; ev.x = fp2_zero(); ev.y = fp2_zero(); cp_sqr12(R, c, ev); }
+    park_get(R, ws, n, it, cpj(c));
+    if (op == 0) { CpEval ev; ev.on = false; ev.yinf = true; ev.xp = ev.yp = ws; cp_sqr12(R, c, ev); }
     else if (op == 1) cp_cyc_sqr(R, c);
     else if (op == 2 || op == 3) cp_mul12(R, c, op == 3, b_soa, n, it);
     else if (op >= 4 && op <= 6) cp_frob(R, c, op - 3);
@@ -149,14 +152,14 @@ extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_debug(int op, u32 
         fp2 b, cc;
         park_get(b, b_soa, n, it, 0);
         park_get(cc, b_soa, n, it, 1);
-        if (c.j == 0) { cp_put(c, S_LE, b); cp_put(c, S_LE + 1, cc); }
+        if (cpj(c) == 0) { cp_put(c, S_LE, b); cp_put(c, S_LE + 1, cc); }
         cp_sync();
         cp_line(R, c, S_LE, S_LE + 1);
     } else {
         cp_final_exp(R, c, ws, n, it, live);
     }
-    park_put(out, n, it, c.j, live, R);
-    if (live && c.j == 0) {
+    park_put(out, n, it, cpj(c), live, R);
+    if (live && cpj(c) == 0) {
         if (op == 0) fp12_sqr_n(fr, fa);
         else if (op == 1) fp12_cyc_sqr_n(fr, fa);
         else if (op == 2) fp12_mul_n(fr, fa, fb);
@@ -174,10 +177,10 @@ extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_debug(int op, u32 
 
 // ---------------------------------------------------------------- host launch wrappers
 extern "C" void lcbk_coop_tpke_miller(hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups,
-                                      u32 *f_soa, uint8_t *gacc, uint8_t *fb) {
+                                      u32 *f_soa, uint8_t *gacc, uint8_t *fb, u32 npairs) {
     dim3 grid((n_groups + CP_G - 1) / CP_G);
     hipLaunchKernelGGL(k_coop_tpke_miller, grid, dim3(CP_BLOCK), 0, s, lines, (const uint4 *)desc, (const g1a_st *)gpts,
-                       n_groups, f_soa, gacc, fb);
+                       n_groups, f_soa, gacc, fb, npairs);
     grid = dim3((n_groups + LCB_BLOCK - 1) / LCB_BLOCK);
     LCB_LAUNCH(k_rlc_miller_fallback, lines, (const uint4 *)desc, (const g1a_st *)gpts, n_groups, f_soa, fb);
 }

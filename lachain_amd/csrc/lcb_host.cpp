@@ -483,6 +483,8 @@ void ctx_free(lcb_ctx *c) {
         (void)hipStreamSynchronize(c->aux);
         for (auto &e : c->fork_ev) (void)hipEventDestroy(e);
         (void)hipStreamDestroy(c->aux);
+        (void)hipStreamSynchronize(c->hi);
+        (void)hipStreamDestroy(c->hi);
     }
     lcb_int::ecdsa_ctx_release(c);
     if (c->ver_ev_ready) for (auto &e : c->ver_ev) (void)hipEventDestroy(e);
@@ -579,6 +581,8 @@ bool tpke_shape_ok(lcb_ctx *c, size_t n_keys, size_t n_cts, const char *what) {
     }
     return true;
 }
+std::atomic<int> g_fork_mode{1};            // lcb_set_fork_mode: stream layout of the fused batched verify (1: measured
+                                            // 104.8 vs 117.8 ms per 1M-share TPKE step, profiles/r03/ab1)
 std::atomic<uint32_t> g_coop_max{32768};    // lcb_set_coop_max: batches / levels of <= this many checks use the 9-lane kernels
 // the exact check of n shares against prepared line sets (lines, ctok: n_cts ciphertexts) and decompressed keys
 int tpke_verify_core(lcb_ctx *c, const u32 *lines, const uint8_t *ctok, size_t n_cts, size_t n_keys, uint8_t *d_accept,
@@ -607,7 +611,7 @@ int tpke_verify_core(lcb_ctx *c, const u32 *lines, const uint8_t *ctok, size_t n
             if (coop) {
                 lcbk_tpke_exact_points(s, ctok, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct, d_dec, d_ui, (u32)m, gpts,
                                        desc, d_accept);
-                lcbk_coop_tpke_miller(s, lines, desc, gpts, (u32)m, f, fl, fl + n);
+                lcbk_coop_tpke_miller(s, lines, desc, gpts, (u32)m, f, fl, fl + n, 2);
             } else {
                 lcbk_tpke_miller(dim3(nblk(m)), s, lines, ctok, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct + o,
                                  d_dec + o, d_ui + 48 * o, (u32)m, f, d_accept + o);
@@ -813,7 +817,7 @@ void rlc_checks(lcb_ctx *c, const RlcKindInfo &K, RlcWs &w, const uint8_t *desc,
                                gacc + o);
         else if (coop)
             lcbk_coop_tpke_miller(s, K.lines, desc + 16 * o, (const uint8_t *)gpts + K.rec * o, (u32)m, f, gacc + o,
-                                  (uint8_t *)c->rlc[15].get(m));
+                                  (uint8_t *)c->rlc[15].get(m), 2);
         else
             lcbk_tpke_rlc_miller(dim3(nblk(m)), s, K.lines, desc + 16 * o, (const uint8_t *)gpts + K.rec * o, (u32)m, f,
                                  gacc + o);
@@ -979,6 +983,9 @@ int tpke_verify_prepared_rlc(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_k
 bool fork_ready(lcb_ctx *c) {
     if (c->fork_ready) return true;
     hipError_t e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
+    int least = 0, greatest = 0;
+    if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->hi, hipStreamNonBlocking, greatest);
     for (auto &ev : c->fork_ev)
         if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     if (e != hipSuccess) { set_err("batched verify: stream creation", e); return false; }
@@ -1003,27 +1010,40 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
     if (n_keys) lcbk_g1_decompress(dim3(nblk(n_keys)), s, d_y, (u32)n_keys, keys);
     RlcWs w;
     const RlcIo io{d_dec, d_ui, d_ct};
+    // mode 0: randomisation on the second stream, preparation + census on the caller's; mode 1: the latency-bound
+    // preparation chain (one lane per ciphertext / line set, < 1.5 waves per SIMD) on a high-priority stream, so
+    // its waves are dispatched ahead of the randomisation's 16 K waves, which run on the caller's stream
+    const bool hp = g_fork_mode.load() == 1;
+    hipStream_t sr = hp ? s : c->aux, sp = hp ? c->hi : s;
     if (n) {
         if (!rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G1_JAC_BYTES, n_keys, census_size(n, n_keys), s)) return -1;
         hipEventRecord(c->fork_ev[0], s);
-        hipStreamWaitEvent(c->aux, c->fork_ev[0], 0);
-        if (rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, c->aux)) return -1;
-        hipEventRecord(c->fork_ev[1], c->aux);
+        hipStreamWaitEvent(hp ? sp : sr, c->fork_ev[0], 0);
+        if (rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, sr)) return -1;
+        if (!hp) hipEventRecord(c->fork_ev[1], sr);
+    } else if (hp) {
+        hipEventRecord(c->fork_ev[0], s);
+        hipStreamWaitEvent(sp, c->fork_ev[0], 0);
     }
     if (n_cts) {
-        lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), s, d_u, d_w, d_v, d_voff, (u32)n_cts, lines, ctok,
+        lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), sp, d_u, d_w, d_v, d_voff, (u32)n_cts, lines, ctok,
                              g_orig_cofactor | (g_line_mode << 1), nullptr);
-        lcbk_lineset_fill(dim3(nblk(2 * n_cts)), s, lines, (u32)(2 * n_cts), nullptr);
+        lcbk_lineset_fill(dim3(nblk(2 * n_cts)), sp, lines, (u32)(2 * n_cts), nullptr);
     }
     if (!launched("tpke prepare launch")) return -1;
     c->t_n_cts = n_cts;
     c->t_n_keys = n_keys;
     c->t_gen++;
     c->t_ready = true;
+    if (n && rlc_g2check(c, sp)) return -1;      // still beside the randomisation
+    if (n && rlc_census(c, RLC_TPKE, w, d_accept, io, sp)) return -1;
+    if (hp) {
+        hipEventRecord(c->fork_ev[1], sp);
+        hipStreamWaitEvent(s, c->fork_ev[1], 0);
+    } else if (n) {
+        hipStreamWaitEvent(s, c->fork_ev[1], 0);
+    }
     if (!n) return 0;
-    if (rlc_g2check(c, s)) return -1;      // still beside the randomisation on the second stream
-    if (rlc_census(c, RLC_TPKE, w, d_accept, io, s)) return -1;
-    hipStreamWaitEvent(s, c->fork_ev[1], 0);
     return rlc_levels(c, RLC_TPKE, w, d_accept, n, io, s);
 }
 
@@ -1108,23 +1128,34 @@ int ts_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const ui
     if (n_pks) lcbk_g1_decompress(dim3(nblk(n_pks)), s, d_pks, (u32)n_pks, keys);
     RlcWs w;
     const RlcIo io{d_pidx, d_sigs, d_midx};
+    // stream layout as in tpke_verify_shares_rlc_fused (lcb_set_fork_mode)
+    const bool hp = g_fork_mode.load() == 1;
+    hipStream_t sr = hp ? s : c->aux, sp = hp ? c->hi : s;
     if (n) {
         if (!rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G2_JAC_BYTES, n_pks, census_size(n, n_pks), s)) return -1;
         hipEventRecord(c->fork_ev[0], s);
-        hipStreamWaitEvent(c->aux, c->fork_ev[0], 0);
-        if (ts_rlc_points_enqueue(c, w, d_accept, n, n_pks, n_msgs, d_sigs, d_midx, d_pidx, c->aux)) return -1;
-        hipEventRecord(c->fork_ev[1], c->aux);
+        hipStreamWaitEvent(hp ? sp : sr, c->fork_ev[0], 0);
+        if (ts_rlc_points_enqueue(c, w, d_accept, n, n_pks, n_msgs, d_sigs, d_midx, d_pidx, sr)) return -1;
+        if (!hp) hipEventRecord(c->fork_ev[1], sr);
+    } else if (hp) {
+        hipEventRecord(c->fork_ev[0], s);
+        hipStreamWaitEvent(sp, c->fork_ev[0], 0);
     }
-    if (n_msgs) lcbk_ts_msg_prepare(dim3(nblk(n_msgs)), s, d_msg, d_moff, (u32)n_msgs, lines, mok,
+    if (n_msgs) lcbk_ts_msg_prepare(dim3(nblk(n_msgs)), sp, d_msg, d_moff, (u32)n_msgs, lines, mok,
                                     g_orig_cofactor | (g_line_mode << 1));
     if (!launched("ts prepare launch")) return -1;
     c->s_n_msgs = n_msgs;
     c->s_n_pks = n_pks;
     c->s_gen++;
     c->s_ready = true;
+    if (n && rlc_census(c, RLC_TS, w, d_accept, io, sp)) return -1;
+    if (hp) {
+        hipEventRecord(c->fork_ev[1], sp);
+        hipStreamWaitEvent(s, c->fork_ev[1], 0);
+    } else if (n) {
+        hipStreamWaitEvent(s, c->fork_ev[1], 0);
+    }
     if (!n) return 0;
-    if (rlc_census(c, RLC_TS, w, d_accept, io, s)) return -1;
-    hipStreamWaitEvent(s, c->fork_ev[1], 0);
     return rlc_levels(c, RLC_TS, w, d_accept, n, io, s);
 }
 
@@ -1385,6 +1416,7 @@ extern "C" void lcb_set_batch_seed(const uint8_t *seed32) {
 }
 extern "C" void lcb_set_batch_census(size_t min_shares) { g_census_min.store(min_shares); }
 extern "C" void lcb_set_coop_max(uint32_t max_checks) { g_coop_max.store(max_checks); }
+extern "C" void lcb_set_fork_mode(int mode) { g_fork_mode.store(mode == 1 ? 1 : 0); }
 // one cooperative Fp12 operation (k_coop_debug) on n values a (and b) vs the one-lane field.hpp routine: AoS in / out
 extern "C" int lcb_debug_coop_op(int op, const uint32_t *a, const uint32_t *b, size_t n, uint32_t *out, uint32_t *ref) {
     SYNC_CTX_OR(c, -1)
@@ -2178,7 +2210,7 @@ extern "C" void mclBn_pairing(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) {
     if (!hit) hipMemcpyAsync(in + 36, y, 288, hipMemcpyHostToDevice, s);
     lcbk_pairing_prep(s, in, gpts, lines, desc, slot, hit ? 0 : 1);
     if (!hit) lcbk_lineset_fill(dim3(1), s, lines + (size_t)2 * slot * (LCB_LINESET_BYTES / 4), 2, nullptr);
-    lcbk_coop_tpke_miller(s, lines, desc, gpts, 1, park, fl, fl + 32);
+    lcbk_coop_tpke_miller(s, lines, desc, gpts, 1, park, fl, fl + 32, 1);
     lcbk_coop_final_exp_check(s, park, 1, nullptr);
     u32 r[144];
     hipMemcpyAsync(r, park, 576, hipMemcpyDeviceToHost, s);

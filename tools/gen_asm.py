@@ -202,29 +202,6 @@ def r_fp_mul2():
     return a.text(), 92
 
 
-def r_fp2_mul():
-    a = Asm()
-    a.label("lcb_r_fp2_mul_eager")
-    P_ = 120
-    load_p(a, P_)
-    XA, XB, YA, YB, SA, SB = vr(0), vr(12), vr(24), vr(36), vr(48), vr(60)
-    M0, M1, M2 = vr(72), vr(84), vr(96)
-    add_unreduced(a, SA, XA, XB)
-    add_unreduced(a, SB, YA, YB)
-    products(a, [dict(a=XA, b=YA, m=M0, acc=108, out=XA),
-                 dict(a=XB, b=YB, m=M1, acc=112, out=XB),
-                 dict(a=SA, b=SB, m=M2, acc=116, out=SA)], P_)
-    reduce_once(a, XA, M0, P_)        # t0 = xa*ya
-    reduce_once(a, XB, M1, P_)        # t1 = xb*yb
-    reduce_once(a, SA, M2, P_)        # t2 = (xa+xb)(ya+yb)
-    sub_mod(a, YA, SA, XA, M0, P_)    # u = t2 - t0
-    sub_mod(a, YA, YA, XB, M1, P_)    # u = t2 - t0 - t1  (= r.b)
-    sub_mod(a, XA, XA, XB, M2, P_)    # r.a = t0 - t1
-    mov(a, XB, YA)
-    a("s_setpc_b64 s[30:31]")
-    return a.text(), 132
-
-
 def products_sqr(a, A, F, E, M, acc, pbase):
     """Montgomery square of A (FIPS as products(), one chain): a^2 = sum_i a_i 2^(32i) W_i with
     W_i = a_i 2^(32i) + 2 sum_{j>i} a_j 2^(32j), whose limbs are a_i (j = i), F[j] = a_j << 1 (j = i + 1) and
@@ -477,7 +454,7 @@ def r_fp2_mul_lazy():
     return a.text(), 132
 
 
-ROUTINES = [r_fp_mul, r_fp_sqr, r_fp_mul2, r_fp2_mul, r_fp2_mul_lazy, r_fp2_sqr, r_fp2_mul_fp]
+ROUTINES = [r_fp_mul, r_fp_sqr, r_fp_mul2, r_fp2_mul_lazy, r_fp2_sqr, r_fp2_mul_fp]
 
 
 def clobber_list(nvgpr, keep):
@@ -540,22 +517,13 @@ __device__ __forceinline__ void lcb_asm_fp_mul2(u32x12 &a0, u32x12 b0, u32x12 &a
         :
         : {clobber_list(nv['r_fp_mul2'], set(range(48)))});
 }}
-// x*y in Fp2: (xa, xb) <- (xa, xb) * (ya, yb); lazy reduction (one REDC per coefficient) unless LCB_FP2_MUL_EAGER
-#ifndef LCB_FP2_MUL_EAGER
+// x*y in Fp2: (xa, xb) <- (xa, xb) * (ya, yb); lazy reduction (one REDC per coefficient)
 __device__ __forceinline__ void lcb_asm_fp2_mul(u32x12 &xa, u32x12 &xb, u32x12 ya, u32x12 yb) {{
     asm({call_seq("lcb_r_fp2_mul")}
         : "+{{v[0:11]}}"(xa), "+{{v[12:23]}}"(xb), "+{{v[24:35]}}"(ya), "+{{v[36:47]}}"(yb)
         :
         : {clobber_list(nv['r_fp2_mul_lazy'], set(range(48)))});
 }}
-#else
-__device__ __forceinline__ void lcb_asm_fp2_mul(u32x12 &xa, u32x12 &xb, u32x12 ya, u32x12 yb) {{
-    asm({call_seq("lcb_r_fp2_mul_eager")}
-        : "+{{v[0:11]}}"(xa), "+{{v[12:23]}}"(xb), "+{{v[24:35]}}"(ya), "+{{v[36:47]}}"(yb)
-        :
-        : {clobber_list(nv['r_fp2_mul'], set(range(48)))});
-}}
-#endif
 // x^2 in Fp2
 __device__ __forceinline__ void lcb_asm_fp2_sqr(u32x12 &xa, u32x12 &xb) {{
     asm({call_seq("lcb_r_fp2_sqr")}
