@@ -1486,6 +1486,8 @@ def main():
     ap.add_argument("--pattern-steps", type=int, default=2,
                     help="timed steps per Byzantine pattern and path (0 = skip the patterns)")
     ap.add_argument("--patterns", default="", help="comma-separated subset of the Byzantine patterns (default all)")
+    ap.add_argument("--coop-miller-max", type=int, default=-1,
+                    help="levels of <= this many group checks run their Miller loops cooperatively (-1: default)")
     ap.add_argument("--fork-mode", type=int, default=-1,
                     help="fused batched verify stream layout (lcb_set_fork_mode; -1: library default)")
     ap.add_argument("--coop-max", type=int, default=-1,
@@ -1532,6 +1534,8 @@ def main():
         nat.set_coop_max(args.coop_max)
     if args.fork_mode >= 0:
         nat.set_fork_mode(args.fork_mode)
+    if args.coop_miller_max >= 0:
+        nat.set_coop_miller_max(args.coop_miller_max)
 
     t_gen = time.perf_counter()
     inp = make_inputs(nat, rank, args.shares, args.n, args.f, args.vlen)

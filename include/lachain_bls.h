@@ -306,6 +306,9 @@ int lcb_batched_census(uint32_t out[4]);
 /* levels of at most max_checks group checks run on the cooperative kernels (k_coop.hip: nine lanes per pairing check,
    lower latency below one wave per SIMD); 0 = always one check per lane.  Default 32768. */
 void lcb_set_coop_max(uint32_t max_checks);
+/* the cooperative threshold of the group Miller loops alone (default 65536; the final exponentiations keep
+   lcb_set_coop_max's) */
+void lcb_set_coop_miller_max(uint32_t max_checks);
 /* stream layout of the fused batched verifies (lcb_tpke_verify_shares_batched_dev, lcb_ts_verify_shares_batched_dev):
    0 = randomisation on the context's second stream beside the preparation on the caller's; 1 (default) = the
    latency-bound preparation chain (hash-to-G2, line sets, census) on a high-priority stream and the randomisation on

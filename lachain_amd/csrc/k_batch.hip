@@ -435,15 +435,16 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum(const uint4 *sdesc, u32 n_
 }
 
 // Level 2 of TPKE (two-error location, see k_tpke_rlc_search2): the weighted sums of the failed level-1 groups listed
-// in sdesc, formed from the shares' randomised records: two lanes per group (U side, Y side), last share to first,
+// in sdesc, formed from the shares' randomised records: four lanes per group ((U, Y) side x (w, v) output), last share to first,
 // s = suffix sum, w = sum of the s (weights c_j = j + 1), v = sum of the w (weights t_j = c_j (c_j + 1) / 2).  Shares of
 // suspect keys keep their positions and add nothing.  gpts[2g + side] = w, gpts[2 (ns + g) + side] = v (Y side
 // negated), so checks g and ns + g give gamma_c = prod g_i^(c_i s_i) and gamma_t = prod g_i^(t_i s_i).
 extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum2(const uint4 *sdesc, u32 ns, const u32 *rU, const u32 *rY, u32 n,
                                                       const u32 *dec_idx, u32 n_keys, const u32 *susp, g1a_st *gpts) {
+    // four lanes per group: (side, which) — each lane one output record, so one inversion (to affine) per lane
     u32 t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= 2 * ns) return;
-    const u32 g = t >> 1, side = t & 1;
+    if (t >= 4 * ns) return;
+    const u32 g = t >> 2, side = t & 1, which = (t >> 1) & 1;
     const uint4 d = sdesc[g];
     const u32 *rec = side ? rY : rU;
     g1 sa, wa, va, p;
@@ -456,13 +457,11 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum2(const uint4 *sdesc, u32 n
             grp_add(sa, sa, p);
         }
         grp_add(wa, wa, sa);
-        grp_add(va, va, wa);
+        if (which) grp_add(va, va, wa);
     }
     g1a_st o;
-    g1_to_st(o, wa, side != 0);
-    gpts[2 * (size_t)g + side] = o;
-    g1_to_st(o, va, side != 0);
-    gpts[2 * ((size_t)ns + g) + side] = o;
+    g1_to_st(o, which ? va : wa, side != 0);
+    gpts[2 * ((size_t)(which ? ns : 0) + g) + side] = o;
 }
 
 // W of every ciphertext in G2 (Scott's psi test, curve.hpp g2_in_subgroup); H = hash-to-G2 output is in G2 by
@@ -991,7 +990,7 @@ extern "C" void lcbk_rlc_search(dim3 grid, hipStream_t s, const void *search, u3
 }
 extern "C" void lcbk_tpke_rlc_wsum2(hipStream_t s, const void *sdesc, u32 ns, const u32 *rU, const u32 *rY, u32 n,
                                     const u32 *dec_idx, u32 n_keys, const u32 *susp, void *gpts) {
-    dim3 grid((2 * ns + LCB_BLOCK - 1) / LCB_BLOCK);
+    dim3 grid((4 * (size_t)ns + LCB_BLOCK - 1) / LCB_BLOCK);
     LCB_LAUNCH(k_tpke_rlc_wsum2, (const uint4 *)sdesc, ns, rU, rY, n, dec_idx, n_keys, susp, (g1a_st *)gpts);
 }
 extern "C" void lcbk_rlc_park_copy(hipStream_t s, const u32 *park, u32 o, u32 m, u32 *dst) {

@@ -81,7 +81,7 @@ struct lcb_ctx {
     uint64_t rlc_calls = 0;
     hipStream_t aux = nullptr;        // second stream of the fused batched verify (randomisation beside preparation)
     hipStream_t hi = nullptr;         // high-priority stream: the latency-bound preparation chain (lcb_set_fork_mode 1)
-    hipEvent_t fork_ev[2] = {};
+    hipEvent_t fork_ev[3] = {};
     bool fork_ready = false;
     hipEvent_t msm_ev[7] = {};
     bool msm_ev_ready = false, msm_ran = false;

@@ -584,6 +584,8 @@ bool tpke_shape_ok(lcb_ctx *c, size_t n_keys, size_t n_cts, const char *what) {
 std::atomic<int> g_fork_mode{1};            // lcb_set_fork_mode: stream layout of the fused batched verify (1: measured
                                             // 104.8 vs 117.8 ms per 1M-share TPKE step, profiles/r03/ab1)
 std::atomic<uint32_t> g_coop_max{32768};    // lcb_set_coop_max: batches / levels of <= this many checks use the 9-lane kernels
+std::atomic<uint32_t> g_coop_miller_max{65536};   // lcb_set_coop_miller_max: the same for the group Miller loops only
+                                                  // (65536: level 1 too, 105.5 vs 106.1 ms, profiles/r03/ab2)
 // the exact check of n shares against prepared line sets (lines, ctok: n_cts ciphertexts) and decompressed keys
 int tpke_verify_core(lcb_ctx *c, const u32 *lines, const uint8_t *ctok, size_t n_cts, size_t n_keys, uint8_t *d_accept,
                      size_t n, const uint32_t *d_ct, const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
@@ -811,11 +813,11 @@ void rlc_checks(lcb_ctx *c, const RlcKindInfo &K, RlcWs &w, const uint8_t *desc,
         const size_t m = count - o < LCB_VERIFY_CHUNK ? count - o : LCB_VERIFY_CHUNK;
         hipEventRecord(ev[1], s);
         // small levels (below one wave per SIMD as one check per lane): nine lanes per check (k_coop.hip)
-        const bool coop = m <= g_coop_max.load();
+        const bool coop = m <= g_coop_max.load(), coop_ml = m <= g_coop_miller_max.load();
         if (K.ts)
             lcbk_ts_rlc_miller(dim3(nblk(m)), s, K.lines, desc + 16 * o, (const uint8_t *)gpts + K.rec * o, (u32)m, f,
                                gacc + o);
-        else if (coop)
+        else if (coop_ml)
             lcbk_coop_tpke_miller(s, K.lines, desc + 16 * o, (const uint8_t *)gpts + K.rec * o, (u32)m, f, gacc + o,
                                   (uint8_t *)c->rlc[15].get(m), 2);
         else
@@ -1028,6 +1030,12 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
     if (n_cts) {
         lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), sp, d_u, d_w, d_v, d_voff, (u32)n_cts, lines, ctok,
                              g_orig_cofactor | (g_line_mode << 1), nullptr);
+        if (hp && n) {                   // W's G2 check (needs only the prepared points) beside the line sets
+            hipEventRecord(c->fork_ev[2], sp);
+            hipStreamWaitEvent(c->aux, c->fork_ev[2], 0);
+            if (rlc_g2check(c, c->aux)) return -1;
+            hipEventRecord(c->fork_ev[2], c->aux);
+        }
         lcbk_lineset_fill(dim3(nblk(2 * n_cts)), sp, lines, (u32)(2 * n_cts), nullptr);
     }
     if (!launched("tpke prepare launch")) return -1;
@@ -1035,7 +1043,8 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
     c->t_n_keys = n_keys;
     c->t_gen++;
     c->t_ready = true;
-    if (n && rlc_g2check(c, sp)) return -1;      // still beside the randomisation
+    if (hp && n && n_cts) hipStreamWaitEvent(s, c->fork_ev[2], 0);
+    else if (n && rlc_g2check(c, sp)) return -1;      // still beside the randomisation
     if (n && rlc_census(c, RLC_TPKE, w, d_accept, io, sp)) return -1;
     if (hp) {
         hipEventRecord(c->fork_ev[1], sp);
@@ -1415,7 +1424,11 @@ extern "C" void lcb_set_batch_seed(const uint8_t *seed32) {
     else g_rlc_seed_set = false;
 }
 extern "C" void lcb_set_batch_census(size_t min_shares) { g_census_min.store(min_shares); }
-extern "C" void lcb_set_coop_max(uint32_t max_checks) { g_coop_max.store(max_checks); }
+extern "C" void lcb_set_coop_max(uint32_t max_checks) {
+    g_coop_max.store(max_checks);
+    g_coop_miller_max.store(max_checks);
+}
+extern "C" void lcb_set_coop_miller_max(uint32_t max_checks) { g_coop_miller_max.store(max_checks); }
 extern "C" void lcb_set_fork_mode(int mode) { g_fork_mode.store(mode == 1 ? 1 : 0); }
 // one cooperative Fp12 operation (k_coop_debug) on n values a (and b) vs the one-lane field.hpp routine: AoS in / out
 extern "C" int lcb_debug_coop_op(int op, const uint32_t *a, const uint32_t *b, size_t n, uint32_t *out, uint32_t *ref) {

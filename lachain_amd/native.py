@@ -84,6 +84,7 @@ _SIGS = {
     "lcb_set_batch_census": (None, [c_size]),
     "lcb_set_coop_max": (None, [ctypes.c_uint32]),
     "lcb_set_fork_mode": (None, [ctypes.c_int]),
+    "lcb_set_coop_miller_max": (None, [ctypes.c_uint32]),
     "lcb_debug_coop_op": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                                          c_size, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
     "lcb_debug_final_exp": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), c_size, ctypes.POINTER(ctypes.c_uint32),
@@ -721,6 +722,11 @@ def set_batch_census(min_shares):
 def set_coop_max(max_checks):
     """levels of <= max_checks group checks use the nine-lane cooperative kernels (0 = never; default 32768)"""
     lib().lcb_set_coop_max(max_checks)
+
+
+def set_coop_miller_max(max_checks):
+    """levels of <= max_checks group checks run their Miller loops on the cooperative kernels"""
+    lib().lcb_set_coop_miller_max(max_checks)
 
 
 def set_fork_mode(mode):
