@@ -354,68 +354,100 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_groups(const u32 *key_idx, u32 i0, u
 // handed to exact checks (gexact = 1: resolve re-emits its shares as desc.w = 1 singles).  Both check two points at
 // infinity (they pass).  desc.w = 1: the exact single check of share desc.x, e(U_i, H) e(-Y_i, W) == 1 as
 // k_tpke_miller does it (a share already rejected checks infinity).
-// first != 0 (level 1): also the weighted sums sum (j+1) s_j U_j, sum (j+1) s_j Y_j (j = position in the group) into
-// wsum (Jacobian SoA, stride n_groups) for the level-2 search.  Shares of suspect keys are skipped (they have singles of
-// their own); they keep their positions, so the weights stay c_j = j + 1.  A single re-derives the share's whole
+// Shares of suspect keys are skipped (they have singles of their own).  A single re-derives the share's whole
 // validity (census singles have had none yet): a share that is not live is rejected, and cval (census only) records
 // which shares were live.
-extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_groups, u32 first, const uint8_t *ct_ok,
+extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_groups, u32 lanes, const uint8_t *ct_ok,
                                                     const uint8_t *ct_g2, const g1a_st *keys, u32 n_keys,
                                                     const u32 *dec_idx, const uint8_t *ui, const u32 *rU,
                                                     const u32 *rY, u32 n, g1a_st *gpts, uint8_t *accept,
                                                     uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval) {
-    // two lanes per group: side 0 sums the U records (and handles singles / invalid ciphertexts), side 1 the Y records
-    u32 t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= 2 * n_groups) return;
-    const u32 g = t >> 1, side = t & 1;
-    uint4 dsc = desc[g];
-    g1a_st o;
-    g1_inf_st(o);
-    if (dsc.w == 1) {                    // exact single of share dsc.x of ciphertext dsc.z
-        if (side) return;
-        gexact[g] = 0;
-        g1a U, Y;
-        U.inf = Y.inf = true;
-        u32 d = dec_idx[dsc.x];
-        bool live = accept[dsc.x] != 0 && d < n_keys && ct_ok[dsc.z];
-        if (live) {
-            g1a_st ks = keys[d];
-            live = ks.ok && g1_decompress(U, ui + 48 * (size_t)dsc.x);
-            st_to_g1a(Y, ks);
-        }
-        if (!live) accept[dsc.x] = 0;
-        if (cval) cval[dsc.x] = live;
-        if (live && !U.inf) { o.x = U.x; o.y = U.y; o.inf = 0; }
-        gpts[2 * (size_t)g] = o;
+    // lanes = 4 (latency-bound levels): four lanes per group, t = 4g + 2 half + side — side 0 sums the U records,
+    // side 1 the Y records, each half half of the group's shares; half 1's partial sum reaches half 0 through LDS (one
+    // addition), so the serial chain is ~len/2 additions + one inversion.  lanes = 1 (levels of many entries, e.g.
+    // every share a single when every key is suspect): one lane per group does both sides.  Singles and invalid
+    // ciphertexts are handled by the group's first lane.  (wsum: unused — TPKE forms its weighted sums at level 2.)
+    __shared__ g1 part[LCB_BLOCK];
+    const u32 t = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool four = lanes == 4;
+    const bool in = t < (four ? 4 * n_groups : n_groups);
+    const u32 g = four ? t >> 2 : t, side = four ? t & 1 : 0, half = four ? (t >> 1) & 1 : 0;
+    const bool lead = in && !side && !half;
+    bool work = false;
+    g1 su[2];
+    jac_set_inf(su[0]);
+    jac_set_inf(su[1]);
+    if (in) {
+        const uint4 dsc = desc[g];
+        g1a_st o;
         g1_inf_st(o);
-        if (live && !Y.inf) { o.x = Y.x; fp_neg(o.y, Y.y); o.inf = 0; }
-        gpts[2 * (size_t)g + 1] = o;
-        return;
-    }
-    const bool cok = ct_ok[dsc.z];
-    if (!cok || !ct_g2[dsc.z]) {
-        gpts[2 * (size_t)g + side] = o;
-        if (side) return;
-        gexact[g] = cok ? 1 : 0;
-        if (!cok)
-            for (u32 j = 0; j < dsc.y; j++) accept[dsc.x + j] = 0;
-        return;
-    }
-    if (!side) gexact[g] = 0;
-    const u32 *rec = side ? rY : rU;
-    g1 su, tp, wu;
-    jac_set_inf(su);
-    jac_set_inf(wu);
-    for (u32 j = dsc.y; j-- > 0;) {      // last to first: su = suffix sums, wu = sum of the suffix sums (TS-style
-        if (!key_suspect(susp, dec_idx[dsc.x + j], n_keys)) {      // weighted sum, only when wsum is given)
-            g1_load_soa(tp, rec, n, dsc.x + j);
-            grp_add(su, su, tp);
+        if (dsc.w == 1) {                // exact single of share dsc.x of ciphertext dsc.z
+            if (lead) {
+                gexact[g] = 0;
+                g1a U, Y;
+                U.inf = Y.inf = true;
+                u32 d = dec_idx[dsc.x];
+                bool live = accept[dsc.x] != 0 && d < n_keys && ct_ok[dsc.z];
+                if (live) {
+                    g1a_st ks = keys[d];
+                    live = ks.ok && g1_decompress(U, ui + 48 * (size_t)dsc.x);
+                    st_to_g1a(Y, ks);
+                }
+                if (!live) accept[dsc.x] = 0;
+                if (cval) cval[dsc.x] = live;
+                if (live && !U.inf) { o.x = U.x; o.y = U.y; o.inf = 0; }
+                gpts[2 * (size_t)g] = o;
+                g1_inf_st(o);
+                if (live && !Y.inf) { o.x = Y.x; fp_neg(o.y, Y.y); o.inf = 0; }
+                gpts[2 * (size_t)g + 1] = o;
+            }
+        } else {
+            const bool cok = ct_ok[dsc.z];
+            if (!cok || !ct_g2[dsc.z]) {
+                if (!half) {
+                    gpts[2 * (size_t)g + side] = o;
+                    if (!four) gpts[2 * (size_t)g + 1] = o;
+                }
+                if (lead) {
+                    gexact[g] = cok ? 1 : 0;
+                    if (!cok)
+                        for (u32 j = 0; j < dsc.y; j++) accept[dsc.x + j] = 0;
+                }
+            } else {
+                if (lead) gexact[g] = 0;
+                work = true;
+                const u32 mid = four ? dsc.y / 2 : 0, j0 = half ? mid : 0, j1 = (four && !half) ? mid : dsc.y;
+                g1 tp;
+                for (u32 j = j0; j < j1; j++) {
+                    if (key_suspect(susp, dec_idx[dsc.x + j], n_keys)) continue;
+                    g1_load_soa(tp, side ? rY : rU, n, dsc.x + j);
+                    grp_add(su[0], su[0], tp);
+                    if (!four) {
+                        g1_load_soa(tp, rY, n, dsc.x + j);
+                        grp_add(su[1], su[1], tp);
+                    }
+                }
+            }
         }
-        if (first && wsum) grp_add(wu, wu, su);
     }
-    if (first && wsum) g1_store_soa(wsum, 2 * (size_t)n_groups, 2 * (size_t)g + side, wu);
-    g1_to_st(o, su, side != 0);
-    gpts[2 * (size_t)g + side] = o;
+    if (four) {
+        if (half) part[threadIdx.x] = su[0];
+        __syncthreads();
+        if (half) work = false;
+        else {
+            g1 other = part[threadIdx.x + 2];
+            if (work) grp_add(su[0], su[0], other);
+        }
+    }
+    if (work) {
+        g1a_st o;
+        g1_to_st(o, su[0], side != 0);
+        gpts[2 * (size_t)g + side] = o;
+        if (!four) {
+            g1_to_st(o, su[1], true);
+            gpts[2 * (size_t)g + 1] = o;
+        }
+    }
 }
 
 // the weighted sums of the level-1 groups listed in sdesc (.w = level-1 group index) as affine records
@@ -776,6 +808,13 @@ DN void gt_pow_small(fp12 &r, const fp12 &a, u32 e) {
     }
     r = t;
 }
+DI u32 fp12_fingerprint(const fp12 &a) {
+    const u32 *w = (const u32 *)&a;
+    u32 h = 0;
+#pragma unroll
+    for (int q = 0; q < 144; q++) h = ((h << 5) | (h >> 27)) ^ w[q];
+    return h;
+}
 DI u32 half_ballot(bool p) {
     const unsigned long long m = __ballot(p);
     return (u32)(m >> (32 * ((threadIdx.x >> 5) & 1)));
@@ -820,7 +859,7 @@ extern "C" __global__ void __launch_bounds__(64) k_tpke_rlc_search2b(const uint4
     const uint4 d = live ? search[g] : make_uint4(0, 0, 0, 0);
     const bool cand = live && j < d.y && accept[d.x + j] && !key_suspect(susp, key_idx[d.x + j], n_keys);
     const u32 cj = j + 1;
-    fp12 a, b, D, E;
+    fp12 a, b, D;
     fp12_load_row(a, gamma0 + (size_t)g * 144);
     gt_pow_small(b, a, cj);
     fp12_conj(b, b);
@@ -830,12 +869,35 @@ extern "C" __global__ void __launch_bounds__(64) k_tpke_rlc_search2b(const uint4
     fp12_conj(b, b);
     fp12_load_row(a, gamma12 + ((size_t)ns + g) * 144);    // gamma_t
     fp12_cyc_sqr_n(a, a);
-    fp12_mul_n(E, a, b);                                   // E_j = gamma_t^2 / gamma_c^(c_j + 1) = gamma_2 / gamma_c^(c_j)
+    fp12_mul_n(a, a, b);                                   // E_j = gamma_t^2 / gamma_c^(c_j + 1) = gamma_2 / gamma_c^(c_j)
+    // E_j = D_j^c for some c in [1, len] (len <= 32): baby-step giant-step with m = 6 — 32-bit fingerprints of the
+    // baby values D^k (k = 1..6), giant steps Y_i = E D^(-6 i) (D is unitary: D^-6 = conj(D^6)), a fingerprint match
+    // confirmed by the full comparison E == D^c: 10 products instead of up to len
     u32 found = 0;
-    a = D;
-    for (u32 c = 1; cand && c <= d.y; c++) {
-        if (c != cj && fp12_words_eq(a, E)) { found = c; break; }
-        if (c < d.y) fp12_mul_n(a, a, D);
+    if (cand) {
+        u32 fpb[6];
+        fpb[0] = fp12_fingerprint(D);
+        b = D;
+#pragma unroll
+        for (int k = 1; k < 6; k++) {
+            fp12_mul_n(b, b, D);
+            fpb[k] = fp12_fingerprint(b);
+        }
+        fp12_conj(b, b);                                   // D^-6
+        fp12 E = a;                                        // Y_0
+        for (int i = 0; i < 6 && !found; i++) {
+            const u32 h = fp12_fingerprint(a);
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+                const u32 c = 6 * i + k + 1;
+                if (!found && h == fpb[k] && c <= d.y && c != cj) {
+                    fp12 chk;
+                    gt_pow_small(chk, D, c);
+                    if (fp12_words_eq(chk, E)) found = c;
+                }
+            }
+            if (i < 5) fp12_mul_n(a, a, b);
+        }
     }
     const u32 m2 = half_ballot(found != 0);
     const u32 m3 = half_ballot(found != 0 && !((m2 >> (found - 1)) & 1u));
@@ -940,12 +1002,12 @@ extern "C" void lcbk_rlc_groups(hipStream_t s, const u32 *key_idx, u32 i0, u32 n
     dim3 grid((n - i0 + LCB_BLOCK - 1) / LCB_BLOCK);
     LCB_LAUNCH(k_rlc_groups, key_idx, i0, n, n_keys, cap, (uint4 *)desc, count);
 }
-extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 first,
+extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 lanes,
                                   const uint8_t *ct_ok, const uint8_t *ct_g2, const void *keys, u32 n_keys,
                                   const u32 *dec_idx, const uint8_t *ui, const u32 *rU, const u32 *rY, u32 n,
                                   void *gpts, uint8_t *accept, uint8_t *gexact, u32 *wsum, const u32 *susp,
                                   uint8_t *cval) {
-    LCB_LAUNCH(k_tpke_rlc_sum, (const uint4 *)desc, n_groups, first, ct_ok, ct_g2, (const g1a_st *)keys, n_keys,
+    LCB_LAUNCH(k_tpke_rlc_sum, (const uint4 *)desc, n_groups, lanes, ct_ok, ct_g2, (const g1a_st *)keys, n_keys,
                dec_idx, ui, rU, rY, n, (g1a_st *)gpts, accept, gexact, wsum, susp, cval);
 }
 extern "C" void lcbk_tpke_rlc_wsum(dim3 grid, hipStream_t s, const void *sdesc, u32 n_s, const u32 *wsum, u32 n_l1,

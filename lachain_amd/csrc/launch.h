@@ -66,7 +66,7 @@ extern "C" void lcbk_rlc_key_tables(dim3 grid, hipStream_t s, const void *keys, 
 extern "C" void lcbk_tpke_rlc_points(hipStream_t s, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 i0, u32 n, const u32 key[10], u32 *rU, u32 *rY, uint8_t *accept, const u32 *ktab, const uint8_t *ktab_ok, const u32 *susp);
 extern "C" void lcbk_ts_rlc_points(hipStream_t s, u32 n_msgs, const void *pks, u32 n_pks, const u32 *msg_idx, const u32 *pk_idx, const uint8_t *sigs, u32 i0, u32 n, const u32 key[10], u32 *rP, u32 *rS, uint8_t *accept, void *desc, u32 *count, const u32 *ktab, const uint8_t *ktab_ok, const u32 *susp);
 extern "C" void lcbk_rlc_groups(hipStream_t s, const u32 *key_idx, u32 i0, u32 n, u32 n_keys, u32 cap, void *desc, u32 *count);
-extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 first, const uint8_t *ct_ok, const uint8_t *ct_g2, const void *keys, u32 n_keys, const u32 *dec_idx, const uint8_t *ui, const u32 *rU, const u32 *rY, u32 n, void *gpts, uint8_t *accept, uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval);
+extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 lanes, const uint8_t *ct_ok, const uint8_t *ct_g2, const void *keys, u32 n_keys, const u32 *dec_idx, const uint8_t *ui, const u32 *rU, const u32 *rY, u32 n, void *gpts, uint8_t *accept, uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval);
 extern "C" void lcbk_tpke_rlc_wsum(dim3 grid, hipStream_t s, const void *sdesc, u32 n_s, const u32 *wsum, u32 n_l1, void *gpts);
 extern "C" void lcbk_tpke_ct_g2check(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, uint8_t *ct_g2);
 extern "C" void lcbk_tpke_rlc_miller(dim3 grid, hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups, u32 *f_soa, uint8_t *gacc);

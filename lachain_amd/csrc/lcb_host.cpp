@@ -799,7 +799,9 @@ void rlc_sum_enqueue(const RlcKindInfo &K, RlcWs &w, const uint8_t *desc, u32 gr
         lcbk_ts_rlc_sum(dim3(nblk(groups)), s, desc, groups, first, K.okv, K.keys, (u32)K.n_keys, io.d_key, io.d_pts,
                         w.rA, w.rB, (u32)n, gpts, d_accept, gex, wsum, susp, cval);
     else
-        lcbk_tpke_rlc_sum(dim3(nblk(2 * (size_t)groups)), s, desc, groups, first, K.okv, K.ctg2, K.keys, (u32)K.n_keys, io.d_key,
+        // four lanes per group while the level is latency-bound, one when it is large (e.g. all singles)
+        lcbk_tpke_rlc_sum(dim3(nblk((groups <= 262144 ? 4 : 1) * (size_t)groups)), s, desc, groups,
+                          groups <= 262144 ? 4u : 1u, K.okv, K.ctg2, K.keys, (u32)K.n_keys, io.d_key,
                           io.d_pts, w.rA, w.rB, (u32)n, gpts, d_accept, gex, wsum, susp, cval);
 }
 // Miller + final exponentiation (+ resolve / search) over the groups of desc in chunks; gpts holds the points
