@@ -46,7 +46,7 @@ BUDGET = {
     "k_rlc_miller_fallback": (0, 2376),
     "k_rlc_search": (93, 2264),
     "k_tpke_rlc_search2a": (92, 2264),         # level-2 searches: three Fp12 values per lane, one lane per group
-    "k_tpke_rlc_search2b": (102, 4024),
+    "k_tpke_rlc_search2b": (133, 4088),
     "k_secp_scalars": (0, 528),
     "k_tpke_ct_g2check": (0, 1048),
     "k_tpke_ct_prepare": (0, 3736),
