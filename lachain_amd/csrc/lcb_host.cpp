@@ -758,12 +758,13 @@ bool read_counts(u32 *v, const u32 *d, int k, hipStream_t s) {
     return true;
 }
 // W of every prepared ciphertext in G2 -> rlc[8]
-int rlc_g2check(lcb_ctx *c, hipStream_t s) {
-    uint8_t *ctg2 = (uint8_t *)c->rlc[8].get(c->t_n_cts);
+// (n_cts: the ciphertexts just prepared — the fused call runs this before it records the prepared shape)
+int rlc_g2check(lcb_ctx *c, size_t n_cts, hipStream_t s) {
+    uint8_t *ctg2 = (uint8_t *)c->rlc[8].get(n_cts);
     if (!ctg2) { set_err("device allocation failed"); return -1; }
-    if (c->t_n_cts)
-        lcbk_tpke_ct_g2check(dim3(nblk(c->t_n_cts)), s, (const u32 *)c->t_lines.p, (const uint8_t *)c->t_ctok.p,
-                             (u32)c->t_n_cts, ctg2);
+    if (n_cts)
+        lcbk_tpke_ct_g2check(dim3(nblk(n_cts)), s, (const u32 *)c->t_lines.p, (const uint8_t *)c->t_ctok.p,
+                             (u32)n_cts, ctg2);
     return 0;
 }
 struct RlcIo {                     // the per-share inputs the exact singles re-read
@@ -979,7 +980,7 @@ int tpke_verify_prepared_rlc(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_k
     RlcWs w;
     const RlcIo io{d_dec, d_ui, d_ct};
     if (!rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G1_JAC_BYTES, n_keys, census_size(n, n_keys), s)) return -1;
-    if (rlc_g2check(c, s)) return -1;
+    if (rlc_g2check(c, c->t_n_cts, s)) return -1;
     if (rlc_census(c, RLC_TPKE, w, d_accept, io, s)) return -1;   // before the randomisation: suspects skip it
     if (rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, s)) return -1;
     return rlc_levels(c, RLC_TPKE, w, d_accept, n, io, s);
@@ -1035,7 +1036,7 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
         if (hp && n) {                   // W's G2 check (needs only the prepared points) beside the line sets
             hipEventRecord(c->fork_ev[2], sp);
             hipStreamWaitEvent(c->aux, c->fork_ev[2], 0);
-            if (rlc_g2check(c, c->aux)) return -1;
+            if (rlc_g2check(c, n_cts, c->aux)) return -1;
             hipEventRecord(c->fork_ev[2], c->aux);
         }
         lcbk_lineset_fill(dim3(nblk(2 * n_cts)), sp, lines, (u32)(2 * n_cts), nullptr);
@@ -1046,7 +1047,7 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
     c->t_gen++;
     c->t_ready = true;
     if (hp && n && n_cts) hipStreamWaitEvent(s, c->fork_ev[2], 0);
-    else if (n && rlc_g2check(c, sp)) return -1;      // still beside the randomisation
+    else if (n && rlc_g2check(c, n_cts, sp)) return -1;      // still beside the randomisation
     if (n && rlc_census(c, RLC_TPKE, w, d_accept, io, sp)) return -1;
     if (hp) {
         hipEventRecord(c->fork_ev[1], sp);

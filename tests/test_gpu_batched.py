@@ -312,6 +312,32 @@ def test_batched_w_outside_g2(nat, tdev, fused):
     assert [int(x) for x in exact] == expect
 
 
+def test_batched_fused_g2check_after_smaller_batch(nat, tdev):
+    """the fused call checks W of every ciphertext it has just prepared, whatever the previous call's shape: a batch of
+    5 good ciphertexts, then 1, then 5 whose last W carries G2 cofactor torsion — that ciphertext's shares still get
+    their exact decisions (regression: the check once used the previous call's ciphertext count)"""
+    big = Batch(b"gpu-batched-g2check-seq", 6, 1, 5)
+    small = Batch(b"gpu-batched-g2check-seq1", 6, 1, 1)
+    for b in (big, small):
+        ct = np.repeat(np.arange(b.c, dtype=np.uint32), 6)
+        dec = np.tile(np.arange(6, dtype=np.uint32), b.c)
+        shares = [b.good[c][j] for c, j in zip(ct, dec)]
+        assert run_dev(nat, tdev, b, ct, dec, shares, fused=True).tolist() == [1] * len(shares)
+    b = Batch(b"gpu-batched-g2check-seq2", 6, 1, 5)
+    q = off_subgroup_g2(b.d)
+    t2 = o.g2_add(o.g2_mul(q, o.fr(R - 1)), q)
+    u, v, w = b.cts[4]
+    b.cts[4] = (u, v, o.g2_add(w, t2))
+    ct = np.repeat(np.arange(5, dtype=np.uint32), 6)
+    dec = np.tile(np.arange(6, dtype=np.uint32), 5)
+    shares = [b.good[c][j] for c, j in zip(ct, dec)]
+    shares[24 + 1] = b.bad[4][1]
+    shares[24 + 3] = o.g1_add(b.good[4][3], torsion_g1(b.d))
+    expect = [int(b.expect(c, j, s)) for c, j, s in zip(ct, dec, shares)]
+    got = run_dev(nat, tdev, b, ct, dec, shares, fused=True)
+    assert got.tolist() == expect
+
+
 @pytest.mark.parametrize("fused", [False, True])
 def test_batched_small_order_key(nat, tdev, fused):
     """a verification key of order 3 ((0, -2) is on y^2 = x^3 + 4): its fixed-base table meets the point at infinity
