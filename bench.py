@@ -1420,7 +1420,7 @@ def run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, dd, n, n_cts, n_d
         p["ctx"].close()
     if K == 1:
         levels = levels[0]
-    ms_points, ms_groups, ms_sum, ms_miller, ms_fe, ms_resolve = ms
+    ms_points, ms_groups, ms_sum, ms_miller, ms_fe, ms_prep = ms
     t = shard.max_time_sum(dist, torch, dev, elapsed, mism, n)
     elapsed = t[0]
     checks = sum(sum(lv) for lv in levels) if K > 1 else sum(levels)
@@ -1440,7 +1440,8 @@ def run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, dd, n, n_cts, n_d
         concurrent_parts=K,
         levels=levels, group_checks_per_share=checks / n,
         device_ms={"randomise_and_group (beside prepare)": ms_points, "all_levels": ms_groups, "group_sums": ms_sum,
-                   "k_tpke_rlc_miller": ms_miller, "k_final_exp_check": ms_fe, "resolve_and_count_reads": ms_resolve},
+                   "k_tpke_rlc_miller": ms_miller, "k_final_exp_check": ms_fe,
+                   "prepare_chain (fused, beside the randomisation)": ms_prep},
         roofline={"bound": "valu_int32",
                   "kernel": ("whole batched step: k_tpke_rlc_points + k_tpke_ct_prepare / k_lineset_fill + "
                              "k_tpke_rlc_miller / k_final_exp_check over all levels"),

@@ -289,7 +289,8 @@ int lcb_ts_verify_shares_batched(uint8_t *accept, size_t n, const uint8_t *pks, 
    lcb_ctx_ form: the last one of that context): groups checked per level
    (levels[0] = level 1, levels[1] = the level-2 weighted re-checks of failed groups, then single checks) and device
    ms of [randomisation + grouping, all levels, then summed over the levels: group sums, group Miller loops, final
-   exponentiations (+ resolve / search), 0]; returns the number of levels (waits for the call) */
+   exponentiations (+ resolve / search), the fused call's preparation chain (hashing, line sets and census on the
+   preparation stream, beside the randomisation; 0 for other calls)]; returns the number of levels (waits for the call) */
 int lcb_tpke_batched_stats(uint32_t levels[8], float ms[6]);
 /* test hook: fixed 32-byte ChaCha20 key for the batch exponents (NULL restores getrandom).  Honoured only when the
    environment has LCB_ALLOW_FIXED_BATCH_SEED=1 (a fixed key makes the exponents predictable); ignored otherwise. */
@@ -312,7 +313,8 @@ void lcb_set_coop_miller_max(uint32_t max_checks);
 /* stream layout of the fused batched verifies (lcb_tpke_verify_shares_batched_dev, lcb_ts_verify_shares_batched_dev):
    0 = randomisation on the context's second stream beside the preparation on the caller's; 1 (default) = the
    latency-bound preparation chain (hash-to-G2, line sets, census) on a high-priority stream and the randomisation on
-   the caller's.  Decisions are unchanged. */
+   the caller's; 2 = as 1 with the preparation's first kernel enqueued ahead of the randomisation.  Decisions are
+   unchanged. */
 void lcb_set_fork_mode(int mode);
 /* test hook: final exponentiation of n Fp12 values (144 x u32 each, Montgomery form, field.hpp layout) by the one-lane
    (coop = 0) or the cooperative (coop = 1) kernel */

@@ -5,7 +5,7 @@
 // e(., .) is a reduced pairing, so the ratio g_i = e(U_i, H) / e(Y_i, W) lies in mu_r (order r, prime) whatever
 // U_i is: for a G2 point Q the (ate) pairing is linear in its G1 argument on all of E(Fp) (Weil reciprocity; the
 // error term is an r-th power, killed by the final exponentiation) and kills the cofactor-torsion part, so off-
-// subgroup U_i / Y_i are covered.  H is in G2 by construction; W is checked (k_tpke_ct_g2check) and a ciphertext with
+// subgroup U_i / Y_i are covered.  H is in G2 by construction; W is checked (k_lineset_fill, lineset_in_g2) and a ciphertext with
 // W outside G2 gets exact per-share checks.  For secret random exponents s_i (2^64 values, none 0 mod r; rlc_scalar):
 // prod_i g_i^(s_i) == 1  <=>  e(sum s_i U_i, H) e(-sum s_i Y_i, W) == 1, and if some g_i != 1 the product is 1 with
 // probability <= 2^-64.  So one Miller pair + final exponentiation decides a whole group of shares of one ciphertext;
@@ -25,7 +25,7 @@
 //                       s_i Y_i with s_i = a_i + b_i lambda (32-bit GLV form, rlc_scalar) -> quad-major SoA Jacobian
 //                       records (invalid share: infinity)
 //   k_rlc_groups        one lane per 256 consecutive shares: runs of equal ciphertext index (<= 32) -> level-1 groups
-//   k_tpke_ct_g2check   one lane per ciphertext: W in G2 (else its shares get exact per-share checks)
+//   k_lineset_fill      (k_tpke.hip) W's line set also decides W in G2 (else its shares get exact per-share checks)
 //   k_tpke_rlc_sum      one lane per group: ciphertext validity, the two sums, to affine with one shared inversion,
 //                       -sum s_i Y_i (or an exact single share's own U_i, -Y_i)
 //   k_tpke_rlc_miller   one lane per group: the two-pair Miller loop over the ciphertext's line sets
@@ -494,17 +494,6 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum2(const uint4 *sdesc, u32 n
     g1a_st o;
     g1_to_st(o, which ? va : wa, side != 0);
     gpts[2 * ((size_t)(which ? ns : 0) + g) + side] = o;
-}
-
-// W of every ciphertext in G2 (Scott's psi test, curve.hpp g2_in_subgroup); H = hash-to-G2 output is in G2 by
-// construction
-extern "C" __global__ void LCB_BOUNDS k_tpke_ct_g2check(const u32 *lines, const uint8_t *ct_ok, u32 n_cts,
-                                                       uint8_t *ct_g2) {
-    u32 c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n_cts) return;
-    g2a W;
-    lineset_point(W, lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS);
-    ct_g2[c] = ct_ok[c] ? g2_in_subgroup(W) : 0;
 }
 
 // ---------------------------------------------------------------- TPKE group Miller loops (k_tpke_miller's loop)
@@ -1013,10 +1002,6 @@ extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u3
 extern "C" void lcbk_tpke_rlc_wsum(dim3 grid, hipStream_t s, const void *sdesc, u32 n_s, const u32 *wsum, u32 n_l1,
                                    void *gpts) {
     LCB_LAUNCH(k_tpke_rlc_wsum, (const uint4 *)sdesc, n_s, wsum, n_l1, (g1a_st *)gpts);
-}
-extern "C" void lcbk_tpke_ct_g2check(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts,
-                                     uint8_t *ct_g2) {
-    LCB_LAUNCH(k_tpke_ct_g2check, lines, ct_ok, n_cts, ct_g2);
 }
 extern "C" void lcbk_tpke_rlc_miller(dim3 grid, hipStream_t s, const u32 *lines, const void *desc, const void *gpts,
                                      u32 n_groups, u32 *f_soa, uint8_t *gacc) {

@@ -60,16 +60,19 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_ct_prepare(const uint8_t *cts_u, co
 }
 
 // line sets of points stored by a prepare kernel (lineset_put_point): one lane per set; sets (nullable) lists the
-// set indices to fill (the prepared-ciphertext cache fills scattered slots)
-extern "C" __global__ void LCB_BOUNDS k_lineset_fill(u32 *lines, u32 n_sets, const u32 *sets) {
+// set indices to fill (the prepared-ciphertext cache fills scattered slots).  w_g2 (nullable, with sets == nullptr):
+// the batched check's W-in-G2 flags, w_g2[c] for set 2c + 1 (W of ciphertext c) from the loop's last point
+// (lineset_in_g2): the membership test costs no ladder of its own.
+extern "C" __global__ void LCB_BOUNDS k_lineset_fill(u32 *lines, u32 n_sets, const u32 *sets, uint8_t *w_g2) {
     u32 k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_sets) return;
     u32 *ls = lines + (size_t)(sets ? sets[k] : k) * LCB_LINESET_WORDS;
     g2a Q;
     lineset_get_point(Q, ls);
     u32 force_general = ls[LCB_LS_FLAG + 2];
-    lineset_compute(ls, Q);
+    u32 r = lineset_compute(ls, Q);
     if (force_general) ls[LCB_LS_FLAG] = 0;
+    if (w_g2 && (k & 1)) w_g2[k >> 1] = (r & LCB_LS_IN_G2) ? 1 : 0;
 }
 
 // Exact per-share check, two kernels: the Miller loop parks f in HBM (SoA, 576 B/share) and k_final_exp_check finishes;
@@ -158,8 +161,8 @@ extern "C" void lcbk_g2_decompress(dim3 grid, hipStream_t s, const uint8_t *in, 
 extern "C" void lcbk_tpke_ct_prepare(dim3 grid, hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data, const u32 *v_off, u32 n_cts, u32 *lines, uint8_t *ct_ok, int orig_cof, const u32 *slot) {
     LCB_LAUNCH(k_tpke_ct_prepare, cts_u, cts_w, v_data, v_off, n_cts, lines, ct_ok, orig_cof, slot);
 }
-extern "C" void lcbk_lineset_fill(dim3 grid, hipStream_t s, u32 *lines, u32 n_sets, const u32 *sets) {
-    LCB_LAUNCH(k_lineset_fill, lines, n_sets, sets);
+extern "C" void lcbk_lineset_fill(dim3 grid, hipStream_t s, u32 *lines, u32 n_sets, const u32 *sets, uint8_t *w_g2) {
+    LCB_LAUNCH(k_lineset_fill, lines, n_sets, sets, w_g2);
 }
 extern "C" void lcbk_tpke_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, u32 *f_soa, uint8_t *accept) {
     LCB_LAUNCH(k_tpke_miller, lines, ct_ok, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, f_soa, accept);

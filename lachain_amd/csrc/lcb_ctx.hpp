@@ -73,7 +73,7 @@ struct lcb_ctx {
     hipEvent_t rlc_ev[3] = {};
     hipEvent_t rlc_lev_ev[4] = {};    // per level: before sum / Miller / final exp / resolve
     float rlc_ms[4] = {};             // accumulated over the levels of the last call: sums, Miller, final exp (+ resolve
-                                      // / search), unused
+                                      // / search), the fused call's preparation chain (0 for other calls)
     bool rlc_ev_ready = false, rlc_ran = false;
     uint32_t rlc_levels[8] = {};
     uint32_t rlc_census[4] = {};      // census shares, suspect keys, level-1 groups before / entries after the split
@@ -81,7 +81,9 @@ struct lcb_ctx {
     uint64_t rlc_calls = 0;
     hipStream_t aux = nullptr;        // second stream of the fused batched verify (randomisation beside preparation)
     hipStream_t hi = nullptr;         // high-priority stream: the latency-bound preparation chain (lcb_set_fork_mode 1)
-    hipEvent_t fork_ev[3] = {};
+    hipEvent_t fork_ev[2] = {};
+    hipEvent_t prep_ev[3] = {};       // timed: the fused call's preparation chain (stats ms[5]); [2] after the hashing
+    bool prep_timed = false;
     bool fork_ready = false;
     hipEvent_t msm_ev[7] = {};
     bool msm_ev_ready = false, msm_ran = false;

@@ -482,6 +482,7 @@ void ctx_free(lcb_ctx *c) {
     if (c->fork_ready) {
         (void)hipStreamSynchronize(c->aux);
         for (auto &e : c->fork_ev) (void)hipEventDestroy(e);
+        for (auto &e : c->prep_ev) (void)hipEventDestroy(e);
         (void)hipStreamDestroy(c->aux);
         (void)hipStreamSynchronize(c->hi);
         (void)hipStreamDestroy(c->hi);
@@ -559,12 +560,13 @@ int tpke_prepare(lcb_ctx *c, const uint8_t *d_y, size_t n_keys, const uint8_t *d
     u32 *lines = (u32 *)c->t_lines.get((size_t)n_cts * 2 * LCB_LINESET_BYTES);
     uint8_t *ctok = (uint8_t *)c->t_ctok.get(n_cts);
     void *keys = c->t_keys.get(n_keys * LCB_G1A_ST_BYTES);
-    if (!lines || !ctok || !keys) { set_err("device allocation failed"); return -1; }
+    uint8_t *ctg2 = (uint8_t *)c->rlc[8].get(n_cts);     // W in G2 (the batched check's flags), from the line sets
+    if (!lines || !ctok || !keys || !ctg2) { set_err("device allocation failed"); return -1; }
     if (n_keys) lcbk_g1_decompress(dim3(nblk(n_keys)), s, d_y, (u32)n_keys, keys);
     if (n_cts) {
         lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), s, d_u, d_w, d_v, d_voff, (u32)n_cts, lines, ctok,
                              g_orig_cofactor | (g_line_mode << 1), nullptr);
-        lcbk_lineset_fill(dim3(nblk(2 * n_cts)), s, lines, (u32)(2 * n_cts), nullptr);
+        lcbk_lineset_fill(dim3(nblk(2 * n_cts)), s, lines, (u32)(2 * n_cts), nullptr, ctg2);
     }
     if (!launched("tpke prepare launch")) return -1;
     c->t_n_cts = n_cts;
@@ -704,6 +706,7 @@ bool rlc_ws(lcb_ctx *c, RlcWs &w, size_t n, size_t rec_a, size_t rec_b, size_t n
     hipMemsetAsync(w.cnt, 0, 32, s);
     if (m) hipMemsetAsync(w.susp, 0, 4 * sw, s);
     c->rlc_census[0] = m;
+    c->prep_timed = false;
     c->rlc_census[1] = c->rlc_census[2] = c->rlc_census[3] = 0;
     return true;
 }
@@ -756,16 +759,6 @@ bool read_counts(u32 *v, const u32 *d, int k, hipStream_t s) {
         return false;
     }
     return true;
-}
-// W of every prepared ciphertext in G2 -> rlc[8]
-// (n_cts: the ciphertexts just prepared — the fused call runs this before it records the prepared shape)
-int rlc_g2check(lcb_ctx *c, size_t n_cts, hipStream_t s) {
-    uint8_t *ctg2 = (uint8_t *)c->rlc[8].get(n_cts);
-    if (!ctg2) { set_err("device allocation failed"); return -1; }
-    if (n_cts)
-        lcbk_tpke_ct_g2check(dim3(nblk(n_cts)), s, (const u32 *)c->t_lines.p, (const uint8_t *)c->t_ctok.p,
-                             (u32)n_cts, ctg2);
-    return 0;
 }
 struct RlcIo {                     // the per-share inputs the exact singles re-read
     const uint32_t *d_key;         // dec_idx (TPKE) / pk_idx (TS)
@@ -963,6 +956,14 @@ int rlc_levels(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, size_t n, 
     // the calling thread's copy of the statistics (lcb_tpke_batched_stats without a context)
     RlcStats &st = t_rlc_stats;
     st.valid = hipEventSynchronize(c->rlc_ev[2]) == hipSuccess;
+    if (st.valid && c->prep_timed && hipEventElapsedTime(&c->rlc_ms[3], c->prep_ev[0], c->prep_ev[1]) != hipSuccess)
+        c->rlc_ms[3] = -1.0f;
+    if (st.valid && c->prep_timed && getenv("LCB_PREP_TRACE")) {       // diagnostics: hashing / line sets + census
+        float a = -1.0f, b = -1.0f;
+        hipEventElapsedTime(&a, c->prep_ev[0], c->prep_ev[2]);
+        hipEventElapsedTime(&b, c->prep_ev[2], c->prep_ev[1]);
+        fprintf(stderr, "prep_trace hash %.2f lines+census %.2f ms\n", a, b);
+    }
     st.nlev = c->rlc_nlev;
     for (int i = 0; i < 8; i++) st.levels[i] = i < c->rlc_nlev ? c->rlc_levels[i] : 0;
     for (int i = 0; i < 2; i++)
@@ -980,7 +981,6 @@ int tpke_verify_prepared_rlc(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_k
     RlcWs w;
     const RlcIo io{d_dec, d_ui, d_ct};
     if (!rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G1_JAC_BYTES, n_keys, census_size(n, n_keys), s)) return -1;
-    if (rlc_g2check(c, c->t_n_cts, s)) return -1;
     if (rlc_census(c, RLC_TPKE, w, d_accept, io, s)) return -1;   // before the randomisation: suspects skip it
     if (rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, s)) return -1;
     return rlc_levels(c, RLC_TPKE, w, d_accept, n, io, s);
@@ -993,6 +993,8 @@ bool fork_ready(lcb_ctx *c) {
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->hi, hipStreamNonBlocking, greatest);
     for (auto &ev : c->fork_ev)
         if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    for (auto &ev : c->prep_ev)
+        if (e == hipSuccess) e = hipEventCreate(&ev);
     if (e != hipSuccess) { set_err("batched verify: stream creation", e); return false; }
     c->fork_ready = true;
     return true;
@@ -1010,7 +1012,8 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
     u32 *lines = (u32 *)c->t_lines.get((size_t)n_cts * 2 * LCB_LINESET_BYTES);
     uint8_t *ctok = (uint8_t *)c->t_ctok.get(n_cts);
     void *keys = c->t_keys.get(n_keys * LCB_G1A_ST_BYTES);
-    if (!lines || !ctok || !keys) { set_err("device allocation failed"); return -1; }
+    uint8_t *ctg2 = (uint8_t *)c->rlc[8].get(n_cts);     // W in G2, from the line sets (k_lineset_fill)
+    if (!lines || !ctok || !keys || !ctg2) { set_err("device allocation failed"); return -1; }
     if (!fork_ready(c)) return -1;
     if (n_keys) lcbk_g1_decompress(dim3(nblk(n_keys)), s, d_y, (u32)n_keys, keys);
     RlcWs w;
@@ -1018,38 +1021,37 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
     // mode 0: randomisation on the second stream, preparation + census on the caller's; mode 1: the latency-bound
     // preparation chain (one lane per ciphertext / line set, < 1.5 waves per SIMD) on a high-priority stream, so
     // its waves are dispatched ahead of the randomisation's 16 K waves, which run on the caller's stream
-    const bool hp = g_fork_mode.load() == 1;
+    const int fm = g_fork_mode.load();
+    const bool hp = fm >= 1, prep_first = fm == 2 && n_cts;
     hipStream_t sr = hp ? s : c->aux, sp = hp ? c->hi : s;
     if (n) {
         if (!rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G1_JAC_BYTES, n_keys, census_size(n, n_keys), s)) return -1;
         hipEventRecord(c->fork_ev[0], s);
         hipStreamWaitEvent(hp ? sp : sr, c->fork_ev[0], 0);
-        if (rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, sr)) return -1;
+        if (hp) hipEventRecord(c->prep_ev[0], sp);
+        if (!prep_first && rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, sr)) return -1;
         if (!hp) hipEventRecord(c->fork_ev[1], sr);
     } else if (hp) {
         hipEventRecord(c->fork_ev[0], s);
         hipStreamWaitEvent(sp, c->fork_ev[0], 0);
+        hipEventRecord(c->prep_ev[0], sp);
     }
     if (n_cts) {
         lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), sp, d_u, d_w, d_v, d_voff, (u32)n_cts, lines, ctok,
                              g_orig_cofactor | (g_line_mode << 1), nullptr);
-        if (hp && n) {                   // W's G2 check (needs only the prepared points) beside the line sets
-            hipEventRecord(c->fork_ev[2], sp);
-            hipStreamWaitEvent(c->aux, c->fork_ev[2], 0);
-            if (rlc_g2check(c, n_cts, c->aux)) return -1;
-            hipEventRecord(c->fork_ev[2], c->aux);
-        }
-        lcbk_lineset_fill(dim3(nblk(2 * n_cts)), sp, lines, (u32)(2 * n_cts), nullptr);
+        if (hp) hipEventRecord(c->prep_ev[2], sp);
+        if (prep_first && n && rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, sr)) return -1;
+        lcbk_lineset_fill(dim3(nblk(2 * n_cts)), sp, lines, (u32)(2 * n_cts), nullptr, ctg2);
     }
     if (!launched("tpke prepare launch")) return -1;
     c->t_n_cts = n_cts;
     c->t_n_keys = n_keys;
     c->t_gen++;
     c->t_ready = true;
-    if (hp && n && n_cts) hipStreamWaitEvent(s, c->fork_ev[2], 0);
-    else if (n && rlc_g2check(c, n_cts, sp)) return -1;      // still beside the randomisation
     if (n && rlc_census(c, RLC_TPKE, w, d_accept, io, sp)) return -1;
     if (hp) {
+        hipEventRecord(c->prep_ev[1], sp);
+        c->prep_timed = true;
         hipEventRecord(c->fork_ev[1], sp);
         hipStreamWaitEvent(s, c->fork_ev[1], 0);
     } else if (n) {
@@ -1140,18 +1142,20 @@ int ts_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const ui
     if (n_pks) lcbk_g1_decompress(dim3(nblk(n_pks)), s, d_pks, (u32)n_pks, keys);
     RlcWs w;
     const RlcIo io{d_pidx, d_sigs, d_midx};
-    // stream layout as in tpke_verify_shares_rlc_fused (lcb_set_fork_mode)
-    const bool hp = g_fork_mode.load() == 1;
+    // stream layout as in tpke_verify_shares_rlc_fused (lcb_set_fork_mode; 2 acts as 1 here)
+    const bool hp = g_fork_mode.load() >= 1;
     hipStream_t sr = hp ? s : c->aux, sp = hp ? c->hi : s;
     if (n) {
         if (!rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G2_JAC_BYTES, n_pks, census_size(n, n_pks), s)) return -1;
         hipEventRecord(c->fork_ev[0], s);
         hipStreamWaitEvent(hp ? sp : sr, c->fork_ev[0], 0);
+        if (hp) hipEventRecord(c->prep_ev[0], sp);
         if (ts_rlc_points_enqueue(c, w, d_accept, n, n_pks, n_msgs, d_sigs, d_midx, d_pidx, sr)) return -1;
         if (!hp) hipEventRecord(c->fork_ev[1], sr);
     } else if (hp) {
         hipEventRecord(c->fork_ev[0], s);
         hipStreamWaitEvent(sp, c->fork_ev[0], 0);
+        hipEventRecord(c->prep_ev[0], sp);
     }
     if (n_msgs) lcbk_ts_msg_prepare(dim3(nblk(n_msgs)), sp, d_msg, d_moff, (u32)n_msgs, lines, mok,
                                     g_orig_cofactor | (g_line_mode << 1));
@@ -1162,6 +1166,8 @@ int ts_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const ui
     c->s_ready = true;
     if (n && rlc_census(c, RLC_TS, w, d_accept, io, sp)) return -1;
     if (hp) {
+        hipEventRecord(c->prep_ev[1], sp);
+        c->prep_timed = true;
         hipEventRecord(c->fork_ev[1], sp);
         hipStreamWaitEvent(s, c->fork_ev[1], 0);
     } else if (n) {
@@ -1432,7 +1438,7 @@ extern "C" void lcb_set_coop_max(uint32_t max_checks) {
     g_coop_miller_max.store(max_checks);
 }
 extern "C" void lcb_set_coop_miller_max(uint32_t max_checks) { g_coop_miller_max.store(max_checks); }
-extern "C" void lcb_set_fork_mode(int mode) { g_fork_mode.store(mode == 1 ? 1 : 0); }
+extern "C" void lcb_set_fork_mode(int mode) { g_fork_mode.store(mode == 1 || mode == 2 ? mode : 0); }
 // one cooperative Fp12 operation (k_coop_debug) on n values a (and b) vs the one-lane field.hpp routine: AoS in / out
 extern "C" int lcb_debug_coop_op(int op, const uint32_t *a, const uint32_t *b, size_t n, uint32_t *out, uint32_t *ref) {
     SYNC_CTX_OR(c, -1)
@@ -1633,7 +1639,7 @@ extern "C" int lcb_tpke_verify_shares_cached(uint8_t *accept, size_t n, const ui
         const uint32_t *dse = up(c->sel[1], msets.data(), 2 * m, s);
         if (!du || !dw || !dv || !dvo || !dsl || !dse) { set_err("device allocation failed"); return -1; }
         lcbk_tpke_ct_prepare(dim3(nblk(m)), s, du, dw, dv, dvo, (u32)m, lines, ctok, flags, dsl);
-        lcbk_lineset_fill(dim3(nblk(2 * m)), s, lines, (u32)(2 * m), dse);
+        lcbk_lineset_fill(dim3(nblk(2 * m)), s, lines, (u32)(2 * m), dse, nullptr);
     }
     std::vector<u32> cslot(n);
     for (size_t i = 0; i < n; i++) cslot[i] = slot_of[ct_idx[i]];
@@ -2225,7 +2231,7 @@ extern "C" void mclBn_pairing(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) {
     hipMemcpyAsync(in, x, 144, hipMemcpyHostToDevice, s);
     if (!hit) hipMemcpyAsync(in + 36, y, 288, hipMemcpyHostToDevice, s);
     lcbk_pairing_prep(s, in, gpts, lines, desc, slot, hit ? 0 : 1);
-    if (!hit) lcbk_lineset_fill(dim3(1), s, lines + (size_t)2 * slot * (LCB_LINESET_BYTES / 4), 2, nullptr);
+    if (!hit) lcbk_lineset_fill(dim3(1), s, lines + (size_t)2 * slot * (LCB_LINESET_BYTES / 4), 2, nullptr, nullptr);
     lcbk_coop_tpke_miller(s, lines, desc, gpts, 1, park, fl, fl + 32, 1);
     lcbk_coop_final_exp_check(s, park, 1, nullptr);
     u32 r[144];

@@ -132,9 +132,30 @@ DI void fp2_load_w(fp2 &x, const u32 *src) {
     }
 }
 
+// G2 membership of Q from the Miller loop's last point: the line steps run T from Q through the bits of |z| (top bit
+// first), so T = [|z|]Q in homogeneous coordinates (x = X/Z, y = Y/Z), and Q is in G2 iff psi(Q) == [z]Q = -T
+// (Scott's test, curve.hpp g2_in_subgroup).  On a point of G2 no step is exceptional (T = +-Q or Y = 0 would need
+// (k -+ 1)Q = 0 for some k < r); off G2 an exceptional addition or doubling leaves Z = 0 for every later step, and Z = 0
+// is rejected, so the answer is g2_in_subgroup's for every on-curve Q.
+DI bool lineset_in_g2(const g2 &T, const g2a &Q) {
+    if (fp2_is_zero(T.z)) return false;
+    g2 P, S;
+    jac_from_aff(P, Q);
+    g2_psi(S, P);                                     // psi(Q), affine (Z stays 1)
+    fp2 t, ny;
+    fp2_mul(t, S.x, T.z);
+    bool okx = fp2_eq(t, T.x);
+    fp2_mul(t, S.y, T.z);
+    fp2_neg(ny, T.y);
+    return okx && fp2_eq(t, ny);
+}
+
+#define LCB_LS_NORMALISED 1u                          // lineset_compute result bits
+#define LCB_LS_IN_G2 2u
 // the 68 lines of a G2 point (affine, possibly infinity) into dst[LCB_LINESET_WORDS], normalised to A = 1 with
-// one Fp2 inversion (Montgomery's batch trick over the 68 A's).  Returns false (flag 0) iff some A_k == 0.
-DN bool lineset_compute(u32 *dst, const g2a &Q) {
+// one Fp2 inversion (Montgomery's batch trick over the 68 A's).  Returns LCB_LS_NORMALISED unless some A_k == 0
+// (flag 0), | LCB_LS_IN_G2 when Q lies in G2 (lineset_in_g2; infinity does).
+DN u32 lineset_compute(u32 *dst, const g2a &Q) {
     fp2_store_w(dst + LCB_LS_POINT, Q.x);
     fp2_store_w(dst + LCB_LS_POINT + 24, Q.y);
     dst[LCB_LS_FLAG + 1] = Q.inf ? 1 : 0;
@@ -145,7 +166,7 @@ DN bool lineset_compute(u32 *dst, const g2a &Q) {
             fp2_store_w(dst + k * LCB_NLINE_WORDS + 24, z);
         }
         dst[LCB_LS_FLAG] = 1;
-        return true;
+        return LCB_LS_NORMALISED | LCB_LS_IN_G2;
     }
     g2 T;
     T.x = Q.x; T.y = Q.y; T.z = fp2_one();
@@ -165,9 +186,10 @@ DN bool lineset_compute(u32 *dst, const g2a &Q) {
             k++;
         }
     }
+    const u32 g2m = lineset_in_g2(T, Q) ? LCB_LS_IN_G2 : 0u;
     bool ok = !fp2_is_zero(acc);
     dst[LCB_LS_FLAG] = ok;
-    if (!ok) return false;
+    if (!ok) return g2m;
     fp2 inv;
     fp2_inv_n(inv, acc);                               // (A_0 ... A_67)^-1
     for (k = LCB_NLINES - 1; k >= 0; k--) {
@@ -188,7 +210,7 @@ DN bool lineset_compute(u32 *dst, const g2a &Q) {
         fp2_store_w(dst + k * LCB_NLINE_WORDS, b);
         fp2_store_w(dst + k * LCB_NLINE_WORDS + 24, c);
     }
-    return true;
+    return LCB_LS_NORMALISED | g2m;
 }
 
 // f *= l evaluated at P = (xP, yP)

@@ -149,6 +149,7 @@ def test_batched_malicious_kinds_tiled(nat, tdev):
         got = run_dev(nat, tdev, b, ct, dec, b"".join(base) * reps, fused=fused)
         assert np.array_equal(got, np.tile(expect, reps))
         levels, ms = nat.tpke_batched_stats()
+        assert (ms[5] > 0) == fused          # the fused call times its preparation chain (fork mode 1, the default)
         # 65,536 shares get a census (the first 512 shares checked one by one); decryptor 0's share is wrong in two of
         # the four rows, so the census marks key 0 suspect and its shares become exact singles at level 1
         m, n_susp, groups, entries = nat.batched_census()
@@ -289,7 +290,7 @@ def off_subgroup_g2(d):
 def test_batched_w_outside_g2(nat, tdev, fused):
     """a ciphertext whose W carries a G2 cofactor-torsion component (on the curve, so G2.FromBytes accepts it; the
     pairing is not linear in the G1 argument against such a W): its shares must get their exact per-share decisions
-    (k_tpke_ct_g2check -> exact singles), equal to the oracle's and to the exact GPU path; the other ciphertexts'
+    (k_lineset_fill's W-in-G2 flags -> exact singles), equal to the oracle's and to the exact GPU path; the other ciphertexts'
     groups are unaffected"""
     b = Batch(b"gpu-batched-w-torsion", 8, 2, 3)
     q = off_subgroup_g2(b.d)
@@ -336,6 +337,58 @@ def test_batched_fused_g2check_after_smaller_batch(nat, tdev):
     expect = [int(b.expect(c, j, s)) for c, j, s in zip(ct, dec, shares)]
     got = run_dev(nat, tdev, b, ct, dec, shares, fused=True)
     assert got.tolist() == expect
+
+
+G2_COFACTOR = 0x5D543A95414E7F1091D50792876A202CD91DE4547085ABAA68A205B2E5A7DDFA628F1CB4D9E82EF21537E293A6691AE1616EC6E786F0C70CF1C38E31C7238E5
+
+
+def g2_mul_int(q, k):
+    """[k] q for any non-negative integer k (double-and-add over the oracle's G2 addition)"""
+    acc = None
+    for bit in bin(k)[2:]:
+        if acc is not None:
+            acc = o.g2_add(acc, acc)
+        if bit == "1":
+            acc = q if acc is None else o.g2_add(acc, q)
+    return acc
+
+
+def order13_g2(d):
+    """a point of order 13 on E'(Fp2) (13^2 divides the G2 cofactor): [#E' / 169] of a random point, until nonzero"""
+    n = G2_COFACTOR * R
+    while True:
+        t = g2_mul_int(off_subgroup_g2(d), n // 169)
+        if t != bytes(96):
+            assert g2_mul_int(t, 13) == bytes(96)
+            return t
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_batched_w_small_order(nat, tdev, fused):
+    """W of order 13, and W with an order-13 component: the G2 membership test now comes from W's line set
+    (pairing.hpp lineset_in_g2: T = [|z|]W from the Miller loop's steps), and for a point of order 13 the loop's
+    steps are exceptional (T = -W after the prefix 12 of |z|), which must read as "not in G2" (Z = 0) — both
+    ciphertexts' shares get their exact decisions, equal to the oracle's and to the exact GPU path"""
+    b = Batch(b"gpu-batched-w-order13", 8, 2, 3)
+    t13 = order13_g2(b.d)
+    assert o.g2_valid(t13) and not o.g2_in_subgroup(t13)
+    u, v, w = b.cts[1]
+    b.cts[1] = (u, v, t13)
+    u, v, w = b.cts[2]
+    w2 = o.g2_add(w, t13)
+    assert o.g2_valid(w2) and not o.g2_in_subgroup(w2)
+    b.cts[2] = (u, v, w2)
+    ct = np.repeat(np.arange(3, dtype=np.uint32), 8)
+    dec = np.tile(np.arange(8, dtype=np.uint32), 3)
+    shares = [b.good[c][j] for c, j in zip(ct, dec)]
+    shares[8 + 3] = b.bad[1][3]
+    shares[16 + 5] = b.bad[2][5]
+    shares[2] = b.bad[0][2]
+    expect = [int(b.expect(c, j, s)) for c, j, s in zip(ct, dec, shares)]
+    got = run_dev(nat, tdev, b, ct, dec, shares, fused=fused)
+    assert got.tolist() == expect
+    exact = nat.tpke_verify_shares(b.yi, b.cts, [(int(c), int(j), s) for c, j, s in zip(ct, dec, shares)])
+    assert [int(x) for x in exact] == expect
 
 
 @pytest.mark.parametrize("fused", [False, True])

@@ -48,7 +48,6 @@ BUDGET = {
     "k_tpke_rlc_search2a": (92, 2264),         # level-2 searches: three Fp12 values per lane, one lane per group
     "k_tpke_rlc_search2b": (133, 4088),
     "k_secp_scalars": (0, 528),
-    "k_tpke_ct_g2check": (0, 1048),
     "k_tpke_ct_prepare": (0, 3736),
     "k_tpke_encrypt1": (0, 6432),
     "k_tpke_encrypt2": (0, 3912),
