@@ -313,8 +313,9 @@ void lcb_set_coop_miller_max(uint32_t max_checks);
 /* stream layout of the fused batched verifies (lcb_tpke_verify_shares_batched_dev, lcb_ts_verify_shares_batched_dev):
    0 = randomisation on the context's second stream beside the preparation on the caller's; 1 (default) = the
    latency-bound preparation chain (hash-to-G2, line sets, census) on a high-priority stream and the randomisation on
-   the caller's; 2 = as 1 with the preparation's first kernel enqueued ahead of the randomisation.  Decisions are
-   unchanged. */
+   the caller's; 2 = as 1 with the preparation's first kernel enqueued ahead of the randomisation; 3 (default) = as 2
+   with the TPKE preparation split into hash + H's line set and U / W decoding + W's line set, on two high-priority
+   streams (threshold signatures: as 1).  Decisions are unchanged. */
 void lcb_set_fork_mode(int mode);
 /* test hook: final exponentiation of n Fp12 values (144 x u32 each, Montgomery form, field.hpp layout) by the one-lane
    (coop = 0) or the cooperative (coop = 1) kernel */

@@ -32,292 +32,9 @@
 //   k_final_exp_check   (k_tpke.hip) group decision
 //   k_rlc_resolve       one lane per group: failed single share -> reject; failed group -> sub-groups of the next level
 #include "kcommon.hpp"
+#include "rlc_common.hpp"
 
 LCB_ASM_LIBRARY(k_batch)
-
-struct rlc_key { u32 k[8]; u32 nonce[2]; };   // ChaCha20 key (256 bit, from getrandom) and a per-call nonce
-
-#define LCB_RLC_SINGLES 8       // a failed group this short (below level 1) splits into single shares
-
-// ---------------------------------------------------------------- suspect keys (Byzantine validators)
-// A faulty validator corrupts its share in EVERY ciphertext / coin (HoneyBadgerMalicious.cs:17-23 reverses each
-// share it sends; HoneyBadgerSmartMalicious.cs:28-48 sends valid off-subgroup points), so with F of them every group
-// carries F bad shares and every group check fails.  The census (exact single checks of a prefix of the batch, before
-// the groups are formed) marks a key suspect when at least half of its sampled shares that decoded failed their exact
-// check; every share of a suspect key is then checked on its own and the groups are summed over the other keys only.
-// The bitmap only changes the cost: every decision is still an exact single check or a group check.
-DI bool key_suspect(const u32 *susp, u32 k, u32 n_keys) {
-    return susp && k < n_keys && ((susp[k >> 5] >> (k & 31)) & 1u);
-}
-// the same read while the census may still be writing the bitmap (k_*_rlc_points runs beside it on the other
-// stream): a stale 0 only costs a randomisation that is not used
-DI bool key_suspect_live(const u32 *susp, u32 k, u32 n_keys) {
-    if (!susp || k >= n_keys) return false;
-    return (__atomic_load_n(susp + (k >> 5), __ATOMIC_RELAXED) >> (k & 31)) & 1u;
-}
-
-// ---------------------------------------------------------------- ChaCha20 (RFC 8439 block function)
-DI u32 rotl32(u32 x, int r) { return (x << r) | (x >> (32 - r)); }
-#define CHACHA_QR(a, b, c, d)                  \
-    a += b; d ^= a; d = rotl32(d, 16);         \
-    c += d; b ^= c; b = rotl32(b, 12);         \
-    a += b; d ^= a; d = rotl32(d, 8);          \
-    c += d; b ^= c; b = rotl32(b, 7);
-// share exponent s_i = a_i + b_i lambda (lambda = z^2 - 1, phi(x, y) = (beta x, y)) from the 32-bit words a_i, b_i of
-// ChaCha20 block i: a_i P + b_i phi(P) takes 32 shared doublings.  phi acts as lambda on the r-torsion and the reduced
-// pairing kills every other component of an E(Fp) point, so e(a P + b phi(P), Q) = e(P, Q)^(a + b lambda) for ANY
-// P on the curve; the 2^64 pairs (a, b) give 2^64 distinct exponents mod r (a + b lambda < 2^160 < r), none zero
-// ((0, 0) -> (1, 0)): the soundness of a uniform 64-bit exponent.
-DI void rlc_scalar(const rlc_key &key, u32 i, u32 &a, u32 &b) {
-    u32 x[16], s[16];
-    s[0] = 0x61707865u; s[1] = 0x3320646eu; s[2] = 0x79622d32u; s[3] = 0x6b206574u;
-#pragma unroll
-    for (int j = 0; j < 8; j++) s[4 + j] = key.k[j];
-    s[12] = i; s[13] = 0; s[14] = key.nonce[0]; s[15] = key.nonce[1];
-#pragma unroll
-    for (int j = 0; j < 16; j++) x[j] = s[j];
-#pragma unroll 1
-    for (int r = 0; r < 10; r++) {
-        CHACHA_QR(x[0], x[4], x[8], x[12]);
-        CHACHA_QR(x[1], x[5], x[9], x[13]);
-        CHACHA_QR(x[2], x[6], x[10], x[14]);
-        CHACHA_QR(x[3], x[7], x[11], x[15]);
-        CHACHA_QR(x[0], x[5], x[10], x[15]);
-        CHACHA_QR(x[1], x[6], x[11], x[12]);
-        CHACHA_QR(x[2], x[7], x[8], x[13]);
-        CHACHA_QR(x[3], x[4], x[9], x[14]);
-    }
-    a = x[0] + s[0];
-    b = x[1] + s[1];
-    if ((a | b) == 0) a = 1;
-}
-
-// ---------------------------------------------------------------- quad-major SoA records (NW words, NW % 4 == 0)
-template <int NW> DI void soa_store(u32 *base, size_t n, size_t i, const void *v) {
-    const u32 *s = (const u32 *)v;
-#pragma unroll
-    for (int q = 0; q < NW / 4; q++)
-        *(uint4 *)(base + ((size_t)q * n + i) * 4) = make_uint4(s[4 * q], s[4 * q + 1], s[4 * q + 2], s[4 * q + 3]);
-}
-template <int NW> DI void soa_load(void *v, const u32 *base, size_t n, size_t i) {
-    u32 *d = (u32 *)v;
-#pragma unroll
-    for (int q = 0; q < NW / 4; q++) {
-        uint4 x = *(const uint4 *)(base + ((size_t)q * n + i) * 4);
-        d[4 * q] = x.x; d[4 * q + 1] = x.y; d[4 * q + 2] = x.z; d[4 * q + 3] = x.w;
-    }
-}
-DI void g1_store_soa(u32 *base, size_t n, size_t i, const g1 &p) { soa_store<36>(base, n, i, &p); }
-DI void g1_load_soa(g1 &p, const u32 *base, size_t n, size_t i) { soa_load<36>(&p, base, n, i); }
-DI void g2_store_soa(u32 *base, size_t n, size_t i, const g2 &p) { soa_store<72>(base, n, i, &p); }
-DI void g2_load_soa(g2 &p, const u32 *base, size_t n, size_t i) { soa_load<72>(&p, base, n, i); }
-
-// a P + b phi(P) for an affine P, phi(x, y) = (beta x, y).  Joint bits: the addend is P (1, 0), phi(P) (0, 1) or
-// P + phi(P) = (beta^2 x, -y) (1, 1; the chord through two points of equal y has slope 0 and 1 + beta + beta^2 = 0),
-// so each bit costs one mixed addition, and a wave (whose lanes' bits differ) executes 32 of them instead of 64.
-DI void g1_ab_addends(fp &bx, fp &b2x, fp &ny, const g1a &P) {
-    fp beta;
-    fp_load_const(beta, LCB_G1_BETA);
-    fp_mul(bx, P.x, beta);
-    fp_mul(b2x, bx, beta);
-    fp_neg(ny, P.y);
-}
-DN void g1_mul_ab_n(g1 &r, const g1a &P, u32 a, u32 b) {
-    g1 acc;
-    jac_set_inf(acc);
-    if (!P.inf) {
-        fp bx, b2x, ny;
-        g1_ab_addends(bx, b2x, ny, P);
-        for (int k = 31; k >= 0; k--) {
-            grp_dbl(acc, acc);
-            u32 da = (a >> k) & 1, db = (b >> k) & 1;
-            if (da | db) grp_madd(acc, acc, da ? (db ? b2x : P.x) : bx, (da & db) ? ny : P.y);
-        }
-    }
-    r = acc;
-}
-// (a + b lambda) S for S in G2: psi^2(x, y) = (beta x, -y) acts on G2 as z^2 (mod r) and psi^4(x, y) = (beta^2 x, y)
-// as z^4 = z^2 - 1 = lambda, so (a + b lambda) S = a S + b psi^4(S); the joint addend S + psi^4(S) = psi^2(S) (equal
-// y again): one mixed addition per bit as in G1
-DI void g2_ab_addends(fp2 &x4, fp2 &x2, fp2 &ny, const g2a &S) {
-    fp beta, b2;
-    fp_load_const(beta, LCB_G1_BETA);
-    fp_sqr(b2, beta);
-    fp2_mul_fp(x4, S.x, b2);
-    fp2_mul_fp(x2, S.x, beta);
-    fp2_neg(ny, S.y);
-}
-// the same with the point arithmetic inlined (no call frames: the DN form passes the accumulator through scratch at
-// every doubling / addition)
-DI void g1_mul_ab_inl(g1 &r, const g1a &P, u32 a, u32 b) {
-    jac_set_inf(r);
-    if (P.inf) return;
-    fp bx, b2x, ny;
-    g1_ab_addends(bx, b2x, ny, P);
-#pragma unroll 1
-    for (int k = 31; k >= 0; k--) {
-        jac_dbl(r, r);
-        u32 da = (a >> k) & 1, db = (b >> k) & 1;
-        if (da | db) jac_add_aff(r, r, da ? (db ? b2x : P.x) : bx, (da & db) ? ny : P.y);
-    }
-}
-// G2 form of g1_mul_ab_inl: a S + b psi^4(S) with the point arithmetic inlined
-DI void g2_mul_ab_inl(g2 &r, const g2a &S, u32 a, u32 b) {
-    jac_set_inf(r);
-    if (S.inf) return;
-    fp2 x4, x2, ny;
-    g2_ab_addends(x4, x2, ny, S);
-#pragma unroll 1
-    for (int k = 31; k >= 0; k--) {
-        jac_dbl(r, r);
-        u32 da = (a >> k) & 1, db = (b >> k) & 1;
-        if (da | db) jac_add_aff(r, r, da ? (db ? x2 : S.x) : x4, (da & db) ? ny : S.y);
-    }
-}
-// affine records of Jacobian points (inf = 1 for the point at infinity), optionally negated
-DI void g1_to_st(g1a_st &o, const g1 &p, bool neg) {
-    g1a a;
-    jac_to_aff(a, p);
-    o.ok = 1; o.pad[0] = o.pad[1] = 0;
-    o.inf = a.inf;
-    o.x = a.x;
-    if (neg && !a.inf) fp_neg(o.y, a.y);
-    else o.y = a.y;
-}
-DI void g2_to_st(g2a_st &o, const g2 &p) {
-    g2a a;
-    jac_to_aff(a, p);
-    o.ok = 1; o.pad[0] = o.pad[1] = 0;
-    o.inf = a.inf;
-    o.x = a.x;
-    o.y = a.y;
-}
-DI void g1_inf_st(g1a_st &o) { o.ok = 1; o.pad[0] = o.pad[1] = 0; o.inf = 1; o.x = fp_zero(); o.y = fp_zero(); }
-DI void g2_inf_st(g2a_st &o) { o.ok = 1; o.pad[0] = o.pad[1] = 0; o.inf = 1; o.x = fp2_zero(); o.y = fp2_zero(); }
-
-// ---------------------------------------------------------------- fixed-base tables of the validators' keys
-// The keys (TPKE verification keys Y_d, threshold-signature public keys PK_k) are the same for every ciphertext /
-// coin of a batch: per key, table[w][d - 1] = d 2^(8w) K (affine x, y and beta x, d = 1..255, w = 0..3) turns
-// a K + b phi(K) for 32-bit a, b into at most 8 mixed additions (4 byte digits of a, 4 of b on the phi entries) instead
-// of 32 doublings + ~32 mixed additions.  One lane per (key, window): 8w doublings, 254 additions into a
-// Jacobian scratch, then one batched inversion (Montgomery's trick) to affine.  A key whose chain meets the point at
-// infinity (a key with no r-torsion part) or that did not decompress gets ktab_ok = 0: its shares use the ladder.
-#define LCB_KTAB_ENTRIES (4 * 255)
-#define LCB_KTAB_CHUNK 32                              // entries per lane: 8 lanes per (key, window)
-#define LCB_KTAB_LANES 32                              // lanes (and flags) per key
-extern "C" __global__ void LCB_BOUNDS k_rlc_key_tables(const g1a_st *keys, u32 n_keys, u32 *jtab, u32 *pre, u32 *tab,
-                                                      uint8_t *ktab_ok) {
-    u32 t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= LCB_KTAB_LANES * n_keys) return;
-    u32 k = t / LCB_KTAB_LANES, w = (t / 8) & 3, ch = t & 7;
-    u32 d0 = ch * LCB_KTAB_CHUNK + 1, d1 = min(255u, d0 + LCB_KTAB_CHUNK - 1);   // entries d0 .. d1
-    g1a K;
-    g1a_st ks = keys[k];
-    st_to_g1a(K, ks);
-    const size_t stride = (size_t)n_keys * LCB_KTAB_ENTRIES;      // SoA over every (key, entry)
-    const size_t e0 = (size_t)k * LCB_KTAB_ENTRIES + (size_t)w * 255;
-    bool ok = ks.ok && !K.inf;
-    g1 B, acc;
-    jac_from_aff(B, K);
-#pragma unroll 1
-    for (u32 j = 0; ok && j < 8 * w; j++) jac_dbl(B, B);            // B = 2^(8w) K
-    jac_mul_u64_inl(acc, B, d0);                                   // d0 B
-    fp run = fp_one();
-#pragma unroll 1
-    for (u32 d = d0; ok && d <= d1; d++) {            // Jacobian entries and the running product of their z
-        if (jac_is_inf(acc)) { ok = false; break; }
-        g1_store_soa(jtab, stride, e0 + d - 1, acc);
-        fp_mul(run, run, acc.z);
-        soa_store<12>(pre, stride, e0 + d - 1, &run);
-        jac_add(acc, acc, B);
-    }
-    ktab_ok[t] = ok;
-    if (!ok) return;
-    fp inv, beta;
-    fp_inv(inv, run);                                  // 1 / (z_d0 ... z_d1)
-    fp_load_const(beta, LCB_G1_BETA);
-#pragma unroll 1
-    for (u32 d = d1; d >= d0; d--) {
-        g1 p;
-        g1_load_soa(p, jtab, stride, e0 + d - 1);
-        fp zi, zi2, pd;
-        if (d > d0) {
-            soa_load<12>(&pd, pre, stride, e0 + d - 2);
-            fp_mul(zi, inv, pd);                       // 1 / z_d
-            fp_mul(inv, inv, p.z);
-        } else {
-            zi = inv;
-        }
-        fp_sqr(zi2, zi);
-        fp xyb[3];                                     // x, y, beta x (phi(x, y) = (beta x, y))
-        fp_mul(xyb[0], p.x, zi2);
-        fp_mul(zi2, zi2, zi);
-        fp_mul(xyb[1], p.y, zi2);
-        fp_mul(xyb[2], xyb[0], beta);
-        soa_store<36>(tab, stride, e0 + d - 1, xyb);
-    }
-}
-// a K + b phi(K) from key k's affine table (phi(x, y) = (beta x, y) also acts on Jacobian coordinates)
-DN void g1_mul_ab_tab(g1 &r, const u32 *tab, u32 n_keys, u32 k, u32 a, u32 b) {
-    const size_t stride = (size_t)n_keys * LCB_KTAB_ENTRIES, e0 = (size_t)k * LCB_KTAB_ENTRIES;
-    g1 acc;
-    jac_set_inf(acc);
-    fp xyb[3];
-    // one digit at a time (the loads are not hoisted: eight live table points would cost 192 registers); the b digits
-    // add phi(entry) = (beta x, y), stored beside the entry
-#pragma unroll 1
-    for (u32 j = 0; j < 8; j++) {
-        u32 w = j & 3, dg = ((j < 4 ? b : a) >> (8 * w)) & 255;
-        if (!dg) continue;
-        asm volatile("" ::: "memory");
-        soa_load<36>(xyb, tab, stride, e0 + w * 255 + dg - 1);
-        grp_madd(acc, acc, j < 4 ? xyb[2] : xyb[0], xyb[1]);
-    }
-    r = acc;
-}
-DI bool ktab_usable(const uint8_t *ktab_ok, u32 k) {      // all 32 lanes of the key's table succeeded
-    if (!ktab_ok) return false;
-    const uint4 *f = (const uint4 *)(ktab_ok + (size_t)LCB_KTAB_LANES * k);
-    uint4 x = f[0], y = f[1];
-    return (x.x & x.y & x.z & x.w & y.x & y.y & y.z & y.w) == 0x01010101u;
-}
-
-// ---------------------------------------------------------------- TPKE: per-share randomisation
-// validity as k_tpke_miller except the ciphertext's (applied per group by k_tpke_rlc_sum, so this kernel needs only
-// the decompressed keys and may run beside the ciphertext preparation)
-// Shares [i0, n) (the census decides [0, i0) exactly); a share of a key the census has already marked suspect only
-// gets its validity (it is checked on its own).
-extern "C" __global__ void __launch_bounds__(LCB_BLOCK) __attribute__((amdgpu_waves_per_eu(1)))
-k_tpke_rlc_points(u32 n_cts, const g1a_st *keys, u32 n_keys, const u32 *ct_idx,
-                                                       const u32 *dec_idx, const uint8_t *ui, u32 i0, u32 n,
-                                                       rlc_key key, u32 *rU, u32 *rY, uint8_t *accept,
-                                                       const u32 *ktab, const uint8_t *ktab_ok, const u32 *susp) {
-    u32 i = i0 + blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    u32 c = ct_idx[i], d = dec_idx[i];
-    bool ok = d < n_keys && c < n_cts;
-    g1a Ui, Y;
-    ok = g1_decompress(Ui, ui + 48 * (size_t)i) && ok;
-    g1a_st ks = keys[d < n_keys ? d : 0];
-    ok = ok && ks.ok;
-    st_to_g1a(Y, ks);
-    g1 p, q;
-    if (ok && !key_suspect_live(susp, d, n_keys)) {
-        u32 a, b;
-        rlc_scalar(key, i, a, b);
-        // share side inlined (measured 144.7 vs 148.8 ms per 1M-share step with the call), key side from the key's
-        // fixed-base table (148.8 vs 159.8 ms without)
-        g1_mul_ab_inl(p, Ui, a, b);
-        if (ktab_usable(ktab_ok, d)) g1_mul_ab_tab(q, ktab, n_keys, d, a, b);
-        else g1_mul_ab_n(q, Y, a, b);
-    } else {                             // an invalid (or suspect) share contributes nothing to its group
-        jac_set_inf(p);
-        jac_set_inf(q);
-    }
-    g1_store_soa(rU, n, i, p);
-    g1_store_soa(rY, n, i, q);
-    accept[i] = ok;
-}
 
 // ---------------------------------------------------------------- level-1 groups: runs of one ciphertext / message
 // one lane per share; the first share of a run emits the run as groups of at most `cap` shares.
@@ -347,109 +64,6 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_groups(const u32 *key_idx, u32 i0, u
     }
 }
 
-// ---------------------------------------------------------------- TPKE group sums -> two affine points per group
-// gpts[2g] = sum s_i U_i, gpts[2g + 1] = -sum s_i Y_i (g1a_st records; inf = 1 for the point at infinity).
-// desc.w = 0: a randomized group.  A group of an invalid ciphertext rejects its shares; a group whose ciphertext's W
-// is outside G2 (the pairing is linear in its G1 argument only for a G2 point: W comes from the wire unchecked) is
-// handed to exact checks (gexact = 1: resolve re-emits its shares as desc.w = 1 singles).  Both check two points at
-// infinity (they pass).  desc.w = 1: the exact single check of share desc.x, e(U_i, H) e(-Y_i, W) == 1 as
-// k_tpke_miller does it (a share already rejected checks infinity).
-// Shares of suspect keys are skipped (they have singles of their own).  A single re-derives the share's whole
-// validity (census singles have had none yet): a share that is not live is rejected, and cval (census only) records
-// which shares were live.
-extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_groups, u32 lanes, const uint8_t *ct_ok,
-                                                    const uint8_t *ct_g2, const g1a_st *keys, u32 n_keys,
-                                                    const u32 *dec_idx, const uint8_t *ui, const u32 *rU,
-                                                    const u32 *rY, u32 n, g1a_st *gpts, uint8_t *accept,
-                                                    uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval) {
-    // lanes = 4 (latency-bound levels): four lanes per group, t = 4g + 2 half + side — side 0 sums the U records,
-    // side 1 the Y records, each half half of the group's shares; half 1's partial sum reaches half 0 through LDS (one
-    // addition), so the serial chain is ~len/2 additions + one inversion.  lanes = 1 (levels of many entries, e.g.
-    // every share a single when every key is suspect): one lane per group does both sides.  Singles and invalid
-    // ciphertexts are handled by the group's first lane.  (wsum: unused — TPKE forms its weighted sums at level 2.)
-    __shared__ g1 part[LCB_BLOCK];
-    const u32 t = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool four = lanes == 4;
-    const bool in = t < (four ? 4 * n_groups : n_groups);
-    const u32 g = four ? t >> 2 : t, side = four ? t & 1 : 0, half = four ? (t >> 1) & 1 : 0;
-    const bool lead = in && !side && !half;
-    bool work = false;
-    g1 su[2];
-    jac_set_inf(su[0]);
-    jac_set_inf(su[1]);
-    if (in) {
-        const uint4 dsc = desc[g];
-        g1a_st o;
-        g1_inf_st(o);
-        if (dsc.w == 1) {                // exact single of share dsc.x of ciphertext dsc.z
-            if (lead) {
-                gexact[g] = 0;
-                g1a U, Y;
-                U.inf = Y.inf = true;
-                u32 d = dec_idx[dsc.x];
-                bool live = accept[dsc.x] != 0 && d < n_keys && ct_ok[dsc.z];
-                if (live) {
-                    g1a_st ks = keys[d];
-                    live = ks.ok && g1_decompress(U, ui + 48 * (size_t)dsc.x);
-                    st_to_g1a(Y, ks);
-                }
-                if (!live) accept[dsc.x] = 0;
-                if (cval) cval[dsc.x] = live;
-                if (live && !U.inf) { o.x = U.x; o.y = U.y; o.inf = 0; }
-                gpts[2 * (size_t)g] = o;
-                g1_inf_st(o);
-                if (live && !Y.inf) { o.x = Y.x; fp_neg(o.y, Y.y); o.inf = 0; }
-                gpts[2 * (size_t)g + 1] = o;
-            }
-        } else {
-            const bool cok = ct_ok[dsc.z];
-            if (!cok || !ct_g2[dsc.z]) {
-                if (!half) {
-                    gpts[2 * (size_t)g + side] = o;
-                    if (!four) gpts[2 * (size_t)g + 1] = o;
-                }
-                if (lead) {
-                    gexact[g] = cok ? 1 : 0;
-                    if (!cok)
-                        for (u32 j = 0; j < dsc.y; j++) accept[dsc.x + j] = 0;
-                }
-            } else {
-                if (lead) gexact[g] = 0;
-                work = true;
-                const u32 mid = four ? dsc.y / 2 : 0, j0 = half ? mid : 0, j1 = (four && !half) ? mid : dsc.y;
-                g1 tp;
-                for (u32 j = j0; j < j1; j++) {
-                    if (key_suspect(susp, dec_idx[dsc.x + j], n_keys)) continue;
-                    g1_load_soa(tp, side ? rY : rU, n, dsc.x + j);
-                    grp_add(su[0], su[0], tp);
-                    if (!four) {
-                        g1_load_soa(tp, rY, n, dsc.x + j);
-                        grp_add(su[1], su[1], tp);
-                    }
-                }
-            }
-        }
-    }
-    if (four) {
-        if (half) part[threadIdx.x] = su[0];
-        __syncthreads();
-        if (half) work = false;
-        else {
-            g1 other = part[threadIdx.x + 2];
-            if (work) grp_add(su[0], su[0], other);
-        }
-    }
-    if (work) {
-        g1a_st o;
-        g1_to_st(o, su[0], side != 0);
-        gpts[2 * (size_t)g + side] = o;
-        if (!four) {
-            g1_to_st(o, su[1], true);
-            gpts[2 * (size_t)g + 1] = o;
-        }
-    }
-}
-
 // the weighted sums of the level-1 groups listed in sdesc (.w = level-1 group index) as affine records
 extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum(const uint4 *sdesc, u32 n_s, const u32 *wsum, u32 n_l1,
                                                      g1a_st *gpts) {
@@ -464,36 +78,6 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum(const uint4 *sdesc, u32 n_
     g1_load_soa(p, wsum, 2 * (size_t)n_l1, 2 * (size_t)l + 1);
     g1_to_st(o, p, true);
     gpts[2 * (size_t)g + 1] = o;
-}
-
-// Level 2 of TPKE (two-error location, see k_tpke_rlc_search2): the weighted sums of the failed level-1 groups listed
-// in sdesc, formed from the shares' randomised records: four lanes per group ((U, Y) side x (w, v) output), last share to first,
-// s = suffix sum, w = sum of the s (weights c_j = j + 1), v = sum of the w (weights t_j = c_j (c_j + 1) / 2).  Shares of
-// suspect keys keep their positions and add nothing.  gpts[2g + side] = w, gpts[2 (ns + g) + side] = v (Y side
-// negated), so checks g and ns + g give gamma_c = prod g_i^(c_i s_i) and gamma_t = prod g_i^(t_i s_i).
-extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum2(const uint4 *sdesc, u32 ns, const u32 *rU, const u32 *rY, u32 n,
-                                                      const u32 *dec_idx, u32 n_keys, const u32 *susp, g1a_st *gpts) {
-    // four lanes per group: (side, which) — each lane one output record, so one inversion (to affine) per lane
-    u32 t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= 4 * ns) return;
-    const u32 g = t >> 2, side = t & 1, which = (t >> 1) & 1;
-    const uint4 d = sdesc[g];
-    const u32 *rec = side ? rY : rU;
-    g1 sa, wa, va, p;
-    jac_set_inf(sa);
-    jac_set_inf(wa);
-    jac_set_inf(va);
-    for (u32 j = d.y; j-- > 0;) {
-        if (!key_suspect(susp, dec_idx[d.x + j], n_keys)) {
-            g1_load_soa(p, rec, n, d.x + j);
-            grp_add(sa, sa, p);
-        }
-        grp_add(wa, wa, sa);
-        if (which) grp_add(va, va, wa);
-    }
-    g1a_st o;
-    g1_to_st(o, which ? va : wa, side != 0);
-    gpts[2 * ((size_t)(which ? ns : 0) + g) + side] = o;
 }
 
 // ---------------------------------------------------------------- TPKE group Miller loops (k_tpke_miller's loop)
@@ -952,28 +536,6 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_suspect_split(const uint4 *desc, u32
 extern "C" size_t lcbk_key_table_bytes(u32 n_keys) {
     return (size_t)n_keys * (LCB_KTAB_ENTRIES * 336 + LCB_KTAB_LANES) + 16;
 }
-extern "C" void lcbk_rlc_key_tables(dim3 grid, hipStream_t s, const void *keys, u32 n_keys, u32 *ws, u32 **tab,
-                                    uint8_t **ktab_ok) {
-    const size_t ne = (size_t)n_keys * LCB_KTAB_ENTRIES;
-    u32 *jtab = ws, *pre = ws + 36 * ne, *t = ws + 48 * ne;
-    uint8_t *okv = (uint8_t *)(ws + 84 * ne);
-    *tab = t;
-    *ktab_ok = okv;
-    grid = dim3((LCB_KTAB_LANES * n_keys + LCB_BLOCK - 1) / LCB_BLOCK);
-    LCB_LAUNCH(k_rlc_key_tables, (const g1a_st *)keys, n_keys, jtab, pre, t, okv);
-}
-extern "C" void lcbk_tpke_rlc_points(hipStream_t s, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx,
-                                     const u32 *dec_idx, const uint8_t *ui, u32 i0, u32 n, const u32 key[10], u32 *rU,
-                                     u32 *rY, uint8_t *accept, const u32 *ktab, const uint8_t *ktab_ok,
-                                     const u32 *susp) {
-    rlc_key k;
-    for (int j = 0; j < 8; j++) k.k[j] = key[j];
-    k.nonce[0] = key[8];
-    k.nonce[1] = key[9];
-    dim3 grid((n - i0 + LCB_BLOCK - 1) / LCB_BLOCK);
-    LCB_LAUNCH(k_tpke_rlc_points, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, i0, n, k, rU, rY, accept,
-               ktab, ktab_ok, susp);
-}
 extern "C" void lcbk_ts_rlc_points(hipStream_t s, u32 n_msgs, const void *pks, u32 n_pks, const u32 *msg_idx,
                                    const u32 *pk_idx, const uint8_t *sigs, u32 i0, u32 n, const u32 key[10], u32 *rP,
                                    u32 *rS, uint8_t *accept, void *desc, u32 *count, const u32 *ktab,
@@ -990,14 +552,6 @@ extern "C" void lcbk_rlc_groups(hipStream_t s, const u32 *key_idx, u32 i0, u32 n
                                 u32 *count) {
     dim3 grid((n - i0 + LCB_BLOCK - 1) / LCB_BLOCK);
     LCB_LAUNCH(k_rlc_groups, key_idx, i0, n, n_keys, cap, (uint4 *)desc, count);
-}
-extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 lanes,
-                                  const uint8_t *ct_ok, const uint8_t *ct_g2, const void *keys, u32 n_keys,
-                                  const u32 *dec_idx, const uint8_t *ui, const u32 *rU, const u32 *rY, u32 n,
-                                  void *gpts, uint8_t *accept, uint8_t *gexact, u32 *wsum, const u32 *susp,
-                                  uint8_t *cval) {
-    LCB_LAUNCH(k_tpke_rlc_sum, (const uint4 *)desc, n_groups, lanes, ct_ok, ct_g2, (const g1a_st *)keys, n_keys,
-               dec_idx, ui, rU, rY, n, (g1a_st *)gpts, accept, gexact, wsum, susp, cval);
 }
 extern "C" void lcbk_tpke_rlc_wsum(dim3 grid, hipStream_t s, const void *sdesc, u32 n_s, const u32 *wsum, u32 n_l1,
                                    void *gpts) {
@@ -1034,11 +588,6 @@ extern "C" void lcbk_rlc_search(dim3 grid, hipStream_t s, const void *search, u3
                                 u32 n_keys, const u32 *susp) {
     LCB_LAUNCH(k_rlc_search, (const uint4 *)search, o, m, gamma, park, accept, (uint4 *)next, next_count, key_idx,
                n_keys, susp);
-}
-extern "C" void lcbk_tpke_rlc_wsum2(hipStream_t s, const void *sdesc, u32 ns, const u32 *rU, const u32 *rY, u32 n,
-                                    const u32 *dec_idx, u32 n_keys, const u32 *susp, void *gpts) {
-    dim3 grid((4 * (size_t)ns + LCB_BLOCK - 1) / LCB_BLOCK);
-    LCB_LAUNCH(k_tpke_rlc_wsum2, (const uint4 *)sdesc, ns, rU, rY, n, dec_idx, n_keys, susp, (g1a_st *)gpts);
 }
 extern "C" void lcbk_rlc_park_copy(hipStream_t s, const u32 *park, u32 o, u32 m, u32 *dst) {
     dim3 grid((m + LCB_BLOCK - 1) / LCB_BLOCK);

@@ -68,8 +68,9 @@ struct lcb_ctx {
     hipEvent_t ver_ev[3] = {};
     bool ver_ev_ready = false, ver_ran = false;
     // randomized batch verification (k_batch.hip): r_i U_i / r_i Y_i records, group lists, group points, counts
-    DevBuf rlc[18];                   // [12]: the keys' fixed-base tables, [13] suspect-key bitmap, [14] census validity,
-                                      // [15] coop Miller fallback flags, [16] TPKE level-2 gamma_c / gamma_t rows, [17] its open groups
+    DevBuf rlc[19];                   // [12]: the keys' fixed-base tables, [13] suspect-key bitmap, [14] census validity,
+                                      // [15] coop Miller fallback flags, [16] TPKE level-2 gamma_c / gamma_t rows, [17] its open groups,
+                                      // [18] H's hash validity (split preparation, fork mode 3)
     hipEvent_t rlc_ev[3] = {};
     hipEvent_t rlc_lev_ev[4] = {};    // per level: before sum / Miller / final exp / resolve
     float rlc_ms[4] = {};             // accumulated over the levels of the last call: sums, Miller, final exp (+ resolve
@@ -81,7 +82,8 @@ struct lcb_ctx {
     uint64_t rlc_calls = 0;
     hipStream_t aux = nullptr;        // second stream of the fused batched verify (randomisation beside preparation)
     hipStream_t hi = nullptr;         // high-priority stream: the latency-bound preparation chain (lcb_set_fork_mode 1)
-    hipEvent_t fork_ev[2] = {};
+    hipStream_t hi2 = nullptr;        // second high-priority stream: U / W decompression + W's line sets (fork mode 3)
+    hipEvent_t fork_ev[3] = {};
     hipEvent_t prep_ev[3] = {};       // timed: the fused call's preparation chain (stats ms[5]); [2] after the hashing
     bool prep_timed = false;
     bool fork_ready = false;

@@ -486,6 +486,8 @@ void ctx_free(lcb_ctx *c) {
         (void)hipStreamDestroy(c->aux);
         (void)hipStreamSynchronize(c->hi);
         (void)hipStreamDestroy(c->hi);
+        (void)hipStreamSynchronize(c->hi2);
+        (void)hipStreamDestroy(c->hi2);
     }
     lcb_int::ecdsa_ctx_release(c);
     if (c->ver_ev_ready) for (auto &e : c->ver_ev) (void)hipEventDestroy(e);
@@ -583,8 +585,9 @@ bool tpke_shape_ok(lcb_ctx *c, size_t n_keys, size_t n_cts, const char *what) {
     }
     return true;
 }
-std::atomic<int> g_fork_mode{1};            // lcb_set_fork_mode: stream layout of the fused batched verify (1: measured
-                                            // 104.8 vs 117.8 ms per 1M-share TPKE step, profiles/r03/ab1)
+std::atomic<int> g_fork_mode{3};            // lcb_set_fork_mode: stream layout of the fused batched verify (1: measured
+                                            // 104.8 vs 117.8 ms per 1M-share TPKE step, profiles/r03/ab1; 3, the split
+                                            // preparation: 99.6 vs 103.2 ms, profiles/r03/ab8)
 std::atomic<uint32_t> g_coop_max{32768};    // lcb_set_coop_max: batches / levels of <= this many checks use the 9-lane kernels
 std::atomic<uint32_t> g_coop_miller_max{65536};   // lcb_set_coop_miller_max: the same for the group Miller loops only
                                                   // (65536: level 1 too, 105.5 vs 106.1 ms, profiles/r03/ab2)
@@ -991,6 +994,7 @@ bool fork_ready(lcb_ctx *c) {
     int least = 0, greatest = 0;
     if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->hi, hipStreamNonBlocking, greatest);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->hi2, hipStreamNonBlocking, greatest);
     for (auto &ev : c->fork_ev)
         if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     for (auto &ev : c->prep_ev)
@@ -1022,7 +1026,7 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
     // preparation chain (one lane per ciphertext / line set, < 1.5 waves per SIMD) on a high-priority stream, so
     // its waves are dispatched ahead of the randomisation's 16 K waves, which run on the caller's stream
     const int fm = g_fork_mode.load();
-    const bool hp = fm >= 1, prep_first = fm == 2 && n_cts;
+    const bool hp = fm >= 1, prep_first = fm >= 2 && n_cts, split = fm == 3;
     hipStream_t sr = hp ? s : c->aux, sp = hp ? c->hi : s;
     if (n) {
         if (!rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G1_JAC_BYTES, n_keys, census_size(n, n_keys), s)) return -1;
@@ -1036,7 +1040,22 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
         hipStreamWaitEvent(sp, c->fork_ev[0], 0);
         hipEventRecord(c->prep_ev[0], sp);
     }
-    if (n_cts) {
+    if (n_cts && split) {
+        // split preparation: hash + H's line set per lane on the preparation stream, U / W decompression + W's line
+        // set (and its G2 flag) per lane on a second high-priority stream; each lane keeps its SIMD from the hash to
+        // the last line, so no second dispatch waits behind the randomisation's waves
+        uint8_t *hok = (uint8_t *)c->rlc[18].get(n_cts);
+        if (!hok) { set_err("device allocation failed"); return -1; }
+        hipStreamWaitEvent(c->hi2, c->fork_ev[0], 0);
+        const int fl = g_orig_cofactor | (g_line_mode << 1);
+        lcbk_tpke_ct_prepare_h(dim3(nblk(n_cts)), sp, d_u, d_v, d_voff, (u32)n_cts, lines, hok, fl);
+        lcbk_tpke_ct_prepare_w(dim3(nblk(n_cts)), c->hi2, d_u, d_w, (u32)n_cts, lines, ctok, ctg2, fl);
+        hipEventRecord(c->prep_ev[2], sp);
+        if (n && rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, sr)) return -1;
+        hipEventRecord(c->fork_ev[2], c->hi2);
+        hipStreamWaitEvent(sp, c->fork_ev[2], 0);
+        lcbk_ct_ok_merge(dim3(nblk(n_cts)), sp, ctok, hok, (u32)n_cts);
+    } else if (n_cts) {
         lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), sp, d_u, d_w, d_v, d_voff, (u32)n_cts, lines, ctok,
                              g_orig_cofactor | (g_line_mode << 1), nullptr);
         if (hp) hipEventRecord(c->prep_ev[2], sp);
@@ -1438,7 +1457,7 @@ extern "C" void lcb_set_coop_max(uint32_t max_checks) {
     g_coop_miller_max.store(max_checks);
 }
 extern "C" void lcb_set_coop_miller_max(uint32_t max_checks) { g_coop_miller_max.store(max_checks); }
-extern "C" void lcb_set_fork_mode(int mode) { g_fork_mode.store(mode == 1 || mode == 2 ? mode : 0); }
+extern "C" void lcb_set_fork_mode(int mode) { g_fork_mode.store(mode >= 1 && mode <= 3 ? mode : 0); }
 // one cooperative Fp12 operation (k_coop_debug) on n values a (and b) vs the one-lane field.hpp routine: AoS in / out
 extern "C" int lcb_debug_coop_op(int op, const uint32_t *a, const uint32_t *b, size_t n, uint32_t *out, uint32_t *ref) {
     SYNC_CTX_OR(c, -1)

@@ -730,8 +730,9 @@ def set_coop_miller_max(max_checks):
 
 
 def set_fork_mode(mode):
-    """stream layout of the fused batched verify: 0 = randomisation on a second stream (default), 1 = preparation chain
-    on a high-priority stream"""
+    """stream layout of the fused batched verify (include/lachain_bls.h lcb_set_fork_mode): 0 = randomisation on a
+    second stream, 1 = preparation chain on a high-priority stream, 2 = 1 with the preparation enqueued first,
+    3 (default) = 2 with the TPKE preparation split into hash / decode lanes on two high-priority streams"""
     lib().lcb_set_fork_mode(mode)
 
 

@@ -391,6 +391,40 @@ def test_batched_w_small_order(nat, tdev, fused):
     assert [int(x) for x in exact] == expect
 
 
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_batched_fork_modes(nat, tdev, mode):
+    """every stream layout of the fused call (lcb_set_fork_mode; 3 = split preparation: hash + H's line set and
+    U / W decode + W's line set in separate lanes, validity merged afterwards) decides as the oracle: undecodable U,
+    undecodable W, W of order 13, wrong shares, 65,536 shares so the census runs"""
+    b = Batch(b"gpu-batched-fork-modes", 8, 2, 5)
+    u, v, w = b.cts[1]
+    b.cts[1] = (bytes([0x9A]) + u[1:], v, w)                # U off the curve (or non-canonical): undecodable
+    u, v, w = b.cts[2]
+    k = 0
+    while o.g2_valid(bytes([k]) + w[1:]):
+        k += 1
+    b.cts[2] = (u, v, bytes([k]) + w[1:])                   # W undecodable (x off the twist)
+    assert not o.g1_valid(b.cts[1][0]) and not o.g2_valid(b.cts[2][2])
+    u, v, w = b.cts[3]
+    b.cts[3] = (u, v, order13_g2(b.d))
+    base = [b.good[c][j] for c in range(5) for j in range(8)]
+    base[4 * 8 + 2] = b.bad[4][2]
+    base[0 * 8 + 6] = b.bad[0][6]
+    expect = [int(b.expect(i // 8, i % 8, base[i])) for i in range(40)]
+    assert expect[8:32] == [0] * 24 and sum(expect) == 14
+    reps = 1640                                               # 65,600 shares: the census runs
+    ct = np.tile(np.repeat(np.arange(5, dtype=np.uint32), 8), reps)
+    dec = np.tile(np.arange(8, dtype=np.uint32), 5 * reps)
+    try:
+        nat.set_fork_mode(mode)
+        got = run_dev(nat, tdev, b, ct, dec, b"".join(base) * reps, fused=True)
+        levels, ms = nat.tpke_batched_stats()
+    finally:
+        nat.set_fork_mode(3)
+    assert np.array_equal(got, np.tile(np.array(expect, dtype=np.uint8), reps))
+    assert (ms[5] > 0) == (mode != 0)
+
+
 @pytest.mark.parametrize("fused", [False, True])
 def test_batched_small_order_key(nat, tdev, fused):
     """a verification key of order 3 ((0, -2) is on y^2 = x^3 + 4): its fixed-base table meets the point at infinity

@@ -42,7 +42,7 @@ BUDGET = {
     "k_msm_bucket_reduce": (0, 600),
     "k_msm_horner": (0, 168),
     "k_op": (3038, 8484),                     # mcl single-element surface: every operation in one kernel
-    "k_rlc_key_tables": (12, 576),
+    "k_rlc_key_tables": (12, 768),            # k_rlc_rand.hip: spills to scratch, not AGPRs (<= 256 registers)
     "k_rlc_miller_fallback": (0, 2376),
     "k_rlc_search": (93, 2264),
     "k_tpke_rlc_search2a": (92, 2264),         # level-2 searches: three Fp12 values per lane, one lane per group
@@ -54,7 +54,7 @@ BUDGET = {
     "k_tpke_miller": (348, 2616),
     "k_tpke_partial_decrypt": (972, 7652),
     "k_tpke_rlc_miller": (360, 2616),
-    "k_tpke_rlc_points": (60, 944),
+    "k_tpke_rlc_points": (60, 1216),          # k_rlc_rand.hip: 248 registers, two waves per SIMD
     "k_tpke_rlc_sum": (0, 1328),
     "k_tpke_rlc_wsum": (0, 576),
     "k_ts_miller": (1248, 3292),
