@@ -77,7 +77,7 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_ts_miller(const u32 *lines, const u
 // signer index) of the j-th share to arrive; entries >= per_group are absent arrivals.  Null: index order.
 extern "C" __global__ void LCB_BOUNDS k_select_first_valid(const uint8_t *accept, const uint8_t *pts, u32 pbytes,
                                                           u32 per_group, u32 k, u32 n_groups, uint8_t *xs,
-                                                          uint8_t *ys, u32 *off, const u32 *order) {
+                                                          uint8_t *ys, u32 *off, const u32 *order, u32 *src_out) {
     u32 r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n_groups) return;
     off[r] = r * k;
@@ -96,6 +96,7 @@ extern "C" __global__ void LCB_BOUNDS k_select_first_valid(const uint8_t *accept
         const u32 *sw = (const u32 *)(pts + (size_t)pbytes * src);
         u32 *yw = (u32 *)(ys + (size_t)pbytes * dst);
         for (u32 q = 0; q < pw; q++) yw[q] = sw[q];
+        if (src_out) src_out[dst] = (u32)src;           // the share's index in pts (its ts_share_st record)
         cnt++;
     }
     for (; cnt < k; cnt++) {
@@ -104,6 +105,7 @@ extern "C" __global__ void LCB_BOUNDS k_select_first_valid(const uint8_t *accept
         u32 *yw = (u32 *)(ys + (size_t)pbytes * dst);
         for (int q = 0; q < 8; q++) xw[q] = 0;
         for (u32 q = 0; q < pw; q++) yw[q] = 0;
+        if (src_out) src_out[dst] = 0xffffffffu;
     }
 }
 
@@ -131,8 +133,8 @@ extern "C" void lcbk_ts_msg_prepare(dim3 grid, hipStream_t s, const uint8_t *msg
 extern "C" void lcbk_ts_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *msg_ok, u32 n_msgs, const void *pks, u32 n_pks, const uint8_t *sigs, const u32 *msg_idx, const u32 *pk_idx, u32 n, u32 *f_soa, uint8_t *accept) {
     LCB_LAUNCH(k_ts_miller, lines, msg_ok, n_msgs, (const g1a_st *)pks, n_pks, sigs, msg_idx, pk_idx, n, f_soa, accept);
 }
-extern "C" void lcbk_select_first_valid(dim3 grid, hipStream_t s, const uint8_t *accept, const uint8_t *pts, u32 pbytes, u32 per_group, u32 k, u32 n_groups, uint8_t *xs, uint8_t *ys, u32 *off, const u32 *order) {
-    LCB_LAUNCH(k_select_first_valid, accept, pts, pbytes, per_group, k, n_groups, xs, ys, off, order);
+extern "C" void lcbk_select_first_valid(dim3 grid, hipStream_t s, const uint8_t *accept, const uint8_t *pts, u32 pbytes, u32 per_group, u32 k, u32 n_groups, uint8_t *xs, uint8_t *ys, u32 *off, const u32 *order, u32 *src) {
+    LCB_LAUNCH(k_select_first_valid, accept, pts, pbytes, per_group, k, n_groups, xs, ys, off, order, src);
 }
 extern "C" void lcbk_coin_fold(dim3 grid, hipStream_t s, const uint8_t *sigs, u32 n, uint8_t *parity, uint64_t *nonce) {
     LCB_LAUNCH(k_coin_fold, sigs, n, parity, nonce);

@@ -12,6 +12,11 @@
 // affine point records in device memory
 struct g1a_st { fp x, y; u32 inf, ok, pad[2]; };   // 112 B
 struct g2a_st { fp2 x, y; u32 inf, ok, pad[2]; };  // 208 B
+// a signature share as the batched CommonCoin check decoded it (k_ts_rlc_points): its 96 wire bytes, the affine point,
+// ok = 1 for a written record and pad[0] = 1 when the point is in G2; the assembly's Lagrange lanes reuse a record
+// whose bytes equal their input (k_g2_mul_lanes) instead of decompressing and testing the share again
+struct ts_share_st { u32 raw[24]; g2a_st p; };        // 304 B
+static_assert(sizeof(ts_share_st) == 304, "ts_share_st layout (launch.h LCB_TS_SHARE_REC_BYTES)");
 DI void st_to_g1a(g1a &a, const g1a_st &s) { a.x = s.x; a.y = s.y; a.inf = s.inf != 0; }
 DI void st_to_g2a(g2a &a, const g2a_st &s) { a.x = s.x; a.y = s.y; a.inf = s.inf != 0; }
 

@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include "ops.h"
 typedef uint32_t u32;
+#define LCB_TS_SHARE_REC_BYTES 304     // ts_share_st (kcommon.hpp): a decoded CommonCoin share
 extern "C" void lcbk_g1_decompress(dim3 grid, hipStream_t s, const uint8_t *in, u32 n, void *out);
 extern "C" void lcbk_g2_decompress(dim3 grid, hipStream_t s, const uint8_t *in, u32 n, void *out);
 extern "C" void lcbk_tpke_ct_prepare(dim3 grid, hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data, const u32 *v_off, u32 n_cts, u32 *lines, uint8_t *ct_ok, int orig_cof, const u32 *slot);
@@ -19,7 +20,7 @@ extern "C" void lcbk_tpke_partial_decrypt(dim3 grid, hipStream_t s, const u32 *l
 extern "C" void lcbk_ts_msg_prepare(dim3 grid, hipStream_t s, const uint8_t *msg_data, const u32 *msg_off, u32 n_msgs, u32 *lines, uint8_t *msg_ok, int orig_cof);
 extern "C" void lcbk_ts_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *msg_ok, u32 n_msgs, const void *pks, u32 n_pks, const uint8_t *sigs, const u32 *msg_idx, const u32 *pk_idx, u32 n, u32 *f_soa, uint8_t *accept);
 extern "C" void lcbk_coin_fold(dim3 grid, hipStream_t s, const uint8_t *sigs, u32 n, uint8_t *parity, uint64_t *nonce);
-extern "C" void lcbk_select_first_valid(dim3 grid, hipStream_t s, const uint8_t *accept, const uint8_t *pts, u32 pbytes, u32 per_group, u32 k, u32 n_groups, uint8_t *xs, uint8_t *ys, u32 *off, const u32 *order);
+extern "C" void lcbk_select_first_valid(dim3 grid, hipStream_t s, const uint8_t *accept, const uint8_t *pts, u32 pbytes, u32 per_group, u32 k, u32 n_groups, uint8_t *xs, uint8_t *ys, u32 *off, const u32 *order, u32 *src);
 extern "C" void lcbk_g1_mul(dim3 grid, hipStream_t s, const uint8_t *pts, int use_gen, const uint8_t *scalars, u32 n, uint8_t *out, uint8_t *ok_out);
 extern "C" void lcbk_g2_mul(dim3 grid, hipStream_t s, const uint8_t *pts, int use_gen, const uint8_t *scalars, u32 n, uint8_t *out, uint8_t *ok_out);
 extern "C" void lcbk_g2_hash(dim3 grid, hipStream_t s, const uint8_t *msg_data, const u32 *msg_off, u32 n, uint8_t *out, uint8_t *ok_out, int orig_cof);
@@ -28,7 +29,7 @@ extern "C" void lcbk_tpke_encrypt2(dim3 grid, hipStream_t s, const uint8_t *u, c
 extern "C" void lcbk_ts_sign(dim3 grid, hipStream_t s, const uint8_t *sks, const uint8_t *msg_data, const u32 *msg_off, const u32 *msg_idx, u32 n, uint8_t *out, uint8_t *ok_out, int orig_cof);
 extern "C" void lcbk_lagrange_coeffs(dim3 grid, hipStream_t s, const uint8_t *xs, const u32 *off, u32 n_problems, void *lam_raw, uint8_t *status);
 extern "C" void lcbk_g1_mul_lanes(dim3 grid, hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out);
-extern "C" void lcbk_g2_mul_lanes(dim3 grid, hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out);
+extern "C" void lcbk_g2_mul_lanes(dim3 grid, hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out, const void *dec, u32 n_dec, const u32 *src);
 extern "C" void lcbk_g1_sum(dim3 grid, hipStream_t s, const void *parts, const uint8_t *ok_in, const u32 *off, u32 n_problems, uint8_t *status, uint8_t *out);
 extern "C" void lcbk_g2_sum(dim3 grid, hipStream_t s, const void *parts, const uint8_t *ok_in, const u32 *off, u32 n_problems, uint8_t *status, uint8_t *out);
 extern "C" void lcbk_msm_digits(dim3 grid, hipStream_t s, const uint8_t *scalars, u32 n, u32 c, u32 nwin, u32 *keys, u32 *vals);
@@ -67,7 +68,7 @@ extern "C" void lcbk_secp_sign(hipStream_t s, const uint8_t *hashes, const uint8
 extern "C" size_t lcbk_key_table_bytes(u32 n_keys);
 extern "C" void lcbk_rlc_key_tables(dim3 grid, hipStream_t s, const void *keys, u32 n_keys, u32 *ws, u32 **tab, uint8_t **ktab_ok);
 extern "C" void lcbk_tpke_rlc_points(hipStream_t s, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 i0, u32 n, const u32 key[10], u32 *rU, u32 *rY, uint8_t *accept, const u32 *ktab, const uint8_t *ktab_ok, const u32 *susp);
-extern "C" void lcbk_ts_rlc_points(hipStream_t s, u32 n_msgs, const void *pks, u32 n_pks, const u32 *msg_idx, const u32 *pk_idx, const uint8_t *sigs, u32 i0, u32 n, const u32 key[10], u32 *rP, u32 *rS, uint8_t *accept, void *desc, u32 *count, const u32 *ktab, const uint8_t *ktab_ok, const u32 *susp);
+extern "C" void lcbk_ts_rlc_points(hipStream_t s, u32 n_msgs, const void *pks, u32 n_pks, const u32 *msg_idx, const u32 *pk_idx, const uint8_t *sigs, u32 i0, u32 n, const u32 key[10], u32 *rP, u32 *rS, uint8_t *accept, void *desc, u32 *count, const u32 *ktab, const uint8_t *ktab_ok, const u32 *susp, void *dec);
 extern "C" void lcbk_rlc_groups(hipStream_t s, const u32 *key_idx, u32 i0, u32 n, u32 n_keys, u32 cap, void *desc, u32 *count);
 extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 lanes, const uint8_t *ct_ok, const uint8_t *ct_g2, const void *keys, u32 n_keys, const u32 *dec_idx, const uint8_t *ui, const u32 *rU, const u32 *rY, u32 n, void *gpts, uint8_t *accept, uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval);
 extern "C" void lcbk_tpke_rlc_wsum(dim3 grid, hipStream_t s, const void *sdesc, u32 n_s, const u32 *wsum, u32 n_l1, void *gpts);

@@ -54,11 +54,13 @@ struct lcb_ctx {
     bool t_ready = false;
     // threshold-signature workspace (lcb_*ts_prepare_dev): line sets of H(m) per message, keys
     DevBuf s_lines, s_mok, s_keys, s_f;
+    DevBuf s_dec;                     // decoded shares of the batched CommonCoin checks (ts_share_st), for the assembly
+    size_t s_dec_n = 0;
     size_t s_n_msgs = 0, s_n_pks = 0;
     uint64_t s_gen = 0;
     bool s_ready = false;
     // Lagrange / assembly / MSM / staging
-    DevBuf lag[3], sel[3], msm[12], in[8], out[4], dkg[9];
+    DevBuf lag[3], sel[4], msm[12], in[8], out[4], dkg[9];
     DevBuf mcl[8];                    // the mcl surface's pairing / multi-scalar / Horner / Lagrange staging
     // mclBn_pairing's cache of G2 line sets (mcl[2]: slot k = Q_k's set and the infinity set), least recently used
     // slot replaced: the protocol pairs every share of a ciphertext / coin with the same H, W (TPKE/PublicKey.cs:91)

@@ -749,8 +749,14 @@ int ts_rlc_points_enqueue(lcb_ctx *c, RlcWs &w, uint8_t *d_accept, size_t n, siz
     if (w.m < n) {
         uint8_t *kok = nullptr;
         u32 *ktab = rlc_key_tables(c, c->s_keys.p, n_pks, s, &kok);
+        // decoded-share records for the assembly (optional: without the buffer the assembly decodes the shares)
+        const size_t rec = n * (size_t)LCB_TS_SHARE_REC_BYTES;
+        const bool grow = c->s_dec.cap < rec;
+        void *dec = c->s_dec.get(rec);
+        if (dec && grow) hipMemsetAsync(dec, 0, c->s_dec.cap, s);   // no record is valid until written
+        c->s_dec_n = dec ? c->s_dec.cap / LCB_TS_SHARE_REC_BYTES : 0;
         lcbk_ts_rlc_points(s, (u32)n_msgs, c->s_keys.p, (u32)n_pks, d_midx, d_pidx, d_sigs, w.m, (u32)n, key, w.rA,
-                           w.rB, d_accept, w.dA, w.cnt, ktab, kok, w.susp);
+                           w.rB, d_accept, w.dA, w.cnt, ktab, kok, w.susp, dec);
         lcbk_rlc_groups(s, d_midx, w.m, (u32)n, (u32)n_msgs, 128, w.dA, w.cnt);
     }
     hipEventRecord(c->rlc_ev[1], s);
@@ -1199,7 +1205,7 @@ int ts_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const ui
 // ------------------------------------------------------------------ Lagrange / assembly
 // device-side Lagrange at 0 for np problems (entries off[j]..off[j+1]); dout = serialized results, dst = status
 int lagrange_enqueue(lcb_ctx *c, int g, uint8_t *dout, uint8_t *dst, const uint8_t *dx, const uint8_t *dy,
-                     const uint32_t *doff, size_t np, size_t ne, hipStream_t s) {
+                     const uint32_t *doff, size_t np, size_t ne, hipStream_t s, const u32 *src = nullptr) {
     if (np > 0xffffffffu || ne > 0xffffffffu) { set_err("lagrange: batch too large"); return -1; }
     void *lam = c->lag[0].get(LCB_FR_BYTES * (ne ? ne : 1));
     void *parts = c->lag[1].get((g == 1 ? LCB_G1_JAC_BYTES : LCB_G2_JAC_BYTES) * (ne ? ne : 1));
@@ -1208,7 +1214,8 @@ int lagrange_enqueue(lcb_ctx *c, int g, uint8_t *dout, uint8_t *dst, const uint8
     lcbk_lagrange_coeffs(dim3(nblk(np)), s, dx, doff, (u32)np, lam, dst);
     if (ne) {
         if (g == 1) lcbk_g1_mul_lanes(dim3(nblk(ne)), s, dy, lam, (u32)ne, parts, pok);
-        else lcbk_g2_mul_lanes(dim3(nblk(ne)), s, dy, lam, (u32)ne, parts, pok);
+        else lcbk_g2_mul_lanes(dim3(nblk(ne)), s, dy, lam, (u32)ne, parts, pok, src ? c->s_dec.p : nullptr,
+                               (u32)std::min<size_t>(c->s_dec_n, 0xffffffffu), src);
     }
     if (g == 1) lcbk_g1_sum(dim3(nblk(np)), s, parts, pok, doff, (u32)np, dst, dout);
     else lcbk_g2_sum(dim3(nblk(np)), s, parts, pok, doff, (u32)np, dst, dout);
@@ -1222,10 +1229,12 @@ int assemble_enqueue(lcb_ctx *c, int g, uint8_t *out, uint8_t *status, const uin
     if (ne > 0xffffffffu || (size_t)n_groups * per_group > 0xffffffffu) { set_err("assemble: batch too large"); return -1; }
     uint8_t *xs = (uint8_t *)c->sel[0].get(32 * ne), *ys = (uint8_t *)c->sel[1].get(pb * ne);
     u32 *off = (u32 *)c->sel[2].get(4 * (n_groups + 1));
+    // G2 (signature shares): each entry's share index, so the lanes can reuse the batched check's decoded shares
+    u32 *src = g == 2 && c->s_dec_n ? (u32 *)c->sel[3].get(4 * ne) : nullptr;
     if (!xs || !ys || !off) { set_err("device allocation failed"); return -1; }
     lcbk_select_first_valid(dim3(nblk(n_groups)), s, accept, pts, (u32)pb, (u32)per_group, (u32)k, (u32)n_groups, xs,
-                            ys, off, order);
-    return lagrange_enqueue(c, g, out, status, xs, ys, off, n_groups, ne, s);
+                            ys, off, order, src);
+    return lagrange_enqueue(c, g, out, status, xs, ys, off, n_groups, ne, s, src);
 }
 
 // ------------------------------------------------------------------ Pippenger MSM (k_msm.hip)

@@ -201,3 +201,43 @@ def test_two_bad_per_group_search_fails(nat, tdev, kind):
     # TS: the one-error search fails on the two-bad group, whose shares get single checks; TPKE: level 2 re-checks each
     # failed group twice (weights c and t) and the two-error location names both bad shares
     assert levels == ([2, 2, 12] if kind == "ts" else [2, 4])
+
+
+def test_ts_assembly_reuses_decoded_shares(nat, tdev):
+    """the assembly after a batched CommonCoin check takes each selected share's decoded point and G2 flag from the
+    check's records (ts_share_st) when the record holds the same 96 bytes, and decodes the share itself otherwise:
+    AddShare's Lagrange combination (ThresholdSigner.cs:62-75) equals the oracle's for a share with a G2
+    cofactor-torsion component (ladder, not GLS), for shares the check decoded, and for an input whose bytes differ
+    from the checked share"""
+    torch, dev = tdev
+    n, k, rounds = 7, 3, 4
+    b = Rounds(b"gpu-ts-assembly-records", n, rounds)
+    q = off_subgroup_g2(b.d)
+    t2 = o.g2_add(o.g2_mul(q, o.fr(R - 1)), q)
+    sigs = [list(row) for row in b.good]
+    sigs[0][0] = o.g2_add(sigs[0][0], t2)                  # torsion component
+    sigs[2][1] = b.bad[2][1]
+    items = [(r, i, sigs[r][i]) for r in range(rounds) for i in range(n)]
+    acc = nat.ts_verify_shares(b.pks, b.msgs, items, batched=True)
+    assert acc == [b.expect(r, i, s) for r, i, s in items]
+    assert not acc[0]                                       # the torsion share fails the check ...
+    flat = [s for row in sigs for s in row]
+    changed = list(flat)
+    changed[7 + 1] = o.g2_add(b.good[1][1], b.good[1][1])   # bytes the check never saw (accept bit kept)
+    forced = list(acc)
+    forced[0] = True                                        # ... a caller may still hand it to the assembly
+    for v, a in ((flat, acc), (changed, acc), (flat, forced)):
+        d_acc = up(torch, dev, bytes(int(x) for x in a))
+        d_sig = up(torch, dev, b"".join(v))
+        d_out = torch.zeros(96 * rounds, dtype=torch.uint8, device=dev)
+        d_st = torch.zeros(rounds, dtype=torch.uint8, device=dev)
+        sh = torch.cuda.current_stream(dev).cuda_stream
+        assert nat.lib().lcb_ts_assemble_dev(d_out.data_ptr(), d_st.data_ptr(), d_acc.data_ptr(), d_sig.data_ptr(),
+                                             n, k, rounds, sh) == 0
+        torch.cuda.synchronize(dev)
+        out = d_out.cpu().numpy().tobytes()
+        assert d_st.cpu().numpy().tolist() == [1] * rounds
+        for r in range(rounds):
+            valid = [i for i in range(n) if a[r * n + i]][:k]
+            want = o.g2_lagrange([o.fr(i + 1) for i in valid], [v[r * n + i] for i in valid])
+            assert out[96 * r:96 * r + 96] == want, (r, valid)

@@ -36,7 +36,7 @@ BUDGET = {
     "k_g2_decompress": (0, 992),
     "k_g2_hash": (0, 3336),
     "k_g2_mul": (206, 10624),
-    "k_g2_mul_lanes": (1276, 10288),
+    "k_g2_mul_lanes": (1300, 10288),
     "k_g2_sum": (204, 1008),
     "k_lineset_fill": (0, 1824),
     "k_msm_bucket_reduce": (0, 600),
@@ -60,7 +60,7 @@ BUDGET = {
     "k_ts_miller": (1248, 3292),
     "k_ts_msg_prepare": (0, 3624),
     "k_ts_rlc_miller": (0, 2524),
-    "k_ts_rlc_points": (554, 1376),
+    "k_ts_rlc_points": (554, 1568),
     "k_ts_rlc_sum": (0, 2136),
     "k_ts_rlc_wsum": (12, 992),
     "k_ts_sign": (0, 3912),
