@@ -9,9 +9,9 @@ typedef uint32_t u32;
 extern "C" void lcbk_g1_decompress(dim3 grid, hipStream_t s, const uint8_t *in, u32 n, void *out);
 extern "C" void lcbk_g2_decompress(dim3 grid, hipStream_t s, const uint8_t *in, u32 n, void *out);
 extern "C" void lcbk_tpke_ct_prepare(dim3 grid, hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data, const u32 *v_off, u32 n_cts, u32 *lines, uint8_t *ct_ok, int orig_cof, const u32 *slot);
-extern "C" void lcbk_tpke_ct_prepare_h(dim3 grid, hipStream_t s, const uint8_t *cts_u, const uint8_t *v_data, const u32 *v_off, u32 n_cts, u32 *lines, uint8_t *h_ok, int flags);
-extern "C" void lcbk_tpke_ct_prepare_w(dim3 grid, hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, u32 n_cts, u32 *lines, uint8_t *ct_ok, uint8_t *w_g2, int flags);
-extern "C" void lcbk_ct_ok_merge(dim3 grid, hipStream_t s, uint8_t *ct_ok, const uint8_t *h_ok, u32 n_cts);
+extern "C" void lcbk_tpke_ct_prepare_h(hipStream_t s, const uint8_t *cts_u, const uint8_t *v_data, const u32 *v_off, u32 c0, u32 c1, u32 *lines, uint8_t *h_ok, int flags);
+extern "C" void lcbk_tpke_ct_prepare_w(hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, u32 c0, u32 c1, u32 *lines, uint8_t *ct_ok, uint8_t *w_g2, int flags);
+extern "C" void lcbk_ct_ok_merge(hipStream_t s, uint8_t *ct_ok, const uint8_t *h_ok, u32 c0, u32 c1);
 extern "C" void lcbk_lineset_fill(dim3 grid, hipStream_t s, u32 *lines, u32 n_sets, const u32 *sets, uint8_t *w_g2);
 extern "C" void lcbk_tpke_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, u32 *f_soa, uint8_t *accept);
 extern "C" int lcbk_fe_slots();

@@ -85,7 +85,8 @@ struct lcb_ctx {
     hipStream_t aux = nullptr;        // second stream of the fused batched verify (randomisation beside preparation)
     hipStream_t hi = nullptr;         // high-priority stream: the latency-bound preparation chain (lcb_set_fork_mode 1)
     hipStream_t hi2 = nullptr;        // second high-priority stream: U / W decompression + W's line sets (fork mode 3)
-    hipEvent_t fork_ev[3] = {};
+    hipStream_t hi3 = nullptr;        // third: the bulk of the split preparation when the census ciphertexts go first
+    hipEvent_t fork_ev[5] = {};
     hipEvent_t prep_ev[3] = {};       // timed: the fused call's preparation chain (stats ms[5]); [2] after the hashing
     bool prep_timed = false;
     bool fork_ready = false;

@@ -488,6 +488,8 @@ void ctx_free(lcb_ctx *c) {
         (void)hipStreamDestroy(c->hi);
         (void)hipStreamSynchronize(c->hi2);
         (void)hipStreamDestroy(c->hi2);
+        (void)hipStreamSynchronize(c->hi3);
+        (void)hipStreamDestroy(c->hi3);
     }
     lcb_int::ecdsa_ctx_release(c);
     if (c->ver_ev_ready) for (auto &e : c->ver_ev) (void)hipEventDestroy(e);
@@ -1001,6 +1003,7 @@ bool fork_ready(lcb_ctx *c) {
     if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->hi, hipStreamNonBlocking, greatest);
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->hi2, hipStreamNonBlocking, greatest);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->hi3, hipStreamNonBlocking, greatest);
     for (auto &ev : c->fork_ev)
         if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     for (auto &ev : c->prep_ev)
@@ -1025,17 +1028,30 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
     uint8_t *ctg2 = (uint8_t *)c->rlc[8].get(n_cts);     // W in G2, from the line sets (k_lineset_fill)
     if (!lines || !ctok || !keys || !ctg2) { set_err("device allocation failed"); return -1; }
     if (!fork_ready(c)) return -1;
+    const int fm = g_fork_mode.load();
+    const bool hp = fm >= 1, prep_first = fm >= 2 && n_cts, split = fm == 3;
+    // split mode with a census: the ciphertexts of the census shares [0, m) (indices read to the host before this call
+    // launches anything; used when they all lie below a small bound c_early) are prepared first, on the preparation
+    // stream, so the census runs while the bulk is prepared
+    u32 c_early = 0;
+    const u32 m_census = n ? census_size(n, n_keys) : 0;
+    if (n_cts && split && m_census) {
+        std::vector<uint32_t> ci(m_census);
+        if (hipMemcpyAsync(ci.data(), d_ct, 4 * (size_t)m_census, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) { set_err("tpke batched verify: census index read"); return -1; }
+        u32 mx = 0;
+        for (uint32_t x : ci) mx = std::max(mx, x);
+        if ((size_t)mx + 1 < n_cts && mx < 4096u) c_early = mx + 1;
+    }
     if (n_keys) lcbk_g1_decompress(dim3(nblk(n_keys)), s, d_y, (u32)n_keys, keys);
     RlcWs w;
     const RlcIo io{d_dec, d_ui, d_ct};
     // mode 0: randomisation on the second stream, preparation + census on the caller's; mode 1: the latency-bound
     // preparation chain (one lane per ciphertext / line set, < 1.5 waves per SIMD) on a high-priority stream, so
     // its waves are dispatched ahead of the randomisation's 16 K waves, which run on the caller's stream
-    const int fm = g_fork_mode.load();
-    const bool hp = fm >= 1, prep_first = fm >= 2 && n_cts, split = fm == 3;
     hipStream_t sr = hp ? s : c->aux, sp = hp ? c->hi : s;
     if (n) {
-        if (!rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G1_JAC_BYTES, n_keys, census_size(n, n_keys), s)) return -1;
+        if (!rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G1_JAC_BYTES, n_keys, m_census, s)) return -1;
         hipEventRecord(c->fork_ev[0], s);
         hipStreamWaitEvent(hp ? sp : sr, c->fork_ev[0], 0);
         if (hp) hipEventRecord(c->prep_ev[0], sp);
@@ -1047,20 +1063,31 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
         hipEventRecord(c->prep_ev[0], sp);
     }
     if (n_cts && split) {
-        // split preparation: hash + H's line set per lane on the preparation stream, U / W decompression + W's line
-        // set (and its G2 flag) per lane on a second high-priority stream; each lane keeps its SIMD from the hash to
-        // the last line, so no second dispatch waits behind the randomisation's waves
+        // split preparation: hash + H's line set per lane, U / W decompression + W's line set (and its G2 flag) per
+        // lane, on separate high-priority streams; each lane keeps its SIMD from the hash to the last line, so no
+        // second dispatch waits behind the randomisation's waves.  With c_early: ciphertexts [0, c_early) first
+        // (point lanes, hash lanes, validity, then the census, all on the preparation stream), the rest [c_early,
+        // n_cts) beside them on the second and third streams.
         uint8_t *hok = (uint8_t *)c->rlc[18].get(n_cts);
         if (!hok) { set_err("device allocation failed"); return -1; }
-        hipStreamWaitEvent(c->hi2, c->fork_ev[0], 0);
         const int fl = g_orig_cofactor | (g_line_mode << 1);
-        lcbk_tpke_ct_prepare_h(dim3(nblk(n_cts)), sp, d_u, d_v, d_voff, (u32)n_cts, lines, hok, fl);
-        lcbk_tpke_ct_prepare_w(dim3(nblk(n_cts)), c->hi2, d_u, d_w, (u32)n_cts, lines, ctok, ctg2, fl);
-        hipEventRecord(c->prep_ev[2], sp);
+        hipStreamWaitEvent(c->hi2, c->fork_ev[0], 0);
+        hipStreamWaitEvent(c->hi3, c->fork_ev[0], 0);
+        const u32 nc = (u32)n_cts, ce = c_early;
+        if (ce) {
+            lcbk_tpke_ct_prepare_w(sp, d_u, d_w, 0u, ce, lines, ctok, ctg2, fl);
+            lcbk_tpke_ct_prepare_h(sp, d_u, d_v, d_voff, 0u, ce, lines, hok, fl);
+            lcbk_ct_ok_merge(sp, ctok, hok, 0u, ce);
+        }
+        lcbk_tpke_ct_prepare_h(c->hi2, d_u, d_v, d_voff, ce, nc, lines, hok, fl);
+        lcbk_tpke_ct_prepare_w(c->hi3, d_u, d_w, ce, nc, lines, ctok, ctg2, fl);
+        hipEventRecord(c->prep_ev[2], c->hi2);
         if (n && rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, sr)) return -1;
         hipEventRecord(c->fork_ev[2], c->hi2);
-        hipStreamWaitEvent(sp, c->fork_ev[2], 0);
-        lcbk_ct_ok_merge(dim3(nblk(n_cts)), sp, ctok, hok, (u32)n_cts);
+        hipStreamWaitEvent(c->hi3, c->fork_ev[2], 0);
+        lcbk_ct_ok_merge(c->hi3, ctok, hok, ce, nc);
+        hipEventRecord(c->fork_ev[3], c->hi3);
+        if (!ce) hipStreamWaitEvent(sp, c->fork_ev[3], 0);     // the census (below) needs every ciphertext
     } else if (n_cts) {
         lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), sp, d_u, d_w, d_v, d_voff, (u32)n_cts, lines, ctok,
                              g_orig_cofactor | (g_line_mode << 1), nullptr);
@@ -1074,6 +1101,7 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
     c->t_gen++;
     c->t_ready = true;
     if (n && rlc_census(c, RLC_TPKE, w, d_accept, io, sp)) return -1;
+    if (n_cts && split && c_early) hipStreamWaitEvent(sp, c->fork_ev[3], 0);   // the bulk's preparation
     if (hp) {
         hipEventRecord(c->prep_ev[1], sp);
         c->prep_timed = true;

@@ -425,6 +425,40 @@ def test_batched_fork_modes(nat, tdev, mode):
     assert (ms[5] > 0) == (mode != 0)
 
 
+@pytest.mark.parametrize("scatter", [False, True])
+def test_batched_census_ciphertexts_first(nat, tdev, scatter):
+    """fork mode 3 with a census: when the census shares' ciphertexts all lie below a small bound, those ciphertexts
+    are prepared first and the census runs beside the bulk's preparation (scatter=False); when a census share names a
+    late ciphertext, everything is prepared before the census (scatter=True).  2,048 ciphertext slots (five distinct
+    ciphertexts repeated, with an undecodable U and a W of order 13 among them), 16,384 shares: decisions equal the
+    oracle's"""
+    import copy
+    b = Batch(b"gpu-batched-census-first", 8, 2, 5)
+    u, v, w = b.cts[1]
+    b.cts[1] = (bytes([0x9A]) + u[1:], v, w)
+    u, v, w = b.cts[3]
+    b.cts[3] = (u, v, order13_g2(b.d))
+    base = [b.good[c][j] for c in range(5) for j in range(8)]
+    base[4 * 8 + 2] = b.bad[4][2]
+    base[0 * 8 + 6] = b.bad[0][6]
+    expect5 = [int(b.expect(i // 8, i % 8, base[i])) for i in range(40)]
+    slots = 2048
+    bb = copy.copy(b)
+    bb.cts = [b.cts[c % 5] for c in range(slots)]
+    bb.c = slots
+    ct = np.repeat(np.arange(slots, dtype=np.uint32), 8)
+    dec = np.tile(np.arange(8, dtype=np.uint32), slots)
+    if scatter:
+        ct[[0, 1]] = ct[[-1, -2]]                                # census shares 0, 1 name the last slot
+        dec[[0, 1]] = dec[[-1, -2]]
+    shares = b"".join(base[(int(c) % 5) * 8 + int(j)] for c, j in zip(ct, dec))
+    expect = np.array([expect5[(int(c) % 5) * 8 + int(j)] for c, j in zip(ct, dec)], dtype=np.uint8)
+    got = run_dev(nat, tdev, bb, ct, dec, shares, fused=True)
+    assert np.array_equal(got, expect)
+    m, n_susp, groups, entries = nat.batched_census()
+    assert m == 512
+
+
 @pytest.mark.parametrize("fused", [False, True])
 def test_batched_small_order_key(nat, tdev, fused):
     """a verification key of order 3 ((0, -2) is on y^2 = x^3 + 4): its fixed-base table meets the point at infinity
