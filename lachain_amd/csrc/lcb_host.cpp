@@ -1233,8 +1233,7 @@ int ts_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const ui
 // ------------------------------------------------------------------ Lagrange / assembly
 // device-side Lagrange at 0 for np problems (entries off[j]..off[j+1]); dout = serialized results, dst = status
 int lagrange_enqueue(lcb_ctx *c, int g, uint8_t *dout, uint8_t *dst, const uint8_t *dx, const uint8_t *dy,
-                     const uint32_t *doff, size_t np, size_t ne, hipStream_t s, const u32 *src = nullptr,
-                     bool pairs = false) {
+                     const uint32_t *doff, size_t np, size_t ne, hipStream_t s, const u32 *src = nullptr) {
     if (np > 0xffffffffu || ne > 0xffffffffu) { set_err("lagrange: batch too large"); return -1; }
     void *lam = c->lag[0].get(LCB_FR_BYTES * (ne ? ne : 1));
     void *parts = c->lag[1].get((g == 1 ? LCB_G1_JAC_BYTES : LCB_G2_JAC_BYTES) * (ne ? ne : 1));
@@ -1243,9 +1242,6 @@ int lagrange_enqueue(lcb_ctx *c, int g, uint8_t *dout, uint8_t *dst, const uint8
     lcbk_lagrange_coeffs(dim3(nblk(np)), s, dx, doff, (u32)np, lam, dst);
     if (ne) {
         if (g == 1) lcbk_g1_mul_lanes(dim3(nblk(ne)), s, dy, lam, (u32)ne, parts, pok);
-        else if (pairs)   // even problem offsets (assembly with even k): two entries per lane, shared doublings
-            lcbk_g2_mul2_lanes(s, dy, lam, (u32)ne, parts, pok, src ? c->s_dec.p : nullptr,
-                               (u32)std::min<size_t>(c->s_dec_n, 0xffffffffu), src);
         else lcbk_g2_mul_lanes(dim3(nblk(ne)), s, dy, lam, (u32)ne, parts, pok, src ? c->s_dec.p : nullptr,
                                (u32)std::min<size_t>(c->s_dec_n, 0xffffffffu), src);
     }
@@ -1266,7 +1262,7 @@ int assemble_enqueue(lcb_ctx *c, int g, uint8_t *out, uint8_t *status, const uin
     if (!xs || !ys || !off) { set_err("device allocation failed"); return -1; }
     lcbk_select_first_valid(dim3(nblk(n_groups)), s, accept, pts, (u32)pb, (u32)per_group, (u32)k, (u32)n_groups, xs,
                             ys, off, order, src);
-    return lagrange_enqueue(c, g, out, status, xs, ys, off, n_groups, ne, s, src, g == 2 && k % 2 == 0);
+    return lagrange_enqueue(c, g, out, status, xs, ys, off, n_groups, ne, s, src);
 }
 
 // ------------------------------------------------------------------ Pippenger MSM (k_msm.hip)
