@@ -7,22 +7,29 @@ MclBls12381.EvaluatePolynomial, ...) so the parity tests read like test/Lachain.
 Failures raise (the reference's wrapper throws on a failed FromBytes / interpolation).
 """
 import ctypes
+import threading
 
 from . import native
 from .native import mclBnFr, mclBnG1, mclBnG2, mclBnGT
 
 _FN = {}
+_FN_LOCK = threading.Lock()
 
 
 def _f(name, res, args):
-    lib = native.lib()
-    key = name
-    if key not in _FN:
-        fn = getattr(lib, name)
-        fn.restype = res
-        fn.argtypes = args
-        _FN[key] = fn
-    return _FN[key]
+    # a function object of its own per name (CDLL.__getitem__ does not cache; attribute access returns the object
+    # native.py configured), configured once under a lock: setting restype / argtypes on an object another thread is
+    # calling through frees the converters that call is using (a segfault with many calling threads)
+    fn = _FN.get(name)
+    if fn is None:
+        with _FN_LOCK:
+            fn = _FN.get(name)
+            if fn is None:
+                fn = native.lib()[name]
+                fn.restype = res
+                fn.argtypes = args
+                _FN[name] = fn
+    return fn
 
 
 P = ctypes.POINTER
