@@ -1463,6 +1463,124 @@ def run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, dd, n, n_cts, n_d
 
 PREP_ARGS = []
 
+LINE_MAX_BYTES = 6144    # the driver keeps only the tail of stdout (≈ 8 KB incl. stderr): the headline must fit in it
+
+
+def _short(s, n=160):
+    s = str(s)
+    return s if len(s) <= n else s[:n - 3] + "..."
+
+
+def _r(x, d=4):
+    """Round a float for the compact line (relative precision: 6 significant digits)."""
+    if isinstance(x, float):
+        return float(f"{x:.6g}")
+    return x
+
+
+def _pick(d, *keys):
+    if not d:
+        return None
+    return {k: _r(d[k]) for k in keys if k in d and d[k] is not None}
+
+
+def compact_line(full):
+    """The driver-facing headline: the contract keys, the headline roofline and CPU baseline, the exact path's
+    like-for-like numbers, and one short summary per sub-bench.  Everything else stays in the detail record
+    (`bench_detail_<hash>.json` and the `BENCH_DETAIL` stdout line printed before this one)."""
+    rf = full.get("roofline") or {}
+    cpu = full.get("cpu_baseline") or {}
+    cfg = full.get("config") or {}
+    line = {k: full[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                 "higher_is_better", "scaling", "vs_baseline", "dtype", "data") if k in full}
+    line["config"] = {k: cfg[k] for k in ("workload", "shares_per_rank", "ciphertexts_per_rank", "decryptors",
+                                          "degree", "corrupted_fraction", "parallelism", "decision_mismatches")
+                      if k in cfg}
+    if "algorithm" in cfg:
+        line["config"]["algorithm"] = _short(cfg["algorithm"], 120)
+    line["roofline"] = {k: _r(rf[k]) for k in ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic")
+                        if k in rf}
+    if "kernel" in rf:
+        line["roofline"]["kernel"] = _short(rf["kernel"], 120)
+    if rf.get("traffic_source"):
+        line["roofline"]["traffic_source"] = _short(rf["traffic_source"], 100)
+    if rf.get("kernel_frac"):
+        line["roofline"]["kernel_frac"] = {_short(k, 48): _r(v) for k, v in rf["kernel_frac"].items()}
+    if cpu:
+        line["cpu_baseline"] = {k: _r(cpu[k]) for k in ("value", "unit", "cores", "kind") if k in cpu}
+        line["cpu_baseline"]["sample"] = _short(cpu.get("sample", ""), 200)
+        for k in ("amortized_exact", "as_reference"):
+            if cpu.get(k):
+                line["cpu_baseline"][k] = _r(cpu[k].get("value"))
+    else:
+        line["cpu_baseline"] = None
+    line["source_hash"] = full.get("source_hash")
+    ex = full.get("tpke_exact")
+    if ex:
+        exr = ex.get("roofline") or {}
+        line["tpke_exact"] = {"value": _r(ex.get("value")), "ms_per_step": _r(ex.get("ms_per_step")),
+                              "decision_mismatches": ex.get("decision_mismatches"),
+                              "roofline": {"kernel": exr.get("kernel"), "frac": _r(exr.get("frac")),
+                                           "traffic": _r(exr.get("traffic")),
+                                           "kernel_ms": {k: _r(v) for k, v in (exr.get("kernel_ms") or {}).items()}}}
+    else:
+        line["tpke_exact"] = None
+    s = {}
+    byz = full.get("tpke_byzantine")
+    if byz:
+        s["tpke_byzantine"] = {"worst_batched_over_exact": _r(byz.get("worst_batched_over_exact")),
+                               "mismatches": sum(int((p.get("batched") or {}).get("decision_mismatches", 0)) +
+                                                 int((p.get("exact") or {}).get("decision_mismatches", 0))
+                                                 for p in (byz.get("patterns") or {}).values())}
+    if full.get("msm"):
+        s["msm"] = [{"points": m.get("total_points"), "value": _r(m.get("value")), "ms": _r(m.get("ms_per_step")),
+                     "known_answer_ok": m.get("known_answer_ok"),
+                     "frac": _r((m.get("roofline") or {}).get("frac"))} for m in full["msm"]]
+    ts = full.get("threshold_signature")
+    if ts:
+        s["threshold_signature"] = {"value": _r(ts.get("value")), "unit": ts.get("unit"),
+                                    "ms_per_step": _r(ts.get("ms_per_step")),
+                                    "mismatches": ts.get("decision_mismatches"), "phase_ms": {
+                                        _short(k, 24): _r(v) for k, v in (ts.get("phase_ms") or {}).items()},
+                                    "exact": _r((ts.get("exact") or {}).get("value")),
+                                    "cpu": _r((ts.get("cpu_baseline") or {}).get("value"))}
+    for key, vk in (("epoch_replay", "mismatches"), ("ecdsa_headers", "decision_mismatches")):
+        sub = full.get(key)
+        if sub:
+            s[key] = {"value": _r(sub.get("value")), "unit": sub.get("unit"), "mismatches": sub.get(vk),
+                      "cpu": _r((sub.get("cpu_baseline") or {}).get("value"))}
+            if (sub.get("roofline") or {}).get("frac") is not None:
+                s[key]["frac"] = _r(sub["roofline"]["frac"])
+    for key in ("dkg", "rbc_erasure_coding"):
+        sub = full.get(key)
+        if sub:
+            s[key] = {"value": _r(sub.get("value")), "unit": sub.get("unit"),
+                      "cpu": _r((sub.get("cpu_baseline") or {}).get("value"))}
+    ml = full.get("mcl_latency")
+    if ml:
+        s["mcl_latency_us"] = {k: _r(v) for k, v in (ml.get("gpu") or {}).items()}
+    line["summary"] = s
+    text = json.dumps(line, separators=(",", ":"))
+    if len(text) > LINE_MAX_BYTES:            # never let the line outgrow the driver's tail: drop the summaries
+        line["summary"] = {"dropped": "line too long; see the BENCH_DETAIL record"}
+    return line
+
+
+def emit(full):
+    """Print the detail record first (one line, prefixed so it never parses as the headline), write it under
+    gpurun_out/ when that exists, then the compact headline as the LAST stdout line."""
+    detail = json.dumps(full)
+    print("BENCH_DETAIL " + detail, flush=True)
+    out = os.path.join(ROOT, "gpurun_out")
+    if os.path.isdir(out):
+        try:
+            with open(os.path.join(out, f"bench_detail_{full.get('source_hash')}.json"), "w") as fh:
+                fh.write(detail + "\n")
+        except OSError:
+            pass
+    sys.stderr.flush()
+    print(json.dumps(compact_line(full), separators=(",", ":")), flush=True)
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -1709,7 +1827,7 @@ def main():
             "rbc_erasure_coding": rs,
             "mcl_latency": mcl_lat,
         }
-        print(json.dumps(line), flush=True)
+        emit(line)
     if world > 1:
         dist.destroy_process_group()
 

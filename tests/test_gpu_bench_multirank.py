@@ -31,7 +31,11 @@ def test_bench_world_size_two():
            "--no-cpu-baseline"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=420)
     assert r.returncode == 0, r.stderr[-3000:]
-    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    lines = r.stdout.splitlines()
+    head = json.loads([x for x in lines if x.startswith("{")][-1])
+    assert lines[-1].startswith("{") and len(lines[-1]) <= 6144       # the compact headline is the last line
+    assert head["summary"]["tpke_byzantine"]["mismatches"] == 0
+    line = json.loads([x for x in lines if x.startswith("BENCH_DETAIL ")][-1][len("BENCH_DETAIL "):])
     assert line["n_gpus"] == 2 and line["config"]["parallelism"] == "shard2"
     assert line["config"]["decision_mismatches"] == 0
     assert line["tpke_exact"]["decision_mismatches"] == 0
