@@ -1649,6 +1649,8 @@ def main():
     dev = torch.device("cuda", gpu)
     nat.load(False).lcb_set_device(gpu)
     nat.lib()
+    if args.coop_max >= 0 or args.fork_mode >= 0 or args.coop_miller_max >= 0:
+        os.environ["LCB_ALLOW_TUNING"] = "1"          # A/B runs only: the default line never touches the hooks
     if args.coop_max >= 0:
         nat.set_coop_max(args.coop_max)
     if args.fork_mode >= 0:

@@ -155,9 +155,19 @@ int lcb_get_device(void);
 void lcb_set_original_g2_cofactor(int enable);     /* unpinned mcl choice, DESIGN.md §Parity */
 /* Line sets prepared for TPKE ciphertexts / signed messages are normalised (A = 1) unless a line has A == 0, in
    which case the Miller loop computes that point's lines on the fly.  general = 1 makes every later prepare take
-   the on-the-fly path (test hook: the fallback must give the same decisions); 0 restores the default. */
-void lcb_set_line_mode(int general);
+   the on-the-fly path (test hook: the fallback must give the same decisions); 0 restores the default.
+   Tuning hook: returns -1 (and changes nothing) unless the environment has LCB_ALLOW_TUNING=1. */
+int lcb_set_line_mode(int general);
 const char *lcb_last_error(void);
+/* number of failures recorded on the calling thread so far (each sets lcb_last_error).  The mcl entry points that
+   return void (mclBnG1_mul, mclBn_pairing, ...) have no return code: a caller detects their failure by this counter
+   changing across the call.  A failed void call also writes a random, non-canonical value to its output (the top limb
+   of the first coordinate is all ones), so two failed calls never compare equal. */
+uint64_t lcb_error_count(void);
+/* test hook: the next `count` passes through fault site `site` fail (1: the single-operation staging's pinned host
+   buffer, 2: the prepared-ciphertext cache's uploads after its slots were assigned, 3: mclBn_pairing, 4: a
+   single-operation round trip); 0 disables.  Returns -1 unless the environment has LCB_ALLOW_TEST_HOOKS=1. */
+int lcb_test_inject_failure(int site, int count);
 
 /* TPKE.PublicKey.VerifyShare for a batch (TPKE/PublicKey.cs:88-92, called per share from
    HoneyBadger.cs:211-212).  Ciphertext c = (U_c, V_c, W_c) with V_c = v_data[v_off[c] .. v_off[c+1]);
@@ -305,18 +315,19 @@ void lcb_set_batch_census(size_t min_shares);
    suspect keys' shares to single checks} (lcb_ctx_ form: that context's last one) */
 int lcb_batched_census(uint32_t out[4]);
 /* levels of at most max_checks group checks run on the cooperative kernels (k_coop.hip: nine lanes per pairing check,
-   lower latency below one wave per SIMD); 0 = always one check per lane.  Default 32768. */
-void lcb_set_coop_max(uint32_t max_checks);
+   lower latency below one wave per SIMD); 0 = always one check per lane.  Default 32768.  This and the next two are
+   tuning hooks: each returns -1 (and changes nothing) unless the environment has LCB_ALLOW_TUNING=1. */
+int lcb_set_coop_max(uint32_t max_checks);
 /* the cooperative threshold of the group Miller loops alone (default 65536; the final exponentiations keep
    lcb_set_coop_max's) */
-void lcb_set_coop_miller_max(uint32_t max_checks);
+int lcb_set_coop_miller_max(uint32_t max_checks);
 /* stream layout of the fused batched verifies (lcb_tpke_verify_shares_batched_dev, lcb_ts_verify_shares_batched_dev):
    0 = randomisation on the context's second stream beside the preparation on the caller's; 1 (default) = the
    latency-bound preparation chain (hash-to-G2, line sets, census) on a high-priority stream and the randomisation on
    the caller's; 2 = as 1 with the preparation's first kernel enqueued ahead of the randomisation; 3 (default) = as 2
    with the TPKE preparation split into hash + H's line set and U / W decoding + W's line set, on two high-priority
    streams (threshold signatures: as 1).  Decisions are unchanged. */
-void lcb_set_fork_mode(int mode);
+int lcb_set_fork_mode(int mode);
 /* test hook: final exponentiation of n Fp12 values (144 x u32 each, Montgomery form, field.hpp layout) by the one-lane
    (coop = 0) or the cooperative (coop = 1) kernel */
 int lcb_debug_final_exp(const uint32_t *in, size_t n, uint32_t *out, int coop);

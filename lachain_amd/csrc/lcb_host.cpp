@@ -45,6 +45,8 @@ bool g_ready = false;
 int g_orig_cofactor = 0;
 const size_t IO_WORDS = 4096; // 16 KB staging per thread
 thread_local std::string g_err;
+thread_local uint64_t g_err_count = 0;   // failures on this thread (lcb_error_count): the void mcl entry points have no
+                                         // return code, so a caller detects their failure by this counter changing
 thread_local int t_bound_device = -1;
 
 void set_err(const char *what, hipError_t e = hipSuccess) {
@@ -52,6 +54,44 @@ void set_err(const char *what, hipError_t e = hipSuccess) {
     if (e != hipSuccess) snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
     else snprintf(buf, sizeof buf, "%s", what);
     g_err = buf;
+    g_err_count++;
+}
+
+// opt-in switches read from the environment at call time: the tuning hooks (lcb_set_coop_max, ...) change the kernel
+// families a batch runs on and the fault-injection hooks make calls fail; neither belongs in a production process
+bool env_on(const char *name) {
+    const char *e = getenv(name);
+    return e && e[0] == '1';
+}
+bool tuning_allowed(const char *what) {
+    if (env_on("LCB_ALLOW_TUNING")) return true;
+    set_err((std::string(what) + ": tuning hooks need LCB_ALLOW_TUNING=1").c_str());
+    return false;
+}
+// fault injection (lcb_test_inject_failure, LCB_ALLOW_TEST_HOOKS=1): the next `count` passes through site `site` fail
+std::atomic<int> g_inject_site{0}, g_inject_count{0};
+bool injected(int site) {
+    if (g_inject_site.load(std::memory_order_relaxed) != site) return false;
+    int c = g_inject_count.load();
+    while (c > 0)
+        if (g_inject_count.compare_exchange_weak(c, c - 1)) return true;
+    return false;
+}
+enum { INJ_STAGE_HOST_ALLOC = 1, INJ_CT_CACHE_ALLOC = 2, INJ_PAIRING_ALLOC = 3, INJ_STAGE_OP = 4 };
+
+// the output of a failed void mcl call (mclBnG1_mul, mclBn_pairing, ...): random words with the top limb of the first
+// coordinate set to all ones, so it is not a canonical field element (isValid / serialize reject it), and two failed
+// calls never compare equal (an equality check between two failed pairings cannot pass)
+void fail_out(void *out, size_t bytes) {
+    uint8_t *b = (uint8_t *)out;
+    size_t got = 0;
+    while (got < bytes) {
+        ssize_t r = getrandom(b + got, bytes - got, 0);
+        if (r <= 0) break;
+        got += (size_t)r;
+    }
+    for (size_t i = got; i < bytes; i++) b[i] = (uint8_t)(0x5a ^ i);
+    if (bytes >= 48) memset(b + 44, 0xff, 4);
 }
 
 // HIP's current device is per thread: bind every thread that enters the library to the configured device
@@ -97,11 +137,25 @@ struct OpStage {
 thread_local OpStage t_stage;
 bool stage_ready() {
     if (!ready()) return false;
-    if (t_stage.s) return true;
-    hipError_t e = hipStreamCreateWithFlags(&t_stage.s, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipMalloc(&t_stage.dev, IO_WORDS * 4);
-    if (e == hipSuccess) e = hipHostMalloc(&t_stage.host, IO_WORDS * 4, hipHostMallocDefault);
-    if (e != hipSuccess) { set_err("single-operation staging", e); return false; }
+    if (t_stage.s && t_stage.dev && t_stage.host) return true;
+    // all three or none: a partial failure releases what was created, so the next call retries from scratch instead
+    // of passing a half-built stage (a set stream with a null host buffer would be written through)
+    hipError_t e = t_stage.s ? hipSuccess : hipStreamCreateWithFlags(&t_stage.s, hipStreamNonBlocking);
+    if (e == hipSuccess && !t_stage.dev) e = hipMalloc(&t_stage.dev, IO_WORDS * 4);
+    if (e == hipSuccess && !t_stage.host) {
+        if (injected(INJ_STAGE_HOST_ALLOC)) e = hipErrorOutOfMemory;
+        else e = hipHostMalloc(&t_stage.host, IO_WORDS * 4, hipHostMallocDefault);
+    }
+    if (e != hipSuccess) {
+        set_err("single-operation staging", e);
+        if (t_stage.host) (void)hipHostFree(t_stage.host);
+        if (t_stage.dev) (void)hipFree(t_stage.dev);
+        if (t_stage.s) (void)hipStreamDestroy(t_stage.s);
+        t_stage.host = nullptr;
+        t_stage.dev = nullptr;
+        t_stage.s = nullptr;
+        return false;
+    }
     return true;
 }
 #define IOH (t_stage.host)
@@ -109,6 +163,7 @@ bool stage_ready() {
 // run one k_op on the thread's staging buffer: copy `in_words` words to the device, launch, copy `out_words` back
 bool run_op(int op, size_t in_words, size_t out_words) {
     hipError_t e;
+    if (injected(INJ_STAGE_OP)) { set_err("injected failure (single operation)"); return false; }
     if ((e = hipMemcpyAsync(t_stage.dev, t_stage.host, in_words * 4, hipMemcpyHostToDevice, t_stage.s)) != hipSuccess) { set_err("H2D", e); return false; }
     lcbk_op(dim3(1), t_stage.s, op, t_stage.dev, g_orig_cofactor);
     if ((e = hipGetLastError()) != hipSuccess) { set_err("k_op launch", e); return false; }
@@ -143,7 +198,11 @@ extern "C" int lcb_set_device(int id) {
 extern "C" int lcb_get_device(void) { return g_device; }
 extern "C" void lcb_set_original_g2_cofactor(int enable) { g_orig_cofactor = enable != 0; }
 int g_line_mode = 0;   // 1: prepare marks every line set un-normalised (test hook for the on-the-fly fallback)
-extern "C" void lcb_set_line_mode(int general) { g_line_mode = general != 0; }
+extern "C" int lcb_set_line_mode(int general) {
+    if (!tuning_allowed("lcb_set_line_mode")) return -1;
+    g_line_mode = general != 0;
+    return 0;
+}
 extern "C" const char *lcb_last_error(void) { return g_err.c_str(); }
 
 extern "C" int mclBn_init(int curve, int compiledTimeVar) {
@@ -266,11 +325,12 @@ extern "C" int mclBnG1_isZero(const mclBnG1 *x) {
 }
 extern "C" void mclBnG1_clear(mclBnG1 *x) { memset(x, 0, sizeof *x); }
 static void g1_op(int op, mclBnG1 *z, const mclBnG1 *x, const mclBnG1 *y, const mclBnFr *k) {
-    LOCKED_OR()
+    if (!stage_ready()) { fail_out(z, 144); return; }
     memcpy(IOH + 36, x, 144);
     if (y) memcpy(IOH + 72, y, 144);
     if (k) memcpy(IOH + 108, k, 32);
     if (run_op(op, 116, 36)) memcpy(z, IOH, 144);
+    else fail_out(z, 144);
 }
 extern "C" void mclBnG1_neg(mclBnG1 *y, const mclBnG1 *x) { g1_op(OP_G1_NEG, y, x, nullptr, nullptr); }
 extern "C" void mclBnG1_dbl(mclBnG1 *y, const mclBnG1 *x) { g1_op(OP_G1_DBL, y, x, nullptr, nullptr); }
@@ -283,8 +343,9 @@ extern "C" void mclBnG1_sub(mclBnG1 *z, const mclBnG1 *x, const mclBnG1 *y) {
 }
 extern "C" void mclBnG1_mul(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y) { g1_op(OP_G1_MUL, z, x, nullptr, y); }
 extern "C" void lcb_g1_generator(mclBnG1 *g) {
-    LOCKED_OR()
+    if (!stage_ready()) { fail_out(g, 144); return; }
     if (run_op(OP_G1_GEN, 0, 36)) memcpy(g, IOH, 144);
+    else fail_out(g, 144);
 }
 
 // ================================================================== G2
@@ -328,11 +389,12 @@ extern "C" int mclBnG2_hashAndMapTo(mclBnG2 *x, const void *buf, mclSize n) {
     return 0;
 }
 static void g2_op(int op, mclBnG2 *z, const mclBnG2 *x, const mclBnG2 *y, const mclBnFr *k) {
-    LOCKED_OR()
+    if (!stage_ready()) { fail_out(z, 288); return; }
     memcpy(IOH + 72, x, 288);
     if (y) memcpy(IOH + 144, y, 288);
     if (k) memcpy(IOH + 216, k, 32);
     if (run_op(op, 224, 72)) memcpy(z, IOH, 288);
+    else fail_out(z, 288);
 }
 extern "C" void mclBnG2_neg(mclBnG2 *y, const mclBnG2 *x) { g2_op(OP_G2_NEG, y, x, nullptr, nullptr); }
 extern "C" void mclBnG2_dbl(mclBnG2 *y, const mclBnG2 *x) { g2_op(OP_G2_DBL, y, x, nullptr, nullptr); }
@@ -345,33 +407,38 @@ extern "C" void mclBnG2_sub(mclBnG2 *z, const mclBnG2 *x, const mclBnG2 *y) {
 }
 extern "C" void mclBnG2_mul(mclBnG2 *z, const mclBnG2 *x, const mclBnFr *y) { g2_op(OP_G2_MUL, z, x, nullptr, y); }
 extern "C" void lcb_g2_generator(mclBnG2 *g) {
-    LOCKED_OR()
+    if (!stage_ready()) { fail_out(g, 288); return; }
     if (run_op(OP_G2_GEN, 0, 72)) memcpy(g, IOH, 288);
+    else fail_out(g, 288);
 }
 
 // ================================================================== GT / pairing
 static void pair_op(int op, mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) {
-    LOCKED_OR()
+    if (!stage_ready()) { fail_out(z, 576); return; }
     memcpy(IOH + 144, x, 144);
     memcpy(IOH + 180, y, 288);
     if (run_op(op, 252, 144)) memcpy(z, IOH, 576);
+    else fail_out(z, 576);
 }
 extern "C" void mclBn_millerLoop(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) { pair_op(OP_MILLER, z, x, y); }
 static void gt_op(int op, mclBnGT *z, const mclBnGT *a, const mclBnGT *b, const mclBnFr *k) {
-    LOCKED_OR()
+    if (!stage_ready()) { fail_out(z, 576); return; }
     memcpy(IOH + 252, a, 576);
     if (b) memcpy(IOH + 396, b, 576);
     if (k) memcpy(IOH + 540, k, 32);
     if (run_op(op, 548, 144)) memcpy(z, IOH, 576);
+    else fail_out(z, 576);
 }
 extern "C" void mclBn_millerLoopVec(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y, mclSize n) {
     mclBnGT acc, t;
     memset(&acc, 0, sizeof acc);
-    for (mclSize i = 0; i < n; i++) {
+    const uint64_t errs = g_err_count;
+    for (mclSize i = 0; i < n && g_err_count == errs; i++) {
         mclBn_millerLoop(&t, &x[i], &y[i]);
         if (i == 0) acc = t;
         else gt_op(OP_GT_MUL, &acc, &acc, &t, nullptr);
     }
+    if (g_err_count != errs) fail_out(&acc, 576);
     *z = acc;
 }
 // debug-only (not in include/lachain_bls.h): apply tower routine `which` (k_ops.hip OP_DEBUG_FP12) to raw GT words
@@ -609,7 +676,8 @@ int tpke_verify_core(lcb_ctx *c, const u32 *lines, const uint8_t *ctok, size_t n
         }
         // small batches (the protocol's one-share-per-call shape, the queue's flushes): nine lanes per check
         // (k_coop.hip) instead of one, below the size where the one-lane kernels fill the GPU
-        const bool coop = n <= g_coop_max.load();
+        // (never above one chunk: the cooperative buffers below are sized for n)
+        const bool coop = n <= g_coop_max.load() && n <= LCB_VERIFY_CHUNK;
         void *gpts = coop ? c->t_coop[0].get(n * 2 * LCB_G1A_ST_BYTES) : nullptr;
         void *desc = coop ? c->t_coop[1].get(n * 16) : nullptr;
         uint8_t *fl = coop ? (uint8_t *)c->t_coop[2].get(2 * n) : nullptr;
@@ -618,9 +686,9 @@ int tpke_verify_core(lcb_ctx *c, const u32 *lines, const uint8_t *ctok, size_t n
             const size_t m = n - o < LCB_VERIFY_CHUNK ? n - o : LCB_VERIFY_CHUNK;
             if (o == 0) hipEventRecord(c->ver_ev[0], s);
             if (coop) {
-                lcbk_tpke_exact_points(s, ctok, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct, d_dec, d_ui, (u32)m, gpts,
-                                       desc, d_accept);
-                lcbk_coop_tpke_miller(s, lines, desc, gpts, (u32)m, f, fl, fl + n, 2);
+                lcbk_tpke_exact_points(s, ctok, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct + o, d_dec + o,
+                                       d_ui + 48 * o, (u32)m, gpts, desc, d_accept + o);
+                lcbk_coop_tpke_miller(s, lines, desc, gpts, (u32)m, f, fl, fl + m, 2);
             } else {
                 lcbk_tpke_miller(dim3(nblk(m)), s, lines, ctok, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct + o,
                                  d_dec + o, d_ui + 48 * o, (u32)m, f, d_accept + o);
@@ -1489,12 +1557,30 @@ extern "C" void lcb_set_batch_seed(const uint8_t *seed32) {
     else g_rlc_seed_set = false;
 }
 extern "C" void lcb_set_batch_census(size_t min_shares) { g_census_min.store(min_shares); }
-extern "C" void lcb_set_coop_max(uint32_t max_checks) {
+extern "C" int lcb_set_coop_max(uint32_t max_checks) {
+    if (!tuning_allowed("lcb_set_coop_max")) return -1;
     g_coop_max.store(max_checks);
     g_coop_miller_max.store(max_checks);
+    return 0;
 }
-extern "C" void lcb_set_coop_miller_max(uint32_t max_checks) { g_coop_miller_max.store(max_checks); }
-extern "C" void lcb_set_fork_mode(int mode) { g_fork_mode.store(mode >= 1 && mode <= 3 ? mode : 0); }
+extern "C" int lcb_set_coop_miller_max(uint32_t max_checks) {
+    if (!tuning_allowed("lcb_set_coop_miller_max")) return -1;
+    g_coop_miller_max.store(max_checks);
+    return 0;
+}
+extern "C" int lcb_set_fork_mode(int mode) {
+    if (!tuning_allowed("lcb_set_fork_mode")) return -1;
+    g_fork_mode.store(mode >= 1 && mode <= 3 ? mode : 0);
+    return 0;
+}
+extern "C" int lcb_test_inject_failure(int site, int count) {
+    if (!env_on("LCB_ALLOW_TEST_HOOKS")) { set_err("lcb_test_inject_failure: needs LCB_ALLOW_TEST_HOOKS=1"); return -1; }
+    g_inject_count.store(0);
+    g_inject_site.store(site);
+    g_inject_count.store(count);
+    return 0;
+}
+extern "C" uint64_t lcb_error_count(void) { return g_err_count; }
 // one cooperative Fp12 operation (k_coop_debug) on n values a (and b) vs the one-lane field.hpp routine: AoS in / out
 extern "C" int lcb_debug_coop_op(int op, const uint32_t *a, const uint32_t *b, size_t n, uint32_t *out, uint32_t *ref) {
     SYNC_CTX_OR(c, -1)
@@ -1647,6 +1733,12 @@ extern "C" int lcb_tpke_verify_shares_cached(uint8_t *accept, size_t n, const ui
     void *keys = c->t_keys.get((n_keys ? n_keys : 1) * LCB_G1A_ST_BYTES);
     if (!lines || !ctok || !keys) { set_err("device allocation failed"); return -1; }
     const uint64_t tick = ++c->cc_tick;
+    // the map below names slots before their line sets exist: any failure from here on empties the whole cache (the
+    // next call starts from first use), so no later call can take a slot this call left unprepared
+    auto cache_fail = [c]() {
+        c->cc_used.clear();
+        return -1;
+    };
     std::vector<u32> slot_of(n_cts), miss;
     for (size_t k = 0; k < n_cts; k++) {
         const u32 v0 = v_off[k], v1 = v_off[k + 1];
@@ -1693,7 +1785,10 @@ extern "C" int lcb_tpke_verify_shares_cached(uint8_t *accept, size_t n, const ui
         const uint32_t *dvo = up(c->in[4], mvo.data(), mvo.size(), s);
         const uint32_t *dsl = up(c->sel[0], mslot.data(), m, s);
         const uint32_t *dse = up(c->sel[1], msets.data(), 2 * m, s);
-        if (!du || !dw || !dv || !dvo || !dsl || !dse) { set_err("device allocation failed"); return -1; }
+        if (!du || !dw || !dv || !dvo || !dsl || !dse || injected(INJ_CT_CACHE_ALLOC)) {
+            set_err("device allocation failed");
+            return cache_fail();
+        }
         lcbk_tpke_ct_prepare(dim3(nblk(m)), s, du, dw, dv, dvo, (u32)m, lines, ctok, flags, dsl);
         lcbk_lineset_fill(dim3(nblk(2 * m)), s, lines, (u32)(2 * m), dse, nullptr);
     }
@@ -1703,13 +1798,10 @@ extern "C" int lcb_tpke_verify_shares_cached(uint8_t *accept, size_t n, const ui
     const uint32_t *ddec = up(c->in[6], dec_idx, n, s);
     const uint8_t *dui = up(c->in[7], ui, 48 * n, s);
     uint8_t *dacc = (uint8_t *)c->out[0].get(n);
-    if (!dy || !dct || !ddec || !dui || !dacc) { set_err("device allocation failed"); return -1; }
-    if (tpke_verify_core(c, lines, ctok, LCB_CT_CACHE, n_keys, dacc, n, dct, ddec, dui, s)) return -1;
+    if (!dy || !dct || !ddec || !dui || !dacc) { set_err("device allocation failed"); return cache_fail(); }
+    if (tpke_verify_core(c, lines, ctok, LCB_CT_CACHE, n_keys, dacc, n, dct, ddec, dui, s)) return cache_fail();
     if (n) hipMemcpyAsync(accept, dacc, n, hipMemcpyDeviceToHost, s);
-    if (!sync_check(c, "tpke verify (cached)")) {
-        c->cc_used.clear();              // slots written by a failed call may be incomplete
-        return -1;
-    }
+    if (!sync_check(c, "tpke verify (cached)")) return cache_fail();
     return 0;
 }
 extern "C" int lcb_tpke_verify_shares(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys,
@@ -2261,6 +2353,8 @@ extern "C" int lcb_g2_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_
 // the nine-lane final exponentiation.  The lines are normalised (divided by their Fp2 leading coefficient), which
 // changes the Miller value by a factor the final exponentiation removes: the GT value is mcl's.
 extern "C" void mclBn_pairing(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) {
+    fail_out(z, 576);                  // overwritten on success; a failed call leaves a value no other call produces
+    if (injected(INJ_PAIRING_ALLOC)) { set_err("injected failure (pairing)"); return; }
     SYNC_CTX_OR(c, )
     Enq q(c, c->stream);
     hipStream_t s = c->stream;
@@ -2297,6 +2391,9 @@ extern "C" void mclBn_pairing(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) {
 }
 // mclBn_finalExp on the nine-lane kernel (park slot 0 of a one-value workspace)
 extern "C" void mclBn_finalExp(mclBnGT *y, const mclBnGT *x) {
+    mclBnGT xin = *x;                  // y may alias x
+    x = &xin;
+    fail_out(y, 576);
     SYNC_CTX_OR(c, )
     Enq q(c, c->stream);
     hipStream_t s = c->stream;
@@ -2311,10 +2408,9 @@ extern "C" void mclBn_finalExp(mclBnGT *y, const mclBnGT *x) {
 }
 // mclBnG1_mulVec: sum_i [y_i] x_i with the canonical scalars (mcl's per-term product, exact for any on-curve x_i):
 // one lane per term (windowed ladder), then block reductions and a one-lane sum
-extern "C" void mclBnG1_mulVec(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y, mclSize n) {
-    if (n == 0) { mclBnG1_clear(z); return; }
-    SYNC_CTX_OR(c, )
-    if (n > 0xffffffffu) { set_err("mulVec: too large"); return; }
+static bool g1_mulvec(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y, mclSize n) {
+    SYNC_CTX_OR(c, false)
+    if (n > 0xffffffffu) { set_err("mulVec: too large"); return false; }
     std::vector<uint64_t> raw(4 * n);
     for (size_t i = 0; i < n; i++) frh::to_raw(&raw[4 * i], FRV(&y[i]));
     Enq q(c, c->stream);
@@ -2324,7 +2420,7 @@ extern "C" void mclBnG1_mulVec(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y, m
     uint8_t *terms = (uint8_t *)c->mcl[2].get(LCB_G1_JAC_BYTES * n);
     uint8_t *tmp = (uint8_t *)c->mcl[3].get(LCB_G1_JAC_BYTES * ((n + 255) / 256));
     uint8_t *dz = (uint8_t *)c->mcl[5].get(LCB_G1_JAC_BYTES);
-    if (!pts || !sc || !terms || !tmp || !dz) { set_err("device allocation failed"); return; }
+    if (!pts || !sc || !terms || !tmp || !dz) { set_err("device allocation failed"); return false; }
     lcbk_mcl_g1_terms(s, pts, sc, (u32)n, terms);
     uint8_t *cur = terms;
     size_t cnt = n;
@@ -2337,7 +2433,13 @@ extern "C" void mclBnG1_mulVec(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y, m
     lcbk_mcl_g1_sum(s, cur, (u32)cnt, dz);
     mclBnG1 r;
     hipMemcpyAsync(&r, dz, 144, hipMemcpyDeviceToHost, s);
-    if (sync_check(c, "mulVec")) *z = r;
+    if (!sync_check(c, "mulVec")) return false;
+    *z = r;
+    return true;
+}
+extern "C" void mclBnG1_mulVec(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y, mclSize n) {
+    if (n == 0) { mclBnG1_clear(z); return; }
+    if (!g1_mulvec(z, x, y, n)) fail_out(z, 144);
 }
 // G1 / G2 Lagrange interpolation of one problem on the batch kernels: mcl records -> wire bytes on the device, the
 // k_lagrange.hip coefficient + product kernels, the result decoded back into an mcl record (one round trip)

@@ -4,7 +4,8 @@
 Method names follow the C# API census in SURVEY.md §8b (Fr.FromInt, Fr.GetRandom, G1.Generator,
 G1.FromBytes, G2.SetHashOf, GT.Pairing, GT.Pow, MclBls12381.LagrangeInterpolate,
 MclBls12381.EvaluatePolynomial, ...) so the parity tests read like test/Lachain.CryptoTest/MclTests.cs.
-Failures raise (the reference's wrapper throws on a failed FromBytes / interpolation).
+Failures raise (the reference's wrapper throws on a failed FromBytes / interpolation), including those of the
+void GPU-backed calls (detected through lcb_error_count).
 """
 import ctypes
 import threading
@@ -34,6 +35,17 @@ def _f(name, res, args):
 
 P = ctypes.POINTER
 _sz = ctypes.c_size_t
+
+
+def _void(name, args, *call):
+    """call a void mcl entry point that runs on the GPU and raise if it failed: the C ABI has no return code for these
+    (mcl's own signatures), so the library counts failures per thread (lcb_error_count) and a failed call also writes
+    a random non-canonical value to its output (include/lachain_bls.h)"""
+    cnt = _f("lcb_error_count", ctypes.c_uint64, [])
+    before = cnt()
+    _f(name, None, args)(*call)
+    if cnt() != before:
+        raise RuntimeError(f"{name} failed: {native.last_error()}")
 
 
 class Fr:
@@ -150,8 +162,8 @@ class _Point:
 
     def _bin(self, op, other):
         r = type(self)()
-        _f(f"mclBn{self._P}_{op}", None, [P(self._T), P(self._T), P(self._T)])(
-            ctypes.byref(r.v), ctypes.byref(self.v), ctypes.byref(other.v))
+        _void(f"mclBn{self._P}_{op}", [P(self._T), P(self._T), P(self._T)],
+              ctypes.byref(r.v), ctypes.byref(self.v), ctypes.byref(other.v))
         return r
 
     def __add__(self, o):
@@ -162,15 +174,15 @@ class _Point:
 
     def __neg__(self):
         r = type(self)()
-        _f(f"mclBn{self._P}_neg", None, [P(self._T), P(self._T)])(ctypes.byref(r.v), ctypes.byref(self.v))
+        _void(f"mclBn{self._P}_neg", [P(self._T), P(self._T)], ctypes.byref(r.v), ctypes.byref(self.v))
         return r
 
     def __mul__(self, k):
         if not isinstance(k, Fr):
             return NotImplemented
         r = type(self)()
-        _f(f"mclBn{self._P}_mul", None, [P(self._T), P(self._T), P(mclBnFr)])(
-            ctypes.byref(r.v), ctypes.byref(self.v), ctypes.byref(k.v))
+        _void(f"mclBn{self._P}_mul", [P(self._T), P(self._T), P(mclBnFr)],
+              ctypes.byref(r.v), ctypes.byref(self.v), ctypes.byref(k.v))
         return r
 
     def IsValid(self):
@@ -200,7 +212,7 @@ class G1(_Point):
     @staticmethod
     def Generator():
         r = G1()
-        _f("lcb_g1_generator", None, [P(mclBnG1)])(ctypes.byref(r.v))
+        _void("lcb_g1_generator", [P(mclBnG1)], ctypes.byref(r.v))
         return r
 
 
@@ -212,7 +224,7 @@ class G2(_Point):
     @staticmethod
     def Generator():
         r = G2()
-        _f("lcb_g2_generator", None, [P(mclBnG2)])(ctypes.byref(r.v))
+        _void("lcb_g2_generator", [P(mclBnG2)], ctypes.byref(r.v))
         return r
 
     def SetHashOf(self, msg):
@@ -232,21 +244,21 @@ class GT:
     @staticmethod
     def Pairing(a, b):
         r = GT()
-        _f("mclBn_pairing", None, [P(mclBnGT), P(mclBnG1), P(mclBnG2)])(ctypes.byref(r.v), ctypes.byref(a.v),
-                                                                       ctypes.byref(b.v))
+        _void("mclBn_pairing", [P(mclBnGT), P(mclBnG1), P(mclBnG2)], ctypes.byref(r.v), ctypes.byref(a.v),
+              ctypes.byref(b.v))
         return r
 
     @staticmethod
     def Pow(a, k):
         r = GT()
-        _f("mclBnGT_pow", None, [P(mclBnGT), P(mclBnGT), P(mclBnFr)])(ctypes.byref(r.v), ctypes.byref(a.v),
-                                                                     ctypes.byref(k.v))
+        _void("mclBnGT_pow", [P(mclBnGT), P(mclBnGT), P(mclBnFr)], ctypes.byref(r.v), ctypes.byref(a.v),
+              ctypes.byref(k.v))
         return r
 
     def __mul__(self, o):
         r = GT()
-        _f("mclBnGT_mul", None, [P(mclBnGT), P(mclBnGT), P(mclBnGT)])(ctypes.byref(r.v), ctypes.byref(self.v),
-                                                                     ctypes.byref(o.v))
+        _void("mclBnGT_mul", [P(mclBnGT), P(mclBnGT), P(mclBnGT)], ctypes.byref(r.v), ctypes.byref(self.v),
+              ctypes.byref(o.v))
         return r
 
     def ToBytes(self):

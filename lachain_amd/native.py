@@ -51,8 +51,10 @@ _SIGS = {
     "lcb_set_device": (ctypes.c_int, [ctypes.c_int]),
     "lcb_get_device": (ctypes.c_int, []),
     "lcb_set_original_g2_cofactor": (None, [ctypes.c_int]),
-    "lcb_set_line_mode": (None, [ctypes.c_int]),
+    "lcb_set_line_mode": (ctypes.c_int, [ctypes.c_int]),
     "lcb_last_error": (ctypes.c_char_p, []),
+    "lcb_error_count": (ctypes.c_uint64, []),
+    "lcb_test_inject_failure": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "lcb_tpke_verify_shares": (ctypes.c_int, [c_u8p, c_size, c_u8p, c_size, c_u8p, c_u8p, c_u8p, c_u32p, c_size,
                                               c_u32p, c_u32p, c_u8p]),
     "lcb_tpke_verify_shares_cached": (ctypes.c_int, [c_u8p, c_size, c_u8p, c_size, c_u8p, c_u8p, c_u8p, c_u32p, c_size,
@@ -82,9 +84,9 @@ _SIGS = {
     "lcb_tpke_batched_stats": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_float)]),
     "lcb_set_batch_seed": (None, [ctypes.c_char_p]),
     "lcb_set_batch_census": (None, [c_size]),
-    "lcb_set_coop_max": (None, [ctypes.c_uint32]),
-    "lcb_set_fork_mode": (None, [ctypes.c_int]),
-    "lcb_set_coop_miller_max": (None, [ctypes.c_uint32]),
+    "lcb_set_coop_max": (ctypes.c_int, [ctypes.c_uint32]),
+    "lcb_set_fork_mode": (ctypes.c_int, [ctypes.c_int]),
+    "lcb_set_coop_miller_max": (ctypes.c_int, [ctypes.c_uint32]),
     "lcb_debug_coop_op": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                                          c_size, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]),
     "lcb_debug_final_exp": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint32), c_size, ctypes.POINTER(ctypes.c_uint32),
@@ -719,21 +721,37 @@ def set_batch_census(min_shares):
     lib().lcb_set_batch_census(min_shares)
 
 
+def _tuning(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what}: {last_error()} (tuning hooks are opt-in: LCB_ALLOW_TUNING=1)")
+
+
+def error_count():
+    """failures recorded on the calling thread (lcb_error_count): how the void mcl calls report failure"""
+    return int(lib().lcb_error_count())
+
+
+def inject_failure(site, count=1):
+    """test hook (LCB_ALLOW_TEST_HOOKS=1): the next `count` passes through fault site `site` fail"""
+    if lib().lcb_test_inject_failure(int(site), int(count)) != 0:
+        raise RuntimeError("inject_failure: " + last_error())
+
+
 def set_coop_max(max_checks):
     """levels of <= max_checks group checks use the nine-lane cooperative kernels (0 = never; default 32768)"""
-    lib().lcb_set_coop_max(max_checks)
+    _tuning(lib().lcb_set_coop_max(max_checks), "set_coop_max")
 
 
 def set_coop_miller_max(max_checks):
     """levels of <= max_checks group checks run their Miller loops on the cooperative kernels"""
-    lib().lcb_set_coop_miller_max(max_checks)
+    _tuning(lib().lcb_set_coop_miller_max(max_checks), "set_coop_miller_max")
 
 
 def set_fork_mode(mode):
     """stream layout of the fused batched verify (include/lachain_bls.h lcb_set_fork_mode): 0 = randomisation on a
     second stream, 1 = preparation chain on a high-priority stream, 2 = 1 with the preparation enqueued first,
     3 (default) = 2 with the TPKE preparation split into hash / decode lanes on two high-priority streams"""
-    lib().lcb_set_fork_mode(mode)
+    _tuning(lib().lcb_set_fork_mode(mode), "set_fork_mode")
 
 
 def debug_final_exp(values, coop):
@@ -776,4 +794,4 @@ def tpke_batched_stats():
 def set_line_mode(general):
     """general=True: later prepares mark every line set un-normalised, so the Miller loops take the on-the-fly
     fallback (pairing.hpp miller2_sets_fallback); False restores the normalised default"""
-    lib().lcb_set_line_mode(1 if general else 0)
+    _tuning(lib().lcb_set_line_mode(1 if general else 0), "set_line_mode")
