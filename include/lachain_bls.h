@@ -153,6 +153,11 @@ int mclBn_G2EvaluatePolynomial(mclBnG2 *out, const mclBnG2 *cVec, mclSize cSize,
 int lcb_set_device(int device_id);                 /* before mclBn_init; default: HIP device 0 */
 int lcb_get_device(void);
 void lcb_set_original_g2_cofactor(int enable);     /* unpinned mcl choice, DESIGN.md §Parity */
+/* unpinned mcl convention: the G2 wire flag (bit 7 of byte 95) is the parity of y.a (use_b = 0, the
+   default) or of y.b (use_b = 1), for every G2 (de)serialization — the mcl surface and every batch kernel alike.
+   Mirrors the oracle's orc_set_g2_sign_from_b (oracle/bls.c:517-521,691).  Call before batch work, not during it.
+   Returns -1 without a device. */
+int lcb_set_g2_sign_from_b(int use_b);
 /* Line sets prepared for TPKE ciphertexts / signed messages are normalised (A = 1) unless a line has A == 0, in
    which case the Miller loop computes that point's lines on the fly.  general = 1 makes every later prepare take
    the on-the-fly path (test hook: the fallback must give the same decisions); 0 restores the default.

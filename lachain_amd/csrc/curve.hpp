@@ -425,6 +425,11 @@ DN void g1_mul_glv(g1 &r, const g1a &A, const u32 k[8]) {
 }
 
 // ---------------------------------------------------------------- serialization
+// Which coordinate's parity the G2 wire flag carries (unpinned mcl convention): 0 = y.a (default),
+// 1 = y.b.  One copy per translation unit, set by every unit's lcbk_cfg_<unit> (kcommon.hpp LCB_TU_CONFIG) through
+// lcb_set_g2_sign_from_b; read once per (de)compression.
+static __device__ u32 lcb_g2_sign_b = 0;
+DI const fp &g2_sign_coord(const fp2 &y) { return lcb_g2_sign_b ? y.b : y.a; }
 DI void bytes48_to_raw(fp &raw, const uint8_t *b) { // 4-byte aligned source
     const u32 *w = (const u32 *)b;
 #pragma unroll
@@ -484,7 +489,7 @@ DN bool g2_decompress(g2a &out, const uint8_t *b) {
     fp2_load_const(b2, LCB_B2);
     fp2_add(t, t, b2);
     if (!fp2_sqrt_any(y, t)) return false;            // the sign is fixed below, so any root serves
-    if (fp_is_odd(y.a) != odd) fp2_neg(y, y);
+    if (fp_is_odd(g2_sign_coord(y)) != odd) fp2_neg(y, y);
     out.x = x; out.y = y; out.inf = false;
     return true;
 }
@@ -498,7 +503,7 @@ DI void g2_compress(uint8_t *b, const g2a &a) {
     fp xa, xb, ya;
     fp_to_raw(xa, a.x.a);
     fp_to_raw(xb, a.x.b);
-    fp_to_raw(ya, a.y.a);
+    fp_to_raw(ya, g2_sign_coord(a.y));
     if (ya.v[0] & 1) xb.v[11] |= 0x80000000u;
     raw_to_bytes48(b, xa);
     raw_to_bytes48(b + 48, xb);

@@ -1,0 +1,531 @@
+// lachain_amd/csrc/fp_host.hpp — BLS12-381 base field, G1 and G2 on the host for the mcl single-element surface.
+//
+// The reference's Lachain.Crypto code calls mcl one element at a time (TPKE/PublicKey.cs:25-37 builds a ciphertext
+// with G1 / G2 additions and serializations, TPKE/TrustedKeyGen.cs:15-33 and ThresholdKeygen/Data/Commitment.cs:23-55
+// add and compare points, every message (de)serializes them).  Those are O(1) field work — a handful of Fp products,
+// or one exponentiation for a decompression / normalisation — which is nanoseconds to microseconds on a host core
+// and a ~40 us synchronous round trip as a GPU call.  So, like Fr (fr_host.hpp), they run here; every operation that
+// carries a scalar (G1 / G2 multiplication, GT power), the hash to G2 and the pairing stay on the GPU.
+//
+// Values are bit-identical to the kernels': mclBnG1 / mclBnG2 / mclBnGT hold Fp elements as 12 x u32 Montgomery limbs
+// (R = 2^384), read here as 6 x u64 little-endian (the same bytes); every operation returns the fully reduced residue
+// (unique), and the group formulas are the kernels' own (curve.hpp: dbl-2009-l, add-2007-bl with the same special
+// cases, the same point-at-infinity encoding (1, 1, 0)), so the Jacobian coordinates agree word for word.  The square
+// roots follow field.hpp's root choices where a choice is visible (fp2_sqrt's order for x.b == 0).  CIOS Montgomery
+// product over unsigned __int128.
+#pragma once
+#include <stdint.h>
+#include <string.h>
+#include "bls_constants_host.h"
+
+namespace fph {
+typedef unsigned __int128 u128;
+struct fp { uint64_t v[6]; };
+struct fp2 { fp a, b; };
+struct fp6 { fp2 c0, c1, c2; };
+struct fp12 { fp6 c0, c1; };
+template <class F> struct jac { F x, y, z; };
+template <class F> struct aff { F x, y; bool inf; };
+typedef jac<fp> g1;
+typedef jac<fp2> g2;
+typedef aff<fp> g1a;
+typedef aff<fp2> g2a;
+static_assert(sizeof(g1) == 144 && sizeof(g2) == 288 && sizeof(fp12) == 576, "mcl layouts");
+
+inline fp from_u32(const uint32_t *c) {
+    fp r;
+    for (int i = 0; i < 6; i++) r.v[i] = (uint64_t)c[2 * i] | (uint64_t)c[2 * i + 1] << 32;
+    return r;
+}
+static const fp P = from_u32(LCB_P_HOST);
+static const fp ONE = from_u32(LCB_ONE_HOST);
+static const fp R2 = from_u32(LCB_R2_HOST);
+static const fp B1 = from_u32(LCB_B1_HOST);
+static const fp INV2 = from_u32(LCB_INV2_HOST);
+static const uint64_t PINV = LCB_P_INV64_HOST;   // -p^-1 mod 2^64
+
+inline fp zero() { fp r; memset(&r, 0, sizeof r); return r; }
+inline bool is_zero(const fp &a) { return (a.v[0] | a.v[1] | a.v[2] | a.v[3] | a.v[4] | a.v[5]) == 0; }
+inline bool eq(const fp &a, const fp &b) { return memcmp(&a, &b, sizeof a) == 0; }
+inline bool raw_lt_p(const fp &a) {
+    for (int i = 5; i >= 0; i--)
+        if (a.v[i] != P.v[i]) return a.v[i] < P.v[i];
+    return false;
+}
+inline void add(fp &r, const fp &a, const fp &b) {
+    fp t, d;
+    uint64_t c = 0, br = 0;
+    for (int i = 0; i < 6; i++) {
+        u128 s = (u128)a.v[i] + b.v[i] + c;
+        t.v[i] = (uint64_t)s;
+        c = (uint64_t)(s >> 64);
+    }
+    for (int i = 0; i < 6; i++) {           // a + b < 2p < 2^382: no carry out; subtract p unless that borrows
+        u128 x = (u128)t.v[i] - P.v[i] - br;
+        d.v[i] = (uint64_t)x;
+        br = (uint64_t)(x >> 64) & 1;
+    }
+    r = br ? t : d;
+}
+inline void sub(fp &r, const fp &a, const fp &b) {
+    fp t;
+    uint64_t br = 0;
+    for (int i = 0; i < 6; i++) {
+        u128 x = (u128)a.v[i] - b.v[i] - br;
+        t.v[i] = (uint64_t)x;
+        br = (uint64_t)(x >> 64) & 1;
+    }
+    if (br) {
+        uint64_t c = 0;
+        for (int i = 0; i < 6; i++) {
+            u128 s = (u128)t.v[i] + P.v[i] + c;
+            t.v[i] = (uint64_t)s;
+            c = (uint64_t)(s >> 64);
+        }
+    }
+    r = t;
+}
+inline void neg(fp &r, const fp &a) { sub(r, zero(), a); }   // -0 = 0 (field.hpp lcb_fp_neg_asm)
+// CIOS Montgomery product, result fully reduced
+inline void mul(fp &r, const fp &a, const fp &b) {
+    uint64_t t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 6; i++) {
+        uint64_t c = 0;
+        for (int j = 0; j < 6; j++) {
+            u128 s = (u128)a.v[j] * b.v[i] + t[j] + c;
+            t[j] = (uint64_t)s;
+            c = (uint64_t)(s >> 64);
+        }
+        u128 s = (u128)t[6] + c;
+        t[6] = (uint64_t)s;
+        t[7] = (uint64_t)(s >> 64);
+        const uint64_t m = t[0] * PINV;
+        s = (u128)m * P.v[0] + t[0];
+        c = (uint64_t)(s >> 64);
+        for (int j = 1; j < 6; j++) {
+            s = (u128)m * P.v[j] + t[j] + c;
+            t[j - 1] = (uint64_t)s;
+            c = (uint64_t)(s >> 64);
+        }
+        s = (u128)t[6] + c;
+        t[5] = (uint64_t)s;
+        t[6] = t[7] + (uint64_t)(s >> 64);
+    }
+    fp x, d;
+    memcpy(x.v, t, 48);
+    uint64_t br = 0;
+    for (int i = 0; i < 6; i++) {
+        u128 y = (u128)x.v[i] - P.v[i] - br;
+        d.v[i] = (uint64_t)y;
+        br = (uint64_t)(y >> 64) & 1;
+    }
+    r = (t[6] == 0 && br) ? x : d;        // result < 2p
+}
+inline void sqr(fp &r, const fp &a) { mul(r, a, a); }
+inline void from_raw(fp &r, const fp &raw) { mul(r, raw, R2); }
+inline void to_raw(fp &r, const fp &a) {
+    fp one = zero();
+    one.v[0] = 1;
+    mul(r, a, one);
+}
+inline bool is_odd(const fp &a) {
+    fp t;
+    to_raw(t, a);
+    return t.v[0] & 1;
+}
+// a^e, e given as 12 LE u32 limbs (public constants: p - 2, (p + 1) / 4, (p - 3) / 4)
+inline void pow_const(fp &r, const fp &a, const uint32_t *e) {
+    fp acc = ONE;
+    for (int i = 383; i >= 0; i--) {
+        sqr(acc, acc);
+        if ((e[i >> 5] >> (i & 31)) & 1) mul(acc, acc, a);
+    }
+    r = acc;
+}
+inline void inv(fp &r, const fp &a) { pow_const(r, a, LCB_P_MINUS_2_HOST); }  // inv(0) = 0, as on the device
+inline bool sqrt(fp &r, const fp &a) {           // mcl Fp::squareRoot, p = 3 mod 4
+    fp y, t;
+    pow_const(y, a, LCB_P_PLUS1_DIV4_HOST);
+    sqr(t, y);
+    bool ok = eq(t, a);
+    r = y;
+    return ok;
+}
+
+// ---------------------------------------------------------------- Fp2 = Fp[i] / (i^2 + 1)
+inline fp2 zero2() { fp2 r; r.a = zero(); r.b = zero(); return r; }
+inline fp2 one2() { fp2 r; r.a = ONE; r.b = zero(); return r; }
+inline bool is_zero(const fp2 &x) { return is_zero(x.a) && is_zero(x.b); }
+inline bool eq(const fp2 &x, const fp2 &y) { return eq(x.a, y.a) && eq(x.b, y.b); }
+inline void add(fp2 &r, const fp2 &x, const fp2 &y) { add(r.a, x.a, y.a); add(r.b, x.b, y.b); }
+inline void sub(fp2 &r, const fp2 &x, const fp2 &y) { sub(r.a, x.a, y.a); sub(r.b, x.b, y.b); }
+inline void neg(fp2 &r, const fp2 &x) { neg(r.a, x.a); neg(r.b, x.b); }
+inline void mul(fp2 &r, const fp2 &x, const fp2 &y) {
+    fp t0, t1, s0, s1, m;
+    mul(t0, x.a, y.a);
+    mul(t1, x.b, y.b);
+    add(s0, x.a, x.b);
+    add(s1, y.a, y.b);
+    mul(m, s0, s1);
+    sub(r.a, t0, t1);
+    sub(m, m, t0);
+    sub(r.b, m, t1);
+}
+inline void sqr(fp2 &r, const fp2 &x) { mul(r, x, x); }
+inline void mul_fp(fp2 &r, const fp2 &x, const fp &s) { mul(r.a, x.a, s); mul(r.b, x.b, s); }
+inline void mul_xi(fp2 &r, const fp2 &x) {        // (a + b i)(1 + i)
+    fp2 t;
+    sub(t.a, x.a, x.b);
+    add(t.b, x.a, x.b);
+    r = t;
+}
+inline void inv(fp2 &r, const fp2 &x) {
+    fp n, t;
+    sqr(n, x.a);
+    sqr(t, x.b);
+    add(n, n, t);
+    inv(n, n);
+    fp2 y;
+    mul_fp(y, x, n);
+    r.a = y.a;
+    neg(r.b, y.b);
+}
+// field.hpp fp2_sqrt (mcl Fp2T::squareRoot, norm method) — its root choice is visible when x.b == 0
+inline bool sqrt_mcl(fp2 &y, const fp2 &x) {
+    fp t1, t2;
+    if (is_zero(x.b)) {
+        if (sqrt(t1, x.a)) {
+            y.a = t1;
+            y.b = zero();
+        } else {
+            fp na;
+            neg(na, x.a);
+            if (!sqrt(t1, na)) return false;
+            y.a = zero();
+            y.b = t1;
+        }
+        return true;
+    }
+    sqr(t1, x.a);
+    sqr(t2, x.b);
+    add(t1, t1, t2);
+    if (!sqrt(t1, t1)) return false;
+    add(t2, x.a, t1);
+    mul(t2, t2, INV2);
+    if (!sqrt(t2, t2)) {
+        sub(t2, x.a, t1);
+        mul(t2, t2, INV2);
+        if (!sqrt(t2, t2)) return false;
+    }
+    y.a = t2;
+    add(t2, t2, t2);
+    inv(t2, t2);
+    mul(y.b, x.b, t2);
+    return true;
+}
+// a root for G2 decompression (the caller fixes the sign): field.hpp fp2_sqrt_any — for x.b != 0 both roots have
+// nonzero a and b parts, so the sign flag selects one whatever root is found; for x.b == 0 the mcl order is kept
+inline bool sqrt_any(fp2 &y, const fp2 &x) {
+    if (is_zero(x.b)) return sqrt_mcl(y, x);
+    fp t, u, c, s, cs, bs;
+    sqr(t, x.a);
+    sqr(u, x.b);
+    add(t, t, u);
+    if (!sqrt(t, t)) return false;
+    add(c, x.a, t);
+    mul(c, c, INV2);
+    pow_const(s, c, LCB_P_MINUS3_DIV4_HOST);
+    sqr(u, s);
+    mul(u, u, c);
+    mul(bs, x.b, s);
+    mul(bs, bs, INV2);
+    mul(cs, c, s);
+    fp2 r;
+    if (eq(u, ONE)) {
+        r.a = cs;
+        r.b = bs;
+    } else {
+        r.a = bs;
+        neg(r.b, cs);
+    }
+    fp2 chk;
+    sqr(chk, r);
+    if (!eq(chk, x)) return false;
+    y = r;
+    return true;
+}
+
+// ---------------------------------------------------------------- Fp6 = Fp2[v] / (v^3 - xi), Fp12 = Fp6[w] / (w^2 - v)
+inline void add(fp6 &r, const fp6 &x, const fp6 &y) { add(r.c0, x.c0, y.c0); add(r.c1, x.c1, y.c1); add(r.c2, x.c2, y.c2); }
+inline void sub(fp6 &r, const fp6 &x, const fp6 &y) { sub(r.c0, x.c0, y.c0); sub(r.c1, x.c1, y.c1); sub(r.c2, x.c2, y.c2); }
+inline void mul(fp6 &r, const fp6 &a, const fp6 &b) {
+    fp2 t0, t1, t2, s, u, c0, c1, c2;
+    mul(t0, a.c0, b.c0);
+    mul(t1, a.c1, b.c1);
+    mul(t2, a.c2, b.c2);
+    // c0 = t0 + xi ((a1 + a2)(b1 + b2) - t1 - t2)
+    add(s, a.c1, a.c2);
+    add(u, b.c1, b.c2);
+    mul(s, s, u);
+    sub(s, s, t1);
+    sub(s, s, t2);
+    mul_xi(s, s);
+    add(c0, t0, s);
+    // c1 = (a0 + a1)(b0 + b1) - t0 - t1 + xi t2
+    add(s, a.c0, a.c1);
+    add(u, b.c0, b.c1);
+    mul(s, s, u);
+    sub(s, s, t0);
+    sub(s, s, t1);
+    mul_xi(u, t2);
+    add(c1, s, u);
+    // c2 = (a0 + a2)(b0 + b2) - t0 - t2 + t1
+    add(s, a.c0, a.c2);
+    add(u, b.c0, b.c2);
+    mul(s, s, u);
+    sub(s, s, t0);
+    sub(s, s, t2);
+    add(c2, s, t1);
+    r.c0 = c0;
+    r.c1 = c1;
+    r.c2 = c2;
+}
+inline void mul_v(fp6 &r, const fp6 &a) {         // a v = (xi c2, c0, c1)
+    fp6 t;
+    mul_xi(t.c0, a.c2);
+    t.c1 = a.c0;
+    t.c2 = a.c1;
+    r = t;
+}
+inline void mul(fp12 &r, const fp12 &a, const fp12 &b) {
+    fp6 t0, t1, s, u;
+    mul(t0, a.c0, b.c0);
+    mul(t1, a.c1, b.c1);
+    add(s, a.c0, a.c1);
+    add(u, b.c0, b.c1);
+    mul(s, s, u);
+    sub(s, s, t0);
+    sub(r.c1, s, t1);
+    mul_v(u, t1);
+    add(r.c0, t0, u);
+}
+
+// ---------------------------------------------------------------- curves (curve.hpp's formulas, same special cases)
+template <class F> inline void set_one(F &r);
+template <> inline void set_one<fp>(fp &r) { r = ONE; }
+template <> inline void set_one<fp2>(fp2 &r) { r = one2(); }
+template <class F> inline void set_zero(F &r) { memset(&r, 0, sizeof r); }
+
+template <class F> inline bool jac_is_inf(const jac<F> &p) { return is_zero(p.z); }
+template <class F> inline void jac_set_inf(jac<F> &p) { set_one(p.x); set_one(p.y); set_zero(p.z); }
+template <class F> inline void jac_from_aff(jac<F> &r, const aff<F> &a) {
+    if (a.inf) { jac_set_inf(r); return; }
+    r.x = a.x;
+    r.y = a.y;
+    set_one(r.z);
+}
+template <class F> inline void jac_dbl(jac<F> &r, const jac<F> &p) {        // dbl-2009-l (a = 0)
+    F A, B, C, D, E, Fv, t, x3, y3, z3;
+    sqr(A, p.x);
+    sqr(B, p.y);
+    sqr(C, B);
+    add(D, p.x, B);
+    sqr(D, D);
+    sub(D, D, A);
+    sub(D, D, C);
+    add(D, D, D);
+    add(E, A, A);
+    add(E, E, A);
+    sqr(Fv, E);
+    add(t, D, D);
+    sub(x3, Fv, t);
+    sub(t, D, x3);
+    mul(y3, E, t);
+    add(t, C, C);
+    add(t, t, t);
+    add(t, t, t);
+    sub(y3, y3, t);
+    mul(z3, p.y, p.z);
+    add(z3, z3, z3);
+    r.x = x3;
+    r.y = y3;
+    r.z = z3;
+}
+template <class F> inline void jac_add(jac<F> &r, const jac<F> &p, const jac<F> &q) {   // add-2007-bl
+    if (jac_is_inf(p)) { r = q; return; }
+    if (jac_is_inf(q)) { r = p; return; }
+    F z1z1, z2z2, u1, u2, s1, s2, h, i, j, rr, v, t, x3, y3, z3;
+    sqr(z1z1, p.z);
+    sqr(z2z2, q.z);
+    mul(u1, p.x, z2z2);
+    mul(u2, q.x, z1z1);
+    mul(s1, p.y, q.z);
+    mul(s1, s1, z2z2);
+    mul(s2, q.y, p.z);
+    mul(s2, s2, z1z1);
+    if (eq(u1, u2)) {
+        if (eq(s1, s2)) { jac_dbl(r, p); return; }
+        jac_set_inf(r);
+        return;
+    }
+    sub(h, u2, u1);
+    add(i, h, h);
+    sqr(i, i);
+    mul(j, h, i);
+    sub(rr, s2, s1);
+    add(rr, rr, rr);
+    mul(v, u1, i);
+    sqr(x3, rr);
+    sub(x3, x3, j);
+    sub(x3, x3, v);
+    sub(x3, x3, v);
+    sub(t, v, x3);
+    mul(y3, rr, t);
+    mul(t, s1, j);
+    add(t, t, t);
+    sub(y3, y3, t);
+    add(z3, p.z, q.z);
+    sqr(z3, z3);
+    sub(z3, z3, z1z1);
+    sub(z3, z3, z2z2);
+    mul(z3, z3, h);
+    r.x = x3;
+    r.y = y3;
+    r.z = z3;
+}
+template <class F> inline void jac_neg(jac<F> &r, const jac<F> &p) { r.x = p.x; neg(r.y, p.y); r.z = p.z; }
+template <class F> inline void jac_to_aff(aff<F> &a, const jac<F> &p) {
+    if (jac_is_inf(p)) { a.inf = true; set_zero(a.x); set_zero(a.y); return; }
+    F zi, zi2;
+    inv(zi, p.z);
+    sqr(zi2, zi);
+    mul(a.x, p.x, zi2);
+    mul(zi2, zi2, zi);
+    mul(a.y, p.y, zi2);
+    a.inf = false;
+}
+template <class F> inline void jac_normalize(jac<F> &r, const jac<F> &p) {
+    aff<F> a;
+    jac_to_aff(a, p);
+    jac<F> q;
+    jac_from_aff(q, a);
+    if (a.inf) jac_set_inf(q);
+    r = q;
+}
+template <class F> inline bool jac_eq(const jac<F> &p, const jac<F> &q) {
+    bool pi = jac_is_inf(p), qi = jac_is_inf(q);
+    if (pi || qi) return pi && qi;
+    F z1z1, z2z2, u1, u2, s1, s2;
+    sqr(z1z1, p.z);
+    sqr(z2z2, q.z);
+    mul(u1, p.x, z2z2);
+    mul(u2, q.x, z1z1);
+    mul(s1, p.y, q.z);
+    mul(s1, s1, z2z2);
+    mul(s2, q.y, p.z);
+    mul(s2, s2, z1z1);
+    return eq(u1, u2) && eq(s1, s2);
+}
+inline fp2 b2() { fp2 r; r.a = from_u32(LCB_B2_HOST); r.b = from_u32(LCB_B2_HOST + 12); return r; }
+inline void curve_b(fp &r) { r = B1; }
+inline void curve_b(fp2 &r) { r = b2(); }
+// Y^2 = X^3 + b Z^6 (infinity counts as on the curve)
+template <class F> inline bool jac_on_curve(const jac<F> &p) {
+    if (jac_is_inf(p)) return true;
+    F l, r, z2, z6, b;
+    sqr(l, p.y);
+    sqr(r, p.x);
+    mul(r, r, p.x);
+    sqr(z2, p.z);
+    mul(z6, z2, z2);
+    mul(z6, z6, z2);
+    curve_b(b);
+    mul(z6, z6, b);
+    add(r, r, z6);
+    return eq(l, r);
+}
+inline bool limbs_ok(const fp &a) { return raw_lt_p(a); }
+inline bool limbs_ok(const fp2 &a) { return raw_lt_p(a.a) && raw_lt_p(a.b); }
+template <class F> inline bool jac_valid(const jac<F> &p) {
+    return limbs_ok(p.x) && limbs_ok(p.y) && limbs_ok(p.z) && jac_on_curve(p);
+}
+
+// ---------------------------------------------------------------- wire formats (curve.hpp g1/g2 (de)compress)
+inline void bytes_to_raw(fp &r, const uint8_t *b) { memcpy(r.v, b, 48); }
+inline void raw_to_bytes(uint8_t *b, const fp &r) { memcpy(b, r.v, 48); }
+inline bool g1_decompress(g1a &out, const uint8_t b[48]) {
+    fp raw;
+    bytes_to_raw(raw, b);
+    if (is_zero(raw)) { out.inf = true; out.x = zero(); out.y = zero(); return true; }
+    const bool odd = raw.v[5] >> 63;
+    raw.v[5] &= 0x7fffffffffffffffull;
+    if (!raw_lt_p(raw)) return false;
+    fp x, t, y;
+    from_raw(x, raw);
+    sqr(t, x);
+    mul(t, t, x);
+    add(t, t, B1);
+    if (!sqrt(y, t)) return false;
+    if (is_odd(y) != odd) neg(y, y);
+    out.x = x;
+    out.y = y;
+    out.inf = false;
+    return true;
+}
+inline void g1_compress(uint8_t b[48], const g1 &p) {
+    g1a a;
+    jac_to_aff(a, p);
+    if (a.inf) { memset(b, 0, 48); return; }
+    fp rx, ry;
+    to_raw(rx, a.x);
+    to_raw(ry, a.y);
+    if (ry.v[0] & 1) rx.v[5] |= 0x8000000000000000ull;
+    raw_to_bytes(b, rx);
+}
+// sign_b: the G2 sign flag is the parity of y.b instead of y.a (lcb_set_g2_sign_from_b; unpinned mcl convention)
+inline bool g2_decompress(g2a &out, const uint8_t b[96], bool sign_b) {
+    fp ra, rb;
+    bytes_to_raw(ra, b);
+    bytes_to_raw(rb, b + 48);
+    if (is_zero(ra) && is_zero(rb)) { out.inf = true; out.x = zero2(); out.y = zero2(); return true; }
+    const bool odd = rb.v[5] >> 63;
+    rb.v[5] &= 0x7fffffffffffffffull;
+    if (!raw_lt_p(ra) || !raw_lt_p(rb)) return false;
+    fp2 x, t, y;
+    from_raw(x.a, ra);
+    from_raw(x.b, rb);
+    sqr(t, x);
+    mul(t, t, x);
+    add(t, t, b2());
+    if (!sqrt_any(y, t)) return false;
+    if (is_odd(sign_b ? y.b : y.a) != odd) neg(y, y);
+    out.x = x;
+    out.y = y;
+    out.inf = false;
+    return true;
+}
+inline void g2_compress(uint8_t b[96], const g2 &p, bool sign_b) {
+    g2a a;
+    jac_to_aff(a, p);
+    if (a.inf) { memset(b, 0, 96); return; }
+    fp xa, xb, ys;
+    to_raw(xa, a.x.a);
+    to_raw(xb, a.x.b);
+    to_raw(ys, sign_b ? a.y.b : a.y.a);
+    if (ys.v[0] & 1) xb.v[5] |= 0x8000000000000000ull;
+    raw_to_bytes(b, xa);
+    raw_to_bytes(b + 48, xb);
+}
+inline void g1_generator(g1 &g) {
+    g.x = from_u32(LCB_G1_GEN_HOST);
+    g.y = from_u32(LCB_G1_GEN_HOST + 12);
+    g.z = ONE;
+}
+inline void g2_generator(g2 &g) {
+    g.x.a = from_u32(LCB_G2_GEN_HOST);
+    g.x.b = from_u32(LCB_G2_GEN_HOST + 12);
+    g.y.a = from_u32(LCB_G2_GEN_HOST + 24);
+    g.y.b = from_u32(LCB_G2_GEN_HOST + 36);
+    g.z = one2();
+}
+} // namespace fph

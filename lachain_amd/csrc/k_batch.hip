@@ -35,6 +35,7 @@
 #include "rlc_common.hpp"
 
 LCB_ASM_LIBRARY(k_batch)
+LCB_TU_CONFIG(k_batch)
 
 // ---------------------------------------------------------------- level-1 groups: runs of one ciphertext / message
 // one lane per share; the first share of a run emits the run as groups of at most `cap` shares.

@@ -5,6 +5,7 @@
 #include "coop.hpp"
 
 LCB_ASM_LIBRARY(k_coop)
+LCB_TU_CONFIG(k_coop)
 
 // TPKE group check Miller pair (k_tpke_rlc_miller's function): f = f_{|z|,H}(sum s_i U_i) f_{|z|,W}(-sum s_i Y_i)
 // conjugated, from the ciphertext's two normalised line sets.  Lanes 3..6 evaluate the line coefficients

@@ -16,6 +16,7 @@
 #include "kcommon.hpp"
 
 LCB_ASM_LIBRARY(k_dkg)
+LCB_TU_CONFIG(k_dkg)
 
 DI u32 dkg_index(u32 i, u32 j) {   // Commitment.Index: symmetric, i <= j
     if (i > j) { u32 t = i; i = j; j = t; }

@@ -5,6 +5,7 @@
 #include "coop.hpp"
 
 LCB_ASM_LIBRARY(k_mcl)
+LCB_TU_CONFIG(k_mcl)
 
 // mclBn_pairing(P, Q) (GT.Pairing in the reference, e.g. TPKE/PublicKey.cs:91) as a one-group cooperative check:
 // P and the point at infinity as the group's two G1 points, Q's line set and the set of infinity (every line 1).

@@ -19,6 +19,7 @@
 #include <hipcub/hipcub.hpp>
 
 LCB_ASM_LIBRARY(k_msm)
+LCB_TU_CONFIG(k_msm)
 
 // s mod r for any 256-bit s (2^256 < 3r: at most two subtractions)
 DI void fr_raw_reduce(fr &s) {

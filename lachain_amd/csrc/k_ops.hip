@@ -2,6 +2,7 @@
 #include "kcommon.hpp"
 
 LCB_ASM_LIBRARY(k_ops)
+LCB_TU_CONFIG(k_ops)
 
 // ================================================================================= single operations
 // One lane executes one mcl-shaped operation on mcl-layout structs held in `io` (u32 words).

@@ -7,6 +7,7 @@
 #include "rlc_common.hpp"
 
 LCB_ASM_LIBRARY(k_rlc_rand)
+LCB_TU_CONFIG(k_rlc_rand)
 
 extern "C" __global__ void LCB_BOUNDS k_rlc_key_tables(const g1a_st *keys, u32 n_keys, u32 *jtab, u32 *pre, u32 *tab,
                                                       uint8_t *ktab_ok) {

@@ -2,6 +2,7 @@
 #include "kcommon.hpp"
 
 LCB_ASM_LIBRARY(k_scalar)
+LCB_TU_CONFIG(k_scalar)
 
 // ================================================================================= scalar multiplication
 // out[i] = s_i * P_i (or s_i * generator), serialized; scalars are canonical 32-byte LE (< r checked)

@@ -3,6 +3,7 @@
 #include "fe_asm.hpp"
 
 LCB_ASM_LIBRARY(k_tpke)
+LCB_TU_CONFIG(k_tpke)
 LCB_ASM_TOWER_LIBRARY(k_tpke)
 
 // ================================================================================= decompression

@@ -2,6 +2,7 @@
 #include "kcommon.hpp"
 
 LCB_ASM_LIBRARY(k_ts)
+LCB_TU_CONFIG(k_ts)
 
 // ================================================================================= threshold signatures
 extern "C" __global__ void LCB_BOUNDS k_ts_msg_prepare(const uint8_t *msg_data, const u32 *msg_off, u32 n_msgs,

@@ -52,6 +52,12 @@ DI void fp12_load_soa_fresh(fp12 &f, const u32 *base, size_t n, size_t i) {
     fp12_load_soa(f, base, n, i);
 }
 
+// per-unit configuration setter (curve.hpp lcb_g2_sign_b): one per kernel translation unit, called by
+// lcbk_set_g2_sign_b (lcb_host.cpp) for every unit
+#define LCB_TU_CONFIG(tag)                                                                                        \
+    extern "C" int lcbk_cfg_##tag(u32 sign_b) {                                                                 \
+        return hipMemcpyToSymbol(HIP_SYMBOL(lcb_g2_sign_b), &sign_b, sizeof sign_b) == hipSuccess ? 0 : -1;     \
+    }
 #define LCB_LAUNCH(name, ...) hipLaunchKernelGGL(name, grid, dim3(LCB_BLOCK), 0, s, __VA_ARGS__)
 static_assert(sizeof(g1a_st) == 112 && sizeof(g2a_st) == 208, "record sizes");
 static_assert(sizeof(g1) == 144 && sizeof(g2) == 288 && sizeof(fr) == 32, "struct sizes");

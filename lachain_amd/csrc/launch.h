@@ -30,6 +30,8 @@ extern "C" void lcbk_ts_sign(dim3 grid, hipStream_t s, const uint8_t *sks, const
 extern "C" void lcbk_lagrange_coeffs(dim3 grid, hipStream_t s, const uint8_t *xs, const u32 *off, u32 n_problems, void *lam_raw, uint8_t *status);
 extern "C" void lcbk_g1_mul_lanes(dim3 grid, hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out);
 extern "C" void lcbk_g2_mul_lanes(dim3 grid, hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out, const void *dec, u32 n_dec, const u32 *src);
+// two entries per lane (n_entries even, problems at even offsets): shared doublings for two points of G2
+extern "C" void lcbk_g2_mul2_lanes(hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out, const void *dec, u32 n_dec, const u32 *src);
 extern "C" void lcbk_g1_sum(dim3 grid, hipStream_t s, const void *parts, const uint8_t *ok_in, const u32 *off, u32 n_problems, uint8_t *status, uint8_t *out);
 extern "C" void lcbk_g2_sum(dim3 grid, hipStream_t s, const void *parts, const uint8_t *ok_in, const u32 *off, u32 n_problems, uint8_t *status, uint8_t *out);
 extern "C" void lcbk_msm_digits(dim3 grid, hipStream_t s, const uint8_t *scalars, u32 n, u32 c, u32 nwin, u32 *keys, u32 *vals);
@@ -104,3 +106,30 @@ extern "C" void lcbk_op(dim3 grid, hipStream_t s, int op, u32 *io, int orig_cof)
 #define LCB_G1_JAC_BYTES 144
 #define LCB_G2_JAC_BYTES 288
 #define LCB_LINESET_BYTES 26368   /* pairing.hpp LCB_LINESET_WORDS * 4 */
+extern "C" int lcbk_cfg_k_batch(u32 sign_b);
+extern "C" int lcbk_cfg_k_coop(u32 sign_b);
+extern "C" int lcbk_cfg_k_dkg(u32 sign_b);
+extern "C" int lcbk_cfg_k_lagrange(u32 sign_b);
+extern "C" int lcbk_cfg_k_mcl(u32 sign_b);
+extern "C" int lcbk_cfg_k_msm(u32 sign_b);
+extern "C" int lcbk_cfg_k_ops(u32 sign_b);
+extern "C" int lcbk_cfg_k_rlc_rand(u32 sign_b);
+extern "C" int lcbk_cfg_k_scalar(u32 sign_b);
+extern "C" int lcbk_cfg_k_tpke(u32 sign_b);
+extern "C" int lcbk_cfg_k_ts(u32 sign_b);
+// every kernel unit's G2 sign-flag convention (curve.hpp lcb_g2_sign_b)
+static inline int lcbk_set_g2_sign_b(int sign_b) {
+    int rc = 0;
+    rc |= lcbk_cfg_k_batch((u32)sign_b);
+    rc |= lcbk_cfg_k_coop((u32)sign_b);
+    rc |= lcbk_cfg_k_dkg((u32)sign_b);
+    rc |= lcbk_cfg_k_lagrange((u32)sign_b);
+    rc |= lcbk_cfg_k_mcl((u32)sign_b);
+    rc |= lcbk_cfg_k_msm((u32)sign_b);
+    rc |= lcbk_cfg_k_ops((u32)sign_b);
+    rc |= lcbk_cfg_k_rlc_rand((u32)sign_b);
+    rc |= lcbk_cfg_k_scalar((u32)sign_b);
+    rc |= lcbk_cfg_k_tpke((u32)sign_b);
+    rc |= lcbk_cfg_k_ts((u32)sign_b);
+    return rc;
+}

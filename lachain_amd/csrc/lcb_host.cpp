@@ -34,6 +34,7 @@
 #include "lcb_ctx.hpp"
 #include "lcb_internal.hpp"
 #include "fr_host.hpp"
+#include "fp_host.hpp"
 
 #define LCB_BLOCK 256
 
@@ -293,37 +294,9 @@ extern "C" void mclBnFr_div(mclBnFr *z, const mclBnFr *x, const mclBnFr *y) {
     mclBnFr_mul(z, x, &t);
 }
 
-// ================================================================== G1
-extern "C" mclSize mclBnG1_serialize(void *buf, mclSize max, const mclBnG1 *x) {
-    if (max < 48) return 0;
-    LOCKED_OR(0)
-    memcpy(IOH + 36, x, 144);
-    if (!run_op(OP_G1_SER, 72, 128)) return 0;
-    memcpy(buf, IOH + 116, 48);
-    return 48;
-}
-extern "C" mclSize mclBnG1_deserialize(mclBnG1 *x, const void *buf, mclSize n) {
-    if (n < 48) return 0;
-    LOCKED_OR(0)
-    memcpy(IOH + 116, buf, 48);
-    if (!run_op(OP_G1_DESER, 128, 129) || !IOH[128]) return 0;
-    memcpy(x, IOH, 144);
-    return 48;
-}
-static int g1_flag_op(int op, const mclBnG1 *x, const mclBnG1 *y) {
-    LOCKED_OR(0)
-    memcpy(IOH + 36, x, 144);
-    if (y) memcpy(IOH + 72, y, 144);
-    if (!run_op(op, 108, 129)) return 0;
-    return (int)IOH[128];
-}
-extern "C" int mclBnG1_isValid(const mclBnG1 *x) { return g1_flag_op(OP_G1_VALID, x, nullptr); }
-extern "C" int mclBnG1_isEqual(const mclBnG1 *x, const mclBnG1 *y) { return g1_flag_op(OP_G1_EQ, x, y); }
-extern "C" int mclBnG1_isZero(const mclBnG1 *x) {
-    static const u32 z[12] = {0};
-    return memcmp(&x->z, z, 48) == 0;
-}
-extern "C" void mclBnG1_clear(mclBnG1 *x) { memset(x, 0, sizeof *x); }
+// ================================================================== G1 / G2 (host field work, fp_host.hpp)
+// O(1) field work runs on the host like Fr (fp_host.hpp header); G1 / G2 multiplication, the hash to G2 and the
+// pairing below stay on the GPU.  Bit-identical to the kernels' results (same formulas, fully reduced residues).
 static void g1_op(int op, mclBnG1 *z, const mclBnG1 *x, const mclBnG1 *y, const mclBnFr *k) {
     if (!stage_ready()) { fail_out(z, 144); return; }
     memcpy(IOH + 36, x, 144);
@@ -332,48 +305,61 @@ static void g1_op(int op, mclBnG1 *z, const mclBnG1 *x, const mclBnG1 *y, const 
     if (run_op(op, 116, 36)) memcpy(z, IOH, 144);
     else fail_out(z, 144);
 }
-extern "C" void mclBnG1_neg(mclBnG1 *y, const mclBnG1 *x) { g1_op(OP_G1_NEG, y, x, nullptr, nullptr); }
-extern "C" void mclBnG1_dbl(mclBnG1 *y, const mclBnG1 *x) { g1_op(OP_G1_DBL, y, x, nullptr, nullptr); }
-extern "C" void mclBnG1_normalize(mclBnG1 *y, const mclBnG1 *x) { g1_op(OP_G1_NORM, y, x, nullptr, nullptr); }
-extern "C" void mclBnG1_add(mclBnG1 *z, const mclBnG1 *x, const mclBnG1 *y) { g1_op(OP_G1_ADD, z, x, y, nullptr); }
+std::atomic<int> g_g2_sign_b{0};      // lcb_set_g2_sign_from_b: the G2 wire flag is parity(y.b) instead of parity(y.a)
+static inline fph::g1 *G1W(mclBnG1 *x) { return (fph::g1 *)x; }
+static inline const fph::g1 *G1R(const mclBnG1 *x) { return (const fph::g1 *)x; }
+static inline fph::g2 *G2W(mclBnG2 *x) { return (fph::g2 *)x; }
+static inline const fph::g2 *G2R(const mclBnG2 *x) { return (const fph::g2 *)x; }
+extern "C" mclSize mclBnG1_serialize(void *buf, mclSize max, const mclBnG1 *x) {
+    if (max < 48) return 0;
+    fph::g1_compress((uint8_t *)buf, *G1R(x));
+    return 48;
+}
+extern "C" mclSize mclBnG1_deserialize(mclBnG1 *x, const void *buf, mclSize n) {
+    if (n < 48) return 0;
+    fph::g1a a;
+    if (!fph::g1_decompress(a, (const uint8_t *)buf)) return 0;
+    fph::jac_from_aff(*G1W(x), a);
+    return 48;
+}
+extern "C" int mclBnG1_isValid(const mclBnG1 *x) { return fph::jac_valid(*G1R(x)); }
+extern "C" int mclBnG1_isEqual(const mclBnG1 *x, const mclBnG1 *y) { return fph::jac_eq(*G1R(x), *G1R(y)); }
+extern "C" int mclBnG1_isZero(const mclBnG1 *x) {
+    static const u32 z[12] = {0};
+    return memcmp(&x->z, z, 48) == 0;
+}
+extern "C" void mclBnG1_clear(mclBnG1 *x) { memset(x, 0, sizeof *x); }
+extern "C" void mclBnG1_neg(mclBnG1 *y, const mclBnG1 *x) { fph::jac_neg(*G1W(y), *G1R(x)); }
+extern "C" void mclBnG1_dbl(mclBnG1 *y, const mclBnG1 *x) { fph::g1 t; fph::jac_dbl(t, *G1R(x)); *G1W(y) = t; }
+extern "C" void mclBnG1_normalize(mclBnG1 *y, const mclBnG1 *x) { fph::jac_normalize(*G1W(y), *G1R(x)); }
+extern "C" void mclBnG1_add(mclBnG1 *z, const mclBnG1 *x, const mclBnG1 *y) {
+    fph::g1 t;
+    fph::jac_add(t, *G1R(x), *G1R(y));
+    *G1W(z) = t;
+}
 extern "C" void mclBnG1_sub(mclBnG1 *z, const mclBnG1 *x, const mclBnG1 *y) {
-    mclBnG1 ny;
-    mclBnG1_neg(&ny, y);
-    mclBnG1_add(z, x, &ny);
+    fph::g1 ny, t;
+    fph::jac_neg(ny, *G1R(y));
+    fph::jac_add(t, *G1R(x), ny);
+    *G1W(z) = t;
 }
 extern "C" void mclBnG1_mul(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y) { g1_op(OP_G1_MUL, z, x, nullptr, y); }
-extern "C" void lcb_g1_generator(mclBnG1 *g) {
-    if (!stage_ready()) { fail_out(g, 144); return; }
-    if (run_op(OP_G1_GEN, 0, 36)) memcpy(g, IOH, 144);
-    else fail_out(g, 144);
-}
+extern "C" void lcb_g1_generator(mclBnG1 *g) { fph::g1_generator(*G1W(g)); }
 
-// ================================================================== G2
 extern "C" mclSize mclBnG2_serialize(void *buf, mclSize max, const mclBnG2 *x) {
     if (max < 96) return 0;
-    LOCKED_OR(0)
-    memcpy(IOH + 72, x, 288);
-    if (!run_op(OP_G2_SER, 144, 248)) return 0;
-    memcpy(buf, IOH + 224, 96);
+    fph::g2_compress((uint8_t *)buf, *G2R(x), g_g2_sign_b.load() != 0);
     return 96;
 }
 extern "C" mclSize mclBnG2_deserialize(mclBnG2 *x, const void *buf, mclSize n) {
     if (n < 96) return 0;
-    LOCKED_OR(0)
-    memcpy(IOH + 224, buf, 96);
-    if (!run_op(OP_G2_DESER, 248, 249) || !IOH[248]) return 0;
-    memcpy(x, IOH, 288);
+    fph::g2a a;
+    if (!fph::g2_decompress(a, (const uint8_t *)buf, g_g2_sign_b.load() != 0)) return 0;
+    fph::jac_from_aff(*G2W(x), a);
     return 96;
 }
-static int g2_flag_op(int op, const mclBnG2 *x, const mclBnG2 *y) {
-    LOCKED_OR(0)
-    memcpy(IOH + 72, x, 288);
-    if (y) memcpy(IOH + 144, y, 288);
-    if (!run_op(op, 216, 249)) return 0;
-    return (int)IOH[248];
-}
-extern "C" int mclBnG2_isValid(const mclBnG2 *x) { return g2_flag_op(OP_G2_VALID, x, nullptr); }
-extern "C" int mclBnG2_isEqual(const mclBnG2 *x, const mclBnG2 *y) { return g2_flag_op(OP_G2_EQ, x, y); }
+extern "C" int mclBnG2_isValid(const mclBnG2 *x) { return fph::jac_valid(*G2R(x)); }
+extern "C" int mclBnG2_isEqual(const mclBnG2 *x, const mclBnG2 *y) { return fph::jac_eq(*G2R(x), *G2R(y)); }
 extern "C" int mclBnG2_isZero(const mclBnG2 *x) {
     static const u32 z[24] = {0};
     return memcmp(&x->z, z, 96) == 0;
@@ -396,21 +382,22 @@ static void g2_op(int op, mclBnG2 *z, const mclBnG2 *x, const mclBnG2 *y, const 
     if (run_op(op, 224, 72)) memcpy(z, IOH, 288);
     else fail_out(z, 288);
 }
-extern "C" void mclBnG2_neg(mclBnG2 *y, const mclBnG2 *x) { g2_op(OP_G2_NEG, y, x, nullptr, nullptr); }
-extern "C" void mclBnG2_dbl(mclBnG2 *y, const mclBnG2 *x) { g2_op(OP_G2_DBL, y, x, nullptr, nullptr); }
-extern "C" void mclBnG2_normalize(mclBnG2 *y, const mclBnG2 *x) { g2_op(OP_G2_NORM, y, x, nullptr, nullptr); }
-extern "C" void mclBnG2_add(mclBnG2 *z, const mclBnG2 *x, const mclBnG2 *y) { g2_op(OP_G2_ADD, z, x, y, nullptr); }
+extern "C" void mclBnG2_neg(mclBnG2 *y, const mclBnG2 *x) { fph::jac_neg(*G2W(y), *G2R(x)); }
+extern "C" void mclBnG2_dbl(mclBnG2 *y, const mclBnG2 *x) { fph::g2 t; fph::jac_dbl(t, *G2R(x)); *G2W(y) = t; }
+extern "C" void mclBnG2_normalize(mclBnG2 *y, const mclBnG2 *x) { fph::jac_normalize(*G2W(y), *G2R(x)); }
+extern "C" void mclBnG2_add(mclBnG2 *z, const mclBnG2 *x, const mclBnG2 *y) {
+    fph::g2 t;
+    fph::jac_add(t, *G2R(x), *G2R(y));
+    *G2W(z) = t;
+}
 extern "C" void mclBnG2_sub(mclBnG2 *z, const mclBnG2 *x, const mclBnG2 *y) {
-    mclBnG2 ny;
-    mclBnG2_neg(&ny, y);
-    mclBnG2_add(z, x, &ny);
+    fph::g2 ny, t;
+    fph::jac_neg(ny, *G2R(y));
+    fph::jac_add(t, *G2R(x), ny);
+    *G2W(z) = t;
 }
 extern "C" void mclBnG2_mul(mclBnG2 *z, const mclBnG2 *x, const mclBnFr *y) { g2_op(OP_G2_MUL, z, x, nullptr, y); }
-extern "C" void lcb_g2_generator(mclBnG2 *g) {
-    if (!stage_ready()) { fail_out(g, 288); return; }
-    if (run_op(OP_G2_GEN, 0, 72)) memcpy(g, IOH, 288);
-    else fail_out(g, 288);
-}
+extern "C" void lcb_g2_generator(mclBnG2 *g) { fph::g2_generator(*G2W(g)); }
 
 // ================================================================== GT / pairing
 static void pair_op(int op, mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) {
@@ -436,7 +423,7 @@ extern "C" void mclBn_millerLoopVec(mclBnGT *z, const mclBnG1 *x, const mclBnG2 
     for (mclSize i = 0; i < n && g_err_count == errs; i++) {
         mclBn_millerLoop(&t, &x[i], &y[i]);
         if (i == 0) acc = t;
-        else gt_op(OP_GT_MUL, &acc, &acc, &t, nullptr);
+        else mclBnGT_mul(&acc, &acc, &t);
     }
     if (g_err_count != errs) fail_out(&acc, 576);
     *z = acc;
@@ -450,7 +437,11 @@ extern "C" int lcb_debug_fp12(int which, const uint32_t in[144], uint32_t out[14
     memcpy(out, IOH, 576);
     return 0;
 }
-extern "C" void mclBnGT_mul(mclBnGT *z, const mclBnGT *x, const mclBnGT *y) { gt_op(OP_GT_MUL, z, x, y, nullptr); }
+extern "C" void mclBnGT_mul(mclBnGT *z, const mclBnGT *x, const mclBnGT *y) {
+    fph::fp12 t;
+    fph::mul(t, *(const fph::fp12 *)x, *(const fph::fp12 *)y);
+    memcpy(z, &t, 576);
+}
 extern "C" void mclBnGT_pow(mclBnGT *z, const mclBnGT *x, const mclBnFr *y) { gt_op(OP_GT_POW, z, x, nullptr, y); }
 extern "C" int mclBnGT_isEqual(const mclBnGT *x, const mclBnGT *y) { return memcmp(x, y, 576) == 0; }
 extern "C" int mclBnGT_isOne(const mclBnGT *x) {
@@ -468,19 +459,35 @@ extern "C" int mclBnGT_isZero(const mclBnGT *x) {
 extern "C" void mclBnGT_clear(mclBnGT *x) { memset(x, 0, sizeof *x); }
 extern "C" mclSize mclBnGT_serialize(void *buf, mclSize max, const mclBnGT *x) {
     if (max < 576) return 0;
-    LOCKED_OR(0)
-    memcpy(IOH + 252, x, 576);
-    if (!run_op(OP_GT_SER, 396, 144)) return 0;
-    memcpy(buf, IOH, 576);
+    const fph::fp *a = (const fph::fp *)x;
+    uint8_t *b = (uint8_t *)buf;
+    for (int i = 0; i < 12; i++) {
+        fph::fp r;
+        fph::to_raw(r, a[i]);
+        memcpy(b + 48 * i, r.v, 48);
+    }
     return 576;
 }
 extern "C" mclSize mclBnGT_deserialize(mclBnGT *x, const void *buf, mclSize n) {
     if (n < 576) return 0;
-    LOCKED_OR(0)
-    memcpy(IOH + 252, buf, 576);
-    if (!run_op(OP_GT_DESER, 396, 549) || !IOH[548]) return 0;
-    memcpy(x, IOH, 576);
+    fph::fp m[12];
+    for (int i = 0; i < 12; i++) {
+        fph::fp raw;
+        memcpy(raw.v, (const uint8_t *)buf + 48 * i, 48);
+        if (!fph::raw_lt_p(raw)) return 0;
+        fph::from_raw(m[i], raw);
+    }
+    memcpy(x, m, 576);
     return 576;
+}
+extern "C" int lcb_set_g2_sign_from_b(int use_b) {
+    // unpinned mcl convention: which coordinate's parity the G2 wire flag carries.  Applies to every
+    // later call, host (de)serialization and every kernel that (de)compresses G2 points alike; call it before any
+    // batch work, not while one is running.
+    if (!ready()) return -1;
+    g_g2_sign_b.store(use_b != 0);
+    if (lcbk_set_g2_sign_b(use_b != 0)) { set_err("lcb_set_g2_sign_from_b: device configuration failed"); return -1; }
+    return 0;
 }
 
 // ================================================================== Fr Lagrange / polynomials (host, fr_host.hpp)
@@ -1301,7 +1308,8 @@ int ts_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const ui
 // ------------------------------------------------------------------ Lagrange / assembly
 // device-side Lagrange at 0 for np problems (entries off[j]..off[j+1]); dout = serialized results, dst = status
 int lagrange_enqueue(lcb_ctx *c, int g, uint8_t *dout, uint8_t *dst, const uint8_t *dx, const uint8_t *dy,
-                     const uint32_t *doff, size_t np, size_t ne, hipStream_t s, const u32 *src = nullptr) {
+                     const uint32_t *doff, size_t np, size_t ne, hipStream_t s, const u32 *src = nullptr,
+                     bool pairs = false) {
     if (np > 0xffffffffu || ne > 0xffffffffu) { set_err("lagrange: batch too large"); return -1; }
     void *lam = c->lag[0].get(LCB_FR_BYTES * (ne ? ne : 1));
     void *parts = c->lag[1].get((g == 1 ? LCB_G1_JAC_BYTES : LCB_G2_JAC_BYTES) * (ne ? ne : 1));
@@ -1310,6 +1318,9 @@ int lagrange_enqueue(lcb_ctx *c, int g, uint8_t *dout, uint8_t *dst, const uint8
     lcbk_lagrange_coeffs(dim3(nblk(np)), s, dx, doff, (u32)np, lam, dst);
     if (ne) {
         if (g == 1) lcbk_g1_mul_lanes(dim3(nblk(ne)), s, dy, lam, (u32)ne, parts, pok);
+        else if (pairs)   // even problem offsets (assembly with even k): two entries per lane, shared doublings
+            lcbk_g2_mul2_lanes(s, dy, lam, (u32)ne, parts, pok, src ? c->s_dec.p : nullptr,
+                               (u32)std::min<size_t>(c->s_dec_n, 0xffffffffu), src);
         else lcbk_g2_mul_lanes(dim3(nblk(ne)), s, dy, lam, (u32)ne, parts, pok, src ? c->s_dec.p : nullptr,
                                (u32)std::min<size_t>(c->s_dec_n, 0xffffffffu), src);
     }
@@ -1330,7 +1341,7 @@ int assemble_enqueue(lcb_ctx *c, int g, uint8_t *out, uint8_t *status, const uin
     if (!xs || !ys || !off) { set_err("device allocation failed"); return -1; }
     lcbk_select_first_valid(dim3(nblk(n_groups)), s, accept, pts, (u32)pb, (u32)per_group, (u32)k, (u32)n_groups, xs,
                             ys, off, order, src);
-    return lagrange_enqueue(c, g, out, status, xs, ys, off, n_groups, ne, s, src);
+    return lagrange_enqueue(c, g, out, status, xs, ys, off, n_groups, ne, s, src, g == 2 && k % 2 == 0);
 }
 
 // ------------------------------------------------------------------ Pippenger MSM (k_msm.hip)

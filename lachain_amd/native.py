@@ -52,6 +52,7 @@ _SIGS = {
     "lcb_get_device": (ctypes.c_int, []),
     "lcb_set_original_g2_cofactor": (None, [ctypes.c_int]),
     "lcb_set_line_mode": (ctypes.c_int, [ctypes.c_int]),
+    "lcb_set_g2_sign_from_b": (ctypes.c_int, [ctypes.c_int]),
     "lcb_last_error": (ctypes.c_char_p, []),
     "lcb_error_count": (ctypes.c_uint64, []),
     "lcb_test_inject_failure": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
@@ -704,6 +705,11 @@ class Context:
 
     def __exit__(self, *exc):
         self.close()
+
+
+def set_g2_sign_from_b(use_b):
+    """the G2 wire flag's convention (include/lachain_bls.h lcb_set_g2_sign_from_b): parity of y.b instead of y.a"""
+    _check(lib().lcb_set_g2_sign_from_b(1 if use_b else 0), "set_g2_sign_from_b")
 
 
 def set_original_g2_cofactor(enable):

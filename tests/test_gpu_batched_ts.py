@@ -203,14 +203,15 @@ def test_two_bad_per_group_search_fails(nat, tdev, kind):
     assert levels == ([2, 2, 12] if kind == "ts" else [2, 4])
 
 
-def test_ts_assembly_reuses_decoded_shares(nat, tdev):
+@pytest.mark.parametrize("k", [3, 4])
+def test_ts_assembly_reuses_decoded_shares(nat, tdev, k):
     """the assembly after a batched CommonCoin check takes each selected share's decoded point and G2 flag from the
     check's records (ts_share_st) when the record holds the same 96 bytes, and decodes the share itself otherwise:
     AddShare's Lagrange combination (ThresholdSigner.cs:62-75) equals the oracle's for a share with a G2
     cofactor-torsion component (ladder, not GLS), for shares the check decoded, and for an input whose bytes differ
     from the checked share"""
     torch, dev = tdev
-    n, k, rounds = 7, 3, 4
+    n, rounds = 7, 4                                        # k = 4: two entries per lane (k_g2_mul2_lanes)
     b = Rounds(b"gpu-ts-assembly-records", n, rounds)
     q = off_subgroup_g2(b.d)
     t2 = o.g2_add(o.g2_mul(q, o.fr(R - 1)), q)

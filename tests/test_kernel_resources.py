@@ -37,6 +37,7 @@ BUDGET = {
     "k_g2_hash": (0, 3336),
     "k_g2_mul": (206, 10624),
     "k_g2_mul_lanes": (1300, 10288),
+    "k_g2_mul2_lanes": (4530, 22672),         # two GLS tables (31 entries) per lane: the assembly's paired lanes
     "k_g2_sum": (204, 1008),
     "k_lineset_fill": (0, 1824),
     "k_msm_bucket_reduce": (0, 600),
