@@ -1235,8 +1235,9 @@ def run_rs(args, nat, rank):
 
 def run_mcl_latency(args, nat, rank):
     """Per-call latency of the mcl single-element surface (include/lachain_bls.h, the calls Lachain's protocol code
-    makes one at a time): scalar Fr product (host), G1 / G2 products and addition (k_op), the pairing and the final
-    exponentiation (nine-lane cooperative kernels), mulVec / Lagrange / Horner at the consensus sizes (N = 22,
+    makes one at a time): scalar Fr product and G1 / G2 addition / (de)serialization (host field code, fr_host.hpp /
+    fp_host.hpp), G1 / G2 scalar products (k_ptmul.hip: GLV / GLS ladders on four lanes each, membership ladder beside),
+    the pairing and the final exponentiation (nine-lane cooperative kernels), mulVec / Lagrange / Horner at the consensus sizes (N = 22,
     F = 7), and PublicKey.VerifyShare written as the reference writes it (HashToG2 + two GT.Pairing + Equals,
     TPKE/PublicKey.cs:88-92) beside the library's one-share batch call.  Median wall time per call from Python
     through ctypes (the ctypes overhead, ~1 us, is included); the oracle's single-threaded time for the same call
@@ -1303,7 +1304,10 @@ def run_mcl_latency(args, nat, rank):
     assert verify_mcl() and pk.VerifyShare(share, ps)
     res = {
         "Fr_mul": 1e3 * med(lambda: a * b, 2000),
-        "G1_add": 1e3 * med(lambda: P + P),
+        "G1_add": 1e3 * med(lambda: P + P, 2000),
+        "G2_add": 1e3 * med(lambda: Q + Q, 2000),
+        "G1_deserialize": 1e3 * med(lambda: G1.FromBytes(Pb), 200),
+        "G2_deserialize": 1e3 * med(lambda: G2.FromBytes(Qb), 200),
         "G1_mul": 1e3 * med(lambda: P * a),
         "G2_mul": 1e3 * med(lambda: Q * a),
         "pairing": 1e3 * med(lambda: GT.Pairing(P, Q)),
@@ -1323,8 +1327,8 @@ def run_mcl_latency(args, nat, rank):
     }
     return dict(metric="mcl single-call latency (median, one thread, through ctypes)", unit="us per call",
                 gpu=res, oracle_cpu=ref,
-                note="GPU-backed calls are a synchronous round trip each (launch + copies); Fr arithmetic is host "
-                     "code (fr_host.hpp).  pairing: a repeated G2 argument (its line set cached per thread, as for "
+                note="GPU-backed calls are a synchronous round trip each (launch + copies); Fr arithmetic and the "
+                     "O(1) G1 / G2 field work (add, (de)serialize) are host code (fr_host.hpp, fp_host.hpp).  pairing: a repeated G2 argument (its line set cached per thread, as for "
                      "the H and W every share of a ciphertext is paired with); pairing_new_Q: 40 rotating G2 "
                      "arguments (every call computes its line set).  oracle_cpu: the oracle's plain-C routines "
                      "(portable build), one thread, same inputs")
@@ -1387,6 +1391,10 @@ def run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, dd, n, n_cts, n_d
     def step():
         for f in [pool.submit(one, p) for p in parts]:
             f.result()
+
+    P = max(1, args.tpke_pipeline)
+    if P > 1 and K == 1:
+        return run_tpke_pipelined(args, nat, torch, dev, world, inp, dd, n, n_cts, n_dec, P)
 
     d_acc.fill_(7)
     torch.cuda.synchronize(dev)
@@ -1462,6 +1470,94 @@ def run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, dd, n, n_cts, n_d
 
 
 PREP_ARGS = []
+
+
+def run_tpke_pipelined(args, nat, torch, dev, world, inp, dd, n, n_cts, n_dec, P):
+    """--tpke-pipeline P: P whole 1M-share batches in flight.  Each of P host threads owns a library context, a HIP
+    stream and an accept buffer and verifies the full batch on its steps (thread t: steps t, t + P, ...); thread t
+    starts t/P of a step after thread 0, so one batch's splitting levels (latency-bound launches of < 1 wave per SIMD)
+    run beside another batch's randomisation and preparation.  Every step is the complete batched verify of the whole
+    batch (prepare + all levels); the timed region covers all args.steps steps, bracketed like the other paths."""
+    import concurrent.futures
+    import threading
+    import torch.distributed as dist
+    lib = nat.lib()
+    d_ct, d_dec, d_ui = dd
+    py, nk, pu, pw, pv, pvo, nc = PREP_ARGS[0]
+    lanes = []
+    for t in range(P):
+        lanes.append(dict(ctx=nat.Context(), stream=torch.cuda.Stream(dev),
+                          acc=torch.full((n,), 7, dtype=torch.uint8, device=dev)))
+
+    def one(ln):
+        rc = lib.lcb_ctx_tpke_verify_shares_batched_dev(
+            ln["ctx"].ptr, ln["acc"].data_ptr(), n, py, nk, pu, pw, pv, pvo, nc, d_ct.data_ptr(), d_dec.data_ptr(),
+            d_ui.data_ptr(), ln["stream"].cuda_stream)
+        if rc != 0:
+            raise RuntimeError(nat.last_error())
+        ln["stream"].synchronize()
+
+    for ln in lanes:                      # warmup: every context once, alone
+        for _ in range(max(1, args.warmup)):
+            one(ln)
+    torch.cuda.synchronize(dev)
+    t_one = time.perf_counter()
+    one(lanes[0])
+    t_one = time.perf_counter() - t_one
+    mism = sum(int(np.sum(ln["acc"].cpu().numpy() != inp["expect"])) for ln in lanes)
+    for ln in lanes:
+        ln["acc"].fill_(7)
+    go = threading.Barrier(P)
+
+    def lane_run(t):
+        ln = lanes[t]
+        go.wait()
+        time.sleep(t_one * t / P)
+        for _ in range(t, args.steps, P):
+            one(ln)
+
+    pool = concurrent.futures.ThreadPoolExecutor(max_workers=P)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for f in [pool.submit(lane_run, t) for t in range(P)]:
+        f.result()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    pool.shutdown()
+    for t, ln in enumerate(lanes):
+        if t < args.steps:
+            mism += int(np.sum(ln["acc"].cpu().numpy() != inp["expect"]))
+    levels = []
+    for ln in lanes:
+        lv = (ctypes.c_uint32 * 8)()
+        m6 = (ctypes.c_float * 6)()
+        k = lib.lcb_ctx_tpke_batched_stats(ln["ctx"].ptr, lv, m6)
+        levels.append(list(lv[:max(k, 0)]))
+        ln["ctx"].close()
+    t = shard.max_time_sum(dist, torch, dev, elapsed, mism, n)
+    elapsed = t[0]
+    checks = sum(levels[0])
+    step_fpmul = n * W_RLC_POINTS + checks * (C["C_ML2_NORM2"] + C["C_FE"]) + n_cts * W_PREPARE
+    step_ach = step_fpmul * MAC_PER_FPMUL / (elapsed / args.steps)
+    return dict(
+        metric="BLS12-381 TPKE decryption-share verifications/sec, randomized batch check (small-exponent test)",
+        value=float(t[2]) * args.steps / elapsed, unit="share verifications/s", steps=args.steps,
+        ms_per_step=1e3 * elapsed / args.steps, decision_mismatches=int(t[1]),
+        algorithm=("per ciphertext group: e(sum s_i U_i, H) == e(sum s_i Y_i, W), secret s_i = a_i + b_i lambda "
+                   "(32-bit a_i, b_i from ChaCha20 keyed by getrandom per call: 2^64 exponents); failed groups "
+                   "located (two errors) or checked singly; every rejection exact, false accept <= 2^-64 per group"),
+        api=f"lcb_ctx_tpke_verify_shares_batched_dev, {P} batches in flight (contexts / streams / host threads)",
+        pipeline=P, single_batch_ms=1e3 * t_one, levels=levels[0],
+        roofline={"bound": "valu_int32",
+                  "kernel": ("whole batched step: k_tpke_rlc_points + k_tpke_ct_prepare_h/_w + coop Miller / "
+                             "k_final_exp_check over all levels"),
+                  "achieved": step_ach / 1e12, "peak": PEAK_MAC32 / 1e12, "unit": "Tmac32/s",
+                  "frac": step_ach / PEAK_MAC32, "traffic": None, "mac_per_fpmul": MAC_PER_FPMUL,
+                  "work_per_step_fpmul": step_fpmul})
 
 LINE_MAX_BYTES = 6144    # the driver keeps only the tail of stdout (≈ 8 KB incl. stderr): the headline must fit in it
 
@@ -1599,6 +1695,8 @@ def main():
     ap.add_argument("--tpke-streams", type=int, default=1,
                     help="batched verify: concurrent parts (contexts / streams / host threads) per step; measured "
                          "no faster with 2 or 3 parts (147 - 159 vs 145 ms per 1M shares)")
+    ap.add_argument("--tpke-pipeline", type=int, default=1,
+                    help="batched verify: whole batches in flight (each on its own context / stream / host thread)")
     ap.add_argument("--headline", choices=("batched", "exact"), default="batched",
                     help="which TPKE path the line's value / roofline / cpu_baseline describe")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)

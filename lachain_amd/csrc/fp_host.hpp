@@ -516,6 +516,37 @@ inline void g2_compress(uint8_t b[96], const g2 &p, bool sign_b) {
     raw_to_bytes(b, xa);
     raw_to_bytes(b + 48, xb);
 }
+// endomorphisms used by the scalar splits (curve.hpp): phi(x, y) = (beta x, y) on G1, psi(x, y) =
+// (conj(x) psi_x, conj(y) psi_y) on the twist (affine points; infinity maps to itself)
+inline void g1_phi(g1a &r, const g1a &a) {
+    r = a;
+    if (!a.inf) mul(r.x, a.x, from_u32(LCB_G1_BETA_HOST));
+}
+inline void conj(fp2 &r, const fp2 &x) { r.a = x.a; neg(r.b, x.b); }
+inline void g2_psi(g2a &r, const g2a &a) {
+    r = a;
+    if (a.inf) return;
+    fp2 cx, cy, t;
+    cx.a = from_u32(LCB_PSI_X_HOST);
+    cx.b = from_u32(LCB_PSI_X_HOST + 12);
+    cy.a = from_u32(LCB_PSI_Y_HOST);
+    cy.b = from_u32(LCB_PSI_Y_HOST + 12);
+    conj(t, a.x);
+    mul(r.x, t, cx);
+    conj(t, a.y);
+    mul(r.y, t, cy);
+}
+// Jacobian p equals the affine point a (a finite)
+template <class F> inline bool jac_eq_aff(const jac<F> &p, const aff<F> &a) {
+    if (jac_is_inf(p) || a.inf) return jac_is_inf(p) && a.inf;
+    F z2, z3, t;
+    sqr(z2, p.z);
+    mul(z3, z2, p.z);
+    mul(t, a.x, z2);
+    if (!eq(t, p.x)) return false;
+    mul(t, a.y, z3);
+    return eq(t, p.y);
+}
 inline void g1_generator(g1 &g) {
     g.x = from_u32(LCB_G1_GEN_HOST);
     g.y = from_u32(LCB_G1_GEN_HOST + 12);

@@ -197,11 +197,90 @@ extern "C" __global__ void LCB_BOUNDS k_msm_bucket_acc(const fp *pts, const fp *
     buckets[b] = acc;
 }
 
+#define MSM_ADD(r, p, q) grp_add(r, p, q)
+#define MSM_DBL(r, p) grp_dbl(r, p)
+// Record-balanced form of k_msm_bucket_acc: lane j adds exactly the K sorted records [jK, (j + 1)K) (the digit
+// distribution is uneven — Poisson bucket sizes, and a short top window piles its records into few buckets — so one
+// lane per bucket waits for the wave's largest bucket).  A bucket wholly inside the chunk is written to buckets[k]
+// directly; the chunk's first bucket when it started in an earlier chunk goes to headp[j], its last bucket when it
+// continues into a later chunk to tailp[j] (both always written, infinity when unused), and k_msm_bucket_fix adds the
+// pieces of the buckets that span chunks.  The sentinel records (digit 0) sort last and end a chunk.
+DI void msm_flush(const g1 &acc, u32 k, u32 e0, u32 e1, const u32 *start, const u32 *end, g1 *buckets, g1 *head,
+                  g1 *tail) {
+    const u32 s = start[k], en = end[k];
+    if (s >= e0 && en <= e1) buckets[k] = acc;
+    else if (s < e0) *head = acc;
+    else *tail = acc;
+}
+extern "C" __global__ void LCB_BOUNDS k_msm_chunk_acc(const fp *pts, const fp *pts2, u32 n_pts, const u32 *keys,
+                                                     const u32 *vals, u32 m, u32 K, u32 sentinel, const u32 *start,
+                                                     const u32 *end, g1 *buckets, g1 *headp, g1 *tailp) {
+    const u32 j = blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t e0s = (size_t)j * K;
+    if (e0s >= m) return;
+    const u32 e0 = (u32)e0s, e1 = (u32)min((size_t)m, e0s + K);
+    g1 acc, inf;
+    jac_set_inf(inf);
+    headp[j] = inf;
+    tailp[j] = inf;
+    acc = inf;
+    u32 cur = keys[e0];
+    if (cur >= sentinel) return;
+    fp nx, ny;
+    u32 nv = vals[e0];
+    {
+        const u32 idx = nv & 0x7fffffffu;
+        load_aff(nx, ny, idx < n_pts ? pts : pts2, idx < n_pts ? idx : idx - n_pts);
+    }
+#pragma unroll 1
+    for (u32 e = e0; e < e1; e++) {
+        const u32 k = keys[e];
+        if (k >= sentinel) break;
+        fp x = nx, y = ny;
+        const u32 v = nv;
+        if (e + 1 < e1) {                                   // the next record's point, loaded during this addition
+            nv = vals[e + 1];
+            const u32 idx = nv & 0x7fffffffu;
+            load_aff(nx, ny, idx < n_pts ? pts : pts2, idx < n_pts ? idx : idx - n_pts);
+        }
+        if (k != cur) {
+            msm_flush(acc, cur, e0, e1, start, end, buckets, headp + j, tailp + j);
+            acc = inf;
+            cur = k;
+        }
+        if (fp_is_zero(x) && fp_is_zero(y)) continue;      // point at infinity
+        if (v >> 31) fp_neg(y, y);
+        jac_add_aff(acc, acc, x, y);
+    }
+    msm_flush(acc, cur, e0, e1, start, end, buckets, headp + j, tailp + j);
+}
+// buckets spanning chunks: tail of the first chunk + heads of the later ones; empty buckets: infinity
+extern "C" __global__ void LCB_BOUNDS k_msm_bucket_fix(const u32 *start, const u32 *end, u32 K, const g1 *headp,
+                                                      const g1 *tailp, u32 nb, g1 *buckets) {
+    const u32 k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nb) return;
+    const u32 s = start[k], en = end[k];
+    if (s == en) {
+        g1 inf;
+        jac_set_inf(inf);
+        buckets[k] = inf;
+        return;
+    }
+    const u32 j0 = s / K, j1 = (en - 1) / K;
+    if (j0 == j1) return;
+    g1 acc = tailp[j0];
+#pragma unroll 1
+    for (u32 j = j0 + 1; j <= j1; j++) MSM_ADD(acc, acc, headp[j]);
+    buckets[k] = acc;
+}
+
 // The reduction / combination kernels are latency chains (one lane's serial additions and doublings); their group
 // operations are the call forms (inlining them measured mixed: 2^20 bucket reduce 1.21 vs 1.06 ms, combine 2.17 vs
 // 1.98 ms; 2^24 combine 3.26 vs 3.59 ms).
+#ifndef MSM_ADD
 #define MSM_ADD(r, p, q) grp_add(r, p, q)
 #define MSM_DBL(r, p) grp_dbl(r, p)
+#endif
 // segment q of window w covers buckets a = q*L .. a+L-1 (digit values a+1 .. a+L)
 // hi_win: the key window that holds the upper half of the GLV top window's digits (digit = half + a + j + 1), or
 // ~0u when there is none
@@ -301,6 +380,15 @@ extern "C" void lcbk_msm_bounds(dim3 grid, hipStream_t s, const u32 *keys, u32 m
 }
 extern "C" void lcbk_msm_bucket_acc(dim3 grid, hipStream_t s, const void *pts, const void *pts2, u32 n_pts, const u32 *vals, const u32 *start, const u32 *end, u32 nb, void *buckets) {
     LCB_LAUNCH(k_msm_bucket_acc, (const fp *)pts, (const fp *)pts2, n_pts, vals, start, end, nb, (g1 *)buckets);
+}
+extern "C" void lcbk_msm_chunk_acc(hipStream_t s, const void *pts, const void *pts2, u32 n_pts, const u32 *keys, const u32 *vals, u32 m, u32 K, u32 sentinel, const u32 *start, const u32 *end, void *buckets, void *headp, void *tailp) {
+    const u32 n_chunks = (u32)(((size_t)m + K - 1) / K);
+    dim3 grid((n_chunks + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_msm_chunk_acc, (const fp *)pts, (const fp *)pts2, n_pts, keys, vals, m, K, sentinel, start, end, (g1 *)buckets, (g1 *)headp, (g1 *)tailp);
+}
+extern "C" void lcbk_msm_bucket_fix(hipStream_t s, const u32 *start, const u32 *end, u32 K, const void *headp, const void *tailp, u32 nb, void *buckets) {
+    dim3 grid((nb + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_msm_bucket_fix, start, end, K, (const g1 *)headp, (const g1 *)tailp, nb, (g1 *)buckets);
 }
 extern "C" void lcbk_msm_digits_glv(dim3 grid, hipStream_t s, const uint8_t *scalars, u32 n, u32 c, u32 nwin, u32 *keys, u32 *vals) {
     LCB_LAUNCH(k_msm_digits_glv, scalars, n, c, nwin, keys, vals);

@@ -343,7 +343,94 @@ extern "C" void mclBnG1_sub(mclBnG1 *z, const mclBnG1 *x, const mclBnG1 *y) {
     fph::jac_add(t, *G1R(x), ny);
     *G1W(z) = t;
 }
-extern "C" void mclBnG1_mul(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y) { g1_op(OP_G1_MUL, z, x, nullptr, y); }
+// ---- mclBnG1_mul / mclBnG2_mul: the cooperative ladders of k_ptmul.hip (four lanes per ladder, several ladders per
+// wave) on the scalar split below, the result assembled here; a base point outside the subgroup (the split is only
+// valid on it) takes the exact one-lane ladder of k_op
+struct PtJobG1 { u32 x[12], y[12], inf, nwin, pad[2]; uint8_t nib[36]; };
+struct PtJobG2 { u32 x[24], y[24], inf, nwin, pad[2]; uint8_t nib[36]; };
+static_assert(sizeof(PtJobG1) == 148 && sizeof(PtJobG2) == 244, "k_ptmul.hip PtJob layouts");
+typedef unsigned __int128 u128h;
+static const uint64_t Z_ABS_H = 0xd201000000010000ull;
+// q <- q / u (256-bit), returns q mod u
+static uint64_t divmod_u(uint64_t q[4]) {
+    u128h rem = 0;
+    for (int i = 3; i >= 0; i--) {
+        u128h cur = rem << 64 | q[i];
+        q[i] = (uint64_t)(cur / Z_ABS_H);
+        rem = cur % Z_ABS_H;
+    }
+    return (uint64_t)rem;
+}
+// nwin 4-bit nibbles of the little-endian words v (nw 64-bit words), most significant first
+template <class J> static void put_nibbles(J &job, const uint64_t *v, int nw, u32 nwin) {
+    job.nwin = nwin;
+    for (u32 w = 0; w < nwin; w++) {
+        const u32 bit = 4 * (nwin - 1 - w), word = bit / 64;
+        job.nib[w] = word < (u32)nw ? (uint8_t)((v[word] >> (bit % 64)) & 15) : 0;
+    }
+}
+template <class J, class A> static void put_point(J &job, const A &a) {
+    job.inf = a.inf ? 1u : 0u;
+    memcpy(job.x, &a.x, sizeof a.x);
+    memcpy(job.y, &a.y, sizeof a.y);
+}
+// run n_jobs ladders (k_ptmul_g1 / _g2) on the thread's staging; outputs the groups' Jacobian results
+static bool ptmul_run(int g, const void *jobs, size_t job_bytes, u32 n_jobs, void *out, size_t out_bytes) {
+    if (!stage_ready()) return false;
+    memcpy(IOH, jobs, job_bytes * n_jobs);
+    const size_t out_w = 1024;                    // results at word 1024 of the 16 KB staging
+    hipError_t e;
+    if ((e = hipMemcpyAsync(t_stage.dev, t_stage.host, job_bytes * n_jobs, hipMemcpyHostToDevice, t_stage.s)) != hipSuccess) { set_err("H2D", e); return false; }
+    if (g == 1) lcbk_ptmul_g1(t_stage.s, t_stage.dev, n_jobs, t_stage.dev + out_w);
+    else lcbk_ptmul_g2(t_stage.s, t_stage.dev, n_jobs, t_stage.dev + out_w);
+    if ((e = hipGetLastError()) != hipSuccess) { set_err("k_ptmul launch", e); return false; }
+    if ((e = hipMemcpyAsync(t_stage.host + out_w, t_stage.dev + out_w, out_bytes * n_jobs, hipMemcpyDeviceToHost, t_stage.s)) != hipSuccess) { set_err("D2H", e); return false; }
+    if ((e = hipStreamSynchronize(t_stage.s)) != hipSuccess) { set_err("k_ptmul", e); return false; }
+    memcpy(out, IOH + out_w, out_bytes * n_jobs);
+    return true;
+}
+extern "C" void mclBnG1_mul(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y) {
+    uint64_t k[4];
+    frh::to_raw(k, FRV(y));                       // canonical scalar < r
+    fph::g1a P;
+    fph::jac_to_aff(P, *G1R(x));
+    if (P.inf || (k[0] | k[1] | k[2] | k[3]) == 0 || !fph::jac_on_curve(*G1R(x))) {
+        if (P.inf || (k[0] | k[1] | k[2] | k[3]) == 0) { fph::jac_set_inf(*G1W(z)); return; }
+        g1_op(OP_G1_MUL, z, x, nullptr, y);       // not a curve point: mcl's generic ladder semantics
+        return;
+    }
+    // GLV (curve.hpp g1_mul_glv): k = d0 + d1 u + a1 u^2 = (a0 + a1) + a1 lambda, a0 = d0 + d1 u
+    uint64_t q[4] = {k[0], k[1], k[2], k[3]};
+    const uint64_t d0 = divmod_u(q), d1 = divmod_u(q);   // q = a1 < 2^128
+    u128h a0 = (u128h)d1 * Z_ABS_H + d0, a1 = (u128h)q[1] << 64 | q[0];
+    u128h s = a0 + a1;
+    const uint64_t s_top = s < a0 ? 1 : 0;
+    const uint64_t k1[3] = {(uint64_t)s, (uint64_t)(s >> 64), s_top}, k2[2] = {(uint64_t)a1, (uint64_t)(a1 >> 64)};
+    const u128h zz = (u128h)Z_ABS_H * Z_ABS_H;
+    const uint64_t z2[2] = {(uint64_t)zz, (uint64_t)(zz >> 64)};
+    PtJobG1 jobs[3];
+    memset(jobs, 0, sizeof jobs);
+    fph::g1a phiP;
+    fph::g1_phi(phiP, P);
+    put_point(jobs[0], P);
+    put_nibbles(jobs[0], k1, 3, 33);
+    put_point(jobs[1], phiP);
+    put_nibbles(jobs[1], k2, 2, 33);
+    put_point(jobs[2], P);                        // membership: [z^2] P == P + phi(P) = (beta^2 x, -y)
+    put_nibbles(jobs[2], z2, 2, 33);
+    fph::g1 acc[3];
+    if (!ptmul_run(1, jobs, sizeof(PtJobG1), 3, acc, sizeof(fph::g1))) { fail_out(z, 144); return; }
+    fph::g1a chk;
+    fph::g1_phi(chk, phiP);                       // (beta^2 x, y)
+    fph::neg(chk.y, chk.y);
+    if (!fph::jac_eq_aff(acc[2], chk)) {          // outside G1: the split does not apply
+        g1_op(OP_G1_MUL, z, x, nullptr, y);
+        return;
+    }
+    fph::g1 r;
+    fph::jac_add(r, acc[0], acc[1]);
+    *G1W(z) = r;
+}
 extern "C" void lcb_g1_generator(mclBnG1 *g) { fph::g1_generator(*G1W(g)); }
 
 extern "C" mclSize mclBnG2_serialize(void *buf, mclSize max, const mclBnG2 *x) {
@@ -396,7 +483,52 @@ extern "C" void mclBnG2_sub(mclBnG2 *z, const mclBnG2 *x, const mclBnG2 *y) {
     fph::jac_add(t, *G2R(x), ny);
     *G2W(z) = t;
 }
-extern "C" void mclBnG2_mul(mclBnG2 *z, const mclBnG2 *x, const mclBnFr *y) { g2_op(OP_G2_MUL, z, x, nullptr, y); }
+extern "C" void mclBnG2_mul(mclBnG2 *z, const mclBnG2 *x, const mclBnFr *y) {
+    uint64_t k[4];
+    frh::to_raw(k, FRV(y));
+    fph::g2a Q;
+    fph::jac_to_aff(Q, *G2R(x));
+    if (Q.inf || (k[0] | k[1] | k[2] | k[3]) == 0 || !fph::jac_on_curve(*G2R(x))) {
+        if (Q.inf || (k[0] | k[1] | k[2] | k[3]) == 0) { fph::jac_set_inf(*G2W(z)); return; }
+        g2_op(OP_G2_MUL, z, x, nullptr, y);
+        return;
+    }
+    // GLS (curve.hpp g2_mul_gls): k = d0 + d1 u + d2 u^2 + d3 u^3 over Q, -psi Q, psi^2 Q, -psi^3 Q
+    uint64_t q[4] = {k[0], k[1], k[2], k[3]}, d[4];
+    d[0] = divmod_u(q);
+    d[1] = divmod_u(q);
+    d[2] = divmod_u(q);
+    d[3] = q[0];                                  // k < r < u^4
+    fph::g2a B[4];
+    B[0] = Q;
+    fph::g2_psi(B[1], Q);
+    fph::g2_psi(B[2], B[1]);
+    fph::g2_psi(B[3], B[2]);
+    fph::g2a psiQ = B[1];
+    fph::neg(B[1].y, B[1].y);
+    fph::neg(B[3].y, B[3].y);
+    PtJobG2 jobs[5];
+    memset(jobs, 0, sizeof jobs);
+    for (int i = 0; i < 4; i++) {
+        put_point(jobs[i], B[i]);
+        put_nibbles(jobs[i], &d[i], 1, 16);
+    }
+    put_point(jobs[4], Q);                        // membership: psi(Q) == -[|z|] Q
+    put_nibbles(jobs[4], &Z_ABS_H, 1, 16);
+    fph::g2 acc[5];
+    if (!ptmul_run(2, jobs, sizeof(PtJobG2), 5, acc, sizeof(fph::g2))) { fail_out(z, 288); return; }
+    fph::g2a chk = psiQ;
+    fph::neg(chk.y, chk.y);
+    if (!fph::jac_eq_aff(acc[4], chk)) {          // outside G2
+        g2_op(OP_G2_MUL, z, x, nullptr, y);
+        return;
+    }
+    fph::g2 r;
+    fph::jac_add(r, acc[0], acc[1]);
+    fph::jac_add(r, r, acc[2]);
+    fph::jac_add(r, r, acc[3]);
+    *G2W(z) = r;
+}
 extern "C" void lcb_g2_generator(mclBnG2 *g) { fph::g2_generator(*G2W(g)); }
 
 // ================================================================== GT / pairing
@@ -1348,6 +1480,7 @@ int assemble_enqueue(lcb_ctx *c, int g, uint8_t *out, uint8_t *status, const uin
 // window width minimising ceil-windows * (n mixed adds * 11 + 2^(c-1) buckets * 2 Jacobian adds * 16) Fp-mul
 // GLV form: 2n points with 128-bit scalars, windows ceil(128 / c); only widths whose top window is nearly full
 // (a short top window concentrates 2n records in few buckets, one lane each)
+std::atomic<int> g_msm_chunk{64};   // records per lane of k_msm_chunk_acc (0: one lane per bucket, k_msm_bucket_acc)
 u32 msm_window(size_t n, bool glv = false) {
     u32 best = 4;
     double best_cost = 1e300;
@@ -1423,7 +1556,16 @@ int msm_enqueue(lcb_ctx *cx, void *out_jac, const void *pts, const uint8_t *scal
     hipMemsetAsync(en, 0, (size_t)nb * 4, s);
     if (m) lcbk_msm_bounds(dim3(nblk(m)), s, keys, (u32)m, sentinel, st, en);
     hipEventRecord(cx->msm_ev[3], s);
-    lcbk_msm_bucket_acc(dim3(nblk(nb)), s, pts, phi, (u32)n, vals, st, en, nb, buckets);
+    if (g_msm_chunk > 0) {                       // record-balanced accumulation (k_msm_chunk_acc)
+        const u32 K = (u32)g_msm_chunk.load();
+        const size_t nch = (m + K - 1) / K;
+        void *hp = b[12].get((nch ? nch : 1) * LCB_G1_JAC_BYTES), *tp = b[13].get((nch ? nch : 1) * LCB_G1_JAC_BYTES);
+        if (!hp || !tp) { set_err("msm: device allocation failed"); return -1; }
+        if (m) lcbk_msm_chunk_acc(s, pts, phi, (u32)n, keys, vals, (u32)m, K, sentinel, st, en, buckets, hp, tp);
+        lcbk_msm_bucket_fix(s, st, en, K, hp, tp, nb, buckets);
+    } else {
+        lcbk_msm_bucket_acc(dim3(nblk(nb)), s, pts, phi, (u32)n, vals, st, en, nb, buckets);
+    }
     hipEventRecord(cx->msm_ev[4], s);
     lcbk_msm_bucket_reduce(dim3(nblk(n_seg)), s, buckets, half, L, n_seg, glv ? nwin : 0xffffffffu, segs);
     hipEventRecord(cx->msm_ev[5], s);
@@ -1582,6 +1724,12 @@ extern "C" int lcb_set_coop_miller_max(uint32_t max_checks) {
 extern "C" int lcb_set_fork_mode(int mode) {
     if (!tuning_allowed("lcb_set_fork_mode")) return -1;
     g_fork_mode.store(mode >= 1 && mode <= 3 ? mode : 0);
+    return 0;
+}
+extern "C" int lcb_set_msm_chunk(int records_per_lane) {
+    if (!tuning_allowed("lcb_set_msm_chunk")) return -1;
+    if (records_per_lane < 0 || records_per_lane > 65536) { set_err("lcb_set_msm_chunk: 0..65536"); return -1; }
+    g_msm_chunk.store(records_per_lane);
     return 0;
 }
 extern "C" int lcb_test_inject_failure(int site, int count) {

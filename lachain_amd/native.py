@@ -53,6 +53,7 @@ _SIGS = {
     "lcb_set_original_g2_cofactor": (None, [ctypes.c_int]),
     "lcb_set_line_mode": (ctypes.c_int, [ctypes.c_int]),
     "lcb_set_g2_sign_from_b": (ctypes.c_int, [ctypes.c_int]),
+    "lcb_set_msm_chunk": (ctypes.c_int, [ctypes.c_int]),
     "lcb_last_error": (ctypes.c_char_p, []),
     "lcb_error_count": (ctypes.c_uint64, []),
     "lcb_test_inject_failure": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
@@ -741,6 +742,11 @@ def inject_failure(site, count=1):
     """test hook (LCB_ALLOW_TEST_HOOKS=1): the next `count` passes through fault site `site` fail"""
     if lib().lcb_test_inject_failure(int(site), int(count)) != 0:
         raise RuntimeError("inject_failure: " + last_error())
+
+
+def set_msm_chunk(records_per_lane):
+    """records per lane of the MSM bucket accumulation (0: one lane per bucket)"""
+    _tuning(lib().lcb_set_msm_chunk(int(records_per_lane)), "set_msm_chunk")
 
 
 def set_coop_max(max_checks):

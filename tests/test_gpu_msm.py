@@ -179,3 +179,30 @@ def test_glv_msm_known_answer_1m(nat, torch_dev):
     pts = nat.mul_batch_raw(1, None, b"".join(o.fr(v) for v in a), n, generator=True)
     got, _ = _dev_msm(nat, torch, dev, [pts[48 * i:48 * i + 48] for i in range(n)], [o.fr(v) for v in s], 0, glv=True)
     assert got == o.g1_mul(o.g1_gen(), o.fr(sum(x * y for x, y in zip(a, s)) % R))
+
+
+@pytest.mark.parametrize("chunk", [0, 1, 3, 64, 4096])
+@pytest.mark.parametrize("glv", [False, True])
+def test_msm_record_chunks(nat, torch_dev, chunk, glv):
+    """record-balanced bucket accumulation (k_msm_chunk_acc + k_msm_bucket_fix) at several chunk sizes, on a skewed
+    digit distribution: one scalar repeated (every record of a window in one bucket, spanning many chunks), duplicated
+    points, P and -P, zero scalars, and random ones; the result equals the oracle's and the one-lane-per-bucket form's
+    (chunk 0)"""
+    torch, dev = torch_dev
+    d = Drbg(b"gpu-msm-chunks")
+    n = 700
+    base = [o.g1_mul(o.g1_gen(), d.fr()) for _ in range(n // 2)]
+    pts = base + base[: n - len(base)]
+    pts[5] = o.g1_neg(pts[4])
+    sc = [d.fr_int() for _ in range(n)]
+    for i in range(0, n, 3):
+        sc[i] = 0x1234567890ABCDEF1234567890ABCDEF12345678
+    for i in range(1, n, 17):
+        sc[i] = 0
+    want = _expected(pts, sc)
+    nat.set_msm_chunk(chunk)
+    try:
+        got, _ = _dev_msm(nat, torch, dev, pts, [s.to_bytes(32, "little") for s in sc], 8 if glv else 6, glv)
+    finally:
+        nat.set_msm_chunk(64)
+    assert got == want

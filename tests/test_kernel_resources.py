@@ -42,7 +42,9 @@ BUDGET = {
     "k_lineset_fill": (0, 1824),
     "k_msm_bucket_reduce": (0, 600),
     "k_msm_horner": (0, 168),
-    "k_op": (3038, 8484),                     # mcl single-element surface: every operation in one kernel
+    "k_msm_bucket_fix": (0, 168),
+    "k_op": (3038, 8484),
+    "k_ptmul_g2": (32, 68),                   # mcl G2 multiplication latency kernel: four ladder lanes share each op                     # mcl single-element surface: every operation in one kernel
     "k_rlc_key_tables": (12, 768),            # k_rlc_rand.hip: spills to scratch, not AGPRs (<= 256 registers)
     "k_rlc_miller_fallback": (0, 2376),
     "k_rlc_search": (93, 2264),
