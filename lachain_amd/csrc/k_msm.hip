@@ -15,7 +15,7 @@
 //   6. k_g1_jac_reduce_block (LDS tree, until one sum per window) + k_msm_horner: sum_w 2^(c w) W_w by doubling.
 // Points are affine, Montgomery form, 12 x u32 limbs per coordinate (= the x,y words of mcl's mclBnG1 with
 // z = 1); (0, 0) encodes the point at infinity.
-#include "kcommon.hpp"
+#include "coop_pt.hpp"
 #include <hipcub/hipcub.hpp>
 
 LCB_ASM_LIBRARY(k_msm)
@@ -353,6 +353,23 @@ extern "C" __global__ void LCB_BOUNDS k_msm_horner(const g1 *win, u32 nwin, u32 
     out[0] = acc;
 }
 
+// the same combination on one group of four lanes (coop_pt.hpp: a doubling in 3 product latencies instead of 7, an
+// addition in 5 instead of 16) — the serial tail of every MSM
+extern "C" __global__ void __launch_bounds__(64, 1) k_msm_horner_coop(const g1 *win, u32 nwin, u32 c, u32 fold_top,
+                                                                     g1 *out) {
+    __shared__ PtLds<fp> lds;
+    g1 acc = win[nwin - 1];
+    if (fold_top) { g1 t = win[nwin]; pt_add(&lds, acc, acc, t); }
+#pragma unroll 1
+    for (u32 w = nwin - 1; w-- > 0;) {
+#pragma unroll 1
+        for (u32 t = 0; t < c; t++) pt_dbl(&lds, acc, acc);
+        g1 t = win[w];
+        pt_add(&lds, acc, acc, t);
+    }
+    if (threadIdx.x == 0) out[0] = acc;
+}
+
 extern "C" __global__ void LCB_BOUNDS k_g1_jac_compress(const g1 *in, u32 n, uint8_t *out) {
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -407,8 +424,7 @@ extern "C" void lcbk_g1_jac_reduce_block(hipStream_t s, const void *in, u32 n_in
     LCB_LAUNCH(k_g1_jac_reduce_block, (const g1 *)in, n_in, group, (g1 *)out);
 }
 extern "C" void lcbk_msm_horner(hipStream_t s, const void *win, u32 nwin, u32 c, u32 fold_top, void *out) {
-    dim3 grid(1);
-    LCB_LAUNCH(k_msm_horner, (const g1 *)win, nwin, c, fold_top, (g1 *)out);
+    hipLaunchKernelGGL(k_msm_horner_coop, dim3(1), dim3(PT_LANES), 0, s, (const g1 *)win, nwin, c, fold_top, (g1 *)out);
 }
 extern "C" void lcbk_g1_jac_compress(dim3 grid, hipStream_t s, const void *in, u32 n, uint8_t *out) {
     LCB_LAUNCH(k_g1_jac_compress, (const g1 *)in, n, out);
