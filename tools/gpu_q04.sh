@@ -13,6 +13,12 @@ for P in $PIPES; do
   timeout -k 10 300 python3 -u bench.py --tpke-exact 0 --ts-rounds 0 --msm-sizes= --replay-n 0 --ecdsa-sigs 0 --dkg-n 0 --rs-n 0 --mcl-reps 0 --no-cpu-baseline --pattern-steps 0 --steps ${STEPS:-10} --warmup 2 --tpke-pipeline $P > gpurun_out/${TAG}_p$P.txt 2> gpurun_out/${TAG}_p$P.err || { echo "BENCH FAILED p$P"; tail -20 gpurun_out/${TAG}_p$P.err; exit 1; }
   python3 -c "import json,sys; d=json.loads(open('gpurun_out/${TAG}_p$P.txt').read().strip().splitlines()[-1]); print('pipe $P', round(d['value']/1e6,3), 'M/s', round(d['ms_per_step'],2), 'ms', d['config']['decision_mismatches'], 'mism')"
 done
+if [ -n "$MSMB" ]; then
+  for K in $MSMB; do
+    LCB_ALLOW_TUNING=1 LCB_MSM_CHUNK=$K timeout -k 10 300 python3 -u bench.py --tpke-exact 0 --tpke-batched 0 --ts-rounds 0 --replay-n 0 --ecdsa-sigs 0 --dkg-n 0 --rs-n 0 --mcl-reps 0 --no-cpu-baseline --pattern-steps 0 --shares 22000 --headline exact --tpke-exact 1 --steps 1 --warmup 1 --msm-steps 5 > gpurun_out/${TAG}_msm$K.txt 2> gpurun_out/${TAG}_msm$K.err || { echo "MSM BENCH FAILED"; tail -20 gpurun_out/${TAG}_msm$K.err; exit 1; }
+    python3 -c "import json; d=json.loads([l for l in open('gpurun_out/${TAG}_msm$K.txt') if l.startswith('BENCH_DETAIL')][-1][13:]); [print('msm chunk $K', m['total_points'], round(m['value']/1e6,1), 'M/s', m['ms_per_step'], m['phase_ms'], m['known_answer_ok']) for m in d['msm']]"
+  done
+fi
 if [ -n "$MCL" ]; then
   timeout -k 10 300 python3 -u bench.py --tpke-exact 0 --tpke-batched 0 --ts-rounds 0 --msm-sizes= --replay-n 0 --ecdsa-sigs 0 --dkg-n 0 --rs-n 0 --mcl-reps 30 --no-cpu-baseline --pattern-steps 0 --shares 22000 --headline exact --tpke-exact 1 --steps 1 --warmup 1 > gpurun_out/${TAG}_mcl.txt 2> gpurun_out/${TAG}_mcl.err || { echo "MCL BENCH FAILED"; tail -20 gpurun_out/${TAG}_mcl.err; exit 1; }
   python3 -c "import json; d=json.loads(open('gpurun_out/${TAG}_mcl.txt').read().strip().splitlines()[-1]); print(d['summary']['mcl_latency_us'])"
