@@ -1662,13 +1662,13 @@ def compact_line(full):
     return line
 
 
-def emit(full):
+def emit(full, write_file=True):
     """Print the detail record first (one line, prefixed so it never parses as the headline), write it under
     gpurun_out/ when that exists, then the compact headline as the LAST stdout line."""
     detail = json.dumps(full)
     print("BENCH_DETAIL " + detail, flush=True)
     out = os.path.join(ROOT, "gpurun_out")
-    if os.path.isdir(out):
+    if write_file and os.path.isdir(out):
         try:
             with open(os.path.join(out, f"bench_detail_{full.get('source_hash')}.json"), "w") as fh:
                 fh.write(detail + "\n")

@@ -43,7 +43,7 @@ def test_compact_line_size_and_keys():
 
 def test_emit_prints_headline_last(capsys):
     full = _full()
-    bench.emit(full)
+    bench.emit(full, write_file=False)
     out = capsys.readouterr().out.splitlines()
     assert out[0].startswith("BENCH_DETAIL ")
     assert json.loads(out[0][len("BENCH_DETAIL "):]) == full
