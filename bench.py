@@ -1755,6 +1755,8 @@ def main():
         nat.set_fork_mode(args.fork_mode)
     if args.coop_miller_max >= 0:
         nat.set_coop_miller_max(args.coop_miller_max)
+    if os.environ.get("LCB_WAVE_PRIO"):           # A/B of the latency kernels' wave priority
+        nat.set_wave_priority(int(os.environ["LCB_WAVE_PRIO"]))
     if os.environ.get("LCB_MSM_CHUNK"):           # A/B of the MSM bucket accumulation (0: one lane per bucket)
         nat.set_msm_chunk(int(os.environ["LCB_MSM_CHUNK"]))
 

@@ -336,6 +336,9 @@ int lcb_set_fork_mode(int mode);
 /* tuning hook (LCB_ALLOW_TUNING=1): records per lane of the MSM bucket accumulation (k_msm_chunk_acc, default 64);
    0 = one lane per bucket (k_msm_bucket_acc).  Results are unchanged. */
 int lcb_set_msm_chunk(int records_per_lane);
+/* tuning hook (LCB_ALLOW_TUNING=1): 1 (default) = the latency-bound kernels of the batched checks (preparation chain,
+   every level) raise their waves' issue priority over the bulk randomisation waves sharing their SIMDs; 0 = off */
+int lcb_set_wave_priority(int on);
 /* test hook: final exponentiation of n Fp12 values (144 x u32 each, Montgomery form, field.hpp layout) by the one-lane
    (coop = 0) or the cooperative (coop = 1) kernel */
 int lcb_debug_final_exp(const uint32_t *in, size_t n, uint32_t *out, int coop);

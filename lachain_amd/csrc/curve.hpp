@@ -429,6 +429,13 @@ DN void g1_mul_glv(g1 &r, const g1a &A, const u32 k[8]) {
 // 1 = y.b.  One copy per translation unit, set by every unit's lcbk_cfg_<unit> (kcommon.hpp LCB_TU_CONFIG) through
 // lcb_set_g2_sign_from_b; read once per (de)compression.
 static __device__ u32 lcb_g2_sign_b = 0;
+// 1 = the latency-bound kernels of the batched checks (preparation chain, every level) raise their waves' issue
+// priority (s_setprio) over the bulk randomisation waves that share their SIMDs (lcb_set_wave_priority)
+static __device__ u32 lcb_wave_prio = 1;
+#define LCB_LATENCY_PRIO()                                                                                         \
+    do {                                                                                                          \
+        if (lcb_wave_prio) __builtin_amdgcn_s_setprio(3);                                                         \
+    } while (0)
 DI const fp &g2_sign_coord(const fp2 &y) { return lcb_g2_sign_b ? y.b : y.a; }
 DI void bytes48_to_raw(fp &raw, const uint8_t *b) { // 4-byte aligned source
     const u32 *w = (const u32 *)b;

@@ -42,6 +42,7 @@ LCB_TU_CONFIG(k_batch)
 // desc = {first share, length, ciphertext / message, 0}; order of the records is irrelevant
 extern "C" __global__ void LCB_BOUNDS k_rlc_groups(const u32 *key_idx, u32 i0, u32 n, u32 n_keys, u32 cap,
                                                   uint4 *desc, u32 *count) {
+    LCB_LATENCY_PRIO();
     u32 i = i0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u32 c = key_idx[i];
@@ -68,6 +69,7 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_groups(const u32 *key_idx, u32 i0, u
 // the weighted sums of the level-1 groups listed in sdesc (.w = level-1 group index) as affine records
 extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum(const uint4 *sdesc, u32 n_s, const u32 *wsum, u32 n_l1,
                                                      g1a_st *gpts) {
+    LCB_LATENCY_PRIO();
     u32 g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n_s) return;
     u32 l = sdesc[g].w;
@@ -84,6 +86,7 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum(const uint4 *sdesc, u32 n_
 // ---------------------------------------------------------------- TPKE group Miller loops (k_tpke_miller's loop)
 extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_rlc_miller(const u32 *lines, const uint4 *desc, const g1a_st *gpts,
                                                             u32 n_groups, u32 *f_soa, uint8_t *gacc) {
+    LCB_LATENCY_PRIO();
     __shared__ uint4 lds_pts[12 * LCB_BLOCK];
     u32 g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n_groups) return;
@@ -160,6 +163,7 @@ extern "C" __global__ void LCB_BOUNDS k_ts_rlc_sum(const uint4 *desc, u32 n_grou
                                                   const g1a_st *pks, u32 n_pks, const u32 *pk_idx, const uint8_t *sigs,
                                                   const u32 *rP, const u32 *rS, u32 n, ts_grp *gpts, uint8_t *accept,
                                                   uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval) {
+    LCB_LATENCY_PRIO();
     u32 g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n_groups) return;
     uint4 dsc = desc[g];
@@ -216,6 +220,7 @@ extern "C" __global__ void LCB_BOUNDS k_ts_rlc_sum(const uint4 *desc, u32 n_grou
 }
 extern "C" __global__ void LCB_BOUNDS k_ts_rlc_wsum(const uint4 *sdesc, u32 n_s, const u32 *wsum, u32 n_l1,
                                                    ts_grp *gpts) {
+    LCB_LATENCY_PRIO();
     u32 g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n_s) return;
     u32 l = sdesc[g].w;
@@ -245,6 +250,7 @@ DN void miller2_ts_grp(fp12 &f, const u32 *lsH, const g1a &PK, const g2a &S, con
 }
 extern "C" __global__ void LCB_PAIR_BOUNDS k_ts_rlc_miller(const u32 *lines, const uint4 *desc, const ts_grp *gpts,
                                                           u32 n_groups, u32 *f_soa, uint8_t *gacc) {
+    LCB_LATENCY_PRIO();
     u32 g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n_groups) return;
     u32 m = desc[g].z;
@@ -283,6 +289,7 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_resolve(const uint4 *desc, u32 o, u3
                                                    const uint8_t *gexact, const u32 *park, u32 first, uint8_t *accept,
                                                    uint4 *next, u32 *next_count, uint4 *search, u32 *search_count,
                                                    u32 *gamma, const u32 *key_idx, u32 n_keys, const u32 *susp) {
+    LCB_LATENCY_PRIO();
     u32 gl = blockIdx.x * blockDim.x + threadIdx.x;
     if (gl >= m) return;
     u32 g = o + gl;
@@ -324,6 +331,7 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_resolve(const uint4 *desc, u32 o, u3
 extern "C" __global__ void LCB_BOUNDS k_rlc_search(const uint4 *search, u32 o, u32 m, const u32 *gamma, const u32 *park,
                                                   uint8_t *accept, uint4 *next, u32 *next_count, const u32 *key_idx,
                                                   u32 n_keys, const u32 *susp) {
+    LCB_LATENCY_PRIO();
     u32 gl = blockIdx.x * blockDim.x + threadIdx.x;
     if (gl >= m) return;
     u32 g = o + gl;
@@ -356,6 +364,7 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_search(const uint4 *search, u32 o, u
 
 // the final-exponentiation outputs of checks [o, o + m) (park stride m) -> rows o.. of dst (576 B each)
 extern "C" __global__ void LCB_BOUNDS k_rlc_park_copy(const u32 *park, u32 o, u32 m, u32 *dst) {
+    LCB_LATENCY_PRIO();
     u32 gl = blockIdx.x * blockDim.x + threadIdx.x;
     if (gl >= m) return;
     fp12 f;
@@ -416,6 +425,7 @@ DI u32 half_ballot(bool p) {
 extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_search2a(const uint4 *search, u32 ns, const u32 *gamma0,
                                                          const u32 *gamma12, uint8_t *accept, u32 *open,
                                                          u32 *open_count) {
+    LCB_LATENCY_PRIO();
     u32 g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= ns) return;
     const uint4 d = search[g];
@@ -436,6 +446,7 @@ extern "C" __global__ void __launch_bounds__(64) k_tpke_rlc_search2b(const uint4
                                                                     const u32 *open_count, uint8_t *accept, uint4 *next,
                                                                     u32 *next_count, const u32 *key_idx, u32 n_keys,
                                                                     const u32 *susp) {
+    LCB_LATENCY_PRIO();
     const u32 j = threadIdx.x & 31, k = blockIdx.x * 2 + (threadIdx.x >> 5);
     if (blockIdx.x * 2 >= *open_count) return;          // (uniform per block)
     const bool live = k < *open_count;
@@ -496,6 +507,7 @@ extern "C" __global__ void __launch_bounds__(64) k_tpke_rlc_search2b(const uint4
 // exact singles of shares [0, m): desc = {i, 1, group index (ciphertext / message), 1}; an out-of-range index rejects
 extern "C" __global__ void LCB_BOUNDS k_rlc_census_desc(const u32 *grp_idx, const u32 *key_idx, u32 m, u32 n_grp,
                                                        u32 n_keys, uint4 *desc, uint8_t *accept) {
+    LCB_LATENCY_PRIO();
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
     u32 c = grp_idx[i];
@@ -507,6 +519,7 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_census_desc(const u32 *grp_idx, cons
 // and at least half of them failed their exact check.  count[0] += suspect keys.
 extern "C" __global__ void LCB_BOUNDS k_rlc_census_stats(const u32 *key_idx, u32 m, u32 n_keys, const uint8_t *cval,
                                                         const uint8_t *accept, u32 *susp, u32 *count) {
+    LCB_LATENCY_PRIO();
     u32 k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_keys) return;
     u32 live = 0, bad = 0;
@@ -525,6 +538,7 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_census_stats(const u32 *key_idx, u32
 extern "C" __global__ void LCB_BOUNDS k_rlc_suspect_split(const uint4 *desc, u32 n_groups, const u32 *key_idx,
                                                          u32 n_keys, const u32 *susp, const uint8_t *accept,
                                                          uint4 *out, u32 *count) {
+    LCB_LATENCY_PRIO();
     u32 g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n_groups) return;
     uint4 d = desc[g];

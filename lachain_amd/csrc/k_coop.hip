@@ -17,6 +17,7 @@ extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_tpke_miller(const 
                                                                          const g1a_st *gpts, u32 n_groups,
                                                                          u32 *f_soa, uint8_t *gacc, uint8_t *fb,
                                                                          u32 npairs) {
+    LCB_LATENCY_PRIO();
     __shared__ uint4 lds[CP_LDS_QUADS];
     const Cp c = cp_init(lds);
     const u32 item = blockIdx.x * CP_G + c.g;
@@ -68,6 +69,7 @@ extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_tpke_miller(const 
 // on the fly)
 extern "C" __global__ void LCB_PAIR_BOUNDS k_rlc_miller_fallback(const u32 *lines, const uint4 *desc, const g1a_st *gpts,
                                                                 u32 n_groups, u32 *f_soa, const uint8_t *fb) {
+    LCB_LATENCY_PRIO();
     u32 g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= n_groups || !fb[g]) return;
     u32 c = desc[g].z;
@@ -82,6 +84,7 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_rlc_miller_fallback(const u32 *line
 // accept[i] &= (final_exp(f_i) == 1) for f_i in park slot 0 (slots 0..4 as working space); slot 0 <- the final
 // exponentiation (the GT value: the level-2 search of k_batch.hip compares these), as k_final_exp_check leaves it
 extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_final_exp_check(u32 *park, u32 n, uint8_t *accept) {
+    LCB_LATENCY_PRIO();
     __shared__ uint4 lds[CP_LDS_QUADS];
     const Cp c = cp_init(lds);
     const u32 item = blockIdx.x * CP_G + c.g;
@@ -103,6 +106,7 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_exact_points(const uint8_t *ct_ok, 
                                                          u32 n_keys, const u32 *ct_idx, const u32 *dec_idx,
                                                          const uint8_t *ui, u32 n, g1a_st *gpts, uint4 *desc,
                                                          uint8_t *accept) {
+    LCB_LATENCY_PRIO();
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u32 c = ct_idx[i], d = dec_idx[i];

@@ -115,6 +115,7 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_gr
                                                     const u32 *dec_idx, const uint8_t *ui, const u32 *rU,
                                                     const u32 *rY, u32 n, g1a_st *gpts, uint8_t *accept,
                                                     uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval) {
+    LCB_LATENCY_PRIO();
     // lanes = 4 (latency-bound levels): four lanes per group, t = 4g + 2 half + side — side 0 sums the U records,
     // side 1 the Y records, each half half of the group's shares; half 1's partial sum reaches half 0 through LDS (one
     // addition), so the serial chain is ~len/2 additions + one inversion.  lanes = 1 (levels of many entries, e.g.
@@ -210,6 +211,7 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_gr
 // negated), so checks g and ns + g give gamma_c = prod g_i^(c_i s_i) and gamma_t = prod g_i^(t_i s_i).
 extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum2(const uint4 *sdesc, u32 ns, const u32 *rU, const u32 *rY, u32 n,
                                                       const u32 *dec_idx, u32 n_keys, const u32 *susp, g1a_st *gpts) {
+    LCB_LATENCY_PRIO();
     // four lanes per group: (side, which) — each lane one output record, so one inversion (to affine) per lane
     u32 t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= 4 * ns) return;

@@ -66,6 +66,7 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_ct_prepare(const uint8_t *cts_u, co
 // ct_ok.  An undecodable ciphertext keeps H's real line set (ct_ok = 0 gates every use) and gets W = infinity.
 extern "C" __global__ void LCB_BOUNDS k_tpke_ct_prepare_h(const uint8_t *cts_u, const uint8_t *v_data, const u32 *v_off,
                                                          u32 c0, u32 n_cts, u32 *lines, uint8_t *h_ok, int flags) {
+    LCB_LATENCY_PRIO();
     u32 c = c0 + blockIdx.x * blockDim.x + threadIdx.x;     // ciphertexts [c0, n_cts)
     if (c >= n_cts) return;
     uint8_t d[64];
@@ -84,6 +85,7 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_ct_prepare_h(const uint8_t *cts_u, 
 extern "C" __global__ void LCB_BOUNDS k_tpke_ct_prepare_w(const uint8_t *cts_u, const uint8_t *cts_w, u32 c0,
                                                          u32 n_cts, u32 *lines, uint8_t *ct_ok, uint8_t *w_g2,
                                                          int flags) {
+    LCB_LATENCY_PRIO();
     u32 c = c0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_cts) return;
     g1a U;
@@ -98,6 +100,7 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_ct_prepare_w(const uint8_t *cts_u, 
     w_g2[c] = (r & LCB_LS_IN_G2) ? 1 : 0;
 }
 extern "C" __global__ void LCB_BOUNDS k_ct_ok_merge(uint8_t *ct_ok, const uint8_t *h_ok, u32 c0, u32 n_cts) {
+    LCB_LATENCY_PRIO();
     u32 c = c0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (c < n_cts) ct_ok[c] = ct_ok[c] && h_ok[c];
 }
@@ -107,6 +110,7 @@ extern "C" __global__ void LCB_BOUNDS k_ct_ok_merge(uint8_t *ct_ok, const uint8_
 // the batched check's W-in-G2 flags, w_g2[c] for set 2c + 1 (W of ciphertext c) from the loop's last point
 // (lineset_in_g2): the membership test costs no ladder of its own.
 extern "C" __global__ void LCB_BOUNDS k_lineset_fill(u32 *lines, u32 n_sets, const u32 *sets, uint8_t *w_g2) {
+    LCB_LATENCY_PRIO();
     u32 k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_sets) return;
     u32 *ls = lines + (size_t)(sets ? sets[k] : k) * LCB_LINESET_WORDS;
@@ -158,6 +162,7 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_miller(const u32 *lines, const
 // shares, Fp12 state parked in LDS 30 % slower than the former.
 extern "C" int lcbk_fe_slots() { return LCB_FE_ASM_SLOTS; }
 extern "C" __global__ void LCB_PAIR_BOUNDS k_final_exp_check(u32 *park, u32 n, uint8_t *accept) {
+    LCB_LATENCY_PRIO();
     __shared__ uint4 fx_lds[36 * LCB_BLOCK];      // per lane: the two Fp6 products of a slot multiplication
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;

@@ -57,6 +57,9 @@ DI void fp12_load_soa_fresh(fp12 &f, const u32 *base, size_t n, size_t i) {
 #define LCB_TU_CONFIG(tag)                                                                                        \
     extern "C" int lcbk_cfg_##tag(u32 sign_b) {                                                                 \
         return hipMemcpyToSymbol(HIP_SYMBOL(lcb_g2_sign_b), &sign_b, sizeof sign_b) == hipSuccess ? 0 : -1;     \
+    }                                                                                                             \
+    extern "C" int lcbk_prio_##tag(u32 on) {                                                                    \
+        return hipMemcpyToSymbol(HIP_SYMBOL(lcb_wave_prio), &on, sizeof on) == hipSuccess ? 0 : -1;             \
     }
 #define LCB_LAUNCH(name, ...) hipLaunchKernelGGL(name, grid, dim3(LCB_BLOCK), 0, s, __VA_ARGS__)
 static_assert(sizeof(g1a_st) == 112 && sizeof(g2a_st) == 208, "record sizes");

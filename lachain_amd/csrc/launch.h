@@ -124,6 +124,34 @@ extern "C" int lcbk_cfg_k_ptmul(u32 sign_b);
 // cooperative single scalar multiplications (k_ptmul.hip): n_groups ladders of one wave
 extern "C" void lcbk_ptmul_g1(hipStream_t s, const void *jobs, u32 n_groups, void *out);
 extern "C" void lcbk_ptmul_g2(hipStream_t s, const void *jobs, u32 n_groups, void *out);
+extern "C" int lcbk_prio_k_batch(u32 on);
+extern "C" int lcbk_prio_k_coop(u32 on);
+extern "C" int lcbk_prio_k_dkg(u32 on);
+extern "C" int lcbk_prio_k_lagrange(u32 on);
+extern "C" int lcbk_prio_k_mcl(u32 on);
+extern "C" int lcbk_prio_k_msm(u32 on);
+extern "C" int lcbk_prio_k_ops(u32 on);
+extern "C" int lcbk_prio_k_rlc_rand(u32 on);
+extern "C" int lcbk_prio_k_scalar(u32 on);
+extern "C" int lcbk_prio_k_tpke(u32 on);
+extern "C" int lcbk_prio_k_ts(u32 on);
+extern "C" int lcbk_prio_k_ptmul(u32 on);
+static inline int lcbk_set_wave_prio(int on) {
+    int rc = 0;
+    rc |= lcbk_prio_k_batch((u32)on);
+    rc |= lcbk_prio_k_coop((u32)on);
+    rc |= lcbk_prio_k_dkg((u32)on);
+    rc |= lcbk_prio_k_lagrange((u32)on);
+    rc |= lcbk_prio_k_mcl((u32)on);
+    rc |= lcbk_prio_k_msm((u32)on);
+    rc |= lcbk_prio_k_ops((u32)on);
+    rc |= lcbk_prio_k_rlc_rand((u32)on);
+    rc |= lcbk_prio_k_scalar((u32)on);
+    rc |= lcbk_prio_k_tpke((u32)on);
+    rc |= lcbk_prio_k_ts((u32)on);
+    rc |= lcbk_prio_k_ptmul((u32)on);
+    return rc;
+}
 // every kernel unit's G2 sign-flag convention (curve.hpp lcb_g2_sign_b)
 static inline int lcbk_set_g2_sign_b(int sign_b) {
     int rc = 0;

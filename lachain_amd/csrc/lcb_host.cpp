@@ -1726,6 +1726,12 @@ extern "C" int lcb_set_fork_mode(int mode) {
     g_fork_mode.store(mode >= 1 && mode <= 3 ? mode : 0);
     return 0;
 }
+extern "C" int lcb_set_wave_priority(int on) {
+    if (!tuning_allowed("lcb_set_wave_priority")) return -1;
+    if (!ready()) return -1;
+    if (lcbk_set_wave_prio(on != 0)) { set_err("lcb_set_wave_priority: device configuration failed"); return -1; }
+    return 0;
+}
 extern "C" int lcb_set_msm_chunk(int records_per_lane) {
     if (!tuning_allowed("lcb_set_msm_chunk")) return -1;
     if (records_per_lane < 0 || records_per_lane > 65536) { set_err("lcb_set_msm_chunk: 0..65536"); return -1; }

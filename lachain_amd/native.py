@@ -54,6 +54,7 @@ _SIGS = {
     "lcb_set_line_mode": (ctypes.c_int, [ctypes.c_int]),
     "lcb_set_g2_sign_from_b": (ctypes.c_int, [ctypes.c_int]),
     "lcb_set_msm_chunk": (ctypes.c_int, [ctypes.c_int]),
+    "lcb_set_wave_priority": (ctypes.c_int, [ctypes.c_int]),
     "lcb_last_error": (ctypes.c_char_p, []),
     "lcb_error_count": (ctypes.c_uint64, []),
     "lcb_test_inject_failure": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
@@ -742,6 +743,11 @@ def inject_failure(site, count=1):
     """test hook (LCB_ALLOW_TEST_HOOKS=1): the next `count` passes through fault site `site` fail"""
     if lib().lcb_test_inject_failure(int(site), int(count)) != 0:
         raise RuntimeError("inject_failure: " + last_error())
+
+
+def set_wave_priority(on):
+    """latency-bound batched-check kernels at raised wave priority (default on)"""
+    _tuning(lib().lcb_set_wave_priority(1 if on else 0), "set_wave_priority")
 
 
 def set_msm_chunk(records_per_lane):

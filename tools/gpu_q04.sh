@@ -9,9 +9,11 @@ if [ -n "$TESTS" ]; then
   timeout -k 10 500 python -u -X faulthandler -m pytest $TESTS -m gpu -x -v --timeout 150 --timeout-method thread > gpurun_out/${TAG}_tests.txt 2>&1 || { echo "TESTS FAILED"; tail -40 gpurun_out/${TAG}_tests.txt; exit 1; }
   tail -2 gpurun_out/${TAG}_tests.txt
 fi
+for PR in ${PRIOS:-1}; do
 for P in $PIPES; do
-  timeout -k 10 300 python3 -u bench.py --tpke-exact 0 --ts-rounds 0 --msm-sizes= --replay-n 0 --ecdsa-sigs 0 --dkg-n 0 --rs-n 0 --mcl-reps 0 --no-cpu-baseline --pattern-steps 0 --steps ${STEPS:-10} --warmup 2 --tpke-pipeline $P > gpurun_out/${TAG}_p$P.txt 2> gpurun_out/${TAG}_p$P.err || { echo "BENCH FAILED p$P"; tail -20 gpurun_out/${TAG}_p$P.err; exit 1; }
-  python3 -c "import json,sys; d=json.loads(open('gpurun_out/${TAG}_p$P.txt').read().strip().splitlines()[-1]); print('pipe $P', round(d['value']/1e6,3), 'M/s', round(d['ms_per_step'],2), 'ms', d['config']['decision_mismatches'], 'mism')"
+  LCB_ALLOW_TUNING=1 LCB_WAVE_PRIO=$PR timeout -k 10 300 python3 -u bench.py --tpke-exact 0 --ts-rounds 0 --msm-sizes= --replay-n 0 --ecdsa-sigs 0 --dkg-n 0 --rs-n 0 --mcl-reps 0 --no-cpu-baseline --pattern-steps 0 --steps ${STEPS:-10} --warmup 2 --tpke-pipeline $P > gpurun_out/${TAG}_p${P}_w$PR.txt 2> gpurun_out/${TAG}_p${P}_w$PR.err || { echo "BENCH FAILED p$P"; tail -20 gpurun_out/${TAG}_p${P}_w$PR.err; exit 1; }
+  python3 -c "import json,sys; d=json.loads(open('gpurun_out/${TAG}_p${P}_w$PR.txt').read().strip().splitlines()[-1]); print('prio $PR pipe $P', round(d['value']/1e6,3), 'M/s', round(d['ms_per_step'],2), 'ms', d['config']['decision_mismatches'], 'mism')"
+done
 done
 if [ -n "$MSMB" ]; then
   for K in $MSMB; do
