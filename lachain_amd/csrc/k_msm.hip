@@ -166,10 +166,16 @@ DI void load_aff(fp &x, fp &y, const fp *pts, u32 idx) {
     for (int j = 0; j < 12; j++) { x.v[j] = w[j]; y.v[j] = w[12 + j]; }
 }
 
+// Bucket layout: bucket k = (segment s = k / L, position j = k % L) of the reduction (k_msm_bucket_reduce) is stored at
+// j * n_seg + s, so the reduction's lanes (one segment each, all at the same position j per step) read 64 consecutive
+// buckets per wave instruction instead of 64 buckets L apart.
+DI size_t bidx(u32 k, u32 L, u32 n_seg) { return (size_t)(k % L) * n_seg + k / L; }
+
 // point index v < n_pts reads pts, v >= n_pts reads pts2 (the phi(P) half of the GLV form).  The next record's
 // point is loaded while the current addition runs (one gather in flight per lane).
 extern "C" __global__ void LCB_BOUNDS k_msm_bucket_acc(const fp *pts, const fp *pts2, u32 n_pts, const u32 *vals,
-                                                      const u32 *start, const u32 *end, u32 nb, g1 *buckets) {
+                                                      const u32 *start, const u32 *end, u32 nb, g1 *buckets, u32 L,
+                                                      u32 n_seg) {
     u32 b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
     g1 acc;
@@ -194,7 +200,7 @@ extern "C" __global__ void LCB_BOUNDS k_msm_bucket_acc(const fp *pts, const fp *
         if (v >> 31) fp_neg(y, y);
         jac_add_aff(acc, acc, x, y);
     }
-    buckets[b] = acc;
+    buckets[bidx(b, L, n_seg)] = acc;
 }
 
 #define MSM_ADD(r, p, q) grp_add(r, p, q)
@@ -206,15 +212,16 @@ extern "C" __global__ void LCB_BOUNDS k_msm_bucket_acc(const fp *pts, const fp *
 // continues into a later chunk to tailp[j] (both always written, infinity when unused), and k_msm_bucket_fix adds the
 // pieces of the buckets that span chunks.  The sentinel records (digit 0) sort last and end a chunk.
 DI void msm_flush(const g1 &acc, u32 k, u32 e0, u32 e1, const u32 *start, const u32 *end, g1 *buckets, g1 *head,
-                  g1 *tail) {
+                  g1 *tail, u32 L, u32 n_seg) {
     const u32 s = start[k], en = end[k];
-    if (s >= e0 && en <= e1) buckets[k] = acc;
+    if (s >= e0 && en <= e1) buckets[bidx(k, L, n_seg)] = acc;
     else if (s < e0) *head = acc;
     else *tail = acc;
 }
 extern "C" __global__ void LCB_BOUNDS k_msm_chunk_acc(const fp *pts, const fp *pts2, u32 n_pts, const u32 *keys,
                                                      const u32 *vals, u32 m, u32 K, u32 sentinel, const u32 *start,
-                                                     const u32 *end, g1 *buckets, g1 *headp, g1 *tailp) {
+                                                     const u32 *end, g1 *buckets, g1 *headp, g1 *tailp, u32 L,
+                                                     u32 n_seg) {
     const u32 j = blockIdx.x * blockDim.x + threadIdx.x;
     const size_t e0s = (size_t)j * K;
     if (e0s >= m) return;
@@ -244,7 +251,7 @@ extern "C" __global__ void LCB_BOUNDS k_msm_chunk_acc(const fp *pts, const fp *p
             load_aff(nx, ny, idx < n_pts ? pts : pts2, idx < n_pts ? idx : idx - n_pts);
         }
         if (k != cur) {
-            msm_flush(acc, cur, e0, e1, start, end, buckets, headp + j, tailp + j);
+            msm_flush(acc, cur, e0, e1, start, end, buckets, headp + j, tailp + j, L, n_seg);
             acc = inf;
             cur = k;
         }
@@ -252,18 +259,18 @@ extern "C" __global__ void LCB_BOUNDS k_msm_chunk_acc(const fp *pts, const fp *p
         if (v >> 31) fp_neg(y, y);
         jac_add_aff(acc, acc, x, y);
     }
-    msm_flush(acc, cur, e0, e1, start, end, buckets, headp + j, tailp + j);
+    msm_flush(acc, cur, e0, e1, start, end, buckets, headp + j, tailp + j, L, n_seg);
 }
 // buckets spanning chunks: tail of the first chunk + heads of the later ones; empty buckets: infinity
 extern "C" __global__ void LCB_BOUNDS k_msm_bucket_fix(const u32 *start, const u32 *end, u32 K, const g1 *headp,
-                                                      const g1 *tailp, u32 nb, g1 *buckets) {
+                                                      const g1 *tailp, u32 nb, g1 *buckets, u32 L, u32 n_seg) {
     const u32 k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nb) return;
     const u32 s = start[k], en = end[k];
     if (s == en) {
         g1 inf;
         jac_set_inf(inf);
-        buckets[k] = inf;
+        buckets[bidx(k, L, n_seg)] = inf;
         return;
     }
     const u32 j0 = s / K, j1 = (en - 1) / K;
@@ -271,7 +278,7 @@ extern "C" __global__ void LCB_BOUNDS k_msm_bucket_fix(const u32 *start, const u
     g1 acc = tailp[j0];
 #pragma unroll 1
     for (u32 j = j0 + 1; j <= j1; j++) MSM_ADD(acc, acc, headp[j]);
-    buckets[k] = acc;
+    buckets[bidx(k, L, n_seg)] = acc;
 }
 
 // The reduction / combination kernels are latency chains (one lane's serial additions and doublings); their group
@@ -289,14 +296,17 @@ extern "C" __global__ void LCB_BOUNDS k_msm_bucket_reduce(const g1 *buckets, u32
     u32 s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= n_seg) return;
     u32 per_win = half / L, w = s / per_win, a = (s % per_win) * L;
-    const g1 *B = buckets + (size_t)w * half + a;
+    const g1 *B = buckets + s;                      // position j of segment s at j * n_seg + s (bidx)
     if (w == hi_win) a += half;
     g1 run, acc;
     jac_set_inf(run);
     jac_set_inf(acc);
+    g1 nb = B[(size_t)(L - 1) * n_seg];
 #pragma unroll 1
     for (u32 j = L; j-- > 0;) {
-        MSM_ADD(run, run, B[j]);
+        const g1 cb = nb;
+        if (j) nb = B[(size_t)(j - 1) * n_seg];      // the next bucket, loaded during these additions
+        MSM_ADD(run, run, cb);
         MSM_ADD(acc, acc, run);
     }
     if (a) {
@@ -395,17 +405,17 @@ extern "C" void lcbk_msm_digits(dim3 grid, hipStream_t s, const uint8_t *scalars
 extern "C" void lcbk_msm_bounds(dim3 grid, hipStream_t s, const u32 *keys, u32 m, u32 sentinel, u32 *start, u32 *end) {
     LCB_LAUNCH(k_msm_bounds, keys, m, sentinel, start, end);
 }
-extern "C" void lcbk_msm_bucket_acc(dim3 grid, hipStream_t s, const void *pts, const void *pts2, u32 n_pts, const u32 *vals, const u32 *start, const u32 *end, u32 nb, void *buckets) {
-    LCB_LAUNCH(k_msm_bucket_acc, (const fp *)pts, (const fp *)pts2, n_pts, vals, start, end, nb, (g1 *)buckets);
+extern "C" void lcbk_msm_bucket_acc(dim3 grid, hipStream_t s, const void *pts, const void *pts2, u32 n_pts, const u32 *vals, const u32 *start, const u32 *end, u32 nb, void *buckets, u32 L, u32 n_seg) {
+    LCB_LAUNCH(k_msm_bucket_acc, (const fp *)pts, (const fp *)pts2, n_pts, vals, start, end, nb, (g1 *)buckets, L, n_seg);
 }
-extern "C" void lcbk_msm_chunk_acc(hipStream_t s, const void *pts, const void *pts2, u32 n_pts, const u32 *keys, const u32 *vals, u32 m, u32 K, u32 sentinel, const u32 *start, const u32 *end, void *buckets, void *headp, void *tailp) {
+extern "C" void lcbk_msm_chunk_acc(hipStream_t s, const void *pts, const void *pts2, u32 n_pts, const u32 *keys, const u32 *vals, u32 m, u32 K, u32 sentinel, const u32 *start, const u32 *end, void *buckets, void *headp, void *tailp, u32 L, u32 n_seg) {
     const u32 n_chunks = (u32)(((size_t)m + K - 1) / K);
     dim3 grid((n_chunks + LCB_BLOCK - 1) / LCB_BLOCK);
-    LCB_LAUNCH(k_msm_chunk_acc, (const fp *)pts, (const fp *)pts2, n_pts, keys, vals, m, K, sentinel, start, end, (g1 *)buckets, (g1 *)headp, (g1 *)tailp);
+    LCB_LAUNCH(k_msm_chunk_acc, (const fp *)pts, (const fp *)pts2, n_pts, keys, vals, m, K, sentinel, start, end, (g1 *)buckets, (g1 *)headp, (g1 *)tailp, L, n_seg);
 }
-extern "C" void lcbk_msm_bucket_fix(hipStream_t s, const u32 *start, const u32 *end, u32 K, const void *headp, const void *tailp, u32 nb, void *buckets) {
+extern "C" void lcbk_msm_bucket_fix(hipStream_t s, const u32 *start, const u32 *end, u32 K, const void *headp, const void *tailp, u32 nb, void *buckets, u32 L, u32 n_seg) {
     dim3 grid((nb + LCB_BLOCK - 1) / LCB_BLOCK);
-    LCB_LAUNCH(k_msm_bucket_fix, start, end, K, (const g1 *)headp, (const g1 *)tailp, nb, (g1 *)buckets);
+    LCB_LAUNCH(k_msm_bucket_fix, start, end, K, (const g1 *)headp, (const g1 *)tailp, nb, (g1 *)buckets, L, n_seg);
 }
 extern "C" void lcbk_msm_digits_glv(dim3 grid, hipStream_t s, const uint8_t *scalars, u32 n, u32 c, u32 nwin, u32 *keys, u32 *vals) {
     LCB_LAUNCH(k_msm_digits_glv, scalars, n, c, nwin, keys, vals);

@@ -36,10 +36,10 @@ extern "C" void lcbk_g1_sum(dim3 grid, hipStream_t s, const void *parts, const u
 extern "C" void lcbk_g2_sum(dim3 grid, hipStream_t s, const void *parts, const uint8_t *ok_in, const u32 *off, u32 n_problems, uint8_t *status, uint8_t *out);
 extern "C" void lcbk_msm_digits(dim3 grid, hipStream_t s, const uint8_t *scalars, u32 n, u32 c, u32 nwin, u32 *keys, u32 *vals);
 extern "C" void lcbk_msm_bounds(dim3 grid, hipStream_t s, const u32 *keys, u32 m, u32 sentinel, u32 *start, u32 *end);
-extern "C" void lcbk_msm_bucket_acc(dim3 grid, hipStream_t s, const void *pts, const void *pts2, u32 n_pts, const u32 *vals, const u32 *start, const u32 *end, u32 nb, void *buckets);
+extern "C" void lcbk_msm_bucket_acc(dim3 grid, hipStream_t s, const void *pts, const void *pts2, u32 n_pts, const u32 *vals, const u32 *start, const u32 *end, u32 nb, void *buckets, u32 L, u32 n_seg);
 // record-balanced bucket accumulation (K records per lane) and the fix-up of buckets spanning chunks
-extern "C" void lcbk_msm_chunk_acc(hipStream_t s, const void *pts, const void *pts2, u32 n_pts, const u32 *keys, const u32 *vals, u32 m, u32 K, u32 sentinel, const u32 *start, const u32 *end, void *buckets, void *headp, void *tailp);
-extern "C" void lcbk_msm_bucket_fix(hipStream_t s, const u32 *start, const u32 *end, u32 K, const void *headp, const void *tailp, u32 nb, void *buckets);
+extern "C" void lcbk_msm_chunk_acc(hipStream_t s, const void *pts, const void *pts2, u32 n_pts, const u32 *keys, const u32 *vals, u32 m, u32 K, u32 sentinel, const u32 *start, const u32 *end, void *buckets, void *headp, void *tailp, u32 L, u32 n_seg);
+extern "C" void lcbk_msm_bucket_fix(hipStream_t s, const u32 *start, const u32 *end, u32 K, const void *headp, const void *tailp, u32 nb, void *buckets, u32 L, u32 n_seg);
 extern "C" void lcbk_msm_digits_glv(dim3 grid, hipStream_t s, const uint8_t *scalars, u32 n, u32 c, u32 nwin, u32 *keys, u32 *vals);
 extern "C" void lcbk_msm_phi(dim3 grid, hipStream_t s, const void *pts, u32 n, void *out);
 extern "C" void lcbk_msm_bucket_reduce(dim3 grid, hipStream_t s, const void *buckets, u32 half, u32 L, u32 n_seg, u32 hi_win, void *seg_out);

@@ -1561,10 +1561,10 @@ int msm_enqueue(lcb_ctx *cx, void *out_jac, const void *pts, const uint8_t *scal
         const size_t nch = (m + K - 1) / K;
         void *hp = b[12].get((nch ? nch : 1) * LCB_G1_JAC_BYTES), *tp = b[13].get((nch ? nch : 1) * LCB_G1_JAC_BYTES);
         if (!hp || !tp) { set_err("msm: device allocation failed"); return -1; }
-        if (m) lcbk_msm_chunk_acc(s, pts, phi, (u32)n, keys, vals, (u32)m, K, sentinel, st, en, buckets, hp, tp);
-        lcbk_msm_bucket_fix(s, st, en, K, hp, tp, nb, buckets);
+        if (m) lcbk_msm_chunk_acc(s, pts, phi, (u32)n, keys, vals, (u32)m, K, sentinel, st, en, buckets, hp, tp, L, n_seg);
+        lcbk_msm_bucket_fix(s, st, en, K, hp, tp, nb, buckets, L, n_seg);
     } else {
-        lcbk_msm_bucket_acc(dim3(nblk(nb)), s, pts, phi, (u32)n, vals, st, en, nb, buckets);
+        lcbk_msm_bucket_acc(dim3(nblk(nb)), s, pts, phi, (u32)n, vals, st, en, nb, buckets, L, n_seg);
     }
     hipEventRecord(cx->msm_ev[4], s);
     lcbk_msm_bucket_reduce(dim3(nblk(n_seg)), s, buckets, half, L, n_seg, glv ? nwin : 0xffffffffu, segs);
