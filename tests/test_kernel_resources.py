@@ -40,7 +40,7 @@ BUDGET = {
     "k_g2_mul2_lanes": (4530, 22672),         # two GLS tables (31 entries) per lane: the assembly's paired lanes
     "k_g2_sum": (204, 1008),
     "k_lineset_fill": (0, 1824),
-    "k_msm_bucket_reduce": (0, 600),
+    "k_msm_bucket_reduce": (0, 744),          # + the prefetched next bucket
     "k_msm_horner": (0, 168),
     "k_msm_bucket_fix": (0, 168),
     "k_op": (3038, 8484),
