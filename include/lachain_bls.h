@@ -512,6 +512,10 @@ int64_t lcb_queue_tpke_verify(lcb_queue *q, const uint8_t y48[48], const uint8_t
                               size_t v_len, const uint8_t w96[96], const uint8_t ui48[48]);
 int64_t lcb_queue_ts_verify(lcb_queue *q, const uint8_t pk48[48], const uint8_t *msg, size_t msg_len,
                             const uint8_t sig96[96]);
+/* prepare a TPKE ciphertext (U || V || W: hash-to-G2 of U || V and both line sets) on the worker its shares go to,
+   ahead of them — the reference decrypts every ciphertext of the common subset (HoneyBadger.cs:144-146) before it
+   handles the other validators' shares for it (HoneyBadger.cs:190-213).  Asynchronous; 0 or -1 (bad arguments). */
+int lcb_queue_tpke_prepare(lcb_queue *q, const uint8_t u48[48], const uint8_t *v, size_t v_len, const uint8_t w96[96]);
 int lcb_queue_wait(lcb_queue *q, int64_t ticket);
 int lcb_queue_flush(lcb_queue *q);
 int lcb_queue_stats(lcb_queue *q, uint64_t out[3]);

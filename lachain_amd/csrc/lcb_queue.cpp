@@ -13,6 +13,13 @@
 // same per-share results the batch entry points produce (bit-exact with VerifyShare / ValidateSignature).
 // lcb_queue_set_batched(q, m) sends flushes of at least m shares through the randomized batch checks instead
 // (k_batch.hip): more shares per GPU-second, a few more latency-bound launches per flush.
+//
+// Worker affinity (round 4): each worker keeps the prepared line sets of the ciphertexts it has seen (its thread
+// context's cache), so a ciphertext's shares always go to the same worker (hash of its bytes), and
+// lcb_queue_tpke_prepare(ct) prepares a ciphertext on that worker AHEAD of its shares — the reference decrypts every
+// ciphertext of the common subset (PrivateKey.Decrypt, which hashes U || V to G2: HoneyBadger.cs:144-146) before the
+// other validators' decryption shares for it are handled (HoneyBadger.cs:190-213), so the first share no longer waits
+// for hash-to-G2 and two line sets.
 #include <stdint.h>
 #include <string.h>
 #include <algorithm>
@@ -43,14 +50,17 @@ struct TsItem {
 };
 }  // namespace
 
+#define LCB_QUEUE_WORKERS 2
 struct lcb_queue {
     std::mutex mu;
     std::condition_variable cv_work, cv_done;
     size_t max_batch;
     std::chrono::microseconds max_delay;
-    std::vector<TpkeItem> tpke;
-    std::vector<TsItem> ts;
-    clk::time_point oldest;
+    std::vector<TpkeItem> tpke[LCB_QUEUE_WORKERS];     // per worker (ciphertext affinity)
+    std::vector<std::string> prep[LCB_QUEUE_WORKERS];  // ciphertexts to prepare ahead of their shares
+    clk::time_point oldest[LCB_QUEUE_WORKERS];
+    std::vector<TsItem> ts;                            // any worker
+    clk::time_point ts_oldest;
     bool stop = false, flush_now = false;
     int64_t next_ticket = 1;
     std::unordered_map<int64_t, int8_t> results;     // ticket -> 1 / 0 / -1 (batch failed), until waited for
@@ -63,8 +73,8 @@ struct lcb_queue {
     // two workers, each with its own thread context (and prepared-ciphertext cache): a flush does not wait for the
     // previous one's GPU round trip, so a share's latency is its own batch's, not two
     std::vector<std::thread> workers;
+    uint64_t prepared = 0;
 };
-#define LCB_QUEUE_WORKERS 2
 
 namespace {
 
@@ -166,30 +176,62 @@ void run_ts(lcb_queue *q, std::vector<TsItem> &items, size_t batched_min) {
     }
 }
 
-void worker_loop(lcb_queue *q) {
+// prepare ciphertexts (U || W || V) into this worker's cache: the cached verify with no shares
+void run_prepare(lcb_queue *q, std::vector<std::string> &cts) {
+    std::unordered_map<std::string, uint32_t> cidx;
+    std::vector<uint8_t> us, ws, vs;
+    std::vector<uint32_t> voff(1, 0);
+    for (auto &ct : cts) {
+        if (!cidx.emplace(ct, (uint32_t)cidx.size()).second) continue;
+        const uint8_t *b = (const uint8_t *)ct.data();
+        us.insert(us.end(), b, b + 48);
+        ws.insert(ws.end(), b + 48, b + 144);
+        vs.insert(vs.end(), b + 144, b + ct.size());
+        voff.push_back((uint32_t)vs.size());
+    }
+    if (vs.empty()) vs.push_back(0);
+    int rc = lcb_tpke_verify_shares_cached(nullptr, 0, nullptr, 0, us.data(), ws.data(), vs.data(), voff.data(),
+                                           cidx.size(), nullptr, nullptr, nullptr);
+    std::lock_guard<std::mutex> lk(q->mu);
+    if (rc) q->last_error = lcb_last_error();
+    else q->prepared += cidx.size();
+}
+
+void worker_loop(lcb_queue *q, int w) {
     std::unique_lock<std::mutex> lk(q->mu);
     for (;;) {
-        size_t pending = q->tpke.size() + q->ts.size();
-        if (pending == 0) {
+        const size_t pt = q->tpke[w].size(), ps = q->ts.size(), pp = q->prep[w].size();
+        if (pt + ps + pp == 0) {
             if (q->stop) return;
             q->cv_work.wait(lk);
             continue;
         }
-        bool due = q->stop || q->flush_now || pending >= q->max_batch || clk::now() >= q->oldest + q->max_delay;
-        if (!due) {
-            q->cv_work.wait_until(lk, q->oldest + q->max_delay);
+        const clk::time_point now = clk::now();
+        const bool due_t = pt && (q->stop || q->flush_now || pt >= q->max_batch || now >= q->oldest[w] + q->max_delay);
+        const bool due_s = ps && (q->stop || q->flush_now || ps >= q->max_batch || now >= q->ts_oldest + q->max_delay);
+        if (!pp && !due_t && !due_s) {
+            clk::time_point next = clk::time_point::max();
+            if (pt) next = std::min(next, q->oldest[w] + q->max_delay);
+            if (ps) next = std::min(next, q->ts_oldest + q->max_delay);
+            q->cv_work.wait_until(lk, next);
             continue;
         }
         std::vector<TpkeItem> t;
         std::vector<TsItem> s;
-        t.swap(q->tpke);
-        s.swap(q->ts);
-        q->flush_now = false;
+        std::vector<std::string> p;
+        p.swap(q->prep[w]);
+        if (due_t) t.swap(q->tpke[w]);
+        if (due_s) s.swap(q->ts);
+        if (q->tpke[0].empty() && q->tpke[1].empty() && q->ts.empty()) q->flush_now = false;
         const size_t batched_min = q->batched_min;     // read under the lock (lcb_queue_set_batched writes it)
-        q->batches++;
-        q->items += pending;
-        if (pending > q->max_seen) q->max_seen = pending;
+        const size_t pending = t.size() + s.size();
+        if (pending) {
+            q->batches++;
+            q->items += pending;
+            if (pending > q->max_seen) q->max_seen = pending;
+        }
         lk.unlock();
+        if (!p.empty()) run_prepare(q, p);              // ahead of the shares: they then hit the cache
         if (!t.empty()) run_tpke(q, t, batched_min);
         if (!s.empty()) run_ts(q, s, batched_min);
         lk.lock();
@@ -197,12 +239,9 @@ void worker_loop(lcb_queue *q) {
     }
 }
 
-int64_t enqueue_common(lcb_queue *q, std::unique_lock<std::mutex> &lk) {
-    (void)lk;
-    size_t pending = q->tpke.size() + q->ts.size();
-    if (pending == 1) q->oldest = clk::now();
-    if (pending == 1 || pending >= q->max_batch) q->cv_work.notify_one();
-    return q->next_ticket - 1;
+int worker_of(const std::string &ct) { return (int)(std::hash<std::string>{}(ct) % LCB_QUEUE_WORKERS); }
+void wake(lcb_queue *q, size_t pending, size_t max_batch) {
+    if (pending == 1 || pending >= max_batch) q->cv_work.notify_all();
 }
 
 }  // namespace
@@ -211,7 +250,7 @@ extern "C" lcb_queue *lcb_queue_create(size_t max_batch, uint32_t max_delay_us) 
     lcb_queue *q = new lcb_queue;
     q->max_batch = max_batch ? max_batch : 1;
     q->max_delay = std::chrono::microseconds(max_delay_us);
-    for (int k = 0; k < LCB_QUEUE_WORKERS; k++) q->workers.emplace_back(worker_loop, q);
+    for (int k = 0; k < LCB_QUEUE_WORKERS; k++) q->workers.emplace_back(worker_loop, q, k);
     return q;
 }
 extern "C" void lcb_queue_destroy(lcb_queue *q) {
@@ -235,12 +274,31 @@ extern "C" int64_t lcb_queue_tpke_verify(lcb_queue *q, const uint8_t y48[48], co
     it.ct.append((const char *)w96, 96);
     if (v_len) it.ct.append((const char *)v, v_len);
     memcpy(it.ui, ui48, 48);
+    const int w = worker_of(it.ct);
     std::unique_lock<std::mutex> lk(q->mu);
     if (q->stop) return -1;
     it.ticket = q->next_ticket++;
     q->open.insert(it.ticket);
-    q->tpke.push_back(std::move(it));
-    return enqueue_common(q, lk);
+    q->tpke[w].push_back(std::move(it));
+    const size_t pending = q->tpke[w].size();
+    if (pending == 1) q->oldest[w] = clk::now();
+    wake(q, pending, q->max_batch);
+    return q->next_ticket - 1;
+}
+extern "C" int lcb_queue_tpke_prepare(lcb_queue *q, const uint8_t u48[48], const uint8_t *v, size_t v_len,
+                                      const uint8_t w96[96]) {
+    if (!q || !u48 || !w96 || (v_len && !v)) return -1;
+    std::string ct;
+    ct.reserve(144 + v_len);
+    ct.append((const char *)u48, 48);
+    ct.append((const char *)w96, 96);
+    if (v_len) ct.append((const char *)v, v_len);
+    const int w = worker_of(ct);
+    std::lock_guard<std::mutex> lk(q->mu);
+    if (q->stop) return -1;
+    q->prep[w].push_back(std::move(ct));
+    q->cv_work.notify_all();
+    return 0;
 }
 extern "C" int64_t lcb_queue_ts_verify(lcb_queue *q, const uint8_t pk48[48], const uint8_t *msg, size_t msg_len,
                                        const uint8_t sig96[96]) {
@@ -254,7 +312,10 @@ extern "C" int64_t lcb_queue_ts_verify(lcb_queue *q, const uint8_t pk48[48], con
     it.ticket = q->next_ticket++;
     q->open.insert(it.ticket);
     q->ts.push_back(std::move(it));
-    return enqueue_common(q, lk);
+    const size_t pending = q->ts.size();
+    if (pending == 1) q->ts_oldest = clk::now();
+    wake(q, pending, q->max_batch);
+    return q->next_ticket - 1;
 }
 extern "C" int lcb_queue_flush(lcb_queue *q) {
     if (!q) return -1;

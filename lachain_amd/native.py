@@ -153,6 +153,8 @@ _SIGS = {
                                                c_size, ctypes.c_char_p, ctypes.c_char_p]),
     "lcb_queue_ts_verify": (ctypes.c_int64, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, c_size,
                                              ctypes.c_char_p]),
+    "lcb_queue_tpke_prepare": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, c_size,
+                                              ctypes.c_char_p]),
     "lcb_queue_wait": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     "lcb_queue_flush": (ctypes.c_int, [ctypes.c_void_p]),
     "lcb_queue_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
@@ -647,6 +649,14 @@ class BatchQueue:
         if t <= 0:
             raise ValueError("lcb_queue_tpke_verify: bad arguments")
         return t
+
+    def prepare_tpke(self, u48, v, w96):
+        """prepare a ciphertext ahead of its shares (lcb_queue_tpke_prepare; HoneyBadger.cs:144-146 decrypts every
+        ciphertext of the common subset before the other validators' shares for it arrive)"""
+        if len(u48) != 48 or len(w96) != 96:
+            raise ValueError("lcb_queue_tpke_prepare: U is 48 bytes, W 96")
+        if lib().lcb_queue_tpke_prepare(self.ptr, u48, v, len(v), w96) != 0:
+            raise ValueError("lcb_queue_tpke_prepare: bad arguments")
 
     def submit_ts(self, pk48, msg, sig96):
         t = lib().lcb_queue_ts_verify(self.ptr, pk48, msg, len(msg), sig96)

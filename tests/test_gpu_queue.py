@@ -93,3 +93,37 @@ def test_queue_deadline_flush_and_tickets(nat, items):
         tickets = [(q.submit_ts(*a) if k == "ts" else q.submit_tpke(*a), e) for k, a, e in items]
         for tk, e in reversed(tickets):
             assert q.wait(tk) == e
+
+
+def test_queue_prepare_ahead(nat, items):
+    """lcb_queue_tpke_prepare: the ciphertexts prepared on their workers before any share (HoneyBadger.cs:144-146
+    decrypts the common subset's ciphertexts first), an undecodable ciphertext and a repeated prepare among them; the
+    shares then submitted from 16 threads get the oracle's decisions, TS shares beside them"""
+    cts = []
+    for kind, args, _ in items:
+        if kind == "tpke" and (args[1], args[2], args[3]) not in cts:
+            cts.append((args[1], args[2], args[3]))
+    errors = []
+    with nat.BatchQueue(max_batch=64, max_delay_ms=2.0) as q:
+        for u, v, w in cts + cts[:2]:
+            q.prepare_tpke(u, v, w)
+        q.prepare_tpke(b"\xff" * 48, b"x", b"\xff" * 96)       # not a ciphertext: prepared as invalid, harmless
+        with pytest.raises(ValueError):
+            q.prepare_tpke(b"", b"", b"")
+
+        def worker(k):
+            try:
+                for idx in range(k, len(items), 16):
+                    kind, args, expect = items[idx]
+                    got = q.verify_tpke(*args) if kind == "tpke" else q.verify_ts(*args)
+                    if got != expect:
+                        errors.append((k, idx, got, expect))
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e))
+        th = [threading.Thread(target=worker, args=(k,)) for k in range(16)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=100)
+        assert not any(t.is_alive() for t in th)
+    assert not errors, errors[:5]

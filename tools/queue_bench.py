@@ -28,6 +28,10 @@ def main():
     ap.add_argument("--deadlines", default="1,5,20")
     ap.add_argument("--threads", default="16,64")
     ap.add_argument("--max-batch", type=int, default=65536)
+    ap.add_argument("--prepare-ahead", type=int, default=1,
+                    help="1: every ciphertext is prepared (lcb_queue_tpke_prepare) before its shares are submitted, as "
+                         "HoneyBadger decrypts the common subset's ciphertexts (HoneyBadger.cs:144-146) before it "
+                         "handles the other validators' shares (HoneyBadger.cs:190-213); 0: first sight in a flush")
     ap.add_argument("--burst", type=int, default=1,
                     help="shares a caller submits before waiting for them (1 = strict one-share-per-call)")
     args = ap.parse_args()
@@ -47,6 +51,13 @@ def main():
             lat, bad, count = [], [0], [0]
             stop = time.perf_counter() + args.seconds
             with nat.BatchQueue(max_batch=args.max_batch, max_delay_ms=dl) as q:
+                if args.prepare_ahead:                  # the epoch's ciphertexts, decrypted before shares arrive
+                    for u, v, w in inp["cts_list"]:
+                        q.prepare_tpke(u, v, w)
+                    q.flush()
+                    y, u, v, w, ui, e = recs[0]
+                    assert q.verify_tpke(y, u, v, w, ui) == e   # the prepares ran (one worker queue is FIFO)
+                    time.sleep(0.5)
                 def caller(k):
                     idx, my = k, []
                     while time.perf_counter() < stop:
@@ -72,7 +83,7 @@ def main():
                 elapsed = time.perf_counter() - t_start
                 st = q.stats()
             ms = np.array(lat) * 1e3
-            rows.append(dict(deadline_ms=dl, callers=nt, burst=args.burst, shares_per_s=count[0] / elapsed,
+            rows.append(dict(deadline_ms=dl, callers=nt, burst=args.burst, prepare_ahead=args.prepare_ahead, shares_per_s=count[0] / elapsed,
                              mean_batch=st["shares"] / max(1, st["batches"]), batches=st["batches"],
                              latency_ms={"p50": float(np.percentile(ms, 50)), "p90": float(np.percentile(ms, 90)),
                                          "p99": float(np.percentile(ms, 99))},
