@@ -21,6 +21,7 @@ import hashlib
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -955,8 +956,52 @@ def run_replay(args, nat, torch, dev, rank, world):
     d_shared = to_dev(torch, dev, np.full(nm, n, dtype=np.uint32))
 
     batched = not args.replay_exact
+    # the era's TPKE decryptions and its coins are independent (HoneyBadger runs them in separate protocol
+    # instances): with --replay-concurrent 1 they run side by side, each chain on its own host thread (so its own
+    # default library context) and HIP stream, and one chain's latency-bound check levels overlap the other's bulk
+    conc = args.replay_concurrent and batched
+    s_tp = torch.cuda.Stream(dev) if conc else None
+    s_ts = torch.cuda.Stream(dev) if conc else None
+
+    def tpke_chain(sh):
+        rc = lib.lcb_tpke_verify_shares_batched_dev(d_acc_t.data_ptr(), V * n * n, d_y.data_ptr(), n, d_u.data_ptr(),
+                                                    d_w.data_ptr(), d_v.data_ptr(), d_voff.data_ptr(), V * n,
+                                                    d_ct.data_ptr(), d_dec.data_ptr(), d_sh.data_ptr(), sh)
+        rc |= lib.lcb_tpke_partial_decrypt_prepared_dev(d_own.data_ptr(), d_own_st.data_ptr(), d_x.data_ptr(), 1,
+                                                        d_u.data_ptr(), V * n, sh)
+        rc |= lib.lcb_tpke_combine_dev(d_uc.data_ptr(), d_ucst.data_ptr(), d_acc_t.data_ptr(), d_sh.data_ptr(), n,
+                                       f + 1, V * n, sh)
+        return rc
+
+    def ts_chain(sh):
+        rc = lib.lcb_ts_verify_shares_batched_dev(d_acc_s.data_ptr(), nm * n, d_pks.data_ptr(), n + 1,
+                                                  d_sigs.data_ptr(), d_msg.data_ptr(), d_moff.data_ptr(), nm,
+                                                  d_midx.data_ptr(), d_pidx.data_ptr(), sh)
+        rc |= lib.lcb_ts_assemble_dev(d_comb.data_ptr(), d_cst.data_ptr(), d_acc_s.data_ptr(), d_sigs.data_ptr(), n,
+                                      f + 1, nm, sh)
+        rc |= lib.lcb_ts_verify_prepared_dev(d_cacc.data_ptr(), nm, n + 1, nm, d_comb.data_ptr(), d_ridx.data_ptr(),
+                                             d_shared.data_ptr(), sh)
+        return rc
+
+    import concurrent.futures
+    # one persistent thread per chain: each keeps its own default library context (and its workspaces) across steps
+    pools = [concurrent.futures.ThreadPoolExecutor(max_workers=1) for _ in range(2)] if conc else []
+
+    def run_chain(k):
+        st = s_tp if k == 0 else s_ts
+        rc = (tpke_chain if k == 0 else ts_chain)(st.cuda_stream)
+        st.synchronize()
+        return rc, (nat.last_error() if rc else "")
+
+    def step_concurrent():
+        res = [f.result() for f in [pools[k].submit(run_chain, k) for k in range(2)]]
+        for rc, err in res:
+            if rc:
+                raise RuntimeError(err)
 
     def step():
+        if conc:
+            return step_concurrent()
         if batched:      # prepare + randomized group checks in one call each (k_batch.hip)
             rc = lib.lcb_tpke_verify_shares_batched_dev(d_acc_t.data_ptr(), V * n * n, d_y.data_ptr(), n,
                                                         d_u.data_ptr(), d_w.data_ptr(), d_v.data_ptr(),
@@ -999,6 +1044,8 @@ def run_replay(args, nat, torch, dev, rank, world):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    for pl in pools:
+        pl.shutdown()
     # checks: bitmaps, every view decrypts every ciphertext and assembles every coin, spot values vs oracle
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as o
@@ -1027,6 +1074,7 @@ def run_replay(args, nat, torch, dev, rank, world):
                 steps=args.replay_steps, mismatches=int(t[1]), input_gen_s=t_gen,
                 share_checks=("randomized batch checks (lcb_tpke_verify_shares_batched_dev, "
                               "lcb_ts_verify_shares_batched_dev)" if batched else "exact per-share checks"),
+                concurrent_chains=bool(conc),
                 config=f"configs[4]: all {n} nodes' views of one era (N={n}, F={f}), views block-partitioned over "
                        f"ranks; per view {checks_per_view} pairing checks, {n} G1 and {n_coins} G2 Lagrange (k={f + 1})")
 
@@ -1724,6 +1772,8 @@ def main():
     ap.add_argument("--replay-n", type=int, default=256, help="epoch-replay network size N (0 = skip)")
     ap.add_argument("--replay-steps", type=int, default=1)
     ap.add_argument("--replay-exact", type=int, default=0, help="epoch replay with the exact per-share checks")
+    ap.add_argument("--replay-concurrent", type=int, default=1,
+                    help="epoch replay: the TPKE and coin chains side by side (own host thread, context, stream)")
     ap.add_argument("--ecdsa-sigs", type=int, default=1 << 20, help="header signatures per rank (0 = skip)")
     ap.add_argument("--ecdsa-validators", type=int, default=256)
     ap.add_argument("--ecdsa-steps", type=int, default=3)
