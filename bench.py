@@ -994,6 +994,7 @@ def run_replay(args, nat, torch, dev, rank, world):
         return rc, (nat.last_error() if rc else "")
 
     def step_concurrent():
+        torch.cuda.current_stream(dev).synchronize()    # inputs uploaded on the default stream are complete
         res = [f.result() for f in [pools[k].submit(run_chain, k) for k in range(2)]]
         for rc, err in res:
             if rc:
