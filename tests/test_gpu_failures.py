@@ -52,15 +52,15 @@ def test_half_built_stage_is_rebuilt(nat):
     ref = mcl.G1.Generator().ToBytes()
 
     def fresh_thread():                   # a new thread: its staging area does not exist yet
+        g = mcl.G1.Generator()            # host code: no staging
+        k = mcl.Fr.FromInt(5)
         nat.inject_failure(1, 1)          # the pinned host buffer of this thread's stage fails once
         try:
-            mcl.G1.Generator()
+            g * k                         # a GPU call: builds the stage, which fails half-way
             raised = None
         except RuntimeError as e:
             raised = str(e)
-        g = mcl.G1.Generator()            # the stage is rebuilt from scratch
-        k = mcl.Fr.FromInt(5)
-        return raised, g.ToBytes(), (g * k).ToBytes(), (g + g + g + g + g).ToBytes()
+        return raised, g.ToBytes(), (g * k).ToBytes(), (g + g + g + g + g).ToBytes()   # rebuilt from scratch
     out = _in_thread(fresh_thread)
     assert "e" not in out, out.get("e")
     raised, g, g5a, g5b = out["v"]
