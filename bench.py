@@ -442,13 +442,16 @@ def run_msm(args, nat, torch, dev, rank, world, cpu, n):
     c = lib.lcb_g1_msm_window(n) if args.msm_no_glv else lib.lcb_g1_msm_glv_window(n)
     glv = c > 0 and not args.msm_no_glv
     c = abs(c)
+    wbits = 0
+    if args.msm_glv_window > 0 and not args.msm_no_glv:     # A/B: the GLV form at an explicit width
+        wbits, c, glv = args.msm_glv_window, args.msm_glv_window, True
 
     def sum_partials(allp, w):
         if lib.lcb_g1_jac_sum_dev(d_out.data_ptr(), None, allp.data_ptr(), w, sh) != 0:
             raise RuntimeError(nat.last_error())
 
     def step():
-        if msm_fn(d_jac.data_ptr(), d_aff.data_ptr(), d_sc.data_ptr(), n, 0, sh) != 0:
+        if msm_fn(d_jac.data_ptr(), d_aff.data_ptr(), d_sc.data_ptr(), n, wbits, sh) != 0:
             raise RuntimeError(nat.last_error())
         # RCCL over xGMI: all-gather of the 144 B Jacobian partials, summed on the GPU (lachain_amd/shard.py)
         shard.msm_combine(dist, d_jac, world, sum_partials)
@@ -1765,6 +1768,7 @@ def main():
                     help="total G1 MSM points per measurement, sharded over ranks (empty = skip)")
     ap.add_argument("--msm-steps", type=int, default=3)
     ap.add_argument("--msm-no-glv", action="store_true", help="plain 255-bit Pippenger instead of the GLV form")
+    ap.add_argument("--msm-glv-window", type=int, default=0, help="A/B: the GLV form at this window width")
     ap.add_argument("--ts-rounds", type=int, default=65536, help="CommonCoin rounds per rank (0 = skip)")
     ap.add_argument("--ts-n", type=int, default=100)
     ap.add_argument("--ts-steps", type=int, default=1)
