@@ -377,6 +377,7 @@ template <class J, class A> static void put_point(J &job, const A &a) {
 // run n_jobs ladders (k_ptmul_g1 / _g2) on the thread's staging; outputs the groups' Jacobian results
 static bool ptmul_run(int g, const void *jobs, size_t job_bytes, u32 n_jobs, void *out, size_t out_bytes) {
     if (!stage_ready()) return false;
+    if (injected(INJ_STAGE_OP)) { set_err("injected failure (single operation)"); return false; }
     memcpy(IOH, jobs, job_bytes * n_jobs);
     const size_t out_w = 1024;                    // results at word 1024 of the 16 KB staging
     hipError_t e;
