@@ -1750,6 +1750,8 @@ def main():
     ap.add_argument("--tpke-streams", type=int, default=1,
                     help="batched verify: concurrent parts (contexts / streams / host threads) per step; measured "
                          "no faster with 2 or 3 parts (147 - 159 vs 145 ms per 1M shares)")
+    ap.add_argument("--hw-queues", type=int, default=int(os.environ.get("LCB_BENCH_HWQ", "0")),
+                    help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's)")
     ap.add_argument("--tpke-pipeline", type=int, default=1,
                     help="batched verify: whole batches in flight (each on its own context / stream / host thread)")
     ap.add_argument("--headline", choices=("batched", "exact"), default="batched",
@@ -1792,6 +1794,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.hw_queues > 0:
+        # hardware queues per process, read when the HIP runtime starts (before torch / the library touch the GPU):
+        # the batched call uses five streams per context, so batches in flight need more than HIP's default four
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, args.hw_queues))
     import torch
     import torch.distributed as dist
     from lachain_amd import native as nat
@@ -1815,6 +1821,8 @@ def main():
         nat.set_coop_miller_max(args.coop_miller_max)
     if os.environ.get("LCB_WAVE_PRIO"):           # A/B of the latency kernels' wave priority
         nat.set_wave_priority(int(os.environ["LCB_WAVE_PRIO"]))
+    if os.environ.get("LCB_MSM_SEGS"):            # A/B of the bucket-reduction lane count
+        nat.set_msm_segments(int(os.environ["LCB_MSM_SEGS"]))
     if os.environ.get("LCB_MSM_CHUNK"):           # A/B of the MSM bucket accumulation (0: one lane per bucket)
         nat.set_msm_chunk(int(os.environ["LCB_MSM_CHUNK"]))
 

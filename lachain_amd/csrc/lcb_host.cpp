@@ -1481,6 +1481,7 @@ int assemble_enqueue(lcb_ctx *c, int g, uint8_t *out, uint8_t *status, const uin
 // window width minimising ceil-windows * (n mixed adds * 11 + 2^(c-1) buckets * 2 Jacobian adds * 16) Fp-mul
 // GLV form: 2n points with 128-bit scalars, windows ceil(128 / c); only widths whose top window is nearly full
 // (a short top window concentrates 2n records in few buckets, one lane each)
+std::atomic<int> g_msm_segs{0};     // lcb_set_msm_segments: bucket-reduction lanes rule (0: >= 65,536 segments)
 std::atomic<int> g_msm_chunk{64};   // records per lane of k_msm_chunk_acc (0: one lane per bucket, k_msm_bucket_acc)
 u32 msm_window(size_t n, bool glv = false) {
     u32 best = 4;
@@ -1517,7 +1518,12 @@ int msm_enqueue(lcb_ctx *cx, void *out_jac, const void *pts, const uint8_t *scal
     int end_bit = 1;
     while ((1ull << end_bit) <= sentinel) end_bit++;
     u32 L = 1;
-    while ((size_t)nb / (L * 2) >= 65536 && L * 2 <= half) L *= 2;
+    const int seg_rule = g_msm_segs.load();
+    if (seg_rule > 0) {                          // the fewest segments (serial lanes) up to seg_rule of them
+        while ((size_t)nb / L > (size_t)seg_rule && L * 2 <= half) L *= 2;
+    } else {                                     // the most segments of at least 65,536
+        while ((size_t)nb / (L * 2) >= 65536 && L * 2 <= half) L *= 2;
+    }
     u32 n_seg = nb / L, per_win = half / L, n_l1 = n_seg / (per_win < 256 ? per_win : 256);
     u32 kwin = nb / half;                        // key windows (nwin, or nwin + 1 in the GLV form)
     if (!cx->msm_ev_ready) {
@@ -1731,6 +1737,11 @@ extern "C" int lcb_set_wave_priority(int on) {
     if (!tuning_allowed("lcb_set_wave_priority")) return -1;
     if (!ready()) return -1;
     if (lcbk_set_wave_prio(on != 0)) { set_err("lcb_set_wave_priority: device configuration failed"); return -1; }
+    return 0;
+}
+extern "C" int lcb_set_msm_segments(int max_segments) {
+    if (!tuning_allowed("lcb_set_msm_segments")) return -1;
+    g_msm_segs.store(max_segments > 0 ? max_segments : 0);
     return 0;
 }
 extern "C" int lcb_set_msm_chunk(int records_per_lane) {

@@ -54,6 +54,7 @@ _SIGS = {
     "lcb_set_line_mode": (ctypes.c_int, [ctypes.c_int]),
     "lcb_set_g2_sign_from_b": (ctypes.c_int, [ctypes.c_int]),
     "lcb_set_msm_chunk": (ctypes.c_int, [ctypes.c_int]),
+    "lcb_set_msm_segments": (ctypes.c_int, [ctypes.c_int]),
     "lcb_set_wave_priority": (ctypes.c_int, [ctypes.c_int]),
     "lcb_last_error": (ctypes.c_char_p, []),
     "lcb_error_count": (ctypes.c_uint64, []),
@@ -758,6 +759,11 @@ def inject_failure(site, count=1):
 def set_wave_priority(on):
     """latency-bound batched-check kernels at raised wave priority (default on)"""
     _tuning(lib().lcb_set_wave_priority(1 if on else 0), "set_wave_priority")
+
+
+def set_msm_segments(max_segments):
+    """MSM bucket-reduction lanes: the fewest segments up to max_segments (0: default rule)"""
+    _tuning(lib().lcb_set_msm_segments(int(max_segments)), "set_msm_segments")
 
 
 def set_msm_chunk(records_per_lane):
