@@ -18,9 +18,11 @@ done
 done
 done
 if [ -n "$MSMB" ]; then
+  for SG in ${MSMSEGS:-0}; do
   for K in $MSMB; do
-    LCB_MSM_SEGS=${MSMSEGS:-0} LCB_ALLOW_TUNING=1 LCB_MSM_CHUNK=$K timeout -k 10 300 python3 -u bench.py --tpke-exact 0 --tpke-batched 0 --ts-rounds 0 --replay-n 0 --ecdsa-sigs 0 --dkg-n 0 --rs-n 0 --mcl-reps 0 --no-cpu-baseline --pattern-steps 0 --shares 22000 --headline exact --tpke-exact 1 --steps 1 --warmup 1 --msm-steps 5 > gpurun_out/${TAG}_msm$K.txt 2> gpurun_out/${TAG}_msm$K.err || { echo "MSM BENCH FAILED"; tail -20 gpurun_out/${TAG}_msm$K.err; exit 1; }
-    python3 -c "import json; d=json.loads([l for l in open('gpurun_out/${TAG}_msm$K.txt') if l.startswith('BENCH_DETAIL')][-1][13:]); [print('msm chunk $K', m['total_points'], round(m['value']/1e6,1), 'M/s', m['ms_per_step'], m['phase_ms'], m['known_answer_ok']) for m in d['msm']]"
+    LCB_MSM_SEGS=$SG LCB_ALLOW_TUNING=1 LCB_MSM_CHUNK=$K timeout -k 10 300 python3 -u bench.py --tpke-exact 0 --tpke-batched 0 --ts-rounds 0 --replay-n 0 --ecdsa-sigs 0 --dkg-n 0 --rs-n 0 --mcl-reps 0 --no-cpu-baseline --pattern-steps 0 --shares 22000 --headline exact --tpke-exact 1 --steps 1 --warmup 1 --msm-steps 5 > gpurun_out/${TAG}_msm$K.txt 2> gpurun_out/${TAG}_msm$K.err || { echo "MSM BENCH FAILED"; tail -20 gpurun_out/${TAG}_msm$K.err; exit 1; }
+    python3 -c "import json; d=json.loads([l for l in open('gpurun_out/${TAG}_msm$K.txt') if l.startswith('BENCH_DETAIL')][-1][13:]); [print('msm segs $SG chunk $K', m['total_points'], round(m['value']/1e6,1), 'M/s', m['ms_per_step'], m['phase_ms'], m['known_answer_ok']) for m in d['msm']]"
+  done
   done
 fi
 if [ -n "$MCL" ]; then
