@@ -1750,10 +1750,12 @@ def main():
     ap.add_argument("--tpke-streams", type=int, default=1,
                     help="batched verify: concurrent parts (contexts / streams / host threads) per step; measured "
                          "no faster with 2 or 3 parts (147 - 159 vs 145 ms per 1M shares)")
-    ap.add_argument("--hw-queues", type=int, default=int(os.environ.get("LCB_BENCH_HWQ", "0")),
-                    help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's)")
-    ap.add_argument("--tpke-pipeline", type=int, default=1,
-                    help="batched verify: whole batches in flight (each on its own context / stream / host thread)")
+    ap.add_argument("--hw-queues", type=int, default=int(os.environ.get("LCB_BENCH_HWQ", "8")),
+                    help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's; 8 measured 12.30 vs 11.95 M "
+                         "shares/s with two batches in flight, profiles/r04/q2)")
+    ap.add_argument("--tpke-pipeline", type=int, default=2,
+                    help="batched verify: whole batches in flight (each on its own context / stream / host thread); "
+                         "2 measured 12.3 vs 10.6 M shares/s for one at a time, 3 no better (profiles/r04/q1, q2)")
     ap.add_argument("--headline", choices=("batched", "exact"), default="batched",
                     help="which TPKE path the line's value / roofline / cpu_baseline describe")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)

@@ -337,7 +337,8 @@ int lcb_set_fork_mode(int mode);
    0 = one lane per bucket (k_msm_bucket_acc).  Results are unchanged. */
 int lcb_set_msm_chunk(int records_per_lane);
 /* tuning hook (LCB_ALLOW_TUNING=1): the MSM bucket reduction uses the fewest serial segments up to max_segments lanes
-   (0 = the default rule: the most segments of at least 65,536).  Results are unchanged. */
+   (0 = by form: the GLV form the fewest segments up to 65,536, the plain form the most of at least 65,536).
+   Results are unchanged. */
 int lcb_set_msm_segments(int max_segments);
 /* tuning hook (LCB_ALLOW_TUNING=1): 1 (default) = the latency-bound kernels of the batched checks (preparation chain,
    every level) raise their waves' issue priority over the bulk randomisation waves sharing their SIMDs; 0 = off */

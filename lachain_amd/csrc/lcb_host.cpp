@@ -1481,7 +1481,7 @@ int assemble_enqueue(lcb_ctx *c, int g, uint8_t *out, uint8_t *status, const uin
 // window width minimising ceil-windows * (n mixed adds * 11 + 2^(c-1) buckets * 2 Jacobian adds * 16) Fp-mul
 // GLV form: 2n points with 128-bit scalars, windows ceil(128 / c); only widths whose top window is nearly full
 // (a short top window concentrates 2n records in few buckets, one lane each)
-std::atomic<int> g_msm_segs{0};     // lcb_set_msm_segments: bucket-reduction lanes rule (0: >= 65,536 segments)
+std::atomic<int> g_msm_segs{0};     // lcb_set_msm_segments: bucket-reduction lanes rule (0: by form, see msm_enqueue)
 std::atomic<int> g_msm_chunk{64};   // records per lane of k_msm_chunk_acc (0: one lane per bucket, k_msm_bucket_acc)
 u32 msm_window(size_t n, bool glv = false) {
     u32 best = 4;
@@ -1518,7 +1518,9 @@ int msm_enqueue(lcb_ctx *cx, void *out_jac, const void *pts, const uint8_t *scal
     int end_bit = 1;
     while ((1ull << end_bit) <= sentinel) end_bit++;
     u32 L = 1;
-    const int seg_rule = g_msm_segs.load();
+    // GLV form (n <= 2^22): the fewest segments up to 65,536 (2^20: 0.87 vs 1.05 ms of reduction); the plain form at
+    // 2^24 keeps the most segments of at least 65,536 (6.3 vs 7.7 ms) — profiles/r04/q2
+    const int seg_rule = g_msm_segs.load() ? g_msm_segs.load() : (glv ? 65536 : 0);
     if (seg_rule > 0) {                          // the fewest segments (serial lanes) up to seg_rule of them
         while ((size_t)nb / L > (size_t)seg_rule && L * 2 <= half) L *= 2;
     } else {                                     // the most segments of at least 65,536
