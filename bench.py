@@ -53,6 +53,13 @@ W_PREPARE = (C["C_DEC1"] + C["C_DEC2"] + C["C_H2G2"] + C["C_AFF2"] + 2 * C["C_LI
              + 2 * C["C_NORM"])                                                        # per ciphertext
 # gfx950 v_mad_u64_u32 is half rate: 64 lane-MACs / clk / CU (profiles/r01_valu_rates.jsonl)
 PEAK_MAC32 = 256 * 64 * 2.4e9            # 3.93e13 MAC/s at the 2.4 GHz max clock
+_T_START = time.perf_counter()
+
+
+def progress(msg):
+    """One stderr line per bench stage on rank 0 (the full run takes minutes; stdout carries only the result)."""
+    if os.environ.get("RANK", "0") == "0":
+        print(f"[bench {time.perf_counter() - _T_START:7.1f} s] {msg}", file=sys.stderr, flush=True)
 
 
 def oracle_timing_lib():
@@ -412,6 +419,7 @@ def run_msm_sizes(args, nat, torch, dev, rank, world, cpu):
     MSM sharded over the ranks (n / world per rank) with the RCCL all-gather of the 144-byte partials."""
     out = []
     for k, total in enumerate(int(x) for x in args.msm_sizes.split(",") if x):
+        progress(f"MSM {total} points")
         r = run_msm(args, nat, torch, dev, rank, world, cpu and k == 0, max(1, total // world))
         if r is not None:
             r["total_points"] = total
@@ -1828,6 +1836,7 @@ def main():
     if os.environ.get("LCB_MSM_CHUNK"):           # A/B of the MSM bucket accumulation (0: one lane per bucket)
         nat.set_msm_chunk(int(os.environ["LCB_MSM_CHUNK"]))
 
+    progress(f"inputs: {args.shares} TPKE shares")
     t_gen = time.perf_counter()
     inp = make_inputs(nat, rank, args.shares, args.n, args.f, args.vlen)
     t_gen = time.perf_counter() - t_gen
@@ -1864,6 +1873,7 @@ def main():
 
     exact = None
     if args.tpke_exact:
+        progress("TPKE exact verify")
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize(dev)
@@ -1910,9 +1920,11 @@ def main():
                           "k_final_exp_check": n * C["C_FE"] * MAC_PER_FPMUL / (fexp_ms * 1e-3) / PEAK_MAC32}})
     batched = None
     if args.tpke_batched:
+        progress("TPKE batched verify")
         batched = run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, (d_ct, d_dec, d_ui), n, n_cts, n_dec, sh)
         if args.tpke_pipeline > 1 and args.tpke_streams <= 1:
             # batches in flight: the headline is the pipelined rate; the one-batch-at-a-time rate stays in the record
+            progress(f"TPKE batched verify, {args.tpke_pipeline} batches in flight")
             piped = run_tpke_pipelined(args, nat, torch, dev, world, inp, (d_ct, d_dec, d_ui), n, n_cts, n_dec,
                                        args.tpke_pipeline)
             piped["single_batch"] = {k: batched[k] for k in ("value", "ms_per_step", "decision_mismatches", "levels")
@@ -1922,22 +1934,29 @@ def main():
             batched = piped
     byz = None
     if args.pattern_steps > 0:
+        progress("Byzantine patterns")
         byz = run_tpke_patterns(args, nat, torch, dev, world, inp, n, n_cts, n_dec)
     head = batched if (args.headline == "batched" and batched) else exact
     if head is None:
         raise SystemExit("nothing to report: --tpke-exact 0 and --tpke-batched 0")
     msm = ts = replay = ecdsa = dkg = rs = mcl_lat = None
     if args.mcl_reps > 0 and world == 1:
+        progress("mcl latency")
         mcl_lat = run_mcl_latency(args, nat, rank)
     if args.dkg_n > 0 and world == 1:
+        progress("DKG")
         dkg = run_dkg(args, nat, rank)
     if args.rs_n > 0 and world == 1:
+        progress("RBC erasure coding")
         rs = run_rs(args, nat, rank)
     if args.ecdsa_sigs > 0:
+        progress("ECDSA headers")
         ecdsa = run_ecdsa(args, nat, torch, dev, rank, world, cpu=(world == 1 and not args.no_cpu_baseline))
     if args.replay_n > 0:
+        progress("epoch replay")
         replay = run_replay(args, nat, torch, dev, rank, world)
     if args.ts_rounds > 0:
+        progress("threshold signatures")
         ts = run_ts(args, nat, torch, dev, rank, world)
     if args.msm_sizes:
         msm = run_msm_sizes(args, nat, torch, dev, rank, world, cpu=(world == 1 and not args.no_cpu_baseline))
@@ -1975,6 +1994,7 @@ def main():
             batched["roofline"]["traffic_source"] = bnote
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
+            progress("TPKE CPU baseline")
             cpu = cpu_baseline(inp, args.cpu_seconds, batched=batched is not None)
         if head is batched:
             roofline = dict(batched.pop("roofline"))
