@@ -126,19 +126,42 @@ bool ready() {
 
 // single-element operations: every calling thread owns its staging (device and pinned host buffers, a stream), so the
 // protocol threads (AbstractProtocol.cs:46-47) never queue behind each other's round trips
-struct OpStage {
+// A thread's staging and implicit contexts are NOT released when it exits: HIP calls from thread-local destructors
+// race the runtime's (and a profiler's) own per-thread teardown (an abort under rocprofv3 in round 4).  They are
+// retired to process-wide free lists instead and handed to the next thread that needs one, so their number stays
+// bounded by the peak number of calling threads.  The lists are leaked on purpose (no static-destruction order issue).
+struct StageRes {
     u32 *dev = nullptr, *host = nullptr;
     hipStream_t s = nullptr;
+};
+std::mutex &retired_mu() {
+    static std::mutex *m = new std::mutex;
+    return *m;
+}
+std::vector<StageRes> &retired_stages() {
+    static std::vector<StageRes> *v = new std::vector<StageRes>;
+    return *v;
+}
+struct OpStage : StageRes {
     ~OpStage() {
-        if (s) (void)hipStreamDestroy(s);
-        if (dev) (void)hipFree(dev);
-        if (host) (void)hipHostFree(host);
+        if (!(s && dev && host)) return;             // a half-built stage never survives stage_ready
+        std::lock_guard<std::mutex> lk(retired_mu());
+        retired_stages().push_back(*this);
     }
 };
 thread_local OpStage t_stage;
 bool stage_ready() {
     if (!ready()) return false;
     if (t_stage.s && t_stage.dev && t_stage.host) return true;
+    {
+        std::lock_guard<std::mutex> lk(retired_mu());
+        auto &v = retired_stages();
+        if (!v.empty() && !t_stage.s && !t_stage.dev && !t_stage.host) {
+            static_cast<StageRes &>(t_stage) = v.back();
+            v.pop_back();
+            return true;
+        }
+    }
     // all three or none: a partial failure releases what was created, so the next call retries from scratch instead
     // of passing a half-built stage (a set stream with a null host buffer would be written through)
     hipError_t e = t_stage.s ? hipSuccess : hipStreamCreateWithFlags(&t_stage.s, hipStreamNonBlocking);
@@ -716,23 +739,50 @@ lcb_ctx *ctx_new() {
 }
 // each thread owns two implicit contexts: one for the *_dev entry points without a context argument, one for the
 // synchronous host-pointer entry points (so a host-pointer call never touches a workspace a *_dev caller prepared)
+std::vector<lcb_ctx *> &retired_ctxs() {
+    static std::vector<lcb_ctx *> *v = new std::vector<lcb_ctx *>;
+    return *v;
+}
 struct ThreadCtx {
     lcb_ctx *c = nullptr;
-    ~ThreadCtx() { ctx_free(c); }
+    ~ThreadCtx() {                                   // retired, not freed (see OpStage)
+        if (!c) return;
+        std::lock_guard<std::mutex> lk(retired_mu());
+        retired_ctxs().push_back(c);
+    }
 };
 thread_local ThreadCtx t_dev_ctx, t_sync_ctx;
+// an implicit context for this thread: a retired one of the current device (its prepared state dropped, its
+// buffers, caches keyed by content and event chain kept), else a new one
+lcb_ctx *implicit_ctx_new() {
+    {
+        std::lock_guard<std::mutex> lk(retired_mu());
+        auto &v = retired_ctxs();
+        for (size_t k = v.size(); k-- > 0;) {
+            lcb_ctx *c = v[k];
+            if (c->device != g_device) continue;
+            v.erase(v.begin() + (long)k);
+            std::lock_guard<std::recursive_mutex> cl(c->mu);
+            c->t_ready = c->s_ready = false;
+            c->t_gen++;
+            c->s_gen++;
+            return c;
+        }
+    }
+    return ctx_new();
+}
 lcb_ctx *resolve(lcb_ctx *c) {
     if (!ready()) return nullptr;
     if (c) {
         if (c->device != g_device) { set_err("context belongs to another device"); return nullptr; }
         return c;
     }
-    if (!t_dev_ctx.c) t_dev_ctx.c = ctx_new();
+    if (!t_dev_ctx.c) t_dev_ctx.c = implicit_ctx_new();
     return t_dev_ctx.c;
 }
 lcb_ctx *sync_ctx() {
     if (!ready()) return nullptr;
-    if (!t_sync_ctx.c) t_sync_ctx.c = ctx_new();
+    if (!t_sync_ctx.c) t_sync_ctx.c = implicit_ctx_new();
     return t_sync_ctx.c;
 }
 

@@ -156,6 +156,30 @@ def test_single_operations_from_many_threads(mcl):
     assert got == want
 
 
+def test_thread_churn_reuses_retired_staging(mcl):
+    """Threads that exit hand their staging and implicit contexts to the next threads (no HIP call at thread exit):
+    four generations of six short-lived threads, each doing a scalar multiplication, all exact"""
+    Fr, G1 = mcl.Fr, mcl.G1
+    errs, got = [], {}
+
+    def work(gen, i):
+        try:
+            k = 1000 * gen + i + 2
+            got[(gen, i)] = (G1.Generator() * Fr.FromInt(k)).ToBytes()
+        except Exception as e:          # noqa: BLE001 — reported below
+            errs.append(e)
+
+    for gen in range(4):
+        ts = [threading.Thread(target=work, args=(gen, i)) for i in range(6)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    assert not errs, errs
+    for (gen, i), b in got.items():
+        assert b == o.g1_mul(o.g1_gen(), o.fr(1000 * gen + i + 2)), (gen, i)
+
+
 def test_pairing_line_cache(mcl):
     """mclBn_pairing keeps the line sets of the last 32 distinct G2 arguments per thread: hits, misses and evictions
     (40 distinct Q, revisited out of order) all give the oracle's GT value"""
