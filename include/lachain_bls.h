@@ -173,6 +173,11 @@ uint64_t lcb_error_count(void);
    buffer, 2: the prepared-ciphertext cache's uploads after its slots were assigned, 3: mclBn_pairing, 4: a
    single-operation round trip); 0 disables.  Returns -1 unless the environment has LCB_ALLOW_TEST_HOOKS=1. */
 int lcb_test_inject_failure(int site, int count);
+/* test hook: the line sets of n G2 wire points (96-byte encodings; an undecodable one is the point at infinity), on the
+   five-lane kernel (coop = 1) or the one-lane kernel, force[k] = 1 forcing set k's flag to the on-the-fly path.
+   out: n sets of 26,368 bytes (pairing.hpp layout); w_g2[k] = 1 iff point 2k + 1 lies in G2.  Returns -1 unless the
+   environment has LCB_ALLOW_TEST_HOOKS=1. */
+int lcb_test_linesets(int coop, const uint8_t *g2_wire, const uint8_t *force, size_t n, uint32_t *out, uint8_t *w_g2);
 
 /* TPKE.PublicKey.VerifyShare for a batch (TPKE/PublicKey.cs:88-92, called per share from
    HoneyBadger.cs:211-212).  Ciphertext c = (U_c, V_c, W_c) with V_c = v_data[v_off[c] .. v_off[c+1]);
@@ -258,6 +263,9 @@ int lcb_ts_assemble_ordered_dev(uint8_t *sig_out, uint8_t *status, const uint8_t
 
 /* device time (ms) of k_tpke_miller and k_final_exp_check in the last split TPKE verify (waits for it) */
 int lcb_tpke_verify_phase_ms(float ms[2]);
+/* Line sets of up to max_sets points per preparation on the five-lane kernel (latency), larger preparations one lane
+   per set (throughput); -1 restores the default (8,192).  Tuning hook: -1 unless LCB_ALLOW_TUNING=1. */
+int lcb_set_lines_coop_max(int max_sets);
 
 /* Randomized batch form of lcb_tpke_verify_prepared_dev (same arguments, same workspace, same validity rules;
    replaces the per-share loop over TPKE/PublicKey.cs:88-92 driven from HoneyBadger.cs:211-212).  Shares are grouped

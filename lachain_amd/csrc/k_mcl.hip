@@ -7,35 +7,8 @@
 LCB_ASM_LIBRARY(k_mcl)
 LCB_TU_CONFIG(k_mcl)
 
-// mclBn_pairing(P, Q) (GT.Pairing in the reference, e.g. TPKE/PublicKey.cs:91) as a one-group cooperative check:
-// P and the point at infinity as the group's two G1 points, Q's line set and the set of infinity (every line 1).
-// The line sets live in the calling context's cache of Q line sets (slot k = sets 2k, 2k + 1): with fill != 0 the
-// kernel stores Q and the infinity point in slot k for k_lineset_fill, otherwise the slot already holds Q's lines.
-// in: P Jacobian (36 words) then Q Jacobian (72 words)
-extern "C" __global__ void LCB_BOUNDS k_pairing_prep(const u32 *in, g1a_st *gpts, u32 *lines, uint4 *desc, u32 slot,
-                                                    u32 fill) {
-    if (blockIdx.x || threadIdx.x) return;
-    g1 p = *(const g1 *)in;
-    g1a pa;
-    jac_to_aff(pa, p);
-    g1a_st s;
-    s.x = pa.x; s.y = pa.y; s.inf = pa.inf; s.ok = 1; s.pad[0] = s.pad[1] = 0;
-    gpts[0] = s;
-    s.inf = 1; s.x = fp_zero(); s.y = fp_zero();
-    gpts[1] = s;
-    desc[0] = make_uint4(0, 1, slot, 0);
-    if (!fill) return;
-    g2 q = *(const g2 *)(in + 36);
-    g2a qa, inf;
-    jac_to_aff(qa, q);
-    inf.inf = true;
-    inf.x = fp2_zero();
-    inf.y = fp2_zero();
-    u32 *ls = lines + (size_t)(2 * slot) * LCB_LINESET_WORDS;
-    lineset_put_point(ls, qa);
-    lineset_put_point(ls + LCB_LINESET_WORDS, inf);
-    ls[LCB_LS_FLAG + 2] = ls[LCB_LINESET_WORDS + LCB_LS_FLAG + 2] = 0;
-}
+// the line-set layout the host stages for mclBn_pairing (launch.h LCB_LS_POINT_WORD, LCB_LINESET_BYTES)
+static_assert(LCB_LS_POINT == 6528 && LCB_LS_FLAG == 6528 + 48 && LCB_LINESET_WORDS * 4 == 26368, "line-set layout");
 
 // terms[i] = [k_i] P_i for n G1 points (Jacobian) and canonical 256-bit scalars: the 4-bit windowed ladder over the
 // point's affine table, exact for every on-curve input (k_lagrange.hip)
@@ -106,10 +79,6 @@ extern "C" __global__ void LCB_BOUNDS k_mcl_to_bytes(int g, const u32 *in, u32 n
 }
 
 // ---------------------------------------------------------------- host launch wrappers
-extern "C" void lcbk_pairing_prep(hipStream_t s, const u32 *in, void *gpts, u32 *lines, void *desc, u32 slot, u32 fill) {
-    dim3 grid(1);
-    LCB_LAUNCH(k_pairing_prep, in, (g1a_st *)gpts, lines, (uint4 *)desc, slot, fill);
-}
 extern "C" void lcbk_mcl_g1_terms(hipStream_t s, const void *pts, const void *scal, u32 n, void *terms) {
     dim3 grid((n + LCB_BLOCK - 1) / LCB_BLOCK);
     LCB_LAUNCH(k_mcl_g1_terms, (const g1 *)pts, (const fr *)scal, n, (g1 *)terms);

@@ -82,6 +82,23 @@ extern "C" __global__ void __launch_bounds__(64, 1) k_ptmul_g2(const PtJob<fp2> 
 static_assert(sizeof(PtJob<fp>) == 96 + 16 + 36, "PtJob<fp> layout (launch.h LCB_PTJOB_G1_BYTES)");
 static_assert(sizeof(PtJob<fp2>) == 192 + 16 + 36, "PtJob<fp2> layout (launch.h LCB_PTJOB_G2_BYTES)");
 
+// mclBnG2_hashAndMapTo (G2.SetHashOf: TPKE/Utils.cs:21-27, ThresholdSignature/PrivateKeyShare.cs:23-25) on one lane
+// in a kernel of its own: k_op's single-operation switch carries every operation's state (3,038 spilled registers).
+// io as k_op's OP_G2_HASH: io[250] = message length, the message at io + 256; out: the Jacobian point at io[0..72),
+// io[248] = 1 on success (0: no point, infinity written)
+extern "C" __global__ void __launch_bounds__(64, 1) k_mcl_g2_hash(u32 *io, int orig_cof) {
+    if (threadIdx.x) return;
+    uint8_t d[64];
+    sha512_2(d, (const uint8_t *)(io + 256), io[250], (const uint8_t *)(io + 256), 0);
+    g2 H;
+    const bool ok = g2_hash_digest(H, d, orig_cof != 0);
+    if (!ok) jac_set_inf(H);
+    *(g2 *)io = H;
+    io[248] = ok ? 1u : 0u;
+}
+extern "C" void lcbk_mcl_g2_hash(hipStream_t s, u32 *io, int orig_cof) {
+    hipLaunchKernelGGL(k_mcl_g2_hash, dim3(1), dim3(64), 0, s, io, orig_cof);
+}
 extern "C" void lcbk_ptmul_g1(hipStream_t s, const void *jobs, u32 n_groups, void *out) {
     hipLaunchKernelGGL(k_ptmul_g1, dim3(1), dim3(64), 0, s, (const PtJob<fp> *)jobs, n_groups, (g1 *)out);
 }

@@ -11,9 +11,10 @@ LCB_TU_CONFIG(k_rlc_rand)
 
 extern "C" __global__ void LCB_BOUNDS k_rlc_key_tables(const g1a_st *keys, u32 n_keys, u32 *jtab, u32 *pre, u32 *tab,
                                                       uint8_t *ktab_ok) {
+    LCB_LATENCY_PRIO();          // a short serial chain ahead of the randomisation, beside the preparation's waves
     u32 t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= LCB_KTAB_LANES * n_keys) return;
-    u32 k = t / LCB_KTAB_LANES, w = (t / 8) & 3, ch = t & 7;
+    u32 k = t / LCB_KTAB_LANES, w = (t / LCB_KTAB_CHUNKS) & 3, ch = t % LCB_KTAB_CHUNKS;
     u32 d0 = ch * LCB_KTAB_CHUNK + 1, d1 = min(255u, d0 + LCB_KTAB_CHUNK - 1);   // entries d0 .. d1
     g1a K;
     g1a_st ks = keys[k];

@@ -33,6 +33,7 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_ct_prepare(const uint8_t *cts_u, co
                                                        const uint8_t *v_data, const u32 *v_off, u32 n_cts,
                                                        u32 *lines, uint8_t *ct_ok, int flags, const u32 *slot) {
     // flags: bit 0 = mcl's original G2 cofactor clearing in hash-to-G2, bit 1 = mark the line sets un-normalised
+    LCB_LATENCY_PRIO();
     u32 c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= n_cts) return;
     const u32 o = slot ? slot[c] : c;

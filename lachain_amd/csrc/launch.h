@@ -13,6 +13,8 @@ extern "C" void lcbk_tpke_ct_prepare_h(hipStream_t s, const uint8_t *cts_u, cons
 extern "C" void lcbk_tpke_ct_prepare_w(hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, u32 c0, u32 c1, u32 *lines, uint8_t *ct_ok, uint8_t *w_g2, int flags);
 extern "C" void lcbk_ct_ok_merge(hipStream_t s, uint8_t *ct_ok, const uint8_t *h_ok, u32 c0, u32 c1);
 extern "C" void lcbk_lineset_fill(dim3 grid, hipStream_t s, u32 *lines, u32 n_sets, const u32 *sets, uint8_t *w_g2);
+extern "C" void lcbk_mcl_g2_hash(hipStream_t s, u32 *io, int orig_cof);
+extern "C" void lcbk_lineset_coop(hipStream_t s, u32 *lines, u32 n_sets, const u32 *sets, uint8_t *w_g2);
 extern "C" void lcbk_tpke_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, u32 *f_soa, uint8_t *accept);
 extern "C" int lcbk_fe_slots();
 extern "C" void lcbk_final_exp_check(dim3 grid, hipStream_t s, u32 *park, u32 n, uint8_t *accept);
@@ -91,7 +93,6 @@ extern "C" void lcbk_rlc_census_stats(hipStream_t s, const u32 *key_idx, u32 m, 
 extern "C" void lcbk_rlc_suspect_split(hipStream_t s, const void *desc, u32 n_groups, const u32 *key_idx, u32 n_keys, const u32 *susp, const uint8_t *accept, void *out, u32 *count);
 extern "C" size_t lcbk_ts_grp_bytes();
 extern "C" void lcbk_coop_tpke_miller(hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups, u32 *f_soa, uint8_t *gacc, uint8_t *fb, u32 npairs);
-extern "C" void lcbk_pairing_prep(hipStream_t s, const u32 *in, void *gpts, u32 *lines, void *desc, u32 slot, u32 fill);
 extern "C" void lcbk_mcl_g1_terms(hipStream_t s, const void *pts, const void *scal, u32 n, void *terms);
 extern "C" void lcbk_mcl_horner(hipStream_t s, int g, const u32 *coef, u32 n, const void *x_raw, u32 *out);
 extern "C" void lcbk_mcl_g1_sum(hipStream_t s, const void *in, u32 n, void *out);
@@ -109,6 +110,7 @@ extern "C" void lcbk_op(dim3 grid, hipStream_t s, int op, u32 *io, int orig_cof)
 #define LCB_G1_JAC_BYTES 144
 #define LCB_G2_JAC_BYTES 288
 #define LCB_LINESET_BYTES 26368   /* pairing.hpp LCB_LINESET_WORDS * 4 */
+#define LCB_LS_POINT_WORD 6528    /* pairing.hpp LCB_LS_POINT: the set's affine point (48 words), then LCB_LS_FLAG */
 extern "C" int lcbk_cfg_k_batch(u32 sign_b);
 extern "C" int lcbk_cfg_k_coop(u32 sign_b);
 extern "C" int lcbk_cfg_k_dkg(u32 sign_b);

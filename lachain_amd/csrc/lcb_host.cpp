@@ -196,6 +196,18 @@ bool run_op(int op, size_t in_words, size_t out_words) {
     return true;
 }
 
+// mclBnG2_hashAndMapTo's round trip: as run_op, on the dedicated one-lane hash kernel (k_ptmul.hip)
+bool run_hash(size_t in_words, size_t out_words) {
+    hipError_t e;
+    if (injected(INJ_STAGE_OP)) { set_err("injected failure (single operation)"); return false; }
+    if ((e = hipMemcpyAsync(t_stage.dev, t_stage.host, in_words * 4, hipMemcpyHostToDevice, t_stage.s)) != hipSuccess) { set_err("H2D", e); return false; }
+    lcbk_mcl_g2_hash(t_stage.s, t_stage.dev, g_orig_cofactor);
+    if ((e = hipGetLastError()) != hipSuccess) { set_err("k_mcl_g2_hash launch", e); return false; }
+    if ((e = hipMemcpyAsync(t_stage.host, t_stage.dev, out_words * 4, hipMemcpyDeviceToHost, t_stage.s)) != hipSuccess) { set_err("D2H", e); return false; }
+    if ((e = hipStreamSynchronize(t_stage.s)) != hipSuccess) { set_err("k_mcl_g2_hash", e); return false; }
+    return true;
+}
+
 #define LOCKED_OR(ret)                        \
     if (!stage_ready()) return ret;
 
@@ -481,7 +493,7 @@ extern "C" int mclBnG2_hashAndMapTo(mclBnG2 *x, const void *buf, mclSize n) {
     LOCKED_OR(-1)
     IOH[250] = (u32)n;
     memcpy(IOH + 256, buf, n);
-    if (!run_op(OP_G2_HASH, 256 + (n + 3) / 4, 249) || !IOH[248]) return -1;
+    if (!run_hash(256 + (n + 3) / 4, 249) || !IOH[248]) return -1;
     memcpy(x, IOH, 288);
     return 0;
 }
@@ -685,6 +697,17 @@ extern "C" int mclBn_FrEvaluatePolynomial(mclBnFr *out, const mclBnFr *c, mclSiz
     return 0;
 }
 
+// line sets of n points a prepare kernel (or the host) stored in their sets: the five-lane kernel (k_lines.hip, ~1.5 ms
+// of latency) for the small preparations the single calls and the aggregation queue make, one lane per set (~4 ms of
+// latency, but about half the work per set) for large batches
+#define LCB_LINES_COOP_MAX 8192
+std::atomic<int> g_lines_coop_max{LCB_LINES_COOP_MAX};
+void lines_fill(hipStream_t s, u32 *lines, size_t n, const u32 *sets, uint8_t *w_g2) {
+    if (!n) return;
+    if (n <= (size_t)g_lines_coop_max.load()) lcbk_lineset_coop(s, lines, (u32)n, sets, w_g2);
+    else lcbk_lineset_fill(dim3(nblk(n)), s, lines, (u32)n, sets, w_g2);
+}
+
 // ================================================================== execution contexts
 namespace {
 
@@ -827,7 +850,7 @@ int tpke_prepare(lcb_ctx *c, const uint8_t *d_y, size_t n_keys, const uint8_t *d
     if (n_cts) {
         lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), s, d_u, d_w, d_v, d_voff, (u32)n_cts, lines, ctok,
                              g_orig_cofactor | (g_line_mode << 1), nullptr);
-        lcbk_lineset_fill(dim3(nblk(2 * n_cts)), s, lines, (u32)(2 * n_cts), nullptr, ctg2);
+        lines_fill(s, lines, 2 * n_cts, nullptr, ctg2);
     }
     if (!launched("tpke prepare launch")) return -1;
     c->t_n_cts = n_cts;
@@ -974,14 +997,14 @@ bool rlc_ws(lcb_ctx *c, RlcWs &w, size_t n, size_t rec_a, size_t rec_b, size_t n
     return true;
 }
 // fixed-base tables of the batch's keys (k_rlc_key_tables), when the batch is large enough to repay them
-// (4 x 255 points per key, 32 lanes per key, ~40 additions of latency); nullptr: the points kernel multiplies the keys directly
+// (4 x 255 points per key, 64 lanes per key, ~24 additions of latency); nullptr: the points kernel multiplies the keys directly
 u32 *rlc_key_tables(lcb_ctx *c, const void *keys, size_t n_keys, hipStream_t s, uint8_t **ktab_ok) {
     *ktab_ok = nullptr;
     if (!n_keys || n_keys > 4096) return nullptr;
     u32 *ws = (u32 *)c->rlc[12].get(lcbk_key_table_bytes((u32)n_keys));
     if (!ws) return nullptr;
     u32 *tab = nullptr;
-    lcbk_rlc_key_tables(dim3(nblk(32 * n_keys)), s, keys, (u32)n_keys, ws, &tab, ktab_ok);
+    lcbk_rlc_key_tables(dim3(1), s, keys, (u32)n_keys, ws, &tab, ktab_ok);
     return tab;
 }
 // phase 1 (needs the decompressed keys only): per-share exponent multiples of shares [m, n) + level-1 groups (count
@@ -1324,18 +1347,17 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
         // split preparation: hash + H's line set per lane, U / W decompression + W's line set (and its G2 flag) per
         // lane, on separate high-priority streams; each lane keeps its SIMD from the hash to the last line, so no
         // second dispatch waits behind the randomisation's waves.  With c_early: ciphertexts [0, c_early) first
-        // (point lanes, hash lanes, validity, then the census, all on the preparation stream), the rest [c_early,
-        // n_cts) beside them on the second and third streams.
+        // (one decode + hash lane each, then their line sets on the five-lane kernel, then the census, all on the
+        // preparation stream), the rest [c_early, n_cts) beside them on the second and third streams.
         uint8_t *hok = (uint8_t *)c->rlc[18].get(n_cts);
         if (!hok) { set_err("device allocation failed"); return -1; }
         const int fl = g_orig_cofactor | (g_line_mode << 1);
         hipStreamWaitEvent(c->hi2, c->fork_ev[0], 0);
         hipStreamWaitEvent(c->hi3, c->fork_ev[0], 0);
         const u32 nc = (u32)n_cts, ce = c_early;
-        if (ce) {
-            lcbk_tpke_ct_prepare_w(sp, d_u, d_w, 0u, ce, lines, ctok, ctg2, fl);
-            lcbk_tpke_ct_prepare_h(sp, d_u, d_v, d_voff, 0u, ce, lines, hok, fl);
-            lcbk_ct_ok_merge(sp, ctok, hok, 0u, ce);
+        if (ce) {                    // the census's ciphertexts: decode + hash per lane, then the five-lane line sets
+            lcbk_tpke_ct_prepare(dim3(nblk(ce)), sp, d_u, d_w, d_v, d_voff, ce, lines, ctok, fl, nullptr);
+            lines_fill(sp, lines, 2 * (size_t)ce, nullptr, ctg2);
         }
         lcbk_tpke_ct_prepare_h(c->hi2, d_u, d_v, d_voff, ce, nc, lines, hok, fl);
         lcbk_tpke_ct_prepare_w(c->hi3, d_u, d_w, ce, nc, lines, ctok, ctg2, fl);
@@ -1351,7 +1373,7 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
                              g_orig_cofactor | (g_line_mode << 1), nullptr);
         if (hp) hipEventRecord(c->prep_ev[2], sp);
         if (prep_first && n && rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, sr)) return -1;
-        lcbk_lineset_fill(dim3(nblk(2 * n_cts)), sp, lines, (u32)(2 * n_cts), nullptr, ctg2);
+        lines_fill(sp, lines, 2 * n_cts, nullptr, ctg2);
     }
     if (!launched("tpke prepare launch")) return -1;
     c->t_n_cts = n_cts;
@@ -1796,6 +1818,11 @@ extern "C" int lcb_set_msm_segments(int max_segments) {
     g_msm_segs.store(max_segments > 0 ? max_segments : 0);
     return 0;
 }
+extern "C" int lcb_set_lines_coop_max(int max_sets) {
+    if (!tuning_allowed("lcb_set_lines_coop_max")) return -1;
+    g_lines_coop_max.store(max_sets < 0 ? LCB_LINES_COOP_MAX : max_sets);
+    return 0;
+}
 extern "C" int lcb_set_msm_chunk(int records_per_lane) {
     if (!tuning_allowed("lcb_set_msm_chunk")) return -1;
     if (records_per_lane < 0 || records_per_lane > 65536) { set_err("lcb_set_msm_chunk: 0..65536"); return -1; }
@@ -1810,6 +1837,40 @@ extern "C" int lcb_test_inject_failure(int site, int count) {
     return 0;
 }
 extern "C" uint64_t lcb_error_count(void) { return g_err_count; }
+// test hook: the line sets of n G2 wire points (an undecodable encoding -> the point at infinity) on the five-lane
+// (coop = 1) or the one-lane kernel, force[k] = the set's force-general flag; out: n sets of LCB_LINESET_BYTES,
+// w_g2[k] = the G2 flag of set 2k + 1 (k_lineset_fill's contract)
+extern "C" int lcb_test_linesets(int coop, const uint8_t *g2_wire, const uint8_t *force, size_t n, uint32_t *out,
+                                 uint8_t *w_g2) {
+    if (!env_on("LCB_ALLOW_TEST_HOOKS")) { set_err("lcb_test_linesets: needs LCB_ALLOW_TEST_HOOKS=1"); return -1; }
+    if (!n || n > 4096) { set_err("lcb_test_linesets: 1..4096 points"); return -1; }
+    SYNC_CTX_OR(c, -1)
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    const size_t W = LCB_LINESET_BYTES / 4;
+    u32 *lines = (u32 *)c->in[0].get(n * LCB_LINESET_BYTES);
+    uint8_t *dg = (uint8_t *)c->in[1].get(n / 2 + 1);
+    if (!lines || !dg) { set_err("device allocation failed"); return -1; }
+    std::vector<u32> host(n * W, 0u);
+    for (size_t k = 0; k < n; k++) {
+        fph::g2a a;
+        const bool ok = fph::g2_decompress(a, g2_wire + 96 * k, g_g2_sign_b.load() != 0);
+        u32 *pt = &host[k * W + LCB_LS_POINT_WORD];
+        if (ok && !a.inf) {
+            memcpy(pt, &a.x, 96);
+            memcpy(pt + 24, &a.y, 96);
+        }
+        pt[49] = (ok && !a.inf) ? 0u : 1u;
+        pt[50] = force[k] ? 1u : 0u;
+    }
+    if (hipMemcpyAsync(lines, host.data(), n * LCB_LINESET_BYTES, hipMemcpyHostToDevice, s) != hipSuccess ||
+        hipMemsetAsync(dg, 0, n / 2 + 1, s) != hipSuccess) { set_err("lcb_test_linesets: upload"); return -1; }
+    if (coop) lcbk_lineset_coop(s, lines, (u32)n, nullptr, dg);
+    else lcbk_lineset_fill(dim3(nblk(n)), s, lines, (u32)n, nullptr, dg);
+    hipMemcpyAsync(out, lines, n * LCB_LINESET_BYTES, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(w_g2, dg, n / 2, hipMemcpyDeviceToHost, s);
+    return sync_check(c, "lcb_test_linesets") ? 0 : -1;
+}
 // one cooperative Fp12 operation (k_coop_debug) on n values a (and b) vs the one-lane field.hpp routine: AoS in / out
 extern "C" int lcb_debug_coop_op(int op, const uint32_t *a, const uint32_t *b, size_t n, uint32_t *out, uint32_t *ref) {
     SYNC_CTX_OR(c, -1)
@@ -2019,7 +2080,7 @@ extern "C" int lcb_tpke_verify_shares_cached(uint8_t *accept, size_t n, const ui
             return cache_fail();
         }
         lcbk_tpke_ct_prepare(dim3(nblk(m)), s, du, dw, dv, dvo, (u32)m, lines, ctok, flags, dsl);
-        lcbk_lineset_fill(dim3(nblk(2 * m)), s, lines, (u32)(2 * m), dse, nullptr);
+        lines_fill(s, lines, 2 * m, dse, nullptr);
     }
     std::vector<u32> cslot(n);
     for (size_t i = 0; i < n; i++) cslot[i] = slot_of[ct_idx[i]];
@@ -2588,13 +2649,18 @@ extern "C" void mclBn_pairing(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) {
     Enq q(c, c->stream);
     hipStream_t s = c->stream;
     const size_t slots = lcbk_fe_slots() > 6 ? (size_t)lcbk_fe_slots() : 6;
-    u32 *in = (u32 *)c->mcl[0].get(108 * 4);
-    void *gpts = c->mcl[1].get(2 * LCB_G1A_ST_BYTES);
+    // the group record (P and infinity, then the check's descriptor), staged in one copy
+    struct PairIn {
+        uint32_t g[2][LCB_G1A_ST_BYTES / 4];
+        uint32_t desc[4];
+    };
+    static_assert(sizeof(PairIn) == 2 * LCB_G1A_ST_BYTES + 16, "PairIn layout");
+    uint8_t *gin = (uint8_t *)c->mcl[1].get(sizeof(PairIn));
     u32 *lines = (u32 *)c->mcl[2].get((size_t)2 * LCB_PAIR_CACHE * LCB_LINESET_BYTES);
-    void *desc = c->mcl[3].get(16);
     u32 *park = (u32 *)c->mcl[4].get(576 * slots);
     uint8_t *fl = (uint8_t *)c->mcl[5].get(64);
-    if (!in || !gpts || !lines || !desc || !park || !fl) { set_err("device allocation failed"); return; }
+    if (!gin || !lines || !park || !fl) { set_err("device allocation failed"); return; }
+    void *gpts = gin, *desc = gin + 2 * LCB_G1A_ST_BYTES;
     if (c->pc_used.empty()) {
         c->pc_keys.assign((size_t)72 * LCB_PAIR_CACHE, 0);
         c->pc_used.assign(LCB_PAIR_CACHE, 0);
@@ -2607,10 +2673,42 @@ extern "C" void mclBn_pairing(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) {
     }
     c->pc_used[slot] = ++c->pc_tick;
     if (!hit) memcpy(&c->pc_keys[72 * (size_t)slot], y, 288);
-    hipMemcpyAsync(in, x, 144, hipMemcpyHostToDevice, s);
-    if (!hit) hipMemcpyAsync(in + 36, y, 288, hipMemcpyHostToDevice, s);
-    lcbk_pairing_prep(s, in, gpts, lines, desc, slot, hit ? 0 : 1);
-    if (!hit) lcbk_lineset_fill(dim3(1), s, lines + (size_t)2 * slot * (LCB_LINESET_BYTES / 4), 2, nullptr, nullptr);
+    // P and Q to affine on the calling thread (host inversions, tens of us) rather than in a one-lane kernel (~0.5 ms
+    // per inversion): the same canonical residues the device's jac_to_aff gives
+    PairIn pin;
+    memset(&pin, 0, sizeof pin);
+    {
+        fph::g1 P;
+        fph::g1a pa;
+        memcpy(&P, x, sizeof P);
+        fph::jac_to_aff(pa, P);
+        memcpy(&pin.g[0][0], &pa.x, 48);
+        memcpy(&pin.g[0][12], &pa.y, 48);
+        pin.g[0][24] = pa.inf ? 1u : 0u;
+        pin.g[0][25] = 1u;                           // ok
+        pin.g[1][24] = 1u;                           // the point at infinity
+        pin.g[1][25] = 1u;
+        pin.desc[0] = 0u;                            // check 0: points 0 and 1, line-set pair `slot`
+        pin.desc[1] = 1u;
+        pin.desc[2] = slot;
+    }
+    hipMemcpyAsync(gin, &pin, sizeof pin, hipMemcpyHostToDevice, s);
+    if (!hit) {                                      // the two sets' points for k_lineset_fill: Q, then infinity
+        fph::g2 Q;
+        fph::g2a qa;
+        memcpy(&Q, y, sizeof Q);
+        fph::jac_to_aff(qa, Q);
+        uint32_t pt[2][51];                          // x, y (48 words), LCB_LS_FLAG, + 1 (infinity), + 2 (force general)
+        memset(pt, 0, sizeof pt);
+        memcpy(&pt[0][0], &qa.x, 96);
+        memcpy(&pt[0][24], &qa.y, 96);
+        pt[0][49] = qa.inf ? 1u : 0u;
+        pt[1][49] = 1u;
+        for (int k = 0; k < 2; k++)
+            hipMemcpyAsync(lines + (size_t)(2 * slot + k) * (LCB_LINESET_BYTES / 4) + LCB_LS_POINT_WORD, pt[k],
+                           sizeof pt[k], hipMemcpyHostToDevice, s);
+    }
+    if (!hit) lcbk_lineset_coop(s, lines + (size_t)2 * slot * (LCB_LINESET_BYTES / 4), 2, nullptr, nullptr);
     lcbk_coop_tpke_miller(s, lines, desc, gpts, 1, park, fl, fl + 32, 1);
     lcbk_coop_final_exp_check(s, park, 1, nullptr);
     u32 r[144];

@@ -168,12 +168,13 @@ DI void g2_inf_st(g2a_st &o) { o.ok = 1; o.pad[0] = o.pad[1] = 0; o.inf = 1; o.x
 // The keys (TPKE verification keys Y_d, threshold-signature public keys PK_k) are the same for every ciphertext /
 // coin of a batch: per key, table[w][d - 1] = d 2^(8w) K (affine x, y and beta x, d = 1..255, w = 0..3) turns
 // a K + b phi(K) for 32-bit a, b into at most 8 mixed additions (4 byte digits of a, 4 of b on the phi entries) instead
-// of 32 doublings + ~32 mixed additions.  One lane per (key, window): 8w doublings, 254 additions into a
-// Jacobian scratch, then one batched inversion (Montgomery's trick) to affine.  A key whose chain meets the point at
+// of 32 doublings + ~32 mixed additions.  LCB_KTAB_CHUNKS lanes per (key, window), each 8w doublings, a start multiple and
+// LCB_KTAB_CHUNK - 1 additions into a Jacobian scratch, then one batched inversion (Montgomery's trick) to affine.  A key whose chain meets the point at
 // infinity (a key with no r-torsion part) or that did not decompress gets ktab_ok = 0: its shares use the ladder.
 #define LCB_KTAB_ENTRIES (4 * 255)
-#define LCB_KTAB_CHUNK 32                              // entries per lane: 8 lanes per (key, window)
-#define LCB_KTAB_LANES 32                              // lanes (and flags) per key
+#define LCB_KTAB_CHUNK 16                              // entries per lane: 16 lanes per (key, window)
+#define LCB_KTAB_CHUNKS 16                             // (255 + LCB_KTAB_CHUNK - 1) / LCB_KTAB_CHUNK
+#define LCB_KTAB_LANES 64                              // lanes (and flags) per key: 4 windows x LCB_KTAB_CHUNKS
 DN void g1_mul_ab_tab(g1 &r, const u32 *tab, u32 n_keys, u32 k, u32 a, u32 b) {
     const size_t stride = (size_t)n_keys * LCB_KTAB_ENTRIES, e0 = (size_t)k * LCB_KTAB_ENTRIES;
     g1 acc;
@@ -191,9 +192,16 @@ DN void g1_mul_ab_tab(g1 &r, const u32 *tab, u32 n_keys, u32 k, u32 a, u32 b) {
     }
     r = acc;
 }
-DI bool ktab_usable(const uint8_t *ktab_ok, u32 k) {      // all 32 lanes of the key's table succeeded
+DI bool ktab_usable(const uint8_t *ktab_ok, u32 k) {      // all LCB_KTAB_LANES lanes of the key's table succeeded
     if (!ktab_ok) return false;
     const uint4 *f = (const uint4 *)(ktab_ok + (size_t)LCB_KTAB_LANES * k);
-    uint4 x = f[0], y = f[1];
-    return (x.x & x.y & x.z & x.w & y.x & y.y & y.z & y.w) == 0x01010101u;
+    u32 a = 0x01010101u;
+#pragma unroll
+    for (int q = 0; q < LCB_KTAB_LANES / 16; q++) {
+        const uint4 x = f[q];
+        a &= x.x & x.y & x.z & x.w;
+    }
+    return a == 0x01010101u;
 }
+static_assert(LCB_KTAB_CHUNK * LCB_KTAB_CHUNKS >= 255 && LCB_KTAB_CHUNK * (LCB_KTAB_CHUNKS - 1) < 255, "key-table chunks");
+static_assert(LCB_KTAB_LANES == 4 * LCB_KTAB_CHUNKS && LCB_KTAB_LANES % 16 == 0, "key-table lanes");

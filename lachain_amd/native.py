@@ -59,6 +59,9 @@ _SIGS = {
     "lcb_last_error": (ctypes.c_char_p, []),
     "lcb_error_count": (ctypes.c_uint64, []),
     "lcb_test_inject_failure": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "lcb_set_lines_coop_max": (ctypes.c_int, [ctypes.c_int]),
+    "lcb_test_linesets": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t,
+                                          ctypes.c_void_p, ctypes.c_void_p]),
     "lcb_tpke_verify_shares": (ctypes.c_int, [c_u8p, c_size, c_u8p, c_size, c_u8p, c_u8p, c_u8p, c_u32p, c_size,
                                               c_u32p, c_u32p, c_u8p]),
     "lcb_tpke_verify_shares_cached": (ctypes.c_int, [c_u8p, c_size, c_u8p, c_size, c_u8p, c_u8p, c_u8p, c_u32p, c_size,
@@ -754,6 +757,24 @@ def inject_failure(site, count=1):
     """test hook (LCB_ALLOW_TEST_HOOKS=1): the next `count` passes through fault site `site` fail"""
     if lib().lcb_test_inject_failure(int(site), int(count)) != 0:
         raise RuntimeError("inject_failure: " + last_error())
+
+
+def test_linesets(points, coop, force=None):
+    """test hook (LCB_ALLOW_TEST_HOOKS=1): the line sets of G2 wire points on the five-lane (coop) or one-lane kernel;
+    returns (uint32 array [n, 6592], the G2 flags of the odd-indexed points)"""
+    import numpy as np
+    n = len(points)
+    force = bytes(force) if force is not None else bytes(n)
+    out = np.zeros((n, 6592), dtype=np.uint32)
+    g2f = np.zeros(max(1, n // 2), dtype=np.uint8)
+    if lib().lcb_test_linesets(1 if coop else 0, b"".join(points), force, n, out.ctypes.data, g2f.ctypes.data) != 0:
+        raise RuntimeError("test_linesets: " + last_error())
+    return out, g2f[: n // 2]
+
+
+def set_lines_coop_max(max_sets):
+    """line sets of up to max_sets points per preparation on the five-lane kernel (-1: default)"""
+    _tuning(lib().lcb_set_lines_coop_max(int(max_sets)), "set_lines_coop_max")
 
 
 def set_wave_priority(on):

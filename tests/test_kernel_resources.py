@@ -35,18 +35,20 @@ BUDGET = {
     "k_g1_to_affine": (0, 704),
     "k_g2_decompress": (0, 992),
     "k_g2_hash": (0, 3336),
+    "k_mcl_g2_hash": (0, 3336),               # mclBnG2_hashAndMapTo: the same one-lane hash as k_g2_hash
     "k_g2_mul": (206, 10624),
     "k_g2_mul_lanes": (1300, 10288),
     "k_g2_mul2_lanes": (4530, 22672),         # two GLS tables (31 entries) per lane: the assembly's paired lanes
     "k_g2_sum": (204, 1008),
     "k_lineset_fill": (0, 1824),
+    "k_lineset_coop": (86, 800),              # five-lane line sets (latency path): T, Q, acc and five products live
     "k_msm_bucket_reduce": (0, 744),          # + the prefetched next bucket
     "k_msm_horner": (0, 168),
     "k_msm_bucket_fix": (0, 168),
     "k_op": (3038, 8484),
     "k_ptmul_g2": (32, 68),                   # mcl G2 multiplication latency kernel: four ladder lanes share each op                     # mcl single-element surface: every operation in one kernel
     "k_rlc_key_tables": (12, 768),            # k_rlc_rand.hip: spills to scratch, not AGPRs (<= 256 registers)
-    "k_rlc_miller_fallback": (0, 2376),
+    "k_rlc_miller_fallback": (2, 4532),       # two waves per SIMD (dispatchable beside the randomisation), rare path
     "k_rlc_search": (93, 2264),
     "k_tpke_rlc_search2a": (92, 2264),         # level-2 searches: three Fp12 values per lane, one lane per group
     "k_tpke_rlc_search2b": (133, 4088),
