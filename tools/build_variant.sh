@@ -6,6 +6,5 @@ TAG=$1; DEFS=$2
 R=$(cd "$(dirname "$0")/.." && pwd)
 OBJ=$R/build/ab_obj/$TAG
 mkdir -p $OBJ $R/lachain_amd/ab/$TAG
-make -s -j8 -C $R/lachain_amd/csrc OBJDIR=$OBJ OUT=$R/lachain_amd/ab/$TAG/liblachain_bls.so \
-    HIPFLAGS="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-function -Wno-unused-variable $DEFS"
+make -s -j8 -C $R/lachain_amd/csrc OBJDIR=$OBJ OUT=$R/lachain_amd/ab/$TAG/liblachain_bls.so DEFS="$DEFS"
 echo built $R/lachain_amd/ab/$TAG/liblachain_bls.so
