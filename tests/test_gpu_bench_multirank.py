@@ -30,7 +30,10 @@ def test_bench_world_size_two():
            "--ecdsa-sigs", "4096", "--ecdsa-validators", "16", "--msm-sizes", "8192", "--msm-steps", "1",
            "--no-cpu-baseline"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=420)
-    assert r.returncode == 0, r.stderr[-3000:]
+    if r.returncode != 0 and os.path.isdir(os.path.join(ROOT, "gpurun_out")):
+        with open(os.path.join(ROOT, "gpurun_out", "bench_multirank_failure.txt"), "w") as fh:
+            fh.write(r.stdout + "\n----- stderr -----\n" + r.stderr)
+    assert r.returncode == 0, r.stderr[:2000] + "\n...\n" + r.stderr[-2000:]
     lines = r.stdout.splitlines()
     head = json.loads([x for x in lines if x.startswith("{")][-1])
     assert lines[-1].startswith("{") and len(lines[-1]) <= 6144       # the compact headline is the last line
