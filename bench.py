@@ -1833,6 +1833,8 @@ def main():
         nat.set_wave_priority(int(os.environ["LCB_WAVE_PRIO"]))
     if os.environ.get("LCB_MSM_SEGS"):            # A/B of the bucket-reduction lane count
         nat.set_msm_segments(int(os.environ["LCB_MSM_SEGS"]))
+    if os.environ.get("LCB_KEYS_FIRST"):          # A/B of the key tables' place in the fused batched calls
+        nat.set_keys_first(int(os.environ["LCB_KEYS_FIRST"]))
     if os.environ.get("LCB_LINES_COOP"):          # A/B of the five-lane line-set kernel's size limit
         nat.set_lines_coop_max(int(os.environ["LCB_LINES_COOP"]))
     if os.environ.get("LCB_MSM_CHUNK"):           # A/B of the MSM bucket accumulation (0: one lane per bucket)

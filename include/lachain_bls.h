@@ -266,6 +266,9 @@ int lcb_tpke_verify_phase_ms(float ms[2]);
 /* Line sets of up to max_sets points per preparation on the five-lane kernel (latency), larger preparations one lane
    per set (throughput); -1 restores the default (8,192).  Tuning hook: -1 unless LCB_ALLOW_TUNING=1. */
 int lcb_set_lines_coop_max(int max_sets);
+/* 1 (default): the fused batched calls build the validators' fixed-base tables before forking the preparation streams;
+   0: on the randomisation stream beside them.  Tuning hook: -1 unless LCB_ALLOW_TUNING=1. */
+int lcb_set_keys_first(int on);
 
 /* Randomized batch form of lcb_tpke_verify_prepared_dev (same arguments, same workspace, same validity rules;
    replaces the per-share loop over TPKE/PublicKey.cs:88-92 driven from HoneyBadger.cs:211-212).  Shares are grouped

@@ -275,7 +275,11 @@ DI void fp2_inv(fp2 &r, const fp2 &x) {
     r.a = t.a;
     fp_neg(r.b, t.b);
 }
-// mcl Fp2T::squareRoot (norm method; root choice reproduced exactly)
+// mcl Fp2T::squareRoot (norm method; root choice reproduced exactly): t = sqrt(a^2 + b^2), then the
+// root of c = (a + t)/2, else of (a - t)/2, as y.a, and y.b = b / (2 y.a).  mcl takes that root and inverts it with two
+// exponentiations; here one gives both: s = c^((p-3)/4), c s = c^((p+1)/4) (mcl's root) and, when c is a square
+// (c s^2 = c^((p-1)/2) = 1, Euler's criterion — mcl's check y.a^2 == c), 1/(c s) = s.  For b != 0, c != 0 (c = 0 would
+// need t = -a, so b = 0), so the two tests agree and every output is the same field element.
 DI bool fp2_sqrt(fp2 &y, const fp2 &x) {
     fp t1, t2, inv2;
     fp_load_const(inv2, LCB_INV2);
@@ -296,18 +300,23 @@ DI bool fp2_sqrt(fp2 &y, const fp2 &x) {
     fp_sqr(t2, x.b);
     fp_add(t1, t1, t2);
     if (!fp_sqrt(t1, t1)) return false;
-    fp_add(t2, x.a, t1);
-    fp_mul(t2, t2, inv2);
-    if (!fp_sqrt(t2, t2)) {
-        fp_sub(t2, x.a, t1);
-        fp_mul(t2, t2, inv2);
-        if (!fp_sqrt(t2, t2)) return false;
+#pragma unroll 1
+    for (int k = 0; k < 2; k++) {
+        fp c, s, cs, e;
+        if (k == 0) fp_add(c, x.a, t1);
+        else fp_sub(c, x.a, t1);
+        fp_mul(c, c, inv2);
+        fp_pow_const(s, c, LCB_P_MINUS3_DIV4);
+        fp_mul(cs, c, s);                              // c^((p+1)/4)
+        fp_mul(e, cs, s);                              // c^((p-1)/2)
+        if (fp_eq(e, fp_one())) {
+            y.a = cs;
+            fp_mul(t2, x.b, s);
+            fp_mul(y.b, t2, inv2);                     // b / (2 c^((p+1)/4)) = b s / 2
+            return true;
+        }
     }
-    y.a = t2;
-    fp_add(t2, t2, t2);
-    fp_inv(t2, t2);
-    fp_mul(y.b, x.b, t2);
-    return true;
+    return false;
 }
 // A square root of x in Fp2 when the caller fixes the sign itself (G2 decompression): two exponentiations instead
 // of fp2_sqrt's four per wave (its second Fp root runs whenever one lane needs it, and it ends in an inversion).

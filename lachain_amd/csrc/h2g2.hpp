@@ -91,9 +91,16 @@ DI void fp_set_hash_digest(fp &r, const uint8_t d[64]) {
 
 // MapTo::calcBN<G2, Fp2>
 DI bool g2_calc_bn(g2 &P, const fp2 &t) {
-    fp nrm;
-    fp2_norm(nrm, t);
-    int leg = fp_legendre(nrm);
+    // mcl's sign: the Legendre symbol of N(t).  For the hash's t = (t.a, 0), N(t) = t.a^2 is a square, so the symbol
+    // is 1 unless t = 0 — no exponentiation needed
+    int leg;
+    if (fp_is_zero(t.b)) {
+        leg = fp_is_zero(t.a) ? 0 : 1;
+    } else {
+        fp nrm;
+        fp2_norm(nrm, t);
+        leg = fp_legendre(nrm);
+    }
     if (leg == 0) return false;
     bool negative = leg < 0;
     fp2 w, x, y, tmp, b2;

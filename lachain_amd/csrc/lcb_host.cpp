@@ -949,7 +949,26 @@ struct RlcStats {
 thread_local RlcStats t_rlc_stats;
 // cnt: [0] current level's groups, [1] next level's, [2] search entries, [3] suspect keys, [4] level-1 entries after
 // the suspect split; susp: the suspect-key bitmap; m: census shares [0, m)
-struct RlcWs { u32 *rA, *rB; uint8_t *dA, *dB; u32 *cnt; u32 *susp; u32 m; };
+struct RlcWs {
+    u32 *rA, *rB;
+    uint8_t *dA, *dB;
+    u32 *cnt;
+    u32 *susp;
+    u32 m;
+    u32 *ktab = nullptr;               // the keys' fixed-base tables when built ahead of the fork (keys_first_tables)
+    uint8_t *kok = nullptr;
+    bool ktab_pre = false;
+};
+// the fused batched calls build the keys' fixed-base tables on the caller's stream BEFORE forking the preparation: a
+// key-table wave (277 registers) cannot be placed beside a preparation wave (346), so launched beside them the tables
+// (and the randomisation behind them) waited up to ~20 ms for the preparation to drain (profiles/r04/ab1)
+std::atomic<int> g_keys_first{1};
+u32 *rlc_key_tables(lcb_ctx *c, const void *keys, size_t n_keys, hipStream_t s, uint8_t **ktab_ok);
+void keys_first_tables(lcb_ctx *c, RlcWs &w, const void *keys, size_t n_keys, size_t n, hipStream_t s) {
+    if (!g_keys_first.load() || w.m >= n) return;
+    w.ktab = rlc_key_tables(c, keys, n_keys, s, &w.kok);
+    w.ktab_pre = true;
+}
 bool rlc_key_fill(lcb_ctx *c, u32 key[10]) {
     bool fixed;
     {
@@ -1015,8 +1034,8 @@ int rlc_points_enqueue(lcb_ctx *c, RlcWs &w, uint8_t *d_accept, size_t n, size_t
     if (!rlc_key_fill(c, key)) return -1;
     hipEventRecord(c->rlc_ev[0], s);
     if (w.m < n) {
-        uint8_t *kok = nullptr;
-        u32 *ktab = rlc_key_tables(c, c->t_keys.p, n_keys, s, &kok);
+        uint8_t *kok = w.kok;
+        u32 *ktab = w.ktab_pre ? w.ktab : rlc_key_tables(c, c->t_keys.p, n_keys, s, &kok);
         lcbk_tpke_rlc_points(s, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct, d_dec, d_ui, w.m, (u32)n, key, w.rA, w.rB,
                              d_accept, ktab, kok, w.susp);
         lcbk_rlc_groups(s, d_ct, w.m, (u32)n, (u32)n_cts, 32, w.dA, w.cnt);
@@ -1030,8 +1049,8 @@ int ts_rlc_points_enqueue(lcb_ctx *c, RlcWs &w, uint8_t *d_accept, size_t n, siz
     if (!rlc_key_fill(c, key)) return -1;
     hipEventRecord(c->rlc_ev[0], s);
     if (w.m < n) {
-        uint8_t *kok = nullptr;
-        u32 *ktab = rlc_key_tables(c, c->s_keys.p, n_pks, s, &kok);
+        uint8_t *kok = w.kok;
+        u32 *ktab = w.ktab_pre ? w.ktab : rlc_key_tables(c, c->s_keys.p, n_pks, s, &kok);
         // decoded-share records for the assembly (optional: without the buffer the assembly decodes the shares)
         const size_t rec = n * (size_t)LCB_TS_SHARE_REC_BYTES;
         const bool grow = c->s_dec.cap < rec;
@@ -1333,6 +1352,7 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
     hipStream_t sr = hp ? s : c->aux, sp = hp ? c->hi : s;
     if (n) {
         if (!rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G1_JAC_BYTES, n_keys, m_census, s)) return -1;
+        keys_first_tables(c, w, keys, n_keys, n, s);
         hipEventRecord(c->fork_ev[0], s);
         hipStreamWaitEvent(hp ? sp : sr, c->fork_ev[0], 0);
         if (hp) hipEventRecord(c->prep_ev[0], sp);
@@ -1480,6 +1500,7 @@ int ts_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const ui
     hipStream_t sr = hp ? s : c->aux, sp = hp ? c->hi : s;
     if (n) {
         if (!rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G2_JAC_BYTES, n_pks, census_size(n, n_pks), s)) return -1;
+        keys_first_tables(c, w, keys, n_pks, n, s);
         hipEventRecord(c->fork_ev[0], s);
         hipStreamWaitEvent(hp ? sp : sr, c->fork_ev[0], 0);
         if (hp) hipEventRecord(c->prep_ev[0], sp);
@@ -1816,6 +1837,11 @@ extern "C" int lcb_set_wave_priority(int on) {
 extern "C" int lcb_set_msm_segments(int max_segments) {
     if (!tuning_allowed("lcb_set_msm_segments")) return -1;
     g_msm_segs.store(max_segments > 0 ? max_segments : 0);
+    return 0;
+}
+extern "C" int lcb_set_keys_first(int on) {
+    if (!tuning_allowed("lcb_set_keys_first")) return -1;
+    g_keys_first.store(on ? 1 : 0);
     return 0;
 }
 extern "C" int lcb_set_lines_coop_max(int max_sets) {

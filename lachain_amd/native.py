@@ -60,6 +60,7 @@ _SIGS = {
     "lcb_error_count": (ctypes.c_uint64, []),
     "lcb_test_inject_failure": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "lcb_set_lines_coop_max": (ctypes.c_int, [ctypes.c_int]),
+    "lcb_set_keys_first": (ctypes.c_int, [ctypes.c_int]),
     "lcb_test_linesets": (ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t,
                                           ctypes.c_void_p, ctypes.c_void_p]),
     "lcb_tpke_verify_shares": (ctypes.c_int, [c_u8p, c_size, c_u8p, c_size, c_u8p, c_u8p, c_u8p, c_u32p, c_size,
@@ -775,6 +776,11 @@ def test_linesets(points, coop, force=None):
 def set_lines_coop_max(max_sets):
     """line sets of up to max_sets points per preparation on the five-lane kernel (-1: default)"""
     _tuning(lib().lcb_set_lines_coop_max(int(max_sets)), "set_lines_coop_max")
+
+
+def set_keys_first(on):
+    """fused batched calls: the key tables before the preparation fork (default on)"""
+    _tuning(lib().lcb_set_keys_first(1 if on else 0), "set_keys_first")
 
 
 def set_wave_priority(on):
