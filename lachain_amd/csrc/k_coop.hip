@@ -66,11 +66,10 @@ extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_tpke_miller(const 
     }
 }
 // the groups k_coop_tpke_miller flagged: one lane each, the one-lane fallback (lines of the un-normalised set computed
-// on the fly).  Built for two waves per SIMD (<= 256 registers, the rest spilled): a flagged group is rare (only an
-// adversarial W has an A_k == 0), but every level launches the kernel, and at 360 registers its waves could not be
-// dispatched beside the randomisation's (248 registers, two per SIMD) until that kernel's tail — the census chain
-// waited 14.6 ms for lanes that all return at once (profiles/r04/ab1)
-extern "C" __global__ void __launch_bounds__(LCB_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) k_rlc_miller_fallback(const u32 *lines, const uint4 *desc, const g1a_st *gpts,
+// on the fly).  (Built for two waves per SIMD, its waves could be placed beside the randomisation's, but the doubled
+// resident-wave count doubled the scratch each HIP queue reserves for it — 4.5 KB per lane — and two bench ranks on
+// one GPU then failed a dispatch with HSA_STATUS_ERROR_OUT_OF_RESOURCES: reverted, profiles/r04/r04f.)
+extern "C" __global__ void LCB_PAIR_BOUNDS k_rlc_miller_fallback(const u32 *lines, const uint4 *desc, const g1a_st *gpts,
                                                                 u32 n_groups, u32 *f_soa, const uint8_t *fb) {
     LCB_LATENCY_PRIO();
     u32 g = blockIdx.x * blockDim.x + threadIdx.x;

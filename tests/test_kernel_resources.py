@@ -48,7 +48,7 @@ BUDGET = {
     "k_op": (3038, 8484),
     "k_ptmul_g2": (32, 68),                   # mcl G2 multiplication latency kernel: four ladder lanes share each op                     # mcl single-element surface: every operation in one kernel
     "k_rlc_key_tables": (12, 768),            # k_rlc_rand.hip: spills to scratch, not AGPRs (<= 256 registers)
-    "k_rlc_miller_fallback": (2, 4532),       # two waves per SIMD (dispatchable beside the randomisation), rare path
+    "k_rlc_miller_fallback": (0, 2376),
     "k_rlc_search": (93, 2264),
     "k_tpke_rlc_search2a": (92, 2264),         # level-2 searches: three Fp12 values per lane, one lane per group
     "k_tpke_rlc_search2b": (133, 4088),
