@@ -213,8 +213,14 @@ def load(check_device=True):
             if not os.path.exists(LIB_PATH):
                 raise RuntimeError(f"{LIB_PATH} is not built (run __graft_entry__.build() or make -C lachain_amd/csrc)")
             lib_ = ctypes.CDLL(LIB_PATH)
+            ab = bool(os.environ.get("LCB_LIB_PATH"))
             for name, (res, args) in _SIGS.items():
-                fn = getattr(lib_, name)
+                try:
+                    fn = getattr(lib_, name)
+                except AttributeError:
+                    if ab:          # an A/B build of an earlier revision may lack newer entry points
+                        continue
+                    raise
                 fn.restype = res
                 fn.argtypes = args
             _lib = lib_

@@ -22,7 +22,10 @@ def _free_port():
 
 
 def test_bench_world_size_two():
-    env = dict(os.environ, LCB_BENCH_BACKEND="gloo", OMP_NUM_THREADS="4")
+    # HIP's default four hardware queues per rank: with bench.py's eight, the two ranks' 16 queues on the one GPU
+    # exhausted the scratch pool (HSA_STATUS_ERROR_OUT_OF_RESOURCES at a 7.6 KB-per-lane dispatch, profiles/r04/r04f);
+    # the driver's N > 1 runs have one rank per GPU
+    env = dict(os.environ, LCB_BENCH_BACKEND="gloo", OMP_NUM_THREADS="4", LCB_BENCH_HWQ="4")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "1", "--warmup", "1", "--shares", "8800", "--pattern-steps", "1",
