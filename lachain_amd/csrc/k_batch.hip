@@ -114,51 +114,6 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_rlc_miller(const u32 *lines, c
 // emitted straight away as an exact single (desc.w = 1) and contributes nothing to its group.
 // TS group record: g1a_st P (sum s_i PK_i) then g2a_st S (sum s_i sig_i), 320 B
 struct ts_grp { g1a_st p; g2a_st s; };
-extern "C" __global__ void LCB_BOUNDS k_ts_rlc_points(u32 n_msgs, const g1a_st *pks, u32 n_pks, const u32 *msg_idx,
-                                                     const u32 *pk_idx, const uint8_t *sigs, u32 i0, u32 n,
-                                                     rlc_key key, u32 *rP, u32 *rS, uint8_t *accept, uint4 *desc,
-                                                     u32 *count, const u32 *ktab, const uint8_t *ktab_ok,
-                                                     const u32 *susp, ts_share_st *dec) {
-    u32 i = i0 + blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    u32 m = msg_idx[i], k = pk_idx[i];
-    bool ok = k < n_pks && m < n_msgs;
-    g2a S;
-    g1a PK;
-    ok = g2_decompress(S, sigs + 96 * (size_t)i) && ok;
-    g1a_st ps = pks[k < n_pks ? k : 0];
-    ok = ok && ps.ok;
-    st_to_g1a(PK, ps);
-    g1 p;
-    g2 q;
-    jac_set_inf(p);
-    jac_set_inf(q);
-    if (ok && !key_suspect_live(susp, k, n_pks)) {      // (a suspect key's shares get their singles from the split)
-        const bool in_g2 = g2_in_subgroup_inl(S);       // inline: measured faster than the call (CommonCoin batch)
-        if (dec) {                                      // the decoded share for the assembly (ts_share_st)
-            ts_share_st *e = dec + i;
-            const uint4 *src = (const uint4 *)(sigs + 96 * (size_t)i);
-#pragma unroll
-            for (int q = 0; q < 6; q++) ((uint4 *)e->raw)[q] = src[q];
-            g2a_st o;
-            o.x = S.x; o.y = S.y; o.inf = 0; o.ok = 1; o.pad[0] = in_g2 ? 1u : 0u; o.pad[1] = 0;
-            e->p = o;
-        }
-        if (in_g2) {
-            u32 a, b;
-            rlc_scalar(key, i, a, b);
-            if (ktab_usable(ktab_ok, k)) g1_mul_ab_tab(p, ktab, n_pks, k, a, b);
-            else g1_mul_ab_n(p, PK, a, b);
-            g2_mul_ab_inl(q, S, a, b);  // inline: 937 vs 1015 ms per 6.55M-share CommonCoin batch with the call
-        } else {
-            u32 slot = atomicAdd(count, 1u);
-            desc[slot] = make_uint4(i, 1, m < n_msgs ? m : 0, 1);
-        }
-    }
-    g1_store_soa(rP, n, i, p);
-    g2_store_soa(rS, n, i, q);
-    accept[i] = ok;
-}
 extern "C" __global__ void LCB_BOUNDS k_ts_rlc_sum(const uint4 *desc, u32 n_groups, u32 first, const uint8_t *msg_ok,
                                                   const g1a_st *pks, u32 n_pks, const u32 *pk_idx, const uint8_t *sigs,
                                                   const u32 *rP, const u32 *rS, u32 n, ts_grp *gpts, uint8_t *accept,
@@ -560,18 +515,6 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_suspect_split(const uint4 *desc, u32
 // table workspace per key: Jacobian scratch 144 B + prefix products 48 B + table 144 B per entry + 32 flags
 extern "C" size_t lcbk_key_table_bytes(u32 n_keys) {
     return (size_t)n_keys * (LCB_KTAB_ENTRIES * 336 + LCB_KTAB_LANES) + 16;
-}
-extern "C" void lcbk_ts_rlc_points(hipStream_t s, u32 n_msgs, const void *pks, u32 n_pks, const u32 *msg_idx,
-                                   const u32 *pk_idx, const uint8_t *sigs, u32 i0, u32 n, const u32 key[10], u32 *rP,
-                                   u32 *rS, uint8_t *accept, void *desc, u32 *count, const u32 *ktab,
-                                   const uint8_t *ktab_ok, const u32 *susp, void *dec) {
-    rlc_key k;
-    for (int j = 0; j < 8; j++) k.k[j] = key[j];
-    k.nonce[0] = key[8];
-    k.nonce[1] = key[9];
-    dim3 grid((n - i0 + LCB_BLOCK - 1) / LCB_BLOCK);
-    LCB_LAUNCH(k_ts_rlc_points, n_msgs, (const g1a_st *)pks, n_pks, msg_idx, pk_idx, sigs, i0, n, k, rP, rS, accept,
-               (uint4 *)desc, count, ktab, ktab_ok, susp, (ts_share_st *)dec);
 }
 extern "C" void lcbk_rlc_groups(hipStream_t s, const u32 *key_idx, u32 i0, u32 n, u32 n_keys, u32 cap, void *desc,
                                 u32 *count) {

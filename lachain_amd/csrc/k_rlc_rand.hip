@@ -236,7 +236,70 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum2(const uint4 *sdesc, u32 n
     gpts[2 * ((size_t)(which ? ns : 0) + g) + side] = o;
 }
 
+// ---------------------------------------------------------------- threshold signatures: per-share randomisation
+// (k_batch.hip describes the check).  Built here, without VGPR-to-AGPR spilling and for two waves per SIMD (256
+// registers, the rest spilled to scratch), like k_tpke_rlc_points: in k_batch.hip it took 512 registers, one wave
+// per SIMD.
+extern "C" __global__ void __launch_bounds__(LCB_BLOCK) __attribute__((amdgpu_waves_per_eu(2))) k_ts_rlc_points(u32 n_msgs, const g1a_st *pks, u32 n_pks, const u32 *msg_idx,
+                                                     const u32 *pk_idx, const uint8_t *sigs, u32 i0, u32 n,
+                                                     rlc_key key, u32 *rP, u32 *rS, uint8_t *accept, uint4 *desc,
+                                                     u32 *count, const u32 *ktab, const uint8_t *ktab_ok,
+                                                     const u32 *susp, ts_share_st *dec) {
+    u32 i = i0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    u32 m = msg_idx[i], k = pk_idx[i];
+    bool ok = k < n_pks && m < n_msgs;
+    g2a S;
+    g1a PK;
+    ok = g2_decompress(S, sigs + 96 * (size_t)i) && ok;
+    g1a_st ps = pks[k < n_pks ? k : 0];
+    ok = ok && ps.ok;
+    st_to_g1a(PK, ps);
+    g1 p;
+    g2 q;
+    jac_set_inf(p);
+    jac_set_inf(q);
+    if (ok && !key_suspect_live(susp, k, n_pks)) {      // (a suspect key's shares get their singles from the split)
+        const bool in_g2 = g2_in_subgroup_inl(S);       // inline: measured faster than the call (CommonCoin batch)
+        if (dec) {                                      // the decoded share for the assembly (ts_share_st)
+            ts_share_st *e = dec + i;
+            const uint4 *src = (const uint4 *)(sigs + 96 * (size_t)i);
+#pragma unroll
+            for (int q = 0; q < 6; q++) ((uint4 *)e->raw)[q] = src[q];
+            g2a_st o;
+            o.x = S.x; o.y = S.y; o.inf = 0; o.ok = 1; o.pad[0] = in_g2 ? 1u : 0u; o.pad[1] = 0;
+            e->p = o;
+        }
+        if (in_g2) {
+            u32 a, b;
+            rlc_scalar(key, i, a, b);
+            if (ktab_usable(ktab_ok, k)) g1_mul_ab_tab(p, ktab, n_pks, k, a, b);
+            else g1_mul_ab_n(p, PK, a, b);
+            g2_mul_ab_inl(q, S, a, b);  // inline: 937 vs 1015 ms per 6.55M-share CommonCoin batch with the call
+        } else {
+            u32 slot = atomicAdd(count, 1u);
+            desc[slot] = make_uint4(i, 1, m < n_msgs ? m : 0, 1);
+        }
+    }
+    g1_store_soa(rP, n, i, p);
+    g2_store_soa(rS, n, i, q);
+    accept[i] = ok;
+}
+
 // ---------------------------------------------------------------- host launch wrappers
+extern "C" void lcbk_ts_rlc_points(hipStream_t s, u32 n_msgs, const void *pks, u32 n_pks, const u32 *msg_idx,
+                                   const u32 *pk_idx, const uint8_t *sigs, u32 i0, u32 n, const u32 key[10], u32 *rP,
+                                   u32 *rS, uint8_t *accept, void *desc, u32 *count, const u32 *ktab,
+                                   const uint8_t *ktab_ok, const u32 *susp, void *dec) {
+    rlc_key k;
+    for (int j = 0; j < 8; j++) k.k[j] = key[j];
+    k.nonce[0] = key[8];
+    k.nonce[1] = key[9];
+    dim3 grid((n - i0 + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_ts_rlc_points, n_msgs, (const g1a_st *)pks, n_pks, msg_idx, pk_idx, sigs, i0, n, k, rP, rS, accept,
+               (uint4 *)desc, count, ktab, ktab_ok, susp, (ts_share_st *)dec);
+}
+
 extern "C" void lcbk_rlc_key_tables(dim3 grid, hipStream_t s, const void *keys, u32 n_keys, u32 *ws, u32 **tab,
                                     uint8_t **ktab_ok) {
     const size_t ne = (size_t)n_keys * LCB_KTAB_ENTRIES;

@@ -65,7 +65,7 @@ BUDGET = {
     "k_ts_miller": (1248, 3292),
     "k_ts_msg_prepare": (0, 3624),
     "k_ts_rlc_miller": (0, 2524),
-    "k_ts_rlc_points": (554, 1568),
+    "k_ts_rlc_points": (677, 3360),           # k_rlc_rand.hip: 256 registers, two waves per SIMD (spills to scratch)
     "k_ts_rlc_sum": (0, 2136),
     "k_ts_rlc_wsum": (12, 992),
     "k_ts_sign": (0, 3912),
