@@ -79,6 +79,9 @@ bool injected(int site) {
     return false;
 }
 enum { INJ_STAGE_HOST_ALLOC = 1, INJ_CT_CACHE_ALLOC = 2, INJ_PAIRING_ALLOC = 3, INJ_STAGE_OP = 4 };
+bool inject_armed(int site) {             // a pending failure at `site` (not consumed)
+    return g_inject_site.load(std::memory_order_relaxed) == site && g_inject_count.load() > 0;
+}
 
 // the output of a failed void mcl call (mclBnG1_mul, mclBn_pairing, ...): random words with the top limb of the first
 // coordinate set to all ones, so it is not a canonical field element (isValid / serialize reject it), and two failed
@@ -156,7 +159,8 @@ bool stage_ready() {
     {
         std::lock_guard<std::mutex> lk(retired_mu());
         auto &v = retired_stages();
-        if (!v.empty() && !t_stage.s && !t_stage.dev && !t_stage.host) {
+        // (a pending staging-allocation failure builds a new stage, so the test hook reaches the allocation)
+        if (!v.empty() && !t_stage.s && !t_stage.dev && !t_stage.host && !inject_armed(INJ_STAGE_HOST_ALLOC)) {
             static_cast<StageRes &>(t_stage) = v.back();
             v.pop_back();
             return true;
