@@ -1,9 +1,9 @@
 // lachain_amd/csrc/coop_pt.hpp — point operations shared by a group of four lanes (k_ptmul.hip, k_msm.hip's window
 // combination): every lane of the group holds the group's values, a ROUND is one Fp (G1) or Fp2 (G2) product per lane
-// on operands it selects by its role, and the four products are exchanged by DPP quad permutations (a group is one
-// quad of lanes: no LDS round trip, no barrier).  dbl-2009-l takes 3 rounds instead of 7 serial products, add-2007-bl 5
-// instead of 16, with curve.hpp's formulas and special cases (the results are the same Jacobian coordinates as jac_dbl /
-// jac_add).  Every lane of the quad must execute each round: callers keep the control flow around them wave-uniform.
+// on operands it selects by its role, and the four products are exchanged through the group's LDS area.
+// dbl-2009-l takes 3 rounds instead of 7 serial products, add-2007-bl 5 instead of 16, with curve.hpp's formulas and
+// special cases (the results are the same Jacobian coordinates as jac_dbl / jac_add).  The rounds synchronise the
+// workgroup: callers keep the control flow around them wave-uniform (one wave per workgroup).
 #pragma once
 #include "kcommon.hpp"
 
@@ -31,29 +31,19 @@ template <class F> DI void f_sel4(F &r, int role, const F &a, const F &b, const 
     f_sel(r, role == 1, b, r);
     f_sel(r, role == 2, c, r);
 }
-// lane K of the quad's value of v, in every lane of the quad: a DPP quad permutation (K, K, K, K) of the VGPR — a VALU
-// operand modifier, no LDS round trip and no barrier (the group's four lanes are one DPP quad of the wave)
-template <int K, class F> DI void f_quad_bcast(F &r, const F &v) {
-    const u32 *vw = (const u32 *)&v;
-    u32 *rw = (u32 *)&r;
-#pragma unroll
-    for (int q = 0; q < (int)(sizeof(F) / 4); q++)
-        rw[q] = (u32)__builtin_amdgcn_mov_dpp((int)vw[q], K * 0x55, 0xf, 0xf, false);
-}
-// one round: lane `role` computes x_role * y_role; returns with every lane holding the four products.  Every lane of
-// the wave must execute it (callers keep the control flow around the rounds wave-uniform).
+// one round: lane `role` computes x_role * y_role; returns with every lane holding the four products
 template <class F> DI void pt_round(PtLds<F> *L, F (&p)[PT_LANES], const F &x0, const F &y0, const F &x1,
                                     const F &y1, const F &x2, const F &y2, const F &x3, const F &y3) {
-    (void)L;
     const int role = pt_role();
     F x, y, m;
     f_sel4(x, role, x0, x1, x2, x3);
     f_sel4(y, role, y0, y1, y2, y3);
     f_mul(m, x, y);
-    f_quad_bcast<0>(p[0], m);
-    f_quad_bcast<1>(p[1], m);
-    f_quad_bcast<2>(p[2], m);
-    f_quad_bcast<3>(p[3], m);
+    L->prod[role] = m;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PT_LANES; k++) p[k] = L->prod[k];
+    __syncthreads();
 }
 template <class F> DI void f_dbl(F &r, const F &a) { f_add(r, a, a); }
 
