@@ -1789,8 +1789,11 @@ def main():
     ap.add_argument("--replay-n", type=int, default=256, help="epoch-replay network size N (0 = skip)")
     ap.add_argument("--replay-steps", type=int, default=1)
     ap.add_argument("--replay-exact", type=int, default=0, help="epoch replay with the exact per-share checks")
-    ap.add_argument("--replay-concurrent", type=int, default=1,
-                    help="epoch replay: the TPKE and coin chains side by side (own host thread, context, stream)")
+    ap.add_argument("--replay-concurrent", type=int, default=0,
+                    help="epoch replay: 1 = the TPKE and coin chains side by side (own host thread, context, stream): "
+                         "+3 %% views/s, but the two chains' large-scratch kernels (CommonCoin assembly 22.7 KB per "
+                         "lane) on two hardware queues at once exhausted the scratch pool on some boxes "
+                         "(HSA_STATUS_ERROR_OUT_OF_RESOURCES, profiles/r04/final), so off by default")
     ap.add_argument("--ecdsa-sigs", type=int, default=1 << 20, help="header signatures per rank (0 = skip)")
     ap.add_argument("--ecdsa-validators", type=int, default=256)
     ap.add_argument("--ecdsa-steps", type=int, default=3)
