@@ -57,3 +57,17 @@ def test_oversized_summary_is_dropped():
     line = bench.compact_line(full)
     assert len(json.dumps(line, separators=(",", ":"))) <= bench.LINE_MAX_BYTES
     assert line["roofline"]["frac"] > 0 and line["cpu_baseline"]["value"] > 0
+
+
+def test_round4_driver_run_line_is_its_detail_compacted():
+    """the final round-4 driver-command run (profiles/r04/final/bench_full.txt): its last stdout line is exactly
+    compact_line() of the BENCH_DETAIL record printed above it, within the size limit, with the step's HBM traffic
+    attached (the PMC files were taken on the same build)"""
+    with open(os.path.join(ROOT, "profiles", "r04", "final", "bench_full.txt")) as fh:
+        lines = fh.read().strip().splitlines()
+    detail = json.loads([x for x in lines if x.startswith("BENCH_DETAIL ")][-1][len("BENCH_DETAIL "):])
+    assert len(lines[-1]) <= bench.LINE_MAX_BYTES
+    assert json.loads(lines[-1]) == json.loads(json.dumps(bench.compact_line(detail)))
+    head = json.loads(lines[-1])
+    assert head["roofline"]["traffic"] and head["n_gpus"] == 1 and head["config"]["decision_mismatches"] == 0
+    assert head["source_hash"] == detail["source_hash"]
