@@ -202,7 +202,172 @@ DN u32x12 lcb_fp_pow_v(u32x12 av, const u32 *e) {
     return acc;
 }
 DI void fp_pow_const(fp &r, const fp &a, const u32 *e) { r = fp_from_v(lcb_fp_pow_v(fp_to_v(a), e)); }
-DI void fp_inv(fp &r, const fp &a) { fp_pow_const(r, a, LCB_P_MINUS_2); }
+DI void fp_inv(fp &r, const fp &a) { fp_pow_const(r, a, LCB_P_MINUS_2); }   // a^(p-2): 463 products
+
+// ---- inversion by binary GCD (Pornin, "Optimized Binary GCD for Modular Inversion", eprint 2020/972): 26 outer
+// iterations; each runs 30 divsteps on 62-bit approximations of a, b (the low 30 bits and the top 32 bits of the
+// longer one) to get a 2 x 2 matrix of signed coefficients (|f|, |g| <= 2^30), then applies it to the full a, b
+// (exact: the low 30 bits of the combinations are zero) and to the coefficients u, v with one 32-bit Montgomery
+// reduction modulo p.  From a = X, b = p, u = 1, v = 0 the loop ends with b = 1 and v = X^-1 2^(26 (30 - 32)), so one
+// Montgomery product by LCB_BINV_C = 2^52 R^3 gives the Montgomery form of x^-1 for X = x R (0 -> 0, as a^(p-2)).
+// About 40 K instructions against the exponentiation's 263 K; the same canonical result.  A call (not inlined): its
+// ~150 live registers would otherwise add to the caller's.  Used where the caller's state around the call is small —
+// every Fp2 / Fp6 / Fp12 inversion (line-set normalisation, hash-to-G2, the final exponentiation's easy part) and the
+// key tables; the G1 affine conversions of the group sums and the nine-lane kernels keep fp_inv (the exponentiation
+// routine's narrow calling convention), where the call measured spills.
+DI void fpi_mul32(u32 (&r)[13], const u32 (&x)[12], u32 m) {           // r = x m (13 limbs)
+    u64 c = 0;
+#pragma unroll
+    for (int j = 0; j < 12; j++) {
+        u64 t = (u64)x[j] * m + c;
+        r[j] = (u32)t;
+        c = t >> 32;
+    }
+    r[12] = (u32)c;
+}
+DI void fpi_cneg13(u32 (&r)[13], bool neg) {                           // two's complement negation if neg
+    const u32 m = neg ? 0xffffffffu : 0u;
+    u64 c = neg ? 1u : 0u;
+#pragma unroll
+    for (int j = 0; j < 13; j++) {
+        u64 t = (u64)(r[j] ^ m) + c;
+        r[j] = (u32)t;
+        c = t >> 32;
+    }
+}
+DI void fpi_add13(u32 (&r)[13], const u32 (&x)[13]) {
+    u64 c = 0;
+#pragma unroll
+    for (int j = 0; j < 13; j++) {
+        u64 t = (u64)r[j] + x[j] + c;
+        r[j] = (u32)t;
+        c = t >> 32;
+    }
+}
+// t = x f + y g as 13-limb two's complement (x, y < 2^384 unsigned, |f|, |g| <= 2^30)
+DI void fpi_lin(u32 (&t)[13], const u32 (&x)[12], const u32 (&y)[12], int f, int g) {
+    u32 t2[13];
+    fpi_mul32(t, x, (u32)(f < 0 ? -f : f));
+    fpi_cneg13(t, f < 0);
+    fpi_mul32(t2, y, (u32)(g < 0 ? -g : g));
+    fpi_cneg13(t2, g < 0);
+    fpi_add13(t, t2);
+}
+// r = |x f + y g| >> 30; returns true when x f + y g < 0
+DI bool fpi_lin_shift(u32 (&r)[12], const u32 (&x)[12], const u32 (&y)[12], int f, int g) {
+    u32 t[13];
+    fpi_lin(t, x, y, f, g);
+#pragma unroll
+    for (int j = 0; j < 12; j++) t[j] = (t[j] >> 30) | (t[j + 1] << 2);
+    t[12] = (u32)((int)t[12] >> 30);
+    const bool neg = (int)t[12] < 0;
+    fpi_cneg13(t, neg);
+#pragma unroll
+    for (int j = 0; j < 12; j++) r[j] = t[j];
+    return neg;
+}
+// r = (x f + y g) 2^-32 mod p in [0, p) (x, y in [0, p))
+DI void fpi_mont_lin(u32 (&r)[12], const u32 (&x)[12], const u32 (&y)[12], int f, int g) {
+    u32 t[13], qp[13];
+    fpi_lin(t, x, y, f, g);
+    const u32 q = t[0] * LCB_P_INV;                   // t + q p = 0 mod 2^32
+    u32 pl[12];
+#pragma unroll
+    for (int j = 0; j < 12; j++) pl[j] = LCB_P[j];
+    fpi_mul32(qp, pl, q);
+    fpi_add13(t, qp);                                 // |t| < 2^33 p < 2^415: no overflow of 13 signed limbs
+    // t / 2^32 (t[0] == 0): limbs 1..12, sign in t[12]; the value lies in (-p/2, 3p/2)
+    u32 s[12], d[12];
+    const bool neg = (int)t[12] < 0;
+#pragma unroll
+    for (int j = 0; j < 12; j++) s[j] = t[j + 1];     // two's complement low 384 bits of t / 2^32
+    // neg: s + p (the true value + p is in [0, p)); else s - p if s >= p
+    u64 c = 0;
+    u32 br = 0;
+#pragma unroll
+    for (int j = 0; j < 12; j++) {
+        if (neg) {
+            u64 x2 = (u64)s[j] + LCB_P[j] + c;
+            d[j] = (u32)x2;
+            c = x2 >> 32;
+        } else {
+            u64 x2 = (u64)s[j] - LCB_P[j] - br;
+            d[j] = (u32)x2;
+            br = (u32)(x2 >> 32) & 1;
+        }
+    }
+    const bool take = neg || !br;                      // s + p, or s - p when s >= p
+#pragma unroll
+    for (int j = 0; j < 12; j++) r[j] = take ? d[j] : s[j];
+}
+// the top 32 bits of x below bit position s + 32 (x < 2^384, 30 <= s <= 352), i.e. bits s .. s + 31
+DI u32 fpi_bits32(const u32 (&x)[12], u32 li, u32 o) {
+    u32 lo = 0, hi = 0;
+#pragma unroll
+    for (int j = 0; j < 12; j++) {
+        lo = (u32)j == li ? x[j] : lo;
+        hi = (u32)j == li + 1 ? x[j] : hi;
+    }
+    return o ? (lo >> o) | (hi << (32 - o)) : lo;
+}
+DN void fp_inv_gcd(fp &r, const fp &x) {
+    u32 a[12], b[12], u[12], v[12];
+#pragma unroll
+    for (int j = 0; j < 12; j++) {
+        a[j] = x.v[j];
+        b[j] = LCB_P[j];
+        u[j] = j == 0 ? 1u : 0u;
+        v[j] = 0u;
+    }
+#pragma unroll 1
+    for (int it = 0; it < 26; it++) {
+        // approximations: the low 30 bits and bits n - 32 .. n - 1 of a, b, n = max(bit length of a | b, 62)
+        u32 hiw = 0, top = 0;
+#pragma unroll
+        for (int j = 0; j < 12; j++) {
+            const u32 w = a[j] | b[j];
+            hiw = w ? (u32)j : hiw;
+            top = w ? w : top;
+        }
+        u32 n = 32 * hiw + (32 - (u32)__clz(top | 1));
+        n = n < 62 ? 62 : n;
+        const u32 s = n - 32, li = s >> 5, o = s & 31;
+        u64 ab = ((u64)fpi_bits32(a, li, o) << 30) | (a[0] & 0x3fffffffu);
+        u64 bb = ((u64)fpi_bits32(b, li, o) << 30) | (b[0] & 0x3fffffffu);
+        int f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+#pragma unroll 2
+        for (int i = 0; i < 30; i++) {
+            const bool odd = ab & 1;
+            const bool sw = odd && ab < bb;
+            const u64 ta = sw ? bb : ab, tb = sw ? ab : bb;
+            const int tf0 = sw ? f1 : f0, tg0 = sw ? g1 : g0, tf1 = sw ? f0 : f1, tg1 = sw ? g0 : g1;
+            ab = (odd ? ta - tb : ta) >> 1;
+            bb = tb;
+            f0 = odd ? tf0 - tf1 : tf0;
+            g0 = odd ? tg0 - tg1 : tg0;
+            f1 = tf1 * 2;
+            g1 = tg1 * 2;
+        }
+        u32 na[12], nb[12], nu[12], nv[12];
+        if (fpi_lin_shift(na, a, b, f0, g0)) { f0 = -f0; g0 = -g0; }
+        if (fpi_lin_shift(nb, a, b, f1, g1)) { f1 = -f1; g1 = -g1; }
+        fpi_mont_lin(nu, u, v, f0, g0);
+        fpi_mont_lin(nv, u, v, f1, g1);
+#pragma unroll
+        for (int j = 0; j < 12; j++) {
+            a[j] = na[j];
+            b[j] = nb[j];
+            u[j] = nu[j];
+            v[j] = nv[j];
+        }
+    }
+    fp vv, c;
+#pragma unroll
+    for (int j = 0; j < 12; j++) vv.v[j] = v[j];
+    fp_load_const(c, LCB_BINV_C);
+    fp_mul(r, vv, c);
+    if (fp_is_zero(x)) r = fp_zero();
+}
 // mcl Fp::squareRoot for p = 3 mod 4: y = a^((p+1)/4), valid iff y^2 == a
 DI bool fp_sqrt(fp &r, const fp &a) {
     fp y, t;
@@ -270,6 +435,16 @@ DI void fp2_inv(fp2 &r, const fp2 &x) {
     fp n;
     fp2_norm(n, x);
     fp_inv(n, n);
+    fp2 t;
+    fp2_mul_fp(t, x, n);
+    r.a = t.a;
+    fp_neg(r.b, t.b);
+}
+// the same with the binary-GCD Fp inversion (fp_inv_gcd: its call is cheap where few values are live around it)
+DI void fp2_inv_g(fp2 &r, const fp2 &x) {
+    fp n;
+    fp2_norm(n, x);
+    fp_inv_gcd(n, n);
     fp2 t;
     fp2_mul_fp(t, x, n);
     r.a = t.a;
@@ -437,7 +612,7 @@ DI void fp6_inv(fp6 &r, const fp6 &a) {
     fp2_mul_xi(t, t);
     fp2_mul(s, a.c0, c0);
     fp2_add(t, t, s);
-    fp2_inv(t, t);
+    fp2_inv_g(t, t);     // (reached only from fp12_inv_n / the single-op switch: calls)
     fp2_mul(r.c0, c0, t);
     fp2_mul(r.c1, c1, t);
     fp2_mul(r.c2, c2, t);
@@ -715,4 +890,5 @@ DN void fp12_frob1_n(fp12 &r, const fp12 &a) { fp12 t; fp12_frob1(t, a); r = t; 
 DN void fp12_frob2_n(fp12 &r, const fp12 &a) { fp12 t; fp12_frob2(t, a); r = t; }
 DN void fp12_frob3_n(fp12 &r, const fp12 &a) { fp12 t; fp12_frob3(t, a); r = t; }
 DN void fp2_inv_n(fp2 &r, const fp2 &a) { fp2 t; fp2_inv(t, a); r = t; }
+DN void fp2_inv_gn(fp2 &r, const fp2 &a) { fp2 t; fp2_inv_g(t, a); r = t; }   // line-set normalisation
 DN bool fp2_sqrt_n(fp2 &r, const fp2 &a) { fp2 t; bool ok = fp2_sqrt(t, a); r = t; return ok; }

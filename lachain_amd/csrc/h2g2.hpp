@@ -112,7 +112,7 @@ DI bool g2_calc_bn(g2 &P, const fp2 &t) {
     fp2_add(w, w, b2);
     fp_add(w.a, w.a, one);
     if (fp2_is_zero(w)) return false;
-    fp2_inv(w, w);
+    fp2_inv_g(w, w);
     fp2_mul_fp(w, w, c1);
     fp2_mul(w, w, t);
     for (int i = 0; i < 3; i++) {
@@ -125,7 +125,7 @@ DI bool g2_calc_bn(g2 &P, const fp2 &t) {
             fp_sub(x.a, x.a, one);
         } else {
             fp2_sqr(x, w);
-            fp2_inv(x, x);
+            fp2_inv_g(x, x);
             fp_add(x.a, x.a, one);
         }
         fp2_sqr(tmp, x);

@@ -160,7 +160,7 @@ extern "C" __global__ void __launch_bounds__(64, 1) k_lineset_coop(u32 *lines, u
     const bool g2m = Q.inf || lineset_in_g2(T, Q);
     const bool ok = Q.inf || !fp2_is_zero(acc);
     fp2 inv;
-    fp2_inv_n(inv, acc);                                 // (A_0 ... A_67)^-1 (0 when some A_k = 0: not stored)
+    fp2_inv_gn(inv, acc);                                // (A_0 ... A_67)^-1 (0 when some A_k = 0: not stored)
     __syncthreads();                                     // the group's line stores are visible to its five lanes
     // backward pass: round j = 67 .. -1 gives a_j (lane 0) and the new inv (lane 1), lanes 2 and 3 normalise line j + 1
     const bool nst = st && ok;

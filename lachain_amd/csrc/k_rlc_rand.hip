@@ -39,7 +39,7 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_key_tables(const g1a_st *keys, u32 n
     ktab_ok[t] = ok;
     if (!ok) return;
     fp inv, beta;
-    fp_inv(inv, run);                                  // 1 / (z_d0 ... z_d1)
+    fp_inv_gcd(inv, run);                              // 1 / (z_d0 ... z_d1)
     fp_load_const(beta, LCB_G1_BETA);
 #pragma unroll 1
     for (u32 d = d1; d >= d0; d--) {

@@ -191,7 +191,7 @@ DN u32 lineset_compute(u32 *dst, const g2a &Q) {
     dst[LCB_LS_FLAG] = ok;
     if (!ok) return g2m;
     fp2 inv;
-    fp2_inv_n(inv, acc);                               // (A_0 ... A_67)^-1
+    fp2_inv_gn(inv, acc);                              // (A_0 ... A_67)^-1
     for (k = LCB_NLINES - 1; k >= 0; k--) {
         fp2 ai, a, b, c;
         if (k > 0) {

@@ -23,7 +23,7 @@ BUDGET = {
     "k_dkg_exact_terms": (0, 408),
     "k_dkg_horner": (0, 896),
     "k_dkg_rows": (0, 312),
-    "k_final_exp_check": (0, 4288),
+    "k_final_exp_check": (0, 3864),
     "k_g1_decompress": (0, 800),
     "k_g1_jac_compress": (0, 704),
     "k_g1_jac_reduce_block": (0, 456),
@@ -34,18 +34,18 @@ BUDGET = {
     "k_g1_sum": (0, 752),
     "k_g1_to_affine": (0, 704),
     "k_g2_decompress": (0, 992),
-    "k_g2_hash": (0, 3336),
-    "k_mcl_g2_hash": (0, 3336),               # mclBnG2_hashAndMapTo: the same one-lane hash as k_g2_hash
+    "k_g2_hash": (0, 3352),
+    "k_mcl_g2_hash": (0, 3352),               # mclBnG2_hashAndMapTo: the same one-lane hash as k_g2_hash
     "k_g2_mul": (206, 10624),
     "k_g2_mul_lanes": (1300, 10288),
     "k_g2_mul2_lanes": (4530, 22672),         # two GLS tables (31 entries) per lane: the assembly's paired lanes
     "k_g2_sum": (204, 1008),
-    "k_lineset_fill": (0, 1824),
-    "k_lineset_coop": (86, 800),              # five-lane line sets (latency path): T, Q, acc and five products live
+    "k_lineset_fill": (0, 1256),
+    "k_lineset_coop": (86, 280),              # five-lane line sets (latency path): T, Q, acc and five products live
     "k_msm_bucket_reduce": (0, 744),          # + the prefetched next bucket
     "k_msm_horner": (0, 168),
     "k_msm_bucket_fix": (0, 168),
-    "k_op": (3038, 8484),
+    "k_op": (3098, 8484),
     "k_ptmul_g2": (32, 68),                   # mcl G2 multiplication latency kernel: four ladder lanes share each op                     # mcl single-element surface: every operation in one kernel
     "k_rlc_key_tables": (12, 768),            # k_rlc_rand.hip: spills to scratch, not AGPRs (<= 256 registers)
     "k_rlc_miller_fallback": (0, 2376),
@@ -53,9 +53,9 @@ BUDGET = {
     "k_tpke_rlc_search2a": (92, 2264),         # level-2 searches: three Fp12 values per lane, one lane per group
     "k_tpke_rlc_search2b": (133, 4088),
     "k_secp_scalars": (0, 528),
-    "k_tpke_ct_prepare": (0, 3736),
+    "k_tpke_ct_prepare": (0, 3752),
     "k_tpke_encrypt1": (0, 6432),
-    "k_tpke_encrypt2": (0, 3912),
+    "k_tpke_encrypt2": (0, 3928),
     "k_tpke_miller": (348, 2616),
     "k_tpke_partial_decrypt": (972, 7652),
     "k_tpke_rlc_miller": (360, 2616),
@@ -63,12 +63,12 @@ BUDGET = {
     "k_tpke_rlc_sum": (0, 1328),
     "k_tpke_rlc_wsum": (0, 576),
     "k_ts_miller": (1248, 3292),
-    "k_ts_msg_prepare": (0, 3624),
+    "k_ts_msg_prepare": (0, 3640),
     "k_ts_rlc_miller": (0, 2524),
     "k_ts_rlc_points": (677, 3360),           # k_rlc_rand.hip: 256 registers, two waves per SIMD (spills to scratch)
     "k_ts_rlc_sum": (0, 2136),
     "k_ts_rlc_wsum": (12, 992),
-    "k_ts_sign": (0, 3912),
+    "k_ts_sign": (0, 3928),
 }
 ZERO_SPILL = ["k_coop_tpke_miller", "k_coop_final_exp_check", "k_msm_bucket_acc", "k_secp_verify",
               "k_rlc_census_stats", "k_rlc_suspect_split", "k_rlc_resolve", "k_tpke_rlc_sum", "k_ts_rlc_miller"]
