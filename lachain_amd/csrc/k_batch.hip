@@ -356,6 +356,20 @@ DN void gt_pow_small(fp12 &r, const fp12 &a, u32 e) {
     }
     r = t;
 }
+// x <- x_0 x_1 ... x_j over lane j's half-wave (inclusive product scan; Hillis-Steele, five shuffle rounds).  Every
+// lane of the wave must be active.
+DN void gt_half_scan(fp12 &x) {
+    const u32 j = threadIdx.x & 31;
+#pragma unroll 1
+    for (u32 off = 1; off < 32; off <<= 1) {
+        fp12 y;
+        u32 *yw = (u32 *)&y;
+        const u32 *xw = (const u32 *)&x;
+#pragma unroll
+        for (int q = 0; q < 144; q++) yw[q] = (u32)__shfl_up((int)xw[q], off, 32);
+        if (j >= off) fp12_mul_n(x, x, y);
+    }
+}
 DI u32 fp12_fingerprint(const fp12 &a) {
     const u32 *w = (const u32 *)&a;
     u32 h = 0;
@@ -370,7 +384,7 @@ DI u32 half_ballot(bool p) {
 // Level 2 of TPKE: locate up to TWO bad shares per failed group.  With e_i = s_i log g_i (nonzero exactly for the bad
 // shares) the three group values are gamma_0 (level 1) ~ sum e_i, gamma_c ~ sum e_i c_i and gamma_t ~ sum e_i t_i, so
 // gamma_2 = gamma_t^2 / gamma_c ~ sum e_i c_i^2 (c^2 = 2t - c).
-//   one error at j:      gamma_c = gamma_0^(c_j)  (k_tpke_rlc_search2a: one lane per group, c = 1..len as k_rlc_search);
+//   one error at j:      gamma_c = gamma_0^(c_j)  (k_tpke_rlc_search2a: four lanes per group, c = 1..len);
 //   two errors at j, k:  for lane j of the group's half-wave (k_tpke_rlc_search2b, only the groups 2a left open),
 //                        D_j = gamma_c / gamma_0^(c_j) ~ e_k (c_k - c_j) and E_j = gamma_2 / gamma_c^(c_j) ~
 //                        e_k c_k (c_k - c_j), so E_j = D_j^(c_k): exactly two lanes whose searches name each other
@@ -381,20 +395,31 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_search2a(const uint4 *search, u
                                                          const u32 *gamma12, uint8_t *accept, u32 *open,
                                                          u32 *open_count) {
     LCB_LATENCY_PRIO();
-    u32 g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= ns) return;
-    const uint4 d = search[g];
-    fp12 gm, gc, acc;
-    fp12_load_row(gm, gamma0 + (size_t)g * 144);
-    fp12_load_row(gc, gamma12 + (size_t)g * 144);
-    acc = gm;
-    u32 found = 0;
-    for (u32 c = 1; c <= d.y; c++) {
-        if (fp12_words_eq(acc, gc)) { found = c; break; }
-        if (c < d.y) fp12_mul_n(acc, acc, gm);
+    // four lanes per group (a latency-bound launch of ~1 % of the groups): lane r tries c = r + 1, r + 5, ... from
+    // gamma_0^(r+1) in steps of gamma_0^4, so the serial chain is ~len/4 products instead of len.  The smallest c that
+    // matches wins, as in the one-lane scan.  No lane returns early: the shuffles below need the whole wave.
+    const u32 t = blockIdx.x * blockDim.x + threadIdx.x, g = t >> 2, r = t & 3;
+    const bool live = g < ns;
+    const uint4 d = live ? search[g] : make_uint4(0, 0, 0, 0);
+    u32 found = 0xffffffffu;
+    if (live) {
+        fp12 gm, gc, acc, st;
+        fp12_load_row(gm, gamma0 + (size_t)g * 144);
+        fp12_load_row(gc, gamma12 + (size_t)g * 144);
+        gt_pow_small(acc, gm, r + 1);
+        fp12_cyc_sqr_n(st, gm);
+        fp12_cyc_sqr_n(st, st);
+        for (u32 c = r + 1; c <= d.y; c += 4) {
+            if (fp12_words_eq(acc, gc)) { found = c; break; }
+            if (c + 4 <= d.y) fp12_mul_n(acc, acc, st);
+        }
     }
-    if (found) accept[d.x + found - 1] = 0;
-    else open[atomicAdd(open_count, 1u)] = g;
+    found = min(found, (u32)__shfl_xor((int)found, 1));
+    found = min(found, (u32)__shfl_xor((int)found, 2));
+    if (live && r == 0) {
+        if (found != 0xffffffffu) accept[d.x + found - 1] = 0;
+        else open[atomicAdd(open_count, 1u)] = g;
+    }
 }
 extern "C" __global__ void __launch_bounds__(64) k_tpke_rlc_search2b(const uint4 *search, u32 ns, const u32 *gamma0,
                                                                     const u32 *gamma12, const u32 *open,
@@ -410,19 +435,24 @@ extern "C" __global__ void __launch_bounds__(64) k_tpke_rlc_search2b(const uint4
     const bool cand = live && j < d.y && accept[d.x + j] && !key_suspect(susp, key_idx[d.x + j], n_keys);
     const u32 cj = j + 1;
     fp12 a, b, D;
-    fp12_load_row(a, gamma0 + (size_t)g * 144);
-    gt_pow_small(b, a, cj);
+    // gamma_0^(c_j) and gamma_c^(c_j + 1) for every lane j of the half-wave from product scans over its 32 lanes
+    // (5 products each) instead of one square-and-multiply per lane
+    fp12_load_row(b, gamma0 + (size_t)g * 144);
+    gt_half_scan(b);                                       // gamma_0^(c_j)
     fp12_conj(b, b);
     fp12_load_row(a, gamma12 + (size_t)g * 144);           // gamma_c
     fp12_mul_n(D, a, b);                                   // D_j = gamma_c / gamma_0^(c_j)
-    gt_pow_small(b, a, cj + 1);                            // gamma_c^(c_j + 1)
+    gt_half_scan(a);                                       // gamma_c^(c_j)
+    fp12_load_row(b, gamma12 + (size_t)g * 144);
+    fp12_mul_n(b, a, b);                                   // gamma_c^(c_j + 1)
     fp12_conj(b, b);
     fp12_load_row(a, gamma12 + ((size_t)ns + g) * 144);    // gamma_t
     fp12_cyc_sqr_n(a, a);
     fp12_mul_n(a, a, b);                                   // E_j = gamma_t^2 / gamma_c^(c_j + 1) = gamma_2 / gamma_c^(c_j)
     // E_j = D_j^c for some c in [1, len] (len <= 32): baby-step giant-step with m = 6 — 32-bit fingerprints of the
     // baby values D^k (k = 1..6), giant steps Y_i = E D^(-6 i) (D is unitary: D^-6 = conj(D^6)), a fingerprint match
-    // confirmed by the full comparison E == D^c: 10 products instead of up to len
+    // Y_i ~ D^(k+1) confirmed by the full comparison Y_i == D^(k+1) (<=> E == D^c, c = 6 i + k + 1): 10 products
+    // instead of up to len
     u32 found = 0;
     if (cand) {
         u32 fpb[6];
@@ -434,16 +464,16 @@ extern "C" __global__ void __launch_bounds__(64) k_tpke_rlc_search2b(const uint4
             fpb[k] = fp12_fingerprint(b);
         }
         fp12_conj(b, b);                                   // D^-6
-        fp12 E = a;                                        // Y_0
         for (int i = 0; i < 6 && !found; i++) {
             const u32 h = fp12_fingerprint(a);
-#pragma unroll
+#pragma unroll 1
             for (int k = 0; k < 6; k++) {
                 const u32 c = 6 * i + k + 1;
                 if (!found && h == fpb[k] && c <= d.y && c != cj) {
-                    fp12 chk;
-                    gt_pow_small(chk, D, c);
-                    if (fp12_words_eq(chk, E)) found = c;
+                    fp12 chk = D;
+#pragma unroll 1
+                    for (int q = 0; q < k; q++) fp12_mul_n(chk, chk, D);
+                    if (fp12_words_eq(chk, a)) found = c;
                 }
             }
             if (i < 5) fp12_mul_n(a, a, b);
@@ -565,7 +595,7 @@ extern "C" void lcbk_tpke_rlc_search2(hipStream_t s, const void *search, u32 ns,
                                       uint8_t *accept, void *next, u32 *next_count, const u32 *key_idx, u32 n_keys,
                                       const u32 *susp, u32 *open, u32 *open_count) {
     (void)hipMemsetAsync(open_count, 0, 4, s);
-    dim3 grid((ns + LCB_BLOCK - 1) / LCB_BLOCK);
+    dim3 grid((4 * ns + LCB_BLOCK - 1) / LCB_BLOCK);
     LCB_LAUNCH(k_tpke_rlc_search2a, (const uint4 *)search, ns, gamma0, gamma12, accept, open, open_count);
     hipLaunchKernelGGL(k_tpke_rlc_search2b, dim3((ns + 1) / 2), dim3(64), 0, s, (const uint4 *)search, ns, gamma0,
                        gamma12, open, open_count, accept, (uint4 *)next, next_count, key_idx, n_keys, susp);

@@ -196,10 +196,10 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_gr
     }
     if (work) {
         g1a_st o;
-        g1_to_st(o, su[0], side != 0);
+        g1_to_st_gcd(o, su[0], side != 0);
         gpts[2 * (size_t)g + side] = o;
         if (!four) {
-            g1_to_st(o, su[1], true);
+            g1_to_st_gcd(o, su[1], true);
             gpts[2 * (size_t)g + 1] = o;
         }
     }
@@ -232,7 +232,7 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum2(const uint4 *sdesc, u32 n
         if (which) grp_add(va, va, wa);
     }
     g1a_st o;
-    g1_to_st(o, which ? va : wa, side != 0);
+    g1_to_st_gcd(o, which ? va : wa, side != 0);
     gpts[2 * ((size_t)(which ? ns : 0) + g) + side] = o;
 }
 

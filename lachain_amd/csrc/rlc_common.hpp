@@ -153,6 +153,21 @@ DI void g1_to_st(g1a_st &o, const g1 &p, bool neg) {
     if (neg && !a.inf) fp_neg(o.y, a.y);
     else o.y = a.y;
 }
+// the same record with the binary-GCD inversion (field.hpp fp_inv_gcd): the group sums' chains are a few additions,
+// so the inversion is most of their work
+DI void g1_to_st_gcd(g1a_st &o, const g1 &p, bool neg) {
+    o.ok = 1; o.pad[0] = o.pad[1] = 0;
+    if (jac_is_inf(p)) { o.inf = 1; o.x = fp_zero(); o.y = fp_zero(); return; }
+    fp zi, zi2, y;
+    fp_inv_gcd(zi, p.z);
+    fp_sqr(zi2, zi);
+    fp_mul(o.x, p.x, zi2);
+    fp_mul(zi2, zi2, zi);
+    fp_mul(y, p.y, zi2);
+    o.inf = 0;
+    if (neg) fp_neg(o.y, y);
+    else o.y = y;
+}
 DI void g2_to_st(g2a_st &o, const g2 &p) {
     g2a a;
     jac_to_aff(a, p);

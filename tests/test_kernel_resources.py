@@ -50,7 +50,7 @@ BUDGET = {
     "k_rlc_key_tables": (12, 768),            # k_rlc_rand.hip: spills to scratch, not AGPRs (<= 256 registers)
     "k_rlc_miller_fallback": (0, 2376),
     "k_rlc_search": (93, 2264),
-    "k_tpke_rlc_search2a": (92, 2264),         # level-2 searches: three Fp12 values per lane, one lane per group
+    "k_tpke_rlc_search2a": (97, 3448),         # level-2 searches: four Fp12 values per lane, four lanes per group
     "k_tpke_rlc_search2b": (133, 4088),
     "k_secp_scalars": (0, 528),
     "k_tpke_ct_prepare": (0, 3752),
