@@ -318,14 +318,14 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_search(const uint4 *search, u32 o, u
 }
 
 // the final-exponentiation outputs of checks [o, o + m) (park stride m) -> rows o.. of dst (576 B each)
-extern "C" __global__ void LCB_BOUNDS k_rlc_park_copy(const u32 *park, u32 o, u32 m, u32 *dst) {
+extern "C" __global__ void LCB_BOUNDS k_rlc_park_copy(const u32 *park, u32 o, u32 m, u32 *dst, const u32 *map) {
     LCB_LATENCY_PRIO();
     u32 gl = blockIdx.x * blockDim.x + threadIdx.x;
     if (gl >= m) return;
     fp12 f;
     fp12_load_soa(f, park, m, gl);
     const u32 *w = (const u32 *)&f;
-    uint4 *d = (uint4 *)(dst + (size_t)(o + gl) * 144);
+    uint4 *d = (uint4 *)(dst + (size_t)(map ? map[o + gl] : o + gl) * 144);   // (map: row of check o + gl)
 #pragma unroll
     for (int q = 0; q < 36; q++) d[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
@@ -480,7 +480,7 @@ extern "C" __global__ void __launch_bounds__(64) k_tpke_rlc_search2b(const uint4
         }
     }
     const u32 m2 = half_ballot(found != 0);
-    const u32 m3 = half_ballot(found != 0 && !((m2 >> (found - 1)) & 1u));
+    const u32 m3 = half_ballot(found != 0 && !((m2 >> ((found - 1) & 31u)) & 1u));
     if (__popc(m2) == 2 && !m3) {
         if (found) accept[d.x + j] = 0;
     } else if (live && j == 0) {
@@ -587,17 +587,22 @@ extern "C" void lcbk_rlc_search(dim3 grid, hipStream_t s, const void *search, u3
     LCB_LAUNCH(k_rlc_search, (const uint4 *)search, o, m, gamma, park, accept, (uint4 *)next, next_count, key_idx,
                n_keys, susp);
 }
-extern "C" void lcbk_rlc_park_copy(hipStream_t s, const u32 *park, u32 o, u32 m, u32 *dst) {
+extern "C" void lcbk_rlc_park_copy(hipStream_t s, const u32 *park, u32 o, u32 m, u32 *dst, const u32 *map) {
     dim3 grid((m + LCB_BLOCK - 1) / LCB_BLOCK);
-    LCB_LAUNCH(k_rlc_park_copy, park, o, m, dst);
+    LCB_LAUNCH(k_rlc_park_copy, park, o, m, dst, map);
 }
-extern "C" void lcbk_tpke_rlc_search2(hipStream_t s, const void *search, u32 ns, const u32 *gamma0, const u32 *gamma12,
-                                      uint8_t *accept, void *next, u32 *next_count, const u32 *key_idx, u32 n_keys,
-                                      const u32 *susp, u32 *open, u32 *open_count) {
+extern "C" void lcbk_tpke_rlc_search2a(hipStream_t s, const void *search, u32 ns, const u32 *gamma0,
+                                       const u32 *gamma12, uint8_t *accept, u32 *open, u32 *open_count) {
     (void)hipMemsetAsync(open_count, 0, 4, s);
     dim3 grid((4 * ns + LCB_BLOCK - 1) / LCB_BLOCK);
     LCB_LAUNCH(k_tpke_rlc_search2a, (const uint4 *)search, ns, gamma0, gamma12, accept, open, open_count);
-    hipLaunchKernelGGL(k_tpke_rlc_search2b, dim3((ns + 1) / 2), dim3(64), 0, s, (const uint4 *)search, ns, gamma0,
+}
+// n_open = *open_count (read by the host after search2a); gamma12 + 144 (ns + g) holds gamma_t of the open group g
+extern "C" void lcbk_tpke_rlc_search2b(hipStream_t s, const void *search, u32 ns, u32 n_open, const u32 *gamma0,
+                                       const u32 *gamma12, const u32 *open, const u32 *open_count, uint8_t *accept,
+                                       void *next, u32 *next_count, const u32 *key_idx, u32 n_keys, const u32 *susp) {
+    if (!n_open) return;
+    hipLaunchKernelGGL(k_tpke_rlc_search2b, dim3((n_open + 1) / 2), dim3(64), 0, s, (const uint4 *)search, ns, gamma0,
                        gamma12, open, open_count, accept, (uint4 *)next, next_count, key_idx, n_keys, susp);
 }
 extern "C" void lcbk_rlc_census_desc(hipStream_t s, const u32 *grp_idx, const u32 *key_idx, u32 m, u32 n_grp,

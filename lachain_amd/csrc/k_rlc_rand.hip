@@ -205,19 +205,24 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_sum(const uint4 *desc, u32 n_gr
     }
 }
 
-// Level 2 of TPKE (two-error location, see k_tpke_rlc_search2): the weighted sums of the failed level-1 groups listed
-// in sdesc, formed from the shares' randomised records: four lanes per group ((U, Y) side x (w, v) output), last share to first,
-// s = suffix sum, w = sum of the s (weights c_j = j + 1), v = sum of the w (weights t_j = c_j (c_j + 1) / 2).  Shares of
-// suspect keys keep their positions and add nothing.  gpts[2g + side] = w, gpts[2 (ns + g) + side] = v (Y side
-// negated), so checks g and ns + g give gamma_c = prod g_i^(c_i s_i) and gamma_t = prod g_i^(t_i s_i).
-extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum2(const uint4 *sdesc, u32 ns, const u32 *rU, const u32 *rY, u32 n,
-                                                      const u32 *dec_idx, u32 n_keys, const u32 *susp, g1a_st *gpts) {
+// Level 2 of TPKE (two-error location, see k_tpke_rlc_search2a/2b): the weighted sums of failed level-1 groups,
+// formed from the shares' randomised records, last share to first: s = suffix sum, w = sum of the s (weights c_j =
+// j + 1), v = sum of the w (weights t_j = c_j (c_j + 1) / 2).  Shares of suspect keys keep their positions and add
+// nothing.  Two lanes per group ((U, Y) side), the Y side negated, so a check gives gamma_c = prod g_i^(c_i s_i) (w) or
+// gamma_t = prod g_i^(t_i s_i) (v):
+//   open == nullptr: the w sums of the ns groups of sdesc -> gpts[2 g + side]
+//   open != nullptr: the v sums of the ns groups open[k] the one-error search left open -> gpts[2 k + side], and
+//                    their descriptors -> sdesc_out[k] (gamma_t is needed for those alone)
+extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum2(const uint4 *sdesc, u32 ns, const u32 *open, const u32 *rU,
+                                                      const u32 *rY, u32 n, const u32 *dec_idx, u32 n_keys,
+                                                      const u32 *susp, g1a_st *gpts, uint4 *sdesc_out) {
     LCB_LATENCY_PRIO();
-    // four lanes per group: (side, which) — each lane one output record, so one inversion (to affine) per lane
-    u32 t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= 4 * ns) return;
-    const u32 g = t >> 2, side = t & 1, which = (t >> 1) & 1;
+    const u32 t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 2 * ns) return;
+    const u32 k = t >> 1, side = t & 1, g = open ? open[k] : k;
+    const bool which = open != nullptr;
     const uint4 d = sdesc[g];
+    if (which && !side) sdesc_out[k] = d;
     const u32 *rec = side ? rY : rU;
     g1 sa, wa, va, p;
     jac_set_inf(sa);
@@ -233,7 +238,7 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum2(const uint4 *sdesc, u32 n
     }
     g1a_st o;
     g1_to_st_gcd(o, which ? va : wa, side != 0);
-    gpts[2 * ((size_t)(which ? ns : 0) + g) + side] = o;
+    gpts[2 * (size_t)k + side] = o;
 }
 
 // ---------------------------------------------------------------- threshold signatures: per-share randomisation
@@ -330,8 +335,11 @@ extern "C" void lcbk_tpke_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u3
     LCB_LAUNCH(k_tpke_rlc_sum, (const uint4 *)desc, n_groups, lanes, ct_ok, ct_g2, (const g1a_st *)keys, n_keys,
                dec_idx, ui, rU, rY, n, (g1a_st *)gpts, accept, gexact, wsum, susp, cval);
 }
-extern "C" void lcbk_tpke_rlc_wsum2(hipStream_t s, const void *sdesc, u32 ns, const u32 *rU, const u32 *rY, u32 n,
-                                    const u32 *dec_idx, u32 n_keys, const u32 *susp, void *gpts) {
-    dim3 grid((4 * (size_t)ns + LCB_BLOCK - 1) / LCB_BLOCK);
-    LCB_LAUNCH(k_tpke_rlc_wsum2, (const uint4 *)sdesc, ns, rU, rY, n, dec_idx, n_keys, susp, (g1a_st *)gpts);
+extern "C" void lcbk_tpke_rlc_wsum2(hipStream_t s, const void *sdesc, u32 ns, const u32 *open, const u32 *rU,
+                                    const u32 *rY, u32 n, const u32 *dec_idx, u32 n_keys, const u32 *susp, void *gpts,
+                                    void *sdesc_out) {
+    if (!ns) return;
+    dim3 grid((2 * (size_t)ns + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_tpke_rlc_wsum2, (const uint4 *)sdesc, ns, open, rU, rY, n, dec_idx, n_keys, susp, (g1a_st *)gpts,
+               (uint4 *)sdesc_out);
 }

@@ -84,9 +84,10 @@ extern "C" void lcbk_ts_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 
 extern "C" void lcbk_ts_rlc_wsum(dim3 grid, hipStream_t s, const void *sdesc, u32 n_s, const u32 *wsum, u32 n_l1, void *gpts);
 extern "C" void lcbk_ts_rlc_miller(dim3 grid, hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups, u32 *f_soa, uint8_t *gacc);
 extern "C" void lcbk_rlc_resolve(dim3 grid, hipStream_t s, const void *desc, u32 o, u32 m, const uint8_t *gacc, const uint8_t *gexact, const u32 *park, u32 first, uint8_t *accept, void *next, u32 *next_count, void *search, u32 *search_count, u32 *gamma, const u32 *key_idx, u32 n_keys, const u32 *susp);
-extern "C" void lcbk_tpke_rlc_wsum2(hipStream_t s, const void *sdesc, u32 ns, const u32 *rU, const u32 *rY, u32 n, const u32 *dec_idx, u32 n_keys, const u32 *susp, void *gpts);
-extern "C" void lcbk_rlc_park_copy(hipStream_t s, const u32 *park, u32 o, u32 m, u32 *dst);
-extern "C" void lcbk_tpke_rlc_search2(hipStream_t s, const void *search, u32 ns, const u32 *gamma0, const u32 *gamma12, uint8_t *accept, void *next, u32 *next_count, const u32 *key_idx, u32 n_keys, const u32 *susp, u32 *open, u32 *open_count);
+extern "C" void lcbk_tpke_rlc_wsum2(hipStream_t s, const void *sdesc, u32 ns, const u32 *open, const u32 *rU, const u32 *rY, u32 n, const u32 *dec_idx, u32 n_keys, const u32 *susp, void *gpts, void *sdesc_out);
+extern "C" void lcbk_rlc_park_copy(hipStream_t s, const u32 *park, u32 o, u32 m, u32 *dst, const u32 *map);
+extern "C" void lcbk_tpke_rlc_search2a(hipStream_t s, const void *search, u32 ns, const u32 *gamma0, const u32 *gamma12, uint8_t *accept, u32 *open, u32 *open_count);
+extern "C" void lcbk_tpke_rlc_search2b(hipStream_t s, const void *search, u32 ns, u32 n_open, const u32 *gamma0, const u32 *gamma12, const u32 *open, const u32 *open_count, uint8_t *accept, void *next, u32 *next_count, const u32 *key_idx, u32 n_keys, const u32 *susp);
 extern "C" void lcbk_rlc_search(dim3 grid, hipStream_t s, const void *search, u32 o, u32 m, const u32 *gamma, const u32 *park, uint8_t *accept, void *next, u32 *next_count, const u32 *key_idx, u32 n_keys, const u32 *susp);
 extern "C" void lcbk_rlc_census_desc(hipStream_t s, const u32 *grp_idx, const u32 *key_idx, u32 m, u32 n_grp, u32 n_keys, void *desc, uint8_t *accept);
 extern "C" void lcbk_rlc_census_stats(hipStream_t s, const u32 *key_idx, u32 m, u32 n_keys, const uint8_t *cval, const uint8_t *accept, u32 *susp, u32 *count);

@@ -1117,7 +1117,7 @@ void rlc_sum_enqueue(const RlcKindInfo &K, RlcWs &w, const uint8_t *desc, u32 gr
 enum RlcStage { RLC_RESOLVE = 0, RLC_SEARCH = 1, RLC_COPY = 2 };   // after a chunk's checks: resolve / search / copy out
 void rlc_checks(lcb_ctx *c, const RlcKindInfo &K, RlcWs &w, const uint8_t *desc, u32 count, void *gpts, uint8_t *gacc,
                 u32 *f, RlcStage stage, bool first, uint8_t *gex, uint4 *sdesc, u32 *gamma, uint8_t *d_accept,
-                RlcIo io, hipStream_t s) {
+                RlcIo io, hipStream_t s, const u32 *copy_map = nullptr) {
     hipEvent_t *ev = c->rlc_lev_ev;
     float t;
     for (size_t o = 0; o < count; o += LCB_VERIFY_CHUNK) {
@@ -1139,7 +1139,7 @@ void rlc_checks(lcb_ctx *c, const RlcKindInfo &K, RlcWs &w, const uint8_t *desc,
         else lcbk_final_exp_check(dim3(nblk(m)), s, f, (u32)m, gacc + o);
         hipEventRecord(ev[3], s);
         if (stage == RLC_COPY)
-            lcbk_rlc_park_copy(s, f, (u32)o, (u32)m, gamma);
+            lcbk_rlc_park_copy(s, f, (u32)o, (u32)m, gamma, copy_map);
         else if (stage == RLC_SEARCH)
             lcbk_rlc_search(dim3(nblk(m)), s, sdesc, (u32)o, (u32)m, gamma, f, d_accept, w.dB, w.cnt + 1, io.d_key,
                             (u32)K.n_keys, w.susp);
@@ -1223,28 +1223,44 @@ int rlc_levels(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, size_t n, 
         rlc_checks(c, K, w, w.dA, groups, gpts, gacc, f, RLC_RESOLVE, first, gex, sdesc, gamma, d_accept, io, s);
         if (!launched("batched verify launch")) return -1;
         if (!read_counts(cnt, w.cnt, 3, s)) return -1;
-        if (first && cnt[2] && !K.ts) {  // TPKE level 2: two weighted re-checks per failed group, two-error location
+        if (first && cnt[2] && !K.ts) {  // TPKE level 2: weighted re-check per failed group, one-error search, then
+            // for the groups it leaves open a second weighted check and the two-error location
             const u32 ns = cnt[2];
-            if (lev + 1 < 8) c->rlc_levels[lev + 1] = 2 * ns;
+            if (lev + 1 < 8) c->rlc_levels[lev + 1] = ns;
             c->rlc_nlev = ++lev + 1;
-            const size_t nc = 2 * (size_t)ns, nf2 = nc < LCB_VERIFY_CHUNK ? nc : LCB_VERIFY_CHUNK;
-            hipMemcpyAsync(sdesc + ns, sdesc, (size_t)ns * 16, hipMemcpyDeviceToDevice, s);
-            void *gp2 = c->rlc[5].get(nc * K.rec);
-            uint8_t *gacc2 = (uint8_t *)c->rlc[6].get(nc);
-            u32 *g12 = (u32 *)c->rlc[16].get(nc * 576);
+            const size_t nf2 = ns < LCB_VERIFY_CHUNK ? ns : LCB_VERIFY_CHUNK;
+            void *gp2 = c->rlc[5].get((size_t)ns * K.rec);
+            uint8_t *gacc2 = (uint8_t *)c->rlc[6].get(ns);
+            u32 *g12 = (u32 *)c->rlc[16].get(2 * (size_t)ns * 576);     // gamma_c rows, then gamma_t rows
             u32 *f2 = (u32 *)c->t_f.get(nf2 * 576 * (size_t)lcbk_fe_slots());
-            if (!gp2 || !gacc2 || !g12 || !f2) { set_err("device allocation failed"); return -1; }
+            u32 *open = (u32 *)c->rlc[17].get((size_t)ns * 4 + 16);    // unresolved groups + their count
+            if (!gp2 || !gacc2 || !g12 || !f2 || !open) { set_err("device allocation failed"); return -1; }
             hipEventRecord(ev[0], s);
-            lcbk_tpke_rlc_wsum2(s, sdesc, ns, w.rA, w.rB, (u32)n, io.d_key, (u32)K.n_keys, w.susp, gp2);
+            lcbk_tpke_rlc_wsum2(s, sdesc, ns, nullptr, w.rA, w.rB, (u32)n, io.d_key, (u32)K.n_keys, w.susp, gp2, nullptr);
             hipEventRecord(ev[1], s);
             if (hipEventSynchronize(ev[1]) == hipSuccess && hipEventElapsedTime(&t, ev[0], ev[1]) == hipSuccess)
                 c->rlc_ms[0] += t;
-            rlc_checks(c, K, w, (const uint8_t *)sdesc, (u32)nc, gp2, gacc2, f2, RLC_COPY, false, nullptr, sdesc, g12,
+            rlc_checks(c, K, w, (const uint8_t *)sdesc, ns, gp2, gacc2, f2, RLC_COPY, false, nullptr, sdesc, g12,
                        d_accept, io, s);
-            u32 *open = (u32 *)c->rlc[17].get((size_t)ns * 4 + 16);    // unresolved groups + their count
-            if (!open) { set_err("device allocation failed"); return -1; }
-            lcbk_tpke_rlc_search2(s, sdesc, ns, gamma, g12, d_accept, w.dB, w.cnt + 1, io.d_key, (u32)K.n_keys, w.susp,
-                                  open + 4, open);
+            lcbk_tpke_rlc_search2a(s, sdesc, ns, gamma, g12, d_accept, open + 4, open);
+            u32 no = 0;
+            if (!launched("batched verify launch") || !read_counts(&no, open, 1, s)) return -1;
+            if (no) {
+                if (lev + 1 < 8) c->rlc_levels[lev + 1] = no;
+                c->rlc_nlev = ++lev + 1;
+                hipEventRecord(ev[0], s);
+                // sdesc[ns, 2 ns) is free (sized for two entries per level-1 group): the open groups' descriptors
+                lcbk_tpke_rlc_wsum2(s, sdesc, no, open + 4, w.rA, w.rB, (u32)n, io.d_key, (u32)K.n_keys, w.susp, gp2,
+                                    sdesc + ns);
+                hipEventRecord(ev[1], s);
+                if (hipEventSynchronize(ev[1]) == hipSuccess && hipEventElapsedTime(&t, ev[0], ev[1]) == hipSuccess)
+                    c->rlc_ms[0] += t;
+                // gamma_t of open group g -> row ns + g
+                rlc_checks(c, K, w, (const uint8_t *)(sdesc + ns), no, gp2, gacc2, f2, RLC_COPY, false, nullptr,
+                           sdesc + ns, g12 + (size_t)ns * 144, d_accept, io, s, open + 4);
+                lcbk_tpke_rlc_search2b(s, sdesc, ns, no, gamma, g12, open + 4, open, d_accept, w.dB, w.cnt + 1,
+                                       io.d_key, (u32)K.n_keys, w.susp);
+            }
             if (!launched("batched verify launch")) return -1;
             if (!read_counts(cnt + 1, w.cnt + 1, 1, s)) return -1;
         } else if (first && cnt[2]) {    // level 2: weighted re-check of the failed groups, then the search

@@ -199,8 +199,9 @@ def test_two_bad_per_group_search_fails(nat, tdev, kind):
     assert got == expect and expect.count(False) == 3
     levels, _ = nat.tpke_batched_stats()
     # TS: the one-error search fails on the two-bad group, whose shares get single checks; TPKE: level 2 re-checks each
-    # failed group twice (weights c and t) and the two-error location names both bad shares
-    assert levels == ([2, 2, 12] if kind == "ts" else [2, 4])
+    # failed group with weights c (the one-error search names the single bad share), the open group with weights t, and
+    # the two-error location names both bad shares
+    assert levels == ([2, 2, 12] if kind == "ts" else [2, 2, 1])
 
 
 @pytest.mark.parametrize("k", [3, 4])
