@@ -1544,13 +1544,19 @@ def run_tpke_pipelined(args, nat, torch, dev, world, inp, dd, n, n_cts, n_dec, P
     for t in range(P):
         lanes.append(dict(ctx=nat.Context(), stream=torch.cuda.Stream(dev),
                           acc=torch.full((n,), 7, dtype=torch.uint8, device=dev)))
+    # every timed step's decisions are kept (one slot per step, copied on the lane's stream after its step) and all of
+    # them are compared with the oracle's after the timed region (the last step of each lane only, before)
+    slots = torch.full((max(1, args.steps), n), 7, dtype=torch.uint8, device=dev)
 
-    def one(ln):
+    def one(ln, step=None):
         rc = lib.lcb_ctx_tpke_verify_shares_batched_dev(
             ln["ctx"].ptr, ln["acc"].data_ptr(), n, py, nk, pu, pw, pv, pvo, nc, d_ct.data_ptr(), d_dec.data_ptr(),
             d_ui.data_ptr(), ln["stream"].cuda_stream)
         if rc != 0:
             raise RuntimeError(nat.last_error())
+        if step is not None:
+            with torch.cuda.stream(ln["stream"]):
+                slots[step].copy_(ln["acc"], non_blocking=True)
         ln["stream"].synchronize()
 
     for ln in lanes:                      # warmup: every context once, alone
@@ -1569,8 +1575,8 @@ def run_tpke_pipelined(args, nat, torch, dev, world, inp, dd, n, n_cts, n_dec, P
         ln = lanes[t]
         go.wait()
         time.sleep(t_one * t / P)
-        for _ in range(t, args.steps, P):
-            one(ln)
+        for step in range(t, args.steps, P):
+            one(ln, step)
 
     pool = concurrent.futures.ThreadPoolExecutor(max_workers=P)
     if world > 1:
@@ -1584,9 +1590,9 @@ def run_tpke_pipelined(args, nat, torch, dev, world, inp, dd, n, n_cts, n_dec, P
         dist.barrier()
     elapsed = time.perf_counter() - t0
     pool.shutdown()
-    for t, ln in enumerate(lanes):
-        if t < args.steps:
-            mism += int(np.sum(ln["acc"].cpu().numpy() != inp["expect"]))
+    expect_dev = torch.from_numpy(np.ascontiguousarray(inp["expect"]).astype(np.uint8)).to(dev)
+    mism += int((slots[:args.steps] != expect_dev.unsqueeze(0)).sum().item())
+    del slots
     levels = []
     for ln in lanes:
         lv = (ctypes.c_uint32 * 8)()
@@ -1605,7 +1611,8 @@ def run_tpke_pipelined(args, nat, torch, dev, world, inp, dd, n, n_cts, n_dec, P
         ms_per_step=1e3 * elapsed / args.steps, decision_mismatches=int(t[1]),
         algorithm=("per ciphertext group: e(sum s_i U_i, H) == e(sum s_i Y_i, W), secret s_i = a_i + b_i lambda "
                    "(32-bit a_i, b_i from ChaCha20 keyed by getrandom per call: 2^64 exponents); failed groups "
-                   "located (two errors) or checked singly; every rejection exact, false accept <= 2^-64 per group"),
+                   "located (one or two errors: a false location <= len^2 2^-64 per group) or checked singly; "
+                   "other rejections exact, false accept <= 2^-64 per group; every step's decisions checked"),
         api=f"lcb_ctx_tpke_verify_shares_batched_dev, {P} batches in flight (contexts / streams / host threads)",
         pipeline=P, single_batch_ms=1e3 * t_one, levels=levels[0],
         roofline={"bound": "valu_int32",
@@ -1684,6 +1691,8 @@ def compact_line(full):
                                                                 "roofline_frac")}
         line["config"]["batches_in_flight"] = tb.get("pipeline")
         line["config"]["single_batch_latency_ms"] = _r(tb.get("single_batch_ms"))
+    if cfg.get("hw_queues"):
+        line["config"]["hw_queues"] = cfg["hw_queues"]
     s = {}
     byz = full.get("tpke_byzantine")
     if byz:
@@ -1759,8 +1768,9 @@ def main():
                     help="batched verify: concurrent parts (contexts / streams / host threads) per step; measured "
                          "no faster with 2 or 3 parts (147 - 159 vs 145 ms per 1M shares)")
     ap.add_argument("--hw-queues", type=int, default=int(os.environ.get("LCB_BENCH_HWQ", "8")),
-                    help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's; 8 measured 12.30 vs 11.95 M "
-                         "shares/s with two batches in flight, profiles/r04/q2)")
+                    help="GPU_MAX_HW_QUEUES for this process when the environment does not set it (an operator's "
+                         "setting, e.g. 4 on a shared GPU, is kept; 0: never set it); 8 measured 12.30 vs 11.95 M "
+                         "shares/s with two batches in flight, profiles/r04/q2")
     ap.add_argument("--tpke-pipeline", type=int, default=2,
                     help="batched verify: whole batches in flight (each on its own context / stream / host thread); "
                          "2 measured 12.3 vs 10.6 M shares/s for one at a time, 3 no better (profiles/r04/q1, q2)")
@@ -1789,11 +1799,12 @@ def main():
     ap.add_argument("--replay-n", type=int, default=256, help="epoch-replay network size N (0 = skip)")
     ap.add_argument("--replay-steps", type=int, default=1)
     ap.add_argument("--replay-exact", type=int, default=0, help="epoch replay with the exact per-share checks")
-    ap.add_argument("--replay-concurrent", type=int, default=0,
-                    help="epoch replay: 1 = the TPKE and coin chains side by side (own host thread, context, stream): "
-                         "+3 %% views/s, but the two chains' large-scratch kernels (CommonCoin assembly 22.7 KB per "
-                         "lane) on two hardware queues at once exhausted the scratch pool on some boxes "
-                         "(HSA_STATUS_ERROR_OUT_OF_RESOURCES, profiles/r04/final), so off by default")
+    ap.add_argument("--replay-concurrent", type=int, default=1,
+                    help="epoch replay: 1 = the TPKE and coin chains side by side (own host thread, context, stream); "
+                         "0 = one after the other.  Round 4 kept this off after the CommonCoin assembly's 22.7 KB of "
+                         "scratch per lane on two hardware queues aborted the process (HSA_STATUS_ERROR_OUT_OF_RESOURCES); "
+                         "round 5 moved every multi-wave kernel to <= 4 KB (lanetab.hpp workspaces) and gates larger "
+                         "reservations onto one stream per device (lcb_set_scratch_gate)")
     ap.add_argument("--ecdsa-sigs", type=int, default=1 << 20, help="header signatures per rank (0 = skip)")
     ap.add_argument("--ecdsa-validators", type=int, default=256)
     ap.add_argument("--ecdsa-steps", type=int, default=3)
@@ -1807,9 +1818,10 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.hw_queues > 0:
+    if args.hw_queues > 0 and not os.environ.get("GPU_MAX_HW_QUEUES"):
         # hardware queues per process, read when the HIP runtime starts (before torch / the library touch the GPU):
-        # the batched call uses five streams per context, so batches in flight need more than HIP's default four
+        # the batched call uses five streams per context, so batches in flight need more than HIP's default four;
+        # an explicit setting in the environment wins
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, args.hw_queues))
     import torch
     import torch.distributed as dist
@@ -2019,7 +2031,8 @@ def main():
             "config": {"workload": "configs[1]: 1M TPKE decryption shares, N=22 F=7 validators, one MI355X per rank",
                        "shares_per_rank": n, "ciphertexts_per_rank": n_cts, "decryptors": n_dec, "degree": args.f,
                        "v_bytes": args.vlen, "corrupted_fraction": 0.01, "parallelism": f"shard{world}",
-                       "decision_mismatches": head["decision_mismatches"], "algorithm": algo, "api": head["api"]},
+                       "decision_mismatches": head["decision_mismatches"], "algorithm": algo, "api": head["api"],
+                       "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")},
             "roofline": roofline,
             "source_hash": src_hash,
             "cpu_baseline": cpu_line,

@@ -344,6 +344,18 @@ int lcb_set_coop_miller_max(uint32_t max_checks);
    with the TPKE preparation split into hash + H's line set and U / W decoding + W's line set, on two high-priority
    streams (threshold signatures: as 1).  Decisions are unchanged. */
 int lcb_set_fork_mode(int mode);
+/* the scratch gate (round 5): a launch whose scratch reservation — private segment per lane x the lanes of
+   min(dispatch waves, 32 wave slots per CU) — reaches `bytes` runs on one process-wide stream per device, ordered with
+   the caller's stream by events, so concurrent callers never hold more than one such reservation per process (the HIP
+   runtime aborts the process when it cannot reserve scratch).  Default 4 GiB (environment LCB_SCRATCH_GATE_MB); -1 = off,
+   0 = every launch with scratch.  Tuning hook (LCB_ALLOW_TUNING=1). */
+int lcb_set_scratch_gate(long long bytes);
+/* launches routed through the gate / launches checked, since the process started */
+void lcb_scratch_gate_stats(uint64_t *routed, uint64_t *seen);
+/* the persistent grids of the table-walking kernels (Lagrange lanes, scalar-multiplication batches) use at most this
+   many blocks of 256 lanes (0 = as many as are resident): a test hook that makes small batches walk several items per
+   lane.  Tuning hook (LCB_ALLOW_TUNING=1). */
+int lcb_set_persist_blocks(uint32_t max_blocks);
 /* tuning hook (LCB_ALLOW_TUNING=1): records per lane of the MSM bucket accumulation (k_msm_chunk_acc, default 64);
    0 = one lane per bucket (k_msm_bucket_acc).  Results are unchanged. */
 int lcb_set_msm_chunk(int records_per_lane);

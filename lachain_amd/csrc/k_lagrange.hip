@@ -1,5 +1,6 @@
 // lachain_amd/csrc/k_lagrange.hip — gfx950 kernels: Lagrange interpolation at 0 and MSM.
 #include "kcommon.hpp"
+#include "lanetab.hpp"
 
 LCB_ASM_LIBRARY(k_lagrange)
 LCB_TU_CONFIG(k_lagrange)
@@ -77,120 +78,6 @@ template <class F> DI void jac_mul_aff_inl(jac<F> &r, const aff<F> &p, const u32
         if ((k[i >> 5] >> (i & 31)) & 1) jac_add_aff(r, r, p.x, p.y);
     }
 }
-// g2_mul_gls (curve.hpp) with the loop inlined
-DI void g2_mul_gls_inl(g2 &r, const g2a &A, const u32 k[8]) {
-    jac_set_inf(r);
-    if (A.inf) return;
-    u32 q[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) q[j] = k[j];
-    u64 d[4];
-    u256_divmod_u(q, d[0]);
-    u256_divmod_u(q, d[1]);
-    u256_divmod_u(q, d[2]);
-    d[3] = (u64)q[0] | ((u64)q[1] << 32);
-    g2 P, T;
-    jac_from_aff(P, A);
-    g2a Q[4];
-    Q[0] = A;
-    g2_psi(T, P);
-    Q[1].x = T.x; fp2_neg(Q[1].y, T.y); Q[1].inf = false;
-    g2_psi2(T, P);
-    Q[2].x = T.x; Q[2].y = T.y; Q[2].inf = false;
-    g2_psi(T, T);
-    Q[3].x = T.x; fp2_neg(Q[3].y, T.y); Q[3].inf = false;
-#pragma unroll 1
-    for (int b = 63; b >= 0; b--) {
-        jac_dbl(r, r);
-#pragma unroll 1
-        for (int i = 0; i < 4; i++)
-            if ((d[i] >> b) & 1) jac_add_aff(r, r, Q[i].x, Q[i].y);
-    }
-}
-// GLS in G2 with one addition per digit column: the 15 non-empty sums of Q = {A, -psi A, psi^2 A, -psi^3 A} (index
-// bit i <-> Q_i) in an affine table — Q_2, Q_3 = psi^2(Q_0, Q_1), so 1 + 9 additions and one batched inversion —
-// then 64 doublings and 64 mixed additions instead of 64 doublings and 256 additions per wave.  For A in G2 no entry
-// is infinity (|i0 - i1 z + i2 z^2 - i3 z^3| < r); the plain GLS loop stays as a guard.
-DI void g2_mul_gls_tab(g2 &r, const g2a &A, const u32 k[8]) {
-    jac_set_inf(r);
-    if (A.inf) return;
-    u32 q[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) q[j] = k[j];
-    u64 d[4];
-    u256_divmod_u(q, d[0]);
-    u256_divmod_u(q, d[1]);
-    u256_divmod_u(q, d[2]);
-    d[3] = (u64)q[0] | ((u64)q[1] << 32);
-    g2 t[16];
-    jac_from_aff(t[1], A);
-    g2_psi(t[2], t[1]);
-    fp2_neg(t[2].y, t[2].y);                         // -psi(A), z = 1
-    jac_add_aff(t[3], t[1], t[2].x, t[2].y);
-#pragma unroll 1
-    for (int j = 1; j < 4; j++) g2_psi2(t[4 * j], t[j]);
-#pragma unroll 1
-    for (int j = 4; j < 16; j += 4)
-#pragma unroll 1
-        for (int i = 1; i < 4; i++) jac_add(t[j + i], t[i], t[j]);
-    g2a ta[16];
-    if (!jac_table_to_aff(ta, t)) { g2_mul_gls_inl(r, A, k); return; }
-#pragma unroll 1
-    for (int b = 63; b >= 0; b--) {
-        jac_dbl(r, r);
-        u32 idx = (u32)((d[0] >> b) & 1) | (u32)((d[1] >> b) & 1) << 1 | (u32)((d[2] >> b) & 1) << 2 |
-                  (u32)((d[3] >> b) & 1) << 3;
-        if (idx) jac_add_aff(r, r, ta[idx].x, ta[idx].y);
-    }
-}
-// GLS digits of k (< r): k = d0 + d1 u + d2 u^2 + d3 u^3, u = |z| (curve.hpp u256_divmod_u)
-DI void g2_gls_digits(u64 d[4], const u32 k[8]) {
-    u32 q[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) q[j] = k[j];
-    u256_divmod_u(q, d[0]);
-    u256_divmod_u(q, d[1]);
-    u256_divmod_u(q, d[2]);
-    d[3] = (u64)q[0] | ((u64)q[1] << 32);
-}
-// g2_mul_gls_tab's 15 sums of {A, -psi A, psi^2 A, -psi^3 A} (index bit i <-> Q_i) into t[1..15], Jacobian
-DI void g2_gls_sums(g2 *t, const g2a &A) {
-    jac_from_aff(t[1], A);
-    g2_psi(t[2], t[1]);
-    fp2_neg(t[2].y, t[2].y);
-    jac_add_aff(t[3], t[1], t[2].x, t[2].y);
-#pragma unroll 1
-    for (int j = 1; j < 4; j++) g2_psi2(t[4 * j], t[j]);
-#pragma unroll 1
-    for (int j = 4; j < 16; j += 4)
-#pragma unroll 1
-        for (int i = 1; i < 4; i++) jac_add(t[j + i], t[i], t[j]);
-}
-// lambda_a A + lambda_b B for two points of G2 with one shared run of 64 doublings (Straus) and one batched inversion
-// for both tables (entries 1..15: A's sums, 16..30: B's); false when a table entry is infinity (never in G2, as for
-// g2_mul_gls_tab) — the caller then multiplies the points one by one
-DI bool g2_mul2_gls_tab(g2 &r, const g2a &A, const u32 ka[8], const g2a &B, const u32 kb[8]) {
-    u64 da[4], db[4];
-    g2_gls_digits(da, ka);
-    g2_gls_digits(db, kb);
-    g2 t[31];
-    g2_gls_sums(t, A);
-    g2_gls_sums(t + 15, B);
-    g2a ta[31];
-    if (!jac_table_to_aff(ta, t)) return false;
-    jac_set_inf(r);
-#pragma unroll 1
-    for (int b = 63; b >= 0; b--) {
-        jac_dbl(r, r);
-        u32 ia = (u32)((da[0] >> b) & 1) | (u32)((da[1] >> b) & 1) << 1 | (u32)((da[2] >> b) & 1) << 2 |
-                 (u32)((da[3] >> b) & 1) << 3;
-        u32 ib = (u32)((db[0] >> b) & 1) | (u32)((db[1] >> b) & 1) << 1 | (u32)((db[2] >> b) & 1) << 2 |
-                 (u32)((db[3] >> b) & 1) << 3;
-        if (ia) jac_add_aff(r, r, ta[ia].x, ta[ia].y);
-        if (ib) jac_add_aff(r, r, ta[15 + ib].x, ta[15 + ib].y);
-    }
-    return true;
-}
 // a G2 entry's point: the ts_share_st record when it holds exactly the entry's bytes, else decoded and psi-tested here
 DI void g2_entry_point(g2a &A, bool &ok, bool &in_g2, const uint8_t *y, const ts_share_st *dec, u32 n_dec, u32 si) {
     bool hit = false;
@@ -214,67 +101,99 @@ DI void g2_entry_point(g2a &A, bool &ok, bool &in_g2, const uint8_t *y, const ts
     }
 }
 
+// Lagrange lanes with their tables in a workspace slot (lanetab.hpp): persistent grids of as many blocks as are resident
+// at once, each lane walking the entries gid, gid + grid, ... with its own slot, so the workspace is sized by the grid
+// and the kernels need no scratch for their tables (round 5; the register-resident tables spilled 5.4 / 10.3 / 22.7 KB
+// of scratch per lane for the G1 / G2 / paired G2 lanes).
+//
 // partial products lambda_i * Y_i for every entry (one lane per entry)
 extern "C" __global__ void LCB_BOUNDS k_g1_mul_lanes(const uint8_t *ys, const fr *lam_raw, u32 n_entries, g1 *out,
-                                                    uint8_t *ok_out) {
-    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_entries) return;
-    g1a A;
-    bool ok = g1_decompress(A, ys + 48 * (size_t)i);
-    // plain double-and-add on the canonical integer lambda: exact for every on-curve input, including points
-    // outside the r-torsion that G1.FromBytes accepts (GLV would be wrong for their cofactor component)
-    g1 R;
-    fr k = lam_raw[i];
-    jac_mul_win4(R, A, k.v);      // 4-bit window, affine table (measured faster than the plain ladder)
-    out[i] = R;
-    ok_out[i] = ok;
+                                                    uint8_t *ok_out, u32 *ws) {
+    const u32 gid = blockIdx.x * blockDim.x + threadIdx.x, gsz = gridDim.x * blockDim.x;
+    char *slot = lw_slot(ws, LW_WIN4_QUADS(fp), gid);
+#pragma unroll 1
+    for (u32 i = gid; i < n_entries; i += gsz) {
+        g1a A;
+        bool ok = g1_decompress(A, ys + 48 * (size_t)i);
+        // the canonical integer lambda with a 4-bit window: exact for every on-curve input, including points outside
+        // the r-torsion that G1.FromBytes accepts (GLV would be wrong for their cofactor component)
+        g1 R;
+        fr k = lam_raw[i];
+        lw_mul_win4(R, slot, A, k.v);
+        out[i] = R;
+        ok_out[i] = ok;
+    }
+}
+// k A for one G2 entry: GLS over the slot's table (entries 1..15) for a point proven to lie in G2, else the plain
+// ladder, so the result equals the oracle's for every on-curve input
+DI void lw_g2_mul_entry(g2 &R, char *slot, const g2a &A, bool in_g2, const fr &k) {
+    if (A.inf) { jac_set_inf(R); return; }
+    if (in_g2) {
+        u64 d[4];
+        lw_gls_digits(d, k.v);
+        lw_g2_gls_sums(slot, 0, A);
+        if (lw_table_to_aff<fp2>(slot, 15)) { lw_g2_gls_ladder(R, slot, d); return; }
+    }
+    jac_mul_aff_inl(R, A, k.v, 256);
 }
 // dec / src (nullable): the decoded shares of the context's last batched CommonCoin check (ts_share_st) and each
 // entry's index among them; an entry whose record holds exactly its input bytes takes the record's point and G2 flag
 extern "C" __global__ void LCB_BOUNDS k_g2_mul_lanes(const uint8_t *ys, const fr *lam_raw, u32 n_entries, g2 *out,
                                                     uint8_t *ok_out, const ts_share_st *dec, u32 n_dec,
-                                                    const u32 *src) {
-    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_entries) return;
-    g2a A;
-    bool ok, in_g2;
-    g2_entry_point(A, ok, in_g2, ys + 96 * (size_t)i, dec, n_dec, src ? src[i] : 0xffffffffu);
-    // GLS (64 shared doublings) only for points proven to lie in G2 (psi(P) == [z]P, 64 doublings); any other
-    // on-curve input takes the plain ladder, so the result equals the oracle's for every input
-    g2 R;
-    fr k = lam_raw[i];
-    if (in_g2) g2_mul_gls_tab(R, A, k.v);
-    else jac_mul_aff_inl(R, A, k.v, 256);
-    out[i] = R;
-    ok_out[i] = ok;
+                                                    const u32 *src, u32 *ws) {
+    const u32 gid = blockIdx.x * blockDim.x + threadIdx.x, gsz = gridDim.x * blockDim.x;
+    char *slot = lw_slot(ws, LW_G2_TAB_QUADS, gid);
+#pragma unroll 1
+    for (u32 i = gid; i < n_entries; i += gsz) {
+        g2a A;
+        bool ok, in_g2;
+        g2_entry_point(A, ok, in_g2, ys + 96 * (size_t)i, dec, n_dec, src ? src[i] : 0xffffffffu);
+        g2 R;
+        lw_g2_mul_entry(R, slot, A, in_g2, lam_raw[i]);
+        out[i] = R;
+        ok_out[i] = ok;
+    }
 }
 // two entries per lane (entries 2p, 2p + 1 of one problem: the caller guarantees even problem offsets): both in G2 ->
-// lambda_a A + lambda_b B by g2_mul2_gls_tab into out[2p] (out[2p + 1] = infinity), else each on its own as
-// k_g2_mul_lanes does; the problem sums (k_g2_sum) are the same points
+// lambda_a A + lambda_b B with one shared run of 64 doublings over both tables (Straus) and one batched inversion for
+// the 30 entries, into out[2p] (out[2p + 1] = infinity), else each on its own as k_g2_mul_lanes does; the problem sums
+// (k_g2_sum) are the same points
 extern "C" __global__ void LCB_BOUNDS k_g2_mul2_lanes(const uint8_t *ys, const fr *lam_raw, u32 n_pairs, g2 *out,
                                                      uint8_t *ok_out, const ts_share_st *dec, u32 n_dec,
-                                                     const u32 *src) {
-    u32 p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n_pairs) return;
-    const u32 i0 = 2 * p, i1 = 2 * p + 1;
-    g2a A, B;
-    bool oka, okb, ga, gb;
-    g2_entry_point(A, oka, ga, ys + 96 * (size_t)i0, dec, n_dec, src ? src[i0] : 0xffffffffu);
-    g2_entry_point(B, okb, gb, ys + 96 * (size_t)i1, dec, n_dec, src ? src[i1] : 0xffffffffu);
-    fr ka = lam_raw[i0], kb = lam_raw[i1];
-    g2 R0, R1;
-    jac_set_inf(R1);
-    if (!(ga && gb && !A.inf && !B.inf && g2_mul2_gls_tab(R0, A, ka.v, B, kb.v))) {
-        // inline (measured 199 ms per 65,536-round assembly vs 205 ms with one shared call, despite more spills)
-        if (ga) g2_mul_gls_tab(R0, A, ka.v);
-        else jac_mul_aff_inl(R0, A, ka.v, 256);
-        if (gb) g2_mul_gls_tab(R1, B, kb.v);
-        else jac_mul_aff_inl(R1, B, kb.v, 256);
+                                                     const u32 *src, u32 *ws) {
+    const u32 gid = blockIdx.x * blockDim.x + threadIdx.x, gsz = gridDim.x * blockDim.x;
+    char *slot = lw_slot(ws, 2 * LW_G2_TAB_QUADS, gid);
+#pragma unroll 1
+    for (u32 p = gid; p < n_pairs; p += gsz) {
+        const u32 i0 = 2 * p, i1 = 2 * p + 1;
+        g2a A, B;
+        bool oka, okb, ga, gb;
+        g2_entry_point(A, oka, ga, ys + 96 * (size_t)i0, dec, n_dec, src ? src[i0] : 0xffffffffu);
+        g2_entry_point(B, okb, gb, ys + 96 * (size_t)i1, dec, n_dec, src ? src[i1] : 0xffffffffu);
+        const fr ka = lam_raw[i0], kb = lam_raw[i1];
+        g2 R0, R1;
+        jac_set_inf(R1);
+        bool done = false;
+        if (ga && gb && !A.inf && !B.inf) {
+            lw_g2_gls_sums(slot, 0, A);
+            lw_g2_gls_sums(slot, 15, B);
+            if (lw_table_to_aff<fp2>(slot, 30)) {
+                u64 da[4], db[4];
+                lw_gls_digits(da, ka.v);
+                lw_gls_digits(db, kb.v);
+                lw_g2_gls_ladder2(R0, slot, da, db);
+                done = true;
+            }
+        }
+        if (!done) {
+            lw_g2_mul_entry(R0, slot, A, ga, ka);
+            lw_g2_mul_entry(R1, slot, B, gb, kb);
+        }
+        out[i0] = R0;
+        out[i1] = R1;
+        ok_out[i0] = oka;
+        ok_out[i1] = okb;
     }
-    out[i0] = R0;
-    out[i1] = R1;
-    ok_out[i0] = oka;
-    ok_out[i1] = okb;
 }
 extern "C" __global__ void LCB_BOUNDS k_g1_sum(const g1 *parts, const uint8_t *ok_in, const u32 *off, u32 n_problems,
                                               uint8_t *status, uint8_t *out) {
@@ -311,16 +230,29 @@ extern "C" __global__ void LCB_BOUNDS k_g2_sum(const g2 *parts, const uint8_t *o
 extern "C" void lcbk_lagrange_coeffs(dim3 grid, hipStream_t s, const uint8_t *xs, const u32 *off, u32 n_problems, void *lam_raw, uint8_t *status) {
     LCB_LAUNCH(k_lagrange_coeffs, xs, off, n_problems, (fr *)lam_raw, status);
 }
-extern "C" void lcbk_g1_mul_lanes(dim3 grid, hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out) {
-    LCB_LAUNCH(k_g1_mul_lanes, ys, (const fr *)lam_raw, n_entries, (g1 *)out, ok_out);
+static u32 g_rb_g1, g_rb_g2, g_rb_g2p;
+static u32 lanes_blocks(int which, u32 n) {
+    const void *k = which == 1 ? (const void *)k_g1_mul_lanes : which == 2 ? (const void *)k_g2_mul_lanes : (const void *)k_g2_mul2_lanes;
+    u32 *cache = which == 1 ? &g_rb_g1 : which == 2 ? &g_rb_g2 : &g_rb_g2p;
+    return lcb_persist_blocks(k, cache, which == 3 ? n / 2 : n);
 }
-extern "C" void lcbk_g2_mul_lanes(dim3 grid, hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out, const void *dec, u32 n_dec, const u32 *src) {
-    LCB_LAUNCH(k_g2_mul_lanes, ys, (const fr *)lam_raw, n_entries, (g2 *)out, ok_out, (const ts_share_st *)dec, n_dec, src);
+static u32 lanes_quads(int which) { return which == 1 ? LW_WIN4_QUADS(fp) : which == 2 ? LW_G2_TAB_QUADS : 2 * LW_G2_TAB_QUADS; }
+// workspace bytes of the Lagrange lanes over n entries: 1 = G1, 2 = G2, 3 = paired G2
+extern "C" size_t lcbk_lanes_ws_bytes(int which, u32 n) {
+    return LCB_WS_BYTES(lanes_blocks(which, n), lanes_quads(which));
 }
-extern "C" void lcbk_g2_mul2_lanes(hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out, const void *dec, u32 n_dec, const u32 *src) {
+extern "C" void lcbk_g1_mul_lanes(hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out, u32 *ws) {
+    dim3 grid(lanes_blocks(1, n_entries));
+    LCB_LAUNCH(k_g1_mul_lanes, ys, (const fr *)lam_raw, n_entries, (g1 *)out, ok_out, ws);
+}
+extern "C" void lcbk_g2_mul_lanes(hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out, const void *dec, u32 n_dec, const u32 *src, u32 *ws) {
+    dim3 grid(lanes_blocks(2, n_entries));
+    LCB_LAUNCH(k_g2_mul_lanes, ys, (const fr *)lam_raw, n_entries, (g2 *)out, ok_out, (const ts_share_st *)dec, n_dec, src, ws);
+}
+extern "C" void lcbk_g2_mul2_lanes(hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out, const void *dec, u32 n_dec, const u32 *src, u32 *ws) {
     const u32 n_pairs = n_entries / 2;
-    dim3 grid((n_pairs + LCB_BLOCK - 1) / LCB_BLOCK);
-    LCB_LAUNCH(k_g2_mul2_lanes, ys, (const fr *)lam_raw, n_pairs, (g2 *)out, ok_out, (const ts_share_st *)dec, n_dec, src);
+    dim3 grid(lanes_blocks(3, n_entries));
+    LCB_LAUNCH(k_g2_mul2_lanes, ys, (const fr *)lam_raw, n_pairs, (g2 *)out, ok_out, (const ts_share_st *)dec, n_dec, src, ws);
 }
 extern "C" void lcbk_g1_sum(dim3 grid, hipStream_t s, const void *parts, const uint8_t *ok_in, const u32 *off, u32 n_problems, uint8_t *status, uint8_t *out) {
     LCB_LAUNCH(k_g1_sum, (const g1 *)parts, ok_in, off, n_problems, status, out);

@@ -3,6 +3,7 @@
 // conversion of mcl's Jacobian records to wire bytes for the batched Lagrange path.  mcl's G1 / G2 records are the
 // device's own Jacobian layout (x, y, z in Montgomery form, 12 x u32 per Fp), scalars arrive as canonical integers.
 #include "coop.hpp"
+#include "lanetab.hpp"
 
 LCB_ASM_LIBRARY(k_mcl)
 LCB_TU_CONFIG(k_mcl)
@@ -11,16 +12,19 @@ LCB_TU_CONFIG(k_mcl)
 static_assert(LCB_LS_POINT == 6528 && LCB_LS_FLAG == 6528 + 48 && LCB_LINESET_WORDS * 4 == 26368, "line-set layout");
 
 // terms[i] = [k_i] P_i for n G1 points (Jacobian) and canonical 256-bit scalars: the 4-bit windowed ladder over the
-// point's affine table, exact for every on-curve input (k_lagrange.hip)
-extern "C" __global__ void LCB_BOUNDS k_mcl_g1_terms(const g1 *pts, const fr *scal, u32 n, g1 *terms) {
-    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    g1a a;
-    jac_to_aff(a, pts[i]);
-    fr k = scal[i];
-    g1 r;
-    jac_mul_win4(r, a, k.v);
-    terms[i] = r;
+// point's affine table, exact for every on-curve input (persistent grid, the table in a workspace slot: lanetab.hpp)
+extern "C" __global__ void LCB_BOUNDS k_mcl_g1_terms(const g1 *pts, const fr *scal, u32 n, g1 *terms, u32 *ws) {
+    const u32 gid = blockIdx.x * blockDim.x + threadIdx.x, gsz = gridDim.x * blockDim.x;
+    char *slot = lw_slot(ws, LW_WIN4_QUADS(fp), gid);
+#pragma unroll 1
+    for (u32 i = gid; i < n; i += gsz) {
+        g1a a;
+        jac_to_aff(a, pts[i]);
+        fr k = scal[i];
+        g1 r;
+        lw_mul_win4(r, slot, a, k.v);
+        terms[i] = r;
+    }
 }
 
 // Horner with an Fr point x (mcl evaluatePolynomial: y = c[n-1]; y = y x + c[i]), one lane; g = 1 (G1) or 2 (G2)
@@ -79,9 +83,13 @@ extern "C" __global__ void LCB_BOUNDS k_mcl_to_bytes(int g, const u32 *in, u32 n
 }
 
 // ---------------------------------------------------------------- host launch wrappers
-extern "C" void lcbk_mcl_g1_terms(hipStream_t s, const void *pts, const void *scal, u32 n, void *terms) {
-    dim3 grid((n + LCB_BLOCK - 1) / LCB_BLOCK);
-    LCB_LAUNCH(k_mcl_g1_terms, (const g1 *)pts, (const fr *)scal, n, (g1 *)terms);
+static u32 g_rb_terms;
+extern "C" size_t lcbk_mcl_terms_ws_bytes(u32 n) {
+    return LCB_WS_BYTES(lcb_persist_blocks((const void *)k_mcl_g1_terms, &g_rb_terms, n), LW_WIN4_QUADS(fp));
+}
+extern "C" void lcbk_mcl_g1_terms(hipStream_t s, const void *pts, const void *scal, u32 n, void *terms, u32 *ws) {
+    dim3 grid(lcb_persist_blocks((const void *)k_mcl_g1_terms, &g_rb_terms, n));
+    LCB_LAUNCH(k_mcl_g1_terms, (const g1 *)pts, (const fr *)scal, n, (g1 *)terms, ws);
 }
 extern "C" void lcbk_mcl_horner(hipStream_t s, int g, const u32 *coef, u32 n, const void *x_raw, u32 *out) {
     dim3 grid(1);

@@ -5,7 +5,6 @@ LCB_ASM_LIBRARY(k_ops)
 LCB_TU_CONFIG(k_ops)
 
 // ================================================================================= single operations
-// One lane executes one mcl-shaped operation on mcl-layout structs held in `io` (u32 words).
 DI bool g1_on_curve(const g1 &p) { // Jacobian: Y^2 = X^3 + 4 Z^6
     if (jac_is_inf(p)) return true;
     fp l, r, z2, z6, b;
@@ -50,7 +49,12 @@ template <class G> DI bool jac_eq(const G &p, const G &q) {
     f_mul(s2, s2, z1z1);
     return f_eq(u1, u2) && f_eq(s1, s2);
 }
-extern "C" __global__ void LCB_BOUNDS k_op(int op, u32 *io, int orig_cof) {
+// One lane executes one mcl-shaped operation on mcl-layout structs held in `io` (u32 words).  One kernel per operation
+// family (round 5: the single switch kernel inlined every family into one 512-register frame with 8.4 KB of scratch per
+// lane); lcbk_op picks the family.
+//
+// Fr, G1, G2 (group operations, (de)serialization, hash to G2, generators)
+extern "C" __global__ void LCB_BOUNDS k_op_grp(int op, u32 *io, int orig_cof) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     switch (op) {
     // ---- Fr: io[0..8) = out, io[8..16) = x, io[16..24) = y (mclBnFr layout = 8 u32 Montgomery)
@@ -113,6 +117,15 @@ extern "C" __global__ void LCB_BOUNDS k_op(int op, u32 *io, int orig_cof) {
         g2 H; bool ok = g2_hash_digest(H, d, orig_cof != 0);
         if (!ok) jac_set_inf(H); *(g2 *)io = H; io[248] = ok; break;
     }
+    case OP_G1_GEN: { g1a a; g1_generator(a); jac_from_aff(*(g1 *)io, a); break; }
+    case OP_G2_GEN: { g2a a; g2_generator(a); jac_from_aff(*(g2 *)io, a); break; }
+    default: break;
+    }
+}
+// the Miller loop (and the pairing) of one pair
+extern "C" __global__ void LCB_BOUNDS k_op_pair(int op, u32 *io, int orig_cof) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    switch (op) {
     // ---- pairing / GT: io[0..144) out GT, io[144..180) G1, io[180..252) G2, io[252..396) GT a, io[396..540) GT b,
     //      io[540..548) Fr, io[548] flag
     case OP_PAIRING:
@@ -125,6 +138,13 @@ extern "C" __global__ void LCB_BOUNDS k_op(int op, u32 *io, int orig_cof) {
         else *(fp12 *)io = f;
         break;
     }
+    default: break;
+    }
+}
+// GT: final exponentiation, product, power, comparison, (de)serialization
+extern "C" __global__ void LCB_BOUNDS k_op_gt(int op, u32 *io, int orig_cof) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    switch (op) {
     case OP_FINAL_EXP: { fp12 a = *(fp12 *)(io + 252); fp12 e; final_exp(e, a); *(fp12 *)io = e; break; }
     case OP_GT_MUL: { fp12 a = *(fp12 *)(io + 252), b = *(fp12 *)(io + 396); fp12_mul(*(fp12 *)io, a, b); break; }
     case OP_GT_POW: {
@@ -152,8 +172,13 @@ extern "C" __global__ void LCB_BOUNDS k_op(int op, u32 *io, int orig_cof) {
         for (int i = 0; i < 12; i++) { ok = ok && fp_raw_lt_p(x[i]); fp m; fp_from_raw(m, x[i]); *(fp *)(io + 12 * i) = m; }
         io[548] = ok; break;
     }
-    case OP_G1_GEN: { g1a a; g1_generator(a); jac_from_aff(*(g1 *)io, a); break; }
-    case OP_G2_GEN: { g2a a; g2_generator(a); jac_from_aff(*(g2 *)io, a); break; }
+    default: break;
+    }
+}
+// tower routines on raw GT words (tools/debug)
+extern "C" __global__ void LCB_BOUNDS k_op_debug(int op, u32 *io, int orig_cof) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    switch (op) {
     case OP_DEBUG_FP12: {
         fp12 a = *(fp12 *)(io + 252), r = a;
         switch (io[548]) {
@@ -180,5 +205,8 @@ extern "C" __global__ void LCB_BOUNDS k_op(int op, u32 *io, int orig_cof) {
 
 // ---------------------------------------------------------------- host launch wrappers
 extern "C" void lcbk_op(dim3 grid, hipStream_t s, int op, u32 *io, int orig_cof) {
-    LCB_LAUNCH(k_op, op, io, orig_cof);
+    if (op == OP_PAIRING || op == OP_MILLER) LCB_LAUNCH(k_op_pair, op, io, orig_cof);
+    else if (op >= OP_FINAL_EXP && op <= OP_GT_DESER) LCB_LAUNCH(k_op_gt, op, io, orig_cof);
+    else if (op == OP_DEBUG_FP12) LCB_LAUNCH(k_op_debug, op, io, orig_cof);
+    else LCB_LAUNCH(k_op_grp, op, io, orig_cof);
 }

@@ -173,30 +173,40 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_final_exp_check(u32 *park, u32 n, u
     accept[i] = accept[i] && fp12_is_one(f);
 }
 
-// TPKE.PrivateKey.Decrypt: validity e(G, W) == e(U, H) <=> e(-G, W) e(U, H) == 1; then Ui = x U
-extern "C" __global__ void LCB_BOUNDS k_tpke_partial_decrypt(const u32 *lines, const uint8_t *ct_ok,
-                                                            const uint8_t *cts_u, const fr *x_raw, u32 x_stride,
-                                                            u32 n_cts, uint8_t *ui_out, uint8_t *status) {
-    u32 c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n_cts) return;
+// TPKE.PrivateKey.Decrypt (TPKE/PrivateKey.cs:21-31): validity e(G, W) == e(U, H) <=> e(-G, W) e(U, H) == 1, then
+// Ui = x U.  Three launches over ciphertexts c0 + [0, m) (round 5; one fused kernel spilled 7.7 KB of scratch per lane):
+// the Miller loop parks f (SoA, as k_tpke_miller), k_final_exp_check ANDs f^((p^12-1)/r) == 1 into status, and the
+// ladder writes x U for the valid ones (zero bytes otherwise).
+extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_pd_miller(const u32 *lines, const uint8_t *ct_ok, const uint8_t *cts_u,
+                                                            u32 c0, u32 m, u32 *f_soa, uint8_t *status) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const u32 c = c0 + i;
     g1a U, G;
     bool ok = g1_decompress(U, cts_u + 48 * (size_t)c) && ct_ok[c];
     g1_generator(G);
     fp_neg(G.y, G.y);
-    fp12 f, e;
+    fp12 f;
     miller2_sets(f, lines + (size_t)(2 * c) * LCB_LINESET_WORDS, U, lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS, G);
-    final_exp(e, f);
-    ok = ok && fp12_is_one(e);
+    fp12_store_soa(f_soa, m, i, f);
     status[c] = ok;
+}
+extern "C" __global__ void LCB_BOUNDS k_tpke_pd_mul(const uint8_t *cts_u, const fr *x_raw, u32 x_stride, u32 c0, u32 m,
+                                                   const uint8_t *status, uint8_t *ui_out) {
+    u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const u32 c = c0 + i;
+    uint8_t *o = ui_out + 48 * (size_t)c;
+    g1a U;
+    if (!status[c] || !g1_decompress(U, cts_u + 48 * (size_t)c)) {
+        fp z = fp_zero();
+        raw_to_bytes48(o, z);
+        return;
+    }
     g1 R;
     fr k = x_raw[(size_t)c * x_stride];
     jac_mul_aff(R, U, k.v, 256);
-    uint8_t *o = ui_out + 48 * (size_t)c;
-    if (ok) g1_compress_jac(o, R);
-    else {
-        fp z = fp_zero();
-        raw_to_bytes48(o, z);
-    }
+    g1_compress_jac(o, R);
 }
 
 
@@ -232,6 +242,11 @@ extern "C" void lcbk_tpke_miller(dim3 grid, hipStream_t s, const u32 *lines, con
 extern "C" void lcbk_final_exp_check(dim3 grid, hipStream_t s, u32 *park, u32 n, uint8_t *accept) {
     LCB_LAUNCH(k_final_exp_check, park, n, accept);
 }
-extern "C" void lcbk_tpke_partial_decrypt(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, const uint8_t *cts_u, const void *x_raw, u32 x_stride, u32 n_cts, uint8_t *ui_out, uint8_t *status) {
-    LCB_LAUNCH(k_tpke_partial_decrypt, lines, ct_ok, cts_u, (const fr *)x_raw, x_stride, n_cts, ui_out, status);
+extern "C" void lcbk_tpke_pd_miller(hipStream_t s, const u32 *lines, const uint8_t *ct_ok, const uint8_t *cts_u, u32 c0, u32 m, u32 *f_soa, uint8_t *status) {
+    dim3 grid((m + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_tpke_pd_miller, lines, ct_ok, cts_u, c0, m, f_soa, status);
+}
+extern "C" void lcbk_tpke_pd_mul(hipStream_t s, const uint8_t *cts_u, const void *x_raw, u32 x_stride, u32 c0, u32 m, const uint8_t *status, uint8_t *ui_out) {
+    dim3 grid((m + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_tpke_pd_mul, cts_u, (const fr *)x_raw, x_stride, c0, m, status, ui_out);
 }

@@ -18,22 +18,30 @@ extern "C" void lcbk_lineset_coop(hipStream_t s, u32 *lines, u32 n_sets, const u
 extern "C" void lcbk_tpke_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, u32 *f_soa, uint8_t *accept);
 extern "C" int lcbk_fe_slots();
 extern "C" void lcbk_final_exp_check(dim3 grid, hipStream_t s, u32 *park, u32 n, uint8_t *accept);
-extern "C" void lcbk_tpke_partial_decrypt(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, const uint8_t *cts_u, const void *x_raw, u32 x_stride, u32 n_cts, uint8_t *ui_out, uint8_t *status);
+// TPKE partial decryption over ciphertexts c0 + [0, m): Miller loop into f_soa (m x 576 B x lcbk_fe_slots()), then
+// lcbk_final_exp_check(f_soa, m, status + c0), then the ladder
+extern "C" void lcbk_tpke_pd_miller(hipStream_t s, const u32 *lines, const uint8_t *ct_ok, const uint8_t *cts_u, u32 c0, u32 m, u32 *f_soa, uint8_t *status);
+extern "C" void lcbk_tpke_pd_mul(hipStream_t s, const uint8_t *cts_u, const void *x_raw, u32 x_stride, u32 c0, u32 m, const uint8_t *status, uint8_t *ui_out);
 extern "C" void lcbk_ts_msg_prepare(dim3 grid, hipStream_t s, const uint8_t *msg_data, const u32 *msg_off, u32 n_msgs, u32 *lines, uint8_t *msg_ok, int orig_cof);
 extern "C" void lcbk_ts_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *msg_ok, u32 n_msgs, const void *pks, u32 n_pks, const uint8_t *sigs, const u32 *msg_idx, const u32 *pk_idx, u32 n, u32 *f_soa, uint8_t *accept);
 extern "C" void lcbk_coin_fold(dim3 grid, hipStream_t s, const uint8_t *sigs, u32 n, uint8_t *parity, uint64_t *nonce);
 extern "C" void lcbk_select_first_valid(dim3 grid, hipStream_t s, const uint8_t *accept, const uint8_t *pts, u32 pbytes, u32 per_group, u32 k, u32 n_groups, uint8_t *xs, uint8_t *ys, u32 *off, const u32 *order, u32 *src);
-extern "C" void lcbk_g1_mul(dim3 grid, hipStream_t s, const uint8_t *pts, int use_gen, const uint8_t *scalars, u32 n, uint8_t *out, uint8_t *ok_out);
-extern "C" void lcbk_g2_mul(dim3 grid, hipStream_t s, const uint8_t *pts, int use_gen, const uint8_t *scalars, u32 n, uint8_t *out, uint8_t *ok_out);
+// scalar-multiplication lanes (persistent grids, window tables in the workspace of lcbk_scalar_ws_bytes: 1 = G1, 2 = G2,
+// 3 = TPKE encrypt phase 1)
+extern "C" size_t lcbk_scalar_ws_bytes(int which, u32 n);
+extern "C" void lcbk_g1_mul(hipStream_t s, const uint8_t *pts, int use_gen, const uint8_t *scalars, u32 n, uint8_t *out, uint8_t *ok_out, u32 *ws);
+extern "C" void lcbk_g2_mul(hipStream_t s, const uint8_t *pts, int use_gen, const uint8_t *scalars, u32 n, uint8_t *out, uint8_t *ok_out, u32 *ws);
 extern "C" void lcbk_g2_hash(dim3 grid, hipStream_t s, const uint8_t *msg_data, const u32 *msg_off, u32 n, uint8_t *out, uint8_t *ok_out, int orig_cof);
-extern "C" void lcbk_tpke_encrypt1(dim3 grid, hipStream_t s, const uint8_t *ybytes, const uint8_t *rs, u32 n, uint8_t *u_out, uint8_t *t_out, uint8_t *ok_out);
+extern "C" void lcbk_tpke_encrypt1(hipStream_t s, const uint8_t *ybytes, const uint8_t *rs, u32 n, uint8_t *u_out, uint8_t *t_out, uint8_t *ok_out, u32 *ws);
 extern "C" void lcbk_tpke_encrypt2(dim3 grid, hipStream_t s, const uint8_t *u, const uint8_t *rs, const uint8_t *v_data, const u32 *v_off, u32 n, uint8_t *w_out, uint8_t *ok_out, int orig_cof);
 extern "C" void lcbk_ts_sign(dim3 grid, hipStream_t s, const uint8_t *sks, const uint8_t *msg_data, const u32 *msg_off, const u32 *msg_idx, u32 n, uint8_t *out, uint8_t *ok_out, int orig_cof);
 extern "C" void lcbk_lagrange_coeffs(dim3 grid, hipStream_t s, const uint8_t *xs, const u32 *off, u32 n_problems, void *lam_raw, uint8_t *status);
-extern "C" void lcbk_g1_mul_lanes(dim3 grid, hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out);
-extern "C" void lcbk_g2_mul_lanes(dim3 grid, hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out, const void *dec, u32 n_dec, const u32 *src);
+// Lagrange lanes (persistent grids, tables in the workspace `ws` of lcbk_lanes_ws_bytes: 1 = G1, 2 = G2, 3 = paired G2)
+extern "C" size_t lcbk_lanes_ws_bytes(int which, u32 n_entries);
+extern "C" void lcbk_g1_mul_lanes(hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out, u32 *ws);
+extern "C" void lcbk_g2_mul_lanes(hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out, const void *dec, u32 n_dec, const u32 *src, u32 *ws);
 // two entries per lane (n_entries even, problems at even offsets): shared doublings for two points of G2
-extern "C" void lcbk_g2_mul2_lanes(hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out, const void *dec, u32 n_dec, const u32 *src);
+extern "C" void lcbk_g2_mul2_lanes(hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out, const void *dec, u32 n_dec, const u32 *src, u32 *ws);
 extern "C" void lcbk_g1_sum(dim3 grid, hipStream_t s, const void *parts, const uint8_t *ok_in, const u32 *off, u32 n_problems, uint8_t *status, uint8_t *out);
 extern "C" void lcbk_g2_sum(dim3 grid, hipStream_t s, const void *parts, const uint8_t *ok_in, const u32 *off, u32 n_problems, uint8_t *status, uint8_t *out);
 extern "C" void lcbk_msm_digits(dim3 grid, hipStream_t s, const uint8_t *scalars, u32 n, u32 c, u32 nwin, u32 *keys, u32 *vals);
@@ -94,7 +102,8 @@ extern "C" void lcbk_rlc_census_stats(hipStream_t s, const u32 *key_idx, u32 m, 
 extern "C" void lcbk_rlc_suspect_split(hipStream_t s, const void *desc, u32 n_groups, const u32 *key_idx, u32 n_keys, const u32 *susp, const uint8_t *accept, void *out, u32 *count);
 extern "C" size_t lcbk_ts_grp_bytes();
 extern "C" void lcbk_coop_tpke_miller(hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups, u32 *f_soa, uint8_t *gacc, uint8_t *fb, u32 npairs);
-extern "C" void lcbk_mcl_g1_terms(hipStream_t s, const void *pts, const void *scal, u32 n, void *terms);
+extern "C" size_t lcbk_mcl_terms_ws_bytes(u32 n);
+extern "C" void lcbk_mcl_g1_terms(hipStream_t s, const void *pts, const void *scal, u32 n, void *terms, u32 *ws);
 extern "C" void lcbk_mcl_horner(hipStream_t s, int g, const u32 *coef, u32 n, const void *x_raw, u32 *out);
 extern "C" void lcbk_mcl_g1_sum(hipStream_t s, const void *in, u32 n, void *out);
 extern "C" void lcbk_mcl_from_bytes(hipStream_t s, int g, const uint8_t *in, u32 n, u32 *out, uint8_t *ok);

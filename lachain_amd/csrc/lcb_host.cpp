@@ -245,6 +245,95 @@ extern "C" int lcb_set_line_mode(int general) {
 }
 extern "C" const char *lcb_last_error(void) { return g_err.c_str(); }
 
+// ================================================================== the scratch gate (kcommon.hpp LCB_LAUNCH_GATED)
+// Launches whose scratch reservation (private segment per lane x the lanes of min(dispatch waves, device wave slots))
+// reaches the threshold are serialized onto one stream per device: the launch waits for the caller's stream, the
+// caller's stream then waits for the launch, and the per-device mutex orders the crossings of concurrent callers.
+namespace {
+struct GateDev {
+    std::mutex mu;
+    hipStream_t s = nullptr;
+    hipEvent_t in = nullptr, out = nullptr;
+    int cus = 0;
+};
+GateDev g_gate[64];
+std::atomic<long long> g_gate_bytes{-2};            // -2: not read from LCB_SCRATCH_GATE_MB yet
+std::atomic<unsigned long long> g_gate_routed{0}, g_gate_seen{0};
+thread_local int t_gate_dev = -1;                   // device whose gate mutex this thread holds (-1: none)
+long long gate_threshold() {
+    long long v = g_gate_bytes.load(std::memory_order_relaxed);
+    if (v != -2) return v;
+    const char *e = getenv("LCB_SCRATCH_GATE_MB");
+    v = e && *e ? atoll(e) * (1ll << 20) : (4ll << 30);   // default: 4 GiB of reservation
+    long long expect = -2;
+    g_gate_bytes.compare_exchange_strong(expect, v);
+    return g_gate_bytes.load();
+}
+}  // namespace
+extern "C" hipStream_t lcb_gate_enter(const void *kern, long long *scratch_cache, size_t lanes, hipStream_t s) {
+    long long sc = __atomic_load_n(scratch_cache, __ATOMIC_RELAXED);
+    if (sc < 0) {
+        hipFuncAttributes a;
+        sc = hipFuncGetAttributes(&a, kern) == hipSuccess ? (long long)a.localSizeBytes : 0;
+        __atomic_store_n(scratch_cache, sc, __ATOMIC_RELAXED);
+    }
+    g_gate_seen.fetch_add(1, std::memory_order_relaxed);
+    const long long thr = gate_threshold();
+    if (sc == 0 || thr < 0 || lanes == 0) return s;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return s;
+    GateDev &g = g_gate[dev];
+    if (!g.cus) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+        __atomic_store_n(&g.cus, cus, __ATOMIC_RELAXED);
+    }
+    const size_t waves = (lanes + 63) / 64, slots = (size_t)g.cus * 32;
+    const long long reserve = sc * 64 * (long long)std::min(waves, slots);
+    if (reserve < thr) return s;
+    g.mu.lock();
+    if (!g.s && (hipStreamCreateWithFlags(&g.s, hipStreamNonBlocking) != hipSuccess ||
+                 hipEventCreateWithFlags(&g.in, hipEventDisableTiming) != hipSuccess ||
+                 hipEventCreateWithFlags(&g.out, hipEventDisableTiming) != hipSuccess)) {
+        g.s = nullptr;          // (the launch stays on the caller's stream)
+        g.mu.unlock();
+        return s;
+    }
+    t_gate_dev = dev;
+    g_gate_routed.fetch_add(1, std::memory_order_relaxed);
+    (void)hipEventRecord(g.in, s);
+    (void)hipStreamWaitEvent(g.s, g.in, 0);
+    return g.s;
+}
+extern "C" void lcb_gate_exit(hipStream_t s, hipStream_t used) {
+    if (used == s || t_gate_dev < 0) return;
+    GateDev &g = g_gate[t_gate_dev];
+    (void)hipEventRecord(g.out, used);
+    (void)hipStreamWaitEvent(s, g.out, 0);
+    t_gate_dev = -1;
+    g.mu.unlock();
+}
+// tuning / test hook: the gate's threshold in bytes of reservation (-1: off, 0: every launch with scratch is routed)
+extern "C" int lcb_set_scratch_gate(long long bytes) {
+    if (!tuning_allowed("lcb_set_scratch_gate")) return -1;
+    gate_threshold();
+    g_gate_bytes.store(bytes < 0 ? -1 : bytes);
+    return 0;
+}
+// test hook: at most this many blocks in the persistent grids (lanetab.hpp workspaces), so a small batch walks several
+// items per lane; 0 = as many as are resident
+std::atomic<uint32_t> g_persist_cap{0};
+extern "C" uint32_t lcb_persist_cap(void) { return g_persist_cap.load(std::memory_order_relaxed); }
+extern "C" int lcb_set_persist_blocks(uint32_t max_blocks) {
+    if (!tuning_allowed("lcb_set_persist_blocks")) return -1;
+    g_persist_cap.store(max_blocks);
+    return 0;
+}
+extern "C" void lcb_scratch_gate_stats(uint64_t *routed, uint64_t *seen) {
+    if (routed) *routed = g_gate_routed.load();
+    if (seen) *seen = g_gate_seen.load();
+}
+
 extern "C" int mclBn_init(int curve, int compiledTimeVar) {
     if (curve != MCL_BLS12_381 || compiledTimeVar != MCLBN_COMPILED_TIME_VAR) {
         set_err("unsupported curve / compiledTimeVar");
@@ -722,6 +811,7 @@ void ctx_free(lcb_ctx *c) {
     for (DevBuf *b : {&c->t_lines, &c->t_ctok, &c->t_keys, &c->t_f, &c->s_lines, &c->s_mok, &c->s_keys, &c->s_f})
         b->release();
     for (auto &b : c->lag) b.release();
+    c->lws.release();
     for (auto &b : c->sel) b.release();
     for (auto &b : c->msm) b.release();
     for (auto &b : c->in) b.release();
@@ -928,9 +1018,14 @@ int tpke_verify_prepared(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_keys,
 int tpke_partial_decrypt_prepared(lcb_ctx *c, uint8_t *ui_out, uint8_t *status, const uint8_t *x_raw, size_t x_stride,
                                   const uint8_t *cts_u, size_t n_cts, hipStream_t s) {
     if (!tpke_shape_ok(c, c->t_n_keys, n_cts, "tpke partial decrypt")) return -1;
-    if (n_cts)
-        lcbk_tpke_partial_decrypt(dim3(nblk(n_cts)), s, (const u32 *)c->t_lines.p, (const uint8_t *)c->t_ctok.p, cts_u,
-                                  x_raw, (u32)x_stride, (u32)n_cts, ui_out, status);
+    for (size_t o = 0; o < n_cts; o += LCB_VERIFY_CHUNK) {
+        const size_t m = std::min(LCB_VERIFY_CHUNK, n_cts - o);
+        u32 *f = (u32 *)c->t_f.get(m * 576 * (size_t)lcbk_fe_slots());
+        if (!f) { set_err("device allocation failed"); return -1; }
+        lcbk_tpke_pd_miller(s, (const u32 *)c->t_lines.p, (const uint8_t *)c->t_ctok.p, cts_u, (u32)o, (u32)m, f, status);
+        lcbk_final_exp_check(dim3(nblk(m)), s, f, (u32)m, status + o);
+        lcbk_tpke_pd_mul(s, cts_u, x_raw, (u32)x_stride, (u32)o, (u32)m, status, ui_out);
+    }
     return launched("tpke partial decrypt launch") ? 0 : -1;
 }
 
@@ -1563,12 +1658,15 @@ int lagrange_enqueue(lcb_ctx *c, int g, uint8_t *dout, uint8_t *dst, const uint8
     if (!lam || !parts || !pok) { set_err("device allocation failed"); return -1; }
     lcbk_lagrange_coeffs(dim3(nblk(np)), s, dx, doff, (u32)np, lam, dst);
     if (ne) {
-        if (g == 1) lcbk_g1_mul_lanes(dim3(nblk(ne)), s, dy, lam, (u32)ne, parts, pok);
-        else if (pairs)   // even problem offsets (assembly with even k): two entries per lane, shared doublings
+        const int which = g == 1 ? 1 : pairs ? 3 : 2;   // pairs: even problem offsets (assembly with even k)
+        u32 *ws = (u32 *)c->lag[3].get(lcbk_lanes_ws_bytes(which, (u32)ne));
+        if (!ws) { set_err("device allocation failed (Lagrange lanes workspace)"); return -1; }
+        if (g == 1) lcbk_g1_mul_lanes(s, dy, lam, (u32)ne, parts, pok, ws);
+        else if (pairs)   // two entries per lane, shared doublings
             lcbk_g2_mul2_lanes(s, dy, lam, (u32)ne, parts, pok, src ? c->s_dec.p : nullptr,
-                               (u32)std::min<size_t>(c->s_dec_n, 0xffffffffu), src);
-        else lcbk_g2_mul_lanes(dim3(nblk(ne)), s, dy, lam, (u32)ne, parts, pok, src ? c->s_dec.p : nullptr,
-                               (u32)std::min<size_t>(c->s_dec_n, 0xffffffffu), src);
+                               (u32)std::min<size_t>(c->s_dec_n, 0xffffffffu), src, ws);
+        else lcbk_g2_mul_lanes(s, dy, lam, (u32)ne, parts, pok, src ? c->s_dec.p : nullptr,
+                               (u32)std::min<size_t>(c->s_dec_n, 0xffffffffu), src, ws);
     }
     if (g == 1) lcbk_g1_sum(dim3(nblk(np)), s, parts, pok, doff, (u32)np, dst, dout);
     else lcbk_g2_sum(dim3(nblk(np)), s, parts, pok, doff, (u32)np, dst, dout);
@@ -2186,8 +2284,9 @@ extern "C" int lcb_tpke_encrypt_phase1(uint8_t *u_out, uint8_t *t_out, const uin
     const uint8_t *dy = up(c->in[0], y, 48, s);
     const uint8_t *dr = up(c->in[1], r, 32 * n, s);
     uint8_t *du = (uint8_t *)c->out[0].get(48 * n), *dt = (uint8_t *)c->out[1].get(48 * n), *dok = (uint8_t *)c->out[2].get(n);
-    if (!dy || !dr || !du || !dt || !dok) { set_err("device allocation failed"); return -1; }
-    lcbk_tpke_encrypt1(dim3(nblk(n)), s, dy, dr, (u32)n, du, dt, dok);
+    u32 *ws = (u32 *)c->lws.get(lcbk_scalar_ws_bytes(3, (u32)n));
+    if (!dy || !dr || !du || !dt || !dok || !ws) { set_err("device allocation failed"); return -1; }
+    lcbk_tpke_encrypt1(s, dy, dr, (u32)n, du, dt, dok, ws);
     std::vector<uint8_t> ok(n);
     hipMemcpyAsync(u_out, du, 48 * n, hipMemcpyDeviceToHost, s);
     hipMemcpyAsync(t_out, dt, 48 * n, hipMemcpyDeviceToHost, s);
@@ -2793,8 +2892,9 @@ static bool g1_mulvec(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y, mclSize n)
     uint8_t *terms = (uint8_t *)c->mcl[2].get(LCB_G1_JAC_BYTES * n);
     uint8_t *tmp = (uint8_t *)c->mcl[3].get(LCB_G1_JAC_BYTES * ((n + 255) / 256));
     uint8_t *dz = (uint8_t *)c->mcl[5].get(LCB_G1_JAC_BYTES);
-    if (!pts || !sc || !terms || !tmp || !dz) { set_err("device allocation failed"); return false; }
-    lcbk_mcl_g1_terms(s, pts, sc, (u32)n, terms);
+    u32 *ws = (u32 *)c->lws.get(lcbk_mcl_terms_ws_bytes((u32)n));
+    if (!pts || !sc || !terms || !tmp || !dz || !ws) { set_err("device allocation failed"); return false; }
+    lcbk_mcl_g1_terms(s, pts, sc, (u32)n, terms, ws);
     uint8_t *cur = terms;
     size_t cnt = n;
     while (cnt > 256) {
@@ -2893,9 +2993,10 @@ static int mul_batch(int g, uint8_t *out, const uint8_t *points, int use_gen, co
     const uint8_t *dp = use_gen ? (const uint8_t *)c->in[0].get(16) : up(c->in[0], points, pb * n, s);
     const uint8_t *dsc = up(c->in[1], scalars, 32 * n, s);
     uint8_t *dout = (uint8_t *)c->out[0].get(pb * n), *dok = (uint8_t *)c->out[1].get(n);
-    if (!dp || !dsc || !dout || !dok) { set_err("device allocation failed"); return -1; }
-    if (g == 1) lcbk_g1_mul(dim3(nblk(n)), s, dp, use_gen, dsc, (u32)n, dout, dok);
-    else lcbk_g2_mul(dim3(nblk(n)), s, dp, use_gen, dsc, (u32)n, dout, dok);
+    u32 *ws = (u32 *)c->lws.get(lcbk_scalar_ws_bytes(g, (u32)n));
+    if (!dp || !dsc || !dout || !dok || !ws) { set_err("device allocation failed"); return -1; }
+    if (g == 1) lcbk_g1_mul(s, dp, use_gen, dsc, (u32)n, dout, dok, ws);
+    else lcbk_g2_mul(s, dp, use_gen, dsc, (u32)n, dout, dok, ws);
     std::vector<uint8_t> ok(n);
     hipMemcpyAsync(out, dout, pb * n, hipMemcpyDeviceToHost, s);
     hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, s);

@@ -93,6 +93,9 @@ _SIGS = {
     "lcb_set_batch_seed": (None, [ctypes.c_char_p]),
     "lcb_set_batch_census": (None, [c_size]),
     "lcb_set_coop_max": (ctypes.c_int, [ctypes.c_uint32]),
+    "lcb_set_scratch_gate": (ctypes.c_int, [ctypes.c_longlong]),
+    "lcb_scratch_gate_stats": (None, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "lcb_set_persist_blocks": (ctypes.c_int, [ctypes.c_uint32]),
     "lcb_set_fork_mode": (ctypes.c_int, [ctypes.c_int]),
     "lcb_set_coop_miller_max": (ctypes.c_int, [ctypes.c_uint32]),
     "lcb_debug_coop_op": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
@@ -802,6 +805,24 @@ def set_msm_segments(max_segments):
 def set_msm_chunk(records_per_lane):
     """records per lane of the MSM bucket accumulation (0: one lane per bucket)"""
     _tuning(lib().lcb_set_msm_chunk(int(records_per_lane)), "set_msm_chunk")
+
+
+def set_scratch_gate(nbytes):
+    """launches whose scratch reservation reaches nbytes run on the device's gate stream (-1 = off, 0 = every launch
+    with scratch; default 4 GiB): include/lachain_bls.h lcb_set_scratch_gate"""
+    _tuning(lib().lcb_set_scratch_gate(int(nbytes)), "set_scratch_gate")
+
+
+def scratch_gate_stats():
+    """(launches routed through the scratch gate, launches checked) since the process started"""
+    a, b = ctypes.c_uint64(), ctypes.c_uint64()
+    lib().lcb_scratch_gate_stats(ctypes.byref(a), ctypes.byref(b))
+    return a.value, b.value
+
+
+def set_persist_blocks(max_blocks):
+    """at most max_blocks blocks in the persistent table-walking grids (0 = as many as are resident)"""
+    _tuning(lib().lcb_set_persist_blocks(int(max_blocks)), "set_persist_blocks")
 
 
 def set_coop_max(max_checks):

@@ -22,10 +22,13 @@ def _free_port():
 
 
 def test_bench_world_size_two():
-    # HIP's default four hardware queues per rank: with bench.py's eight, the two ranks' 16 queues on the one GPU
-    # exhausted the scratch pool (HSA_STATUS_ERROR_OUT_OF_RESOURCES at a 7.6 KB-per-lane dispatch, profiles/r04/r04f);
-    # the driver's N > 1 runs have one rank per GPU
-    env = dict(os.environ, LCB_BENCH_BACKEND="gloo", OMP_NUM_THREADS="4", LCB_BENCH_HWQ="4")
+    # bench.py's default hardware queues (eight per rank: 16 on the one GPU) and its default concurrent epoch replay.
+    # Round 4 ran this at four queues because a 7.6 KB-per-lane dispatch (k_tpke_partial_decrypt) exhausted the scratch
+    # resources with 16 (HSA_STATUS_ERROR_OUT_OF_RESOURCES, profiles/r04/r04f); round 5 holds every multi-wave kernel
+    # to <= 4 KB (tests/test_kernel_resources.py) and gates larger reservations (lcb_set_scratch_gate)
+    env = dict(os.environ, LCB_BENCH_BACKEND="gloo", OMP_NUM_THREADS="4")
+    env.pop("GPU_MAX_HW_QUEUES", None)
+    env.pop("LCB_BENCH_HWQ", None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "1", "--warmup", "1", "--shares", "8800", "--pattern-steps", "1",

@@ -23,45 +23,58 @@ BUDGET = {
     "k_dkg_exact_terms": (0, 408),
     "k_dkg_horner": (0, 896),
     "k_dkg_rows": (0, 312),
-    "k_final_exp_check": (0, 3864),
+    "k_final_exp_check": (0, 3880),
     "k_g1_decompress": (0, 800),
     "k_g1_jac_compress": (0, 704),
     "k_g1_jac_reduce_block": (0, 456),
     "k_g1_jac_reduce_groups": (0, 168),
-    "k_g1_mul": (0, 5568),
-    "k_g1_mul_lanes": (0, 5424),
+    "k_g1_mul": (0, 1040),
+    "k_g1_mul_lanes": (0, 896),
     "k_g1_subgroup_any": (12, 0),
     "k_g1_sum": (0, 752),
     "k_g1_to_affine": (0, 704),
     "k_g2_decompress": (0, 992),
     "k_g2_hash": (0, 3352),
-    "k_mcl_g2_hash": (0, 3352),               # mclBnG2_hashAndMapTo: the same one-lane hash as k_g2_hash
-    "k_g2_mul": (206, 10624),
-    "k_g2_mul_lanes": (1300, 10288),
-    "k_g2_mul2_lanes": (4530, 22672),         # two GLS tables (31 entries) per lane: the assembly's paired lanes
+    "k_g2_mul": (302, 1584),                  # 4-bit window, table in the lanetab workspace (was 10,624 B)
+    "k_g2_mul2_lanes": (4660, 2000),          # paired GLS ladders, tables in the lanetab workspace (was 22,672 B of scratch)
+    "k_g2_mul_lanes": (1212, 1424),           # GLS ladder, table in the lanetab workspace (was 10,288 B)
     "k_g2_sum": (204, 1008),
-    "k_lineset_fill": (0, 1256),
     "k_lineset_coop": (86, 280),              # five-lane line sets (latency path): T, Q, acc and five products live
+    "k_lineset_fill": (0, 1256),
+    "k_mcl_from_bytes": (0, 800),
+    "k_mcl_g1_sum": (0, 168),
+    "k_mcl_g1_terms": (0, 880),
+    "k_mcl_g2_hash": (0, 3352),               # mclBnG2_hashAndMapTo: the same one-lane hash as k_g2_hash
+    "k_mcl_horner": (0, 1320),
+    "k_mcl_to_bytes": (0, 1008),
+    "k_msm_bucket_fix": (0, 168),
     "k_msm_bucket_reduce": (0, 744),          # + the prefetched next bucket
     "k_msm_horner": (0, 168),
-    "k_msm_bucket_fix": (0, 168),
-    "k_op": (3098, 8484),
-    "k_ptmul_g2": (32, 68),                   # mcl G2 multiplication latency kernel: four ladder lanes share each op                     # mcl single-element surface: every operation in one kernel
-    "k_rlc_key_tables": (12, 768),            # k_rlc_rand.hip: spills to scratch, not AGPRs (<= 256 registers)
+    "k_op_debug": (96, 6956),
+    "k_op_grp": (408, 4104),
+    "k_op_gt": (1788, 8148),                  # single-lane mcl operations (one wave per dispatch), one kernel per family
+    "k_op_pair": (830, 7572),
+    "k_ptmul_g2": (32, 68),                   # mcl G2 multiplication latency kernel: four ladder lanes share each op
+    "k_rlc_key_tables": (12, 168),            # k_rlc_rand.hip: spills to scratch, not AGPRs (<= 256 registers)
     "k_rlc_miller_fallback": (0, 2376),
     "k_rlc_search": (93, 2264),
-    "k_tpke_rlc_search2a": (97, 3448),         # level-2 searches: four Fp12 values per lane, four lanes per group
-    "k_tpke_rlc_search2b": (133, 4088),
     "k_secp_scalars": (0, 528),
     "k_tpke_ct_prepare": (0, 3752),
-    "k_tpke_encrypt1": (0, 6432),
+    "k_tpke_ct_prepare_h": (0, 3640),
+    "k_tpke_ct_prepare_w": (0, 1352),
+    "k_tpke_encrypt1": (0, 1184),
     "k_tpke_encrypt2": (0, 3928),
+    "k_tpke_exact_points": (0, 704),
     "k_tpke_miller": (348, 2616),
-    "k_tpke_partial_decrypt": (972, 7652),
-    "k_tpke_rlc_miller": (360, 2616),
+    "k_tpke_pd_miller": (962, 2664),          # partial decryption split in three (was k_tpke_partial_decrypt, 7,652 B)
+    "k_tpke_pd_mul": (0, 992),
+    "k_tpke_rlc_miller": (324, 2616),
     "k_tpke_rlc_points": (60, 1216),          # k_rlc_rand.hip: 248 registers, two waves per SIMD
-    "k_tpke_rlc_sum": (0, 1328),
+    "k_tpke_rlc_search2a": (97, 3448),        # level-2 searches: four Fp12 values per lane, four lanes per group
+    "k_tpke_rlc_search2b": (0, 3656),
+    "k_tpke_rlc_sum": (0, 1168),
     "k_tpke_rlc_wsum": (0, 576),
+    "k_tpke_rlc_wsum2": (0, 648),
     "k_ts_miller": (1248, 3292),
     "k_ts_msg_prepare": (0, 3640),
     "k_ts_rlc_miller": (0, 2524),
@@ -70,6 +83,11 @@ BUDGET = {
     "k_ts_rlc_wsum": (12, 992),
     "k_ts_sign": (0, 3928),
 }
+# Round 5: no kernel that runs on more than one wave may take more than 4 KB of scratch per lane — the
+# HIP runtime reserves a dispatch's scratch for min(waves, device wave slots) waves per hardware queue, and the 22.7 KB
+# paired G2 lanes aborted processes with HSA_STATUS_ERROR_OUT_OF_RESOURCES.  The single-lane kernels below run one wave.
+SCRATCH_CAP = 4096
+SINGLE_WAVE = {"k_op_grp", "k_op_pair", "k_op_gt", "k_op_debug", "k_coop_debug"}
 ZERO_SPILL = ["k_coop_tpke_miller", "k_coop_final_exp_check", "k_msm_bucket_acc", "k_secp_verify",
               "k_rlc_census_stats", "k_rlc_suspect_split", "k_rlc_resolve", "k_tpke_rlc_sum", "k_ts_rlc_miller"]
 
@@ -103,3 +121,10 @@ def test_hot_kernels_do_not_spill(resources):
     for name in ZERO_SPILL:
         assert name in resources, name
         assert resources[name]["vgpr_spill_count"] == 0, name
+
+
+def test_multi_wave_kernels_within_4kb_scratch(resources):
+    over = [(n, r["private_segment_fixed_size"]) for n, r in resources.items()
+            if not n.startswith(("lcb_asm_", "_Z")) and n not in SINGLE_WAVE
+            and r["private_segment_fixed_size"] > SCRATCH_CAP]
+    assert not over, over
