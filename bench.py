@@ -1691,8 +1691,9 @@ def compact_line(full):
                                                                 "roofline_frac")}
         line["config"]["batches_in_flight"] = tb.get("pipeline")
         line["config"]["single_batch_latency_ms"] = _r(tb.get("single_batch_ms"))
-    if cfg.get("hw_queues"):
-        line["config"]["hw_queues"] = cfg["hw_queues"]
+    for k in ("hw_queues", "hw_queues_env"):
+        if cfg.get(k):
+            line["config"][k] = cfg[k]
     s = {}
     byz = full.get("tpke_byzantine")
     if byz:
@@ -1768,9 +1769,9 @@ def main():
                     help="batched verify: concurrent parts (contexts / streams / host threads) per step; measured "
                          "no faster with 2 or 3 parts (147 - 159 vs 145 ms per 1M shares)")
     ap.add_argument("--hw-queues", type=int, default=int(os.environ.get("LCB_BENCH_HWQ", "8")),
-                    help="GPU_MAX_HW_QUEUES for this process when the environment does not set it (an operator's "
-                         "setting, e.g. 4 on a shared GPU, is kept; 0: never set it); 8 measured 12.30 vs 11.95 M "
-                         "shares/s with two batches in flight, profiles/r04/q2")
+                    help="GPU_MAX_HW_QUEUES for this process (0: keep the environment's; 8 measured 12.30 vs 11.95 M "
+                         "shares/s with two batches in flight, profiles/r04/q2).  The environment's value is recorded "
+                         "in the line (config.hw_queues_env) beside the one used (config.hw_queues)")
     ap.add_argument("--tpke-pipeline", type=int, default=2,
                     help="batched verify: whole batches in flight (each on its own context / stream / host thread); "
                          "2 measured 12.3 vs 10.6 M shares/s for one at a time, 3 no better (profiles/r04/q1, q2)")
@@ -1818,10 +1819,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.hw_queues > 0 and not os.environ.get("GPU_MAX_HW_QUEUES"):
+    HWQ_ENV = os.environ.get("GPU_MAX_HW_QUEUES")
+    if args.hw_queues > 0:
         # hardware queues per process, read when the HIP runtime starts (before torch / the library touch the GPU):
-        # the batched call uses five streams per context, so batches in flight need more than HIP's default four;
-        # an explicit setting in the environment wins
+        # the batched call uses five streams per context, so batches in flight need more than HIP's default four.
+        # The GPU boxes export HIP's default (4) in the environment, so an environment value cannot tell an operator's
+        # choice from the default: --hw-queues 0 keeps it, and the line records both
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, args.hw_queues))
     import torch
     import torch.distributed as dist
@@ -2032,7 +2035,7 @@ def main():
                        "shares_per_rank": n, "ciphertexts_per_rank": n_cts, "decryptors": n_dec, "degree": args.f,
                        "v_bytes": args.vlen, "corrupted_fraction": 0.01, "parallelism": f"shard{world}",
                        "decision_mismatches": head["decision_mismatches"], "algorithm": algo, "api": head["api"],
-                       "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")},
+                       "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"), "hw_queues_env": HWQ_ENV},
             "roofline": roofline,
             "source_hash": src_hash,
             "cpu_baseline": cpu_line,

@@ -11,7 +11,7 @@ LCB_TU_CONFIG(k_scalar)
 template <class F>
 DI void scalar_mul_lanes(const uint8_t *pts, int use_gen, const uint8_t *scalars, u32 n, uint8_t *out, uint8_t *ok_out,
                          u32 *ws) {
-    constexpr u32 PB = sizeof(F) * 2;           // wire bytes: 48 (G1) / 96 (G2)
+    constexpr u32 PB = sizeof(F);               // wire bytes: 48 (G1) / 96 (G2), one coordinate
     const u32 gid = blockIdx.x * blockDim.x + threadIdx.x, gsz = gridDim.x * blockDim.x;
     char *slot = lw_slot(ws, LW_WIN4_QUADS(F), gid);
 #pragma unroll 1
