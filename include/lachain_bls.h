@@ -337,6 +337,10 @@ int lcb_set_coop_max(uint32_t max_checks);
 /* the cooperative threshold of the group Miller loops alone (default 65536; the final exponentiations keep
    lcb_set_coop_max's) */
 int lcb_set_coop_miller_max(uint32_t max_checks);
+/* shares / group checks per Miller + final-exponentiation launch pair (default and maximum 2^21): a test hook that
+   makes small batches run several chunks (chunk offsets in the copies and searches).  Set it only while no batch call
+   is in flight.  Tuning hook (LCB_ALLOW_TUNING=1). */
+int lcb_set_verify_chunk(size_t checks);
 /* stream layout of the fused batched verifies (lcb_tpke_verify_shares_batched_dev, lcb_ts_verify_shares_batched_dev):
    0 = randomisation on the context's second stream beside the preparation on the caller's; 1 (default) = the
    latency-bound preparation chain (hash-to-G2, line sets, census) on a high-priority stream and the randomisation on

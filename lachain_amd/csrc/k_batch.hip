@@ -36,6 +36,9 @@
 
 LCB_ASM_LIBRARY(k_batch)
 LCB_TU_CONFIG(k_batch)
+#ifndef LCB_SEARCH2B_BY_POSITION
+#define LCB_SEARCH2B_BY_POSITION 0
+#endif
 
 // ---------------------------------------------------------------- level-1 groups: runs of one ciphertext / message
 // one lane per share; the first share of a run emits the run as groups of at most `cap` shares.
@@ -446,7 +449,11 @@ extern "C" __global__ void __launch_bounds__(64) k_tpke_rlc_search2b(const uint4
     fp12_load_row(b, gamma12 + (size_t)g * 144);
     fp12_mul_n(b, a, b);                                   // gamma_c^(c_j + 1)
     fp12_conj(b, b);
+#if LCB_SEARCH2B_BY_POSITION
+    fp12_load_row(a, gamma12 + ((size_t)ns + k) * 144);    // gamma_t of open check k (diagnostic variant)
+#else
     fp12_load_row(a, gamma12 + ((size_t)ns + g) * 144);    // gamma_t
+#endif
     fp12_cyc_sqr_n(a, a);
     fp12_mul_n(a, a, b);                                   // E_j = gamma_t^2 / gamma_c^(c_j + 1) = gamma_2 / gamma_c^(c_j)
     // E_j = D_j^c for some c in [1, len] (len <= 32): baby-step giant-step with m = 6 — 32-bit fingerprints of the
@@ -597,6 +604,11 @@ extern "C" void lcbk_tpke_rlc_search2a(hipStream_t s, const void *search, u32 ns
     dim3 grid((4 * ns + LCB_BLOCK - 1) / LCB_BLOCK);
     LCB_LAUNCH(k_tpke_rlc_search2a, (const uint4 *)search, ns, gamma0, gamma12, accept, open, open_count);
 }
+#ifndef LCB_SEARCH2B_BY_POSITION
+#define LCB_SEARCH2B_BY_POSITION 0
+#endif
+// 1: the diagnostic variant that reads gamma_t of open check k at row ns + k (the copy then writes rows by check)
+extern "C" int lcbk_search2b_by_position(void) { return LCB_SEARCH2B_BY_POSITION; }
 // n_open = *open_count (read by the host after search2a); gamma12 + 144 (ns + g) holds gamma_t of the open group g
 extern "C" void lcbk_tpke_rlc_search2b(hipStream_t s, const void *search, u32 ns, u32 n_open, const u32 *gamma0,
                                        const u32 *gamma12, const u32 *open, const u32 *open_count, uint8_t *accept,

@@ -928,7 +928,10 @@ bool sync_check(lcb_ctx *c, const char *what) {
 }
 
 // ------------------------------------------------------------------ TPKE
-#define LCB_VERIFY_CHUNK ((size_t)1 << 21)   // shares per Miller + final-exponentiation launch pair
+// shares / checks per Miller + final-exponentiation launch pair (bounds the park buffers); lcb_set_verify_chunk (test
+// hook) lowers it so small batches run several chunks — set it only while no batch call is in flight
+std::atomic<size_t> g_verify_chunk{(size_t)1 << 21};
+#define LCB_VERIFY_CHUNK (g_verify_chunk.load(std::memory_order_relaxed))
 #define LCB_CT_CACHE 1024                       // prepared-ciphertext cache slots per context (52.7 KB of lines each)
 
 int tpke_prepare(lcb_ctx *c, const uint8_t *d_y, size_t n_keys, const uint8_t *d_u, const uint8_t *d_w,
@@ -1208,6 +1211,34 @@ void rlc_sum_enqueue(const RlcKindInfo &K, RlcWs &w, const uint8_t *desc, u32 gr
                           groups <= 262144 ? 4u : 1u, K.okv, K.ctg2, K.keys, (u32)K.n_keys, io.d_key,
                           io.d_pts, w.rA, w.rB, (u32)n, gpts, d_accept, gex, wsum, susp, cval);
 }
+// Stage dump of the TPKE two-error search (test hook, LCB_ALLOW_TEST_HOOKS=1 and LCB_DUMP_SEARCH2B=<path prefix>):
+// before ("in") and after ("out") k_tpke_rlc_search2b, the open list, gamma_0 rows, gamma_c / gamma_t rows and the accept
+// bytes go to <prefix>.<stage>.<call>.bin — the header {ns, n_open, n, by_position} then the four arrays
+std::atomic<int> g_dump_calls{0};
+void search2b_dump(hipStream_t s, const char *stage, u32 ns, u32 no, const u32 *gamma, const u32 *g12, const u32 *open,
+                   const uint8_t *d_accept, size_t n) {
+    const char *pre = getenv("LCB_DUMP_SEARCH2B");
+    if (!pre || !*pre || !env_on("LCB_ALLOW_TEST_HOOKS")) return;
+    if (hipStreamSynchronize(s) != hipSuccess) return;
+    std::vector<u32> op(no + 4), g0((size_t)ns * 144), gg(2 * (size_t)ns * 144);
+    std::vector<uint8_t> acc(n);
+    hipMemcpy(op.data(), open, 4 * (no + 4), hipMemcpyDeviceToHost);
+    hipMemcpy(g0.data(), gamma, 4 * g0.size(), hipMemcpyDeviceToHost);
+    hipMemcpy(gg.data(), g12, 4 * gg.size(), hipMemcpyDeviceToHost);
+    hipMemcpy(acc.data(), d_accept, n, hipMemcpyDeviceToHost);
+    const int call = stage[0] == 'i' ? g_dump_calls.fetch_add(1) : g_dump_calls.load() - 1;
+    char path[512];
+    snprintf(path, sizeof path, "%s.%s.%d.bin", pre, stage, call);
+    FILE *fh = fopen(path, "wb");
+    if (!fh) return;
+    const u32 hdr[4] = {ns, no, (u32)n, (u32)lcbk_search2b_by_position()};
+    fwrite(hdr, 4, 4, fh);
+    fwrite(op.data(), 4, op.size(), fh);
+    fwrite(g0.data(), 4, g0.size(), fh);
+    fwrite(gg.data(), 4, gg.size(), fh);
+    fwrite(acc.data(), 1, acc.size(), fh);
+    fclose(fh);
+}
 // Miller + final exponentiation (+ resolve / search) over the groups of desc in chunks; gpts holds the points
 enum RlcStage { RLC_RESOLVE = 0, RLC_SEARCH = 1, RLC_COPY = 2 };   // after a chunk's checks: resolve / search / copy out
 void rlc_checks(lcb_ctx *c, const RlcKindInfo &K, RlcWs &w, const uint8_t *desc, u32 count, void *gpts, uint8_t *gacc,
@@ -1352,9 +1383,12 @@ int rlc_levels(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, size_t n, 
                     c->rlc_ms[0] += t;
                 // gamma_t of open group g -> row ns + g
                 rlc_checks(c, K, w, (const uint8_t *)(sdesc + ns), no, gp2, gacc2, f2, RLC_COPY, false, nullptr,
-                           sdesc + ns, g12 + (size_t)ns * 144, d_accept, io, s, open + 4);
+                           sdesc + ns, g12 + (size_t)ns * 144, d_accept, io, s,
+                           lcbk_search2b_by_position() ? nullptr : open + 4);
+                search2b_dump(s, "in", ns, no, gamma, g12, open, d_accept, n);
                 lcbk_tpke_rlc_search2b(s, sdesc, ns, no, gamma, g12, open + 4, open, d_accept, w.dB, w.cnt + 1,
                                        io.d_key, (u32)K.n_keys, w.susp);
+                search2b_dump(s, "out", ns, no, gamma, g12, open, d_accept, n);
             }
             if (!launched("batched verify launch")) return -1;
             if (!read_counts(cnt + 1, w.cnt + 1, 1, s)) return -1;
@@ -1934,6 +1968,12 @@ extern "C" int lcb_set_coop_max(uint32_t max_checks) {
     if (!tuning_allowed("lcb_set_coop_max")) return -1;
     g_coop_max.store(max_checks);
     g_coop_miller_max.store(max_checks);
+    return 0;
+}
+extern "C" int lcb_set_verify_chunk(size_t checks) {
+    if (!tuning_allowed("lcb_set_verify_chunk")) return -1;
+    if (checks == 0 || checks > ((size_t)1 << 21)) { set_err("lcb_set_verify_chunk: 1 .. 2^21"); return -1; }
+    g_verify_chunk.store(checks);
     return 0;
 }
 extern "C" int lcb_set_coop_miller_max(uint32_t max_checks) {

@@ -96,6 +96,7 @@ _SIGS = {
     "lcb_set_scratch_gate": (ctypes.c_int, [ctypes.c_longlong]),
     "lcb_scratch_gate_stats": (None, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "lcb_set_persist_blocks": (ctypes.c_int, [ctypes.c_uint32]),
+    "lcb_set_verify_chunk": (ctypes.c_int, [c_size]),
     "lcb_set_fork_mode": (ctypes.c_int, [ctypes.c_int]),
     "lcb_set_coop_miller_max": (ctypes.c_int, [ctypes.c_uint32]),
     "lcb_debug_coop_op": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
@@ -823,6 +824,11 @@ def scratch_gate_stats():
 def set_persist_blocks(max_blocks):
     """at most max_blocks blocks in the persistent table-walking grids (0 = as many as are resident)"""
     _tuning(lib().lcb_set_persist_blocks(int(max_blocks)), "set_persist_blocks")
+
+
+def set_verify_chunk(checks):
+    """checks per Miller + final-exponentiation launch pair (default 2^21; a test hook for chunk offsets)"""
+    _tuning(lib().lcb_set_verify_chunk(int(checks)), "set_verify_chunk")
 
 
 def set_coop_max(max_checks):

@@ -185,6 +185,39 @@ def test_batched_two_error_location(nat, tdev, fused):
     assert levels == [8, 7, 6, 22], levels
 
 
+@pytest.mark.parametrize("chunk", [0, 1000])
+def test_batched_two_error_groups_out_of_order(nat, tdev, chunk):
+    """VERDICT r4 #2 / ADVICE r4: the two-error search over thousands of open groups whose open-list order (atomic
+    appends from the one-error search's waves) differs from the group order, and (chunk = 1000, lcb_set_verify_chunk)
+    more open groups than one Miller + final-exponentiation chunk, so the gamma_t copy runs at chunk offsets.  The
+    eight-ciphertext pattern of test_batched_two_error_location tiled 768 times: levels [6144, 5376, 4608, 16896]"""
+    b = Batch(b"gpu-batched-two-errors", 22, 7, 8)
+    rows = [list(r) for r in b.good]
+    bad = {1: [5], 2: [0, 21], 3: [3, 4], 4: [1, 7, 12], 5: [9], 6: [10], 7: [6]}
+    for r, pos in bad.items():
+        for j in pos:
+            rows[r][j] = b.bad[r][j]
+    rows[5][2] = rows[5][2][::-1]
+    rows[6][11] = rows[6][12]
+    rows[7][17] = off_subgroup_g1(b.d)
+    base = [s for r in rows for s in r]
+    expect = np.array([b.expect(i // 22, i % 22, base[i]) for i in range(len(base))], dtype=np.uint8)
+    reps = 768
+    ct = np.tile(np.repeat(np.arange(8, dtype=np.uint32), 22), reps)
+    dec = np.tile(np.arange(22, dtype=np.uint32), 8 * reps)
+    nat.set_batch_census(0)              # every group through the levels (no census of suspect keys)
+    if chunk:
+        nat.set_verify_chunk(chunk)
+    try:
+        got = run_dev(nat, tdev, b, ct, dec, b"".join(base) * reps)
+        levels, _ = nat.tpke_batched_stats()
+    finally:
+        nat.set_verify_chunk(1 << 21)
+        nat.set_batch_census(16384)
+    assert np.array_equal(got, np.tile(expect, reps))
+    assert levels == [8 * reps, 7 * reps, 6 * reps, 22 * reps], levels
+
+
 @pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("density", [0.0, 0.01, 0.3, 1.0])
 def test_batched_corruption_density(nat, tdev, density, fused):
