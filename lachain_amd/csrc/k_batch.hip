@@ -39,6 +39,13 @@ LCB_TU_CONFIG(k_batch)
 #ifndef LCB_SEARCH2B_BY_POSITION
 #define LCB_SEARCH2B_BY_POSITION 0
 #endif
+#ifndef LCB_SEARCH2B_DEBUG
+#define LCB_SEARCH2B_DEBUG 0
+#endif
+#if LCB_SEARCH2B_DEBUG
+// diagnostic builds only: per (open check, lane) fingerprints of D, E, gamma_c^-(c_j + 1), the group, found, cand
+__device__ u32 *lcb_s2b_dbg = nullptr;
+#endif
 
 // ---------------------------------------------------------------- level-1 groups: runs of one ciphertext / message
 // one lane per share; the first share of a run emits the run as groups of at most `cap` shares.
@@ -456,6 +463,15 @@ extern "C" __global__ void __launch_bounds__(64) k_tpke_rlc_search2b(const uint4
 #endif
     fp12_cyc_sqr_n(a, a);
     fp12_mul_n(a, a, b);                                   // E_j = gamma_t^2 / gamma_c^(c_j + 1) = gamma_2 / gamma_c^(c_j)
+#if LCB_SEARCH2B_DEBUG
+    if (lcb_s2b_dbg && live) {
+        u32 *o = lcb_s2b_dbg + ((size_t)k * 32 + j) * 8;
+        o[0] = fp12_fingerprint(D);
+        o[1] = fp12_fingerprint(a);
+        o[2] = fp12_fingerprint(b);
+        o[3] = g;
+    }
+#endif
     // E_j = D_j^c for some c in [1, len] (len <= 32): baby-step giant-step with m = 6 — 32-bit fingerprints of the
     // baby values D^k (k = 1..6), giant steps Y_i = E D^(-6 i) (D is unitary: D^-6 = conj(D^6)), a fingerprint match
     // Y_i ~ D^(k+1) confirmed by the full comparison Y_i == D^(k+1) (<=> E == D^c, c = 6 i + k + 1): 10 products
@@ -486,6 +502,13 @@ extern "C" __global__ void __launch_bounds__(64) k_tpke_rlc_search2b(const uint4
             if (i < 5) fp12_mul_n(a, a, b);
         }
     }
+#if LCB_SEARCH2B_DEBUG
+    if (lcb_s2b_dbg && live) {
+        u32 *o = lcb_s2b_dbg + ((size_t)k * 32 + j) * 8;
+        o[4] = found;
+        o[5] = cand;
+    }
+#endif
     const u32 m2 = half_ballot(found != 0);
     const u32 m3 = half_ballot(found != 0 && !((m2 >> ((found - 1) & 31u)) & 1u));
     if (__popc(m2) == 2 && !m3) {
@@ -604,11 +627,17 @@ extern "C" void lcbk_tpke_rlc_search2a(hipStream_t s, const void *search, u32 ns
     dim3 grid((4 * ns + LCB_BLOCK - 1) / LCB_BLOCK);
     LCB_LAUNCH(k_tpke_rlc_search2a, (const uint4 *)search, ns, gamma0, gamma12, accept, open, open_count);
 }
-#ifndef LCB_SEARCH2B_BY_POSITION
-#define LCB_SEARCH2B_BY_POSITION 0
-#endif
 // 1: the diagnostic variant that reads gamma_t of open check k at row ns + k (the copy then writes rows by check)
 extern "C" int lcbk_search2b_by_position(void) { return LCB_SEARCH2B_BY_POSITION; }
+// diagnostic builds (-DLCB_SEARCH2B_DEBUG=1): point the kernel's record buffer at p (nullptr: off); -1 in other builds
+extern "C" int lcbk_search2b_debug(void *p) {
+#if LCB_SEARCH2B_DEBUG
+    return hipMemcpyToSymbol(HIP_SYMBOL(lcb_s2b_dbg), &p, sizeof p) == hipSuccess ? 0 : -1;
+#else
+    (void)p;
+    return -1;
+#endif
+}
 // n_open = *open_count (read by the host after search2a); gamma12 + 144 (ns + g) holds gamma_t of the open group g
 extern "C" void lcbk_tpke_rlc_search2b(hipStream_t s, const void *search, u32 ns, u32 n_open, const u32 *gamma0,
                                        const u32 *gamma12, const u32 *open, const u32 *open_count, uint8_t *accept,

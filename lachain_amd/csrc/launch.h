@@ -96,6 +96,7 @@ extern "C" void lcbk_tpke_rlc_wsum2(hipStream_t s, const void *sdesc, u32 ns, co
 extern "C" void lcbk_rlc_park_copy(hipStream_t s, const u32 *park, u32 o, u32 m, u32 *dst, const u32 *map);
 extern "C" void lcbk_tpke_rlc_search2a(hipStream_t s, const void *search, u32 ns, const u32 *gamma0, const u32 *gamma12, uint8_t *accept, u32 *open, u32 *open_count);
 extern "C" int lcbk_search2b_by_position(void);
+extern "C" int lcbk_search2b_debug(void *p);
 extern "C" void lcbk_tpke_rlc_search2b(hipStream_t s, const void *search, u32 ns, u32 n_open, const u32 *gamma0, const u32 *gamma12, const u32 *open, const u32 *open_count, uint8_t *accept, void *next, u32 *next_count, const u32 *key_idx, u32 n_keys, const u32 *susp);
 extern "C" void lcbk_rlc_search(dim3 grid, hipStream_t s, const void *search, u32 o, u32 m, const u32 *gamma, const u32 *park, uint8_t *accept, void *next, u32 *next_count, const u32 *key_idx, u32 n_keys, const u32 *susp);
 extern "C" void lcbk_rlc_census_desc(hipStream_t s, const u32 *grp_idx, const u32 *key_idx, u32 m, u32 n_grp, u32 n_keys, void *desc, uint8_t *accept);

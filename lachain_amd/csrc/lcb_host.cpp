@@ -1215,11 +1215,20 @@ void rlc_sum_enqueue(const RlcKindInfo &K, RlcWs &w, const uint8_t *desc, u32 gr
 // before ("in") and after ("out") k_tpke_rlc_search2b, the open list, gamma_0 rows, gamma_c / gamma_t rows and the accept
 // bytes go to <prefix>.<stage>.<call>.bin — the header {ns, n_open, n, by_position} then the four arrays
 std::atomic<int> g_dump_calls{0};
-void search2b_dump(hipStream_t s, const char *stage, u32 ns, u32 no, const u32 *gamma, const u32 *g12, const u32 *open,
-                   const uint8_t *d_accept, size_t n) {
+// Diagnostic builds (-DLCB_SEARCH2B_DEBUG=1) also record per (open check, lane) fingerprints inside the kernel: the
+// "in" stage returns the record buffer (set on the kernel), the "out" stage appends it to its file and frees it.
+void *search2b_dump(hipStream_t s, const char *stage, u32 ns, u32 no, const u32 *gamma, const u32 *g12, const u32 *open,
+                    const uint8_t *d_accept, size_t n, void *dbg = nullptr) {
     const char *pre = getenv("LCB_DUMP_SEARCH2B");
-    if (!pre || !*pre || !env_on("LCB_ALLOW_TEST_HOOKS")) return;
-    if (hipStreamSynchronize(s) != hipSuccess) return;
+    if (!pre || !*pre || !env_on("LCB_ALLOW_TEST_HOOKS")) return nullptr;
+    if (hipStreamSynchronize(s) != hipSuccess) return nullptr;
+    std::vector<u32> rec;
+    if (stage[0] == 'o' && dbg) {
+        rec.resize((size_t)no * 32 * 8);
+        hipMemcpy(rec.data(), dbg, 4 * rec.size(), hipMemcpyDeviceToHost);
+        lcbk_search2b_debug(nullptr);
+        hipFree(dbg);
+    }
     std::vector<u32> op(no + 4), g0((size_t)ns * 144), gg(2 * (size_t)ns * 144);
     std::vector<uint8_t> acc(n);
     hipMemcpy(op.data(), open, 4 * (no + 4), hipMemcpyDeviceToHost);
@@ -1230,14 +1239,21 @@ void search2b_dump(hipStream_t s, const char *stage, u32 ns, u32 no, const u32 *
     char path[512];
     snprintf(path, sizeof path, "%s.%s.%d.bin", pre, stage, call);
     FILE *fh = fopen(path, "wb");
-    if (!fh) return;
+    if (!fh) return nullptr;
     const u32 hdr[4] = {ns, no, (u32)n, (u32)lcbk_search2b_by_position()};
     fwrite(hdr, 4, 4, fh);
     fwrite(op.data(), 4, op.size(), fh);
     fwrite(g0.data(), 4, g0.size(), fh);
     fwrite(gg.data(), 4, gg.size(), fh);
     fwrite(acc.data(), 1, acc.size(), fh);
+    if (!rec.empty()) fwrite(rec.data(), 4, rec.size(), fh);
     fclose(fh);
+    void *buf = nullptr;
+    if (stage[0] == 'i' && hipMalloc(&buf, (size_t)no * 32 * 8 * 4) == hipSuccess) {
+        hipMemset(buf, 0xff, (size_t)no * 32 * 8 * 4);
+        if (lcbk_search2b_debug(buf) != 0) { hipFree(buf); buf = nullptr; }
+    }
+    return buf;
 }
 // Miller + final exponentiation (+ resolve / search) over the groups of desc in chunks; gpts holds the points
 enum RlcStage { RLC_RESOLVE = 0, RLC_SEARCH = 1, RLC_COPY = 2 };   // after a chunk's checks: resolve / search / copy out
@@ -1385,10 +1401,10 @@ int rlc_levels(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, size_t n, 
                 rlc_checks(c, K, w, (const uint8_t *)(sdesc + ns), no, gp2, gacc2, f2, RLC_COPY, false, nullptr,
                            sdesc + ns, g12 + (size_t)ns * 144, d_accept, io, s,
                            lcbk_search2b_by_position() ? nullptr : open + 4);
-                search2b_dump(s, "in", ns, no, gamma, g12, open, d_accept, n);
+                void *dbg = search2b_dump(s, "in", ns, no, gamma, g12, open, d_accept, n);
                 lcbk_tpke_rlc_search2b(s, sdesc, ns, no, gamma, g12, open + 4, open, d_accept, w.dB, w.cnt + 1,
                                        io.d_key, (u32)K.n_keys, w.susp);
-                search2b_dump(s, "out", ns, no, gamma, g12, open, d_accept, n);
+                search2b_dump(s, "out", ns, no, gamma, g12, open, d_accept, n, dbg);
             }
             if (!launched("batched verify launch")) return -1;
             if (!read_counts(cnt + 1, w.cnt + 1, 1, s)) return -1;

@@ -88,8 +88,81 @@ def compare(pa, pb, call=0):
     return rep
 
 
+# ---------------------------------------------------------------- in-kernel records (diagnostic builds)
+def _fp12_words(gt):
+    """canonical GT bytes (oracle) -> the device's 144 Montgomery words"""
+    import oracle as o
+    w = []
+    for i in range(12):
+        x = int.from_bytes(gt[48 * i:48 * i + 48], "little") * (1 << 384) % o.P
+        w += [(x >> (32 * t)) & 0xffffffff for t in range(12)]
+    return w
+
+
+def _row_gt(row):
+    import oracle as o
+    rinv = pow(1 << 384, -1, o.P)
+    out = b""
+    for i in range(12):
+        x = sum(int(row[12 * i + t]) << (32 * t) for t in range(12))
+        out += (x * rinv % o.P).to_bytes(48, "little")
+    return out
+
+
+def _conj(gt):
+    import oracle as o
+    out = gt[:288]
+    for i in range(6, 12):
+        x = int.from_bytes(gt[48 * i:48 * i + 48], "little")
+        out += ((o.P - x) % o.P).to_bytes(48, "little")
+    return out
+
+
+def _fpr(words):
+    h = 0
+    for w in words:
+        h = (((h << 5) | (h >> 27)) & 0xffffffff) ^ w
+    return h
+
+
+def check_records(prefix, call=0, positions=3):
+    """recompute D_j, E_j and gamma_c^-(c_j+1) from the dumped rows and compare their fingerprints with the kernel's"""
+    import oracle as o
+    raw = open(f"{prefix}.out.{call}.bin", "rb").read()
+    D = load(f"{prefix}.out.{call}.bin")
+    ns, no = D["ns"], D["no"]
+    base = 16 + 4 * (no + 4) + 4 * ns * 144 + 8 * ns * 144 + D["n"]
+    rec = np.frombuffer(raw[base:base + 4 * no * 32 * 8], dtype="<u4").reshape(no, 32, 8)
+    Din = load(f"{prefix}.in.{call}.bin")
+    report = []
+    for k in range(positions):
+        g = int(D["open"][k])
+        g0, gc = _row_gt(Din["g0"][g]), _row_gt(Din["gg"][g])
+        gt = _row_gt(Din["gg"][ns + (k if D["bypos"] else g)])
+        p0, pc = g0, gc
+        bad = []
+        for j in range(22):
+            cj = j + 1
+            d_ = o.gt_mul(gc, _conj(p0))                       # gamma_c / gamma_0^(c_j)
+            pc1 = o.gt_mul(pc, gc)                             # gamma_c^(c_j + 1)
+            b_ = _conj(pc1)
+            e_ = o.gt_mul(o.gt_mul(gt, gt), b_)
+            want = (_fpr(_fp12_words(d_)), _fpr(_fp12_words(e_)), _fpr(_fp12_words(b_)), g)
+            got = tuple(int(x) for x in rec[k, j, :4])
+            if want != got:
+                bad.append(dict(lane=j, want=[hex(x) for x in want], got=[hex(x) for x in got]))
+            p0 = o.gt_mul(p0, g0)
+            pc = o.gt_mul(pc, gc)
+        found = [int(x) for x in rec[k, :22, 4]]
+        report.append(dict(k=k, g=g, found=found, mismatched_lanes=len(bad), first=bad[:3]))
+        print(json.dumps(report[-1]), flush=True)
+    return report
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "run":
         run(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 256)
+    elif sys.argv[1] == "records":
+        check_records(sys.argv[2])
     else:
         compare(sys.argv[2], sys.argv[3], int(sys.argv[4]) if len(sys.argv) > 4 else 0)
