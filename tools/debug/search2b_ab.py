@@ -45,7 +45,7 @@ def run(tag, reps=256):
     nat.set_batch_census(0)
     nat.set_batch_seed(bytes(range(32)))
     res = []
-    for it in range(3):
+    for it in range(int(os.environ.get("S2B_ITERS", "3"))):
         got = tb.run_dev(nat, (torch, dev), b, ct, dec, b"".join(base) * reps)
         levels, _ = nat.tpke_batched_stats()
         res.append(dict(iteration=it, levels=levels, mismatches=int(np.sum(got != np.tile(expect, reps)))))
