@@ -703,6 +703,16 @@ def run_ts(args, nat, torch, dev, rank, world):
                                "assemble_and_verify_combined": t_asm / per}
             out["levels"] = levels
             out["api"] = "lcb_ts_verify_shares_batched_dev (prepare + randomized group checks)"
+            step_fpmul = rounds * ts_round_fpmul(n, f + 1) + sum(levels or []) * C["C_TS_CHECK"]
+            step_s = elapsed / per
+            out["roofline"] = {"bound": "valu_int32",
+                               "kernel": ("whole CommonCoin step: k_ts_rlc_points, message preparation, group checks, "
+                                          "G2 Lagrange lanes, combined-signature checks"),
+                               "achieved": step_fpmul * MAC_PER_FPMUL / step_s / 1e12, "peak": PEAK_MAC32 / 1e12,
+                               "unit": "Tmac32/s", "frac": step_fpmul * MAC_PER_FPMUL / step_s / PEAK_MAC32,
+                               "fpmul_per_step": step_fpmul,
+                               "work_model": {k_: C[k_] for k_ in ("C_TS_POINTS", "C_GSUM_TS", "C_TS_CHECK",
+                                                                  "C_MSG_PREP", "C_G2_LAG1", "C_G2_LAG2")}}
         else:
             ver_s = t_ver / per * 1e-3
             out["phase_ms"] = {"prepare": t_prep / per, "verify_shares": t_ver / per,
@@ -1080,8 +1090,13 @@ def run_replay(args, nat, torch, dev, rank, world):
     elapsed = float(t[0]) / args.replay_steps
     checks_per_view = n + n * n + n_coins * n + n_coins
     cpu = replay_cpu_baseline(inp, n, f, n_coins) if (world == 1 and not args.no_cpu_baseline) else None
+    era_fpmul = n * replay_view_fpmul(n, f, n_coins)
+    roof = {"bound": "valu_int32", "kernel": "whole era (every view): bench.py replay_view_fpmul",
+            "achieved": era_fpmul * MAC_PER_FPMUL / elapsed / 1e12, "peak": PEAK_MAC32 / 1e12, "unit": "Tmac32/s",
+            "frac": era_fpmul * MAC_PER_FPMUL / elapsed / PEAK_MAC32, "fpmul_per_era": era_fpmul}
     return dict(metric="HoneyBadgerBFT epoch crypto replay: node views/sec (TPKE + CommonCoin)", cpu_baseline=cpu,
                 value=n / elapsed, unit="views/s", scaling="strong", views_total=n, n=n, f=f, coins=n_coins,
+                roofline=roof,
                 pairing_checks_per_s=n * checks_per_view / elapsed, ms_per_era=1e3 * elapsed,
                 steps=args.replay_steps, mismatches=int(t[1]), input_gen_s=t_gen,
                 share_checks=("randomized batch checks (lcb_tpke_verify_shares_batched_dev, "
@@ -1401,6 +1416,47 @@ C["C_DBL1"] = (C["C_MUL1"] - 127.5 * C["C_MADD1"]) / 255   # G1 doubling, from t
 C["C_MUL_AB32"] = round(32 * C["C_DBL1"] + 32 * C["C_MADD1"]) + 1   # a P + b phi(P): 32 dbl, ~2 x 16 madds, beta x
 C["C_KTAB"] = 7 * C["C_JADD1"] + 1                         # a Y + b phi(Y) from the key's byte tables
 W_RLC_POINTS = C["C_DEC1"] + C["C_MUL_AB32"] + C["C_KTAB"]  # per share: decompress U_i, s_i U_i, s_i Y_i
+# Round 5: whole-step work models of configs[2] and configs[4] from the same frozen counts.  G2 group
+# operations in Fp-mul: a mixed addition is 7 Fp2 products + 4 squares (3 / 2 Fp-mul), a Jacobian addition 11 + 5; the
+# doubling comes from the frozen 255-bit G2 ladder as C_DBL1 does from the G1 one.
+C["C_MADD2"] = 7 * 3 + 4 * 2
+C["C_JADD2"] = 11 * 3 + 5 * 2
+C["C_DBL2"] = (C["C_MUL2"] - 127.5 * C["C_MADD2"]) / 255
+# CommonCoin share randomisation (k_ts_rlc_points): decompress sigma, psi membership (63 doublings + 5 mixed additions
+# + psi), a sigma + b psi^4(sigma) (32 doublings + ~32 mixed additions with the joint addend), the key's byte tables
+C["C_TS_POINTS"] = round(C["C_DEC2"] + 63 * C["C_DBL2"] + 5 * C["C_MADD2"] + 10 + 32 * C["C_DBL2"]
+                         + 32 * C["C_MADD2"] + C["C_KTAB"])
+C["C_GSUM_TS"] = C["C_JADD1"] + C["C_JADD2"]              # per share: the group sums of both sides
+C["C_GSUM_TPKE"] = 2 * C["C_JADD1"]
+C["C_TS_CHECK"] = C["C_ML2_NORM1"] + C["C_LINES"] + C["C_FE"]   # a group check, the sigma side's lines on the fly
+C["C_MSG_PREP"] = C["C_H2G2"] + C["C_LINES"] + C["C_NORM"]      # per message: hash to G2 + its normalised line set
+# G2 Lagrange lanes (lanetab.hpp): GLS over the 15 sums of the psi-images, 64 doublings + 60 mixed additions (15 of 16
+# digit columns nonzero) per table, the table's 1 + 9 additions, ~20 Fp-mul per entry of the batched affine conversion
+# and one Fp2 inversion per lane; a pair of entries shares the doublings and the inversion
+C["C_G2_LAG1"] = round(64 * C["C_DBL2"] + 60 * C["C_MADD2"] + C["C_MADD2"] + 9 * C["C_JADD2"] + 15 * 20 + C["C_FP2_INV"])
+C["C_G2_LAG2"] = round(64 * C["C_DBL2"] + 120 * C["C_MADD2"] + 2 * (C["C_MADD2"] + 9 * C["C_JADD2"]) + 30 * 20
+                       + C["C_FP2_INV"])
+
+
+def ts_round_fpmul(n, k):
+    """per CommonCoin round of n shares and threshold k: randomisation + group sums of every share, the message's
+    preparation, the assembly's Lagrange lanes (k // 2 pairs + k % 2 single, the k - 1 additions and the affine output)
+    and the combined signature's exact check; the group checks are counted separately (from the levels run)"""
+    asm = (k // 2) * C["C_G2_LAG2"] + (k % 2) * C["C_G2_LAG1"] + (k - 1) * C["C_JADD2"] + C["C_AFF2"]
+    return n * (C["C_TS_POINTS"] + C["C_GSUM_TS"]) + C["C_MSG_PREP"] + asm + W_TS
+
+
+def replay_view_fpmul(n, f, n_coins):
+    """per node view of configs[4] (all shares valid: level 1 only): the TPKE batch check of n x n shares (groups of
+    <= 32) with the n ciphertexts' preparation, the node's partial decryptions (pairing check + x U), the n FullDecrypt
+    G1 Lagrange combinations (k = f + 1 ladders of C_MUL1), and n_coins coins (batch check of n shares in groups of
+    <= 128, assembly, combined check)"""
+    k = f + 1
+    tpke = n * n * (W_RLC_POINTS + C["C_GSUM_TPKE"]) + n * -(-n // 32) * (C["C_ML2_NORM2"] + C["C_FE"]) + n * W_PREPARE
+    pdec = n * (C["C_DEC1"] + C["C_ML2_NORM2"] + C["C_FE"] + C["C_MUL1"])
+    comb = n * (k * C["C_MUL1"] + (k - 1) * C["C_JADD1"] + C["C_AFF2"])
+    coins = n_coins * ts_round_fpmul(n, k) + n_coins * -(-n // 128) * C["C_TS_CHECK"]
+    return tpke + pdec + comb + coins
 
 
 def run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, dd, n, n_cts, n_dec, sh):
@@ -1713,6 +1769,8 @@ def compact_line(full):
                                         _short(k, 24): _r(v) for k, v in (ts.get("phase_ms") or {}).items()},
                                     "exact": _r((ts.get("exact") or {}).get("value")),
                                     "cpu": _r((ts.get("cpu_baseline") or {}).get("value"))}
+        if (ts.get("roofline") or {}).get("frac") is not None:
+            s["threshold_signature"]["frac"] = _r(ts["roofline"]["frac"])
     for key, vk in (("epoch_replay", "mismatches"), ("ecdsa_headers", "decision_mismatches")):
         sub = full.get(key)
         if sub:
