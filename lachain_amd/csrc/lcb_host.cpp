@@ -1,9 +1,11 @@
 // lachain_amd/csrc/lcb_host.cpp — host implementation of include/lachain_bls.h (liblachain_bls.so).
 //
-// Every arithmetic operation is executed by a gfx950 kernel (k_*.hip); the host only moves bytes, validates
-// arguments and orders GPU work.  There is deliberately no CPU fallback: without a gfx950 device mclBn_init
-// returns -1 and every entry point fails (returns -1 / 0 bytes / leaves outputs zeroed) with lcb_last_error()
-// describing why.
+// Batch work (share verification, Lagrange combination, MSM, scalar multiplications, pairings, hashing to G2) runs
+// on gfx950 kernels (k_*.hip).  The mcl single-element calls that are O(1) field work — Fr arithmetic (fr_host.hpp)
+// and G1 / G2 add, sub, neg, dbl, normalize, compare, validity, (de)serialization, GT products (fp_host.hpp) — run on
+// the calling thread, word for word the kernels' formulas, because a GPU round trip costs 50-100x the operation.
+// There is deliberately no CPU fallback for the GPU work: without a gfx950 device mclBn_init returns -1 and every
+// entry point fails (returns -1 / 0 bytes / leaves outputs zeroed) with lcb_last_error() describing why.
 //
 // Concurrency model (the reference calls mcl from one thread per consensus protocol,
 // /root/reference/src/Lachain.Consensus/AbstractProtocol.cs:46-47):
