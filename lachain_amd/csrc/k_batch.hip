@@ -328,6 +328,13 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_search(const uint4 *search, u32 o, u
 }
 
 // the final-exponentiation outputs of checks [o, o + m) (park stride m) -> rows o.. of dst (576 B each)
+// *flag |= 1 when a line set of ciphertexts [c0, c1) is not normalised (the Miller fallback will be needed)
+extern "C" __global__ void LCB_BOUNDS k_lines_unnormalised(const u32 *lines, u32 c0, u32 c1, u32 *flag) {
+    LCB_LATENCY_PRIO();
+    const u32 k = 2 * c0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= 2 * c1) return;
+    if (!lineset_normalised(lines + (size_t)k * LCB_LINESET_WORDS)) atomicOr(flag, 1u);
+}
 extern "C" __global__ void LCB_BOUNDS k_rlc_park_copy(const u32 *park, u32 o, u32 m, u32 *dst, const u32 *map) {
     LCB_LATENCY_PRIO();
     u32 gl = blockIdx.x * blockDim.x + threadIdx.x;
@@ -616,6 +623,11 @@ extern "C" void lcbk_rlc_search(dim3 grid, hipStream_t s, const void *search, u3
                                 u32 n_keys, const u32 *susp) {
     LCB_LAUNCH(k_rlc_search, (const uint4 *)search, o, m, gamma, park, accept, (uint4 *)next, next_count, key_idx,
                n_keys, susp);
+}
+extern "C" void lcbk_lines_unnormalised(hipStream_t s, const u32 *lines, u32 c0, u32 c1, u32 *flag) {
+    if (c1 <= c0) return;
+    dim3 grid((2 * (c1 - c0) + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_lines_unnormalised, lines, c0, c1, flag);
 }
 extern "C" void lcbk_rlc_park_copy(hipStream_t s, const u32 *park, u32 o, u32 m, u32 *dst, const u32 *map) {
     dim3 grid((m + LCB_BLOCK - 1) / LCB_BLOCK);

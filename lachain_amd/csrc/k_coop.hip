@@ -183,11 +183,14 @@ extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_debug(int op, u32 
 }
 
 // ---------------------------------------------------------------- host launch wrappers
+// fallback = 0: the caller knows every line set the groups use is normalised (no group can be flagged), so the one-lane
+// fallback kernel is not dispatched
 extern "C" void lcbk_coop_tpke_miller(hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups,
-                                      u32 *f_soa, uint8_t *gacc, uint8_t *fb, u32 npairs) {
+                                      u32 *f_soa, uint8_t *gacc, uint8_t *fb, u32 npairs, int fallback) {
     dim3 grid((n_groups + CP_G - 1) / CP_G);
     hipLaunchKernelGGL(k_coop_tpke_miller, grid, dim3(CP_BLOCK), 0, s, lines, (const uint4 *)desc, (const g1a_st *)gpts,
                        n_groups, f_soa, gacc, fb, npairs);
+    if (!fallback) return;
     grid = dim3((n_groups + LCB_BLOCK - 1) / LCB_BLOCK);
     LCB_LAUNCH(k_rlc_miller_fallback, lines, (const uint4 *)desc, (const g1a_st *)gpts, n_groups, f_soa, fb);
 }

@@ -103,7 +103,9 @@ extern "C" void lcbk_rlc_census_desc(hipStream_t s, const u32 *grp_idx, const u3
 extern "C" void lcbk_rlc_census_stats(hipStream_t s, const u32 *key_idx, u32 m, u32 n_keys, const uint8_t *cval, const uint8_t *accept, u32 *susp, u32 *count);
 extern "C" void lcbk_rlc_suspect_split(hipStream_t s, const void *desc, u32 n_groups, const u32 *key_idx, u32 n_keys, const u32 *susp, const uint8_t *accept, void *out, u32 *count);
 extern "C" size_t lcbk_ts_grp_bytes();
-extern "C" void lcbk_coop_tpke_miller(hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups, u32 *f_soa, uint8_t *gacc, uint8_t *fb, u32 npairs);
+extern "C" void lcbk_coop_tpke_miller(hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups, u32 *f_soa, uint8_t *gacc, uint8_t *fb, u32 npairs, int fallback);
+// *flag |= 1 when a line set of ciphertexts [c0, c1) is not normalised
+extern "C" void lcbk_lines_unnormalised(hipStream_t s, const u32 *lines, u32 c0, u32 c1, u32 *flag);
 extern "C" size_t lcbk_mcl_terms_ws_bytes(u32 n);
 extern "C" void lcbk_mcl_g1_terms(hipStream_t s, const void *pts, const void *scal, u32 n, void *terms, u32 *ws);
 extern "C" void lcbk_mcl_horner(hipStream_t s, int g, const u32 *coef, u32 n, const void *x_raw, u32 *out);

@@ -83,6 +83,14 @@ struct lcb_ctx {
     uint32_t rlc_census[4] = {};      // census shares, suspect keys, level-1 groups before / entries after the split
     int rlc_nlev = 0;
     uint64_t rlc_calls = 0;
+    // which prepared line sets are not normalised (adversarial W): [0] the census's ciphertexts, [1] all; the one-lane
+    // Miller fallback is dispatched only when the flag is set (round 5: an idle fallback dispatch waited ~15 ms for a
+    // SIMD with 360 free registers behind the randomisation).  Device words, pinned copies, events after the copies.
+    DevBuf unn;
+    uint32_t *unn_pin = nullptr;
+    hipEvent_t unn_ev[2] = {};
+    bool unn_set[2] = {false, false};
+    int unn_census = 1;               // the flag the census reads: 0 when its ciphertexts were prepared first (split)
     hipStream_t aux = nullptr;        // second stream of the fused batched verify (randomisation beside preparation)
     hipStream_t hi = nullptr;         // high-priority stream: the latency-bound preparation chain (lcb_set_fork_mode 1)
     hipStream_t hi2 = nullptr;        // second high-priority stream: U / W decompression + W's line sets (fork mode 3)

@@ -802,6 +802,30 @@ void lines_fill(hipStream_t s, u32 *lines, size_t n, const u32 *sets, uint8_t *w
     if (n <= (size_t)g_lines_coop_max.load()) lcbk_lineset_coop(s, lines, (u32)n, sets, w_g2);
     else lcbk_lineset_fill(dim3(nblk(n)), s, lines, (u32)n, sets, w_g2);
 }
+// Un-normalised line sets (only an adversarial W, or the line-mode test hook, makes one): after a preparation the flag
+// `which` (0 = the census's ciphertexts, 1 = all) is reduced on the device and copied to pinned memory; the host reads
+// it (lines_unnormalised) before it enqueues the checks that use those sets and dispatches the one-lane Miller
+// fallback only when it is set.  Any failure reads as "set" (the fallback then runs, as before round 5).
+void lines_flag_enqueue(lcb_ctx *c, int which, const u32 *lines, u32 c0, u32 c1, hipStream_t s) {
+    c->unn_set[which] = false;
+    if (!c->unn_pin && hipHostMalloc((void **)&c->unn_pin, 16, hipHostMallocDefault) != hipSuccess) {
+        c->unn_pin = nullptr;
+        return;
+    }
+    for (auto &e : c->unn_ev)
+        if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return;
+    u32 *d = (u32 *)c->unn.get(16);
+    if (!d) return;
+    if (hipMemsetAsync(d + which, 0, 4, s) != hipSuccess) return;
+    lcbk_lines_unnormalised(s, lines, c0, c1, d + which);
+    if (hipMemcpyAsync(c->unn_pin + which, d + which, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return;
+    if (hipEventRecord(c->unn_ev[which], s) != hipSuccess) return;
+    c->unn_set[which] = true;
+}
+bool lines_unnormalised(lcb_ctx *c, int which) {
+    if (!c->unn_set[which] || hipEventSynchronize(c->unn_ev[which]) != hipSuccess) return true;
+    return __atomic_load_n(c->unn_pin + which, __ATOMIC_ACQUIRE) != 0;
+}
 
 // ================================================================== execution contexts
 namespace {
@@ -824,6 +848,10 @@ void ctx_free(lcb_ctx *c) {
     c->cc_lines.release();
     c->cc_ok.release();
     for (auto &b : c->rlc) b.release();
+    c->unn.release();
+    if (c->unn_pin) (void)hipHostFree(c->unn_pin);
+    for (auto &e : c->unn_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->rlc_ev_ready) {
         for (auto &e : c->rlc_ev) (void)hipEventDestroy(e);
         for (auto &e : c->rlc_lev_ev) (void)hipEventDestroy(e);
@@ -940,6 +968,7 @@ int tpke_prepare(lcb_ctx *c, const uint8_t *d_y, size_t n_keys, const uint8_t *d
                  const uint8_t *d_v, const uint32_t *d_voff, size_t n_cts, hipStream_t s) {
     if (n_cts > 0xffffffffu || n_keys > 0xffffffffu) { set_err("tpke prepare: batch too large"); return -1; }
     c->t_ready = false;
+    c->unn_set[0] = c->unn_set[1] = false;     // the fallback flags describe the line sets prepared below
     u32 *lines = (u32 *)c->t_lines.get((size_t)n_cts * 2 * LCB_LINESET_BYTES);
     uint8_t *ctok = (uint8_t *)c->t_ctok.get(n_cts);
     void *keys = c->t_keys.get(n_keys * LCB_G1A_ST_BYTES);
@@ -951,6 +980,8 @@ int tpke_prepare(lcb_ctx *c, const uint8_t *d_y, size_t n_keys, const uint8_t *d
                              g_orig_cofactor | (g_line_mode << 1), nullptr);
         lines_fill(s, lines, 2 * n_cts, nullptr, ctg2);
     }
+    c->unn_census = 1;
+    lines_flag_enqueue(c, 1, lines, 0, (u32)n_cts, s);
     if (!launched("tpke prepare launch")) return -1;
     c->t_n_cts = n_cts;
     c->t_n_keys = n_keys;
@@ -1000,7 +1031,7 @@ int tpke_verify_core(lcb_ctx *c, const u32 *lines, const uint8_t *ctok, size_t n
             if (coop) {
                 lcbk_tpke_exact_points(s, ctok, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct + o, d_dec + o,
                                        d_ui + 48 * o, (u32)m, gpts, desc, d_accept + o);
-                lcbk_coop_tpke_miller(s, lines, desc, gpts, (u32)m, f, fl, fl + m, 2);
+                lcbk_coop_tpke_miller(s, lines, desc, gpts, (u32)m, f, fl, fl + m, 2, 1);
             } else {
                 lcbk_tpke_miller(dim3(nblk(m)), s, lines, ctok, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct + o,
                                  d_dec + o, d_ui + 48 * o, (u32)m, f, d_accept + o);
@@ -1182,6 +1213,7 @@ struct RlcIo {                     // the per-share inputs the exact singles re-
 };
 struct RlcKindInfo {
     bool ts;
+    bool fb = true;                   // TPKE: some line set the checks use may be un-normalised (dispatch the fallback)
     const u32 *lines;
     const uint8_t *okv, *ctg2;
     const void *keys;
@@ -1274,7 +1306,7 @@ void rlc_checks(lcb_ctx *c, const RlcKindInfo &K, RlcWs &w, const uint8_t *desc,
                                gacc + o);
         else if (coop_ml)
             lcbk_coop_tpke_miller(s, K.lines, desc + 16 * o, (const uint8_t *)gpts + K.rec * o, (u32)m, f, gacc + o,
-                                  (uint8_t *)c->rlc[15].get(m), 2);
+                                  (uint8_t *)c->rlc[15].get(m), 2, K.fb ? 1 : 0);
         else
             lcbk_tpke_rlc_miller(dim3(nblk(m)), s, K.lines, desc + 16 * o, (const uint8_t *)gpts + K.rec * o, (u32)m, f,
                                  gacc + o);
@@ -1300,7 +1332,8 @@ void rlc_checks(lcb_ctx *c, const RlcKindInfo &K, RlcWs &w, const uint8_t *desc,
 // then the suspect-key bitmap and its count (cnt[3]); everything stays on the device (no host read)
 int rlc_census(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, RlcIo io, hipStream_t s) {
     if (!w.m) return 0;
-    const RlcKindInfo K = rlc_kind(c, kind);
+    RlcKindInfo K = rlc_kind(c, kind);
+    if (!K.ts) K.fb = lines_unnormalised(c, c->unn_census);    // waits for the census ciphertexts' line sets
     const u32 m = w.m;
     // the census uses dB as its desc list (dA is the level-1 list being built on the second stream)
     void *gpts = c->rlc[5].get((size_t)m * K.rec);
@@ -1320,10 +1353,11 @@ int rlc_census(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, RlcIo io, 
 // over the other keys, every share of a suspect key as an exact single); level 2: weighted re-check + search of the
 // failed groups; then single checks
 int rlc_levels(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, size_t n, RlcIo io, hipStream_t s) {
-    const RlcKindInfo K = rlc_kind(c, kind);
+    RlcKindInfo K = rlc_kind(c, kind);
     u32 cnt[5] = {0, 0, 0, 0, 0};
     for (auto &m : c->rlc_ms) m = 0.0f;
     if (!read_counts(cnt, w.cnt, 4, s)) return -1;
+    if (!K.ts) K.fb = lines_unnormalised(c, 1) || (c->unn_census == 0 && lines_unnormalised(c, 0));
     u32 groups = cnt[0];
     c->rlc_census[1] = cnt[3];
     c->rlc_census[2] = c->rlc_census[3] = groups;
@@ -1488,6 +1522,7 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
                                  hipStream_t s) {
     if (n_cts > 0xffffffffu || n_keys > 0xffffffffu || n > 0xffffffffu) { set_err("tpke batched verify: batch too large"); return -1; }
     c->t_ready = false;
+    c->unn_set[0] = c->unn_set[1] = false;     // the fallback flags describe the line sets prepared below
     c->rlc_nlev = 0;
     u32 *lines = (u32 *)c->t_lines.get((size_t)n_cts * 2 * LCB_LINESET_BYTES);
     uint8_t *ctok = (uint8_t *)c->t_ctok.get(n_cts);
@@ -1542,9 +1577,11 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
         hipStreamWaitEvent(c->hi2, c->fork_ev[0], 0);
         hipStreamWaitEvent(c->hi3, c->fork_ev[0], 0);
         const u32 nc = (u32)n_cts, ce = c_early;
+        c->unn_census = ce ? 0 : 1;
         if (ce) {                    // the census's ciphertexts: decode + hash per lane, then the five-lane line sets
             lcbk_tpke_ct_prepare(dim3(nblk(ce)), sp, d_u, d_w, d_v, d_voff, ce, lines, ctok, fl, nullptr);
             lines_fill(sp, lines, 2 * (size_t)ce, nullptr, ctg2);
+            lines_flag_enqueue(c, 0, lines, 0, ce, sp);
         }
         lcbk_tpke_ct_prepare_h(c->hi2, d_u, d_v, d_voff, ce, nc, lines, hok, fl);
         lcbk_tpke_ct_prepare_w(c->hi3, d_u, d_w, ce, nc, lines, ctok, ctg2, fl);
@@ -1553,6 +1590,7 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
         hipEventRecord(c->fork_ev[2], c->hi2);
         hipStreamWaitEvent(c->hi3, c->fork_ev[2], 0);
         lcbk_ct_ok_merge(c->hi3, ctok, hok, ce, nc);
+        lines_flag_enqueue(c, 1, lines, ce, nc, c->hi3);
         hipEventRecord(c->fork_ev[3], c->hi3);
         if (!ce) hipStreamWaitEvent(sp, c->fork_ev[3], 0);     // the census (below) needs every ciphertext
     } else if (n_cts) {
@@ -1561,6 +1599,8 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
         if (hp) hipEventRecord(c->prep_ev[2], sp);
         if (prep_first && n && rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, sr)) return -1;
         lines_fill(sp, lines, 2 * n_cts, nullptr, ctg2);
+        c->unn_census = 1;
+        lines_flag_enqueue(c, 1, lines, 0, (u32)n_cts, sp);
     }
     if (!launched("tpke prepare launch")) return -1;
     c->t_n_cts = n_cts;
@@ -2912,7 +2952,7 @@ extern "C" void mclBn_pairing(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) {
                            sizeof pt[k], hipMemcpyHostToDevice, s);
     }
     if (!hit) lcbk_lineset_coop(s, lines + (size_t)2 * slot * (LCB_LINESET_BYTES / 4), 2, nullptr, nullptr);
-    lcbk_coop_tpke_miller(s, lines, desc, gpts, 1, park, fl, fl + 32, 1);
+    lcbk_coop_tpke_miller(s, lines, desc, gpts, 1, park, fl, fl + 32, 1, 1);
     lcbk_coop_final_exp_check(s, park, 1, nullptr);
     u32 r[144];
     hipMemcpyAsync(r, park, 576, hipMemcpyDeviceToHost, s);
