@@ -1,0 +1,63 @@
+// lachain_amd/csrc/k_prep.hip — gfx950 kernels: the split TPKE preparation of the fused batched verify (hash lane and
+// point lane, each through its line set).  A translation unit of its own, built like k_rlc_rand.hip without
+// VGPR-to-AGPR spilling and with every kernel at two waves per SIMD, so the attribute reaches the non-inlined callees
+// (line sets, hash to G2, decompression) and the lanes fit in 256 registers: one preparation wave (256) then shares a
+// SIMD with one randomisation wave (248) instead of holding it to itself with 346 (round 5, VERDICT r4 #4: the
+// randomisation started 14-16 ms into the step, when the preparation waves retired).
+#include "kcommon.hpp"
+
+LCB_ASM_LIBRARY(k_prep)
+LCB_TU_CONFIG(k_prep)
+
+#define LCB_PREP_BOUNDS __launch_bounds__(LCB_BLOCK) __attribute__((amdgpu_waves_per_eu(2)))
+
+// k_tpke_ct_prepare split in two lane kinds that run side by side (fused batched verify, fork mode 3), each through
+// its line set: the hash lane (H = G2.SetHashOf(U || V), then H's line set; h_ok = the hash succeeded) and the point
+// lane (U and W decode, then W's line set with its G2 flag; ct_ok = both decode).  k_ct_ok_merge then ANDs h_ok into
+// ct_ok.  An undecodable ciphertext keeps H's real line set (ct_ok = 0 gates every use) and gets W = infinity.
+extern "C" __global__ void LCB_PREP_BOUNDS k_tpke_ct_prepare_h(const uint8_t *cts_u, const uint8_t *v_data, const u32 *v_off,
+                                                         u32 c0, u32 n_cts, u32 *lines, uint8_t *h_ok, int flags) {
+    LCB_LATENCY_PRIO();
+    u32 c = c0 + blockIdx.x * blockDim.x + threadIdx.x;     // ciphertexts [c0, n_cts)
+    if (c >= n_cts) return;
+    uint8_t d[64];
+    u32 v0 = v_off[c], v1 = v_off[c + 1];
+    sha512_2(d, cts_u + 48 * (size_t)c, 48, v_data + v0, v1 - v0);
+    g2 H;
+    g2a Ha;
+    bool hok = g2_hash_digest(H, d, (flags & 1) != 0);
+    if (hok) jac_to_aff(Ha, H);
+    else { Ha.inf = true; Ha.x = fp2_zero(); Ha.y = fp2_zero(); }
+    u32 *ls = lines + (size_t)(2 * c) * LCB_LINESET_WORDS;
+    lineset_compute(ls, Ha);
+    if (flags & 2) ls[LCB_LS_FLAG] = 0;
+    h_ok[c] = hok;
+}
+extern "C" __global__ void LCB_PREP_BOUNDS k_tpke_ct_prepare_w(const uint8_t *cts_u, const uint8_t *cts_w, u32 c0,
+                                                         u32 n_cts, u32 *lines, uint8_t *ct_ok, uint8_t *w_g2,
+                                                         int flags) {
+    LCB_LATENCY_PRIO();
+    u32 c = c0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_cts) return;
+    g1a U;
+    g2a W;
+    bool ok = g1_decompress(U, cts_u + 48 * (size_t)c);
+    ok = g2_decompress(W, cts_w + 96 * (size_t)c) && ok;
+    if (!ok) { W.inf = true; W.x = fp2_zero(); W.y = fp2_zero(); }
+    u32 *ls = lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS;
+    u32 r = lineset_compute(ls, W);
+    if (flags & 2) ls[LCB_LS_FLAG] = 0;
+    ct_ok[c] = ok;
+    w_g2[c] = (r & LCB_LS_IN_G2) ? 1 : 0;
+}
+
+// ---------------------------------------------------------------- host launch wrappers
+// ciphertexts [c0, c1)
+extern "C" void lcbk_tpke_ct_prepare_h(hipStream_t s, const uint8_t *cts_u, const uint8_t *v_data, const u32 *v_off, u32 c0, u32 c1, u32 *lines, uint8_t *h_ok, int flags) {
+    dim3 grid((c1 - c0 + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_tpke_ct_prepare_h, cts_u, v_data, v_off, c0, c1, lines, h_ok, flags);
+}
+extern "C" void lcbk_tpke_ct_prepare_w(hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, u32 c0, u32 c1, u32 *lines, uint8_t *ct_ok, uint8_t *w_g2, int flags) {
+    dim3 grid((c1 - c0 + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_tpke_ct_prepare_w, cts_u, cts_w, c0, c1, lines, ct_ok, w_g2, flags);
+}

@@ -137,6 +137,7 @@ extern "C" int lcbk_cfg_k_scalar(u32 sign_b);
 extern "C" int lcbk_cfg_k_tpke(u32 sign_b);
 extern "C" int lcbk_cfg_k_ts(u32 sign_b);
 extern "C" int lcbk_cfg_k_ptmul(u32 sign_b);
+extern "C" int lcbk_cfg_k_prep(u32 sign_b);
 // cooperative single scalar multiplications (k_ptmul.hip): n_groups ladders of one wave
 extern "C" void lcbk_ptmul_g1(hipStream_t s, const void *jobs, u32 n_groups, void *out);
 extern "C" void lcbk_ptmul_g2(hipStream_t s, const void *jobs, u32 n_groups, void *out);
@@ -152,6 +153,7 @@ extern "C" int lcbk_prio_k_scalar(u32 on);
 extern "C" int lcbk_prio_k_tpke(u32 on);
 extern "C" int lcbk_prio_k_ts(u32 on);
 extern "C" int lcbk_prio_k_ptmul(u32 on);
+extern "C" int lcbk_prio_k_prep(u32 on);
 static inline int lcbk_set_wave_prio(int on) {
     int rc = 0;
     rc |= lcbk_prio_k_batch((u32)on);
@@ -166,6 +168,7 @@ static inline int lcbk_set_wave_prio(int on) {
     rc |= lcbk_prio_k_tpke((u32)on);
     rc |= lcbk_prio_k_ts((u32)on);
     rc |= lcbk_prio_k_ptmul((u32)on);
+    rc |= lcbk_prio_k_prep((u32)on);
     return rc;
 }
 // every kernel unit's G2 sign-flag convention (curve.hpp lcb_g2_sign_b)
@@ -183,5 +186,6 @@ static inline int lcbk_set_g2_sign_b(int sign_b) {
     rc |= lcbk_cfg_k_tpke((u32)sign_b);
     rc |= lcbk_cfg_k_ts((u32)sign_b);
     rc |= lcbk_cfg_k_ptmul((u32)sign_b);
+    rc |= lcbk_cfg_k_prep((u32)sign_b);
     return rc;
 }
