@@ -1580,7 +1580,7 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
         c->unn_census = ce ? 0 : 1;
         if (ce) {                    // the census's ciphertexts: decode + hash per lane, then the five-lane line sets
             lcbk_tpke_ct_prepare(dim3(nblk(ce)), sp, d_u, d_w, d_v, d_voff, ce, lines, ctok, fl, nullptr);
-            lines_fill(sp, lines, 2 * (size_t)ce, nullptr, ctg2);
+            lcbk_lineset_coop_2w(sp, lines, 2 * ce, nullptr, ctg2);   // (2 ce <= 8192 sets: lines_fill's coop range)
             lines_flag_enqueue(c, 0, lines, 0, ce, sp);
         }
         lcbk_tpke_ct_prepare_h(c->hi2, d_u, d_v, d_voff, ce, nc, lines, hok, fl);
@@ -2107,7 +2107,8 @@ extern "C" int lcb_test_linesets(int coop, const uint8_t *g2_wire, const uint8_t
     }
     if (hipMemcpyAsync(lines, host.data(), n * LCB_LINESET_BYTES, hipMemcpyHostToDevice, s) != hipSuccess ||
         hipMemsetAsync(dg, 0, n / 2 + 1, s) != hipSuccess) { set_err("lcb_test_linesets: upload"); return -1; }
-    if (coop) lcbk_lineset_coop(s, lines, (u32)n, nullptr, dg);
+    if (coop == 2) lcbk_lineset_coop_2w(s, lines, (u32)n, nullptr, dg);     // the fused census's instance (k_prep.hip)
+    else if (coop) lcbk_lineset_coop(s, lines, (u32)n, nullptr, dg);
     else lcbk_lineset_fill(dim3(nblk(n)), s, lines, (u32)n, nullptr, dg);
     hipMemcpyAsync(out, lines, n * LCB_LINESET_BYTES, hipMemcpyDeviceToHost, s);
     hipMemcpyAsync(w_g2, dg, n / 2, hipMemcpyDeviceToHost, s);

@@ -778,7 +778,8 @@ def test_linesets(points, coop, force=None):
     force = bytes(force) if force is not None else bytes(n)
     out = np.zeros((n, 6592), dtype=np.uint32)
     g2f = np.zeros(max(1, n // 2), dtype=np.uint8)
-    if lib().lcb_test_linesets(1 if coop else 0, b"".join(points), force, n, out.ctypes.data, g2f.ctypes.data) != 0:
+    mode = coop if isinstance(coop, int) and not isinstance(coop, bool) else (1 if coop else 0)   # 2: the two-wave instance
+    if lib().lcb_test_linesets(mode, b"".join(points), force, n, out.ctypes.data, g2f.ctypes.data) != 0:
         raise RuntimeError("test_linesets: " + last_error())
     return out, g2f[: n // 2]
 

@@ -53,6 +53,19 @@ def test_coop_line_sets_equal_one_lane_sets(nat):
     assert not coop[4][:68 * 48].any()
 
 
+def test_two_wave_coop_line_sets_equal_one_lane_sets(nat):
+    """k_lineset_coop_2w (k_prep.hip, the fused census's instance at 256 registers) gives the same sets"""
+    d = Drbg(b"gpu-lines-coop-2w")
+    pts = _points(d, 26)
+    force = bytearray(26)
+    force[8] = 1
+    two, g2t = nat.test_linesets(pts, 2, force)
+    ref, g2r = nat.test_linesets(pts, False, force)
+    for k in range(26):
+        assert np.array_equal(two[k], ref[k]), k
+    assert g2t.tolist() == g2r.tolist()
+
+
 def test_coop_line_sets_single_and_partial_block(nat):
     d = Drbg(b"gpu-lines-coop-small")
     for n in (1, 2, 13):
