@@ -42,7 +42,10 @@ DN void sha512_2(uint8_t out[64], const uint8_t *p1, u32 n1, const uint8_t *p2, 
     u32 n = n1 + n2;
     u32 nblocks = (n + 17 + 127) / 128;
     for (u32 blk = 0; blk < nblocks; blk++) {
-        u64 w[80];
+        // the message schedule in a ring of 16 words, every index a compile-time constant (registers, not the 640-byte
+        // scratch array of the textbook 80-word schedule): rounds r + i, i = 0..15, with W_t (t >= 16) formed in place
+        u64 w[16];
+#pragma unroll
         for (int i = 0; i < 16; i++) {
             u64 v = 0;
             for (int k = 0; k < 8; k++) {
@@ -57,20 +60,25 @@ DN void sha512_2(uint8_t out[64], const uint8_t *p1, u32 n1, const uint8_t *p2, 
             if (blk == nblocks - 1 && i == 15) v = (u64)n * 8;
             w[i] = v;
         }
-        for (int i = 16; i < 80; i++) {
-            u64 s0 = rotr64(w[i - 15], 1) ^ rotr64(w[i - 15], 8) ^ (w[i - 15] >> 7);
-            u64 s1 = rotr64(w[i - 2], 19) ^ rotr64(w[i - 2], 61) ^ (w[i - 2] >> 6);
-            w[i] = w[i - 16] + s0 + w[i - 7] + s1;
-        }
         u64 a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
-        for (int i = 0; i < 80; i++) {
-            u64 S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
-            u64 ch = (e & f) ^ (~e & g);
-            u64 t1 = hh + S1 + ch + LCB_K512[i] + w[i];
-            u64 S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-            u64 mj = (a & b) ^ (a & c) ^ (b & c);
-            u64 t2 = S0 + mj;
-            hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+#pragma unroll 1
+        for (int r = 0; r < 80; r += 16) {
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                if (r) {
+                    const u64 x15 = w[(i + 1) & 15], x2 = w[(i + 14) & 15];
+                    const u64 s0 = rotr64(x15, 1) ^ rotr64(x15, 8) ^ (x15 >> 7);
+                    const u64 s1 = rotr64(x2, 19) ^ rotr64(x2, 61) ^ (x2 >> 6);
+                    w[i] = w[i] + s0 + w[(i + 9) & 15] + s1;
+                }
+                u64 S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
+                u64 ch = (e & f) ^ (~e & g);
+                u64 t1 = hh + S1 + ch + LCB_K512[r + i] + w[i];
+                u64 S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
+                u64 mj = (a & b) ^ (a & c) ^ (b & c);
+                u64 t2 = S0 + mj;
+                hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+            }
         }
         h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
     }

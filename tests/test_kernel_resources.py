@@ -16,6 +16,7 @@ SO = os.path.join(ROOT, "lachain_amd", "liblachain_bls.so")
 
 # kernel: (max VGPR spills, max scratch bytes per lane) — measured on this build
 BUDGET = {
+    "k_lineset_coop_2w": (270, 1080),         # k_prep.hip: the fused census's line sets at 256 registers
     "k_coop_debug": (96, 7620),               # test hook: the one-lane reference routines beside the coop ones
     "k_coop_final_exp_check": (0, 576),
     "k_coop_tpke_miller": (0, 0),
@@ -60,8 +61,8 @@ BUDGET = {
     "k_rlc_search": (93, 2264),
     "k_secp_scalars": (0, 528),
     "k_tpke_ct_prepare": (0, 3752),
-    "k_tpke_ct_prepare_h": (0, 3640),
-    "k_tpke_ct_prepare_w": (0, 1352),
+    "k_tpke_ct_prepare_h": (5, 4632),
+    "k_tpke_ct_prepare_w": (5, 1688),
     "k_tpke_encrypt1": (0, 1184),
     "k_tpke_encrypt2": (0, 3928),
     "k_tpke_exact_points": (0, 704),
@@ -88,6 +89,9 @@ BUDGET = {
 # paired G2 lanes aborted processes with HSA_STATUS_ERROR_OUT_OF_RESOURCES.  The single-lane kernels below run one wave.
 SCRATCH_CAP = 4096
 SINGLE_WAVE = {"k_op_grp", "k_op_pair", "k_op_gt", "k_op_debug", "k_coop_debug"}
+# one lane per ciphertext (748 waves for configs[1]'s 1M shares: a 222 MB reservation at 4.6 KB per lane), at 256
+# registers so a wave shares its SIMD with a randomisation wave (k_prep.hip)
+PER_CIPHERTEXT = {"k_tpke_ct_prepare_h": 4700}
 ZERO_SPILL = ["k_coop_tpke_miller", "k_coop_final_exp_check", "k_msm_bucket_acc", "k_secp_verify",
               "k_rlc_census_stats", "k_rlc_suspect_split", "k_rlc_resolve", "k_tpke_rlc_sum", "k_ts_rlc_miller"]
 
@@ -126,5 +130,5 @@ def test_hot_kernels_do_not_spill(resources):
 def test_multi_wave_kernels_within_4kb_scratch(resources):
     over = [(n, r["private_segment_fixed_size"]) for n, r in resources.items()
             if not n.startswith(("lcb_asm_", "_Z")) and n not in SINGLE_WAVE
-            and r["private_segment_fixed_size"] > SCRATCH_CAP]
+            and r["private_segment_fixed_size"] > PER_CIPHERTEXT.get(n, SCRATCH_CAP)]
     assert not over, over
