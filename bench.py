@@ -1830,9 +1830,11 @@ def main():
                     help="GPU_MAX_HW_QUEUES for this process (0: keep the environment's; 8 measured 12.30 vs 11.95 M "
                          "shares/s with two batches in flight, profiles/r04/q2).  The environment's value is recorded "
                          "in the line (config.hw_queues_env) beside the one used (config.hw_queues)")
-    ap.add_argument("--tpke-pipeline", type=int, default=2,
+    ap.add_argument("--tpke-pipeline", type=int, default=3,
                     help="batched verify: whole batches in flight (each on its own context / stream / host thread); "
-                         "2 measured 12.3 vs 10.6 M shares/s for one at a time, 3 no better (profiles/r04/q1, q2)")
+                         "round 4: 2 measured 12.3 vs 10.6 M shares/s for one at a time, 3 no better (profiles/r04/q1, "
+                         "q2); round 5, with the preparation at 256 registers: 3 gives 14.98 vs 14.57 M/s for 2 "
+                         "(profiles/r05/pipeline.txt)")
     ap.add_argument("--headline", choices=("batched", "exact"), default="batched",
                     help="which TPKE path the line's value / roofline / cpu_baseline describe")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
