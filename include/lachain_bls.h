@@ -616,6 +616,7 @@ int lcb_g1_to_affine_dev(void *out_aff, uint8_t *ok, const uint8_t *points, size
 /* sum of k Jacobian G1 points (device, 144 B each, e.g. the per-GPU MSM partials after an RCCL all-gather);
    writes the serialized sum to out48 and/or the Jacobian sum to out_jac (device pointers, either nullable) */
 int lcb_g1_jac_sum_dev(uint8_t *out48, void *out_jac, const void *parts, size_t k, void *stream);
+int lcb_ctx_g1_jac_sum_dev(lcb_ctx *ctx, uint8_t *out48, void *out_jac, const void *parts, size_t k, void *stream);
 
 /* batched scalar multiplication of the G1 / G2 generator or of given points (key generation, synthetic inputs) */
 int lcb_g1_mul_batch(uint8_t *out, const uint8_t *points, int points_is_generator, const uint8_t *scalars, size_t n);

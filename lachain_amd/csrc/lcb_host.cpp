@@ -3167,14 +3167,18 @@ extern "C" int lcb_g1_to_affine_dev(void *out_aff, uint8_t *ok, const uint8_t *p
     if (n) lcbk_g1_to_affine(dim3(nblk(n)), (hipStream_t)stream, points, (u32)n, out_aff, ok);
     return launched("to_affine launch") ? 0 : -1;
 }
-extern "C" int lcb_g1_jac_sum_dev(uint8_t *out48, void *out_jac, const void *parts, size_t k, void *stream) {
-    CTX_OR(c, nullptr, -1)
+extern "C" int lcb_ctx_g1_jac_sum_dev(lcb_ctx *ctx, uint8_t *out48, void *out_jac, const void *parts, size_t k,
+                                      void *stream) {
+    CTX_OR(c, ctx, -1)
     Enq q(c, (hipStream_t)stream);
-    void *acc = out_jac ? out_jac : c->msm[11].get(LCB_G1_JAC_BYTES);
+    void *acc = out_jac ? out_jac : c->msm[14].get(LCB_G1_JAC_BYTES);
     if (!acc) { set_err("device allocation failed"); return -1; }
     lcbk_g1_jac_reduce_groups(dim3(1), q.s, parts, (u32)k, k ? (u32)k : 1u, acc);
     if (out48) lcbk_g1_jac_compress(dim3(1), q.s, acc, 1, out48);
     return launched("jac sum launch") ? 0 : -1;
+}
+extern "C" int lcb_g1_jac_sum_dev(uint8_t *out48, void *out_jac, const void *parts, size_t k, void *stream) {
+    return lcb_ctx_g1_jac_sum_dev(nullptr, out48, out_jac, parts, k, stream);
 }
 extern "C" int lcb_g1_msm(uint8_t out[48], const uint8_t *points, const uint8_t *scalars, size_t n) {
     SYNC_CTX_OR(c, -1)

@@ -202,7 +202,7 @@ _SIGS = {
 for _name in ("tpke_prepare_dev", "tpke_verify_prepared_dev", "tpke_verify_prepared_batched_dev", "tpke_batched_stats",
               "tpke_verify_shares_batched_dev", "ts_verify_prepared_batched_dev", "ts_verify_shares_batched_dev", "tpke_partial_decrypt_prepared_dev", "tpke_combine_dev",
               "tpke_verify_phase_ms", "ts_prepare_dev", "ts_verify_prepared_dev", "ts_assemble_dev", "g1_lagrange_dev",
-              "g2_lagrange_dev", "g1_msm_dev", "g1_msm_glv_dev", "g1_msm_phase_ms", "ecdsa_verify_hashed_dev",
+              "g2_lagrange_dev", "g1_msm_dev", "g1_msm_glv_dev", "g1_msm_phase_ms", "g1_jac_sum_dev", "ecdsa_verify_hashed_dev",
               "root_header_verify_dev", "ecdsa_pubkey_dev", "ecdsa_sign_hashed_dev", "ecdsa_phase_ms", "batched_census",
               "tpke_combine_ordered_dev", "ts_assemble_ordered_dev"):
     _res, _args = _SIGS["lcb_" + _name]
