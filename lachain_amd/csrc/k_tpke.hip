@@ -125,10 +125,13 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_miller(const u32 *lines, const
 extern "C" int lcbk_fe_slots() { return LCB_FE_ASM_SLOTS; }
 extern "C" __global__ void LCB_PAIR_BOUNDS k_final_exp_check(u32 *park, u32 n, uint8_t *accept) {
     LCB_LATENCY_PRIO();
-    __shared__ uint4 fx_lds[36 * LCB_BLOCK];      // per lane: the two Fp6 products of a slot multiplication
+    __shared__ uint4 fx_lds[36 * LCB_BLOCK];      // per lane: the double-width Fp2 products of an Fp6 product
+    typedef __attribute__((address_space(3))) uint4 lds_quad_t;
+    // wave w's 36 KB: quad g of lane l at g * 1024 + l * 16 (a wave's access is 1 KB contiguous per quad)
+    const u32 lds = (u32)(uintptr_t)(lds_quad_t *)fx_lds + (threadIdx.x >> 6) * (36u * 1024u) + (threadIdx.x & 63u) * 16u;
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    final_exp_asm(park, n, i, FxLds{fx_lds + threadIdx.x});
+    final_exp_asm(park, n, i, lds);
     fp12 f;
     fp12_load_soa(f, park, n, i);
     accept[i] = accept[i] && fp12_is_one(f);

@@ -136,3 +136,125 @@ def call(routines, label, inputs, agprs=None):
     def read(base):
         return sum(lane.v[base + j] << (32 * j) for j in range(12))
     return lane, read
+
+
+# ---------------------------------------------------------------- whole-library programs (asm_tower.hpp, round 5)
+# Labels, branches, calls with a return stack, SALU, global memory (a dict of 32-bit words keyed by byte address) and
+# LDS: enough to run lcb_r_pow_z / lcb_r_fp12_mul_n and their callees for one lane.
+def load_program(path=TOWER_HPP, macro="LCB_ASM_TOWER_LIBRARY_TEXT"):
+    """-> (instructions [(mnemonic, [operands])], {label: index})"""
+    src = open(path).read()
+    body = src[src.index("#define " + macro):]
+    body = body[:body.index('    ""\n')]
+    prog, labels = [], {}
+    for raw in re.findall(r'"(.*?)\\n"', body):
+        line = raw.strip()
+        if not line or line.startswith("."):
+            continue
+        if line.endswith(":"):
+            labels[line[:-1]] = len(prog)
+            continue
+        mn, _, rest = line.partition(" ")
+        ops = [o.strip() for o in rest.split(",")] if rest else []
+        prog.append((mn, ops))
+    return prog, labels
+
+
+def _split_off(op):
+    """'v[72:75] offset:1024' -> ('v[72:75]', 1024)"""
+    m = re.fullmatch(r"(\S+)\s+offset:(\d+)", op)
+    return (m.group(1), int(m.group(2))) if m else (op, 0)
+
+
+class ProgLane(Lane):
+    def __init__(self):
+        super().__init__()
+        self.mem, self.lds, self.scc = {}, {}, 0
+
+    def load(self, addr, n):
+        out = 0
+        for k in range(n):
+            a = addr + 4 * k
+            if a not in self.mem:
+                raise KeyError(f"load of unwritten memory 0x{a:x}")
+            out |= self.mem[a] << (32 * k)
+        return out
+
+    def store(self, addr, val, n):
+        for k in range(n):
+            self.mem[addr + 4 * k] = (val >> (32 * k)) & M32
+
+
+def run_program(prog, labels, entry, lane, max_steps=50_000_000):
+    pc, stack, target = labels[entry], [], None
+    g = lane.get
+    for _ in range(max_steps):
+        mn, ops = prog[pc]
+        pc += 1
+        lane.counts[mn] = lane.counts.get(mn, 0) + 1
+        if mn == "v_mad_u64_u32":
+            r = g(ops[2]) * g(ops[3]) + g(ops[4])
+            lane.put(ops[0], r & ((1 << 64) - 1)); lane.put(ops[1], r >> 64)
+        elif mn in ("v_add_co_u32_e64", "v_addc_co_u32_e64"):
+            r = g(ops[2]) + g(ops[3]) + (lane.getmask(ops[4]) if mn == "v_addc_co_u32_e64" else 0)
+            lane.put(ops[0], r & M32); lane.put(ops[1], r >> 32)
+        elif mn in ("v_sub_co_u32_e64", "v_subb_co_u32_e64"):
+            r = g(ops[2]) - g(ops[3]) - (lane.getmask(ops[4]) if mn == "v_subb_co_u32_e64" else 0)
+            lane.put(ops[0], r & M32); lane.put(ops[1], 1 if r < 0 else 0)
+        elif mn == "v_cndmask_b32_e64":
+            lane.put(ops[0], g(ops[2]) if lane.getmask(ops[3]) else g(ops[1]))
+        elif mn == "v_mul_lo_u32":
+            lane.put(ops[0], (g(ops[1]) * g(ops[2])) & M32)
+        elif mn in ("v_mov_b32", "s_mov_b32", "s_mov_b64", "v_accvgpr_read_b32", "v_accvgpr_write_b32"):
+            lane.put(ops[0], g(ops[1]))
+        elif mn == "s_add_u32":
+            if "@" in ops[2]:
+                target = ops[2].split("@")[0]
+            else:
+                r = g(ops[1]) + g(ops[2])
+                lane.put(ops[0], r & M32); lane.scc = r >> 32
+        elif mn == "s_addc_u32":
+            if "@" not in ops[2]:
+                r = g(ops[1]) + g(ops[2]) + lane.scc
+                lane.put(ops[0], r & M32); lane.scc = r >> 32
+        elif mn == "s_sub_u32":
+            r = g(ops[1]) - g(ops[2])
+            lane.put(ops[0], r & M32); lane.scc = 1 if r < 0 else 0
+        elif mn == "s_mul_i32":
+            lane.put(ops[0], (g(ops[1]) * g(ops[2])) & M32)
+        elif mn == "s_cmp_eq_u32":
+            lane.scc = 1 if g(ops[0]) == g(ops[1]) else 0
+        elif mn == "s_cmp_lg_u32":
+            lane.scc = 1 if g(ops[0]) != g(ops[1]) else 0
+        elif mn in ("s_cbranch_scc1", "s_cbranch_scc0"):
+            if lane.scc == (1 if mn.endswith("1") else 0):
+                pc = labels[ops[0]]
+        elif mn in ("s_nop", "s_waitcnt", "s_getpc_b64"):
+            pass
+        elif mn == "s_swappc_b64":
+            stack.append(pc)
+            pc = labels[target]
+        elif mn == "s_setpc_b64":
+            if not stack:
+                return
+            pc = stack.pop()
+        elif mn in ("global_load_dwordx4", "global_store_dwordx4"):
+            if mn == "global_load_dwordx4":
+                dst, voff, sbase = ops
+                lane.put(dst, lane.load(g(sbase) + g(voff), 4))
+            else:
+                voff, src, sbase = ops
+                lane.store(g(sbase) + g(voff), g(src), 4)
+        elif mn in ("ds_write_b128", "ds_read_b128"):
+            if mn == "ds_write_b128":
+                src, off = _split_off(ops[1])
+                a = g(ops[0]) + off
+                for k in range(4):
+                    lane.lds[a + 4 * k] = (g(src) >> (32 * k)) & M32
+            else:
+                addr, off = _split_off(ops[1])
+                a = g(addr) + off
+                lane.put(ops[0], sum(lane.lds[a + 4 * k] << (32 * k) for k in range(4)))
+        else:
+            raise NotImplementedError(mn)
+    raise RuntimeError("step limit")

@@ -449,6 +449,301 @@ def gen_cyc_sqr_n():
     return ["lcb_r_cyc_sqr_n:"] + b
 
 
+# ------------------------------------------------------------------ Fp12 product over the AGPR accumulator (round 5)
+# lcb_r_fp12m: a[0:143] <- a[0:143] * M, M an Fp12 in a memory slot.  Karatsuba over Fp6 (t0 = a0 m0, t1 = a1 m1,
+# t2 = (a0 + a1)(m0 + m1); r0 = t0 + v t1, r1 = t2 - t0 - t1), each Fp6 product lazily reduced: its six Fp2 products
+# (Karatsuba, three 12 x 12 products each) stay double-width (mod 2^768) and every output coefficient is ONE Montgomery
+# reduction of its double-width sum plus a multiple of p^2 that makes it nonnegative — 18 products + 6 REDCs per Fp6
+# product (3,528 MADs) where the Fp2-level lazy product needs 12 REDCs (4,464).  Double-width Fp2 products go through
+# LDS (three per Fp6 product, 144 words per lane); the t0 / t1 halves through a caller-supplied memory slot.
+# Entry points: lcb_r_fp12_mul_n (slot x slot -> slot, optional conjugate of the first operand) and lcb_r_pow_z
+# (conj(base^|z|): the squaring runs of lcb_r_cyc_sqr and the five products by the base with the accumulator in
+# AGPRs throughout).
+S_N16, S_M, S_T = 19, 20, 22            # n * 16; s[20:21] M slot; s[22:23] tmp slot
+S_A, S_CONJ, S_DST = 56, 65, 60         # s[56:57] first-operand slot; conj flag; s[60:61] destination slot
+S_Q0, S_SUM = 62, 64                    # y operand of lcb_r_fp6m: first quad in M; 1 = M[q0..] + M[q0 + 18..]
+S_ADDR, S_QT = 66, 68                   # s[66:67] address, s68 quad temp
+S_RET6 = 72                             # s[72:73] lcb_r_fp6m return address
+V_OFF, V_LDS = 248, 249                 # lane byte offset in slots; lane byte address in LDS (quad g at + g * 1024)
+FP12_SGPRS = [16, 17, 18, 24, 25] + list(range(56, 74))
+
+F2_XA, F2_XB, F2_YA, F2_YB = [list(range(12 * i, 12 * i + 12)) for i in range(4)]
+F2_SX, F2_SY = list(range(48, 60)), list(range(60, 72))
+F2_P0, F2_P1, F2_P2 = list(range(72, 96)), list(range(96, 120)), list(range(120, 144))
+F2_ACCS = [144, 148, 152]
+F2_RE, F2_IM = F2_P0, F2_P2
+PR = list(range(160, 172))
+T1, T2, T3 = list(range(172, 196)), list(range(196, 220)), list(range(220, 244))
+FP12_VMAX = 244
+
+
+def pp_limbs(k):
+    return limbs(k * P * P, 2 * N)
+
+
+def gen_fp2dw():
+    """lcb_r_fp2dw: (XA + XB i)(YA + YB i), inputs < p, -> RE = XA YA - XB YB, IM = (XA + XB)(YA + YB) - XA YA - XB YB,
+    double-width mod 2^768 (RE may be 'negative').  Leaf: v0..v155, returns through s[28:29]."""
+    b = merge([add_chain(F2_SX, F2_XA, F2_XB, LIN_CARRY[0]), add_chain(F2_SY, F2_YA, F2_YB, LIN_CARRY[1])])
+    b += comba([dict(a=F2_XA, b=F2_YA, acc=F2_ACCS[0], out=F2_P0, c=MAD_CARRY[0]),
+                dict(a=F2_XB, b=F2_YB, acc=F2_ACCS[1], out=F2_P1, c=MAD_CARRY[1]),
+                dict(a=F2_SX, b=F2_SY, acc=F2_ACCS[2], out=F2_P2, c=MAD_CARRY[2])])
+    # the IM stream reads P0[j] in the round before the RE stream overwrites it
+    b += merge([sub_chain(F2_P2, F2_P2, F2_P0, LIN_CARRY[0]), sub_chain(F2_P0, F2_P0, F2_P1, LIN_CARRY[1])])
+    b += sub_chain(F2_P2, F2_P2, F2_P1, LIN_CARRY[0])
+    return ["lcb_r_fp2dw:"] + hazard_fix(b + ["s_setpc_b64 s[28:29]"])
+
+
+def quad_addr(base, q):
+    """s[66:67] = slot base s[base:base+1] + q * n16; q = (sgpr or None, constant)"""
+    sg, k = q
+    out = [f"s_mov_b32 s{S_QT}, {k}" if sg is None else f"s_add_u32 s{S_QT}, s{sg}, {k}"]
+    return out + [f"s_mul_i32 s{S_QT}, s{S_QT}, s{S_N16}", f"s_add_u32 s{S_ADDR}, s{base}, s{S_QT}",
+                  f"s_addc_u32 s{S_ADDR + 1}, s{base + 1}, 0"]
+
+
+def next_quad():
+    return [f"s_add_u32 s{S_ADDR}, s{S_ADDR}, s{S_N16}", f"s_addc_u32 s{S_ADDR + 1}, s{S_ADDR + 1}, 0"]
+
+
+def gload(dst, base, q, kind="v"):
+    """len(dst) // 4 consecutive quads from quad q of a slot into contiguous registers dst (v or a)"""
+    out = quad_addr(base, q)
+    for g in range(len(dst) // 4):
+        out.append(f"global_load_dwordx4 {kind}[{dst[4 * g]}:{dst[4 * g] + 3}], v{V_OFF}, s[{S_ADDR}:{S_ADDR + 1}]")
+        if g < len(dst) // 4 - 1:
+            out += next_quad()
+    return out
+
+
+def gstore(base, q, src, kind="v"):
+    out = quad_addr(base, q)
+    for g in range(len(src) // 4):
+        out.append(f"global_store_dwordx4 v{V_OFF}, {kind}[{src[4 * g]}:{src[4 * g] + 3}], s[{S_ADDR}:{S_ADDR + 1}]")
+        if g < len(src) // 4 - 1:
+            out += next_quad()
+    return out
+
+
+def lds_write(q, src):
+    return [f"ds_write_b128 v{V_LDS}, v[{src[4 * g]}:{src[4 * g] + 3}] offset:{(q + g) * 1024}"
+            for g in range(len(src) // 4)]
+
+
+def lds_read(dst, q):
+    return [f"ds_read_b128 v[{dst[4 * g]}:{dst[4 * g] + 3}], v{V_LDS} offset:{(q + g) * 1024}"
+            for g in range(len(dst) // 4)]
+
+
+def modadd(r, x, y, tmp, c):
+    return add_chain(r, x, y, c) + condsub(r, PR, tmp, c)
+
+
+def modsub(r, x, y, tmp, c1, c2):
+    """r = x - y mod p (x, y < p): borrow ? r + p : r"""
+    s = sub_chain(r, x, y, c1) + add_chain(tmp, r, PR, c2)
+    return s + [f"v_cndmask_b32_e64 v{r[j]}, v{r[j]}, v{tmp[j]}, {sp(c1)}" for j in range(N)]
+
+
+_lbl = [0]
+
+
+def label(stem):
+    _lbl[0] += 1
+    return f"lcb_{stem}_{_lbl[0]}"
+
+
+def fp6_x(k, part, dst):                       # x_k.part of lcb_r_fp6m's x = a[0:71]
+    return agpr_read(dst, 24 * k + 12 * part)
+
+
+def fp6_y(k, part, dst, tmp, c):
+    """y_k.part: M quads q0 + 6k + 3 part (+ the same 18 quads on when s64 = 1, reduced mod p)"""
+    skip = label("fp6y")
+    s = gload(dst, S_M, (S_Q0, 6 * k + 3 * part))
+    s += [f"s_cmp_eq_u32 s{S_SUM}, 0", f"s_cbranch_scc1 {skip}"]
+    s += gload(tmp[:12], S_M, (S_Q0, 18 + 6 * k + 3 * part)) + ["s_waitcnt vmcnt(0)"]
+    s += modadd(dst, dst, tmp[:12], tmp[12:24], c)
+    s += [f"{skip}:", "s_nop 4", "s_waitcnt vmcnt(0)"]
+    return s
+
+
+def fp6_operands(ks):
+    """fp2dw inputs: x = x_k (one index) or x_k1 + x_k2 (two), same for y"""
+    s = []
+    for part, X, Y in ((0, F2_XA, F2_YA), (1, F2_XB, F2_YB)):
+        s += fp6_x(ks[0], part, X)
+        if len(ks) == 2:
+            s += fp6_x(ks[1], part, T1[:12]) + ["s_nop 1"] + modadd(X, X, T1[:12], T1[12:], LIN_CARRY[0])
+        s += fp6_y(ks[0], part, Y, T2, LIN_CARRY[1])
+        if len(ks) == 2:
+            s += fp6_y(ks[1], part, T1[:12], T2, LIN_CARRY[1]) + modadd(Y, Y, T1[:12], T2[:12], LIN_CARRY[2])
+    return s + call_fp2dw()
+
+
+def call_fp2dw():
+    return [f"s_getpc_b64 s[{S_CALL}:{S_CALL + 1}]", f"s_add_u32 s{S_CALL}, s{S_CALL}, lcb_r_fp2dw@rel32@lo+4",
+            f"s_addc_u32 s{S_CALL + 1}, s{S_CALL + 1}, lcb_r_fp2dw@rel32@hi+12",
+            f"s_swappc_b64 s[28:29], s[{S_CALL}:{S_CALL + 1}]"]
+
+
+def call_ret(label_, ret):
+    return [f"s_getpc_b64 s[{S_CALL}:{S_CALL + 1}]", f"s_add_u32 s{S_CALL}, s{S_CALL}, {label_}@rel32@lo+4",
+            f"s_addc_u32 s{S_CALL + 1}, s{S_CALL + 1}, {label_}@rel32@hi+12",
+            f"s_swappc_b64 s[{ret}:{ret + 1}], s[{S_CALL}:{S_CALL + 1}]"]
+
+
+# LDS quads of the three double-width diagonal products v_k = x_k y_k: re at 12k, im at 12k + 6
+def lds_v(k, part):
+    return 12 * k + 6 * part
+
+
+def fp6_finish(RE, IM, offs, nsub, out_a):
+    """RE, IM (+ offs[0], offs[1] multiples of p^2) -> Montgomery reductions -> < p (nsub conditional subtractions)
+    -> a[out_a .. out_a + 23]"""
+    s = []
+    s += merge([movs_const(T2, pp_limbs(offs[0])), movs_const(T3, pp_limbs(offs[1]))])
+    s += merge([add_chain(RE, RE, T2, LIN_CARRY[0]), add_chain(IM, IM, T3, LIN_CARRY[1])])
+    M1, M2 = list(range(0, 12)), list(range(12, 24))
+    s += redc([dict(u=RE, m=M1, acc=F2_ACCS[0], c=MAD_CARRY[0]), dict(u=IM, m=M2, acc=F2_ACCS[1], c=MAD_CARRY[1])], PR)
+    ra, rb = RE[N:], IM[N:]
+    for _ in range(nsub):
+        s += merge([condsub(ra, PR, list(range(24, 36)), LIN_CARRY[0]),
+                    condsub(rb, PR, list(range(36, 48)), LIN_CARRY[1])])
+    return s + agpr_write(out_a, ra) + agpr_write(out_a + 12, rb)
+
+
+def gen_fp6m():
+    """lcb_r_fp6m: a[144:215] <- x * y (Fp6, reduced < p); x = a[0:71], y from the M slot at quad s62 (+ quad s62 + 18
+    when s64 = 1).  Returns through s[72:73]; clobbers v0..v243, LDS quads 0..35 of the lane."""
+    b = []
+    for k in range(3):                                               # v_k = x_k y_k -> LDS
+        b += fp6_operands([k])
+        b += lds_write(lds_v(k, 0), F2_RE) + lds_write(lds_v(k, 1), F2_IM) + ["s_waitcnt lgkmcnt(0)"]
+    # c0 = v0 + xi (X12 - v1 - v2).  The sums x1 + x2, y1 + y2 are reduced, so X12 - v1 - v2 is congruent to, not
+    # equal to, x1 y2 + x2 y1: as integers re in (-3p^2, 3p^2), im in (-4p^2, 2p^2), and c0 re in (-6p^2, 8p^2),
+    # im in (-7p^2, 7p^2): + (6, 7) p^2 -> [0, 14p^2), REDC < 2.43p, two conditional subtractions
+    b += fp6_operands([1, 2])
+    RE, IM = F2_RE, F2_IM
+    for k in (1, 2):
+        b += lds_read(T1, lds_v(k, 0)) + lds_read(T2, lds_v(k, 1)) + ["s_waitcnt lgkmcnt(0)"]
+        b += merge([sub_chain(RE, RE, T1, LIN_CARRY[0]), sub_chain(IM, IM, T2, LIN_CARRY[1])])
+    # xi D = (RE - IM, RE + IM): the T1 stream reads IM[j] in the round before the IM stream overwrites it
+    b += merge([sub_chain(T1, RE, IM, LIN_CARRY[0]), add_chain(IM, RE, IM, LIN_CARRY[1])])
+    b += lds_read(T2, lds_v(0, 0)) + lds_read(T3, lds_v(0, 1)) + ["s_waitcnt lgkmcnt(0)"]
+    b += merge([add_chain(T1, T1, T2, LIN_CARRY[0]), add_chain(IM, IM, T3, LIN_CARRY[1])])
+    b += fp6_finish(T1, IM, (6, 7), 2, 144)
+    # c1 = X01 - v0 - v1 + xi v2: re in (-6p^2, 4p^2), im in (-5p^2, 5p^2) -> [0, 10p^2), REDC < 2.02p
+    b += fp6_operands([0, 1])
+    for k in (0, 1):
+        b += lds_read(T1, lds_v(k, 0)) + lds_read(T2, lds_v(k, 1)) + ["s_waitcnt lgkmcnt(0)"]
+        b += merge([sub_chain(RE, RE, T1, LIN_CARRY[0]), sub_chain(IM, IM, T2, LIN_CARRY[1])])
+    b += lds_read(T1, lds_v(2, 0)) + lds_read(T2, lds_v(2, 1)) + ["s_waitcnt lgkmcnt(0)"]
+    b += merge([sub_chain(T3, T1, T2, LIN_CARRY[0]), add_chain(T1, T1, T2, LIN_CARRY[1])])
+    b += merge([add_chain(RE, RE, T3, LIN_CARRY[0]), add_chain(IM, IM, T1, LIN_CARRY[1])])
+    b += fp6_finish(RE, IM, (6, 5), 2, 168)
+    # c2 = X02 - v0 - v2 + v1: re, im in (-4p^2, 4p^2) -> [0, 8p^2), REDC < 1.82p
+    b += fp6_operands([0, 2])
+    for k, op in ((0, sub_chain), (2, sub_chain), (1, add_chain)):
+        b += lds_read(T1, lds_v(k, 0)) + lds_read(T2, lds_v(k, 1)) + ["s_waitcnt lgkmcnt(0)"]
+        b += merge([op(RE, RE, T1, LIN_CARRY[0]), op(IM, IM, T2, LIN_CARRY[1])])
+    b += fp6_finish(RE, IM, (4, 4), 1, 192)
+    return ["lcb_r_fp6m:"] + hazard_fix(b + [f"s_setpc_b64 s[{S_RET6}:{S_RET6 + 1}]"])
+
+
+def gen_fp12m():
+    """lcb_r_fp12m: a[0:143] <- a[0:143] * M (components < p in and out); M slot s[20:21], tmp slot s[22:23] (its
+    36 quads are overwritten).  Returns through s[30:31]; clobbers v0..v243, a144..a215."""
+    X, Y, Z, W = T1[:12], T1[12:], T2[:12], T2[12:]
+    b = movs_const(PR, PL) + [f"s_mov_b32 s{S_PINV}, 0x{PINV:08x}"]
+    b += [f"s_mov_b32 s{S_Q0}, 0", f"s_mov_b32 s{S_SUM}, 0"] + call_ret("lcb_r_fp6m", S_RET6)   # t0 = a0 m0
+    b += ["s_nop 4"] + gstore(S_T, (None, 0), list(range(144, 216)), "a")
+    for i in range(6):                                   # a[0:71] <- a1, a[72:143] <- s = a0 + a1
+        b += agpr_read(X, 12 * i) + agpr_read(Y, 72 + 12 * i) + ["s_nop 1"]
+        b += agpr_write(12 * i, Y) + modadd(X, X, Y, Z, LIN_CARRY[0]) + agpr_write(72 + 12 * i, X)
+    b += [f"s_mov_b32 s{S_Q0}, 18"] + call_ret("lcb_r_fp6m", S_RET6)                            # t1 = a1 m1
+    b += ["s_nop 4"] + gstore(S_T, (None, 18), list(range(144, 216)), "a")
+    for i in range(6):                                   # a[0:71] <- s
+        b += agpr_read(X, 72 + 12 * i) + ["s_nop 1"] + agpr_write(12 * i, X)
+    b += [f"s_mov_b32 s{S_Q0}, 0", f"s_mov_b32 s{S_SUM}, 1"] + call_ret("lcb_r_fp6m", S_RET6)   # t2 = s (m0 + m1)
+    b += ["s_nop 4", "s_waitcnt vmcnt(0)"]
+    # r1 = t2 - t0 - t1 -> a[72:143]
+    for k in range(3):
+        for part in range(2):
+            i = 2 * k + part
+            b += agpr_read(X, 144 + 12 * i) + gload(Y, S_T, (None, 3 * i)) + gload(Z, S_T, (None, 18 + 3 * i))
+            b += ["s_waitcnt vmcnt(0)"] + modsub(X, X, Y, W, LIN_CARRY[0], LIN_CARRY[1])
+            b += modsub(X, X, Z, W, LIN_CARRY[2], LIN_CARRY[3]) + agpr_write(72 + 12 * i, X)
+    # r0 = t0 + v t1 -> a[0:71]: (v t1)_0 = xi t1_2 = (t1_2a - t1_2b, t1_2a + t1_2b), (v t1)_1 = t1_0, (v t1)_2 = t1_1
+    U = T3[:12]
+    b += gload(Y, S_T, (None, 18 + 12)) + gload(Z, S_T, (None, 18 + 15)) + ["s_waitcnt vmcnt(0)"]
+    b += modsub(U, Y, Z, W, LIN_CARRY[0], LIN_CARRY[1]) + modadd(Y, Y, Z, W, LIN_CARRY[2])      # U = re, Y = im
+    for part, V in ((0, U), (1, Y)):
+        b += gload(X, S_T, (None, 3 * part)) + ["s_waitcnt vmcnt(0)"] + modadd(X, X, V, W, LIN_CARRY[0])
+        b += agpr_write(12 * part, X)
+    for k in (1, 2):
+        for part in range(2):
+            i = 2 * k + part
+            b += gload(X, S_T, (None, 3 * i)) + gload(Y, S_T, (None, 18 + 3 * (i - 2))) + ["s_waitcnt vmcnt(0)"]
+            b += modadd(X, X, Y, W, LIN_CARRY[0]) + agpr_write(12 * i, X)
+    return ["lcb_r_fp12m:"] + hazard_fix(b + ["s_setpc_b64 s[30:31]"])
+
+
+def conj_c1():
+    """a[72:143] <- p - a[72:143] reduced (0 stays 0)"""
+    X, Y = T1[:12], T1[12:]
+    s = movs_const(PR, PL)
+    for i in range(6, 12):
+        s += agpr_read(X, 12 * i) + ["s_nop 1"] + sub_chain(Y, PR, X, LIN_CARRY[0])
+        s += condsub(Y, PR, X, LIN_CARRY[1]) + agpr_write(12 * i, Y)
+    return s
+
+
+def walk_load(base):
+    """a[0:143] <- the 36 quads of the slot at s[base:base+1] (s[16:17] walks)"""
+    s = [f"s_mov_b64 s[16:17], s[{base}:{base + 1}]"]
+    for g in range(36):
+        s.append(f"global_load_dwordx4 a[{4 * g}:{4 * g + 3}], v{V_OFF}, s[16:17]")
+        if g < 35:
+            s += ["s_add_u32 s16, s16, s19", "s_addc_u32 s17, s17, 0"]
+    return s + ["s_waitcnt vmcnt(0)"]
+
+
+def walk_store(base):
+    s = ["s_nop 4", f"s_mov_b64 s[16:17], s[{base}:{base + 1}]"]
+    for g in range(36):
+        s.append(f"global_store_dwordx4 v{V_OFF}, a[{4 * g}:{4 * g + 3}], s[16:17]")
+        if g < 35:
+            s += ["s_add_u32 s16, s16, s19", "s_addc_u32 s17, s17, 0"]
+    return s
+
+
+def gen_fp12_mul_n():
+    """lcb_r_fp12_mul_n: slot s[60:61] <- (s65 ? conj(A) : A) * M; A slot s[56:57], M slot s[20:21], tmp slot
+    s[22:23] (may be the destination or A; not M)"""
+    skip = label("mulnc")
+    b = ["s_mov_b64 s[24:25], s[30:31]"] + walk_load(S_A)
+    b += [f"s_cmp_eq_u32 s{S_CONJ}, 0", f"s_cbranch_scc1 {skip}"] + conj_c1() + [f"{skip}:", "s_nop 4"]
+    b += call_ret("lcb_r_fp12m", 30) + walk_store(S_DST) + ["s_setpc_b64 s[24:25]"]
+    return ["lcb_r_fp12_mul_n:"] + hazard_fix(b)
+
+
+def gen_pow_z():
+    """lcb_r_pow_z: slot s[60:61] <- conj(B^|z|), B the unitary Fp12 in slot s[20:21] (the same slot may be the
+    destination); tmp slot s[22:23].  The runs of squarings between the set bits of |z| (1, 2, 3, 9, 32, 16) are
+    lcb_r_cyc_sqr calls, the five products by B lcb_r_fp12m; the accumulator never leaves a[0:143]."""
+    b = ["s_mov_b64 s[24:25], s[30:31]"] + walk_load(S_M)
+    runs = [1, 2, 3, 9, 32, 16]
+    for t, cnt in enumerate(runs):
+        loop = label("pzrun")
+        b += [f"s_mov_b32 s18, {cnt}", f"{loop}:"] + call_ret("lcb_r_cyc_sqr", 30)
+        b += ["s_sub_u32 s18, s18, 1", "s_cmp_lg_u32 s18, 0", f"s_cbranch_scc1 {loop}", "s_nop 4"]
+        if t < len(runs) - 1:
+            b += call_ret("lcb_r_fp12m", 30) + ["s_nop 4"]
+    b += conj_c1() + walk_store(S_DST) + ["s_setpc_b64 s[24:25]"]
+    return ["lcb_r_pow_z:"] + hazard_fix(b)
+
+
 # ------------------------------------------------------------------ emit
 def clobbers_n():
     regs = [f'"v{i}"' for i in range(VMAX)] + [f'"a{i}"' for i in range(A_PARK + 2 * N)]
@@ -465,7 +760,8 @@ def clobbers(nv=VMAX):
 def emit():
     fp4_txt, fp4_outs, fp4_used = gen_fp4()
     cyc_txt = gen_cyc_sqr(fp4_outs, fp4_used)
-    routines = [gen_cyc_sqr_n(), cyc_txt, fp4_txt]
+    routines = [gen_cyc_sqr_n(), cyc_txt, fp4_txt, gen_pow_z(), gen_fp12_mul_n(), gen_fp12m(), gen_fp6m(),
+                gen_fp2dw()]
     lib = "\n".join("  .p2align 8\n" + "\n".join(("  " + l) if not l.endswith(":") else l for l in r)
                     for r in routines)
     esc = lib.replace("\\", "\\\\").replace('"', '\\"')
@@ -492,6 +788,35 @@ __device__ __forceinline__ void lcb_asm_cyc_sqr_n(const u32 *slot_in, u32 *slot_
         : "+{{s18}}"(count)
         : "{{s[20:21]}}"(slot_in), "{{s[22:23]}}"(slot_out), "{{s19}}"(n16), "{{v248}}"(lane_off)
         : {clobbers_n()}, "memory");
+}}
+""")
+    fp12_clob = ", ".join([f'"v{i}"' for i in range(VMAX)] + [f'"a{i}"' for i in range(216)] +
+                          [f'"s{x}"' for x in sorted(set(CLOBBER_SGPRS) | {16, 17, 18, 24, 25, 62, 64, 66, 67, 68,
+                                                                              72, 73})] + ['"scc"', '"vcc"'])
+    call_seq = lambda lbl: (f'"s_getpc_b64 s[{S_CALL}:{S_CALL + 1}]\\n\\t"\n'
+                            f'        "s_add_u32 s{S_CALL}, s{S_CALL}, {lbl}@rel32@lo+4\\n\\t"\n'
+                            f'        "s_addc_u32 s{S_CALL + 1}, s{S_CALL + 1}, {lbl}@rel32@hi+12\\n\\t"\n'
+                            f'        "s_swappc_b64 s[30:31], s[{S_CALL}:{S_CALL + 1}]"')
+    o.append(f"""
+// dst <- (conj_a ? conj(a) : a) * m over Fp12 slots (lcb_r_fp12_mul_n: Karatsuba over lazily reduced Fp6 products,
+// the accumulator in AGPRs); tmp: a slot the call may overwrite (the destination or a, never m); lds_addr: this
+// lane's LDS byte address (36 quads at lds_addr + g * 1024).  Clobbers v0..v247, a0..a215.
+__device__ __forceinline__ void lcb_asm_fp12_mul_n(const u32 *a, u32 conj_a, const u32 *m, u32 *tmp, u32 *dst, u32 n16,
+                                                   u32 lane_off, u32 lds_addr) {{
+    asm volatile({call_seq("lcb_r_fp12_mul_n")}
+        :
+        : "{{s[56:57]}}"(a), "{{s65}}"(conj_a), "{{s[20:21]}}"(m), "{{s[22:23]}}"(tmp), "{{s[60:61]}}"(dst), "{{s19}}"(n16),
+          "{{v248}}"(lane_off), "{{v249}}"(lds_addr)
+        : {fp12_clob}, "memory");
+}}
+// dst <- conj(base^|z|) = base^z for a unitary base (lcb_r_pow_z; dst may be base); tmp: a slot the call may
+// overwrite (not base).  Clobbers v0..v247, a0..a215.
+__device__ __forceinline__ void lcb_asm_pow_z(const u32 *base, u32 *tmp, u32 *dst, u32 n16, u32 lane_off, u32 lds_addr) {{
+    asm volatile({call_seq("lcb_r_pow_z")}
+        :
+        : "{{s[20:21]}}"(base), "{{s[22:23]}}"(tmp), "{{s[60:61]}}"(dst), "{{s19}}"(n16), "{{v248}}"(lane_off),
+          "{{v249}}"(lds_addr)
+        : {fp12_clob}, "memory");
 }}
 """)
     return "".join(o), dict(fp4_outs=fp4_outs, fp4_used=len(fp4_used), n_cyc=len(cyc_txt), n_fp4=len(fp4_txt))
