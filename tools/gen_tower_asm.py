@@ -557,27 +557,40 @@ def fp6_x(k, part, dst):                       # x_k.part of lcb_r_fp6m's x = a[
     return agpr_read(dst, 24 * k + 12 * part)
 
 
-def fp6_y(k, part, dst, tmp, c):
-    """y_k.part: M quads q0 + 6k + 3 part (+ the same 18 quads on when s64 = 1, reduced mod p)"""
-    skip = label("fp6y")
-    s = gload(dst, S_M, (S_Q0, 6 * k + 3 * part))
-    s += [f"s_cmp_eq_u32 s{S_SUM}, 0", f"s_cbranch_scc1 {skip}"]
-    s += gload(tmp[:12], S_M, (S_Q0, 18 + 6 * k + 3 * part)) + ["s_waitcnt vmcnt(0)"]
-    s += modadd(dst, dst, tmp[:12], tmp[12:24], c)
-    s += [f"{skip}:", "s_nop 4", "s_waitcnt vmcnt(0)"]
-    return s
-
-
 def fp6_operands(ks):
-    """fp2dw inputs: x = x_k (one index) or x_k1 + x_k2 (two), same for y"""
+    """fp2dw inputs: x = x_k (one index) or x_k1 + x_k2 (two), the same for y (each y_k itself M[q0 + ..] or, when
+    s64 = 1, M[q0 + ..] + M[q0 + 18 + ..]), all reduced mod p.  Every load is issued first and the x work (AGPR
+    reads and sums) runs while they are in flight."""
+    P0 = F2_P0
+    q = lambda k, part, hi: (S_Q0, 18 * hi + 6 * k + 3 * part)                      # noqa: E731
+    first = [(ks[0], YA_, YB_) for YA_, YB_ in [(F2_YA, F2_YB)]]
+    if len(ks) == 2:
+        first.append((ks[1], T2[:12], T2[12:]))
+    second = [(ks[0], T1[:12], T1[12:])] + ([(ks[1], T3[:12], T3[12:])] if len(ks) == 2 else [])
     s = []
-    for part, X, Y in ((0, F2_XA, F2_YA), (1, F2_XB, F2_YB)):
-        s += fp6_x(ks[0], part, X)
-        if len(ks) == 2:
-            s += fp6_x(ks[1], part, T1[:12]) + ["s_nop 1"] + modadd(X, X, T1[:12], T1[12:], LIN_CARRY[0])
-        s += fp6_y(ks[0], part, Y, T2, LIN_CARRY[1])
-        if len(ks) == 2:
-            s += fp6_y(ks[1], part, T1[:12], T2, LIN_CARRY[1]) + modadd(Y, Y, T1[:12], T2[:12], LIN_CARRY[2])
+    for k, A, B in first:
+        s += gload(A, S_M, q(k, 0, 0)) + gload(B, S_M, q(k, 1, 0))
+    skip1, skip2 = label("fp6ld"), label("fp6sum")
+    s += [f"s_cmp_eq_u32 s{S_SUM}, 0", f"s_cbranch_scc1 {skip1}"]
+    for k, A, B in second:
+        s += gload(A, S_M, q(k, 0, 1)) + gload(B, S_M, q(k, 1, 1))
+    s += [f"{skip1}:", "s_nop 4"]
+    # x (AGPRs) while the loads are in flight
+    s += fp6_x(ks[0], 0, F2_XA) + fp6_x(ks[0], 1, F2_XB)
+    if len(ks) == 2:
+        s += fp6_x(ks[1], 0, F2_SX) + fp6_x(ks[1], 1, P0[:12]) + ["s_nop 1"]
+        s += merge([modadd(F2_XA, F2_XA, F2_SX, F2_SY, LIN_CARRY[0]),
+                    modadd(F2_XB, F2_XB, P0[:12], P0[12:], LIN_CARRY[1])])
+    s += ["s_waitcnt vmcnt(0)", f"s_cmp_eq_u32 s{S_SUM}, 0", f"s_cbranch_scc1 {skip2}"]
+    tmps = [P0[:12], P0[12:], F2_P1[:12], F2_P1[12:]]
+    streams = []
+    for t, ((k, A, B), (_, A2, B2)) in enumerate(zip(first, second)):
+        streams.append(modadd(A, A, A2, tmps[2 * t], LIN_CARRY[2 * t]))
+        streams.append(modadd(B, B, B2, tmps[2 * t + 1], LIN_CARRY[2 * t + 1]))
+    s += merge(streams) + [f"{skip2}:", "s_nop 4"]
+    if len(ks) == 2:
+        s += merge([modadd(F2_YA, F2_YA, T2[:12], P0[:12], LIN_CARRY[0]),
+                    modadd(F2_YB, F2_YB, T2[12:], P0[12:], LIN_CARRY[1])])
     return s + call_fp2dw()
 
 
