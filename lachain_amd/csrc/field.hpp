@@ -165,7 +165,13 @@ DI u32x12 lcb_fp_pow_sel(int k, const u32x12 &t1, const u32x12 &t3, const u32x12
     default: return t15;
     }
 }
-DN u32x12 lcb_fp_pow_v(u32x12 av, const u32 *e) {
+// which: 0 = p - 2, 1 = (p + 1)/4, 2 = (p - 1)/2, 3 = (p - 3)/4.  The selector is made wave-uniform (readfirstlane)
+// so the exponent words come through the scalar cache and every bit test is a scalar branch: with the constant's
+// address as a (VGPR) argument each of the ~450 bit reads was a vector load the lane waited for.
+DN u32x12 lcb_fp_pow_v(u32x12 av, int which) {
+    which = __builtin_amdgcn_readfirstlane(which);
+    const u32 *e = which == 0 ? LCB_P_MINUS_2 : which == 1 ? LCB_P_PLUS1_DIV4 : which == 2 ? LCB_P_MINUS1_DIV2
+                                                                                          : LCB_P_MINUS3_DIV4;
     int top = 383;
     while (top > 0 && !((e[top >> 5] >> (top & 31)) & 1)) top--;
     u32x12 a2 = lcb_asm_fp_mul(av, av);
@@ -201,8 +207,8 @@ DN u32x12 lcb_fp_pow_v(u32x12 av, const u32 *e) {
     }
     return acc;
 }
-DI void fp_pow_const(fp &r, const fp &a, const u32 *e) { r = fp_from_v(lcb_fp_pow_v(fp_to_v(a), e)); }
-DI void fp_inv(fp &r, const fp &a) { fp_pow_const(r, a, LCB_P_MINUS_2); }   // a^(p-2): 463 products
+DI void fp_pow_const(fp &r, const fp &a, int which) { r = fp_from_v(lcb_fp_pow_v(fp_to_v(a), which)); }
+DI void fp_inv(fp &r, const fp &a) { fp_pow_const(r, a, 0); }   // a^(p-2): 463 products
 
 // ---- inversion by binary GCD (Pornin, "Optimized Binary GCD for Modular Inversion", eprint 2020/972): 26 outer
 // iterations; each runs 30 divsteps on 62-bit approximations of a, b (the low 30 bits and the top 32 bits of the
@@ -371,7 +377,7 @@ DN void fp_inv_gcd(fp &r, const fp &x) {
 // mcl Fp::squareRoot for p = 3 mod 4: y = a^((p+1)/4), valid iff y^2 == a
 DI bool fp_sqrt(fp &r, const fp &a) {
     fp y, t;
-    fp_pow_const(y, a, LCB_P_PLUS1_DIV4);
+    fp_pow_const(y, a, 1);
     fp_sqr(t, y);
     bool ok = fp_eq(t, a); // compare before writing r: callers pass r aliasing a
     r = y;
@@ -380,7 +386,7 @@ DI bool fp_sqrt(fp &r, const fp &a) {
 DI int fp_legendre(const fp &a) {
     if (fp_is_zero(a)) return 0;
     fp t;
-    fp_pow_const(t, a, LCB_P_MINUS1_DIV2);
+    fp_pow_const(t, a, 2);
     return fp_eq(t, fp_one()) ? 1 : -1;
 }
 
@@ -481,7 +487,7 @@ DI bool fp2_sqrt(fp2 &y, const fp2 &x) {
         if (k == 0) fp_add(c, x.a, t1);
         else fp_sub(c, x.a, t1);
         fp_mul(c, c, inv2);
-        fp_pow_const(s, c, LCB_P_MINUS3_DIV4);
+        fp_pow_const(s, c, 3);
         fp_mul(cs, c, s);                              // c^((p+1)/4)
         fp_mul(e, cs, s);                              // c^((p-1)/2)
         if (fp_eq(e, fp_one())) {
@@ -508,7 +514,7 @@ DI bool fp2_sqrt_any(fp2 &y, const fp2 &x) {
     if (!fp_sqrt(t, t)) return false;                  // N(x) is a square iff x is
     fp_add(c, x.a, t);
     fp_mul(c, c, inv2);
-    fp_pow_const(s, c, LCB_P_MINUS3_DIV4);
+    fp_pow_const(s, c, 3);
     fp_sqr(u, s);
     fp_mul(u, u, c);                                   // c^((p-1)/2) = +-1
     fp_mul(bs, x.b, s);

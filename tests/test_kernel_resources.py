@@ -35,7 +35,7 @@ BUDGET = {
     "k_g1_sum": (0, 752),
     "k_g1_to_affine": (0, 704),
     "k_g2_decompress": (0, 992),
-    "k_g2_hash": (0, 3352),
+    "k_g2_hash": (0, 3400),
     "k_g2_mul": (302, 1584),                  # 4-bit window, table in the lanetab workspace (was 10,624 B)
     "k_g2_mul2_lanes": (4660, 2000),          # paired GLS ladders, tables in the lanetab workspace (was 22,672 B of scratch)
     "k_g2_mul_lanes": (1212, 1424),           # GLS ladder, table in the lanetab workspace (was 10,288 B)
@@ -45,26 +45,26 @@ BUDGET = {
     "k_mcl_from_bytes": (0, 800),
     "k_mcl_g1_sum": (0, 168),
     "k_mcl_g1_terms": (0, 880),
-    "k_mcl_g2_hash": (0, 3352),               # mclBnG2_hashAndMapTo: the same one-lane hash as k_g2_hash
+    "k_mcl_g2_hash": (0, 3400),               # mclBnG2_hashAndMapTo: the same one-lane hash as k_g2_hash
     "k_mcl_horner": (0, 1320),
-    "k_mcl_to_bytes": (0, 1008),
+    "k_mcl_to_bytes": (0, 1024),
     "k_msm_bucket_fix": (0, 168),
     "k_msm_bucket_reduce": (0, 744),          # + the prefetched next bucket
     "k_msm_horner": (0, 168),
     "k_op_debug": (96, 6956),
-    "k_op_grp": (408, 4104),
+    "k_op_grp": (420, 4104),
     "k_op_gt": (1788, 8148),                  # single-lane mcl operations (one wave per dispatch), one kernel per family
-    "k_op_pair": (830, 7572),
+    "k_op_pair": (842, 7620),
     "k_ptmul_g2": (32, 68),                   # mcl G2 multiplication latency kernel: four ladder lanes share each op
     "k_rlc_key_tables": (12, 168),            # k_rlc_rand.hip: spills to scratch, not AGPRs (<= 256 registers)
     "k_rlc_miller_fallback": (0, 2376),
     "k_rlc_search": (93, 2264),
     "k_secp_scalars": (0, 528),
-    "k_tpke_ct_prepare": (0, 3752),
-    "k_tpke_ct_prepare_h": (5, 4632),
+    "k_tpke_ct_prepare": (0, 3800),
+    "k_tpke_ct_prepare_h": (5, 4824),
     "k_tpke_ct_prepare_w": (5, 1688),
     "k_tpke_encrypt1": (0, 1184),
-    "k_tpke_encrypt2": (0, 3928),
+    "k_tpke_encrypt2": (0, 3976),
     "k_tpke_exact_points": (0, 704),
     "k_tpke_miller": (348, 2616),
     "k_tpke_pd_miller": (962, 2664),          # partial decryption split in three (was k_tpke_partial_decrypt, 7,652 B)
@@ -77,12 +77,12 @@ BUDGET = {
     "k_tpke_rlc_wsum": (0, 576),
     "k_tpke_rlc_wsum2": (0, 648),
     "k_ts_miller": (1248, 3292),
-    "k_ts_msg_prepare": (0, 3640),
+    "k_ts_msg_prepare": (0, 3688),
     "k_ts_rlc_miller": (0, 2524),
     "k_ts_rlc_points": (677, 3360),           # k_rlc_rand.hip: 256 registers, two waves per SIMD (spills to scratch)
     "k_ts_rlc_sum": (0, 2136),
     "k_ts_rlc_wsum": (12, 992),
-    "k_ts_sign": (0, 3928),
+    "k_ts_sign": (0, 3976),
 }
 # Round 5: no kernel that runs on more than one wave may take more than 4 KB of scratch per lane — the
 # HIP runtime reserves a dispatch's scratch for min(waves, device wave slots) waves per hardware queue, and the 22.7 KB
@@ -91,7 +91,7 @@ SCRATCH_CAP = 4096
 SINGLE_WAVE = {"k_op_grp", "k_op_pair", "k_op_gt", "k_op_debug", "k_coop_debug"}
 # one lane per ciphertext (748 waves for configs[1]'s 1M shares: a 222 MB reservation at 4.6 KB per lane), at 256
 # registers so a wave shares its SIMD with a randomisation wave (k_prep.hip)
-PER_CIPHERTEXT = {"k_tpke_ct_prepare_h": 4700}
+PER_CIPHERTEXT = {"k_tpke_ct_prepare_h": 4900}
 ZERO_SPILL = ["k_coop_tpke_miller", "k_coop_final_exp_check", "k_msm_bucket_acc", "k_secp_verify",
               "k_rlc_census_stats", "k_rlc_suspect_split", "k_rlc_resolve", "k_tpke_rlc_sum", "k_ts_rlc_miller"]
 
