@@ -14,6 +14,7 @@
 #pragma once
 #include "kcommon.hpp"
 #include "asm_tower.hpp"
+#include "pairing.hpp"
 
 #define LCB_FE_ASM_SLOTS 6
 
@@ -79,4 +80,33 @@ DI void final_exp_asm(u32 *park, size_t n, size_t i, u32 t) {
     fx_mul(U, U, V, 1, n, i, t);                         // x^(2-z) v
     fx_mul(U, U, X, 0, n, i, t);                         //   ... x
     fx_mul(X, A, U, 0, n, i, t);
+}
+
+// ---- the two-pair Miller loop in assembly (asm_tower.hpp lcb_r_miller2, round 5): f = conj(prod_k l1_k(P1) l2_k(P2))
+// over two normalised line sets with the accumulator in AGPRs from the first line to the last — the same residues as
+// miller2_norm_lds (pairing.hpp).  Park buffer slots (of n items): P1 / P2 at quads 0..5 / 6..11 of slot 3 ((0, 0)
+// for a point at infinity: its lines evaluate to 1), slots 1 and 2 the squarings' operands, f -> slot 0.
+DI void g1_park_slot(u32 *slot, u32 q0, size_t n, size_t i, const g1a &P) {
+    const fp x = P.inf ? fp_zero() : P.x, y = P.inf ? fp_zero() : P.y;
+    char *b = (char *)slot;
+    u32 off = (u32)(i * 16);
+    asm volatile("" : "+v"(off));
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        *(uint4 *)(b + (size_t)(q0 + q) * n * 16 + off) = make_uint4(x.v[4 * q], x.v[4 * q + 1], x.v[4 * q + 2], x.v[4 * q + 3]);
+        *(uint4 *)(b + (size_t)(q0 + 3 + q) * n * 16 + off) = make_uint4(y.v[4 * q], y.v[4 * q + 1], y.v[4 * q + 2], y.v[4 * q + 3]);
+    }
+}
+DI void miller2_asm(u32 *park, size_t n, size_t i, u32 lds, const u32 *ls1, const g1a &P1, const u32 *ls2,
+                    const g1a &P2) {
+    u32 *pslot = park + (size_t)3 * 144 * n;
+    g1_park_slot(pslot, 0, n, i, P1);
+    g1_park_slot(pslot, 6, n, i, P2);
+    lcb_asm_miller2(ls1, ls2, pslot, park + (size_t)144 * n, park + (size_t)288 * n, park, (u32)(n * 16), (u32)(i * 16),
+                    lds);
+}
+// this lane's 36 LDS quads (quad g at + g * 1024) in a block's 36 x LCB_BLOCK quads: wave w's 36 KB, lane l at l * 16
+DI u32 lane_lds36(uint4 *base) {
+    typedef __attribute__((address_space(3))) uint4 lds_quad_t;
+    return (u32)(uintptr_t)(lds_quad_t *)base + (threadIdx.x >> 6) * (36u * 1024u) + (threadIdx.x & 63u) * 16u;
 }

@@ -93,31 +93,6 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum(const uint4 *sdesc, u32 n_
     gpts[2 * (size_t)g + 1] = o;
 }
 
-// ---------------------------------------------------------------- TPKE group Miller loops (k_tpke_miller's loop)
-extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_rlc_miller(const u32 *lines, const uint4 *desc, const g1a_st *gpts,
-                                                            u32 n_groups, u32 *f_soa, uint8_t *gacc) {
-    LCB_LATENCY_PRIO();
-    __shared__ uint4 lds_pts[12 * LCB_BLOCK];
-    u32 g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= n_groups) return;
-    u32 c = desc[g].z;
-    g1a P, Q;
-    st_to_g1a(P, gpts[2 * (size_t)g]);
-    st_to_g1a(Q, gpts[2 * (size_t)g + 1]);
-    fp12 f;
-    const u32 *lsH = lines + (size_t)(2 * c) * LCB_LINESET_WORDS, *lsW = lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS;
-    if (lineset_normalised(lsH) && lineset_normalised(lsW)) {
-        uint4 *pt = lds_pts + threadIdx.x;
-        g1_park_lds(pt, P);
-        g1_park_lds(pt + 6 * LCB_BLOCK_PTS, Q);
-        miller2_norm_lds(f, lsH, pt, P.inf, lsW, pt + 6 * LCB_BLOCK_PTS, Q.inf);
-    } else {
-        miller2_sets_fallback(f, lsH, P, lsW, Q);
-    }
-    fp12_store_soa(f_soa, n_groups, g, f);
-    gacc[g] = 1;
-}
-
 // ---------------------------------------------------------------- threshold signatures (ValidateSignature)
 // e(PK_i, H(m)) == e(G, sig_i) <=> e(PK_i, H) e(-G, sig_i) == 1.  The randomisation of sig_i uses linearity of the
 // pairing in its G2 argument, which holds on G2: a share whose sig_i is outside G2 (G2.FromBytes does not check) is
@@ -591,10 +566,6 @@ extern "C" void lcbk_rlc_groups(hipStream_t s, const u32 *key_idx, u32 i0, u32 n
 extern "C" void lcbk_tpke_rlc_wsum(dim3 grid, hipStream_t s, const void *sdesc, u32 n_s, const u32 *wsum, u32 n_l1,
                                    void *gpts) {
     LCB_LAUNCH(k_tpke_rlc_wsum, (const uint4 *)sdesc, n_s, wsum, n_l1, (g1a_st *)gpts);
-}
-extern "C" void lcbk_tpke_rlc_miller(dim3 grid, hipStream_t s, const u32 *lines, const void *desc, const void *gpts,
-                                     u32 n_groups, u32 *f_soa, uint8_t *gacc) {
-    LCB_LAUNCH(k_tpke_rlc_miller, lines, (const uint4 *)desc, (const g1a_st *)gpts, n_groups, f_soa, gacc);
 }
 extern "C" void lcbk_ts_rlc_sum(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 first,
                                 const uint8_t *msg_ok, const void *pks, u32 n_pks, const u32 *pk_idx,

@@ -91,7 +91,8 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_miller(const u32 *lines, const
                                                          const g1a_st *keys, u32 n_keys, const u32 *ct_idx,
                                                          const u32 *dec_idx, const uint8_t *ui, u32 n, u32 *f_soa,
                                                          uint8_t *accept) {
-    __shared__ uint4 lds_pts[12 * LCB_BLOCK];   // the lane's two G1 points (LinesNormLds)
+    __shared__ uint4 ml_lds[36 * LCB_BLOCK];    // the assembly Miller loop's double-width products (lcb_r_miller2)
+    const u32 lds = lane_lds36(ml_lds);
     u32 i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     u32 c = ct_idx[i], d = dec_idx[i];
@@ -104,17 +105,14 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_miller(const u32 *lines, const
     ok = ok && ks.ok;
     st_to_g1a(Y, ks);
     fp_neg(Y.y, Y.y);
-    fp12 f;
     const u32 *lsH = lines + (size_t)(2 * c) * LCB_LINESET_WORDS, *lsW = lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS;
     if (lineset_normalised(lsH) && lineset_normalised(lsW)) {
-        uint4 *pt = lds_pts + threadIdx.x;               // Ui at quads 0..5, -Y at quads 6..11
-        g1_park_lds(pt, Ui);
-        g1_park_lds(pt + 6 * LCB_BLOCK_PTS, Y);
-        miller2_norm_lds(f, lsH, pt, Ui.inf, lsW, pt + 6 * LCB_BLOCK_PTS, Y.inf);
+        miller2_asm(f_soa, n, i, lds, lsH, Ui, lsW, Y);  // f -> slot 0 (slots 1..3 as its scratch)
     } else {
+        fp12 f;
         miller2_sets_fallback(f, lsH, Ui, lsW, Y);
+        fp12_store_soa(f_soa, n, i, f);
     }
-    fp12_store_soa(f_soa, n, i, f);
     accept[i] = ok;
 }
 // accept[i] &= (final_exp(f_i) == 1).  park: SoA Fp12 slots per item (lcbk_fe_slots()), slot 0 = f from the Miller
@@ -190,6 +188,34 @@ extern "C" void lcbk_ct_ok_merge(hipStream_t s, uint8_t *ct_ok, const uint8_t *h
 }
 extern "C" void lcbk_lineset_fill(dim3 grid, hipStream_t s, u32 *lines, u32 n_sets, const u32 *sets, uint8_t *w_g2) {
     LCB_LAUNCH(k_lineset_fill, lines, n_sets, sets, w_g2);
+}
+// ---------------------------------------------------------------- TPKE group Miller loops of the batched check
+// (k_batch.hip describes the levels): one lane per group, the two-pair loop of k_tpke_miller over the group's two
+// points (sum s_i U_i, -sum s_i Y_i) — here, beside the assembly library the loop calls
+extern "C" __global__ void LCB_PAIR_BOUNDS k_tpke_rlc_miller(const u32 *lines, const uint4 *desc, const g1a_st *gpts,
+                                                            u32 n_groups, u32 *f_soa, uint8_t *gacc) {
+    LCB_LATENCY_PRIO();
+    __shared__ uint4 ml_lds[36 * LCB_BLOCK];
+    const u32 lds = lane_lds36(ml_lds);
+    u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_groups) return;
+    u32 c = desc[g].z;
+    g1a P, Q;
+    st_to_g1a(P, gpts[2 * (size_t)g]);
+    st_to_g1a(Q, gpts[2 * (size_t)g + 1]);
+    const u32 *lsH = lines + (size_t)(2 * c) * LCB_LINESET_WORDS, *lsW = lines + (size_t)(2 * c + 1) * LCB_LINESET_WORDS;
+    if (lineset_normalised(lsH) && lineset_normalised(lsW)) {
+        miller2_asm(f_soa, n_groups, g, lds, lsH, P, lsW, Q);
+    } else {
+        fp12 f;
+        miller2_sets_fallback(f, lsH, P, lsW, Q);
+        fp12_store_soa(f_soa, n_groups, g, f);
+    }
+    gacc[g] = 1;
+}
+extern "C" void lcbk_tpke_rlc_miller(dim3 grid, hipStream_t s, const u32 *lines, const void *desc, const void *gpts,
+                                     u32 n_groups, u32 *f_soa, uint8_t *gacc) {
+    LCB_LAUNCH(k_tpke_rlc_miller, lines, (const uint4 *)desc, (const g1a_st *)gpts, n_groups, f_soa, gacc);
 }
 extern "C" void lcbk_tpke_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *ct_ok, u32 n_cts, const void *keys, u32 n_keys, const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, u32 *f_soa, uint8_t *accept) {
     LCB_LAUNCH(k_tpke_miller, lines, ct_ok, n_cts, (const g1a_st *)keys, n_keys, ct_idx, dec_idx, ui, n, f_soa, accept);

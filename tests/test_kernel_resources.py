@@ -66,10 +66,10 @@ BUDGET = {
     "k_tpke_encrypt1": (0, 1184),
     "k_tpke_encrypt2": (0, 3976),
     "k_tpke_exact_points": (0, 704),
-    "k_tpke_miller": (348, 2616),
+    "k_tpke_miller": (0, 2376),          # round 5: the two-pair loop in assembly (lcb_r_miller2); scratch = the fallback path
     "k_tpke_pd_miller": (962, 2664),          # partial decryption split in three (was k_tpke_partial_decrypt, 7,652 B)
     "k_tpke_pd_mul": (0, 992),
-    "k_tpke_rlc_miller": (324, 2616),
+    "k_tpke_rlc_miller": (0, 2376),          # round 5: the two-pair loop in assembly (lcb_r_miller2); scratch = the fallback path
     "k_tpke_rlc_points": (60, 1216),          # k_rlc_rand.hip: 248 registers, two waves per SIMD
     "k_tpke_rlc_search2a": (97, 3448),        # level-2 searches: four Fp12 values per lane, four lanes per group
     "k_tpke_rlc_search2b": (0, 3656),

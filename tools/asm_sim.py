@@ -226,6 +226,8 @@ def run_program(prog, labels, entry, lane, max_steps=50_000_000):
             lane.scc = 1 if g(ops[0]) == g(ops[1]) else 0
         elif mn == "s_cmp_lg_u32":
             lane.scc = 1 if g(ops[0]) != g(ops[1]) else 0
+        elif mn == "s_branch":
+            pc = labels[ops[0]]
         elif mn in ("s_cbranch_scc1", "s_cbranch_scc0"):
             if lane.scc == (1 if mn.endswith("1") else 0):
                 pc = labels[ops[0]]
@@ -239,12 +241,15 @@ def run_program(prog, labels, entry, lane, max_steps=50_000_000):
                 return
             pc = stack.pop()
         elif mn in ("global_load_dwordx4", "global_store_dwordx4"):
+            last, off = _split_off(ops[2])
+            if last == "off":                       # 64-bit VGPR address
+                addr = g(ops[1] if mn == "global_load_dwordx4" else ops[0]) + off
+            else:                                   # SGPR base + 32-bit VGPR offset
+                addr = g(last) + g(ops[1] if mn == "global_load_dwordx4" else ops[0]) + off
             if mn == "global_load_dwordx4":
-                dst, voff, sbase = ops
-                lane.put(dst, lane.load(g(sbase) + g(voff), 4))
+                lane.put(ops[0], lane.load(addr, 4))
             else:
-                voff, src, sbase = ops
-                lane.store(g(sbase) + g(voff), g(src), 4)
+                lane.store(addr, g(ops[1]), 4)
         elif mn in ("ds_write_b128", "ds_read_b128"):
             if mn == "ds_write_b128":
                 src, off = _split_off(ops[1])

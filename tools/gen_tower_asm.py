@@ -494,6 +494,25 @@ def gen_fp2dw():
     return ["lcb_r_fp2dw:"] + hazard_fix(b + ["s_setpc_b64 s[28:29]"])
 
 
+def gen_redc2():
+    """lcb_r_redc2: Montgomery reductions of the double-width U1 = v[72:95], U2 = v[120:143] (each < 19.68 p^2, so
+    < 3p) and two conditional subtractions -> v[84:95], v[132:143] (< p).  Leaf: m in v0..v23, temps v24..v47,
+    accumulators v144..v151; returns through s[28:29].  One copy shared by every reduction of the Fp6 / line products
+    keeps their code within the instruction cache."""
+    b = redc([dict(u=F2_RE, m=list(range(0, 12)), acc=F2_ACCS[0], c=MAD_CARRY[0]),
+              dict(u=F2_IM, m=list(range(12, 24)), acc=F2_ACCS[1], c=MAD_CARRY[1])], PR)
+    for _ in range(2):
+        b += merge([condsub(F2_RE[N:], PR, list(range(24, 36)), LIN_CARRY[0]),
+                    condsub(F2_IM[N:], PR, list(range(36, 48)), LIN_CARRY[1])])
+    return ["lcb_r_redc2:"] + hazard_fix(b + ["s_setpc_b64 s[28:29]"])
+
+
+def call_redc2():
+    return [f"s_getpc_b64 s[{S_CALL}:{S_CALL + 1}]", f"s_add_u32 s{S_CALL}, s{S_CALL}, lcb_r_redc2@rel32@lo+4",
+            f"s_addc_u32 s{S_CALL + 1}, s{S_CALL + 1}, lcb_r_redc2@rel32@hi+12",
+            f"s_swappc_b64 s[28:29], s[{S_CALL}:{S_CALL + 1}]"]
+
+
 def quad_addr(base, q):
     """s[66:67] = slot base s[base:base+1] + q * n16; q = (sgpr or None, constant)"""
     sg, k = q
@@ -612,18 +631,14 @@ def lds_v(k, part):
 
 
 def fp6_finish(RE, IM, offs, nsub, out_a):
-    """RE, IM (+ offs[0], offs[1] multiples of p^2) -> Montgomery reductions -> < p (nsub conditional subtractions)
-    -> a[out_a .. out_a + 23]"""
+    """RE, IM (+ offs[0], offs[1] multiples of p^2) -> lcb_r_redc2 (reductions + two conditional subtractions) ->
+    a[out_a .. out_a + 23]"""
     s = []
+    if RE != F2_RE:
+        s += mov_regs(F2_RE, RE)
     s += merge([movs_const(T2, pp_limbs(offs[0])), movs_const(T3, pp_limbs(offs[1]))])
-    s += merge([add_chain(RE, RE, T2, LIN_CARRY[0]), add_chain(IM, IM, T3, LIN_CARRY[1])])
-    M1, M2 = list(range(0, 12)), list(range(12, 24))
-    s += redc([dict(u=RE, m=M1, acc=F2_ACCS[0], c=MAD_CARRY[0]), dict(u=IM, m=M2, acc=F2_ACCS[1], c=MAD_CARRY[1])], PR)
-    ra, rb = RE[N:], IM[N:]
-    for _ in range(nsub):
-        s += merge([condsub(ra, PR, list(range(24, 36)), LIN_CARRY[0]),
-                    condsub(rb, PR, list(range(36, 48)), LIN_CARRY[1])])
-    return s + agpr_write(out_a, ra) + agpr_write(out_a + 12, rb)
+    s += merge([add_chain(F2_RE, F2_RE, T2, LIN_CARRY[0]), add_chain(F2_IM, F2_IM, T3, LIN_CARRY[1])])
+    return s + call_redc2() + agpr_write(out_a, F2_RE[N:]) + agpr_write(out_a + 12, F2_IM[N:])
 
 
 def gen_fp6m():
@@ -757,6 +772,232 @@ def gen_pow_z():
     return ["lcb_r_pow_z:"] + hazard_fix(b)
 
 
+# ------------------------------------------------------------------ the two-pair Miller loop (round 5)
+# lcb_r_miller2: f = conj(prod_k l1_k(P1) l2_k(P2)) over two normalised line sets (pairing.hpp miller2_norm_lds), the
+# accumulator in a[0:143] from the first line to the last.  A line 1 + b v + c v w (b = B' xP, c = C' yP) is applied
+# by lcb_r_line with lazily reduced products: per coefficient position the three double-width Fp2 products (t0 = b X,
+# t1 = c Y, S = (b + c)(X + Y)) are combined before reduction — f1_k' = REDC(S - t0 - t1 + f1_k R) and
+# f0_k' = REDC(t0_k + f0_k R + t1_{k-1}) — 12 Montgomery reductions per line instead of 18.  A point at infinity is
+# stored as (0, 0): b = c = 0 and the line is 1.  The squarings are lcb_r_fp12sq (complex method: two lazily
+# reduced Fp6 products through lcb_r_fp6m).
+S_P, S_S2, S_PQ, S_SET = 56, 58, 62, 63          # P slot (P1 quads 0..5, P2 6..11); second tmp slot; P quad base; set
+V_LS = [244, 246]                                 # working line pointers of the two sets (copies of v[250:253])
+L_T, L_PEND, L_T12 = 0, 12, 24                    # LDS quads: parked t, pending f0 sum, t1 of position 2
+A_TF1, A_TF0, A_T0 = 144, 168, 192                # AGPRs: new f1_2, new f0_2 (written at the end), parked t0
+LINE_B, LINE_C, LINE_BC = T1, T2, T3              # b, c, b + c (< p) across the line's fp2dw calls
+K4PP = pp_limbs(4)
+
+
+def add_hi(U, f):
+    """U (24 words, mod 2^768) += f * 2^384"""
+    return add_chain(U[N:], U[N:], f, LIN_CARRY[2])
+
+
+def dw_park_a(abase, RE, IM):
+    return agpr_write(abase, RE) + agpr_write(abase + 24, IM)
+
+
+def dw_from_a(RE, IM, abase):
+    return agpr_read(RE, abase) + agpr_read(IM, abase + 24)
+
+
+def redc_pair(RE, IM, nsub, out):
+    """(RE, IM) = (F2_RE, F2_IM) + 4p^2 each -> lcb_r_redc2 -> out(ra, rb)"""
+    assert RE == F2_RE and IM == F2_IM
+    s = movs_const(list(range(0, 24)), K4PP)
+    s += merge([add_chain(RE, RE, list(range(0, 24)), LIN_CARRY[0]), add_chain(IM, IM, list(range(0, 24)), LIN_CARRY[1])])
+    return s + call_redc2() + out(RE[N:], IM[N:])
+
+
+def mov_regs(dst, src):
+    return [f"v_mov_b32 v{d}, v{x}" for d, x in zip(dst, src)]
+
+
+def xi_into(dst_a, dst_b, src_a, src_b, tmp):
+    """(dst_a, dst_b) = xi (src_a + src_b u) = (src_a - src_b, src_a + src_b) mod p; sources < p"""
+    return merge([modsub(dst_a, src_a, src_b, tmp[:12], LIN_CARRY[0], LIN_CARRY[1]),
+                  modadd(dst_b, src_a, src_b, tmp[12:], LIN_CARRY[2])])
+
+
+def line_operand_y(k, which):
+    """fp2dw's y operand (YA, YB) for position k: X = f0_{k-1} / Y = f1_{k-1}, or xi f0_2 / xi f1_2 at k = 0"""
+    base = (0 if which == "X" else 72)
+    if k > 0:
+        return agpr_read(F2_YA, base + 24 * (k - 1)) + agpr_read(F2_YB, base + 24 * (k - 1) + 12)
+    return (agpr_read(F2_SX, base + 48) + agpr_read(F2_SY, base + 60) + ["s_nop 1"] +
+            xi_into(F2_YA, F2_YB, F2_SX, F2_SY, F2_P0))
+
+
+def line_operand_xy_sum(k):
+    """YA, YB = X + Y (mod p) for position k"""
+    s = line_operand_y(k, "X") + mov_regs(list(range(96, 120)), F2_YA + F2_YB)
+    s += line_operand_y(k, "Y")
+    s += merge([modadd(F2_YA, F2_YA, list(range(96, 108)), F2_P0[:12], LIN_CARRY[0]),
+                modadd(F2_YB, F2_YB, list(range(108, 120)), F2_P0[12:], LIN_CARRY[1])])
+    return s
+
+
+def gen_line():
+    """lcb_r_line: a[0:143] <- f * (1 + b v + c v w) for the line at the set pointer v[244:245] (s63 = 0) or
+    v[246:247] (s63 = 1), b = B' xP, c = C' yP with P at quads s62 .. s62 + 5 of the P slot s[56:57].  PR = p and
+    s88 set by the caller.  Returns through s[30:31]."""
+    b = []
+    other = label("lineset")
+    done = label("lineld")
+    for half, dst in ((0, LINE_B), (1, LINE_C)):   # b = B' xP, then c = C' yP: products, lcb_r_redc2
+        b += [f"s_cmp_eq_u32 s{S_SET}, 0", f"s_cbranch_scc0 {other}_{half}"]
+        for t, vp in enumerate(V_LS):
+            if t == 1:
+                b += [f"{other}_{half}:", "s_nop 4"]
+            for g in range(6):
+                b.append(f"global_load_dwordx4 v[{48 + 4 * g}:{48 + 4 * g + 3}], v[{vp}:{vp + 1}], "
+                         f"off offset:{96 * half + 16 * g}")
+            if t == 0:
+                b += [f"s_branch {done}_{half}"]
+        b += [f"{done}_{half}:", "s_nop 4"]
+        b += gload(list(range(24, 36)), S_P, (S_PQ, 3 * half)) + ["s_waitcnt vmcnt(0)"]
+        b += comba([dict(a=list(range(48, 60)), b=list(range(24, 36)), acc=F2_ACCS[0], out=F2_RE, c=MAD_CARRY[0]),
+                    dict(a=list(range(60, 72)), b=list(range(24, 36)), acc=F2_ACCS[1], out=F2_IM, c=MAD_CARRY[1])])
+        b += call_redc2() + mov_regs(dst, F2_RE[N:] + F2_IM[N:])
+    b += merge([modadd(LINE_BC[:12], LINE_B[:12], LINE_C[:12], list(range(0, 12)), LIN_CARRY[0]),
+                modadd(LINE_BC[12:], LINE_B[12:], LINE_C[12:], list(range(12, 24)), LIN_CARRY[1])])
+    RE, IM = F2_RE, F2_IM
+    T = list(range(0, 24)), list(range(24, 48))          # temps after a call (fp2dw inputs are dead)
+
+    def call_xy(xregs, yprep):
+        return yprep + mov_regs(F2_XA + F2_XB, xregs) + call_fp2dw()
+
+    def sub_lds(q, c0, c1):                               # RE -= LDS[q..q+5], IM -= LDS[q+6..q+11]
+        return (lds_read(T[0], q) + lds_read(T[1], q + 6) + ["s_waitcnt lgkmcnt(0)"] +
+                merge([sub_chain(RE, RE, T[0], c0), sub_chain(IM, IM, T[1], c1)]))
+
+    def add_lds(q, c0, c1):
+        return (lds_read(T[0], q) + lds_read(T[1], q + 6) + ["s_waitcnt lgkmcnt(0)"] +
+                merge([add_chain(RE, RE, T[0], c0), add_chain(IM, IM, T[1], c1)]))
+
+    def add_f_hi(abase):                                  # (RE, IM) += (f.a, f.b) * 2^384, f from a[abase..]
+        return (agpr_read(T[0][:12], abase) + agpr_read(T[1][:12], abase + 12) + ["s_nop 1"] +
+                merge([add_chain(RE[N:], RE[N:], T[0][:12], LIN_CARRY[2]),
+                       add_chain(IM[N:], IM[N:], T[1][:12], LIN_CARRY[3])]))
+
+    to_a = lambda abase: (lambda ra, rb: agpr_write(abase, ra) + agpr_write(abase + 12, rb))   # noqa: E731
+    # ---- position 2: X = f0_1, Y = f1_1
+    b += call_xy(LINE_C, line_operand_y(2, "Y"))                                   # t1_2
+    b += lds_write(L_T12, RE) + lds_write(L_T12 + 6, IM)
+    b += call_xy(LINE_B, line_operand_y(2, "X"))                                   # t0_2
+    b += lds_write(L_T, RE) + lds_write(L_T + 6, IM) + add_f_hi(48)               # + f0_2 R -> pending
+    b += lds_write(L_PEND, RE) + lds_write(L_PEND + 6, IM) + ["s_waitcnt lgkmcnt(0)"]
+    b += call_xy(LINE_BC, line_operand_xy_sum(2))                                   # S_2
+    b += sub_lds(L_T, LIN_CARRY[0], LIN_CARRY[1]) + sub_lds(L_T12, LIN_CARRY[0], LIN_CARRY[1]) + add_f_hi(120)
+    b += redc_pair(RE, IM, 2, to_a(A_TF1))                                          # f1_2' (kept aside)
+    # ---- position 1: X = f0_0, Y = f1_0
+    b += call_xy(LINE_C, line_operand_y(1, "Y"))                                   # t1_1
+    b += lds_write(L_T, RE) + lds_write(L_T + 6, IM) + add_lds(L_PEND, LIN_CARRY[0], LIN_CARRY[1])
+    b += redc_pair(RE, IM, 2, to_a(A_TF0))                                          # f0_2' (kept aside)
+    b += call_xy(LINE_B, line_operand_y(1, "X"))                                   # t0_1
+    b += dw_park_a(A_T0, RE, IM) + add_f_hi(24)
+    b += lds_write(L_PEND, RE) + lds_write(L_PEND + 6, IM) + ["s_waitcnt lgkmcnt(0)"]
+    b += call_xy(LINE_BC, line_operand_xy_sum(1))                                   # S_1
+    b += dw_from_a(T[0], T[1], A_T0) + ["s_nop 1"]
+    b += merge([sub_chain(RE, RE, T[0], LIN_CARRY[0]), sub_chain(IM, IM, T[1], LIN_CARRY[1])])
+    b += sub_lds(L_T, LIN_CARRY[0], LIN_CARRY[1]) + add_f_hi(96)
+    b += redc_pair(RE, IM, 2, to_a(96))                                             # f1_1'
+    # ---- position 0: X = xi f0_2, Y = xi f1_2 (the originals: f0_2', f1_2' are aside)
+    b += call_xy(LINE_C, line_operand_y(0, "Y"))                                   # t1_0
+    b += lds_write(L_T, RE) + lds_write(L_T + 6, IM) + add_lds(L_PEND, LIN_CARRY[0], LIN_CARRY[1])
+    b += redc_pair(RE, IM, 2, to_a(24))                                             # f0_1'
+    b += call_xy(LINE_B, line_operand_y(0, "X"))                                   # t0_0
+    b += dw_park_a(A_T0, RE, IM) + add_f_hi(0)
+    # + xi t1_2: (re - im, re + im) of the parked double-width t1_2
+    b += lds_read(T[0], L_T12) + lds_read(T[1], L_T12 + 6) + ["s_waitcnt lgkmcnt(0)"]
+    X2 = list(range(48, 72))
+    b += merge([sub_chain(X2, T[0], T[1], LIN_CARRY[0]), add_chain(T[1], T[0], T[1], LIN_CARRY[1])])
+    b += merge([add_chain(RE, RE, X2, LIN_CARRY[0]), add_chain(IM, IM, T[1], LIN_CARRY[1])])
+    b += redc_pair(RE, IM, 2, to_a(0))                                              # f0_0'
+    b += call_xy(LINE_BC, line_operand_xy_sum(0))                                   # S_0
+    b += dw_from_a(T[0], T[1], A_T0) + ["s_nop 1"]
+    b += merge([sub_chain(RE, RE, T[0], LIN_CARRY[0]), sub_chain(IM, IM, T[1], LIN_CARRY[1])])
+    b += sub_lds(L_T, LIN_CARRY[0], LIN_CARRY[1]) + add_f_hi(72)
+    b += redc_pair(RE, IM, 2, to_a(72))                                             # f1_0'
+    # the positions-2 results into place
+    b += ["s_nop 1"] + agpr_read(T[0], A_TF1) + agpr_read(T[1], A_TF0) + ["s_nop 1"]
+    b += agpr_write(120, T[0]) + agpr_write(48, T[1])
+    return ["lcb_r_line:"] + hazard_fix(b + ["s_setpc_b64 s[30:31]"])
+
+
+def gen_fp12sq():
+    """lcb_r_fp12sq: a[0:143] <- a^2 (f = a + b w, components < p): t = a b, u = (a + b)(a + v b) (lcb_r_fp6m, y from
+    the tmp slots s[22:23] = [a | b] and s[58:59] = [a | v b]); c0 = u - t - v t, c1 = 2t.  Returns through s[30:31]."""
+    X, Y, Z, W = T1[:12], T1[12:], T2[:12], T2[12:]
+    b = ["s_nop 4"] + gstore(S_T, (None, 0), list(range(0, 144)), "a")              # S1 = [a | b]
+    b += gstore(S_S2, (None, 0), list(range(0, 72)), "a")                            # S2 = [a | v b]
+    b += gstore(S_S2, (None, 24), list(range(72, 120)), "a")                         # (v b)_1 = b0, (v b)_2 = b1
+    b += agpr_read(X, 120) + agpr_read(Y, 132) + ["s_nop 1"] + xi_into(Z, W, X, Y, T3)
+    b += gstore(S_S2, (None, 18), Z + W) + ["s_waitcnt vmcnt(0)"]                   # (v b)_0 = xi b2
+    b += [f"s_mov_b64 s[{S_M}:{S_M + 1}], s[{S_T}:{S_T + 1}]", f"s_mov_b32 s{S_Q0}, 18", f"s_mov_b32 s{S_SUM}, 0"]
+    b += call_ret("lcb_r_fp6m", S_RET6)                                              # t = a b -> a[144:215]
+    b += ["s_nop 4"] + gstore(S_T, (None, 0), list(range(144, 216)), "a")
+    for i in range(6):                                                               # a[0:71] <- a + b
+        b += agpr_read(X, 12 * i) + agpr_read(Y, 72 + 12 * i) + ["s_nop 1"]
+        b += modadd(X, X, Y, Z, LIN_CARRY[0]) + agpr_write(12 * i, X)
+    b += ["s_waitcnt vmcnt(0)", f"s_mov_b64 s[{S_M}:{S_M + 1}], s[{S_S2}:{S_S2 + 1}]", f"s_mov_b32 s{S_Q0}, 0",
+          f"s_mov_b32 s{S_SUM}, 1"]
+    b += call_ret("lcb_r_fp6m", S_RET6)                                              # u -> a[144:215]
+    b += ["s_nop 4"]
+    # t from S1 quads 0..17: c1 = 2t -> a[72:143]
+    tq = lambda i: (None, 3 * i)                                                     # noqa: E731
+    for i in range(6):
+        b += gload(X, S_T, tq(i)) + ["s_waitcnt vmcnt(0)"] + modadd(X, X, X, Z, LIN_CARRY[0])
+        b += agpr_write(72 + 12 * i, X)
+    # c0_k = u_k - t_k - (v t)_k, (v t)_0 = xi t_2, (v t)_1 = t_0, (v t)_2 = t_1
+    U3 = T3[:12]
+    b += gload(Y, S_T, tq(4)) + gload(Z, S_T, tq(5)) + ["s_waitcnt vmcnt(0)"]
+    b += modsub(U3, Y, Z, W, LIN_CARRY[0], LIN_CARRY[1]) + modadd(Y, Y, Z, W, LIN_CARRY[2])   # xi t2 = (U3, Y)
+    for part, V in ((0, U3), (1, Y)):
+        b += agpr_read(X, 144 + 12 * part) + gload(Z, S_T, tq(part)) + ["s_waitcnt vmcnt(0)"]
+        b += modsub(X, X, Z, W, LIN_CARRY[0], LIN_CARRY[1]) + modsub(X, X, V, W, LIN_CARRY[2], LIN_CARRY[3])
+        b += agpr_write(12 * part, X)
+    for k in (1, 2):
+        for part in range(2):
+            i = 2 * k + part
+            b += agpr_read(X, 144 + 12 * i) + gload(Z, S_T, tq(i)) + gload(Y, S_T, tq(i - 2))
+            b += ["s_waitcnt vmcnt(0)"] + modsub(X, X, Z, W, LIN_CARRY[0], LIN_CARRY[1])
+            b += modsub(X, X, Y, W, LIN_CARRY[2], LIN_CARRY[3]) + agpr_write(12 * i, X)
+    return ["lcb_r_fp12sq:"] + hazard_fix(b + ["s_setpc_b64 s[30:31]"])
+
+
+def gen_miller2():
+    """lcb_r_miller2: slot s[60:61] <- conj(prod over the 68 lines of l1_k(P1) l2_k(P2)), squarings before every
+    doubling line but the first.  Line sets at the lanes' v[250:251], v[252:253] (68 x 48 words each), P1 / P2 at quads
+    0..5 / 6..11 of s[56:57] ((0, 0) for infinity), tmp slots s[22:23], s[58:59]."""
+    ONE = limbs((1 << 384) % P)
+    b = ["s_waitcnt vmcnt(0) lgkmcnt(0)", "s_mov_b64 s[24:25], s[30:31]"] + movs_const(PR, PL)
+    b += [f"s_mov_b32 s{S_PINV}, 0x{PINV:08x}"]
+    b += mov_regs([V_LS[0], V_LS[0] + 1, V_LS[1], V_LS[1] + 1], [250, 251, 252, 253])
+    b += movs_const(list(range(0, 12)), ONE) + ["v_mov_b32 v12, 0"]
+    b += [f"v_accvgpr_write_b32 a{j}, v{j}" for j in range(12)] + [f"v_accvgpr_write_b32 a{j}, v12" for j in range(12, 144)]
+    b += [f"s_mov_b32 s{S_QT + 1}, {4 * 48}"]                                      # bytes per line
+    i, add_next = 62, False
+    for k in range(68):
+        if add_next:
+            add_next = False
+        else:
+            if k > 0:
+                b += call_ret("lcb_r_fp12sq", 30)
+            add_next = bool((Z_ABS_BITS >> i) & 1)
+            i -= 1
+        for t in range(2):
+            b += [f"s_mov_b32 s{S_SET}, {t}", f"s_mov_b32 s{S_PQ}, {6 * t}"] + call_ret("lcb_r_line", 30)
+            vp = V_LS[t]
+            b += [f"v_add_co_u32_e64 v{vp}, {sp(LIN_CARRY[0])}, v{vp}, s{S_QT + 1}",
+                  f"v_addc_co_u32_e64 v{vp + 1}, {sp(LIN_CARRY[0])}, v{vp + 1}, 0, {sp(LIN_CARRY[0])}", "s_nop 2"]
+    b += ["s_nop 4"] + conj_c1() + walk_store(S_DST) + ["s_setpc_b64 s[24:25]"]
+    return ["lcb_r_miller2:"] + hazard_fix(b)
+
+
+Z_ABS_BITS = 0xd201000000010000
+
+
 # ------------------------------------------------------------------ emit
 def clobbers_n():
     regs = [f'"v{i}"' for i in range(VMAX)] + [f'"a{i}"' for i in range(A_PARK + 2 * N)]
@@ -774,7 +1015,7 @@ def emit():
     fp4_txt, fp4_outs, fp4_used = gen_fp4()
     cyc_txt = gen_cyc_sqr(fp4_outs, fp4_used)
     routines = [gen_cyc_sqr_n(), cyc_txt, fp4_txt, gen_pow_z(), gen_fp12_mul_n(), gen_fp12m(), gen_fp6m(),
-                gen_fp2dw()]
+                gen_fp2dw(), gen_redc2(), gen_miller2(), gen_fp12sq(), gen_line()]
     lib = "\n".join("  .p2align 8\n" + "\n".join(("  " + l) if not l.endswith(":") else l for l in r)
                     for r in routines)
     esc = lib.replace("\\", "\\\\").replace('"', '\\"')
@@ -830,6 +1071,22 @@ __device__ __forceinline__ void lcb_asm_pow_z(const u32 *base, u32 *tmp, u32 *ds
         : "{{s[20:21]}}"(base), "{{s[22:23]}}"(tmp), "{{s[60:61]}}"(dst), "{{s19}}"(n16), "{{v248}}"(lane_off),
           "{{v249}}"(lds_addr)
         : {fp12_clob}, "memory");
+}}
+""")
+    ml_clob = ", ".join([f'"v{i}"' for i in range(VMAX)] + [f'"a{i}"' for i in range(240)] +
+                        [f'"s{x}"' for x in sorted(set(CLOBBER_SGPRS) | {16, 17, 18, 20, 21, 24, 25, 62, 63, 64, 66,
+                                                                            67, 68, 69, 72, 73})] + ['"scc"', '"vcc"'])
+    o.append(f"""// dst <- conj(prod_k l1_k(P1) l2_k(P2)), the 68 normalised lines of two line sets (pairing.hpp miller2_norm_lds,
+// the same residues): ls1 / ls2 the lane's line sets (68 x 48 words), pslot a slot holding P1 at quads 0..5 and P2
+// at quads 6..11 ((0, 0) for a point at infinity), s1 / s2 two tmp slots, lds_addr the lane's 36 LDS quads.
+// Clobbers v0..v247, a0..a239.
+__device__ __forceinline__ void lcb_asm_miller2(const u32 *ls1, const u32 *ls2, const u32 *pslot, u32 *s1, u32 *s2,
+                                                u32 *dst, u32 n16, u32 lane_off, u32 lds_addr) {{
+    asm volatile({call_seq("lcb_r_miller2")}
+        :
+        : "{{v[250:251]}}"(ls1), "{{v[252:253]}}"(ls2), "{{s[56:57]}}"(pslot), "{{s[22:23]}}"(s1), "{{s[58:59]}}"(s2),
+          "{{s[60:61]}}"(dst), "{{s19}}"(n16), "{{v248}}"(lane_off), "{{v249}}"(lds_addr)
+        : {ml_clob}, "memory");
 }}
 """)
     return "".join(o), dict(fp4_outs=fp4_outs, fp4_used=len(fp4_used), n_cyc=len(cyc_txt), n_fp4=len(fp4_txt))
