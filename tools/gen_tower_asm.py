@@ -926,43 +926,43 @@ def gen_line():
 
 
 def gen_fp12sq():
-    """lcb_r_fp12sq: a[0:143] <- a^2 (f = a + b w, components < p): t = a b, u = (a + b)(a + v b) (lcb_r_fp6m, y from
-    the tmp slots s[22:23] = [a | b] and s[58:59] = [a | v b]); c0 = u - t - v t, c1 = 2t.  Returns through s[30:31]."""
+    """lcb_r_fp12sq: a[0:143] <- a^2 (f = a + b w, components < p), complex method: t = a b (lcb_r_fp6m, y = b from
+    the tmp slot s[22:23] = [a | b]), x = a + v b, u = x (a + b) (y = the slot's sum variant), c0 = u - t - v t,
+    c1 = 2t — t kept in a[72:143] once b is consumed, so the slot is written once and only read after.  Returns
+    through s[30:31]."""
     X, Y, Z, W = T1[:12], T1[12:], T2[:12], T2[12:]
-    b = ["s_nop 4"] + gstore(S_T, (None, 0), list(range(0, 144)), "a")              # S1 = [a | b]
-    b += gstore(S_S2, (None, 0), list(range(0, 72)), "a")                            # S2 = [a | v b]
-    b += gstore(S_S2, (None, 24), list(range(72, 120)), "a")                         # (v b)_1 = b0, (v b)_2 = b1
-    b += agpr_read(X, 120) + agpr_read(Y, 132) + ["s_nop 1"] + xi_into(Z, W, X, Y, T3)
-    b += gstore(S_S2, (None, 18), Z + W) + ["s_waitcnt vmcnt(0)"]                   # (v b)_0 = xi b2
+    b = ["s_nop 4"] + gstore(S_T, (None, 0), list(range(0, 144)), "a") + ["s_waitcnt vmcnt(0)"]   # S1 = [a | b]
     b += [f"s_mov_b64 s[{S_M}:{S_M + 1}], s[{S_T}:{S_T + 1}]", f"s_mov_b32 s{S_Q0}, 18", f"s_mov_b32 s{S_SUM}, 0"]
     b += call_ret("lcb_r_fp6m", S_RET6)                                              # t = a b -> a[144:215]
-    b += ["s_nop 4"] + gstore(S_T, (None, 0), list(range(144, 216)), "a")
-    for i in range(6):                                                               # a[0:71] <- a + b
-        b += agpr_read(X, 12 * i) + agpr_read(Y, 72 + 12 * i) + ["s_nop 1"]
-        b += modadd(X, X, Y, Z, LIN_CARRY[0]) + agpr_write(12 * i, X)
-    b += ["s_waitcnt vmcnt(0)", f"s_mov_b64 s[{S_M}:{S_M + 1}], s[{S_S2}:{S_S2 + 1}]", f"s_mov_b32 s{S_Q0}, 0",
-          f"s_mov_b32 s{S_SUM}, 1"]
-    b += call_ret("lcb_r_fp6m", S_RET6)                                              # u -> a[144:215]
     b += ["s_nop 4"]
-    # t from S1 quads 0..17: c1 = 2t -> a[72:143]
-    tq = lambda i: (None, 3 * i)                                                     # noqa: E731
-    for i in range(6):
-        b += gload(X, S_T, tq(i)) + ["s_waitcnt vmcnt(0)"] + modadd(X, X, X, Z, LIN_CARRY[0])
-        b += agpr_write(72 + 12 * i, X)
-    # c0_k = u_k - t_k - (v t)_k, (v t)_0 = xi t_2, (v t)_1 = t_0, (v t)_2 = t_1
-    U3 = T3[:12]
-    b += gload(Y, S_T, tq(4)) + gload(Z, S_T, tq(5)) + ["s_waitcnt vmcnt(0)"]
-    b += modsub(U3, Y, Z, W, LIN_CARRY[0], LIN_CARRY[1]) + modadd(Y, Y, Z, W, LIN_CARRY[2])   # xi t2 = (U3, Y)
-    for part, V in ((0, U3), (1, Y)):
-        b += agpr_read(X, 144 + 12 * part) + gload(Z, S_T, tq(part)) + ["s_waitcnt vmcnt(0)"]
+    # x = a + v b -> a[0:71]: (a0 + xi b2, a1 + b0, a2 + b1)
+    b += agpr_read(X, 120) + agpr_read(Y, 132) + ["s_nop 1"] + xi_into(Z, W, X, Y, T3)          # xi b2
+    for part, V in ((0, Z), (1, W)):
+        b += agpr_read(X, 12 * part) + ["s_nop 1"] + modadd(X, X, V, Y, LIN_CARRY[0]) + agpr_write(12 * part, X)
+    for i in range(2, 6):
+        b += agpr_read(X, 12 * i) + agpr_read(Y, 72 + 12 * (i - 2)) + ["s_nop 1"]
+        b += modadd(X, X, Y, Z, LIN_CARRY[0]) + agpr_write(12 * i, X)
+    for i in range(6):                                                               # t -> a[72:143] (b consumed)
+        b += agpr_read(X, 144 + 12 * i) + ["s_nop 1"] + agpr_write(72 + 12 * i, X)
+    b += [f"s_mov_b32 s{S_Q0}, 0", f"s_mov_b32 s{S_SUM}, 1"]
+    b += call_ret("lcb_r_fp6m", S_RET6)                                              # u = x (a + b) -> a[144:215]
+    b += ["s_nop 4"]
+    # c0_k = u_k - t_k - (v t)_k with (v t)_0 = xi t_2, (v t)_1 = t_0, (v t)_2 = t_1; then c1 = 2t
+    U3, U4 = T3[:12], T3[12:]
+    b += agpr_read(Y, 72 + 48) + agpr_read(Z, 72 + 60) + ["s_nop 1"]
+    b += modsub(U3, Y, Z, W, LIN_CARRY[0], LIN_CARRY[1]) + modadd(U4, Y, Z, W, LIN_CARRY[2])  # xi t2 = (U3, U4)
+    for i in range(6):                                                               # i = 2k + part
+        k, part = divmod(i, 2)
+        b += agpr_read(X, 144 + 12 * i) + agpr_read(Z, 72 + 12 * i) + ["s_nop 1"]
+        if k == 0:
+            V = U3 if part == 0 else U4
+        else:
+            b += agpr_read(Y, 72 + 12 * (i - 2)) + ["s_nop 1"]
+            V = Y
         b += modsub(X, X, Z, W, LIN_CARRY[0], LIN_CARRY[1]) + modsub(X, X, V, W, LIN_CARRY[2], LIN_CARRY[3])
-        b += agpr_write(12 * part, X)
-    for k in (1, 2):
-        for part in range(2):
-            i = 2 * k + part
-            b += agpr_read(X, 144 + 12 * i) + gload(Z, S_T, tq(i)) + gload(Y, S_T, tq(i - 2))
-            b += ["s_waitcnt vmcnt(0)"] + modsub(X, X, Z, W, LIN_CARRY[0], LIN_CARRY[1])
-            b += modsub(X, X, Y, W, LIN_CARRY[2], LIN_CARRY[3]) + agpr_write(12 * i, X)
+        b += agpr_write(12 * i, X)
+    for i in range(6):
+        b += agpr_read(X, 72 + 12 * i) + ["s_nop 1"] + modadd(X, X, X, Z, LIN_CARRY[0]) + agpr_write(72 + 12 * i, X)
     return ["lcb_r_fp12sq:"] + hazard_fix(b + ["s_setpc_b64 s[30:31]"])
 
 
