@@ -49,6 +49,11 @@ struct lcb_ctx {
     std::vector<uint64_t> cc_used;
     uint64_t cc_tick = 0;
     int cc_flags = -1;
+    // decompressed-key cache of the same entry point (an epoch's verification keys recur in every flush): one slot per
+    // 48-byte key, filled in order; a call that would overflow it starts it afresh
+    DevBuf kc_pts;
+    std::unordered_map<std::string, uint32_t> kc_map;
+    uint32_t kc_n = 0;
     size_t t_n_cts = 0, t_n_keys = 0;
     uint64_t t_gen = 0;
     bool t_ready = false;

@@ -962,7 +962,8 @@ bool sync_check(lcb_ctx *c, const char *what) {
 // hook) lowers it so small batches run several chunks — set it only while no batch call is in flight
 std::atomic<size_t> g_verify_chunk{(size_t)1 << 21};
 #define LCB_VERIFY_CHUNK (g_verify_chunk.load(std::memory_order_relaxed))
-#define LCB_CT_CACHE 1024                       // prepared-ciphertext cache slots per context (52.7 KB of lines each)
+#define LCB_CT_CACHE 2048                       // prepared-ciphertext cache slots per context (52.7 KB of lines each)
+#define LCB_KEY_CACHE 4096                      // decompressed verification keys per context (LCB_G1A_ST_BYTES each)
 
 int tpke_prepare(lcb_ctx *c, const uint8_t *d_y, size_t n_keys, const uint8_t *d_u, const uint8_t *d_w,
                  const uint8_t *d_v, const uint32_t *d_voff, size_t n_cts, hipStream_t s) {
@@ -1004,8 +1005,9 @@ std::atomic<uint32_t> g_coop_max{32768};    // lcb_set_coop_max: batches / level
 std::atomic<uint32_t> g_coop_miller_max{65536};   // lcb_set_coop_miller_max: the same for the group Miller loops only
                                                   // (65536: level 1 too, 105.5 vs 106.1 ms, profiles/r03/ab2)
 // the exact check of n shares against prepared line sets (lines, ctok: n_cts ciphertexts) and decompressed keys
-int tpke_verify_core(lcb_ctx *c, const u32 *lines, const uint8_t *ctok, size_t n_cts, size_t n_keys, uint8_t *d_accept,
-                     size_t n, const uint32_t *d_ct, const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
+int tpke_verify_core(lcb_ctx *c, const u32 *lines, const uint8_t *ctok, size_t n_cts, const void *keys, size_t n_keys,
+                     uint8_t *d_accept, size_t n, const uint32_t *d_ct, const uint32_t *d_dec, const uint8_t *d_ui,
+                     hipStream_t s) {
     if (n > 0xffffffffu) { set_err("tpke verify: batch too large"); return -1; }
     if (n) {
         // chunks of at most LCB_VERIFY_CHUNK shares: bounded park buffer (slots x 576 B per share) whatever n is;
@@ -1029,11 +1031,11 @@ int tpke_verify_core(lcb_ctx *c, const u32 *lines, const uint8_t *ctok, size_t n
             const size_t m = n - o < LCB_VERIFY_CHUNK ? n - o : LCB_VERIFY_CHUNK;
             if (o == 0) hipEventRecord(c->ver_ev[0], s);
             if (coop) {
-                lcbk_tpke_exact_points(s, ctok, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct + o, d_dec + o,
+                lcbk_tpke_exact_points(s, ctok, (u32)n_cts, keys, (u32)n_keys, d_ct + o, d_dec + o,
                                        d_ui + 48 * o, (u32)m, gpts, desc, d_accept + o);
                 lcbk_coop_tpke_miller(s, lines, desc, gpts, (u32)m, f, fl, fl + m, 2, 1);
             } else {
-                lcbk_tpke_miller(dim3(nblk(m)), s, lines, ctok, (u32)n_cts, c->t_keys.p, (u32)n_keys, d_ct + o,
+                lcbk_tpke_miller(dim3(nblk(m)), s, lines, ctok, (u32)n_cts, keys, (u32)n_keys, d_ct + o,
                                  d_dec + o, d_ui + 48 * o, (u32)m, f, d_accept + o);
             }
             if (o == 0) hipEventRecord(c->ver_ev[1], s);
@@ -1048,8 +1050,8 @@ int tpke_verify_core(lcb_ctx *c, const u32 *lines, const uint8_t *ctok, size_t n
 int tpke_verify_prepared(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_keys, size_t n_cts, const uint32_t *d_ct,
                          const uint32_t *d_dec, const uint8_t *d_ui, hipStream_t s) {
     if (!tpke_shape_ok(c, n_keys, n_cts, "tpke verify")) return -1;
-    return tpke_verify_core(c, (const u32 *)c->t_lines.p, (const uint8_t *)c->t_ctok.p, n_cts, n_keys, d_accept, n, d_ct,
-                            d_dec, d_ui, s);
+    return tpke_verify_core(c, (const u32 *)c->t_lines.p, (const uint8_t *)c->t_ctok.p, n_cts, c->t_keys.p, n_keys,
+                            d_accept, n, d_ct, d_dec, d_ui, s);
 }
 int tpke_partial_decrypt_prepared(lcb_ctx *c, uint8_t *ui_out, uint8_t *status, const uint8_t *x_raw, size_t x_stride,
                                   const uint8_t *cts_u, size_t n_cts, hipStream_t s) {
@@ -2263,15 +2265,42 @@ extern "C" int lcb_tpke_verify_shares_cached(uint8_t *accept, size_t n, const ui
     }
     u32 *lines = (u32 *)c->cc_lines.get((size_t)LCB_CT_CACHE * 2 * LCB_LINESET_BYTES);
     uint8_t *ctok = (uint8_t *)c->cc_ok.get(LCB_CT_CACHE);
-    void *keys = c->t_keys.get((n_keys ? n_keys : 1) * LCB_G1A_ST_BYTES);
+    void *keys = c->kc_pts.get((size_t)LCB_KEY_CACHE * LCB_G1A_ST_BYTES);
     if (!lines || !ctok || !keys) { set_err("device allocation failed"); return -1; }
     const uint64_t tick = ++c->cc_tick;
-    // the map below names slots before their line sets exist: any failure from here on empties the whole cache (the
-    // next call starts from first use), so no later call can take a slot this call left unprepared
+    // the maps below name slots before their line sets / points exist: any failure from here on empties both caches
+    // (the next call starts from first use), so no later call can take a slot this call left unfilled
     auto cache_fail = [c]() {
         c->cc_used.clear();
+        c->kc_map.clear();
+        c->kc_n = 0;
         return -1;
     };
+    // verification keys -> key-cache slots; the misses are decompressed into consecutive slots [kc_n, kc_n + misses)
+    if (n_keys > LCB_KEY_CACHE) { set_err("tpke verify (cached): more than 4096 keys in one call"); return -1; }
+    std::vector<u32> kslot(n_keys);
+    u32 kfirst = c->kc_n;
+    for (int pass = 0; pass < 2; pass++) {
+        kfirst = c->kc_n;
+        u32 next = kfirst;
+        bool full = false;
+        for (size_t k = 0; k < n_keys && !full; k++) {
+            std::string key((const char *)y_keys + 48 * k, 48);
+            auto it = c->kc_map.find(key);
+            if (it != c->kc_map.end()) { kslot[k] = it->second; continue; }
+            if (next == LCB_KEY_CACHE) { full = true; break; }
+            kslot[k] = next;
+            c->kc_map.emplace(std::move(key), next++);
+        }
+        if (!full) { c->kc_n = next; break; }
+        c->kc_map.clear();                               // this call's keys do not fit beside the old ones: start afresh
+        c->kc_n = 0;
+    }
+    std::vector<uint8_t> kmiss;
+    for (size_t k = 0; k < n_keys; k++)
+        if (kslot[k] >= kfirst) {                        // first sight, in slot order (a repeated key maps to one slot)
+            if (kmiss.size() / 48 == kslot[k] - kfirst) kmiss.insert(kmiss.end(), y_keys + 48 * k, y_keys + 48 * k + 48);
+        }
     std::vector<u32> slot_of(n_cts), miss;
     for (size_t k = 0; k < n_cts; k++) {
         const u32 v0 = v_off[k], v1 = v_off[k + 1];
@@ -2295,8 +2324,12 @@ extern "C" int lcb_tpke_verify_shares_cached(uint8_t *accept, size_t n, const ui
         miss.push_back((u32)k);
     }
     // prepare the misses straight into their slots
-    const uint8_t *dy = up(c->in[0], y_keys, 48 * n_keys, s);
-    if (n_keys) lcbk_g1_decompress(dim3(nblk(n_keys)), s, dy, (u32)n_keys, keys);
+    if (!kmiss.empty()) {
+        const size_t km = kmiss.size() / 48;
+        const uint8_t *dy = up(c->in[0], kmiss.data(), kmiss.size(), s);
+        if (!dy) { set_err("device allocation failed"); return cache_fail(); }
+        lcbk_g1_decompress(dim3(nblk(km)), s, dy, (u32)km, (uint8_t *)keys + (size_t)kfirst * LCB_G1A_ST_BYTES);
+    }
     if (!miss.empty()) {
         const size_t m = miss.size();
         std::vector<uint8_t> mu(48 * m), mw(96 * m), mv;
@@ -2328,11 +2361,13 @@ extern "C" int lcb_tpke_verify_shares_cached(uint8_t *accept, size_t n, const ui
     std::vector<u32> cslot(n);
     for (size_t i = 0; i < n; i++) cslot[i] = slot_of[ct_idx[i]];
     const uint32_t *dct = up(c->in[5], cslot.data(), n, s);
-    const uint32_t *ddec = up(c->in[6], dec_idx, n, s);
+    std::vector<u32> kdec(n);
+    for (size_t i = 0; i < n; i++) kdec[i] = kslot[dec_idx[i]];
+    const uint32_t *ddec = up(c->in[6], kdec.data(), n, s);
     const uint8_t *dui = up(c->in[7], ui, 48 * n, s);
     uint8_t *dacc = (uint8_t *)c->out[0].get(n);
-    if (!dy || !dct || !ddec || !dui || !dacc) { set_err("device allocation failed"); return cache_fail(); }
-    if (tpke_verify_core(c, lines, ctok, LCB_CT_CACHE, n_keys, dacc, n, dct, ddec, dui, s)) return cache_fail();
+    if (!dct || !ddec || !dui || !dacc) { set_err("device allocation failed"); return cache_fail(); }
+    if (tpke_verify_core(c, lines, ctok, LCB_CT_CACHE, keys, c->kc_n, dacc, n, dct, ddec, dui, s)) return cache_fail();
     if (n) hipMemcpyAsync(accept, dacc, n, hipMemcpyDeviceToHost, s);
     if (!sync_check(c, "tpke verify (cached)")) return cache_fail();
     return 0;

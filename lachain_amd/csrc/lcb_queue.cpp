@@ -5,22 +5,27 @@
 //   HoneyBadger.HandleCommonSubset filter                         (HoneyBadger.cs:156-158)
 //   ThresholdSigner.AddShare -> IsShareValid -> ValidateSignature  (src/Lachain.Crypto/ThresholdSignature/ThresholdSigner.cs:62)
 //   threads: AbstractProtocol.cs:46-47
-// A GPU launch per share would be latency-bound, so callers submit single shares and get a ticket; a worker thread (two
-// of them, so one flush runs while the next collects) flushes the pending shares as ONE batch (lcb_tpke_verify_shares / lcb_ts_verify_shares on its own context) when
-// max_batch shares are pending or the oldest pending share is max_delay_us old, and lcb_queue_wait(ticket) returns
-// that share's decision.  Ciphertexts, verification keys and messages are de-duplicated per batch, so the batch
+// A GPU launch per share would be latency-bound, so callers submit single shares and get a ticket; worker threads flush
+// the pending shares as ONE batch (lcb_tpke_verify_shares_cached / lcb_ts_verify_shares on the worker's own context)
+// when max_batch shares are pending or the oldest pending share is max_delay_us old, and lcb_queue_wait(ticket)
+// returns that share's decision.  Ciphertexts, verification keys and messages are de-duplicated per batch, so the batch
 // shares hash-to-G2 and Miller-line precomputation exactly as a caller-built batch would.  Decisions are the
 // same per-share results the batch entry points produce (bit-exact with VerifyShare / ValidateSignature).
 // lcb_queue_set_batched(q, m) sends flushes of at least m shares through the randomized batch checks instead
 // (k_batch.hip): more shares per GPU-second, a few more latency-bound launches per flush.
 //
-// Worker affinity (round 4): each worker keeps the prepared line sets of the ciphertexts it has seen (its thread
-// context's cache), so a ciphertext's shares always go to the same worker (hash of its bytes), and
-// lcb_queue_tpke_prepare(ct) prepares a ciphertext on that worker AHEAD of its shares — the reference decrypts every
-// ciphertext of the common subset (PrivateKey.Decrypt, which hashes U || V to G2: HoneyBadger.cs:144-146) before the
-// other validators' decryption shares for it are handled (HoneyBadger.cs:190-213), so the first share no longer waits
-// for hash-to-G2 and two line sets.
+// Flushes overlap (round 5): a flush is a serial chain of latency-bound launches (decompression, the nine-lane Miller
+// loop and final exponentiation: ~5 ms whatever its size) that leaves the GPU nearly idle, so three workers
+// (LCB_QUEUE_WORKERS_DEFAULT), each with its own thread context and stream, take due shares from ONE pending list: a
+// share waits for the deadline and a free worker, not for the flush in progress to end and then its own (round 4: two
+// workers with ciphertext affinity, ~1.5 flushes per share).  Each worker's context keeps the prepared line sets of the
+// ciphertexts it has seen and the decompressed verification keys, and lcb_queue_tpke_prepare(ct) prepares a ciphertext
+// on EVERY worker ahead of its shares — the reference decrypts every ciphertext of the common subset
+// (PrivateKey.Decrypt, which hashes U || V to G2: HoneyBadger.cs:144-146) before the other validators' decryption
+// shares for it are handled (HoneyBadger.cs:190-213), so no flush waits for hash-to-G2 and two line sets.  A share of a
+// ciphertext that was not prepared ahead is prepared by the worker that flushes it (and cached there).
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 #include <algorithm>
 #include <chrono>
@@ -50,15 +55,19 @@ struct TsItem {
 };
 }  // namespace
 
-#define LCB_QUEUE_WORKERS 2
+#define LCB_QUEUE_WORKERS 4      // most flushes in flight (LCB_QUEUE_WORKERS in the environment: 1 .. 4)
+#define LCB_QUEUE_WORKERS_DEFAULT 3   // three: at the default GPU_MAX_HW_QUEUES = 4 a fourth worker's stream shares a
+                                      // hardware queue with another's, and a flush queued behind a flush doubles its
+                                      // latency (profiles/r05/queue/ab.txt: p90 10.6-10.9 ms at four, 6.7 at three)
+#define LCB_QUEUE_PREP_CHUNK 1024  // ciphertexts per preparation call (the widest batch the context cache takes)
 struct lcb_queue {
     std::mutex mu;
     std::condition_variable cv_work, cv_done;
     size_t max_batch;
     std::chrono::microseconds max_delay;
-    std::vector<TpkeItem> tpke[LCB_QUEUE_WORKERS];     // per worker (ciphertext affinity)
-    std::vector<std::string> prep[LCB_QUEUE_WORKERS];  // ciphertexts to prepare ahead of their shares
-    clk::time_point oldest[LCB_QUEUE_WORKERS];
+    std::vector<TpkeItem> tpke;                        // any worker
+    clk::time_point oldest;
+    std::vector<std::string> prep[LCB_QUEUE_WORKERS];  // ciphertexts to prepare ahead of their shares, on every worker
     std::vector<TsItem> ts;                            // any worker
     clk::time_point ts_oldest;
     bool stop = false, flush_now = false;
@@ -70,9 +79,9 @@ struct lcb_queue {
     // *_batched entry points, shares ordered by ciphertext / message so each one's shares form a group
     size_t batched_min = 0;
     std::string last_error;
-    // two workers, each with its own thread context (and prepared-ciphertext cache): a flush does not wait for the
-    // previous one's GPU round trip, so a share's latency is its own batch's, not two
+    // the workers, each with its own thread context (prepared-ciphertext and key caches) and stream
     std::vector<std::thread> workers;
+    int n_workers = LCB_QUEUE_WORKERS_DEFAULT;
     uint64_t prepared = 0;
 };
 
@@ -190,8 +199,13 @@ void run_prepare(lcb_queue *q, std::vector<std::string> &cts) {
         voff.push_back((uint32_t)vs.size());
     }
     if (vs.empty()) vs.push_back(0);
-    int rc = lcb_tpke_verify_shares_cached(nullptr, 0, nullptr, 0, us.data(), ws.data(), vs.data(), voff.data(),
-                                           cidx.size(), nullptr, nullptr, nullptr);
+    int rc = 0;
+    for (size_t k0 = 0; k0 < cidx.size() && !rc; k0 += LCB_QUEUE_PREP_CHUNK) {
+        const size_t m = std::min((size_t)LCB_QUEUE_PREP_CHUNK, cidx.size() - k0);
+        std::vector<uint32_t> vo(voff.begin() + k0, voff.begin() + k0 + m + 1);
+        rc = lcb_tpke_verify_shares_cached(nullptr, 0, nullptr, 0, us.data() + 48 * k0, ws.data() + 96 * k0, vs.data(),
+                                           vo.data(), m, nullptr, nullptr, nullptr);
+    }
     std::lock_guard<std::mutex> lk(q->mu);
     if (rc) q->last_error = lcb_last_error();
     else q->prepared += cidx.size();
@@ -200,18 +214,18 @@ void run_prepare(lcb_queue *q, std::vector<std::string> &cts) {
 void worker_loop(lcb_queue *q, int w) {
     std::unique_lock<std::mutex> lk(q->mu);
     for (;;) {
-        const size_t pt = q->tpke[w].size(), ps = q->ts.size(), pp = q->prep[w].size();
+        const size_t pt = q->tpke.size(), ps = q->ts.size(), pp = q->prep[w].size();
         if (pt + ps + pp == 0) {
             if (q->stop) return;
             q->cv_work.wait(lk);
             continue;
         }
         const clk::time_point now = clk::now();
-        const bool due_t = pt && (q->stop || q->flush_now || pt >= q->max_batch || now >= q->oldest[w] + q->max_delay);
+        const bool due_t = pt && (q->stop || q->flush_now || pt >= q->max_batch || now >= q->oldest + q->max_delay);
         const bool due_s = ps && (q->stop || q->flush_now || ps >= q->max_batch || now >= q->ts_oldest + q->max_delay);
         if (!pp && !due_t && !due_s) {
             clk::time_point next = clk::time_point::max();
-            if (pt) next = std::min(next, q->oldest[w] + q->max_delay);
+            if (pt) next = std::min(next, q->oldest + q->max_delay);
             if (ps) next = std::min(next, q->ts_oldest + q->max_delay);
             q->cv_work.wait_until(lk, next);
             continue;
@@ -220,9 +234,11 @@ void worker_loop(lcb_queue *q, int w) {
         std::vector<TsItem> s;
         std::vector<std::string> p;
         p.swap(q->prep[w]);
-        if (due_t) t.swap(q->tpke[w]);
-        if (due_s) s.swap(q->ts);
-        if (q->tpke[0].empty() && q->tpke[1].empty() && q->ts.empty()) q->flush_now = false;
+        if (p.empty()) {              // this worker's preparations first: the shares it takes then hit its cache
+            if (due_t) t.swap(q->tpke);
+            if (due_s) s.swap(q->ts);
+        }
+        if (q->tpke.empty() && q->ts.empty()) q->flush_now = false;
         const size_t batched_min = q->batched_min;     // read under the lock (lcb_queue_set_batched writes it)
         const size_t pending = t.size() + s.size();
         if (pending) {
@@ -231,15 +247,15 @@ void worker_loop(lcb_queue *q, int w) {
             if (pending > q->max_seen) q->max_seen = pending;
         }
         lk.unlock();
-        if (!p.empty()) run_prepare(q, p);              // ahead of the shares: they then hit the cache
+        if (!p.empty()) run_prepare(q, p);
         if (!t.empty()) run_tpke(q, t, batched_min);
         if (!s.empty()) run_ts(q, s, batched_min);
         lk.lock();
-        q->cv_done.notify_all();
+        if (pending) q->cv_done.notify_all();
+        else q->cv_work.notify_all();   // due shares this worker left while it prepared: another worker may be idle
     }
 }
 
-int worker_of(const std::string &ct) { return (int)(std::hash<std::string>{}(ct) % LCB_QUEUE_WORKERS); }
 void wake(lcb_queue *q, size_t pending, size_t max_batch) {
     if (pending == 1 || pending >= max_batch) q->cv_work.notify_all();
 }
@@ -250,7 +266,11 @@ extern "C" lcb_queue *lcb_queue_create(size_t max_batch, uint32_t max_delay_us) 
     lcb_queue *q = new lcb_queue;
     q->max_batch = max_batch ? max_batch : 1;
     q->max_delay = std::chrono::microseconds(max_delay_us);
-    for (int k = 0; k < LCB_QUEUE_WORKERS; k++) q->workers.emplace_back(worker_loop, q, k);
+    if (const char *e = getenv("LCB_QUEUE_WORKERS")) {    // A/B knob: 1 .. LCB_QUEUE_WORKERS
+        const int k = atoi(e);
+        if (k >= 1 && k <= LCB_QUEUE_WORKERS) q->n_workers = k;
+    }
+    for (int k = 0; k < q->n_workers; k++) q->workers.emplace_back(worker_loop, q, k);
     return q;
 }
 extern "C" void lcb_queue_destroy(lcb_queue *q) {
@@ -274,14 +294,13 @@ extern "C" int64_t lcb_queue_tpke_verify(lcb_queue *q, const uint8_t y48[48], co
     it.ct.append((const char *)w96, 96);
     if (v_len) it.ct.append((const char *)v, v_len);
     memcpy(it.ui, ui48, 48);
-    const int w = worker_of(it.ct);
     std::unique_lock<std::mutex> lk(q->mu);
     if (q->stop) return -1;
     it.ticket = q->next_ticket++;
     q->open.insert(it.ticket);
-    q->tpke[w].push_back(std::move(it));
-    const size_t pending = q->tpke[w].size();
-    if (pending == 1) q->oldest[w] = clk::now();
+    q->tpke.push_back(std::move(it));
+    const size_t pending = q->tpke.size();
+    if (pending == 1) q->oldest = clk::now();
     wake(q, pending, q->max_batch);
     return q->next_ticket - 1;
 }
@@ -293,10 +312,9 @@ extern "C" int lcb_queue_tpke_prepare(lcb_queue *q, const uint8_t u48[48], const
     ct.append((const char *)u48, 48);
     ct.append((const char *)w96, 96);
     if (v_len) ct.append((const char *)v, v_len);
-    const int w = worker_of(ct);
     std::lock_guard<std::mutex> lk(q->mu);
     if (q->stop) return -1;
-    q->prep[w].push_back(std::move(ct));
+    for (int w = 0; w < q->n_workers; w++) q->prep[w].push_back(ct);
     q->cv_work.notify_all();
     return 0;
 }

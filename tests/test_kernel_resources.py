@@ -17,8 +17,8 @@ SO = os.path.join(ROOT, "lachain_amd", "liblachain_bls.so")
 # kernel: (max VGPR spills, max scratch bytes per lane) — measured on this build
 BUDGET = {
     "k_lineset_coop_2w": (270, 1080),         # k_prep.hip: the fused census's line sets at 256 registers
-    "k_coop_debug": (96, 7620),               # test hook: the one-lane reference routines beside the coop ones
-    "k_coop_final_exp_check": (0, 576),
+    "k_coop_debug": (204, 7620),              # test hook: the one-lane reference routines beside the coop ones
+    "k_coop_final_exp_check": (36, 576),     # round 5: three quads saved around the one binary-GCD call per check
     "k_coop_tpke_miller": (0, 0),
     "k_dkg_exact_combine": (0, 312),
     "k_dkg_exact_terms": (0, 408),
@@ -92,7 +92,7 @@ SINGLE_WAVE = {"k_op_grp", "k_op_pair", "k_op_gt", "k_op_debug", "k_coop_debug"}
 # one lane per ciphertext (748 waves for configs[1]'s 1M shares: a 222 MB reservation at 4.6 KB per lane), at 256
 # registers so a wave shares its SIMD with a randomisation wave (k_prep.hip)
 PER_CIPHERTEXT = {"k_tpke_ct_prepare_h": 4900}
-ZERO_SPILL = ["k_coop_tpke_miller", "k_coop_final_exp_check", "k_msm_bucket_acc", "k_secp_verify",
+ZERO_SPILL = ["k_coop_tpke_miller", "k_msm_bucket_acc", "k_secp_verify",
               "k_rlc_census_stats", "k_rlc_suspect_split", "k_rlc_resolve", "k_tpke_rlc_sum", "k_ts_rlc_miller"]
 
 
