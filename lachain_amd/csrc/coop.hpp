@@ -525,3 +525,18 @@ DI void cp_final_exp(fp2 &R, const Cp &c, u32 *park, size_t n, size_t i, bool li
         else cp_inv(R, c);
     }
 }
+// accept[i] &= (final_exp(f_i) == 1) for f_i in park slot 0, slot 0 <- the GT value (k_coop_final_exp_check, and the
+// census copy in k_prep.hip at 256 registers); lds = the wave's CP_LDS_QUADS
+DI void cp_final_exp_check_run(uint4 *lds, u32 *park, u32 n, uint8_t *accept) {
+    const Cp c = cp_init(lds);
+    const u32 item = blockIdx.x * CP_G + c.g;
+    const bool live = c.g < CP_G && item < n;
+    const size_t it = live ? item : 0;
+    if (cpj(c) == 0) cp_put(c, S_Z, fp2_zero());
+    cp_sync();
+    fp2 R;
+    cp_final_exp(R, c, park, n, it, live);
+    const bool one = cp_is_one(R, c);
+    park_put(park, n, it, cpj(c), live, R);
+    if (live && cpj(c) == 0 && accept) accept[item] = accept[item] && one;
+}

@@ -159,6 +159,18 @@ template <class F> DI void jac_to_aff(aff<F> &a, const jac<F> &p) {
     f_mul(a.y, p.y, zi2);
     a.inf = false;
 }
+// the same for G2 with the binary-GCD Fp inversion (field.hpp fp2_inv_gn: ~40 K instructions against the
+// exponentiation's 263 K; the same canonical result), for the one-lane hash lanes where the call is cheap
+DI void g2_jac_to_aff_g(g2a &a, const g2 &p) {
+    if (jac_is_inf(p)) { a.inf = true; f_zero(a.x); f_zero(a.y); return; }
+    fp2 zi, zi2;
+    fp2_inv_gn(zi, p.z);
+    f_sqr(zi2, zi);
+    f_mul(a.x, p.x, zi2);
+    f_mul(zi2, zi2, zi);
+    f_mul(a.y, p.y, zi2);
+    a.inf = false;
+}
 DN void g1_dbl_n(g1 &r, const g1 &p) { g1 t; jac_dbl(t, p); r = t; }
 DN void g1_add_n(g1 &r, const g1 &p, const g1 &q) { g1 t; jac_add(t, p, q); r = t; }
 DN void g2_dbl_n(g2 &r, const g2 &p) { g2 t; jac_dbl(t, p); r = t; }

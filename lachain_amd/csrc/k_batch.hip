@@ -33,6 +33,7 @@
 //   k_rlc_resolve       one lane per group: failed single share -> reject; failed group -> sub-groups of the next level
 #include "kcommon.hpp"
 #include "rlc_common.hpp"
+#include "ts_rlc.hpp"
 
 LCB_ASM_LIBRARY(k_batch)
 LCB_TU_CONFIG(k_batch)
@@ -93,70 +94,15 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum(const uint4 *sdesc, u32 n_
     gpts[2 * (size_t)g + 1] = o;
 }
 
-// ---------------------------------------------------------------- threshold signatures (ValidateSignature)
-// e(PK_i, H(m)) == e(G, sig_i) <=> e(PK_i, H) e(-G, sig_i) == 1.  The randomisation of sig_i uses linearity of the
-// pairing in its G2 argument, which holds on G2: a share whose sig_i is outside G2 (G2.FromBytes does not check) is
-// emitted straight away as an exact single (desc.w = 1) and contributes nothing to its group.
-// TS group record: g1a_st P (sum s_i PK_i) then g2a_st S (sum s_i sig_i), 320 B
-struct ts_grp { g1a_st p; g2a_st s; };
+// ---------------------------------------------------------------- threshold signatures: the group sums and Miller
+// loops (ts_rlc.hpp)
 extern "C" __global__ void LCB_BOUNDS k_ts_rlc_sum(const uint4 *desc, u32 n_groups, u32 first, const uint8_t *msg_ok,
                                                   const g1a_st *pks, u32 n_pks, const u32 *pk_idx, const uint8_t *sigs,
                                                   const u32 *rP, const u32 *rS, u32 n, ts_grp *gpts, uint8_t *accept,
                                                   uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval) {
     LCB_LATENCY_PRIO();
-    u32 g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= n_groups) return;
-    uint4 dsc = desc[g];
-    ts_grp o;
-    g1_inf_st(o.p);
-    g2_inf_st(o.s);
-    gexact[g] = 0;
-    if (dsc.w == 1) {                    // exact single: the share's own PK and sig (whole validity re-derived)
-        u32 k = pk_idx[dsc.x];
-        bool live = accept[dsc.x] && msg_ok[dsc.z] && k < n_pks;
-        if (live) {
-            g2a S;
-            live = pks[k].ok && g2_decompress(S, sigs + 96 * (size_t)dsc.x);
-            if (live) {
-                o.p = pks[k];
-                o.s.x = S.x; o.s.y = S.y; o.s.inf = S.inf;
-            }
-        }
-        if (!live) accept[dsc.x] = 0;
-        if (cval) cval[dsc.x] = live;
-        gpts[g] = o;
-        return;
-    }
-    if (!msg_ok[dsc.z]) {
-        for (u32 j = 0; j < dsc.y; j++) accept[dsc.x + j] = 0;
-        gpts[g] = o;
-        return;
-    }
-    g1 sp, t, wp;
-    g2 ss, u, ws;
-    jac_set_inf(sp);
-    jac_set_inf(wp);
-    jac_set_inf(ss);
-    jac_set_inf(ws);
-    for (u32 j = dsc.y; j-- > 0;) {
-        if (!key_suspect(susp, pk_idx[dsc.x + j], n_pks)) {
-            g1_load_soa(t, rP, n, dsc.x + j);
-            grp_add(sp, sp, t);
-            g2_load_soa(u, rS, n, dsc.x + j);
-            grp_add(ss, ss, u);
-        }
-        if (first) {
-            grp_add(wp, wp, sp);
-            grp_add(ws, ws, ss);
-        }
-    }
-    if (first) {
-        g1_store_soa(wsum, n_groups, g, wp);
-        g2_store_soa(wsum + (size_t)36 * n_groups, n_groups, g, ws);
-    }
-    g1_to_st(o.p, sp, false);
-    g2_to_st(o.s, ss);
-    gpts[g] = o;
+    ts_rlc_sum_run(desc, n_groups, first, msg_ok, pks, n_pks, pk_idx, sigs, rP, rS, n, gpts, accept, gexact, wsum, susp,
+                   cval);
 }
 extern "C" __global__ void LCB_BOUNDS k_ts_rlc_wsum(const uint4 *sdesc, u32 n_s, const u32 *wsum, u32 n_l1,
                                                    ts_grp *gpts) {
@@ -169,41 +115,14 @@ extern "C" __global__ void LCB_BOUNDS k_ts_rlc_wsum(const uint4 *sdesc, u32 n_s,
     ts_grp o;
     g1_load_soa(p, wsum, n_l1, l);
     g2_load_soa(q, wsum + (size_t)36 * n_l1, n_l1, l);
-    g1_to_st(o.p, p, false);
-    g2_to_st(o.s, q);
+    g1_to_st_gcd(o.p, p, false);
+    g2_to_st_gcd(o.s, q);
     gpts[g] = o;
-}
-// miller2_ts (k_ts.hip): the message's line set with sum s_i PK_i, the group signature's lines on the fly with -G
-DN void miller2_ts_grp(fp12 &f, const u32 *lsH, const g1a &PK, const g2a &S, const g1a &G) {
-    g2a Q;
-    LinesOnTheFly sS;
-    sS.init(S);
-    if (lineset_normalised(lsH)) {
-        LinesNorm sH{lsH};
-        miller2(f, sH, PK, sS, G);
-    } else {
-        lineset_point(Q, lsH);
-        LinesOnTheFly sH;
-        sH.init(Q);
-        miller2(f, sH, PK, sS, G);
-    }
 }
 extern "C" __global__ void LCB_PAIR_BOUNDS k_ts_rlc_miller(const u32 *lines, const uint4 *desc, const ts_grp *gpts,
                                                           u32 n_groups, u32 *f_soa, uint8_t *gacc) {
     LCB_LATENCY_PRIO();
-    u32 g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= n_groups) return;
-    u32 m = desc[g].z;
-    g1a P, G;
-    g2a S;
-    st_to_g1a(P, gpts[g].p);
-    st_to_g2a(S, gpts[g].s);
-    g1_generator(G);
-    fp_neg(G.y, G.y);
-    fp12 f;
-    miller2_ts_grp(f, lines + (size_t)m * LCB_LINESET_WORDS, P, S, G);
-    fp12_store_soa(f_soa, n_groups, g, f);
-    gacc[g] = 1;
+    ts_rlc_miller_run(lines, desc, gpts, n_groups, f_soa, gacc);
 }
 
 // ---------------------------------------------------------------- resolve a level (TPKE and TS)
@@ -265,43 +184,6 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_resolve(const uint4 *desc, u32 o, u3
         next[slot + k] = make_uint4(st, len, d.z, 0);
     }
 }
-// Level 2: search entries [o, o + m): gamma' (the weighted group check's final-exponentiation output, park stride m)
-// against gamma^c, c = 1..len.  A match rejects share c - 1 of the group (the only bad one, see the header); no match
-// sends every share of the group to a single check at the next level.
-extern "C" __global__ void LCB_BOUNDS k_rlc_search(const uint4 *search, u32 o, u32 m, const u32 *gamma, const u32 *park,
-                                                  uint8_t *accept, uint4 *next, u32 *next_count, const u32 *key_idx,
-                                                  u32 n_keys, const u32 *susp) {
-    LCB_LATENCY_PRIO();
-    u32 gl = blockIdx.x * blockDim.x + threadIdx.x;
-    if (gl >= m) return;
-    u32 g = o + gl;
-    uint4 d = search[g];
-    fp12 gm, gp, acc;
-    u32 *w = (u32 *)&gm;
-    const uint4 *src = (const uint4 *)(gamma + (size_t)g * 144);
-#pragma unroll
-    for (int q = 0; q < 36; q++) {
-        uint4 v = src[q];
-        w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
-    }
-    fp12_load_soa(gp, park, m, gl);
-    acc = gm;
-    u32 found = 0;
-    for (u32 c = 1; c <= d.y; c++) {
-        const u32 *a = (const u32 *)&acc, *b = (const u32 *)&gp;
-        u32 x = 0;
-#pragma unroll
-        for (int q = 0; q < 144; q++) x |= a[q] ^ b[q];
-        if (x == 0) { found = c; break; }
-        fp12_mul_n(acc, acc, gm);
-    }
-    if (found) {
-        accept[d.x + found - 1] = 0;
-        return;
-    }
-    emit_singles(d, 0, accept, key_idx, n_keys, susp, next, next_count);
-}
-
 // the final-exponentiation outputs of checks [o, o + m) (park stride m) -> rows o.. of dst (576 B each)
 // *flag |= 1 when a line set of ciphertexts [c0, c1) is not normalised (the Miller fallback will be needed)
 extern "C" __global__ void LCB_BOUNDS k_lines_unnormalised(const u32 *lines, u32 c0, u32 c1, u32 *flag) {
@@ -337,10 +219,10 @@ DI bool fp12_words_eq(const fp12 &a, const fp12 &b) {
     for (int q = 0; q < 144; q++) d |= x[q] ^ y[q];
     return d == 0;
 }
-// r = a^e for a in the cyclotomic subgroup (GT), 1 <= e < 2^8
+// r = a^e for a in the cyclotomic subgroup (GT), e >= 1
 DN void gt_pow_small(fp12 &r, const fp12 &a, u32 e) {
     fp12 t = a;
-    int top = 7;
+    int top = 31;
     while (top > 0 && !((e >> top) & 1)) top--;
     for (int b = top - 1; b >= 0; b--) {
         fp12_cyc_sqr_n(t, t);
@@ -372,6 +254,70 @@ DI u32 fp12_fingerprint(const fp12 &a) {
 DI u32 half_ballot(bool p) {
     const unsigned long long m = __ballot(p);
     return (u32)(m >> (32 * ((threadIdx.x >> 5) & 1)));
+}
+// Level 2: search entries [o, o + m): gamma' (the weighted group check's final-exponentiation output, park stride m)
+// against gamma^c, c = 1..len.  A match rejects share c - 1 of the group (the only bad one, see the header); no match
+// sends every share of the group to a single check at the next level.  gamma != 1 (the group failed) has order r, so at
+// most one c in [1, len] matches.  Baby-step giant-step (round 5; the linear scan took len / 2 products on average,
+// 13.5 ms for configs[2]'s 100-share rounds): 32-bit fingerprints of gamma^1 .. gamma^M, giant steps
+// Y_i = gamma' gamma^(-M i) (gamma is unitary: gamma^-M = conj(gamma^M)); the first fingerprint match Y_i ~ gamma^(k+1)
+// names the candidate c = M i + k + 1, confirmed by the full comparison gamma^c == gamma' — M + len / (2M) + ~10
+// products.  A fingerprint collision that is not a match (probability ~ len 2^-32) falls back to the linear scan, so
+// the decision is the linear scan's in every case.
+#define RLC_BS_M 12
+DN u32 rlc_search_linear(const fp12 &gm, const fp12 &gp, u32 len) {
+    fp12 acc = gm;
+    for (u32 c = 1; c <= len; c++) {
+        if (fp12_words_eq(acc, gp)) return c;
+        fp12_mul_n(acc, acc, gm);
+    }
+    return 0;
+}
+extern "C" __global__ void LCB_BOUNDS k_rlc_search(const uint4 *search, u32 o, u32 m, const u32 *gamma, const u32 *park,
+                                                  uint8_t *accept, uint4 *next, u32 *next_count, const u32 *key_idx,
+                                                  u32 n_keys, const u32 *susp) {
+    LCB_LATENCY_PRIO();
+    u32 gl = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gl >= m) return;
+    u32 g = o + gl;
+    uint4 d = search[g];
+    const u32 *grow = gamma + (size_t)g * 144;
+    fp12 y, t;
+    u32 fpb[RLC_BS_M];
+    fp12_load_row(t, grow);
+    fpb[0] = fp12_fingerprint(t);
+    if (d.y > 1) {
+        fp12 gm;
+        fp12_load_row(gm, grow);
+#pragma unroll
+        for (int k = 1; k < RLC_BS_M; k++) {
+            fp12_mul_n(t, t, gm);
+            fpb[k] = fp12_fingerprint(t);
+        }
+    }
+    fp12_conj(t, t);                                       // gamma^-M
+    fp12_load_soa(y, park, m, gl);                         // Y_0 = gamma'
+    u32 cand = 0;
+    for (u32 base = 0; base < d.y && !cand; base += RLC_BS_M) {
+        const u32 fy = fp12_fingerprint(y);
+#pragma unroll
+        for (int k = 0; k < RLC_BS_M; k++)
+            if (!cand && base + k + 1 <= d.y && fpb[k] == fy) cand = base + k + 1;
+        if (!cand && base + RLC_BS_M < d.y) fp12_mul_n(y, y, t);
+    }
+    u32 found = 0;
+    if (cand) {
+        fp12 gm, gp;
+        fp12_load_row(gm, grow);
+        fp12_load_soa(gp, park, m, gl);
+        gt_pow_small(t, gm, cand);
+        found = fp12_words_eq(t, gp) ? cand : rlc_search_linear(gm, gp, d.y);
+    }
+    if (found) {
+        accept[d.x + found - 1] = 0;
+        return;
+    }
+    emit_singles(d, 0, accept, key_idx, n_keys, susp, next, next_count);
 }
 // Level 2 of TPKE: locate up to TWO bad shares per failed group.  With e_i = s_i log g_i (nonzero exactly for the bad
 // shares) the three group values are gamma_0 (level 1) ~ sum e_i, gamma_c ~ sum e_i c_i and gamma_t ~ sum e_i t_i, so

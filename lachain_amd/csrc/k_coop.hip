@@ -88,17 +88,7 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_rlc_miller_fallback(const u32 *line
 extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_final_exp_check(u32 *park, u32 n, uint8_t *accept) {
     LCB_LATENCY_PRIO();
     __shared__ uint4 lds[CP_LDS_QUADS];
-    const Cp c = cp_init(lds);
-    const u32 item = blockIdx.x * CP_G + c.g;
-    const bool live = c.g < CP_G && item < n;
-    const size_t it = live ? item : 0;
-    if (cpj(c) == 0) cp_put(c, S_Z, fp2_zero());
-    cp_sync();
-    fp2 R;
-    cp_final_exp(R, c, park, n, it, live);
-    const bool one = cp_is_one(R, c);
-    park_put(park, n, it, cpj(c), live, R);
-    if (live && cpj(c) == 0 && accept) accept[item] = accept[item] && one;
+    cp_final_exp_check_run(lds, park, n, accept);
 }
 
 // The exact per-share check (k_tpke_miller's inputs) in the cooperative kernels' form, for small batches: share i

@@ -6,6 +6,8 @@
 // randomisation started 14-16 ms into the step, when the preparation waves retired).
 #include "kcommon.hpp"
 #include "lines_coop.hpp"
+#include "coop.hpp"
+#include "ts_rlc.hpp"
 
 LCB_ASM_LIBRARY(k_prep)
 LCB_TU_CONFIG(k_prep)
@@ -27,7 +29,7 @@ extern "C" __global__ void LCB_PREP_BOUNDS k_tpke_ct_prepare_h(const uint8_t *ct
     g2 H;
     g2a Ha;
     bool hok = g2_hash_digest(H, d, (flags & 1) != 0);
-    if (hok) jac_to_aff(Ha, H);
+    if (hok) g2_jac_to_aff_g(Ha, H);
     else { Ha.inf = true; Ha.x = fp2_zero(); Ha.y = fp2_zero(); }
     u32 *ls = lines + (size_t)(2 * c) * LCB_LINESET_WORDS;
     lineset_compute(ls, Ha);
@@ -52,6 +54,28 @@ extern "C" __global__ void LCB_PREP_BOUNDS k_tpke_ct_prepare_w(const uint8_t *ct
     w_g2[c] = (r & LCB_LS_IN_G2) ? 1 : 0;
 }
 
+// H(m) and its line set per message (the CommonCoin preparation, ThresholdSigner.cs:44-87 hashes each coin's message):
+// here at 256 registers, so the 1,024 waves of configs[2] share their SIMDs with the randomisation's instead of
+// waiting for whole SIMDs to drain (at 346 registers the kernel ran 462 ms beside k_ts_rlc_points against 16 ms
+// ahead of it, round-5 trace)
+extern "C" __global__ void LCB_PREP_BOUNDS k_ts_msg_prepare(const uint8_t *msg_data, const u32 *msg_off, u32 n_msgs,
+                                                           u32 *lines, uint8_t *msg_ok, int flags) {
+    LCB_LATENCY_PRIO();
+    u32 m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= n_msgs) return;
+    uint8_t d[64];
+    u32 o0 = msg_off[m], o1 = msg_off[m + 1];
+    sha512_2(d, msg_data + o0, o1 - o0, msg_data, 0);
+    g2 H;
+    g2a Ha;
+    bool ok = g2_hash_digest(H, d, (flags & 1) != 0);
+    if (ok) g2_jac_to_aff_g(Ha, H);
+    else { Ha.inf = true; Ha.x = fp2_zero(); Ha.y = fp2_zero(); }
+    lineset_compute(lines + (size_t)m * LCB_LINESET_WORDS, Ha);
+    if (flags & 2) lines[(size_t)m * LCB_LINESET_WORDS + LCB_LS_FLAG] = 0;
+    msg_ok[m] = ok;
+}
+
 // k_lineset_coop (k_lines.hip) at two waves per SIMD: the census ciphertexts' line sets, which run while the
 // randomisation and the preparation hold the SIMDs (at 417 registers a wave of k_lineset_coop found room only as
 // those waves retired: 4 -> 24 ms in the round-5 A/B)
@@ -61,11 +85,58 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
     lineset_coop_run(lds, lines, n_sets, sets, w_g2);
 }
 
+// The CommonCoin census chain (lcb_host.cpp rlc_census: the census shares' exact singles, their two-pair Miller loops,
+// the nine-lane final exponentiation) at 256 registers: k_ts_rlc_points holds two 256-register waves per SIMD for
+// ~450 ms, and the 294 / 360 / 284-register copies of k_batch.hip / k_coop.hip found no SIMD with room until it
+// retired, so the census ran after the randomisation, on the step's critical path (round-5 trace: 20 ms).  At 256 a
+// census wave takes the slot of the first randomisation wave that retires (its stream has the higher priority).
+extern "C" __global__ void LCB_PREP_BOUNDS k_ts_rlc_sum_census(const uint4 *desc, u32 n_groups, u32 first,
+                                                              const uint8_t *msg_ok, const g1a_st *pks, u32 n_pks,
+                                                              const u32 *pk_idx, const uint8_t *sigs, const u32 *rP,
+                                                              const u32 *rS, u32 n, ts_grp *gpts, uint8_t *accept,
+                                                              uint8_t *gexact, u32 *wsum, const u32 *susp,
+                                                              uint8_t *cval) {
+    LCB_LATENCY_PRIO();
+    ts_rlc_sum_run(desc, n_groups, first, msg_ok, pks, n_pks, pk_idx, sigs, rP, rS, n, gpts, accept, gexact, wsum, susp,
+                   cval);
+}
+extern "C" __global__ void LCB_PREP_BOUNDS k_ts_rlc_miller_census(const u32 *lines, const uint4 *desc,
+                                                                 const ts_grp *gpts, u32 n_groups, u32 *f_soa,
+                                                                 uint8_t *gacc) {
+    LCB_LATENCY_PRIO();
+    ts_rlc_miller_run(lines, desc, gpts, n_groups, f_soa, gacc);
+}
+extern "C" __global__ void __launch_bounds__(CP_BLOCK) __attribute__((amdgpu_waves_per_eu(2)))
+k_coop_final_exp_check_census(u32 *park, u32 n, uint8_t *accept) {
+    LCB_LATENCY_PRIO();
+    __shared__ uint4 lds[CP_LDS_QUADS];
+    cp_final_exp_check_run(lds, park, n, accept);
+}
+
 // ---------------------------------------------------------------- host launch wrappers
+extern "C" void lcbk_ts_rlc_sum_census(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 first,
+                                       const uint8_t *msg_ok, const void *pks, u32 n_pks, const u32 *pk_idx,
+                                       const uint8_t *sigs, const u32 *rP, const u32 *rS, u32 n, void *gpts,
+                                       uint8_t *accept, uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval) {
+    LCB_LAUNCH(k_ts_rlc_sum_census, (const uint4 *)desc, n_groups, first, msg_ok, (const g1a_st *)pks, n_pks, pk_idx,
+               sigs, rP, rS, n, (ts_grp *)gpts, accept, gexact, wsum, susp, cval);
+}
+extern "C" void lcbk_ts_rlc_miller_census(dim3 grid, hipStream_t s, const u32 *lines, const void *desc,
+                                          const void *gpts, u32 n_groups, u32 *f_soa, uint8_t *gacc) {
+    LCB_LAUNCH(k_ts_rlc_miller_census, lines, (const uint4 *)desc, (const ts_grp *)gpts, n_groups, f_soa, gacc);
+}
+extern "C" void lcbk_coop_final_exp_check_census(hipStream_t s, u32 *park, u32 n, uint8_t *accept) {
+    dim3 grid((n + CP_G - 1) / CP_G);
+    hipLaunchKernelGGL(k_coop_final_exp_check_census, grid, dim3(CP_BLOCK), 0, s, park, n, accept);
+}
 extern "C" void lcbk_lineset_coop_2w(hipStream_t s, u32 *lines, u32 n_sets, const u32 *sets, uint8_t *w_g2) {
     if (!n_sets) return;
     hipLaunchKernelGGL(k_lineset_coop_2w, dim3((n_sets + LS_GROUPS - 1) / LS_GROUPS), dim3(64), 0, s, lines, n_sets,
                        sets, w_g2);
+}
+extern "C" void lcbk_ts_msg_prepare(dim3 grid, hipStream_t s, const uint8_t *msg_data, const u32 *msg_off, u32 n_msgs,
+                                    u32 *lines, uint8_t *msg_ok, int orig_cof) {
+    LCB_LAUNCH(k_ts_msg_prepare, msg_data, msg_off, n_msgs, lines, msg_ok, orig_cof);
 }
 // ciphertexts [c0, c1)
 extern "C" void lcbk_tpke_ct_prepare_h(hipStream_t s, const uint8_t *cts_u, const uint8_t *v_data, const u32 *v_off, u32 c0, u32 c1, u32 *lines, uint8_t *h_ok, int flags) {

@@ -5,22 +5,7 @@ LCB_ASM_LIBRARY(k_ts)
 LCB_TU_CONFIG(k_ts)
 
 // ================================================================================= threshold signatures
-extern "C" __global__ void LCB_BOUNDS k_ts_msg_prepare(const uint8_t *msg_data, const u32 *msg_off, u32 n_msgs,
-                                                      u32 *lines, uint8_t *msg_ok, int flags) {
-    u32 m = blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= n_msgs) return;
-    uint8_t d[64];
-    u32 o0 = msg_off[m], o1 = msg_off[m + 1];
-    sha512_2(d, msg_data + o0, o1 - o0, msg_data, 0);
-    g2 H;
-    g2a Ha;
-    bool ok = g2_hash_digest(H, d, (flags & 1) != 0);
-    if (ok) jac_to_aff(Ha, H);
-    else { Ha.inf = true; Ha.x = fp2_zero(); Ha.y = fp2_zero(); }
-    lineset_compute(lines + (size_t)m * LCB_LINESET_WORDS, Ha);
-    if (flags & 2) lines[(size_t)m * LCB_LINESET_WORDS + LCB_LS_FLAG] = 0;
-    msg_ok[m] = ok;
-}
+// k_ts_msg_prepare (hash to G2 + the message's line set) lives in k_prep.hip at 256 registers (round 5)
 // two-pair Miller loop of a signature check: the message's line set (normalised, or its point's lines on the fly
 // when it could not be normalised) and the share's lines on the fly
 DN void miller2_ts_fallback(fp12 &f, const u32 *lsH, const g1a &PK, const g2a &S, const g1a &G) {
@@ -128,9 +113,6 @@ extern "C" __global__ void LCB_BOUNDS k_coin_fold(const uint8_t *sigs, u32 n, ui
 }
 
 // ---------------------------------------------------------------- host launch wrappers
-extern "C" void lcbk_ts_msg_prepare(dim3 grid, hipStream_t s, const uint8_t *msg_data, const u32 *msg_off, u32 n_msgs, u32 *lines, uint8_t *msg_ok, int orig_cof) {
-    LCB_LAUNCH(k_ts_msg_prepare, msg_data, msg_off, n_msgs, lines, msg_ok, orig_cof);
-}
 extern "C" void lcbk_ts_miller(dim3 grid, hipStream_t s, const u32 *lines, const uint8_t *msg_ok, u32 n_msgs, const void *pks, u32 n_pks, const uint8_t *sigs, const u32 *msg_idx, const u32 *pk_idx, u32 n, u32 *f_soa, uint8_t *accept) {
     LCB_LAUNCH(k_ts_miller, lines, msg_ok, n_msgs, (const g1a_st *)pks, n_pks, sigs, msg_idx, pk_idx, n, f_soa, accept);
 }

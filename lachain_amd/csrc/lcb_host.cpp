@@ -1235,10 +1235,15 @@ RlcKindInfo rlc_kind(lcb_ctx *c, RlcKind kind) {
     return k;
 }
 // the group sums / singles of a level's desc list -> gpts (k_*_rlc_sum)
+// (census: the CommonCoin census's 256-register copies, k_prep.hip)
 void rlc_sum_enqueue(const RlcKindInfo &K, RlcWs &w, const uint8_t *desc, u32 groups, bool first, uint8_t *d_accept,
-                     size_t n, RlcIo io, void *gpts, uint8_t *gex, u32 *wsum, uint8_t *cval, hipStream_t s) {
+                     size_t n, RlcIo io, void *gpts, uint8_t *gex, u32 *wsum, uint8_t *cval, hipStream_t s,
+                     bool census = false) {
     const u32 *susp = w.susp;
-    if (K.ts)
+    if (K.ts && census)
+        lcbk_ts_rlc_sum_census(dim3(nblk(groups)), s, desc, groups, first, K.okv, K.keys, (u32)K.n_keys, io.d_key,
+                               io.d_pts, w.rA, w.rB, (u32)n, gpts, d_accept, gex, wsum, susp, cval);
+    else if (K.ts)
         lcbk_ts_rlc_sum(dim3(nblk(groups)), s, desc, groups, first, K.okv, K.keys, (u32)K.n_keys, io.d_key, io.d_pts,
                         w.rA, w.rB, (u32)n, gpts, d_accept, gex, wsum, susp, cval);
     else
@@ -1295,15 +1300,19 @@ void *search2b_dump(hipStream_t s, const char *stage, u32 ns, u32 no, const u32 
 enum RlcStage { RLC_RESOLVE = 0, RLC_SEARCH = 1, RLC_COPY = 2 };   // after a chunk's checks: resolve / search / copy out
 void rlc_checks(lcb_ctx *c, const RlcKindInfo &K, RlcWs &w, const uint8_t *desc, u32 count, void *gpts, uint8_t *gacc,
                 u32 *f, RlcStage stage, bool first, uint8_t *gex, uint4 *sdesc, u32 *gamma, uint8_t *d_accept,
-                RlcIo io, hipStream_t s, const u32 *copy_map = nullptr) {
+                RlcIo io, hipStream_t s, const u32 *copy_map = nullptr, bool census = false) {
     hipEvent_t *ev = c->rlc_lev_ev;
+    const bool tsc = census && K.ts;      // the CommonCoin census: the 256-register copies (k_prep.hip)
     float t;
     for (size_t o = 0; o < count; o += LCB_VERIFY_CHUNK) {
         const size_t m = count - o < LCB_VERIFY_CHUNK ? count - o : LCB_VERIFY_CHUNK;
         hipEventRecord(ev[1], s);
         // small levels (below one wave per SIMD as one check per lane): nine lanes per check (k_coop.hip)
         const bool coop = m <= g_coop_max.load(), coop_ml = m <= g_coop_miller_max.load();
-        if (K.ts)
+        if (tsc)
+            lcbk_ts_rlc_miller_census(dim3(nblk(m)), s, K.lines, desc + 16 * o, (const uint8_t *)gpts + K.rec * o,
+                                      (u32)m, f, gacc + o);
+        else if (K.ts)
             lcbk_ts_rlc_miller(dim3(nblk(m)), s, K.lines, desc + 16 * o, (const uint8_t *)gpts + K.rec * o, (u32)m, f,
                                gacc + o);
         else if (coop_ml)
@@ -1313,7 +1322,9 @@ void rlc_checks(lcb_ctx *c, const RlcKindInfo &K, RlcWs &w, const uint8_t *desc,
             lcbk_tpke_rlc_miller(dim3(nblk(m)), s, K.lines, desc + 16 * o, (const uint8_t *)gpts + K.rec * o, (u32)m, f,
                                  gacc + o);
         hipEventRecord(ev[2], s);
-        if (coop) lcbk_coop_final_exp_check(s, f, (u32)m, gacc + o);
+        static const bool fe2w = env_on("LCB_ALLOW_TUNING") && env_on("LCB_COOP_FE_2W");   // A/B: every level
+        if (coop && (tsc || fe2w)) lcbk_coop_final_exp_check_census(s, f, (u32)m, gacc + o);
+        else if (coop) lcbk_coop_final_exp_check(s, f, (u32)m, gacc + o);
         else lcbk_final_exp_check(dim3(nblk(m)), s, f, (u32)m, gacc + o);
         hipEventRecord(ev[3], s);
         if (stage == RLC_COPY)
@@ -1346,8 +1357,9 @@ int rlc_census(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, RlcIo io, 
     lcbk_rlc_census_desc(s, io.d_grp, io.d_key, m, (u32)K.n_grp, (u32)K.n_keys, w.dB, d_accept);
     RlcWs cw = w;
     cw.susp = nullptr;                  // the census singles are exact checks whatever the bitmap says
-    rlc_sum_enqueue(K, cw, w.dB, m, false, d_accept, m, io, gpts, gex, nullptr, cval, s);
-    rlc_checks(c, K, cw, w.dB, m, gpts, gacc, f, RLC_RESOLVE, false, gex, nullptr, nullptr, d_accept, io, s);
+    rlc_sum_enqueue(K, cw, w.dB, m, false, d_accept, m, io, gpts, gex, nullptr, cval, s, true);
+    rlc_checks(c, K, cw, w.dB, m, gpts, gacc, f, RLC_RESOLVE, false, gex, nullptr, nullptr, d_accept, io, s, nullptr,
+               true);
     lcbk_rlc_census_stats(s, io.d_key, m, (u32)K.n_keys, cval, d_accept, w.susp, w.cnt + 3);
     return launched("batched verify census launch") ? 0 : -1;
 }
@@ -1713,15 +1725,20 @@ int ts_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const ui
         hipEventRecord(c->fork_ev[0], s);
         hipStreamWaitEvent(hp ? sp : sr, c->fork_ev[0], 0);
         if (hp) hipEventRecord(c->prep_ev[0], sp);
-        if (ts_rlc_points_enqueue(c, w, d_accept, n, n_pks, n_msgs, d_sigs, d_midx, d_pidx, sr)) return -1;
-        if (!hp) hipEventRecord(c->fork_ev[1], sr);
     } else if (hp) {
         hipEventRecord(c->fork_ev[0], s);
         hipStreamWaitEvent(sp, c->fork_ev[0], 0);
         hipEventRecord(c->prep_ev[0], sp);
     }
+    // the message preparation (latency-bound, one lane per message) is enqueued ahead of the randomisation, so its
+    // waves take their SIMD slots before the randomisation's fill the device (round 5: enqueued after it, the
+    // preparation ran 462 ms beside a 447 ms randomisation and the census chain waited for it)
     if (n_msgs) lcbk_ts_msg_prepare(dim3(nblk(n_msgs)), sp, d_msg, d_moff, (u32)n_msgs, lines, mok,
                                     g_orig_cofactor | (g_line_mode << 1));
+    if (n) {
+        if (ts_rlc_points_enqueue(c, w, d_accept, n, n_pks, n_msgs, d_sigs, d_midx, d_pidx, sr)) return -1;
+        if (!hp) hipEventRecord(c->fork_ev[1], sr);
+    }
     if (!launched("ts prepare launch")) return -1;
     c->s_n_msgs = n_msgs;
     c->s_n_pks = n_pks;

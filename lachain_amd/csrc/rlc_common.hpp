@@ -176,6 +176,14 @@ DI void g2_to_st(g2a_st &o, const g2 &p) {
     o.x = a.x;
     o.y = a.y;
 }
+DI void g2_to_st_gcd(g2a_st &o, const g2 &p) {      // (curve.hpp g2_jac_to_aff_g: the binary-GCD inversion)
+    g2a a;
+    g2_jac_to_aff_g(a, p);
+    o.ok = 1; o.pad[0] = o.pad[1] = 0;
+    o.inf = a.inf;
+    o.x = a.x;
+    o.y = a.y;
+}
 DI void g1_inf_st(g1a_st &o) { o.ok = 1; o.pad[0] = o.pad[1] = 0; o.inf = 1; o.x = fp_zero(); o.y = fp_zero(); }
 DI void g2_inf_st(g2a_st &o) { o.ok = 1; o.pad[0] = o.pad[1] = 0; o.inf = 1; o.x = fp2_zero(); o.y = fp2_zero(); }
 

@@ -104,7 +104,10 @@ class PublicKey:
         return EncryptedShare(u, v, w, raw_share.Id)
 
     def VerifyShare(self, share: EncryptedShare, ps: PartiallyDecryptedShare) -> bool:
-        return native.tpke_verify_shares([self._y], [(share.U, share.V, share.W)], [(0, 0, ps.Ui)])[0]
+        # the reference calls this once per (ciphertext, validator) (HoneyBadger.cs:211-212): the thread context's
+        # prepared-ciphertext and key caches (lcb_tpke_verify_shares_cached) keep H(U, V), the line sets and Y_i
+        # across the N calls of one ciphertext; the decision is the same exact check
+        return native.tpke_verify_shares([self._y], [(share.U, share.V, share.W)], [(0, 0, ps.Ui)], cached=True)[0]
 
     @staticmethod
     def VerifyShares(verification_keys, shares, partials):

@@ -18,7 +18,10 @@ SO = os.path.join(ROOT, "lachain_amd", "liblachain_bls.so")
 BUDGET = {
     "k_lineset_coop_2w": (270, 1080),         # k_prep.hip: the fused census's line sets at 256 registers
     "k_coop_debug": (204, 7620),              # test hook: the one-lane reference routines beside the coop ones
-    "k_coop_final_exp_check": (36, 576),     # round 5: three quads saved around the one binary-GCD call per check
+    "k_coop_final_exp_check": (36, 576),
+    "k_coop_final_exp_check_census": (36, 576),   # k_prep.hip: the CommonCoin census copies at 256 registers
+    "k_ts_rlc_sum_census": (34, 2248),
+    "k_ts_rlc_miller_census": (2, 4180),     # round 5: three quads saved around the one binary-GCD call per check
     "k_coop_tpke_miller": (0, 0),
     "k_dkg_exact_combine": (0, 312),
     "k_dkg_exact_terms": (0, 408),
@@ -58,7 +61,7 @@ BUDGET = {
     "k_ptmul_g2": (32, 68),                   # mcl G2 multiplication latency kernel: four ladder lanes share each op
     "k_rlc_key_tables": (12, 168),            # k_rlc_rand.hip: spills to scratch, not AGPRs (<= 256 registers)
     "k_rlc_miller_fallback": (0, 2376),
-    "k_rlc_search": (93, 2264),
+    "k_rlc_search": (106, 4056),              # round 5: baby-step giant-step (fingerprint table + the confirming power)
     "k_secp_scalars": (0, 528),
     "k_tpke_ct_prepare": (0, 3800),
     "k_tpke_ct_prepare_h": (5, 4824),
@@ -77,11 +80,11 @@ BUDGET = {
     "k_tpke_rlc_wsum": (0, 576),
     "k_tpke_rlc_wsum2": (0, 648),
     "k_ts_miller": (1248, 3292),
-    "k_ts_msg_prepare": (0, 3688),
+    "k_ts_msg_prepare": (5, 4824),            # round 5: k_prep.hip at 256 registers (was 346, 0 spills, 3,688 B)
     "k_ts_rlc_miller": (0, 2524),
     "k_ts_rlc_points": (677, 3360),           # k_rlc_rand.hip: 256 registers, two waves per SIMD (spills to scratch)
-    "k_ts_rlc_sum": (0, 2136),
-    "k_ts_rlc_wsum": (12, 992),
+    "k_ts_rlc_sum": (26, 2136),               # round 5: binary-GCD affine conversions (spills around the two calls)
+    "k_ts_rlc_wsum": (96, 992),               # round 5: binary-GCD affine conversions
     "k_ts_sign": (0, 3976),
 }
 # Round 5: no kernel that runs on more than one wave may take more than 4 KB of scratch per lane — the
@@ -91,7 +94,8 @@ SCRATCH_CAP = 4096
 SINGLE_WAVE = {"k_op_grp", "k_op_pair", "k_op_gt", "k_op_debug", "k_coop_debug"}
 # one lane per ciphertext (748 waves for configs[1]'s 1M shares: a 222 MB reservation at 4.6 KB per lane), at 256
 # registers so a wave shares its SIMD with a randomisation wave (k_prep.hip)
-PER_CIPHERTEXT = {"k_tpke_ct_prepare_h": 4900}
+PER_CIPHERTEXT = {"k_tpke_ct_prepare_h": 4900, "k_ts_msg_prepare": 4900,   # (the same hash lane, one per message)
+                  "k_ts_rlc_miller_census": 4200}   # the census's <= 1,024 lanes (16 waves: a 4.3 MB reservation)
 ZERO_SPILL = ["k_coop_tpke_miller", "k_msm_bucket_acc", "k_secp_verify",
               "k_rlc_census_stats", "k_rlc_suspect_split", "k_rlc_resolve", "k_tpke_rlc_sum", "k_ts_rlc_miller"]
 
