@@ -89,7 +89,9 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
 // the nine-lane final exponentiation) at 256 registers: k_ts_rlc_points holds two 256-register waves per SIMD for
 // ~450 ms, and the 294 / 360 / 284-register copies of k_batch.hip / k_coop.hip found no SIMD with room until it
 // retired, so the census ran after the randomisation, on the step's critical path (round-5 trace: 20 ms).  At 256 a
-// census wave takes the slot of the first randomisation wave that retires (its stream has the higher priority).
+// census wave takes the slot of the first randomisation wave that retires (its stream has the higher priority).  The
+// nine-lane final exponentiation's copy (248 registers, the same spills) serves every batched level (rlc_checks): with
+// three TPKE batches in flight its waves share SIMDs with the other batches' randomisation waves.
 extern "C" __global__ void LCB_PREP_BOUNDS k_ts_rlc_sum_census(const uint4 *desc, u32 n_groups, u32 first,
                                                               const uint8_t *msg_ok, const g1a_st *pks, u32 n_pks,
                                                               const u32 *pk_idx, const uint8_t *sigs, const u32 *rP,
@@ -100,6 +102,16 @@ extern "C" __global__ void LCB_PREP_BOUNDS k_ts_rlc_sum_census(const uint4 *desc
     ts_rlc_sum_run(desc, n_groups, first, msg_ok, pks, n_pks, pk_idx, sigs, rP, rS, n, gpts, accept, gexact, wsum, susp,
                    cval);
 }
+// the CommonCoin group sums of every level with two lanes per group (ts_rlc.hpp ts_rlc_sum2_run)
+extern "C" __global__ void LCB_PREP_BOUNDS k_ts_rlc_sum2(const uint4 *desc, u32 n_groups, u32 first,
+                                                        const uint8_t *msg_ok, const g1a_st *pks, u32 n_pks,
+                                                        const u32 *pk_idx, const uint8_t *sigs, const u32 *rP,
+                                                        const u32 *rS, u32 n, ts_grp *gpts, uint8_t *accept,
+                                                        uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval) {
+    LCB_LATENCY_PRIO();
+    ts_rlc_sum2_run(desc, n_groups, first, msg_ok, pks, n_pks, pk_idx, sigs, rP, rS, n, gpts, accept, gexact, wsum, susp,
+                    cval);
+}
 extern "C" __global__ void LCB_PREP_BOUNDS k_ts_rlc_miller_census(const u32 *lines, const uint4 *desc,
                                                                  const ts_grp *gpts, u32 n_groups, u32 *f_soa,
                                                                  uint8_t *gacc) {
@@ -107,7 +119,7 @@ extern "C" __global__ void LCB_PREP_BOUNDS k_ts_rlc_miller_census(const u32 *lin
     ts_rlc_miller_run(lines, desc, gpts, n_groups, f_soa, gacc);
 }
 extern "C" __global__ void __launch_bounds__(CP_BLOCK) __attribute__((amdgpu_waves_per_eu(2)))
-k_coop_final_exp_check_census(u32 *park, u32 n, uint8_t *accept) {
+k_coop_final_exp_check_2w(u32 *park, u32 n, uint8_t *accept) {
     LCB_LATENCY_PRIO();
     __shared__ uint4 lds[CP_LDS_QUADS];
     cp_final_exp_check_run(lds, park, n, accept);
@@ -121,13 +133,21 @@ extern "C" void lcbk_ts_rlc_sum_census(dim3 grid, hipStream_t s, const void *des
     LCB_LAUNCH(k_ts_rlc_sum_census, (const uint4 *)desc, n_groups, first, msg_ok, (const g1a_st *)pks, n_pks, pk_idx,
                sigs, rP, rS, n, (ts_grp *)gpts, accept, gexact, wsum, susp, cval);
 }
+extern "C" void lcbk_ts_rlc_sum2(hipStream_t s, const void *desc, u32 n_groups, u32 first, const uint8_t *msg_ok,
+                                 const void *pks, u32 n_pks, const u32 *pk_idx, const uint8_t *sigs, const u32 *rP,
+                                 const u32 *rS, u32 n, void *gpts, uint8_t *accept, uint8_t *gexact, u32 *wsum,
+                                 const u32 *susp, uint8_t *cval) {
+    dim3 grid((2 * (size_t)n_groups + LCB_BLOCK - 1) / LCB_BLOCK);
+    LCB_LAUNCH(k_ts_rlc_sum2, (const uint4 *)desc, n_groups, first, msg_ok, (const g1a_st *)pks, n_pks, pk_idx, sigs,
+               rP, rS, n, (ts_grp *)gpts, accept, gexact, wsum, susp, cval);
+}
 extern "C" void lcbk_ts_rlc_miller_census(dim3 grid, hipStream_t s, const u32 *lines, const void *desc,
                                           const void *gpts, u32 n_groups, u32 *f_soa, uint8_t *gacc) {
     LCB_LAUNCH(k_ts_rlc_miller_census, lines, (const uint4 *)desc, (const ts_grp *)gpts, n_groups, f_soa, gacc);
 }
-extern "C" void lcbk_coop_final_exp_check_census(hipStream_t s, u32 *park, u32 n, uint8_t *accept) {
+extern "C" void lcbk_coop_final_exp_check_2w(hipStream_t s, u32 *park, u32 n, uint8_t *accept) {
     dim3 grid((n + CP_G - 1) / CP_G);
-    hipLaunchKernelGGL(k_coop_final_exp_check_census, grid, dim3(CP_BLOCK), 0, s, park, n, accept);
+    hipLaunchKernelGGL(k_coop_final_exp_check_2w, grid, dim3(CP_BLOCK), 0, s, park, n, accept);
 }
 extern "C" void lcbk_lineset_coop_2w(hipStream_t s, u32 *lines, u32 n_sets, const u32 *sets, uint8_t *w_g2) {
     if (!n_sets) return;

@@ -1235,6 +1235,12 @@ RlcKindInfo rlc_kind(lcb_ctx *c, RlcKind kind) {
     return k;
 }
 // the group sums / singles of a level's desc list -> gpts (k_*_rlc_sum)
+// the CommonCoin level sums on two lanes per group (1) or one (0: k_batch.hip); LCB_TS_SUM2 (with LCB_ALLOW_TUNING=1)
+// overrides it for A/B runs
+std::atomic<int> g_ts_sum2{[] {
+    const char *e = getenv("LCB_TS_SUM2");
+    return (e && env_on("LCB_ALLOW_TUNING")) ? atoi(e) : 1;
+}()};
 // (census: the CommonCoin census's 256-register copies, k_prep.hip)
 void rlc_sum_enqueue(const RlcKindInfo &K, RlcWs &w, const uint8_t *desc, u32 groups, bool first, uint8_t *d_accept,
                      size_t n, RlcIo io, void *gpts, uint8_t *gex, u32 *wsum, uint8_t *cval, hipStream_t s,
@@ -1243,6 +1249,9 @@ void rlc_sum_enqueue(const RlcKindInfo &K, RlcWs &w, const uint8_t *desc, u32 gr
     if (K.ts && census)
         lcbk_ts_rlc_sum_census(dim3(nblk(groups)), s, desc, groups, first, K.okv, K.keys, (u32)K.n_keys, io.d_key,
                                io.d_pts, w.rA, w.rB, (u32)n, gpts, d_accept, gex, wsum, susp, cval);
+    else if (K.ts && g_ts_sum2.load())          // two lanes per group (k_prep.hip)
+        lcbk_ts_rlc_sum2(s, desc, groups, first, K.okv, K.keys, (u32)K.n_keys, io.d_key, io.d_pts, w.rA, w.rB, (u32)n,
+                         gpts, d_accept, gex, wsum, susp, cval);
     else if (K.ts)
         lcbk_ts_rlc_sum(dim3(nblk(groups)), s, desc, groups, first, K.okv, K.keys, (u32)K.n_keys, io.d_key, io.d_pts,
                         w.rA, w.rB, (u32)n, gpts, d_accept, gex, wsum, susp, cval);
@@ -1322,9 +1331,9 @@ void rlc_checks(lcb_ctx *c, const RlcKindInfo &K, RlcWs &w, const uint8_t *desc,
             lcbk_tpke_rlc_miller(dim3(nblk(m)), s, K.lines, desc + 16 * o, (const uint8_t *)gpts + K.rec * o, (u32)m, f,
                                  gacc + o);
         hipEventRecord(ev[2], s);
-        static const bool fe2w = env_on("LCB_ALLOW_TUNING") && env_on("LCB_COOP_FE_2W");   // A/B: every level
-        if (coop && (tsc || fe2w)) lcbk_coop_final_exp_check_census(s, f, (u32)m, gacc + o);
-        else if (coop) lcbk_coop_final_exp_check(s, f, (u32)m, gacc + o);
+        // the nine-lane final exponentiation at 248 registers (k_prep.hip): it shares a SIMD with a randomisation wave
+        // of the batches in flight (three TPKE batches: 15.50-15.78 vs 15.26-15.46 M/s, profiles/r05/abfe2w)
+        if (coop) lcbk_coop_final_exp_check_2w(s, f, (u32)m, gacc + o);
         else lcbk_final_exp_check(dim3(nblk(m)), s, f, (u32)m, gacc + o);
         hipEventRecord(ev[3], s);
         if (stage == RLC_COPY)

@@ -67,6 +67,96 @@ DI void ts_rlc_sum_run(const uint4 *desc, u32 n_groups, u32 first, const uint8_t
     g2_to_st_gcd(o.s, ss);
     gpts[g] = o;
 }
+// The same sums with TWO lanes per group (k_prep.hip k_ts_rlc_sum2, 256 registers: the 2,048 waves of configs[2]'s
+// level 1 run two per SIMD where one lane per group left one 294-register wave per SIMD issue-starved).  Lane h sums
+// shares [a_h, b_h) (a_0 = 0, a_1 = L = ceil(len / 2)) into sp_h, ss_h and the locally weighted wp_h = sum (j - a_h + 1)
+// P_j; lane 1 adds L sp_1 (so its weights become the global j + 1), the pair exchanges its four partial sums by
+// shuffles and both lanes add them; lane 0 converts and stores the G1 side, lane 1 the G2 side.  The group law makes
+// the affine records the same field elements as the one-lane sums' (the Jacobian wsum rows are converted before use).
+template <class J> DI void jac_shfl_pair(J &r, const J &x) {      // r = partner lane's x (lanes 2g, 2g + 1)
+    u32 *rw = (u32 *)&r;
+    const u32 *xw = (const u32 *)&x;
+#pragma unroll
+    for (int q = 0; q < (int)(sizeof(J) / 4); q++) rw[q] = (u32)__shfl_xor((int)xw[q], 1);
+}
+DI void ts_rlc_sum2_run(const uint4 *desc, u32 n_groups, u32 first, const uint8_t *msg_ok, const g1a_st *pks,
+                        u32 n_pks, const u32 *pk_idx, const uint8_t *sigs, const u32 *rP, const u32 *rS, u32 n,
+                        ts_grp *gpts, uint8_t *accept, uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval) {
+    const u32 t = blockIdx.x * blockDim.x + threadIdx.x, g = t >> 1, h = t & 1;
+    if (g >= n_groups) return;                         // (both lanes of a pair)
+    const uint4 dsc = desc[g];
+    if (dsc.w == 1 || !msg_ok[dsc.z]) {                // an exact single / an undecodable message: lane 0 alone
+        if (h) return;
+        ts_grp o;
+        g1_inf_st(o.p);
+        g2_inf_st(o.s);
+        gexact[g] = 0;
+        if (dsc.w == 1) {
+            u32 k = pk_idx[dsc.x];
+            bool live = accept[dsc.x] && msg_ok[dsc.z] && k < n_pks;
+            if (live) {
+                g2a S;
+                live = pks[k].ok && g2_decompress(S, sigs + 96 * (size_t)dsc.x);
+                if (live) {
+                    o.p = pks[k];
+                    o.s.x = S.x; o.s.y = S.y; o.s.inf = S.inf;
+                }
+            }
+            if (!live) accept[dsc.x] = 0;
+            if (cval) cval[dsc.x] = live;
+        } else {
+            for (u32 j = 0; j < dsc.y; j++) accept[dsc.x + j] = 0;
+        }
+        gpts[g] = o;
+        return;
+    }
+    const u32 L = (dsc.y + 1) >> 1, a = h ? L : 0, b = h ? dsc.y : L;
+    g1 sp, t1, wp;
+    g2 ss, u, ws;
+    jac_set_inf(sp);
+    jac_set_inf(wp);
+    jac_set_inf(ss);
+    jac_set_inf(ws);
+    for (u32 j = b; j-- > a;) {
+        if (!key_suspect(susp, pk_idx[dsc.x + j], n_pks)) {
+            g1_load_soa(t1, rP, n, dsc.x + j);
+            grp_add(sp, sp, t1);
+            g2_load_soa(u, rS, n, dsc.x + j);
+            grp_add(ss, ss, u);
+        }
+        if (first) {
+            grp_add(wp, wp, sp);
+            grp_add(ws, ws, ss);
+        }
+    }
+    if (first && h) {                                  // weights j - L + 1 -> j + 1
+        jac_mul_u64(t1, sp, L);
+        grp_add(wp, wp, t1);
+        jac_mul_u64(u, ss, L);
+        grp_add(ws, ws, u);
+    }
+    jac_shfl_pair(t1, sp);
+    grp_add(sp, sp, t1);
+    jac_shfl_pair(u, ss);
+    grp_add(ss, ss, u);
+    if (first) {
+        jac_shfl_pair(t1, wp);
+        jac_shfl_pair(u, ws);
+        if (h) {
+            grp_add(ws, ws, u);
+            g2_store_soa(wsum + (size_t)36 * n_groups, n_groups, g, ws);
+        } else {
+            grp_add(wp, wp, t1);
+            g1_store_soa(wsum, n_groups, g, wp);
+        }
+    }
+    if (h) {
+        g2_to_st_gcd(gpts[g].s, ss);
+    } else {
+        gexact[g] = 0;
+        g1_to_st_gcd(gpts[g].p, sp, false);
+    }
+}
 // miller2_ts (k_ts.hip): the message's line set with sum s_i PK_i, the group signature's lines on the fly with -G
 DN void miller2_ts_grp(fp12 &f, const u32 *lsH, const g1a &PK, const g2a &S, const g1a &G) {
     g2a Q;

@@ -19,7 +19,8 @@ BUDGET = {
     "k_lineset_coop_2w": (270, 1080),         # k_prep.hip: the fused census's line sets at 256 registers
     "k_coop_debug": (204, 7620),              # test hook: the one-lane reference routines beside the coop ones
     "k_coop_final_exp_check": (36, 576),
-    "k_coop_final_exp_check_census": (36, 576),   # k_prep.hip: the CommonCoin census copies at 256 registers
+    "k_coop_final_exp_check_2w": (36, 576),   # k_prep.hip: 248 registers (every batched level); census copies at 256
+    "k_ts_rlc_sum2": (20, 2376),              # k_prep.hip: two lanes per group
     "k_ts_rlc_sum_census": (34, 2248),
     "k_ts_rlc_miller_census": (2, 4180),     # round 5: three quads saved around the one binary-GCD call per check
     "k_coop_tpke_miller": (0, 0),
