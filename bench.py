@@ -1609,9 +1609,9 @@ def run_tpke_batched(args, nat, torch, dev, world, inp, d_acc, dd, n, n_cts, n_d
         value=float(t[2]) * args.steps / elapsed, unit="share verifications/s", steps=args.steps,
         ms_per_step=1e3 * elapsed / args.steps, decision_mismatches=int(t[1]),
         algorithm=("per ciphertext group: e(sum s_i U_i, H) == e(sum s_i Y_i, W), secret s_i = a_i + b_i lambda "
-                   "(32-bit a_i, b_i from ChaCha20 keyed by getrandom per call: 2^64 exponents); failed groups split "
-                   "~sqrt(len) ways, groups <= 8 into single shares; every rejection exact, false accept <= 2^-64 "
-                   "per group"),
+                   "(32-bit a_i, b_i from ChaCha20 keyed by getrandom per call: 2^64 exponents); failed groups "
+                   "located (one or two errors: a false location <= len^2 2^-64 per group) or checked singly; "
+                   "other rejections exact, false accept <= 2^-64 per group"),
         api="lcb_ctx_tpke_verify_shares_batched_dev (prepare + verify, randomisation on a second stream)",
         concurrent_parts=K,
         levels=levels, group_checks_per_share=checks / n,
@@ -1675,9 +1675,11 @@ def run_tpke_pipelined(args, nat, torch, dev, world, inp, dd, n, n_cts, n_dec, P
         for _ in range(max(1, args.warmup)):
             one(ln)
     torch.cuda.synchronize(dev)
-    t_one = time.perf_counter()
-    one(lanes[0])
-    t_one = time.perf_counter() - t_one
+    t_one = float("inf")                  # one batch alone, the least of three calls (host wall clock)
+    for _ in range(3):
+        t0 = time.perf_counter()
+        one(lanes[0])
+        t_one = min(t_one, time.perf_counter() - t0)
     mism = sum(int(np.sum(ln["acc"].cpu().numpy() != inp["expect"])) for ln in lanes)
     for ln in lanes:
         ln["acc"].fill_(7)
