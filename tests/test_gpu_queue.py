@@ -127,3 +127,40 @@ def test_queue_prepare_ahead(nat, items):
             t.join(timeout=100)
         assert not any(t.is_alive() for t in th)
     assert not errors, errors[:5]
+
+
+@pytest.mark.parametrize("workers", ["1", "4"])
+def test_queue_worker_counts(nat, items, workers, monkeypatch):
+    """LCB_QUEUE_WORKERS (read when the queue is created): one worker (every flush serial) and four (flushes side by
+    side, two of the workers' streams sharing a hardware queue at the default GPU_MAX_HW_QUEUES) give the same decisions,
+    with ciphertexts prepared ahead on every worker and some not"""
+    monkeypatch.setenv("LCB_QUEUE_WORKERS", workers)
+    errors = []
+    cts = []
+    for kind, args, _ in items:
+        if kind == "tpke" and (args[1], args[2], args[3]) not in cts:
+            cts.append((args[1], args[2], args[3]))
+    with nat.BatchQueue(max_batch=16, max_delay_ms=1.0) as q:
+        for u, v, w in cts[::2]:                        # half prepared ahead, half met first in a flush
+            q.prepare_tpke(u, v, w)
+
+        def worker(k):
+            try:
+                for rep in range(2):
+                    for idx in range(k, len(items), 8):
+                        kind, args, expect = items[idx]
+                        got = q.verify_tpke(*args) if kind == "tpke" else q.verify_ts(*args)
+                        if got != expect:
+                            errors.append((k, rep, idx, got, expect))
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e))
+        th = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=100)
+        assert not any(t.is_alive() for t in th)
+        st = q.stats()
+    assert not errors, errors[:5]
+    assert st["shares"] == 2 * len(items)
+
