@@ -7,9 +7,12 @@ LCB_TU_CONFIG(k_lagrange)
 
 // ================================================================================= Lagrange at 0
 // lambda_i = prod_{j != i} x_j / (x_j - x_i) (mcl: a = prod x_j, b_i = x_i prod_{j!=i}(x_j - x_i),
-// lambda_i = a / b_i); one lane per problem; writes canonical raw lambdas and a status byte.
+// lambda_i = a / b_i); one lane per problem; writes canonical raw lambdas and a status byte.  Every x is used as its
+// raw integer read as a Montgomery representation (the value x R^-1): a and every b_i are products of k such factors,
+// so both carry R^-k and lambda_i = a / b_i is exact without converting any x (round 5: the conversions were one
+// product per (i, j) pair).  The batch inversion keeps its prefix products in pre (one slot per entry).
 extern "C" __global__ void LCB_BOUNDS k_lagrange_coeffs(const uint8_t *xs, const u32 *off, u32 n_problems,
-                                                       fr *lam_raw, uint8_t *status) {
+                                                       fr *lam_raw, fr *pre, uint8_t *status) {
     u32 j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n_problems) return;
     u32 o0 = off[j], k = off[j + 1] - o0;
@@ -17,49 +20,41 @@ extern "C" __global__ void LCB_BOUNDS k_lagrange_coeffs(const uint8_t *xs, const
     // a = prod x
     fr a = fr_one();
     for (u32 i = 0; i < k && ok; i++) {
-        fr xr, x;
+        fr xr;
         const u32 *w = (const u32 *)(xs + 32 * (size_t)(o0 + i));
         for (int q = 0; q < 8; q++) xr.v[q] = w[q];
         if (!fr_raw_lt_r(xr) || fr_is_zero(xr)) { ok = false; break; }
-        fr_from_raw(x, xr);
-        fr_mul(a, a, x);
+        fr_mul(a, a, xr);
     }
-    // b_i and prefix products for one batch inversion (stored in lam_raw as scratch)
+    // b_i, and the prefix products b_0 .. b_(i-1) for one batch inversion
     fr acc = fr_one();
     for (u32 i = 0; i < k && ok; i++) {
-        fr xi_r, xi;
+        fr xi;
         const u32 *w = (const u32 *)(xs + 32 * (size_t)(o0 + i));
-        for (int q = 0; q < 8; q++) xi_r.v[q] = w[q];
-        fr_from_raw(xi, xi_r);
+        for (int q = 0; q < 8; q++) xi.v[q] = w[q];
         fr b = xi;
         for (u32 t = 0; t < k; t++) {
             if (t == i) continue;
-            fr xt_r, xt, d;
+            fr xt, d;
             const u32 *wt = (const u32 *)(xs + 32 * (size_t)(o0 + t));
-            for (int q = 0; q < 8; q++) xt_r.v[q] = wt[q];
-            fr_from_raw(xt, xt_r);
+            for (int q = 0; q < 8; q++) xt.v[q] = wt[q];
             fr_sub(d, xt, xi);
             if (fr_is_zero(d)) { ok = false; break; }
             fr_mul(b, b, d);
         }
         if (!ok) break;
-        lam_raw[o0 + i] = b;      // b_i (Montgomery) for now
+        lam_raw[o0 + i] = b;      // b_i for now
+        pre[o0 + i] = acc;        // b_0 .. b_(i-1)
+        fr_mul(acc, acc, b);
     }
     if (ok) {
-        // batch inversion of b_i: prefix products, one inversion, back-substitution
-        for (u32 i = 0; i < k; i++) {
-            fr b = lam_raw[o0 + i];
-            fr_mul(acc, acc, b);
-        }
         fr inv;
-        fr_inv(inv, acc);
+        fr_inv(inv, acc);         // 1 / (b_0 .. b_(k-1))
         for (u32 i = k; i-- > 0;) {
-            // inv = 1/(b_0..b_i); prefix up to i-1 recomputed (k is small: O(k^2) Fr muls overall)
-            fr pre = fr_one();
-            for (u32 t = 0; t < i; t++) fr_mul(pre, pre, lam_raw[o0 + t]);
+            const fr bi = lam_raw[o0 + i];
             fr bi_inv, l, lr;
-            fr_mul(bi_inv, inv, pre);
-            fr_mul(inv, inv, lam_raw[o0 + i]);
+            fr_mul(bi_inv, inv, pre[o0 + i]);   // 1 / b_i
+            fr_mul(inv, inv, bi);               // 1 / (b_0 .. b_(i-1))
             fr_mul(l, a, bi_inv);
             fr_to_raw(lr, l);
             lam_raw[o0 + i] = lr;
@@ -227,8 +222,8 @@ extern "C" __global__ void LCB_BOUNDS k_g2_sum(const g2 *parts, const uint8_t *o
 }
 
 // ---------------------------------------------------------------- host launch wrappers
-extern "C" void lcbk_lagrange_coeffs(dim3 grid, hipStream_t s, const uint8_t *xs, const u32 *off, u32 n_problems, void *lam_raw, uint8_t *status) {
-    LCB_LAUNCH(k_lagrange_coeffs, xs, off, n_problems, (fr *)lam_raw, status);
+extern "C" void lcbk_lagrange_coeffs(dim3 grid, hipStream_t s, const uint8_t *xs, const u32 *off, u32 n_problems, void *lam_raw, void *pre, uint8_t *status) {
+    LCB_LAUNCH(k_lagrange_coeffs, xs, off, n_problems, (fr *)lam_raw, (fr *)pre, status);
 }
 static u32 g_rb_g1, g_rb_g2, g_rb_g2p;
 static u32 lanes_blocks(int which, u32 n) {

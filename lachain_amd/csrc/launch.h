@@ -41,7 +41,7 @@ extern "C" void lcbk_g2_hash(dim3 grid, hipStream_t s, const uint8_t *msg_data, 
 extern "C" void lcbk_tpke_encrypt1(hipStream_t s, const uint8_t *ybytes, const uint8_t *rs, u32 n, uint8_t *u_out, uint8_t *t_out, uint8_t *ok_out, u32 *ws);
 extern "C" void lcbk_tpke_encrypt2(dim3 grid, hipStream_t s, const uint8_t *u, const uint8_t *rs, const uint8_t *v_data, const u32 *v_off, u32 n, uint8_t *w_out, uint8_t *ok_out, int orig_cof);
 extern "C" void lcbk_ts_sign(dim3 grid, hipStream_t s, const uint8_t *sks, const uint8_t *msg_data, const u32 *msg_off, const u32 *msg_idx, u32 n, uint8_t *out, uint8_t *ok_out, int orig_cof);
-extern "C" void lcbk_lagrange_coeffs(dim3 grid, hipStream_t s, const uint8_t *xs, const u32 *off, u32 n_problems, void *lam_raw, uint8_t *status);
+extern "C" void lcbk_lagrange_coeffs(dim3 grid, hipStream_t s, const uint8_t *xs, const u32 *off, u32 n_problems, void *lam_raw, void *pre, uint8_t *status);
 // Lagrange lanes (persistent grids, tables in the workspace `ws` of lcbk_lanes_ws_bytes: 1 = G1, 2 = G2, 3 = paired G2)
 extern "C" size_t lcbk_lanes_ws_bytes(int which, u32 n_entries);
 extern "C" void lcbk_g1_mul_lanes(hipStream_t s, const uint8_t *ys, const void *lam_raw, u32 n_entries, void *out, uint8_t *ok_out, u32 *ws);

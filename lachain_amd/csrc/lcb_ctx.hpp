@@ -65,7 +65,7 @@ struct lcb_ctx {
     uint64_t s_gen = 0;
     bool s_ready = false;
     // Lagrange / assembly / MSM / staging
-    DevBuf lag[4], sel[4], msm[15], in[8], out[4], dkg[9];
+    DevBuf lag[5], sel[4], msm[15], in[8], out[4], dkg[9];
     DevBuf lws;                       // lanetab.hpp workspaces of the persistent scalar-multiplication grids
     DevBuf mcl[8];                    // the mcl surface's pairing / multi-scalar / Horner / Lagrange staging
     // mclBn_pairing's cache of G2 line sets (mcl[2]: slot k = Q_k's set and the infinity set), least recently used

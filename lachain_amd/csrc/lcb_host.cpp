@@ -1773,10 +1773,11 @@ int lagrange_enqueue(lcb_ctx *c, int g, uint8_t *dout, uint8_t *dst, const uint8
                      bool pairs = false) {
     if (np > 0xffffffffu || ne > 0xffffffffu) { set_err("lagrange: batch too large"); return -1; }
     void *lam = c->lag[0].get(LCB_FR_BYTES * (ne ? ne : 1));
+    void *pre = c->lag[4].get(LCB_FR_BYTES * (ne ? ne : 1));      // the batch inversion's prefix products
     void *parts = c->lag[1].get((g == 1 ? LCB_G1_JAC_BYTES : LCB_G2_JAC_BYTES) * (ne ? ne : 1));
     uint8_t *pok = (uint8_t *)c->lag[2].get(ne ? ne : 1);
-    if (!lam || !parts || !pok) { set_err("device allocation failed"); return -1; }
-    lcbk_lagrange_coeffs(dim3(nblk(np)), s, dx, doff, (u32)np, lam, dst);
+    if (!lam || !pre || !parts || !pok) { set_err("device allocation failed"); return -1; }
+    lcbk_lagrange_coeffs(dim3(nblk(np)), s, dx, doff, (u32)np, lam, pre, dst);
     if (ne) {
         const int which = g == 1 ? 1 : pairs ? 3 : 2;   // pairs: even problem offsets (assembly with even k)
         u32 *ws = (u32 *)c->lag[3].get(lcbk_lanes_ws_bytes(which, (u32)ne));
