@@ -196,9 +196,10 @@ def test_concurrent_assemblies_two_threads(nat, tdev):
         try:
             ctx = nat.Context()
             st = torch.cuda.Stream(dev)
-            d_acc = torch.ones(rounds * per, dtype=torch.uint8, device=dev)
-            d_comb = torch.zeros(96 * rounds, dtype=torch.uint8, device=dev)
-            d_cst = torch.zeros(rounds, dtype=torch.uint8, device=dev)
+            with torch.cuda.stream(st):     # the fills are ordered before the library's kernels on st
+                d_acc = torch.ones(rounds * per, dtype=torch.uint8, device=dev)
+                d_comb = torch.zeros(96 * rounds, dtype=torch.uint8, device=dev)
+                d_cst = torch.zeros(rounds, dtype=torch.uint8, device=dev)
             for _ in range(3):
                 rc = lib.lcb_ctx_ts_assemble_dev(ctx.ptr, d_comb.data_ptr(), d_cst.data_ptr(), d_acc.data_ptr(),
                                                  d_sigs.data_ptr(), per, k, rounds, st.cuda_stream)
@@ -210,14 +211,21 @@ def test_concurrent_assemblies_two_threads(nat, tdev):
         except Exception as e:          # noqa: BLE001 — reported below
             errs.append(repr(e))
 
+    torch.cuda.synchronize(dev)             # the shared inputs, written on the default stream
     ths = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
     for th in ths:
         th.start()
     for th in ths:
         th.join()
     assert not errs, errs
+    import numpy as np
+    want = np.frombuffer(expect * tile, dtype=np.uint8).reshape(rounds, 96)
     for t in range(2):
         assert len(outs[t]) == 3
-        for comb, cst in outs[t]:
-            assert cst.tolist() == [1] * rounds
-            assert comb == expect * tile
+        for rep, (comb, cst) in enumerate(outs[t]):
+            bad_st = np.nonzero(cst != 1)[0]
+            got = np.frombuffer(comb, dtype=np.uint8).reshape(rounds, 96)
+            bad_sig = np.nonzero((got != want).any(axis=1))[0]
+            # (counts and first indices only: a list diff of 16,384 statuses outlives the test's time limit)
+            assert bad_st.size == 0 and bad_sig.size == 0, (t, rep, bad_st.size, bad_st[:16].tolist(),
+                                                           bad_sig.size, bad_sig[:16].tolist())
