@@ -8,7 +8,6 @@
 #include "lines_coop.hpp"
 #include "coop.hpp"
 #include "ts_rlc.hpp"
-#include "ct_prepare.hpp"
 
 LCB_ASM_LIBRARY(k_prep)
 LCB_TU_CONFIG(k_prep)
@@ -103,15 +102,6 @@ extern "C" __global__ void LCB_PREP_BOUNDS k_ts_rlc_sum_census(const uint4 *desc
     ts_rlc_sum_run(desc, n_groups, first, msg_ok, pks, n_pks, pk_idx, sigs, rP, rS, n, gpts, accept, gexact, wsum, susp,
                    cval);
 }
-// the batched check's census ciphertexts (decode + hash, ct_prepare.hpp) at 256 registers: the 346-register
-// k_tpke_ct_prepare found a SIMD only when both randomisation waves of one retired together, 11-13 ms in some steps
-// and 45-48 ms in others (round-5 trace), and the census chain behind it then held level 1 back
-extern "C" __global__ void LCB_PREP_BOUNDS k_tpke_ct_prepare_2w(const uint8_t *cts_u, const uint8_t *cts_w,
-                                                               const uint8_t *v_data, const u32 *v_off, u32 n_cts,
-                                                               u32 *lines, uint8_t *ct_ok, int flags, const u32 *slot) {
-    LCB_LATENCY_PRIO();
-    tpke_ct_prepare_run(cts_u, cts_w, v_data, v_off, n_cts, lines, ct_ok, flags, slot);
-}
 // the CommonCoin group sums of every level with two lanes per group (ts_rlc.hpp ts_rlc_sum2_run)
 extern "C" __global__ void LCB_PREP_BOUNDS k_ts_rlc_sum2(const uint4 *desc, u32 n_groups, u32 first,
                                                         const uint8_t *msg_ok, const g1a_st *pks, u32 n_pks,
@@ -142,11 +132,6 @@ extern "C" void lcbk_ts_rlc_sum_census(dim3 grid, hipStream_t s, const void *des
                                        uint8_t *accept, uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval) {
     LCB_LAUNCH(k_ts_rlc_sum_census, (const uint4 *)desc, n_groups, first, msg_ok, (const g1a_st *)pks, n_pks, pk_idx,
                sigs, rP, rS, n, (ts_grp *)gpts, accept, gexact, wsum, susp, cval);
-}
-extern "C" void lcbk_tpke_ct_prepare_2w(dim3 grid, hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w,
-                                        const uint8_t *v_data, const u32 *v_off, u32 n_cts, u32 *lines, uint8_t *ct_ok,
-                                        int orig_cof, const u32 *slot) {
-    LCB_LAUNCH(k_tpke_ct_prepare_2w, cts_u, cts_w, v_data, v_off, n_cts, lines, ct_ok, orig_cof, slot);
 }
 extern "C" void lcbk_ts_rlc_sum2(hipStream_t s, const void *desc, u32 n_groups, u32 first, const uint8_t *msg_ok,
                                  const void *pks, u32 n_pks, const u32 *pk_idx, const uint8_t *sigs, const u32 *rP,

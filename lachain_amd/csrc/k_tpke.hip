@@ -1,6 +1,5 @@
 // lachain_amd/csrc/k_tpke.hip — gfx950 kernels: TPKE decryption-share pipeline (decompression, per-ciphertext preparation, per-share verification, partial decryption).
 #include "kcommon.hpp"
-#include "ct_prepare.hpp"
 #include "fe_asm.hpp"
 
 LCB_ASM_LIBRARY(k_tpke)
@@ -33,8 +32,33 @@ extern "C" __global__ void LCB_BOUNDS k_g2_decompress(const uint8_t *in, u32 n, 
 extern "C" __global__ void LCB_BOUNDS k_tpke_ct_prepare(const uint8_t *cts_u, const uint8_t *cts_w,
                                                        const uint8_t *v_data, const u32 *v_off, u32 n_cts,
                                                        u32 *lines, uint8_t *ct_ok, int flags, const u32 *slot) {
+    // flags: bit 0 = mcl's original G2 cofactor clearing in hash-to-G2, bit 1 = mark the line sets un-normalised
     LCB_LATENCY_PRIO();
-    tpke_ct_prepare_run(cts_u, cts_w, v_data, v_off, n_cts, lines, ct_ok, flags, slot);
+    u32 c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_cts) return;
+    const u32 o = slot ? slot[c] : c;
+    const uint8_t *ub = cts_u + 48 * (size_t)c;
+    g1a U;
+    g2a W, Ha;
+    bool ok = g1_decompress(U, ub);
+    ok = g2_decompress(W, cts_w + 96 * (size_t)c) && ok;
+    // H = G2.SetHashOf(U.ToBytes() || V): for a valid U the wire bytes are its canonical encoding
+    uint8_t d[64];
+    u32 v0 = v_off[c], v1 = v_off[c + 1];
+    sha512_2(d, ub, 48, v_data + v0, v1 - v0);
+    g2 H;
+    bool hok = g2_hash_digest(H, d, (flags & 1) != 0);
+    ok = ok && hok;
+    if (hok) jac_to_aff(Ha, H);
+    else { Ha.inf = true; Ha.x = fp2_zero(); Ha.y = fp2_zero(); }
+    if (!ok) { W.inf = true; Ha.inf = true; }
+    // the two points go to their line sets' point slots; k_lineset_fill computes the 2 * n_cts line sets one lane
+    // each (the per-ciphertext serial path is hash + one line set instead of hash + two)
+    u32 *lsH = lines + (size_t)(2 * o) * LCB_LINESET_WORDS, *lsW = lines + (size_t)(2 * o + 1) * LCB_LINESET_WORDS;
+    lineset_put_point(lsH, Ha);
+    lineset_put_point(lsW, W);
+    lsH[LCB_LS_FLAG + 2] = lsW[LCB_LS_FLAG + 2] = (flags & 2) ? 1 : 0;
+    ct_ok[o] = ok;
 }
 
 extern "C" __global__ void LCB_BOUNDS k_ct_ok_merge(uint8_t *ct_ok, const uint8_t *h_ok, u32 c0, u32 n_cts) {

@@ -25,7 +25,6 @@ extern "C" void lcbk_final_exp_check(dim3 grid, hipStream_t s, u32 *park, u32 n,
 extern "C" void lcbk_tpke_pd_miller(hipStream_t s, const u32 *lines, const uint8_t *ct_ok, const uint8_t *cts_u, u32 c0, u32 m, u32 *f_soa, uint8_t *status);
 extern "C" void lcbk_tpke_pd_mul(hipStream_t s, const uint8_t *cts_u, const void *x_raw, u32 x_stride, u32 c0, u32 m, const uint8_t *status, uint8_t *ui_out);
 extern "C" void lcbk_ts_rlc_sum_census(dim3 grid, hipStream_t s, const void *desc, u32 n_groups, u32 first, const uint8_t *msg_ok, const void *pks, u32 n_pks, const u32 *pk_idx, const uint8_t *sigs, const u32 *rP, const u32 *rS, u32 n, void *gpts, uint8_t *accept, uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval);
-extern "C" void lcbk_tpke_ct_prepare_2w(dim3 grid, hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data, const u32 *v_off, u32 n_cts, u32 *lines, uint8_t *ct_ok, int orig_cof, const u32 *slot);
 extern "C" void lcbk_ts_rlc_sum2(hipStream_t s, const void *desc, u32 n_groups, u32 first, const uint8_t *msg_ok, const void *pks, u32 n_pks, const u32 *pk_idx, const uint8_t *sigs, const u32 *rP, const u32 *rS, u32 n, void *gpts, uint8_t *accept, uint8_t *gexact, u32 *wsum, const u32 *susp, uint8_t *cval);
 extern "C" void lcbk_ts_rlc_miller_census(dim3 grid, hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups, u32 *f_soa, uint8_t *gacc);
 extern "C" void lcbk_coop_final_exp_check_2w(hipStream_t s, u32 *park, u32 n, uint8_t *accept);

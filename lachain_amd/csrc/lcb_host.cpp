@@ -1602,7 +1602,7 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
         const u32 nc = (u32)n_cts, ce = c_early;
         c->unn_census = ce ? 0 : 1;
         if (ce) {                    // the census's ciphertexts: decode + hash per lane, then the five-lane line sets
-            lcbk_tpke_ct_prepare_2w(dim3(nblk(ce)), sp, d_u, d_w, d_v, d_voff, ce, lines, ctok, fl, nullptr);
+            lcbk_tpke_ct_prepare(dim3(nblk(ce)), sp, d_u, d_w, d_v, d_voff, ce, lines, ctok, fl, nullptr);
             lcbk_lineset_coop_2w(sp, lines, 2 * ce, nullptr, ctg2);   // (2 ce <= 8192 sets: lines_fill's coop range)
             lines_flag_enqueue(c, 0, lines, 0, ce, sp);
         }

@@ -65,7 +65,6 @@ BUDGET = {
     "k_rlc_search": (106, 4056),              # round 5: baby-step giant-step (fingerprint table + the confirming power)
     "k_secp_scalars": (0, 528),
     "k_tpke_ct_prepare": (0, 3800),
-    "k_tpke_ct_prepare_2w": (6, 4936),       # k_prep.hip: the census ciphertexts at 256 registers
     "k_tpke_ct_prepare_h": (5, 4824),
     "k_tpke_ct_prepare_w": (5, 1688),
     "k_tpke_encrypt1": (0, 1184),
@@ -97,8 +96,7 @@ SINGLE_WAVE = {"k_op_grp", "k_op_pair", "k_op_gt", "k_op_debug", "k_coop_debug"}
 # one lane per ciphertext (748 waves for configs[1]'s 1M shares: a 222 MB reservation at 4.6 KB per lane), at 256
 # registers so a wave shares its SIMD with a randomisation wave (k_prep.hip)
 PER_CIPHERTEXT = {"k_tpke_ct_prepare_h": 4900, "k_ts_msg_prepare": 4900,   # (the same hash lane, one per message)
-                  "k_ts_rlc_miller_census": 4200,   # the census's <= 1,024 lanes (16 waves: a 4.3 MB reservation)
-                  "k_tpke_ct_prepare_2w": 5000}     # the census ciphertexts (< 4,096 lanes: <= 20 MB reserved)
+                  "k_ts_rlc_miller_census": 4200}   # the census's <= 1,024 lanes (16 waves: a 4.3 MB reservation)
 ZERO_SPILL = ["k_coop_tpke_miller", "k_msm_bucket_acc", "k_secp_verify",
               "k_rlc_census_stats", "k_rlc_suspect_split", "k_rlc_resolve", "k_tpke_rlc_sum", "k_ts_rlc_miller"]
 
