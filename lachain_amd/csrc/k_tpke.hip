@@ -182,6 +182,13 @@ extern "C" void lcbk_g2_decompress(dim3 grid, hipStream_t s, const uint8_t *in, 
 extern "C" void lcbk_tpke_ct_prepare(dim3 grid, hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data, const u32 *v_off, u32 n_cts, u32 *lines, uint8_t *ct_ok, int orig_cof, const u32 *slot) {
     LCB_LAUNCH(k_tpke_ct_prepare, cts_u, cts_w, v_data, v_off, n_cts, lines, ct_ok, orig_cof, slot);
 }
+// the same kernel in one-wave workgroups, for the few census ciphertexts of the batched check: a wave at 346 registers
+// needs one SIMD with that many free, where a 256-lane workgroup needs four on one CU (round 5: behind the
+// randomisation's two waves per SIMD the census's single workgroup waited 34 ms for a whole CU in about half the steps)
+extern "C" void lcbk_tpke_ct_prepare_w64(hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data, const u32 *v_off, u32 n_cts, u32 *lines, uint8_t *ct_ok, int orig_cof) {
+    LCB_LAUNCH_GATED(k_tpke_ct_prepare, dim3((n_cts + 63) / 64), dim3(64), 0, s, cts_u, cts_w, v_data, v_off, n_cts,
+                     lines, ct_ok, orig_cof, (const u32 *)nullptr);
+}
 extern "C" void lcbk_ct_ok_merge(hipStream_t s, uint8_t *ct_ok, const uint8_t *h_ok, u32 c0, u32 c1) {
     dim3 grid((c1 - c0 + LCB_BLOCK - 1) / LCB_BLOCK);
     LCB_LAUNCH(k_ct_ok_merge, ct_ok, h_ok, c0, c1);

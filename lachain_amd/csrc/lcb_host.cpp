@@ -1568,6 +1568,17 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
         for (uint32_t x : ci) mx = std::max(mx, x);
         if ((size_t)mx + 1 < n_cts && mx < 4096u) c_early = mx + 1;
     }
+    const int fl = g_orig_cofactor | (g_line_mode << 1);
+    // the census ciphertexts' decode + hash needs no key: it starts before the keys' decompression and tables (≈ 2 ms
+    // on an otherwise idle device in a single batch), ordered after the context's earlier work like the caller's stream
+    // (c_early is set in split mode only, whose preparation stream is c->hi)
+    const bool early = c_early != 0;
+    if (early) {
+        hipEventRecord(c->fork_ev[4], s);
+        hipStreamWaitEvent(c->hi, c->fork_ev[4], 0);
+        hipEventRecord(c->prep_ev[0], c->hi);
+        lcbk_tpke_ct_prepare_w64(c->hi, d_u, d_w, d_v, d_voff, c_early, lines, ctok, fl);
+    }
     if (n_keys) lcbk_g1_decompress(dim3(nblk(n_keys)), s, d_y, (u32)n_keys, keys);
     RlcWs w;
     const RlcIo io{d_dec, d_ui, d_ct};
@@ -1580,7 +1591,7 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
         keys_first_tables(c, w, keys, n_keys, n, s);
         hipEventRecord(c->fork_ev[0], s);
         hipStreamWaitEvent(hp ? sp : sr, c->fork_ev[0], 0);
-        if (hp) hipEventRecord(c->prep_ev[0], sp);
+        if (hp && !early) hipEventRecord(c->prep_ev[0], sp);
         if (!prep_first && rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, sr)) return -1;
         if (!hp) hipEventRecord(c->fork_ev[1], sr);
     } else if (hp) {
@@ -1596,13 +1607,12 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
         // preparation stream), the rest [c_early, n_cts) beside them on the second and third streams.
         uint8_t *hok = (uint8_t *)c->rlc[18].get(n_cts);
         if (!hok) { set_err("device allocation failed"); return -1; }
-        const int fl = g_orig_cofactor | (g_line_mode << 1);
         hipStreamWaitEvent(c->hi2, c->fork_ev[0], 0);
         hipStreamWaitEvent(c->hi3, c->fork_ev[0], 0);
         const u32 nc = (u32)n_cts, ce = c_early;
         c->unn_census = ce ? 0 : 1;
-        if (ce) {                    // the census's ciphertexts: decode + hash per lane, then the five-lane line sets
-            lcbk_tpke_ct_prepare(dim3(nblk(ce)), sp, d_u, d_w, d_v, d_voff, ce, lines, ctok, fl, nullptr);
+        if (ce) {                    // the census's ciphertexts (decode + hash per lane launched above): their
+                                     // line sets on the five-lane kernel
             lcbk_lineset_coop_2w(sp, lines, 2 * ce, nullptr, ctg2);   // (2 ce <= 8192 sets: lines_fill's coop range)
             lines_flag_enqueue(c, 0, lines, 0, ce, sp);
         }
