@@ -8,10 +8,11 @@
 #include "kcommon.hpp"
 
 #define PT_LANES 4                 // lanes per group
+#define PT_TAB_MAX 8               // k_ptmul.hip's signed-digit table T[1..8]
 
 template <class F> struct PtLds {
     F prod[PT_LANES];
-    jac<F> tab[16];
+    jac<F> tab[PT_TAB_MAX + 1];
 };
 
 DI int pt_role() {

@@ -4,9 +4,10 @@
 //
 // A one-lane ladder is ~2,500-3,500 serial Fp products at ~1.1 us each (the issue time of one wave), whatever else
 // the GPU does.  Here one wave runs up to 16 LADDERS side by side, each on a GROUP of four lanes:
-//   * every group runs the SAME program — a 4-bit window table T[1..15] of its base point, then for each window four
-//     doublings and one addition of T[nibble] — on its own base point and digit string, so the wave never diverges
-//     between groups (a skipped addition for a zero nibble is the only data-dependent branch);
+//   * every group runs the SAME program — a signed 4-bit window table T[1..8] of its base point, then for each window
+//     four doublings and one addition of +-T[|digit|] (digits in [-7, 8]: 6 table additions instead of 13) — on its
+//     own base point and digit string, so the wave never diverges between groups (a skipped addition for a zero
+//     digit is the only data-dependent branch);
 //   * inside a group the four lanes share each point operation: every lane holds the group's values (X, Y, Z, the
 //     temporaries) and a ROUND is one Fp (G1) or Fp2 (G2) product per lane on operands it selects by its role, then the
 //     four products are exchanged through LDS.  dbl-2009-l takes 3 rounds instead of 7 serial products, add-2007-bl 5
@@ -21,9 +22,10 @@ LCB_ASM_LIBRARY(k_ptmul)
 LCB_TU_CONFIG(k_ptmul)
 
 #define PT_MAX_GROUPS 8               // G1 uses 3, G2 5 (LDS: 9 areas, 22 / 45 KB)
-#define PT_MAX_WIN 33              // 4-bit windows (129-bit GLV halves)
+#define PT_MAX_WIN 33              // signed 4-bit windows (129-bit GLV halves; 17 for the 64-bit GLS digits)
 
-// one group's job: affine base point (inf = 1: the point at infinity) and nwin nibbles, most significant first
+// one group's job: affine base point (inf = 1: the point at infinity) and nwin signed digits, most significant
+// first, one byte each: |digit| (<= 8) in bits 0-3, bit 7 set for a negative digit (lcb_host.cpp put_digits)
 template <class F> struct PtJob {
     F x, y;
     u32 inf, nwin, pad[2];
@@ -40,13 +42,13 @@ template <class F> DI void pt_ladder(const PtJob<F> *jobs, u32 n_groups, jac<F> 
     jac<F> P, acc;
     if (J.inf) jac_set_inf(P);
     else { P.x = J.x; P.y = J.y; f_one(P.z); }
-    // table T[1..15] = d P
+    // table T[1..8] = d P; a negative digit adds -T[|d|] = (X, -Y, Z)
     if (pt_role() == 0) L->tab[1] = P;
     jac<F> cur;
     pt_dbl(L, cur, P);
     if (pt_role() == 0) L->tab[2] = cur;
 #pragma unroll 1
-    for (int d = 3; d < 16; d++) {
+    for (int d = 3; d <= PT_TAB_MAX; d++) {
         pt_add(L, cur, cur, P);
         if (pt_role() == 0) L->tab[d] = cur;
     }
@@ -61,10 +63,11 @@ template <class F> DI void pt_ladder(const PtJob<F> *jobs, u32 n_groups, jac<F> 
             pt_dbl(L, acc, acc);
             pt_dbl(L, acc, acc);
         }
-        const u32 nib = J.nib[w];
-        if (__any(nib != 0)) {                       // wave-uniform; a group with a zero nibble adds infinity
-            jac<F> T = L->tab[nib ? nib : 1];
-            if (!nib) jac_set_inf(T);
+        const u32 dig = J.nib[w], mag = dig & 15u;
+        if (__any(mag != 0)) {                       // wave-uniform; a group with a zero digit adds infinity
+            jac<F> T = L->tab[(mag && mag <= PT_TAB_MAX) ? mag : 1];
+            if (dig & 0x80u) f_neg(T.y, T.y);
+            if (!mag) jac_set_inf(T);
             pt_add(L, acc, acc, T);
         }
     }

@@ -491,13 +491,21 @@ static uint64_t divmod_u(uint64_t q[4]) {
     }
     return (uint64_t)rem;
 }
-// nwin 4-bit nibbles of the little-endian words v (nw 64-bit words), most significant first
-template <class J> static void put_nibbles(J &job, const uint64_t *v, int nw, u32 nwin) {
+// nwin signed 4-bit digits of the little-endian words v (nw 64-bit words), most significant first: each window's
+// nibble plus the carry, minus 16 (carry 1) when above 8, so every digit is in [-7, 8] and k_ptmul.hip's table holds
+// T[1..8].  A byte is |digit| with bit 7 set for a negative digit.  False if a carry leaves the top window (the
+// callers size nwin so that it cannot: 33 windows for < 2^129, 17 for one 64-bit word).
+template <class J> static bool put_digits(J &job, const uint64_t *v, int nw, u32 nwin) {
     job.nwin = nwin;
-    for (u32 w = 0; w < nwin; w++) {
-        const u32 bit = 4 * (nwin - 1 - w), word = bit / 64;
-        job.nib[w] = word < (u32)nw ? (uint8_t)((v[word] >> (bit % 64)) & 15) : 0;
+    int carry = 0;
+    for (u32 i = 0; i < nwin; i++) {              // i: window index from the least significant
+        const u32 bit = 4 * i, word = bit / 64;
+        int d = (word < (u32)nw ? (int)((v[word] >> (bit % 64)) & 15) : 0) + carry;
+        carry = d > 8;
+        if (carry) d -= 16;
+        job.nib[nwin - 1 - i] = d < 0 ? (uint8_t)(0x80 | -d) : (uint8_t)d;
     }
+    return carry == 0;
 }
 template <class J, class A> static void put_point(J &job, const A &a) {
     job.inf = a.inf ? 1u : 0u;
@@ -544,11 +552,12 @@ extern "C" void mclBnG1_mul(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y) {
     fph::g1a phiP;
     fph::g1_phi(phiP, P);
     put_point(jobs[0], P);
-    put_nibbles(jobs[0], k1, 3, 33);
     put_point(jobs[1], phiP);
-    put_nibbles(jobs[1], k2, 2, 33);
     put_point(jobs[2], P);                        // membership: [z^2] P == P + phi(P) = (beta^2 x, -y)
-    put_nibbles(jobs[2], z2, 2, 33);
+    if (!put_digits(jobs[0], k1, 3, 33) || !put_digits(jobs[1], k2, 2, 33) || !put_digits(jobs[2], z2, 2, 33)) {
+        g1_op(OP_G1_MUL, z, x, nullptr, y);       // unreachable (k1 < 2^129): the exact ladder
+        return;
+    }
     fph::g1 acc[3];
     if (!ptmul_run(1, jobs, sizeof(PtJobG1), 3, acc, sizeof(fph::g1))) { fail_out(z, 144); return; }
     fph::g1a chk;
@@ -640,12 +649,14 @@ extern "C" void mclBnG2_mul(mclBnG2 *z, const mclBnG2 *x, const mclBnFr *y) {
     fph::neg(B[3].y, B[3].y);
     PtJobG2 jobs[5];
     memset(jobs, 0, sizeof jobs);
+    bool dig_ok = true;
     for (int i = 0; i < 4; i++) {
         put_point(jobs[i], B[i]);
-        put_nibbles(jobs[i], &d[i], 1, 16);
+        dig_ok &= put_digits(jobs[i], &d[i], 1, 17);
     }
     put_point(jobs[4], Q);                        // membership: psi(Q) == -[|z|] Q
-    put_nibbles(jobs[4], &Z_ABS_H, 1, 16);
+    dig_ok &= put_digits(jobs[4], &Z_ABS_H, 1, 17);
+    if (!dig_ok) { g2_op(OP_G2_MUL, z, x, nullptr, y); return; }   // unreachable (64-bit digits): the exact ladder
     fph::g2 acc[5];
     if (!ptmul_run(2, jobs, sizeof(PtJobG2), 5, acc, sizeof(fph::g2))) { fail_out(z, 288); return; }
     fph::g2a chk = psiQ;

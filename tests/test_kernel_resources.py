@@ -59,7 +59,7 @@ BUDGET = {
     "k_op_grp": (420, 4104),
     "k_op_gt": (1788, 8148),                  # single-lane mcl operations (one wave per dispatch), one kernel per family
     "k_op_pair": (842, 7620),
-    "k_ptmul_g2": (32, 68),                   # mcl G2 multiplication latency kernel: four ladder lanes share each op
+    "k_ptmul_g2": (36, 68),                   # mcl G2 multiplication latency kernel: four ladder lanes share each op (signed digits: 34)
     "k_rlc_key_tables": (12, 168),            # k_rlc_rand.hip: spills to scratch, not AGPRs (<= 256 registers)
     "k_rlc_miller_fallback": (0, 2376),
     "k_rlc_search": (106, 4056),              # round 5: baby-step giant-step (fingerprint table + the confirming power)
