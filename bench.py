@@ -1884,10 +1884,11 @@ def main():
     ap.add_argument("--tpke-streams", type=int, default=1,
                     help="batched verify: concurrent parts (contexts / streams / host threads) per step; measured "
                          "no faster with 2 or 3 parts (147 - 159 vs 145 ms per 1M shares)")
-    ap.add_argument("--hw-queues", type=int, default=int(os.environ.get("LCB_BENCH_HWQ", "8")),
-                    help="GPU_MAX_HW_QUEUES for this process (0: keep the environment's; 8 measured 12.30 vs 11.95 M "
-                         "shares/s with two batches in flight, profiles/r04/q2).  The environment's value is recorded "
-                         "in the line (config.hw_queues_env) beside the one used (config.hw_queues)")
+    ap.add_argument("--hw-queues", type=int, default=int(os.environ.get("LCB_BENCH_HWQ", "0")),
+                    help="GPU_MAX_HW_QUEUES for this process (0, the default: keep the environment's, the box's 4; "
+                         "round 6 stopped overriding it: every hardware queue can hold a full-device scratch "
+                         "reservation, DESIGN.md §14.1).  The environment's value is recorded in the line "
+                         "(config.hw_queues_env) beside the one used (config.hw_queues)")
     ap.add_argument("--tpke-pipeline", type=int, default=3,
                     help="batched verify: whole batches in flight (each on its own context / stream / host thread); "
                          "round 4: 2 measured 12.3 vs 10.6 M shares/s for one at a time, 3 no better (profiles/r04/q1, "
@@ -1941,10 +1942,8 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     HWQ_ENV = os.environ.get("GPU_MAX_HW_QUEUES")
     if args.hw_queues > 0:
-        # hardware queues per process, read when the HIP runtime starts (before torch / the library touch the GPU):
-        # the batched call uses five streams per context, so batches in flight need more than HIP's default four.
-        # The GPU boxes export HIP's default (4) in the environment, so an environment value cannot tell an operator's
-        # choice from the default: --hw-queues 0 keeps it, and the line records both
+        # hardware queues per process, read when the HIP runtime starts (before torch / the library touch the GPU);
+        # an A/B knob only (the default 0 keeps the environment's value), the line records both
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, args.hw_queues))
     import torch
     import torch.distributed as dist

@@ -286,15 +286,17 @@ int lcb_tpke_verify_shares_batched_dev(uint8_t *accept, size_t n_shares, const u
                                        const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
                                        const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
                                        const uint32_t *dec_idx, const uint8_t *ui, void *stream);
-/* host-pointer form of the batched verify (arguments of lcb_tpke_verify_shares) */
-/* lcb_tpke_verify_shares with a per-thread cache of prepared ciphertexts (1024 slots: the line sets of H and W and the
-   ciphertext's validity, keyed by its bytes U || W || V, least recently used replaced).  For callers that verify a
-   ciphertext's shares over several calls (HoneyBadger.cs:211-212 verifies one share per call): each ciphertext is
-   hashed to G2 and its Miller lines computed once.  Same decisions as lcb_tpke_verify_shares. */
+/* lcb_tpke_verify_shares with a per-context cache of prepared ciphertexts (2048 slots: the line sets of H and W and
+   the ciphertext's validity, keyed by its bytes U || W || V, least recently used replaced) and of decompressed
+   verification keys (4096 slots).  For callers that verify a ciphertext's shares over several calls
+   (HoneyBadger.cs:211-212 verifies one share per call): each ciphertext is hashed to G2 and its Miller lines computed
+   once.  A call with more than 1024 ciphertexts or more than 4096 keys runs uncached.  Same decisions as
+   lcb_tpke_verify_shares for any input. */
 int lcb_tpke_verify_shares_cached(uint8_t *accept, size_t n, const uint8_t *y_keys, size_t n_keys,
                                   const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
                                   const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx, const uint32_t *dec_idx,
                                   const uint8_t *ui);
+/* host-pointer form of the batched verify (arguments of lcb_tpke_verify_shares) */
 int lcb_tpke_verify_shares_batched(uint8_t *accept, size_t n_shares, const uint8_t *y_keys, size_t n_keys,
                                    const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
                                    const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,

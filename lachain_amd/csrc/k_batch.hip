@@ -572,7 +572,7 @@ extern "C" void lcbk_tpke_rlc_search2b(hipStream_t s, const void *search, u32 ns
                                        const u32 *gamma12, const u32 *open, const u32 *open_count, uint8_t *accept,
                                        void *next, u32 *next_count, const u32 *key_idx, u32 n_keys, const u32 *susp) {
     if (!n_open) return;
-    hipLaunchKernelGGL(k_tpke_rlc_search2b, dim3((n_open + 1) / 2), dim3(64), 0, s, (const uint4 *)search, ns, gamma0,
+    LCB_LAUNCH_GATED(k_tpke_rlc_search2b, dim3((n_open + 1) / 2), dim3(64), 0, s, (const uint4 *)search, ns, gamma0,
                        gamma12, open, open_count, accept, (uint4 *)next, next_count, key_idx, n_keys, susp);
 }
 extern "C" void lcbk_rlc_census_desc(hipStream_t s, const u32 *grp_idx, const u32 *key_idx, u32 m, u32 n_grp,

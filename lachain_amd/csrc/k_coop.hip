@@ -178,7 +178,7 @@ extern "C" __global__ void __launch_bounds__(CP_BLOCK) k_coop_debug(int op, u32 
 extern "C" void lcbk_coop_tpke_miller(hipStream_t s, const u32 *lines, const void *desc, const void *gpts, u32 n_groups,
                                       u32 *f_soa, uint8_t *gacc, uint8_t *fb, u32 npairs, int fallback) {
     dim3 grid((n_groups + CP_G - 1) / CP_G);
-    hipLaunchKernelGGL(k_coop_tpke_miller, grid, dim3(CP_BLOCK), 0, s, lines, (const uint4 *)desc, (const g1a_st *)gpts,
+    LCB_LAUNCH_GATED(k_coop_tpke_miller, grid, dim3(CP_BLOCK), 0, s, lines, (const uint4 *)desc, (const g1a_st *)gpts,
                        n_groups, f_soa, gacc, fb, npairs);
     if (!fallback) return;
     grid = dim3((n_groups + LCB_BLOCK - 1) / LCB_BLOCK);
@@ -186,7 +186,7 @@ extern "C" void lcbk_coop_tpke_miller(hipStream_t s, const u32 *lines, const voi
 }
 extern "C" void lcbk_coop_final_exp_check(hipStream_t s, u32 *park, u32 n, uint8_t *accept) {
     dim3 grid((n + CP_G - 1) / CP_G);
-    hipLaunchKernelGGL(k_coop_final_exp_check, grid, dim3(CP_BLOCK), 0, s, park, n, accept);
+    LCB_LAUNCH_GATED(k_coop_final_exp_check, grid, dim3(CP_BLOCK), 0, s, park, n, accept);
 }
 extern "C" void lcbk_tpke_exact_points(hipStream_t s, const uint8_t *ct_ok, u32 n_cts, const void *keys, u32 n_keys,
                                        const u32 *ct_idx, const u32 *dec_idx, const uint8_t *ui, u32 n, void *gpts,
@@ -197,5 +197,5 @@ extern "C" void lcbk_tpke_exact_points(hipStream_t s, const uint8_t *ct_ok, u32 
 }
 extern "C" void lcbk_coop_debug(hipStream_t s, int op, u32 *ws, const u32 *b_soa, u32 n, u32 *out, u32 *ref) {
     dim3 grid((n + CP_G - 1) / CP_G);
-    hipLaunchKernelGGL(k_coop_debug, grid, dim3(CP_BLOCK), 0, s, op, ws, b_soa, n, out, ref);
+    LCB_LAUNCH_GATED(k_coop_debug, grid, dim3(CP_BLOCK), 0, s, op, ws, b_soa, n, out, ref);
 }

@@ -25,6 +25,6 @@ extern "C" __global__ void __launch_bounds__(64, 1) k_lineset_coop(u32 *lines, u
 
 extern "C" void lcbk_lineset_coop(hipStream_t s, u32 *lines, u32 n_sets, const u32 *sets, uint8_t *w_g2) {
     if (!n_sets) return;
-    hipLaunchKernelGGL(k_lineset_coop, dim3((n_sets + LS_GROUPS - 1) / LS_GROUPS), dim3(64), 0, s, lines, n_sets, sets,
+    LCB_LAUNCH_GATED(k_lineset_coop, dim3((n_sets + LS_GROUPS - 1) / LS_GROUPS), dim3(64), 0, s, lines, n_sets, sets,
                        w_g2);
 }

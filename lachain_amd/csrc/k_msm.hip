@@ -434,7 +434,7 @@ extern "C" void lcbk_g1_jac_reduce_block(hipStream_t s, const void *in, u32 n_in
     LCB_LAUNCH(k_g1_jac_reduce_block, (const g1 *)in, n_in, group, (g1 *)out);
 }
 extern "C" void lcbk_msm_horner(hipStream_t s, const void *win, u32 nwin, u32 c, u32 fold_top, void *out) {
-    hipLaunchKernelGGL(k_msm_horner_coop, dim3(1), dim3(PT_LANES), 0, s, (const g1 *)win, nwin, c, fold_top, (g1 *)out);
+    LCB_LAUNCH_GATED(k_msm_horner_coop, dim3(1), dim3(PT_LANES), 0, s, (const g1 *)win, nwin, c, fold_top, (g1 *)out);
 }
 extern "C" void lcbk_g1_jac_compress(dim3 grid, hipStream_t s, const void *in, u32 n, uint8_t *out) {
     LCB_LAUNCH(k_g1_jac_compress, (const g1 *)in, n, out);

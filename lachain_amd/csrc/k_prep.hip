@@ -147,11 +147,11 @@ extern "C" void lcbk_ts_rlc_miller_census(dim3 grid, hipStream_t s, const u32 *l
 }
 extern "C" void lcbk_coop_final_exp_check_2w(hipStream_t s, u32 *park, u32 n, uint8_t *accept) {
     dim3 grid((n + CP_G - 1) / CP_G);
-    hipLaunchKernelGGL(k_coop_final_exp_check_2w, grid, dim3(CP_BLOCK), 0, s, park, n, accept);
+    LCB_LAUNCH_GATED(k_coop_final_exp_check_2w, grid, dim3(CP_BLOCK), 0, s, park, n, accept);
 }
 extern "C" void lcbk_lineset_coop_2w(hipStream_t s, u32 *lines, u32 n_sets, const u32 *sets, uint8_t *w_g2) {
     if (!n_sets) return;
-    hipLaunchKernelGGL(k_lineset_coop_2w, dim3((n_sets + LS_GROUPS - 1) / LS_GROUPS), dim3(64), 0, s, lines, n_sets,
+    LCB_LAUNCH_GATED(k_lineset_coop_2w, dim3((n_sets + LS_GROUPS - 1) / LS_GROUPS), dim3(64), 0, s, lines, n_sets,
                        sets, w_g2);
 }
 extern "C" void lcbk_ts_msg_prepare(dim3 grid, hipStream_t s, const uint8_t *msg_data, const u32 *msg_off, u32 n_msgs,

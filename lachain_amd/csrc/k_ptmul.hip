@@ -100,11 +100,11 @@ extern "C" __global__ void __launch_bounds__(64, 1) k_mcl_g2_hash(u32 *io, int o
     io[248] = ok ? 1u : 0u;
 }
 extern "C" void lcbk_mcl_g2_hash(hipStream_t s, u32 *io, int orig_cof) {
-    hipLaunchKernelGGL(k_mcl_g2_hash, dim3(1), dim3(64), 0, s, io, orig_cof);
+    LCB_LAUNCH_GATED(k_mcl_g2_hash, dim3(1), dim3(64), 0, s, io, orig_cof);
 }
 extern "C" void lcbk_ptmul_g1(hipStream_t s, const void *jobs, u32 n_groups, void *out) {
-    hipLaunchKernelGGL(k_ptmul_g1, dim3(1), dim3(64), 0, s, (const PtJob<fp> *)jobs, n_groups, (g1 *)out);
+    LCB_LAUNCH_GATED(k_ptmul_g1, dim3(1), dim3(64), 0, s, (const PtJob<fp> *)jobs, n_groups, (g1 *)out);
 }
 extern "C" void lcbk_ptmul_g2(hipStream_t s, const void *jobs, u32 n_groups, void *out) {
-    hipLaunchKernelGGL(k_ptmul_g2, dim3(1), dim3(64), 0, s, (const PtJob<fp2> *)jobs, n_groups, (g2 *)out);
+    LCB_LAUNCH_GATED(k_ptmul_g2, dim3(1), dim3(64), 0, s, (const PtJob<fp2> *)jobs, n_groups, (g2 *)out);
 }

@@ -12,6 +12,7 @@
 // any correct RS encoder/erasure decoder's, the reference's included.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "gate.hpp"
 
 typedef uint32_t u32;
 #define RS_THREADS 256
@@ -126,12 +127,12 @@ extern "C" __global__ void __launch_bounds__(RS_THREADS) k_rs_apply(const uint8_
 // ---------------------------------------------------------------- host launch wrappers
 extern "C" const void *lcbk_rs_matrix_kernel() { return (const void *)k_rs_matrix; }
 extern "C" void lcbk_rs_matrix(hipStream_t s, const int *pe, int m, const int *pk, int k, int n, uint8_t *M, uint8_t *ok) {
-    hipLaunchKernelGGL(k_rs_matrix, dim3(1), dim3(RS_THREADS), (size_t)m * (m + k), s, pe, m, pk, k, n, M, ok);
+    LCB_LAUNCH_GATED(k_rs_matrix, dim3(1), dim3(RS_THREADS), (size_t)m * (m + k), s, pe, m, pk, k, n, M, ok);
 }
 extern "C" void lcbk_rs_apply(hipStream_t s, const uint8_t *M, const uint8_t *ok, int m, int k, const uint8_t *src, size_t S,
                               const int *pe, uint8_t *dst) {
     size_t lanes = (size_t)m * ((S + 3) / 4);
     if (!lanes) return;
-    hipLaunchKernelGGL(k_rs_apply, dim3((unsigned)((lanes + RS_THREADS - 1) / RS_THREADS)), dim3(RS_THREADS), 0, s, M, ok, m,
+    LCB_LAUNCH_GATED(k_rs_apply, dim3((unsigned)((lanes + RS_THREADS - 1) / RS_THREADS)), dim3(RS_THREADS), 0, s, M, ok, m,
                        k, src, S, pe, dst);
 }

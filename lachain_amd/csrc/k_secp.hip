@@ -15,6 +15,9 @@
 //   k_secp_scalars     signature parsing / recId / low-s checks, s^-1, u1 = z/s, u2 = r/s -> signed digits (job records)
 //   k_secp_verify      sum of the table entries, then x(R) mod n == r on Jacobian coordinates (no inversion)
 #include "secp.hpp"
+#ifndef SECP_HOST_EMULATION
+#include "gate.hpp"
+#endif
 
 #define SECP_BLOCK 256
 #define SECP_WIN 33                  // signed 8-bit digits of a scalar < n: 32 bytes + the final carry
@@ -449,7 +452,7 @@ extern "C" size_t lcbk_secp_table_bytes(void) { return (size_t)SECP_WIN * SECP_T
 extern "C" size_t lcbk_secp_aff_bytes(void) { return sizeof(secp_aff); }
 extern "C" void lcbk_secp_key_parse(hipStream_t s, const uint8_t *pks, u32 pk_len, u32 n_keys, void *out, u32 *ok) {
     if (!n_keys) return;
-    hipLaunchKernelGGL(k_secp_key_parse, dim3(blocks_for(n_keys)), dim3(SECP_BLOCK), 0, s, pks, pk_len, n_keys,
+    LCB_LAUNCH_GATED(k_secp_key_parse, dim3(blocks_for(n_keys)), dim3(SECP_BLOCK), 0, s, pks, pk_len, n_keys,
                        (secp_aff *)out, ok);
 }
 // tmp must hold 2 * 128 * n_tables * 33 field elements (32 B each)
@@ -458,40 +461,40 @@ extern "C" void lcbk_secp_comb_build(hipStream_t s, const void *base, const u32 
     if (!n_tables) return;
     size_t lanes = (size_t)n_tables * SECP_WIN;
     fe *tz = (fe *)tmp, *tp = tz + lanes * SECP_TAB;
-    hipLaunchKernelGGL(k_secp_comb_build, dim3(blocks_for(lanes)), dim3(SECP_BLOCK), 0, s, (const secp_aff *)base,
+    LCB_LAUNCH_GATED(k_secp_comb_build, dim3(blocks_for(lanes)), dim3(SECP_BLOCK), 0, s, (const secp_aff *)base,
                        base_ok, n_tables, (secp_aff *)tables, tz, tp);
 }
 extern "C" void lcbk_secp_header_hash(hipStream_t s, const uint8_t *hdr, u32 n, u64 era, uint8_t *hash, uint8_t *pre_ok) {
     if (!n) return;
-    hipLaunchKernelGGL(k_secp_header_hash, dim3(blocks_for(n)), dim3(SECP_BLOCK), 0, s, hdr, n, era, hash, pre_ok);
+    LCB_LAUNCH_GATED(k_secp_header_hash, dim3(blocks_for(n)), dim3(SECP_BLOCK), 0, s, hdr, n, era, hash, pre_ok);
 }
 extern "C" void lcbk_secp_scalars(hipStream_t s, const uint8_t *hashes, const uint8_t *sigs, u32 sig_len, u32 want_len,
                                   int chain_id, const int32_t *key_idx, u32 n_keys, const u32 *key_ok,
                                   const uint8_t *pre_ok, u32 n, void *jobs) {
     if (!n) return;
     size_t threads = (n + SECP_BATCH - 1) / SECP_BATCH;
-    hipLaunchKernelGGL(k_secp_scalars, dim3(blocks_for(threads)), dim3(SECP_BLOCK), 0, s, hashes, sigs, sig_len,
+    LCB_LAUNCH_GATED(k_secp_scalars, dim3(blocks_for(threads)), dim3(SECP_BLOCK), 0, s, hashes, sigs, sig_len,
                        want_len, chain_id, key_idx, n_keys, key_ok, pre_ok, n, (secp_job *)jobs);
 }
 extern "C" void lcbk_secp_verify(hipStream_t s, const void *jobs, u32 n, const void *g_table, const void *key_tables,
                                  uint8_t *out) {
     if (!n) return;
-    hipLaunchKernelGGL(k_secp_verify, dim3(blocks_for(n)), dim3(SECP_BLOCK), 0, s, (const secp_job *)jobs, n,
+    LCB_LAUNCH_GATED(k_secp_verify, dim3(blocks_for(n)), dim3(SECP_BLOCK), 0, s, (const secp_job *)jobs, n,
                        (const secp_aff *)g_table, (const secp_aff *)key_tables, out);
 }
 extern "C" void lcbk_secp_pubkey(hipStream_t s, const uint8_t *privs, u32 n, const void *g_table, uint8_t *out33,
                                  uint8_t *ok) {
     if (!n) return;
-    hipLaunchKernelGGL(k_secp_pubkey, dim3(blocks_for(n)), dim3(SECP_BLOCK), 0, s, privs, n, (const secp_aff *)g_table,
+    LCB_LAUNCH_GATED(k_secp_pubkey, dim3(blocks_for(n)), dim3(SECP_BLOCK), 0, s, privs, n, (const secp_aff *)g_table,
                        out33, ok);
 }
 extern "C" void lcbk_secp_sign(hipStream_t s, const uint8_t *hashes, const uint8_t *privs, const uint8_t *nonces, u32 n,
                                const void *g_table, int chain_id, int use_new, uint8_t *out, uint8_t *ok) {
     if (!n) return;
-    hipLaunchKernelGGL(k_secp_sign, dim3(blocks_for(n)), dim3(SECP_BLOCK), 0, s, hashes, privs, nonces, n,
+    LCB_LAUNCH_GATED(k_secp_sign, dim3(blocks_for(n)), dim3(SECP_BLOCK), 0, s, hashes, privs, nonces, n,
                        (const secp_aff *)g_table, chain_id, use_new, out, ok);
 }
 extern "C" void lcbk_secp_gen(hipStream_t s, void *out, u32 *ok) {
-    hipLaunchKernelGGL(k_secp_gen, dim3(1), dim3(64), 0, s, (secp_aff *)out, ok);
+    LCB_LAUNCH_GATED(k_secp_gen, dim3(1), dim3(64), 0, s, (secp_aff *)out, ok);
 }
 #endif  // SECP_HOST_EMULATION

@@ -61,24 +61,7 @@ DI void fp12_load_soa_fresh(fp12 &f, const u32 *base, size_t n, size_t i) {
     extern "C" int lcbk_prio_##tag(u32 on) {                                                                    \
         return hipMemcpyToSymbol(HIP_SYMBOL(lcb_wave_prio), &on, sizeof on) == hipSuccess ? 0 : -1;             \
     }
-// The scratch gate (lcb_host.cpp lcb_gate_enter, round 5): the HIP runtime reserves a dispatch's scratch on its
-// hardware queue for min(waves, device wave slots) waves, so a large-grid launch of a kernel with kilobytes of private
-// segment per lane reserves gigabytes on that queue.  Launches whose reservation would reach the gate's threshold run on
-// one process-wide stream per device (ordered with the caller's stream by events), so at most one queue per process holds
-// such a reservation and concurrent callers cannot exhaust the scratch resources (which the runtime reports by aborting
-// the process).  The kernel's private segment size is read once per launch site (hipFuncGetAttributes).
-extern "C" hipStream_t lcb_gate_enter(const void *kern, long long *scratch_cache, size_t lanes, hipStream_t s);
-extern "C" void lcb_gate_exit(hipStream_t s, hipStream_t used);
-#define LCB_LAUNCH_GATED(name, grd, blk, shm, strm, ...)                                                            \
-    do {                                                                                                          \
-        static long long lcb_sc_ = -1;                                                                            \
-        const dim3 lcb_g_ = (grd), lcb_b_ = (blk);                                                                \
-        hipStream_t lcb_s_ = lcb_gate_enter((const void *)name, &lcb_sc_,                                         \
-                                            (size_t)lcb_g_.x * lcb_g_.y * lcb_g_.z * lcb_b_.x * lcb_b_.y * lcb_b_.z, \
-                                            (strm));                                                              \
-        hipLaunchKernelGGL(name, lcb_g_, lcb_b_, (shm), lcb_s_, __VA_ARGS__);                                     \
-        lcb_gate_exit((strm), lcb_s_);                                                                            \
-    } while (0)
+#include "gate.hpp"
 #define LCB_LAUNCH(name, ...) LCB_LAUNCH_GATED(name, grid, dim3(LCB_BLOCK), 0, s, __VA_ARGS__)
 // Persistent grids (the kernels with a lanetab.hpp workspace): as many blocks as are resident at once on the calling
 // thread's device (occupancy x CUs, cached per kernel), at most one block per LCB_BLOCK work items; the workspace holds

@@ -39,6 +39,8 @@ struct lcb_ctx {
     hipStream_t stream = nullptr;   // for the synchronous host-pointer entry points
     hipEvent_t order = nullptr;     // completion of the last work enqueued in this context
     bool order_valid = false;
+    int enq_depth = 0;              // nesting of Enq scopes held by the owning thread
+    size_t chunk = (size_t)1 << 21; // lcb_set_verify_chunk's value, read once per outermost enqueue (LCB_VERIFY_CHUNK)
     // TPKE workspace (lcb_*tpke_prepare_dev): line sets of H and W per ciphertext, validity, decompressed keys
     DevBuf t_lines, t_ctok, t_keys, t_f;
     DevBuf t_coop[3];                 // small exact batches on the cooperative kernels: point records, checks, flags
@@ -116,15 +118,19 @@ struct lcb_ctx {
 };
 
 // Enqueue scope: exclusive use of the context, stream ordered after the context's previous work, and the
-// context's order event recorded after this call's work.
+// context's order event recorded after this call's work.  The outermost scope snapshots the verify chunk, so a call
+// sizes its park buffers and steps its chunk loops with one value even if lcb_set_verify_chunk runs meanwhile.
+size_t lcb_verify_chunk_now();
 struct Enq {
     lcb_ctx *c;
     hipStream_t s;
     std::unique_lock<std::recursive_mutex> lk;
     Enq(lcb_ctx *c_, hipStream_t s_) : c(c_), s(s_), lk(c_->mu) {
+        if (c->enq_depth++ == 0) c->chunk = lcb_verify_chunk_now();
         if (c->order_valid) (void)hipStreamWaitEvent(s, c->order, 0);
     }
     ~Enq() {
         if (hipEventRecord(c->order, s) == hipSuccess) c->order_valid = true;
+        --c->enq_depth;
     }
 };

@@ -970,9 +970,10 @@ bool sync_check(lcb_ctx *c, const char *what) {
 
 // ------------------------------------------------------------------ TPKE
 // shares / checks per Miller + final-exponentiation launch pair (bounds the park buffers); lcb_set_verify_chunk (test
-// hook) lowers it so small batches run several chunks — set it only while no batch call is in flight
+// hook) lowers it so small batches run several chunks.  A call reads it once, when it takes its context (lcb_ctx.hpp
+// Enq), and uses that value for its buffer sizes and its chunk loops alike.
 std::atomic<size_t> g_verify_chunk{(size_t)1 << 21};
-#define LCB_VERIFY_CHUNK (g_verify_chunk.load(std::memory_order_relaxed))
+#define LCB_VERIFY_CHUNK (c->chunk)
 #define LCB_CT_CACHE 2048                       // prepared-ciphertext cache slots per context (52.7 KB of lines each)
 #define LCB_KEY_CACHE 4096                      // decompressed verification keys per context (LCB_G1A_ST_BYTES each)
 
@@ -1950,6 +1951,7 @@ int msm_enqueue(lcb_ctx *cx, void *out_jac, const void *pts, const uint8_t *scal
 }
 
 } // namespace
+size_t lcb_verify_chunk_now() { return g_verify_chunk.load(std::memory_order_relaxed); }
 
 extern "C" lcb_ctx *lcb_ctx_create(void) { return ctx_new(); }
 extern "C" void lcb_ctx_destroy(lcb_ctx *ctx) {
@@ -2295,7 +2297,9 @@ extern "C" int lcb_tpke_verify_shares_cached(uint8_t *accept, size_t n, const ui
                                              const uint32_t *v_off, size_t n_cts, const uint32_t *ct_idx,
                                              const uint32_t *dec_idx, const uint8_t *ui) {
     SYNC_CTX_OR(c, -1)
-    if (n_cts > LCB_CT_CACHE / 2)        // a batch this wide gains nothing from the cache
+    // a batch this wide gains nothing from the caches (and more keys than the key cache holds cannot use it): the
+    // uncached call gives the same decisions
+    if (n_cts > LCB_CT_CACHE / 2 || n_keys > LCB_KEY_CACHE)
         return tpke_verify_shares_host(accept, n, y_keys, n_keys, cts_u, cts_w, v_data, v_off, n_cts, ct_idx, dec_idx,
                                        ui, false);
     for (size_t i = 0; i < n; i++) {
@@ -2325,7 +2329,6 @@ extern "C" int lcb_tpke_verify_shares_cached(uint8_t *accept, size_t n, const ui
         return -1;
     };
     // verification keys -> key-cache slots; the misses are decompressed into consecutive slots [kc_n, kc_n + misses)
-    if (n_keys > LCB_KEY_CACHE) { set_err("tpke verify (cached): more than 4096 keys in one call"); return -1; }
     std::vector<u32> kslot(n_keys);
     u32 kfirst = c->kc_n;
     for (int pass = 0; pass < 2; pass++) {

@@ -20,10 +20,12 @@
 // share waits for the deadline and a free worker, not for the flush in progress to end and then its own (round 4: two
 // workers with ciphertext affinity, ~1.5 flushes per share).  Each worker's context keeps the prepared line sets of the
 // ciphertexts it has seen and the decompressed verification keys, and lcb_queue_tpke_prepare(ct) prepares a ciphertext
-// on EVERY worker ahead of its shares — the reference decrypts every ciphertext of the common subset
-// (PrivateKey.Decrypt, which hashes U || V to G2: HoneyBadger.cs:144-146) before the other validators' decryption
-// shares for it are handled (HoneyBadger.cs:190-213), so no flush waits for hash-to-G2 and two line sets.  A share of a
-// ciphertext that was not prepared ahead is prepared by the worker that flushes it (and cached there).
+// ahead of its shares — the reference decrypts every ciphertext of the common subset (PrivateKey.Decrypt, which hashes
+// U || V to G2: HoneyBadger.cs:144-146) before the other validators' decryption shares for it are handled
+// (HoneyBadger.cs:190-213), so no flush waits for hash-to-G2 and two line sets.  Round 6: the ciphertext is
+// prepared at once by ONE worker (round robin), and by the others only while they have no due shares and no
+// preparation of their own, so a stream of prepares never holds every worker away from due shares.  A share of a
+// ciphertext its flushing worker has not prepared is prepared by that worker in the flush (and cached there).
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -60,6 +62,7 @@ struct TsItem {
                                       // hardware queue with another's, and a flush queued behind a flush doubles its
                                       // latency (profiles/r05/queue/ab.txt: p90 10.6-10.9 ms at four, 6.7 at three)
 #define LCB_QUEUE_PREP_CHUNK 1024  // ciphertexts per preparation call (the widest batch the context cache takes)
+#define LCB_QUEUE_IDLE_CHUNK 64    // ciphertexts per idle-time preparation (one wave of the preparation kernel)
 struct lcb_queue {
     std::mutex mu;
     std::condition_variable cv_work, cv_done;
@@ -67,7 +70,9 @@ struct lcb_queue {
     std::chrono::microseconds max_delay;
     std::vector<TpkeItem> tpke;                        // any worker
     clk::time_point oldest;
-    std::vector<std::string> prep[LCB_QUEUE_WORKERS];  // ciphertexts to prepare ahead of their shares, on every worker
+    std::vector<std::string> prep[LCB_QUEUE_WORKERS];  // ciphertexts this worker prepares before anything else
+    std::vector<std::string> idle_prep[LCB_QUEUE_WORKERS];   // ... and the others' ones, when it has nothing due
+    uint32_t prep_rr = 0;                              // round robin over the workers for the eager preparation
     std::vector<TsItem> ts;                            // any worker
     clk::time_point ts_oldest;
     bool stop = false, flush_now = false;
@@ -214,8 +219,8 @@ void run_prepare(lcb_queue *q, std::vector<std::string> &cts) {
 void worker_loop(lcb_queue *q, int w) {
     std::unique_lock<std::mutex> lk(q->mu);
     for (;;) {
-        const size_t pt = q->tpke.size(), ps = q->ts.size(), pp = q->prep[w].size();
-        if (pt + ps + pp == 0) {
+        const size_t pt = q->tpke.size(), ps = q->ts.size(), pp = q->prep[w].size(), pi = q->idle_prep[w].size();
+        if (pt + ps + pp + pi == 0) {
             if (q->stop) return;
             q->cv_work.wait(lk);
             continue;
@@ -223,7 +228,7 @@ void worker_loop(lcb_queue *q, int w) {
         const clk::time_point now = clk::now();
         const bool due_t = pt && (q->stop || q->flush_now || pt >= q->max_batch || now >= q->oldest + q->max_delay);
         const bool due_s = ps && (q->stop || q->flush_now || ps >= q->max_batch || now >= q->ts_oldest + q->max_delay);
-        if (!pp && !due_t && !due_s) {
+        if (!pp && !due_t && !due_s && !pi) {
             clk::time_point next = clk::time_point::max();
             if (pt) next = std::min(next, q->oldest + q->max_delay);
             if (ps) next = std::min(next, q->ts_oldest + q->max_delay);
@@ -237,6 +242,12 @@ void worker_loop(lcb_queue *q, int w) {
         if (p.empty()) {              // this worker's preparations first: the shares it takes then hit its cache
             if (due_t) t.swap(q->tpke);
             if (due_s) s.swap(q->ts);
+            if (t.empty() && s.empty() && pi) {      // nothing due: prepare the others' ciphertexts here too, in
+                auto &ip = q->idle_prep[w];          // chunks, so due shares find this worker free again soon
+                const size_t m = std::min(ip.size(), (size_t)LCB_QUEUE_IDLE_CHUNK);
+                p.assign(std::make_move_iterator(ip.begin()), std::make_move_iterator(ip.begin() + (long)m));
+                ip.erase(ip.begin(), ip.begin() + (long)m);
+            }
         }
         if (q->tpke.empty() && q->ts.empty()) q->flush_now = false;
         const size_t batched_min = q->batched_min;     // read under the lock (lcb_queue_set_batched writes it)
@@ -314,7 +325,8 @@ extern "C" int lcb_queue_tpke_prepare(lcb_queue *q, const uint8_t u48[48], const
     if (v_len) ct.append((const char *)v, v_len);
     std::lock_guard<std::mutex> lk(q->mu);
     if (q->stop) return -1;
-    for (int w = 0; w < q->n_workers; w++) q->prep[w].push_back(ct);
+    const int owner = (int)(q->prep_rr++ % (uint32_t)q->n_workers);
+    for (int w = 0; w < q->n_workers; w++) (w == owner ? q->prep[w] : q->idle_prep[w]).push_back(ct);
     q->cv_work.notify_all();
     return 0;
 }

@@ -83,3 +83,19 @@ def test_key_cache_reorder_and_overflow(nat):
         sh = [(ci, 3000 + i, s) for ci, i, s in shares] + [(0, 5, shares[0][2])]   # + one share under a junk key
         assert nat.tpke_verify_shares(keys, cts, sh, cached=True) == want + [False], rep
     assert nat.tpke_verify_shares(ys, cts, shares, cached=True) == want
+
+
+def test_more_keys_than_the_key_cache(nat):
+    """a call with more distinct keys than the 4096-slot key cache runs uncached and keeps the decisions (ADVICE r5:
+    it returned -1 before)"""
+    t = T["tpke_n4"]
+    ys = [H(y) for y in t["y_i"]]
+    cts = [(H(c["u"]), H(c["v"]), H(c["w"])) for c in t["ciphertexts"]]
+    want = [a for c in t["ciphertexts"] for a in c["accept"]]
+    shares = [(ci, i, H(s)) for ci, c in enumerate(t["ciphertexts"]) for i, s in enumerate(c["shares"])]
+    rng = np.random.default_rng(11)
+    junk = [b"\x9f" + rng.bytes(47) for _ in range(4097)]
+    keys = junk + ys
+    sh = [(ci, 4097 + i, s) for ci, i, s in shares] + [(0, 4096, shares[0][2])]
+    assert nat.tpke_verify_shares(keys, cts, sh, cached=True) == want + [False]
+    assert nat.tpke_verify_shares(ys, cts, shares, cached=True) == want      # the caches still work afterwards
