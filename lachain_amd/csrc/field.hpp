@@ -165,9 +165,21 @@ DI u32x12 lcb_fp_pow_sel(int k, const u32x12 &t1, const u32x12 &t3, const u32x12
     default: return t15;
     }
 }
-// which: 0 = p - 2, 1 = (p + 1)/4, 2 = (p - 1)/2, 3 = (p - 3)/4.  The selector is made wave-uniform (readfirstlane)
-// so the exponent words come through the scalar cache and every bit test is a scalar branch: with the constant's
-// address as a (VGPR) argument each of the ~450 bit reads was a vector load the lane waited for.
+// which: 0 = p - 2, 1 = (p + 1)/4, 2 = (p - 1)/2, 3 = (p - 3)/4, made wave-uniform (readfirstlane).
+// Round 6: the generated routine lcb_r_fp_pow (tools/gen_asm.py) runs the same windows with the table t1..t15 in
+// VGPRs above the leaf routines' clobbers.  The compiled loop below (LCB_FP_POW_COMPILED=1) kept the table in scratch
+// and reloaded 48 B per window, ~4.6 KB of scratch reads per exponentiation: most of the HBM traffic of every
+// decompression lane.  A call (not inlined): the routine clobbers only the ABI's caller-saved registers beyond the
+// leaf routines' own, so its callers see an ordinary call.
+#ifndef LCB_FP_POW_COMPILED
+#define LCB_FP_POW_COMPILED 0
+#endif
+#if !LCB_FP_POW_COMPILED
+DN u32x12 lcb_fp_pow_v(u32x12 av, int which) {
+    return lcb_asm_fp_pow(av, __builtin_amdgcn_readfirstlane(which));
+}
+#else
+// the compiled form: the exponent words come through the scalar cache and every bit test is a scalar branch
 DN u32x12 lcb_fp_pow_v(u32x12 av, int which) {
     which = __builtin_amdgcn_readfirstlane(which);
     const u32 *e = which == 0 ? LCB_P_MINUS_2 : which == 1 ? LCB_P_PLUS1_DIV4 : which == 2 ? LCB_P_MINUS1_DIV2
@@ -207,6 +219,7 @@ DN u32x12 lcb_fp_pow_v(u32x12 av, int which) {
     }
     return acc;
 }
+#endif
 DI void fp_pow_const(fp &r, const fp &a, int which) { r = fp_from_v(lcb_fp_pow_v(fp_to_v(a), which)); }
 DI void fp_inv(fp &r, const fp &a) { fp_pow_const(r, a, 0); }   // a^(p-2): 463 products
 

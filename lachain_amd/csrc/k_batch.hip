@@ -87,10 +87,10 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_rlc_wsum(const uint4 *sdesc, u32 n_
     g1 p;
     g1a_st o;
     g1_load_soa(p, wsum, 2 * (size_t)n_l1, 2 * (size_t)l);
-    g1_to_st(o, p, false);
+    g1_to_st_gcd(o, p, false);
     gpts[2 * (size_t)g] = o;
     g1_load_soa(p, wsum, 2 * (size_t)n_l1, 2 * (size_t)l + 1);
-    g1_to_st(o, p, true);
+    g1_to_st_gcd(o, p, true);
     gpts[2 * (size_t)g + 1] = o;
 }
 

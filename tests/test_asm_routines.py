@@ -33,7 +33,8 @@ def lib():
 def wrapper_contract(label):
     """(VGPRs, SGPRs) the HIP wrapper of `label` lets the routine write (outputs + clobbers)."""
     src = open(asm_sim.HPP).read()
-    i = src.index(f"{label}@rel32@lo")
+    body_end = src.index('    ""\n', src.index("#define LCB_ASM_LIBRARY_TEXT"))   # past the routines' own calls
+    i = src.index(f"{label}@rel32@lo", body_end)
     blk = src[i:src.index("\n}", i)]
     vs = {int(x) for x in re.findall(r'"v(\d+)"', blk)}
     for lo, hi in re.findall(r'\{v\[(\d+):(\d+)\]\}', blk):
@@ -112,3 +113,25 @@ def test_fp2_mul_fp(lib):
         lane, rd = asm_sim.call(lib, "lcb_r_fp2_mul_fp", {0: xa, 12: xb, 24: s})
         assert rd(0) == mont(xa, s) and rd(12) == mont(xb, s)
     check_contract("lcb_r_fp2_mul_fp", lane)
+
+
+@pytest.mark.parametrize("which", [0, 1, 2, 3])
+def test_fp_pow(which):
+    """lcb_r_fp_pow (round 6): a^e for the four field exponents with the window table in VGPR islands, run as a
+    program (labels, branches, nested calls) in the simulator; every register it writes is declared by its wrapper"""
+    prog, labels = asm_sim.load_program(asm_sim.HPP, "LCB_ASM_LIBRARY_TEXT")
+    e = [P - 2, (P + 1) // 4, (P - 1) // 2, (P - 3) // 4][which]
+    vs, ss = wrapper_contract("lcb_r_fp_pow")
+    rng = random.Random(which)
+    for a in (rng.randrange(P), 1, P - 1):
+        lane = asm_sim.ProgLane()
+        am = a * R % P
+        for j in range(12):
+            lane.v[j] = (am >> (32 * j)) & 0xFFFFFFFF
+        lane.s[84] = which
+        lane.s[30] = lane.s[31] = 0
+        asm_sim.run_program(prog, labels, "lcb_r_fp_pow", lane)
+        got = sum(lane.v[j] << (32 * j) for j in range(12))
+        assert got == pow(a, e, P) * R % P
+        assert lane.written_v <= vs, sorted(lane.written_v - vs)
+        assert lane.written_s <= ss | {84}, sorted(lane.written_s - ss)

@@ -56,7 +56,7 @@ BUDGET = {
     "k_msm_bucket_reduce": (0, 744),          # + the prefetched next bucket
     "k_msm_horner": (0, 168),
     "k_op_debug": (96, 6956),
-    "k_op_grp": (420, 4104),
+    "k_op_grp": (444, 4104),                  # round 6: the exponentiation routine's table in VGPRs (lcb_r_fp_pow)
     "k_op_gt": (1788, 8148),                  # single-lane mcl operations (one wave per dispatch), one kernel per family
     "k_op_pair": (842, 7620),
     "k_ptmul_g2": (36, 68),                   # mcl G2 multiplication latency kernel: four ladder lanes share each op (signed digits: 34)
@@ -78,7 +78,7 @@ BUDGET = {
     "k_tpke_rlc_search2a": (97, 3448),        # level-2 searches: four Fp12 values per lane, four lanes per group
     "k_tpke_rlc_search2b": (0, 3656),
     "k_tpke_rlc_sum": (0, 1168),
-    "k_tpke_rlc_wsum": (0, 576),
+    "k_tpke_rlc_wsum": (48, 576),             # round 6: binary-GCD conversions; the live record saved around the calls
     "k_tpke_rlc_wsum2": (0, 648),
     "k_ts_miller": (1248, 3292),
     "k_ts_msg_prepare": (5, 4824),            # round 5: k_prep.hip at 256 registers (was 346, 0 spills, 3,688 B)

@@ -205,6 +205,16 @@ def run_program(prog, labels, entry, lane, max_steps=50_000_000):
             lane.put(ops[0], g(ops[2]) if lane.getmask(ops[3]) else g(ops[1]))
         elif mn == "v_mul_lo_u32":
             lane.put(ops[0], (g(ops[1]) * g(ops[2])) & M32)
+        elif mn == "v_alignbit_b32":
+            lane.put(ops[0], (((g(ops[1]) << 32) | g(ops[2])) >> (g(ops[3]) & 31)) & M32)
+        elif mn == "v_lshlrev_b32":
+            lane.put(ops[0], (g(ops[2]) << (g(ops[1]) & 31)) & M32)
+        elif mn == "s_and_b32":
+            r = g(ops[1]) & g(ops[2])
+            lane.put(ops[0], r); lane.scc = 1 if r else 0
+        elif mn == "s_lshr_b32":
+            r = g(ops[1]) >> (g(ops[2]) & 31)
+            lane.put(ops[0], r); lane.scc = 1 if r else 0
         elif mn in ("v_mov_b32", "s_mov_b32", "s_mov_b64", "v_accvgpr_read_b32", "v_accvgpr_write_b32"):
             lane.put(ops[0], g(ops[1]))
         elif mn == "s_add_u32":

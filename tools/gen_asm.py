@@ -454,7 +454,120 @@ def r_fp2_mul_lazy():
     return a.text(), 132
 
 
-ROUTINES = [r_fp_mul, r_fp_sqr, r_fp_mul2, r_fp2_mul_lazy, r_fp2_sqr, r_fp2_mul_fp]
+# ------------------------------------------------------------------ exponentiation by the field's constants
+# lcb_r_fp_pow: v[0:11] = a, s84 = which (wave-uniform: 0 = p - 2, 1 = (p + 1)/4, 2 = (p - 1)/2, 3 = (p - 3)/4)
+# -> v[0:11] = a^e.  The same sliding 4-bit windows as the compiled lcb_fp_pow_v (field.hpp), but the window table
+# t1, t3, ..., t15 stays in VGPRs across the product calls: 12 caller-saved 8-register islands of the AMDGPU ABI from
+# v64 (v64-71, v80-87, ..., v240-247), above every leaf routine's clobbers (<= v61), so neither this routine nor its
+# callers save or reload it.  The compiled form kept the table in scratch (48 B reloaded per window, ~4.6 KB per
+# exponentiation: most of the HBM traffic of every decompression lane, round 6).  The windows are known here, so
+# each exponent is a straight-line program of steps `s_mov_b32 s82, cnt | idx << 16` + a call of lcb_r_fp_pow_step
+# (cnt squarings, then one product by table entry idx; idx = 0xff: none).  Return addresses: s[80:81] (the
+# routine), s[86:87] (the step); s83 counts.
+POW_ISLANDS = [64 + 16 * k + j for k in range(12) for j in range(8)]           # v64-71, v80-87, ..., v240-247
+POW_T = [POW_ISLANDS[12 * e:12 * e + 12] for e in range(8)]                     # t_(2e+1)
+POW_EXPS = [P - 2, (P + 1) // 4, (P - 1) // 2, (P - 3) // 4]
+
+
+def pow_program(e):
+    """the sliding windows of field.hpp lcb_fp_pow_v for exponent e: (first table index, [(squarings, idx)])"""
+    bit = lambda i: (e >> i) & 1
+    i = e.bit_length() - 1
+    first, steps, pend = None, [], 0
+    while i >= 0:
+        if not bit(i):
+            pend += 1
+            i -= 1
+            continue
+        j = max(i - 3, 0)
+        while not bit(j):
+            j += 1
+        w = 0
+        for b in range(i, j - 1, -1):
+            w = (w << 1) | bit(b)
+        if first is None:
+            first = (w - 1) // 2
+        else:
+            steps.append((pend + i - j + 1, (w - 1) // 2))
+        pend = 0
+        i = j - 1
+    if pend:
+        steps.append((pend, 0xff))
+    return first, steps
+
+
+def pow_eval(a, e):
+    """the program's value in plain integers (generator self-check)"""
+    first, steps = pow_program(e)
+    T = [pow(a, 2 * k + 1, P) for k in range(8)]
+    acc = T[first]
+    for cnt, idx in steps:
+        for _ in range(cnt):
+            acc = acc * acc % P
+        if idx != 0xff:
+            acc = acc * T[idx] % P
+    return acc
+
+
+def r_fp_pow():
+    a = Asm()
+    for ex in POW_EXPS:                         # generation-time check of the window programs
+        assert pow_eval(7, ex) == pow(7, ex, P) and pow_eval(P - 3, ex) == pow(P - 3, ex, P)
+    a.label("lcb_r_fp_pow")
+    a("s_mov_b64 s[80:81], s[30:31]")
+    mov(a, POW_T[0], vr(0))                     # t1 = a
+    a(call_seq_asm("lcb_r_fp_sqr"))
+    mov(a, POW_T[7], vr(0))                     # a^2, parked in t15's slot until t15 is formed
+    for k in range(1, 8):
+        mov(a, vr(0), POW_T[k - 1])
+        mov(a, vr(12), POW_T[7])
+        a(call_seq_asm("lcb_r_fp_mul"))
+        mov(a, POW_T[k], vr(0))
+    for w, ex in enumerate(POW_EXPS):
+        a(f"s_cmp_eq_u32 s84, {w}")
+        a(f"s_cbranch_scc1 lcb_r_fp_pow_e{w}")
+    a("s_branch lcb_r_fp_pow_e0")
+    for w, ex in enumerate(POW_EXPS):
+        first, steps = pow_program(ex)
+        a.label(f"lcb_r_fp_pow_e{w}")
+        mov(a, vr(0), POW_T[first])
+        for cnt, idx in steps:
+            a(f"s_mov_b32 s82, {cnt | (idx << 16)}")
+            a(call_seq_asm("lcb_r_fp_pow_step"))
+        a("s_setpc_b64 s[80:81]")
+    # the step: s82 = cnt | idx << 16
+    a.label("lcb_r_fp_pow_step")
+    a("s_mov_b64 s[86:87], s[30:31]")
+    a("s_and_b32 s83, s82, 0xffff")
+    a.label("lcb_r_fp_pow_sq")
+    a("s_cmp_eq_u32 s83, 0")
+    a("s_cbranch_scc1 lcb_r_fp_pow_sel")
+    a(call_seq_asm("lcb_r_fp_sqr"))
+    a("s_sub_u32 s83, s83, 1")
+    a("s_branch lcb_r_fp_pow_sq")
+    a.label("lcb_r_fp_pow_sel")
+    a("s_lshr_b32 s83, s82, 16")
+    for k in range(8):
+        a(f"s_cmp_eq_u32 s83, {k}")
+        a(f"s_cbranch_scc1 lcb_r_fp_pow_t{k}")
+    a("s_setpc_b64 s[86:87]")                   # idx 0xff: squarings only
+    for k in range(8):
+        a.label(f"lcb_r_fp_pow_t{k}")
+        mov(a, vr(12), POW_T[k])
+        a("s_branch lcb_r_fp_pow_mul")
+    a.label("lcb_r_fp_pow_mul")
+    a(call_seq_asm("lcb_r_fp_mul"))
+    a("s_setpc_b64 s[86:87]")
+    return a.text(), 64
+
+
+def call_seq_asm(label):
+    """the call sequence of call_seq() as plain assembly lines (a routine calling a leaf routine)"""
+    return (f"s_getpc_b64 s[{S_TMP}:{S_TMP + 1}]\n  s_add_u32 s{S_TMP}, s{S_TMP}, {label}@rel32@lo+4\n"
+            f"  s_addc_u32 s{S_TMP + 1}, s{S_TMP + 1}, {label}@rel32@hi+12\n  s_swappc_b64 s[30:31], s[{S_TMP}:{S_TMP + 1}]")
+
+
+ROUTINES = [r_fp_mul, r_fp_sqr, r_fp_mul2, r_fp2_mul_lazy, r_fp2_sqr, r_fp2_mul_fp, r_fp_pow]
 
 
 def clobber_list(nvgpr, keep):
@@ -462,6 +575,13 @@ def clobber_list(nvgpr, keep):
     regs += [f'"s{s}"' for s in CLOBBER_SGPRS]
     regs += ['"scc"']  # the call sequence's s_add_u32/s_addc_u32 write SCC; a compare the compiler hoisted
     return ", ".join(regs)  # above the call would otherwise feed a stale SCC to the branch after it
+
+
+def pow_clobbers():
+    regs = [f'"v{i}"' for i in list(range(12, 64)) + POW_ISLANDS]
+    regs += [f'"s{x}"' for x in [30, 31, 80, 81, 82, 83, 86, 87] + CLOBBER_SGPRS[2:]]
+    regs += ['"scc"']
+    return ", ".join(regs)
 
 
 def call_seq(label):
@@ -530,6 +650,14 @@ __device__ __forceinline__ void lcb_asm_fp2_sqr(u32x12 &xa, u32x12 &xb) {{
         : "+{{v[0:11]}}"(xa), "+{{v[12:23]}}"(xb)
         :
         : {clobber_list(nv['r_fp2_sqr'], set(range(24)))});
+}}
+// a^e for e = p - 2, (p + 1)/4, (p - 1)/2, (p - 3)/4 (which = 0..3, wave-uniform): the window table in VGPR islands
+__device__ __forceinline__ u32x12 lcb_asm_fp_pow(u32x12 a, int which) {{
+    asm({call_seq("lcb_r_fp_pow")}
+        : "+{{v[0:11]}}"(a)
+        : "{{s84}}"(which)
+        : {pow_clobbers()});
+    return a;
 }}
 // x*s for x in Fp2, s in Fp
 __device__ __forceinline__ void lcb_asm_fp2_mul_fp(u32x12 &xa, u32x12 &xb, u32x12 s) {{
