@@ -350,12 +350,19 @@ int lcb_set_verify_chunk(size_t checks);
    with the TPKE preparation split into hash + H's line set and U / W decoding + W's line set, on two high-priority
    streams (threshold signatures: as 1).  Decisions are unchanged. */
 int lcb_set_fork_mode(int mode);
-/* the scratch gate (round 5): a launch whose scratch reservation — private segment per lane x the lanes of
-   min(dispatch waves, 32 wave slots per CU) — reaches `bytes` runs on one process-wide stream per device, ordered with
-   the caller's stream by events, so concurrent callers never hold more than one such reservation per process (the HIP
-   runtime aborts the process when it cannot reserve scratch).  Default 4 GiB (environment LCB_SCRATCH_GATE_MB); -1 = off,
-   0 = every launch with scratch.  Tuning hook (LCB_ALLOW_TUNING=1). */
+/* the scratch gate (round 6 model): the HSA runtime binds a dispatch's FULL-device scratch
+   (private segment per lane rounded to 16 B x 64 lanes x CUs x 32 wave slots) to its hardware queue whenever that is
+   below the agent's bind limit (24 GiB on the box), and all queues share one pool (32 GiB); a request the pool cannot
+   serve aborts the process.  A launch whose full-device size exceeds the per-queue share T = (pool - 4.5 GiB) / Q
+   (Q = 2 x GPU_MAX_HW_QUEUES: the library uses two stream priorities) runs on one process-wide stream per device,
+   ordered with the caller's stream by events, so the queues' bound scratch stays within the pool.  `bytes` replaces T
+   (environment LCB_SCRATCH_GATE_MB); -1 = off, 0 = every launch with scratch, < -1 = back to the model.  Tuning hook
+   (LCB_ALLOW_TUNING=1). */
 int lcb_set_scratch_gate(long long bytes);
+/* the calling thread's device's scratch model: out[0] pool bytes (HSA_AMD_AGENT_INFO_SCRATCH_LIMIT_MAX, 0 unknown),
+   [1] bind limit (..._SCRATCH_LIMIT_CURRENT), [2] wave slots (CUs x waves per CU), [3] Q, [4] the per-queue share T,
+   [5] the threshold in force (UINT64_MAX: gate off).  0 on success. */
+int lcb_scratch_info(uint64_t out[6]);
 /* launches routed through the gate / launches checked, since the process started */
 void lcb_scratch_gate_stats(uint64_t *routed, uint64_t *seen);
 /* the persistent grids of the table-walking kernels (Lagrange lanes, scalar-multiplication batches) use at most this

@@ -28,6 +28,8 @@
 #include <string>
 #include <algorithm>
 #include <sys/random.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include "launch.h"
 #include "bls_constants_host.h"
@@ -247,29 +249,90 @@ extern "C" int lcb_set_line_mode(int general) {
 }
 extern "C" const char *lcb_last_error(void) { return g_err.c_str(); }
 
-// ================================================================== the scratch gate (kcommon.hpp LCB_LAUNCH_GATED)
-// Launches whose scratch reservation (private segment per lane x the lanes of min(dispatch waves, device wave slots))
-// reaches the threshold are serialized onto one stream per device: the launch waits for the caller's stream, the
-// caller's stream then waits for the launch, and the per-device mutex orders the crossings of concurrent callers.
+// ================================================================== the scratch gate (gate.hpp LCB_LAUNCH_GATED)
+// What the runtime does with a dispatch's private segment (ROCr's queue scratch handler; hsa_ext_amd.h:686-703 for the
+// two agent limits, measured on the box in profiles/r06/scratch_limits.txt): the per-lane size S is rounded up to 16 B
+// (a wave's 1 KB granule) and the FULL-device size  full(S) = S x 64 lanes x CUs x wave slots per CU  is requested for
+// the dispatch's hardware queue.  When full(S) <= the agent's async scratch limit (HSA_AMD_AGENT_INFO_SCRATCH_LIMIT_
+// CURRENT) the memory stays BOUND to that queue after the dispatch and serves its later dispatches; above it, it is a
+// use-once allocation of the dispatch's own size, released when the dispatch retires.  All queues share one pool
+// (SCRATCH_LIMIT_MAX).  A use-once request that does not fit waits while another use-once allocation is outstanding;
+// a request that finds the pool held by bound reservations of busy queues aborts the process with
+// HSA_STATUS_ERROR_OUT_OF_RESOURCES (the round-5 aborts: DESIGN.md §14.1).
+// Measured on the box (profiles/r06/scratch_limits.txt): pool 32 GiB, bind limit 24 GiB, 256 CUs x 32 slots — every
+// kernel of this library binds (the largest, k_op_gt at 8,148 B per lane, binds 4.27 GB), so the sum of the
+// hardware queues' bound reservations is what must stay within the pool.  HIP keeps GPU_MAX_HW_QUEUES queues per stream
+// priority and the library uses two priorities (the preparation chains run on high-priority streams), so a process
+// holds up to Q = 2 x GPU_MAX_HW_QUEUES queues: 8 at the box's default 4, 16 when a caller raises it to 8 (the round-5
+// bench did: 16 queues x up to 2.5 GB bound by the preparation lanes exceed the 32 GiB pool — the aborts).
+// The gate therefore bounds the bound reservations: a launch whose full(S) exceeds the per-queue share
+// T = (pool - LCB_GATE_RESERVE) / Q runs on one process-wide stream per device, ordered with the caller's stream by
+// events, so every other queue binds <= T and the gate's queue at most LCB_GATE_RESERVE (>= every kernel's full(S):
+// tests/test_kernel_resources.py), and  Q x T + reserve <= pool.  At Q = 8: T = 3.44 GiB, and only the single-lane
+// mcl-surface / debug kernels (> 6.7 KB per lane) are routed; at Q = 16 the pairing kernels above ~3.5 KB are too.
+// Launches whose scratch is use-once (full(S) above the bind limit) are left on the caller's stream.
+#define LCB_GATE_RESERVE (9ull << 29)                 // 4.5 GiB: the gate queue's bound reservation, >= every kernel's full(S)
 namespace {
 struct GateDev {
-    std::mutex mu;
+    std::mutex mu, init_mu;
     hipStream_t s = nullptr;
     hipEvent_t in = nullptr, out = nullptr;
-    int cus = 0;
+    std::atomic<int> ready{0};
+    uint64_t slots = 0;           // CUs x wave slots per CU
+    uint64_t pool = 0;            // HSA_AMD_AGENT_INFO_SCRATCH_LIMIT_MAX (0: unknown)
+    uint64_t bind_limit = 0;      // HSA_AMD_AGENT_INFO_SCRATCH_LIMIT_CURRENT (0: unknown: every full(S) binds)
+    uint64_t per_queue = 0;       // T
+    int hwq = 8;                  // hardware queues the process may hold (both priorities)
 };
 GateDev g_gate[64];
-std::atomic<long long> g_gate_bytes{-2};            // -2: not read from LCB_SCRATCH_GATE_MB yet
+std::atomic<long long> g_gate_bytes{-2};            // -2: not read from LCB_SCRATCH_GATE_MB yet; -3: the model's T
 std::atomic<unsigned long long> g_gate_routed{0}, g_gate_seen{0};
 thread_local int t_gate_dev = -1;                   // device whose gate mutex this thread holds (-1: none)
-long long gate_threshold() {
+long long gate_override() {
     long long v = g_gate_bytes.load(std::memory_order_relaxed);
     if (v != -2) return v;
     const char *e = getenv("LCB_SCRATCH_GATE_MB");
-    v = e && *e ? atoll(e) * (1ll << 20) : (4ll << 30);   // default: 4 GiB of reservation
+    v = e && *e ? atoll(e) * (1ll << 20) : -3;
     long long expect = -2;
     g_gate_bytes.compare_exchange_strong(expect, v);
     return g_gate_bytes.load();
+}
+struct HsaFind { int want, seen; hsa_agent_t agent; bool found; };
+hsa_status_t hsa_find_gpu(hsa_agent_t a, void *d) {
+    HsaFind *f = (HsaFind *)d;
+    hsa_device_type_t t;
+    if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS || t != HSA_DEVICE_TYPE_GPU)
+        return HSA_STATUS_SUCCESS;
+    if (f->seen++ == f->want) { f->agent = a; f->found = true; return HSA_STATUS_INFO_BREAK; }
+    return HSA_STATUS_SUCCESS;
+}
+// the device's scratch model, read once (HIP device ordinal i = the i-th GPU agent of the runtime)
+void gate_model(GateDev &g, int dev) {
+    if (g.ready.load(std::memory_order_acquire)) return;
+    std::lock_guard<std::mutex> lk(g.init_mu);
+    if (g.ready.load()) return;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+    uint32_t wpc = 0;
+    HsaFind f{dev, 0, {0}, false};
+    if (hsa_init() == HSA_STATUS_SUCCESS) {
+        hsa_iterate_agents(hsa_find_gpu, &f);
+        if (f.found) {
+            uint64_t v = 0;
+            if (hsa_agent_get_info(f.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_SCRATCH_LIMIT_MAX, &v) == HSA_STATUS_SUCCESS) g.pool = v;
+            v = 0;
+            if (hsa_agent_get_info(f.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_SCRATCH_LIMIT_CURRENT, &v) == HSA_STATUS_SUCCESS) g.bind_limit = v;
+            if (hsa_agent_get_info(f.agent, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_MAX_WAVES_PER_CU, &wpc) != HSA_STATUS_SUCCESS) wpc = 0;
+        }
+        hsa_shut_down();
+    }
+    g.slots = (uint64_t)cus * (wpc ? wpc : 32);
+    const char *q = getenv("GPU_MAX_HW_QUEUES");
+    g.hwq = 2 * (q && atoi(q) > 0 ? atoi(q) : 4);      // queues per priority x the two priorities the library uses
+    // unknown pool: assume the measured 32 GiB rather than none
+    const uint64_t pool = g.pool ? g.pool : (32ull << 30);
+    g.per_queue = pool > LCB_GATE_RESERVE ? (pool - LCB_GATE_RESERVE) / (uint64_t)g.hwq : 0;
+    g.ready.store(1, std::memory_order_release);
 }
 }  // namespace
 extern "C" hipStream_t lcb_gate_enter(const void *kern, long long *scratch_cache, size_t lanes, hipStream_t s) {
@@ -280,26 +343,34 @@ extern "C" hipStream_t lcb_gate_enter(const void *kern, long long *scratch_cache
         __atomic_store_n(scratch_cache, sc, __ATOMIC_RELAXED);
     }
     g_gate_seen.fetch_add(1, std::memory_order_relaxed);
-    const long long thr = gate_threshold();
-    if (sc == 0 || thr < 0 || lanes == 0) return s;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return s;
-    GateDev &g = g_gate[dev];
-    if (!g.cus) {
-        int cus = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
-        __atomic_store_n(&g.cus, cus, __ATOMIC_RELAXED);
+    const long long ovr = gate_override();
+    if (sc == 0 || ovr == -1 || lanes == 0) return s;
+    int dev = -1;
+    if (hipStreamGetDevice(s, &dev) != hipSuccess || dev < 0) {          // (the caller's stream decides the device)
+        if (hipGetDevice(&dev) != hipSuccess) return s;
     }
-    const size_t waves = (lanes + 63) / 64, slots = (size_t)g.cus * 32;
-    const long long reserve = sc * 64 * (long long)std::min(waves, slots);
-    if (reserve < thr) return s;
+    if (dev < 0 || dev >= 64) return s;
+    GateDev &g = g_gate[dev];
+    gate_model(g, dev);
+    const uint64_t per_lane = ((uint64_t)sc + 15) & ~(uint64_t)15;
+    const uint64_t full = per_lane * 64 * g.slots;
+    const bool binds = g.bind_limit == 0 || full <= g.bind_limit;
+    const uint64_t thr = ovr >= 0 ? (uint64_t)ovr : g.per_queue;
+    if (ovr != 0 && !(binds && full > thr)) return s;   // (override 0: every launch with scratch is routed)
     g.mu.lock();
-    if (!g.s && (hipStreamCreateWithFlags(&g.s, hipStreamNonBlocking) != hipSuccess ||
-                 hipEventCreateWithFlags(&g.in, hipEventDisableTiming) != hipSuccess ||
-                 hipEventCreateWithFlags(&g.out, hipEventDisableTiming) != hipSuccess)) {
-        g.s = nullptr;          // (the launch stays on the caller's stream)
-        g.mu.unlock();
-        return s;
+    if (!g.s) {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (cur != dev) (void)hipSetDevice(dev);
+        if (hipStreamCreateWithFlags(&g.s, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&g.in, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&g.out, hipEventDisableTiming) != hipSuccess)
+            g.s = nullptr;
+        if (cur >= 0 && cur != dev) (void)hipSetDevice(cur);
+        if (!g.s) {                   // (the launch stays on the caller's stream)
+            g.mu.unlock();
+            return s;
+        }
     }
     t_gate_dev = dev;
     g_gate_routed.fetch_add(1, std::memory_order_relaxed);
@@ -315,11 +386,27 @@ extern "C" void lcb_gate_exit(hipStream_t s, hipStream_t used) {
     t_gate_dev = -1;
     g.mu.unlock();
 }
+// the scratch model of the calling thread's device: out[0] pool, [1] bind limit, [2] wave slots, [3] hardware queues,
+// [4] the per-queue share T, [5] the gate threshold in force (-1 off)
+extern "C" int lcb_scratch_info(uint64_t out[6]) {
+    int dev = 0;
+    if (!out || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
+    GateDev &g = g_gate[dev];
+    gate_model(g, dev);
+    const long long ovr = gate_override();
+    out[0] = g.pool;
+    out[1] = g.bind_limit;
+    out[2] = g.slots;
+    out[3] = (uint64_t)g.hwq;
+    out[4] = g.per_queue;
+    out[5] = ovr == -1 ? ~0ull : ovr >= 0 ? (uint64_t)ovr : g.per_queue;
+    return 0;
+}
 // tuning / test hook: the gate's threshold in bytes of reservation (-1: off, 0: every launch with scratch is routed)
 extern "C" int lcb_set_scratch_gate(long long bytes) {
     if (!tuning_allowed("lcb_set_scratch_gate")) return -1;
-    gate_threshold();
-    g_gate_bytes.store(bytes < 0 ? -1 : bytes);
+    gate_override();
+    g_gate_bytes.store(bytes < -1 ? -3 : bytes);    // < -1: back to the model's per-queue share
     return 0;
 }
 // test hook: at most this many blocks in the persistent grids (lanetab.hpp workspaces), so a small batch walks several

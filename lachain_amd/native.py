@@ -95,6 +95,7 @@ _SIGS = {
     "lcb_set_coop_max": (ctypes.c_int, [ctypes.c_uint32]),
     "lcb_set_scratch_gate": (ctypes.c_int, [ctypes.c_longlong]),
     "lcb_scratch_gate_stats": (None, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "lcb_scratch_info": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64)]),
     "lcb_set_persist_blocks": (ctypes.c_int, [ctypes.c_uint32]),
     "lcb_set_verify_chunk": (ctypes.c_int, [c_size]),
     "lcb_set_fork_mode": (ctypes.c_int, [ctypes.c_int]),
@@ -810,9 +811,18 @@ def set_msm_chunk(records_per_lane):
 
 
 def set_scratch_gate(nbytes):
-    """launches whose scratch reservation reaches nbytes run on the device's gate stream (-1 = off, 0 = every launch
-    with scratch; default 4 GiB): include/lachain_bls.h lcb_set_scratch_gate"""
+    """launches whose full-device scratch exceeds nbytes run on the device's gate stream (-1 = off, 0 = every launch
+    with scratch, < -1 = the model's per-queue share): include/lachain_bls.h lcb_set_scratch_gate"""
     _tuning(lib().lcb_set_scratch_gate(int(nbytes)), "set_scratch_gate")
+
+
+def scratch_info():
+    """the device's scratch model: dict(pool, bind_limit, slots, queues, per_queue, threshold) (lcb_scratch_info)"""
+    out = (ctypes.c_uint64 * 6)()
+    if lib().lcb_scratch_info(out) != 0:
+        raise RuntimeError("lcb_scratch_info failed")
+    keys = ("pool", "bind_limit", "slots", "queues", "per_queue", "threshold")
+    return dict(zip(keys, (int(v) for v in out)))
 
 
 def scratch_gate_stats():

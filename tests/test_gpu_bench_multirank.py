@@ -22,10 +22,9 @@ def _free_port():
 
 
 def test_bench_world_size_two():
-    # bench.py's default hardware queues (eight per rank: 16 on the one GPU) and its default concurrent epoch replay.
-    # Round 4 ran this at four queues because a 7.6 KB-per-lane dispatch (k_tpke_partial_decrypt) exhausted the scratch
-    # resources with 16 (HSA_STATUS_ERROR_OUT_OF_RESOURCES, profiles/r04/r04f); round 5 holds every multi-wave kernel
-    # to <= 4 KB (tests/test_kernel_resources.py) and gates larger reservations (lcb_set_scratch_gate)
+    # bench.py's default hardware queues (the environment's: HIP's default four per priority) and its default
+    # concurrent epoch replay, two ranks on the one GPU.  Each process has its own 32 GiB scratch pool; the library's
+    # gate keeps the bound reservations of its queues within it
     env = dict(os.environ, LCB_BENCH_BACKEND="gloo", OMP_NUM_THREADS="4")
     env.pop("GPU_MAX_HW_QUEUES", None)
     env.pop("LCB_BENCH_HWQ", None)

@@ -172,7 +172,7 @@ def test_gate_forced_on_gives_identical_results(nat, tdev):
         assert nat.tpke_verify_shares(yi, [(U, V, W)], shares, batched=True) == want
         torch.cuda.synchronize(dev)
     finally:
-        nat.set_scratch_gate(4 << 30)
+        nat.set_scratch_gate(-3)                     # back to the model's per-queue share
     routed1, seen1 = nat.scratch_gate_stats()
     assert routed1 > routed0 and seen1 > seen0
     comb = d_comb.cpu().numpy().tobytes()
@@ -229,3 +229,36 @@ def test_concurrent_assemblies_two_threads(nat, tdev):
             # (counts and first indices only: a list diff of 16,384 statuses outlives the test's time limit)
             assert bad_st.size == 0 and bad_sig.size == 0, (t, rep, bad_st.size, bad_st[:16].tolist(),
                                                            bad_sig.size, bad_sig[:16].tolist())
+
+
+def test_scratch_model_bounds_the_bound_reservations(nat, tdev):
+    """round 6: the runtime binds a kernel's full-device scratch to its hardware queue; the gate's
+    per-queue share T keeps Q x T + the gate queue's 4.5 GiB within the pool, a batched TPKE verify at the default share
+    routes nothing (its largest kernel binds 2.5 GB), and a GT power (k_op_gt, 8,148 B per lane: 4.27 GB full-device)
+    is routed"""
+    import lachain_amd.mcl as mcl
+    torch, dev = tdev
+    info = nat.scratch_info()
+    assert info["slots"] >= 64 and info["queues"] >= 2 and info["threshold"] == info["per_queue"]
+    if info["pool"]:
+        assert info["queues"] * info["per_queue"] + (9 << 29) <= info["pool"]
+    full = lambda per_lane: ((per_lane + 15) // 16 * 16) * 64 * info["slots"]
+    if info["per_queue"] < full(5000):
+        pytest.skip("the environment's queue count makes the preparation kernels gated too")
+    n, f = 4, 1
+    coeffs = [o.fr(3), o.fr(9)]
+    x = [o.fr_eval_poly(coeffs, o.fr(i + 1)) for i in range(n)]
+    y = o.g1_mul(o.g1_gen(), o.fr_eval_poly(coeffs, o.fr(0)))
+    yi = [o.g1_mul(o.g1_gen(), xi) for xi in x]
+    U, V, W = o.tpke_encrypt(y, b"model test", o.fr(11))
+    shares = [(0, i, o.tpke_decrypt(U, V, W, x[i])) for i in range(n)]
+    r0, s0 = nat.scratch_gate_stats()
+    assert nat.tpke_verify_shares(yi, [(U, V, W)], shares, batched=True) == [True] * n
+    r1, s1 = nat.scratch_gate_stats()
+    assert s1 > s0 and r1 == r0
+    g = mcl.GT.Pairing(mcl.G1.Generator(), mcl.G2.Generator())
+    r1, _ = nat.scratch_gate_stats()
+    h = mcl.GT.Pow(g, mcl.Fr.FromInt(2))             # k_op_gt on the device
+    r2, _ = nat.scratch_gate_stats()
+    assert r2 > r1
+    assert h == g * g                                # (the product runs on the host)

@@ -137,3 +137,15 @@ def test_multi_wave_kernels_within_4kb_scratch(resources):
             if not n.startswith(("lcb_asm_", "_Z")) and n not in SINGLE_WAVE
             and r["private_segment_fixed_size"] > PER_CIPHERTEXT.get(n, SCRATCH_CAP)]
     assert not over, over
+
+
+def test_every_kernel_fits_the_gate_reserve(resources):
+    """the gate queue binds at most LCB_GATE_RESERVE (4.5 GiB, lcb_host.cpp): every kernel's full-device scratch
+    (per lane rounded to 16 B x 64 lanes x 256 CUs x 32 wave slots, the runtime's request) must fit it"""
+    reserve = 9 << 29
+    over = []
+    for k, r in resources.items():
+        full = ((r.get("private_segment_fixed_size", 0) + 15) // 16 * 16) * 64 * 256 * 32
+        if full > reserve:
+            over.append((k, full))
+    assert not over, over

@@ -30,7 +30,11 @@ for a in agents:
     out.append(rec)
 print(json.dumps(out))
 for p in sorted(glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties")):
-    kv = dict(l.split()[:2] for l in open(p) if l.strip())
+    try:
+        kv = dict(l.split()[:2] for l in open(p) if l.strip())
+    except OSError as e:                  # (not readable by the box's user)
+        print(p, "unreadable:", e)
+        continue
     if int(kv.get("simd_count", 0)) > 0:
         print(p, {k: kv[k] for k in kv if "scratch" in k or k in ("simd_count", "num_xcc", "max_waves_per_simd",
                                                                "cu_per_simd_array", "simd_per_cu", "array_count")})
