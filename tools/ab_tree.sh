@@ -1,0 +1,19 @@
+#!/bin/bash
+# A/B of the TPKE headline between this tree and another built tree (lachain_amd/abv/<tree>, e.g. a git archive of an
+# earlier commit built in place): each argument is "TREE:bench flags", TREE "base" for this tree.
+set -o pipefail
+TAG=${1:-abt}
+R=$GRAFT_REPO_ROOT
+mkdir -p $R/gpurun_out/$TAG
+B="--tpke-exact 0 --pattern-steps 0 --mcl-reps 0 --ts-rounds 0 --msm-sizes= --replay-n 0 --ecdsa-sigs 0 --dkg-n 0 --rs-n 0 --no-cpu-baseline"
+shift
+i=0
+for spec in "$@"; do
+  i=$((i+1))
+  tree=${spec%%:*}; flags=${spec#*:}
+  if [[ $tree == base ]]; then d=$R; else d=$R/lachain_amd/abv/$tree; fi
+  out=$R/gpurun_out/$TAG/run$i
+  (cd $d && timeout -k 10 240 python -u bench.py $B $flags > $out.txt 2> $out.err) || { echo "FAILED $spec"; tail -5 $out.err; exit 1; }
+  python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], '|', round(d['value']/1e6,3), 'M/s', round(d['ms_per_step'],2), 'ms/step, single', round(d['config'].get('single_batch_latency_ms') or 0, 2), 'ms, hwq', d['config'].get('hw_queues'))" $out.txt "$spec"
+done
+echo done
