@@ -18,11 +18,8 @@ LCB_TU_CONFIG(k_prep)
 // its line set: the hash lane (H = G2.SetHashOf(U || V), then H's line set; h_ok = the hash succeeded) and the point
 // lane (U and W decode, then W's line set with its G2 flag; ct_ok = both decode).  k_ct_ok_merge then ANDs h_ok into
 // ct_ok.  An undecodable ciphertext keeps H's real line set (ct_ok = 0 gates every use) and gets W = infinity.
-extern "C" __global__ void LCB_PREP_BOUNDS k_tpke_ct_prepare_h(const uint8_t *cts_u, const uint8_t *v_data, const u32 *v_off,
-                                                         u32 c0, u32 n_cts, u32 *lines, uint8_t *h_ok, int flags) {
-    LCB_LATENCY_PRIO();
-    u32 c = c0 + blockIdx.x * blockDim.x + threadIdx.x;     // ciphertexts [c0, n_cts)
-    if (c >= n_cts) return;
+DI void ct_prepare_h_run(u32 c, const uint8_t *cts_u, const uint8_t *v_data, const u32 *v_off, u32 *lines, uint8_t *h_ok,
+                        int flags) {
     uint8_t d[64];
     u32 v0 = v_off[c], v1 = v_off[c + 1];
     sha512_2(d, cts_u + 48 * (size_t)c, 48, v_data + v0, v1 - v0);
@@ -36,12 +33,8 @@ extern "C" __global__ void LCB_PREP_BOUNDS k_tpke_ct_prepare_h(const uint8_t *ct
     if (flags & 2) ls[LCB_LS_FLAG] = 0;
     h_ok[c] = hok;
 }
-extern "C" __global__ void LCB_PREP_BOUNDS k_tpke_ct_prepare_w(const uint8_t *cts_u, const uint8_t *cts_w, u32 c0,
-                                                         u32 n_cts, u32 *lines, uint8_t *ct_ok, uint8_t *w_g2,
-                                                         int flags) {
-    LCB_LATENCY_PRIO();
-    u32 c = c0 + blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= n_cts) return;
+DI void ct_prepare_w_run(u32 c, const uint8_t *cts_u, const uint8_t *cts_w, u32 *lines, uint8_t *ct_ok, uint8_t *w_g2,
+                        int flags) {
     g1a U;
     g2a W;
     bool ok = g1_decompress(U, cts_u + 48 * (size_t)c);
@@ -52,6 +45,35 @@ extern "C" __global__ void LCB_PREP_BOUNDS k_tpke_ct_prepare_w(const uint8_t *ct
     if (flags & 2) ls[LCB_LS_FLAG] = 0;
     ct_ok[c] = ok;
     w_g2[c] = (r & LCB_LS_IN_G2) ? 1 : 0;
+}
+extern "C" __global__ void LCB_PREP_BOUNDS k_tpke_ct_prepare_h(const uint8_t *cts_u, const uint8_t *v_data, const u32 *v_off,
+                                                         u32 c0, u32 n_cts, u32 *lines, uint8_t *h_ok, int flags) {
+    LCB_LATENCY_PRIO();
+    u32 c = c0 + blockIdx.x * blockDim.x + threadIdx.x;     // ciphertexts [c0, n_cts)
+    if (c >= n_cts) return;
+    ct_prepare_h_run(c, cts_u, v_data, v_off, lines, h_ok, flags);
+}
+extern "C" __global__ void LCB_PREP_BOUNDS k_tpke_ct_prepare_w(const uint8_t *cts_u, const uint8_t *cts_w, u32 c0,
+                                                         u32 n_cts, u32 *lines, uint8_t *ct_ok, uint8_t *w_g2,
+                                                         int flags) {
+    LCB_LATENCY_PRIO();
+    u32 c = c0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= n_cts) return;
+    ct_prepare_w_run(c, cts_u, cts_w, lines, ct_ok, w_g2, flags);
+}
+// Both lane kinds in one dispatch (fork mode 4: one high-priority stream per context): blocks [0, nb_h) are hash
+// lanes, the rest point lanes, over ciphertexts [0, n_cts).  At the box's GPU_MAX_HW_QUEUES = 4 a context's two
+// preparation streams of fork mode 3 shared hardware queues with the other batches in flight.
+extern "C" __global__ void LCB_PREP_BOUNDS k_tpke_ct_prepare_hw(const uint8_t *cts_u, const uint8_t *cts_w,
+                                                          const uint8_t *v_data, const u32 *v_off, u32 n_cts, u32 nb_h,
+                                                          u32 *lines, uint8_t *h_ok, uint8_t *ct_ok, uint8_t *w_g2,
+                                                          int flags) {
+    LCB_LATENCY_PRIO();
+    const bool hash = blockIdx.x < nb_h;
+    u32 c = (hash ? blockIdx.x : blockIdx.x - nb_h) * blockDim.x + threadIdx.x;
+    if (c >= n_cts) return;
+    if (hash) ct_prepare_h_run(c, cts_u, v_data, v_off, lines, h_ok, flags);
+    else ct_prepare_w_run(c, cts_u, cts_w, lines, ct_ok, w_g2, flags);
 }
 
 // H(m) and its line set per message (the CommonCoin preparation, ThresholdSigner.cs:44-87 hashes each coin's message):
@@ -166,4 +188,12 @@ extern "C" void lcbk_tpke_ct_prepare_h(hipStream_t s, const uint8_t *cts_u, cons
 extern "C" void lcbk_tpke_ct_prepare_w(hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, u32 c0, u32 c1, u32 *lines, uint8_t *ct_ok, uint8_t *w_g2, int flags) {
     dim3 grid((c1 - c0 + LCB_BLOCK - 1) / LCB_BLOCK);
     LCB_LAUNCH(k_tpke_ct_prepare_w, cts_u, cts_w, c0, c1, lines, ct_ok, w_g2, flags);
+}
+extern "C" void lcbk_tpke_ct_prepare_hw(hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data,
+                                        const u32 *v_off, u32 n_cts, u32 *lines, uint8_t *h_ok, uint8_t *ct_ok,
+                                        uint8_t *w_g2, int flags) {
+    if (!n_cts) return;
+    const u32 nb = (n_cts + LCB_BLOCK - 1) / LCB_BLOCK;
+    dim3 grid(2 * nb);
+    LCB_LAUNCH(k_tpke_ct_prepare_hw, cts_u, cts_w, v_data, v_off, n_cts, nb, lines, h_ok, ct_ok, w_g2, flags);
 }

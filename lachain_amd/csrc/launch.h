@@ -12,6 +12,7 @@ extern "C" void lcbk_tpke_ct_prepare(dim3 grid, hipStream_t s, const uint8_t *ct
 extern "C" void lcbk_tpke_ct_prepare_w64(hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data, const u32 *v_off, u32 n_cts, u32 *lines, uint8_t *ct_ok, int orig_cof);
 extern "C" void lcbk_tpke_ct_prepare_h(hipStream_t s, const uint8_t *cts_u, const uint8_t *v_data, const u32 *v_off, u32 c0, u32 c1, u32 *lines, uint8_t *h_ok, int flags);
 extern "C" void lcbk_tpke_ct_prepare_w(hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, u32 c0, u32 c1, u32 *lines, uint8_t *ct_ok, uint8_t *w_g2, int flags);
+extern "C" void lcbk_tpke_ct_prepare_hw(hipStream_t s, const uint8_t *cts_u, const uint8_t *cts_w, const uint8_t *v_data, const u32 *v_off, u32 n_cts, u32 *lines, uint8_t *h_ok, uint8_t *ct_ok, uint8_t *w_g2, int flags);
 extern "C" void lcbk_ct_ok_merge(hipStream_t s, uint8_t *ct_ok, const uint8_t *h_ok, u32 c0, u32 c1);
 extern "C" void lcbk_lineset_fill(dim3 grid, hipStream_t s, u32 *lines, u32 n_sets, const u32 *sets, uint8_t *w_g2);
 extern "C" void lcbk_mcl_g2_hash(hipStream_t s, u32 *io, int orig_cof);

@@ -955,16 +955,13 @@ void ctx_free(lcb_ctx *c) {
         for (auto &e : c->rlc_lev_ev) (void)hipEventDestroy(e);
     }
     if (c->fork_ready) {
-        (void)hipStreamSynchronize(c->aux);
+        for (hipStream_t x : {c->aux, c->hi, c->hi2, c->hi3})
+            if (x) {
+                (void)hipStreamSynchronize(x);
+                (void)hipStreamDestroy(x);
+            }
         for (auto &e : c->fork_ev) (void)hipEventDestroy(e);
         for (auto &e : c->prep_ev) (void)hipEventDestroy(e);
-        (void)hipStreamDestroy(c->aux);
-        (void)hipStreamSynchronize(c->hi);
-        (void)hipStreamDestroy(c->hi);
-        (void)hipStreamSynchronize(c->hi2);
-        (void)hipStreamDestroy(c->hi2);
-        (void)hipStreamSynchronize(c->hi3);
-        (void)hipStreamDestroy(c->hi3);
     }
     lcb_int::ecdsa_ctx_release(c);
     if (c->ver_ev_ready) for (auto &e : c->ver_ev) (void)hipEventDestroy(e);
@@ -1097,9 +1094,10 @@ bool tpke_shape_ok(lcb_ctx *c, size_t n_keys, size_t n_cts, const char *what) {
     }
     return true;
 }
-std::atomic<int> g_fork_mode{3};            // lcb_set_fork_mode: stream layout of the fused batched verify (1: measured
+std::atomic<int> g_fork_mode{4};            // lcb_set_fork_mode: stream layout of the fused batched verify (1: measured
                                             // 104.8 vs 117.8 ms per 1M-share TPKE step, profiles/r03/ab1; 3, the split
-                                            // preparation: 99.6 vs 103.2 ms, profiles/r03/ab8)
+                                            // preparation: 99.6 vs 103.2 ms, profiles/r03/ab8; 4, the split preparation
+                                            // in one dispatch on one high-priority stream: DESIGN.md §14.2)
 std::atomic<uint32_t> g_coop_max{32768};    // lcb_set_coop_max: batches / levels of <= this many checks use the 9-lane kernels
 std::atomic<uint32_t> g_coop_miller_max{65536};   // lcb_set_coop_miller_max: the same for the group Miller loops only
                                                   // (65536: level 1 too, 105.5 vs 106.1 ms, profiles/r03/ab2)
@@ -1621,18 +1619,34 @@ int tpke_verify_prepared_rlc(lcb_ctx *c, uint8_t *d_accept, size_t n, size_t n_k
 }
 bool fork_ready(lcb_ctx *c) {
     if (c->fork_ready) return true;
-    hipError_t e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
     int least = 0, greatest = 0;
-    if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->hi, hipStreamNonBlocking, greatest);
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->hi2, hipStreamNonBlocking, greatest);
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->hi3, hipStreamNonBlocking, greatest);
     for (auto &ev : c->fork_ev)
         if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     for (auto &ev : c->prep_ev)
         if (e == hipSuccess) e = hipEventCreate(&ev);
     if (e != hipSuccess) { set_err("batched verify: stream creation", e); return false; }
     c->fork_ready = true;
+    return true;
+}
+// fork mode 0's second normal-priority stream, created on first use
+bool aux_ready(lcb_ctx *c) {
+    if (c->aux) return true;
+    hipError_t e = hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking);
+    if (e != hipSuccess) { c->aux = nullptr; set_err("batched verify: stream creation", e); return false; }
+    return true;
+}
+// fork mode 3's two more preparation streams, created on first use: HIP hands every stream a hardware queue when it
+// is created (GPU_MAX_HW_QUEUES per priority, shared round-robin beyond that), so streams a context never uses would
+// still crowd the other contexts' queues
+bool split_ready(lcb_ctx *c) {
+    if (c->hi2) return true;
+    int least = 0, greatest = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->hi2, hipStreamNonBlocking, greatest);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->hi3, hipStreamNonBlocking, greatest);
+    if (e != hipSuccess) { set_err("batched verify: stream creation", e); return false; }
     return true;
 }
 // prepare + batched verify in one call: the randomisation (needs only the keys) runs on the context's second
@@ -1653,13 +1667,13 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
     if (!lines || !ctok || !keys || !ctg2) { set_err("device allocation failed"); return -1; }
     if (!fork_ready(c)) return -1;
     const int fm = g_fork_mode.load();
-    const bool hp = fm >= 1, prep_first = fm >= 2 && n_cts, split = fm == 3;
+    const bool hp = fm >= 1, prep_first = fm >= 2 && n_cts, split = fm >= 3, one_hi = fm == 4;
     // split mode with a census: the ciphertexts of the census shares [0, m) (indices read to the host before this call
     // launches anything; used when they all lie below a small bound c_early) are prepared first, on the preparation
     // stream, so the census runs while the bulk is prepared
     u32 c_early = 0;
     const u32 m_census = n ? census_size(n, n_keys) : 0;
-    if (n_cts && split && m_census) {
+    if (n_cts && split && !one_hi && m_census) {
         std::vector<uint32_t> ci(m_census);
         if (hipMemcpyAsync(ci.data(), d_ct, 4 * (size_t)m_census, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess) { set_err("tpke batched verify: census index read"); return -1; }
@@ -1684,6 +1698,7 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
     // mode 0: randomisation on the second stream, preparation + census on the caller's; mode 1: the latency-bound
     // preparation chain (one lane per ciphertext / line set, < 1.5 waves per SIMD) on a high-priority stream, so
     // its waves are dispatched ahead of the randomisation's 16 K waves, which run on the caller's stream
+    if (!hp && !aux_ready(c)) return -1;
     hipStream_t sr = hp ? s : c->aux, sp = hp ? c->hi : s;
     if (n) {
         if (!rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G1_JAC_BYTES, n_keys, m_census, s)) return -1;
@@ -1706,9 +1721,22 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
         // preparation stream), the rest [c_early, n_cts) beside them on the second and third streams.
         uint8_t *hok = (uint8_t *)c->rlc[18].get(n_cts);
         if (!hok) { set_err("device allocation failed"); return -1; }
+        const u32 nc = (u32)n_cts;
+        if (one_hi) {
+            // fork mode 4: both lane kinds in one dispatch on the context's one high-priority stream, then the census
+            // behind it on the same stream; a context holds one queue per priority, so three batches in flight fit
+            // the box's GPU_MAX_HW_QUEUES = 4
+            lcbk_tpke_ct_prepare_hw(sp, d_u, d_w, d_v, d_voff, nc, lines, hok, ctok, ctg2, fl);
+            hipEventRecord(c->prep_ev[2], sp);
+            if (n && rlc_points_enqueue(c, w, d_accept, n, n_keys, n_cts, d_ct, d_dec, d_ui, sr)) return -1;
+            lcbk_ct_ok_merge(sp, ctok, hok, 0, nc);
+            lines_flag_enqueue(c, 1, lines, 0, nc, sp);
+            c->unn_census = 1;
+        } else {
+        if (!split_ready(c)) return -1;
         hipStreamWaitEvent(c->hi2, c->fork_ev[0], 0);
         hipStreamWaitEvent(c->hi3, c->fork_ev[0], 0);
-        const u32 nc = (u32)n_cts, ce = c_early;
+        const u32 ce = c_early;
         c->unn_census = ce ? 0 : 1;
         if (ce) {                    // the census's ciphertexts (decode + hash per lane launched above): their
                                      // line sets on the five-lane kernel
@@ -1725,6 +1753,7 @@ int tpke_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const 
         lines_flag_enqueue(c, 1, lines, ce, nc, c->hi3);
         hipEventRecord(c->fork_ev[3], c->hi3);
         if (!ce) hipStreamWaitEvent(sp, c->fork_ev[3], 0);     // the census (below) needs every ciphertext
+        }
     } else if (n_cts) {
         lcbk_tpke_ct_prepare(dim3(nblk(n_cts)), sp, d_u, d_w, d_v, d_voff, (u32)n_cts, lines, ctok,
                              g_orig_cofactor | (g_line_mode << 1), nullptr);
@@ -1836,6 +1865,7 @@ int ts_verify_shares_rlc_fused(lcb_ctx *c, uint8_t *d_accept, size_t n, const ui
     const RlcIo io{d_pidx, d_sigs, d_midx};
     // stream layout as in tpke_verify_shares_rlc_fused (lcb_set_fork_mode; 2 acts as 1 here)
     const bool hp = g_fork_mode.load() >= 1;
+    if (!hp && !aux_ready(c)) return -1;
     hipStream_t sr = hp ? s : c->aux, sp = hp ? c->hi : s;
     if (n) {
         if (!rlc_ws(c, w, n, LCB_G1_JAC_BYTES, LCB_G2_JAC_BYTES, n_pks, census_size(n, n_pks), s)) return -1;
@@ -2180,7 +2210,7 @@ extern "C" int lcb_set_coop_miller_max(uint32_t max_checks) {
 }
 extern "C" int lcb_set_fork_mode(int mode) {
     if (!tuning_allowed("lcb_set_fork_mode")) return -1;
-    g_fork_mode.store(mode >= 1 && mode <= 3 ? mode : 0);
+    g_fork_mode.store(mode >= 1 && mode <= 4 ? mode : 0);
     return 0;
 }
 extern "C" int lcb_set_wave_priority(int on) {

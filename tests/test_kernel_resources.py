@@ -67,6 +67,7 @@ BUDGET = {
     "k_tpke_ct_prepare": (0, 3800),
     "k_tpke_ct_prepare_h": (5, 4824),
     "k_tpke_ct_prepare_w": (5, 1688),
+    "k_tpke_ct_prepare_hw": (8, 4824),        # round 6: both lane kinds in one dispatch (fork mode 4)
     "k_tpke_encrypt1": (0, 1184),
     "k_tpke_encrypt2": (0, 3976),
     "k_tpke_exact_points": (0, 704),
@@ -95,7 +96,7 @@ SCRATCH_CAP = 4096
 SINGLE_WAVE = {"k_op_grp", "k_op_pair", "k_op_gt", "k_op_debug", "k_coop_debug"}
 # one lane per ciphertext (748 waves for configs[1]'s 1M shares: a 222 MB reservation at 4.6 KB per lane), at 256
 # registers so a wave shares its SIMD with a randomisation wave (k_prep.hip)
-PER_CIPHERTEXT = {"k_tpke_ct_prepare_h": 4900, "k_ts_msg_prepare": 4900,   # (the same hash lane, one per message)
+PER_CIPHERTEXT = {"k_tpke_ct_prepare_h": 4900, "k_tpke_ct_prepare_hw": 4900, "k_ts_msg_prepare": 4900,   # (the same hash lane, one per message)
                   "k_ts_rlc_miller_census": 4200}   # the census's <= 1,024 lanes (16 waves: a 4.3 MB reservation)
 ZERO_SPILL = ["k_coop_tpke_miller", "k_msm_bucket_acc", "k_secp_verify",
               "k_rlc_census_stats", "k_rlc_suspect_split", "k_rlc_resolve", "k_tpke_rlc_sum", "k_ts_rlc_miller"]
