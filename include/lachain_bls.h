@@ -344,11 +344,13 @@ int lcb_set_coop_miller_max(uint32_t max_checks);
    is in flight.  Tuning hook (LCB_ALLOW_TUNING=1). */
 int lcb_set_verify_chunk(size_t checks);
 /* stream layout of the fused batched verifies (lcb_tpke_verify_shares_batched_dev, lcb_ts_verify_shares_batched_dev):
-   0 = randomisation on the context's second stream beside the preparation on the caller's; 1 (default) = the
+   0 = randomisation on the context's second stream beside the preparation on the caller's; 1 = the
    latency-bound preparation chain (hash-to-G2, line sets, census) on a high-priority stream and the randomisation on
-   the caller's; 2 = as 1 with the preparation's first kernel enqueued ahead of the randomisation; 3 (default) = as 2
-   with the TPKE preparation split into hash + H's line set and U / W decoding + W's line set, on two high-priority
-   streams (threshold signatures: as 1).  Decisions are unchanged. */
+   the caller's; 2 = as 1 with the preparation's first kernel enqueued ahead of the randomisation; 3 = as 2 with the
+   TPKE preparation split into hash + H's line set and U / W decoding + W's line set, on two more high-priority
+   streams; 4 (default, round 6) = the split preparation's two lane kinds in one dispatch on the one high-priority
+   stream, the census behind it, so a context uses one hardware queue per priority (threshold signatures: modes 2-4
+   act as 1).  Decisions are unchanged. */
 int lcb_set_fork_mode(int mode);
 /* the scratch gate (round 6 model): the HSA runtime binds a dispatch's FULL-device scratch
    (private segment per lane rounded to 16 B x 64 lanes x CUs x 32 wave slots) to its hardware queue whenever that is

@@ -6,7 +6,7 @@ set -o pipefail
 TAG=${1:-ab}
 R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out/$TAG
-B="--tpke-exact 0 --pattern-steps 0 --mcl-reps 0 --ts-rounds 0 --msm-sizes= --replay-n 0 --ecdsa-sigs 0 --dkg-n 0 --rs-n 0 --no-cpu-baseline"
+B="--steps 20 --warmup 5 --tpke-exact 0 --pattern-steps 0 --mcl-reps 0 --ts-rounds 0 --msm-sizes= --replay-n 0 --ecdsa-sigs 0 --dkg-n 0 --rs-n 0 --no-cpu-baseline"
 shift
 i=0
 for spec in "$@"; do
