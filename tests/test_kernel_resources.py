@@ -75,7 +75,7 @@ BUDGET = {
     "k_tpke_pd_miller": (962, 2664),          # partial decryption split in three (was k_tpke_partial_decrypt, 7,652 B)
     "k_tpke_pd_mul": (0, 992),
     "k_tpke_rlc_miller": (0, 2376),          # round 5: the two-pair loop in assembly (lcb_r_miller2); scratch = the fallback path
-    "k_tpke_rlc_points": (60, 1216),          # k_rlc_rand.hip: 248 registers, two waves per SIMD
+    "k_tpke_rlc_points": (48, 808),           # k_rlc_rand.hip: 256 registers, two waves per SIMD (round 6: lean ladder 60 -> 48)
     "k_tpke_rlc_search2a": (97, 3448),        # level-2 searches: four Fp12 values per lane, four lanes per group
     "k_tpke_rlc_search2b": (0, 3656),
     "k_tpke_rlc_sum": (0, 1168),
@@ -84,7 +84,7 @@ BUDGET = {
     "k_ts_miller": (1248, 3292),
     "k_ts_msg_prepare": (5, 4824),            # round 5: k_prep.hip at 256 registers (was 346, 0 spills, 3,688 B)
     "k_ts_rlc_miller": (0, 2524),
-    "k_ts_rlc_points": (677, 3360),           # k_rlc_rand.hip: 256 registers, two waves per SIMD (spills to scratch)
+    "k_ts_rlc_points": (594, 2328),           # k_rlc_rand.hip: 256 registers, two waves per SIMD (round 6: lean ladder 677 -> 594)
     "k_ts_rlc_sum": (26, 2136),               # round 5: binary-GCD affine conversions (spills around the two calls)
     "k_ts_rlc_wsum": (96, 992),               # round 5: binary-GCD affine conversions
     "k_ts_sign": (0, 3976),
