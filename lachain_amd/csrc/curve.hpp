@@ -45,6 +45,40 @@ template <class F> DI void jac_from_aff(jac<F> &r, const aff<F> &a) {
     if (a.inf) { jac_set_inf(r); return; }
     r.x = a.x; r.y = a.y; f_one(r.z);
 }
+// Round 6 (LCB_LEAN_FORMULAS, default): the same formulas with their operations ordered so that fewer values are live
+// at once — Z3 first (Y, Z dead after B), (Z1 + H)^2 right after HH (Z1, Z1Z1 dead) — for the kernels at a register
+// cap (the two-waves-per-SIMD randomisation lanes, the G2 ladders): dbl 7 -> 5 live values, madd 9 -> 7.
+#ifndef LCB_LEAN_FORMULAS
+#define LCB_LEAN_FORMULAS 1
+#endif
+#if LCB_LEAN_FORMULAS
+// dbl-2009-l (a = 0)
+template <class F> DI void jac_dbl(jac<F> &r, const jac<F> &p) {
+    F A, B, C, D, E, t, z3;
+    f_mul(z3, p.y, p.z);
+    f_add(z3, z3, z3);                  // Z3 = 2 Y Z
+    f_sqr(B, p.y);                      // B = Y^2           (Y, Z dead)
+    f_add(D, p.x, B);
+    f_sqr(D, D);                        // (X + B)^2
+    f_sqr(A, p.x);                      // A = X^2           (X dead)
+    f_sqr(C, B);                        // C = B^2           (B dead)
+    f_sub(D, D, A);
+    f_sub(D, D, C);
+    f_add(D, D, D);                     // D = 2((X + B)^2 - A - C)
+    f_add(E, A, A);
+    f_add(E, E, A);                     // E = 3A            (A dead)
+    f_sqr(A, E);                        // F = E^2
+    f_add(t, D, D);
+    f_sub(r.x, A, t);                   // X3 = F - 2D
+    f_sub(t, D, r.x);
+    f_mul(r.y, E, t);
+    f_add(t, C, C);
+    f_add(t, t, t);
+    f_add(t, t, t);
+    f_sub(r.y, r.y, t);                 // Y3 = E (D - X3) - 8C
+    r.z = z3;
+}
+#else
 // dbl-2009-l (a = 0)
 template <class F> DI void jac_dbl(jac<F> &r, const jac<F> &p) {
     F A, B, C, D, E, Fv, t, x3, y3, z3;
@@ -71,6 +105,7 @@ template <class F> DI void jac_dbl(jac<F> &r, const jac<F> &p) {
     f_add(z3, z3, z3);
     r.x = x3; r.y = y3; r.z = z3;
 }
+#endif
 // add-2007-bl, complete for the doubling / inverse / infinity special cases
 template <class F> DI void jac_add(jac<F> &r, const jac<F> &p, const jac<F> &q) {
     if (jac_is_inf(p)) { r = q; return; }
@@ -113,6 +148,43 @@ template <class F> DI void jac_add(jac<F> &r, const jac<F> &p, const jac<F> &q) 
     r.x = x3; r.y = y3; r.z = z3;
 }
 // madd-2007-bl: p + q with q affine (q finite)
+#if LCB_LEAN_FORMULAS
+template <class F> DI void jac_add_aff(jac<F> &r, const jac<F> &p, const F &qx, const F &qy) {
+    if (jac_is_inf(p)) { r.x = qx; r.y = qy; f_one(r.z); return; }
+    F z1z1, u2, s2, h, hh, rr, z3;
+    f_sqr(z1z1, p.z);
+    f_mul(u2, qx, z1z1);
+    f_mul(s2, qy, p.z);
+    f_mul(s2, s2, z1z1);
+    if (f_eq(u2, p.x)) {
+        if (f_eq(s2, p.y)) { jac_dbl(r, p); return; }
+        jac_set_inf(r);
+        return;
+    }
+    f_sub(h, u2, p.x);                  // H = U2 - X1
+    f_sub(rr, s2, p.y);
+    f_add(rr, rr, rr);                  // r = 2 (S2 - Y1)
+    f_sqr(hh, h);                       // HH = H^2
+    f_add(z3, p.z, h);
+    f_sqr(z3, z3);
+    f_sub(z3, z3, z1z1);
+    f_sub(z3, z3, hh);                  // Z3 = (Z1 + H)^2 - Z1Z1 - HH   (Z1, Z1Z1 dead)
+    f_add(hh, hh, hh);
+    f_add(hh, hh, hh);                  // I = 4 HH
+    f_mul(u2, h, hh);                   // J = H I                      (H dead)
+    f_mul(s2, p.x, hh);                 // V = X1 I                     (X1, I dead)
+    f_mul(h, p.y, u2);                  // Y1 J                         (Y1 dead)
+    f_sqr(hh, rr);
+    f_sub(hh, hh, u2);
+    f_sub(hh, hh, s2);
+    f_sub(r.x, hh, s2);                 // X3 = r^2 - J - 2V
+    f_sub(hh, s2, r.x);
+    f_mul(r.y, rr, hh);
+    f_add(h, h, h);
+    f_sub(r.y, r.y, h);                 // Y3 = r (V - X3) - 2 Y1 J
+    r.z = z3;
+}
+#else
 template <class F> DI void jac_add_aff(jac<F> &r, const jac<F> &p, const F &qx, const F &qy) {
     if (jac_is_inf(p)) { r.x = qx; r.y = qy; f_one(r.z); return; }
     F z1z1, u2, s2, h, hh, i, j, rr, v, t, x3, y3, z3;
@@ -148,6 +220,7 @@ template <class F> DI void jac_add_aff(jac<F> &r, const jac<F> &p, const F &qx, 
     f_sub(z3, z3, hh);
     r.x = x3; r.y = y3; r.z = z3;
 }
+#endif
 template <class F> DI void jac_neg(jac<F> &r, const jac<F> &p) { r.x = p.x; f_neg(r.y, p.y); r.z = p.z; }
 template <class F> DI void jac_to_aff(aff<F> &a, const jac<F> &p) {
     if (jac_is_inf(p)) { a.inf = true; f_zero(a.x); f_zero(a.y); return; }

@@ -20,8 +20,8 @@ BUDGET = {
     "k_coop_debug": (204, 7620),              # test hook: the one-lane reference routines beside the coop ones
     "k_coop_final_exp_check": (36, 576),
     "k_coop_final_exp_check_2w": (36, 576),   # k_prep.hip: 248 registers (every batched level); census copies at 256
-    "k_ts_rlc_sum2": (20, 2376),              # k_prep.hip: two lanes per group
-    "k_ts_rlc_sum_census": (34, 2248),
+    "k_ts_rlc_sum2": (20, 2464),              # k_prep.hip: two lanes per group
+    "k_ts_rlc_sum_census": (34, 2336),
     "k_ts_rlc_miller_census": (2, 4180),     # round 5: three quads saved around the one binary-GCD call per check
     "k_coop_tpke_miller": (0, 0),
     "k_dkg_exact_combine": (0, 312),
@@ -35,28 +35,28 @@ BUDGET = {
     "k_g1_jac_reduce_groups": (0, 168),
     "k_g1_mul": (0, 1040),
     "k_g1_mul_lanes": (0, 896),
-    "k_g1_subgroup_any": (12, 0),
+    "k_g1_subgroup_any": (24, 0),
     "k_g1_sum": (0, 752),
     "k_g1_to_affine": (0, 704),
     "k_g2_decompress": (0, 992),
-    "k_g2_hash": (0, 3400),
-    "k_g2_mul": (302, 1584),                  # 4-bit window, table in the lanetab workspace (was 10,624 B)
-    "k_g2_mul2_lanes": (4660, 2000),          # paired GLS ladders, tables in the lanetab workspace (was 22,672 B of scratch)
-    "k_g2_mul_lanes": (1212, 1424),           # GLS ladder, table in the lanetab workspace (was 10,288 B)
-    "k_g2_sum": (204, 1008),
+    "k_g2_hash": (0, 3352),
+    "k_g2_mul": (288, 1272),                  # 4-bit window, table in the lanetab workspace (was 10,624 B)
+    "k_g2_mul2_lanes": (3506, 1768),          # paired GLS ladders, tables in the lanetab workspace (was 22,672 B of scratch)
+    "k_g2_mul_lanes": (856, 952),           # GLS ladder, table in the lanetab workspace (was 10,288 B)
+    "k_g2_sum": (192, 440),
     "k_lineset_coop": (86, 280),              # five-lane line sets (latency path): T, Q, acc and five products live
     "k_lineset_fill": (0, 1256),
     "k_mcl_from_bytes": (0, 800),
     "k_mcl_g1_sum": (0, 168),
     "k_mcl_g1_terms": (0, 880),
-    "k_mcl_g2_hash": (0, 3400),               # mclBnG2_hashAndMapTo: the same one-lane hash as k_g2_hash
+    "k_mcl_g2_hash": (0, 3352),               # mclBnG2_hashAndMapTo: the same one-lane hash as k_g2_hash
     "k_mcl_horner": (0, 1320),
     "k_mcl_to_bytes": (0, 1024),
     "k_msm_bucket_fix": (0, 168),
     "k_msm_bucket_reduce": (0, 744),          # + the prefetched next bucket
     "k_msm_horner": (0, 168),
     "k_op_debug": (96, 6956),
-    "k_op_grp": (444, 4104),                  # round 6: the exponentiation routine's table in VGPRs (lcb_r_fp_pow)
+    "k_op_grp": (372, 4008),                  # round 6: the exponentiation routine's table in VGPRs (lcb_r_fp_pow)
     "k_op_gt": (1788, 8148),                  # single-lane mcl operations (one wave per dispatch), one kernel per family
     "k_op_pair": (842, 7620),
     "k_ptmul_g2": (36, 68),                   # mcl G2 multiplication latency kernel: four ladder lanes share each op (signed digits: 34)
@@ -64,30 +64,30 @@ BUDGET = {
     "k_rlc_miller_fallback": (0, 2376),
     "k_rlc_search": (106, 4056),              # round 5: baby-step giant-step (fingerprint table + the confirming power)
     "k_secp_scalars": (0, 528),
-    "k_tpke_ct_prepare": (0, 3800),
-    "k_tpke_ct_prepare_h": (5, 4824),
+    "k_tpke_ct_prepare": (0, 3752),
+    "k_tpke_ct_prepare_h": (5, 4800),
     "k_tpke_ct_prepare_w": (5, 1688),
-    "k_tpke_ct_prepare_hw": (8, 4824),        # round 6: both lane kinds in one dispatch (fork mode 4)
+    "k_tpke_ct_prepare_hw": (8, 4800),        # round 6: both lane kinds in one dispatch (fork mode 4)
     "k_tpke_encrypt1": (0, 1184),
-    "k_tpke_encrypt2": (0, 3976),
+    "k_tpke_encrypt2": (0, 3928),
     "k_tpke_exact_points": (0, 704),
     "k_tpke_miller": (0, 2376),          # round 5: the two-pair loop in assembly (lcb_r_miller2); scratch = the fallback path
     "k_tpke_pd_miller": (962, 2664),          # partial decryption split in three (was k_tpke_partial_decrypt, 7,652 B)
     "k_tpke_pd_mul": (0, 992),
     "k_tpke_rlc_miller": (0, 2376),          # round 5: the two-pair loop in assembly (lcb_r_miller2); scratch = the fallback path
-    "k_tpke_rlc_points": (48, 808),           # k_rlc_rand.hip: 256 registers, two waves per SIMD (round 6: lean ladder 60 -> 48)
+    "k_tpke_rlc_points": (36, 760),           # k_rlc_rand.hip: 256 registers, two waves per SIMD (round 6: lean ladder 60 -> 48)
     "k_tpke_rlc_search2a": (97, 3448),        # level-2 searches: four Fp12 values per lane, four lanes per group
     "k_tpke_rlc_search2b": (0, 3656),
     "k_tpke_rlc_sum": (0, 1168),
     "k_tpke_rlc_wsum": (48, 576),             # round 6: binary-GCD conversions; the live record saved around the calls
     "k_tpke_rlc_wsum2": (0, 648),
     "k_ts_miller": (1248, 3292),
-    "k_ts_msg_prepare": (5, 4824),            # round 5: k_prep.hip at 256 registers (was 346, 0 spills, 3,688 B)
+    "k_ts_msg_prepare": (5, 4800),            # round 5: k_prep.hip at 256 registers (was 346, 0 spills, 3,688 B)
     "k_ts_rlc_miller": (0, 2524),
-    "k_ts_rlc_points": (594, 2328),           # k_rlc_rand.hip: 256 registers, two waves per SIMD (round 6: lean ladder 677 -> 594)
+    "k_ts_rlc_points": (492, 2296),           # k_rlc_rand.hip: 256 registers, two waves per SIMD (round 6: lean ladder 677 -> 594)
     "k_ts_rlc_sum": (26, 2136),               # round 5: binary-GCD affine conversions (spills around the two calls)
     "k_ts_rlc_wsum": (96, 992),               # round 5: binary-GCD affine conversions
-    "k_ts_sign": (0, 3976),
+    "k_ts_sign": (0, 3928),
 }
 # Round 5: no kernel that runs on more than one wave may take more than 4 KB of scratch per lane — the
 # HIP runtime reserves a dispatch's scratch for min(waves, device wave slots) waves per hardware queue, and the 22.7 KB
