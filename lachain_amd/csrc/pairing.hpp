@@ -152,9 +152,153 @@ DI bool lineset_in_g2(const g2 &T, const g2a &Q) {
 
 #define LCB_LS_NORMALISED 1u                          // lineset_compute result bits
 #define LCB_LS_IN_G2 2u
+// Round 6 (LCB_LEAN_LINES, default): the line steps of lineset_compute with every coefficient stored to the set as soon
+// as it is formed (no `line` struct live across the step), the operations ordered so that fewer values are live at once
+// (X Y and Y Z first, then the squares; Z3 before the coefficient A), and Q re-read from the set's point slot in the
+// five addition steps instead of held across the 68 steps: the loop carries T and the prefix product only.  The same
+// operations on the same operands as line_dbl_step / line_add_step, so the same words.
+#ifndef LCB_LEAN_LINES
+#define LCB_LEAN_LINES 1
+#endif
+DI void ls_put_line(u32 *dst, int k, const fp2 &A, const fp2 &Bc, const fp2 &Cc, fp2 &acc) {
+    fp2_store_w(dst + k * LCB_NLINE_WORDS, Bc);          // not yet normalised
+    fp2_store_w(dst + k * LCB_NLINE_WORDS + 24, Cc);
+    fp2_store_w(dst + LCB_LS_A + 24 * k, A);
+    fp2_mul(acc, acc, A);
+    fp2_store_w(dst + LCB_LS_PRE + 24 * k, acc);         // A_0 ... A_k
+}
+DI void ls_dbl_store(g2 &T, u32 *dst, int k, fp2 &acc) {
+    fp2 YZ, XY, ZZ, YY, t, u;
+    fp2_mul(YZ, T.y, T.z);
+    fp2_mul(XY, T.x, T.y);
+    fp2_sqr(ZZ, T.z);                                     // (Z dead)
+    fp2_sqr(YY, T.y);                                     // (Y dead)
+    fp2_sqr(t, T.x);                                      // XX (X dead)
+    fp2_add(u, t, t);
+    fp2_add(u, u, t);
+    fp2_neg(t, u);                                        // Bc = -3 X^2
+    fp2_add(u, YZ, YZ);                                   // Cc = 2 Y Z
+    fp2_mul(T.z, YY, YZ);
+    fp2_add(T.z, T.z, T.z);                               // Z3 = 2 Y^3 Z  (YZ dead)
+    {
+        fp2 b3;
+        fp2_load_const(b3, LCB_B2_3);
+        fp2_mul(ZZ, ZZ, b3);                              // bZZ = 3 b' Z^2
+    }
+    {
+        fp2 A;
+        fp2_sub(A, YY, ZZ);                               // A = Y^2 - 3 b' Z^2
+        ls_put_line(dst, k, A, t, u, acc);
+    }
+    fp inv2;
+    fp_load_const(inv2, LCB_INV2);
+    fp2_add(t, ZZ, ZZ);
+    fp2_add(t, t, ZZ);                                    // b9 = 9 b' Z^2
+    fp2_mul_fp(XY, XY, inv2);
+    fp2_sub(u, YY, t);
+    fp2_mul(T.x, XY, u);                                  // X3 = X Y / 2 (Y^2 - 9 b' Z^2)
+    fp2_add(u, YY, t);
+    fp2_mul_fp(u, u, inv2);
+    fp2_sqr(T.y, u);
+    fp2_sqr(t, ZZ);
+    fp2_add(u, t, t);
+    fp2_add(u, u, t);
+    fp2_sub(T.y, T.y, u);                                 // Y3 = ((Y^2 + 9 b' Z^2) / 2)^2 - 27 b'^2 Z^4
+}
+DI void ls_add_store(g2 &T, u32 *dst, int k, fp2 &acc) {
+    fp2 xQ, yQ, th, la, t;
+    fp2_load_w(xQ, dst + LCB_LS_POINT);
+    fp2_load_w(yQ, dst + LCB_LS_POINT + 24);
+    fp2_mul(t, yQ, T.z);
+    fp2_sub(th, T.y, t);
+    fp2_mul(t, xQ, T.z);
+    fp2_sub(la, T.x, t);
+    {
+        fp2 A, nth;
+        fp2_mul(A, th, xQ);
+        fp2_mul(t, la, yQ);
+        fp2_sub(A, A, t);
+        fp2_neg(nth, th);
+        ls_put_line(dst, k, A, nth, la, acc);
+    }
+    fp2 D, E, G;
+    fp2_sqr(D, la);
+    fp2_mul(E, la, D);
+    fp2_mul(G, T.x, D);                                   // (X, D dead)
+    fp2_sqr(t, th);
+    fp2_mul(D, T.z, t);                                   // F = Z C
+    fp2_mul(T.z, T.z, E);                                 // Z3 = Z E
+    fp2_add(D, E, D);
+    fp2_sub(D, D, G);
+    fp2_sub(D, D, G);                                     // H = E + F - 2 G
+    fp2_mul(T.x, la, D);                                  // X3 = la H
+    fp2_sub(t, G, D);
+    fp2_mul(G, th, t);
+    fp2_mul(t, T.y, E);
+    fp2_sub(T.y, G, t);                                   // Y3 = th (G - H) - Y E
+}
+
 // the 68 lines of a G2 point (affine, possibly infinity) into dst[LCB_LINESET_WORDS], normalised to A = 1 with
 // one Fp2 inversion (Montgomery's batch trick over the 68 A's).  Returns LCB_LS_NORMALISED unless some A_k == 0
 // (flag 0), | LCB_LS_IN_G2 when Q lies in G2 (lineset_in_g2; infinity does).
+#if LCB_LEAN_LINES
+DN u32 lineset_compute(u32 *dst, const g2a &Q) {
+    fp2_store_w(dst + LCB_LS_POINT, Q.x);
+    fp2_store_w(dst + LCB_LS_POINT + 24, Q.y);
+    dst[LCB_LS_FLAG + 1] = Q.inf ? 1 : 0;
+    if (Q.inf) {                                      // every line is the constant 1: B' = C' = 0
+        fp2 z = fp2_zero();
+        for (int k = 0; k < LCB_NLINES; k++) {
+            fp2_store_w(dst + k * LCB_NLINE_WORDS, z);
+            fp2_store_w(dst + k * LCB_NLINE_WORDS + 24, z);
+        }
+        dst[LCB_LS_FLAG] = 1;
+        return LCB_LS_NORMALISED | LCB_LS_IN_G2;
+    }
+    g2 T;
+    T.x = Q.x; T.y = Q.y; T.z = fp2_one();
+    fp2 acc = fp2_one();
+    int k = 0;
+#pragma unroll 1
+    for (int i = 62; i >= 0; i--) {
+        ls_dbl_store(T, dst, k++, acc);
+        if ((LCB_Z_ABS >> i) & 1) ls_add_store(T, dst, k++, acc);
+    }
+    u32 g2m;
+    {
+        g2a Qr;
+        fp2_load_w(Qr.x, dst + LCB_LS_POINT);
+        fp2_load_w(Qr.y, dst + LCB_LS_POINT + 24);
+        Qr.inf = false;
+        g2m = lineset_in_g2(T, Qr) ? LCB_LS_IN_G2 : 0u;
+    }
+    bool ok = !fp2_is_zero(acc);
+    dst[LCB_LS_FLAG] = ok;
+    if (!ok) return g2m;
+    fp2 inv;
+    fp2_inv_gn(inv, acc);                              // (A_0 ... A_67)^-1
+#pragma unroll 1
+    for (k = LCB_NLINES - 1; k >= 0; k--) {
+        fp2 ai, a, b, c;
+        if (k > 0) {
+            fp2 pre;
+            fp2_load_w(pre, dst + LCB_LS_PRE + 24 * (k - 1));
+            fp2_mul(ai, inv, pre);                     // A_k^-1
+        } else {
+            ai = inv;
+        }
+        fp2_load_w(a, dst + LCB_LS_A + 24 * k);
+        fp2_mul(inv, inv, a);                          // (A_0 ... A_{k-1})^-1
+        fp2_load_w(b, dst + k * LCB_NLINE_WORDS);
+        fp2_load_w(c, dst + k * LCB_NLINE_WORDS + 24);
+        fp2_mul(b, b, ai);
+        fp2_mul(c, c, ai);
+        fp2_store_w(dst + k * LCB_NLINE_WORDS, b);
+        fp2_store_w(dst + k * LCB_NLINE_WORDS + 24, c);
+    }
+    return LCB_LS_NORMALISED | g2m;
+}
+#else
 DN u32 lineset_compute(u32 *dst, const g2a &Q) {
     fp2_store_w(dst + LCB_LS_POINT, Q.x);
     fp2_store_w(dst + LCB_LS_POINT + 24, Q.y);
@@ -212,6 +356,7 @@ DN u32 lineset_compute(u32 *dst, const g2a &Q) {
     }
     return LCB_LS_NORMALISED | g2m;
 }
+#endif
 
 // f *= l evaluated at P = (xP, yP)
 DI void fp12_mul_line_at(fp12 &f, const line &l, const fp &xP, const fp &yP) {

@@ -45,7 +45,7 @@ BUDGET = {
     "k_g2_mul_lanes": (856, 952),           # GLS ladder, table in the lanetab workspace (was 10,288 B)
     "k_g2_sum": (192, 440),
     "k_lineset_coop": (86, 280),              # five-lane line sets (latency path): T, Q, acc and five products live
-    "k_lineset_fill": (0, 1256),
+    "k_lineset_fill": (0, 984),
     "k_mcl_from_bytes": (0, 800),
     "k_mcl_g1_sum": (0, 168),
     "k_mcl_g1_terms": (0, 880),
@@ -66,7 +66,7 @@ BUDGET = {
     "k_secp_scalars": (0, 528),
     "k_tpke_ct_prepare": (0, 3752),
     "k_tpke_ct_prepare_h": (5, 4800),
-    "k_tpke_ct_prepare_w": (5, 1688),
+    "k_tpke_ct_prepare_w": (5, 1208),
     "k_tpke_ct_prepare_hw": (8, 4800),        # round 6: both lane kinds in one dispatch (fork mode 4)
     "k_tpke_encrypt1": (0, 1184),
     "k_tpke_encrypt2": (0, 3928),

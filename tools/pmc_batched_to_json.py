@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from bench import source_hash  # noqa: E402
 
 STEP_KERNELS = ("k_g1_decompress", "k_rlc_key_tables", "k_tpke_rlc_points", "k_rlc_groups", "k_tpke_ct_prepare",
-                "k_tpke_ct_prepare_h", "k_tpke_ct_prepare_w", "k_ct_ok_merge", "k_lineset_fill", "k_lineset_coop", "k_rlc_census_desc", "k_rlc_census_stats", "k_rlc_suspect_split",
+                "k_tpke_ct_prepare_h", "k_tpke_ct_prepare_w", "k_tpke_ct_prepare_hw", "k_ct_ok_merge", "k_lineset_fill", "k_lineset_coop", "k_rlc_census_desc", "k_rlc_census_stats", "k_rlc_suspect_split",
                 "k_tpke_rlc_sum", "k_tpke_rlc_wsum", "k_tpke_rlc_wsum2", "k_tpke_rlc_miller", "k_final_exp_check",
                 "k_coop_tpke_miller", "k_rlc_miller_fallback", "k_coop_final_exp_check", "k_rlc_resolve",
                 "k_rlc_search", "k_rlc_park_copy", "k_tpke_rlc_search2a", "k_tpke_rlc_search2b")
