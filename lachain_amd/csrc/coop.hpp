@@ -116,8 +116,22 @@ DI void cp_lin4(fp2 &o, const Cp &c, int a, int b, int cc, int d, bool fa, bool 
     fp2_cxi(x, x, fd);
     fp2_add(o, o, x);
 }
-// one product per lane: (L[xa] + L[xb]) * xi^yx (L[ya] + L[yb]) -> P[pk] (pk = -1: nothing published)
-DI void cp_prod(const Cp &c, int xa, int xb, int ya, int yb, bool yx, int pk) {
+// cp_lin4 without the fourth value's xi (no lane of the call site applies it): the wave skips one xi product and one
+// select per recombination (round 6; the squarings, line products and Fp12 products' last stage)
+DI void cp_lin3(fp2 &o, const Cp &c, int a, int b, int cc, int d, bool fa) {
+    fp2 x;
+    cp_get(o, c, a);
+    cp_get(x, c, b);
+    fp2_sub(o, o, x);
+    cp_get(x, c, cc);
+    fp2_sub(o, o, x);
+    fp2_cxi(o, o, fa);
+    cp_get(x, c, d);
+    fp2_add(o, o, x);
+}
+// one product per lane: (L[xa] + L[xb]) * xi^yx (L[ya] + L[yb]) -> P[pk] (pk = -1: nothing published); XI = false:
+// no lane applies xi (the wave skips the xi product and its select)
+template <bool XI = true> DI void cp_prod(const Cp &c, int xa, int xb, int ya, int yb, bool yx, int pk) {
     fp2 x, y, t;
     cp_get(x, c, xa);
     cp_get(t, c, xb);
@@ -125,7 +139,7 @@ DI void cp_prod(const Cp &c, int xa, int xb, int ya, int yb, bool yx, int pk) {
     cp_get(y, c, ya);
     cp_get(t, c, yb);
     fp2_add(y, y, t);
-    fp2_cxi(y, y, yx);
+    if (XI) fp2_cxi(y, y, yx);
     fp2_mul(x, x, y);
     cp_put(c, pk >= 0 ? S_P + pk : S_JUNK, x);
 }
@@ -192,7 +206,7 @@ DI void cp_sqr12(fp2 &R, const Cp &c, const CpEval &ev) {
     }
     cp_sync();
     // round A: T's six products, Q's first three
-    cp_prod(c, sel9(PK9(0, 1, 2, 1, 0, 0, A_(0), A_(1), A_(2)), j), sel9(PK9(Z_, Z_, Z_, 2, 1, 2, Z_, Z_, Z_), j),
+    cp_prod<false>(c, sel9(PK9(0, 1, 2, 1, 0, 0, A_(0), A_(1), A_(2)), j), sel9(PK9(Z_, Z_, Z_, 2, 1, 2, Z_, Z_, Z_), j),
             sel9(PK9(3, 4, 5, 4, 3, 3, A_(3), A_(4), A_(5)), j), sel9(PK9(Z_, Z_, Z_, 5, 4, 5, Z_, Z_, Z_), j), false, j);
     {   // round B: Q's cross products (lanes 0..2) + the line evaluations (lanes 3..6)
         fp2 x, y, t;
@@ -247,10 +261,10 @@ DI void cp_line(fp2 &R, const Cp &c, int sb, int sc) {
             j == 0 || j == 3 || j == 6, j);
     cp_sync();
     fp2 o;
-    cp_lin4(o, c, sel9(PK9(P_(5), P_(3), P_(4), P_(6), P_(7), P_(8), Z_, Z_, Z_), j),
+    cp_lin3(o, c, sel9(PK9(P_(5), P_(3), P_(4), P_(6), P_(7), P_(8), Z_, Z_, Z_), j),
             sel9(PK9(Z_, Z_, Z_, P_(0), P_(1), P_(2), Z_, Z_, Z_), j),
             sel9(PK9(Z_, Z_, Z_, P_(3), P_(4), P_(5), Z_, Z_, Z_), j),
-            sel9(PK9(P_(0), P_(1), P_(2), Z_, Z_, Z_, Z_, Z_, Z_), j), bit9(0x001u, j), false);
+            sel9(PK9(P_(0), P_(1), P_(2), Z_, Z_, Z_, Z_, Z_, Z_), j), bit9(0x001u, j));
     fp2_add(o, o, R);
     if (j < 6) R = o;
 }
@@ -280,10 +294,10 @@ DI void cp_cyc_sqr(fp2 &R, const Cp &c) {
     cp_sync();
     fp2 y, u;
     // F0: c0(0) = P0 + xi P1, F1: c0(1) = P3 + xi P4, F2: c0(2) = P6 + xi P7, F3: xi c1(2), F4: c1(0), F5: c1(1)
-    cp_lin4(y, c, sel9(PK9(P_(1), P_(4), P_(7), P_(8), P_(2), P_(5), Z_, Z_, Z_), j),
+    cp_lin3(y, c, sel9(PK9(P_(1), P_(4), P_(7), P_(8), P_(2), P_(5), Z_, Z_, Z_), j),
             sel9(PK9(Z_, Z_, Z_, P_(6), P_(0), P_(3), Z_, Z_, Z_), j),
             sel9(PK9(Z_, Z_, Z_, P_(7), P_(1), P_(4), Z_, Z_, Z_), j),
-            sel9(PK9(P_(0), P_(3), P_(6), Z_, Z_, Z_, Z_, Z_, Z_), j), bit9(0x00fu, j), false);
+            sel9(PK9(P_(0), P_(3), P_(6), Z_, Z_, Z_, Z_, Z_, Z_), j), bit9(0x00fu, j));
     fp2_cneg(u, R, j < 3);          // 3y - 2z (c0 outputs) or 3y + 2z (c1 outputs) = y + 2 (y -/+ z)
     fp2_add(u, u, y);
     fp2_add(u, u, u);
@@ -322,10 +336,12 @@ DI void cp_mul12(fp2 &R, const Cp &c, bool conj_a, const u32 *bslot, size_t n, s
         park_coef(y, bslot, n, i, sel9(Y0, j));
         park_coef(t, bslot, n, i, sel9(Y1, j));
         fp2_add(y, y, t);
-        park_coef(t, bslot, n, i, sel9(Y2, j));
-        fp2_add(y, y, t);
-        park_coef(t, bslot, n, i, sel9(Y3, j));
-        fp2_add(y, y, t);
+        if (r == 1) {                 // (round 0's third and fourth terms are zero for every role)
+            park_coef(t, bslot, n, i, sel9(Y2, j));
+            fp2_add(y, y, t);
+            park_coef(t, bslot, n, i, sel9(Y3, j));
+            fp2_add(y, y, t);
+        }
         fp2_mul(x, x, y);
         cp_put(c, S_P + 9 * r + j, x);
     }
@@ -342,10 +358,10 @@ DI void cp_mul12(fp2 &R, const Cp &c, bool conj_a, const u32 *bslot, size_t n, s
     cp_sync();
     {   // c0 = (T0 + xi U2, T1 + U0, T2 + U1) (lanes 0..2), c1_k = M_k - T_k - U_k (lanes 3..5)
         fp2 o;
-        cp_lin4(o, c, sel9(PK9(A_(5), A_(3), A_(4), A_(6), A_(7), A_(8), Z_, Z_, Z_), j),
+        cp_lin3(o, c, sel9(PK9(A_(5), A_(3), A_(4), A_(6), A_(7), A_(8), Z_, Z_, Z_), j),
                 sel9(PK9(Z_, Z_, Z_, A_(0), A_(1), A_(2), Z_, Z_, Z_), j),
                 sel9(PK9(Z_, Z_, Z_, A_(3), A_(4), A_(5), Z_, Z_, Z_), j),
-                sel9(PK9(A_(0), A_(1), A_(2), Z_, Z_, Z_, Z_, Z_, Z_), j), bit9(0x001u, j), false);
+                sel9(PK9(A_(0), A_(1), A_(2), Z_, Z_, Z_, Z_, Z_, Z_), j), bit9(0x001u, j));
         if (j < 6) R = o;
     }
 }
@@ -378,7 +394,7 @@ DI void cp_fp6_pair(const Cp &c, int xa, int ya, int xb, int yb) {
         const int i0 = (int)((0x001210u >> (4 * m)) & 15), i1 = (int)((0x212000u >> (4 * m)) & 15);
         const bool two = m >= 3;
         const bool on = pk < 12;
-        cp_prod(c, bx + i0, two ? bx + i1 : S_Z, by + i0, two ? by + i1 : S_Z, false, on ? pk : -1);
+        cp_prod<false>(c, bx + i0, two ? bx + i1 : S_Z, by + i0, two ? by + i1 : S_Z, false, on ? pk : -1);
     }
 }
 // R <- R^-1 (field.hpp fp12_inv / fp6_inv / fp2_inv): c0^2 and c1^2, d = c0^2 - v c1^2, d^-1 by the fp6 adjugate and
@@ -408,7 +424,7 @@ DI void cp_inv(fp2 &R, const Cp &c) {
     }
     cp_sync();
     // adjugate products: d0^2, d1 d2, d2^2, d0 d1, d1^2, d0 d2 -> P0..5
-    cp_prod(c, sel9(PK9(A_(6), A_(7), A_(8), A_(6), A_(7), A_(6), Z_, Z_, Z_), j), S_Z,
+    cp_prod<false>(c, sel9(PK9(A_(6), A_(7), A_(8), A_(6), A_(7), A_(6), Z_, Z_, Z_), j), S_Z,
             sel9(PK9(A_(6), A_(8), A_(8), A_(7), A_(7), A_(8), Z_, Z_, Z_), j), S_Z, false, j < 6 ? j : -1);
     cp_sync();
     {   // A = d0^2 - xi d1 d2, B = xi d2^2 - d0 d1, C = d1^2 - d0 d2 (lanes 0..2) -> AUX0..2
@@ -420,7 +436,7 @@ DI void cp_inv(fp2 &R, const Cp &c) {
     }
     cp_sync();
     // N = d0 A + xi (d2 B + d1 C): products d0 A, d2 B, d1 C -> P0..2
-    cp_prod(c, sel9(PK9(A_(6), A_(8), A_(7), Z_, Z_, Z_, Z_, Z_, Z_), j), S_Z,
+    cp_prod<false>(c, sel9(PK9(A_(6), A_(8), A_(7), Z_, Z_, Z_, Z_, Z_, Z_), j), S_Z,
             sel9(PK9(A_(0), A_(1), A_(2), Z_, Z_, Z_, Z_, Z_, Z_), j), S_Z, false, j < 3 ? j : -1);
     cp_sync();
     if (j == 0) {      // N^-1 = conj(N) / (a^2 + b^2): the one Fp inversion of the check (role-0 lanes only)
@@ -441,7 +457,7 @@ DI void cp_inv(fp2 &R, const Cp &c) {
     }
     cp_sync();
     // d^-1 = (A, B, C) N^-1 -> AUX6..8 (lanes 0..2)
-    cp_prod(c, j < 3 ? S_AUX + j : S_Z, S_Z, S_AUX + 3, S_Z, false, j < 3 ? j : -1);
+    cp_prod<false>(c, j < 3 ? S_AUX + j : S_Z, S_Z, S_AUX + 3, S_Z, false, j < 3 ? j : -1);
     cp_sync();
     {
         fp2 o;
