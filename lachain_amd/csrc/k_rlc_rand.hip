@@ -83,21 +83,27 @@ k_tpke_rlc_points(u32 n_cts, const g1a_st *keys, u32 n_keys, const u32 *ct_idx,
     g1a_st ks = keys[d < n_keys ? d : 0];
     ok = ok && ks.ok;
     st_to_g1a(Y, ks);
-    g1 p, q;
     if (ok && !key_suspect_live(susp, d, n_keys)) {
         u32 a, b;
         rlc_scalar(key, i, a, b);
         // share side inlined (measured 144.7 vs 148.8 ms per 1M-share step with the call), key side from the key's
-        // fixed-base table (148.8 vs 159.8 ms without)
-        g1_mul_ab_inl(p, Ui, a, b);
+        // fixed-base table (148.8 vs 159.8 ms without).  Each record is stored as soon as it is formed (round 6): the
+        // share side's point is then not live across the key side's call (its 36 words were the kernel's spills)
+        {
+            g1 p;
+            g1_mul_ab_inl(p, Ui, a, b);
+            g1_store_soa(rU, n, i, p);
+        }
+        g1 q;
         if (ktab_usable(ktab_ok, d)) g1_mul_ab_tab(q, ktab, n_keys, d, a, b);
         else g1_mul_ab_n(q, Y, a, b);
+        g1_store_soa(rY, n, i, q);
     } else {                             // an invalid (or suspect) share contributes nothing to its group
+        g1 p;
         jac_set_inf(p);
-        jac_set_inf(q);
+        g1_store_soa(rU, n, i, p);
+        g1_store_soa(rY, n, i, p);
     }
-    g1_store_soa(rU, n, i, p);
-    g1_store_soa(rY, n, i, q);
     accept[i] = ok;
 }
 

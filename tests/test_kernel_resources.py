@@ -75,7 +75,7 @@ BUDGET = {
     "k_tpke_pd_miller": (962, 2664),          # partial decryption split in three (was k_tpke_partial_decrypt, 7,652 B)
     "k_tpke_pd_mul": (0, 992),
     "k_tpke_rlc_miller": (0, 2376),          # round 5: the two-pair loop in assembly (lcb_r_miller2); scratch = the fallback path
-    "k_tpke_rlc_points": (36, 760),           # k_rlc_rand.hip: 256 registers, two waves per SIMD (round 6: lean ladder 60 -> 48)
+    "k_tpke_rlc_points": (0, 664),            # k_rlc_rand.hip: 248 registers, two waves per SIMD (round 6: 60 -> 0 spills)
     "k_tpke_rlc_search2a": (97, 3448),        # level-2 searches: four Fp12 values per lane, four lanes per group
     "k_tpke_rlc_search2b": (0, 3656),
     "k_tpke_rlc_sum": (0, 1168),
@@ -98,7 +98,7 @@ SINGLE_WAVE = {"k_op_grp", "k_op_pair", "k_op_gt", "k_op_debug", "k_coop_debug"}
 # registers so a wave shares its SIMD with a randomisation wave (k_prep.hip)
 PER_CIPHERTEXT = {"k_tpke_ct_prepare_h": 4900, "k_tpke_ct_prepare_hw": 4900, "k_ts_msg_prepare": 4900,   # (the same hash lane, one per message)
                   "k_ts_rlc_miller_census": 4200}   # the census's <= 1,024 lanes (16 waves: a 4.3 MB reservation)
-ZERO_SPILL = ["k_coop_tpke_miller", "k_msm_bucket_acc", "k_secp_verify",
+ZERO_SPILL = ["k_coop_tpke_miller", "k_tpke_rlc_points", "k_msm_bucket_acc", "k_secp_verify",
               "k_rlc_census_stats", "k_rlc_suspect_split", "k_rlc_resolve", "k_tpke_rlc_sum", "k_ts_rlc_miller"]
 
 
