@@ -286,7 +286,11 @@ extern "C" __global__ void __launch_bounds__(LCB_BLOCK) __attribute__((amdgpu_wa
             rlc_scalar(key, i, a, b);
             if (ktab_usable(ktab_ok, k)) g1_mul_ab_tab(p, ktab, n_pks, k, a, b);
             else g1_mul_ab_n(p, PK, a, b);
+#if LCB_G2AB_MEM
+            g2_mul_ab_rec(q, S, a, b, rS, n, i);         // (its addends in the output record; rS is written below)
+#else
             g2_mul_ab_inl(q, S, a, b);  // inline: 937 vs 1015 ms per 6.55M-share CommonCoin batch with the call
+#endif
         } else {
             u32 slot = atomicAdd(count, 1u);
             desc[slot] = make_uint4(i, 1, m < n_msgs ? m : 0, 1);

@@ -201,6 +201,46 @@ DI void g2_mul_ab_inl(g2 &r, const g2a &S, u32 a, u32 b) {
     }
 #endif
 }
+// The same G2 ladder with its addends read from a record slot instead of held in registers (round 6, LCB_G2AB_MEM): x,
+// y and beta x of S are stored in the output record's x, y, z words (g2_store_soa layout, wave-coalesced), read back at
+// every column (L1 / L2), and the record is overwritten with the result after the last column — 72 registers fewer live
+// across the ladder of the 256-register CommonCoin randomisation lanes
+#ifndef LCB_G2AB_MEM
+#define LCB_G2AB_MEM 1
+#endif
+DI void g2_mul_ab_rec(g2 &r, const g2a &S, u32 a, u32 b, u32 *rec, size_t n, size_t i) {
+    jac_set_inf(r);
+    if (S.inf) return;
+    {
+        g2 st;
+        st.x = S.x;
+        st.y = S.y;
+        fp beta;
+        fp_load_const(beta, LCB_G1_BETA);
+        fp2_mul_fp(st.z, S.x, beta);                     // beta x in the z words
+        g2_store_soa(rec, n, i, st);
+    }
+#pragma unroll 1
+    for (int k = 31; k >= 0; k--) {
+        jac_dbl(r, r);
+        u32 da = (a >> k) & 1, db = (b >> k) & 1;
+        if (da | db) {
+            fp2 ax, ay, x2;
+            asm volatile("" ::: "memory");
+            soa_load<24>(&ax, rec, n, i);
+            soa_load<24>(&ay, rec + (size_t)24 * n, n, i);
+            soa_load<24>(&x2, rec + (size_t)48 * n, n, i);
+            if (da & db) {                               // S + psi^4(S) = psi^2(S) = (beta x, -y)
+                ax = x2;
+                fp2_neg(ay, ay);
+            } else if (!da) {                            // psi^4(S) = (beta^2 x, y)
+                fp2_add(ax, ax, x2);
+                fp2_neg(ax, ax);
+            }
+            jac_add_aff(r, r, ax, ay);
+        }
+    }
+}
 // affine records of Jacobian points (inf = 1 for the point at infinity), optionally negated
 DI void g1_to_st(g1a_st &o, const g1 &p, bool neg) {
     g1a a;

@@ -84,7 +84,7 @@ BUDGET = {
     "k_ts_miller": (1248, 3292),
     "k_ts_msg_prepare": (5, 4800),            # round 5: k_prep.hip at 256 registers (was 346, 0 spills, 3,688 B)
     "k_ts_rlc_miller": (0, 2524),
-    "k_ts_rlc_points": (492, 2296),           # k_rlc_rand.hip: 256 registers, two waves per SIMD (round 6: lean ladder 677 -> 594)
+    "k_ts_rlc_points": (396, 1960),           # k_rlc_rand.hip: 256 registers, two waves per SIMD (round 6: 677 -> 396; G2 addends in the record)
     "k_ts_rlc_sum": (26, 2136),               # round 5: binary-GCD affine conversions (spills around the two calls)
     "k_ts_rlc_wsum": (96, 992),               # round 5: binary-GCD affine conversions
     "k_ts_sign": (0, 3928),
