@@ -32,6 +32,10 @@ def main():
                     help="1: every ciphertext is prepared (lcb_queue_tpke_prepare) before its shares are submitted, as "
                          "HoneyBadger decrypts the common subset's ciphertexts (HoneyBadger.cs:144-146) before it "
                          "handles the other validators' shares (HoneyBadger.cs:190-213); 0: first sight in a flush")
+    ap.add_argument("--prepare-stream", type=float, default=0.0,
+                    help="ciphertexts per second prepared CONTINUOUSLY by a producer thread while the callers run "
+                         "(ADVICE r5: the queue's latency with prepares arriving); callers verify shares of the "
+                         "ciphertexts prepared so far.  0: off (--prepare-ahead decides)")
     ap.add_argument("--burst", type=int, default=1,
                     help="shares a caller submits before waiting for them (1 = strict one-share-per-call)")
     args = ap.parse_args()
@@ -50,8 +54,29 @@ def main():
         for nt in [int(x) for x in args.threads.split(",")]:
             lat, bad, count = [], [0], [0]
             stop = time.perf_counter() + args.seconds
+            n_cts = len(inp["cts_list"])
+            ready = [n_cts]                             # ciphertexts whose shares may be submitted
             with nat.BatchQueue(max_batch=args.max_batch, max_delay_ms=dl) as q:
-                if args.prepare_ahead:                  # the epoch's ciphertexts, decrypted before shares arrive
+                stream = args.prepare_stream > 0
+                if stream:                              # prepares arrive while the callers run
+                    ready[0] = 0
+                    n_prep = [0]
+
+                    def producer():
+                        t0 = time.perf_counter()
+                        while ready[0] < n_cts and time.perf_counter() < stop:
+                            u, v, w = inp["cts_list"][ready[0]]
+                            q.prepare_tpke(u, v, w)
+                            ready[0] += 1
+                            n_prep[0] += 1
+                            nxt = t0 + ready[0] / args.prepare_stream
+                            while time.perf_counter() < nxt:
+                                time.sleep(0.0002)
+                    prod = threading.Thread(target=producer)
+                    prod.start()
+                    while ready[0] == 0:
+                        time.sleep(0.0005)
+                elif args.prepare_ahead:                # the epoch's ciphertexts, decrypted before shares arrive
                     for u, v, w in inp["cts_list"]:
                         q.prepare_tpke(u, v, w)
                     q.flush()
@@ -64,7 +89,9 @@ def main():
                         t0 = time.perf_counter()
                         pend = []
                         for _ in range(args.burst):
-                            y, u, v, w, ui, e = recs[idx % len(recs)]
+                            # shares of the ciphertexts prepared so far (ciphertext-major: 22 shares per ciphertext)
+                            lim = max(1, min(len(recs), 22 * ready[0]))
+                            y, u, v, w, ui, e = recs[idx % lim]
                             pend.append((q.submit_tpke(y, u, v, w, ui), e))
                             idx += nt
                         for tk, e in pend:
@@ -81,9 +108,12 @@ def main():
                 for t in th:
                     t.join()
                 elapsed = time.perf_counter() - t_start
+                if stream:
+                    prod.join()
                 st = q.stats()
             ms = np.array(lat) * 1e3
-            rows.append(dict(deadline_ms=dl, callers=nt, burst=args.burst, prepare_ahead=args.prepare_ahead, shares_per_s=count[0] / elapsed,
+            rows.append(dict(deadline_ms=dl, callers=nt, burst=args.burst, prepare_ahead=args.prepare_ahead,
+                             prepare_stream_cts_per_s=args.prepare_stream, shares_per_s=count[0] / elapsed,
                              mean_batch=st["shares"] / max(1, st["batches"]), batches=st["batches"],
                              latency_ms={"p50": float(np.percentile(ms, 50)), "p90": float(np.percentile(ms, 90)),
                                          "p99": float(np.percentile(ms, 99))},
