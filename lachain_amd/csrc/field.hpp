@@ -512,6 +512,29 @@ DI bool fp2_sqrt(fp2 &y, const fp2 &x) {
     }
     return false;
 }
+// fp2_sqrt for an x whose norm N(x) = a^2 + b^2 the caller has already found square, with nr = N(x)^((p+1)/4) (fp_sqrt's
+// root of the norm): the same root as fp2_sqrt(x) (its x.b == 0 branch included)
+DI void fp2_sqrt_normed(fp2 &y, const fp2 &x, const fp &nr) {
+    if (fp_is_zero(x.b)) { (void)fp2_sqrt(y, x); return; }
+    fp inv2;
+    fp_load_const(inv2, LCB_INV2);
+#pragma unroll 1
+    for (int k = 0; k < 2; k++) {
+        fp c, s, cs, e, t2;
+        if (k == 0) fp_add(c, x.a, nr);
+        else fp_sub(c, x.a, nr);
+        fp_mul(c, c, inv2);
+        fp_pow_const(s, c, 3);
+        fp_mul(cs, c, s);                              // c^((p+1)/4)
+        fp_mul(e, cs, s);                              // c^((p-1)/2)
+        if (fp_eq(e, fp_one())) {
+            y.a = cs;
+            fp_mul(t2, x.b, s);
+            fp_mul(y.b, t2, inv2);                     // b / (2 c^((p+1)/4)) = b s / 2
+            return;
+        }
+    }
+}
 // A square root of x in Fp2 when the caller fixes the sign itself (G2 decompression): two exponentiations instead
 // of fp2_sqrt's four per wave (its second Fp root runs whenever one lane needs it, and it ends in an inversion).
 // With t = sqrt(a^2 + b^2), c = (a + t)/2 and s = c^((p-3)/4): if c is a square, y = (c s, b s / 2) (c s = c^((p+1)/4)

@@ -98,6 +98,9 @@ DI void fp_set_hash_digest(fp &r, const uint8_t d[64]) {
 }
 
 // MapTo::calcBN<G2, Fp2>
+#ifndef LCB_SVDW_UNIFORM
+#define LCB_SVDW_UNIFORM 1
+#endif
 DI bool g2_calc_bn(g2 &P, const fp2 &t) {
     // mcl's sign: the Legendre symbol of N(t).  For the hash's t = (t.a, 0), N(t) = t.a^2 is a square, so the symbol
     // is 1 unless t = 0 — no exponentiation needed
@@ -123,6 +126,53 @@ DI bool g2_calc_bn(g2 &P, const fp2 &t) {
     fp2_inv_g(w, w);
     fp2_mul_fp(w, w, c1);
     fp2_mul(w, w, t);
+#if LCB_SVDW_UNIFORM
+    // Round 6: the first candidate whose g(x) = x^3 + b is a square, found with ONE exponentiation per candidate (the
+    // root of the norm, which fp2_sqrt takes first and which tells squareness), all three tested for every lane, then
+    // one fp2_sqrt of the chosen value from that root (fp2_sqrt_normed: the same root as fp2_sqrt).  The loop with an
+    // early exit ran up to three exponentiations per candidate for the wave whenever any lane needed them (9 per wave
+    // against 5 here); the selected x, and so H, is the same.
+    fp2 xs, ts;
+    fp ns;
+    bool found = false;
+#pragma unroll 1
+    for (int i = 0; i < 3; i++) {
+        if (i == 0) {
+            fp2_mul(x, t, w);
+            fp2_neg(x, x);
+            fp_add(x.a, x.a, c2);
+        } else if (i == 1) {
+            fp2_neg(x, x);
+            fp_sub(x.a, x.a, one);
+        } else {
+            fp2_sqr(x, w);
+            fp2_inv_g(x, x);
+            fp_add(x.a, x.a, one);
+        }
+        fp2_sqr(tmp, x);
+        fp2_mul(tmp, tmp, x);
+        fp2_add(tmp, tmp, b2);
+        fp n, nr;
+        {
+            fp u;
+            fp_sqr(n, tmp.a);
+            fp_sqr(u, tmp.b);
+            fp_add(n, n, u);                      // N(g(x)): a square iff g(x) is one
+        }
+        const bool sq = fp_sqrt(nr, n);
+        if (!found && sq) {
+            found = true;
+            xs = x;
+            ts = tmp;
+            ns = nr;
+        }
+    }
+    if (!found) return false;
+    fp2_sqrt_normed(y, ts, ns);
+    if (negative) fp2_neg(y, y);
+    P.x = xs; P.y = y; P.z = fp2_one();
+    return true;
+#else
     for (int i = 0; i < 3; i++) {
         if (i == 0) {
             fp2_mul(x, t, w);
@@ -146,13 +196,25 @@ DI bool g2_calc_bn(g2 &P, const fp2 &t) {
         }
     }
     return false;
+#endif
 }
 // Budroni-Pintore: (z^2 - z - 1) P + psi((z - 1) P) + psi^2(2P), z = -|z|
 // the cofactor clearing's two 64-bit ladders with the group operations inlined (measured faster than the calls)
 #define H2G2_MUL_U64(r, p, k) jac_mul_u64_inl(r, p, k)
+// [k] P for P with Z = 1 (the map's output): mixed additions (7M + 4S over Fp2 instead of 11M + 5S); the same point
+DI void g2_mul_u64_z1_inl(g2 &r, const g2 &p, u64 k) {
+    int top = 63 - __clzll(k);
+    g2 acc = p;
+#pragma unroll 1
+    for (int i = top - 1; i >= 0; i--) {
+        jac_dbl(acc, acc);
+        if ((k >> i) & 1) jac_add_aff(acc, acc, p.x, p.y);
+    }
+    r = acc;
+}
 DI void g2_clear_cofactor_bp(g2 &Q, const g2 &P) {
     g2 T0, T1, T2;
-    H2G2_MUL_U64(T0, P, LCB_Z_ABS + 1);   // |z - 1| P
+    g2_mul_u64_z1_inl(T0, P, LCB_Z_ABS + 1);   // |z - 1| P   (P.z = 1: g2_calc_bn)
     jac_neg(T0, T0);                     // (z - 1) P
     H2G2_MUL_U64(T1, T0, LCB_Z_ABS);
     jac_neg(T1, T1);                     // z (z - 1) P
