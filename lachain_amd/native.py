@@ -855,7 +855,8 @@ def set_coop_miller_max(max_checks):
 def set_fork_mode(mode):
     """stream layout of the fused batched verify (include/lachain_bls.h lcb_set_fork_mode): 0 = randomisation on a
     second stream, 1 = preparation chain on a high-priority stream, 2 = 1 with the preparation enqueued first,
-    3 (default) = 2 with the TPKE preparation split into hash / decode lanes on two high-priority streams"""
+    3 = 2 with the TPKE preparation split into hash / decode lanes on two more high-priority streams, 4 (default) = the
+    split lanes in one dispatch on the one high-priority stream (one hardware queue per priority per context)"""
     _tuning(lib().lcb_set_fork_mode(mode), "set_fork_mode")
 
 

@@ -425,10 +425,11 @@ def test_batched_w_small_order(nat, tdev, fused):
     assert [int(x) for x in exact] == expect
 
 
-@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, 4])
 def test_batched_fork_modes(nat, tdev, mode):
     """every stream layout of the fused call (lcb_set_fork_mode; 3 = split preparation: hash + H's line set and
-    U / W decode + W's line set in separate lanes, validity merged afterwards) decides as the oracle: undecodable U,
+    U / W decode + W's line set in separate lanes, validity merged afterwards; 4, the default = both lane kinds in one
+    dispatch on one high-priority stream, the census behind it) decides as the oracle: undecodable U,
     undecodable W, W of order 13, wrong shares, 65,536 shares so the census runs"""
     b = Batch(b"gpu-batched-fork-modes", 8, 2, 5)
     u, v, w = b.cts[1]
@@ -454,7 +455,7 @@ def test_batched_fork_modes(nat, tdev, mode):
         got = run_dev(nat, tdev, b, ct, dec, b"".join(base) * reps, fused=True)
         levels, ms = nat.tpke_batched_stats()
     finally:
-        nat.set_fork_mode(3)
+        nat.set_fork_mode(4)
     assert np.array_equal(got, np.tile(np.array(expect, dtype=np.uint8), reps))
     assert (ms[5] > 0) == (mode != 0)
 
@@ -487,9 +488,13 @@ def test_batched_census_ciphertexts_first(nat, tdev, scatter):
         dec[[0, 1]] = dec[[-1, -2]]
     shares = b"".join(base[(int(c) % 5) * 8 + int(j)] for c, j in zip(ct, dec))
     expect = np.array([expect5[(int(c) % 5) * 8 + int(j)] for c, j in zip(ct, dec)], dtype=np.uint8)
-    got = run_dev(nat, tdev, bb, ct, dec, shares, fused=True)
+    try:
+        nat.set_fork_mode(3)                                     # (the census-first ordering is fork mode 3's)
+        got = run_dev(nat, tdev, bb, ct, dec, shares, fused=True)
+        m, n_susp, groups, entries = nat.batched_census()
+    finally:
+        nat.set_fork_mode(4)
     assert np.array_equal(got, expect)
-    m, n_susp, groups, entries = nat.batched_census()
     assert m == 512
 
 
