@@ -126,20 +126,6 @@ extern "C" __global__ void LCB_PAIR_BOUNDS k_ts_rlc_miller(const u32 *lines, con
 }
 
 // ---------------------------------------------------------------- resolve a level (TPKE and TS)
-// The shares of group d that still need a check of their own, as singles of kind w (0: a group of one randomized
-// share, 1: an exact single): not those already rejected, nor those of suspect keys (they have exact singles since
-// level 1).
-DI void emit_singles(const uint4 &d, u32 w, const uint8_t *accept, const u32 *key_idx, u32 n_keys, const u32 *susp,
-                     uint4 *next, u32 *next_count) {
-    u32 cnt = 0;
-    for (u32 k = 0; k < d.y; k++)
-        cnt += accept[d.x + k] && !key_suspect(susp, key_idx[d.x + k], n_keys);
-    if (!cnt) return;
-    u32 slot = atomicAdd(next_count, cnt);
-    for (u32 k = 0; k < d.y; k++)
-        if (accept[d.x + k] && !key_suspect(susp, key_idx[d.x + k], n_keys))
-            next[slot++] = make_uint4(d.x + k, 1, d.z, w);
-}
 // Groups [o, o + m) of this level, decided by the final-exponentiation chunk park (stride m).  A failed group of one
 // share rejects it.  At level 1 (first) a failed group of len > 1 goes to the search list (its gamma copied out of the
 // park); below level 1 it becomes ceil(len / s) sub-groups of s = ceil(len / ceil(sqrt(len))) shares, or single
@@ -203,22 +189,6 @@ extern "C" __global__ void LCB_BOUNDS k_rlc_park_copy(const u32 *park, u32 o, u3
 #pragma unroll
     for (int q = 0; q < 36; q++) d[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
 }
-DI void fp12_load_row(fp12 &f, const u32 *row) {
-    u32 *w = (u32 *)&f;
-    const uint4 *src = (const uint4 *)row;
-#pragma unroll
-    for (int q = 0; q < 36; q++) {
-        uint4 v = src[q];
-        w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
-    }
-}
-DI bool fp12_words_eq(const fp12 &a, const fp12 &b) {
-    const u32 *x = (const u32 *)&a, *y = (const u32 *)&b;
-    u32 d = 0;
-#pragma unroll
-    for (int q = 0; q < 144; q++) d |= x[q] ^ y[q];
-    return d == 0;
-}
 // r = a^e for a in the cyclotomic subgroup (GT), e >= 1
 DN void gt_pow_small(fp12 &r, const fp12 &a, u32 e) {
     fp12 t = a;
@@ -243,17 +213,6 @@ DN void gt_half_scan(fp12 &x) {
         for (int q = 0; q < 144; q++) yw[q] = (u32)__shfl_up((int)xw[q], off, 32);
         if (j >= off) fp12_mul_n(x, x, y);
     }
-}
-DI u32 fp12_fingerprint(const fp12 &a) {
-    const u32 *w = (const u32 *)&a;
-    u32 h = 0;
-#pragma unroll
-    for (int q = 0; q < 144; q++) h = ((h << 5) | (h >> 27)) ^ w[q];
-    return h;
-}
-DI u32 half_ballot(bool p) {
-    const unsigned long long m = __ballot(p);
-    return (u32)(m >> (32 * ((threadIdx.x >> 5) & 1)));
 }
 // Level 2: search entries [o, o + m): gamma' (the weighted group check's final-exponentiation output, park stride m)
 // against gamma^c, c = 1..len.  A match rejects share c - 1 of the group (the only bad one, see the header); no match

@@ -1,6 +1,7 @@
 // lachain_amd/csrc/k_tpke.hip — gfx950 kernels: TPKE decryption-share pipeline (decompression, per-ciphertext preparation, per-share verification, partial decryption).
 #include "kcommon.hpp"
 #include "fe_asm.hpp"
+#include "rlc_common.hpp"
 
 LCB_ASM_LIBRARY(k_tpke)
 LCB_TU_CONFIG(k_tpke)
@@ -237,4 +238,116 @@ extern "C" void lcbk_tpke_pd_miller(hipStream_t s, const u32 *lines, const uint8
 extern "C" void lcbk_tpke_pd_mul(hipStream_t s, const uint8_t *cts_u, const void *x_raw, u32 x_stride, u32 c0, u32 m, const uint8_t *status, uint8_t *ui_out) {
     dim3 grid((m + LCB_BLOCK - 1) / LCB_BLOCK);
     LCB_LAUNCH(k_tpke_pd_mul, cts_u, (const fr *)x_raw, x_stride, c0, m, status, ui_out);
+}
+
+// ================================================================================= level-2 two-error search (TPKE)
+// k_tpke_rlc_search2b (k_batch.hip: the algorithm and its proof) with every Fp12 product and squaring on the assembly
+// routines (asm_tower.hpp lcb_r_fp12_mul_n / lcb_r_cyc_sqr_n) over per-lane park slots, instead of the compiled
+// products that passed three Fp12 values through the lane's stack each (round 6: 133 KB of HBM traffic per lane, and
+// the level's longest kernel on the single batch's critical path).  The same products in the same order on canonical
+// values, so the same words, fingerprints and decisions.  Slots (n = the launch's lanes, 144 words each): X, Y (the
+// scans), D, E0 / E1 (the giant steps), the baby powers D^1 .. D^6.
+#define S2B_SLOTS 11
+DI void s2b_half_scan(u32 *SX, u32 *SY, size_t n, size_t i, u32 n16, u32 i16, u32 la) {
+    const u32 j = threadIdx.x & 31;
+#pragma unroll 1
+    for (u32 off = 1; off < 32; off <<= 1) {          // x <- x_0 x_1 ... x_j (the lanes below off multiply by 1)
+        fp12 x, y;
+        fp12_load_soa_fresh(x, SX, n, i);
+        u32 *yw = (u32 *)&y;
+        const u32 *xw = (const u32 *)&x;
+#pragma unroll
+        for (int q = 0; q < 144; q++) yw[q] = (u32)__shfl_up((int)xw[q], off, 32);
+        if (j < off) y = fp12_one();
+        fp12_store_soa(SY, n, i, y);
+        lcb_asm_fp12_mul_n(SX, 0, SY, SX, SX, n16, i16, la);
+    }
+}
+extern "C" __global__ void __launch_bounds__(64) k_tpke_rlc_search2b_asm(const uint4 *search, u32 ns, const u32 *gamma0,
+                                                                        const u32 *gamma12, const u32 *open,
+                                                                        const u32 *open_count, uint8_t *accept,
+                                                                        uint4 *next, u32 *next_count,
+                                                                        const u32 *key_idx, u32 n_keys,
+                                                                        const u32 *susp, u32 *park) {
+    __shared__ uint4 lds[36 * 64];
+    LCB_LATENCY_PRIO();
+    const u32 j = threadIdx.x & 31, k = blockIdx.x * 2 + (threadIdx.x >> 5);
+    if (blockIdx.x * 2 >= *open_count) return;          // (uniform per block)
+    const bool live = k < *open_count;
+    const u32 g = live ? open[k] : 0;
+    const uint4 d = live ? search[g] : make_uint4(0, 0, 0, 0);
+    const bool cand = live && j < d.y && accept[d.x + j] && !key_suspect(susp, key_idx[d.x + j], n_keys);
+    const u32 cj = j + 1;
+    const size_t n = (size_t)gridDim.x * 64, i = (size_t)blockIdx.x * 64 + threadIdx.x;
+    const u32 n16 = (u32)(n * 16), i16 = (u32)(i * 16), la = lane_lds36(lds);
+    u32 *SX = park, *SY = park + 144 * n, *SD = park + 288 * n, *SE0 = park + 432 * n, *SE1 = park + 576 * n;
+    u32 *BP = park + 720 * n;                           // D^(k + 1) at BP + 144 n k
+    fp12 t;
+    fp12_load_row(t, gamma0 + (size_t)g * 144);
+    fp12_store_soa(SX, n, i, t);
+    s2b_half_scan(SX, SY, n, i, n16, i16, la);          // gamma_0^(c_j)
+    fp12_load_row(t, gamma12 + (size_t)g * 144);
+    fp12_store_soa(SE0, n, i, t);                       // gamma_c
+    lcb_asm_fp12_mul_n(SX, 1, SE0, SD, SD, n16, i16, la);        // D_j = gamma_c / gamma_0^(c_j)
+    s2b_half_scan(SE0, SY, n, i, n16, i16, la);         // gamma_c^(c_j)
+    fp12_load_row(t, gamma12 + (size_t)g * 144);
+    fp12_store_soa(SE1, n, i, t);
+    lcb_asm_fp12_mul_n(SE0, 0, SE1, SX, SX, n16, i16, la);       // gamma_c^(c_j + 1)
+    fp12_load_row(t, gamma12 + ((size_t)ns + g) * 144); // gamma_t
+    fp12_store_soa(SE1, n, i, t);
+    lcb_asm_cyc_sqr_n(SE1, SE1, n16, i16, 1);
+    lcb_asm_fp12_mul_n(SX, 1, SE1, SE0, SE0, n16, i16, la);      // E_j = gamma_t^2 / gamma_c^(c_j + 1)
+    // baby steps: fingerprints of D^1 .. D^6 (every lane: the products stay uniform across the wave)
+    u32 fpb[6];
+    fp12_load_soa_fresh(t, SD, n, i);
+    fpb[0] = fp12_fingerprint(t);
+    fp12_store_soa(BP, n, i, t);
+#pragma unroll 1
+    for (int kk = 1; kk < 6; kk++) {
+        u32 *dst = BP + 144 * n * (size_t)kk;
+        lcb_asm_fp12_mul_n(BP + 144 * n * (size_t)(kk - 1), 0, SD, dst, dst, n16, i16, la);
+        fp12_load_soa_fresh(t, dst, n, i);
+        fpb[kk] = fp12_fingerprint(t);
+    }
+    // giant steps Y_i = E D^(-6 i): a fingerprint match Y_i ~ D^(k+1) confirmed against the stored baby power
+    u32 found = 0;
+    u32 *Y = SE0, *Yn = SE1;
+#pragma unroll 1
+    for (int gi = 0; gi < 6; gi++) {
+        fp12_load_soa_fresh(t, Y, n, i);
+        const u32 h = fp12_fingerprint(t);
+#pragma unroll 1
+        for (int kk = 0; kk < 6; kk++) {
+            const u32 c = 6 * gi + kk + 1;
+            if (cand && !found && h == fpb[kk] && c <= d.y && c != cj) {
+                fp12 chk;
+                fp12_load_soa_fresh(chk, BP + 144 * n * (size_t)kk, n, i);
+                if (fp12_words_eq(chk, t)) found = c;
+            }
+        }
+        if (gi < 5) {
+            lcb_asm_fp12_mul_n(BP + 144 * n * 5, 1, Y, Yn, Yn, n16, i16, la);   // Y D^-6 (D unitary)
+            u32 *sw = Y;
+            Y = Yn;
+            Yn = sw;
+        }
+    }
+    const u32 m2 = half_ballot(found != 0);
+    const u32 m3 = half_ballot(found != 0 && !((m2 >> ((found - 1) & 31u)) & 1u));
+    if (__popc(m2) == 2 && !m3) {
+        if (found) accept[d.x + j] = 0;
+    } else if (live && j == 0) {
+        emit_singles(d, 0, accept, key_idx, n_keys, susp, next, next_count);
+    }
+}
+extern "C" size_t lcbk_tpke_rlc_search2b_asm_park_bytes(u32 n_open) {
+    return (size_t)((n_open + 1) / 2) * 64 * S2B_SLOTS * 576;
+}
+extern "C" void lcbk_tpke_rlc_search2b_asm(hipStream_t s, const void *search, u32 ns, u32 n_open, const u32 *gamma0,
+                                           const u32 *gamma12, const u32 *open, const u32 *open_count, uint8_t *accept,
+                                           void *next, u32 *next_count, const u32 *key_idx, u32 n_keys,
+                                           const u32 *susp, u32 *park) {
+    if (!n_open) return;
+    LCB_LAUNCH_GATED(k_tpke_rlc_search2b_asm, dim3((n_open + 1) / 2), dim3(64), 0, s, (const uint4 *)search, ns, gamma0,
+                     gamma12, open, open_count, accept, (uint4 *)next, next_count, key_idx, n_keys, susp, park);
 }

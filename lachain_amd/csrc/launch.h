@@ -106,6 +106,8 @@ extern "C" void lcbk_tpke_rlc_search2a(hipStream_t s, const void *search, u32 ns
 extern "C" int lcbk_search2b_by_position(void);
 extern "C" int lcbk_search2b_debug(void *p);
 extern "C" void lcbk_tpke_rlc_search2b(hipStream_t s, const void *search, u32 ns, u32 n_open, const u32 *gamma0, const u32 *gamma12, const u32 *open, const u32 *open_count, uint8_t *accept, void *next, u32 *next_count, const u32 *key_idx, u32 n_keys, const u32 *susp);
+extern "C" void lcbk_tpke_rlc_search2b_asm(hipStream_t s, const void *search, u32 ns, u32 n_open, const u32 *gamma0, const u32 *gamma12, const u32 *open, const u32 *open_count, uint8_t *accept, void *next, u32 *next_count, const u32 *key_idx, u32 n_keys, const u32 *susp, u32 *park);
+extern "C" size_t lcbk_tpke_rlc_search2b_asm_park_bytes(u32 n_open);
 extern "C" void lcbk_rlc_search(dim3 grid, hipStream_t s, const void *search, u32 o, u32 m, const u32 *gamma, const u32 *park, uint8_t *accept, void *next, u32 *next_count, const u32 *key_idx, u32 n_keys, const u32 *susp);
 extern "C" void lcbk_rlc_census_desc(hipStream_t s, const u32 *grp_idx, const u32 *key_idx, u32 m, u32 n_grp, u32 n_keys, void *desc, uint8_t *accept);
 extern "C" void lcbk_rlc_census_stats(hipStream_t s, const u32 *key_idx, u32 m, u32 n_keys, const uint8_t *cval, const uint8_t *accept, u32 *susp, u32 *count);

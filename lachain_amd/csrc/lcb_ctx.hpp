@@ -78,7 +78,7 @@ struct lcb_ctx {
     hipEvent_t ver_ev[3] = {};
     bool ver_ev_ready = false, ver_ran = false;
     // randomized batch verification (k_batch.hip): r_i U_i / r_i Y_i records, group lists, group points, counts
-    DevBuf rlc[19];                   // [12]: the keys' fixed-base tables, [13] suspect-key bitmap, [14] census validity,
+    DevBuf rlc[20];                   // [12]: the keys' fixed-base tables, [13] suspect-key bitmap, [14] census validity,
                                       // [15] coop Miller fallback flags, [16] TPKE level-2 gamma_c / gamma_t rows, [17] its open groups,
                                       // [18] H's hash validity (split preparation, fork mode 3)
     hipEvent_t rlc_ev[3] = {};

@@ -1094,6 +1094,10 @@ bool tpke_shape_ok(lcb_ctx *c, size_t n_keys, size_t n_cts, const char *what) {
     }
     return true;
 }
+// level-2 two-error search on the assembly Fp12 products (k_tpke.hip k_tpke_rlc_search2b_asm, round 6)
+#ifndef LCB_SEARCH2B_ASM
+#define LCB_SEARCH2B_ASM 1
+#endif
 std::atomic<int> g_fork_mode{4};            // lcb_set_fork_mode: stream layout of the fused batched verify (1: measured
                                             // 104.8 vs 117.8 ms per 1M-share TPKE step, profiles/r03/ab1; 3, the split
                                             // preparation: 99.6 vs 103.2 ms, profiles/r03/ab8; 4, the split preparation
@@ -1558,8 +1562,15 @@ int rlc_levels(lcb_ctx *c, RlcKind kind, RlcWs &w, uint8_t *d_accept, size_t n, 
                            sdesc + ns, g12 + (size_t)ns * 144, d_accept, io, s,
                            lcbk_search2b_by_position() ? nullptr : open + 4);
                 void *dbg = search2b_dump(s, "in", ns, no, gamma, g12, open, d_accept, n);
+#if LCB_SEARCH2B_ASM
+                u32 *s2b_park = (u32 *)c->rlc[19].get(lcbk_tpke_rlc_search2b_asm_park_bytes(no));
+                if (!s2b_park) { set_err("device allocation failed (level-2 search slots)"); return -1; }
+                lcbk_tpke_rlc_search2b_asm(s, sdesc, ns, no, gamma, g12, open + 4, open, d_accept, w.dB, w.cnt + 1,
+                                           io.d_key, (u32)K.n_keys, w.susp, s2b_park);
+#else
                 lcbk_tpke_rlc_search2b(s, sdesc, ns, no, gamma, g12, open + 4, open, d_accept, w.dB, w.cnt + 1,
                                        io.d_key, (u32)K.n_keys, w.susp);
+#endif
                 search2b_dump(s, "out", ns, no, gamma, g12, open, d_accept, n, dbg);
             }
             if (!launched("batched verify launch")) return -1;

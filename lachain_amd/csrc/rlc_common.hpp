@@ -326,3 +326,46 @@ DI bool ktab_usable(const uint8_t *ktab_ok, u32 k) {      // all LCB_KTAB_LANES 
 }
 static_assert(LCB_KTAB_CHUNK * LCB_KTAB_CHUNKS >= 255 && LCB_KTAB_CHUNK * (LCB_KTAB_CHUNKS - 1) < 255, "key-table chunks");
 static_assert(LCB_KTAB_LANES == 4 * LCB_KTAB_CHUNKS && LCB_KTAB_LANES % 16 == 0, "key-table lanes");
+
+// ---------------------------------------------------------------- level helpers shared by k_batch.hip and k_tpke.hip
+// The shares of group d that still need a check of their own, as singles of kind w (0: a group of one randomized
+// share, 1: an exact single): not those already rejected, nor those of suspect keys (they have exact singles since
+// level 1).
+DI void emit_singles(const uint4 &d, u32 w, const uint8_t *accept, const u32 *key_idx, u32 n_keys, const u32 *susp,
+                     uint4 *next, u32 *next_count) {
+    u32 cnt = 0;
+    for (u32 k = 0; k < d.y; k++)
+        cnt += accept[d.x + k] && !key_suspect(susp, key_idx[d.x + k], n_keys);
+    if (!cnt) return;
+    u32 slot = atomicAdd(next_count, cnt);
+    for (u32 k = 0; k < d.y; k++)
+        if (accept[d.x + k] && !key_suspect(susp, key_idx[d.x + k], n_keys))
+            next[slot++] = make_uint4(d.x + k, 1, d.z, w);
+}
+DI void fp12_load_row(fp12 &f, const u32 *row) {
+    u32 *w = (u32 *)&f;
+    const uint4 *src = (const uint4 *)row;
+#pragma unroll
+    for (int q = 0; q < 36; q++) {
+        uint4 v = src[q];
+        w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+}
+DI bool fp12_words_eq(const fp12 &a, const fp12 &b) {
+    const u32 *x = (const u32 *)&a, *y = (const u32 *)&b;
+    u32 d = 0;
+#pragma unroll
+    for (int q = 0; q < 144; q++) d |= x[q] ^ y[q];
+    return d == 0;
+}
+DI u32 fp12_fingerprint(const fp12 &a) {
+    const u32 *w = (const u32 *)&a;
+    u32 h = 0;
+#pragma unroll
+    for (int q = 0; q < 144; q++) h = ((h << 5) | (h >> 27)) ^ w[q];
+    return h;
+}
+DI u32 half_ballot(bool p) {
+    const unsigned long long m = __ballot(p);
+    return (u32)(m >> (32 * ((threadIdx.x >> 5) & 1)));
+}

@@ -39,7 +39,7 @@ BUDGET = {
     "k_g1_sum": (0, 752),
     "k_g1_to_affine": (0, 704),
     "k_g2_decompress": (0, 992),
-    "k_g2_hash": (0, 3352),
+    "k_g2_hash": (0, 3400),
     "k_g2_mul": (288, 1272),                  # 4-bit window, table in the lanetab workspace (was 10,624 B)
     "k_g2_mul2_lanes": (3506, 1768),          # paired GLS ladders, tables in the lanetab workspace (was 22,672 B of scratch)
     "k_g2_mul_lanes": (856, 952),           # GLS ladder, table in the lanetab workspace (was 10,288 B)
@@ -49,7 +49,7 @@ BUDGET = {
     "k_mcl_from_bytes": (0, 800),
     "k_mcl_g1_sum": (0, 168),
     "k_mcl_g1_terms": (0, 880),
-    "k_mcl_g2_hash": (0, 3352),               # mclBnG2_hashAndMapTo: the same one-lane hash as k_g2_hash
+    "k_mcl_g2_hash": (0, 3400),               # mclBnG2_hashAndMapTo: the same one-lane hash as k_g2_hash
     "k_mcl_horner": (0, 1320),
     "k_mcl_to_bytes": (0, 1024),
     "k_msm_bucket_fix": (0, 168),
@@ -64,12 +64,12 @@ BUDGET = {
     "k_rlc_miller_fallback": (0, 2376),
     "k_rlc_search": (106, 4056),              # round 5: baby-step giant-step (fingerprint table + the confirming power)
     "k_secp_scalars": (0, 528),
-    "k_tpke_ct_prepare": (0, 3752),
+    "k_tpke_ct_prepare": (0, 3800),
     "k_tpke_ct_prepare_h": (5, 4800),
     "k_tpke_ct_prepare_w": (5, 1208),
     "k_tpke_ct_prepare_hw": (8, 4800),        # round 6: both lane kinds in one dispatch (fork mode 4)
     "k_tpke_encrypt1": (0, 1184),
-    "k_tpke_encrypt2": (0, 3928),
+    "k_tpke_encrypt2": (0, 3976),
     "k_tpke_exact_points": (0, 704),
     "k_tpke_miller": (0, 2376),          # round 5: the two-pair loop in assembly (lcb_r_miller2); scratch = the fallback path
     "k_tpke_pd_miller": (962, 2664),          # partial decryption split in three (was k_tpke_partial_decrypt, 7,652 B)
@@ -78,6 +78,7 @@ BUDGET = {
     "k_tpke_rlc_points": (0, 664),            # k_rlc_rand.hip: 248 registers, two waves per SIMD (round 6: 60 -> 0 spills)
     "k_tpke_rlc_search2a": (97, 3448),        # level-2 searches: four Fp12 values per lane, four lanes per group
     "k_tpke_rlc_search2b": (0, 3656),
+    "k_tpke_rlc_search2b_asm": (0, 0),        # round 6: the two-error search on the assembly Fp12 products (park slots)
     "k_tpke_rlc_sum": (0, 1168),
     "k_tpke_rlc_wsum": (48, 576),             # round 6: binary-GCD conversions; the live record saved around the calls
     "k_tpke_rlc_wsum2": (0, 648),
@@ -87,7 +88,7 @@ BUDGET = {
     "k_ts_rlc_points": (396, 1960),           # k_rlc_rand.hip: 256 registers, two waves per SIMD (round 6: 677 -> 396; G2 addends in the record)
     "k_ts_rlc_sum": (26, 2136),               # round 5: binary-GCD affine conversions (spills around the two calls)
     "k_ts_rlc_wsum": (96, 992),               # round 5: binary-GCD affine conversions
-    "k_ts_sign": (0, 3928),
+    "k_ts_sign": (0, 3976),
 }
 # Round 5: no kernel that runs on more than one wave may take more than 4 KB of scratch per lane — the
 # HIP runtime reserves a dispatch's scratch for min(waves, device wave slots) waves per hardware queue, and the 22.7 KB
