@@ -1889,11 +1889,12 @@ def main():
                          "round 6 stopped overriding it: every hardware queue can hold a full-device scratch "
                          "reservation, DESIGN.md §14.1).  The environment's value is recorded in the line "
                          "(config.hw_queues_env) beside the one used (config.hw_queues)")
-    ap.add_argument("--tpke-pipeline", type=int, default=3,
+    ap.add_argument("--tpke-pipeline", type=int, default=4,
                     help="batched verify: whole batches in flight (each on its own context / stream / host thread); "
                          "round 4: 2 measured 12.3 vs 10.6 M shares/s for one at a time, 3 no better (profiles/r04/q1, "
                          "q2); round 5, with the preparation at 256 registers: 3 gives 14.98 vs 14.57 M/s for 2 "
-                         "(profiles/r05/pipeline.txt)")
+                         "(profiles/r05/pipeline.txt); round 6, with the merged preparation (fork mode 4): 4 gives 17.14 vs 16.93 M/s "
+                         "for 3, every pair of three (profiles/r06/ab_kernels/pipeline4.txt)")
     ap.add_argument("--headline", choices=("batched", "exact"), default="batched",
                     help="which TPKE path the line's value / roofline / cpu_baseline describe")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
