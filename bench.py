@@ -1730,7 +1730,7 @@ def run_tpke_pipelined(args, nat, torch, dev, world, inp, dd, n, n_cts, n_dec, P
         api=f"lcb_ctx_tpke_verify_shares_batched_dev, {P} batches in flight (contexts / streams / host threads)",
         pipeline=P, single_batch_ms=1e3 * t_one, levels=levels[0],
         roofline={"bound": "valu_int32",
-                  "kernel": ("whole batched step: k_tpke_rlc_points + k_tpke_ct_prepare_h/_w + coop Miller / "
+                  "kernel": ("whole batched step: k_tpke_rlc_points + k_tpke_ct_prepare_hw + coop Miller / "
                              "k_final_exp_check over all levels"),
                   "achieved": step_ach / 1e12, "peak": PEAK_MAC32 / 1e12, "unit": "Tmac32/s",
                   "frac": step_ach / PEAK_MAC32, "traffic": None, "mac_per_fpmul": MAC_PER_FPMUL,

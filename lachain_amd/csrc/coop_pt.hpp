@@ -14,6 +14,9 @@ template <class F> struct PtLds {
     F prod[PT_LANES];
     jac<F> tab[PT_TAB_MAX + 1];
 };
+template <class F> struct PtProd {   // a group's product exchange alone (k_msm.hip's block reductions: 64 groups)
+    F prod[PT_LANES];
+};
 
 DI int pt_role() {
     int r = (int)(threadIdx.x & (PT_LANES - 1));
@@ -33,7 +36,7 @@ template <class F> DI void f_sel4(F &r, int role, const F &a, const F &b, const 
     f_sel(r, role == 2, c, r);
 }
 // one round: lane `role` computes x_role * y_role; returns with every lane holding the four products
-template <class F> DI void pt_round(PtLds<F> *L, F (&p)[PT_LANES], const F &x0, const F &y0, const F &x1,
+template <class LT, class F> DI void pt_round(LT *L, F (&p)[PT_LANES], const F &x0, const F &y0, const F &x1,
                                     const F &y1, const F &x2, const F &y2, const F &x3, const F &y3) {
     const int role = pt_role();
     F x, y, m;
@@ -49,7 +52,7 @@ template <class F> DI void pt_round(PtLds<F> *L, F (&p)[PT_LANES], const F &x0, 
 template <class F> DI void f_dbl(F &r, const F &a) { f_add(r, a, a); }
 
 // dbl-2009-l (curve.hpp jac_dbl): rounds {A = X^2, B = Y^2, YZ}, {C = B^2, (X + B)^2, F = E^2}, {E (D - X3)}
-template <class F> DI void pt_dbl(PtLds<F> *L, jac<F> &r, const jac<F> &q) {
+template <class LT, class F> DI void pt_dbl(LT *L, jac<F> &r, const jac<F> &q) {
     F p[PT_LANES], A, B, C, D, E, Fv, t, x3, y3, z3;
     pt_round(L, p, q.x, q.x, q.y, q.y, q.y, q.z, q.x, q.x);
     A = p[0];
@@ -77,8 +80,9 @@ template <class F> DI void pt_dbl(PtLds<F> *L, jac<F> &r, const jac<F> &q) {
     r.y = y3;
     r.z = z3;
 }
-// add-2007-bl with jac_add's special cases (either input at infinity, P == Q -> doubling, P == -Q -> infinity)
-template <class F> DI void pt_add(PtLds<F> *L, jac<F> &r, const jac<F> &a, const jac<F> &b) {
+// add-2007-bl with jac_add's special cases (either input at infinity, P == Q -> doubling, P == -Q -> infinity).
+// BLK: several waves share the workgroup's barriers, so the doubling branch is taken block-wide (__syncthreads_or)
+template <bool BLK = false, class LT, class F> DI void pt_add(LT *L, jac<F> &r, const jac<F> &a, const jac<F> &b) {
     const bool ai = f_is_zero(a.z), bi = f_is_zero(b.z);
     F p[PT_LANES], z1z1, z2z2, u1, u2, s1, s2, h, i, rr, j, v, t, x3, y3, z3;
     pt_round(L, p, a.z, a.z, b.z, b.z, a.y, b.z, b.y, a.z);
@@ -116,7 +120,7 @@ template <class F> DI void pt_add(PtLds<F> *L, jac<F> &r, const jac<F> &a, const
     o.z = z3;
     const bool same_x = !ai && !bi && f_eq(u1, u2);  // uniform within the group (every lane holds u1, u2, s1, s2)
     const bool need_dbl = same_x && f_eq(s1, s2);
-    if (__any(need_dbl)) {                           // wave-uniform branch: the rounds' LDS exchange stays convergent
+    if (BLK ? __syncthreads_or(need_dbl) : __any(need_dbl)) {   // uniform branch: the rounds' exchange stays convergent
         jac<F> d;
         pt_dbl(L, d, a);
         if (need_dbl) o = d;

@@ -350,6 +350,36 @@ extern "C" __global__ void LCB_BOUNDS k_g1_jac_reduce_block(const g1 *in, u32 n_
     if (t == 0) out[b] = sh[0];
 }
 
+// the same sums with the tree's additions on groups of four lanes (coop_pt.hpp: 5 product latencies per addition
+// instead of 16; 64 groups per block, the first level in two passes) — the same pairs in the same order, so the same
+// Jacobian coordinates as k_g1_jac_reduce_block
+extern "C" __global__ void LCB_BOUNDS k_g1_jac_reduce_block_coop(const g1 *in, u32 n_in, u32 group, g1 *out) {
+    __shared__ g1 sh[LCB_BLOCK];
+    __shared__ PtProd<fp> lds[LCB_BLOCK / PT_LANES];
+    const u32 t = threadIdx.x, b = blockIdx.x, gi = t / PT_LANES;
+    size_t lo = (size_t)b * group, hi = min((size_t)n_in, lo + group);
+    g1 acc;
+    jac_set_inf(acc);
+    for (size_t i = lo + t; i < hi; i += LCB_BLOCK) MSM_ADD(acc, acc, in[i]);
+    sh[t] = acc;
+    __syncthreads();
+#pragma unroll 1
+    for (u32 s = LCB_BLOCK / 2; s > 0; s >>= 1) {
+#pragma unroll 1
+        for (u32 base = 0; base < s; base += LCB_BLOCK / PT_LANES) {
+            const u32 p = base + gi;
+            const bool live = p < s;
+            g1 x, y;
+            if (live) { x = sh[p]; y = sh[p + s]; }
+            else { jac_set_inf(x); jac_set_inf(y); }
+            pt_add<true>(lds + gi, x, x, y);              // every lane of the block: the rounds' barriers
+            if (live && pt_role() == 0) sh[p] = x;          // pt_add's last round ended with a barrier after the reads
+            __syncthreads();
+        }
+    }
+    if (t == 0) out[b] = sh[0];
+}
+
 // fold_top: win[nwin] has the same weight as win[nwin - 1] (the GLV top window's upper digit half)
 extern "C" __global__ void LCB_BOUNDS k_msm_horner(const g1 *win, u32 nwin, u32 c, u32 fold_top, g1 *out) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
@@ -429,9 +459,16 @@ extern "C" void lcbk_msm_bucket_reduce(dim3 grid, hipStream_t s, const void *buc
 extern "C" void lcbk_g1_jac_reduce_groups(dim3 grid, hipStream_t s, const void *in, u32 n_in, u32 group, void *out) {
     LCB_LAUNCH(k_g1_jac_reduce_groups, (const g1 *)in, n_in, group, (g1 *)out);
 }
+#ifndef LCB_TREE_COOP
+#define LCB_TREE_COOP 1
+#endif
 extern "C" void lcbk_g1_jac_reduce_block(hipStream_t s, const void *in, u32 n_in, u32 group, void *out) {
     dim3 grid((n_in + group - 1) / group);
+#if LCB_TREE_COOP
+    LCB_LAUNCH(k_g1_jac_reduce_block_coop, (const g1 *)in, n_in, group, (g1 *)out);
+#else
     LCB_LAUNCH(k_g1_jac_reduce_block, (const g1 *)in, n_in, group, (g1 *)out);
+#endif
 }
 extern "C" void lcbk_msm_horner(hipStream_t s, const void *win, u32 nwin, u32 c, u32 fold_top, void *out) {
     LCB_LAUNCH_GATED(k_msm_horner_coop, dim3(1), dim3(PT_LANES), 0, s, (const g1 *)win, nwin, c, fold_top, (g1 *)out);

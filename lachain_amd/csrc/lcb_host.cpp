@@ -3385,6 +3385,10 @@ extern "C" int lcb_ctx_g1_jac_sum_dev(lcb_ctx *ctx, uint8_t *out48, void *out_ja
                                       void *stream) {
     CTX_OR(c, ctx, -1)
     Enq q(c, (hipStream_t)stream);
+    if (k == 1 && !out_jac && out48) {          // one partial (a single rank): serialise it as it is
+        lcbk_g1_jac_compress(dim3(1), q.s, parts, 1, out48);
+        return launched("jac sum launch") ? 0 : -1;
+    }
     void *acc = out_jac ? out_jac : c->msm[14].get(LCB_G1_JAC_BYTES);
     if (!acc) { set_err("device allocation failed"); return -1; }
     lcbk_g1_jac_reduce_groups(dim3(1), q.s, parts, (u32)k, k ? (u32)k : 1u, acc);

@@ -43,7 +43,7 @@ BUDGET = {
     "k_g2_mul": (288, 1272),                  # 4-bit window, table in the lanetab workspace (was 10,624 B)
     "k_g2_mul2_lanes": (3506, 1768),          # paired GLS ladders, tables in the lanetab workspace (was 22,672 B of scratch)
     "k_g2_mul_lanes": (856, 952),           # GLS ladder, table in the lanetab workspace (was 10,288 B)
-    "k_g2_sum": (192, 440),
+    "k_g2_sum": (192, 488),
     "k_lineset_coop": (86, 280),              # five-lane line sets (latency path): T, Q, acc and five products live
     "k_lineset_fill": (0, 984),
     "k_mcl_from_bytes": (0, 800),
