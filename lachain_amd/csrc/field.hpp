@@ -387,6 +387,66 @@ DN void fp_inv_gcd(fp &r, const fp &x) {
     fp_mul(r, vv, c);
     if (fp_is_zero(x)) r = fp_zero();
 }
+// Legendre symbol (x / p) by the binary Jacobi-symbol algorithm, on the Montgomery words (x R / p = x / p: R = 2^384 is
+// a square): a = xR, b = p; strip factors 2 from a ((2 / b) = -1 for b = 3, 5 mod 8), swap when a < b (reciprocity: -1
+// when both are 3 mod 4), a -= b; at a = 0, b = gcd = 1 unless x = 0.  About 500 subtract-and-shift steps of ~120
+// instructions against the exponentiation's 263 K (fp_legendre below); the step count depends on x (a wave runs its
+// lanes' longest), which is public here: the candidates of hash-to-G2.  Returns 1, -1, or 0 for x = 0.
+DN int fp_jacobi(const fp &x) {
+    u32 a[12], b[12];
+#pragma unroll
+    for (int j = 0; j < 12; j++) {
+        a[j] = x.v[j];
+        b[j] = LCB_P[j];
+    }
+    u32 neg = 0;
+#pragma unroll 1
+    for (;;) {
+        u32 any = 0;
+#pragma unroll
+        for (int j = 0; j < 12; j++) any |= a[j];
+        if (!any) break;
+#pragma unroll 1
+        while (a[0] == 0) {                            // a zero word: 2^32 is a square, the sign stays
+#pragma unroll
+            for (int j = 0; j < 11; j++) a[j] = a[j + 1];
+            a[11] = 0;
+        }
+        const u32 t = (u32)__builtin_ctz(a[0]);
+        if (t) {
+#pragma unroll
+            for (int j = 0; j < 11; j++) a[j] = __builtin_amdgcn_alignbit(a[j + 1], a[j], t);
+            a[11] >>= t;
+            const u32 b8 = b[0] & 7u;
+            if ((t & 1u) && (b8 == 3u || b8 == 5u)) neg ^= 1u;
+        }
+        u32 d[12], br = 0;                             // a odd: d = a - b
+#pragma unroll
+        for (int j = 0; j < 12; j++) {
+            const u64 w = (u64)a[j] - b[j] - br;
+            d[j] = (u32)w;
+            br = (u32)(w >> 32) & 1u;
+        }
+        if (br) {                                      // a < b: (a, b) <- (b - a, a)
+            if ((a[0] & 3u) == 3u && (b[0] & 3u) == 3u) neg ^= 1u;
+            u32 c = 1;
+#pragma unroll
+            for (int j = 0; j < 12; j++) {
+                const u64 w = (u64)(~d[j]) + c;
+                b[j] = a[j];
+                a[j] = (u32)w;
+                c = (u32)(w >> 32);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 12; j++) a[j] = d[j];
+        }
+    }
+    u32 one = b[0] == 1u;
+#pragma unroll
+    for (int j = 1; j < 12; j++) one &= b[j] == 0u;
+    return one ? (neg ? -1 : 1) : 0;
+}
 // mcl Fp::squareRoot for p = 3 mod 4: y = a^((p+1)/4), valid iff y^2 == a
 DI bool fp_sqrt(fp &r, const fp &a) {
     fp y, t;
@@ -396,11 +456,18 @@ DI bool fp_sqrt(fp &r, const fp &a) {
     r = y;
     return ok;
 }
+#ifndef LCB_JACOBI
+#define LCB_JACOBI 1
+#endif
 DI int fp_legendre(const fp &a) {
+#if LCB_JACOBI
+    return fp_jacobi(a);
+#else
     if (fp_is_zero(a)) return 0;
     fp t;
     fp_pow_const(t, a, 2);
     return fp_eq(t, fp_one()) ? 1 : -1;
+#endif
 }
 
 // ------------------------------------------------------------------------------------------------ Fp2
@@ -518,6 +585,27 @@ DI void fp2_sqrt_normed(fp2 &y, const fp2 &x, const fp &nr) {
     if (fp_is_zero(x.b)) { (void)fp2_sqrt(y, x); return; }
     fp inv2;
     fp_load_const(inv2, LCB_INV2);
+#if LCB_JACOBI
+    {   // fp2_sqrt's two tries, c = (a + nr)/2 first: the first one that is a nonzero square, chosen by its Legendre
+        // symbol, then ONE exponentiation (the loop below ran the second for the wave whenever one lane needed it)
+        fp c, s, cs, e, t2;
+        fp_add(c, x.a, nr);
+        fp_mul(c, c, inv2);
+        if (fp_jacobi(c) != 1) {
+            fp_sub(c, x.a, nr);
+            fp_mul(c, c, inv2);
+        }
+        fp_pow_const(s, c, 3);
+        fp_mul(cs, c, s);                              // c^((p+1)/4)
+        fp_mul(e, cs, s);                              // c^((p-1)/2)
+        if (fp_eq(e, fp_one())) {
+            y.a = cs;
+            fp_mul(t2, x.b, s);
+            fp_mul(y.b, t2, inv2);                     // b / (2 c^((p+1)/4)) = b s / 2
+        }
+        return;
+    }
+#endif
 #pragma unroll 1
     for (int k = 0; k < 2; k++) {
         fp c, s, cs, e, t2;

@@ -127,11 +127,11 @@ DI bool g2_calc_bn(g2 &P, const fp2 &t) {
     fp2_mul_fp(w, w, c1);
     fp2_mul(w, w, t);
 #if LCB_SVDW_UNIFORM
-    // Round 6: the first candidate whose g(x) = x^3 + b is a square, found with ONE exponentiation per candidate (the
-    // root of the norm, which fp2_sqrt takes first and which tells squareness), all three tested for every lane, then
-    // one fp2_sqrt of the chosen value from that root (fp2_sqrt_normed: the same root as fp2_sqrt).  The loop with an
-    // early exit ran up to three exponentiations per candidate for the wave whenever any lane needed them (9 per wave
-    // against 5 here); the selected x, and so H, is the same.
+    // Round 6: the first candidate whose g(x) = x^3 + b is a square, all three tested for every lane by the Legendre
+    // symbol of the norm N(g(x)) (fp_jacobi, binary; g(x) is a square iff its norm is), then the chosen norm's root
+    // and one fp2_sqrt of the chosen value from it (fp2_sqrt_normed: the same root as fp2_sqrt).  The loop with an
+    // early exit ran up to three exponentiations per candidate for the wave whenever any lane needed them: 9 per wave,
+    // then 5 with one exponentiation (the norm's root) per candidate, now 2; the selected x, and so H, is the same.
     fp2 xs, ts;
     fp ns;
     bool found = false;
@@ -159,7 +159,12 @@ DI bool g2_calc_bn(g2 &P, const fp2 &t) {
             fp_sqr(u, tmp.b);
             fp_add(n, n, u);                      // N(g(x)): a square iff g(x) is one
         }
+#if LCB_JACOBI
+        const bool sq = fp_jacobi(n) >= 0;        // the Legendre symbol only; the chosen norm's root below
+        nr = n;
+#else
         const bool sq = fp_sqrt(nr, n);
+#endif
         if (!found && sq) {
             found = true;
             xs = x;
@@ -168,6 +173,9 @@ DI bool g2_calc_bn(g2 &P, const fp2 &t) {
         }
     }
     if (!found) return false;
+#if LCB_JACOBI
+    (void)fp_sqrt(ns, ns);                        // a square: fp_sqrt's root, as before
+#endif
     fp2_sqrt_normed(y, ts, ns);
     if (negative) fp2_neg(y, y);
     P.x = xs; P.y = y; P.z = fp2_one();

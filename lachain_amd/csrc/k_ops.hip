@@ -194,6 +194,18 @@ extern "C" __global__ void LCB_BOUNDS k_op_debug(int op, u32 *io, int orig_cof) 
         case 9: fp2_inv_n(r.c0.c0, a.c0.c0); break;
         case 10: fp12_conj(r, a); break;
         case 11: fe_hard(r, a); break;
+        case 12: {                                 // Legendre symbols of the 12 Fp words: binary (fp_jacobi), exponent
+            u32 *w = (u32 *)&r;
+            const fp *xs = (const fp *)&a;
+#pragma unroll 1
+            for (int k = 0; k < 12; k++) {
+                fp t;
+                fp_pow_const(t, xs[k], 2);
+                w[2 * k] = (u32)fp_jacobi(xs[k]);
+                w[2 * k + 1] = fp_is_zero(xs[k]) ? 0u : (fp_eq(t, fp_one()) ? 1u : 0xffffffffu);
+            }
+            break;
+        }
         default: break;
         }
         *(fp12 *)io = r;
