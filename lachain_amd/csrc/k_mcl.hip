@@ -19,10 +19,28 @@ extern "C" __global__ void LCB_BOUNDS k_mcl_g1_terms(const g1 *pts, const fr *sc
 #pragma unroll 1
     for (u32 i = gid; i < n; i += gsz) {
         g1a a;
-        jac_to_aff(a, pts[i]);
+        g1_jac_to_aff_g(a, pts[i]);                    // binary-GCD inversion
         fr k = scal[i];
         g1 r;
         lw_mul_win4(r, slot, a, k.v);
+        terms[i] = r;
+    }
+}
+
+// terms[i] = [e_i] P_i with 384-bit scalars (12 words each): mclBn_G1EvaluatePolynomial's e_i = x^i mod #E(Fp), so
+// sum_i [e_i] c_i is the Horner value sum_i [x^i] c_i for every on-curve coefficient (lcb_host.cpp eval_poly)
+extern "C" __global__ void LCB_BOUNDS k_mcl_g1_terms_wide(const g1 *pts, const u32 *scal, u32 n, g1 *terms, u32 *ws) {
+    const u32 gid = blockIdx.x * blockDim.x + threadIdx.x, gsz = gridDim.x * blockDim.x;
+    char *slot = lw_slot(ws, LW_WIN4_QUADS(fp), gid);
+#pragma unroll 1
+    for (u32 i = gid; i < n; i += gsz) {
+        g1a a;
+        g1_jac_to_aff_g(a, pts[i]);
+        u32 k[12];
+#pragma unroll
+        for (int j = 0; j < 12; j++) k[j] = scal[12 * (size_t)i + j];
+        g1 r;
+        lw_mul_win4<fp, 12>(r, slot, a, k);
         terms[i] = r;
     }
 }
@@ -90,6 +108,14 @@ extern "C" size_t lcbk_mcl_terms_ws_bytes(u32 n) {
 extern "C" void lcbk_mcl_g1_terms(hipStream_t s, const void *pts, const void *scal, u32 n, void *terms, u32 *ws) {
     dim3 grid(lcb_persist_blocks((const void *)k_mcl_g1_terms, &g_rb_terms, n));
     LCB_LAUNCH(k_mcl_g1_terms, (const g1 *)pts, (const fr *)scal, n, (g1 *)terms, ws);
+}
+static u32 g_rb_terms_wide;
+extern "C" size_t lcbk_mcl_terms_wide_ws_bytes(u32 n) {
+    return LCB_WS_BYTES(lcb_persist_blocks((const void *)k_mcl_g1_terms_wide, &g_rb_terms_wide, n), LW_WIN4_QUADS(fp));
+}
+extern "C" void lcbk_mcl_g1_terms_wide(hipStream_t s, const void *pts, const u32 *scal, u32 n, void *terms, u32 *ws) {
+    dim3 grid(lcb_persist_blocks((const void *)k_mcl_g1_terms_wide, &g_rb_terms_wide, n));
+    LCB_LAUNCH(k_mcl_g1_terms_wide, (const g1 *)pts, scal, n, (g1 *)terms, ws);
 }
 extern "C" void lcbk_mcl_horner(hipStream_t s, int g, const u32 *coef, u32 n, const void *x_raw, u32 *out) {
     dim3 grid(1);

@@ -84,7 +84,7 @@ extern "C" __global__ void LCB_BOUNDS k_op_grp(int op, u32 *io, int orig_cof) {
         io[128] = fp_words_lt_p(p.x) && fp_words_lt_p(p.y) && fp_words_lt_p(p.z) && g1_on_curve(p); break;
     }
     case OP_G1_NORM: {
-        g1 p = *(g1 *)(io + 36); g1a a; jac_to_aff(a, p); g1 q; jac_from_aff(q, a);
+        g1 p = *(g1 *)(io + 36); g1a a; g1_jac_to_aff_g(a, p); g1 q; jac_from_aff(q, a);
         if (a.inf) jac_set_inf(q); *(g1 *)io = q; break;
     }
     // ---- G2: io[0..72) out, io[72..144) x, io[144..216) y, io[216..224) Fr, io[224..248) bytes, io[248] flag
@@ -107,7 +107,7 @@ extern "C" __global__ void LCB_BOUNDS k_op_grp(int op, u32 *io, int orig_cof) {
                   fp_words_lt_p(p.z.a) && fp_words_lt_p(p.z.b) && g2_on_curve(p); break;
     }
     case OP_G2_NORM: {
-        g2 p = *(g2 *)(io + 72); g2a a; jac_to_aff(a, p); g2 q; jac_from_aff(q, a);
+        g2 p = *(g2 *)(io + 72); g2a a; g2_jac_to_aff_g(a, p); g2 q; jac_from_aff(q, a);
         if (a.inf) jac_set_inf(q); *(g2 *)io = q; break;
     }
     case OP_G2_HASH: {

@@ -50,7 +50,7 @@ extern "C" __global__ void LCB_BOUNDS k_tpke_ct_prepare(const uint8_t *cts_u, co
     g2 H;
     bool hok = g2_hash_digest(H, d, (flags & 1) != 0);
     ok = ok && hok;
-    if (hok) jac_to_aff(Ha, H);
+    if (hok) g2_jac_to_aff_g(Ha, H);                       // binary-GCD inversion (as k_prep.hip)
     else { Ha.inf = true; Ha.x = fp2_zero(); Ha.y = fp2_zero(); }
     if (!ok) { W.inf = true; Ha.inf = true; }
     // the two points go to their line sets' point slots; k_lineset_fill computes the 2 * n_cts line sets one lane

@@ -184,7 +184,8 @@ DI void lw_g2_gls_ladder2(g2 &r, const char *p, const u64 da[4], const u64 db[4]
 // jac_mul_win4 (curve.hpp) with its table in the slot (entries 1..15 = 1P..15P): integer scalar multiplication, exact
 // outside the r-torsion; a table entry at infinity (order <= 15) takes the binary ladder
 #define LW_WIN4_QUADS(F) (15 * LwTab<F>::EQ)
-template <class F> DI void lw_mul_win4(jac<F> &r, char *p, const aff<F> &P, const u32 k[8]) {
+// (NW words of scalar: 8 for Fr, 12 for mclBn_G1EvaluatePolynomial's powers reduced mod the curve order)
+template <class F, int NW = 8> DI void lw_mul_win4(jac<F> &r, char *p, const aff<F> &P, const u32 *k) {
     typedef LwTab<F> T;
     jac_set_inf(r);
     if (P.inf) return;
@@ -200,9 +201,9 @@ template <class F> DI void lw_mul_win4(jac<F> &r, char *p, const aff<F> &P, cons
             T::put_jac(p, i, t);
         }
     }
-    if (!lw_table_to_aff<F>(p, 15)) { jac_mul_aff(r, P, k, 256); return; }
+    if (!lw_table_to_aff<F>(p, 15)) { jac_mul_aff(r, P, k, 32 * NW); return; }
 #pragma unroll 1
-    for (int w = 63; w >= 0; w--) {
+    for (int w = 8 * NW - 1; w >= 0; w--) {
         jac_dbl(r, r); jac_dbl(r, r); jac_dbl(r, r); jac_dbl(r, r);
         const u32 nib = (k[w >> 3] >> (4 * (w & 7))) & 15;
         if (nib) {

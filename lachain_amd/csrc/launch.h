@@ -118,6 +118,8 @@ extern "C" void lcbk_coop_tpke_miller(hipStream_t s, const u32 *lines, const voi
 extern "C" void lcbk_lines_unnormalised(hipStream_t s, const u32 *lines, u32 c0, u32 c1, u32 *flag);
 extern "C" size_t lcbk_mcl_terms_ws_bytes(u32 n);
 extern "C" void lcbk_mcl_g1_terms(hipStream_t s, const void *pts, const void *scal, u32 n, void *terms, u32 *ws);
+extern "C" size_t lcbk_mcl_terms_wide_ws_bytes(u32 n);
+extern "C" void lcbk_mcl_g1_terms_wide(hipStream_t s, const void *pts, const u32 *scal, u32 n, void *terms, u32 *ws);
 extern "C" void lcbk_mcl_horner(hipStream_t s, int g, const u32 *coef, u32 n, const void *x_raw, u32 *out);
 extern "C" void lcbk_mcl_g1_sum(hipStream_t s, const void *in, u32 n, void *out);
 extern "C" void lcbk_mcl_from_bytes(hipStream_t s, int g, const uint8_t *in, u32 n, u32 *out, uint8_t *ok);

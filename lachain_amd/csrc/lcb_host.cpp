@@ -3267,8 +3267,79 @@ extern "C" int mclBn_G2LagrangeInterpolation(mclBnG2 *out, const mclBnFr *xVec, 
     if (k == 1) { *out = yVec[0]; return mclBnFr_isZero(&xVec[0]) ? -1 : 0; }
     return lagrange_points(2, out, xVec, yVec, k);
 }
-// G1 / G2 EvaluatePolynomial: mcl's Horner rule (y = c[n-1]; y = y x + c[i]) in one kernel launch — the products are
-// by the integer x, as mcl's, so off-subgroup coefficients give mcl's value too
+// out = a x mod #E(Fp) for G1 (a < #E, x < 2^256): #E(Fp) = p - z = h r (z = -0xd201000000010000), so [k] P depends
+// only on k mod #E for every point P of E(Fp), in the subgroup or not
+static void ne_mulmod(uint64_t out[6], const uint64_t a[6], const uint64_t x[4]) {
+    static const uint64_t NE[6] = {0x8c0000000000aaabull, 0x1eabfffeb1540000ull, 0x6730d2a0f6b0f624ull,
+                                   0x64774b84f38512bfull, 0x4b1ba7b6434bacd7ull, 0x1a0111ea397fe69aull};
+    typedef unsigned __int128 u128;
+    uint64_t prod[10] = {0};
+    for (int i = 0; i < 6; i++) {
+        uint64_t carry = 0;
+        for (int j = 0; j < 4; j++) {
+            const u128 t = (u128)a[i] * x[j] + prod[i + j] + carry;
+            prod[i + j] = (uint64_t)t;
+            carry = (uint64_t)(t >> 64);
+        }
+        prod[i + 4] = carry;
+    }
+    uint64_t rem[6] = {0};                       // long division by bits: rem < NE < 2^381, so 2 rem + 1 fits
+    for (int b = 639; b >= 0; b--) {
+        for (int k = 5; k > 0; k--) rem[k] = (rem[k] << 1) | (rem[k - 1] >> 63);
+        rem[0] = (rem[0] << 1) | ((prod[b >> 6] >> (b & 63)) & 1);
+        int ge = 1;
+        for (int k = 5; k >= 0; k--) {
+            if (rem[k] != NE[k]) { ge = rem[k] > NE[k]; break; }
+        }
+        if (ge) {
+            uint64_t br = 0;
+            for (int k = 0; k < 6; k++) {
+                const u128 t = (u128)rem[k] - NE[k] - br;
+                rem[k] = (uint64_t)t;
+                br = (uint64_t)(t >> 64) & 1;
+            }
+        }
+    }
+    memcpy(out, rem, 48);
+}
+// G1 EvaluatePolynomial as a sum of independent terms: sum_i [x^i mod #E] c_i (k_mcl_g1_terms_wide, one lane per term,
+// then the mulVec sums) — the value of mcl's Horner rule for every on-curve coefficient, with the products side by
+// side instead of n - 1 dependent ones
+static int eval_poly_g1_terms(lcb_ctx *c, mclBnG1 *out, const mclBnG1 *coef, size_t n, const uint64_t xr[4]) {
+    std::vector<uint32_t> sc(12 * n);
+    uint64_t e[6] = {1, 0, 0, 0, 0, 0};
+    for (size_t i = 0; i < n; i++) {
+        if (i) ne_mulmod(e, e, xr);
+        memcpy(&sc[12 * i], e, 48);
+    }
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    const u32 *pts = up(c->mcl[0], (const u32 *)coef, 36 * n, s);
+    const u32 *dsc = up(c->mcl[1], sc.data(), 12 * n, s);
+    uint8_t *terms = (uint8_t *)c->mcl[2].get(LCB_G1_JAC_BYTES * n);
+    uint8_t *tmp = (uint8_t *)c->mcl[3].get(LCB_G1_JAC_BYTES * ((n + 255) / 256));
+    uint8_t *dz = (uint8_t *)c->mcl[5].get(LCB_G1_JAC_BYTES);
+    u32 *ws = (u32 *)c->lws.get(lcbk_mcl_terms_wide_ws_bytes((u32)n));
+    if (!pts || !dsc || !terms || !tmp || !dz || !ws) { set_err("device allocation failed"); return -1; }
+    lcbk_mcl_g1_terms_wide(s, pts, dsc, (u32)n, terms, ws);
+    uint8_t *cur = terms;
+    size_t cnt = n;
+    while (cnt > 256) {
+        uint8_t *dst = cur == terms ? tmp : terms;
+        lcbk_g1_jac_reduce_block(s, cur, (u32)cnt, 256, dst);
+        cnt = (cnt + 255) / 256;
+        cur = dst;
+    }
+    lcbk_mcl_g1_sum(s, cur, (u32)cnt, dz);
+    mclBnG1 r;
+    hipMemcpyAsync(&r, dz, 144, hipMemcpyDeviceToHost, s);
+    if (!sync_check(c, "evaluate polynomial")) return -1;
+    *out = r;
+    return 0;
+}
+// G1 / G2 EvaluatePolynomial: mcl's Horner rule (y = c[n-1]; y = y x + c[i]) — the products are by the integer x, as
+// mcl's, so off-subgroup coefficients give mcl's value too.  G1 (n >= 2): the same value as independent terms (above);
+// G2 and LCB_EVAL_HORNER=1: the Horner chain in one kernel launch
 static int eval_poly(int g, void *out, const void *coef, mclSize n, const mclBnFr *x) {
     if (n == 0) return -1;
     SYNC_CTX_OR(c, -1)
@@ -3276,6 +3347,8 @@ static int eval_poly(int g, void *out, const void *coef, mclSize n, const mclBnF
     const size_t words = g == 1 ? 36 : 72;
     uint64_t xr[4];
     frh::to_raw(xr, FRV(x));
+    static const bool horner = getenv("LCB_EVAL_HORNER") && atoi(getenv("LCB_EVAL_HORNER")) == 1;
+    if (g == 1 && n >= 2 && !horner) return eval_poly_g1_terms(c, (mclBnG1 *)out, (const mclBnG1 *)coef, n, xr);
     Enq q(c, c->stream);
     hipStream_t s = c->stream;
     const u32 *dc = up(c->mcl[0], (const u32 *)coef, words * n, s);

@@ -128,6 +128,29 @@ def test_evaluate_polynomial_matches_horner(mcl, g):
                                                                                      x.ToBytes())
 
 
+def test_g1_evaluate_polynomial_off_subgroup_and_long(mcl):
+    """G1 EvaluatePolynomial runs as independent terms [x^i mod #E(Fp)] c_i (lcb_host.cpp eval_poly_g1_terms): the
+    Horner value for coefficients outside G1 too (the order-3 point and a random on-curve point, G1.FromBytes accepts
+    them), for x = 0, 1, -1, -3 and random x, for a polynomial longer than one block of terms, and with the point at
+    infinity among the coefficients."""
+    from test_gpu_batched import off_subgroup_g1
+    Fr, G1 = mcl.Fr, mcl.G1
+    d = Drbg(b"mcl-eval-off")
+    t3 = bytes(47) + b"\x80"                        # (0, p - 2): order 3
+    cs = [G1.Generator() * Fr.FromBytes(d.fr()) for _ in range(6)]
+    cs[1] = G1.FromBytes(t3)
+    cs[3] = G1.FromBytes(off_subgroup_g1(d))
+    cs[4] = cs[4] + G1.FromBytes(t3)
+    cs[5] = G1.Zero()                               # the point at infinity
+    for x in (Fr.FromInt(0), Fr.FromInt(1), Fr.FromInt(-1), Fr.FromInt(-3), Fr.FromBytes(d.fr())):
+        got = mcl.MclBls12381.EvaluatePolynomial(cs, x)
+        assert got.ToBytes() == o.g1_eval_poly([c.ToBytes() for c in cs], x.ToBytes())
+    long_cs = [G1.Generator() * Fr.FromBytes(d.fr()) for _ in range(300)]
+    x = Fr.FromBytes(d.fr())
+    got = mcl.MclBls12381.EvaluatePolynomial(long_cs, x)
+    assert got.ToBytes() == o.g1_eval_poly([c.ToBytes() for c in long_cs], x.ToBytes())
+
+
 def test_single_operations_from_many_threads(mcl):
     # each thread owns its staging buffers and stream: results never mix
     Fr, G1, G2, GT = mcl.Fr, mcl.G1, mcl.G2, mcl.GT

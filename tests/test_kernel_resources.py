@@ -49,6 +49,7 @@ BUDGET = {
     "k_mcl_from_bytes": (0, 800),
     "k_mcl_g1_sum": (0, 168),
     "k_mcl_g1_terms": (0, 880),
+    "k_mcl_g1_terms_wide": (12, 312),         # round 6: G1 EvaluatePolynomial's 384-bit terms (the 12-word scalar live)
     "k_mcl_g2_hash": (0, 3400),               # mclBnG2_hashAndMapTo: the same one-lane hash as k_g2_hash
     "k_mcl_horner": (0, 1320),
     "k_mcl_to_bytes": (0, 1024),
