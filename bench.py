@@ -1870,7 +1870,9 @@ def emit(full, write_file=True):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=12,
+                    help="timed TPKE steps (batches); 12 by default so that the default four batches in flight each run "
+                         "three (at 3 steps one of the four contexts idles and the line under-reports the pipeline)")
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--shares", type=int, default=1048576)
     ap.add_argument("--n", type=int, default=22)
