@@ -89,18 +89,77 @@ static_assert(sizeof(PtJob<fp2>) == 192 + 16 + 36, "PtJob<fp2> layout (launch.h 
 // in a kernel of its own: k_op's single-operation switch carries every operation's state (3,038 spilled registers).
 // io as k_op's OP_G2_HASH: io[250] = message length, the message at io + 256; out: the Jacobian point at io[0..72),
 // io[248] = 1 on success (0: no point, infinity written)
+// The map (SHA-512, calcBN) runs on lane 0; the Budroni-Pintore cofactor clearing's two 64-bit ladders and its
+// additions run on groups of four lanes (coop_pt.hpp: a G2 doubling in 3 Fp2-product rounds instead of 7 serial
+// products) — the same point as h2g2.hpp g2_clear_cofactor_bp (its Jacobian coordinates may differ: general instead
+// of mixed additions).  The original-cofactor mode (one 508-bit ladder, a tuning option) stays on lane 0.
+#ifndef LCB_MCL_HASH_COOP
+#define LCB_MCL_HASH_COOP 1
+#endif
+template <class LT> DI void pt_mul_u64(LT *L, g2 &r, const g2 &p, u64 k) {   // k uniform: a wave-uniform ladder
+    const int top = 63 - __clzll(k);
+    g2 acc = p;
+#pragma unroll 1
+    for (int i = top - 1; i >= 0; i--) {
+        pt_dbl(L, acc, acc);
+        if ((k >> i) & 1) pt_add(L, acc, acc, p);
+    }
+    r = acc;
+}
+template <class LT> DI void pt_clear_cofactor_bp(LT *L, g2 &Q, const g2 &P) {   // h2g2.hpp g2_clear_cofactor_bp
+    // with A = (z - 1) P = -[|z| + 1] P: Q = -[|z|] A + (psi^2(2P) - P) + psi(A); three points live at a time
+    g2 V, A, W;
+    pt_dbl(L, V, P);
+    g2_psi2(V, V);
+    jac_neg(W, P);
+    pt_add(L, V, V, W);                          // psi^2(2P) - P
+    pt_mul_u64(L, A, P, LCB_Z_ABS + 1);
+    jac_neg(A, A);                               // A = (z - 1) P
+    g2_psi(W, A);
+    pt_add(L, V, V, W);                          // psi^2(2P) - P + psi(A)
+    pt_mul_u64(L, W, A, LCB_Z_ABS);
+    jac_neg(W, W);                               // z A
+    pt_add(L, Q, W, V);
+}
 extern "C" __global__ void __launch_bounds__(64, 1) k_mcl_g2_hash(u32 *io, int orig_cof) {
     if (threadIdx.x) return;
     uint8_t d[64];
     sha512_2(d, (const uint8_t *)(io + 256), io[250], (const uint8_t *)(io + 256), 0);
+#if LCB_MCL_HASH_COOP
+    fp2 t;                                       // the map only; k_mcl_g2_clear clears the cofactor (io[249] = 1)
+    fp_set_hash_digest(t.a, d);
+    t.b = fp_zero();
+    g2 P;
+    const bool ok = g2_calc_bn(P, t);
+    if (ok && orig_cof) { g2 H; g2_clear_cofactor_h2(H, P); P = H; }
+    if (!ok) jac_set_inf(P);
+    *(g2 *)io = P;
+    io[248] = ok ? 1u : 0u;
+    io[249] = ok && !orig_cof ? 1u : 0u;
+#else
     g2 H;
     const bool ok = g2_hash_digest(H, d, orig_cof != 0);
     if (!ok) jac_set_inf(H);
     *(g2 *)io = H;
     io[248] = ok ? 1u : 0u;
+#endif
+}
+// io[0..72) = the clearing of the mapped point io[0..72) when io[249] is set (every lane group computes it; lane 0
+// stores)
+extern "C" __global__ void __launch_bounds__(64, 1) k_mcl_g2_clear(u32 *io) {
+    __shared__ PtProd<fp2> lds[64 / PT_LANES];
+    if (io[249] == 0u) return;                   // uniform
+    const g2 P = *(const g2 *)io;
+    g2 H;
+    pt_clear_cofactor_bp(lds + threadIdx.x / PT_LANES, H, P);
+    __syncthreads();
+    if (threadIdx.x == 0) *(g2 *)io = H;
 }
 extern "C" void lcbk_mcl_g2_hash(hipStream_t s, u32 *io, int orig_cof) {
     LCB_LAUNCH_GATED(k_mcl_g2_hash, dim3(1), dim3(64), 0, s, io, orig_cof);
+#if LCB_MCL_HASH_COOP
+    LCB_LAUNCH_GATED(k_mcl_g2_clear, dim3(1), dim3(64), 0, s, io);
+#endif
 }
 extern "C" void lcbk_ptmul_g1(hipStream_t s, const void *jobs, u32 n_groups, void *out) {
     LCB_LAUNCH_GATED(k_ptmul_g1, dim3(1), dim3(64), 0, s, (const PtJob<fp> *)jobs, n_groups, (g1 *)out);

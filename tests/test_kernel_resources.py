@@ -50,7 +50,8 @@ BUDGET = {
     "k_mcl_g1_sum": (0, 168),
     "k_mcl_g1_terms": (0, 880),
     "k_mcl_g1_terms_wide": (12, 312),         # round 6: G1 EvaluatePolynomial's 384-bit terms (the 12-word scalar live)
-    "k_mcl_g2_hash": (0, 3400),               # mclBnG2_hashAndMapTo: the same one-lane hash as k_g2_hash
+    "k_mcl_g2_hash": (168, 3400),             # mclBnG2_hashAndMapTo's map (SHA-512, calcBN) on one lane
+    "k_mcl_g2_clear": (564, 1108),            # round 6: its cofactor clearing on four-lane groups (Fp2 point rounds at 512 registers)
     "k_mcl_horner": (0, 1320),
     "k_mcl_to_bytes": (0, 1024),
     "k_msm_bucket_fix": (0, 168),
