@@ -33,11 +33,12 @@ template <class F> struct PtJob {
 };
 // one wave, groups g = lane / 4 (< n_groups <= PT_MAX_GROUPS); out[g] = [digits] base_g (Jacobian, mcl layout).  Every
 // group runs nwin windows (the host pads the digit strings to one length), so the loop is wave-uniform.
-template <class F> DI void pt_ladder(const PtJob<F> *jobs, u32 n_groups, jac<F> *out, PtLds<F> *lds) {
+template <class F, int MAXG = PT_MAX_GROUPS> DI void pt_ladder(const PtJob<F> *jobs, u32 n_groups, jac<F> *out,
+                                                           PtLds<F> *lds) {
     const u32 g = threadIdx.x / PT_LANES;
     const bool live = g < n_groups;
     const u32 gj = live ? g : 0;                 // idle lanes shadow group 0 (same control flow, no stores)
-    PtLds<F> *L = lds + (live ? g : PT_MAX_GROUPS);
+    PtLds<F> *L = lds + (live ? g : MAXG);
     const PtJob<F> &J = jobs[gj];
     jac<F> P, acc;
     if (J.inf) jac_set_inf(P);
@@ -81,6 +82,16 @@ extern "C" __global__ void __launch_bounds__(64, 1) k_ptmul_g1(const PtJob<fp> *
 extern "C" __global__ void __launch_bounds__(64, 1) k_ptmul_g2(const PtJob<fp2> *jobs, u32 n_groups, g2 *out) {
     __shared__ PtLds<fp2> lds[PT_MAX_GROUPS + 1];
     pt_ladder(jobs, n_groups, out, lds);
+}
+// many G1 ladders at once (mclBnG1_mulVec, mclBn_G1LagrangeInterpolation: three groups per term, lcb_host.cpp
+// g1_mulvec_coop): block b runs groups [16 b, 16 b + 16), every group of a wave with its own LDS area
+#define PT_MULTI_GROUPS 16
+extern "C" __global__ void __launch_bounds__(64, 1) k_ptmul_g1_multi(const PtJob<fp> *jobs, u32 n_groups, g1 *out) {
+    __shared__ PtLds<fp> lds[PT_MULTI_GROUPS + 1];
+    const u32 base = blockIdx.x * PT_MULTI_GROUPS;
+    if (base >= n_groups) return;                // uniform
+    const u32 n = min(n_groups - base, (u32)PT_MULTI_GROUPS);
+    pt_ladder<fp, PT_MULTI_GROUPS>(jobs + base, n, out + base, lds);
 }
 static_assert(sizeof(PtJob<fp>) == 96 + 16 + 36, "PtJob<fp> layout (launch.h LCB_PTJOB_G1_BYTES)");
 static_assert(sizeof(PtJob<fp2>) == 192 + 16 + 36, "PtJob<fp2> layout (launch.h LCB_PTJOB_G2_BYTES)");
@@ -163,6 +174,10 @@ extern "C" void lcbk_mcl_g2_hash(hipStream_t s, u32 *io, int orig_cof) {
 }
 extern "C" void lcbk_ptmul_g1(hipStream_t s, const void *jobs, u32 n_groups, void *out) {
     LCB_LAUNCH_GATED(k_ptmul_g1, dim3(1), dim3(64), 0, s, (const PtJob<fp> *)jobs, n_groups, (g1 *)out);
+}
+extern "C" void lcbk_ptmul_g1_multi(hipStream_t s, const void *jobs, u32 n_groups, void *out) {
+    const dim3 grid((n_groups + PT_MULTI_GROUPS - 1) / PT_MULTI_GROUPS);
+    LCB_LAUNCH_GATED(k_ptmul_g1_multi, grid, dim3(64), 0, s, (const PtJob<fp> *)jobs, n_groups, (g1 *)out);
 }
 extern "C" void lcbk_ptmul_g2(hipStream_t s, const void *jobs, u32 n_groups, void *out) {
     LCB_LAUNCH_GATED(k_ptmul_g2, dim3(1), dim3(64), 0, s, (const PtJob<fp2> *)jobs, n_groups, (g2 *)out);

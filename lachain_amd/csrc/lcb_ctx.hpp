@@ -69,9 +69,11 @@ struct lcb_ctx {
     // Lagrange / assembly / MSM / staging
     DevBuf lag[5], sel[4], msm[15], in[8], out[4], dkg[9];
     DevBuf lws;                       // lanetab.hpp workspaces of the persistent scalar-multiplication grids
-    DevBuf mcl[8];                    // the mcl surface's pairing / multi-scalar / Horner / Lagrange staging
-    // mclBn_pairing's cache of G2 line sets (mcl[2]: slot k = Q_k's set and the infinity set), least recently used
-    // slot replaced: the protocol pairs every share of a ciphertext / coin with the same H, W (TPKE/PublicKey.cs:91)
+    DevBuf mcl[10];                   // the mcl surface's pairing / multi-scalar / Horner / Lagrange staging
+    // mclBn_pairing's cache of G2 line sets (pc_lines: slot k = Q_k's set and the infinity set), least recently used
+    // slot replaced: the protocol pairs every share of a ciphertext / coin with the same H, W (TPKE/PublicKey.cs:91).
+    // A buffer of its own: the other mcl calls' staging (mcl[]) must not overwrite cached sets between pairings
+    DevBuf pc_lines;
     std::vector<uint32_t> pc_keys;    // 72 words (the mclBnG2 record) per slot
     std::vector<uint64_t> pc_used;    // last use (0: empty)
     uint64_t pc_tick = 0;

@@ -942,6 +942,7 @@ void ctx_free(lcb_ctx *c) {
     for (auto &b : c->out) b.release();
     for (auto &b : c->dkg) b.release();
     for (auto &b : c->mcl) b.release();
+    c->pc_lines.release();
     for (auto &b : c->t_coop) b.release();
     c->cc_lines.release();
     c->cc_ok.release();
@@ -3114,7 +3115,7 @@ extern "C" void mclBn_pairing(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) {
     };
     static_assert(sizeof(PairIn) == 2 * LCB_G1A_ST_BYTES + 16, "PairIn layout");
     uint8_t *gin = (uint8_t *)c->mcl[1].get(sizeof(PairIn));
-    u32 *lines = (u32 *)c->mcl[2].get((size_t)2 * LCB_PAIR_CACHE * LCB_LINESET_BYTES);
+    u32 *lines = (u32 *)c->pc_lines.get((size_t)2 * LCB_PAIR_CACHE * LCB_LINESET_BYTES);
     u32 *park = (u32 *)c->mcl[4].get(576 * slots);
     uint8_t *fl = (uint8_t *)c->mcl[5].get(64);
     if (!gin || !lines || !park || !fl) { set_err("device allocation failed"); return; }
@@ -3191,13 +3192,78 @@ extern "C" void mclBn_finalExp(mclBnGT *y, const mclBnGT *x) {
     hipMemcpyAsync(r, park, 576, hipMemcpyDeviceToHost, s);
     if (sync_check(c, "final exp")) memcpy(y, r, 576);
 }
+// sum_i [k_i] x_i (canonical scalars k_i < r, raw words) on the cooperative ladders of mclBnG1_mul: three groups per
+// term (GLV halves over P and phi(P), and [z^2] P for the membership the split needs), k_ptmul_g1_multi, the terms
+// added on the host.  Returns 1 with *z set, 0 when a term is not on the curve or outside G1 (the caller then takes
+// its exact path, so every input keeps that path's value), -1 on a device error.
+static const size_t MULVEC_COOP_MAX = 512;
+static const bool g_mulvec_coop = !(getenv("LCB_MULVEC_COOP") && atoi(getenv("LCB_MULVEC_COOP")) == 0);
+static int g1_mulvec_coop(lcb_ctx *c, mclBnG1 *z, const mclBnG1 *x, const uint64_t (*kraw)[4], size_t n) {
+    std::vector<PtJobG1> jobs(3 * n);
+    memset(jobs.data(), 0, jobs.size() * sizeof(PtJobG1));
+    std::vector<fph::g1a> phis(n);
+    std::vector<uint8_t> live(n, 0);
+    const u128h zz = (u128h)Z_ABS_H * Z_ABS_H;
+    const uint64_t z2[2] = {(uint64_t)zz, (uint64_t)(zz >> 64)}, zero[1] = {0};
+    for (size_t i = 0; i < n; i++) {
+        PtJobG1 *J = &jobs[3 * i];
+        const uint64_t *k = kraw[i];
+        fph::g1a P;
+        fph::jac_to_aff(P, *G1R(&x[i]));
+        if (!P.inf && !fph::jac_on_curve(*G1R(&x[i]))) return 0;
+        if (P.inf || (k[0] | k[1] | k[2] | k[3]) == 0) {          // a zero term: three idle ladders
+            for (int j = 0; j < 3; j++) { J[j].inf = 1; put_digits(J[j], zero, 1, 33); }
+            continue;
+        }
+        uint64_t q[4] = {k[0], k[1], k[2], k[3]};
+        const uint64_t d0 = divmod_u(q), d1 = divmod_u(q);
+        const u128h a0 = (u128h)d1 * Z_ABS_H + d0, a1 = (u128h)q[1] << 64 | q[0];
+        const u128h sum = a0 + a1;
+        const uint64_t k1[3] = {(uint64_t)sum, (uint64_t)(sum >> 64), sum < a0 ? 1ull : 0ull};
+        const uint64_t k2[2] = {(uint64_t)a1, (uint64_t)(a1 >> 64)};
+        fph::g1_phi(phis[i], P);
+        put_point(J[0], P);
+        put_point(J[1], phis[i]);
+        put_point(J[2], P);
+        if (!put_digits(J[0], k1, 3, 33) || !put_digits(J[1], k2, 2, 33) || !put_digits(J[2], z2, 2, 33)) return 0;
+        live[i] = 1;
+    }
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    const void *dj = up(c->mcl[8], (const u32 *)jobs.data(), jobs.size() * sizeof(PtJobG1) / 4, s);
+    void *dout = c->mcl[9].get(3 * n * sizeof(fph::g1));
+    if (!dj || !dout) { set_err("device allocation failed"); return -1; }
+    lcbk_ptmul_g1_multi(s, dj, (u32)(3 * n), dout);
+    std::vector<fph::g1> acc(3 * n);
+    hipMemcpyAsync(acc.data(), dout, 3 * n * sizeof(fph::g1), hipMemcpyDeviceToHost, s);
+    if (!sync_check(c, "mulVec")) return -1;
+    fph::g1 r;
+    fph::jac_set_inf(r);
+    for (size_t i = 0; i < n; i++) {
+        if (!live[i]) continue;
+        fph::g1a chk;
+        fph::g1_phi(chk, phis[i]);                // (beta^2 x, y) -> membership: [z^2] P == (beta^2 x, -y)
+        fph::neg(chk.y, chk.y);
+        if (!fph::jac_eq_aff(acc[3 * i + 2], chk)) return 0;
+        fph::g1 t;
+        fph::jac_add(t, acc[3 * i], acc[3 * i + 1]);
+        fph::jac_add(r, r, t);
+    }
+    *G1W(z) = r;
+    return 1;
+}
 // mclBnG1_mulVec: sum_i [y_i] x_i with the canonical scalars (mcl's per-term product, exact for any on-curve x_i):
-// one lane per term (windowed ladder), then block reductions and a one-lane sum
+// up to MULVEC_COOP_MAX terms on the cooperative ladders above; otherwise (or for a term outside G1) one lane per term
+// (windowed ladder), then block reductions and a one-lane sum
 static bool g1_mulvec(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y, mclSize n) {
     SYNC_CTX_OR(c, false)
     if (n > 0xffffffffu) { set_err("mulVec: too large"); return false; }
     std::vector<uint64_t> raw(4 * n);
     for (size_t i = 0; i < n; i++) frh::to_raw(&raw[4 * i], FRV(&y[i]));
+    if (n <= MULVEC_COOP_MAX && g_mulvec_coop) {
+        const int rc = g1_mulvec_coop(c, z, x, (const uint64_t (*)[4])raw.data(), n);
+        if (rc != 0) return rc > 0;
+    }
     Enq q(c, c->stream);
     hipStream_t s = c->stream;
     const u32 *pts = up(c->mcl[0], (const u32 *)x, 36 * n, s);
@@ -3259,8 +3325,40 @@ static int lagrange_points(int g, void *out, const mclBnFr *xVec, const void *yV
     memcpy(out, r, words * 4);
     return 0;
 }
+// G1 Lagrange interpolation of up to 64 points: the coefficients lambda_i = prod_{j != i} x_j / (x_j - x_i) on the host
+// (-1 on a zero or repeated x, as k_lagrange_coeffs), the products on the cooperative ladders (g1_mulvec_coop); 1 done,
+// 0 for the batch kernels' path (a point outside G1, or more points)
+static int g1_lagrange_coop(mclBnG1 *out, const mclBnFr *xVec, const mclBnG1 *yVec, size_t k) {
+    if (k > 64 || !g_mulvec_coop) return 0;
+    SYNC_CTX_OR(c, -1)
+    std::vector<uint64_t> raw(4 * k);
+    for (size_t i = 0; i < k; i++) {
+        const uint64_t *xi = FRV(&xVec[i]);
+        if (frh::is_zero(xi)) { set_err("lagrange: zero x"); return -1; }
+        uint64_t num[4], den[4], t[4];
+        static const uint64_t one_raw[4] = {1, 0, 0, 0};
+        frh::from_raw(num, one_raw);
+        memcpy(den, num, 32);
+        for (size_t j = 0; j < k; j++) {
+            if (j == i) continue;
+            const uint64_t *xj = FRV(&xVec[j]);
+            frh::sub(t, xj, xi);
+            if (frh::is_zero(t)) { set_err("lagrange: repeated x"); return -1; }
+            frh::mul(num, num, xj);
+            frh::mul(den, den, t);
+        }
+        frh::inv(den, den);
+        frh::mul(t, num, den);
+        frh::to_raw(&raw[4 * i], t);
+    }
+    const int rc = g1_mulvec_coop(c, out, yVec, (const uint64_t (*)[4])raw.data(), k);
+    return rc < 0 ? -1 : rc;
+}
 extern "C" int mclBn_G1LagrangeInterpolation(mclBnG1 *out, const mclBnFr *xVec, const mclBnG1 *yVec, mclSize k) {
     if (k == 1) { *out = yVec[0]; return mclBnFr_isZero(&xVec[0]) ? -1 : 0; }
+    if (k == 0) return -1;
+    const int rc = g1_lagrange_coop(out, xVec, yVec, k);
+    if (rc != 0) return rc > 0 ? 0 : -1;
     return lagrange_points(1, out, xVec, yVec, k);
 }
 extern "C" int mclBn_G2LagrangeInterpolation(mclBnG2 *out, const mclBnFr *xVec, const mclBnG2 *yVec, mclSize k) {
@@ -3348,6 +3446,19 @@ static int eval_poly(int g, void *out, const void *coef, mclSize n, const mclBnF
     uint64_t xr[4];
     frh::to_raw(xr, FRV(x));
     static const bool horner = getenv("LCB_EVAL_HORNER") && atoi(getenv("LCB_EVAL_HORNER")) == 1;
+    if (g == 1 && n >= 2 && n <= MULVEC_COOP_MAX && !horner && g_mulvec_coop) {
+        // coefficients in G1: [x^i mod r] c_i on the cooperative ladders (a coefficient outside G1 returns 0 here
+        // and takes the terms below, whose powers are reduced mod #E(Fp) instead)
+        std::vector<uint64_t> raw(4 * n);
+        uint64_t pw[4], one_raw[4] = {1, 0, 0, 0};
+        frh::from_raw(pw, one_raw);
+        for (size_t i = 0; i < n; i++) {
+            frh::to_raw(&raw[4 * i], pw);
+            frh::mul(pw, pw, FRV(x));
+        }
+        const int rc = g1_mulvec_coop(c, (mclBnG1 *)out, (const mclBnG1 *)coef, (const uint64_t (*)[4])raw.data(), n);
+        if (rc != 0) return rc > 0 ? 0 : -1;
+    }
     if (g == 1 && n >= 2 && !horner) return eval_poly_g1_terms(c, (mclBnG1 *)out, (const mclBnG1 *)coef, n, xr);
     Enq q(c, c->stream);
     hipStream_t s = c->stream;

@@ -89,6 +89,50 @@ def test_mul_vec_matches_oracle(mcl, n):
     assert got.ToBytes() == want
 
 
+def test_pairing_cache_survives_other_mcl_calls(mcl):
+    """mclBn_pairing caches G2 line sets per thread; mulVec, Lagrange and EvaluatePolynomial stage their data on the
+    same context and must not overwrite a cached set (a cached second pairing was wrong before the cache had a buffer
+    of its own)."""
+    Fr, G1, G2, GT = mcl.Fr, mcl.G1, mcl.G2, mcl.GT
+    d = Drbg(b"mcl-pair-cache")
+    A, B = G1.Generator() * Fr.FromBytes(d.fr()), G2.Generator() * Fr.FromBytes(d.fr())
+    want = o.pairing(A.ToBytes(), B.ToBytes())
+    assert GT.Pairing(A, B).ToBytes() == want
+    pts = [G1.Generator() * Fr.FromBytes(d.fr()) for _ in range(22)]
+    scs = [Fr.FromBytes(d.fr()) for _ in range(22)]
+    _mul_vec(mcl, pts, scs)
+    mcl.MclBls12381.LagrangeInterpolate([Fr.FromInt(i + 1) for i in range(8)], pts[:8])
+    mcl.MclBls12381.EvaluatePolynomial(pts[:8], scs[0])
+    _mul_vec(mcl, pts * 40, scs * 40)                 # 880 terms: the batch kernels' path
+    assert GT.Pairing(A, B).ToBytes() == want
+    assert GT.Pairing(-A, B) * GT.Pairing(A, B) == GT.Pairing(G1.Zero(), B)
+
+
+def test_mul_vec_and_lagrange_with_points_outside_g1(mcl):
+    """The cooperative ladders split scalars by GLV, valid in G1 only: a term outside G1 (the order-3 point, a random
+    on-curve point) sends the call to the exact per-term path, so the result is sum_i [s_i] P_i for any on-curve
+    input; the point at infinity and zero scalars are idle terms."""
+    from test_gpu_batched import off_subgroup_g1
+    Fr, G1 = mcl.Fr, mcl.G1
+    d = Drbg(b"mcl-mulvec-off")
+    t3 = G1.FromBytes(bytes(47) + b"\x80")
+    off = G1.FromBytes(off_subgroup_g1(d))
+    good = [G1.Generator() * Fr.FromBytes(d.fr()) for _ in range(6)]
+    for case, pts in enumerate((good, good[:3] + [t3] + good[3:], good[:2] + [off], [G1.Zero()] + good[:2])):
+        scs = [Fr.FromBytes(d.fr()) for _ in pts]
+        scs[-1] = Fr.FromInt(0) if len(pts) == 3 else scs[-1]
+        if case == 1:                               # [s] t3 = t3 for s = 1 mod 3: -t3 = (0, 2) serialises as all zeros,
+            s3 = int.from_bytes(scs[3].ToBytes(), "little")   # the encoding of infinity, so the expected sum is
+            scs[3] = Fr.FromBytes((s3 - s3 % 3 + 1).to_bytes(32, "little"))   # accumulated through t3 itself
+        want = G1.Zero().ToBytes()
+        for p, s in zip(pts, scs):
+            want = o.g1_add(want, o.g1_mul(p.ToBytes(), s.ToBytes()))
+        assert _mul_vec(mcl, pts, scs).ToBytes() == want, case
+        xs = [Fr.FromInt(i + 1) for i in range(len(pts))]
+        got = mcl.MclBls12381.LagrangeInterpolate(xs, pts)
+        assert got.ToBytes() == o.g1_lagrange([x.ToBytes() for x in xs], [p.ToBytes() for p in pts]), case
+
+
 @pytest.mark.parametrize("g", [1, 2])
 def test_lagrange_points_match_oracle(mcl, g):
     Fr = mcl.Fr
