@@ -1406,6 +1406,7 @@ def run_mcl_latency(args, nat, rank):
     xs = [Fr.FromInt(i + 1) for i in range(args.f + 1)]
     ys = [G1.Generator() * Fr.GetRandom() for _ in range(args.f + 1)]
     cs = [G1.Generator() * Fr.GetRandom() for _ in range(args.f + 1)]
+    ys2 = [G2.Generator() * Fr.GetRandom() for _ in range(args.f + 1)]
     vs = [G1.Generator() * Fr.GetRandom() for _ in range(args.n)]
     ks = [Fr.GetRandom() for _ in range(args.n)]
     from lachain_amd.native import mclBnG1, mclBnFr
@@ -1447,6 +1448,7 @@ def run_mcl_latency(args, nat, rank):
         "G1_mulVec_n%d" % args.n: 1e3 * med(lambda: mv(ctypes.byref(out.v), pa, sa, args.n)),
         "G1_Lagrange_k%d" % (args.f + 1): 1e3 * med(lambda: M.LagrangeInterpolate(xs, ys)),
         "G1_EvaluatePolynomial_n%d" % (args.f + 1): 1e3 * med(lambda: M.EvaluatePolynomial(cs, xs[3])),
+        "G2_Lagrange_k%d" % (args.f + 1): 1e3 * med(lambda: M.LagrangeInterpolate(xs, ys2)),
         "VerifyShare_via_mcl": 1e3 * med(verify_mcl),
         "VerifyShare_batch_api_n1": 1e3 * med(lambda: pk.VerifyShare(share, ps)),
     }

@@ -93,6 +93,14 @@ extern "C" __global__ void __launch_bounds__(64, 1) k_ptmul_g1_multi(const PtJob
     const u32 n = min(n_groups - base, (u32)PT_MULTI_GROUPS);
     pt_ladder<fp, PT_MULTI_GROUPS>(jobs + base, n, out + base, lds);
 }
+// the same for G2 (five groups per term: the four GLS digits' ladders and [|z|] Q for the membership test)
+extern "C" __global__ void __launch_bounds__(64, 1) k_ptmul_g2_multi(const PtJob<fp2> *jobs, u32 n_groups, g2 *out) {
+    __shared__ PtLds<fp2> lds[PT_MULTI_GROUPS + 1];
+    const u32 base = blockIdx.x * PT_MULTI_GROUPS;
+    if (base >= n_groups) return;                // uniform
+    const u32 n = min(n_groups - base, (u32)PT_MULTI_GROUPS);
+    pt_ladder<fp2, PT_MULTI_GROUPS>(jobs + base, n, out + base, lds);
+}
 static_assert(sizeof(PtJob<fp>) == 96 + 16 + 36, "PtJob<fp> layout (launch.h LCB_PTJOB_G1_BYTES)");
 static_assert(sizeof(PtJob<fp2>) == 192 + 16 + 36, "PtJob<fp2> layout (launch.h LCB_PTJOB_G2_BYTES)");
 
@@ -178,6 +186,10 @@ extern "C" void lcbk_ptmul_g1(hipStream_t s, const void *jobs, u32 n_groups, voi
 extern "C" void lcbk_ptmul_g1_multi(hipStream_t s, const void *jobs, u32 n_groups, void *out) {
     const dim3 grid((n_groups + PT_MULTI_GROUPS - 1) / PT_MULTI_GROUPS);
     LCB_LAUNCH_GATED(k_ptmul_g1_multi, grid, dim3(64), 0, s, (const PtJob<fp> *)jobs, n_groups, (g1 *)out);
+}
+extern "C" void lcbk_ptmul_g2_multi(hipStream_t s, const void *jobs, u32 n_groups, void *out) {
+    const dim3 grid((n_groups + PT_MULTI_GROUPS - 1) / PT_MULTI_GROUPS);
+    LCB_LAUNCH_GATED(k_ptmul_g2_multi, grid, dim3(64), 0, s, (const PtJob<fp2> *)jobs, n_groups, (g2 *)out);
 }
 extern "C" void lcbk_ptmul_g2(hipStream_t s, const void *jobs, u32 n_groups, void *out) {
     LCB_LAUNCH_GATED(k_ptmul_g2, dim3(1), dim3(64), 0, s, (const PtJob<fp2> *)jobs, n_groups, (g2 *)out);

@@ -153,6 +153,7 @@ extern "C" int lcbk_cfg_k_prep(u32 sign_b);
 // cooperative single scalar multiplications (k_ptmul.hip): n_groups ladders of one wave
 extern "C" void lcbk_ptmul_g1(hipStream_t s, const void *jobs, u32 n_groups, void *out);
 extern "C" void lcbk_ptmul_g1_multi(hipStream_t s, const void *jobs, u32 n_groups, void *out);
+extern "C" void lcbk_ptmul_g2_multi(hipStream_t s, const void *jobs, u32 n_groups, void *out);
 extern "C" void lcbk_ptmul_g2(hipStream_t s, const void *jobs, u32 n_groups, void *out);
 extern "C" int lcbk_prio_k_batch(u32 on);
 extern "C" int lcbk_prio_k_coop(u32 on);

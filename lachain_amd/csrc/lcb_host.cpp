@@ -3252,6 +3252,93 @@ static int g1_mulvec_coop(lcb_ctx *c, mclBnG1 *z, const mclBnG1 *x, const uint64
     *G1W(z) = r;
     return 1;
 }
+// the G2 counterpart: sum_i [k_i] x_i on mclBnG2_mul's GLS ladders (five groups per term, k_ptmul_g2_multi); the
+// same return convention (0: a term off the curve or outside G2 — the caller's exact path)
+static int g2_terms_coop(lcb_ctx *c, mclBnG2 *z, const mclBnG2 *x, const uint64_t (*kraw)[4], size_t n) {
+    std::vector<PtJobG2> jobs(5 * n);
+    memset(jobs.data(), 0, jobs.size() * sizeof(PtJobG2));
+    std::vector<fph::g2a> psis(n);
+    std::vector<uint8_t> live(n, 0);
+    const uint64_t zero[1] = {0};
+    for (size_t i = 0; i < n; i++) {
+        PtJobG2 *J = &jobs[5 * i];
+        const uint64_t *k = kraw[i];
+        fph::g2a Q;
+        fph::jac_to_aff(Q, *G2R(&x[i]));
+        if (!Q.inf && !fph::jac_on_curve(*G2R(&x[i]))) return 0;
+        if (Q.inf || (k[0] | k[1] | k[2] | k[3]) == 0) {
+            for (int j = 0; j < 5; j++) { J[j].inf = 1; put_digits(J[j], zero, 1, 17); }
+            continue;
+        }
+        uint64_t q[4] = {k[0], k[1], k[2], k[3]}, d[4];
+        d[0] = divmod_u(q);
+        d[1] = divmod_u(q);
+        d[2] = divmod_u(q);
+        d[3] = q[0];
+        fph::g2a B[4];
+        B[0] = Q;
+        fph::g2_psi(B[1], Q);
+        fph::g2_psi(B[2], B[1]);
+        fph::g2_psi(B[3], B[2]);
+        psis[i] = B[1];
+        fph::neg(B[1].y, B[1].y);
+        fph::neg(B[3].y, B[3].y);
+        bool ok = true;
+        for (int j = 0; j < 4; j++) {
+            put_point(J[j], B[j]);
+            ok &= put_digits(J[j], &d[j], 1, 17);
+        }
+        put_point(J[4], Q);
+        ok &= put_digits(J[4], &Z_ABS_H, 1, 17);
+        if (!ok) return 0;
+        live[i] = 1;
+    }
+    Enq q(c, c->stream);
+    hipStream_t s = c->stream;
+    const void *dj = up(c->mcl[8], (const u32 *)jobs.data(), jobs.size() * sizeof(PtJobG2) / 4, s);
+    void *dout = c->mcl[9].get(5 * n * sizeof(fph::g2));
+    if (!dj || !dout) { set_err("device allocation failed"); return -1; }
+    lcbk_ptmul_g2_multi(s, dj, (u32)(5 * n), dout);
+    std::vector<fph::g2> acc(5 * n);
+    hipMemcpyAsync(acc.data(), dout, 5 * n * sizeof(fph::g2), hipMemcpyDeviceToHost, s);
+    if (!sync_check(c, "G2 terms")) return -1;
+    fph::g2 r;
+    fph::jac_set_inf(r);
+    for (size_t i = 0; i < n; i++) {
+        if (!live[i]) continue;
+        fph::g2a chk = psis[i];                   // membership: psi(Q) == -[|z|] Q
+        fph::neg(chk.y, chk.y);
+        if (!fph::jac_eq_aff(acc[5 * i + 4], chk)) return 0;
+        for (int j = 0; j < 4; j++) fph::jac_add(r, r, acc[5 * i + j]);
+    }
+    *G2W(z) = r;
+    return 1;
+}
+// Lagrange coefficients lambda_i = prod_{j != i} x_j / (x_j - x_i) as canonical raw words; false on a zero or
+// repeated x (the error of k_lagrange_coeffs)
+static bool lagrange_lambdas(std::vector<uint64_t> &raw, const mclBnFr *xVec, size_t k) {
+    raw.assign(4 * k, 0);
+    static const uint64_t one_raw[4] = {1, 0, 0, 0};
+    for (size_t i = 0; i < k; i++) {
+        const uint64_t *xi = FRV(&xVec[i]);
+        if (frh::is_zero(xi)) { set_err("lagrange: zero x"); return false; }
+        uint64_t num[4], den[4], t[4];
+        frh::from_raw(num, one_raw);
+        memcpy(den, num, 32);
+        for (size_t j = 0; j < k; j++) {
+            if (j == i) continue;
+            const uint64_t *xj = FRV(&xVec[j]);
+            frh::sub(t, xj, xi);
+            if (frh::is_zero(t)) { set_err("lagrange: repeated x"); return false; }
+            frh::mul(num, num, xj);
+            frh::mul(den, den, t);
+        }
+        frh::inv(den, den);
+        frh::mul(t, num, den);
+        frh::to_raw(&raw[4 * i], t);
+    }
+    return true;
+}
 // mclBnG1_mulVec: sum_i [y_i] x_i with the canonical scalars (mcl's per-term product, exact for any on-curve x_i):
 // up to MULVEC_COOP_MAX terms on the cooperative ladders above; otherwise (or for a term outside G1) one lane per term
 // (windowed ladder), then block reductions and a one-lane sum
@@ -3331,27 +3418,18 @@ static int lagrange_points(int g, void *out, const mclBnFr *xVec, const void *yV
 static int g1_lagrange_coop(mclBnG1 *out, const mclBnFr *xVec, const mclBnG1 *yVec, size_t k) {
     if (k > 64 || !g_mulvec_coop) return 0;
     SYNC_CTX_OR(c, -1)
-    std::vector<uint64_t> raw(4 * k);
-    for (size_t i = 0; i < k; i++) {
-        const uint64_t *xi = FRV(&xVec[i]);
-        if (frh::is_zero(xi)) { set_err("lagrange: zero x"); return -1; }
-        uint64_t num[4], den[4], t[4];
-        static const uint64_t one_raw[4] = {1, 0, 0, 0};
-        frh::from_raw(num, one_raw);
-        memcpy(den, num, 32);
-        for (size_t j = 0; j < k; j++) {
-            if (j == i) continue;
-            const uint64_t *xj = FRV(&xVec[j]);
-            frh::sub(t, xj, xi);
-            if (frh::is_zero(t)) { set_err("lagrange: repeated x"); return -1; }
-            frh::mul(num, num, xj);
-            frh::mul(den, den, t);
-        }
-        frh::inv(den, den);
-        frh::mul(t, num, den);
-        frh::to_raw(&raw[4 * i], t);
-    }
+    std::vector<uint64_t> raw;
+    if (!lagrange_lambdas(raw, xVec, k)) return -1;
     const int rc = g1_mulvec_coop(c, out, yVec, (const uint64_t (*)[4])raw.data(), k);
+    return rc < 0 ? -1 : rc;
+}
+// the same in G2 (AssembleSignature's interpolation, ThresholdSignature/PublicKeySet.cs:34-42)
+static int g2_lagrange_coop(mclBnG2 *out, const mclBnFr *xVec, const mclBnG2 *yVec, size_t k) {
+    if (k > 64 || !g_mulvec_coop) return 0;
+    SYNC_CTX_OR(c, -1)
+    std::vector<uint64_t> raw;
+    if (!lagrange_lambdas(raw, xVec, k)) return -1;
+    const int rc = g2_terms_coop(c, out, yVec, (const uint64_t (*)[4])raw.data(), k);
     return rc < 0 ? -1 : rc;
 }
 extern "C" int mclBn_G1LagrangeInterpolation(mclBnG1 *out, const mclBnFr *xVec, const mclBnG1 *yVec, mclSize k) {
@@ -3363,6 +3441,9 @@ extern "C" int mclBn_G1LagrangeInterpolation(mclBnG1 *out, const mclBnFr *xVec, 
 }
 extern "C" int mclBn_G2LagrangeInterpolation(mclBnG2 *out, const mclBnFr *xVec, const mclBnG2 *yVec, mclSize k) {
     if (k == 1) { *out = yVec[0]; return mclBnFr_isZero(&xVec[0]) ? -1 : 0; }
+    if (k == 0) return -1;
+    const int rc = g2_lagrange_coop(out, xVec, yVec, k);
+    if (rc != 0) return rc > 0 ? 0 : -1;
     return lagrange_points(2, out, xVec, yVec, k);
 }
 // out = a x mod #E(Fp) for G1 (a < #E, x < 2^256): #E(Fp) = p - z = h r (z = -0xd201000000010000), so [k] P depends
@@ -3460,6 +3541,17 @@ static int eval_poly(int g, void *out, const void *coef, mclSize n, const mclBnF
         if (rc != 0) return rc > 0 ? 0 : -1;
     }
     if (g == 1 && n >= 2 && !horner) return eval_poly_g1_terms(c, (mclBnG1 *)out, (const mclBnG1 *)coef, n, xr);
+    if (g == 2 && n >= 2 && n <= 64 && !horner && g_mulvec_coop) {   // coefficients in G2: [x^i mod r] c_i, GLS
+        std::vector<uint64_t> raw(4 * n);
+        uint64_t pw[4], one_raw[4] = {1, 0, 0, 0};
+        frh::from_raw(pw, one_raw);
+        for (size_t i = 0; i < n; i++) {
+            frh::to_raw(&raw[4 * i], pw);
+            frh::mul(pw, pw, FRV(x));
+        }
+        const int rc = g2_terms_coop(c, (mclBnG2 *)out, (const mclBnG2 *)coef, (const uint64_t (*)[4])raw.data(), n);
+        if (rc != 0) return rc > 0 ? 0 : -1;
+    }
     Enq q(c, c->stream);
     hipStream_t s = c->stream;
     const u32 *dc = up(c->mcl[0], (const u32 *)coef, words * n, s);

@@ -133,6 +133,25 @@ def test_mul_vec_and_lagrange_with_points_outside_g1(mcl):
         assert got.ToBytes() == o.g1_lagrange([x.ToBytes() for x in xs], [p.ToBytes() for p in pts]), case
 
 
+def test_g2_lagrange_and_polynomial_with_points_outside_g2(mcl):
+    """G2 Lagrange interpolation and EvaluatePolynomial run their terms on the cooperative GLS ladders when every point
+    is in G2; a point outside G2 (on the twist, not in the subgroup) sends the call to its exact path."""
+    from test_gpu_batched import off_subgroup_g2
+    Fr, G2 = mcl.Fr, mcl.G2
+    d = Drbg(b"mcl-g2-off")
+    good = [G2.Generator() * Fr.FromBytes(d.fr()) for _ in range(5)]
+    off = G2.FromBytes(off_subgroup_g2(d))
+    for case, pts in enumerate((good, good[:2] + [off] + good[2:], [G2.Zero()] + good[:3])):
+        xs = [Fr.FromInt(3 * i + 2) for i in range(len(pts))]
+        got = mcl.MclBls12381.LagrangeInterpolate(xs, pts)
+        assert got.ToBytes() == o.g2_lagrange([x.ToBytes() for x in xs], [p.ToBytes() for p in pts]), case
+        x = Fr.FromBytes(d.fr())
+        acc = pts[-1].ToBytes()
+        for c in reversed(pts[:-1]):
+            acc = o.g2_add(o.g2_mul(acc, x.ToBytes()), c.ToBytes())
+        assert mcl.MclBls12381.EvaluatePolynomial(pts, x).ToBytes() == acc, case
+
+
 @pytest.mark.parametrize("g", [1, 2])
 def test_lagrange_points_match_oracle(mcl, g):
     Fr = mcl.Fr

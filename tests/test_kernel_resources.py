@@ -61,6 +61,7 @@ BUDGET = {
     "k_op_grp": (372, 4008),                  # round 6: the exponentiation routine's table in VGPRs (lcb_r_fp_pow)
     "k_op_gt": (1788, 8148),                  # single-lane mcl operations (one wave per dispatch), one kernel per family
     "k_op_pair": (842, 7620),
+    "k_ptmul_g2_multi": (36, 68),             # round 6: G2 Lagrange / EvaluatePolynomial terms, 16 ladders per block
     "k_ptmul_g2": (36, 68),                   # mcl G2 multiplication latency kernel: four ladder lanes share each op (signed digits: 34)
     "k_rlc_key_tables": (12, 168),            # k_rlc_rand.hip: spills to scratch, not AGPRs (<= 256 registers)
     "k_rlc_miller_fallback": (0, 2376),
