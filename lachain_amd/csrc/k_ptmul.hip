@@ -12,16 +12,19 @@
 //     temporaries) and a ROUND is one Fp (G1) or Fp2 (G2) product per lane on operands it selects by its role, then the
 //     four products are exchanged through LDS.  dbl-2009-l takes 3 rounds instead of 7 serial products, add-2007-bl 5
 //     instead of 16 (the formulas, special cases and results of curve.hpp's jac_dbl / jac_add exactly).
-// The host splits the scalar (lcb_host.cpp): G1 by GLV (k P = k1 P + k2 phi(P), 129-bit halves) with a third group
-// computing [z^2] P, the G1 membership test the split needs; G2 by GLS (four 64-bit digits over +-psi^i(Q)) with a
-// fifth group computing [|z|] Q for psi(Q) == -[|z|] Q.  The host adds the groups' results and checks membership; a
-// base point outside the subgroup takes the exact one-lane ladder instead (k_op), so every input gets k P exactly.
+// The host splits the scalar (lcb_host.cpp): G1 by GLV (k P = k1 P + k2 phi(P), 129-bit halves), each half cut at
+// bit 65 over P and [2^65] P (four groups of 18 windows); G2 by GLS (four 64-bit digits over +-psi^i(Q)), each digit
+// cut at bit 32 over +-psi^i(Q) and +-psi^i([2^32] Q) (eight groups of 9 windows).  The host computes the [2^65] /
+// [2^32] multiples and the membership test the split needs ([z^2] P == (beta^2 x, -y), psi(Q) == -[|z|] Q) with its
+// own field code, and adds the groups' results; a base point outside the subgroup takes the exact one-lane ladder
+// instead (k_op), so every input gets k P exactly.  The multi-term calls (mulVec, Lagrange, EvaluatePolynomial) keep
+// the ladders' own membership group (three / five groups per term, k_ptmul_g1_multi / _g2_multi).
 #include "coop_pt.hpp"
 
 LCB_ASM_LIBRARY(k_ptmul)
 LCB_TU_CONFIG(k_ptmul)
 
-#define PT_MAX_GROUPS 8               // G1 uses 3, G2 5 (LDS: 9 areas, 22 / 45 KB)
+#define PT_MAX_GROUPS 8               // G1 uses 4, G2 8 (LDS: 9 areas, 22 / 45 KB)
 #define PT_MAX_WIN 33              // signed 4-bit windows (129-bit GLV halves; 17 for the 64-bit GLS digits)
 
 // one group's job: affine base point (inf = 1: the point at infinity) and nwin signed digits, most significant

@@ -633,29 +633,54 @@ extern "C" void mclBnG1_mul(mclBnG1 *z, const mclBnG1 *x, const mclBnFr *y) {
     const uint64_t s_top = s < a0 ? 1 : 0;
     const uint64_t k1[3] = {(uint64_t)s, (uint64_t)(s >> 64), s_top}, k2[2] = {(uint64_t)a1, (uint64_t)(a1 >> 64)};
     const u128h zz = (u128h)Z_ABS_H * Z_ABS_H;
-    const uint64_t z2[2] = {(uint64_t)zz, (uint64_t)(zz >> 64)};
-    PtJobG1 jobs[3];
-    memset(jobs, 0, sizeof jobs);
     fph::g1a phiP;
     fph::g1_phi(phiP, P);
+    {   // membership on the host: [z^2] P == P + phi(P) = (beta^2 x, -y) (128 doublings of host field code)
+        fph::g1 m, PJ;
+        fph::jac_from_aff(PJ, P);
+        fph::jac_set_inf(m);
+        for (int b = 127; b >= 0; b--) {
+            fph::jac_dbl(m, m);
+            if ((zz >> b) & 1) fph::jac_add(m, m, PJ);
+        }
+        fph::g1a chk;
+        fph::g1_phi(chk, phiP);                   // (beta^2 x, y)
+        fph::neg(chk.y, chk.y);
+        if (!fph::jac_eq_aff(m, chk)) {           // outside G1: the split does not apply
+            g1_op(OP_G1_MUL, z, x, nullptr, y);
+            return;
+        }
+    }
+    // four ladders of <= 65 bits: k1 = k1_lo + 2^65 k1_hi over P and [2^65] P, k2 likewise over phi(P) and
+    // [2^65] phi(P) = phi([2^65] P) (the doublings on the host): half the serial rounds of two 129-bit ladders
+    fph::g1a P65, phiP65;
+    {
+        fph::g1 t;
+        fph::jac_from_aff(t, P);
+        for (int i = 0; i < 65; i++) fph::jac_dbl(t, t);
+        fph::jac_to_aff(P65, t);
+        fph::g1_phi(phiP65, P65);
+    }
+    if (P65.inf) { g1_op(OP_G1_MUL, z, x, nullptr, y); return; }    // unreachable in G1 (2^65 < r)
+    const uint64_t k1lo[2] = {k1[0], k1[1] & 1}, k1hi[2] = {(k1[1] >> 1) | (k1[2] << 63), k1[2] >> 1};
+    const uint64_t k2lo[2] = {k2[0], k2[1] & 1}, k2hi[2] = {k2[1] >> 1, 0};
+    PtJobG1 jobs[4];
+    memset(jobs, 0, sizeof jobs);
     put_point(jobs[0], P);
-    put_point(jobs[1], phiP);
-    put_point(jobs[2], P);                        // membership: [z^2] P == P + phi(P) = (beta^2 x, -y)
-    if (!put_digits(jobs[0], k1, 3, 33) || !put_digits(jobs[1], k2, 2, 33) || !put_digits(jobs[2], z2, 2, 33)) {
-        g1_op(OP_G1_MUL, z, x, nullptr, y);       // unreachable (k1 < 2^129): the exact ladder
+    put_point(jobs[1], P65);
+    put_point(jobs[2], phiP);
+    put_point(jobs[3], phiP65);
+    if (!put_digits(jobs[0], k1lo, 2, 18) || !put_digits(jobs[1], k1hi, 2, 18) || !put_digits(jobs[2], k2lo, 2, 18) ||
+        !put_digits(jobs[3], k2hi, 2, 18)) {
+        g1_op(OP_G1_MUL, z, x, nullptr, y);       // unreachable (< 2^66 in 18 signed windows): the exact ladder
         return;
     }
-    fph::g1 acc[3];
-    if (!ptmul_run(1, jobs, sizeof(PtJobG1), 3, acc, sizeof(fph::g1))) { fail_out(z, 144); return; }
-    fph::g1a chk;
-    fph::g1_phi(chk, phiP);                       // (beta^2 x, y)
-    fph::neg(chk.y, chk.y);
-    if (!fph::jac_eq_aff(acc[2], chk)) {          // outside G1: the split does not apply
-        g1_op(OP_G1_MUL, z, x, nullptr, y);
-        return;
-    }
+    fph::g1 acc[4];
+    if (!ptmul_run(1, jobs, sizeof(PtJobG1), 4, acc, sizeof(fph::g1))) { fail_out(z, 144); return; }
     fph::g1 r;
     fph::jac_add(r, acc[0], acc[1]);
+    fph::jac_add(r, r, acc[2]);
+    fph::jac_add(r, r, acc[3]);
     *G1W(z) = r;
 }
 extern "C" void lcb_g1_generator(mclBnG1 *g) { fph::g1_generator(*G1W(g)); }
@@ -732,30 +757,54 @@ extern "C" void mclBnG2_mul(mclBnG2 *z, const mclBnG2 *x, const mclBnFr *y) {
     fph::g2_psi(B[2], B[1]);
     fph::g2_psi(B[3], B[2]);
     fph::g2a psiQ = B[1];
+    {   // membership on the host: psi(Q) == -[|z|] Q (64 doublings of host field code)
+        fph::g2 m, QJ;
+        fph::jac_from_aff(QJ, Q);
+        fph::jac_set_inf(m);
+        for (int b = 63; b >= 0; b--) {
+            fph::jac_dbl(m, m);
+            if ((Z_ABS_H >> b) & 1) fph::jac_add(m, m, QJ);
+        }
+        fph::g2a chk = psiQ;
+        fph::neg(chk.y, chk.y);
+        if (!fph::jac_eq_aff(m, chk)) {           // outside G2: the split does not apply
+            g2_op(OP_G2_MUL, z, x, nullptr, y);
+            return;
+        }
+    }
+    // eight ladders of 32 bits: each digit d_i = lo + 2^32 hi over B_i and [2^32] B_i (= +-psi^i([2^32] Q), the
+    // doublings on the host): half the serial rounds of four 64-bit ladders
+    fph::g2a Q32, C[4];
+    {
+        fph::g2 t;
+        fph::jac_from_aff(t, Q);
+        for (int i = 0; i < 32; i++) fph::jac_dbl(t, t);
+        fph::jac_to_aff(Q32, t);
+    }
+    if (Q32.inf) { g2_op(OP_G2_MUL, z, x, nullptr, y); return; }    // unreachable in G2 (2^32 < r)
+    C[0] = Q32;
+    fph::g2_psi(C[1], Q32);
+    fph::g2_psi(C[2], C[1]);
+    fph::g2_psi(C[3], C[2]);
+    fph::neg(C[1].y, C[1].y);
+    fph::neg(C[3].y, C[3].y);
     fph::neg(B[1].y, B[1].y);
     fph::neg(B[3].y, B[3].y);
-    PtJobG2 jobs[5];
+    PtJobG2 jobs[8];
     memset(jobs, 0, sizeof jobs);
     bool dig_ok = true;
     for (int i = 0; i < 4; i++) {
-        put_point(jobs[i], B[i]);
-        dig_ok &= put_digits(jobs[i], &d[i], 1, 17);
+        const uint64_t lo = d[i] & 0xffffffffull, hi = d[i] >> 32;
+        put_point(jobs[2 * i], B[i]);
+        put_point(jobs[2 * i + 1], C[i]);
+        dig_ok &= put_digits(jobs[2 * i], &lo, 1, 9);
+        dig_ok &= put_digits(jobs[2 * i + 1], &hi, 1, 9);
     }
-    put_point(jobs[4], Q);                        // membership: psi(Q) == -[|z|] Q
-    dig_ok &= put_digits(jobs[4], &Z_ABS_H, 1, 17);
-    if (!dig_ok) { g2_op(OP_G2_MUL, z, x, nullptr, y); return; }   // unreachable (64-bit digits): the exact ladder
-    fph::g2 acc[5];
-    if (!ptmul_run(2, jobs, sizeof(PtJobG2), 5, acc, sizeof(fph::g2))) { fail_out(z, 288); return; }
-    fph::g2a chk = psiQ;
-    fph::neg(chk.y, chk.y);
-    if (!fph::jac_eq_aff(acc[4], chk)) {          // outside G2
-        g2_op(OP_G2_MUL, z, x, nullptr, y);
-        return;
-    }
-    fph::g2 r;
-    fph::jac_add(r, acc[0], acc[1]);
-    fph::jac_add(r, r, acc[2]);
-    fph::jac_add(r, r, acc[3]);
+    if (!dig_ok) { g2_op(OP_G2_MUL, z, x, nullptr, y); return; }   // unreachable (32-bit digits): the exact ladder
+    fph::g2 acc[8];
+    if (!ptmul_run(2, jobs, sizeof(PtJobG2), 8, acc, sizeof(fph::g2))) { fail_out(z, 288); return; }
+    fph::g2 r = acc[0];
+    for (int i = 1; i < 8; i++) fph::jac_add(r, r, acc[i]);
     *G2W(z) = r;
 }
 extern "C" void lcb_g2_generator(mclBnG2 *g) { fph::g2_generator(*G2W(g)); }
