@@ -44,6 +44,29 @@ def test_mul_matches_oracle(mcl, g):
 
 
 @pytest.mark.parametrize("g", [1, 2])
+def test_mul_split_boundaries(mcl, g):
+    """Round 6 cuts the GLV halves at bit 65 (G1) and the GLS digits at bit 32 (G2) over host-computed [2^65] P /
+    [2^32] Q: scalars whose parts sit at those cuts (below lambda ~ 2^128 the G1 split is k1 = k, below |z| ~ 2^64 the G2
+    digit d0 = k) and the parts' extremes, plus sums over the second half / digits."""
+    d = Drbg(b"gpu-ptmul-split-%d" % g)
+    G = mcl.G1 if g == 1 else mcl.G2
+    omul = o.g1_mul if g == 1 else o.g2_mul
+    gen = o.g1_gen() if g == 1 else o.g2_gen()
+    base = omul(gen, d.fr())
+    B = G.FromBytes(base)
+    u = 0xD201000000010000
+    if g == 1:
+        ks = [1 << 64, (1 << 65) - 1, 1 << 65, (1 << 65) + 1, (1 << 66) - 1, (1 << 128) - 1, (1 << 127) + (1 << 65),
+              u * u - 2, u * u - 1, u * u, (u * u - 1) * ((1 << 65) + 3) % R, (1 << 65) * (u * u - 1) % R]
+    else:
+        ks = [(1 << 32) - 1, 1 << 32, (1 << 32) + 1, (1 << 33) - 1, u - 1, (1 << 32) * u, ((1 << 32) - 1) * u + (1 << 32),
+              u ** 3 + (1 << 32) * u ** 2 + 1, ((1 << 32) - 1) * (1 + u + u * u + u ** 3) % R]
+    for k in ks:
+        kb = (k % R).to_bytes(32, "little")
+        assert (B * mcl.Fr.FromBytes(kb)).ToBytes() == omul(base, kb), hex(k)
+
+
+@pytest.mark.parametrize("g", [1, 2])
 def test_mul_outside_subgroup(mcl, g):
     """points with a cofactor-torsion component: the split's membership ladder rejects them and the exact one-lane
     ladder gives k P (G1.FromBytes / G2.FromBytes accept such points: HoneyBadgerSmartMalicious.cs:57-73)"""
