@@ -3150,6 +3150,105 @@ extern "C" int lcb_g2_lagrange_batch(uint8_t *out, uint8_t *status, const uint8_
 // one-group cooperative check: P and the point at infinity, Q's normalised line set and the set of infinity, then
 // the nine-lane final exponentiation.  The lines are normalised (divided by their Fp2 leading coefficient), which
 // changes the Miller value by a factor the final exponentiation removes: the GT value is mcl's.
+// The line set of one G2 point on the host (pairing.hpp lineset_compute: the same 68 steps and formulas with the host
+// field code, which gives the kernels' canonical residues; the normalised lines B' = Bc / A, C' = Cc / A depend only on
+// the affine points, so they are the words k_lineset_coop writes).  False when some A_k == 0 (a point outside G2: the
+// caller then takes the kernel, whose Miller loop computes such a set's lines on the fly).
+static const bool g_pair_host_lines = !(getenv("LCB_PAIR_HOST_LINES") && atoi(getenv("LCB_PAIR_HOST_LINES")) == 0);
+static bool lineset_host(uint32_t *dst, const fph::g2a &Q) {
+    const int PT = LCB_LS_POINT_WORD, FLAG = PT + 48, NL = 68, NLW = 48;
+    memset(dst, 0, LCB_LINESET_BYTES);
+    memcpy(dst + PT, &Q.x, 96);
+    memcpy(dst + PT + 24, &Q.y, 96);
+    dst[FLAG + 1] = Q.inf ? 1u : 0u;
+    if (Q.inf) { dst[FLAG] = 1u; return true; }   // every line is the constant 1: B' = C' = 0
+    fph::fp twelve, raw12 = fph::zero();
+    raw12.v[0] = 12;
+    fph::from_raw(twelve, raw12);
+    fph::fp2 b3;                                  // 3 b' = 12 (1 + u)
+    b3.a = twelve;
+    b3.b = twelve;
+    fph::fp2 Tx = Q.x, Ty = Q.y, Tz = fph::one2();
+    std::vector<fph::fp2> A(NL), B(NL), C(NL);
+    int k = 0;
+    for (int i = 62; i >= 0; i--) {
+        {   // doubling step (ls_dbl_store): A = Y^2 - 3b'Z^2, Bc = -3X^2, Cc = 2YZ; T <- 2T
+            fph::fp2 YZ, XY, ZZ, YY, t, u;
+            fph::mul(YZ, Ty, Tz);
+            fph::mul(XY, Tx, Ty);
+            fph::sqr(ZZ, Tz);
+            fph::sqr(YY, Ty);
+            fph::sqr(t, Tx);
+            fph::add(u, t, t);
+            fph::add(u, u, t);
+            fph::neg(B[k], u);
+            fph::add(C[k], YZ, YZ);
+            fph::mul(Tz, YY, YZ);
+            fph::add(Tz, Tz, Tz);
+            fph::mul(ZZ, ZZ, b3);
+            fph::sub(A[k], YY, ZZ);
+            k++;
+            fph::add(t, ZZ, ZZ);
+            fph::add(t, t, ZZ);
+            fph::mul_fp(XY, XY, fph::INV2);
+            fph::sub(u, YY, t);
+            fph::mul(Tx, XY, u);
+            fph::add(u, YY, t);
+            fph::mul_fp(u, u, fph::INV2);
+            fph::sqr(Ty, u);
+            fph::sqr(t, ZZ);
+            fph::add(u, t, t);
+            fph::add(u, u, t);
+            fph::sub(Ty, Ty, u);
+        }
+        if ((Z_ABS_H >> i) & 1) {   // addition step (ls_add_store): A = th xQ - la yQ, Bc = -th, Cc = la; T <- T + Q
+            fph::fp2 th, la, t, D, E, G;
+            fph::mul(t, Q.y, Tz);
+            fph::sub(th, Ty, t);
+            fph::mul(t, Q.x, Tz);
+            fph::sub(la, Tx, t);
+            fph::mul(A[k], th, Q.x);
+            fph::mul(t, la, Q.y);
+            fph::sub(A[k], A[k], t);
+            fph::neg(B[k], th);
+            C[k] = la;
+            k++;
+            fph::sqr(D, la);
+            fph::mul(E, la, D);
+            fph::mul(G, Tx, D);
+            fph::sqr(t, th);
+            fph::mul(D, Tz, t);
+            fph::mul(Tz, Tz, E);
+            fph::add(D, E, D);
+            fph::sub(D, D, G);
+            fph::sub(D, D, G);
+            fph::mul(Tx, la, D);
+            fph::sub(t, G, D);
+            fph::mul(G, th, t);
+            fph::mul(t, Ty, E);
+            fph::sub(Ty, G, t);
+        }
+    }
+    if (k != NL) return false;
+    std::vector<fph::fp2> pre(NL);                // A_0 ... A_k, then one inversion (Montgomery's trick)
+    pre[0] = A[0];
+    for (int j = 1; j < NL; j++) fph::mul(pre[j], pre[j - 1], A[j]);
+    if (fph::is_zero(pre[NL - 1])) return false;
+    fph::fp2 inv;
+    fph::inv(inv, pre[NL - 1]);
+    for (int j = NL - 1; j >= 0; j--) {
+        fph::fp2 ai, b, c;
+        if (j > 0) fph::mul(ai, inv, pre[j - 1]);
+        else ai = inv;
+        fph::mul(inv, inv, A[j]);
+        fph::mul(b, B[j], ai);
+        fph::mul(c, C[j], ai);
+        memcpy(dst + j * NLW, &b, 96);
+        memcpy(dst + j * NLW + 24, &c, 96);
+    }
+    dst[FLAG] = 1u;
+    return true;
+}
 extern "C" void mclBn_pairing(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) {
     fail_out(z, 576);                  // overwritten on success; a failed call leaves a value no other call produces
     if (injected(INJ_PAIRING_ALLOC)) { set_err("injected failure (pairing)"); return; }
@@ -3201,7 +3300,23 @@ extern "C" void mclBn_pairing(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) {
         pin.desc[2] = slot;
     }
     hipMemcpyAsync(gin, &pin, sizeof pin, hipMemcpyHostToDevice, s);
-    if (!hit) {                                      // the two sets' points for k_lineset_fill: Q, then infinity
+    std::vector<uint32_t> hsets;                     // the host line sets (alive until the call's synchronisation)
+    bool host_sets = false;
+    if (!hit && g_pair_host_lines) {                 // Q's set and the infinity set computed here, one upload
+        fph::g2 Q;
+        fph::g2a qa, ia;
+        memcpy(&Q, y, sizeof Q);
+        fph::jac_to_aff(qa, Q);
+        memset(&ia, 0, sizeof ia);
+        ia.inf = true;
+        hsets.assign((size_t)2 * LCB_LINESET_BYTES / 4, 0u);
+        if (lineset_host(hsets.data(), qa) && lineset_host(hsets.data() + LCB_LINESET_BYTES / 4, ia)) {
+            hipMemcpyAsync(lines + (size_t)2 * slot * (LCB_LINESET_BYTES / 4), hsets.data(), 2 * (size_t)LCB_LINESET_BYTES,
+                           hipMemcpyHostToDevice, s);
+            host_sets = true;
+        }
+    }
+    if (!hit && !host_sets) {                        // the two sets' points for k_lineset_fill: Q, then infinity
         fph::g2 Q;
         fph::g2a qa;
         memcpy(&Q, y, sizeof Q);
@@ -3216,7 +3331,7 @@ extern "C" void mclBn_pairing(mclBnGT *z, const mclBnG1 *x, const mclBnG2 *y) {
             hipMemcpyAsync(lines + (size_t)(2 * slot + k) * (LCB_LINESET_BYTES / 4) + LCB_LS_POINT_WORD, pt[k],
                            sizeof pt[k], hipMemcpyHostToDevice, s);
     }
-    if (!hit) lcbk_lineset_coop(s, lines + (size_t)2 * slot * (LCB_LINESET_BYTES / 4), 2, nullptr, nullptr);
+    if (!hit && !host_sets) lcbk_lineset_coop(s, lines + (size_t)2 * slot * (LCB_LINESET_BYTES / 4), 2, nullptr, nullptr);
     lcbk_coop_tpke_miller(s, lines, desc, gpts, 1, park, fl, fl + 32, 1, 1);
     lcbk_coop_final_exp_check(s, park, 1, nullptr);
     u32 r[144];
